@@ -1,0 +1,70 @@
+// Shared definitions for the gfx950 (CDNA4) SART kernels.
+//
+// Storage conventions (all kernels):
+//   * A is the local row shard of the ray-transfer matrix, row-major fp32, P_pad rows x ld columns.
+//     ld is a multiple of 64 floats (256 B rows) and the padding columns/rows are zero, so every
+//     16-byte vector load is aligned and in bounds and no kernel needs a column tail branch.
+//   * Vectors over voxels (x, ray density, corrections) are padded to ld with zeros.
+//   * Vectors over pixels (measurement, weights, ray length) are padded to P_pad with zeros.
+//
+// Everything that the reference recomputed on the host per iteration (convergence test,
+// iteration counter, solution update) lives in a device-resident SartState, so a whole frame
+// solve runs without host synchronisation (reference: sartsolver_cuda.cpp:231-262 synchronises
+// twice per iteration through cublasSdot and MPI_Allreduce on host buffers).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sart {
+
+constexpr int kWave = 64;
+
+// Layout shared with python (mpi_cuda_sartsolver_amd/ops/state.py). 128 bytes.
+struct alignas(16) SartState {
+    double G;           //  0: sum_{g>0} g^2 / s^2 over all ranks (reference "measurement_squared")
+    double conv_prev;   //  8: convergence metric of the previous SART iteration
+    double conv_last;   // 16: convergence metric of the last SART iteration
+    double F_last;      // 24: ||A x||^2 of the last sweep (fp32 semantics, as the reference)
+    int32_t sweep;      // 32: number of sweeps whose decision has been taken
+    int32_t done;       // 36: 1 once the frame is finished (converged or max iterations)
+    int32_t status;     // 40: 0 SUCCESS, -1 MAX_ITERATIONS_EXCEEDED, -2 running
+    int32_t iterations; // 44: number of SART updates applied to x
+    int32_t max_iter;   // 48
+    int32_t error;      // 52: nonzero when a persistent kernel gave up waiting (protocol timeout)
+    double tol;         // 56: convergence tolerance
+    int32_t epoch;      // 64: exchange epoch of the fused sweep (strictly increasing, never 0)
+    int32_t pad0;       // 68
+    double reserved[7]; // 72..127
+};
+static_assert(sizeof(SartState) == 128, "SartState must be 128 bytes");
+
+enum Status : int32_t { kSuccess = 0, kMaxIterationsExceeded = -1, kRunning = -2 };
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+__device__ __forceinline__ float dot4(const float4 a, const float4 b) {
+    return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+}
+
+__device__ __forceinline__ void fma4(float4& acc, const float4 a, const float s) {
+    acc.x = fmaf(a.x, s, acc.x);
+    acc.y = fmaf(a.y, s, acc.y);
+    acc.z = fmaf(a.z, s, acc.z);
+    acc.w = fmaf(a.w, s, acc.w);
+}
+
+// Launch-time error check used by every host launcher.
+void check_launch(const char* what);
+
+}  // namespace sart

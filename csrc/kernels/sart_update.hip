@@ -1,0 +1,197 @@
+// Per-frame preparation, Laplacian penalty (CSR SpMV), device-side convergence decision and the
+// fused SART solution updates for gfx950.
+//
+// Reference counterparts:
+//   * measurement normalisation / masks / initial-guess weights, done on the host per frame
+//     (reference sartsolver_cuda.cpp:138-194) -> k_prep_rows, k_init_solution.
+//   * GradPenaltyKernel / LogGradPenaltyKernel: COO with 64-bit div/mod and fp32 atomics
+//     (reference sart_kernels.cu:179-202) -> k_penalty_csr: one thread per Laplacian row, fixed order,
+//     written not accumulated (no memset, no atomics).
+//   * UpdateSolutionKernel / UpdateLogSolutionKernel (reference sart_kernels.cu:205-224) ->
+//     k_update_linear / k_update_log, gated by the device-side decision.
+//   * host convergence test `|conv - conv_prev| < tol` after cublasSdot + MPI_Allreduce
+//     (reference sartsolver_cuda.cpp:250-261) -> k_decide, a single-lane kernel on the stream, so
+//     a frame solve never synchronises with the host.
+#include "sart_common.hpp"
+
+#include <math.h>
+#include <stdexcept>
+
+namespace sart {
+
+constexpr float kEpsLog = 1e-7f;  // reference EPSILON_LOG_CUDA (sart_kernels.cu:17-19)
+
+// ghat = fp32(g / s); a = [ghat >= 0][len > tau_l] / len; gpos = max(ghat, 0); wo = a * ghat
+__global__ __launch_bounds__(256) void k_prep_rows(const double* __restrict__ g, int64_t nrows, int64_t nrows_pad,
+                                                   double inv_s, const float* __restrict__ ray_length,
+                                                   float len_thres, float* __restrict__ ghat, float* __restrict__ arow,
+                                                   float* __restrict__ gpos, float* __restrict__ wo) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nrows_pad) return;
+    float gh = 0.f, a = 0.f;
+    if (i < nrows) {
+        gh = (float)(g[i] * inv_s);
+        const float len = ray_length[i];
+        const float inv_len = (len > len_thres) ? 1.f / len : 0.f;
+        a = (gh >= 0.f) ? inv_len : 0.f;
+    }
+    ghat[i] = gh;
+    arow[i] = a;
+    if (gpos) gpos[i] = (gh > 0.f) ? gh : 0.f;
+    if (wo) wo[i] = a * gh;
+}
+
+// x = max(src, 1e-7) on [0, n), 0 on the padding (reference sartsolver_cuda.cpp:180).
+// src_f32 (device, already scaled) or src_f64 * scale (warm start x_prev / s).
+__global__ __launch_bounds__(256) void k_init_solution(float* __restrict__ x, int64_t n, int64_t n_pad,
+                                                       const float* __restrict__ src_f32,
+                                                       const double* __restrict__ src_f64, double scale) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_pad) return;
+    float v = 0.f;
+    if (i < n) {
+        v = src_f32 ? src_f32[i] : (float)(src_f64[i] * scale);
+        if (v < kEpsLog) v = kEpsLog;
+    }
+    x[i] = v;
+}
+
+// pen[i] = beta * sum_k val[k] * h(x[col[k]]), h = identity (linear) or log (logarithmic SART).
+template <bool LOGX>
+__global__ __launch_bounds__(256) void k_penalty_csr(const int64_t* __restrict__ row_ptr,
+                                                     const int32_t* __restrict__ col,
+                                                     const float* __restrict__ val, int64_t n, float beta,
+                                                     const float* __restrict__ x, float* __restrict__ pen,
+                                                     const SartState* __restrict__ st) {
+    if (st != nullptr && st->done) return;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int64_t k0 = row_ptr[i], k1 = row_ptr[i + 1];
+    float acc = 0.f;
+    for (int64_t k = k0; k < k1; ++k) {
+        const float xv = x[col[k]];
+        acc = fmaf(val[k], LOGX ? logf(xv) : xv, acc);
+    }
+    pen[i] = beta * acc;
+}
+
+// Single lane. Consumes ||A x_s||^2 of sweep s and decides, exactly as the reference loop does
+// at its iteration s-1 (its forward projection after the update is our next sweep's forward).
+__global__ void k_decide(SartState* __restrict__ st, const float* __restrict__ Fslot) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (st->done) return;
+    const int s = st->sweep;
+    const double F = (double)(*Fslot);
+    st->F_last = F;
+    int done = 0;
+    int status = kRunning;
+    if (s >= 1) {
+        const double conv = (st->G - F) / st->G;
+        if (s >= 2 && fabs(conv - st->conv_prev) < st->tol) {
+            done = 1;
+            status = kSuccess;
+        }
+        st->conv_prev = conv;
+        st->conv_last = conv;
+    }
+    if (!done && s >= st->max_iter) {
+        done = 1;
+        status = kMaxIterationsExceeded;
+    }
+    st->iterations = done ? s : s + 1;
+    st->sweep = s + 1;
+    st->status = status;
+    st->done = done;
+    st->epoch = st->epoch + 1;
+}
+
+// x = max(x + d - pen, 0)
+__global__ __launch_bounds__(256) void k_update_linear(float* __restrict__ x, const float* __restrict__ d,
+                                                       const float* __restrict__ pen, int64_t n,
+                                                       const SartState* __restrict__ st) {
+    if (st->done) return;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float v = x[i] + d[i];
+    if (pen) v -= pen[i];
+    x[i] = (v > 0.f) ? v : 0.f;
+}
+
+// x *= ((O + eps) / (Fv + eps))^alpha * exp(-pen)
+__global__ __launch_bounds__(256) void k_update_log(float* __restrict__ x, const float* __restrict__ O,
+                                                    const float* __restrict__ Fv, const float* __restrict__ pen,
+                                                    float alpha, int64_t n, const SartState* __restrict__ st) {
+    if (st->done) return;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float r = powf((O[i] + kEpsLog) / (Fv[i] + kEpsLog), alpha);
+    if (pen) r *= expf(-pen[i]);
+    x[i] *= r;
+}
+
+// Device-side state initialisation for a new frame (keeps the epoch counter monotonic).
+__global__ void k_state_begin(SartState* __restrict__ st, double G, double tol, int max_iter) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    st->G = G;
+    st->conv_prev = 0.0;
+    st->conv_last = 0.0;
+    st->F_last = 0.0;
+    st->sweep = 0;
+    st->done = 0;
+    st->status = kRunning;
+    st->iterations = 0;
+    st->max_iter = max_iter;
+    st->error = 0;
+    st->tol = tol;
+    if (st->epoch <= 0) st->epoch = 1;
+}
+
+static inline unsigned nb(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+void launch_prep_rows(const double* g, int64_t nrows, int64_t nrows_pad, double inv_s, const float* ray_length,
+                      float len_thres, float* ghat, float* arow, float* gpos, float* wo, hipStream_t stream) {
+    hipLaunchKernelGGL(k_prep_rows, dim3(nb(nrows_pad)), dim3(256), 0, stream, g, nrows, nrows_pad, inv_s, ray_length,
+                       len_thres, ghat, arow, gpos, wo);
+    check_launch("k_prep_rows");
+}
+
+void launch_init_solution(float* x, int64_t n, int64_t n_pad, const float* src_f32, const double* src_f64,
+                          double scale, hipStream_t stream) {
+    hipLaunchKernelGGL(k_init_solution, dim3(nb(n_pad)), dim3(256), 0, stream, x, n, n_pad, src_f32, src_f64, scale);
+    check_launch("k_init_solution");
+}
+
+void launch_penalty(bool logx, const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta,
+                    const float* x, float* pen, const SartState* st, hipStream_t stream) {
+    if (logx)
+        hipLaunchKernelGGL(k_penalty_csr<true>, dim3(nb(n)), dim3(256), 0, stream, row_ptr, col, val, n, beta, x, pen,
+                           st);
+    else
+        hipLaunchKernelGGL(k_penalty_csr<false>, dim3(nb(n)), dim3(256), 0, stream, row_ptr, col, val, n, beta, x, pen,
+                           st);
+    check_launch("k_penalty_csr");
+}
+
+void launch_decide(SartState* st, const float* Fslot, hipStream_t stream) {
+    hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, stream, st, Fslot);
+    check_launch("k_decide");
+}
+
+void launch_update_linear(float* x, const float* d, const float* pen, int64_t n, const SartState* st,
+                          hipStream_t stream) {
+    hipLaunchKernelGGL(k_update_linear, dim3(nb(n)), dim3(256), 0, stream, x, d, pen, n, st);
+    check_launch("k_update_linear");
+}
+
+void launch_update_log(float* x, const float* O, const float* Fv, const float* pen, float alpha, int64_t n,
+                       const SartState* st, hipStream_t stream) {
+    hipLaunchKernelGGL(k_update_log, dim3(nb(n)), dim3(256), 0, stream, x, O, Fv, pen, alpha, n, st);
+    check_launch("k_update_log");
+}
+
+void launch_state_begin(SartState* st, double G, double tol, int max_iter, hipStream_t stream) {
+    hipLaunchKernelGGL(k_state_begin, dim3(1), dim3(64), 0, stream, st, G, tol, max_iter);
+    check_launch("k_state_begin");
+}
+
+}  // namespace sart

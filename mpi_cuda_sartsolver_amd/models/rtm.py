@@ -1,0 +1,120 @@
+"""Device-resident dense ray-transfer-matrix shard.
+
+The reference keeps the whole shard in a host ``std::vector<float>`` and copies it to the GPU with one
+``cudaMemcpy`` (reference raytransfer.hpp:20, sartsolver_cuda.cpp:104-106); the host copy is never
+freed. Here the shard lives only in HBM: it is filled either on the device (synthetic generator) or by
+streaming row blocks from HDF5 through a pinned staging buffer (``fill_rows``), so a 275 GB shard
+needs no 275 GB of host RAM.
+
+Layout: row-major fp32, ``nrows_pad x ld`` with zero padding. ``ld`` is chosen so the fused sweep can
+split the columns into J slabs of 1024*K floats (``fused_layout``); otherwise it is a multiple of 64.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ..ops import hip
+from ..parallel.partition import round_up
+
+
+@dataclass(frozen=True)
+class FusedGeometry:
+    K: int  # float4 per lane per row in a slab
+    J: int  # column slabs
+    I: int  # row groups
+    grid: int
+
+    @property
+    def tile_rows(self) -> int:
+        return 8 // self.K
+
+
+def choose_ld(nvoxel: int, max_waste: float = 0.10) -> int:
+    """Padded row length. Prefer a width that admits the fused-sweep slab geometry."""
+    if nvoxel >= 1024:
+        for K in (1, 2, 4, 8):
+            wc = 1024 * K
+            J = -(-nvoxel // wc)
+            if J <= 32 or K == 8:
+                ld = J * wc
+                if (ld - nvoxel) <= max_waste * nvoxel:
+                    return ld
+                break
+    return round_up(max(nvoxel, 64), 64)
+
+
+def fused_geometry(ld: int, num_cus: int) -> Optional[FusedGeometry]:
+    for K in (1, 2, 4, 8):
+        wc = 1024 * K
+        if ld % wc:
+            continue
+        J = ld // wc
+        if J <= 32 or K == 8:
+            if J > num_cus or J * (8 // K) > 2048:
+                return None
+            I = max(1, num_cus // J)
+            return FusedGeometry(K=K, J=J, I=I, grid=I * J)
+    return None
+
+
+class DenseRTM:
+    """Local row shard [row_offset, row_offset + npixel) x [0, nvoxel) of the RTM on one GPU."""
+
+    def __init__(self, npixel: int, nvoxel: int, row_offset: int = 0, device: Optional[torch.device] = None,
+                 ld: Optional[int] = None, row_align: int = 64):
+        if npixel <= 0 or nvoxel <= 0:
+            raise ValueError("RTM shard must have npixel > 0 and nvoxel > 0")
+        self.npixel = int(npixel)
+        self.nvoxel = int(nvoxel)
+        self.row_offset = int(row_offset)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.ld = int(ld) if ld is not None else choose_ld(self.nvoxel)
+        if self.ld % 64 or self.ld < self.nvoxel:
+            raise ValueError("ld must be a multiple of 64 and >= nvoxel")
+        self.nrows_pad = round_up(self.npixel, row_align)
+        self.A = torch.empty((self.nrows_pad, self.ld), dtype=torch.float32, device=self.device)
+
+    # ------------------------------------------------------------------ construction helpers
+    @property
+    def nbytes(self) -> int:
+        return self.nrows_pad * self.ld * 4
+
+    @property
+    def stream_handle(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def zero_padding(self) -> None:
+        if self.ld > self.nvoxel:
+            self.A[:, self.nvoxel:].zero_()
+        if self.nrows_pad > self.npixel:
+            self.A[self.npixel:].zero_()
+
+    @classmethod
+    def synthetic(cls, npixel: int, nvoxel: int, row_offset: int = 0, seed: int = 1234, lo: float = 0.0,
+                  hi: float = 1.0, device=None, ld=None) -> "DenseRTM":
+        """On-device random dense RTM; element (p, v) depends only on (seed, global p, v)."""
+        m = cls(npixel, nvoxel, row_offset, device=device, ld=ld)
+        hip().synth_matrix(m.A.data_ptr(), m.ld, m.nrows_pad, m.npixel, m.nvoxel, m.row_offset, int(seed), float(lo),
+                           float(hi), m.stream_handle)
+        return m
+
+    @classmethod
+    def from_dense(cls, A_local, row_offset: int = 0, device=None, ld=None) -> "DenseRTM":
+        """Upload a host (numpy / torch) dense block [npixel, nvoxel]."""
+        t = torch.as_tensor(A_local, dtype=torch.float32)
+        m = cls(t.shape[0], t.shape[1], row_offset, device=device, ld=ld)
+        m.A.zero_()
+        m.A[: m.npixel, : m.nvoxel].copy_(t.to(m.device, non_blocking=False))
+        return m
+
+    def fill_rows(self, local_row: int, block) -> None:
+        """Copy a host block of rows [local_row, local_row + len(block)) x [0, nvoxel) into HBM."""
+        t = torch.as_tensor(block, dtype=torch.float32)
+        n = t.shape[0]
+        self.A[local_row: local_row + n, : self.nvoxel].copy_(t, non_blocking=t.is_pinned())
+
+    def to_host(self):
+        return self.A[: self.npixel, : self.nvoxel].cpu().numpy()

@@ -1,0 +1,145 @@
+"""Communicators for the per-iteration reductions.
+
+The reference reduces the voxel correction through host memory with CUDA-unaware MPI: D2H copy,
+``MPI_Allreduce``, H2D copy, plus a second scalar ``MPI_Allreduce`` every iteration
+(reference sartsolver_cuda.cpp:242-255). Here one collective per iteration runs on device buffers:
+
+* :class:`TorchDistComm` -- ``torch.distributed`` process group; backend ``nccl`` is RCCL over xGMI
+  on MI355X (one process per GPU), backend ``gloo`` is the CPU path used by the multi-process tests.
+* :class:`SingleProcessComm` -- world size 1, every collective is the identity.
+
+The scalar ``||A x||^2`` rides in the same buffer as the correction vector (one collective, not two).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+class Communicator:
+    rank: int = 0
+    world_size: int = 1
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:  # in place
+        raise NotImplementedError
+
+    def all_reduce_scalar(self, v: float, op: str = "sum") -> float:
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        pass
+
+    def broadcast_object(self, obj, src: int = 0):
+        return obj
+
+    def all_gather_object(self, obj) -> list:
+        return [obj]
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+
+class SingleProcessComm(Communicator):
+    def all_reduce_(self, t, op="sum"):
+        return t
+
+    def all_reduce_scalar(self, v, op="sum"):
+        return float(v)
+
+
+_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+
+
+class TorchDistComm(Communicator):
+    """Wraps an initialised torch.distributed process group."""
+
+    def __init__(self, group: Optional[dist.ProcessGroup] = None, device: Optional[torch.device] = None):
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed is not initialised")
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
+        self.device = device
+
+    def all_reduce_(self, t, op="sum"):
+        if self.world_size > 1:
+            dist.all_reduce(t, op=_OPS[op], group=self.group)
+        return t
+
+    def all_reduce_scalar(self, v, op="sum"):
+        if self.world_size == 1:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=_OPS[op], group=self.group)
+        return float(t.item())
+
+    def barrier(self):
+        if self.world_size > 1:
+            if self.backend == "nccl":
+                dist.barrier(group=self.group, device_ids=[self.device.index])
+            else:
+                dist.barrier(group=self.group)
+
+    def broadcast_object(self, obj, src=0):
+        if self.world_size == 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src, group=self.group)
+        return lst[0]
+
+    def all_gather_object(self, obj):
+        if self.world_size == 1:
+            return [obj]
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+
+def env_world() -> tuple[int, int, int]:
+    """(rank, world_size, local_rank) from torchrun / MPI-style environment variables."""
+    rank = int(os.environ.get("RANK", os.environ.get("OMPI_COMM_WORLD_RANK", os.environ.get("PMI_RANK", "0"))))
+    world = int(os.environ.get("WORLD_SIZE", os.environ.get("OMPI_COMM_WORLD_SIZE", os.environ.get("PMI_SIZE", "1"))))
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("OMPI_COMM_WORLD_LOCAL_RANK", str(rank))))
+    return rank, world, local
+
+
+def init_distributed(use_gpu: bool = True, timeout_s: float = 1800.0) -> Communicator:
+    """One process per GPU (torchrun). Rank -> GPU is LOCAL_RANK (reference: rank % device_count,
+    sartsolver_cuda.cpp:96-98). World size 1 needs no process group at all."""
+    import datetime
+
+    rank, world, local = env_world()
+    if use_gpu and torch.cuda.is_available():
+        ndev = torch.cuda.device_count()
+        torch.cuda.set_device(local % ndev)
+    if world == 1:
+        return SingleProcessComm()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    backend = "nccl" if (use_gpu and torch.cuda.is_available()) else "gloo"
+    if not dist.is_initialized():
+        kwargs = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kwargs["device_id"] = torch.device("cuda", torch.cuda.current_device())
+        dist.init_process_group(**kwargs)
+    return TorchDistComm()
+
+
+def abort_all(msg: str, code: int = 1) -> None:
+    """Fatal error in a multi-rank run: tear the group down instead of a bare exit that leaves the
+    peers blocked in a collective (reference exits per rank: sartsolver_cuda.cpp:45-75)."""
+    import sys
+
+    print(msg, file=sys.stderr, flush=True)
+    try:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    finally:
+        os._exit(code)

@@ -1,0 +1,115 @@
+"""GPU SART solvers vs the fp64 oracle of the reference GPU semantics (2048 x 4096, BASELINE config 1)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def problem():
+    from mpi_cuda_sartsolver_amd.utils.synthetic import host_problem
+
+    return host_problem(2048, 4096, seed=21, saturate_fraction=0.02)
+
+
+def _solver(dev, A, fused, log=False, L=None, **kw):
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+
+    m = DenseRTM.from_dense(A, device=dev)
+    p = SolverParams(**kw)
+    return SARTSolver(m, L, None, p, logarithmic=log, use_fused=fused, allow_zero_tolerance=True)
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b) / np.linalg.norm(b)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("log", [False, True])
+def test_fixed_iterations_vs_oracle(dev, problem, fused, log):
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+
+    A, g, _ = problem
+    s = _solver(dev, A, fused, log=log, max_iterations=40, conv_tolerance=0.0)
+    assert s.use_fused == fused
+    r = s.solve(g)
+    x_ref, st_ref, it_ref = sart_gpu_semantics(A, g, logarithmic=log, max_iterations=40, conv_tolerance=0.0)
+    assert r.status == st_ref == -1
+    assert r.iterations == it_ref == 40
+    assert _rel(r.solution, x_ref) < 2e-3
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_convergence_status(dev, problem, fused):
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+
+    A, g, _ = problem
+    s = _solver(dev, A, fused, max_iterations=2000, conv_tolerance=1e-4)
+    r = s.solve(g)
+    x_ref, st_ref, it_ref = sart_gpu_semantics(A, g, max_iterations=2000, conv_tolerance=1e-4)
+    assert r.status == st_ref == 0
+    assert abs(r.iterations - it_ref) <= max(2, it_ref // 20)
+    assert _rel(r.solution, x_ref) < 5e-3
+
+
+def test_fused_matches_two_pass(dev, problem):
+    A, g, _ = problem
+    r1 = _solver(dev, A, True, max_iterations=25, conv_tolerance=0.0).solve(g)
+    r2 = _solver(dev, A, False, max_iterations=25, conv_tolerance=0.0).solve(g)
+    assert r1.used_fused and not r2.used_fused
+    assert _rel(r1.solution, r2.solution) < 1e-3
+
+
+def test_fused_is_deterministic(dev, problem):
+    A, g, _ = problem
+    s = _solver(dev, A, True, max_iterations=15, conv_tolerance=0.0)
+    a = s.solve(g).solution
+    b = s.solve(g).solution
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("log", [False, True])
+def test_laplacian_and_warm_start(dev, log):
+    from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+    from mpi_cuda_sartsolver_amd.utils.synthetic import host_problem
+
+    A, g, x = host_problem(1024, 2048, seed=5)
+    L = LaplacianCSR.grid_3d(8, 16, 16, device=dev)
+    kw = dict(max_iterations=30, conv_tolerance=0.0, beta_laplace=1e-3)
+    s = _solver(dev, A, True, log=log, L=L, **kw)
+    x0 = 0.5 + 0.5 * np.random.default_rng(0).random(2048)
+    r = s.solve(g, solution=x0)
+    x_ref, _, _ = sart_gpu_semantics(A, g, L, logarithmic=log, x_prev=x0, **kw)
+    assert _rel(r.solution, x_ref) < 2e-3
+
+
+def test_ragged_shapes_fallback(dev):
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+    from mpi_cuda_sartsolver_amd.utils.synthetic import host_problem
+
+    A, g, _ = host_problem(333, 1500, seed=8)
+    s = _solver(dev, A, True, max_iterations=20, conv_tolerance=0.0)
+    r = s.solve(g)
+    x_ref, _, _ = sart_gpu_semantics(A, g, max_iterations=20, conv_tolerance=0.0)
+    assert _rel(r.solution, x_ref) < 2e-3
+
+
+def test_synthetic_bench_problem_small(dev):
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+    from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
+
+    prob = make_problem(4096, 8192, seed=3, device=dev)
+    s = SARTSolver(prob.rtm, None, None, SolverParams(max_iterations=10, conv_tolerance=0.0),
+                   allow_zero_tolerance=True)
+    assert s.use_fused
+    r = s.solve(prob.measurement)
+    assert r.iterations == 10 and np.all(np.isfinite(r.solution))

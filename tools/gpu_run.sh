@@ -1,0 +1,37 @@
+#!/usr/bin/env bash
+# GPU-box session script: each GPU step has its own time limit; a fault / abort / timeout ends the
+# session (nothing else touches the GPU afterwards); ordinary test failures (exit 1) do not.
+# Usage: tools/gpu_run.sh <step>...   steps: smoke tests bench bench2 prof probe
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+
+run() {  # run <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))" | tee -a "$OUT/session.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a "$OUT/session.log"
+  tail -n 30 "$OUT/$name.log"
+  case $rc in
+    0|1|5) return 0 ;;          # success, test failures, no tests collected
+    *) echo "FATAL step $name rc=$rc: stopping GPU session" | tee -a "$OUT/session.log"; exit $rc ;;
+  esac
+}
+
+for step in "$@"; do
+  case $step in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    testsall) run pytest_gpu_all 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    bench) run bench 600 python bench.py --steps 5 --warmup 1 ;;
+    bench2) run bench_twopass 600 python bench.py --steps 5 --warmup 1 --no-fused ;;
+    benchlog) run bench_log 600 python bench.py --steps 5 --warmup 1 --variant log ;;
+    probe) run probe 600 python tools/probe.py ;;
+    prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "=== session done"
