@@ -49,7 +49,10 @@ void launch_synth_vector(double* out, int64_t n, int64_t offset, uint64_t seed, 
                          hipStream_t stream);
 // fused_sweep.hip
 int fused_pick_k(int64_t ld);
-void launch_fused_sweep(bool logmode, int K, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
+int fused_tile_rows(int K, int variant);
+int fused_fpart_per_block(int variant);
+void fused_set_debug(int flags);
+void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                         const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                         uint64_t* gran, int I, int J, SartState* st, hipStream_t stream);
 // multiframe.hip
@@ -155,10 +158,13 @@ PYBIND11_MODULE(_sart_hip, m) {
         sart::launch_synth_vector(P<double>(out), n, offset, seed, lo, hi, S(stream));
     });
     m.def("fused_pick_k", &sart::fused_pick_k);
-    m.def("fused_sweep", [](bool logmode, int K, uintptr_t A, int64_t ld, int64_t nrows, int64_t nrows_pad,
+    m.def("fused_tile_rows", &sart::fused_tile_rows);
+    m.def("fused_fpart_per_block", &sart::fused_fpart_per_block);
+    m.def("fused_set_debug", &sart::fused_set_debug);
+    m.def("fused_sweep", [](bool logmode, int K, int variant, uintptr_t A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                             uintptr_t x, uintptr_t ghat, uintptr_t arow, uintptr_t partial, uintptr_t Fpart,
                             uintptr_t gran, int I, int J, uintptr_t st, uintptr_t stream) {
-        sart::launch_fused_sweep(logmode, K, P<const float>(A), ld, nrows, nrows_pad, P<const float>(x),
+        sart::launch_fused_sweep(logmode, K, variant, P<const float>(A), ld, nrows, nrows_pad, P<const float>(x),
                                  P<const float>(ghat), P<const float>(arow), P<float>(partial), P<double>(Fpart),
                                  P<uint64_t>(gran), I, J, P<sart::SartState>(st), S(stream));
     });

@@ -11,13 +11,18 @@
 //
 // Decomposition: a persistent grid of I x J workgroups (<= one per CU, all co-resident).
 // Workgroup (i, j) owns column slab j (Wc = 1024*K columns) of row group i and walks the row tiles
-// (T = 8/K rows) of its group. Per tile it computes the J-th part of each row dot and publishes it
-// as an 8-byte {epoch, value} granule with one write-through (sc1) store -- the data IS the flag,
-// no fences (cdna_hip_programming.md Guideline 16, recipe R2). A dedicated exchange wave gathers the
-// J granules of the previous tile, sums them in a fixed order (every workgroup of the group obtains
-// a bitwise identical f_r), forms w_r and hands it to the four compute waves through LDS; they
-// back-project the tile that is still held in registers (ring of 4 tiles: t-2 being back-projected,
-// t-1 waiting for its weights, t being reduced, t+1 / t+2 in flight).
+// (T = TK/K rows, TK float4 per lane) of its group. Per tile it computes the J-th part of each row dot
+// and publishes it as an 8-byte {epoch, value} granule with one write-through (sc1) store -- the data
+// IS the flag, no fences (cdna_hip_programming.md Guideline 16, recipe R2). A dedicated exchange wave
+// gathers the J granules of a tile, sums them in a fixed lane-parallel tree (every workgroup of the
+// group obtains a bitwise identical f_r), forms w_r and hands it to the four compute waves through
+// LDS; they back-project that tile L steps after reducing it, from a ring of R tiles held in
+// registers (tiles t-L .. t in use, t+1 .. t+R-L-1 in flight).
+//
+// Latency budget per step (one tile): the exchange wave issues the granule loads of tile t-L+2 in
+// step t and consumes them in step t+1, so the memory round trip of the gather (2-3 us under full
+// streaming load, MI355X_MICROARCH.md price list 'handoff-1to1') overlaps a whole step instead of
+// sitting between two barriers.
 //
 // Correctness does not depend on workgroup placement or dispatch order: every wait is on data
 // tagged with this sweep's epoch, every spin is bounded, and a timeout sets SartState::error so
@@ -30,23 +35,26 @@
 namespace sart {
 
 constexpr int kFusedThreads = 320;  // 4 compute waves + 1 exchange wave
-constexpr unsigned kSpinLimit = 1u << 18;
+constexpr unsigned kSpinLimit = 1u << 20;
+constexpr int kMaxGather = 512;     // J*T granules per tile
+constexpr int kGatherRegs = kMaxGather / 64;
 
 __device__ __forceinline__ uint64_t make_granule(int epoch, float v) {
     return ((uint64_t)(uint32_t)epoch << 32) | (uint64_t)__float_as_uint(v);
 }
 
-template <int K, bool LOG>
+template <int K, int TK, int R, int L, bool LOG>
 __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
     const float* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
     const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
     double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st) {
-    constexpr int T = 8 / K;  // rows per tile: T*K float4 = 32 floats per lane per tile
-    static_assert(T * K == 8, "tile must hold 8 float4 per lane");
+    constexpr int T = TK / K;   // rows per tile
+    constexpr int AH = R - L;   // tiles loaded ahead: at step t tiles t+1 .. t+AH-1 are in flight
+    static_assert(T * K == TK && T >= 1, "tile must be whole rows");
+    static_assert(L >= 2 && AH >= 2, "need lag >= 2 and >= 1 tile in flight");
 
-    __shared__ float s_part[4][4][T];  // [tile % 4][compute wave][row]
-    __shared__ float s_w[4][T];        // [tile % 4][row]
-    __shared__ float s_xch[2048];      // gathered partials of one tile, [j][row]
+    __shared__ float s_part[4][4][8];  // [tile % 4][compute wave][row]
+    __shared__ float s_w[4][8];        // [tile % 4][row]
 
     if (st->done) return;
     const int epoch = st->epoch;
@@ -57,6 +65,9 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
     const int64_t ntiles = nrows_pad / T;
     const int64_t t_begin = ntiles * gi / I;
     const int64_t nt = ntiles * (gi + 1) / I - t_begin;
+    // The last L steps only drain the back-projection. Both wave roles execute exactly nsteps
+    // barriers (a multiple of 2R so both unrolled loops end together).
+    const int64_t nsteps = (nt + L + 2 * R - 1) / (2 * R) * (2 * R);
 
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -75,7 +86,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
             acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
 
-        float4 buf[4][T][K];
+        float4 buf[R][T][K];
         auto load_tile = [&](float4(&dst)[T][K], int64_t t) {
             const float4* src = a4 + (t_begin + t) * T * ld4;
 #pragma unroll
@@ -83,12 +94,14 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
 #pragma unroll
                 for (int k = 0; k < K; ++k) dst[r][k] = src[r * ld4 + k * 64];
         };
-        if (nt > 0) load_tile(buf[0], 0);
-        if (nt > 1) load_tile(buf[1], 1);
+        // prologue: tiles 0 .. AH-1
+        [&]<int... Is>(std::integer_sequence<int, Is...>) {
+            ((Is < nt ? load_tile(buf[Is], Is) : void()), ...);
+        }(std::make_integer_sequence<int, AH>{});
 
         auto step = [&](auto bbc, int64_t t) {
-            constexpr int bb = decltype(bbc)::value;
-            constexpr int bp = (bb + 2) & 3;  // slot of tile t-2 == slot of tile t+2
+            constexpr int bb = decltype(bbc)::value;      // slot of tile t
+            constexpr int bp = (bb + R - L) % R;          // slot of tile t-L == slot of tile t-L+R
             if (t < nt) {
 #pragma unroll
                 for (int r = 0; r < T; ++r) {
@@ -96,26 +109,26 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
 #pragma unroll
                     for (int k = 0; k < K; ++k) s += dot4(buf[bb][r][k], xs[k]);
                     s = wave_sum(s);
-                    if (lane == 0) s_part[bb][wave][r] = s;
+                    if (lane == 0) s_part[t & 3][wave][r] = s;
                 }
             }
             __syncthreads();
-            if (t >= 2 && t - 2 < nt) {
+            if (t >= L && t - L < nt) {
+                const int ws = (int)((t - L) & 3);
 #pragma unroll
                 for (int r = 0; r < T; ++r) {
-                    const float wr = s_w[bp][r];
+                    const float wr = s_w[ws][r];
 #pragma unroll
                     for (int k = 0; k < K; ++k) fma4(acc[k], buf[bp][r][k], wr);
                 }
             }
-            if (t + 2 < nt) load_tile(buf[bp], t + 2);
+            if (t - L + R < nt) load_tile(buf[bp], t - L + R);
         };
 
-        for (int64_t t0 = 0; t0 < nt + 2; t0 += 4) {
-            step(std::integral_constant<int, 0>{}, t0 + 0);
-            step(std::integral_constant<int, 1>{}, t0 + 1);
-            step(std::integral_constant<int, 2>{}, t0 + 2);
-            step(std::integral_constant<int, 3>{}, t0 + 3);
+        for (int64_t t0 = 0; t0 < nsteps; t0 += R) {
+            [&]<int... Is>(std::integer_sequence<int, Is...>) {
+                (step(std::integral_constant<int, Is>{}, t0 + Is), ...);
+            }(std::make_integer_sequence<int, R>{});
         }
 
         float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld) + col4;
@@ -126,76 +139,693 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
         const int n = J * T;
         bool failed = false;
         double F = 0.0;
+        uint64_t pv[2][kGatherRegs];  // poll registers, double buffered by step parity
 
-        auto xstep = [&](auto bbc, int64_t t) {
-            constexpr int bb = decltype(bbc)::value;
-            constexpr int bw = (bb + 3) & 3;  // slot of tile t-1
-            __syncthreads();
-            if (t < nt && lane < T) {
-                const float s = ((s_part[bb][0][lane] + s_part[bb][1][lane]) + s_part[bb][2][lane]) +
-                                s_part[bb][3][lane];
-                uint64_t* g = gran + ((t_begin + t) * J + gj) * T + lane;
-                __hip_atomic_store(g, make_granule(epoch, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (t >= 1 && t - 1 < nt) {
-                const uint64_t* g = gran + (t_begin + t - 1) * J * T;
-                if (!failed) {
-                    unsigned spins = 0;
-                    while (true) {
-                        bool ok = true;
-                        for (int idx = lane; idx < n; idx += 64) {
-                            const uint64_t v = __hip_atomic_load(g + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            if ((int)(v >> 32) != epoch) ok = false;
-                            s_xch[idx] = __uint_as_float((uint32_t)v);
-                        }
-                        if (__all(ok)) break;
-                        if (++spins > kSpinLimit) {
-                            failed = true;
-                            if (lane == 0) atomicOr(&st->error, 1);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                if (lane < T) {
-                    float f = 0.f;
-                    if (!failed) {
-                        for (int jj = 0; jj < J; ++jj) f += s_xch[jj * T + lane];
-                    }
-                    const int64_t row = (t_begin + t - 1) * T + lane;
-                    float w = 0.f;
-                    if (row < nrows) {
-                        const float a = arow[row];
-                        w = LOG ? a * f : a * (ghat[row] - f);
-                        if (gj == 0) F += (double)f * (double)f;
-                    }
-                    s_w[bw][lane] = w;
-                }
-                __builtin_amdgcn_wave_barrier();
+        auto issue_poll = [&](uint64_t(&dst)[kGatherRegs], int64_t u) {
+            const uint64_t* g = gran + (t_begin + u) * (int64_t)n;
+#pragma unroll
+            for (int m = 0; m < kGatherRegs; ++m) {
+                const int idx = lane + 64 * m;
+                dst[m] = (idx < n) ? __hip_atomic_load(g + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : make_granule(epoch, 0.f);
             }
         };
 
-        for (int64_t t0 = 0; t0 < nt + 2; t0 += 4) {
-            xstep(std::integral_constant<int, 0>{}, t0 + 0);
+        // consume tile u from poll registers (re-poll synchronously if a granule is not ready yet)
+        auto finish_tile = [&](uint64_t(&v)[kGatherRegs], int64_t u) {
+            if (!failed) {
+                unsigned spins = 0;
+                while (true) {
+                    bool ok = true;
+#pragma unroll
+                    for (int m = 0; m < kGatherRegs; ++m) ok &= ((int)(v[m] >> 32) == epoch);
+                    if (__all(ok)) break;
+                    if (++spins > kSpinLimit) {
+                        failed = true;
+                        if (lane == 0) atomicOr(&st->error, 1);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    issue_poll(v, u);
+                }
+            }
+            float s = 0.f;
+            if (!failed) {
+#pragma unroll
+                for (int m = 0; m < kGatherRegs; ++m) s += __uint_as_float((uint32_t)v[m]);
+            }
+            // lanes l and l' hold the same row iff l == l' (mod T): butterfly over the other bits
+#pragma unroll
+            for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
+            if (lane < T) {
+                const int64_t row = (t_begin + u) * T + lane;
+                float w = 0.f;
+                if (row < nrows) {
+                    const float a = arow[row];
+                    w = LOG ? a * s : a * (ghat[row] - s);
+                    if (gj == 0) F += (double)s * (double)s;
+                }
+                s_w[u & 3][lane] = w;
+            }
+        };
+
+        auto xstep = [&](auto pc, int64_t t) {
+            constexpr int p = decltype(pc)::value;  // parity: pv[p] receives tile t-L+2
+            __syncthreads();
+            if (t < nt && lane < T) {
+                const int ps = (int)(t & 3);
+                const float s = ((s_part[ps][0][lane] + s_part[ps][1][lane]) + s_part[ps][2][lane]) +
+                                s_part[ps][3][lane];
+                uint64_t* g = gran + ((t_begin + t) * J + gj) * T + lane;
+                __hip_atomic_store(g, make_granule(epoch, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const int64_t un = t - L + 2;  // tile whose gather starts now (published >= L-2 steps ago)
+            if (un >= 0 && un < nt) issue_poll(pv[p], un);
+            const int64_t uc = t - L + 1;  // tile whose gather was issued last step; its w is due next step
+            if (uc >= 0 && uc < nt) finish_tile(pv[p ^ 1], uc);
+        };
+
+        for (int64_t t0 = 0; t0 < nsteps; t0 += 2) {
+            xstep(std::integral_constant<int, 0>{}, t0);
             xstep(std::integral_constant<int, 1>{}, t0 + 1);
-            xstep(std::integral_constant<int, 2>{}, t0 + 2);
-            xstep(std::integral_constant<int, 3>{}, t0 + 3);
         }
         F = wave_sum(F);
         if (lane == 0) Fpart[b] = F;
     }
 }
 
-// Geometry chosen by the host for a given padded width: K float4 per lane per row, slab width
-// Wc = 1024*K, J = ld / Wc slabs, I = max(1, ncu / J) row groups.
-struct FusedGeometry {
-    int K, J, I, grid;
-};
+// ---------------------------------------------------------------------------------------------
+// Variant 3 (default): in-flight tiles in registers, held tiles in LDS.
+//
+// Little's law sizing: at ~24.6 GB/s per CU (6.3 TB/s over 256 CUs) and a loaded HBM latency of
+// 2-4 us a CU needs ~100 KB of loads in flight. Holding the L tiles that wait for their SART weights
+// in registers (variants 0-2) leaves room for only ~2 tiles (64 KB) in flight and caps the sweep at
+// ~4 TB/s. Here each compute wave keeps AH = 4 tiles (4 x 8 KB) of loads in flight in VGPRs; once a
+// tile's row partials are reduced it is parked in an LDS ring (NL = L + 1 slots x 32 KB, each wave
+// only touches its own 8 KB per slot, so no barrier guards the ring) and read back L steps later for
+// the back-projection. 128 KB of loads in flight per CU, 128 KB of LDS.
+// ---------------------------------------------------------------------------------------------
+template <int K, bool LOG>
+__global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
+    const float* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
+    const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
+    double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg) {
+    constexpr int TK = 8;       // float4 per lane per tile (8 KB per wave, 32 KB per workgroup)
+    constexpr int T = TK / K;   // rows per tile
+    constexpr int L = 3;        // back-projection lag (steps)
+    constexpr int NL = L + 1;   // LDS ring slots
+    constexpr int AH = 4;       // tiles in flight
+    static_assert(T * K == TK, "tile must be whole rows");
 
+    // all LDS in the one dynamic region (16-B aligned base, cdna_hip_programming.md Guideline 17):
+    // [NL][4 waves][TK][64 lanes] float4 ring, then s_part[4][4][8] and s_w[4][8] floats
+    extern __shared__ __attribute__((aligned(16))) float4 s_ring[];
+    float(*s_part)[4][8] = reinterpret_cast<float(*)[4][8]>(s_ring + NL * 4 * TK * 64);
+    float(*s_w)[8] = reinterpret_cast<float(*)[8]>(reinterpret_cast<float*>(s_ring + NL * 4 * TK * 64) + 128);
+
+    if (st->done) return;
+    const int epoch = st->epoch;
+
+    const int b = blockIdx.x;
+    const int gi = b % I;
+    const int gj = b / I;
+    const int64_t ntiles = nrows_pad / T;
+    const int64_t t_begin = ntiles * gi / I;
+    const int64_t nt = ntiles * (gi + 1) / I - t_begin;
+    constexpr int UNR = 4;  // == AH (register slots are indexed statically)
+    const int64_t nsteps = (nt + L + UNR - 1) / UNR * UNR;
+
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t ld4 = ld >> 2;
+
+    if (wave < 4) {
+        const int64_t col4 = (int64_t)gj * (256 * K) + wave * (64 * K) + lane;
+        const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
+        const float4* __restrict__ a4 = reinterpret_cast<const float4*>(A) + col4;
+        float4* ring = s_ring + (wave * TK) * 64 + lane;  // + slot * (4 * TK * 64) + q * 64
+
+        float4 xs[K], acc[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            xs[k] = x4[col4 + k * 64];
+            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float4 fl[AH][TK];
+        auto load_tile = [&](float4(&dst)[TK], int64_t t) {
+            const float4* src = a4 + (t_begin + t) * T * ld4;
+#pragma unroll
+            for (int r = 0; r < T; ++r)
+#pragma unroll
+                for (int k = 0; k < K; ++k) dst[r * K + k] = src[r * ld4 + k * 64];
+        };
+#pragma unroll
+        for (int i = 0; i < AH; ++i)
+            if (i < nt) load_tile(fl[i], i);
+
+        auto step = [&](auto bbc, int64_t t) {
+            constexpr int bb = decltype(bbc)::value;  // register slot of tile t (t % AH)
+            if (t < nt) {
+#pragma unroll
+                for (int r = 0; r < T; ++r) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) s += dot4(fl[bb][r * K + k], xs[k]);
+                    s = wave_sum(s);
+                    if (lane == 0) s_part[t & 3][wave][r] = s;
+                }
+                float4* slot = ring + (int)(t % NL) * (4 * TK * 64);
+#pragma unroll
+                for (int q = 0; q < TK; ++q) slot[q * 64] = fl[bb][q];
+                if (t + AH < nt) load_tile(fl[bb], t + AH);
+            }
+            __syncthreads();
+            if (t >= L && t - L < nt) {
+                const int64_t u = t - L;
+                const float4* slot = ring + (int)(u % NL) * (4 * TK * 64);
+                const int ws = (int)(u & 3);
+#pragma unroll
+                for (int r = 0; r < T; ++r) {
+                    const float wr = s_w[ws][r];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) fma4(acc[k], slot[(r * K + k) * 64], wr);
+                }
+            }
+        };
+
+        for (int64_t t0 = 0; t0 < nsteps; t0 += UNR) {
+            step(std::integral_constant<int, 0>{}, t0 + 0);
+            step(std::integral_constant<int, 1>{}, t0 + 1);
+            step(std::integral_constant<int, 2>{}, t0 + 2);
+            step(std::integral_constant<int, 3>{}, t0 + 3);
+        }
+        float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld) + col4;
+#pragma unroll
+        for (int k = 0; k < K; ++k) out[k * 64] = acc[k];
+    } else {
+        const int n = J * T;
+        bool failed = false;
+        double F = 0.0;
+        uint64_t pv[2][kGatherRegs];
+
+        auto issue_poll = [&](uint64_t(&dst)[kGatherRegs], int64_t u) {
+            const uint64_t* g = gran + (t_begin + u) * (int64_t)n;
+#pragma unroll
+            for (int m = 0; m < kGatherRegs; ++m) {
+                const int idx = lane + 64 * m;
+                dst[m] = (idx < n) ? __hip_atomic_load(g + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : make_granule(epoch, 0.f);
+            }
+        };
+        auto finish_tile = [&](uint64_t(&v)[kGatherRegs], int64_t u) {
+            if (!failed) {
+                unsigned spins = 0;
+                while (true) {
+                    bool ok = true;
+#pragma unroll
+                    for (int m = 0; m < kGatherRegs; ++m) ok &= ((int)(v[m] >> 32) == epoch);
+                    if (__all(ok)) break;
+                    if (++spins > kSpinLimit) {
+                        failed = true;
+                        if (lane == 0) atomicOr(&st->error, 1);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    issue_poll(v, u);
+                }
+            }
+            float s = 0.f;
+            if (!failed) {
+#pragma unroll
+                for (int m = 0; m < kGatherRegs; ++m) s += __uint_as_float((uint32_t)v[m]);
+            }
+#pragma unroll
+            for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
+            if (lane < T) {
+                const int64_t row = (t_begin + u) * T + lane;
+                float w = 0.f;
+                if (row < nrows) {
+                    const float a = arow[row];
+                    w = LOG ? a * s : a * (ghat[row] - s);
+                    if (gj == 0) F += (double)s * (double)s;
+                }
+                s_w[u & 3][lane] = w;
+            }
+        };
+        auto xstep = [&](auto pc, int64_t t) {
+            constexpr int p = decltype(pc)::value;
+            __syncthreads();
+            if (dbg & 1) {  // ablation: no inter-workgroup exchange (timing diagnostics only)
+                if (lane < T) s_w[(t + 1) & 3][lane] = 0.f;
+                return;
+            }
+            if (t < nt && lane < T) {
+                const int ps = (int)(t & 3);
+                const float s = ((s_part[ps][0][lane] + s_part[ps][1][lane]) + s_part[ps][2][lane]) +
+                                s_part[ps][3][lane];
+                uint64_t* g = gran + ((t_begin + t) * J + gj) * T + lane;
+                __hip_atomic_store(g, make_granule(epoch, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const int64_t un = t - L + 2;
+            if (un >= 0 && un < nt) issue_poll(pv[p], un);
+            const int64_t uc = t - L + 1;
+            if (uc >= 0 && uc < nt) finish_tile(pv[p ^ 1], uc);
+        };
+        for (int64_t t0 = 0; t0 < nsteps; t0 += 2) {
+            xstep(std::integral_constant<int, 0>{}, t0);
+            xstep(std::integral_constant<int, 1>{}, t0 + 1);
+        }
+        F = wave_sum(F);
+        if (lane == 0) Fpart[b] = F;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Variant 4 (default for ld % 2048 == 0): "split rows" + barrier-free LDS hand-offs.
+//
+// Measured on MI355X (tools/probe.py, exchange disabled): the register/LDS pipeline of variant 3
+// streams at the HBM roof (6.2 TB/s) only when each wave performs ONE full-wave reduction per step;
+// with T rows per wave per step the T dependent shuffle reductions dominate. Here every compute wave
+// owns a different row of the 4-row tile over the same 2048-column slab (8 float4 per lane), so a
+// step costs one reduction per wave and no cross-wave partial sum.
+// The per-step __syncthreads of variants 0-3 coupled the compute waves to every jitter of the
+// inter-workgroup exchange; here compute and exchange waves hand off through LDS words tagged with
+// the tile index (written data-then-flag by one wave; LDS serves a wave's requests in order), so the
+// compute waves block only when the weight they need at step t (tile t - L) is not there yet.
+// ---------------------------------------------------------------------------------------------
+template <bool LOG>
+__global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
+    const float* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
+    const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
+    double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg) {
+    constexpr int KW = 8;        // float4 per lane per row: one wave covers 2048 columns
+    constexpr int T = 4;         // rows per tile (one per compute wave)
+    constexpr int L = 3;         // back-projection lag in steps
+    constexpr int NL = L + 1;    // LDS ring slots (32 KB each)
+    constexpr int AH = 4;        // tiles in flight per wave (4 x 8 KB)
+    constexpr int NS = 8;        // LDS hand-off slots
+
+    extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64]
+    float* s_small = reinterpret_cast<float*>(s_ring + NL * 4 * KW * 64);
+    volatile float* s_part = s_small;                                      // [NS][4]
+    volatile float* s_w = s_small + NS * 4;                                 // [NS][4]
+    volatile int* s_pflag = reinterpret_cast<volatile int*>(s_small + 2 * NS * 4);  // [NS][4]
+    volatile int* s_wflag = s_pflag + NS * 4;                               // [NS]
+
+    if (st->done) return;
+    const int epoch = st->epoch;
+    const int b = blockIdx.x;
+    const int gi = b % I;
+    const int gj = b / I;
+    const int64_t ntiles = nrows_pad / T;
+    const int64_t t_begin = ntiles * gi / I;
+    const int64_t nt = ntiles * (gi + 1) / I - t_begin;
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t ld4 = ld >> 2;
+
+    for (int i = threadIdx.x; i < NS * 4 + NS; i += kFusedThreads) s_pflag[i] = -1;
+    __syncthreads();
+
+    if (wave < 4) {
+        const int64_t col4 = (int64_t)gj * (64 * KW) + lane;  // + k * 64
+        const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
+        const float4* __restrict__ a4 = reinterpret_cast<const float4*>(A) + col4 + (int64_t)wave * ld4;
+        float4* ring = s_ring + (wave * KW) * 64 + lane;
+        float4 xs[KW], acc[KW];
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            xs[k] = x4[col4 + k * 64];
+            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float4 fl[AH][KW];
+        auto load_tile = [&](float4(&dst)[KW], int64_t t) {
+            const float4* src = a4 + (t_begin + t) * T * ld4;
+#pragma unroll
+            for (int k = 0; k < KW; ++k) dst[k] = src[k * 64];
+        };
+#pragma unroll
+        for (int i = 0; i < AH; ++i)
+            if (i < nt) load_tile(fl[i], i);
+        bool stuck = false;
+
+        auto step = [&](auto bbc, int64_t t) {
+            constexpr int bb = decltype(bbc)::value;
+            if (t < nt) {
+                float s = 0.f;
+#pragma unroll
+                for (int k = 0; k < KW; ++k) s += dot4(fl[bb][k], xs[k]);
+                s = wave_sum(s);
+                if (lane == 0) {
+                    s_part[(t & (NS - 1)) * 4 + wave] = s;
+                    asm volatile("" ::: "memory");
+                    s_pflag[(t & (NS - 1)) * 4 + wave] = (int)t;
+                }
+                float4* slot = ring + (int)(t % NL) * (4 * KW * 64);
+#pragma unroll
+                for (int k = 0; k < KW; ++k) slot[k * 64] = fl[bb][k];
+                if (t + AH < nt) load_tile(fl[bb], t + AH);
+            }
+            if (t >= L && t - L < nt) {
+                const int64_t u = t - L;
+                const int ws = (int)(u & (NS - 1));
+                unsigned spins = 0;
+                while (s_wflag[ws] != (int)u && !stuck) {
+                    if (++spins > kSpinLimit) {
+                        stuck = true;
+                        if (lane == 0) atomicOr(&st->error, 2);
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                asm volatile("" ::: "memory");
+                const float wr = s_w[ws * 4 + wave];
+                const float4* slot = ring + (int)(u % NL) * (4 * KW * 64);
+#pragma unroll
+                for (int k = 0; k < KW; ++k) fma4(acc[k], slot[k * 64], wr);
+            }
+        };
+        for (int64_t t0 = 0; t0 < nt + L; t0 += AH) {
+            step(std::integral_constant<int, 0>{}, t0 + 0);
+            step(std::integral_constant<int, 1>{}, t0 + 1);
+            step(std::integral_constant<int, 2>{}, t0 + 2);
+            step(std::integral_constant<int, 3>{}, t0 + 3);
+        }
+        // the four waves hold partial sums of the same 2048 columns: combine through LDS
+        __syncthreads();
+        float4* red = s_ring + (wave * KW) * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) red[k * 64] = acc[k];
+        __syncthreads();
+        float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld) + col4;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int k = wave * 2 + kk;
+            float4 v = s_ring[(0 * KW + k) * 64 + lane];
+#pragma unroll
+            for (int ww = 1; ww < 4; ++ww) {
+                const float4 o = s_ring[(ww * KW + k) * 64 + lane];
+                v.x += o.x;
+                v.y += o.y;
+                v.z += o.z;
+                v.w += o.w;
+            }
+            out[k * 64] = v;
+        }
+    } else {
+        const int n = J * T;
+        bool failed = false;
+        double F = 0.0;
+        uint64_t pv[2][kGatherRegs];
+        auto issue_poll = [&](uint64_t(&dst)[kGatherRegs], int64_t u) {
+            const uint64_t* g = gran + (t_begin + u) * (int64_t)n;
+#pragma unroll
+            for (int m = 0; m < kGatherRegs; ++m) {
+                const int idx = lane + 64 * m;
+                dst[m] = (idx < n) ? __hip_atomic_load(g + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : make_granule(epoch, 0.f);
+            }
+        };
+        auto finish_tile = [&](uint64_t(&v)[kGatherRegs], int64_t u) {
+            if (!failed && !(dbg & 1)) {
+                unsigned spins = 0;
+                while (true) {
+                    bool ok = true;
+#pragma unroll
+                    for (int m = 0; m < kGatherRegs; ++m) ok &= ((int)(v[m] >> 32) == epoch);
+                    if (__all(ok)) break;
+                    if (++spins > kSpinLimit) {
+                        failed = true;
+                        if (lane == 0) atomicOr(&st->error, 1);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    issue_poll(v, u);
+                }
+            }
+            float s = 0.f;
+            if (!failed && !(dbg & 1)) {
+#pragma unroll
+                for (int m = 0; m < kGatherRegs; ++m) s += __uint_as_float((uint32_t)v[m]);
+            }
+#pragma unroll
+            for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
+            const int ws = (int)(u & (NS - 1));
+            if (lane < T) {
+                const int64_t row = (t_begin + u) * T + lane;
+                float w = 0.f;
+                if (row < nrows) {
+                    const float a = arow[row];
+                    w = LOG ? a * s : a * (ghat[row] - s);
+                    if (gj == 0) F += (double)s * (double)s;
+                }
+                s_w[ws * 4 + lane] = w;
+            }
+            asm volatile("" ::: "memory");
+            if (lane == 0) s_wflag[ws] = (int)u;
+        };
+        auto xiter = [&](auto pc, int64_t u) {
+            constexpr int p = decltype(pc)::value;  // pv[p] receives tile u-1
+            if (u < nt) {
+                const int ps = (int)(u & (NS - 1));
+                if (lane < T) {
+                    unsigned spins = 0;
+                    while (s_pflag[ps * 4 + lane] != (int)u) {
+                        if (++spins > kSpinLimit) break;  // compute waves always publish: cannot trigger
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    asm volatile("" ::: "memory");
+                    const float sv = s_part[ps * 4 + lane];
+                    if (!(dbg & 1)) {
+                        uint64_t* g = gran + ((t_begin + u) * J + gj) * T + lane;
+                        __hip_atomic_store(g, make_granule(epoch, sv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+            if (u >= 1 && u - 1 < nt && !(dbg & 1)) issue_poll(pv[p], u - 1);
+            if (u >= 2 && u - 2 < nt) finish_tile(pv[p ^ 1], u - 2);
+        };
+        for (int64_t u0 = 0; u0 < nt + 2; u0 += 2) {
+            xiter(std::integral_constant<int, 0>{}, u0);
+            xiter(std::integral_constant<int, 1>{}, u0 + 1);
+        }
+        F = wave_sum(F);
+        if (lane == 0) Fpart[b] = F;
+        __syncthreads();  // matches the compute waves' first combine barrier
+        __syncthreads();  // and the second
+    }
+}
+
+constexpr size_t kRowsLdsBytes = 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (8 * 4 * 3 + 8) * sizeof(float);
+
+// ---------------------------------------------------------------------------------------------
+// Variant 5 (default): variant 4 + compute waves publish their own granules + two exchange waves.
+//
+// A granule hand-off under full HBM streaming load takes 2-3.5 us (MI355X_MICROARCH.md price list,
+// 'handoff-1to1'), two to three 32 KB steps. With one exchange wave serving every tile, the poll of
+// tile u could only be issued one step after the tile was published and had to be consumed one step
+// later; every late peer stalled the sweep. Here the compute wave that owns row r of a tile stores
+// that row's granule itself (one sc1 store from lane 0 right after its reduction), and two exchange
+// waves take alternate tiles: exchange wave e polls tile u (u % 2 == e) once its own workgroup has
+// produced tile u + 1 and may block on that poll for two steps before the weights are due.
+// ---------------------------------------------------------------------------------------------
+constexpr int kFused5Threads = 384;  // 4 compute waves + 2 exchange waves
+
+template <bool LOG>
+__global__ __launch_bounds__(kFused5Threads) void k_fused_sweep_rows2(
+    const float* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
+    const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
+    double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg) {
+    constexpr int KW = 8, T = 4, L = 3, NL = L + 1, AH = 4, NS = 8;
+
+    extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64]
+    float* s_small = reinterpret_cast<float*>(s_ring + NL * 4 * KW * 64);
+    volatile float* s_w = s_small;                                                  // [NS][4]
+    volatile int* s_pflag = reinterpret_cast<volatile int*>(s_small + NS * 4);      // [NS][4]
+    volatile int* s_wflag = s_pflag + NS * 4;                                       // [NS]
+
+    if (st->done) return;
+    const int epoch = st->epoch;
+    const int b = blockIdx.x;
+    const int gi = b % I;
+    const int gj = b / I;
+    const int64_t ntiles = nrows_pad / T;
+    const int64_t t_begin = ntiles * gi / I;
+    const int64_t nt = ntiles * (gi + 1) / I - t_begin;
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int64_t ld4 = ld >> 2;
+    const bool exchange = !(dbg & 1);
+
+    for (int i = threadIdx.x; i < NS * 4 + NS; i += kFused5Threads) s_pflag[i] = -1;
+    __syncthreads();
+
+    if (wave < 4) {
+        const int64_t col4 = (int64_t)gj * (64 * KW) + lane;
+        const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
+        const float4* __restrict__ a4 = reinterpret_cast<const float4*>(A) + col4 + (int64_t)wave * ld4;
+        float4* ring = s_ring + (wave * KW) * 64 + lane;
+        uint64_t* gmine = gran + (int64_t)gj * T + wave;  // + tile * J * T
+        float4 xs[KW], acc[KW];
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            xs[k] = x4[col4 + k * 64];
+            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float4 fl[AH][KW];
+        auto load_tile = [&](float4(&dst)[KW], int64_t t) {
+            const float4* src = a4 + (t_begin + t) * T * ld4;
+#pragma unroll
+            for (int k = 0; k < KW; ++k) dst[k] = src[k * 64];
+        };
+#pragma unroll
+        for (int i = 0; i < AH; ++i)
+            if (i < nt) load_tile(fl[i], i);
+        bool stuck = false;
+
+        auto step = [&](auto bbc, int64_t t) {
+            constexpr int bb = decltype(bbc)::value;
+            if (t < nt) {
+                float s = 0.f;
+#pragma unroll
+                for (int k = 0; k < KW; ++k) s += dot4(fl[bb][k], xs[k]);
+                s = wave_sum(s);
+                if (lane == 0) {
+                    if (exchange)
+                        __hip_atomic_store(gmine + (t_begin + t) * J * T, make_granule(epoch, s), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    s_pflag[(t & (NS - 1)) * 4 + wave] = (int)t;
+                }
+                float4* slot = ring + (int)(t % NL) * (4 * KW * 64);
+#pragma unroll
+                for (int k = 0; k < KW; ++k) slot[k * 64] = fl[bb][k];
+                if (t + AH < nt) load_tile(fl[bb], t + AH);
+            }
+            if (t >= L && t - L < nt) {
+                const int64_t u = t - L;
+                const int ws = (int)(u & (NS - 1));
+                unsigned spins = 0;
+                while (s_wflag[ws] != (int)u && !stuck) {
+                    if (++spins > kSpinLimit) {
+                        stuck = true;
+                        if (lane == 0) atomicOr(&st->error, 2);
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                asm volatile("" ::: "memory");
+                const float wr = s_w[ws * 4 + wave];
+                const float4* slot = ring + (int)(u % NL) * (4 * KW * 64);
+#pragma unroll
+                for (int k = 0; k < KW; ++k) fma4(acc[k], slot[k * 64], wr);
+            }
+        };
+        for (int64_t t0 = 0; t0 < nt + L; t0 += AH) {
+            step(std::integral_constant<int, 0>{}, t0 + 0);
+            step(std::integral_constant<int, 1>{}, t0 + 1);
+            step(std::integral_constant<int, 2>{}, t0 + 2);
+            step(std::integral_constant<int, 3>{}, t0 + 3);
+        }
+        __syncthreads();
+        float4* red = s_ring + (wave * KW) * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) red[k * 64] = acc[k];
+        __syncthreads();
+        float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld) + col4;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int k = wave * 2 + kk;
+            float4 v = s_ring[(0 * KW + k) * 64 + lane];
+#pragma unroll
+            for (int ww = 1; ww < 4; ++ww) {
+                const float4 o = s_ring[(ww * KW + k) * 64 + lane];
+                v.x += o.x;
+                v.y += o.y;
+                v.z += o.z;
+                v.w += o.w;
+            }
+            out[k * 64] = v;
+        }
+    } else {
+        const int e = wave - 4;  // this exchange wave serves tiles u % 2 == e
+        const int n = J * T;
+        bool failed = false;
+        double F = 0.0;
+        for (int64_t u = e; u < nt; u += 2) {
+            // trigger: this workgroup has reduced tile u + 1 (tile u itself for the last tile)
+            const int64_t trig = (u + 1 < nt) ? u + 1 : u;
+            const int tsl = (int)(trig & (NS - 1));
+            if (lane < 4) {
+                unsigned spins = 0;
+                while (s_pflag[tsl * 4 + lane] < (int)trig) {
+                    if (++spins > kSpinLimit) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            const int64_t row = (t_begin + u) * T + (lane & 3);
+            const float a = (lane < T && row < nrows) ? arow[row] : 0.f;
+            const float gh = (lane < T && row < nrows) ? ghat[row] : 0.f;
+            float s = 0.f;
+            if (exchange) {
+                const uint64_t* g = gran + (t_begin + u) * (int64_t)n;
+                uint64_t v[kGatherRegs];
+                unsigned spins = 0;
+                while (!failed) {
+                    bool ok = true;
+#pragma unroll
+                    for (int m = 0; m < kGatherRegs; ++m) {
+                        const int idx = lane + 64 * m;
+                        v[m] = (idx < n) ? __hip_atomic_load(g + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                         : make_granule(epoch, 0.f);
+                    }
+#pragma unroll
+                    for (int m = 0; m < kGatherRegs; ++m) ok &= ((int)(v[m] >> 32) == epoch);
+                    if (__all(ok)) {
+#pragma unroll
+                        for (int m = 0; m < kGatherRegs; ++m) s += __uint_as_float((uint32_t)v[m]);
+                        break;
+                    }
+                    if (++spins > kSpinLimit) {
+                        failed = true;
+                        if (lane == 0) atomicOr(&st->error, 1);
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+#pragma unroll
+            for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
+            const int ws = (int)(u & (NS - 1));
+            if (lane < T) {
+                float w = 0.f;
+                if (row < nrows) {
+                    w = LOG ? a * s : a * (gh - s);
+                    if (gj == 0) F += (double)s * (double)s;
+                }
+                s_w[ws * 4 + lane] = w;
+            }
+            asm volatile("" ::: "memory");
+            if (lane == 0) s_wflag[ws] = (int)u;
+        }
+        F = wave_sum(F);
+        if (lane == 0) Fpart[2 * b + e] = F;
+        __syncthreads();
+        __syncthreads();
+    }
+}
+
+constexpr size_t kRows2LdsBytes = 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (8 * 4 * 2 + 8) * sizeof(float);
+
+static int g_fused_dbg = 0;  // diagnostics only (set through fused_set_debug)
+void fused_set_debug(int flags) { g_fused_dbg = flags; }
+
+constexpr size_t kLdsRingBytes = 4 /*NL*/ * 4 /*waves*/ * 8 /*TK*/ * 64 * sizeof(float4) + 160 * sizeof(float);
+
+// ---------------------------------------------------------------------------------------------
+// Host side. Variants trade register ring depth (latency hiding) against occupancy:
+//   variant 0: TK=8, R=5, L=3      (default)
+//   variant 1: TK=8, R=4, L=2      (shallow ring)
+//   variant 2: TK=4, R=8, L=4      (small tiles, deep ring; K <= 4)
+// ---------------------------------------------------------------------------------------------
 int fused_pick_k(int64_t ld) {
-    // Aim for ~32 slabs (one XCD's CUs share a row group), slabs of 1024..8192 columns.
     for (int K = 1; K <= 8; K *= 2) {
         const int64_t wc = 1024 * (int64_t)K;
         if (ld % wc != 0) return K > 1 ? K / 2 : 0;
@@ -204,31 +834,143 @@ int fused_pick_k(int64_t ld) {
     return 8;
 }
 
-void launch_fused_sweep(bool logmode, int K, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
-                        const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
-                        uint64_t* gran, int I, int J, SartState* st, hipStream_t stream) {
-    if (K != 1 && K != 2 && K != 4 && K != 8) throw std::runtime_error("fused_sweep: K must be 1, 2, 4 or 8");
-    if (ld % (1024 * K) != 0 || ld / (1024 * K) != J)
-        throw std::runtime_error("fused_sweep: ld must equal J * 1024 * K");
-    if (nrows_pad % (8 / K) != 0) throw std::runtime_error("fused_sweep: padded rows must be a multiple of the tile");
-    if (J * (8 / K) > 2048) throw std::runtime_error("fused_sweep: too many slabs for the exchange buffer");
-    const dim3 grid((unsigned)(I * J)), block(kFusedThreads);
-#define SART_FUSED_CASE(KK)                                                                                        \
-    case KK:                                                                                                       \
-        if (logmode)                                                                                               \
-            hipLaunchKernelGGL((k_fused_sweep<KK, true>), grid, block, 0, stream, A, ld, nrows, nrows_pad, x, ghat, \
-                               arow, partial, Fpart, gran, I, J, st);                                              \
-        else                                                                                                       \
-            hipLaunchKernelGGL((k_fused_sweep<KK, false>), grid, block, 0, stream, A, ld, nrows, nrows_pad, x,      \
-                               ghat, arow, partial, Fpart, gran, I, J, st);                                        \
-        break;
-    switch (K) {
-        SART_FUSED_CASE(1)
-        SART_FUSED_CASE(2)
-        SART_FUSED_CASE(4)
-        SART_FUSED_CASE(8)
+template <int K, int TK, int R, int L>
+static void launch_cfg(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
+                       int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
+                       double* Fpart, uint64_t* gran, int I, int J, SartState* st) {
+    if (logmode)
+        hipLaunchKernelGGL((k_fused_sweep<K, TK, R, L, true>), grid, dim3(kFusedThreads), 0, stream, A, ld, nrows,
+                           nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st);
+    else
+        hipLaunchKernelGGL((k_fused_sweep<K, TK, R, L, false>), grid, dim3(kFusedThreads), 0, stream, A, ld, nrows,
+                           nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st);
+}
+
+template <int K>
+static void launch_lds(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
+                       int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
+                       double* Fpart, uint64_t* gran, int I, int J, SartState* st) {
+    static bool configured = false;
+    if (!configured) {  // opt in to > 64 KiB of dynamic LDS once per instantiation
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_lds<K, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsRingBytes);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_lds<K, false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsRingBytes);
+        configured = true;
     }
-#undef SART_FUSED_CASE
+    if (logmode)
+        hipLaunchKernelGGL((k_fused_sweep_lds<K, true>), grid, dim3(kFusedThreads), kLdsRingBytes, stream, A, ld,
+                           nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
+    else
+        hipLaunchKernelGGL((k_fused_sweep_lds<K, false>), grid, dim3(kFusedThreads), kLdsRingBytes, stream, A, ld,
+                           nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
+}
+
+static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
+                        int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
+                        double* Fpart, uint64_t* gran, int I, int J, SartState* st) {
+    static bool configured = false;
+    if (!configured) {
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRowsLdsBytes);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRowsLdsBytes);
+        configured = true;
+    }
+    if (logmode)
+        hipLaunchKernelGGL((k_fused_sweep_rows<true>), grid, dim3(kFusedThreads), kRowsLdsBytes, stream, A, ld, nrows,
+                           nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
+    else
+        hipLaunchKernelGGL((k_fused_sweep_rows<false>), grid, dim3(kFusedThreads), kRowsLdsBytes, stream, A, ld,
+                           nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
+}
+
+static void launch_rows2(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
+                         int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
+                         double* Fpart, uint64_t* gran, int I, int J, SartState* st) {
+    static bool configured = false;
+    if (!configured) {
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows2<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRows2LdsBytes);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows2<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRows2LdsBytes);
+        configured = true;
+    }
+    if (logmode)
+        hipLaunchKernelGGL((k_fused_sweep_rows2<true>), grid, dim3(kFused5Threads), kRows2LdsBytes, stream, A, ld,
+                           nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
+    else
+        hipLaunchKernelGGL((k_fused_sweep_rows2<false>), grid, dim3(kFused5Threads), kRows2LdsBytes, stream, A, ld,
+                           nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
+}
+
+template <int K>
+static void launch_k(int variant, bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld,
+                     int64_t nrows, int64_t nrows_pad, const float* x, const float* ghat, const float* arow,
+                     float* partial, double* Fpart, uint64_t* gran, int I, int J, SartState* st) {
+    if (variant == 3)
+        launch_lds<K>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st);
+    else if (variant == 1)
+        launch_cfg<K, 8, 4, 2>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I,
+                               J, st);
+    else if (variant == 2 && K <= 4) {
+        if constexpr (K <= 4)
+            launch_cfg<K, 4, 8, 4>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart,
+                                   gran, I, J, st);
+    } else
+        launch_cfg<K, 8, 5, 3>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I,
+                               J, st);
+}
+
+int fused_fpart_per_block(int variant) { return variant == 5 ? 2 : 1; }
+
+int fused_tile_rows(int K, int variant) {
+    if (variant == 4 || variant == 5) return 4;
+    return (variant == 2 && K <= 4) ? 4 / K : 8 / K;
+}
+
+void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows,
+                        int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
+                        double* Fpart, uint64_t* gran, int I, int J, SartState* st, hipStream_t stream) {
+    if (variant != 4 && variant != 5) {
+        if (K != 1 && K != 2 && K != 4 && K != 8) throw std::runtime_error("fused_sweep: K must be 1, 2, 4 or 8");
+        if (ld % (1024 * K) != 0 || ld / (1024 * K) != J)
+            throw std::runtime_error("fused_sweep: ld must equal J * 1024 * K");
+    }
+    const int T = fused_tile_rows(K, variant);
+    if (nrows_pad % T != 0) throw std::runtime_error("fused_sweep: padded rows must be a multiple of the tile");
+    if (J * T > kMaxGather) throw std::runtime_error("fused_sweep: too many slabs for the gather registers");
+    const dim3 grid((unsigned)(I * J));
+    if (variant == 4 || variant == 5) {
+        if (ld % 2048 != 0 || ld / 2048 != J) throw std::runtime_error("fused_sweep v4/5: ld must equal J * 2048");
+        if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v4/5: padded rows must be a multiple of 4");
+        if (J * 4 > kMaxGather) throw std::runtime_error("fused_sweep v4/5: too many slabs");
+        if (variant == 4)
+            launch_rows(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st);
+        else
+            launch_rows2(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J,
+                         st);
+        check_launch("k_fused_sweep_rows");
+        return;
+    }
+    switch (K) {
+        case 1:
+            launch_k<1>(variant, logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
+                        I, J, st);
+            break;
+        case 2:
+            launch_k<2>(variant, logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
+                        I, J, st);
+            break;
+        case 4:
+            launch_k<4>(variant, logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
+                        I, J, st);
+            break;
+        case 8:
+            launch_k<8>(variant, logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
+                        I, J, st);
+            break;
+    }
     check_launch("k_fused_sweep");
 }
 

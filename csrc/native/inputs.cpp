@@ -1,0 +1,361 @@
+#include "inputs.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <numeric>
+#include <sstream>
+
+namespace sart {
+
+#ifdef SART_HAVE_HDF5
+
+namespace {
+
+std::string fmt_double(double v) {
+    std::ostringstream os;
+    os << v;
+    return os.str();
+}
+
+struct VoxelMapData {
+    uint64_t nx = 0, ny = 0, nz = 0;
+    std::vector<uint64_t> i, j, k;
+};
+
+VoxelMapData read_voxel_map_indices(hid_t f) {
+    VoxelMapData m;
+    m.nx = h5_attr_u64(f, "rtm/voxel_map", "nx");
+    m.ny = h5_attr_u64(f, "rtm/voxel_map", "ny");
+    m.nz = h5_attr_u64(f, "rtm/voxel_map", "nz");
+    m.i = h5_read_u64(f, "rtm/voxel_map/i");
+    m.j = h5_read_u64(f, "rtm/voxel_map/j");
+    m.k = h5_read_u64(f, "rtm/voxel_map/k");
+    if (m.j.size() != m.i.size() || m.k.size() != m.i.size()) throw Error("Inconsistent voxel map index arrays.");
+    return m;
+}
+
+}  // namespace
+
+void categorize_input_files(const std::vector<std::string>& input_files, std::vector<std::string>& rtm_files,
+                            std::vector<std::string>& image_files) {
+    for (const auto& path : input_files) {
+        H5Id f = h5_open_file(path);
+        if (h5_exists(f, "rtm"))
+            rtm_files.push_back(path);
+        else if (h5_exists(f, "image"))
+            image_files.push_back(path);
+        else
+            throw Error("The file " + path + " is neither an RTM file nor an image file.");
+    }
+}
+
+void check_group_attribute_consistency(const std::vector<std::string>& files, const std::string& group,
+                                       const std::vector<std::string>& names, bool integer) {
+    if (files.empty()) return;
+    std::vector<double> ref_d(names.size());
+    std::vector<uint64_t> ref_u(names.size());
+    {
+        H5Id f = h5_open_file(files.front());
+        for (size_t a = 0; a < names.size(); ++a) {
+            if (integer)
+                ref_u[a] = h5_attr_u64(f, group, names[a]);
+            else
+                ref_d[a] = h5_attr_double(f, group, names[a]);
+        }
+    }
+    for (size_t n = 1; n < files.size(); ++n) {
+        H5Id f = h5_open_file(files[n]);
+        for (size_t a = 0; a < names.size(); ++a) {
+            bool same;
+            std::string sv, sr;
+            if (integer) {
+                const uint64_t v = h5_attr_u64(f, group, names[a]);
+                same = v == ref_u[a];
+                sv = std::to_string(v);
+                sr = std::to_string(ref_u[a]);
+            } else {
+                const double v = h5_attr_double(f, group, names[a]);
+                same = v == ref_d[a];
+                sv = fmt_double(v);
+                sr = fmt_double(ref_d[a]);
+            }
+            if (!same)
+                throw Error("Different " + names[a] + " values in " + files[n] + " (" + sv + ") and in " +
+                            files.front() + " (" + sr + ").");
+        }
+    }
+}
+
+SortedRtmFiles sort_rtm_files(const std::vector<std::string>& files) {
+    std::map<std::string, std::map<uint64_t, std::string>> by_camera;
+    for (const auto& path : files) {
+        H5Id f = h5_open_file(path);
+        const std::string cam = h5_attr_string(f, "rtm", "camera_name");
+        const VoxelMapData m = read_voxel_map_indices(f);
+        uint64_t imin = m.nx * m.ny * m.nz;
+        for (size_t n = 0; n < m.i.size(); ++n) imin = std::min(imin, m.i[n] * m.ny * m.nz + m.j[n] * m.nz + m.k[n]);
+        by_camera[cam][imin] = path;
+    }
+    SortedRtmFiles out;
+    for (auto& [cam, segs] : by_camera) {
+        auto& v = out[cam];
+        for (auto& [key, path] : segs) v.push_back(path);
+    }
+    return out;
+}
+
+void check_rtm_frame_consistency(const SortedRtmFiles& sorted) {
+    for (const auto& [cam, files] : sorted) {
+        if (files.size() < 2) continue;
+        std::vector<int32_t> ref;
+        std::vector<hsize_t> ref_dims;
+        for (size_t n = 0; n < files.size(); ++n) {
+            H5Id f = h5_open_file(files[n]);
+            H5Id d = h5_open_dataset(f, "rtm/frame_mask");
+            const auto dims = h5_dims(d);
+            auto mask = h5_read_i32(f, "rtm/frame_mask");
+            if (n == 0) {
+                ref = std::move(mask);
+                ref_dims = dims;
+            } else if (mask != ref || dims != ref_dims) {
+                throw Error("RTM files for " + cam + " view have different frame masks.");
+            }
+        }
+    }
+}
+
+void check_rtm_voxel_consistency(const SortedRtmFiles& sorted) {
+    std::vector<int64_t> ref_map;
+    std::string ref_cam;
+    for (const auto& [cam, files] : sorted) {
+        uint64_t nx, ny, nz;
+        {
+            H5Id f0 = h5_open_file(files.front());
+            nx = h5_attr_u64(f0, "rtm/voxel_map", "nx");
+            ny = h5_attr_u64(f0, "rtm/voxel_map", "ny");
+            nz = h5_attr_u64(f0, "rtm/voxel_map", "nz");
+        }
+        std::vector<int64_t> vmap(nx * ny * nz, -1);
+        int64_t offset = 0;
+        for (const auto& path : files) {
+            H5Id f = h5_open_file(path);
+            const int64_t nvox = h5_attr_i64(f, "rtm", "nvoxel");
+            const VoxelMapData m = read_voxel_map_indices(f);
+            const auto value = h5_read_i64(f, "rtm/voxel_map/value");
+            if (value.size() != m.i.size()) throw Error("Inconsistent voxel map value array in " + path + ".");
+            for (size_t n = 0; n < m.i.size(); ++n) {
+                const uint64_t flat = m.i[n] * ny * nz + m.j[n] * nz + m.k[n];
+                if (flat >= vmap.size()) throw Error("Voxel map index out of range in " + path + ".");
+                if (vmap[flat] >= 0)
+                    throw Error("RTM segments for " + cam + " view have overlapping voxel maps at element (" +
+                                std::to_string(m.i[n]) + "," + std::to_string(m.j[n]) + "," +
+                                std::to_string(m.k[n]) + ").");
+                vmap[flat] = value[n] + offset;
+            }
+            offset += nvox;
+        }
+        if (ref_map.empty() && ref_cam.empty()) {
+            ref_map = std::move(vmap);
+            ref_cam = cam;
+        } else if (vmap != ref_map) {
+            throw Error("RTM files for " + cam + " and " + ref_cam + " views have different voxel maps.");
+        }
+    }
+}
+
+std::map<std::string, std::vector<int32_t>> read_rtm_frame_masks(const SortedRtmFiles& sorted) {
+    std::map<std::string, std::vector<int32_t>> out;
+    for (const auto& [cam, files] : sorted) {
+        H5Id f = h5_open_file(files.front());
+        out[cam] = h5_read_i32(f, "rtm/frame_mask");
+    }
+    return out;
+}
+
+std::map<std::string, std::pair<uint64_t, uint64_t>> read_rtm_frame_shapes(const SortedRtmFiles& sorted) {
+    std::map<std::string, std::pair<uint64_t, uint64_t>> out;
+    for (const auto& [cam, files] : sorted) {
+        H5Id f = h5_open_file(files.front());
+        H5Id d = h5_open_dataset(f, "rtm/frame_mask");
+        const auto dims = h5_dims(d);
+        if (dims.size() != 2) throw Error("rtm/frame_mask must be 2-D in " + files.front() + ".");
+        out[cam] = {dims[0], dims[1]};
+    }
+    return out;
+}
+
+SortedImageFiles sort_image_files(const std::vector<std::string>& files) {
+    SortedImageFiles out;
+    for (const auto& path : files) {
+        H5Id f = h5_open_file(path);
+        const std::string cam = h5_attr_string(f, "image", "camera_name");
+        auto it = out.find(cam);
+        if (it != out.end())
+            throw Error("Image files " + path + " and " + it->second + " share the same diagnostic view: " + cam + ".");
+        out[cam] = path;
+    }
+    return out;
+}
+
+void check_rtm_image_consistency(const SortedRtmFiles& rtm, const SortedImageFiles& images,
+                                 const std::string& rtm_name, double wavelength_threshold) {
+    for (const auto& kv : rtm)
+        if (!images.count(kv.first)) throw Error("No image file for " + kv.first + " camera.");
+    for (const auto& kv : images)
+        if (!rtm.count(kv.first)) throw Error("No RTM file for " + kv.first + " camera.");
+    if (rtm.empty()) return;
+    {
+        H5Id rf = h5_open_file(rtm.begin()->second.front());
+        H5Id imf = h5_open_file(images.begin()->second);
+        const double rw = h5_attr_double(rf, "rtm/" + rtm_name, "wavelength");
+        const double iw = h5_attr_double(imf, "image", "wavelength");
+        if (std::abs(rw - iw) > wavelength_threshold)
+            throw Error("RTM wavelength (" + fmt_double(rw) + " nm) is not within " + fmt_double(wavelength_threshold) +
+                        " nm threshold from image wavelength (" + fmt_double(iw) + " nm).");
+    }
+    for (const auto& [cam, files] : rtm) {
+        H5Id rf = h5_open_file(files.front());
+        H5Id md = h5_open_dataset(rf, "rtm/frame_mask");
+        const auto mdims = h5_dims(md);
+        H5Id imf = h5_open_file(images.at(cam));
+        H5Id fd = h5_open_dataset(imf, "image/frame");
+        const auto fdims = h5_dims(fd);
+        if (mdims.size() != 2 || fdims.size() != 3 || fdims[1] != mdims[0] || fdims[2] != mdims[1]) {
+            const auto s = [](const std::vector<hsize_t>& d, size_t a, size_t b) {
+                return (d.size() > std::max(a, b)) ? std::to_string(d[b]) + "x" + std::to_string(d[a]) : std::string("?");
+            };
+            throw Error("RTM for " + cam + " view was calculated for resolution " + s(mdims, 0, 1) +
+                        ", but the camera image has resolution " + s(fdims, 1, 2) + ".");
+        }
+    }
+}
+
+std::pair<uint64_t, uint64_t> get_total_rtm_size(const SortedRtmFiles& sorted) {
+    uint64_t npixel = 0, nvoxel = 0;
+    for (const auto& [cam, files] : sorted) {
+        H5Id f = h5_open_file(files.front());
+        npixel += h5_attr_u64(f, "rtm", "npixel");
+    }
+    if (!sorted.empty())
+        for (const auto& path : sorted.begin()->second) {
+            H5Id f = h5_open_file(path);
+            nvoxel += h5_attr_u64(f, "rtm", "nvoxel");
+        }
+    return {npixel, nvoxel};
+}
+
+bool rtm_has_sparse(const SortedRtmFiles& sorted, const std::string& rtm_name) {
+    for (const auto& [cam, files] : sorted)
+        for (const auto& path : files) {
+            H5Id f = h5_open_file(path);
+            if (h5_attr_i64(f, "rtm/" + rtm_name, "is_sparse")) return true;
+        }
+    return false;
+}
+
+void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, uint64_t nvoxel, uint64_t row_begin,
+                   uint64_t row_end, float* out, uint64_t ld) {
+    if (row_end <= row_begin) return;
+    if (ld < nvoxel) throw Error("read_rtm_rows: ld < nvoxel");
+    const std::string grp = "rtm/" + rtm_name;
+    uint64_t start_pixel = 0;
+    for (const auto& [cam, files] : sorted) {
+        uint64_t npix;
+        {
+            H5Id f0 = h5_open_file(files.front());
+            npix = h5_attr_u64(f0, "rtm", "npixel");
+        }
+        const uint64_t cam_end = start_pixel + npix;
+        if (cam_end > row_begin && start_pixel < row_end) {
+            const uint64_t lr0 = std::max(row_begin, start_pixel) - start_pixel;  // camera-local rows
+            const uint64_t lr1 = std::min(row_end, cam_end) - start_pixel;
+            uint64_t start_voxel = 0;
+            for (const auto& path : files) {
+                H5Id f = h5_open_file(path);
+                const uint64_t nvox_seg = h5_attr_u64(f, "rtm", "nvoxel");
+                if (start_voxel + nvox_seg > nvoxel) throw Error("RTM segments exceed the total number of voxels.");
+                const int64_t sparse = h5_attr_i64(f, grp, "is_sparse");
+                if (sparse) {
+                    const auto pix = h5_read_u64(f, grp + "/pixel_index");
+                    const auto vox = h5_read_u64(f, grp + "/voxel_index");
+                    const auto val = h5_read_f32(f, grp + "/value");
+                    if (pix.size() != val.size() || vox.size() != val.size())
+                        throw Error("Inconsistent sparse RTM arrays in " + path + ".");
+                    for (size_t n = 0; n < val.size(); ++n) {
+                        if (pix[n] < lr0 || pix[n] >= lr1) continue;
+                        if (vox[n] >= nvox_seg) throw Error("Sparse RTM voxel index out of range in " + path + ".");
+                        const uint64_t row = start_pixel + pix[n] - row_begin;
+                        out[row * ld + start_voxel + vox[n]] = val[n];
+                    }
+                } else {
+                    H5Id d = h5_open_dataset(f, grp + "/value");
+                    const auto dims = h5_dims(d);
+                    if (dims.size() != 2 || dims[0] != npix || dims[1] != nvox_seg)
+                        throw Error("Dense RTM dataset in " + path + " has unexpected shape.");
+                    // row blocks of <= 64 MiB per hyperslab read (the reference reads one row per call,
+                    // raytransfer.cpp:103-109)
+                    const uint64_t rows_per_read = std::max<uint64_t>(1, (64ull << 20) / (4 * std::max<uint64_t>(1, nvox_seg)));
+                    for (uint64_t r = lr0; r < lr1; r += rows_per_read) {
+                        const uint64_t n = std::min(rows_per_read, lr1 - r);
+                        h5_read_rows_f32(d, r, n, nvox_seg, out + (start_pixel + r - row_begin) * ld, ld, start_voxel);
+                    }
+                }
+                start_voxel += nvox_seg;
+            }
+        }
+        start_pixel = cam_end;
+        if (start_pixel >= row_end) break;
+    }
+}
+
+LaplacianCOO read_laplacian(const std::string& path, uint64_t expected_nvoxel) {
+    H5Id f = h5_open_file(path);
+    LaplacianCOO L;
+    L.nvoxel = h5_attr_u64(f, "laplacian", "nvoxel");
+    if (L.nvoxel != expected_nvoxel) throw Error("Laplacian and ray-transfer matrices have different number of voxels.");
+    auto val = h5_read_f32(f, "laplacian/value");
+    auto ii = h5_read_u64(f, "laplacian/i");
+    auto jj = h5_read_u64(f, "laplacian/j");
+    if (ii.size() != val.size() || jj.size() != val.size()) throw Error("Inconsistent Laplacian arrays in " + path + ".");
+    const uint64_t n = L.nvoxel;
+    std::vector<uint64_t> flat(val.size());
+    for (size_t t = 0; t < val.size(); ++t) {
+        if (ii[t] >= n || jj[t] >= n) throw Error("Laplacian index out of range in " + path + ".");
+        flat[t] = ii[t] * n + jj[t];
+    }
+    std::vector<size_t> order(val.size());
+    std::iota(order.begin(), order.end(), 0);
+    if (!std::is_sorted(flat.begin(), flat.end()))
+        std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return flat[a] < flat[b]; });
+    L.i.resize(val.size());
+    L.j.resize(val.size());
+    L.value.resize(val.size());
+    for (size_t t = 0; t < order.size(); ++t) {
+        L.i[t] = ii[order[t]];
+        L.j[t] = jj[order[t]];
+        L.value[t] = val[order[t]];
+    }
+    return L;
+}
+
+#else  // !SART_HAVE_HDF5
+
+[[noreturn]] static void nohdf5() { throw Error("built without HDF5 support"); }
+void categorize_input_files(const std::vector<std::string>&, std::vector<std::string>&, std::vector<std::string>&) { nohdf5(); }
+void check_group_attribute_consistency(const std::vector<std::string>&, const std::string&, const std::vector<std::string>&, bool) { nohdf5(); }
+SortedRtmFiles sort_rtm_files(const std::vector<std::string>&) { nohdf5(); }
+void check_rtm_frame_consistency(const SortedRtmFiles&) { nohdf5(); }
+void check_rtm_voxel_consistency(const SortedRtmFiles&) { nohdf5(); }
+std::map<std::string, std::vector<int32_t>> read_rtm_frame_masks(const SortedRtmFiles&) { nohdf5(); }
+std::map<std::string, std::pair<uint64_t, uint64_t>> read_rtm_frame_shapes(const SortedRtmFiles&) { nohdf5(); }
+SortedImageFiles sort_image_files(const std::vector<std::string>&) { nohdf5(); }
+void check_rtm_image_consistency(const SortedRtmFiles&, const SortedImageFiles&, const std::string&, double) { nohdf5(); }
+std::pair<uint64_t, uint64_t> get_total_rtm_size(const SortedRtmFiles&) { nohdf5(); }
+void read_rtm_rows(const SortedRtmFiles&, const std::string&, uint64_t, uint64_t, uint64_t, float*, uint64_t) { nohdf5(); }
+bool rtm_has_sparse(const SortedRtmFiles&, const std::string&) { nohdf5(); }
+LaplacianCOO read_laplacian(const std::string&, uint64_t) { nohdf5(); }
+
+#endif
+
+}  // namespace sart

@@ -1,0 +1,53 @@
+// Input-file discovery, validation and matrix loaders (HDF5 schema of manual.pdf p.5-8).
+//
+// Behaviour mirrors the reference validators (reference hdf5files.cpp:20-389, raytransfer.cpp:27-127,
+// laplacian.cpp:34-91); errors are reported by throwing sart::Error with the reference's messages
+// instead of calling std::exit on one rank.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "h5.hpp"
+
+namespace sart {
+
+// camera name -> RTM files ordered by the minimum flat voxel index of their voxel-map segment
+using SortedRtmFiles = std::map<std::string, std::vector<std::string>>;
+// camera name -> image file
+using SortedImageFiles = std::map<std::string, std::string>;
+
+void categorize_input_files(const std::vector<std::string>& input_files, std::vector<std::string>& rtm_files,
+                            std::vector<std::string>& image_files);
+// Attributes `names` of group `group` must be identical in every file (double or integer compare).
+void check_group_attribute_consistency(const std::vector<std::string>& files, const std::string& group,
+                                       const std::vector<std::string>& names, bool integer);
+SortedRtmFiles sort_rtm_files(const std::vector<std::string>& files);
+void check_rtm_frame_consistency(const SortedRtmFiles& sorted);
+void check_rtm_voxel_consistency(const SortedRtmFiles& sorted);
+std::map<std::string, std::vector<int32_t>> read_rtm_frame_masks(const SortedRtmFiles& sorted);
+std::map<std::string, std::pair<uint64_t, uint64_t>> read_rtm_frame_shapes(const SortedRtmFiles& sorted);
+SortedImageFiles sort_image_files(const std::vector<std::string>& files);
+void check_rtm_image_consistency(const SortedRtmFiles& rtm, const SortedImageFiles& images,
+                                 const std::string& rtm_name, double wavelength_threshold);
+std::pair<uint64_t, uint64_t> get_total_rtm_size(const SortedRtmFiles& sorted);
+
+// Reads global RTM rows [row_begin, row_end) (cameras concatenated in name order, voxel segments
+// concatenated along the columns) into out[(r - row_begin) * ld + v]. Dense datasets are read as
+// row blocks with one hyperslab per block, sparse (COO) datasets are scattered. Rows of `out` must
+// be zero-initialised by the caller when sparse data is present.
+void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, uint64_t nvoxel, uint64_t row_begin,
+                   uint64_t row_end, float* out, uint64_t ld);
+bool rtm_has_sparse(const SortedRtmFiles& sorted, const std::string& rtm_name);
+
+struct LaplacianCOO {
+    uint64_t nvoxel = 0;
+    std::vector<uint64_t> i, j;  // sorted by flat index i * nvoxel + j
+    std::vector<float> value;
+};
+LaplacianCOO read_laplacian(const std::string& path, uint64_t expected_nvoxel);
+
+}  // namespace sart

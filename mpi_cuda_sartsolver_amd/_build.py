@@ -101,7 +101,7 @@ def build_hip(verbose: bool = True) -> Path:
     objdir.mkdir(parents=True, exist_ok=True)
     LIBDIR.mkdir(parents=True, exist_ok=True)
     headers = sorted((CSRC / "kernels").glob("*.hpp"))
-    common = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
+    common = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
     jobs = []
     objs = []
     for src in sorted((CSRC / "kernels").glob("*.hip")):

@@ -22,14 +22,12 @@ from ..parallel.partition import round_up
 
 @dataclass(frozen=True)
 class FusedGeometry:
-    K: int  # float4 per lane per row in a slab
-    J: int  # column slabs
-    I: int  # row groups
-    grid: int
-
-    @property
-    def tile_rows(self) -> int:
-        return 8 // self.K
+    K: int        # float4 per lane per row in a slab (slab width 1024*K columns)
+    J: int        # column slabs
+    I: int        # row groups
+    grid: int     # I * J persistent workgroups (<= number of CUs)
+    variant: int  # register-ring configuration (csrc/kernels/fused_sweep.hip)
+    T: int        # rows per tile
 
 
 def choose_ld(nvoxel: int, max_waste: float = 0.10) -> int:
@@ -46,17 +44,31 @@ def choose_ld(nvoxel: int, max_waste: float = 0.10) -> int:
     return round_up(max(nvoxel, 64), 64)
 
 
-def fused_geometry(ld: int, num_cus: int) -> Optional[FusedGeometry]:
+def fused_geometry(ld: int, num_cus: int, variant: int = 3) -> Optional[FusedGeometry]:
+    """Persistent-grid geometry of the fused sweep (csrc/kernels/fused_sweep.hip).
+
+    variant 3 (default, fastest measured at 64k x 64k): 1024*K-column slabs, tiles parked in LDS;
+    variants 5 and 4: 2048-column slabs, one row per compute wave (needs ld % 2048 == 0 and at
+    most 64 slabs); variants 0-3: slabs of 1024*K columns, K chosen for <= 32 slabs. None: no fused path.
+    """
+    if variant in (4, 5):
+        if ld % 2048 == 0 and 0 < ld // 2048 <= min(64, num_cus):
+            J = ld // 2048
+            I = max(1, num_cus // J)
+            return FusedGeometry(K=8, J=J, I=I, grid=I * J, variant=variant, T=4)
+        variant = 3
     for K in (1, 2, 4, 8):
         wc = 1024 * K
         if ld % wc:
             continue
         J = ld // wc
         if J <= 32 or K == 8:
-            if J > num_cus or J * (8 // K) > 2048:
+            v = variant if (variant != 2 or K <= 4) else 3
+            T = (4 // K) if v == 2 else (8 // K)
+            if J > num_cus or J * T > 512:
                 return None
             I = max(1, num_cus // J)
-            return FusedGeometry(K=K, J=J, I=I, grid=I * J)
+            return FusedGeometry(K=K, J=J, I=I, grid=I * J, variant=v, T=T)
     return None
 
 

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -86,7 +87,7 @@ class SARTSolver:
     def __init__(self, rtm: DenseRTM, laplacian: Optional[LaplacianCSR] = None,
                  comm: Optional[Communicator] = None, params: Optional[SolverParams] = None,
                  logarithmic: bool = False, use_fused: bool = True, check_interval: int = 16,
-                 allow_zero_tolerance: bool = False):
+                 allow_zero_tolerance: bool = False, fused_variant: Optional[int] = None):
         self.k = hip()
         self.rtm = rtm
         self.dev = rtm.device
@@ -106,13 +107,16 @@ class SARTSolver:
 
         props = self.k.device_info(self.dev.index if self.dev.index is not None else 0)
         self.num_cus = int(props["multiProcessorCount"])
-        self.geom = fused_geometry(ld, self.num_cus) if use_fused else None
+        if fused_variant is None:
+            fused_variant = int(os.environ.get("SART_FUSED_VARIANT", "3"))
+        self.geom = fused_geometry(ld, self.num_cus, fused_variant) if use_fused else None
         self.use_fused = self.geom is not None
 
         self.nsplit = self.k.backproject_num_splits(ld, Pp)
         n_part = max(self.nsplit, self.geom.I if self.geom else 1)
         self.partial = z(n_part * ld)
-        nF = max(self.k.forward_num_blocks(Pp), self.geom.grid if self.geom else 1)
+        self.nF_fused = self.geom.grid * self.k.fused_fpart_per_block(self.geom.variant) if self.geom else 0
+        nF = max(self.k.forward_num_blocks(Pp), self.nF_fused, 1)
         self.Fpart = z(nF, dtype=torch.float64, device=self.dev)
         self.comm_buf = z(ld + 64)  # [0:ld] correction, [ld] ||A x||^2 (fp32, as the reference)
         self.x = z(ld)
@@ -207,11 +211,11 @@ class SARTSolver:
         Fslot = self.comm_buf.data_ptr() + 4 * self.ld
         if self.use_fused:
             g = self.geom
-            k.fused_sweep(self.log, g.K, A, self.ld, self.P, self.Pp, self.x.data_ptr(), self.ghat.data_ptr(),
+            k.fused_sweep(self.log, g.K, g.variant, A, self.ld, self.P, self.Pp, self.x.data_ptr(), self.ghat.data_ptr(),
                           self.arow.data_ptr(), self.partial.data_ptr(), self.Fpart.data_ptr(),
                           self.gran.data_ptr(), g.I, g.J, st, s)
             k.reduce_partials(self.partial.data_ptr(), self.ld, g.I, scale.data_ptr(), self.comm_buf.data_ptr(),
-                              self.Fpart.data_ptr(), g.grid, Fslot, st, s)
+                              self.Fpart.data_ptr(), self.nF_fused, Fslot, st, s)
         else:
             epi = EPI_LOG if self.log else EPI_LINEAR
             k.forward(epi, A, self.ld, self.P, self.Pp, self.x.data_ptr(), self.ghat.data_ptr(), self.arow.data_ptr(),

@@ -113,3 +113,21 @@ def test_synthetic_bench_problem_small(dev):
     assert s.use_fused
     r = s.solve(prob.measurement)
     assert r.iterations == 10 and np.all(np.isfinite(r.solution))
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("shape", [(2048, 4096), (1000, 16384), (512, 8192 * 4)])
+def test_fused_variants(dev, variant, shape):
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+    from mpi_cuda_sartsolver_amd.utils.synthetic import host_problem
+
+    A, g, _ = host_problem(*shape, seed=variant + 3)
+    s = SARTSolver(DenseRTM.from_dense(A, device=dev), None, None, SolverParams(max_iterations=12, conv_tolerance=0.0),
+                   allow_zero_tolerance=True, fused_variant=variant)
+    assert s.use_fused and s.geom.variant == variant
+    r = s.solve(g)
+    assert r.used_fused, "fused exchange timed out"
+    x_ref, _, _ = sart_gpu_semantics(A, g, max_iterations=12, conv_tolerance=0.0)
+    assert _rel(r.solution, x_ref) < 2e-3

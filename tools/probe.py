@@ -67,7 +67,7 @@ def main():
         arow = torch.rand(m.nrows_pad, device=dev) * 1e-4
         w = torch.zeros(m.nrows_pad, device=dev)
         nb = k.forward_num_blocks(m.nrows_pad)
-        Fp = torch.zeros(max(nb, 4096), dtype=torch.float64, device=dev)
+        Fp = torch.zeros(max(nb, 8192), dtype=torch.float64, device=dev)
         st = new_state(dev)
         k.state_begin(st.data_ptr(), 1.0, 0.0, 100, s)
 
@@ -88,25 +88,31 @@ def main():
         emit(kind="kernel", op="backproject", P=P, V=V, nsplit=ns, ms=med, GBps=nbytes / med / 1e6,
              best_GBps=nbytes / best / 1e6)
 
-        g = fused_geometry(m.ld, int(info["multiProcessorCount"]))
-        if g is not None:
+        for variant in (5, 4, 3):
+            g = fused_geometry(m.ld, int(info["multiProcessorCount"]), variant)
+            if g is None or g.variant != variant:
+                continue
             gran = torch.zeros(m.nrows_pad * g.J, dtype=torch.int64, device=dev)
-            ep = [1]
 
             def fused():
-                # bump the epoch through a fresh state each call (fused kernel reads st->epoch)
-                ep[0] += 1
                 k.state_begin(st.data_ptr(), 1.0, 0.0, 100, s)
                 k.decide(st.data_ptr(), Fp.data_ptr(), s)  # sweep 0 -> epoch+1, not done
-                k.fused_sweep(False, g.K, m.A.data_ptr(), m.ld, P, m.nrows_pad, x.data_ptr(), ghat.data_ptr(),
-                              arow.data_ptr(), part.data_ptr(), Fp.data_ptr(), gran.data_ptr(), g.I, g.J, st.data_ptr(), s)
+                k.fused_sweep(False, g.K, g.variant, m.A.data_ptr(), m.ld, P, m.nrows_pad, x.data_ptr(),
+                              ghat.data_ptr(), arow.data_ptr(), part.data_ptr(), Fp.data_ptr(), gran.data_ptr(),
+                              g.I, g.J, st.data_ptr(), s)
 
             med, best = timeit(fused)
             from mpi_cuda_sartsolver_amd.ops.state import read_state
 
             err = read_state(st).error
-            emit(kind="kernel", op="fused_sweep", P=P, V=V, K=g.K, J=g.J, I=g.I, ms=med, GBps=nbytes / med / 1e6,
-                 best_GBps=nbytes / best / 1e6, error=err)
+            emit(kind="kernel", op=f"fused_sweep_v{variant}", P=P, V=V, K=g.K, J=g.J, I=g.I, T=g.T, ms=med,
+                 GBps=nbytes / med / 1e6, best_GBps=nbytes / best / 1e6, error=err)
+            if variant in (3, 4, 5):
+                k.fused_set_debug(1)
+                med, best = timeit(fused)
+                k.fused_set_debug(0)
+                emit(kind="kernel", op=f"fused_sweep_v{variant}_noexchange", P=P, V=V, ms=med, GBps=nbytes / med / 1e6)
+            del gran
 
         # multi-frame MFMA projections (16 frames)
         X = torch.rand((16, m.ld), device=dev)
