@@ -56,8 +56,10 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
                         const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                         uint64_t* gran, int I, int J, SartState* st, hipStream_t stream);
 // multiframe.hip
+int mf_forward_num_splits(int64_t ld, int64_t nrows_pad);
+int mf_backproject_num_splits(int64_t ld, int64_t nrows);
 void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ldx,
-                       float* Fout, hipStream_t stream);
+                       float* Fout, int nsplit, hipStream_t stream);
 void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,
                            hipStream_t stream);
 }  // namespace sart
@@ -168,10 +170,12 @@ PYBIND11_MODULE(_sart_hip, m) {
                                  P<const float>(ghat), P<const float>(arow), P<float>(partial), P<double>(Fpart),
                                  P<uint64_t>(gran), I, J, P<sart::SartState>(st), S(stream));
     });
+    m.def("mf_forward_num_splits", &sart::mf_forward_num_splits);
+    m.def("mf_backproject_num_splits", &sart::mf_backproject_num_splits);
     m.def("mf_forward", [](uintptr_t A, int64_t ld, int64_t nrows, int64_t nrows_pad, uintptr_t X, int64_t ldx,
-                           uintptr_t Fout, uintptr_t stream) {
+                           uintptr_t Fout, int nsplit, uintptr_t stream) {
         sart::launch_mf_forward(P<const float>(A), ld, nrows, nrows_pad, P<const float>(X), ldx, P<float>(Fout),
-                                S(stream));
+                                nsplit, S(stream));
     });
     m.def("mf_backproject", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t W, int nsplit, uintptr_t partial,
                                uintptr_t stream) {

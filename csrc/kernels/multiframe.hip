@@ -29,21 +29,26 @@ __device__ __forceinline__ float comp(const float4& v, int c) {
 
 // F[row][f] = sum_v A[row][v] X[f][v]. X is frame-major [16][ldx] (ldx == ld), F is [rows][16].
 // One wave: 32 rows (two 16-row tiles sharing the X fragment) x 16 frames, K = all voxels.
+// Split-K: blockIdx.y selects the column range [k0, k1) (multiples of 16 columns) and the kernel
+// writes Fout + blockIdx.y * nrows_pad * 16; the caller sums the splits.
 __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A, int64_t ld, int64_t nrows,
                                                     int64_t nrows_pad, const float* __restrict__ X,
-                                                    int64_t ldx, float* __restrict__ Fout) {
+                                                    int64_t ldx, float* __restrict__ Fout, int64_t cols_per_split) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * 32;
     if (row0 >= nrows_pad) return;  // wave-uniform
     const int g = lane >> 4, r = lane & 15;
     const int64_t ld4 = ld >> 2, ldx4 = ldx >> 2;
-    const float4* __restrict__ a0p = reinterpret_cast<const float4*>(A) + (row0 + r) * ld4 + g;
+    const int64_t c0 = (int64_t)blockIdx.y * cols_per_split;
+    const int64_t c1 = (c0 + cols_per_split < ld) ? c0 + cols_per_split : ld;
+    Fout += (int64_t)blockIdx.y * nrows_pad * kNF;
+    const float4* __restrict__ a0p = reinterpret_cast<const float4*>(A) + (row0 + r) * ld4 + g + c0 / 4;
     const float4* __restrict__ a1p = a0p + 16 * ld4;
-    const float4* __restrict__ xp = reinterpret_cast<const float4*>(X) + (int64_t)r * ldx4 + g;
+    const float4* __restrict__ xp = reinterpret_cast<const float4*>(X) + (int64_t)r * ldx4 + g + c0 / 4;
 
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
     int64_t q = 0;
-    const int64_t nq = ld4;  // float4 columns; each iteration consumes 4 lane-groups x float4 = 16 voxels
+    const int64_t nq = c1 > c0 ? (c1 - c0) / 4 : 0;  // float4 columns; 4 lane-groups x float4 = 16 voxels/step
     for (; q + 8 <= nq; q += 8) {
         const float4 a00 = a0p[q], a10 = a1p[q], x0 = xp[q];
         const float4 a01 = a0p[q + 4], a11 = a1p[q + 4], x1 = xp[q + 4];
@@ -128,14 +133,34 @@ __global__ __launch_bounds__(256) void k_mf_backproject(const float* __restrict_
         }
 }
 
+int mf_forward_num_splits(int64_t ld, int64_t nrows_pad) {
+    const int64_t nblk = (nrows_pad + 127) / 128;
+    int64_t s = (1024 + nblk - 1) / nblk;  // >= ~1024 workgroups
+    const int64_t smax = ld / 1024;        // >= 1024 columns per split
+    if (s > smax) s = smax;
+    if (s < 1) s = 1;
+    return (int)s;
+}
+
 void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ldx,
-                       float* Fout, hipStream_t stream) {
+                       float* Fout, int nsplit, hipStream_t stream) {
     if (ld % 64 != 0 || ldx != ld) throw std::runtime_error("mf_forward: ld must be a multiple of 64 and ldx == ld");
     if (nrows_pad % 32 != 0) throw std::runtime_error("mf_forward: padded rows must be a multiple of 32");
+    if (nsplit < 1) throw std::runtime_error("mf_forward: nsplit must be >= 1");
     const int64_t nblk = (nrows_pad + 127) / 128;
-    hipLaunchKernelGGL(k_mf_forward, dim3((unsigned)nblk), dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx,
-                       Fout);
+    const int64_t cps = ((ld + nsplit - 1) / nsplit + 15) / 16 * 16;
+    hipLaunchKernelGGL(k_mf_forward, dim3((unsigned)nblk, (unsigned)nsplit), dim3(256), 0, stream, A, ld, nrows,
+                       nrows_pad, X, ldx, Fout, cps);
     check_launch("k_mf_forward");
+}
+
+int mf_backproject_num_splits(int64_t ld, int64_t nrows) {
+    const int64_t nblk = (ld / 64 + 3) / 4;
+    int64_t s = (2048 + nblk - 1) / nblk;
+    const int64_t smax = (nrows + 63) / 64;
+    if (s > smax) s = smax;
+    if (s < 1) s = 1;
+    return (int)s;
 }
 
 void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,

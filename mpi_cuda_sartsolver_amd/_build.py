@@ -136,7 +136,9 @@ def build_native(verbose: bool = True) -> Path:
     libs = ["-fopenmp"]
     if hdf5_available():
         flags += ["-DSART_HAVE_HDF5=1", f"-isystem{HDF5_PREFIX / 'include'}"]
-        libs += [str(HDF5_PREFIX / "lib" / "libhdf5.so"), f"-Wl,-rpath,{HDF5_PREFIX / 'lib'}"]
+        # no rpath into /opt/conda/lib: it would also redirect libstdc++ to conda's older copy. The
+        # loader (ops.native) preloads libhdf5 by absolute path instead.
+        libs += [f"-L{HDF5_PREFIX / 'lib'}", "-lhdf5"]
     jobs, objs = [], []
     for src in sorted(srcdir.glob("*.cpp")) + [CSRC / "bindings" / "native_module.cpp"]:
         obj = objdir / (src.stem + ".o")

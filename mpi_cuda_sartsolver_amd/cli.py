@@ -1,0 +1,215 @@
+"""``sartsolver`` command-line driver.
+
+Same CLI, input validation, frame loop, output file and console output as the reference binary
+(reference main.cpp:25-151), re-organised for MI355X:
+
+* one process per GPU launched by ``torchrun`` (``python -m torch.distributed.run --nproc-per-node 8
+  -m mpi_cuda_sartsolver_amd ...``) instead of ``mpirun``; rank -> GPU = LOCAL_RANK;
+* every rank loads only its pixel rows, streamed from HDF5 straight into HBM; with
+  ``--parallel_read`` all ranks read at once, otherwise they take turns (reference main.cpp:78-86);
+* the next composite frame is read on a helper thread while the current one is solved;
+* fatal errors tear the process group down instead of leaving peers blocked in a collective.
+
+Extensions: ``--resume``, ``--batch_frames N`` (multi-frame MFMA solver), ``--two_pass``,
+``--profile FILE`` (JSON lines per frame).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+
+
+def _fail(msg: str, comm=None) -> None:
+    from .parallel.comm import abort_all
+
+    if comm is not None and comm.world_size > 1:
+        abort_all(msg, 1)
+    print(msg, file=sys.stderr, flush=True)
+    raise SystemExit(1)
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    from .ops import native
+
+    n = native()
+    try:
+        cfg = n.parse_arguments(argv)
+    except RuntimeError as exc:
+        _fail(str(exc))
+    if cfg.help:
+        print(n.usage())
+        return 0
+    try:
+        intervals = n.parse_time_intervals(cfg.time_range)
+    except RuntimeError as exc:
+        _fail(str(exc))
+    return run(cfg, intervals)
+
+
+def run(cfg, intervals) -> int:
+    import numpy as np
+    import torch
+
+    from .io import hdf5
+    from .models.sart import SolverParams
+    from .ops import native
+
+    n = native()
+    from .parallel.comm import init_distributed
+    from .parallel.partition import row_partition
+
+    # ---- metadata validation (every rank, before the process group exists: reference main.cpp:27-59)
+    try:
+        inputs = hdf5.validate_inputs(cfg.input_files, cfg.raytransfer_name, cfg.wavelength_threshold)
+    except RuntimeError as exc:
+        _fail(str(exc))
+
+    use_gpu = not cfg.use_cpu
+    if use_gpu and not torch.cuda.is_available():
+        _fail("No GPU available: run with --use_cpu or on an MI355X node.")
+    comm = init_distributed(use_gpu=use_gpu)
+    rank, world = comm.rank, comm.world_size
+    try:
+        block = row_partition(inputs.npixel, world, rank)
+        if block.size == 0:
+            raise RuntimeError(f"rank {rank} owns no pixels: use at most {inputs.npixel} ranks")
+        image = hdf5.open_composite_image(inputs, intervals, block.size, block.offset, cfg.max_cached_frames)
+        params = SolverParams(ray_density_threshold=cfg.ray_density_threshold,
+                              ray_length_threshold=cfg.ray_length_threshold, conv_tolerance=cfg.conv_tolerance,
+                              beta_laplace=cfg.beta_laplace, relaxation=cfg.relaxation,
+                              max_iterations=cfg.max_iterations)
+        device = torch.device("cuda", torch.cuda.current_device()) if use_gpu else None
+        laplacian = hdf5.load_laplacian(cfg.laplacian_file, inputs.nvoxel, device) if cfg.laplacian_file else None
+
+        def load():
+            if use_gpu:
+                return hdf5.load_rtm_shard(inputs, block.offset, block.size, device)
+            return hdf5.read_rtm_rows(inputs, block.offset, block.stop)
+
+        if cfg.parallel_read or world == 1:
+            shard = load()
+        else:
+            shard = None
+            for r in range(world):
+                if r == rank:
+                    shard = load()
+                comm.barrier()
+
+        if use_gpu:
+            if cfg.batch_frames > 1:
+                from .models.multiframe import MultiFrameSARTSolver
+
+                solver = MultiFrameSARTSolver(shard, laplacian, comm, params, logarithmic=cfg.logarithmic,
+                                              batch=cfg.batch_frames)
+            else:
+                from .models.sart import SARTSolver
+
+                solver = SARTSolver(shard, laplacian, comm, params, logarithmic=cfg.logarithmic,
+                                    use_fused=not cfg.two_pass)
+        else:
+            from .models.cpu import CPUSARTSolver
+
+            solver = CPUSARTSolver(shard, laplacian, comm, params, logarithmic=cfg.logarithmic)
+
+        writer = voxelgrid = None
+        skip_until = -float("inf")
+        warm = None
+        if rank == 0:
+            append = False
+            if cfg.resume and os.path.exists(cfg.output_file):
+                stored_t, last_x, _ = n.read_solution_file(cfg.output_file)
+                if len(stored_t):
+                    append = True
+                    skip_until = float(stored_t[-1])
+                    warm = np.asarray(last_x)
+            writer = n.SolutionWriter(cfg.output_file, inputs.camera_names, inputs.nvoxel,
+                                      cfg.max_cached_solutions, append)
+            voxelgrid = hdf5.read_voxel_grid(inputs)
+            for wmsg in voxelgrid.warnings:
+                print("warning:", wmsg, file=sys.stderr)
+        skip_until = comm.broadcast_object(skip_until)
+        warm = comm.broadcast_object(warm if not cfg.no_guess else None)
+        profile = open(cfg.profile_file, "w") if (cfg.profile_file and rank == 0) else None
+
+        solution = warm
+        pool = cf.ThreadPoolExecutor(1)
+        nframes = image.nframe
+        frames = (i for i in range(nframes) if image.frame_time(i) > skip_until + 1e-12)
+        if cfg.batch_frames > 1 and use_gpu:
+            _run_batched(cfg, solver, image, frames, pool, writer, profile, rank)
+        else:
+            idx = next(frames, None)
+            fut = pool.submit(image.frame, idx) if idx is not None else None
+            while fut is not None:
+                frame = fut.result()
+                cur = idx
+                idx = next(frames, None)
+                fut = pool.submit(image.frame, idx) if idx is not None else None  # prefetch
+                t0 = time.perf_counter()
+                res = solver.solve(frame, None if (cfg.no_guess or solution is None) else solution)
+                solution = res.solution
+                if rank == 0:
+                    writer.add(res.solution, int(res.status), image.frame_time(cur), list(image.camera_frame_time(cur)),
+                               int(res.iterations))
+                    ms = 1e3 * (time.perf_counter() - t0)
+                    print(f"Processed in: {ms} ms", flush=True)
+                    if profile:
+                        profile.write(json.dumps({"frame": cur, "time": image.frame_time(cur), "status": res.status,
+                                                  "iterations": res.iterations, "ms": ms,
+                                                  "fused": bool(getattr(res, "used_fused", False))}) + "\n")
+                if cfg.no_guess:
+                    solution = None
+        pool.shutdown()
+        if rank == 0:
+            writer.flush()
+            if not (cfg.resume and skip_until > -float("inf")):
+                voxelgrid.write(cfg.output_file, "voxel_map")
+            if profile:
+                profile.close()
+        comm.barrier()
+    except SystemExit:
+        raise
+    except Exception as exc:  # any rank: report and take the whole job down
+        import traceback
+
+        traceback.print_exc()
+        _fail(f"rank {rank}: {type(exc).__name__}: {exc}", comm)
+    finally:
+        try:
+            import torch.distributed as dist
+
+            if dist.is_initialized():
+                dist.destroy_process_group()
+        except Exception:
+            pass
+    return 0
+
+
+def _run_batched(cfg, solver, image, frames, pool, writer, profile, rank) -> None:
+    """--batch_frames N: independent frames solved together (cold start each, like --no_guess)."""
+    import numpy as np
+
+    idxs = list(frames)
+    for b0 in range(0, len(idxs), cfg.batch_frames):
+        chunk = idxs[b0: b0 + cfg.batch_frames]
+        batch = np.stack(list(pool.map(image.frame, chunk)))
+        t0 = time.perf_counter()
+        results = solver.solve_batch(batch)
+        ms = 1e3 * (time.perf_counter() - t0)
+        if rank == 0:
+            for i, res in zip(chunk, results):
+                writer.add(res.solution, int(res.status), image.frame_time(i), list(image.camera_frame_time(i)),
+                           int(res.iterations))
+                print(f"Processed in: {ms / len(chunk)} ms", flush=True)
+                if profile:
+                    profile.write(json.dumps({"frame": i, "time": image.frame_time(i), "status": res.status,
+                                              "iterations": res.iterations, "ms": ms / len(chunk),
+                                              "batch": len(chunk)}) + "\n")
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -50,9 +50,26 @@ def hip():
     return _HIP
 
 
+def _preload_hdf5() -> None:
+    """Load the HDF5 C library by absolute path (RTLD_GLOBAL) so _sart_native resolves it without an
+    rpath into /opt/conda/lib (which would also pull conda's older libstdc++)."""
+    import ctypes
+
+    prefix = os.environ.get("SART_HDF5_PREFIX", "/opt/conda")
+    for name in ("libhdf5.so", "libhdf5.so.103"):
+        path = os.path.join(prefix, "lib", name)
+        if os.path.exists(path):
+            try:
+                ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+                return
+            except OSError:
+                pass
+
+
 def native():
     global _NATIVE
     if _NATIVE is None:
+        _preload_hdf5()
         try:
             _NATIVE = _import("_sart_native")
         except NativeExtensionMissing:

@@ -6,6 +6,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# build the in-tree native modules on first use if they are missing (hipcc cross-compiles without a GPU)
+os.environ.setdefault("SART_AUTOBUILD", "1")
 
 
 def pytest_configure(config):

@@ -1,0 +1,109 @@
+"""End-to-end CLI runs on generated HDF5 cases: output file vs the fp64 oracle frame by frame."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from mpi_cuda_sartsolver_amd import cli
+from mpi_cuda_sartsolver_amd.io.fixtures import make_case
+from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+from mpi_cuda_sartsolver_amd.models.reference import sart_cpu_semantics, sart_gpu_semantics
+from mpi_cuda_sartsolver_amd.ops import native
+
+
+def _frames(case):
+    """Composite frames of a fixture case (cameras share the time grid): masked pixels in name order."""
+    nf = len(next(iter(case.times.values())))
+    return [np.concatenate([case.frames[c][k].ravel()[case.masks[c].ravel() > 0] for c in sorted(case.masks)])
+            for k in range(nf)]
+
+
+def _laplacian(case):
+    if not case.laplacian_file:
+        return None
+    i, j, v = native().read_laplacian(case.laplacian_file, case.nvoxel)
+    return LaplacianCSR(case.nvoxel, i, j, v)
+
+
+def _expected(case, oracle, warm=True, **kw):
+    xs, sts, its = [], [], []
+    prev = None
+    for g in _frames(case):
+        x, st, it = oracle(case.A, g, _laplacian(case), x_prev=prev if warm else None, **kw)
+        xs.append(x), sts.append(st), its.append(it)
+        prev = x
+    return np.array(xs), np.array(sts), its
+
+
+def _read_all(path):
+    import subprocess
+
+    # read the whole value dataset through the native reader of the last row + the solution times
+    n = native()
+    t, last, st = n.read_solution_file(path)
+    dump = subprocess.run(["/opt/conda/bin/h5dump", "-d", "/solution/value", "-y", "-w", "0", path],
+                          capture_output=True, text=True)
+    return t, last, st, dump.stdout
+
+
+@pytest.mark.parametrize("log", [False, True])
+@pytest.mark.parametrize("no_guess", [False, True])
+def test_cli_cpu_matches_reference_cpu_semantics(tmp_path, capsys, log, no_guess):
+    case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_a",), laplacian=True, nframes=3, saturate=0.05)
+    out = str(tmp_path / "out.h5")
+    argv = ["--use_cpu", "-m", "120", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3", "-o", out]
+    argv += (["-L"] if log else []) + (["--no_guess"] if no_guess else []) + case.files
+    assert cli.main(argv) == 0
+    assert capsys.readouterr().out.count("Processed in:") == 3
+    xs, sts, its = _expected(case, sart_cpu_semantics, warm=not no_guess, logarithmic=log, max_iterations=120,
+                             conv_tolerance=1e-6, beta_laplace=1e-3)
+    t, last, st, _ = _read_all(out)
+    np.testing.assert_allclose(t, next(iter(case.times.values())), atol=1e-12)
+    np.testing.assert_array_equal(st, sts)
+    np.testing.assert_allclose(last, xs[-1], rtol=1e-7, atol=1e-12 * np.abs(xs[-1]).max())
+
+
+def test_cli_time_range_and_resume(tmp_path, capsys):
+    case = make_case(str(tmp_path / "c"), nframes=6, dt=0.1)
+    out = str(tmp_path / "out.h5")
+    base = ["--use_cpu", "-m", "50", "-o", out]
+    assert cli.main(base + ["-t", "0:0.25"] + case.files) == 0
+    t, _, _ = native().read_solution_file(out)
+    np.testing.assert_allclose(t, [0.0, 0.1, 0.2], atol=1e-12)
+    capsys.readouterr()
+    assert cli.main(base + ["--resume"] + case.files) == 0
+    assert capsys.readouterr().out.count("Processed in:") == 3  # only the frames after t = 0.2
+    t, last, _ = native().read_solution_file(out)
+    np.testing.assert_allclose(t, 0.1 * np.arange(6), atol=1e-12)
+    xs, _, _ = _expected(case, sart_cpu_semantics, max_iterations=50, conv_tolerance=1e-5, beta_laplace=2e-2)
+    np.testing.assert_allclose(last, xs[-1], rtol=1e-7)
+
+
+def test_cli_errors(tmp_path, capsys):
+    case = make_case(str(tmp_path / "c"), nframes=2)
+    with pytest.raises(SystemExit):
+        cli.main(["--use_cpu", "-R", "3"] + case.files)
+    assert "relaxation" in capsys.readouterr().err
+    with pytest.raises(SystemExit):
+        cli.main(["--use_cpu", "-t", "100:200"] + case.files)
+    assert "No composite images" in capsys.readouterr().err
+    assert cli.main(["--help"]) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log", [False, True])
+@pytest.mark.parametrize("extra", [[], ["--two_pass"], ["--batch_frames", "4"]])
+def test_cli_gpu_matches_gpu_semantics(tmp_path, capsys, log, extra):
+    case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_b",), laplacian=True, nframes=4, saturate=0.05,
+                     nvoxel=2048, grid=(16, 16, 16), shapes=((24, 32), (20, 30)))
+    out = str(tmp_path / "out.h5")
+    argv = ["-m", "60", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3", "-o", out] + (["-L"] if log else [])
+    batched = "--batch_frames" in extra
+    argv += extra + (["--no_guess"] if batched else []) + case.files
+    assert cli.main(argv) == 0
+    xs, sts, its = _expected(case, sart_gpu_semantics, warm=not batched, logarithmic=log, max_iterations=60,
+                             conv_tolerance=1e-6, beta_laplace=1e-3)
+    t, last, st = native().read_solution_file(out)
+    assert len(t) == 4
+    assert np.linalg.norm(last - xs[-1]) / np.linalg.norm(xs[-1]) < 5e-3

@@ -1,0 +1,68 @@
+"""Native fp64 CPU kernels and the --use_cpu solvers vs numpy oracles (reference sartsolver.cpp)."""
+import numpy as np
+import pytest
+
+from mpi_cuda_sartsolver_amd.models.cpu import CPUSARTSolver
+from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+from mpi_cuda_sartsolver_amd.models.reference import sart_cpu_semantics, sart_gpu_semantics
+from mpi_cuda_sartsolver_amd.models.sart import SolverParams
+from mpi_cuda_sartsolver_amd.ops import native
+from mpi_cuda_sartsolver_amd.utils.synthetic import host_problem
+
+
+@pytest.mark.parametrize("P,V", [(1, 1), (7, 13), (300, 257), (64, 1024)])
+def test_native_cpu_kernels(P, V):
+    n = native()
+    rng = np.random.default_rng(P * V)
+    A = rng.random((P, V), dtype=np.float32)
+    Ald = np.zeros((P, V + 5), np.float32)  # padded leading dimension
+    Ald[:, :V] = A
+    A64 = A.astype(np.float64)
+    rho, ell = n.cpu_raysums(Ald, P, V)
+    np.testing.assert_allclose(rho, A64.sum(0), rtol=1e-12)
+    np.testing.assert_allclose(ell, A64.sum(1), rtol=1e-12)
+    x, w = rng.random(V), rng.random(P) - 0.5
+    f, f2 = n.cpu_forward(Ald, P, V, x)
+    np.testing.assert_allclose(f, A64 @ x, rtol=1e-12)
+    assert np.isclose(f2, np.sum((A64 @ x) ** 2), rtol=1e-12)
+    np.testing.assert_allclose(n.cpu_backproject(Ald, P, V, w), A64.T @ w, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("log", [False, True])
+@pytest.mark.parametrize("semantics", ["cpu", "gpu"])
+@pytest.mark.parametrize("lap", [False, True])
+def test_cpu_solver_vs_oracle(log, semantics, lap):
+    A, g, _ = host_problem(200, 343, seed=11, saturate_fraction=0.05)
+    L = LaplacianCSR.grid_3d(7, 7, 7) if lap else None
+    kw = dict(max_iterations=60, conv_tolerance=1e-7, beta_laplace=2e-3)
+    r = CPUSARTSolver(A, L, params=SolverParams(**kw), logarithmic=log, semantics=semantics).solve(g)
+    oracle = sart_cpu_semantics if semantics == "cpu" else sart_gpu_semantics
+    x, st, it = oracle(A, g, L, logarithmic=log, **kw)
+    assert (r.status, r.iterations) == (st, it)
+    np.testing.assert_allclose(r.solution, x, rtol=1e-9, atol=1e-12 * np.abs(x).max())
+
+
+def test_cpu_solver_convergence_and_warm_start():
+    A, g, xt = host_problem(400, 100, seed=2)
+    s = CPUSARTSolver(A, params=SolverParams(max_iterations=5000, conv_tolerance=1e-9))
+    r = s.solve(g)
+    assert r.status == 0 and r.iterations < 5000
+    assert np.linalg.norm(A @ r.solution - g) / np.linalg.norm(g) < 1e-2
+    r2 = s.solve(g, solution=r.solution)  # warm start from the converged answer converges at once
+    assert r2.status == 0 and r2.iterations <= 3
+
+
+def test_cpu_reference_semantics_use_raw_negative_measurements():
+    A, g, _ = host_problem(50, 30, seed=4, saturate_fraction=0.3)
+    kw = dict(max_iterations=1, conv_tolerance=1e-5)
+    r_cpu = CPUSARTSolver(A, params=SolverParams(**kw), semantics="cpu").solve(g)
+    r_gpu = CPUSARTSolver(A, params=SolverParams(**kw), semantics="gpu").solve(g)
+    assert not np.allclose(r_cpu.solution, r_gpu.solution)  # the two reference paths differ by design
+
+
+def test_parameter_validation():
+    A, g, _ = host_problem(10, 10)
+    for bad in [dict(relaxation=0.0), dict(relaxation=1.1), dict(max_iterations=0), dict(conv_tolerance=0.0),
+                dict(beta_laplace=-1.0), dict(ray_density_threshold=-1.0), dict(ray_length_threshold=-1.0)]:
+        with pytest.raises(ValueError):
+            CPUSARTSolver(A, params=SolverParams(**bad))

@@ -130,8 +130,10 @@ def test_multiframe_mfma(k, dev, P, V):
     X = rng.random((16, V)).astype(np.float32)  # frame-major
     Xd = torch.zeros((16, m.ld), device=dev)
     Xd[:, :V] = torch.from_numpy(X)
-    Fo = torch.zeros((m.nrows_pad, 16), device=dev)
-    k.mf_forward(m.A.data_ptr(), m.ld, P, m.nrows_pad, Xd.data_ptr(), m.ld, Fo.data_ptr(), _stream(dev))
+    nsf = 3 if m.ld >= 3072 else 1
+    Fo3 = torch.zeros((nsf, m.nrows_pad, 16), device=dev)
+    k.mf_forward(m.A.data_ptr(), m.ld, P, m.nrows_pad, Xd.data_ptr(), m.ld, Fo3.data_ptr(), nsf, _stream(dev))
+    Fo = Fo3.sum(0)
     W = (rng.random((P, 16)) - 0.5).astype(np.float32)
     Wd = torch.zeros((m.nrows_pad, 16), device=dev)
     Wd[:P] = torch.from_numpy(W)

@@ -116,13 +116,14 @@ def main():
 
         # multi-frame MFMA projections (16 frames)
         X = torch.rand((16, m.ld), device=dev)
-        Fo = torch.zeros((m.nrows_pad, 16), device=dev)
+        nsf = k.mf_forward_num_splits(m.ld, m.nrows_pad)
+        Fo = torch.zeros((nsf, m.nrows_pad, 16), device=dev)
         med, best = timeit(lambda: k.mf_forward(m.A.data_ptr(), m.ld, P, m.nrows_pad, X.data_ptr(), m.ld,
-                                                Fo.data_ptr(), s))
+                                                Fo.data_ptr(), nsf, s))
         emit(kind="kernel", op="mf_forward16", P=P, V=V, ms=med, GBps=nbytes / med / 1e6,
              TFLOPs=2 * 16 * P * V / med / 1e9)
         W = torch.rand((m.nrows_pad, 16), device=dev)
-        nsm = 4
+        nsm = k.mf_backproject_num_splits(m.ld, P)
         partm = torch.zeros((nsm, m.ld, 16), device=dev)
         med, best = timeit(lambda: k.mf_backproject(m.A.data_ptr(), m.ld, P, W.data_ptr(), nsm, partm.data_ptr(), s))
         emit(kind="kernel", op="mf_backproject16", P=P, V=V, ms=med, GBps=nbytes / med / 1e6,
