@@ -97,6 +97,7 @@ def main() -> int:
         "sart_iterations_per_step": args.iters,
         "status_last": res.status if res else None,
         "fused_sweep": solver.use_fused,
+        "fused_variant": solver.geom.variant if solver.use_fused else None,
         "effective_hbm_TBps_per_gpu": round(bytes_per_iter * iters_per_s / 1e12, 3),
         "config": {
             "model": f"SART-{args.variant} dense RTM",

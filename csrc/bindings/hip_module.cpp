@@ -6,6 +6,7 @@
 // synchronise, so callers may capture them into HIP graphs.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <cstdint>
 #include <stdexcept>
@@ -52,9 +53,10 @@ int fused_pick_k(int64_t ld);
 int fused_tile_rows(int K, int variant);
 int fused_fpart_per_block(int variant);
 void fused_set_debug(int flags);
+std::vector<unsigned long long> fused_debug_stats(int nblocks);
 void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                         const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
-                        uint64_t* gran, int I, int J, SartState* st, hipStream_t stream);
+                        uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream);
 // multiframe.hip
 int mf_forward_num_splits(int64_t ld, int64_t nrows_pad);
 int mf_backproject_num_splits(int64_t ld, int64_t nrows);
@@ -163,12 +165,13 @@ PYBIND11_MODULE(_sart_hip, m) {
     m.def("fused_tile_rows", &sart::fused_tile_rows);
     m.def("fused_fpart_per_block", &sart::fused_fpart_per_block);
     m.def("fused_set_debug", &sart::fused_set_debug);
+    m.def("fused_debug_stats", &sart::fused_debug_stats);
     m.def("fused_sweep", [](bool logmode, int K, int variant, uintptr_t A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                             uintptr_t x, uintptr_t ghat, uintptr_t arow, uintptr_t partial, uintptr_t Fpart,
-                            uintptr_t gran, int I, int J, uintptr_t st, uintptr_t stream) {
+                            uintptr_t gran, int I, int J, uintptr_t st, uintptr_t xcnt, uintptr_t stream) {
         sart::launch_fused_sweep(logmode, K, variant, P<const float>(A), ld, nrows, nrows_pad, P<const float>(x),
                                  P<const float>(ghat), P<const float>(arow), P<float>(partial), P<double>(Fpart),
-                                 P<uint64_t>(gran), I, J, P<sart::SartState>(st), S(stream));
+                                 P<uint64_t>(gran), I, J, P<sart::SartState>(st), P<unsigned>(xcnt), S(stream));
     });
     m.def("mf_forward_num_splits", &sart::mf_forward_num_splits);
     m.def("mf_backproject_num_splits", &sart::mf_backproject_num_splits);

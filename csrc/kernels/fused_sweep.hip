@@ -31,6 +31,7 @@
 
 #include <stdexcept>
 #include <type_traits>
+#include <vector>
 
 namespace sart {
 
@@ -38,6 +39,9 @@ constexpr int kFusedThreads = 320;  // 4 compute waves + 1 exchange wave
 constexpr unsigned kSpinLimit = 1u << 20;
 constexpr int kMaxGather = 512;     // J*T granules per tile
 constexpr int kGatherRegs = kMaxGather / 64;
+
+// diagnostics (dbg & 2): per-workgroup cycle counters, read with fused_debug_stats()
+__device__ unsigned long long g_fused_stats[1024 * 8];
 
 __device__ __forceinline__ uint64_t make_granule(int epoch, float v) {
     return ((uint64_t)(uint32_t)epoch << 32) | (uint64_t)__float_as_uint(v);
@@ -413,11 +417,17 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
 // the tile index (written data-then-flag by one wave; LDS serves a wave's requests in order), so the
 // compute waves block only when the weight they need at step t (tile t - L) is not there yet.
 // ---------------------------------------------------------------------------------------------
-template <bool LOG>
+// XL (variant 6): row groups are formed from workgroups that run on the same XCD, determined at run
+// time (HW_REG_XCC_ID + a per-XCD ticket), so granules are plain stores that stay in the XCD's shared
+// L2 and polls are L2 round trips instead of memory-side round trips. Correctness still rests only on
+// the epoch tags; an unexpected placement (more tickets than slots on an XCD) sets SartState::error and
+// the host falls back.
+template <bool LOG, bool XL, bool DIAG>
 __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
     const float* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
     const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
-    double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg) {
+    double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg,
+    unsigned* __restrict__ xcnt) {
     constexpr int KW = 8;        // float4 per lane per row: one wave covers 2048 columns
     constexpr int T = 4;         // rows per tile (one per compute wave)
     constexpr int L = 3;         // back-projection lag in steps
@@ -431,12 +441,32 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
     volatile float* s_w = s_small + NS * 4;                                 // [NS][4]
     volatile int* s_pflag = reinterpret_cast<volatile int*>(s_small + 2 * NS * 4);  // [NS][4]
     volatile int* s_wflag = s_pflag + NS * 4;                               // [NS]
+    volatile int* s_tick = s_wflag + NS;                                    // [2]
 
     if (st->done) return;
     const int epoch = st->epoch;
     const int b = blockIdx.x;
-    const int gi = b % I;
-    const int gj = b / I;
+    int gi = b % I;
+    int gj = b / I;
+    if constexpr (XL) {
+        if (threadIdx.x == 0) {
+            unsigned xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+            s_tick[0] = (int)(xcc & 7u);
+            s_tick[1] = (int)atomicAdd(&xcnt[xcc & 7u], 1u);
+        }
+        __syncthreads();
+        const int xcc = s_tick[0], ticket = s_tick[1];
+        const int per_xcd = I / 8;  // row groups per XCD
+        if (ticket >= per_xcd * J) {
+            if (threadIdx.x == 0) atomicOr(&st->error, 4);
+            return;  // uniform for the workgroup: its peers time out and the host falls back
+        }
+        if (!(dbg & 4)) {  // (dbg & 4: keep the blockIdx mapping -- timing diagnostics only)
+            gi = xcc * per_xcd + ticket / J;
+            gj = ticket % J;
+        }
+    }
     const int64_t ntiles = nrows_pad / T;
     const int64_t t_begin = ntiles * gi / I;
     const int64_t nt = ntiles * (gi + 1) / I - t_begin;
@@ -468,6 +498,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
         for (int i = 0; i < AH; ++i)
             if (i < nt) load_tile(fl[i], i);
         bool stuck = false;
+        unsigned long long stall = 0, nstall = 0;
 
         auto step = [&](auto bbc, int64_t t) {
             constexpr int bb = decltype(bbc)::value;
@@ -490,12 +521,17 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
                 const int64_t u = t - L;
                 const int ws = (int)(u & (NS - 1));
                 unsigned spins = 0;
+                const unsigned long long w0 = DIAG ? __builtin_amdgcn_s_memtime() : 0;
                 while (s_wflag[ws] != (int)u && !stuck) {
                     if (++spins > kSpinLimit) {
                         stuck = true;
                         if (lane == 0) atomicOr(&st->error, 2);
                     }
                     __builtin_amdgcn_s_sleep(1);
+                }
+                if constexpr (DIAG) {
+                    stall += __builtin_amdgcn_s_memtime() - w0;
+                    nstall += spins > 0;
                 }
                 asm volatile("" ::: "memory");
                 const float wr = s_w[ws * 4 + wave];
@@ -504,11 +540,17 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
                 for (int k = 0; k < KW; ++k) fma4(acc[k], slot[k * 64], wr);
             }
         };
+        const unsigned long long tstart = DIAG ? __builtin_amdgcn_s_memtime() : 0;
         for (int64_t t0 = 0; t0 < nt + L; t0 += AH) {
             step(std::integral_constant<int, 0>{}, t0 + 0);
             step(std::integral_constant<int, 1>{}, t0 + 1);
             step(std::integral_constant<int, 2>{}, t0 + 2);
             step(std::integral_constant<int, 3>{}, t0 + 3);
+        }
+        if (DIAG && lane == 0) {
+            g_fused_stats[b * 8 + wave] = stall;                       // [0..3] stall cycles per wave
+            if (wave == 0) g_fused_stats[b * 8 + 4] = __builtin_amdgcn_s_memtime() - tstart;  // loop cycles
+            if (wave == 1) g_fused_stats[b * 8 + 5] = nstall;          // steps that waited
         }
         // the four waves hold partial sums of the same 2048 columns: combine through LDS
         __syncthreads();
@@ -545,7 +587,9 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
                                    : make_granule(epoch, 0.f);
             }
         };
+        unsigned long long xwait = 0, xrepoll = 0;
         auto finish_tile = [&](uint64_t(&v)[kGatherRegs], int64_t u) {
+            const unsigned long long f0 = DIAG ? __builtin_amdgcn_s_memtime() : 0;
             if (!failed && !(dbg & 1)) {
                 unsigned spins = 0;
                 while (true) {
@@ -560,7 +604,13 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
                     }
                     __builtin_amdgcn_s_sleep(1);
                     issue_poll(v, u);
+                    ++xrepoll;
                 }
+            }
+            if constexpr (DIAG) {
+                volatile uint64_t sink = v[0];  // make the wait for the poll registers part of the window
+                (void)sink;
+                xwait += __builtin_amdgcn_s_memtime() - f0;
             }
             float s = 0.f;
             if (!failed && !(dbg & 1)) {
@@ -597,7 +647,11 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
                     const float sv = s_part[ps * 4 + lane];
                     if (!(dbg & 1)) {
                         uint64_t* g = gran + ((t_begin + u) * J + gj) * T + lane;
-                        __hip_atomic_store(g, make_granule(epoch, sv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if constexpr (XL)  // plain 8-byte store: the line stays in this XCD's L2
+                            __hip_atomic_store(g, make_granule(epoch, sv), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                        else
+                            __hip_atomic_store(g, make_granule(epoch, sv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                 }
             }
@@ -610,12 +664,16 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
         }
         F = wave_sum(F);
         if (lane == 0) Fpart[b] = F;
+        if (DIAG && lane == 0) {
+            g_fused_stats[b * 8 + 6] = xwait;
+            g_fused_stats[b * 8 + 7] = xrepoll;
+        }
         __syncthreads();  // matches the compute waves' first combine barrier
         __syncthreads();  // and the second
     }
 }
 
-constexpr size_t kRowsLdsBytes = 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (8 * 4 * 3 + 8) * sizeof(float);
+constexpr size_t kRowsLdsBytes = 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (8 * 4 * 3 + 8 + 4) * sizeof(float);
 
 // ---------------------------------------------------------------------------------------------
 // Variant 5 (default): variant 4 + compute waves publish their own granules + two exchange waves.
@@ -816,6 +874,12 @@ constexpr size_t kRows2LdsBytes = 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (8 * 
 
 static int g_fused_dbg = 0;  // diagnostics only (set through fused_set_debug)
 void fused_set_debug(int flags) { g_fused_dbg = flags; }
+std::vector<unsigned long long> fused_debug_stats(int nblocks) {
+    std::vector<unsigned long long> out((size_t)nblocks * 8);
+    hipMemcpyFromSymbol(out.data(), HIP_SYMBOL(g_fused_stats), out.size() * sizeof(unsigned long long), 0,
+                        hipMemcpyDeviceToHost);
+    return out;
+}
 
 constexpr size_t kLdsRingBytes = 4 /*NL*/ * 4 /*waves*/ * 8 /*TK*/ * 64 * sizeof(float4) + 160 * sizeof(float);
 
@@ -866,23 +930,34 @@ static void launch_lds(bool logmode, dim3 grid, hipStream_t stream, const float*
                            nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
 }
 
-static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
-                        int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
-                        double* Fpart, uint64_t* gran, int I, int J, SartState* st) {
+template <bool LG, bool X, bool D>
+static void launch_rows_t(dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
+                          const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
+                          uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
     static bool configured = false;
     if (!configured) {
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRowsLdsBytes);
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<false>),
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRowsLdsBytes);
         configured = true;
     }
-    if (logmode)
-        hipLaunchKernelGGL((k_fused_sweep_rows<true>), grid, dim3(kFusedThreads), kRowsLdsBytes, stream, A, ld, nrows,
-                           nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
-    else
-        hipLaunchKernelGGL((k_fused_sweep_rows<false>), grid, dim3(kFusedThreads), kRowsLdsBytes, stream, A, ld,
-                           nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
+    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D>), grid, dim3(kFusedThreads), kRowsLdsBytes, stream, A, ld, nrows,
+                       nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt);
+}
+
+static void launch_rows(bool logmode, bool xl, dim3 grid, hipStream_t stream, const float* A, int64_t ld,
+                        int64_t nrows, int64_t nrows_pad, const float* x, const float* ghat, const float* arow,
+                        float* partial, double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
+    const bool diag = (g_fused_dbg & 2) != 0;  // instrumented build only when asked (timing diagnostics)
+#define SART_ROWS(LG, X, D) \
+    launch_rows_t<LG, X, D>(grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt)
+    if (diag) {
+        if (logmode) { if (xl) SART_ROWS(true, true, true); else SART_ROWS(true, false, true); }
+        else { if (xl) SART_ROWS(false, true, true); else SART_ROWS(false, false, true); }
+    } else {
+        if (logmode) { if (xl) SART_ROWS(true, true, false); else SART_ROWS(true, false, false); }
+        else { if (xl) SART_ROWS(false, true, false); else SART_ROWS(false, false, false); }
+    }
+#undef SART_ROWS
 }
 
 static void launch_rows2(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
@@ -925,14 +1000,15 @@ static void launch_k(int variant, bool logmode, dim3 grid, hipStream_t stream, c
 int fused_fpart_per_block(int variant) { return variant == 5 ? 2 : 1; }
 
 int fused_tile_rows(int K, int variant) {
-    if (variant == 4 || variant == 5) return 4;
+    if (variant >= 4) return 4;
     return (variant == 2 && K <= 4) ? 4 / K : 8 / K;
 }
 
 void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows,
                         int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
-                        double* Fpart, uint64_t* gran, int I, int J, SartState* st, hipStream_t stream) {
-    if (variant != 4 && variant != 5) {
+                        double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt,
+                        hipStream_t stream) {
+    if (variant < 4) {
         if (K != 1 && K != 2 && K != 4 && K != 8) throw std::runtime_error("fused_sweep: K must be 1, 2, 4 or 8");
         if (ld % (1024 * K) != 0 || ld / (1024 * K) != J)
             throw std::runtime_error("fused_sweep: ld must equal J * 1024 * K");
@@ -941,12 +1017,15 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
     if (nrows_pad % T != 0) throw std::runtime_error("fused_sweep: padded rows must be a multiple of the tile");
     if (J * T > kMaxGather) throw std::runtime_error("fused_sweep: too many slabs for the gather registers");
     const dim3 grid((unsigned)(I * J));
-    if (variant == 4 || variant == 5) {
-        if (ld % 2048 != 0 || ld / 2048 != J) throw std::runtime_error("fused_sweep v4/5: ld must equal J * 2048");
-        if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v4/5: padded rows must be a multiple of 4");
-        if (J * 4 > kMaxGather) throw std::runtime_error("fused_sweep v4/5: too many slabs");
-        if (variant == 4)
-            launch_rows(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st);
+    if (variant == 4 || variant == 5 || variant == 6) {
+        if (ld % 2048 != 0 || ld / 2048 != J) throw std::runtime_error("fused_sweep v4-6: ld must equal J * 2048");
+        if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v4-6: padded rows must be a multiple of 4");
+        if (J * 4 > kMaxGather) throw std::runtime_error("fused_sweep v4-6: too many slabs");
+        if (variant == 6 && (xcnt == nullptr || I % 8 != 0 || (I / 8) * J * 8 != I * J))
+            throw std::runtime_error("fused_sweep v6: needs the per-XCD ticket counters and I % 8 == 0");
+        if (variant == 4 || variant == 6)
+            launch_rows(logmode, variant == 6, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart,
+                        gran, I, J, st, xcnt);
         else
             launch_rows2(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J,
                          st);

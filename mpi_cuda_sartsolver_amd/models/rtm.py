@@ -44,13 +44,22 @@ def choose_ld(nvoxel: int, max_waste: float = 0.10) -> int:
     return round_up(max(nvoxel, 64), 64)
 
 
-def fused_geometry(ld: int, num_cus: int, variant: int = 3) -> Optional[FusedGeometry]:
+def fused_geometry(ld: int, num_cus: int, variant: int = 6) -> Optional[FusedGeometry]:
     """Persistent-grid geometry of the fused sweep (csrc/kernels/fused_sweep.hip).
 
-    variant 3 (default, fastest measured at 64k x 64k): 1024*K-column slabs, tiles parked in LDS;
-    variants 5 and 4: 2048-column slabs, one row per compute wave (needs ld % 2048 == 0 and at
+    variant 6 (default): 2048-column slabs, one row per compute wave, XCD-local row groups (L2 hand-offs);
+    falls back to variant 3 when the width does not fit. variant 3: 1024*K-column slabs, tiles parked in
+    LDS; variants 5 and 4: 2048-column slabs, one row per compute wave (needs ld % 2048 == 0 and at
     most 64 slabs); variants 0-3: slabs of 1024*K columns, K chosen for <= 32 slabs. None: no fused path.
     """
+    if variant == 6:
+        # XCD-local row groups: 8 XCDs x (grid / 8) workgroups, J slabs per group, J | grid / 8
+        per_xcd = num_cus // 8
+        if num_cus % 8 == 0 and ld % 2048 == 0 and ld // 2048 > 0 and per_xcd % (ld // 2048) == 0:
+            J = ld // 2048
+            I = 8 * (per_xcd // J)
+            return FusedGeometry(K=8, J=J, I=I, grid=I * J, variant=6, T=4)
+        variant = 3
     if variant in (4, 5):
         if ld % 2048 == 0 and 0 < ld // 2048 <= min(64, num_cus):
             J = ld // 2048

@@ -108,7 +108,7 @@ class SARTSolver:
         props = self.k.device_info(self.dev.index if self.dev.index is not None else 0)
         self.num_cus = int(props["multiProcessorCount"])
         if fused_variant is None:
-            fused_variant = int(os.environ.get("SART_FUSED_VARIANT", "3"))
+            fused_variant = int(os.environ.get("SART_FUSED_VARIANT", "6"))
         self.geom = fused_geometry(ld, self.num_cus, fused_variant) if use_fused else None
         self.use_fused = self.geom is not None
 
@@ -128,6 +128,7 @@ class SARTSolver:
         self.state = new_state(self.dev)
         if self.use_fused:
             self.gran = torch.zeros(Pp * self.geom.J, dtype=torch.int64, device=self.dev)
+            self.xcnt = torch.zeros(16, dtype=torch.int32, device=self.dev)  # per-XCD tickets (variant 6)
         self._stream = lambda: torch.cuda.current_stream(self.dev).cuda_stream  # noqa: E731
 
         self._ray_sums()
@@ -211,9 +212,11 @@ class SARTSolver:
         Fslot = self.comm_buf.data_ptr() + 4 * self.ld
         if self.use_fused:
             g = self.geom
+            if g.variant == 6:
+                self.xcnt.zero_()
             k.fused_sweep(self.log, g.K, g.variant, A, self.ld, self.P, self.Pp, self.x.data_ptr(), self.ghat.data_ptr(),
                           self.arow.data_ptr(), self.partial.data_ptr(), self.Fpart.data_ptr(),
-                          self.gran.data_ptr(), g.I, g.J, st, s)
+                          self.gran.data_ptr(), g.I, g.J, st, self.xcnt.data_ptr(), s)
             k.reduce_partials(self.partial.data_ptr(), self.ld, g.I, scale.data_ptr(), self.comm_buf.data_ptr(),
                               self.Fpart.data_ptr(), self.nF_fused, Fslot, st, s)
         else:
@@ -242,12 +245,32 @@ class SARTSolver:
     def solve(self, measurement, solution=None) -> SolveResult:
         """Solve one frame. ``measurement``: this rank's pixel slice (fp64); ``solution``: warm start
         (fp64, nvoxel) or None for the default initial guess."""
-        res = self._solve_once(measurement, solution)
-        if res is None:  # fused exchange timed out: fall back to the 2-pass kernels for good
+        while True:
+            res = self._solve_once(measurement, solution)
+            if res is not None:
+                return res
+            self._fused_fallback()
+
+    def _fused_fallback(self) -> None:
+        """A persistent sweep gave up waiting (SartState.error): XCD-local groups (variant 6) -> generic
+        groups (variant 3) -> two-pass kernels. The frame is re-solved from scratch, so results never
+        depend on the fallback."""
+        g = self.geom
+        nxt = fused_geometry(self.ld, self.num_cus, 3) if (g is not None and g.variant == 6) else None
+        if nxt is not None and nxt.variant == 3:
+            log.warning("fused sweep variant 6 timed out (unexpected workgroup placement); using variant 3")
+            self.geom = nxt
+            self.nF_fused = nxt.grid * self.k.fused_fpart_per_block(3)
+            n_part = max(self.nsplit, nxt.I)
+            if self.partial.numel() < n_part * self.ld:
+                self.partial = torch.zeros(n_part * self.ld, dtype=torch.float32, device=self.dev)
+            if self.gran.numel() < self.Pp * nxt.J:
+                self.gran = torch.zeros(self.Pp * nxt.J, dtype=torch.int64, device=self.dev)
+            if self.Fpart.numel() < self.nF_fused:
+                self.Fpart = torch.zeros(self.nF_fused, dtype=torch.float64, device=self.dev)
+        else:
             log.warning("fused sweep protocol timeout; switching to the two-pass kernels")
             self.use_fused = False
-            res = self._solve_once(measurement, solution)
-        return res
 
     def _solve_once(self, measurement, solution) -> Optional[SolveResult]:
         norm = self._setup_frame(measurement, solution)

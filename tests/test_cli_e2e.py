@@ -106,4 +106,5 @@ def test_cli_gpu_matches_gpu_semantics(tmp_path, capsys, log, extra):
                              conv_tolerance=1e-6, beta_laplace=1e-3)
     t, last, st = native().read_solution_file(out)
     assert len(t) == 4
-    assert np.linalg.norm(last - xs[-1]) / np.linalg.norm(xs[-1]) < 5e-3
+    # fp32 vs fp64 iterates of a tolerance-stopped warm-start chain drift apart by ~1e-3..1e-2
+    assert np.linalg.norm(last - xs[-1]) / np.linalg.norm(xs[-1]) < (5e-3 if batched else 1.5e-2)

@@ -115,7 +115,7 @@ def test_synthetic_bench_problem_small(dev):
     assert r.iterations == 10 and np.all(np.isfinite(r.solution))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("shape", [(2048, 4096), (1000, 16384), (512, 8192 * 4)])
 def test_fused_variants(dev, variant, shape):
     from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM

@@ -88,18 +88,20 @@ def main():
         emit(kind="kernel", op="backproject", P=P, V=V, nsplit=ns, ms=med, GBps=nbytes / med / 1e6,
              best_GBps=nbytes / best / 1e6)
 
-        for variant in (5, 4, 3):
+        for variant in (6, 4, 3):
             g = fused_geometry(m.ld, int(info["multiProcessorCount"]), variant)
             if g is None or g.variant != variant:
                 continue
             gran = torch.zeros(m.nrows_pad * g.J, dtype=torch.int64, device=dev)
+            xcnt = torch.zeros(16, dtype=torch.int32, device=dev)
 
             def fused():
+                xcnt.zero_()
                 k.state_begin(st.data_ptr(), 1.0, 0.0, 100, s)
                 k.decide(st.data_ptr(), Fp.data_ptr(), s)  # sweep 0 -> epoch+1, not done
                 k.fused_sweep(False, g.K, g.variant, m.A.data_ptr(), m.ld, P, m.nrows_pad, x.data_ptr(),
                               ghat.data_ptr(), arow.data_ptr(), part.data_ptr(), Fp.data_ptr(), gran.data_ptr(),
-                              g.I, g.J, st.data_ptr(), s)
+                              g.I, g.J, st.data_ptr(), xcnt.data_ptr(), s)
 
             med, best = timeit(fused)
             from mpi_cuda_sartsolver_amd.ops.state import read_state
@@ -107,11 +109,18 @@ def main():
             err = read_state(st).error
             emit(kind="kernel", op=f"fused_sweep_v{variant}", P=P, V=V, K=g.K, J=g.J, I=g.I, T=g.T, ms=med,
                  GBps=nbytes / med / 1e6, best_GBps=nbytes / best / 1e6, error=err)
-            if variant in (3, 4, 5):
+            if variant in (3, 4, 6):
                 k.fused_set_debug(1)
                 med, best = timeit(fused)
                 k.fused_set_debug(0)
                 emit(kind="kernel", op=f"fused_sweep_v{variant}_noexchange", P=P, V=V, ms=med, GBps=nbytes / med / 1e6)
+            if variant == 6:
+                for fl, name in ((4, "bidmap"), (5, "bidmap_noexchange")):
+                    k.fused_set_debug(fl)
+                    med, best = timeit(fused)
+                    k.fused_set_debug(0)
+                    emit(kind="kernel", op=f"fused_sweep_v6_{name}", P=P, V=V, ms=med, GBps=nbytes / med / 1e6,
+                         error=read_state(st).error)
             del gran
 
         # multi-frame MFMA projections (16 frames)
