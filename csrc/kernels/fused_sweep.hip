@@ -422,14 +422,19 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
 // L2 and polls are L2 round trips instead of memory-side round trips. Correctness still rests only on
 // the epoch tags; an unexpected placement (more tickets than slots on an XCD) sets SartState::error and
 // the host falls back.
-template <bool LOG, bool XL, bool DIAG>
+// T (rows per tile) trades row-group width against hand-off volume: the 4 compute waves cover T rows x
+// (4 / T) sub-slabs of 2048 columns, so a workgroup's slab is 8192 / T columns and a row's dot is split
+// over J = ld * T / 8192 workgroups. T = 1 needs only J granules per tile (8 peers at ld = 65536 instead
+// of 32), so a late peer delays fewer workgroups; the waves of one row are summed by the exchange wave.
+template <bool LOG, bool XL, bool DIAG, int T>
 __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
     const float* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
     const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
     double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg,
     unsigned* __restrict__ xcnt) {
+    static_assert(T == 1 || T == 2 || T == 4, "rows per tile");
     constexpr int KW = 8;        // float4 per lane per row: one wave covers 2048 columns
-    constexpr int T = 4;         // rows per tile (one per compute wave)
+    constexpr int WPR = 4 / T;   // compute waves per row (each on its own 2048-column sub-slab)
     constexpr int L = 3;         // back-projection lag in steps
     constexpr int NL = L + 1;    // LDS ring slots (32 KB each)
     constexpr int AH = 4;        // tiles in flight per wave (4 x 8 KB)
@@ -478,9 +483,11 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
     __syncthreads();
 
     if (wave < 4) {
-        const int64_t col4 = (int64_t)gj * (64 * KW) + lane;  // + k * 64
+        const int wrow = wave / WPR, wsub = wave % WPR;
+        const int64_t slab4 = (int64_t)gj * (64 * KW * WPR);                // first float4 of the slab
+        const int64_t col4 = slab4 + wsub * (64 * KW) + lane;              // + k * 64
         const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
-        const float4* __restrict__ a4 = reinterpret_cast<const float4*>(A) + col4 + (int64_t)wave * ld4;
+        const float4* __restrict__ a4 = reinterpret_cast<const float4*>(A) + col4 + (int64_t)wrow * ld4;
         float4* ring = s_ring + (wave * KW) * 64 + lane;
         float4 xs[KW], acc[KW];
 #pragma unroll
@@ -534,7 +541,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
                     nstall += spins > 0;
                 }
                 asm volatile("" ::: "memory");
-                const float wr = s_w[ws * 4 + wave];
+                const float wr = s_w[ws * 4 + wrow];
                 const float4* slot = ring + (int)(u % NL) * (4 * KW * 64);
 #pragma unroll
                 for (int k = 0; k < KW; ++k) fma4(acc[k], slot[k * 64], wr);
@@ -552,26 +559,27 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
             if (wave == 0) g_fused_stats[b * 8 + 4] = __builtin_amdgcn_s_memtime() - tstart;  // loop cycles
             if (wave == 1) g_fused_stats[b * 8 + 5] = nstall;          // steps that waited
         }
-        // the four waves hold partial sums of the same 2048 columns: combine through LDS
+        // the T waves of a sub-slab hold partial sums of the same 2048 columns: combine through LDS
         __syncthreads();
         float4* red = s_ring + (wave * KW) * 64 + lane;
 #pragma unroll
         for (int k = 0; k < KW; ++k) red[k * 64] = acc[k];
         __syncthreads();
-        float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld) + col4;
+        float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld) + slab4 + lane;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const int k = wave * 2 + kk;
-            float4 v = s_ring[(0 * KW + k) * 64 + lane];
+        for (int i = 0; i < 2 * WPR; ++i) {  // q = sub * KW + k, spread over the four waves
+            const int q = wave + 4 * i;
+            const int sub = q / KW, k = q % KW;
+            float4 v = s_ring[(sub * KW + k) * 64 + lane];  // wave (row 0, sub)
 #pragma unroll
-            for (int ww = 1; ww < 4; ++ww) {
-                const float4 o = s_ring[(ww * KW + k) * 64 + lane];
+            for (int rr = 1; rr < T; ++rr) {
+                const float4 o = s_ring[((rr * WPR + sub) * KW + k) * 64 + lane];
                 v.x += o.x;
                 v.y += o.y;
                 v.z += o.z;
                 v.w += o.w;
             }
-            out[k * 64] = v;
+            out[q * 64] = v;
         }
     } else {
         const int n = J * T;
@@ -638,13 +646,18 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
             if (u < nt) {
                 const int ps = (int)(u & (NS - 1));
                 if (lane < T) {
-                    unsigned spins = 0;
-                    while (s_pflag[ps * 4 + lane] != (int)u) {
-                        if (++spins > kSpinLimit) break;  // compute waves always publish: cannot trigger
-                        __builtin_amdgcn_s_sleep(1);
+                    float sv = 0.f;
+#pragma unroll
+                    for (int i = 0; i < WPR; ++i) {  // fixed order: bitwise reproducible row partial
+                        const int wv = lane * WPR + i;
+                        unsigned spins = 0;
+                        while (s_pflag[ps * 4 + wv] != (int)u) {
+                            if (++spins > kSpinLimit) break;  // compute waves always publish: cannot trigger
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                        asm volatile("" ::: "memory");
+                        sv += s_part[ps * 4 + wv];
                     }
-                    asm volatile("" ::: "memory");
-                    const float sv = s_part[ps * 4 + lane];
                     if (!(dbg & 1)) {
                         uint64_t* g = gran + ((t_begin + u) * J + gj) * T + lane;
                         if constexpr (XL)  // plain 8-byte store: the line stays in this XCD's L2
@@ -930,26 +943,27 @@ static void launch_lds(bool logmode, dim3 grid, hipStream_t stream, const float*
                            nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
 }
 
-template <bool LG, bool X, bool D>
+template <bool LG, bool X, bool D, int T>
 static void launch_rows_t(dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                           const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                           uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
     static bool configured = false;
     if (!configured) {
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D>),
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRowsLdsBytes);
         configured = true;
     }
-    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D>), grid, dim3(kFusedThreads), kRowsLdsBytes, stream, A, ld, nrows,
+    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T>), grid, dim3(kFusedThreads), kRowsLdsBytes, stream, A, ld, nrows,
                        nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt);
 }
 
+template <int T>
 static void launch_rows(bool logmode, bool xl, dim3 grid, hipStream_t stream, const float* A, int64_t ld,
                         int64_t nrows, int64_t nrows_pad, const float* x, const float* ghat, const float* arow,
                         float* partial, double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
     const bool diag = (g_fused_dbg & 2) != 0;  // instrumented build only when asked (timing diagnostics)
 #define SART_ROWS(LG, X, D) \
-    launch_rows_t<LG, X, D>(grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt)
+    launch_rows_t<LG, X, D, T>(grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt)
     if (diag) {
         if (logmode) { if (xl) SART_ROWS(true, true, true); else SART_ROWS(true, false, true); }
         else { if (xl) SART_ROWS(false, true, true); else SART_ROWS(false, false, true); }
@@ -1000,6 +1014,7 @@ static void launch_k(int variant, bool logmode, dim3 grid, hipStream_t stream, c
 int fused_fpart_per_block(int variant) { return variant == 5 ? 2 : 1; }
 
 int fused_tile_rows(int K, int variant) {
+    if (variant == 4 || variant == 6) return K;  // K carries the rows per tile for variants 4 and 6
     if (variant >= 4) return 4;
     return (variant == 2 && K <= 4) ? 4 / K : 8 / K;
 }
@@ -1018,15 +1033,23 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
     if (J * T > kMaxGather) throw std::runtime_error("fused_sweep: too many slabs for the gather registers");
     const dim3 grid((unsigned)(I * J));
     if (variant == 4 || variant == 5 || variant == 6) {
-        if (ld % 2048 != 0 || ld / 2048 != J) throw std::runtime_error("fused_sweep v4-6: ld must equal J * 2048");
+        if (variant != 5 && T != 1 && T != 2 && T != 4)
+            throw std::runtime_error("fused_sweep v4/v6: rows per tile (K) must be 1, 2 or 4");
+        const int64_t slab = variant == 5 ? 2048 : 8192 / T;  // columns per workgroup
+        if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep v4-6: ld must equal J * slab");
         if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v4-6: padded rows must be a multiple of 4");
         if (J * 4 > kMaxGather) throw std::runtime_error("fused_sweep v4-6: too many slabs");
         if (variant == 6 && (xcnt == nullptr || I % 8 != 0 || (I / 8) * J * 8 != I * J))
             throw std::runtime_error("fused_sweep v6: needs the per-XCD ticket counters and I % 8 == 0");
-        if (variant == 4 || variant == 6)
-            launch_rows(logmode, variant == 6, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart,
-                        gran, I, J, st, xcnt);
-        else
+        if (variant == 4 || variant == 6) {
+#define SART_RT(TT)                                                                                              \
+    launch_rows<TT>(logmode, variant == 6, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, \
+                    gran, I, J, st, xcnt)
+            if (T == 1) SART_RT(1);
+            else if (T == 2) SART_RT(2);
+            else SART_RT(4);
+#undef SART_RT
+        } else
             launch_rows2(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J,
                          st);
         check_launch("k_fused_sweep_rows");

@@ -11,6 +11,7 @@ split the columns into J slabs of 1024*K floats (``fused_layout``); otherwise it
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -44,23 +45,34 @@ def choose_ld(nvoxel: int, max_waste: float = 0.10) -> int:
     return round_up(max(nvoxel, 64), 64)
 
 
-def fused_geometry(ld: int, num_cus: int, variant: int = 6) -> Optional[FusedGeometry]:
+def fused_geometry(ld: int, num_cus: int, variant: int = 6, rows_per_tile: Optional[int] = None
+                   ) -> Optional[FusedGeometry]:
     """Persistent-grid geometry of the fused sweep (csrc/kernels/fused_sweep.hip).
 
-    variant 6 (default): 2048-column slabs, one row per compute wave, XCD-local row groups (L2 hand-offs);
-    falls back to variant 3 when the width does not fit. variant 3: 1024*K-column slabs, tiles parked in
-    LDS; variants 5 and 4: 2048-column slabs, one row per compute wave (needs ld % 2048 == 0 and at
-    most 64 slabs); variants 0-3: slabs of 1024*K columns, K chosen for <= 32 slabs. None: no fused path.
+    variant 6 (default): XCD-local row groups (L2 hand-offs); the four compute waves of a workgroup
+    cover T rows x (4 / T) sub-slabs of 2048 columns, so a row is split over J = ld * T / 8192
+    workgroups (T = rows_per_tile or env SART_FUSED_T; default 4, the fastest on MI355X at every
+    measured shape -- profiles/probe_r1_rows_per_tile.jsonl; where T = 4 does not fit, variant 3 beats
+    T = 1/2 and is used instead). Variant 4: same kernel with blockIdx row groups.
+    Variant 5: 2048-column slabs, two exchange waves. Variants 0-3: slabs of 1024*K columns, K chosen
+    for <= 32 slabs (3: tiles parked in LDS). None: no fused path.
     """
-    if variant == 6:
-        # XCD-local row groups: 8 XCDs x (grid / 8) workgroups, J slabs per group, J | grid / 8
+    if rows_per_tile is None and os.environ.get("SART_FUSED_T"):
+        rows_per_tile = int(os.environ["SART_FUSED_T"])
+    if variant in (4, 6):
         per_xcd = num_cus // 8
-        if num_cus % 8 == 0 and ld % 2048 == 0 and ld // 2048 > 0 and per_xcd % (ld // 2048) == 0:
-            J = ld // 2048
-            I = 8 * (per_xcd // J)
-            return FusedGeometry(K=8, J=J, I=I, grid=I * J, variant=6, T=4)
+        for T in ((rows_per_tile,) if rows_per_tile else (4,)):
+            slab = 8192 // T
+            if T not in (1, 2, 4) or ld % slab or ld // slab == 0:
+                continue
+            J = ld // slab
+            if variant == 6 and num_cus % 8 == 0 and per_xcd % J == 0:
+                I = 8 * (per_xcd // J)
+                return FusedGeometry(K=T, J=J, I=I, grid=I * J, variant=6, T=T)
+            if variant == 4 and J <= min(64, num_cus):
+                return FusedGeometry(K=T, J=J, I=max(1, num_cus // J), grid=max(1, num_cus // J) * J, variant=4, T=T)
         variant = 3
-    if variant in (4, 5):
+    if variant == 5:
         if ld % 2048 == 0 and 0 < ld // 2048 <= min(64, num_cus):
             J = ld // 2048
             I = max(1, num_cus // J)

@@ -87,7 +87,8 @@ class SARTSolver:
     def __init__(self, rtm: DenseRTM, laplacian: Optional[LaplacianCSR] = None,
                  comm: Optional[Communicator] = None, params: Optional[SolverParams] = None,
                  logarithmic: bool = False, use_fused: bool = True, check_interval: int = 16,
-                 allow_zero_tolerance: bool = False, fused_variant: Optional[int] = None):
+                 allow_zero_tolerance: bool = False, fused_variant: Optional[int] = None,
+                 fused_rows_per_tile: Optional[int] = None):
         self.k = hip()
         self.rtm = rtm
         self.dev = rtm.device
@@ -109,7 +110,7 @@ class SARTSolver:
         self.num_cus = int(props["multiProcessorCount"])
         if fused_variant is None:
             fused_variant = int(os.environ.get("SART_FUSED_VARIANT", "6"))
-        self.geom = fused_geometry(ld, self.num_cus, fused_variant) if use_fused else None
+        self.geom = fused_geometry(ld, self.num_cus, fused_variant, fused_rows_per_tile) if use_fused else None
         self.use_fused = self.geom is not None
 
         self.nsplit = self.k.backproject_num_splits(ld, Pp)

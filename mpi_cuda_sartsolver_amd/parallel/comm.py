@@ -76,13 +76,14 @@ class TorchDistComm(Communicator):
     def all_reduce_scalar(self, v, op="sum"):
         if self.world_size == 1:
             return float(v)
-        t = torch.tensor([float(v)], dtype=torch.float64, device=self.device)
+        dev = self.device if self.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=_OPS[op], group=self.group)
         return float(t.item())
 
     def barrier(self):
         if self.world_size > 1:
-            if self.backend == "nccl":
+            if self.backend == "nccl" and self.device is not None and self.device.type == "cuda":
                 dist.barrier(group=self.group, device_ids=[self.device.index])
             else:
                 dist.barrier(group=self.group)
@@ -124,12 +125,16 @@ def init_distributed(use_gpu: bool = True, timeout_s: float = 1800.0) -> Communi
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     backend = "nccl" if (use_gpu and torch.cuda.is_available()) else "gloo"
+    # SART_DIST_BACKEND=gloo: exercise the multi-rank GPU path with several ranks on ONE GPU (tests on a
+    # single-GPU box; RCCL refuses two ranks on the same device). Production uses nccl (= RCCL).
+    backend = os.environ.get("SART_DIST_BACKEND", backend)
     if not dist.is_initialized():
         kwargs = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kwargs["device_id"] = torch.device("cuda", torch.cuda.current_device())
         dist.init_process_group(**kwargs)
-    return TorchDistComm()
+    dev = torch.device("cuda", torch.cuda.current_device()) if (use_gpu and torch.cuda.is_available()) else None
+    return TorchDistComm(device=dev)
 
 
 def abort_all(msg: str, code: int = 1) -> None:

@@ -131,3 +131,26 @@ def test_fused_variants(dev, variant, shape):
     assert r.used_fused, "fused exchange timed out"
     x_ref, _, _ = sart_gpu_semantics(A, g, max_iterations=12, conv_tolerance=0.0)
     assert _rel(r.solution, x_ref) < 2e-3
+
+
+@pytest.mark.parametrize("variant", [4, 6])
+@pytest.mark.parametrize("T", [1, 2, 4])
+@pytest.mark.parametrize("log", [False, True])
+def test_fused_rows_per_tile(dev, variant, T, log):
+    """Variants 4/6 with T rows per tile (J = ld * T / 8192 workgroups per row) vs the fp64 oracle."""
+    from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+    from mpi_cuda_sartsolver_amd.utils.synthetic import host_problem
+
+    A, g, _ = host_problem(1500, 32768, seed=T + 11, saturate_fraction=0.02)
+    L = LaplacianCSR.grid_3d(32, 32, 32, device=dev)
+    kw = dict(max_iterations=12, conv_tolerance=0.0, beta_laplace=1e-3)
+    s = SARTSolver(DenseRTM.from_dense(A, device=dev), L, None, SolverParams(**kw), logarithmic=log,
+                   allow_zero_tolerance=True, fused_variant=variant, fused_rows_per_tile=T)
+    assert s.use_fused and s.geom.variant == variant and s.geom.T == T and s.geom.J == 32768 * T // 8192
+    r = s.solve(g)
+    assert r.used_fused, "fused exchange timed out"
+    x_ref, _, _ = sart_gpu_semantics(A, g, L, logarithmic=log, **kw)
+    assert _rel(r.solution, x_ref) < 2e-3

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Multi-rank consistency check of the GPU solver: solve one synthetic global problem on N ranks
+(row-sharded) and save rank 0's solution. Compare outputs of different N (tests/test_gpu_distributed.py)."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--npix", type=int, default=3000)
+    ap.add_argument("--nvox", type=int, default=4096)
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--logarithmic", action="store_true")
+    ap.add_argument("--fused", action="store_true")
+    ap.add_argument("--multiframe", action="store_true")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+    from mpi_cuda_sartsolver_amd.parallel.comm import init_distributed
+    from mpi_cuda_sartsolver_amd.parallel.partition import row_partition
+    from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
+
+    comm = init_distributed(use_gpu=True)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    b = row_partition(a.npix, comm.world_size, comm.rank)
+    prob = make_problem(b.size, a.nvox, row_offset=b.offset, seed=7, device=dev, saturate_fraction=0.02)
+    L = LaplacianCSR.grid_3d(16, 16, 16, device=dev) if a.nvox == 4096 else None
+    params = SolverParams(max_iterations=a.iters, conv_tolerance=1e-6, beta_laplace=1e-3)
+    if a.multiframe:
+        from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+
+        s = MultiFrameSARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic)
+        g = prob.measurement.cpu().numpy()
+        res = s.solve_batch(np.stack([g, 0.5 * g, 2.0 * g]))
+        x = np.stack([r.solution for r in res])
+        meta = [dict(status=r.status, iterations=r.iterations) for r in res]
+    else:
+        s = SARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic, use_fused=a.fused)
+        r = s.solve(prob.measurement)
+        r2 = s.solve(prob.measurement, solution=r.solution)  # warm start path
+        x = np.stack([r.solution, r2.solution])
+        meta = [dict(status=r.status, iterations=r.iterations, fused=r.used_fused),
+                dict(status=r2.status, iterations=r2.iterations)]
+    if comm.rank == 0:
+        np.save(a.out + ".npy", x)
+        with open(a.out + ".json", "w") as f:
+            json.dump(meta, f)
+    comm.barrier()
+
+
+if __name__ == "__main__":
+    main()

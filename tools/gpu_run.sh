@@ -1,7 +1,8 @@
 #!/usr/bin/env bash
 # GPU-box session script: each GPU step has its own time limit; a fault / abort / timeout ends the
 # session (nothing else touches the GPU afterwards); ordinary test failures (exit 1) do not.
-# Usage: tools/gpu_run.sh <step>...   steps: smoke tests bench bench2 prof probe
+# Usage: tools/gpu_run.sh <step>...   steps: smoke tests testsall testsel(SEL=...) bench bench2 benchlog
+#        probe probef prof
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
@@ -30,6 +31,8 @@ for step in "$@"; do
     bench2) run bench_twopass 600 python bench.py --steps 5 --warmup 1 --no-fused ;;
     benchlog) run bench_log 600 python bench.py --steps 5 --warmup 1 --variant log ;;
     probe) run probe 600 python tools/probe.py ;;
+    probef) PROBE_FUSED_ONLY=1 run probe_fused 600 python tools/probe.py ;;
+    testsel) run pytest_sel 900 python -m pytest ${SEL:-tests} -m gpu -q -p no:cacheprovider ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -88,12 +88,14 @@ def main():
         emit(kind="kernel", op="backproject", P=P, V=V, nsplit=ns, ms=med, GBps=nbytes / med / 1e6,
              best_GBps=nbytes / best / 1e6)
 
-        for variant in (6, 4, 3):
-            g = fused_geometry(m.ld, int(info["multiProcessorCount"]), variant)
-            if g is None or g.variant != variant:
+        for variant, T in ((6, 1), (6, 2), (6, 4), (4, 1), (4, 4), (3, None)):
+            g = fused_geometry(m.ld, int(info["multiProcessorCount"]), variant, T)
+            if g is None or g.variant != variant or (T is not None and g.T != T):
                 continue
             gran = torch.zeros(m.nrows_pad * g.J, dtype=torch.int64, device=dev)
             xcnt = torch.zeros(16, dtype=torch.int32, device=dev)
+            if part.numel() < g.I * m.ld:
+                part = torch.zeros(g.I * m.ld, device=dev)
 
             def fused():
                 xcnt.zero_()
@@ -107,22 +109,19 @@ def main():
             from mpi_cuda_sartsolver_amd.ops.state import read_state
 
             err = read_state(st).error
-            emit(kind="kernel", op=f"fused_sweep_v{variant}", P=P, V=V, K=g.K, J=g.J, I=g.I, T=g.T, ms=med,
+            tag = f"fused_sweep_v{variant}" + (f"_T{g.T}" if variant in (4, 6) else "")
+            emit(kind="kernel", op=tag, P=P, V=V, K=g.K, J=g.J, I=g.I, T=g.T, ms=med,
                  GBps=nbytes / med / 1e6, best_GBps=nbytes / best / 1e6, error=err)
-            if variant in (3, 4, 6):
-                k.fused_set_debug(1)
-                med, best = timeit(fused)
-                k.fused_set_debug(0)
-                emit(kind="kernel", op=f"fused_sweep_v{variant}_noexchange", P=P, V=V, ms=med, GBps=nbytes / med / 1e6)
-            if variant == 6:
-                for fl, name in ((4, "bidmap"), (5, "bidmap_noexchange")):
-                    k.fused_set_debug(fl)
-                    med, best = timeit(fused)
-                    k.fused_set_debug(0)
-                    emit(kind="kernel", op=f"fused_sweep_v6_{name}", P=P, V=V, ms=med, GBps=nbytes / med / 1e6,
-                         error=read_state(st).error)
+            k.fused_set_debug(1)
+            med, best = timeit(fused)
+            k.fused_set_debug(0)
+            emit(kind="kernel", op=f"{tag}_noexchange", P=P, V=V, ms=med, GBps=nbytes / med / 1e6)
             del gran
 
+        if os.environ.get("PROBE_FUSED_ONLY"):
+            del m, part
+            torch.cuda.empty_cache()
+            continue
         # multi-frame MFMA projections (16 frames)
         X = torch.rand((16, m.ld), device=dev)
         nsf = k.mf_forward_num_splits(m.ld, m.nrows_pad)
