@@ -98,6 +98,8 @@ def main() -> int:
         "status_last": res.status if res else None,
         "fused_sweep": solver.use_fused,
         "fused_variant": solver.geom.variant if solver.use_fused else None,
+        "fused_rows_per_tile": solver.geom.T if solver.use_fused else None,
+        "fused_schedule": solver.k.fused_get_schedule() if solver.use_fused else None,
         "effective_hbm_TBps_per_gpu": round(bytes_per_iter * iters_per_s / 1e12, 3),
         "config": {
             "model": f"SART-{args.variant} dense RTM",

@@ -51,6 +51,10 @@ void launch_synth_vector(double* out, int64_t n, int64_t offset, uint64_t seed, 
 // fused_sweep.hip
 int fused_pick_k(int64_t ld);
 int fused_tile_rows(int K, int variant);
+void fused_set_schedule(int sched);
+int fused_get_schedule();
+void fused_set_trace(unsigned long long* buf, long long tiles);
+std::vector<int> fused_debug_map(int nblocks);
 int fused_fpart_per_block(int variant);
 void fused_set_debug(int flags);
 std::vector<unsigned long long> fused_debug_stats(int nblocks);
@@ -163,6 +167,12 @@ PYBIND11_MODULE(_sart_hip, m) {
     });
     m.def("fused_pick_k", &sart::fused_pick_k);
     m.def("fused_tile_rows", &sart::fused_tile_rows);
+    m.def("fused_set_schedule", &sart::fused_set_schedule);
+    m.def("fused_get_schedule", &sart::fused_get_schedule);
+    m.def("fused_debug_map", &sart::fused_debug_map);
+    m.def("fused_set_trace", [](uintptr_t buf, long long tiles) {
+        sart::fused_set_trace(reinterpret_cast<unsigned long long*>(buf), tiles);
+    });
     m.def("fused_fpart_per_block", &sart::fused_fpart_per_block);
     m.def("fused_set_debug", &sart::fused_set_debug);
     m.def("fused_debug_stats", &sart::fused_debug_stats);

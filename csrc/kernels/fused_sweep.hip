@@ -31,6 +31,7 @@
 
 #include <stdexcept>
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 namespace sart {
@@ -39,9 +40,20 @@ constexpr int kFusedThreads = 320;  // 4 compute waves + 1 exchange wave
 constexpr unsigned kSpinLimit = 1u << 20;
 constexpr int kMaxGather = 512;     // J*T granules per tile
 constexpr int kGatherRegs = kMaxGather / 64;
+constexpr int kRowsGather = 256;    // J*T granules per tile, rows kernel (variants 4 and 6)
 
 // diagnostics (dbg & 2): per-workgroup cycle counters, read with fused_debug_stats()
 __device__ unsigned long long g_fused_stats[1024 * 8];
+// per-tile event trace of the instrumented rows kernel (dbg & 2 with a buffer set by fused_set_trace):
+// [block][tile][4] s_memrealtime stamps (100 MHz, one clock for all XCDs): 0 = compute wave 0 published its
+// partial, 1 = compute wave 0 got the weight, 2 = exchange stored the granule, 3 = exchange wrote the weight
+__device__ unsigned long long* g_fused_trace = nullptr;
+__device__ int g_fused_map[1024];  // instrumented builds: gi * 1024 + gj of every block
+__device__ long long g_fused_trace_tiles = 0;
+__device__ __forceinline__ void trace_stamp(int b, int64_t tile, int ev) {
+    if (g_fused_trace != nullptr && tile < g_fused_trace_tiles)
+        g_fused_trace[((int64_t)b * g_fused_trace_tiles + tile) * 4 + ev] = __builtin_amdgcn_s_memrealtime();
+}
 
 __device__ __forceinline__ uint64_t make_granule(int epoch, float v) {
     return ((uint64_t)(uint32_t)epoch << 32) | (uint64_t)__float_as_uint(v);
@@ -426,7 +438,21 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
 // (4 / T) sub-slabs of 2048 columns, so a workgroup's slab is 8192 / T columns and a row's dot is split
 // over J = ld * T / 8192 workgroups. T = 1 needs only J granules per tile (8 peers at ld = 65536 instead
 // of 32), so a late peer delays fewer workgroups; the waves of one row are summed by the exchange wave.
-template <bool LOG, bool XL, bool DIAG, int T>
+// SCHED sets the pipeline budget. A hand-off into a CU that streams A costs ~3 us (the poll waits in the
+// consumer CU's own vector memory queue: MI355X_MICROARCH.md price list, handoff-1to1 'L->L'), more than
+// two 1.3 us steps, so the exchange wave keeps PQ polls in flight (poll tile u - PD in exchange step u,
+// finish tile u - PD - PQ + 1); the weights are consumed L >= PD + PQ steps after the reduction:
+//   SCHED  L  AH(in flight) x slab  PD PQ
+//     0    3  4             VGPR    1  2
+//     1    4  4             LDS     1  3     (the newest tile stays in VGPRs one step before parking)
+//     2    4  4             LDS     2  2
+//     3    3  5             LDS     1  2
+// Schedule 2 is the default (profiles/probe_r1_sched.jsonl: 5-8 % faster than 0 at 64k x 64k, 2-3 %
+// at 16k-wide shapes). Compute waves storing their own granules (instead of the exchange wave) measured
+// 8-10 % slower than 2.
+// (LDS x slab: T >= 2 only.) Scalar-memory (s_load glc) polls were measured and are no faster under load:
+// an s_load round trip to L2 costs ~1.2 us while the chip streams.
+template <bool LOG, bool XL, bool DIAG, int T, int SCHED>
 __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
     const float* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
     const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
@@ -435,13 +461,22 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
     static_assert(T == 1 || T == 2 || T == 4, "rows per tile");
     constexpr int KW = 8;        // float4 per lane per row: one wave covers 2048 columns
     constexpr int WPR = 4 / T;   // compute waves per row (each on its own 2048-column sub-slab)
-    constexpr int L = 3;         // back-projection lag in steps
-    constexpr int NL = L + 1;    // LDS ring slots (32 KB each)
-    constexpr int AH = 4;        // tiles in flight per wave (4 x 8 KB)
+    constexpr int D = (SCHED == 1 || SCHED == 2) ? 1 : 0;  // steps a reduced tile stays in VGPRs
+    constexpr bool XS_LDS = SCHED >= 1;                       // x slab in LDS instead of VGPRs
+    static_assert(!XS_LDS || T >= 2, "the LDS holds the x slab only for T >= 2");
+    constexpr int PD = SCHED == 2 ? 2 : 1;   // exchange step u polls tile u - PD
+    constexpr int PQ = SCHED == 1 ? 3 : 2;   // polls in flight (finishes tile u - PD - PQ + 1)
+    constexpr int L = 3 + D;     // back-projection lag in steps
+    static_assert(L >= PD + PQ, "the weights must be ready one step before they are used");
+    constexpr int NL = 4;        // LDS ring slots (32 KB each)
+    constexpr int RS = XS_LDS ? 5 : 4;  // register tile slots per wave (8 KB each): AH in flight + D held
+    constexpr int AH = RS - D;   // tiles in flight per wave
+    static_assert(L >= PD + 2, "the weights must be ready one step before they are used");
     constexpr int NS = 8;        // LDS hand-off slots
 
     extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64]
-    float* s_small = reinterpret_cast<float*>(s_ring + NL * 4 * KW * 64);
+    float4* s_xs = s_ring + NL * 4 * KW * 64;                         // [WPR][KW][64] if XS_LDS
+    float* s_small = reinterpret_cast<float*>(s_xs + (XS_LDS ? WPR * KW * 64 : 0));
     volatile float* s_part = s_small;                                      // [NS][4]
     volatile float* s_w = s_small + NS * 4;                                 // [NS][4]
     volatile int* s_pflag = reinterpret_cast<volatile int*>(s_small + 2 * NS * 4);  // [NS][4]
@@ -478,8 +513,13 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int64_t ld4 = ld >> 2;
+    if (DIAG && threadIdx.x == 0 && b < 1024) g_fused_map[b] = gi * 1024 + gj;
 
     for (int i = threadIdx.x; i < NS * 4 + NS; i += kFusedThreads) s_pflag[i] = -1;
+    if constexpr (XS_LDS) {
+        const float4* xsrc = reinterpret_cast<const float4*>(x) + (int64_t)gj * (64 * KW * WPR);
+        for (int i = threadIdx.x; i < WPR * KW * 64; i += kFusedThreads) s_xs[i] = xsrc[i];
+    }
     __syncthreads();
 
     if (wave < 4) {
@@ -489,13 +529,14 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
         const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
         const float4* __restrict__ a4 = reinterpret_cast<const float4*>(A) + col4 + (int64_t)wrow * ld4;
         float4* ring = s_ring + (wave * KW) * 64 + lane;
-        float4 xs[KW], acc[KW];
+        float4 xs[XS_LDS ? 1 : KW], acc[KW];
+        const float4* xl = s_xs + wsub * (KW * 64) + lane;
 #pragma unroll
         for (int k = 0; k < KW; ++k) {
-            xs[k] = x4[col4 + k * 64];
+            if constexpr (!XS_LDS) xs[k] = x4[col4 + k * 64];
             acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        float4 fl[AH][KW];
+        float4 fl[RS][KW];
         auto load_tile = [&](float4(&dst)[KW], int64_t t) {
             const float4* src = a4 + (t_begin + t) * T * ld4;
 #pragma unroll
@@ -507,23 +548,34 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
         bool stuck = false;
         unsigned long long stall = 0, nstall = 0;
 
+        auto park = [&](float4(&src)[KW], int64_t t) {
+            float4* slot = ring + (int)(t % NL) * (4 * KW * 64);
+#pragma unroll
+            for (int k = 0; k < KW; ++k) slot[k * 64] = src[k];
+        };
         auto step = [&](auto bbc, int64_t t) {
-            constexpr int bb = decltype(bbc)::value;
+            constexpr int bb = decltype(bbc)::value;        // register slot of tile t (t % RS)
+            constexpr int bp = (bb + RS - D) % RS;          // register slot of tile t - D
             if (t < nt) {
                 float s = 0.f;
 #pragma unroll
-                for (int k = 0; k < KW; ++k) s += dot4(fl[bb][k], xs[k]);
+                for (int k = 0; k < KW; ++k) {
+                    if constexpr (XS_LDS)
+                        s += dot4(fl[bb][k], xl[k * 64]);
+                    else
+                        s += dot4(fl[bb][k], xs[k]);
+                }
                 s = wave_sum(s);
                 if (lane == 0) {
                     s_part[(t & (NS - 1)) * 4 + wave] = s;
                     asm volatile("" ::: "memory");
                     s_pflag[(t & (NS - 1)) * 4 + wave] = (int)t;
+                    if (DIAG && wave == 0) trace_stamp(b, t, 0);
                 }
-                float4* slot = ring + (int)(t % NL) * (4 * KW * 64);
-#pragma unroll
-                for (int k = 0; k < KW; ++k) slot[k * 64] = fl[bb][k];
-                if (t + AH < nt) load_tile(fl[bb], t + AH);
             }
+            // park tile t - D (its LDS slot held tile t - D - NL, back-projected in step t - 1)
+            if (t - D >= 0 && t - D < nt) park(fl[bp], t - D);
+            if (t + AH < nt) load_tile(fl[bp], t + AH);  // slot bp is free again
             if (t >= L && t - L < nt) {
                 const int64_t u = t - L;
                 const int ws = (int)(u & (NS - 1));
@@ -539,6 +591,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
                 if constexpr (DIAG) {
                     stall += __builtin_amdgcn_s_memtime() - w0;
                     nstall += spins > 0;
+                    if (wave == 0 && lane == 0) trace_stamp(b, u, 1);
                 }
                 asm volatile("" ::: "memory");
                 const float wr = s_w[ws * 4 + wrow];
@@ -548,11 +601,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
             }
         };
         const unsigned long long tstart = DIAG ? __builtin_amdgcn_s_memtime() : 0;
-        for (int64_t t0 = 0; t0 < nt + L; t0 += AH) {
-            step(std::integral_constant<int, 0>{}, t0 + 0);
-            step(std::integral_constant<int, 1>{}, t0 + 1);
-            step(std::integral_constant<int, 2>{}, t0 + 2);
-            step(std::integral_constant<int, 3>{}, t0 + 3);
+        for (int64_t t0 = 0; t0 < nt + L; t0 += RS) {  // RS steps per pass: register slots are static
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+            }(std::make_integer_sequence<int, RS>{});
         }
         if (DIAG && lane == 0) {
             g_fused_stats[b * 8 + wave] = stall;                       // [0..3] stall cycles per wave
@@ -585,25 +637,26 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
         const int n = J * T;
         bool failed = false;
         double F = 0.0;
-        uint64_t pv[2][kGatherRegs];
-        auto issue_poll = [&](uint64_t(&dst)[kGatherRegs], int64_t u) {
+        constexpr int GR = kRowsGather / 64;  // poll registers per lane (J * T <= kRowsGather)
+        uint64_t pv[PQ][GR];
+        auto issue_poll = [&](uint64_t(&dst)[GR], int64_t u) {
             const uint64_t* g = gran + (t_begin + u) * (int64_t)n;
 #pragma unroll
-            for (int m = 0; m < kGatherRegs; ++m) {
+            for (int m = 0; m < GR; ++m) {
                 const int idx = lane + 64 * m;
                 dst[m] = (idx < n) ? __hip_atomic_load(g + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                    : make_granule(epoch, 0.f);
             }
         };
         unsigned long long xwait = 0, xrepoll = 0;
-        auto finish_tile = [&](uint64_t(&v)[kGatherRegs], int64_t u) {
+        auto finish_tile = [&](uint64_t(&v)[GR], int64_t u) {
             const unsigned long long f0 = DIAG ? __builtin_amdgcn_s_memtime() : 0;
             if (!failed && !(dbg & 1)) {
                 unsigned spins = 0;
                 while (true) {
                     bool ok = true;
 #pragma unroll
-                    for (int m = 0; m < kGatherRegs; ++m) ok &= ((int)(v[m] >> 32) == epoch);
+                    for (int m = 0; m < GR; ++m) ok &= ((int)(v[m] >> 32) == epoch);
                     if (__all(ok)) break;
                     if (++spins > kSpinLimit) {
                         failed = true;
@@ -623,7 +676,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
             float s = 0.f;
             if (!failed && !(dbg & 1)) {
 #pragma unroll
-                for (int m = 0; m < kGatherRegs; ++m) s += __uint_as_float((uint32_t)v[m]);
+                for (int m = 0; m < GR; ++m) s += __uint_as_float((uint32_t)v[m]);
             }
 #pragma unroll
             for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
@@ -640,9 +693,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
             }
             asm volatile("" ::: "memory");
             if (lane == 0) s_wflag[ws] = (int)u;
+            if (DIAG && lane == 0) trace_stamp(b, u, 3);
         };
         auto xiter = [&](auto pc, int64_t u) {
-            constexpr int p = decltype(pc)::value;  // pv[p] receives tile u-1
+            constexpr int p = decltype(pc)::value;  // pv[p] receives tile u - PD
             if (u < nt) {
                 const int ps = (int)(u & (NS - 1));
                 if (lane < T) {
@@ -666,14 +720,17 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
                         else
                             __hip_atomic_store(g, make_granule(epoch, sv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
+                    if (DIAG && lane == 0) trace_stamp(b, u, 2);
                 }
             }
-            if (u >= 1 && u - 1 < nt && !(dbg & 1)) issue_poll(pv[p], u - 1);
-            if (u >= 2 && u - 2 < nt) finish_tile(pv[p ^ 1], u - 2);
+            if (u >= PD && u - PD < nt && !(dbg & 1)) issue_poll(pv[p], u - PD);
+            const int64_t f = u - PD - PQ + 1;  // polled PQ - 1 steps ago into pv[(p + 1) % PQ]
+            if (f >= 0 && f < nt) finish_tile(pv[(p + 1) % PQ], f);
         };
-        for (int64_t u0 = 0; u0 < nt + 2; u0 += 2) {
-            xiter(std::integral_constant<int, 0>{}, u0);
-            xiter(std::integral_constant<int, 1>{}, u0 + 1);
+        for (int64_t u0 = 0; u0 < nt + PD + PQ - 1; u0 += PQ) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (xiter(std::integral_constant<int, Q>{}, u0 + Q), ...);
+            }(std::make_integer_sequence<int, PQ>{});
         }
         F = wave_sum(F);
         if (lane == 0) Fpart[b] = F;
@@ -686,7 +743,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
     }
 }
 
-constexpr size_t kRowsLdsBytes = 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (8 * 4 * 3 + 8 + 4) * sizeof(float);
+constexpr size_t rows_lds_bytes(int T, int sched) {
+    return 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (sched >= 1 ? (4 / T) * 8 * 64 * sizeof(float4) : 0) +
+           (8 * 4 * 3 + 8 + 4) * sizeof(float);
+}
 
 // ---------------------------------------------------------------------------------------------
 // Variant 5 (default): variant 4 + compute waves publish their own granules + two exchange waves.
@@ -885,8 +945,23 @@ __global__ __launch_bounds__(kFused5Threads) void k_fused_sweep_rows2(
 
 constexpr size_t kRows2LdsBytes = 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (8 * 4 * 2 + 8) * sizeof(float);
 
-static int g_fused_dbg = 0;  // diagnostics only (set through fused_set_debug)
+static int g_fused_dbg = 0;    // diagnostics only (set through fused_set_debug)
+static int g_fused_sched = 2;  // variant 6 pipeline schedule (k_fused_sweep_rows SCHED)
 void fused_set_debug(int flags) { g_fused_dbg = flags; }
+void fused_set_schedule(int sched) {
+    if (sched < 0 || sched > 3) throw std::runtime_error("fused_set_schedule: 0 .. 3");
+    g_fused_sched = sched;
+}
+int fused_get_schedule() { return g_fused_sched; }
+std::vector<int> fused_debug_map(int nblocks) {
+    std::vector<int> out((size_t)nblocks);
+    hipMemcpyFromSymbol(out.data(), HIP_SYMBOL(g_fused_map), out.size() * sizeof(int), 0, hipMemcpyDeviceToHost);
+    return out;
+}
+void fused_set_trace(unsigned long long* buf, long long tiles) {
+    hipMemcpyToSymbol(HIP_SYMBOL(g_fused_trace), &buf, sizeof(buf), 0, hipMemcpyHostToDevice);
+    hipMemcpyToSymbol(HIP_SYMBOL(g_fused_trace_tiles), &tiles, sizeof(tiles), 0, hipMemcpyHostToDevice);
+}
 std::vector<unsigned long long> fused_debug_stats(int nblocks) {
     std::vector<unsigned long long> out((size_t)nblocks * 8);
     hipMemcpyFromSymbol(out.data(), HIP_SYMBOL(g_fused_stats), out.size() * sizeof(unsigned long long), 0,
@@ -943,35 +1018,55 @@ static void launch_lds(bool logmode, dim3 grid, hipStream_t stream, const float*
                            nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
 }
 
-template <bool LG, bool X, bool D, int T>
+template <bool LG, bool X, bool D, int T, int SC>
 static void launch_rows_t(dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                           const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                           uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
     static bool configured = false;
     if (!configured) {
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRowsLdsBytes);
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T, SC>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds_bytes(T, SC));
         configured = true;
     }
-    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T>), grid, dim3(kFusedThreads), kRowsLdsBytes, stream, A, ld, nrows,
+    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC>), grid, dim3(kFusedThreads), rows_lds_bytes(T, SC), stream, A, ld, nrows,
                        nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt);
 }
 
 template <int T>
 static void launch_rows(bool logmode, bool xl, dim3 grid, hipStream_t stream, const float* A, int64_t ld,
-                        int64_t nrows, int64_t nrows_pad, const float* x, const float* ghat, const float* arow,
+                        int64_t nrows, int64_t nrows_pad, const float* x_, const float* ghat, const float* arow,
                         float* partial, double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
     const bool diag = (g_fused_dbg & 2) != 0;  // instrumented build only when asked (timing diagnostics)
-#define SART_ROWS(LG, X, D) \
-    launch_rows_t<LG, X, D, T>(grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt)
-    if (diag) {
-        if (logmode) { if (xl) SART_ROWS(true, true, true); else SART_ROWS(true, false, true); }
-        else { if (xl) SART_ROWS(false, true, true); else SART_ROWS(false, false, true); }
+    // g_fused_sched: pipeline schedule of variant 6 (k_fused_sweep_rows SCHED); schedules 1-3 hold the x
+    // slab in LDS, which has room for it only when T >= 2. Instrumented builds: schedules 0 and 2.
+    int sched = xl && T >= 2 ? g_fused_sched : 0;
+    if (diag && sched != 2) sched = 0;
+    auto go = [&](auto lg, auto x, auto d, auto sc) {
+        launch_rows_t<decltype(lg)::value, decltype(x)::value, decltype(d)::value, T, decltype(sc)::value>(
+            grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
+    };
+    using TT = std::true_type;
+    using FF = std::false_type;
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, (T >= 2 ? 1 : 0)>;
+    using S2 = std::integral_constant<int, (T >= 2 ? 2 : 0)>;
+    using S3 = std::integral_constant<int, (T >= 2 ? 3 : 0)>;
+
+    auto by_log = [&](auto x, auto d, auto sc) {
+        if (logmode) go(TT{}, x, d, sc); else go(FF{}, x, d, sc);
+    };
+    if (!xl) {
+        if (diag) by_log(FF{}, TT{}, S0{}); else by_log(FF{}, FF{}, S0{});
+    } else if (diag) {
+        if (sched == 2) by_log(TT{}, TT{}, S2{}); else by_log(TT{}, TT{}, S0{});
     } else {
-        if (logmode) { if (xl) SART_ROWS(true, true, false); else SART_ROWS(true, false, false); }
-        else { if (xl) SART_ROWS(false, true, false); else SART_ROWS(false, false, false); }
+        switch (sched) {
+            case 1: by_log(TT{}, FF{}, S1{}); break;
+            case 2: by_log(TT{}, FF{}, S2{}); break;
+            case 3: by_log(TT{}, FF{}, S3{}); break;
+            default: by_log(TT{}, FF{}, S0{}); break;
+        }
     }
-#undef SART_ROWS
 }
 
 static void launch_rows2(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
@@ -1039,6 +1134,7 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
         if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep v4-6: ld must equal J * slab");
         if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v4-6: padded rows must be a multiple of 4");
         if (J * 4 > kMaxGather) throw std::runtime_error("fused_sweep v4-6: too many slabs");
+        if (variant != 5 && J * T > kRowsGather) throw std::runtime_error("fused_sweep v4/v6: J * T > 256");
         if (variant == 6 && (xcnt == nullptr || I % 8 != 0 || (I / 8) * J * 8 != I * J))
             throw std::runtime_error("fused_sweep v6: needs the per-XCD ticket counters and I % 8 == 0");
         if (variant == 4 || variant == 6) {

@@ -110,6 +110,8 @@ class SARTSolver:
         self.num_cus = int(props["multiProcessorCount"])
         if fused_variant is None:
             fused_variant = int(os.environ.get("SART_FUSED_VARIANT", "6"))
+        if os.environ.get("SART_FUSED_SCHEDULE"):  # variant 6 pipeline schedule (fused_sweep.hip, SCHED)
+            self.k.fused_set_schedule(int(os.environ["SART_FUSED_SCHEDULE"]))
         self.geom = fused_geometry(ld, self.num_cus, fused_variant, fused_rows_per_tile) if use_fused else None
         self.use_fused = self.geom is not None
 

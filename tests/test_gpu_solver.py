@@ -154,3 +154,32 @@ def test_fused_rows_per_tile(dev, variant, T, log):
     assert r.used_fused, "fused exchange timed out"
     x_ref, _, _ = sart_gpu_semantics(A, g, L, logarithmic=log, **kw)
     assert _rel(r.solution, x_ref) < 2e-3
+
+
+@pytest.mark.parametrize("T,sched", [(4, 0), (4, 1), (4, 2), (4, 3), (2, 1), (2, 2), (1, 0)])
+@pytest.mark.parametrize("log", [False, True])
+def test_fused_v6_schedules(dev, T, sched, log):
+    """Variant 6 pipeline schedules (lag 3 / 4, 4-5 tiles in flight, x slab in VGPRs or LDS, 2-3 polls in
+    flight) agree with the oracle."""
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+    from mpi_cuda_sartsolver_amd.ops import hip
+    from mpi_cuda_sartsolver_amd.utils.synthetic import host_problem
+
+    k = hip()
+    shape = (3000, 16384)
+    A, g, _ = host_problem(*shape, seed=sched + 21, saturate_fraction=0.02)
+    kw = dict(max_iterations=10, conv_tolerance=0.0)
+    prev = k.fused_get_schedule()
+    k.fused_set_schedule(sched)
+    try:
+        s = SARTSolver(DenseRTM.from_dense(A, device=dev), None, None, SolverParams(**kw), logarithmic=log,
+                       allow_zero_tolerance=True, fused_variant=6, fused_rows_per_tile=T)
+        assert s.geom.variant == 6 and s.geom.T == T
+        r = s.solve(g)
+    finally:
+        k.fused_set_schedule(prev)
+    assert r.used_fused, "fused exchange timed out"
+    x_ref, _, _ = sart_gpu_semantics(A, g, logarithmic=log, **kw)
+    assert _rel(r.solution, x_ref) < 2e-3

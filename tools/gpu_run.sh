@@ -31,6 +31,7 @@ for step in "$@"; do
     bench2) run bench_twopass 600 python bench.py --steps 5 --warmup 1 --no-fused ;;
     benchlog) run bench_log 600 python bench.py --steps 5 --warmup 1 --variant log ;;
     probe) run probe 600 python tools/probe.py ;;
+    trace) run fused_trace 600 python tools/fused_trace.py ;;
     probef) PROBE_FUSED_ONLY=1 run probe_fused 600 python tools/probe.py ;;
     testsel) run pytest_sel 900 python -m pytest ${SEL:-tests} -m gpu -q -p no:cacheprovider ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 ;;

@@ -88,7 +88,8 @@ def main():
         emit(kind="kernel", op="backproject", P=P, V=V, nsplit=ns, ms=med, GBps=nbytes / med / 1e6,
              best_GBps=nbytes / best / 1e6)
 
-        for variant, T in ((6, 1), (6, 2), (6, 4), (4, 1), (4, 4), (3, None)):
+        cfgs = [(6, 4, 2), (6, 4, 0), (6, 4, 3), (6, 1, 0), (3, None, 0)]
+        for variant, T, sched in cfgs:
             g = fused_geometry(m.ld, int(info["multiProcessorCount"]), variant, T)
             if g is None or g.variant != variant or (T is not None and g.T != T):
                 continue
@@ -98,6 +99,7 @@ def main():
                 part = torch.zeros(g.I * m.ld, device=dev)
 
             def fused():
+                k.fused_set_schedule(sched if sched is not None else 2)
                 xcnt.zero_()
                 k.state_begin(st.data_ptr(), 1.0, 0.0, 100, s)
                 k.decide(st.data_ptr(), Fp.data_ptr(), s)  # sweep 0 -> epoch+1, not done
@@ -109,13 +111,14 @@ def main():
             from mpi_cuda_sartsolver_amd.ops.state import read_state
 
             err = read_state(st).error
-            tag = f"fused_sweep_v{variant}" + (f"_T{g.T}" if variant in (4, 6) else "")
+            tag = f"fused_sweep_v{variant}" + (f"_T{g.T}" if variant in (4, 6) else "") + (f"_s{sched}" if sched else "")
             emit(kind="kernel", op=tag, P=P, V=V, K=g.K, J=g.J, I=g.I, T=g.T, ms=med,
                  GBps=nbytes / med / 1e6, best_GBps=nbytes / best / 1e6, error=err)
             k.fused_set_debug(1)
             med, best = timeit(fused)
             k.fused_set_debug(0)
             emit(kind="kernel", op=f"{tag}_noexchange", P=P, V=V, ms=med, GBps=nbytes / med / 1e6)
+            k.fused_set_schedule(2)
             del gran
 
         if os.environ.get("PROBE_FUSED_ONLY"):
