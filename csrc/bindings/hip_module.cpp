@@ -5,70 +5,22 @@
 // HIP runtime and works with any PyTorch-ROCm build. Launch functions never allocate, copy or
 // synchronise, so callers may capture them into HIP graphs.
 #include <hip/hip_runtime.h>
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
 #include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 
-#include "../kernels/sart_common.hpp"
+#include "../engine/comm.hpp"
+#include "../engine/engine.hpp"
+#include "../engine/geometry.hpp"
+#include "../kernels/launchers.hpp"
 
 namespace py = pybind11;
 
-namespace sart {
-// projection.hip
-int64_t forward_num_blocks(int64_t nrows_pad);
-void launch_forward(int epi, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* x,
-                    const float* ghat, const float* arow, float* out_f, float* out_w, double* Fpart,
-                    const SartState* st, hipStream_t stream);
-void launch_rowsum_f64(const float* A, int64_t ld, int64_t nrows, double* out, hipStream_t stream);
-int backproject_num_splits(int64_t ld, int64_t nrows);
-void launch_backproject(const float* A, int64_t ld, int64_t nrows, const float* w, int nsplit, float* partial,
-                        const SartState* st, hipStream_t stream);
-void launch_colsum_f64(const float* A, int64_t ld, int64_t nrows, int nsplit, double* partial, hipStream_t stream);
-void launch_reduce_partials(const float* partial, int64_t ld, int nsplit, const float* scale, float* out,
-                            const double* Fpart, int64_t nF, float* Fout, const SartState* st, hipStream_t stream);
-void launch_reduce_partials_f64(const double* partial, int64_t ld, int nsplit, double* out, hipStream_t stream);
-// sart_update.hip
-void launch_prep_rows(const double* g, int64_t nrows, int64_t nrows_pad, double inv_s, const float* ray_length,
-                      float len_thres, float* ghat, float* arow, float* gpos, float* wo, hipStream_t stream);
-void launch_init_solution(float* x, int64_t n, int64_t n_pad, const float* src_f32, const double* src_f64,
-                          double scale, hipStream_t stream);
-void launch_penalty(bool logx, const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta,
-                    const float* x, float* pen, const SartState* st, hipStream_t stream);
-void launch_decide(SartState* st, const float* Fslot, hipStream_t stream);
-void launch_update_linear(float* x, const float* d, const float* pen, int64_t n, const SartState* st,
-                          hipStream_t stream);
-void launch_update_log(float* x, const float* O, const float* Fv, const float* pen, float alpha, int64_t n,
-                       const SartState* st, hipStream_t stream);
-void launch_state_begin(SartState* st, double G, double tol, int max_iter, hipStream_t stream);
-// synth.hip
-void launch_synth_matrix(float* A, int64_t ld, int64_t nrows_pad, int64_t nrows, int64_t ncols, int64_t row_offset,
-                         uint64_t seed, float lo, float hi, hipStream_t stream);
-void launch_synth_vector(double* out, int64_t n, int64_t offset, uint64_t seed, double lo, double hi,
-                         hipStream_t stream);
-// fused_sweep.hip
-int fused_pick_k(int64_t ld);
-int fused_tile_rows(int K, int variant);
-void fused_set_schedule(int sched);
-int fused_get_schedule();
-void fused_set_trace(unsigned long long* buf, long long tiles);
-std::vector<int> fused_debug_map(int nblocks);
-int fused_fpart_per_block(int variant);
-void fused_set_debug(int flags);
-std::vector<unsigned long long> fused_debug_stats(int nblocks);
-void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
-                        const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
-                        uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream);
-// multiframe.hip
-int mf_forward_num_splits(int64_t ld, int64_t nrows_pad);
-int mf_backproject_num_splits(int64_t ld, int64_t nrows);
-void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ldx,
-                       float* Fout, int nsplit, hipStream_t stream);
-void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,
-                           hipStream_t stream);
-}  // namespace sart
 
 template <typename T>
 static T* P(uintptr_t p) {
@@ -76,8 +28,178 @@ static T* P(uintptr_t p) {
 }
 static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+using f64arr = py::array_t<double, py::array::c_style | py::array::forcecast>;
+
+static py::dict solve_info(const sart::SolveInfo& i) {
+    py::dict d;
+    d["status"] = i.status;
+    d["iterations"] = i.iterations;
+    d["convergence"] = i.convergence;
+    d["used_fused"] = i.used_fused;
+    d["fused_variant"] = i.fused_variant;
+    d["fallbacks"] = i.fallbacks;
+    d["ms"] = i.ms;
+    return d;
+}
+
+static void bind_engine(py::module_& m) {
+    py::enum_<sart::ReduceOp>(m, "ReduceOp").value("SUM", sart::ReduceOp::kSum).value("MAX", sart::ReduceOp::kMax);
+    py::class_<sart::Communicator, std::shared_ptr<sart::Communicator>>(m, "Comm")
+        .def_property_readonly("rank", &sart::Communicator::rank)
+        .def_property_readonly("size", &sart::Communicator::size)
+        .def_property_readonly("backend", &sart::Communicator::backend)
+        .def("barrier", &sart::Communicator::barrier, py::call_guard<py::gil_scoped_release>())
+        .def("abort", &sart::Communicator::abort)
+        .def("all_reduce_host",
+             [](sart::Communicator& c, f64arr v, sart::ReduceOp op) {
+                 py::array_t<double> out(v.size());
+                 std::memcpy(out.mutable_data(), v.data(), v.size() * sizeof(double));
+                 double* p = out.mutable_data();
+                 const size_t n = (size_t)v.size();
+                 {
+                     py::gil_scoped_release rel;
+                     c.all_reduce_host(p, n, op);
+                 }
+                 return out;
+             })
+        .def("broadcast_bytes",
+             [](sart::Communicator& c, py::bytes data, size_t nbytes, int root) {
+                 std::string buf(nbytes, '\0');
+                 if (c.rank() == root) {
+                     const std::string d = data;
+                     if (d.size() != nbytes) throw py::value_error("broadcast_bytes: root payload size mismatch");
+                     buf = d;
+                 }
+                 {
+                     py::gil_scoped_release rel;
+                     c.broadcast_host(buf.data(), nbytes, root);
+                 }
+                 return py::bytes(buf);
+             })
+        .def("all_reduce_device",
+             [](sart::Communicator& c, uintptr_t ptr, size_t n, bool f64, sart::ReduceOp op, uintptr_t stream) {
+                 py::gil_scoped_release rel;
+                 if (f64)
+                     c.all_reduce(P<double>(ptr), n, op, S(stream));
+                 else
+                     c.all_reduce(P<float>(ptr), n, op, S(stream));
+             });
+    m.def("local_comm", []() { return std::shared_ptr<sart::Communicator>(sart::make_local_comm()); });
+    m.def("tcp_comm",
+          [](int rank, int size, const std::string& host, int port, double timeout_s) {
+              py::gil_scoped_release rel;
+              return std::shared_ptr<sart::Communicator>(sart::make_tcp_comm(rank, size, host, port, timeout_s));
+          },
+          py::arg("rank"), py::arg("size"), py::arg("host"), py::arg("port"), py::arg("timeout_s") = 3600.0);
+    m.def("rccl_unique_id", []() { return py::bytes(sart::rccl_unique_id()); });
+    m.def("rccl_comm",
+          [](int device, py::bytes uid, int rank, int size, const std::string& host, int port) {
+              const std::string id = uid;
+              py::gil_scoped_release rel;
+              return std::shared_ptr<sart::Communicator>(
+                  sart::make_rccl_comm(device, id, sart::make_tcp_comm(rank, size, host, port)));
+          });
+    m.def("comm_from_env", [](bool gpu, int device) {
+        py::gil_scoped_release rel;
+        return std::shared_ptr<sart::Communicator>(sart::comm_from_env(gpu, device));
+    });
+
+    py::class_<sart::FusedGeometry>(m, "FusedGeometry")
+        .def_readonly("K", &sart::FusedGeometry::K)
+        .def_readonly("J", &sart::FusedGeometry::J)
+        .def_readonly("I", &sart::FusedGeometry::I)
+        .def_readonly("grid", &sart::FusedGeometry::grid)
+        .def_readonly("variant", &sart::FusedGeometry::variant)
+        .def_readonly("T", &sart::FusedGeometry::T)
+        .def("valid", &sart::FusedGeometry::valid);
+    m.def("fused_geometry", &sart::fused_geometry, py::arg("ld"), py::arg("num_cus"), py::arg("variant") = 6,
+          py::arg("rows_per_tile") = 0);
+    m.def("choose_ld", &sart::choose_ld, py::arg("nvoxel"), py::arg("max_waste") = 0.10);
+
+    py::class_<sart::EngineConfig>(m, "EngineConfig")
+        .def(py::init<>())
+        .def_readwrite("logarithmic", &sart::EngineConfig::logarithmic)
+        .def_readwrite("ray_density_threshold", &sart::EngineConfig::ray_density_threshold)
+        .def_readwrite("ray_length_threshold", &sart::EngineConfig::ray_length_threshold)
+        .def_readwrite("conv_tolerance", &sart::EngineConfig::conv_tolerance)
+        .def_readwrite("beta_laplace", &sart::EngineConfig::beta_laplace)
+        .def_readwrite("relaxation", &sart::EngineConfig::relaxation)
+        .def_readwrite("max_iterations", &sart::EngineConfig::max_iterations)
+        .def_readwrite("allow_zero_tolerance", &sart::EngineConfig::allow_zero_tolerance)
+        .def_readwrite("check_interval", &sart::EngineConfig::check_interval)
+        .def_readwrite("use_fused", &sart::EngineConfig::use_fused)
+        .def_readwrite("fused_variant", &sart::EngineConfig::fused_variant)
+        .def_readwrite("rows_per_tile", &sart::EngineConfig::rows_per_tile)
+        .def_readwrite("fused_schedule", &sart::EngineConfig::fused_schedule)
+        .def_readwrite("use_graph", &sart::EngineConfig::use_graph);
+    m.def("validate_config", [](const sart::EngineConfig& c) {
+        try {
+            sart::validate_config(c);
+        } catch (const std::invalid_argument& e) {
+            throw py::value_error(e.what());
+        }
+    });
+
+    py::class_<sart::Engine>(m, "Engine")
+        .def(py::init([](int device, uintptr_t A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
+                         std::shared_ptr<sart::Communicator> comm, const sart::EngineConfig& cfg) {
+                 try {
+                     return new sart::Engine(device, P<const float>(A), nrows, nrows_pad, nvoxel, ld, comm.get(), cfg);
+                 } catch (const std::invalid_argument& e) {
+                     throw py::value_error(e.what());
+                 }
+             }),
+             py::keep_alive<1, 8>())
+        .def("set_laplacian",
+             [](sart::Engine& e, py::array_t<int64_t, py::array::c_style | py::array::forcecast> rp,
+                py::array_t<int32_t, py::array::c_style | py::array::forcecast> col,
+                py::array_t<float, py::array::c_style | py::array::forcecast> val) {
+                 e.set_laplacian(rp.data(), col.data(), val.data(), (int64_t)val.size());
+             })
+        .def("solve",
+             [](sart::Engine& e, f64arr g, py::object x0) {
+                 if ((int64_t)g.size() != e.nrows())
+                     throw py::value_error("measurement has " + std::to_string(g.size()) +
+                                           " pixels, the local shard has " + std::to_string(e.nrows()));
+                 f64arr x0a;
+                 const double* x0p = nullptr;
+                 if (!x0.is_none()) {
+                     x0a = x0.cast<f64arr>();
+                     if ((int64_t)x0a.size() != e.nvoxel())
+                         throw py::value_error("Solution vector must be empty or contain nvoxel elements.");
+                     x0p = x0a.data();
+                 }
+                 py::array_t<double> x(e.nvoxel());
+                 double* xp = x.mutable_data();
+                 const double* gp = g.data();
+                 sart::SolveInfo info;
+                 {
+                     py::gil_scoped_release rel;
+                     info = e.solve(gp, x0p, xp);
+                 }
+                 return py::make_tuple(x, solve_info(info));
+             },
+             py::arg("g"), py::arg("x0") = py::none())
+        .def("forward",
+             [](sart::Engine& e, f64arr x) {
+                 if ((int64_t)x.size() != e.nvoxel()) throw py::value_error("x must have nvoxel elements");
+                 py::array_t<double> f(e.nrows());
+                 e.forward(x.data(), f.mutable_data());
+                 return f;
+             })
+        .def_property_readonly("use_fused", &sart::Engine::use_fused)
+        .def_property_readonly("geometry", &sart::Engine::geometry)
+        .def_property_readonly("num_cus", &sart::Engine::num_cus)
+        .def_property_readonly("nrows", &sart::Engine::nrows)
+        .def_property_readonly("nvoxel", &sart::Engine::nvoxel)
+        .def_property_readonly("stream", [](const sart::Engine& e) { return reinterpret_cast<uintptr_t>(e.stream()); })
+        .def("ray_density", [](const sart::Engine& e) { auto v = e.ray_density(); return py::array_t<double>(v.size(), v.data()); })
+        .def("ray_length", [](const sart::Engine& e) { auto v = e.ray_length(); return py::array_t<double>(v.size(), v.data()); })        ;
+}
+
 PYBIND11_MODULE(_sart_hip, m) {
-    m.doc() = "Hand-written gfx950 (CDNA4) HIP kernels of the SART solver";
+    m.doc() = "Hand-written gfx950 (CDNA4) HIP kernels of the SART solver and the native engine";
+    bind_engine(m);
 
     m.def("arch", []() { return std::string("gfx950"); });
     m.def("state_nbytes", []() { return (int)sizeof(sart::SartState); });

@@ -1,0 +1,366 @@
+#include "engine.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <stdexcept>
+
+#include "../kernels/launchers.hpp"
+
+namespace sart {
+
+namespace {
+
+constexpr int kEpiPlain = 0, kEpiLinear = 1, kEpiLog = 2;
+
+void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+template <typename T>
+void DeviceArray<T>::resize(size_t n) {
+    release();
+    if (n == 0) return;
+    hip_ok(hipMalloc(reinterpret_cast<void**>(&p_), n * sizeof(T)), "hipMalloc");
+    hip_ok(hipMemset(p_, 0, n * sizeof(T)), "hipMemset");
+    // hipMemset is ordered on the null stream only; the engine's stream is non-blocking, so wait here or
+    // the zero fill may land after the first kernel that writes the buffer
+    hip_ok(hipDeviceSynchronize(), "hipMemset sync");
+    n_ = n;
+}
+
+template <typename T>
+void DeviceArray<T>::release() {
+    if (p_) (void)hipFree(p_);
+    p_ = nullptr;
+    n_ = 0;
+}
+
+template class DeviceArray<float>;
+template class DeviceArray<double>;
+template class DeviceArray<SartState>;
+template class DeviceArray<uint64_t>;
+template class DeviceArray<unsigned>;
+template class DeviceArray<int64_t>;
+template class DeviceArray<int32_t>;
+
+void validate_config(const EngineConfig& c) {
+    if (c.ray_density_threshold < 0) throw std::invalid_argument("Ray density threshold must be non-negative.");
+    if (c.ray_length_threshold < 0) throw std::invalid_argument("Ray length threshold must be non-negative.");
+    if (c.conv_tolerance < 0 || (c.conv_tolerance == 0 && !c.allow_zero_tolerance))
+        throw std::invalid_argument("Convolution tolerance must be positive.");
+    if (c.beta_laplace < 0) throw std::invalid_argument("Attribute beta_laplace must be non-negative.");
+    if (!(c.relaxation > 0 && c.relaxation <= 1.0))
+        throw std::invalid_argument("Attribute relaxation must be within (0, 1] interval.");
+    if (c.max_iterations <= 0) throw std::invalid_argument("Attribute max_iterations must be positive.");
+}
+
+Engine::Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
+               Communicator* comm, const EngineConfig& cfg)
+    : device_(device), A_(A), P_(nrows), Pp_(nrows_pad), V_(nvoxel), ld_(ld), comm_(comm), cfg_(cfg) {
+    validate_config(cfg_);
+    if (!comm_) throw std::invalid_argument("Engine: communicator required");
+    if (ld_ % 64 || ld_ < V_ || Pp_ % 64 || Pp_ < P_)
+        throw std::invalid_argument("Engine: ld and nrows_pad must be multiples of 64 covering the shard");
+    cfg_.check_interval = std::max(1, cfg_.check_interval);
+    set_device();
+    hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");  // the shard may have been filled on another stream
+    hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+    for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hstate_), 2 * sizeof(SartState)), "hipHostMalloc");
+    hipDeviceProp_t prop;
+    hip_ok(hipGetDeviceProperties(&prop, device_), "hipGetDeviceProperties");
+    num_cus_ = prop.multiProcessorCount;
+    if (cfg_.fused_schedule >= 0) fused_set_schedule(cfg_.fused_schedule);
+
+    nsplit_ = backproject_num_splits(ld_, Pp_);
+    comm_buf_.resize(ld_ + 64);  // [0, ld) correction, [ld] ||A x||^2
+    x_.resize(ld_);
+    pen_.resize(ld_);
+    if (cfg_.logarithmic) O_.resize(ld_);
+    for (auto* b : {&ghat_, &arow_, &gpos_, &wo_, &w_, &fitted_, &ray_len_}) b->resize(Pp_);
+    for (auto* b : {&dinv_, &dscale_, &dmask_}) b->resize(ld_);
+    g64_.resize(Pp_);
+    x064_.resize(std::max<int64_t>(V_, 1));
+    st_.resize(1);
+    xcnt_.resize(16);
+    use_fused_ = false;
+    if (cfg_.use_fused) {
+        geom_ = fused_geometry(ld_, num_cus_, cfg_.fused_variant, cfg_.rows_per_tile);
+        use_fused_ = geom_.valid();
+    }
+    alloc_fused();
+    ray_sums();
+}
+
+Engine::~Engine() {
+    set_device();
+    drop_graph();
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto& e : ev_)
+        if (e) (void)hipEventDestroy(e);
+    if (hstate_) (void)hipHostFree(hstate_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void Engine::set_device() const { hip_ok(hipSetDevice(device_), "hipSetDevice"); }
+
+void Engine::drop_graph() {
+    if (graph_) (void)hipGraphExecDestroy(graph_);
+    graph_ = nullptr;
+    warm_ = false;
+}
+
+void Engine::alloc_fused() {
+    nF_fused_ = use_fused_ ? (int64_t)geom_.grid * fused_fpart_per_block(geom_.variant) : 0;
+    const int64_t n_part = std::max<int64_t>(nsplit_, use_fused_ ? geom_.I : 1);
+    if ((int64_t)partial_.size() < n_part * ld_) partial_.resize(n_part * ld_);
+    const int64_t nF = std::max<int64_t>({forward_num_blocks(Pp_), nF_fused_, 1});
+    if ((int64_t)Fpart_.size() < nF) Fpart_.resize(nF);
+    if (use_fused_ && (int64_t)gran_.size() < Pp_ * geom_.J) gran_.resize(Pp_ * geom_.J);
+}
+
+void Engine::ray_sums() {
+    // rho_v = sum_p A[p, v] (fp64, all-reduced), l_p = sum_v A[p, v] (fp64, local): on the device
+    // instead of the reference's host loops (sartsolver.cpp:38-56).
+    ell64_.resize(Pp_);
+    rho64_.resize(ld_);
+    launch_rowsum_f64(A_, ld_, P_, ell64_.get(), stream_);
+    {
+        DeviceArray<double> part((size_t)nsplit_ * ld_);
+        launch_colsum_f64(A_, ld_, P_, nsplit_, part.get(), stream_);
+        launch_reduce_partials_f64(part.get(), ld_, nsplit_, rho64_.get(), stream_);
+        hip_ok(hipStreamSynchronize(stream_), "ray sums");
+    }
+    comm_->all_reduce(rho64_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
+    launch_f64_to_f32(ell64_.get(), ray_len_.get(), Pp_, stream_);
+    launch_density_scales(rho64_.get(), V_, ld_, (float)cfg_.ray_density_threshold, (float)cfg_.relaxation,
+                          dinv_.get(), dscale_.get(), dmask_.get(), stream_);
+    hip_ok(hipStreamSynchronize(stream_), "ray sums");
+}
+
+std::vector<double> Engine::ray_density() const {
+    set_device();
+    std::vector<double> h(V_);
+    hip_ok(hipMemcpy(h.data(), rho64_.get(), V_ * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+    return h;
+}
+
+std::vector<double> Engine::ray_length() const {
+    set_device();
+    std::vector<double> h(P_);
+    if (P_) hip_ok(hipMemcpy(h.data(), ell64_.get(), P_ * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+    return h;
+}
+
+void Engine::set_laplacian(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t nnz) {
+    set_device();
+    drop_graph();
+    has_lap_ = false;
+    if (nnz <= 0 || cfg_.beta_laplace <= 0) return;
+    if (row_ptr[V_] != nnz) throw std::invalid_argument("Laplacian CSR row pointer does not match nnz");
+    lap_rp_.resize(V_ + 1);
+    lap_col_.resize(nnz);
+    lap_val_.resize(nnz);
+    hip_ok(hipMemcpy(lap_rp_.get(), row_ptr, (V_ + 1) * sizeof(int64_t), hipMemcpyHostToDevice), "H2D");
+    hip_ok(hipMemcpy(lap_col_.get(), col, nnz * sizeof(int32_t), hipMemcpyHostToDevice), "H2D");
+    hip_ok(hipMemcpy(lap_val_.get(), val, nnz * sizeof(float), hipMemcpyHostToDevice), "H2D");
+    has_lap_ = true;
+}
+
+double Engine::setup_frame(const double* g, const double* x0) {
+    // normalisation by the global maximum and sum_{g > 0} g^2 (reference sartsolver_cuda.cpp:146-157);
+    // the reference divides by zero when every pixel is <= 0, we keep norm = 1 then.
+    double mx = -std::numeric_limits<double>::infinity(), gs = 0.0;
+    for (int64_t i = 0; i < P_; ++i) {
+        mx = std::max(mx, g[i]);
+        if (g[i] > 0) gs += g[i] * g[i];
+    }
+    double norm = comm_->all_reduce_scalar(mx, ReduceOp::kMax);
+    if (!(norm > 0)) norm = 1.0;
+    double G = comm_->all_reduce_scalar(gs, ReduceOp::kSum) / (norm * norm);
+    if (!(G > 0)) G = 1.0;
+    if (P_) hip_ok(hipMemcpyAsync(g64_.get(), g, P_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D g");
+    launch_prep_rows(g64_.get(), P_, Pp_, 1.0 / norm, ray_len_.get(), (float)cfg_.ray_length_threshold, ghat_.get(),
+                     arow_.get(), gpos_.get(), wo_.get(), stream_);
+    if (!x0) {
+        // cold start x0 = [rho > tau] A^T max(ghat, 0) / rho (reference sart_kernels.cu:22-60)
+        launch_backproject(A_, ld_, P_, gpos_.get(), nsplit_, partial_.get(), nullptr, stream_);
+        launch_reduce_partials(partial_.get(), ld_, nsplit_, dinv_.get(), comm_buf_.get(), nullptr, 0, nullptr,
+                               nullptr, stream_);
+        comm_->all_reduce(comm_buf_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
+        launch_init_solution(x_.get(), V_, ld_, comm_buf_.get(), nullptr, 1.0, stream_);
+    } else {
+        hip_ok(hipMemcpyAsync(x064_.get(), x0, V_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D x0");
+        launch_init_solution(x_.get(), V_, ld_, nullptr, x064_.get(), 1.0 / norm, stream_);
+    }
+    if (cfg_.logarithmic) {
+        // frame-constant observed back-projection O = [rho > tau] A^T (a ghat), reduced once per frame
+        launch_backproject(A_, ld_, P_, wo_.get(), nsplit_, partial_.get(), nullptr, stream_);
+        launch_reduce_partials(partial_.get(), ld_, nsplit_, dmask_.get(), O_.get(), nullptr, 0, nullptr, nullptr,
+                               stream_);
+        comm_->all_reduce(O_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
+    }
+    launch_state_begin(st_.get(), G, cfg_.conv_tolerance, cfg_.max_iterations, stream_);
+    return norm;
+}
+
+void Engine::sweep() {
+    SartState* st = st_.get();
+    const float* scale = cfg_.logarithmic ? dmask_.get() : dscale_.get();
+    float* Fslot = comm_buf_.get() + ld_;
+    if (use_fused_) {
+        if (geom_.variant == 6) hip_ok(hipMemsetAsync(xcnt_.get(), 0, 16 * sizeof(unsigned), stream_), "memset");
+        launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, A_, ld_, P_, Pp_, x_.get(), ghat_.get(),
+                           arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I, geom_.J, st, xcnt_.get(),
+                           stream_);
+        launch_reduce_partials(partial_.get(), ld_, geom_.I, scale, comm_buf_.get(), Fpart_.get(), nF_fused_, Fslot,
+                               st, stream_);
+    } else {
+        launch_forward(cfg_.logarithmic ? kEpiLog : kEpiLinear, A_, ld_, P_, Pp_, x_.get(), ghat_.get(), arow_.get(),
+                       nullptr, w_.get(), Fpart_.get(), st, stream_);
+        launch_backproject(A_, ld_, P_, w_.get(), nsplit_, partial_.get(), st, stream_);
+        launch_reduce_partials(partial_.get(), ld_, nsplit_, scale, comm_buf_.get(), Fpart_.get(),
+                               forward_num_blocks(Pp_), Fslot, st, stream_);
+    }
+    const float* pen = nullptr;
+    if (has_lap_) {
+        launch_penalty(cfg_.logarithmic, lap_rp_.get(), lap_col_.get(), lap_val_.get(), V_, (float)cfg_.beta_laplace,
+                       x_.get(), pen_.get(), st, stream_);
+        pen = pen_.get();
+    }
+    if (comm_->size() > 1) comm_->all_reduce(comm_buf_.get(), (size_t)ld_ + 1, ReduceOp::kSum, stream_);
+    launch_decide(st, Fslot, stream_);
+    if (cfg_.logarithmic)
+        launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_);
+    else
+        launch_update_linear(x_.get(), comm_buf_.get(), pen, V_, st, stream_);
+}
+
+void Engine::run_chunk(int n) {
+    // Capture only after an eager chunk with the current kernels: launchers configure function attributes
+    // (dynamic LDS above 64 KiB) on first use, which must not happen inside a capture.
+    const bool graphable = cfg_.use_graph && !graph_failed_ && warm_ && comm_->graph_capturable() &&
+                           n == cfg_.check_interval;
+    if (graphable && !graph_) {
+        hipGraph_t g = nullptr;
+        bool ok = hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal) == hipSuccess;
+        if (ok) {
+            try {
+                for (int i = 0; i < n; ++i) sweep();
+            } catch (...) {
+                ok = false;
+            }
+            ok = (hipStreamEndCapture(stream_, &g) == hipSuccess) && ok && g;
+        }
+        if (ok) ok = hipGraphInstantiate(&graph_, g, nullptr, nullptr, 0) == hipSuccess;
+        if (g) (void)hipGraphDestroy(g);
+        if (!ok) {
+            (void)hipGetLastError();
+            graph_ = nullptr;
+            graph_failed_ = true;
+        }
+    }
+    if (graphable && graph_) {
+        hip_ok(hipGraphLaunch(graph_, stream_), "hipGraphLaunch");
+    } else {
+        for (int i = 0; i < n; ++i) sweep();
+        warm_ = true;
+    }
+}
+
+bool Engine::fallback() {
+    // A persistent sweep gave up waiting (SartState.error): XCD-local groups (variant 6) -> generic
+    // groups (variant 3) -> two-pass kernels. The frame is re-solved from scratch.
+    drop_graph();
+    if (use_fused_ && geom_.variant == 6) {
+        const FusedGeometry g3 = fused_geometry(ld_, num_cus_, 3, 0);
+        if (g3.valid()) {
+            std::fprintf(stderr, "sart: fused sweep variant 6 timed out (unexpected workgroup placement); using variant 3\n");
+            geom_ = g3;
+            alloc_fused();
+            return true;
+        }
+    }
+    if (use_fused_) {
+        std::fprintf(stderr, "sart: fused sweep protocol timeout; switching to the two-pass kernels\n");
+        use_fused_ = false;
+        return true;
+    }
+    return false;
+}
+
+SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
+    set_device();
+    const auto t0 = std::chrono::steady_clock::now();
+    SolveInfo info;
+    const int max_sweeps = cfg_.max_iterations + 1;
+    while (true) {
+        norm_ = setup_frame(g, x0);
+        int enqueued = 0, issued = 0, checked = 0;
+        bool error = false;
+        auto issue = [&]() {
+            const int n = std::min(cfg_.check_interval, max_sweeps - enqueued);
+            run_chunk(n);
+            enqueued += n;
+            const int slot = issued & 1;
+            hip_ok(hipMemcpyAsync(hstate_ + slot, st_.get(), sizeof(SartState), hipMemcpyDeviceToHost, stream_),
+                   "D2H state");
+            hip_ok(hipEventRecord(ev_[slot], stream_), "event");
+            ++issued;
+        };
+        issue();
+        while (true) {
+            if (enqueued < max_sweeps) issue();  // keep the GPU busy while the previous chunk is checked
+            const int slot = checked & 1;
+            hip_ok(hipEventSynchronize(ev_[slot]), "event sync");
+            const SartState s = hstate_[slot];
+            ++checked;
+            if (s.error) {
+                error = true;
+                break;
+            }
+            if (s.done || (checked == issued && enqueued >= max_sweeps)) break;
+        }
+        hip_ok(hipStreamSynchronize(stream_), "solve");
+        if (error) {
+            ++info.fallbacks;
+            if (!fallback()) throw std::runtime_error("SART engine: persistent sweep failed without fallback");
+            continue;
+        }
+        break;
+    }
+    SartState s;
+    hip_ok(hipMemcpy(&s, st_.get(), sizeof(SartState), hipMemcpyDeviceToHost), "D2H state");
+    std::vector<float> xh(V_);
+    if (V_) hip_ok(hipMemcpy(xh.data(), x_.get(), V_ * sizeof(float), hipMemcpyDeviceToHost), "D2H x");
+    for (int64_t i = 0; i < V_; ++i) x_out[i] = (double)xh[i] * norm_;  // reference sartsolver_cuda.cpp:264-265
+    info.status = s.status == kSuccess ? kSuccess : kMaxIterationsExceeded;
+    info.iterations = s.iterations;
+    info.convergence = s.conv_last;
+    info.used_fused = use_fused_;
+    info.fused_variant = use_fused_ ? geom_.variant : -1;
+    info.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return info;
+}
+
+void Engine::forward(const double* x, double* f) {
+    set_device();
+    std::vector<float> xf(ld_, 0.f);
+    for (int64_t i = 0; i < V_; ++i) xf[i] = (float)x[i];
+    DeviceArray<float> xd(ld_);
+    hip_ok(hipMemcpyAsync(xd.get(), xf.data(), ld_ * sizeof(float), hipMemcpyHostToDevice, stream_), "H2D");
+    launch_forward(kEpiPlain, A_, ld_, P_, Pp_, xd.get(), nullptr, nullptr, fitted_.get(), nullptr, nullptr, nullptr,
+                   stream_);
+    std::vector<float> fh(P_);
+    if (P_) hip_ok(hipMemcpyAsync(fh.data(), fitted_.get(), P_ * sizeof(float), hipMemcpyDeviceToHost, stream_), "D2H");
+    hip_ok(hipStreamSynchronize(stream_), "forward");
+    for (int64_t i = 0; i < P_; ++i) f[i] = fh[i];
+}
+
+}  // namespace sart

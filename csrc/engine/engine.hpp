@@ -1,0 +1,145 @@
+// Native per-GPU SART engine: owns the device workspaces of one rank's solver and
+// runs whole frame solves in C++ -- ray sums, frame setup, the sweep loop (fused single-pass sweep with
+// the v6 -> v3 -> two-pass fallback chain, or the two-pass kernels), the per-iteration all-reduce and the
+// device-side convergence decision -- without Python in the loop.
+//
+// Reference parity: BaseSARTSolverMPICuda / SARTSolverMPICuda / LogSARTSolverMPICuda
+// (reference sartsolver_cuda.cpp:78-354, ray sums sartsolver.cpp:20-58, parameter checks :61-123);
+// iteration semantics in mpi_cuda_sartsolver_amd/models/sart.py.
+//
+// MI355X specifics: every buffer is allocated once per engine (the reference mallocs 5 buffers per
+// frame, sartsolver_cuda.cpp:160-191); the host reads the 128-byte SartState once per chunk of
+// `check_interval` sweeps, with the next chunk already queued, so the GPU never drains between chunks;
+// a chunk is captured once into a HIP graph and replayed (local and RCCL communicators).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../kernels/sart_common.hpp"
+#include "comm.hpp"
+#include "geometry.hpp"
+
+namespace sart {
+
+struct EngineConfig {
+    bool logarithmic = false;
+    double ray_density_threshold = 1e-6;
+    double ray_length_threshold = 1e-6;
+    double conv_tolerance = 1e-5;
+    double beta_laplace = 1e-2;
+    double relaxation = 1.0;
+    int max_iterations = 2000;
+    bool allow_zero_tolerance = false;  // benchmarks: run exactly max_iterations
+    int check_interval = 16;
+    bool use_fused = true;
+    int fused_variant = 6;
+    int rows_per_tile = 0;   // 0: default (fused_geometry)
+    int fused_schedule = -1; // -1: keep the launcher's default
+    bool use_graph = false;  // opt-in (SART_GRAPH=1): chunk capture is under validation
+};
+
+// Same checks and messages as the reference setters (sartsolver.cpp:61-123); throws std::invalid_argument.
+void validate_config(const EngineConfig& c);
+
+struct SolveInfo {
+    int status = -1;          // 0 SUCCESS, -1 MAX_ITERATIONS_EXCEEDED
+    int iterations = 0;
+    double convergence = 0.0; // last (G - ||A x||^2) / G
+    bool used_fused = false;
+    int fused_variant = -1;
+    int fallbacks = 0;        // protocol timeouts survived during this solve
+    double ms = 0.0;
+};
+
+template <typename T>
+class DeviceArray {
+   public:
+    DeviceArray() = default;
+    explicit DeviceArray(size_t n) { resize(n); }
+    ~DeviceArray() { release(); }
+    DeviceArray(const DeviceArray&) = delete;
+    DeviceArray& operator=(const DeviceArray&) = delete;
+    void resize(size_t n);  // zero-filled
+    void release();
+    T* get() const { return p_; }
+    size_t size() const { return n_; }
+
+   private:
+    T* p_ = nullptr;
+    size_t n_ = 0;
+};
+
+class Engine {
+   public:
+    // A: device pointer to the row-major fp32 shard [nrows_pad x ld], zero padded (not owned).
+    Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
+           Communicator* comm, const EngineConfig& cfg);
+    ~Engine();
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+
+    // CSR Laplacian over nvoxel rows (host arrays, copied). Ignored when beta_laplace == 0 or nnz == 0.
+    void set_laplacian(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t nnz);
+    // One frame: g = this rank's pixels (host fp64, nrows), x0 = warm start (host fp64, nvoxel) or null,
+    // x_out = solution (host fp64, nvoxel, de-normalised).
+    SolveInfo solve(const double* g, const double* x0, double* x_out);
+    // f = A x for this shard (host fp64 in/out).
+    void forward(const double* x, double* f);
+
+    bool use_fused() const { return use_fused_; }
+    const FusedGeometry& geometry() const { return geom_; }
+    const EngineConfig& config() const { return cfg_; }
+    hipStream_t stream() const { return stream_; }
+    int num_cus() const { return num_cus_; }
+    int64_t nrows() const { return P_; }
+    int64_t nvoxel() const { return V_; }
+    std::vector<double> ray_density() const;  // global, fp64 (nvoxel)
+    std::vector<double> ray_length() const;   // local, fp64 (nrows)
+    double last_norm() const { return norm_; }
+
+   private:
+    void ray_sums();
+    void alloc_fused();
+    double setup_frame(const double* g, const double* x0);
+    void sweep();
+    void run_chunk(int n);
+    bool fallback();  // false when nothing is left to fall back to
+    void drop_graph();
+    void set_device() const;
+
+    int device_;
+    const float* A_;
+    int64_t P_, Pp_, V_, ld_;
+    Communicator* comm_;
+    EngineConfig cfg_;
+    hipStream_t stream_ = nullptr;
+    int num_cus_ = 0;
+    bool use_fused_ = false;
+    FusedGeometry geom_;
+    int nsplit_ = 0;
+    int64_t nF_fused_ = 0;
+    double norm_ = 1.0;
+
+    DeviceArray<float> partial_, comm_buf_, x_, pen_, O_, ghat_, arow_, gpos_, wo_, w_, fitted_, ray_len_, dinv_,
+        dscale_, dmask_;
+    DeviceArray<double> Fpart_, g64_, x064_, rho64_, ell64_;
+    DeviceArray<SartState> st_;
+    DeviceArray<uint64_t> gran_;
+    DeviceArray<unsigned> xcnt_;
+    DeviceArray<int64_t> lap_rp_;
+    DeviceArray<int32_t> lap_col_;
+    DeviceArray<float> lap_val_;
+    bool has_lap_ = false;
+
+    SartState* hstate_ = nullptr;  // pinned [2]
+    hipEvent_t ev_[2] = {nullptr, nullptr};
+    hipGraphExec_t graph_ = nullptr;
+    bool graph_failed_ = false;
+    bool warm_ = false;  // an eager chunk ran with the current kernels
+};
+
+}  // namespace sart

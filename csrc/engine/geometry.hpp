@@ -1,0 +1,27 @@
+// Shard layout and persistent-grid geometry of the fused sweep (single source of truth for the C++
+// engine, the driver and the Python package).
+#pragma once
+
+#include <cstdint>
+
+namespace sart {
+
+struct FusedGeometry {
+    int K = 0;        // variants 0-3: float4 per lane per row slab / 256; variants 4, 6: rows per tile
+    int J = 0;        // workgroups per row (column slabs)
+    int I = 0;        // row groups
+    int grid = 0;     // I * J persistent workgroups
+    int variant = -1; // -1: no fused path for this width
+    int T = 0;        // rows per tile
+    bool valid() const { return variant >= 0; }
+};
+
+// Padded row length of a dense shard: a width the fused sweep can split into slabs when that wastes at
+// most max_waste of the row, else the next multiple of 64 floats (256 B rows).
+int64_t choose_ld(int64_t nvoxel, double max_waste = 0.10);
+
+// Geometry for `variant` (6 default; 4/5/3/0-2 supported), falling back to variant 3 when the width
+// does not fit. rows_per_tile = 0: SART_FUSED_T or the measured default (4).
+FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_tile);
+
+}  // namespace sart

@@ -1,0 +1,67 @@
+// Host launchers of the gfx950 SART kernels (csrc/kernels/*.hip). Launchers never allocate, copy or
+// synchronise, so they may be captured into HIP graphs; every one checks hipGetLastError.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "sart_common.hpp"
+
+namespace sart {
+// projection.hip
+int64_t forward_num_blocks(int64_t nrows_pad);
+void launch_forward(int epi, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* x,
+                    const float* ghat, const float* arow, float* out_f, float* out_w, double* Fpart,
+                    const SartState* st, hipStream_t stream);
+void launch_rowsum_f64(const float* A, int64_t ld, int64_t nrows, double* out, hipStream_t stream);
+int backproject_num_splits(int64_t ld, int64_t nrows);
+void launch_backproject(const float* A, int64_t ld, int64_t nrows, const float* w, int nsplit, float* partial,
+                        const SartState* st, hipStream_t stream);
+void launch_colsum_f64(const float* A, int64_t ld, int64_t nrows, int nsplit, double* partial, hipStream_t stream);
+void launch_reduce_partials(const float* partial, int64_t ld, int nsplit, const float* scale, float* out,
+                            const double* Fpart, int64_t nF, float* Fout, const SartState* st, hipStream_t stream);
+void launch_reduce_partials_f64(const double* partial, int64_t ld, int nsplit, double* out, hipStream_t stream);
+// sart_update.hip
+void launch_prep_rows(const double* g, int64_t nrows, int64_t nrows_pad, double inv_s, const float* ray_length,
+                      float len_thres, float* ghat, float* arow, float* gpos, float* wo, hipStream_t stream);
+void launch_init_solution(float* x, int64_t n, int64_t n_pad, const float* src_f32, const double* src_f64,
+                          double scale, hipStream_t stream);
+void launch_penalty(bool logx, const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta,
+                    const float* x, float* pen, const SartState* st, hipStream_t stream);
+void launch_decide(SartState* st, const float* Fslot, hipStream_t stream);
+void launch_update_linear(float* x, const float* d, const float* pen, int64_t n, const SartState* st,
+                          hipStream_t stream);
+void launch_update_log(float* x, const float* O, const float* Fv, const float* pen, float alpha, int64_t n,
+                       const SartState* st, hipStream_t stream);
+void launch_state_begin(SartState* st, double G, double tol, int max_iter, hipStream_t stream);
+void launch_density_scales(const double* rho, int64_t n, int64_t n_pad, float thres, float alpha, float* dinv,
+                           float* dscale, float* dmask, hipStream_t stream);
+void launch_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t stream);
+// synth.hip
+void launch_synth_matrix(float* A, int64_t ld, int64_t nrows_pad, int64_t nrows, int64_t ncols, int64_t row_offset,
+                         uint64_t seed, float lo, float hi, hipStream_t stream);
+void launch_synth_vector(double* out, int64_t n, int64_t offset, uint64_t seed, double lo, double hi,
+                         hipStream_t stream);
+// fused_sweep.hip
+int fused_pick_k(int64_t ld);
+int fused_tile_rows(int K, int variant);
+void fused_set_schedule(int sched);
+int fused_get_schedule();
+void fused_set_trace(unsigned long long* buf, long long tiles);
+std::vector<int> fused_debug_map(int nblocks);
+int fused_fpart_per_block(int variant);
+void fused_set_debug(int flags);
+std::vector<unsigned long long> fused_debug_stats(int nblocks);
+void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
+                        const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
+                        uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream);
+// multiframe.hip
+int mf_forward_num_splits(int64_t ld, int64_t nrows_pad);
+int mf_backproject_num_splits(int64_t ld, int64_t nrows);
+void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ldx,
+                       float* Fout, int nsplit, hipStream_t stream);
+void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,
+                           hipStream_t stream);
+}  // namespace sart

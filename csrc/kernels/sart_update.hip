@@ -146,7 +146,40 @@ __global__ void k_state_begin(SartState* __restrict__ st, double G, double tol, 
     if (st->epoch <= 0) st->epoch = 1;
 }
 
+// Per-voxel scales from the global fp64 ray density, with the reference's fp32 semantics: the density is
+// converted to fp32 first and compared with the fp32 threshold (reference sartsolver_cuda.cpp:118-124,
+// sart_kernels.cu:82,86): dinv = [rho > t] / rho (cold start), dscale = [rho > t] alpha / rho (linear
+// correction), dmask = [rho > t] (log back-projections). Padding voxels get zeros.
+__global__ void k_density_scales(const double* __restrict__ rho, int64_t n, int64_t n_pad, float thres, float alpha,
+                                 float* __restrict__ dinv, float* __restrict__ dscale, float* __restrict__ dmask) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pad) return;
+    const float r = i < n ? (float)rho[i] : 0.f;
+    const bool valid = i < n && r > thres;
+    dinv[i] = valid ? 1.0f / r : 0.f;
+    dscale[i] = valid ? alpha / r : 0.f;
+    dmask[i] = valid ? 1.f : 0.f;
+}
+
+__global__ void k_f64_to_f32(const double* __restrict__ src, float* __restrict__ dst, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = (float)src[i];
+}
+
 static inline unsigned nb(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+void launch_density_scales(const double* rho, int64_t n, int64_t n_pad, float thres, float alpha, float* dinv,
+                           float* dscale, float* dmask, hipStream_t stream) {
+    hipLaunchKernelGGL(k_density_scales, dim3(nb(n_pad)), dim3(256), 0, stream, rho, n, n_pad, thres, alpha, dinv,
+                       dscale, dmask);
+    check_launch("k_density_scales");
+}
+
+void launch_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t stream) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_f64_to_f32, dim3(nb(n)), dim3(256), 0, stream, src, dst, n);
+    check_launch("k_f64_to_f32");
+}
 
 void launch_prep_rows(const double* g, int64_t nrows, int64_t nrows_pad, double inv_s, const float* ray_length,
                       float len_thres, float* ghat, float* arow, float* gpos, float* wo, hipStream_t stream) {

@@ -26,6 +26,7 @@ ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "csrc"
 LIBDIR = Path(__file__).resolve().parent / "_lib"
 BUILDDIR = ROOT / "build"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("SART_OFFLOAD_ARCH", "gfx950")
 
 HDF5_PREFIX = Path(os.environ.get("SART_HDF5_PREFIX", "/opt/conda"))
@@ -100,7 +101,7 @@ def build_hip(verbose: bool = True) -> Path:
     objdir = BUILDDIR / "hip"
     objdir.mkdir(parents=True, exist_ok=True)
     LIBDIR.mkdir(parents=True, exist_ok=True)
-    headers = sorted((CSRC / "kernels").glob("*.hpp"))
+    headers = sorted((CSRC / "kernels").glob("*.hpp")) + sorted((CSRC / "engine").glob("*.hpp"))
     common = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
     jobs = []
     objs = []
@@ -109,6 +110,12 @@ def build_hip(verbose: bool = True) -> Path:
         obj = objdir / (src.stem + ".o")
         jobs.append(([hipcc, *flags, "-c", str(src), "-o", str(obj)], obj, _digest([src, *headers], flags)))
         objs.append(obj)
+    # native engine (host C++ on the HIP runtime + RCCL): csrc/engine
+    eflags = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}"]
+    for src in sorted((CSRC / "engine").glob("*.cpp")):
+        obj = objdir / ("engine_" + src.stem + ".o")
+        jobs.append(([hipcc, *eflags, "-c", str(src), "-o", str(obj)], obj, _digest([src, *headers], eflags)))
+        objs.append(obj)
     bind = CSRC / "bindings" / "hip_module.cpp"
     bflags = ["-O2", "-std=c++17", "-fPIC", *[f"-I{p}" for p in _py_includes()], "-D__HIP_PLATFORM_AMD__"]
     bobj = objdir / "hip_module.o"
@@ -116,7 +123,8 @@ def build_hip(verbose: bool = True) -> Path:
     objs.append(bobj)
     _compile_many(jobs, verbose)
     out = LIBDIR / ("_sart_hip" + _ext_suffix())
-    _link([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(out)], out, objs, verbose)
+    _link([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), f"-L{ROCM / 'lib'}", "-lrccl",
+           "-o", str(out)], out, objs, verbose)
     return out
 
 

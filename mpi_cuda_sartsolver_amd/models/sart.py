@@ -1,7 +1,9 @@
 """GPU SART solvers (linear and logarithmic, optional Laplacian regulariser) on MI355X.
 
 Functional parity with the reference GPU solvers ``SARTSolverMPICuda`` / ``LogSARTSolverMPICuda``
-(reference sartsolver_cuda.cpp:197-354, math in manual.pdf p.2 eqs. 1-6), re-designed for gfx950:
+(reference sartsolver_cuda.cpp:197-354, math in manual.pdf p.2 eqs. 1-6), re-designed for gfx950.
+The solver runs in the native C++ engine (csrc/engine/engine.cpp, class ``sart::Engine``); this module
+is its Python face (parameters, communicator hand-over, results):
 
 * ray density / ray length: device fp64 column/row sums (reference: CPU loops, sartsolver.cpp:38-56);
 * per iteration ONE fused sweep over the local RTM shard (forward projection + SART weight +
@@ -34,10 +36,10 @@ import numpy as np
 import torch
 
 from ..ops import hip
-from ..ops.state import MAX_ITERATIONS_EXCEEDED, SUCCESS, new_state, read_state
-from ..parallel.comm import Communicator, SingleProcessComm
+from ..ops.state import MAX_ITERATIONS_EXCEEDED, SUCCESS
+from ..parallel.comm import Communicator, SingleProcessComm, native_communicator
 from .laplacian import LaplacianCSR
-from .rtm import DenseRTM, fused_geometry
+from .rtm import DenseRTM
 
 log = logging.getLogger(__name__)
 
@@ -81,14 +83,24 @@ class SolveResult:
     elapsed_ms: float = 0.0
 
 
+def _host_f64(v) -> np.ndarray:
+    if isinstance(v, torch.Tensor):
+        v = v.detach().to("cpu", torch.float64).numpy()
+    return np.ascontiguousarray(np.asarray(v, dtype=np.float64).ravel())
+
+
 class SARTSolver:
-    """Per-GPU SART engine over a device-resident row shard. One instance per rank."""
+    """Per-GPU SART solver over a device-resident row shard (one instance per rank).
+
+    Thin wrapper of ``sart::Engine``: all device work, the per-iteration all-reduce (RCCL for the
+    ``nccl`` process group, host TCP otherwise) and the convergence loop run in C++.
+    """
 
     def __init__(self, rtm: DenseRTM, laplacian: Optional[LaplacianCSR] = None,
                  comm: Optional[Communicator] = None, params: Optional[SolverParams] = None,
                  logarithmic: bool = False, use_fused: bool = True, check_interval: int = 16,
                  allow_zero_tolerance: bool = False, fused_variant: Optional[int] = None,
-                 fused_rows_per_tile: Optional[int] = None):
+                 fused_rows_per_tile: Optional[int] = None, use_graph: Optional[bool] = None):
         self.k = hip()
         self.rtm = rtm
         self.dev = rtm.device
@@ -96,213 +108,68 @@ class SARTSolver:
         self.params = params or SolverParams()
         self.params.validate(allow_zero_tolerance)
         self.log = bool(logarithmic)
-        self.check_interval = max(1, int(check_interval))
         self.L = laplacian if (laplacian is not None and laplacian.nnz > 0 and self.params.beta_laplace > 0) else None
         if self.L is not None and self.L.n != rtm.nvoxel:
             raise ValueError("Laplacian and ray-transfer matrices have different number of voxels.")
-
-        P, Pp, V, ld = rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld
-        self.P, self.Pp, self.V, self.ld = P, Pp, V, ld
-        f32 = dict(dtype=torch.float32, device=self.dev)
-        z = lambda n, **kw: torch.zeros(n, **(kw or f32))  # noqa: E731
-
-        props = self.k.device_info(self.dev.index if self.dev.index is not None else 0)
-        self.num_cus = int(props["multiProcessorCount"])
         if fused_variant is None:
             fused_variant = int(os.environ.get("SART_FUSED_VARIANT", "6"))
-        if os.environ.get("SART_FUSED_SCHEDULE"):  # variant 6 pipeline schedule (fused_sweep.hip, SCHED)
-            self.k.fused_set_schedule(int(os.environ["SART_FUSED_SCHEDULE"]))
-        self.geom = fused_geometry(ld, self.num_cus, fused_variant, fused_rows_per_tile) if use_fused else None
-        self.use_fused = self.geom is not None
-
-        self.nsplit = self.k.backproject_num_splits(ld, Pp)
-        n_part = max(self.nsplit, self.geom.I if self.geom else 1)
-        self.partial = z(n_part * ld)
-        self.nF_fused = self.geom.grid * self.k.fused_fpart_per_block(self.geom.variant) if self.geom else 0
-        nF = max(self.k.forward_num_blocks(Pp), self.nF_fused, 1)
-        self.Fpart = z(nF, dtype=torch.float64, device=self.dev)
-        self.comm_buf = z(ld + 64)  # [0:ld] correction, [ld] ||A x||^2 (fp32, as the reference)
-        self.x = z(ld)
-        self.pen = z(ld)
-        self.O = z(ld) if self.log else None
-        self.ghat, self.arow, self.gpos, self.wo, self.w = (z(Pp) for _ in range(5))
-        self.fitted = z(Pp)
-        self.g64 = z(Pp, dtype=torch.float64, device=self.dev)
-        self.state = new_state(self.dev)
-        if self.use_fused:
-            self.gran = torch.zeros(Pp * self.geom.J, dtype=torch.int64, device=self.dev)
-            self.xcnt = torch.zeros(16, dtype=torch.int32, device=self.dev)  # per-XCD tickets (variant 6)
-        self._stream = lambda: torch.cuda.current_stream(self.dev).cuda_stream  # noqa: E731
-
-        self._ray_sums()
-
-    # ------------------------------------------------------------------------------------------
-    def _ray_sums(self) -> None:
-        """rho_v = sum_p A (global, fp64, all-reduced) and l_p = sum_v A (local, fp64)."""
-        k, s, rtm = self.k, self._stream(), self.rtm
-        ell = torch.zeros(self.Pp, dtype=torch.float64, device=self.dev)
-        k.rowsum_f64(rtm.A.data_ptr(), self.ld, self.P, ell.data_ptr(), s)
-        nsplit = k.backproject_num_splits(self.ld, self.Pp)
-        part = torch.zeros(nsplit * self.ld, dtype=torch.float64, device=self.dev)
-        k.colsum_f64(rtm.A.data_ptr(), self.ld, self.P, nsplit, part.data_ptr(), s)
-        rho = torch.zeros(self.ld, dtype=torch.float64, device=self.dev)
-        k.reduce_partials_f64(part.data_ptr(), self.ld, nsplit, rho.data_ptr(), s)
-        del part
-        self.comm.all_reduce_(rho)
-        self.ray_length64 = ell
-        self.ray_density64 = rho
         p = self.params
-        # fp64 -> fp32 conversion then fp32 threshold comparisons, as the reference does
-        # (sartsolver_cuda.cpp:118-124, sart_kernels.cu:82,86).
-        self.ray_length = ell.to(torch.float32)
-        rho32 = rho.to(torch.float32)
-        valid = rho32 > np.float32(p.ray_density_threshold)
-        one = torch.ones_like(rho32)
-        safe = torch.where(valid, rho32, one)
-        self.dinv = torch.where(valid, one / safe, torch.zeros_like(rho32))
-        alpha = np.float32(p.relaxation)
-        self.dscale = torch.where(valid, torch.tensor(alpha, device=self.dev) / safe, torch.zeros_like(rho32))
-        self.dmask = valid.to(torch.float32)
-
-    # ------------------------------------------------------------------------------------------
-    def _setup_frame(self, measurement, solution) -> float:
-        k, s, p = self.k, self._stream(), self.params
-        g = torch.as_tensor(measurement, dtype=torch.float64)
-        if g.numel() != self.P:
-            raise ValueError(f"measurement has {g.numel()} pixels, the local shard has {self.P}")
-        self.g64[: self.P].copy_(g.to(self.dev, non_blocking=False))
-        gl = self.g64[: self.P]
-        # Normalisation by the global maximum (reference sartsolver_cuda.cpp:146-157). The reference
-        # divides by zero when every pixel is <= 0; we keep norm = 1 in that case.
-        norm = self.comm.all_reduce_scalar(float(gl.max().item()) if self.P else -math.inf, op="max")
-        if not norm > 0:
-            norm = 1.0
-        gpos = torch.clamp(gl, min=0.0)
-        G = self.comm.all_reduce_scalar(float(torch.dot(gpos, gpos).item())) / (norm * norm)
-        if not G > 0:
-            G = 1.0
-        k.prep_rows(self.g64.data_ptr(), self.P, self.Pp, 1.0 / norm, self.ray_length.data_ptr(),
-                    float(np.float32(p.ray_length_threshold)), self.ghat.data_ptr(), self.arow.data_ptr(),
-                    self.gpos.data_ptr(), self.wo.data_ptr(), s)
-        if solution is None:
-            # cold start: x0 = [rho > tau] A^T max(ghat, 0) / rho  (reference sart_kernels.cu:22-60)
-            self._backproject_reduce(self.gpos, self.dinv, out=self.comm_buf)
-            self.comm.all_reduce_(self.comm_buf[: self.ld])
-            k.init_solution(self.x.data_ptr(), self.V, self.ld, self.comm_buf.data_ptr(), 0, 1.0, s)
-        else:
-            x0 = torch.as_tensor(solution, dtype=torch.float64).to(self.dev)
-            if x0.numel() != self.V:
-                raise ValueError("Solution vector must be empty or contain nvoxel elements.")
-            k.init_solution(self.x.data_ptr(), self.V, self.ld, 0, x0.data_ptr(), 1.0 / norm, s)
-        if self.log:
-            # frame-constant observed back-projection O = [rho > tau] A^T (a ghat)
-            self._backproject_reduce(self.wo, self.dmask, out=self.O)
-            self.comm.all_reduce_(self.O)
-        k.state_begin(self.state.data_ptr(), G, float(p.conv_tolerance), int(p.max_iterations), s)
-        return norm
-
-    def _backproject_reduce(self, w, scale, out) -> None:
-        k, s = self.k, self._stream()
-        k.backproject(self.rtm.A.data_ptr(), self.ld, self.P, w.data_ptr(), self.nsplit, self.partial.data_ptr(), 0, s)
-        k.reduce_partials(self.partial.data_ptr(), self.ld, self.nsplit, scale.data_ptr(), out.data_ptr(), 0, 0, 0, 0, s)
-
-    # ------------------------------------------------------------------------------------------
-    def _sweep(self) -> None:
-        """One SART iteration: fused (or 2-pass) projection sweep, penalty, reduction, decision, update."""
-        k, s, st = self.k, self._stream(), self.state.data_ptr()
-        A = self.rtm.A.data_ptr()
-        scale = self.dmask if self.log else self.dscale
-        Fslot = self.comm_buf.data_ptr() + 4 * self.ld
-        if self.use_fused:
-            g = self.geom
-            if g.variant == 6:
-                self.xcnt.zero_()
-            k.fused_sweep(self.log, g.K, g.variant, A, self.ld, self.P, self.Pp, self.x.data_ptr(), self.ghat.data_ptr(),
-                          self.arow.data_ptr(), self.partial.data_ptr(), self.Fpart.data_ptr(),
-                          self.gran.data_ptr(), g.I, g.J, st, self.xcnt.data_ptr(), s)
-            k.reduce_partials(self.partial.data_ptr(), self.ld, g.I, scale.data_ptr(), self.comm_buf.data_ptr(),
-                              self.Fpart.data_ptr(), self.nF_fused, Fslot, st, s)
-        else:
-            epi = EPI_LOG if self.log else EPI_LINEAR
-            k.forward(epi, A, self.ld, self.P, self.Pp, self.x.data_ptr(), self.ghat.data_ptr(), self.arow.data_ptr(),
-                      0, self.w.data_ptr(), self.Fpart.data_ptr(), st, s)
-            k.backproject(A, self.ld, self.P, self.w.data_ptr(), self.nsplit, self.partial.data_ptr(), st, s)
-            k.reduce_partials(self.partial.data_ptr(), self.ld, self.nsplit, scale.data_ptr(),
-                              self.comm_buf.data_ptr(), self.Fpart.data_ptr(), k.forward_num_blocks(self.Pp), Fslot,
-                              st, s)
-        pen = 0
+        cfg = self.k.EngineConfig()
+        cfg.logarithmic = self.log
+        cfg.ray_density_threshold = float(p.ray_density_threshold)
+        cfg.ray_length_threshold = float(p.ray_length_threshold)
+        cfg.conv_tolerance = float(p.conv_tolerance)
+        cfg.beta_laplace = float(p.beta_laplace)
+        cfg.relaxation = float(p.relaxation)
+        cfg.max_iterations = int(p.max_iterations)
+        cfg.allow_zero_tolerance = bool(allow_zero_tolerance)
+        cfg.check_interval = max(1, int(check_interval))
+        cfg.use_fused = bool(use_fused)
+        cfg.fused_variant = int(fused_variant)
+        cfg.rows_per_tile = int(fused_rows_per_tile or 0)
+        cfg.fused_schedule = int(os.environ.get("SART_FUSED_SCHEDULE", "-1"))
+        if use_graph is None:
+            use_graph = os.environ.get("SART_GRAPH", "0") == "1"
+        cfg.use_graph = bool(use_graph)
+        device = self.dev.index if self.dev.index is not None else 0
+        self.native_comm = native_communicator(self.comm, device)
+        self.engine = self.k.Engine(device, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld,
+                                    self.native_comm, cfg)
         if self.L is not None:
-            k.penalty(self.log, self.L.row_ptr.data_ptr(), self.L.col.data_ptr(), self.L.val.data_ptr(), self.V,
-                      float(np.float32(self.params.beta_laplace)), self.x.data_ptr(), self.pen.data_ptr(), st, s)
-            pen = self.pen.data_ptr()
-        if self.comm.world_size > 1:
-            self.comm.all_reduce_(self.comm_buf[: self.ld + 1])
-        k.decide(st, Fslot, s)
-        if self.log:
-            k.update_log(self.x.data_ptr(), self.O.data_ptr(), self.comm_buf.data_ptr(), pen,
-                         float(np.float32(self.params.relaxation)), self.V, st, s)
-        else:
-            k.update_linear(self.x.data_ptr(), self.comm_buf.data_ptr(), pen, self.V, st, s)
+            self.engine.set_laplacian(self.L.row_ptr_host, self.L.col_host, self.L.val_host)
+        self.P, self.Pp, self.V, self.ld = rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld
+        self.num_cus = self.engine.num_cus
 
-    # ------------------------------------------------------------------------------------------
+    @property
+    def use_fused(self) -> bool:
+        return self.engine.use_fused
+
+    @property
+    def geom(self):
+        return self.engine.geometry if self.engine.use_fused else None
+
+    @property
+    def ray_density64(self) -> np.ndarray:
+        return self.engine.ray_density()
+
+    @property
+    def ray_length64(self) -> np.ndarray:
+        return self.engine.ray_length()
+
     def solve(self, measurement, solution=None) -> SolveResult:
         """Solve one frame. ``measurement``: this rank's pixel slice (fp64); ``solution``: warm start
         (fp64, nvoxel) or None for the default initial guess."""
-        while True:
-            res = self._solve_once(measurement, solution)
-            if res is not None:
-                return res
-            self._fused_fallback()
+        g = _host_f64(measurement)
+        x0 = None if solution is None else _host_f64(solution)
+        x, info = self.engine.solve(g, x0)
+        if info["fallbacks"]:
+            log.warning("fused sweep fell back %d time(s); now %s", info["fallbacks"],
+                        f"variant {info['fused_variant']}" if info["used_fused"] else "two-pass kernels")
+        status = SUCCESS if info["status"] == SUCCESS else MAX_ITERATIONS_EXCEEDED
+        return SolveResult(solution=x, status=status, iterations=int(info["iterations"]),
+                           convergence=float(info["convergence"]), used_fused=bool(info["used_fused"]),
+                           elapsed_ms=float(info["ms"]))
 
-    def _fused_fallback(self) -> None:
-        """A persistent sweep gave up waiting (SartState.error): XCD-local groups (variant 6) -> generic
-        groups (variant 3) -> two-pass kernels. The frame is re-solved from scratch, so results never
-        depend on the fallback."""
-        g = self.geom
-        nxt = fused_geometry(self.ld, self.num_cus, 3) if (g is not None and g.variant == 6) else None
-        if nxt is not None and nxt.variant == 3:
-            log.warning("fused sweep variant 6 timed out (unexpected workgroup placement); using variant 3")
-            self.geom = nxt
-            self.nF_fused = nxt.grid * self.k.fused_fpart_per_block(3)
-            n_part = max(self.nsplit, nxt.I)
-            if self.partial.numel() < n_part * self.ld:
-                self.partial = torch.zeros(n_part * self.ld, dtype=torch.float32, device=self.dev)
-            if self.gran.numel() < self.Pp * nxt.J:
-                self.gran = torch.zeros(self.Pp * nxt.J, dtype=torch.int64, device=self.dev)
-            if self.Fpart.numel() < self.nF_fused:
-                self.Fpart = torch.zeros(self.nF_fused, dtype=torch.float64, device=self.dev)
-        else:
-            log.warning("fused sweep protocol timeout; switching to the two-pass kernels")
-            self.use_fused = False
-
-    def _solve_once(self, measurement, solution) -> Optional[SolveResult]:
-        norm = self._setup_frame(measurement, solution)
-        max_sweeps = self.params.max_iterations + 1
-        done_sweeps = 0
-        st = None
-        while done_sweeps < max_sweeps:
-            n = min(self.check_interval, max_sweeps - done_sweeps)
-            for _ in range(n):
-                self._sweep()
-            done_sweeps += n
-            st = read_state(self.state)  # one small D2H per chunk (implicit stream sync)
-            if st.error:
-                return None
-            if st.done:
-                break
-        if st is None or not st.done:
-            st = read_state(self.state)
-        x = self.x[: self.V].to(torch.float64).cpu().numpy() * norm
-        status = SUCCESS if st.status == SUCCESS else MAX_ITERATIONS_EXCEEDED
-        return SolveResult(solution=x, status=status, iterations=st.iterations, convergence=st.conv_last,
-                           used_fused=self.use_fused)
-
-    # ------------------------------------------------------------------------------------------
     def forward_project(self, x_local) -> np.ndarray:
         """f = A x for this shard (utility / tests)."""
-        k, s = self.k, self._stream()
-        xx = torch.zeros(self.ld, dtype=torch.float32, device=self.dev)
-        xx[: self.V] = torch.as_tensor(x_local, dtype=torch.float32).to(self.dev)
-        k.forward(EPI_PLAIN, self.rtm.A.data_ptr(), self.ld, self.P, self.Pp, xx.data_ptr(), 0, 0,
-                  self.fitted.data_ptr(), 0, 0, 0, s)
-        return self.fitted[: self.P].cpu().numpy().astype(np.float64)
+        return self.engine.forward(_host_f64(x_local))

@@ -137,6 +137,43 @@ def init_distributed(use_gpu: bool = True, timeout_s: float = 1800.0) -> Communi
     return TorchDistComm(device=dev)
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("", 0))
+        return s.getsockname()[1]
+
+
+def native_communicator(comm: Optional[Communicator], device: int = 0):
+    """The native engine's communicator (csrc/engine/comm.hpp) for a Python communicator, created once
+    per process group and cached on it:
+
+    * world size 1 -> ``LocalComm``;
+    * ``nccl`` process group -> the engine's own RCCL communicator over xGMI (unique id handed out through
+      the process group) with a TCP side channel for host scalars;
+    * ``gloo`` -> ``TcpComm`` (host-staged reductions in fixed rank order), e.g. several ranks sharing one
+      GPU in tests, or CPU ranks.
+    """
+    from ..ops import hip
+
+    k = hip()
+    if comm is None or comm.world_size == 1:
+        return k.local_comm()
+    cached = getattr(comm, "_native_comm", None)
+    if cached is not None:
+        return cached
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = comm.broadcast_object(_free_port() if comm.rank == 0 else None, src=0)
+    if getattr(comm, "backend", "gloo") == "nccl":
+        uid = comm.broadcast_object(k.rccl_unique_id() if comm.rank == 0 else None, src=0)
+        native = k.rccl_comm(device, uid, comm.rank, comm.world_size, host, int(port))
+    else:
+        native = k.tcp_comm(comm.rank, comm.world_size, host, int(port))
+    comm._native_comm = native
+    return native
+
+
 def abort_all(msg: str, code: int = 1) -> None:
     """Fatal error in a multi-rank run: tear the group down instead of a bare exit that leaves the
     peers blocked in a collective (reference exits per rank: sartsolver_cuda.cpp:45-75)."""
