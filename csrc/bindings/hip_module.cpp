@@ -38,17 +38,18 @@ static py::dict solve_info(const sart::SolveInfo& i) {
     d["used_fused"] = i.used_fused;
     d["fused_variant"] = i.fused_variant;
     d["fallbacks"] = i.fallbacks;
+    d["nonfinite"] = i.nonfinite;
     d["ms"] = i.ms;
     return d;
 }
 
 static void bind_engine(py::module_& m) {
-    py::enum_<sart::ReduceOp>(m, "ReduceOp").value("SUM", sart::ReduceOp::kSum).value("MAX", sart::ReduceOp::kMax);
+    py::enum_<sart::ReduceOp>(m, "ReduceOp", py::module_local()).value("SUM", sart::ReduceOp::kSum).value("MAX", sart::ReduceOp::kMax);
     py::class_<sart::Communicator, std::shared_ptr<sart::Communicator>>(m, "Comm")
-        .def_property_readonly("rank", &sart::Communicator::rank)
-        .def_property_readonly("size", &sart::Communicator::size)
+        .def_property_readonly("rank", [](sart::Communicator& c) { return c.rank(); })
+        .def_property_readonly("size", [](sart::Communicator& c) { return c.size(); })
         .def_property_readonly("backend", &sart::Communicator::backend)
-        .def("barrier", &sart::Communicator::barrier, py::call_guard<py::gil_scoped_release>())
+        .def("barrier", [](sart::Communicator& c) { c.host().barrier(); }, py::call_guard<py::gil_scoped_release>())
         .def("abort", &sart::Communicator::abort)
         .def("all_reduce_host",
              [](sart::Communicator& c, f64arr v, sart::ReduceOp op) {
@@ -58,7 +59,7 @@ static void bind_engine(py::module_& m) {
                  const size_t n = (size_t)v.size();
                  {
                      py::gil_scoped_release rel;
-                     c.all_reduce_host(p, n, op);
+                     c.host().all_reduce_host(p, n, op);
                  }
                  return out;
              })
@@ -72,7 +73,7 @@ static void bind_engine(py::module_& m) {
                  }
                  {
                      py::gil_scoped_release rel;
-                     c.broadcast_host(buf.data(), nbytes, root);
+                     c.host().broadcast_host(buf.data(), nbytes, root);
                  }
                  return py::bytes(buf);
              })
@@ -85,10 +86,11 @@ static void bind_engine(py::module_& m) {
                      c.all_reduce(P<float>(ptr), n, op, S(stream));
              });
     m.def("local_comm", []() { return std::shared_ptr<sart::Communicator>(sart::make_local_comm()); });
-    m.def("tcp_comm",
+    m.def("staged_comm",
           [](int rank, int size, const std::string& host, int port, double timeout_s) {
               py::gil_scoped_release rel;
-              return std::shared_ptr<sart::Communicator>(sart::make_tcp_comm(rank, size, host, port, timeout_s));
+              return std::shared_ptr<sart::Communicator>(
+                  sart::make_staged_comm(sart::make_tcp_host_comm(rank, size, host, port, timeout_s)));
           },
           py::arg("rank"), py::arg("size"), py::arg("host"), py::arg("port"), py::arg("timeout_s") = 3600.0);
     m.def("rccl_unique_id", []() { return py::bytes(sart::rccl_unique_id()); });
@@ -97,11 +99,11 @@ static void bind_engine(py::module_& m) {
               const std::string id = uid;
               py::gil_scoped_release rel;
               return std::shared_ptr<sart::Communicator>(
-                  sart::make_rccl_comm(device, id, sart::make_tcp_comm(rank, size, host, port)));
+                  sart::make_rccl_comm(device, id, sart::make_tcp_host_comm(rank, size, host, port)));
           });
-    m.def("comm_from_env", [](bool gpu, int device) {
+    m.def("comm_from_env", [](int device) {
         py::gil_scoped_release rel;
-        return std::shared_ptr<sart::Communicator>(sart::comm_from_env(gpu, device));
+        return std::shared_ptr<sart::Communicator>(sart::comm_from_env(device));
     });
 
     py::class_<sart::FusedGeometry>(m, "FusedGeometry")
@@ -134,7 +136,7 @@ static void bind_engine(py::module_& m) {
         .def_readwrite("use_graph", &sart::EngineConfig::use_graph);
     m.def("validate_config", [](const sart::EngineConfig& c) {
         try {
-            sart::validate_config(c);
+            sart::validate_params(c);
         } catch (const std::invalid_argument& e) {
             throw py::value_error(e.what());
         }

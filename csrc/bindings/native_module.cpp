@@ -8,6 +8,8 @@
 
 #include "config.hpp"
 #include "cpu_kernels.hpp"
+#include "cpu_solver.hpp"
+#include "host_comm.hpp"
 #include "fixtures.hpp"
 #include "frames.hpp"
 #include "h5.hpp"
@@ -306,4 +308,112 @@ PYBIND11_MODULE(_sart_native, m) {
             write_laplacian_file(path, nvoxel, vec(i), vec(j), vec(v));
         },
         py::arg("path"), py::arg("nvoxel"), py::arg("i"), py::arg("j"), py::arg("value"));
+
+    // ---- host collectives and the CPU solver (the --use_cpu path)
+    py::enum_<ReduceOp>(m, "ReduceOp", py::module_local()).value("SUM", ReduceOp::kSum).value("MAX", ReduceOp::kMax);
+    py::class_<HostComm, std::shared_ptr<HostComm>>(m, "HostComm")
+        .def_property_readonly("rank", &HostComm::rank)
+        .def_property_readonly("size", &HostComm::size)
+        .def_property_readonly("backend", &HostComm::backend)
+        .def("barrier", &HostComm::barrier, py::call_guard<py::gil_scoped_release>())
+        .def("broadcast_bytes",
+             [](HostComm& c, py::bytes data, size_t nbytes, int root) {
+                 std::string buf(nbytes, '\0');
+                 if (c.rank() == root) {
+                     const std::string d = data;
+                     if (d.size() != nbytes) throw py::value_error("broadcast_bytes: root payload size mismatch");
+                     buf = d;
+                 }
+                 {
+                     py::gil_scoped_release rel;
+                     c.broadcast_host(buf.data(), nbytes, root);
+                 }
+                 return py::bytes(buf);
+             })
+        .def("all_reduce_host", [](HostComm& c, f64arr v, ReduceOp op) {
+            py::array_t<double> out(v.size());
+            std::copy(v.data(), v.data() + v.size(), out.mutable_data());
+            double* p = out.mutable_data();
+            const size_t n = (size_t)v.size();
+            {
+                py::gil_scoped_release rel;
+                c.all_reduce_host(p, n, op);
+            }
+            return out;
+        });
+    m.def("local_host_comm", []() { return std::shared_ptr<HostComm>(make_local_host_comm()); });
+    m.def("tcp_host_comm",
+          [](int rank, int size, const std::string& host, int port, double timeout_s) {
+              py::gil_scoped_release rel;
+              return std::shared_ptr<HostComm>(make_tcp_host_comm(rank, size, host, port, timeout_s));
+          },
+          py::arg("rank"), py::arg("size"), py::arg("host"), py::arg("port"), py::arg("timeout_s") = 3600.0);
+    m.def("block_partition", [](uint64_t n, int parts, int part) {
+        const Block b = block_partition(n, parts, part);
+        return py::make_tuple(b.offset, b.size);
+    });
+
+    py::class_<SolverParams>(m, "SolverParams")
+        .def(py::init<>())
+        .def_readwrite("logarithmic", &SolverParams::logarithmic)
+        .def_readwrite("ray_density_threshold", &SolverParams::ray_density_threshold)
+        .def_readwrite("ray_length_threshold", &SolverParams::ray_length_threshold)
+        .def_readwrite("conv_tolerance", &SolverParams::conv_tolerance)
+        .def_readwrite("beta_laplace", &SolverParams::beta_laplace)
+        .def_readwrite("relaxation", &SolverParams::relaxation)
+        .def_readwrite("max_iterations", &SolverParams::max_iterations)
+        .def_readwrite("allow_zero_tolerance", &SolverParams::allow_zero_tolerance);
+
+    py::class_<CpuSolver>(m, "CpuSolver")
+        .def(py::init([](py::array A, int64_t P, int64_t V, std::shared_ptr<HostComm> comm, const SolverParams& p,
+                         bool gpu_semantics) {
+                 py::buffer_info bi = A.request();
+                 if (bi.format != py::format_descriptor<float>::format())
+                     throw std::invalid_argument("A must be float32");
+                 const int64_t ld = bi.ndim == 2 ? bi.shape[1] : V;
+                 check_rows(bi, P, V, ld);
+                 try {
+                     return new CpuSolver(static_cast<const float*>(bi.ptr), P, V, ld, comm.get(), p, gpu_semantics);
+                 } catch (const std::invalid_argument& e) {
+                     throw py::value_error(e.what());
+                 }
+             }),
+             py::keep_alive<1, 2>(), py::keep_alive<1, 5>())
+        .def("set_laplacian",
+             [](CpuSolver& s, int64_t n, py::array_t<int64_t, py::array::c_style | py::array::forcecast> rp,
+                i32arr col, f32arr val) {
+                 Csr c;
+                 c.n = n;
+                 c.row_ptr.assign(rp.data(), rp.data() + rp.size());
+                 c.col.assign(col.data(), col.data() + col.size());
+                 c.val.assign(val.data(), val.data() + val.size());
+                 s.set_laplacian(c);
+             })
+        .def("solve",
+             [](CpuSolver& s, f64arr g, py::object x0) {
+                 f64arr x0a;
+                 const double* x0p = nullptr;
+                 if (!x0.is_none()) {
+                     x0a = x0.cast<f64arr>();
+                     x0p = x0a.data();
+                 }
+                 py::array_t<double> x(s.ray_density().size());
+                 double* xp = x.mutable_data();
+                 const double* gp = g.data();
+                 SolveInfo info;
+                 {
+                     py::gil_scoped_release rel;
+                     info = s.solve(gp, x0p, xp);
+                 }
+                 py::dict d;
+                 d["status"] = info.status;
+                 d["iterations"] = info.iterations;
+                 d["convergence"] = info.convergence;
+                 d["nonfinite"] = info.nonfinite;
+                 d["ms"] = info.ms;
+                 return py::make_tuple(x, d);
+             },
+             py::arg("g"), py::arg("x0") = py::none())
+        .def("ray_density", [](const CpuSolver& s) { return arr(s.ray_density()); })
+        .def("ray_length", [](const CpuSolver& s) { return arr(s.ray_length()); });
 }

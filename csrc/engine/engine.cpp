@@ -49,21 +49,10 @@ template class DeviceArray<unsigned>;
 template class DeviceArray<int64_t>;
 template class DeviceArray<int32_t>;
 
-void validate_config(const EngineConfig& c) {
-    if (c.ray_density_threshold < 0) throw std::invalid_argument("Ray density threshold must be non-negative.");
-    if (c.ray_length_threshold < 0) throw std::invalid_argument("Ray length threshold must be non-negative.");
-    if (c.conv_tolerance < 0 || (c.conv_tolerance == 0 && !c.allow_zero_tolerance))
-        throw std::invalid_argument("Convolution tolerance must be positive.");
-    if (c.beta_laplace < 0) throw std::invalid_argument("Attribute beta_laplace must be non-negative.");
-    if (!(c.relaxation > 0 && c.relaxation <= 1.0))
-        throw std::invalid_argument("Attribute relaxation must be within (0, 1] interval.");
-    if (c.max_iterations <= 0) throw std::invalid_argument("Attribute max_iterations must be positive.");
-}
-
 Engine::Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
                Communicator* comm, const EngineConfig& cfg)
     : device_(device), A_(A), P_(nrows), Pp_(nrows_pad), V_(nvoxel), ld_(ld), comm_(comm), cfg_(cfg) {
-    validate_config(cfg_);
+    validate_params(cfg_);
     if (!comm_) throw std::invalid_argument("Engine: communicator required");
     if (ld_ % 64 || ld_ < V_ || Pp_ % 64 || Pp_ < P_)
         throw std::invalid_argument("Engine: ld and nrows_pad must be multiples of 64 covering the shard");
@@ -181,9 +170,9 @@ double Engine::setup_frame(const double* g, const double* x0) {
         mx = std::max(mx, g[i]);
         if (g[i] > 0) gs += g[i] * g[i];
     }
-    double norm = comm_->all_reduce_scalar(mx, ReduceOp::kMax);
+    double norm = comm_->host().all_reduce_scalar(mx, ReduceOp::kMax);
     if (!(norm > 0)) norm = 1.0;
-    double G = comm_->all_reduce_scalar(gs, ReduceOp::kSum) / (norm * norm);
+    double G = comm_->host().all_reduce_scalar(gs, ReduceOp::kSum) / (norm * norm);
     if (!(G > 0)) G = 1.0;
     if (P_) hip_ok(hipMemcpyAsync(g64_.get(), g, P_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D g");
     launch_prep_rows(g64_.get(), P_, Pp_, 1.0 / norm, ray_len_.get(), (float)cfg_.ray_length_threshold, ghat_.get(),
@@ -343,6 +332,7 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
     info.status = s.status == kSuccess ? kSuccess : kMaxIterationsExceeded;
     info.iterations = s.iterations;
     info.convergence = s.conv_last;
+    info.nonfinite = (s.flags & 1) != 0;
     info.used_fused = use_fused_;
     info.fused_variant = use_fused_ ? geom_.variant : -1;
     info.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

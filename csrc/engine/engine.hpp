@@ -20,39 +20,19 @@
 #include <vector>
 
 #include "../kernels/sart_common.hpp"
+#include "../native/solver_params.hpp"
 #include "comm.hpp"
 #include "geometry.hpp"
 
 namespace sart {
 
-struct EngineConfig {
-    bool logarithmic = false;
-    double ray_density_threshold = 1e-6;
-    double ray_length_threshold = 1e-6;
-    double conv_tolerance = 1e-5;
-    double beta_laplace = 1e-2;
-    double relaxation = 1.0;
-    int max_iterations = 2000;
-    bool allow_zero_tolerance = false;  // benchmarks: run exactly max_iterations
+struct EngineConfig : SolverParams {
     int check_interval = 16;
     bool use_fused = true;
     int fused_variant = 6;
     int rows_per_tile = 0;   // 0: default (fused_geometry)
     int fused_schedule = -1; // -1: keep the launcher's default
     bool use_graph = false;  // opt-in (SART_GRAPH=1): chunk capture is under validation
-};
-
-// Same checks and messages as the reference setters (sartsolver.cpp:61-123); throws std::invalid_argument.
-void validate_config(const EngineConfig& c);
-
-struct SolveInfo {
-    int status = -1;          // 0 SUCCESS, -1 MAX_ITERATIONS_EXCEEDED
-    int iterations = 0;
-    double convergence = 0.0; // last (G - ||A x||^2) / G
-    bool used_fused = false;
-    int fused_variant = -1;
-    int fallbacks = 0;        // protocol timeouts survived during this solve
-    double ms = 0.0;
 };
 
 template <typename T>

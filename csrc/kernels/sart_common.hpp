@@ -34,7 +34,7 @@ struct alignas(16) SartState {
     int32_t error;      // 52: nonzero when a persistent kernel gave up waiting (protocol timeout)
     double tol;         // 56: convergence tolerance
     int32_t epoch;      // 64: exchange epoch of the fused sweep (strictly increasing, never 0)
-    int32_t pad0;       // 68
+    int32_t flags;      // 68: bit 0 = the sweep produced a non-finite ||A x||^2 (solve stopped)
     double reserved[7]; // 72..127
 };
 static_assert(sizeof(SartState) == 128, "SartState must be 128 bytes");

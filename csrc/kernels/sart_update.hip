@@ -85,6 +85,15 @@ __global__ void k_decide(SartState* __restrict__ st, const float* __restrict__ F
     st->F_last = F;
     int done = 0;
     int status = kRunning;
+    if (!isfinite(F)) {  // NaN/Inf guard: stop with the last finite iterate's status
+        st->flags |= 1;
+        st->iterations = s;
+        st->sweep = s + 1;
+        st->status = kMaxIterationsExceeded;
+        st->done = 1;
+        st->epoch = st->epoch + 1;
+        return;
+    }
     if (s >= 1) {
         const double conv = (st->G - F) / st->G;
         if (s >= 2 && fabs(conv - st->conv_prev) < st->tol) {
@@ -142,6 +151,7 @@ __global__ void k_state_begin(SartState* __restrict__ st, double G, double tol, 
     st->iterations = 0;
     st->max_iter = max_iter;
     st->error = 0;
+    st->flags = 0;
     st->tol = tol;
     if (st->epoch <= 0) st->epoch = 1;
 }

@@ -1,0 +1,47 @@
+// Solver parameters, results and the Laplacian CSR shared by the GPU engine and the CPU solver.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+namespace sart {
+
+// Reference defaults (sartsolver.hpp:64-66; the CLI overrides beta_laplace with 2e-2, arguments.cpp:125).
+struct SolverParams {
+    bool logarithmic = false;
+    double ray_density_threshold = 1e-6;
+    double ray_length_threshold = 1e-6;
+    double conv_tolerance = 1e-5;
+    double beta_laplace = 1e-2;
+    double relaxation = 1.0;
+    int max_iterations = 2000;
+    bool allow_zero_tolerance = false;  // benchmarks: run exactly max_iterations
+};
+
+// Same checks and messages as the reference setters (sartsolver.cpp:61-123); throws std::invalid_argument.
+void validate_params(const SolverParams& p);
+
+struct SolveInfo {
+    int status = -1;          // 0 SUCCESS, -1 MAX_ITERATIONS_EXCEEDED (reference sartsolver.cpp:16-17)
+    int iterations = 0;
+    double convergence = 0.0; // last (G - ||A x||^2) / G
+    bool used_fused = false;
+    int fused_variant = -1;
+    int fallbacks = 0;        // persistent-kernel protocol timeouts survived during this solve
+    bool nonfinite = false;   // the iteration produced NaN/Inf and was stopped
+    double ms = 0.0;
+};
+
+// CSR over n rows (row_ptr int64, col int32, val fp32), from the reference's sorted-flat-index COO
+// (laplacian.cpp:34-91).
+struct Csr {
+    int64_t n = 0;
+    std::vector<int64_t> row_ptr;
+    std::vector<int32_t> col;
+    std::vector<float> val;
+    int64_t nnz() const { return (int64_t)val.size(); }
+};
+Csr csr_from_coo(int64_t n, const std::vector<uint64_t>& i, const std::vector<uint64_t>& j,
+                 const std::vector<float>& v);
+
+}  // namespace sart

@@ -101,7 +101,8 @@ def build_hip(verbose: bool = True) -> Path:
     objdir = BUILDDIR / "hip"
     objdir.mkdir(parents=True, exist_ok=True)
     LIBDIR.mkdir(parents=True, exist_ok=True)
-    headers = sorted((CSRC / "kernels").glob("*.hpp")) + sorted((CSRC / "engine").glob("*.hpp"))
+    headers = (sorted((CSRC / "kernels").glob("*.hpp")) + sorted((CSRC / "engine").glob("*.hpp")) +
+               sorted((CSRC / "native").glob("*.hpp")))
     common = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
     jobs = []
     objs = []
@@ -112,7 +113,8 @@ def build_hip(verbose: bool = True) -> Path:
         objs.append(obj)
     # native engine (host C++ on the HIP runtime + RCCL): csrc/engine
     eflags = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}"]
-    for src in sorted((CSRC / "engine").glob("*.cpp")):
+    for src in sorted((CSRC / "engine").glob("*.cpp")) + [CSRC / "native" / "host_comm.cpp",
+                                                          CSRC / "native" / "solver_params.cpp"]:
         obj = objdir / ("engine_" + src.stem + ".o")
         jobs.append(([hipcc, *eflags, "-c", str(src), "-o", str(obj)], obj, _digest([src, *headers], eflags)))
         objs.append(obj)

@@ -10,7 +10,7 @@ import struct
 from dataclasses import dataclass
 
 STATE_NBYTES = 128
-_FMT = "<ddddiiiiiidii"  # up to `pad0`; the rest is reserved
+_FMT = "<ddddiiiiiidii"  # up to `flags`; the rest is reserved
 _SIZE = struct.calcsize(_FMT)
 
 SUCCESS = 0

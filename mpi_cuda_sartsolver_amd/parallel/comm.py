@@ -152,8 +152,8 @@ def native_communicator(comm: Optional[Communicator], device: int = 0):
     * world size 1 -> ``LocalComm``;
     * ``nccl`` process group -> the engine's own RCCL communicator over xGMI (unique id handed out through
       the process group) with a TCP side channel for host scalars;
-    * ``gloo`` -> ``TcpComm`` (host-staged reductions in fixed rank order), e.g. several ranks sharing one
-      GPU in tests, or CPU ranks.
+    * ``gloo`` -> staged communicator (device buffers staged through the TCP host communicator,
+      reductions in fixed rank order), e.g. several ranks sharing one GPU in tests.
     """
     from ..ops import hip
 
@@ -169,9 +169,27 @@ def native_communicator(comm: Optional[Communicator], device: int = 0):
         uid = comm.broadcast_object(k.rccl_unique_id() if comm.rank == 0 else None, src=0)
         native = k.rccl_comm(device, uid, comm.rank, comm.world_size, host, int(port))
     else:
-        native = k.tcp_comm(comm.rank, comm.world_size, host, int(port))
+        native = k.staged_comm(comm.rank, comm.world_size, host, int(port))
     comm._native_comm = native
     return native
+
+
+def native_host_communicator(comm: Optional[Communicator]):
+    """Host-only collectives for the native CPU solver (csrc/native/host_comm.hpp): local for one rank,
+    TCP (fixed rank order) otherwise. Cached on the process group."""
+    from ..ops import native
+
+    n = native()
+    if comm is None or comm.world_size == 1:
+        return n.local_host_comm()
+    cached = getattr(comm, "_native_host_comm", None)
+    if cached is not None:
+        return cached
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = comm.broadcast_object(_free_port() if comm.rank == 0 else None, src=0)
+    hc = n.tcp_host_comm(comm.rank, comm.world_size, host, int(port))
+    comm._native_host_comm = hc
+    return hc
 
 
 def abort_all(msg: str, code: int = 1) -> None:

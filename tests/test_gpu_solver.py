@@ -183,3 +183,31 @@ def test_fused_v6_schedules(dev, T, sched, log):
     assert r.used_fused, "fused exchange timed out"
     x_ref, _, _ = sart_gpu_semantics(A, g, logarithmic=log, **kw)
     assert _rel(r.solution, x_ref) < 2e-3
+
+
+def test_engine_rccl_single_rank(dev):
+    """The RCCL communicator path of the native engine (ncclCommInitRank + ncclAllReduce on the engine
+    stream) with one rank: same iterates as the local communicator."""
+    import socket
+
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.ops import hip
+    from mpi_cuda_sartsolver_amd.utils.synthetic import host_problem
+
+    k = hip()
+    A, g, _ = host_problem(1024, 4096, seed=9)
+    rtm = DenseRTM.from_dense(A, device=dev)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    rc = k.rccl_comm(dev.index or 0, k.rccl_unique_id(), 0, 1, "127.0.0.1", port)
+    assert rc.backend == "rccl" and rc.size == 1
+    cfg = k.EngineConfig()
+    cfg.max_iterations, cfg.conv_tolerance = 20, 1e-9
+    out = []
+    for comm in (k.local_comm(), rc):
+        e = k.Engine(dev.index or 0, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld, comm, cfg)
+        x, info = e.solve(g, None)
+        out.append((x, info))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1]["iterations"] == out[1][1]["iterations"]

@@ -21,8 +21,14 @@ def _tcp_worker(rank, world, port, q):
     sys.path.insert(0, ROOT)
     from mpi_cuda_sartsolver_amd.ops import hip
 
-    k = hip()
-    c = k.tcp_comm(rank, world, "127.0.0.1", port, 60.0)
+    if rank % 2:  # the device communicator's host side (staged) and the native host communicator interoperate
+        k = hip()
+        c = k.staged_comm(rank, world, "127.0.0.1", port, 60.0)
+    else:
+        from mpi_cuda_sartsolver_amd.ops import native
+
+        k = native()
+        c = k.tcp_host_comm(rank, world, "127.0.0.1", port, 60.0)
     v = np.arange(5, dtype=np.float64) * (rank + 1) + 0.1 * rank
     s = c.all_reduce_host(v, k.ReduceOp.SUM)
     m = c.all_reduce_host(np.array([float(rank), -float(rank)]), k.ReduceOp.MAX)
