@@ -1,0 +1,317 @@
+// sartsolver -- native driver binary: same CLI, input validation, frame loop, output file
+// and console output as the reference binary (reference main.cpp:25-151), MI355X-first:
+//
+//   * one process per GPU, any launcher that sets RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR /
+//     MASTER_PORT (torchrun --no-python, mpirun via OMPI_COMM_WORLD_*, or bin/sartsolver); one process
+//     runs without any launcher. Rank -> GPU = LOCAL_RANK % device count (reference: rank % count,
+//     sartsolver_cuda.cpp:96-98).
+//   * per-iteration reductions with RCCL over xGMI on device buffers (csrc/engine/comm.cpp), host
+//     scalars over the TCP bootstrap; the --use_cpu path uses the TCP host communicator.
+//   * every rank streams only its pixel rows from HDF5 straight into HBM through two pinned staging
+//     buffers (the reference keeps the whole shard in host RAM, raytransfer.hpp:20); with
+//     --parallel_read all ranks read at once, otherwise in turn (reference main.cpp:78-86).
+//   * the next composite frame is read on a helper thread while the current one is solved.
+//   * a fatal error on any rank aborts the communicators instead of leaving peers blocked in a
+//     collective (the reference calls std::exit on one rank).
+// Extensions: --resume, --two_pass, --profile FILE (JSON lines per frame). --batch_frames (multi-frame
+// MFMA solver) is provided by the Python driver (python -m mpi_cuda_sartsolver_amd).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <future>
+#include <iostream>
+#include <limits>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <sys/stat.h>
+#include <thread>
+#include <vector>
+
+#include "../engine/comm.hpp"
+#include "../engine/engine.hpp"
+#include "../engine/geometry.hpp"
+#include "../native/config.hpp"
+#include "../native/cpu_solver.hpp"
+#include "../native/frames.hpp"
+#include "../native/h5.hpp"
+#include "../native/host_comm.hpp"
+#include "../native/inputs.hpp"
+#include "../native/solver_params.hpp"
+
+using namespace sart;
+
+namespace {
+
+void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+bool file_exists(const std::string& p) {
+    struct stat st;
+    return ::stat(p.c_str(), &st) == 0;
+}
+
+// Device-resident row shard [nrows_pad x ld] filled by streaming HDF5 row blocks through two pinned
+// buffers: block k+1 is read on a helper thread while block k is copied host -> HBM.
+struct DeviceShard {
+    float* A = nullptr;
+    int64_t nrows = 0, nrows_pad = 0, nvoxel = 0, ld = 0;
+    ~DeviceShard() {
+        if (A) (void)hipFree(A);
+    }
+};
+
+std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0, uint64_t nrows, size_t block_bytes) {
+    auto sh = std::make_unique<DeviceShard>();
+    sh->nrows = (int64_t)nrows;
+    sh->nvoxel = (int64_t)in.nvoxel;
+    sh->ld = choose_ld(sh->nvoxel);
+    sh->nrows_pad = (sh->nrows + 63) / 64 * 64;
+    const size_t bytes = (size_t)sh->nrows_pad * sh->ld * sizeof(float);
+    hip_ok(hipMalloc(reinterpret_cast<void**>(&sh->A), bytes), "hipMalloc(RTM shard)");
+    hip_ok(hipMemset(sh->A, 0, bytes), "hipMemset(RTM shard)");
+    hip_ok(hipDeviceSynchronize(), "hipMemset sync");
+    const uint64_t V = in.nvoxel;
+    const uint64_t rows_per_block = std::max<uint64_t>(1, std::min<uint64_t>(nrows, block_bytes / (4 * V)));
+    float* buf[2] = {nullptr, nullptr};
+    for (auto& b : buf) hip_ok(hipHostMalloc(reinterpret_cast<void**>(&b), rows_per_block * V * sizeof(float)), "hipHostMalloc");
+    hipStream_t s;
+    hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    hipEvent_t ev[2];
+    for (auto& e : ev) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    bool ev_used[2] = {false, false};
+    auto read_into = [&](float* b, uint64_t r0, uint64_t r1) {
+        std::memset(b, 0, (r1 - r0) * V * sizeof(float));  // sparse COO rows are scattered into zeros
+        read_rtm_rows(in.rtm_files, in.rtm_name, V, row0 + r0, row0 + r1, b, V);
+    };
+    std::vector<std::pair<uint64_t, uint64_t>> blocks;
+    for (uint64_t r = 0; r < nrows; r += rows_per_block) blocks.emplace_back(r, std::min(nrows, r + rows_per_block));
+    try {
+        if (!blocks.empty()) read_into(buf[0], blocks[0].first, blocks[0].second);
+        for (size_t k = 0; k < blocks.size(); ++k) {
+            float* cur = buf[k % 2];
+            std::future<void> next;
+            if (k + 1 < blocks.size()) {
+                const int nb = (k + 1) % 2;
+                if (ev_used[nb]) hip_ok(hipEventSynchronize(ev[nb]), "event sync");
+                next = std::async(std::launch::async, read_into, buf[nb], blocks[k + 1].first, blocks[k + 1].second);
+            }
+            const uint64_t r0 = blocks[k].first, nr = blocks[k].second - blocks[k].first;
+            hip_ok(hipMemcpy2DAsync(sh->A + r0 * sh->ld, sh->ld * sizeof(float), cur, V * sizeof(float),
+                                    V * sizeof(float), nr, hipMemcpyHostToDevice, s),
+                   "H2D RTM block");
+            hip_ok(hipEventRecord(ev[k % 2], s), "event");
+            ev_used[k % 2] = true;
+            if (next.valid()) next.get();
+        }
+        hip_ok(hipStreamSynchronize(s), "RTM upload");
+    } catch (...) {
+        (void)hipStreamSynchronize(s);
+        for (auto& b : buf) (void)hipHostFree(b);
+        throw;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(s);
+    for (auto& b : buf) (void)hipHostFree(b);
+    return sh;
+}
+
+std::string json_escape(const std::string& s) {
+    std::string o;
+    for (char c : s) o += (c == '"' || c == '\\') ? std::string("\\") + c : std::string(1, c);
+    return o;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    std::vector<std::string> args(argv + 1, argv + argc);
+    Config cfg;
+    std::vector<std::array<double, 4>> intervals;
+    InputSet in;
+    try {
+        cfg = parse_arguments(args);
+        if (cfg.help) {
+            std::cout << usage() << std::endl;
+            return 0;
+        }
+        intervals = parse_time_intervals(cfg.time_range);
+        // metadata validation on every rank, before any communicator exists (reference main.cpp:27-59)
+        in = validate_inputs(cfg.input_files, cfg.raytransfer_name, cfg.wavelength_threshold);
+    } catch (const std::exception& e) {
+        std::cerr << e.what() << std::endl;
+        return 1;
+    }
+    if (cfg.batch_frames > 1) {
+        std::cerr << "--batch_frames is served by the multi-frame solver of the Python driver "
+                     "(python -m mpi_cuda_sartsolver_amd)" << std::endl;
+        return 1;
+    }
+
+    const bool gpu = !cfg.use_cpu;
+    const EnvWorld w = env_world();
+    int device = 0;
+    std::unique_ptr<Communicator> dcomm;
+    std::unique_ptr<HostComm> hcomm;
+    HostComm* host = nullptr;
+    try {
+        if (gpu) {
+            int ndev = 0;
+            if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+                throw std::runtime_error("No GPU available: run with --use_cpu or on an MI355X node.");
+            device = w.local_rank % ndev;
+            hip_ok(hipSetDevice(device), "hipSetDevice");
+            dcomm = comm_from_env(device);
+            host = &dcomm->host();
+        } else {
+            hcomm = host_comm_from_env();
+            host = hcomm.get();
+        }
+    } catch (const std::exception& e) {
+        std::cerr << e.what() << std::endl;
+        return 1;
+    }
+    const int rank = host->rank(), size = host->size();
+
+    try {
+        const Block blk = block_partition(in.npixel, size, rank);  // reference main.cpp:67-68
+        if (blk.size == 0)
+            throw std::runtime_error("rank " + std::to_string(rank) + " owns no pixels: use at most " +
+                                     std::to_string(in.npixel) + " ranks");
+        CompositeImage image(in.image_files, in.frame_masks, intervals, blk.size, blk.offset);
+        image.set_max_cache_size((uint64_t)cfg.max_cached_frames);
+
+        SolverParams params;
+        params.logarithmic = cfg.logarithmic;
+        params.ray_density_threshold = cfg.ray_density_threshold;
+        params.ray_length_threshold = cfg.ray_length_threshold;
+        params.conv_tolerance = cfg.conv_tolerance;
+        params.beta_laplace = cfg.beta_laplace;
+        params.relaxation = cfg.relaxation;
+        params.max_iterations = cfg.max_iterations;
+        validate_params(params);
+        Csr lap;
+        if (!cfg.laplacian_file.empty()) {
+            const LaplacianCOO coo = read_laplacian(cfg.laplacian_file, in.nvoxel);
+            lap = csr_from_coo((int64_t)in.nvoxel, coo.i, coo.j, coo.value);
+        }
+
+        std::unique_ptr<DeviceShard> dshard;
+        std::vector<float> hshard;
+        auto load = [&]() {
+            if (gpu)
+                dshard = load_device_shard(in, blk.offset, blk.size, (size_t)256 << 20);
+            else {
+                hshard.assign(blk.size * in.nvoxel, 0.f);
+                read_rtm_rows(in.rtm_files, in.rtm_name, in.nvoxel, blk.offset, blk.offset + blk.size, hshard.data(),
+                              in.nvoxel);
+            }
+        };
+        if (cfg.parallel_read || size == 1) {
+            load();
+        } else {
+            for (int r = 0; r < size; ++r) {  // serialized reads (reference main.cpp:80-85)
+                if (r == rank) load();
+                host->barrier();
+            }
+        }
+
+        std::unique_ptr<Engine> engine;
+        std::unique_ptr<CpuSolver> cpu;
+        if (gpu) {
+            EngineConfig ec;
+            static_cast<SolverParams&>(ec) = params;
+            ec.use_fused = !cfg.two_pass;
+            if (const char* v = std::getenv("SART_FUSED_VARIANT"); v && *v) ec.fused_variant = std::atoi(v);
+            engine = std::make_unique<Engine>(device, dshard->A, dshard->nrows, dshard->nrows_pad, dshard->nvoxel,
+                                              dshard->ld, dcomm.get(), ec);
+            if (lap.nnz()) engine->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
+        } else {
+            cpu = std::make_unique<CpuSolver>(hshard.data(), (int64_t)blk.size, (int64_t)in.nvoxel,
+                                              (int64_t)in.nvoxel, host, params, false);
+            if (lap.nnz()) cpu->set_laplacian(lap);
+        }
+
+        // rank 0 owns the output (reference main.cpp:115-125, solution.cpp)
+        std::unique_ptr<SolutionWriter> writer;
+        VoxelGrid voxelgrid;
+        double skip_until = -std::numeric_limits<double>::infinity();
+        std::vector<double> warm;
+        bool appended = false;
+        if (rank == 0) {
+            if (cfg.resume && file_exists(cfg.output_file)) {
+                const StoredSolutions st = read_solution_file(cfg.output_file);
+                if (!st.time.empty()) {
+                    appended = true;
+                    skip_until = st.time.back();
+                    warm = st.last_solution;
+                }
+            }
+            writer = std::make_unique<SolutionWriter>(cfg.output_file, in.camera_names, in.nvoxel,
+                                                      (uint64_t)cfg.max_cached_solutions, appended);
+            voxelgrid.read(in.rtm_files.begin()->second, "rtm/voxel_map");
+            for (const auto& m : voxelgrid.warnings) std::cerr << "warning: " << m << std::endl;
+        }
+        host->broadcast_host(&skip_until, sizeof(skip_until), 0);
+        int has_warm = (!cfg.no_guess && !warm.empty()) ? 1 : 0;
+        host->broadcast_host(&has_warm, sizeof(has_warm), 0);
+        if (has_warm) {
+            warm.resize(in.nvoxel);
+            host->broadcast_host(warm.data(), warm.size() * sizeof(double), 0);
+        } else {
+            warm.clear();
+        }
+        std::ofstream profile;
+        if (rank == 0 && !cfg.profile_file.empty()) profile.open(cfg.profile_file);
+
+        std::vector<uint64_t> frames;
+        for (uint64_t i = 0; i < image.nframe(); ++i)
+            if (image.frame_time(i) > skip_until + 1e-12) frames.push_back(i);
+        std::vector<double> solution = warm, x(in.nvoxel);
+        std::future<std::vector<double>> fut;
+        if (!frames.empty()) fut = std::async(std::launch::async, [&image, i = frames[0]]() { return image.frame(i); });
+        for (size_t k = 0; k < frames.size(); ++k) {
+            const uint64_t cur = frames[k];
+            std::vector<double> frame = fut.get();
+            if (k + 1 < frames.size())  // prefetch the next composite frame during the solve
+                fut = std::async(std::launch::async, [&image, i = frames[k + 1]]() { return image.frame(i); });
+            const auto t0 = std::chrono::steady_clock::now();
+            const double* x0 = (cfg.no_guess || solution.empty()) ? nullptr : solution.data();
+            const SolveInfo info = gpu ? engine->solve(frame.data(), x0, x.data()) : cpu->solve(frame.data(), x0, x.data());
+            if (info.fallbacks)
+                std::cerr << "warning: fused sweep fell back " << info.fallbacks << " time(s)" << std::endl;
+            if (info.nonfinite) std::cerr << "warning: frame " << cur << ": non-finite iterate, stopped" << std::endl;
+            solution = x;
+            if (rank == 0) {
+                writer->add(x, info.status, image.frame_time(cur), image.camera_frame_time(cur), info.iterations);
+                const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                std::cout << "Processed in: " << ms << " ms" << std::endl;  // reference main.cpp:132-137
+                if (profile.is_open())
+                    profile << "{\"frame\": " << cur << ", \"time\": " << image.frame_time(cur)
+                            << ", \"status\": " << info.status << ", \"iterations\": " << info.iterations
+                            << ", \"ms\": " << ms << ", \"solve_ms\": " << info.ms
+                            << ", \"fused\": " << (info.used_fused ? "true" : "false")
+                            << ", \"driver\": \"" << json_escape("native") << "\"}\n";
+            }
+            if (cfg.no_guess) solution.clear();
+        }
+        if (rank == 0) {
+            writer->flush();
+            if (!appended) voxelgrid.write(cfg.output_file, "voxel_map");
+        }
+        host->barrier();
+    } catch (const std::exception& e) {
+        std::cerr << "rank " << rank << ": " << e.what() << std::endl;
+        if (dcomm) dcomm->abort();
+        else if (host) host->abort();
+        std::fflush(nullptr);
+        std::_Exit(1);
+    }
+    return 0;
+}

@@ -8,6 +8,7 @@ namespace sart {
 #ifdef SART_HAVE_HDF5
 
 void write_rtm_file(const RtmFileSpec& s) {
+    SART_H5_LOCK;
     H5Id f = h5_create_file(s.path);
     H5Id rtm = h5_create_group(f, "rtm");
     h5_write_attr_string(rtm, "camera_name", s.camera_name);
@@ -49,6 +50,7 @@ void write_rtm_file(const RtmFileSpec& s) {
 
 void write_image_file(const std::string& path, const std::string& camera_name, double wavelength,
                       const std::vector<double>& time, const std::vector<double>& frames, uint64_t h, uint64_t w) {
+    SART_H5_LOCK;
     if (frames.size() != time.size() * h * w) throw Error("write_image_file: frames have the wrong size");
     H5Id f = h5_create_file(path);
     H5Id g = h5_create_group(f, "image");
@@ -60,6 +62,7 @@ void write_image_file(const std::string& path, const std::string& camera_name, d
 
 void write_laplacian_file(const std::string& path, uint64_t nvoxel, const std::vector<uint64_t>& i,
                           const std::vector<uint64_t>& j, const std::vector<float>& value) {
+    SART_H5_LOCK;
     if (i.size() != value.size() || j.size() != value.size()) throw Error("write_laplacian_file: inconsistent arrays");
     H5Id f = h5_create_file(path);
     H5Id g = h5_create_group(f, "laplacian");
@@ -74,10 +77,12 @@ void write_laplacian_file(const std::string& path, uint64_t nvoxel, const std::v
 void write_rtm_file(const RtmFileSpec&) { throw Error("built without HDF5 support"); }
 void write_image_file(const std::string&, const std::string&, double, const std::vector<double>&,
                       const std::vector<double>&, uint64_t, uint64_t) {
+    SART_H5_LOCK;
     throw Error("built without HDF5 support");
 }
 void write_laplacian_file(const std::string&, uint64_t, const std::vector<uint64_t>&, const std::vector<uint64_t>&,
                           const std::vector<float>&) {
+    SART_H5_LOCK;
     throw Error("built without HDF5 support");
 }
 #endif

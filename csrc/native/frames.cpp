@@ -23,6 +23,7 @@ CompositeImage::CompositeImage(std::map<std::string, std::string> image_files,
                                uint64_t offset_pixel)
     : files_(std::move(image_files)), masks_(std::move(frame_masks)), npix_(npixel), offset_(offset_pixel) {
     if (npix_ == 0) throw Error("Argument npixel must be positive.");
+    SART_H5_LOCK;
     // timelines, cameras in name order (the map order of the mask dictionary)
     std::vector<std::vector<double>> timelines;
     for (const auto& [cam, mask] : masks_) {
@@ -119,6 +120,7 @@ void CompositeImage::build_frames(const std::vector<std::vector<std::pair<double
 }
 
 void CompositeImage::fill_cache(uint64_t first) {
+    SART_H5_LOCK;
     const uint64_t count = std::min<uint64_t>(max_cache_, time_.size() - first);
     cache_.assign(count * npix_, 0.0);
     uint64_t start = 0;  // first global pixel of the current camera
@@ -194,6 +196,7 @@ SolutionWriter::SolutionWriter(std::string filename, std::vector<std::string> ca
 }
 
 SolutionWriter::~SolutionWriter() {
+    SART_H5_LOCK;
     try {
         flush();
     } catch (...) {
@@ -240,6 +243,7 @@ void write_1d_at(hid_t ds, hid_t mtype, hsize_t offset, hsize_t n, const void* d
 }  // namespace
 
 void SolutionWriter::create() {
+    SART_H5_LOCK;
     H5Id f = h5_create_file(filename_);
     H5Id g = h5_create_group(f, "solution");
     const hsize_t n = times_.size();
@@ -260,6 +264,7 @@ void SolutionWriter::create() {
 }
 
 void SolutionWriter::append() {
+    SART_H5_LOCK;
     H5Id f = h5_open_file(filename_, true);
     H5Id tds = h5_open_dataset(f, "solution/time");
     const hsize_t off = h5_dims(tds)[0];
@@ -292,6 +297,7 @@ void SolutionWriter::append() {
 }
 
 void SolutionWriter::flush() {
+    SART_H5_LOCK;
     if (times_.empty()) return;
     if (first_) create();
     first_ = false;
@@ -304,6 +310,7 @@ void SolutionWriter::flush() {
 }
 
 StoredSolutions read_solution_file(const std::string& filename) {
+    SART_H5_LOCK;
     StoredSolutions out;
     h5_quiet();
     if (H5Fis_hdf5(filename.c_str()) <= 0) return out;
@@ -329,6 +336,7 @@ StoredSolutions read_solution_file(const std::string& filename) {
 // VoxelGrid
 // =============================================================================================
 int VoxelGrid::coordinate_system(const std::string& filename, const std::string& group) {
+    SART_H5_LOCK;
     H5Id f = h5_open_file(filename);
     if (!h5_attr_exists(f, group, "coordinate_system")) return kCartesian;
     std::string cs = h5_attr_string(f, group, "coordinate_system");
@@ -337,6 +345,7 @@ int VoxelGrid::coordinate_system(const std::string& filename, const std::string&
 }
 
 void VoxelGrid::read(const std::vector<std::string>& filenames, const std::string& group) {
+    SART_H5_LOCK;
     if (filenames.empty()) throw Error("VoxelGrid::read needs at least one file.");
     coordsys = coordinate_system(filenames.front(), group);
     {
@@ -386,6 +395,7 @@ void VoxelGrid::read(const std::vector<std::string>& filenames, const std::strin
 }
 
 void VoxelGrid::write(const std::string& filename, const std::string& group) const {
+    SART_H5_LOCK;
     H5Id f = h5_open_file(filename, true);
     H5Id g = h5_create_group(f, group);
     h5_write_attr_u64(g, "nx", nx);

@@ -4,6 +4,12 @@
 
 namespace sart {
 
+std::recursive_mutex& h5_mutex() {
+    static std::recursive_mutex m;
+    return m;
+}
+
+
 bool have_hdf5() {
 #ifdef SART_HAVE_HDF5
     return true;

@@ -6,6 +6,7 @@
 #pragma once
 
 #include <cstdint>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -19,6 +20,12 @@ namespace sart {
 struct Error : std::runtime_error {
     using std::runtime_error::runtime_error;
 };
+
+// The HDF5 library (the conda build is not thread-safe) may be entered by one thread at a time: every
+// public entry point of the native runtime that touches HDF5 holds this lock (the drivers read the next
+// frame on a helper thread while the solution writer may flush).
+std::recursive_mutex& h5_mutex();
+#define SART_H5_LOCK std::lock_guard<std::recursive_mutex> sart_h5_lock_(::sart::h5_mutex())
 
 #ifdef SART_HAVE_HDF5
 

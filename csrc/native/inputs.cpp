@@ -39,6 +39,7 @@ VoxelMapData read_voxel_map_indices(hid_t f) {
 
 void categorize_input_files(const std::vector<std::string>& input_files, std::vector<std::string>& rtm_files,
                             std::vector<std::string>& image_files) {
+    SART_H5_LOCK;
     for (const auto& path : input_files) {
         H5Id f = h5_open_file(path);
         if (h5_exists(f, "rtm"))
@@ -52,6 +53,7 @@ void categorize_input_files(const std::vector<std::string>& input_files, std::ve
 
 void check_group_attribute_consistency(const std::vector<std::string>& files, const std::string& group,
                                        const std::vector<std::string>& names, bool integer) {
+    SART_H5_LOCK;
     if (files.empty()) return;
     std::vector<double> ref_d(names.size());
     std::vector<uint64_t> ref_u(names.size());
@@ -88,6 +90,7 @@ void check_group_attribute_consistency(const std::vector<std::string>& files, co
 }
 
 SortedRtmFiles sort_rtm_files(const std::vector<std::string>& files) {
+    SART_H5_LOCK;
     std::map<std::string, std::map<uint64_t, std::string>> by_camera;
     for (const auto& path : files) {
         H5Id f = h5_open_file(path);
@@ -106,6 +109,7 @@ SortedRtmFiles sort_rtm_files(const std::vector<std::string>& files) {
 }
 
 void check_rtm_frame_consistency(const SortedRtmFiles& sorted) {
+    SART_H5_LOCK;
     for (const auto& [cam, files] : sorted) {
         if (files.size() < 2) continue;
         std::vector<int32_t> ref;
@@ -126,6 +130,7 @@ void check_rtm_frame_consistency(const SortedRtmFiles& sorted) {
 }
 
 void check_rtm_voxel_consistency(const SortedRtmFiles& sorted) {
+    SART_H5_LOCK;
     std::vector<int64_t> ref_map;
     std::string ref_cam;
     for (const auto& [cam, files] : sorted) {
@@ -165,6 +170,7 @@ void check_rtm_voxel_consistency(const SortedRtmFiles& sorted) {
 }
 
 std::map<std::string, std::vector<int32_t>> read_rtm_frame_masks(const SortedRtmFiles& sorted) {
+    SART_H5_LOCK;
     std::map<std::string, std::vector<int32_t>> out;
     for (const auto& [cam, files] : sorted) {
         H5Id f = h5_open_file(files.front());
@@ -174,6 +180,7 @@ std::map<std::string, std::vector<int32_t>> read_rtm_frame_masks(const SortedRtm
 }
 
 std::map<std::string, std::pair<uint64_t, uint64_t>> read_rtm_frame_shapes(const SortedRtmFiles& sorted) {
+    SART_H5_LOCK;
     std::map<std::string, std::pair<uint64_t, uint64_t>> out;
     for (const auto& [cam, files] : sorted) {
         H5Id f = h5_open_file(files.front());
@@ -186,6 +193,7 @@ std::map<std::string, std::pair<uint64_t, uint64_t>> read_rtm_frame_shapes(const
 }
 
 SortedImageFiles sort_image_files(const std::vector<std::string>& files) {
+    SART_H5_LOCK;
     SortedImageFiles out;
     for (const auto& path : files) {
         H5Id f = h5_open_file(path);
@@ -200,6 +208,7 @@ SortedImageFiles sort_image_files(const std::vector<std::string>& files) {
 
 void check_rtm_image_consistency(const SortedRtmFiles& rtm, const SortedImageFiles& images,
                                  const std::string& rtm_name, double wavelength_threshold) {
+    SART_H5_LOCK;
     for (const auto& kv : rtm)
         if (!images.count(kv.first)) throw Error("No image file for " + kv.first + " camera.");
     for (const auto& kv : images)
@@ -232,6 +241,7 @@ void check_rtm_image_consistency(const SortedRtmFiles& rtm, const SortedImageFil
 }
 
 std::pair<uint64_t, uint64_t> get_total_rtm_size(const SortedRtmFiles& sorted) {
+    SART_H5_LOCK;
     uint64_t npixel = 0, nvoxel = 0;
     for (const auto& [cam, files] : sorted) {
         H5Id f = h5_open_file(files.front());
@@ -246,6 +256,7 @@ std::pair<uint64_t, uint64_t> get_total_rtm_size(const SortedRtmFiles& sorted) {
 }
 
 bool rtm_has_sparse(const SortedRtmFiles& sorted, const std::string& rtm_name) {
+    SART_H5_LOCK;
     for (const auto& [cam, files] : sorted)
         for (const auto& path : files) {
             H5Id f = h5_open_file(path);
@@ -256,6 +267,7 @@ bool rtm_has_sparse(const SortedRtmFiles& sorted, const std::string& rtm_name) {
 
 void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, uint64_t nvoxel, uint64_t row_begin,
                    uint64_t row_end, float* out, uint64_t ld) {
+    SART_H5_LOCK;
     if (row_end <= row_begin) return;
     if (ld < nvoxel) throw Error("read_rtm_rows: ld < nvoxel");
     const std::string grp = "rtm/" + rtm_name;
@@ -310,6 +322,7 @@ void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, ui
 }
 
 LaplacianCOO read_laplacian(const std::string& path, uint64_t expected_nvoxel) {
+    SART_H5_LOCK;
     H5Id f = h5_open_file(path);
     LaplacianCOO L;
     L.nvoxel = h5_attr_u64(f, "laplacian", "nvoxel");
@@ -339,6 +352,32 @@ LaplacianCOO read_laplacian(const std::string& path, uint64_t expected_nvoxel) {
     return L;
 }
 
+InputSet validate_inputs(const std::vector<std::string>& input_files, const std::string& rtm_name,
+                         double wavelength_threshold) {
+    SART_H5_LOCK;
+    std::vector<std::string> rtm, img;
+    categorize_input_files(input_files, rtm, img);
+    if (rtm.empty()) throw Error("No RTM files given.");
+    if (img.empty()) throw Error("No image files given.");
+    check_group_attribute_consistency(rtm, "rtm/" + rtm_name, {"wavelength"}, false);
+    check_group_attribute_consistency(rtm, "rtm/voxel_map", {"nx", "ny", "nz"}, true);
+    InputSet in;
+    in.rtm_files = sort_rtm_files(rtm);
+    check_rtm_frame_consistency(in.rtm_files);
+    check_rtm_voxel_consistency(in.rtm_files);
+    check_group_attribute_consistency(img, "image", {"wavelength"}, false);
+    in.image_files = sort_image_files(img);
+    check_rtm_image_consistency(in.rtm_files, in.image_files, rtm_name, wavelength_threshold);
+    const auto sz = get_total_rtm_size(in.rtm_files);
+    in.npixel = sz.first;
+    in.nvoxel = sz.second;
+    in.frame_masks = read_rtm_frame_masks(in.rtm_files);
+    for (const auto& kv : in.image_files) in.camera_names.push_back(kv.first);
+    in.rtm_name = rtm_name;
+    in.has_sparse = rtm_has_sparse(in.rtm_files, rtm_name);
+    return in;
+}
+
 #else  // !SART_HAVE_HDF5
 
 [[noreturn]] static void nohdf5() { throw Error("built without HDF5 support"); }
@@ -355,6 +394,7 @@ std::pair<uint64_t, uint64_t> get_total_rtm_size(const SortedRtmFiles&) { nohdf5
 void read_rtm_rows(const SortedRtmFiles&, const std::string&, uint64_t, uint64_t, uint64_t, float*, uint64_t) { nohdf5(); }
 bool rtm_has_sparse(const SortedRtmFiles&, const std::string&) { nohdf5(); }
 LaplacianCOO read_laplacian(const std::string&, uint64_t) { nohdf5(); }
+InputSet validate_inputs(const std::vector<std::string>&, const std::string&, double) { nohdf5(); }
 
 #endif
 

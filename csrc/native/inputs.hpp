@@ -43,6 +43,20 @@ void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, ui
                    uint64_t row_end, float* out, uint64_t ld);
 bool rtm_has_sparse(const SortedRtmFiles& sorted, const std::string& rtm_name);
 
+// Everything the driver needs to know about the inputs, validated with the same checks in the same order
+// as the reference (main.cpp:27-59).
+struct InputSet {
+    SortedRtmFiles rtm_files;
+    SortedImageFiles image_files;
+    std::vector<std::string> camera_names;  // sorted by name: global pixel order
+    uint64_t npixel = 0, nvoxel = 0;
+    std::map<std::string, std::vector<int32_t>> frame_masks;
+    std::string rtm_name;
+    bool has_sparse = false;
+};
+InputSet validate_inputs(const std::vector<std::string>& input_files, const std::string& rtm_name,
+                         double wavelength_threshold);
+
 struct LaplacianCOO {
     uint64_t nvoxel = 0;
     std::vector<uint64_t> i, j;  // sorted by flat index i * nvoxel + j

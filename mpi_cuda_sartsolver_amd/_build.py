@@ -160,13 +160,54 @@ def build_native(verbose: bool = True) -> Path:
     return out
 
 
+def build_driver(verbose: bool = True) -> Path:
+    """Native ``sartsolver`` executable (csrc/driver): the GPU kernels and engine objects of build_hip,
+    the host runtime objects of build_native (g++/OpenMP) and the driver, linked with hipcc against
+    the HIP runtime, RCCL, HDF5 and libgomp. HDF5 is found through a private RUNPATH directory that
+    holds only libhdf5 (conda's libstdc++ must not shadow the system one)."""
+    if not hdf5_available():
+        raise RuntimeError("the native driver needs HDF5 (SART_HDF5_PREFIX)")
+    build_native(verbose)
+    build_hip(verbose)
+    hipcc = _hipcc()
+    objdir = BUILDDIR / "driver"
+    objdir.mkdir(parents=True, exist_ok=True)
+    headers = (sorted((CSRC / "kernels").glob("*.hpp")) + sorted((CSRC / "engine").glob("*.hpp")) +
+               sorted((CSRC / "native").glob("*.hpp")))
+    src = CSRC / "driver" / "sartsolver_main.cpp"
+    dflags = ["-O2", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__", "-DSART_HAVE_HDF5=1",
+              f"-isystem{HDF5_PREFIX / 'include'}", f"-I{ROCM / 'include'}"]
+    dobj = objdir / "sartsolver_main.o"
+    _compile_many([([hipcc, *dflags, "-c", str(src), "-o", str(dobj)], dobj, _digest([src, *headers], dflags))],
+                  verbose)
+    hip_objs = [o for o in sorted((BUILDDIR / "hip").glob("*.o")) if o.name != "hip_module.o"]
+    native_objs = [o for o in sorted((BUILDDIR / "native").glob("*.o"))
+                   if o.name not in ("native_module.o", "host_comm.o", "solver_params.o")]
+    objs = [dobj, *hip_objs, *native_objs]
+    libdir = LIBDIR / "hdf5"  # private RUNPATH entry: only libhdf5
+    libdir.mkdir(parents=True, exist_ok=True)
+    for so in HDF5_PREFIX.joinpath("lib").glob("libhdf5.so.*"):
+        if so.name.count(".") == 2:  # libhdf5.so.<soversion>
+            link = libdir / so.name
+            if not link.exists():
+                link.symlink_to(so)
+    out = LIBDIR / "sartsolver"
+    # libhdf5 by path, not -L: a -L/opt/conda/lib would also resolve libstdc++ to conda's older copy
+    _link([hipcc, f"--offload-arch={ARCH}", *map(str, objs), f"-L{ROCM / 'lib'}", "-lrccl",
+           str(HDF5_PREFIX / "lib" / "libhdf5.so"), "-lgomp", "-lpthread",
+           "-Wl,-rpath,$ORIGIN/hdf5", f"-Wl,-rpath,{ROCM / 'lib'}", "-o", str(out)], out, objs, verbose)
+    return out
+
+
 def build_all(verbose: bool = True) -> list[Path]:
     outs = [build_native(verbose)]
     outs.append(build_hip(verbose))
+    if hdf5_available():
+        outs.append(build_driver(verbose))
     return outs
 
 
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
-    {"hip": build_hip, "native": build_native, "all": build_all}[what]()
+    {"hip": build_hip, "native": build_native, "driver": build_driver, "all": build_all}[what]()
     print(json.dumps({"ok": True}))

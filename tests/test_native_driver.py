@@ -1,0 +1,154 @@
+"""The native ``sartsolver`` executable (csrc/driver/sartsolver_main.cpp) against the Python driver and the
+fp64 oracle: same CLI, same output file, multi-rank runs under torchrun --no-python."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from mpi_cuda_sartsolver_amd.io.fixtures import make_case
+from mpi_cuda_sartsolver_amd.ops import native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "mpi_cuda_sartsolver_amd", "_lib", "sartsolver")
+
+
+@pytest.fixture(scope="module")
+def binary():
+    from mpi_cuda_sartsolver_amd import _build
+
+    if not _build.hdf5_available():
+        pytest.skip("HDF5 not available")
+    _build.build_driver(verbose=False)
+    return BIN
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env():
+    return dict(os.environ, OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONPATH=ROOT)
+
+
+def _run_native(binary, args, nproc=1, cwd=None):
+    if nproc == 1:
+        cmd = [binary, *args]
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "--no-python", binary, *args]
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(), cwd=cwd)
+
+
+def _run_python(args, cwd=None):
+    cmd = [sys.executable, "-m", "mpi_cuda_sartsolver_amd", *args]
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(), cwd=cwd)
+
+
+def _case(tmp_path, **kw):
+    opts = dict(sparse_cameras=("cam_b",), laplacian=True, nframes=3, saturate=0.05)
+    opts.update(kw)
+    return make_case(str(tmp_path / "case"), **opts)
+
+
+@pytest.mark.parametrize("log", [False, True])
+def test_native_cpu_matches_python_driver(tmp_path, binary, log):
+    case = _case(tmp_path)
+    base = ["--use_cpu", "-m", "80", "-c", "1e-7", "-l", case.laplacian_file, "-b", "1e-3"] + (["-L"] if log else [])
+    r1 = _run_native(binary, base + ["-o", str(tmp_path / "n.h5"), *case.files])
+    assert r1.returncode == 0, r1.stdout + r1.stderr
+    assert r1.stdout.count("Processed in:") == 3
+    r2 = _run_python(base + ["-o", str(tmp_path / "p.h5"), *case.files])
+    assert r2.returncode == 0, r2.stdout + r2.stderr
+    n = native()
+    t1, x1, s1 = n.read_solution_file(str(tmp_path / "n.h5"))
+    t2, x2, s2 = n.read_solution_file(str(tmp_path / "p.h5"))
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_array_equal(s1, s2)
+    np.testing.assert_array_equal(x1, x2)  # same C++ solver, same thread count: bitwise
+
+
+def test_native_cpu_ranks_invariance_and_resume(tmp_path, binary):
+    case = _case(tmp_path, nframes=4, dt=0.1)
+    base = ["--use_cpu", "-m", "60", "-c", "1e-7", "-l", case.laplacian_file, "-b", "1e-3"]
+    one = str(tmp_path / "one.h5")
+    r = _run_native(binary, base + ["-o", one, *case.files])
+    assert r.returncode == 0, r.stderr
+    two = str(tmp_path / "two.h5")
+    r = _run_native(binary, base + ["-o", two, *case.files], nproc=2)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    n = native()
+    t1, x1, s1 = n.read_solution_file(one)
+    t2, x2, s2 = n.read_solution_file(two)
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_array_equal(s1, s2)
+    np.testing.assert_allclose(x2, x1, rtol=1e-8)
+    # resume: the first two frames, then the rest appended
+    part = str(tmp_path / "part.h5")
+    r = _run_native(binary, base + ["-t", "0:0.15", "-o", part, *case.files])
+    assert r.returncode == 0, r.stderr
+    r = _run_native(binary, base + ["--resume", "-o", part, *case.files])
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.count("Processed in:") == 2
+    t3, x3, _ = n.read_solution_file(part)
+    np.testing.assert_allclose(t3, t1, atol=1e-12)
+    np.testing.assert_allclose(x3, x1, rtol=1e-10)
+
+
+def test_native_cli_errors(tmp_path, binary):
+    case = _case(tmp_path, nframes=1)
+    r = _run_native(binary, ["--use_cpu", "-R", "3", *case.files])
+    assert r.returncode == 1 and "relaxation" in r.stderr
+    r = _run_native(binary, ["--use_cpu", "-t", "100:200", *case.files])
+    assert r.returncode == 1 and "No composite images" in r.stderr
+    r = _run_native(binary, ["--use_cpu", case.files[0]])
+    assert r.returncode == 1
+    r = _run_native(binary, ["--help"])
+    assert r.returncode == 0 and "Usage: sartsolver" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log", [False, True])
+def test_native_gpu_matches_python_driver(tmp_path, binary, log):
+    case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_b",), laplacian=True, nframes=3, saturate=0.05,
+                     nvoxel=2048, grid=(16, 16, 16), shapes=((24, 32), (20, 30)))
+    base = ["-m", "60", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3"] + (["-L"] if log else [])
+    r1 = _run_native(binary, base + ["-o", str(tmp_path / "n.h5"), *case.files])
+    assert r1.returncode == 0, r1.stdout + r1.stderr
+    r2 = _run_python(base + ["-o", str(tmp_path / "p.h5"), *case.files])
+    assert r2.returncode == 0, r2.stdout + r2.stderr
+    n = native()
+    t1, x1, s1 = n.read_solution_file(str(tmp_path / "n.h5"))
+    t2, x2, s2 = n.read_solution_file(str(tmp_path / "p.h5"))
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_array_equal(s1, s2)
+    np.testing.assert_array_equal(x1, x2)  # same engine and kernels: bitwise
+
+
+@pytest.mark.gpu
+def test_native_gpu_two_ranks_one_device(tmp_path, binary):
+    """Two ranks on the box's single GPU, staged (TCP) reductions: equals the one-rank run."""
+    case = make_case(str(tmp_path / "c"), laplacian=True, nframes=2, nvoxel=2048, grid=(16, 16, 16),
+                     shapes=((24, 32), (20, 30)))
+    base = ["-m", "40", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3", "--two_pass"]
+    r = _run_native(binary, base + ["-o", str(tmp_path / "one.h5"), *case.files])
+    assert r.returncode == 0, r.stderr
+    env_backend = os.environ.get("SART_DIST_BACKEND")
+    os.environ["SART_DIST_BACKEND"] = "tcp"
+    try:
+        r = _run_native(binary, base + ["-o", str(tmp_path / "two.h5"), *case.files], nproc=2)
+    finally:
+        if env_backend is None:
+            os.environ.pop("SART_DIST_BACKEND")
+        else:
+            os.environ["SART_DIST_BACKEND"] = env_backend
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    n = native()
+    _, x1, s1 = n.read_solution_file(str(tmp_path / "one.h5"))
+    _, x2, s2 = n.read_solution_file(str(tmp_path / "two.h5"))
+    np.testing.assert_array_equal(s1, s2)
+    assert np.linalg.norm(x2 - x1) / np.linalg.norm(x1) < 2e-3
