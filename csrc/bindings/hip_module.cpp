@@ -133,7 +133,8 @@ static void bind_engine(py::module_& m) {
         .def_readwrite("fused_variant", &sart::EngineConfig::fused_variant)
         .def_readwrite("rows_per_tile", &sart::EngineConfig::rows_per_tile)
         .def_readwrite("fused_schedule", &sart::EngineConfig::fused_schedule)
-        .def_readwrite("use_graph", &sart::EngineConfig::use_graph);
+        .def_readwrite("use_graph", &sart::EngineConfig::use_graph)
+        .def_readwrite("fault_inject", &sart::EngineConfig::fault_inject);
     m.def("validate_config", [](const sart::EngineConfig& c) {
         try {
             sart::validate_params(c);

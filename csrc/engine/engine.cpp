@@ -4,9 +4,12 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <stdexcept>
+
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "../kernels/launchers.hpp"
 
@@ -21,6 +24,9 @@ void hip_ok(hipError_t e, const char* what) {
 }
 
 }  // namespace
+
+RoctxRange::RoctxRange(const char* name) { roctxRangePushA(name); }
+RoctxRange::~RoctxRange() { roctxRangePop(); }
 
 template <typename T>
 void DeviceArray<T>::resize(size_t n) {
@@ -66,6 +72,8 @@ Engine::Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int
     hip_ok(hipGetDeviceProperties(&prop, device_), "hipGetDeviceProperties");
     num_cus_ = prop.multiProcessorCount;
     if (cfg_.fused_schedule >= 0) fused_set_schedule(cfg_.fused_schedule);
+    if (const char* fi = std::getenv("SART_FAULT_INJECT"); fi && *fi && cfg_.fault_inject == 0)
+        cfg_.fault_inject = std::atoi(fi);
 
     nsplit_ = backproject_num_splits(ld_, Pp_);
     comm_buf_.resize(ld_ + 64);  // [0, ld) correction, [ld] ||A x||^2
@@ -115,6 +123,7 @@ void Engine::alloc_fused() {
 }
 
 void Engine::ray_sums() {
+    RoctxRange r("sart::ray_sums");
     // rho_v = sum_p A[p, v] (fp64, all-reduced), l_p = sum_v A[p, v] (fp64, local): on the device
     // instead of the reference's host loops (sartsolver.cpp:38-56).
     ell64_.resize(Pp_);
@@ -163,6 +172,7 @@ void Engine::set_laplacian(const int64_t* row_ptr, const int32_t* col, const flo
 }
 
 double Engine::setup_frame(const double* g, const double* x0) {
+    RoctxRange r("sart::setup_frame");
     // normalisation by the global maximum and sum_{g > 0} g^2 (reference sartsolver_cuda.cpp:146-157);
     // the reference divides by zero when every pixel is <= 0, we keep norm = 1 then.
     double mx = -std::numeric_limits<double>::infinity(), gs = 0.0;
@@ -232,6 +242,7 @@ void Engine::sweep() {
 }
 
 void Engine::run_chunk(int n) {
+    RoctxRange r("sart::chunk");
     // Capture only after an eager chunk with the current kernels: launchers configure function attributes
     // (dynamic LDS above 64 KiB) on first use, which must not happen inside a capture.
     const bool graphable = cfg_.use_graph && !graph_failed_ && warm_ && comm_->graph_capturable() &&
@@ -264,6 +275,7 @@ void Engine::run_chunk(int n) {
 }
 
 bool Engine::fallback() {
+    RoctxRange r("sart::fallback");
     // A persistent sweep gave up waiting (SartState.error): XCD-local groups (variant 6) -> generic
     // groups (variant 3) -> two-pass kernels. The frame is re-solved from scratch.
     drop_graph();
@@ -285,6 +297,7 @@ bool Engine::fallback() {
 }
 
 SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
+    RoctxRange range("sart::solve");
     set_device();
     const auto t0 = std::chrono::steady_clock::now();
     SolveInfo info;
@@ -308,8 +321,12 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
             if (enqueued < max_sweeps) issue();  // keep the GPU busy while the previous chunk is checked
             const int slot = checked & 1;
             hip_ok(hipEventSynchronize(ev_[slot]), "event sync");
-            const SartState s = hstate_[slot];
+            SartState s = hstate_[slot];
             ++checked;
+            if (use_fused_ && injected_ < cfg_.fault_inject && checked == 1) {  // fault injection (tests)
+                ++injected_;
+                s.error = 1;
+            }
             if (s.error) {
                 error = true;
                 break;

@@ -33,6 +33,15 @@ struct EngineConfig : SolverParams {
     int rows_per_tile = 0;   // 0: default (fused_geometry)
     int fused_schedule = -1; // -1: keep the launcher's default
     bool use_graph = false;  // opt-in (SART_GRAPH=1): chunk capture is under validation
+    // Fault injection (tests; env SART_FAULT_INJECT=N): report a persistent-sweep protocol timeout in the
+    // first N solves, exercising the v6 -> v3 -> two-pass fallback chain end to end.
+    int fault_inject = 0;
+};
+
+// roctx range (rocprofv3 --marker-trace) for the lifetime of the object.
+struct RoctxRange {
+    explicit RoctxRange(const char* name);
+    ~RoctxRange();
 };
 
 template <typename T>
@@ -120,6 +129,7 @@ class Engine {
     hipGraphExec_t graph_ = nullptr;
     bool graph_failed_ = false;
     bool warm_ = false;  // an eager chunk ran with the current kernels
+    int injected_ = 0;
 };
 
 }  // namespace sart

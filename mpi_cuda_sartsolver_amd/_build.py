@@ -126,7 +126,7 @@ def build_hip(verbose: bool = True) -> Path:
     _compile_many(jobs, verbose)
     out = LIBDIR / ("_sart_hip" + _ext_suffix())
     _link([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), f"-L{ROCM / 'lib'}", "-lrccl",
-           "-o", str(out)], out, objs, verbose)
+           "-lrocprofiler-sdk-roctx", "-o", str(out)], out, objs, verbose)
     return out
 
 
@@ -194,7 +194,7 @@ def build_driver(verbose: bool = True) -> Path:
     out = LIBDIR / "sartsolver"
     # libhdf5 by path, not -L: a -L/opt/conda/lib would also resolve libstdc++ to conda's older copy
     _link([hipcc, f"--offload-arch={ARCH}", *map(str, objs), f"-L{ROCM / 'lib'}", "-lrccl",
-           str(HDF5_PREFIX / "lib" / "libhdf5.so"), "-lgomp", "-lpthread",
+           "-lrocprofiler-sdk-roctx", str(HDF5_PREFIX / "lib" / "libhdf5.so"), "-lgomp", "-lpthread",
            "-Wl,-rpath,$ORIGIN/hdf5", f"-Wl,-rpath,{ROCM / 'lib'}", "-o", str(out)], out, objs, verbose)
     return out
 

@@ -211,3 +211,30 @@ def test_engine_rccl_single_rank(dev):
         out.append((x, info))
     np.testing.assert_array_equal(out[0][0], out[1][0])
     assert out[0][1]["iterations"] == out[1][1]["iterations"]
+
+
+
+@pytest.mark.parametrize("faults,expect", [(1, 3), (2, None)])
+def test_fault_injection_fallback_chain(dev, faults, expect):
+    """Injected persistent-sweep timeouts walk the fallback chain v6 -> v3 -> two-pass; the frame is
+    re-solved each time and the answer is unchanged."""
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+    from mpi_cuda_sartsolver_amd.ops import hip
+    from mpi_cuda_sartsolver_amd.utils.synthetic import host_problem
+
+    k = hip()
+    A, g, _ = host_problem(2048, 16384, seed=4)
+    rtm = DenseRTM.from_dense(A, device=dev)
+    cfg = k.EngineConfig()
+    cfg.max_iterations, cfg.conv_tolerance, cfg.allow_zero_tolerance = 12, 0.0, True
+    cfg.fault_inject = faults
+    e = k.Engine(dev.index or 0, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld, k.local_comm(), cfg)
+    assert e.use_fused and e.geometry.variant == 6
+    x, info = e.solve(g, None)
+    assert info["fallbacks"] == faults
+    assert info["used_fused"] == (expect is not None)
+    if expect is not None:
+        assert info["fused_variant"] == expect
+    x_ref, _, _ = sart_gpu_semantics(A, g, max_iterations=12, conv_tolerance=0.0)
+    assert np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref) < 2e-3
