@@ -955,17 +955,17 @@ void fused_set_schedule(int sched) {
 int fused_get_schedule() { return g_fused_sched; }
 std::vector<int> fused_debug_map(int nblocks) {
     std::vector<int> out((size_t)nblocks);
-    hipMemcpyFromSymbol(out.data(), HIP_SYMBOL(g_fused_map), out.size() * sizeof(int), 0, hipMemcpyDeviceToHost);
+    hip_call(hipMemcpyFromSymbol(out.data(), HIP_SYMBOL(g_fused_map), out.size() * sizeof(int), 0, hipMemcpyDeviceToHost), "hipMemcpyFromSymbol");
     return out;
 }
 void fused_set_trace(unsigned long long* buf, long long tiles) {
-    hipMemcpyToSymbol(HIP_SYMBOL(g_fused_trace), &buf, sizeof(buf), 0, hipMemcpyHostToDevice);
-    hipMemcpyToSymbol(HIP_SYMBOL(g_fused_trace_tiles), &tiles, sizeof(tiles), 0, hipMemcpyHostToDevice);
+    hip_call(hipMemcpyToSymbol(HIP_SYMBOL(g_fused_trace), &buf, sizeof(buf), 0, hipMemcpyHostToDevice), "hipMemcpyToSymbol");
+    hip_call(hipMemcpyToSymbol(HIP_SYMBOL(g_fused_trace_tiles), &tiles, sizeof(tiles), 0, hipMemcpyHostToDevice), "hipMemcpyToSymbol");
 }
 std::vector<unsigned long long> fused_debug_stats(int nblocks) {
     std::vector<unsigned long long> out((size_t)nblocks * 8);
-    hipMemcpyFromSymbol(out.data(), HIP_SYMBOL(g_fused_stats), out.size() * sizeof(unsigned long long), 0,
-                        hipMemcpyDeviceToHost);
+    hip_call(hipMemcpyFromSymbol(out.data(), HIP_SYMBOL(g_fused_stats), out.size() * sizeof(unsigned long long), 0,
+                        hipMemcpyDeviceToHost), "hipMemcpyFromSymbol");
     return out;
 }
 
@@ -1004,10 +1004,10 @@ static void launch_lds(bool logmode, dim3 grid, hipStream_t stream, const float*
                        double* Fpart, uint64_t* gran, int I, int J, SartState* st) {
     static bool configured = false;
     if (!configured) {  // opt in to > 64 KiB of dynamic LDS once per instantiation
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_lds<K, true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsRingBytes);
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_lds<K, false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsRingBytes);
+        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_lds<K, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsRingBytes), "hipFuncSetAttribute");
+        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_lds<K, false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsRingBytes), "hipFuncSetAttribute");
         configured = true;
     }
     if (logmode)
@@ -1024,8 +1024,8 @@ static void launch_rows_t(dim3 grid, hipStream_t stream, const float* A, int64_t
                           uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
     static bool configured = false;
     if (!configured) {
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T, SC>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds_bytes(T, SC));
+        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T, SC>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds_bytes(T, SC)), "hipFuncSetAttribute");
         configured = true;
     }
     hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC>), grid, dim3(kFusedThreads), rows_lds_bytes(T, SC), stream, A, ld, nrows,
@@ -1074,10 +1074,10 @@ static void launch_rows2(bool logmode, dim3 grid, hipStream_t stream, const floa
                          double* Fpart, uint64_t* gran, int I, int J, SartState* st) {
     static bool configured = false;
     if (!configured) {
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows2<true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRows2LdsBytes);
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows2<false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRows2LdsBytes);
+        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows2<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRows2LdsBytes), "hipFuncSetAttribute");
+        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows2<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRows2LdsBytes), "hipFuncSetAttribute");
         configured = true;
     }
     if (logmode)

@@ -19,6 +19,10 @@
 
 namespace sart {
 
+void hip_call(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
 void check_launch(const char* what) {
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) {

@@ -66,5 +66,7 @@ __device__ __forceinline__ void fma4(float4& acc, const float4 a, const float s)
 
 // Launch-time error check used by every host launcher.
 void check_launch(const char* what);
+// Checked HIP runtime call (throws std::runtime_error with `what` and the HIP error string).
+void hip_call(hipError_t e, const char* what);
 
 }  // namespace sart
