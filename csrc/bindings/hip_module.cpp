@@ -17,6 +17,7 @@
 #include "../engine/comm.hpp"
 #include "../engine/engine.hpp"
 #include "../engine/geometry.hpp"
+#include "../engine/multiframe.hpp"
 #include "../kernels/launchers.hpp"
 
 namespace py = pybind11;
@@ -198,6 +199,40 @@ static void bind_engine(py::module_& m) {
         .def_property_readonly("stream", [](const sart::Engine& e) { return reinterpret_cast<uintptr_t>(e.stream()); })
         .def("ray_density", [](const sart::Engine& e) { auto v = e.ray_density(); return py::array_t<double>(v.size(), v.data()); })
         .def("ray_length", [](const sart::Engine& e) { auto v = e.ray_length(); return py::array_t<double>(v.size(), v.data()); })        ;
+
+    py::class_<sart::MultiFrameEngine>(m, "MultiFrameEngine")
+        .def(py::init([](int device, uintptr_t A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
+                         std::shared_ptr<sart::Communicator> comm, const sart::EngineConfig& cfg) {
+                 try {
+                     return new sart::MultiFrameEngine(device, P<const float>(A), nrows, nrows_pad, nvoxel, ld,
+                                                       comm.get(), cfg);
+                 } catch (const std::invalid_argument& e) {
+                     throw py::value_error(e.what());
+                 }
+             }),
+             py::keep_alive<1, 8>())
+        .def("set_laplacian",
+             [](sart::MultiFrameEngine& e, py::array_t<int64_t, py::array::c_style | py::array::forcecast> rp,
+                py::array_t<int32_t, py::array::c_style | py::array::forcecast> col,
+                py::array_t<float, py::array::c_style | py::array::forcecast> val) {
+                 e.set_laplacian(rp.data(), col.data(), val.data(), (int64_t)val.size());
+             })
+        .def("solve_batch", [](sart::MultiFrameEngine& e, f64arr g) {
+            if (g.ndim() != 2 || g.shape(1) != e.nrows())
+                throw py::value_error("measurements must be [nframes, nrows of the local shard]");
+            const int nf = (int)g.shape(0);
+            py::array_t<double> x({(py::ssize_t)nf, (py::ssize_t)e.nvoxel()});
+            double* xp = x.mutable_data();
+            const double* gp = g.data();
+            std::vector<sart::SolveInfo> infos;
+            {
+                py::gil_scoped_release rel;
+                infos = e.solve_batch(gp, nf, xp);
+            }
+            py::list li;
+            for (const auto& i : infos) li.append(solve_info(i));
+            return py::make_tuple(x, li);
+        });
 }
 
 PYBIND11_MODULE(_sart_hip, m) {

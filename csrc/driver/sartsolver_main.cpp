@@ -13,8 +13,8 @@
 //   * the next composite frame is read on a helper thread while the current one is solved.
 //   * a fatal error on any rank aborts the communicators instead of leaving peers blocked in a
 //     collective (the reference calls std::exit on one rank).
-// Extensions: --resume, --two_pass, --profile FILE (JSON lines per frame). --batch_frames (multi-frame
-// MFMA solver) is provided by the Python driver (python -m mpi_cuda_sartsolver_amd).
+// Extensions: --resume, --two_pass, --profile FILE (JSON lines per frame), --batch_frames N (N independent
+// frames solved together by the multi-frame MFMA engine, cold-started like --no_guess).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,6 +36,7 @@
 #include "../engine/comm.hpp"
 #include "../engine/engine.hpp"
 #include "../engine/geometry.hpp"
+#include "../engine/multiframe.hpp"
 #include "../native/config.hpp"
 #include "../native/cpu_solver.hpp"
 #include "../native/frames.hpp"
@@ -148,11 +149,6 @@ int main(int argc, char** argv) {
         std::cerr << e.what() << std::endl;
         return 1;
     }
-    if (cfg.batch_frames > 1) {
-        std::cerr << "--batch_frames is served by the multi-frame solver of the Python driver "
-                     "(python -m mpi_cuda_sartsolver_amd)" << std::endl;
-        return 1;
-    }
 
     const bool gpu = !cfg.use_cpu;
     const EnvWorld w = env_world();
@@ -223,8 +219,16 @@ int main(int argc, char** argv) {
         }
 
         std::unique_ptr<Engine> engine;
+        std::unique_ptr<MultiFrameEngine> mf;
         std::unique_ptr<CpuSolver> cpu;
-        if (gpu) {
+        const bool batched = gpu && cfg.batch_frames > 1;
+        if (batched) {
+            EngineConfig ec;
+            static_cast<SolverParams&>(ec) = params;
+            mf = std::make_unique<MultiFrameEngine>(device, dshard->A, dshard->nrows, dshard->nrows_pad,
+                                                    dshard->nvoxel, dshard->ld, dcomm.get(), ec);
+            if (lap.nnz()) mf->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
+        } else if (gpu) {
             EngineConfig ec;
             static_cast<SolverParams&>(ec) = params;
             ec.use_fused = !cfg.two_pass;
@@ -273,6 +277,44 @@ int main(int argc, char** argv) {
         std::vector<uint64_t> frames;
         for (uint64_t i = 0; i < image.nframe(); ++i)
             if (image.frame_time(i) > skip_until + 1e-12) frames.push_back(i);
+        if (batched) {
+            // --batch_frames N: independent frames solved together (cold start each, like --no_guess)
+            const size_t nb = (size_t)cfg.batch_frames;
+            auto read_chunk = [&image, &frames, nb, P = blk.size](size_t c0) {
+                std::vector<double> g;
+                for (size_t k = c0; k < std::min(frames.size(), c0 + nb); ++k) {
+                    const std::vector<double> f = image.frame(frames[k]);
+                    g.insert(g.end(), f.begin(), f.end());
+                }
+                (void)P;
+                return g;
+            };
+            std::future<std::vector<double>> next;
+            if (!frames.empty()) next = std::async(std::launch::async, read_chunk, (size_t)0);
+            for (size_t c0 = 0; c0 < frames.size(); c0 += nb) {
+                std::vector<double> g = next.get();
+                if (c0 + nb < frames.size()) next = std::async(std::launch::async, read_chunk, c0 + nb);
+                const int B = (int)std::min(nb, frames.size() - c0);
+                std::vector<double> xb((size_t)B * in.nvoxel);
+                const auto t0 = std::chrono::steady_clock::now();
+                const std::vector<SolveInfo> infos = mf->solve_batch(g.data(), B, xb.data());
+                const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                if (rank == 0) {
+                    for (int f = 0; f < B; ++f) {
+                        const uint64_t cur = frames[c0 + f];
+                        std::vector<double> xf(xb.begin() + (size_t)f * in.nvoxel, xb.begin() + (size_t)(f + 1) * in.nvoxel);
+                        writer->add(xf, infos[f].status, image.frame_time(cur), image.camera_frame_time(cur),
+                                    infos[f].iterations);
+                        std::cout << "Processed in: " << ms / B << " ms" << std::endl;
+                        if (profile.is_open())
+                            profile << "{\"frame\": " << cur << ", \"time\": " << image.frame_time(cur)
+                                    << ", \"status\": " << infos[f].status << ", \"iterations\": " << infos[f].iterations
+                                    << ", \"ms\": " << ms / B << ", \"batch\": " << B << ", \"driver\": \"native\"}\n";
+                    }
+                }
+            }
+            frames.clear();
+        }
         std::vector<double> solution = warm, x(in.nvoxel);
         std::future<std::vector<double>> fut;
         if (!frames.empty()) fut = std::async(std::launch::async, [&image, i = frames[0]]() { return image.frame(i); });

@@ -50,6 +50,7 @@ void DeviceArray<T>::release() {
 template class DeviceArray<float>;
 template class DeviceArray<double>;
 template class DeviceArray<SartState>;
+template class DeviceArray<MfState>;
 template class DeviceArray<uint64_t>;
 template class DeviceArray<unsigned>;
 template class DeviceArray<int64_t>;
@@ -80,8 +81,7 @@ Engine::Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int
     x_.resize(ld_);
     pen_.resize(ld_);
     if (cfg_.logarithmic) O_.resize(ld_);
-    for (auto* b : {&ghat_, &arow_, &gpos_, &wo_, &w_, &fitted_, &ray_len_}) b->resize(Pp_);
-    for (auto* b : {&dinv_, &dscale_, &dmask_}) b->resize(ld_);
+    for (auto* b : {&ghat_, &arow_, &gpos_, &wo_, &w_, &fitted_}) b->resize(Pp_);
     g64_.resize(Pp_);
     x064_.resize(std::max<int64_t>(V_, 1));
     st_.resize(1);
@@ -122,38 +122,52 @@ void Engine::alloc_fused() {
     if (use_fused_ && (int64_t)gran_.size() < Pp_ * geom_.J) gran_.resize(Pp_ * geom_.J);
 }
 
-void Engine::ray_sums() {
+void DeviceRaySums::compute(const float* A, int64_t P, int64_t Pp, int64_t V, int64_t ld, Communicator* comm,
+                            const SolverParams& p, hipStream_t stream) {
+    // rho_v = sum_p A[p, v] (fp64, all-reduced), l_p = sum_v A[p, v] (fp64, local): on the device instead of
+    // the reference's host loops (sartsolver.cpp:38-56); scales with the reference's fp32 semantics
     RoctxRange r("sart::ray_sums");
-    // rho_v = sum_p A[p, v] (fp64, all-reduced), l_p = sum_v A[p, v] (fp64, local): on the device
-    // instead of the reference's host loops (sartsolver.cpp:38-56).
-    ell64_.resize(Pp_);
-    rho64_.resize(ld_);
-    launch_rowsum_f64(A_, ld_, P_, ell64_.get(), stream_);
+    ell64.resize(Pp);
+    rho64.resize(ld);
+    ray_len.resize(Pp);
+    for (auto* b : {&dinv, &dscale, &dmask}) b->resize(ld);
+    launch_rowsum_f64(A, ld, P, ell64.get(), stream);
+    const int nsplit = backproject_num_splits(ld, Pp);
     {
-        DeviceArray<double> part((size_t)nsplit_ * ld_);
-        launch_colsum_f64(A_, ld_, P_, nsplit_, part.get(), stream_);
-        launch_reduce_partials_f64(part.get(), ld_, nsplit_, rho64_.get(), stream_);
-        hip_ok(hipStreamSynchronize(stream_), "ray sums");
+        DeviceArray<double> part((size_t)nsplit * ld);
+        launch_colsum_f64(A, ld, P, nsplit, part.get(), stream);
+        launch_reduce_partials_f64(part.get(), ld, nsplit, rho64.get(), stream);
+        hip_ok(hipStreamSynchronize(stream), "ray sums");
     }
-    comm_->all_reduce(rho64_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
-    launch_f64_to_f32(ell64_.get(), ray_len_.get(), Pp_, stream_);
-    launch_density_scales(rho64_.get(), V_, ld_, (float)cfg_.ray_density_threshold, (float)cfg_.relaxation,
-                          dinv_.get(), dscale_.get(), dmask_.get(), stream_);
-    hip_ok(hipStreamSynchronize(stream_), "ray sums");
+    comm->all_reduce(rho64.get(), (size_t)ld, ReduceOp::kSum, stream);
+    launch_f64_to_f32(ell64.get(), ray_len.get(), Pp, stream);
+    launch_density_scales(rho64.get(), V, ld, (float)p.ray_density_threshold, (float)p.relaxation, dinv.get(),
+                          dscale.get(), dmask.get(), stream);
+    hip_ok(hipStreamSynchronize(stream), "ray sums");
 }
+
+std::vector<double> DeviceRaySums::density(int64_t V) const {
+    std::vector<double> h(V);
+    if (V) hip_ok(hipMemcpy(h.data(), rho64.get(), V * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+    return h;
+}
+
+std::vector<double> DeviceRaySums::length(int64_t P) const {
+    std::vector<double> h(P);
+    if (P) hip_ok(hipMemcpy(h.data(), ell64.get(), P * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+    return h;
+}
+
+void Engine::ray_sums() { rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_); }
 
 std::vector<double> Engine::ray_density() const {
     set_device();
-    std::vector<double> h(V_);
-    hip_ok(hipMemcpy(h.data(), rho64_.get(), V_ * sizeof(double), hipMemcpyDeviceToHost), "D2H");
-    return h;
+    return rs_.density(V_);
 }
 
 std::vector<double> Engine::ray_length() const {
     set_device();
-    std::vector<double> h(P_);
-    if (P_) hip_ok(hipMemcpy(h.data(), ell64_.get(), P_ * sizeof(double), hipMemcpyDeviceToHost), "D2H");
-    return h;
+    return rs_.length(P_);
 }
 
 void Engine::set_laplacian(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t nnz) {
@@ -185,12 +199,12 @@ double Engine::setup_frame(const double* g, const double* x0) {
     double G = comm_->host().all_reduce_scalar(gs, ReduceOp::kSum) / (norm * norm);
     if (!(G > 0)) G = 1.0;
     if (P_) hip_ok(hipMemcpyAsync(g64_.get(), g, P_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D g");
-    launch_prep_rows(g64_.get(), P_, Pp_, 1.0 / norm, ray_len_.get(), (float)cfg_.ray_length_threshold, ghat_.get(),
+    launch_prep_rows(g64_.get(), P_, Pp_, 1.0 / norm, rs_.ray_len.get(), (float)cfg_.ray_length_threshold, ghat_.get(),
                      arow_.get(), gpos_.get(), wo_.get(), stream_);
     if (!x0) {
         // cold start x0 = [rho > tau] A^T max(ghat, 0) / rho (reference sart_kernels.cu:22-60)
         launch_backproject(A_, ld_, P_, gpos_.get(), nsplit_, partial_.get(), nullptr, stream_);
-        launch_reduce_partials(partial_.get(), ld_, nsplit_, dinv_.get(), comm_buf_.get(), nullptr, 0, nullptr,
+        launch_reduce_partials(partial_.get(), ld_, nsplit_, rs_.dinv.get(), comm_buf_.get(), nullptr, 0, nullptr,
                                nullptr, stream_);
         comm_->all_reduce(comm_buf_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
         launch_init_solution(x_.get(), V_, ld_, comm_buf_.get(), nullptr, 1.0, stream_);
@@ -201,7 +215,7 @@ double Engine::setup_frame(const double* g, const double* x0) {
     if (cfg_.logarithmic) {
         // frame-constant observed back-projection O = [rho > tau] A^T (a ghat), reduced once per frame
         launch_backproject(A_, ld_, P_, wo_.get(), nsplit_, partial_.get(), nullptr, stream_);
-        launch_reduce_partials(partial_.get(), ld_, nsplit_, dmask_.get(), O_.get(), nullptr, 0, nullptr, nullptr,
+        launch_reduce_partials(partial_.get(), ld_, nsplit_, rs_.dmask.get(), O_.get(), nullptr, 0, nullptr, nullptr,
                                stream_);
         comm_->all_reduce(O_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
     }
@@ -211,7 +225,7 @@ double Engine::setup_frame(const double* g, const double* x0) {
 
 void Engine::sweep() {
     SartState* st = st_.get();
-    const float* scale = cfg_.logarithmic ? dmask_.get() : dscale_.get();
+    const float* scale = cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get();
     float* Fslot = comm_buf_.get() + ld_;
     if (use_fused_) {
         if (geom_.variant == 6) hip_ok(hipMemsetAsync(xcnt_.get(), 0, 16 * sizeof(unsigned), stream_), "memset");

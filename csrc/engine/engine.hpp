@@ -62,6 +62,17 @@ class DeviceArray {
     size_t n_ = 0;
 };
 
+// Column / row sums of the shard and the per-voxel / per-pixel scales derived from them (device, fp64
+// accumulation, global column sums all-reduced): shared by the single- and multi-frame engines.
+struct DeviceRaySums {
+    void compute(const float* A, int64_t P, int64_t Pp, int64_t V, int64_t ld, Communicator* comm,
+                 const SolverParams& p, hipStream_t stream);
+    std::vector<double> density(int64_t V) const;  // host copies
+    std::vector<double> length(int64_t P) const;
+    DeviceArray<double> rho64, ell64;
+    DeviceArray<float> ray_len, dinv, dscale, dmask;
+};
+
 class Engine {
    public:
     // A: device pointer to the row-major fp32 shard [nrows_pad x ld], zero padded (not owned).
@@ -113,9 +124,9 @@ class Engine {
     int64_t nF_fused_ = 0;
     double norm_ = 1.0;
 
-    DeviceArray<float> partial_, comm_buf_, x_, pen_, O_, ghat_, arow_, gpos_, wo_, w_, fitted_, ray_len_, dinv_,
-        dscale_, dmask_;
-    DeviceArray<double> Fpart_, g64_, x064_, rho64_, ell64_;
+    DeviceArray<float> partial_, comm_buf_, x_, pen_, O_, ghat_, arow_, gpos_, wo_, w_, fitted_;
+    DeviceArray<double> Fpart_, g64_, x064_;
+    DeviceRaySums rs_;
     DeviceArray<SartState> st_;
     DeviceArray<uint64_t> gran_;
     DeviceArray<unsigned> xcnt_;

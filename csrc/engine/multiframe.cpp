@@ -1,0 +1,176 @@
+#include "multiframe.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <stdexcept>
+
+#include "../kernels/launchers.hpp"
+
+namespace sart {
+
+namespace {
+void hip_ok(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+constexpr int NF = kMfFrames;
+}  // namespace
+
+MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel,
+                                   int64_t ld, Communicator* comm, const EngineConfig& cfg)
+    : device_(device), A_(A), P_(nrows), Pp_(nrows_pad), V_(nvoxel), ld_(ld), comm_(comm), cfg_(cfg) {
+    validate_params(cfg_);
+    if (!comm_) throw std::invalid_argument("MultiFrameEngine: communicator required");
+    if (ld_ % 64 || ld_ < V_ || Pp_ % 64 || Pp_ < P_)
+        throw std::invalid_argument("MultiFrameEngine: ld and nrows_pad must be multiples of 64 covering the shard");
+    cfg_.check_interval = std::max(1, cfg_.check_interval);
+    set_device();
+    hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hstate_), sizeof(MfState)), "hipHostMalloc");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hg_), std::max<int64_t>(P_, 1) * NF * sizeof(double)),
+           "hipHostMalloc");
+    nsf_ = mf_forward_num_splits(ld_, Pp_);
+    nsb_ = mf_backproject_num_splits(ld_, P_);
+    nwb_ = mf_weights_num_blocks(Pp_);
+    X_.resize((size_t)NF * ld_);
+    Fs_.resize((size_t)nsf_ * Pp_ * NF);
+    W_.resize((size_t)Pp_ * NF);
+    part_.resize((size_t)nsb_ * ld_ * NF);
+    buf_.resize((size_t)NF * ld_ + NF);  // [16][ld] correction + [16] ||A x||^2: one all-reduce per sweep
+    pen_.resize((size_t)NF * ld_);
+    if (cfg_.logarithmic) O_.resize((size_t)NF * ld_);
+    for (auto* b : {&ghat_, &arow_, &gpos_, &wo_}) b->resize((size_t)Pp_ * NF);
+    g64_.resize((size_t)Pp_ * NF);
+    norm64_.resize(NF);
+    G64_.resize(NF);
+    F2part_.resize((size_t)nwb_ * NF);
+    st_.resize(1);
+    rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_);
+}
+
+MultiFrameEngine::~MultiFrameEngine() {
+    set_device();
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    if (hstate_) (void)hipHostFree(hstate_);
+    if (hg_) (void)hipHostFree(hg_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void MultiFrameEngine::set_device() const { hip_ok(hipSetDevice(device_), "hipSetDevice"); }
+
+void MultiFrameEngine::set_laplacian(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t nnz) {
+    set_device();
+    has_lap_ = false;
+    if (nnz <= 0 || cfg_.beta_laplace <= 0) return;
+    if (row_ptr[V_] != nnz) throw std::invalid_argument("Laplacian CSR row pointer does not match nnz");
+    lap_rp_.resize(V_ + 1);
+    lap_col_.resize(nnz);
+    lap_val_.resize(nnz);
+    hip_ok(hipMemcpy(lap_rp_.get(), row_ptr, (V_ + 1) * sizeof(int64_t), hipMemcpyHostToDevice), "H2D");
+    hip_ok(hipMemcpy(lap_col_.get(), col, nnz * sizeof(int32_t), hipMemcpyHostToDevice), "H2D");
+    hip_ok(hipMemcpy(lap_val_.get(), val, nnz * sizeof(float), hipMemcpyHostToDevice), "H2D");
+    has_lap_ = true;
+}
+
+void MultiFrameEngine::sweep() {
+    MfState* st = st_.get();
+    float* D = buf_.get();
+    float* F2 = buf_.get() + (int64_t)NF * ld_;
+    launch_mf_forward(A_, ld_, P_, Pp_, X_.get(), ld_, Fs_.get(), nsf_, stream_);
+    launch_mf_weights(Fs_.get(), nsf_, Pp_, ghat_.get(), arow_.get(), cfg_.logarithmic, W_.get(), F2part_.get(),
+                      stream_);
+    launch_mf_backproject(A_, ld_, P_, W_.get(), nsb_, part_.get(), stream_);
+    launch_mf_collect(part_.get(), nsb_, ld_, cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get(), D,
+                      F2part_.get(), nwb_, F2, stream_);
+    const float* pen = nullptr;
+    if (has_lap_) {
+        launch_mf_penalty(lap_rp_.get(), lap_col_.get(), lap_val_.get(), V_, (float)cfg_.beta_laplace,
+                          cfg_.logarithmic, X_.get(), ld_, pen_.get(), st, stream_);
+        pen = pen_.get();
+    }
+    if (comm_->size() > 1) comm_->all_reduce(buf_.get(), (size_t)NF * ld_ + NF, ReduceOp::kSum, stream_);
+    launch_mf_decide(st, F2, stream_);
+    launch_mf_update(X_.get(), D, O_.get(), pen, (float)cfg_.relaxation, cfg_.logarithmic, V_, ld_, st, stream_);
+}
+
+void MultiFrameEngine::solve16(const double* g, int B, double* x_out, SolveInfo* info) {
+    RoctxRange range("sart::solve16");
+    const auto t0 = std::chrono::steady_clock::now();
+    // host: layout [rows][16], per-frame maxima and sums of squares (reference sartsolver_cuda.cpp:146-157)
+    double mx[NF], gs[NF];
+    for (int f = 0; f < NF; ++f) mx[f] = -std::numeric_limits<double>::infinity(), gs[f] = 0.0;
+    for (int64_t p = 0; p < P_; ++p)
+        for (int f = 0; f < NF; ++f) {
+            const double v = f < B ? g[(int64_t)f * P_ + p] : 0.0;
+            hg_[p * NF + f] = v;
+            if (f < B) {
+                mx[f] = std::max(mx[f], v);
+                if (v > 0) gs[f] += v * v;
+            }
+        }
+    comm_->host().all_reduce_host(mx, NF, ReduceOp::kMax);
+    comm_->host().all_reduce_host(gs, NF, ReduceOp::kSum);
+    double norm[NF], G[NF];
+    for (int f = 0; f < NF; ++f) {
+        norm[f] = (f < B && mx[f] > 0) ? mx[f] : 1.0;
+        G[f] = gs[f] / (norm[f] * norm[f]);
+        if (!(G[f] > 0)) G[f] = 1.0;
+    }
+    if (P_) hip_ok(hipMemcpyAsync(g64_.get(), hg_, P_ * NF * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D g");
+    hip_ok(hipMemcpyAsync(norm64_.get(), norm, sizeof(norm), hipMemcpyHostToDevice, stream_), "H2D norm");
+    hip_ok(hipMemcpyAsync(G64_.get(), G, sizeof(G), hipMemcpyHostToDevice, stream_), "H2D G");
+    launch_mf_prep(g64_.get(), P_, Pp_, norm64_.get(), rs_.ray_len.get(), (float)cfg_.ray_length_threshold,
+                   ghat_.get(), arow_.get(), gpos_.get(), wo_.get(), stream_);
+    // cold start x0 = max([rho > tau] A^T max(ghat, 0) / rho, 1e-7) per frame (reference sart_kernels.cu:22-60)
+    launch_mf_backproject(A_, ld_, P_, gpos_.get(), nsb_, part_.get(), stream_);
+    launch_mf_collect(part_.get(), nsb_, ld_, nullptr, buf_.get(), nullptr, 0, nullptr, stream_);
+    comm_->all_reduce(buf_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
+    launch_mf_init(X_.get(), buf_.get(), rs_.dinv.get(), V_, ld_, B, stream_);
+    if (cfg_.logarithmic) {  // frame-constant observed back-projection, reduced once per batch
+        launch_mf_backproject(A_, ld_, P_, wo_.get(), nsb_, part_.get(), stream_);
+        launch_mf_collect(part_.get(), nsb_, ld_, rs_.dmask.get(), O_.get(), nullptr, 0, nullptr, stream_);
+        comm_->all_reduce(O_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
+    }
+    launch_mf_state_begin(st_.get(), G64_.get(), B, cfg_.conv_tolerance, cfg_.max_iterations, stream_);
+    const int max_sweeps = cfg_.max_iterations + 1;
+    for (int done_sweeps = 0; done_sweeps < max_sweeps;) {
+        const int n = std::min(cfg_.check_interval, max_sweeps - done_sweeps);
+        {
+            RoctxRange r("sart::mf_chunk");
+            for (int i = 0; i < n; ++i) sweep();
+        }
+        done_sweeps += n;
+        hip_ok(hipMemcpyAsync(hstate_, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
+        hip_ok(hipStreamSynchronize(stream_), "mf chunk");
+        if (hstate_->all_done) break;
+    }
+    std::vector<float> xh((size_t)NF * ld_);
+    hip_ok(hipMemcpyAsync(xh.data(), X_.get(), xh.size() * sizeof(float), hipMemcpyDeviceToHost, stream_), "D2H X");
+    hip_ok(hipMemcpyAsync(hstate_, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
+    hip_ok(hipStreamSynchronize(stream_), "mf solve");
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (int f = 0; f < B; ++f) {
+        for (int64_t v = 0; v < V_; ++v) x_out[(int64_t)f * V_ + v] = (double)xh[(size_t)f * ld_ + v] * norm[f];
+        info[f].status = hstate_->status[f] == kSuccess ? kSuccess : kMaxIterationsExceeded;
+        info[f].iterations = hstate_->iters[f];
+        info[f].convergence = hstate_->conv[f];
+        info[f].nonfinite = (hstate_->flags >> f) & 1;
+        info[f].used_fused = false;
+        info[f].ms = ms / B;
+    }
+}
+
+std::vector<SolveInfo> MultiFrameEngine::solve_batch(const double* g, int nframes, double* x_out) {
+    set_device();
+    std::vector<SolveInfo> out(std::max(nframes, 0));
+    for (int b0 = 0; b0 < nframes; b0 += NF) {
+        const int B = std::min(NF, nframes - b0);
+        solve16(g + (int64_t)b0 * P_, B, x_out + (int64_t)b0 * V_, out.data() + b0);
+    }
+    return out;
+}
+
+}  // namespace sart

@@ -1,0 +1,59 @@
+// Native multi-frame engine: up to 16 independent frames solved together on the fp32 matrix cores
+// (csrc/kernels/multiframe.hip, multiframe_glue.hip). The reference solves a time series strictly frame
+// by frame (reference main.cpp:131-140), streaming the RTM twice per iteration per frame; batching turns
+// A.x and A^T.w into skinny GEMMs (16 right-hand sides) that reuse every byte of A 16 times. Every frame
+// keeps its own normalisation, saturation mask, convergence history, status and iteration count; frames
+// that finish are frozen while the others continue. Batched frames are cold-started (like --no_guess).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "../kernels/sart_common.hpp"
+#include "../native/solver_params.hpp"
+#include "comm.hpp"
+#include "engine.hpp"
+
+namespace sart {
+
+class MultiFrameEngine {
+   public:
+    MultiFrameEngine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
+                     Communicator* comm, const EngineConfig& cfg);
+    ~MultiFrameEngine();
+    MultiFrameEngine(const MultiFrameEngine&) = delete;
+    MultiFrameEngine& operator=(const MultiFrameEngine&) = delete;
+
+    void set_laplacian(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t nnz);
+    // g: nframes x nrows (host fp64, frame-major); x_out: nframes x nvoxel. Solved 16 at a time.
+    std::vector<SolveInfo> solve_batch(const double* g, int nframes, double* x_out);
+    int64_t nrows() const { return P_; }
+    int64_t nvoxel() const { return V_; }
+
+   private:
+    void solve16(const double* g, int B, double* x_out, SolveInfo* info);
+    void sweep();
+    void set_device() const;
+
+    int device_;
+    const float* A_;
+    int64_t P_, Pp_, V_, ld_;
+    Communicator* comm_;
+    EngineConfig cfg_;
+    hipStream_t stream_ = nullptr;
+    int nsf_ = 1, nsb_ = 1, nwb_ = 1;
+    DeviceRaySums rs_;
+    DeviceArray<float> X_, Fs_, W_, part_, buf_, pen_, O_, ghat_, arow_, gpos_, wo_;
+    DeviceArray<double> g64_, norm64_, G64_, F2part_;
+    DeviceArray<MfState> st_;
+    DeviceArray<int64_t> lap_rp_;
+    DeviceArray<int32_t> lap_col_;
+    DeviceArray<float> lap_val_;
+    bool has_lap_ = false;
+    MfState* hstate_ = nullptr;  // pinned
+    double* hg_ = nullptr;       // pinned [rows][16] staging of a batch
+};
+
+}  // namespace sart

@@ -64,4 +64,20 @@ void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_
                        float* Fout, int nsplit, hipStream_t stream);
 void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,
                            hipStream_t stream);
+// multiframe_glue.hip
+void launch_mf_prep(const double* g, int64_t nrows, int64_t nrows_pad, const double* norm, const float* ray_length,
+                    float len_thres, float* ghat, float* arow, float* gpos, float* wo, hipStream_t stream);
+int mf_weights_num_blocks(int64_t nrows_pad);
+void launch_mf_weights(const float* Fs, int nsplit, int64_t nrows_pad, const float* ghat, const float* arow,
+                       bool logmode, float* W, double* F2part, hipStream_t stream);
+void launch_mf_collect(const float* part, int nsplit, int64_t ld, const float* scale, float* D, const double* F2part,
+                       int nF2, float* F2out, hipStream_t stream);
+void launch_mf_init(float* X, const float* D0, const float* dinv, int64_t nvox, int64_t ld, int nused,
+                    hipStream_t stream);
+void launch_mf_penalty(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta, bool logx,
+                       const float* X, int64_t ld, float* pen, const MfState* st, hipStream_t stream);
+void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream);
+void launch_mf_update(float* X, const float* D, const float* O, const float* pen, float alpha, bool logmode,
+                      int64_t nvox, int64_t ld, const MfState* st, hipStream_t stream);
+void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, int max_iter, hipStream_t stream);
 }  // namespace sart

@@ -41,6 +41,22 @@ static_assert(sizeof(SartState) == 128, "SartState must be 128 bytes");
 
 enum Status : int32_t { kSuccess = 0, kMaxIterationsExceeded = -1, kRunning = -2 };
 
+// Device-resident convergence state of a 16-frame batch (multi-frame solver): one column per frame.
+constexpr int kMfFrames = 16;
+struct alignas(16) MfState {
+    double G[kMfFrames];          // sum_{g>0} g^2 / s^2 per frame
+    double conv_prev[kMfFrames];
+    double conv[kMfFrames];       // last convergence metric per frame
+    int32_t done[kMfFrames];      // frame finished (converged, non-finite, or unused slot)
+    int32_t status[kMfFrames];
+    int32_t iters[kMfFrames];
+    int32_t sweep;
+    int32_t max_iter;
+    int32_t all_done;             // every frame done, or max_iter reached (no further update)
+    int32_t flags;                // bit f: frame f produced a non-finite ||A x||^2
+    double tol;
+};
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);

@@ -113,10 +113,11 @@ def test_native_cli_errors(tmp_path, binary):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("log", [False, True])
-def test_native_gpu_matches_python_driver(tmp_path, binary, log):
+@pytest.mark.parametrize("extra", [[], ["--batch_frames", "2", "--no_guess"]])
+def test_native_gpu_matches_python_driver(tmp_path, binary, log, extra):
     case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_b",), laplacian=True, nframes=3, saturate=0.05,
                      nvoxel=2048, grid=(16, 16, 16), shapes=((24, 32), (20, 30)))
-    base = ["-m", "60", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3"] + (["-L"] if log else [])
+    base = ["-m", "60", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3"] + (["-L"] if log else []) + extra
     r1 = _run_native(binary, base + ["-o", str(tmp_path / "n.h5"), *case.files])
     assert r1.returncode == 0, r1.stdout + r1.stderr
     r2 = _run_python(base + ["-o", str(tmp_path / "p.h5"), *case.files])
