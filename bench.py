@@ -36,6 +36,8 @@ def main() -> int:
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-fused", action="store_true", help="use the two-pass kernels instead of the fused sweep")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--frames", type=int, default=1,
+                    help="frames per step; > 1 solves them together with the multi-frame MFMA engine (16 per batch)")
     args = ap.parse_args()
 
     import torch
@@ -55,12 +57,36 @@ def main() -> int:
     blk = row_partition(npix_total, n, comm.rank)
     prob = make_problem(blk.size, args.nvox, row_offset=blk.offset, seed=args.seed, device=dev)
     params = SolverParams(max_iterations=args.iters, conv_tolerance=0.0)  # fixed iteration count
-    solver = SARTSolver(prob.rtm, None, comm, params, logarithmic=args.variant == "log",
-                        use_fused=not args.no_fused, check_interval=32, allow_zero_tolerance=True)
-    g = prob.measurement
+    if args.frames > 1:
+        import numpy as np
+
+        from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+
+        solver = MultiFrameSARTSolver(prob.rtm, None, comm, params, logarithmic=args.variant == "log",
+                                      batch=min(16, args.frames), check_interval=32, allow_zero_tolerance=True)
+        g1 = prob.measurement.cpu().numpy()
+        g = np.stack([g1 * (1.0 + 0.05 * f) for f in range(args.frames)])  # distinct frames of one problem
+
+        class _Batch:  # one step = all frames
+            def __init__(self, s):
+                self.s = s
+
+            def solve(self, gb):
+                rs = self.s.solve_batch(gb)
+                r = rs[-1]
+                r.iterations = sum(x.iterations for x in rs)
+                return r
+
+        runner = _Batch(solver)
+    else:
+        solver = SARTSolver(prob.rtm, None, comm, params, logarithmic=args.variant == "log",
+                            use_fused=not args.no_fused, check_interval=32, allow_zero_tolerance=True)
+        g = prob.measurement
+        runner = solver
+    multi = args.frames > 1
 
     for _ in range(args.warmup):
-        solver.solve(g)
+        runner.solve(g)
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
@@ -68,7 +94,7 @@ def main() -> int:
     iters = 0
     res = None
     for _ in range(args.steps):
-        res = solver.solve(g)
+        res = runner.solve(g)
         iters += res.iterations
     torch.cuda.synchronize()
     comm.barrier()
@@ -79,7 +105,9 @@ def main() -> int:
     iters_per_s = iters / elapsed
     flop_per_iter = 4.0 * npix_total * args.nvox
     gflops = flop_per_iter * iters_per_s / 1e9
-    bytes_per_iter = prob.rtm.nbytes * (1 if solver.use_fused else 2)
+    use_fused = (not multi) and solver.use_fused
+    # bytes of A per SART iteration of ONE frame: fused 1 read, two-pass 2 reads, multi-frame 2 reads per 16
+    bytes_per_iter = prob.rtm.nbytes * (2.0 / min(16, args.frames) if multi else (1 if use_fused else 2))
     out = {
         "metric": METRIC,
         "value": round(gflops, 2),
@@ -96,16 +124,17 @@ def main() -> int:
         "iters_per_s": round(iters_per_s, 3),
         "sart_iterations_per_step": args.iters,
         "status_last": res.status if res else None,
-        "fused_sweep": solver.use_fused,
-        "fused_variant": solver.geom.variant if solver.use_fused else None,
-        "fused_rows_per_tile": solver.geom.T if solver.use_fused else None,
-        "fused_schedule": solver.k.fused_get_schedule() if solver.use_fused else None,
+        "fused_sweep": use_fused,
+        "fused_variant": solver.geom.variant if use_fused else None,
+        "fused_rows_per_tile": solver.geom.T if use_fused else None,
+        "fused_schedule": solver.k.fused_get_schedule() if use_fused else None,
+        "frames_per_step": args.frames,
         "effective_hbm_TBps_per_gpu": round(bytes_per_iter * iters_per_s / 1e12, 3),
         "config": {
-            "model": f"SART-{args.variant} dense RTM",
+            "model": f"SART-{args.variant} dense RTM" + (" multi-frame (MFMA)" if multi else ""),
             "npixel_total": npix_total,
             "nvoxel": args.nvox,
-            "global_batch": 1,
+            "global_batch": args.frames,
             "seq_len": args.nvox,
             "parallelism": f"row-shard dp{n}" if n > 1 else "single",
             "rtm_GB_per_gpu": round(prob.rtm.nbytes / 1e9, 2),
