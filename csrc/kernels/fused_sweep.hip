@@ -447,13 +447,16 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
 //     1    4  4             LDS     1  3     (the newest tile stays in VGPRs one step before parking)
 //     2    4  4             LDS     2  2
 //     3    3  5             LDS     1  2
-// Schedule 2 is the default (profiles/probe_r1_sched.jsonl: 5-8 % faster than 0 at 64k x 64k, 2-3 %
-// at 16k-wide shapes). Compute waves storing their own granules (instead of the exchange wave) measured
-// 8-10 % slower than 2.
+//     4    4  4             LDS     2  2     + split exchange: a publisher wave stores, a gatherer wave polls
+// Schedule 4 is the default: 6 % faster than 2 at 64k x 64k and 4-5 % at 16k-wide shapes
+// (profiles/probe_r1_split_exchange.jsonl); the per-tile trace shows the publication delay of a granule
+// falling from 1.7 us to 0.16 us (profiles/fused_trace_r1_split_exchange.jsonl). Schedule 2 was 5-8 %
+// faster than 0 (profiles/probe_r1_sched.jsonl). Compute waves storing their own granules measured 8-10 %
+// slower than 2: their stores join the vmcnt queue of their streaming loads.
 // (LDS x slab: T >= 2 only.) Scalar-memory (s_load glc) polls were measured and are no faster under load:
 // an s_load round trip to L2 costs ~1.2 us while the chip streams.
 template <bool LOG, bool XL, bool DIAG, int T, int SCHED>
-__global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
+__global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
     const float* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
     const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
     double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg,
@@ -461,10 +464,12 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
     static_assert(T == 1 || T == 2 || T == 4, "rows per tile");
     constexpr int KW = 8;        // float4 per lane per row: one wave covers 2048 columns
     constexpr int WPR = 4 / T;   // compute waves per row (each on its own 2048-column sub-slab)
-    constexpr int D = (SCHED == 1 || SCHED == 2) ? 1 : 0;  // steps a reduced tile stays in VGPRs
+    constexpr int D = (SCHED == 1 || SCHED == 2 || SCHED == 4) ? 1 : 0;  // steps a reduced tile stays in VGPRs
     constexpr bool XS_LDS = SCHED >= 1;                       // x slab in LDS instead of VGPRs
     static_assert(!XS_LDS || T >= 2, "the LDS holds the x slab only for T >= 2");
-    constexpr int PD = SCHED == 2 ? 2 : 1;   // exchange step u polls tile u - PD
+    constexpr bool SPLIT = SCHED == 4;  // wave 4 publishes granules, wave 5 gathers (no shared vmcnt queue)
+    constexpr int NTHR = SPLIT ? kFusedThreads + 64 : kFusedThreads;
+    constexpr int PD = (SCHED == 2 || SCHED == 4) ? 2 : 1;   // exchange step u polls tile u - PD
     constexpr int PQ = SCHED == 1 ? 3 : 2;   // polls in flight (finishes tile u - PD - PQ + 1)
     constexpr int L = 3 + D;     // back-projection lag in steps
     static_assert(L >= PD + PQ, "the weights must be ready one step before they are used");
@@ -515,10 +520,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
     const int64_t ld4 = ld >> 2;
     if (DIAG && threadIdx.x == 0 && b < 1024) g_fused_map[b] = gi * 1024 + gj;
 
-    for (int i = threadIdx.x; i < NS * 4 + NS; i += kFusedThreads) s_pflag[i] = -1;
+    for (int i = threadIdx.x; i < NS * 4 + NS; i += NTHR) s_pflag[i] = -1;
     if constexpr (XS_LDS) {
         const float4* xsrc = reinterpret_cast<const float4*>(x) + (int64_t)gj * (64 * KW * WPR);
-        for (int i = threadIdx.x; i < WPR * KW * 64; i += kFusedThreads) s_xs[i] = xsrc[i];
+        for (int i = threadIdx.x; i < WPR * KW * 64; i += NTHR) s_xs[i] = xsrc[i];
     }
     __syncthreads();
 
@@ -633,6 +638,38 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
             }
             out[q * 64] = v;
         }
+    } else if (SPLIT && wave == 4) {
+        // Publisher wave (schedule 4): stores this workgroup's row partials as soon as the compute waves
+        // have reduced them. It issues no loads, so no poll ever waits behind a granule store's
+        // acknowledgement in the same wave's vmcnt queue (the coupling that delays publication when one
+        // exchange wave both stores and polls).
+        for (int64_t u = 0; u < nt; ++u) {
+            const int ps = (int)(u & (NS - 1));
+            if (lane < T) {
+                float sv = 0.f;
+#pragma unroll
+                for (int i = 0; i < WPR; ++i) {
+                    const int wv = lane * WPR + i;
+                    unsigned spins = 0;
+                    while (s_pflag[ps * 4 + wv] != (int)u) {
+                        if (++spins > kSpinLimit) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    asm volatile("" ::: "memory");
+                    sv += s_part[ps * 4 + wv];
+                }
+                if (!(dbg & 1)) {
+                    uint64_t* g = gran + ((t_begin + u) * J + gj) * T + lane;
+                    if constexpr (XL)
+                        __hip_atomic_store(g, make_granule(epoch, sv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    else
+                        __hip_atomic_store(g, make_granule(epoch, sv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (DIAG && lane == 0) trace_stamp(b, u, 2);
+            }
+        }
+        __syncthreads();  // matches the compute waves' first combine barrier
+        __syncthreads();  // and the second
     } else {
         const int n = J * T;
         bool failed = false;
@@ -712,7 +749,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
                         asm volatile("" ::: "memory");
                         sv += s_part[ps * 4 + wv];
                     }
-                    if (!(dbg & 1)) {
+                    if (!(dbg & 1) && !SPLIT) {
                         uint64_t* g = gran + ((t_begin + u) * J + gj) * T + lane;
                         if constexpr (XL)  // plain 8-byte store: the line stays in this XCD's L2
                             __hip_atomic_store(g, make_granule(epoch, sv), __ATOMIC_RELAXED,
@@ -720,7 +757,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_rows(
                         else
                             __hip_atomic_store(g, make_granule(epoch, sv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
-                    if (DIAG && lane == 0) trace_stamp(b, u, 2);
+                    if (DIAG && lane == 0 && !SPLIT) trace_stamp(b, u, 2);
                 }
             }
             if (u >= PD && u - PD < nt && !(dbg & 1)) issue_poll(pv[p], u - PD);
@@ -946,10 +983,10 @@ __global__ __launch_bounds__(kFused5Threads) void k_fused_sweep_rows2(
 constexpr size_t kRows2LdsBytes = 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (8 * 4 * 2 + 8) * sizeof(float);
 
 static int g_fused_dbg = 0;    // diagnostics only (set through fused_set_debug)
-static int g_fused_sched = 2;  // variant 6 pipeline schedule (k_fused_sweep_rows SCHED)
+static int g_fused_sched = 4;  // variant 6 pipeline schedule (k_fused_sweep_rows SCHED)
 void fused_set_debug(int flags) { g_fused_dbg = flags; }
 void fused_set_schedule(int sched) {
-    if (sched < 0 || sched > 3) throw std::runtime_error("fused_set_schedule: 0 .. 3");
+    if (sched < 0 || sched > 4) throw std::runtime_error("fused_set_schedule: 0 .. 4");
     g_fused_sched = sched;
 }
 int fused_get_schedule() { return g_fused_sched; }
@@ -1028,7 +1065,8 @@ static void launch_rows_t(dim3 grid, hipStream_t stream, const float* A, int64_t
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds_bytes(T, SC)), "hipFuncSetAttribute");
         configured = true;
     }
-    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC>), grid, dim3(kFusedThreads), rows_lds_bytes(T, SC), stream, A, ld, nrows,
+    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC>), grid, dim3(SC == 4 ? kFusedThreads + 64 : kFusedThreads),
+                       rows_lds_bytes(T, SC), stream, A, ld, nrows,
                        nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt);
 }
 
@@ -1040,7 +1078,7 @@ static void launch_rows(bool logmode, bool xl, dim3 grid, hipStream_t stream, co
     // g_fused_sched: pipeline schedule of variant 6 (k_fused_sweep_rows SCHED); schedules 1-3 hold the x
     // slab in LDS, which has room for it only when T >= 2. Instrumented builds: schedules 0 and 2.
     int sched = xl && T >= 2 ? g_fused_sched : 0;
-    if (diag && sched != 2) sched = 0;
+    if (diag && sched != 2 && sched != 4) sched = 0;
     auto go = [&](auto lg, auto x, auto d, auto sc) {
         launch_rows_t<decltype(lg)::value, decltype(x)::value, decltype(d)::value, T, decltype(sc)::value>(
             grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
@@ -1051,6 +1089,7 @@ static void launch_rows(bool logmode, bool xl, dim3 grid, hipStream_t stream, co
     using S1 = std::integral_constant<int, (T >= 2 ? 1 : 0)>;
     using S2 = std::integral_constant<int, (T >= 2 ? 2 : 0)>;
     using S3 = std::integral_constant<int, (T >= 2 ? 3 : 0)>;
+    using S4 = std::integral_constant<int, (T >= 2 ? 4 : 0)>;
 
     auto by_log = [&](auto x, auto d, auto sc) {
         if (logmode) go(TT{}, x, d, sc); else go(FF{}, x, d, sc);
@@ -1058,12 +1097,15 @@ static void launch_rows(bool logmode, bool xl, dim3 grid, hipStream_t stream, co
     if (!xl) {
         if (diag) by_log(FF{}, TT{}, S0{}); else by_log(FF{}, FF{}, S0{});
     } else if (diag) {
-        if (sched == 2) by_log(TT{}, TT{}, S2{}); else by_log(TT{}, TT{}, S0{});
+        if (sched == 2) by_log(TT{}, TT{}, S2{});
+        else if (sched == 4) by_log(TT{}, TT{}, S4{});
+        else by_log(TT{}, TT{}, S0{});
     } else {
         switch (sched) {
             case 1: by_log(TT{}, FF{}, S1{}); break;
             case 2: by_log(TT{}, FF{}, S2{}); break;
             case 3: by_log(TT{}, FF{}, S3{}); break;
+            case 4: by_log(TT{}, FF{}, S4{}); break;
             default: by_log(TT{}, FF{}, S0{}); break;
         }
     }

@@ -156,7 +156,7 @@ def test_fused_rows_per_tile(dev, variant, T, log):
     assert _rel(r.solution, x_ref) < 2e-3
 
 
-@pytest.mark.parametrize("T,sched", [(4, 0), (4, 1), (4, 2), (4, 3), (2, 1), (2, 2), (1, 0)])
+@pytest.mark.parametrize("T,sched", [(4, 0), (4, 1), (4, 2), (4, 3), (4, 4), (2, 1), (2, 2), (2, 4), (1, 0)])
 @pytest.mark.parametrize("log", [False, True])
 def test_fused_v6_schedules(dev, T, sched, log):
     """Variant 6 pipeline schedules (lag 3 / 4, 4-5 tiles in flight, x slab in VGPRs or LDS, 2-3 polls in

@@ -42,7 +42,7 @@ def main():
     arow = torch.rand(m.nrows_pad, device=dev) * 1e-4
     st = new_state(dev)
     xcnt = torch.zeros(16, dtype=torch.int32, device=dev)
-    for T, sched in ((4, 0), (4, 2)):
+    for T, sched in ((4, 2), (4, 4)):
         g = fused_geometry(m.ld, ncu, 6, T)
         L = 3 if sched in (0, 3) else 4
         ntile = m.nrows_pad // g.T
@@ -70,7 +70,7 @@ def main():
             times.append(a.elapsed_time(b))
         k.fused_set_trace(0, 0)
         k.fused_set_debug(0)
-        k.fused_set_schedule(2)
+        k.fused_set_schedule(4)
         err = read_state(st).error
         ev = tr.view(g.grid, nt, 4).cpu().numpy().astype(np.float64) / 100.0  # -> microseconds
         t0 = ev[:, 0, 0].min()

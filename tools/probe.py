@@ -88,7 +88,7 @@ def main():
         emit(kind="kernel", op="backproject", P=P, V=V, nsplit=ns, ms=med, GBps=nbytes / med / 1e6,
              best_GBps=nbytes / best / 1e6)
 
-        cfgs = [(6, 4, 2), (6, 4, 0), (6, 4, 3), (6, 1, 0), (3, None, 0)]
+        cfgs = [(6, 4, 4), (6, 4, 2), (6, 4, 0), (3, None, 0)]
         for variant, T, sched in cfgs:
             g = fused_geometry(m.ld, int(info["multiProcessorCount"]), variant, T)
             if g is None or g.variant != variant or (T is not None and g.T != T):
@@ -99,7 +99,7 @@ def main():
                 part = torch.zeros(g.I * m.ld, device=dev)
 
             def fused():
-                k.fused_set_schedule(sched if sched is not None else 2)
+                k.fused_set_schedule(sched if sched is not None else 4)
                 xcnt.zero_()
                 k.state_begin(st.data_ptr(), 1.0, 0.0, 100, s)
                 k.decide(st.data_ptr(), Fp.data_ptr(), s)  # sweep 0 -> epoch+1, not done
@@ -118,7 +118,7 @@ def main():
             med, best = timeit(fused)
             k.fused_set_debug(0)
             emit(kind="kernel", op=f"{tag}_noexchange", P=P, V=V, ms=med, GBps=nbytes / med / 1e6)
-            k.fused_set_schedule(2)
+            k.fused_set_schedule(4)
             del gran
 
         if os.environ.get("PROBE_FUSED_ONLY"):
