@@ -23,6 +23,31 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 METRIC = "SART iterations/sec (whole node) on dense RTM; GFLOPS at 1/2/4/8 MI355X"
 
+# BASELINE.json configs as weak-scaling presets (rows per GPU): at N = 8 GPUs "512kx256k" is the
+# 524288 x 262144 RTM (68.7 GB per GPU) and "2tb" is 1966080 x 262144 fp32 = 2.06 TB (258 GB per GPU)
+# with the Laplacian and a 16-frame batch; "256k" fills one GPU with a 262144 x 262144 shard (275 GB).
+PRESETS = {
+    "64k": dict(npix=65536, nvox=65536, iters=100),
+    "256k": dict(npix=262144, nvox=262144, iters=20),
+    "512kx256k": dict(npix=65536, nvox=262144, iters=100),
+    "2tb": dict(npix=245760, nvox=262144, iters=20, frames=16, laplacian=True),
+}
+
+
+def grid_dims(n: int) -> tuple[int, int, int]:
+    """nx * ny * nz == n with the factors as close to a cube as possible (synthetic voxel grid)."""
+    best = (n, 1, 1)
+    for nx in range(1, int(round(n ** (1 / 3))) + 2):
+        if n % nx:
+            continue
+        m = n // nx
+        for ny in range(nx, int(m ** 0.5) + 1):
+            if m % ny == 0:
+                cand = tuple(sorted((nx, ny, m // ny), reverse=True))
+                if max(cand) < max(best):
+                    best = cand
+    return best
+
 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
@@ -38,7 +63,14 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--frames", type=int, default=1,
                     help="frames per step; > 1 solves them together with the multi-frame MFMA engine (16 per batch)")
+    ap.add_argument("--laplacian", action="store_true",
+                    help="add the 7-point grid Laplacian regulariser (beta 1e-2, the reference default)")
+    ap.add_argument("--config", choices=sorted(PRESETS), default=None,
+                    help="BASELINE.json configuration preset (sets npix / nvox / iters / frames / laplacian)")
     args = ap.parse_args()
+    if args.config:
+        for k, v in PRESETS[args.config].items():
+            setattr(args, k, v)
 
     import torch
 
@@ -57,12 +89,17 @@ def main() -> int:
     blk = row_partition(npix_total, n, comm.rank)
     prob = make_problem(blk.size, args.nvox, row_offset=blk.offset, seed=args.seed, device=dev)
     params = SolverParams(max_iterations=args.iters, conv_tolerance=0.0)  # fixed iteration count
+    lap = None
+    if args.laplacian:
+        from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+
+        lap = LaplacianCSR.grid_3d(*grid_dims(args.nvox))
     if args.frames > 1:
         import numpy as np
 
         from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
 
-        solver = MultiFrameSARTSolver(prob.rtm, None, comm, params, logarithmic=args.variant == "log",
+        solver = MultiFrameSARTSolver(prob.rtm, lap, comm, params, logarithmic=args.variant == "log",
                                       batch=min(16, args.frames), check_interval=32, allow_zero_tolerance=True)
         g1 = prob.measurement.cpu().numpy()
         g = np.stack([g1 * (1.0 + 0.05 * f) for f in range(args.frames)])  # distinct frames of one problem
@@ -79,7 +116,7 @@ def main() -> int:
 
         runner = _Batch(solver)
     else:
-        solver = SARTSolver(prob.rtm, None, comm, params, logarithmic=args.variant == "log",
+        solver = SARTSolver(prob.rtm, lap, comm, params, logarithmic=args.variant == "log",
                             use_fused=not args.no_fused, check_interval=32, allow_zero_tolerance=True)
         g = prob.measurement
         runner = solver
@@ -131,7 +168,9 @@ def main() -> int:
         "frames_per_step": args.frames,
         "effective_hbm_TBps_per_gpu": round(bytes_per_iter * iters_per_s / 1e12, 3),
         "config": {
-            "model": f"SART-{args.variant} dense RTM" + (" multi-frame (MFMA)" if multi else ""),
+            "model": f"SART-{args.variant} dense RTM" + (" + Laplacian" if lap is not None else "")
+                     + (" multi-frame (MFMA)" if multi else ""),
+            "preset": args.config,
             "npixel_total": npix_total,
             "nvoxel": args.nvox,
             "global_batch": args.frames,

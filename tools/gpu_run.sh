@@ -30,6 +30,10 @@ for step in "$@"; do
     bench) run bench 600 python bench.py --steps 5 --warmup 1 ;;
     bench2) run bench_twopass 600 python bench.py --steps 5 --warmup 1 --no-fused ;;
     benchlog) run bench_log 600 python bench.py --steps 5 --warmup 1 --variant log ;;
+    presets) run bench_512kx256k 600 python bench.py --config 512kx256k --steps 3 --warmup 1 &&
+             run bench_2tb 900 python bench.py --config 2tb --steps 2 --warmup 1 &&
+             run bench_256k 900 python bench.py --config 256k --steps 2 --warmup 1 ;;
+    benchlap) run bench_lap 600 python bench.py --steps 5 --warmup 1 --laplacian ;;
     probe) run probe 600 python tools/probe.py ;;
     trace) run fused_trace 600 python tools/fused_trace.py ;;
     probef) PROBE_FUSED_ONLY=1 run probe_fused 600 python tools/probe.py ;;
