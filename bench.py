@@ -62,7 +62,7 @@ def main() -> int:
     ap.add_argument("--no-fused", action="store_true", help="use the two-pass kernels instead of the fused sweep")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--frames", type=int, default=1,
-                    help="frames per step; > 1 solves them together with the multi-frame MFMA engine (16 per batch)")
+                    help="frames per step; > 1 solves them together with the multi-frame MFMA engine (up to 64 per batch)")
     ap.add_argument("--laplacian", action="store_true",
                     help="add the 7-point grid Laplacian regulariser (beta 1e-2, the reference default)")
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
@@ -100,7 +100,7 @@ def main() -> int:
         from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
 
         solver = MultiFrameSARTSolver(prob.rtm, lap, comm, params, logarithmic=args.variant == "log",
-                                      batch=min(16, args.frames), check_interval=32, allow_zero_tolerance=True)
+                                      batch=min(64, args.frames), check_interval=32, allow_zero_tolerance=True)
         g1 = prob.measurement.cpu().numpy()
         g = np.stack([g1 * (1.0 + 0.05 * f) for f in range(args.frames)])  # distinct frames of one problem
 
@@ -143,8 +143,8 @@ def main() -> int:
     flop_per_iter = 4.0 * npix_total * args.nvox
     gflops = flop_per_iter * iters_per_s / 1e9
     use_fused = (not multi) and solver.use_fused
-    # bytes of A per SART iteration of ONE frame: fused 1 read, two-pass 2 reads, multi-frame 2 reads per 16
-    bytes_per_iter = prob.rtm.nbytes * (2.0 / min(16, args.frames) if multi else (1 if use_fused else 2))
+    # bytes of A per SART iteration of ONE frame: fused 1 read, two-pass 2 reads, multi-frame 2 reads per batch
+    bytes_per_iter = prob.rtm.nbytes * (2.0 / min(64, args.frames) if multi else (1 if use_fused else 2))
     out = {
         "metric": METRIC,
         "value": round(gflops, 2),

@@ -131,6 +131,7 @@ static void bind_engine(py::module_& m) {
         .def_readwrite("allow_zero_tolerance", &sart::EngineConfig::allow_zero_tolerance)
         .def_readwrite("check_interval", &sart::EngineConfig::check_interval)
         .def_readwrite("use_fused", &sart::EngineConfig::use_fused)
+        .def_readwrite("mf_frames", &sart::EngineConfig::mf_frames)
         .def_readwrite("fused_variant", &sart::EngineConfig::fused_variant)
         .def_readwrite("rows_per_tile", &sart::EngineConfig::rows_per_tile)
         .def_readwrite("fused_schedule", &sart::EngineConfig::fused_schedule)
@@ -211,6 +212,7 @@ static void bind_engine(py::module_& m) {
                  }
              }),
              py::keep_alive<1, 8>())
+        .def_property_readonly("batch_frames", &sart::MultiFrameEngine::batch_frames)
         .def("set_laplacian",
              [](sart::MultiFrameEngine& e, py::array_t<int64_t, py::array::c_style | py::array::forcecast> rp,
                 py::array_t<int32_t, py::array::c_style | py::array::forcecast> col,
@@ -345,14 +347,17 @@ PYBIND11_MODULE(_sart_hip, m) {
     });
     m.def("mf_forward_num_splits", &sart::mf_forward_num_splits);
     m.def("mf_backproject_num_splits", &sart::mf_backproject_num_splits);
+    m.def("mf_set_depth", &sart::mf_set_depth);
     m.def("mf_forward", [](uintptr_t A, int64_t ld, int64_t nrows, int64_t nrows_pad, uintptr_t X, int64_t ldx,
-                           uintptr_t Fout, int nsplit, uintptr_t stream) {
+                           uintptr_t Fout, int nsplit, uintptr_t stream, int nf) {
         sart::launch_mf_forward(P<const float>(A), ld, nrows, nrows_pad, P<const float>(X), ldx, P<float>(Fout),
-                                nsplit, S(stream));
-    });
+                                nsplit, nf, S(stream));
+    }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("nrows_pad"), py::arg("X"), py::arg("ldx"),
+       py::arg("Fout"), py::arg("nsplit"), py::arg("stream"), py::arg("nf") = 16);
     m.def("mf_backproject", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t W, int nsplit, uintptr_t partial,
-                               uintptr_t stream) {
-        sart::launch_mf_backproject(P<const float>(A), ld, nrows, P<const float>(W), nsplit, P<float>(partial),
+                               uintptr_t stream, int nf) {
+        sart::launch_mf_backproject(P<const float>(A), ld, nrows, P<const float>(W), nsplit, P<float>(partial), nf,
                                     S(stream));
-    });
+    }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("W"), py::arg("nsplit"), py::arg("partial"),
+       py::arg("stream"), py::arg("nf") = 16);
 }

@@ -225,6 +225,7 @@ int main(int argc, char** argv) {
         if (batched) {
             EngineConfig ec;
             static_cast<SolverParams&>(ec) = params;
+            ec.mf_frames = cfg.batch_frames;  // batch width 16, 32 or 64 (rounded up, capped at 64)
             mf = std::make_unique<MultiFrameEngine>(device, dshard->A, dshard->nrows, dshard->nrows_pad,
                                                     dshard->nvoxel, dshard->ld, dcomm.get(), ec);
             if (lap.nnz()) mf->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());

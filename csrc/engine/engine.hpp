@@ -36,6 +36,8 @@ struct EngineConfig : SolverParams {
     // Fault injection (tests; env SART_FAULT_INJECT=N): report a persistent-sweep protocol timeout in the
     // first N solves, exercising the v6 -> v3 -> two-pass fallback chain end to end.
     int fault_inject = 0;
+    // Multi-frame engine: frames per batch (16, 32 or 64; MultiFrameEngine rounds other values up).
+    int mf_frames = 16;
 };
 
 // roctx range (rocprofv3 --marker-trace) for the lifetime of the object.

@@ -15,8 +15,9 @@ namespace {
 void hip_ok(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
-constexpr int NF = kMfFrames;
 }  // namespace
+
+int MultiFrameEngine::batch_width(int frames) { return frames <= 16 ? 16 : (frames <= 32 ? 32 : 64); }
 
 MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel,
                                    int64_t ld, Communicator* comm, const EngineConfig& cfg)
@@ -26,6 +27,8 @@ MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, in
     if (ld_ % 64 || ld_ < V_ || Pp_ % 64 || Pp_ < P_)
         throw std::invalid_argument("MultiFrameEngine: ld and nrows_pad must be multiples of 64 covering the shard");
     cfg_.check_interval = std::max(1, cfg_.check_interval);
+    nf_ = batch_width(cfg_.mf_frames);
+    const int NF = nf_;
     set_device();
     hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
     hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -39,7 +42,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, in
     Fs_.resize((size_t)nsf_ * Pp_ * NF);
     W_.resize((size_t)Pp_ * NF);
     part_.resize((size_t)nsb_ * ld_ * NF);
-    buf_.resize((size_t)NF * ld_ + NF);  // [16][ld] correction + [16] ||A x||^2: one all-reduce per sweep
+    buf_.resize((size_t)NF * ld_ + NF);  // [nf][ld] correction + [nf] ||A x||^2: one all-reduce per sweep
     pen_.resize((size_t)NF * ld_);
     if (cfg_.logarithmic) O_.resize((size_t)NF * ld_);
     for (auto* b : {&ghat_, &arow_, &gpos_, &wo_}) b->resize((size_t)Pp_ * NF);
@@ -76,31 +79,33 @@ void MultiFrameEngine::set_laplacian(const int64_t* row_ptr, const int32_t* col,
 }
 
 void MultiFrameEngine::sweep() {
+    const int NF = nf_;
     MfState* st = st_.get();
     float* D = buf_.get();
     float* F2 = buf_.get() + (int64_t)NF * ld_;
-    launch_mf_forward(A_, ld_, P_, Pp_, X_.get(), ld_, Fs_.get(), nsf_, stream_);
+    launch_mf_forward(A_, ld_, P_, Pp_, X_.get(), ld_, Fs_.get(), nsf_, NF, stream_);
     launch_mf_weights(Fs_.get(), nsf_, Pp_, ghat_.get(), arow_.get(), cfg_.logarithmic, W_.get(), F2part_.get(),
-                      stream_);
-    launch_mf_backproject(A_, ld_, P_, W_.get(), nsb_, part_.get(), stream_);
+                      NF, stream_);
+    launch_mf_backproject(A_, ld_, P_, W_.get(), nsb_, part_.get(), NF, stream_);
     launch_mf_collect(part_.get(), nsb_, ld_, cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get(), D,
-                      F2part_.get(), nwb_, F2, stream_);
+                      F2part_.get(), nwb_, F2, NF, stream_);
     const float* pen = nullptr;
     if (has_lap_) {
         launch_mf_penalty(lap_rp_.get(), lap_col_.get(), lap_val_.get(), V_, (float)cfg_.beta_laplace,
-                          cfg_.logarithmic, X_.get(), ld_, pen_.get(), st, stream_);
+                          cfg_.logarithmic, X_.get(), ld_, pen_.get(), st, NF, stream_);
         pen = pen_.get();
     }
     if (comm_->size() > 1) comm_->all_reduce(buf_.get(), (size_t)NF * ld_ + NF, ReduceOp::kSum, stream_);
     launch_mf_decide(st, F2, stream_);
-    launch_mf_update(X_.get(), D, O_.get(), pen, (float)cfg_.relaxation, cfg_.logarithmic, V_, ld_, st, stream_);
+    launch_mf_update(X_.get(), D, O_.get(), pen, (float)cfg_.relaxation, cfg_.logarithmic, V_, ld_, st, NF, stream_);
 }
 
-void MultiFrameEngine::solve16(const double* g, int B, double* x_out, SolveInfo* info) {
-    RoctxRange range("sart::solve16");
+void MultiFrameEngine::solve_group(const double* g, int B, double* x_out, SolveInfo* info) {
+    RoctxRange range("sart::mf_solve");
+    const int NF = nf_;
     const auto t0 = std::chrono::steady_clock::now();
-    // host: layout [rows][16], per-frame maxima and sums of squares (reference sartsolver_cuda.cpp:146-157)
-    double mx[NF], gs[NF];
+    // host: layout [rows][nf], per-frame maxima and sums of squares (reference sartsolver_cuda.cpp:146-157)
+    double mx[kMfMaxFrames], gs[kMfMaxFrames];
     for (int f = 0; f < NF; ++f) mx[f] = -std::numeric_limits<double>::infinity(), gs[f] = 0.0;
     for (int64_t p = 0; p < P_; ++p)
         for (int f = 0; f < NF; ++f) {
@@ -113,28 +118,28 @@ void MultiFrameEngine::solve16(const double* g, int B, double* x_out, SolveInfo*
         }
     comm_->host().all_reduce_host(mx, NF, ReduceOp::kMax);
     comm_->host().all_reduce_host(gs, NF, ReduceOp::kSum);
-    double norm[NF], G[NF];
+    double norm[kMfMaxFrames], G[kMfMaxFrames];
     for (int f = 0; f < NF; ++f) {
         norm[f] = (f < B && mx[f] > 0) ? mx[f] : 1.0;
         G[f] = gs[f] / (norm[f] * norm[f]);
         if (!(G[f] > 0)) G[f] = 1.0;
     }
     if (P_) hip_ok(hipMemcpyAsync(g64_.get(), hg_, P_ * NF * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D g");
-    hip_ok(hipMemcpyAsync(norm64_.get(), norm, sizeof(norm), hipMemcpyHostToDevice, stream_), "H2D norm");
-    hip_ok(hipMemcpyAsync(G64_.get(), G, sizeof(G), hipMemcpyHostToDevice, stream_), "H2D G");
+    hip_ok(hipMemcpyAsync(norm64_.get(), norm, NF * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D norm");
+    hip_ok(hipMemcpyAsync(G64_.get(), G, NF * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D G");
     launch_mf_prep(g64_.get(), P_, Pp_, norm64_.get(), rs_.ray_len.get(), (float)cfg_.ray_length_threshold,
-                   ghat_.get(), arow_.get(), gpos_.get(), wo_.get(), stream_);
+                   ghat_.get(), arow_.get(), gpos_.get(), wo_.get(), NF, stream_);
     // cold start x0 = max([rho > tau] A^T max(ghat, 0) / rho, 1e-7) per frame (reference sart_kernels.cu:22-60)
-    launch_mf_backproject(A_, ld_, P_, gpos_.get(), nsb_, part_.get(), stream_);
-    launch_mf_collect(part_.get(), nsb_, ld_, nullptr, buf_.get(), nullptr, 0, nullptr, stream_);
+    launch_mf_backproject(A_, ld_, P_, gpos_.get(), nsb_, part_.get(), NF, stream_);
+    launch_mf_collect(part_.get(), nsb_, ld_, nullptr, buf_.get(), nullptr, 0, nullptr, NF, stream_);
     comm_->all_reduce(buf_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
-    launch_mf_init(X_.get(), buf_.get(), rs_.dinv.get(), V_, ld_, B, stream_);
+    launch_mf_init(X_.get(), buf_.get(), rs_.dinv.get(), V_, ld_, B, NF, stream_);
     if (cfg_.logarithmic) {  // frame-constant observed back-projection, reduced once per batch
-        launch_mf_backproject(A_, ld_, P_, wo_.get(), nsb_, part_.get(), stream_);
-        launch_mf_collect(part_.get(), nsb_, ld_, rs_.dmask.get(), O_.get(), nullptr, 0, nullptr, stream_);
+        launch_mf_backproject(A_, ld_, P_, wo_.get(), nsb_, part_.get(), NF, stream_);
+        launch_mf_collect(part_.get(), nsb_, ld_, rs_.dmask.get(), O_.get(), nullptr, 0, nullptr, NF, stream_);
         comm_->all_reduce(O_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
     }
-    launch_mf_state_begin(st_.get(), G64_.get(), B, cfg_.conv_tolerance, cfg_.max_iterations, stream_);
+    launch_mf_state_begin(st_.get(), G64_.get(), B, cfg_.conv_tolerance, cfg_.max_iterations, NF, stream_);
     const int max_sweeps = cfg_.max_iterations + 1;
     for (int done_sweeps = 0; done_sweeps < max_sweeps;) {
         const int n = std::min(cfg_.check_interval, max_sweeps - done_sweeps);
@@ -166,9 +171,9 @@ void MultiFrameEngine::solve16(const double* g, int B, double* x_out, SolveInfo*
 std::vector<SolveInfo> MultiFrameEngine::solve_batch(const double* g, int nframes, double* x_out) {
     set_device();
     std::vector<SolveInfo> out(std::max(nframes, 0));
-    for (int b0 = 0; b0 < nframes; b0 += NF) {
-        const int B = std::min(NF, nframes - b0);
-        solve16(g + (int64_t)b0 * P_, B, x_out + (int64_t)b0 * V_, out.data() + b0);
+    for (int b0 = 0; b0 < nframes; b0 += nf_) {
+        const int B = std::min(nf_, nframes - b0);
+        solve_group(g + (int64_t)b0 * P_, B, x_out + (int64_t)b0 * V_, out.data() + b0);
     }
     return out;
 }

@@ -1,7 +1,7 @@
-// Native multi-frame engine: up to 16 independent frames solved together on the fp32 matrix cores
-// (csrc/kernels/multiframe.hip, multiframe_glue.hip). The reference solves a time series strictly frame
-// by frame (reference main.cpp:131-140), streaming the RTM twice per iteration per frame; batching turns
-// A.x and A^T.w into skinny GEMMs (16 right-hand sides) that reuse every byte of A 16 times. Every frame
+// Native multi-frame engine: up to nf = 16, 32 or 64 independent frames solved together on the fp32 matrix
+// cores (csrc/kernels/multiframe.hip, multiframe_glue.hip). The reference solves a time series strictly
+// frame by frame (reference main.cpp:131-140), streaming the RTM twice per iteration per frame; batching
+// turns A.x and A^T.w into skinny GEMMs (nf right-hand sides) that reuse every byte of A nf times. Every frame
 // keeps its own normalisation, saturation mask, convergence history, status and iteration count; frames
 // that finish are frozen while the others continue. Batched frames are cold-started (like --no_guess).
 #pragma once
@@ -27,13 +27,16 @@ class MultiFrameEngine {
     MultiFrameEngine& operator=(const MultiFrameEngine&) = delete;
 
     void set_laplacian(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t nnz);
-    // g: nframes x nrows (host fp64, frame-major); x_out: nframes x nvoxel. Solved 16 at a time.
+    // g: nframes x nrows (host fp64, frame-major); x_out: nframes x nvoxel. Solved batch_frames() at a time.
     std::vector<SolveInfo> solve_batch(const double* g, int nframes, double* x_out);
     int64_t nrows() const { return P_; }
     int64_t nvoxel() const { return V_; }
+    int batch_frames() const { return nf_; }
+    // 16, 32 or 64: the smallest batch width that holds `frames` (64 for anything larger)
+    static int batch_width(int frames);
 
    private:
-    void solve16(const double* g, int B, double* x_out, SolveInfo* info);
+    void solve_group(const double* g, int B, double* x_out, SolveInfo* info);
     void sweep();
     void set_device() const;
 
@@ -43,6 +46,7 @@ class MultiFrameEngine {
     Communicator* comm_;
     EngineConfig cfg_;
     hipStream_t stream_ = nullptr;
+    int nf_ = 16;
     int nsf_ = 1, nsb_ = 1, nwb_ = 1;
     DeviceRaySums rs_;
     DeviceArray<float> X_, Fs_, W_, part_, buf_, pen_, O_, ghat_, arow_, gpos_, wo_;
@@ -53,7 +57,7 @@ class MultiFrameEngine {
     DeviceArray<float> lap_val_;
     bool has_lap_ = false;
     MfState* hstate_ = nullptr;  // pinned
-    double* hg_ = nullptr;       // pinned [rows][16] staging of a batch
+    double* hg_ = nullptr;       // pinned [rows][nf] staging of a batch
 };
 
 }  // namespace sart

@@ -57,27 +57,29 @@ std::vector<unsigned long long> fused_debug_stats(int nblocks);
 void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                         const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                         uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream);
-// multiframe.hip
+// multiframe.hip (nf = frames per batch: 16, 32 or 64)
 int mf_forward_num_splits(int64_t ld, int64_t nrows_pad);
 int mf_backproject_num_splits(int64_t ld, int64_t nrows);
+void mf_set_depth(int d);  // 1..3: register-ring depth of the MFMA projections; 0: default
 void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ldx,
-                       float* Fout, int nsplit, hipStream_t stream);
+                       float* Fout, int nsplit, int nf, hipStream_t stream);
 void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,
-                           hipStream_t stream);
+                           int nf, hipStream_t stream);
 // multiframe_glue.hip
 void launch_mf_prep(const double* g, int64_t nrows, int64_t nrows_pad, const double* norm, const float* ray_length,
-                    float len_thres, float* ghat, float* arow, float* gpos, float* wo, hipStream_t stream);
+                    float len_thres, float* ghat, float* arow, float* gpos, float* wo, int nf, hipStream_t stream);
 int mf_weights_num_blocks(int64_t nrows_pad);
 void launch_mf_weights(const float* Fs, int nsplit, int64_t nrows_pad, const float* ghat, const float* arow,
-                       bool logmode, float* W, double* F2part, hipStream_t stream);
+                       bool logmode, float* W, double* F2part, int nf, hipStream_t stream);
 void launch_mf_collect(const float* part, int nsplit, int64_t ld, const float* scale, float* D, const double* F2part,
-                       int nF2, float* F2out, hipStream_t stream);
-void launch_mf_init(float* X, const float* D0, const float* dinv, int64_t nvox, int64_t ld, int nused,
+                       int nF2, float* F2out, int nf, hipStream_t stream);
+void launch_mf_init(float* X, const float* D0, const float* dinv, int64_t nvox, int64_t ld, int nused, int nf,
                     hipStream_t stream);
 void launch_mf_penalty(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta, bool logx,
-                       const float* X, int64_t ld, float* pen, const MfState* st, hipStream_t stream);
+                       const float* X, int64_t ld, float* pen, const MfState* st, int nf, hipStream_t stream);
 void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream);
 void launch_mf_update(float* X, const float* D, const float* O, const float* pen, float alpha, bool logmode,
-                      int64_t nvox, int64_t ld, const MfState* st, hipStream_t stream);
-void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, int max_iter, hipStream_t stream);
+                      int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream);
+void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, int max_iter, int nf,
+                           hipStream_t stream);
 }  // namespace sart

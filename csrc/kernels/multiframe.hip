@@ -1,39 +1,68 @@
 // Multi-frame (batched right-hand side) projections on the fp32 matrix cores of gfx950.
 //
 // The reference solves frames strictly one after another (reference main.cpp:131-140), streaming
-// the whole RTM twice per iteration per frame. Solving NF = 16 frames together turns A.x and A^T.w
-// into skinny GEMMs (A.X with X in R^{V x 16}, A^T.W with W in R^{P x 16}) that reuse every byte of
-// A 16 times. They run on v_mfma_f32_16x16x4_f32 (exact fp32, 1 fp32 VGPR per operand per lane).
+// the whole RTM twice per iteration per frame. Solving nf = 16, 32 or 64 frames together turns A.x and
+// A^T.w into skinny GEMMs (A.X with X in R^{V x nf}, A^T.W with W in R^{P x nf}) that reuse every byte
+// of A nf times. They run on v_mfma_f32_16x16x4_f32 (exact fp32, 1 fp32 VGPR per operand per lane), one
+// MFMA column group per 16 frames (NG = nf / 16 groups).
+//
+// Rate model (MI355X_MICROARCH.md: 64 fp32 MFMA flop/clk/SIMD, 155 TFLOPS): a column group costs 32 SIMD
+// cycles per 1 KiB wave-load of A, so the matrix cores consume A at ~19.6 TB/s with nf = 16, ~9.8 TB/s
+// with nf = 32 (both above the ~6 TB/s HBM stream: bandwidth-bound) and ~4.9 TB/s with nf = 64
+// (matrix-core-bound, but 4x the frames per byte). Measured per-kernel rates: tools/probe_mf.py.
 //
 // K-permutation trick: each lane loads ONE float4 of A (16 contiguous bytes); component c of that
 // float4 is the lane's operand of MFMA k-step c. Any bijection between k-steps and voxels (forward) /
 // voxels and output rows (back-projection) is legal as long as both operands and the epilogue agree,
 // so no LDS transpose is needed.
 //
+// Latency hiding: each wave keeps DEPTH steps of A (and X / W) loads in flight in a register ring of
+// DEPTH + 1 slots (step t issues the loads of step t + DEPTH into the slot step t - 1 consumed), so the
+// ~2-3 us HBM latency under load is covered by DEPTH steps of matrix-core work instead of one.
+//
 // MFMA 16x16x4 f32 fragment maps (cdna_hip_programming.md section 3):
 //   A operand: lane l holds A[i = l & 15][k = l >> 4]; B operand: B[k = l >> 4][j = l & 15];
 //   C/D: col = l & 15, row = (l >> 4) * 4 + reg.
 #include "sart_common.hpp"
 
+#include <cstdlib>
 #include <stdexcept>
+#include <string>
+#include <type_traits>
+#include <utility>
 
 namespace sart {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-constexpr int kNF = 16;  // frames per batch (the MFMA N dimension)
-
 __device__ __forceinline__ float comp(const float4& v, int c) {
     return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
 
-// F[row][f] = sum_v A[row][v] X[f][v]. X is frame-major [16][ldx] (ldx == ld), F is [rows][16].
-// One wave: 32 rows (two 16-row tiles sharing the X fragment) x 16 frames, K = all voxels.
+// NG contiguous floats (the column groups of one lane's B operand in the back-projection layout).
+template <int NG>
+__device__ __forceinline__ void load_groups(float (&dst)[NG], const float* __restrict__ p) {
+    if constexpr (NG == 4) {
+        const float4 v = *reinterpret_cast<const float4*>(p);
+        dst[0] = v.x, dst[1] = v.y, dst[2] = v.z, dst[3] = v.w;
+    } else if constexpr (NG == 2) {
+        const float2 v = *reinterpret_cast<const float2*>(p);
+        dst[0] = v.x, dst[1] = v.y;
+    } else {
+        dst[0] = *p;
+    }
+}
+
+// F[row][f] = sum_v A[row][v] X[f][v]. X is frame-major [nf][ldx] (ldx == ld), F is [rows][nf].
+// One wave: 32 rows (two 16-row tiles sharing each X fragment) x nf frames, K = the columns of its
+// split; every float4 of A feeds 4 * NG MFMAs (one per k-component and column group).
 // Split-K: blockIdx.y selects the column range [k0, k1) (multiples of 16 columns) and the kernel
-// writes Fout + blockIdx.y * nrows_pad * 16; the caller sums the splits.
+// writes Fout + blockIdx.y * nrows_pad * nf; the caller sums the splits.
+template <int NG, int DEPTH>
 __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A, int64_t ld, int64_t nrows,
                                                     int64_t nrows_pad, const float* __restrict__ X,
                                                     int64_t ldx, float* __restrict__ Fout, int64_t cols_per_split) {
+    constexpr int NF = 16 * NG;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * 32;
     if (row0 >= nrows_pad) return;  // wave-uniform
@@ -41,48 +70,91 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
     const int64_t ld4 = ld >> 2, ldx4 = ldx >> 2;
     const int64_t c0 = (int64_t)blockIdx.y * cols_per_split;
     const int64_t c1 = (c0 + cols_per_split < ld) ? c0 + cols_per_split : ld;
-    Fout += (int64_t)blockIdx.y * nrows_pad * kNF;
+    Fout += (int64_t)blockIdx.y * nrows_pad * NF;
     const float4* __restrict__ a0p = reinterpret_cast<const float4*>(A) + (row0 + r) * ld4 + g + c0 / 4;
     const float4* __restrict__ a1p = a0p + 16 * ld4;
     const float4* __restrict__ xp = reinterpret_cast<const float4*>(X) + (int64_t)r * ldx4 + g + c0 / 4;
+    const int64_t xg = 16 * ldx4;  // next column group of X
 
-    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
-    int64_t q = 0;
-    const int64_t nq = c1 > c0 ? (c1 - c0) / 4 : 0;  // float4 columns; 4 lane-groups x float4 = 16 voxels/step
-    for (; q + 8 <= nq; q += 8) {
-        const float4 a00 = a0p[q], a10 = a1p[q], x0 = xp[q];
-        const float4 a01 = a0p[q + 4], a11 = a1p[q + 4], x1 = xp[q + 4];
+    floatx4 acc[2][2][NG];  // [row tile][k half][column group]
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a00, c), comp(x0, c), acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a10, c), comp(x0, c), acc1, 0, 0, 0);
-            acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a01, c), comp(x1, c), acc2, 0, 0, 0);
-            acc3 = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a11, c), comp(x1, c), acc3, 0, 0, 0);
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < NG; ++j) acc[t][h][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int64_t nq = c1 > c0 ? (c1 - c0) / 4 : 0;  // float4 columns; 4 lane-groups x float4 = 16 voxels
+    const int64_t nst = nq / 8;                        // 8-float4 steps
+    if (nst > 0) {
+        constexpr int RS = DEPTH + 1;
+        float4 a[RS][2][2], x[RS][2][NG];
+        auto load = [&](int sl, int64_t t) {
+            const int64_t qq = t * 8;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                a[sl][0][h] = a0p[qq + 4 * h];
+                a[sl][1][h] = a1p[qq + 4 * h];
+#pragma unroll
+                for (int j = 0; j < NG; ++j) x[sl][h][j] = xp[j * xg + qq + 4 * h];
+            }
+        };
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d)
+            if (d < nst) load(d, d);
+        auto step = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            if (t >= nst) return;
+            if (t + DEPTH < nst) load((sl + DEPTH) % RS, t + DEPTH);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    acc[0][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a[sl][0][0], c), comp(x[sl][0][j], c), acc[0][0][j], 0, 0, 0);
+                    acc[1][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a[sl][1][0], c), comp(x[sl][0][j], c), acc[1][0][j], 0, 0, 0);
+                    acc[0][1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a[sl][0][1], c), comp(x[sl][1][j], c), acc[0][1][j], 0, 0, 0);
+                    acc[1][1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a[sl][1][1], c), comp(x[sl][1][j], c), acc[1][1][j], 0, 0, 0);
+                }
+        };
+        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+            }(std::make_integer_sequence<int, RS>{});
         }
     }
-    for (; q < nq; q += 4) {
-        const float4 a00 = a0p[q], a10 = a1p[q], x0 = xp[q];
+    for (int64_t q = nst * 8; q < nq; q += 4) {  // 4-float4 tail of a ragged split
+        const float4 a00 = a0p[q], a10 = a1p[q];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a00, c), comp(x0, c), acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a10, c), comp(x0, c), acc1, 0, 0, 0);
+        for (int j = 0; j < NG; ++j) {
+            const float4 x0 = xp[j * xg + q];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                acc[0][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a00, c), comp(x0, c), acc[0][0][j], 0, 0, 0);
+                acc[1][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a10, c), comp(x0, c), acc[1][0][j], 0, 0, 0);
+            }
         }
     }
-    // D: col = frame = lane & 15, row = (lane >> 4) * 4 + reg
+    // D: col = frame = 16 j + (lane & 15), row = (lane >> 4) * 4 + reg
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int64_t ra = row0 + g * 4 + i, rb = ra + 16;
-        if (ra < nrows) Fout[ra * kNF + r] = acc0[i] + acc2[i];
-        if (rb < nrows) Fout[rb * kNF + r] = acc1[i] + acc3[i];
-    }
+    for (int j = 0; j < NG; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t ra = row0 + g * 4 + i, rb = ra + 16;
+            if (ra < nrows) Fout[ra * NF + 16 * j + r] = acc[0][0][j][i] + acc[0][1][j][i];
+            if (rb < nrows) Fout[rb * NF + 16 * j + r] = acc[1][0][j][i] + acc[1][1][j][i];
+        }
 }
 
-// partial[s][v][f] = sum_{rows of split s} A[row][v] W[row][f]. W is [rows][16].
-// One wave: 64 voxels x 16 frames; a float4 of A (4 voxels of one row) feeds 4 MFMAs, one per output
-// tile c, whose voxel set is {v0 + 4 i + c : i = 0..15}.
+// partial[s][v][f] = sum_{rows of split s} A[row][v] W[row][f]. W is in the back-projection layout
+// [rows][16][NG] (frame f = 16 j + i at position i * NG + j, mf_bp_slot in multiframe_glue.hip), so a
+// lane's NG column-group operands are one contiguous vector load. partial is [splits][ld][nf] in natural
+// frame order. One wave: 64 voxels x nf frames; a float4 of A (4 voxels of one row) feeds 4 * NG MFMAs,
+// one per output tile c (voxel set {v0 + 4 i + c : i = 0..15}) and column group j.
+template <int NG, int DEPTH>
 __global__ __launch_bounds__(256) void k_mf_backproject(const float* __restrict__ A, int64_t ld, int64_t nrows,
                                                         const float* __restrict__ W, int64_t rows_per_split,
                                                         float* __restrict__ partial) {
+    constexpr int NF = 16 * NG;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t vb = (int64_t)blockIdx.x * 4 + wave;  // 64-voxel block
     if (vb * 64 >= ld) return;
@@ -93,65 +165,83 @@ __global__ __launch_bounds__(256) void k_mf_backproject(const float* __restrict_
     if (r_end > nrows) r_end = nrows;
 
     const float4* __restrict__ ap = reinterpret_cast<const float4*>(A) + vb * 16 + i16;
-    floatx4 acc[4];
+    const float* __restrict__ wp = W + i16 * NG;
+    floatx4 acc[4][NG];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int j = 0; j < NG; ++j) acc[c][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    int64_t r0 = r_begin;
-    for (; r0 + 16 <= r_end; r0 += 16) {
-        float4 av[4];
-        float wv[4];
+    const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 16 : 0;  // 16-row steps
+    if (nst > 0) {
+        constexpr int RS = DEPTH + 1;
+        float4 av[RS][4];
+        float wv[RS][4][NG];
+        auto load = [&](int sl, int64_t t) {
+            const int64_t rr = r_begin + t * 16;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            av[u] = ap[(r0 + 4 * u + g) * ld4];
-            wv[u] = W[(r0 + 4 * u + g) * kNF + i16];
+            for (int u = 0; u < 4; ++u) {
+                av[sl][u] = ap[(rr + 4 * u + g) * ld4];
+                load_groups<NG>(wv[sl][u], wp + (rr + 4 * u + g) * NF);
+            }
+        };
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d)
+            if (d < nst) load(d, d);
+        auto step = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            if (t >= nst) return;
+            if (t + DEPTH < nst) load((sl + DEPTH) % RS, t + DEPTH);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int j = 0; j < NG; ++j)
+                        acc[c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(av[sl][u], c), wv[sl][u][j], acc[c][j], 0, 0, 0);
+        };
+        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+            }(std::make_integer_sequence<int, RS>{});
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(av[u], c), wv[u], acc[c], 0, 0, 0);
     }
-    for (; r0 < r_end; r0 += 4) {
+    for (int64_t r0 = r_begin + nst * 16; r0 < r_end; r0 += 4) {  // ragged tail, 4 rows per MFMA
         const int64_t row = r0 + g;
         float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
-        float wv = 0.f;
+        float wv[NG];
+#pragma unroll
+        for (int j = 0; j < NG; ++j) wv[j] = 0.f;
         if (row < r_end) {
             av = ap[row * ld4];
-            wv = W[row * kNF + i16];
+            load_groups<NG>(wv, wp + row * NF);
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(av, c), wv, acc[c], 0, 0, 0);
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int j = 0; j < NG; ++j)
+                acc[c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(av, c), wv[j], acc[c][j], 0, 0, 0);
     }
-    float* out = partial + (int64_t)blockIdx.y * ld * kNF;
+    float* out = partial + (int64_t)blockIdx.y * ld * NF;
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t v = vb * 64 + 4 * (g * 4 + q) + c;
-            out[v * kNF + i16] = acc[c][q];
+#pragma unroll
+            for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[c][j][q];
         }
 }
 
+// Split-K of the forward projection: >= ~1024 workgroups, >= 1024 columns per split. (Splitting further
+// so that a split's X chunk stays L2-resident measured 0-9 % slower at nf = 16..64, 64k x 64k.)
 int mf_forward_num_splits(int64_t ld, int64_t nrows_pad) {
     const int64_t nblk = (nrows_pad + 127) / 128;
-    int64_t s = (1024 + nblk - 1) / nblk;  // >= ~1024 workgroups
-    const int64_t smax = ld / 1024;        // >= 1024 columns per split
+    int64_t s = (1024 + nblk - 1) / nblk;
+    const int64_t smax = ld / 1024;
     if (s > smax) s = smax;
     if (s < 1) s = 1;
     return (int)s;
-}
-
-void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ldx,
-                       float* Fout, int nsplit, hipStream_t stream) {
-    if (ld % 64 != 0 || ldx != ld) throw std::runtime_error("mf_forward: ld must be a multiple of 64 and ldx == ld");
-    if (nrows_pad % 32 != 0) throw std::runtime_error("mf_forward: padded rows must be a multiple of 32");
-    if (nsplit < 1) throw std::runtime_error("mf_forward: nsplit must be >= 1");
-    const int64_t nblk = (nrows_pad + 127) / 128;
-    const int64_t cps = ((ld + nsplit - 1) / nsplit + 15) / 16 * 16;
-    hipLaunchKernelGGL(k_mf_forward, dim3((unsigned)nblk, (unsigned)nsplit), dim3(256), 0, stream, A, ld, nrows,
-                       nrows_pad, X, ldx, Fout, cps);
-    check_launch("k_mf_forward");
 }
 
 int mf_backproject_num_splits(int64_t ld, int64_t nrows) {
@@ -163,13 +253,77 @@ int mf_backproject_num_splits(int64_t ld, int64_t nrows) {
     return (int)s;
 }
 
+static void check_nf(int nf, const char* what) {
+    if (nf != 16 && nf != 32 && nf != 64) throw std::runtime_error(std::string(what) + ": nf must be 16, 32 or 64");
+}
+
+// Register-ring depth (steps of loads in flight per wave). Defaults per kernel and batch width from
+// tools/probe_mf.py on 64k x 64k; SART_MF_DEPTH=1..3 or mf_set_depth() overrides them.
+static int g_mf_depth = -1;
+void mf_set_depth(int d) { g_mf_depth = d; }
+static int mf_depth(bool forward, int nf) {
+    if (g_mf_depth < 0) {
+        const char* e = std::getenv("SART_MF_DEPTH");
+        g_mf_depth = (e && *e) ? std::atoi(e) : 0;
+    }
+    if (g_mf_depth >= 1 && g_mf_depth <= 3) return g_mf_depth;
+    if (forward) return nf == 16 ? 2 : (nf == 32 ? 1 : 3);
+    return nf == 16 ? 2 : (nf == 32 ? 3 : 2);
+}
+
+template <int NG>
+static void fwd(dim3 grid, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
+                int64_t nrows_pad, const float* X, int64_t ldx, float* Fout, int64_t cps) {
+    if (depth == 1)
+        hipLaunchKernelGGL((k_mf_forward<NG, 1>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+    else if (depth == 3)
+        hipLaunchKernelGGL((k_mf_forward<NG, 3>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+    else
+        hipLaunchKernelGGL((k_mf_forward<NG, 2>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+}
+
+void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ldx,
+                       float* Fout, int nsplit, int nf, hipStream_t stream) {
+    if (ld % 64 != 0 || ldx != ld) throw std::runtime_error("mf_forward: ld must be a multiple of 64 and ldx == ld");
+    if (nrows_pad % 32 != 0) throw std::runtime_error("mf_forward: padded rows must be a multiple of 32");
+    if (nsplit < 1) throw std::runtime_error("mf_forward: nsplit must be >= 1");
+    check_nf(nf, "mf_forward");
+    const int64_t cps = ((ld + nsplit - 1) / nsplit + 15) / 16 * 16;
+    const dim3 grid((unsigned)((nrows_pad + 127) / 128), (unsigned)nsplit);
+    const int d = mf_depth(true, nf);
+    if (nf == 16)
+        fwd<1>(grid, d, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+    else if (nf == 32)
+        fwd<2>(grid, d, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+    else
+        fwd<4>(grid, d, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+    check_launch("k_mf_forward");
+}
+
+template <int NG>
+static void bwd(dim3 grid, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows, const float* W,
+                int64_t rps, float* partial) {
+    if (depth == 1)
+        hipLaunchKernelGGL((k_mf_backproject<NG, 1>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
+    else if (depth == 3)
+        hipLaunchKernelGGL((k_mf_backproject<NG, 3>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
+    else
+        hipLaunchKernelGGL((k_mf_backproject<NG, 2>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
+}
+
 void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,
-                           hipStream_t stream) {
+                           int nf, hipStream_t stream) {
     if (ld % 64 != 0) throw std::runtime_error("mf_backproject: ld must be a multiple of 64");
+    check_nf(nf, "mf_backproject");
     const int64_t rps = ((nrows + nsplit - 1) / nsplit + 15) / 16 * 16;
-    const int64_t nblk = (ld / 64 + 3) / 4;
-    hipLaunchKernelGGL(k_mf_backproject, dim3((unsigned)nblk, (unsigned)nsplit), dim3(256), 0, stream, A, ld, nrows,
-                       W, rps, partial);
+    const dim3 grid((unsigned)((ld / 64 + 3) / 4), (unsigned)nsplit);
+    const int d = mf_depth(false, nf);
+    if (nf == 16)
+        bwd<1>(grid, d, stream, A, ld, nrows, W, rps, partial);
+    else if (nf == 32)
+        bwd<2>(grid, d, stream, A, ld, nrows, W, rps, partial);
+    else
+        bwd<4>(grid, d, stream, A, ld, nrows, W, rps, partial);
     check_launch("k_mf_backproject");
 }
 

@@ -1,6 +1,6 @@
-// Element-wise and reduction kernels of the multi-frame solver (16 frames as the N = 16 columns of the
-// MFMA projections in multiframe.hip). Layouts: pixel-major [rows][16] for measurements, weights and
-// forward projections (the MFMA B/D fragments), frame-major [16][ld] for solutions and corrections (the
+// Element-wise and reduction kernels of the multi-frame solver (nf = 16, 32 or 64 frames as the N columns
+// of the MFMA projections in multiframe.hip). Layouts: pixel-major [rows][nf] for measurements, weights and
+// forward projections (the MFMA B/D fragments), frame-major [nf][ld] for solutions and corrections (the
 // MFMA A operand of the forward projection), so each frame's solution row is contiguous.
 //
 // Per-frame semantics are those of the single-frame solver (sart_update.hip) and the reference GPU path
@@ -10,20 +10,26 @@
 
 #include <math.h>
 #include <stdexcept>
+#include <string>
 
 namespace sart {
 
-constexpr int NF = kMfFrames;
+constexpr int kMaxNF = kMfMaxFrames;
 
-// ghat = fp32(g / s_f); a = [ghat >= 0][len > tau_l] / len; gpos = max(ghat, 0); wo = a * ghat
+// Position of frame f inside a row of a back-projection operand ([rows][16][nf / 16], multiframe.hip
+// k_mf_backproject): frame f = 16 j + i sits at i * (nf / 16) + j, so a lane's column groups are adjacent.
+__device__ __forceinline__ int mf_bp_slot(int f, int nf) { return (f & 15) * (nf >> 4) + (f >> 4); }
+
+// ghat = fp32(g / s_f); a = [ghat >= 0][len > tau_l] / len; gpos = max(ghat, 0); wo = a * ghat.
+// ghat and a are [rows][nf]; gpos and wo feed the back-projection and use its layout (mf_bp_slot).
 __global__ __launch_bounds__(256) void k_mf_prep(const double* __restrict__ g, int64_t nrows, int64_t nrows_pad,
                                                  const double* __restrict__ norm, const float* __restrict__ ray_length,
                                                  float len_thres, float* __restrict__ ghat, float* __restrict__ arow,
-                                                 float* __restrict__ gpos, float* __restrict__ wo) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // element of [rows_pad][16]
-    if (i >= nrows_pad * NF) return;
-    const int64_t row = i / NF;
-    const int f = (int)(i % NF);
+                                                 float* __restrict__ gpos, float* __restrict__ wo, int nf) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // element of [rows_pad][nf]
+    if (i >= nrows_pad * nf) return;
+    const int64_t row = i / nf;
+    const int f = (int)(i % nf);
     float gh = 0.f, a = 0.f;
     if (row < nrows) {
         gh = (float)(g[i] / norm[f]);
@@ -33,72 +39,77 @@ __global__ __launch_bounds__(256) void k_mf_prep(const double* __restrict__ g, i
     }
     ghat[i] = gh;
     arow[i] = a;
-    gpos[i] = gh > 0.f ? gh : 0.f;
-    wo[i] = a * gh;
+    const int64_t ib = row * nf + mf_bp_slot(f, nf);
+    gpos[ib] = gh > 0.f ? gh : 0.f;
+    wo[ib] = a * gh;
 }
 
-// F = sum_s Fsplit[s] (fixed order); W = a F (log) or a (ghat - F) (linear); per-block, per-frame partial
-// sums of F^2 in fp64 (deterministic: fixed thread-to-row assignment, fixed tree).
+// F = sum_s Fsplit[s] (fixed order); W = a F (log) or a (ghat - F) (linear), written in the
+// back-projection layout (mf_bp_slot); per-block, per-frame partial sums of F^2 in fp64 (deterministic:
+// fixed thread-to-row assignment, fixed tree).
 constexpr int kWRows = 256;  // rows per block
 __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs, int nsplit, int64_t nrows_pad,
                                                     const float* __restrict__ ghat, const float* __restrict__ arow,
-                                                    int logmode, float* __restrict__ W, double* __restrict__ F2part) {
+                                                    int logmode, float* __restrict__ W, double* __restrict__ F2part,
+                                                    int nf) {
     __shared__ double red[256];
-    const int f = threadIdx.x & 15, r16 = threadIdx.x >> 4;  // 16 rows x 16 frames per pass
+    const int f = threadIdx.x % nf, rsub = threadIdx.x / nf, rstep = 256 / nf;  // rstep rows x nf frames per pass
     const int64_t r0 = (int64_t)blockIdx.x * kWRows;
     double acc = 0.0;
-    for (int rr = r16; rr < kWRows; rr += 16) {
+    for (int rr = rsub; rr < kWRows; rr += rstep) {
         const int64_t row = r0 + rr;
         if (row >= nrows_pad) break;
-        const int64_t i = row * NF + f;
+        const int64_t i = row * nf + f;
         float F = 0.f;
-        for (int s = 0; s < nsplit; ++s) F += Fs[(int64_t)s * nrows_pad * NF + i];
-        W[i] = logmode ? arow[i] * F : arow[i] * (ghat[i] - F);
+        for (int s = 0; s < nsplit; ++s) F += Fs[(int64_t)s * nrows_pad * nf + i];
+        W[row * nf + mf_bp_slot(f, nf)] = logmode ? arow[i] * F : arow[i] * (ghat[i] - F);
         acc += (double)F * (double)F;
     }
     red[threadIdx.x] = acc;
     __syncthreads();
-    for (int off = 128; off >= 16; off >>= 1) {  // reduce over r16, keep the frame (low 4 bits)
+    for (int off = 128; off >= nf; off >>= 1) {  // reduce over the row index, keep the frame (tid % nf)
         if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
         __syncthreads();
     }
-    if (threadIdx.x < 16) F2part[(int64_t)blockIdx.x * NF + threadIdx.x] = red[threadIdx.x];
+    if (threadIdx.x < nf) F2part[(int64_t)blockIdx.x * nf + threadIdx.x] = red[threadIdx.x];
 }
 
 // D[f][v] = scale[v] * sum_s part[s][v][f] (transpose through LDS); block 0 also writes
 // F2out[f] = (float) sum_b F2part[b][f] when F2part is given.
 __global__ __launch_bounds__(256) void k_mf_collect(const float* __restrict__ part, int nsplit, int64_t ld,
                                                     const float* __restrict__ scale, float* __restrict__ D,
-                                                    const double* __restrict__ F2part, int nF2, float* __restrict__ F2out) {
-    __shared__ float tile[NF][64 + 1];
+                                                    const double* __restrict__ F2part, int nF2, float* __restrict__ F2out,
+                                                    int nf) {
+    __shared__ float tile[kMaxNF][64 + 1];
     const int64_t v0 = (int64_t)blockIdx.x * 64;
-    // load: thread t handles elements t, t+256, t+512, t+768 of the contiguous [64][16] block
-    for (int e = threadIdx.x; e < 64 * NF; e += 256) {
-        const int64_t v = v0 + e / NF;
-        const int f = e % NF;
+    // load: the contiguous [64][nf] block, 256 elements per pass
+    for (int e = threadIdx.x; e < 64 * nf; e += 256) {
+        const int64_t v = v0 + e / nf;
+        const int f = e % nf;
         float acc = 0.f;
         if (v < ld)
-            for (int s = 0; s < nsplit; ++s) acc += part[((int64_t)s * ld + v) * NF + f];
-        tile[f][e / NF] = (v < ld && scale) ? acc * scale[v] : acc;
+            for (int s = 0; s < nsplit; ++s) acc += part[((int64_t)s * ld + v) * nf + f];
+        tile[f][e / nf] = (v < ld && scale) ? acc * scale[v] : acc;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < 64 * NF; e += 256) {
+    for (int e = threadIdx.x; e < 64 * nf; e += 256) {
         const int f = e / 64, vv = e % 64;
         const int64_t v = v0 + vv;
         if (v < ld) D[(int64_t)f * ld + v] = tile[f][vv];
     }
-    if (F2part && blockIdx.x == 0 && threadIdx.x < NF) {
+    if (F2part && blockIdx.x == 0 && threadIdx.x < nf) {
         double s = 0.0;
-        for (int b = 0; b < nF2; ++b) s += F2part[(int64_t)b * NF + threadIdx.x];
+        for (int b = 0; b < nF2; ++b) s += F2part[(int64_t)b * nf + threadIdx.x];
         F2out[threadIdx.x] = (float)s;
     }
 }
 
 // X[f][v] = max(D0[f][v] * dinv[v], 1e-7) for real voxels of used frames, 0 elsewhere.
 __global__ __launch_bounds__(256) void k_mf_init(float* __restrict__ X, const float* __restrict__ D0,
-                                                 const float* __restrict__ dinv, int64_t nvox, int64_t ld, int nused) {
+                                                 const float* __restrict__ dinv, int64_t nvox, int64_t ld, int nused,
+                                                 int nf) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)NF * ld) return;
+    if (i >= (int64_t)nf * ld) return;
     const int f = (int)(i / ld);
     const int64_t v = i % ld;
     float x = 0.f;
@@ -115,10 +126,11 @@ __global__ __launch_bounds__(256) void k_mf_penalty(const int64_t* __restrict__ 
                                                     const float* __restrict__ X, int64_t ld, float* __restrict__ pen,
                                                     const MfState* __restrict__ st) {
     if (st->all_done) return;
+    const int nf = st->nf;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n * NF) return;
-    const int f = (int)(i % NF);
-    const int64_t r = i / NF;
+    if (i >= n * nf) return;
+    const int f = (int)(i % nf);
+    const int64_t r = i / nf;
     if (st->done[f]) return;
     const float* x = X + (int64_t)f * ld;
     float s = 0.f;  // same arithmetic as k_penalty_csr (sart_update.hip)
@@ -138,12 +150,12 @@ __global__ void k_mf_decide(MfState* __restrict__ st, const float* __restrict__ 
     const int s = st->sweep;
     if (f == 0) alld = 1;
     __syncthreads();
-    if (f < NF) {
+    if (f < st->nf) {
         const double F = (double)F2[f];
         int done = st->done[f];
         if (!isfinite(F)) {
             if (!done) {
-                atomicOr(&st->flags, 1 << f);
+                atomicOr(&st->flags, 1ull << f);
                 st->iters[f] = s;
                 done = 1;
             }
@@ -175,7 +187,7 @@ __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const 
                                                    const MfState* __restrict__ st) {
     if (st->all_done) return;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)NF * ld) return;
+    if (i >= (int64_t)st->nf * ld) return;
     const int f = (int)(i / ld);
     const int64_t v = i % ld;
     if (v >= nvox || st->done[f]) return;
@@ -192,10 +204,11 @@ __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const 
 }
 
 __global__ void k_mf_state_begin(MfState* __restrict__ st, const double* __restrict__ G, int nused, double tol,
-                                 int max_iter) {
+                                 int max_iter, int nf) {
     const int f = threadIdx.x;
-    if (f < NF) {
-        st->G[f] = G[f];
+    if (f < kMaxNF) {
+        const bool used = f < nf;
+        st->G[f] = used ? G[f] : 1.0;
         st->conv_prev[f] = 0.0;
         st->conv[f] = 0.0;
         st->done[f] = f < nused ? 0 : 1;
@@ -206,6 +219,7 @@ __global__ void k_mf_state_begin(MfState* __restrict__ st, const double* __restr
         st->sweep = 0;
         st->max_iter = max_iter;
         st->all_done = nused > 0 ? 0 : 1;
+        st->nf = nf;
         st->flags = 0;
         st->tol = tol;
     }
@@ -213,56 +227,70 @@ __global__ void k_mf_state_begin(MfState* __restrict__ st, const double* __restr
 
 static inline unsigned nb(int64_t n) { return (unsigned)((n + 255) / 256); }
 
+static void check_nf(int nf, const char* what) {
+    if (nf != 16 && nf != 32 && nf != 64) throw std::runtime_error(std::string(what) + ": nf must be 16, 32 or 64");
+}
+
 void launch_mf_prep(const double* g, int64_t nrows, int64_t nrows_pad, const double* norm, const float* ray_length,
-                    float len_thres, float* ghat, float* arow, float* gpos, float* wo, hipStream_t stream) {
-    hipLaunchKernelGGL(k_mf_prep, dim3(nb(nrows_pad * NF)), dim3(256), 0, stream, g, nrows, nrows_pad, norm,
-                       ray_length, len_thres, ghat, arow, gpos, wo);
+                    float len_thres, float* ghat, float* arow, float* gpos, float* wo, int nf, hipStream_t stream) {
+    check_nf(nf, "mf_prep");
+    hipLaunchKernelGGL(k_mf_prep, dim3(nb(nrows_pad * nf)), dim3(256), 0, stream, g, nrows, nrows_pad, norm,
+                       ray_length, len_thres, ghat, arow, gpos, wo, nf);
     check_launch("k_mf_prep");
 }
 
 int mf_weights_num_blocks(int64_t nrows_pad) { return (int)((nrows_pad + kWRows - 1) / kWRows); }
 
 void launch_mf_weights(const float* Fs, int nsplit, int64_t nrows_pad, const float* ghat, const float* arow,
-                       bool logmode, float* W, double* F2part, hipStream_t stream) {
+                       bool logmode, float* W, double* F2part, int nf, hipStream_t stream) {
+    check_nf(nf, "mf_weights");
     hipLaunchKernelGGL(k_mf_weights, dim3((unsigned)mf_weights_num_blocks(nrows_pad)), dim3(256), 0, stream, Fs,
-                       nsplit, nrows_pad, ghat, arow, logmode ? 1 : 0, W, F2part);
+                       nsplit, nrows_pad, ghat, arow, logmode ? 1 : 0, W, F2part, nf);
     check_launch("k_mf_weights");
 }
 
 void launch_mf_collect(const float* part, int nsplit, int64_t ld, const float* scale, float* D, const double* F2part,
-                       int nF2, float* F2out, hipStream_t stream) {
+                       int nF2, float* F2out, int nf, hipStream_t stream) {
+    check_nf(nf, "mf_collect");
     hipLaunchKernelGGL(k_mf_collect, dim3((unsigned)((ld + 63) / 64)), dim3(256), 0, stream, part, nsplit, ld, scale,
-                       D, F2part, nF2, F2out);
+                       D, F2part, nF2, F2out, nf);
     check_launch("k_mf_collect");
 }
 
-void launch_mf_init(float* X, const float* D0, const float* dinv, int64_t nvox, int64_t ld, int nused,
+void launch_mf_init(float* X, const float* D0, const float* dinv, int64_t nvox, int64_t ld, int nused, int nf,
                     hipStream_t stream) {
-    hipLaunchKernelGGL(k_mf_init, dim3(nb((int64_t)NF * ld)), dim3(256), 0, stream, X, D0, dinv, nvox, ld, nused);
+    check_nf(nf, "mf_init");
+    hipLaunchKernelGGL(k_mf_init, dim3(nb((int64_t)nf * ld)), dim3(256), 0, stream, X, D0, dinv, nvox, ld, nused, nf);
     check_launch("k_mf_init");
 }
 
+// The kernels below take nf from the state (set by k_mf_state_begin): nf = frames of the engine's batch.
 void launch_mf_penalty(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta, bool logx,
-                       const float* X, int64_t ld, float* pen, const MfState* st, hipStream_t stream) {
-    hipLaunchKernelGGL(k_mf_penalty, dim3(nb(n * NF)), dim3(256), 0, stream, row_ptr, col, val, n, beta,
+                       const float* X, int64_t ld, float* pen, const MfState* st, int nf, hipStream_t stream) {
+    check_nf(nf, "mf_penalty");
+    hipLaunchKernelGGL(k_mf_penalty, dim3(nb(n * nf)), dim3(256), 0, stream, row_ptr, col, val, n, beta,
                        logx ? 1 : 0, X, ld, pen, st);
     check_launch("k_mf_penalty");
 }
 
 void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream) {
-    hipLaunchKernelGGL(k_mf_decide, dim3(1), dim3(64), 0, stream, st, F2);
+    hipLaunchKernelGGL(k_mf_decide, dim3(1), dim3(kMaxNF), 0, stream, st, F2);
     check_launch("k_mf_decide");
 }
 
 void launch_mf_update(float* X, const float* D, const float* O, const float* pen, float alpha, bool logmode,
-                      int64_t nvox, int64_t ld, const MfState* st, hipStream_t stream) {
-    hipLaunchKernelGGL(k_mf_update, dim3(nb((int64_t)NF * ld)), dim3(256), 0, stream, X, D, O, pen, alpha,
+                      int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream) {
+    check_nf(nf, "mf_update");
+    hipLaunchKernelGGL(k_mf_update, dim3(nb((int64_t)nf * ld)), dim3(256), 0, stream, X, D, O, pen, alpha,
                        logmode ? 1 : 0, nvox, ld, st);
     check_launch("k_mf_update");
 }
 
-void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, int max_iter, hipStream_t stream) {
-    hipLaunchKernelGGL(k_mf_state_begin, dim3(1), dim3(64), 0, stream, st, G, nused, tol, max_iter);
+void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, int max_iter, int nf,
+                           hipStream_t stream) {
+    check_nf(nf, "mf_state_begin");
+    if (nused > nf) throw std::runtime_error("mf_state_begin: more frames than the batch holds");
+    hipLaunchKernelGGL(k_mf_state_begin, dim3(1), dim3(kMaxNF), 0, stream, st, G, nused, tol, max_iter, nf);
     check_launch("k_mf_state_begin");
 }
 

@@ -41,19 +41,21 @@ static_assert(sizeof(SartState) == 128, "SartState must be 128 bytes");
 
 enum Status : int32_t { kSuccess = 0, kMaxIterationsExceeded = -1, kRunning = -2 };
 
-// Device-resident convergence state of a 16-frame batch (multi-frame solver): one column per frame.
-constexpr int kMfFrames = 16;
+// Device-resident convergence state of a multi-frame batch (multi-frame solver): one column per frame.
+// A batch holds nf = 16, 32 or 64 frames (the MFMA N dimension is 16; 32 and 64 use 2 or 4 column groups).
+constexpr int kMfMaxFrames = 64;
 struct alignas(16) MfState {
-    double G[kMfFrames];          // sum_{g>0} g^2 / s^2 per frame
-    double conv_prev[kMfFrames];
-    double conv[kMfFrames];       // last convergence metric per frame
-    int32_t done[kMfFrames];      // frame finished (converged, non-finite, or unused slot)
-    int32_t status[kMfFrames];
-    int32_t iters[kMfFrames];
+    double G[kMfMaxFrames];          // sum_{g>0} g^2 / s^2 per frame
+    double conv_prev[kMfMaxFrames];
+    double conv[kMfMaxFrames];       // last convergence metric per frame
+    int32_t done[kMfMaxFrames];      // frame finished (converged, non-finite, or unused slot)
+    int32_t status[kMfMaxFrames];
+    int32_t iters[kMfMaxFrames];
     int32_t sweep;
     int32_t max_iter;
-    int32_t all_done;             // every frame done, or max_iter reached (no further update)
-    int32_t flags;                // bit f: frame f produced a non-finite ||A x||^2
+    int32_t all_done;                // every frame done, or max_iter reached (no further update)
+    int32_t nf;                      // frames per batch (columns in use by the kernels)
+    unsigned long long flags;        // bit f: frame f produced a non-finite ||A x||^2
     double tol;
 };
 

@@ -1,10 +1,10 @@
-"""Multi-frame SART: up to 16 independent frames solved together on the fp32 matrix cores.
+"""Multi-frame SART: up to 64 independent frames solved together on the fp32 matrix cores.
 
 The reference solves the time series strictly frame by frame (reference main.cpp:131-140), streaming
 the RTM twice per iteration per frame. For throughput on long time series (BASELINE.json config 5),
 frames can be batched: the forward and back projections become skinny GEMMs ``A.X`` / ``A^T.W`` with
-16 right-hand sides (csrc/kernels/multiframe.hip, ``v_mfma_f32_16x16x4_f32``), reading A once per
-iteration for all 16 frames. Every frame keeps its own normalisation, saturation mask, convergence
+16, 32 or 64 right-hand sides (csrc/kernels/multiframe.hip, ``v_mfma_f32_16x16x4_f32`` on 1, 2 or 4
+column groups), reading A twice per iteration for the whole batch. Every frame keeps its own normalisation, saturation mask, convergence
 history and status; frames that converge are frozen while the others continue. Batched frames are
 cold-started (no warm start chain between them), like ``--no_guess``.
 
@@ -25,7 +25,8 @@ from .laplacian import LaplacianCSR
 from .rtm import DenseRTM
 from .sart import SolveResult, SolverParams, _host_f64
 
-NF = 16
+NF = 16        # MFMA column group (frames per 16-wide N tile)
+MAX_BATCH = 64  # widest batch: 4 column groups
 
 
 class MultiFrameSARTSolver:
@@ -39,7 +40,7 @@ class MultiFrameSARTSolver:
         self.params = params or SolverParams()
         self.params.validate(allow_zero_tolerance)
         self.log = bool(logarithmic)
-        self.batch = max(1, min(int(batch), NF))
+        self.batch = max(1, min(int(batch), MAX_BATCH))
         self.L = laplacian if (laplacian is not None and laplacian.nnz > 0 and self.params.beta_laplace > 0) else None
         if self.L is not None and self.L.n != rtm.nvoxel:
             raise ValueError("Laplacian and ray-transfer matrices have different number of voxels.")
@@ -54,6 +55,7 @@ class MultiFrameSARTSolver:
         cfg.max_iterations = int(p.max_iterations)
         cfg.allow_zero_tolerance = bool(allow_zero_tolerance)
         cfg.check_interval = max(1, int(check_interval))
+        cfg.mf_frames = self.batch
         device = self.dev.index if self.dev.index is not None else 0
         self.native_comm = native_communicator(self.comm, device)
         self.engine = self.k.MultiFrameEngine(device, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld,
@@ -61,6 +63,7 @@ class MultiFrameSARTSolver:
         if self.L is not None:
             self.engine.set_laplacian(self.L.row_ptr_host, self.L.col_host, self.L.val_host)
         self.P, self.Pp, self.V, self.ld = rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld
+        self.batch_width = int(self.engine.batch_frames)  # 16, 32 or 64 columns on the matrix cores
 
     def solve_batch(self, measurements) -> List[SolveResult]:
         g_all = np.asarray(measurements, dtype=np.float64)

@@ -123,23 +123,25 @@ def test_synthetic_shard_invariance(k, dev):
     assert abs(a.mean().item() - 0.5) < 0.01
 
 
-@pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (64, 1024), (2048, 4096)])
-def test_multiframe_mfma(k, dev, P, V):
+@pytest.mark.parametrize("nf", [16, 32, 64])
+@pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (64, 1024), (2048, 4096), (1000, 1088)])
+def test_multiframe_mfma(k, dev, P, V, nf):
     A, m = _rtm(dev, P, V, seed=11)
     rng = np.random.default_rng(4)
-    X = rng.random((16, V)).astype(np.float32)  # frame-major
-    Xd = torch.zeros((16, m.ld), device=dev)
+    X = rng.random((nf, V)).astype(np.float32)  # frame-major
+    Xd = torch.zeros((nf, m.ld), device=dev)
     Xd[:, :V] = torch.from_numpy(X)
-    nsf = 3 if m.ld >= 3072 else 1
-    Fo3 = torch.zeros((nsf, m.nrows_pad, 16), device=dev)
-    k.mf_forward(m.A.data_ptr(), m.ld, P, m.nrows_pad, Xd.data_ptr(), m.ld, Fo3.data_ptr(), nsf, _stream(dev))
+    nsf = 3 if m.ld > 1024 else 1  # ragged splits exercise the 4-float4 tail loop
+    Fo3 = torch.zeros((nsf, m.nrows_pad, nf), device=dev)
+    k.mf_forward(m.A.data_ptr(), m.ld, P, m.nrows_pad, Xd.data_ptr(), m.ld, Fo3.data_ptr(), nsf, _stream(dev), nf)
     Fo = Fo3.sum(0)
-    W = (rng.random((P, 16)) - 0.5).astype(np.float32)
-    Wd = torch.zeros((m.nrows_pad, 16), device=dev)
-    Wd[:P] = torch.from_numpy(W)
+    W = (rng.random((P, nf)) - 0.5).astype(np.float32)
+    Wd = torch.zeros((m.nrows_pad, nf), device=dev)
+    # back-projection operand layout [rows][16][nf / 16]: frame 16 j + i at position i * (nf / 16) + j
+    Wd[:P] = torch.from_numpy(np.ascontiguousarray(W.reshape(P, nf // 16, 16).transpose(0, 2, 1).reshape(P, nf)))
     ns = 3
-    part = torch.zeros((ns, m.ld, 16), device=dev)
-    k.mf_backproject(m.A.data_ptr(), m.ld, P, Wd.data_ptr(), ns, part.data_ptr(), _stream(dev))
+    part = torch.zeros((ns, m.ld, nf), device=dev)
+    k.mf_backproject(m.A.data_ptr(), m.ld, P, Wd.data_ptr(), ns, part.data_ptr(), _stream(dev), nf)
     torch.cuda.synchronize()
     A64 = A.astype(np.float64)
     np.testing.assert_allclose(Fo[:P].cpu().numpy(), A64 @ X.T.astype(np.float64), rtol=2e-5, atol=2e-4)

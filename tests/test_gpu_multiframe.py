@@ -7,8 +7,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("log", [False, True])
-@pytest.mark.parametrize("nframes", [1, 5, 16, 19])
-def test_multiframe_vs_oracle(log, nframes):
+@pytest.mark.parametrize("nframes,batch", [(1, 16), (5, 16), (16, 16), (19, 16), (27, 32), (40, 64)])
+def test_multiframe_vs_oracle(log, nframes, batch):
     from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
     from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
     from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
@@ -24,7 +24,9 @@ def test_multiframe_vs_oracle(log, nframes):
     G[rng.random(G.shape) < 0.03] = -1.0
     L = LaplacianCSR.grid_3d(10, 10, 10, device=dev)
     kw = dict(max_iterations=40, conv_tolerance=1e-4, beta_laplace=1e-3)
-    s = MultiFrameSARTSolver(DenseRTM.from_dense(A, device=dev), L, None, SolverParams(**kw), logarithmic=log)
+    s = MultiFrameSARTSolver(DenseRTM.from_dense(A, device=dev), L, None, SolverParams(**kw), logarithmic=log,
+                             batch=batch)
+    assert s.batch_width == batch
     res = s.solve_batch(G)
     assert len(res) == nframes
     for f in range(nframes):
