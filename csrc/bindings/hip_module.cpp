@@ -132,6 +132,7 @@ static void bind_engine(py::module_& m) {
         .def_readwrite("check_interval", &sart::EngineConfig::check_interval)
         .def_readwrite("use_fused", &sart::EngineConfig::use_fused)
         .def_readwrite("mf_frames", &sart::EngineConfig::mf_frames)
+        .def_readwrite("fused_min_bytes", &sart::EngineConfig::fused_min_bytes)
         .def_readwrite("fused_variant", &sart::EngineConfig::fused_variant)
         .def_readwrite("rows_per_tile", &sart::EngineConfig::rows_per_tile)
         .def_readwrite("fused_schedule", &sart::EngineConfig::fused_schedule)
@@ -345,6 +346,7 @@ PYBIND11_MODULE(_sart_hip, m) {
                                  P<const float>(ghat), P<const float>(arow), P<float>(partial), P<double>(Fpart),
                                  P<uint64_t>(gran), I, J, P<sart::SartState>(st), P<unsigned>(xcnt), S(stream));
     });
+    m.def("fused_min_bytes_from_env", &sart::fused_min_bytes_from_env);
     m.def("mf_forward_num_splits", &sart::mf_forward_num_splits);
     m.def("mf_backproject_num_splits", &sart::mf_backproject_num_splits);
     m.def("mf_set_depth", &sart::mf_set_depth);

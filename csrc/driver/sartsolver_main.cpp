@@ -233,6 +233,7 @@ int main(int argc, char** argv) {
             EngineConfig ec;
             static_cast<SolverParams&>(ec) = params;
             ec.use_fused = !cfg.two_pass;
+            ec.fused_min_bytes = fused_min_bytes_from_env();
             if (const char* v = std::getenv("SART_FUSED_VARIANT"); v && *v) ec.fused_variant = std::atoi(v);
             engine = std::make_unique<Engine>(device, dshard->A, dshard->nrows, dshard->nrows_pad, dshard->nvoxel,
                                               dshard->ld, dcomm.get(), ec);

@@ -25,6 +25,11 @@ void hip_ok(hipError_t e, const char* what) {
 
 }  // namespace
 
+double fused_min_bytes_from_env() {
+    const char* e = std::getenv("SART_FUSED_MIN_MB");
+    return ((e && *e) ? std::atof(e) : 128.0) * 1024.0 * 1024.0;
+}
+
 RoctxRange::RoctxRange(const char* name) { roctxRangePushA(name); }
 RoctxRange::~RoctxRange() { roctxRangePop(); }
 
@@ -87,7 +92,7 @@ Engine::Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int
     st_.resize(1);
     xcnt_.resize(16);
     use_fused_ = false;
-    if (cfg_.use_fused) {
+    if (cfg_.use_fused && (double)Pp_ * (double)ld_ * sizeof(float) >= cfg_.fused_min_bytes) {
         geom_ = fused_geometry(ld_, num_cus_, cfg_.fused_variant, cfg_.rows_per_tile);
         use_fused_ = geom_.valid();
     }

@@ -32,7 +32,13 @@ struct EngineConfig : SolverParams {
     int fused_variant = 6;
     int rows_per_tile = 0;   // 0: default (fused_geometry)
     int fused_schedule = -1; // -1: keep the launcher's default
-    bool use_graph = false;  // opt-in (SART_GRAPH=1): chunk capture is under validation
+    // Opt-in (SART_GRAPH=1): bitwise equal to eager chunks (tests/test_gpu_solver.py), but measured no
+    // faster for the two-pass kernels and 13-28 % slower for the fused sweep at 8k x 16k and 16k x 64k
+    // (profiles/graph_check_r1.jsonl): launches are already hidden behind the queued chunk.
+    bool use_graph = false;
+    // The fused sweep is used only for shards of at least this many bytes (the drivers pass 128 MiB:
+    // below ~100 MB the two-pass kernels are faster, e.g. 40.6 vs 60.2 us per iteration at 2048 x 4096).
+    double fused_min_bytes = 0;
     // Fault injection (tests; env SART_FAULT_INJECT=N): report a persistent-sweep protocol timeout in the
     // first N solves, exercising the v6 -> v3 -> two-pass fallback chain end to end.
     int fault_inject = 0;
@@ -74,6 +80,9 @@ struct DeviceRaySums {
     DeviceArray<double> rho64, ell64;
     DeviceArray<float> ray_len, dinv, dscale, dmask;
 };
+
+// SART_FUSED_MIN_MB (default 128): the drivers' threshold for EngineConfig::fused_min_bytes.
+double fused_min_bytes_from_env();
 
 class Engine {
    public:

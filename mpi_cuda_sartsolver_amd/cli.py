@@ -107,9 +107,10 @@ def run(cfg, intervals) -> int:
                                               batch=cfg.batch_frames)
             else:
                 from .models.sart import SARTSolver
+                from .ops import hip
 
                 solver = SARTSolver(shard, laplacian, comm, params, logarithmic=cfg.logarithmic,
-                                    use_fused=not cfg.two_pass)
+                                    use_fused=not cfg.two_pass, fused_min_bytes=hip().fused_min_bytes_from_env())
         else:
             from .models.cpu import CPUSARTSolver
 

@@ -100,7 +100,8 @@ class SARTSolver:
                  comm: Optional[Communicator] = None, params: Optional[SolverParams] = None,
                  logarithmic: bool = False, use_fused: bool = True, check_interval: int = 16,
                  allow_zero_tolerance: bool = False, fused_variant: Optional[int] = None,
-                 fused_rows_per_tile: Optional[int] = None, use_graph: Optional[bool] = None):
+                 fused_rows_per_tile: Optional[int] = None, use_graph: Optional[bool] = None,
+                 fused_min_bytes: float = 0.0):
         self.k = hip()
         self.rtm = rtm
         self.dev = rtm.device
@@ -131,6 +132,7 @@ class SARTSolver:
         if use_graph is None:
             use_graph = os.environ.get("SART_GRAPH", "0") == "1"
         cfg.use_graph = bool(use_graph)
+        cfg.fused_min_bytes = float(fused_min_bytes)  # smaller shards use the two-pass kernels
         device = self.dev.index if self.dev.index is not None else 0
         self.native_comm = native_communicator(self.comm, device)
         self.engine = self.k.Engine(device, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld,
