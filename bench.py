@@ -63,6 +63,9 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--frames", type=int, default=1,
                     help="frames per step; > 1 solves them together with the multi-frame MFMA engine (up to 64 per batch)")
+    ap.add_argument("--partition", choices=["rows", "cols"], default="rows",
+                    help="rows: the reference's pixel shards (default); cols: voxel shards, each GPU holds all "
+                         "pixels of --nvox voxels (two-pass kernels, all-reduce of A.x)")
     ap.add_argument("--laplacian", action="store_true",
                     help="add the 7-point grid Laplacian regulariser (beta 1e-2, the reference default)")
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
@@ -71,6 +74,8 @@ def main() -> int:
     if args.config:
         for k, v in PRESETS[args.config].items():
             setattr(args, k, v)
+    if args.partition == "cols" and args.frames > 1:
+        ap.error("--partition cols solves single frames (the multi-frame engine uses row shards)")
 
     import torch
 
@@ -85,15 +90,26 @@ def main() -> int:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {n}; using {n}", file=sys.stderr)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    npix_total = args.npix * n if args.scaling == "weak" else args.npix
-    blk = row_partition(npix_total, n, comm.rank)
-    prob = make_problem(blk.size, args.nvox, row_offset=blk.offset, seed=args.seed, device=dev)
+    cols = args.partition == "cols"
+    nvox_total = args.nvox
+    if cols:  # voxel shards: every GPU holds all --npix pixels of its block of voxels
+        from mpi_cuda_sartsolver_amd.parallel.partition import col_partition
+        from mpi_cuda_sartsolver_amd.utils.synthetic import make_column_problem
+
+        npix_total = args.npix
+        nvox_total = args.nvox * n if args.scaling == "weak" else args.nvox
+        cb = col_partition(nvox_total, n, comm.rank)
+        prob = make_column_problem(npix_total, cb.size, cb.offset, nvox_total, comm, seed=args.seed, device=dev)
+    else:
+        npix_total = args.npix * n if args.scaling == "weak" else args.npix
+        blk = row_partition(npix_total, n, comm.rank)
+        prob = make_problem(blk.size, args.nvox, row_offset=blk.offset, seed=args.seed, device=dev)
     params = SolverParams(max_iterations=args.iters, conv_tolerance=0.0)  # fixed iteration count
     lap = None
     if args.laplacian:
         from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
 
-        lap = LaplacianCSR.grid_3d(*grid_dims(args.nvox))
+        lap = LaplacianCSR.grid_3d(*grid_dims(nvox_total))
     if args.frames > 1:
         import numpy as np
 
@@ -117,7 +133,8 @@ def main() -> int:
         runner = _Batch(solver)
     else:
         solver = SARTSolver(prob.rtm, lap, comm, params, logarithmic=args.variant == "log",
-                            use_fused=not args.no_fused, check_interval=32, allow_zero_tolerance=True)
+                            use_fused=not args.no_fused, check_interval=32, allow_zero_tolerance=True,
+                            partition=args.partition)
         g = prob.measurement
         runner = solver
     multi = args.frames > 1
@@ -140,7 +157,7 @@ def main() -> int:
     elapsed = comm.all_reduce_scalar(elapsed, op="max")
 
     iters_per_s = iters / elapsed
-    flop_per_iter = 4.0 * npix_total * args.nvox
+    flop_per_iter = 4.0 * npix_total * nvox_total
     gflops = flop_per_iter * iters_per_s / 1e9
     use_fused = (not multi) and solver.use_fused
     # bytes of A per SART iteration of ONE frame: fused 1 read, two-pass 2 reads, multi-frame 2 reads per batch
@@ -172,10 +189,11 @@ def main() -> int:
                      + (" multi-frame (MFMA)" if multi else ""),
             "preset": args.config,
             "npixel_total": npix_total,
-            "nvoxel": args.nvox,
+            "nvoxel": nvox_total,
             "global_batch": args.frames,
-            "seq_len": args.nvox,
-            "parallelism": f"row-shard dp{n}" if n > 1 else "single",
+            "seq_len": nvox_total,
+            "parallelism": (f"{'col' if cols else 'row'}-shard dp{n}" if n > 1 else "single"),
+            "partition": args.partition,
             "rtm_GB_per_gpu": round(prob.rtm.nbytes / 1e9, 2),
         },
     }

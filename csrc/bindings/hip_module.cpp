@@ -133,6 +133,9 @@ static void bind_engine(py::module_& m) {
         .def_readwrite("use_fused", &sart::EngineConfig::use_fused)
         .def_readwrite("mf_frames", &sart::EngineConfig::mf_frames)
         .def_readwrite("fused_min_bytes", &sart::EngineConfig::fused_min_bytes)
+        .def_readwrite("column_shard", &sart::EngineConfig::column_shard)
+        .def_readwrite("col_offset", &sart::EngineConfig::col_offset)
+        .def_readwrite("nvoxel_total", &sart::EngineConfig::nvoxel_total)
         .def_readwrite("fused_variant", &sart::EngineConfig::fused_variant)
         .def_readwrite("rows_per_tile", &sart::EngineConfig::rows_per_tile)
         .def_readwrite("fused_schedule", &sart::EngineConfig::fused_schedule)
@@ -196,6 +199,7 @@ static void bind_engine(py::module_& m) {
         .def_property_readonly("use_fused", &sart::Engine::use_fused)
         .def_property_readonly("geometry", &sart::Engine::geometry)
         .def_property_readonly("num_cus", &sart::Engine::num_cus)
+        .def_property_readonly("column_shard", &sart::Engine::column_shard)
         .def_property_readonly("nrows", &sart::Engine::nrows)
         .def_property_readonly("nvoxel", &sart::Engine::nvoxel)
         .def_property_readonly("stream", [](const sart::Engine& e) { return reinterpret_cast<uintptr_t>(e.stream()); })
@@ -321,9 +325,13 @@ PYBIND11_MODULE(_sart_hip, m) {
         sart::launch_state_begin(P<sart::SartState>(st), G, tol, max_iter, S(stream));
     });
     m.def("synth_matrix", [](uintptr_t A, int64_t ld, int64_t nrows_pad, int64_t nrows, int64_t ncols,
-                             int64_t row_offset, uint64_t seed, float lo, float hi, uintptr_t stream) {
-        sart::launch_synth_matrix(P<float>(A), ld, nrows_pad, nrows, ncols, row_offset, seed, lo, hi, S(stream));
-    });
+                             int64_t row_offset, uint64_t seed, float lo, float hi, uintptr_t stream,
+                             int64_t col_offset, int64_t ncols_total) {
+        sart::launch_synth_matrix_block(P<float>(A), ld, nrows_pad, nrows, ncols, row_offset, col_offset,
+                                        ncols_total > 0 ? ncols_total : ncols, seed, lo, hi, S(stream));
+    }, py::arg("A"), py::arg("ld"), py::arg("nrows_pad"), py::arg("nrows"), py::arg("ncols"), py::arg("row_offset"),
+       py::arg("seed"), py::arg("lo"), py::arg("hi"), py::arg("stream"), py::arg("col_offset") = 0,
+       py::arg("ncols_total") = 0);
     m.def("synth_vector", [](uintptr_t out, int64_t n, int64_t offset, uint64_t seed, double lo, double hi,
                              uintptr_t stream) {
         sart::launch_synth_vector(P<double>(out), n, offset, seed, lo, hi, S(stream));

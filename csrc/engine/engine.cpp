@@ -69,6 +69,11 @@ Engine::Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int
     if (ld_ % 64 || ld_ < V_ || Pp_ % 64 || Pp_ < P_)
         throw std::invalid_argument("Engine: ld and nrows_pad must be multiples of 64 covering the shard");
     cfg_.check_interval = std::max(1, cfg_.check_interval);
+    if (cfg_.column_shard) {
+        if (cfg_.nvoxel_total <= 0) cfg_.nvoxel_total = V_;
+        if (cfg_.col_offset < 0 || cfg_.col_offset + V_ > cfg_.nvoxel_total)
+            throw std::invalid_argument("Engine: column shard outside [0, nvoxel_total)");
+    }
     set_device();
     hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");  // the shard may have been filled on another stream
     hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -92,7 +97,7 @@ Engine::Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int
     st_.resize(1);
     xcnt_.resize(16);
     use_fused_ = false;
-    if (cfg_.use_fused && (double)Pp_ * (double)ld_ * sizeof(float) >= cfg_.fused_min_bytes) {
+    if (cfg_.use_fused && !cfg_.column_shard && (double)Pp_ * (double)ld_ * sizeof(float) >= cfg_.fused_min_bytes) {
         geom_ = fused_geometry(ld_, num_cus_, cfg_.fused_variant, cfg_.rows_per_tile);
         use_fused_ = geom_.valid();
     }
@@ -122,13 +127,13 @@ void Engine::alloc_fused() {
     nF_fused_ = use_fused_ ? (int64_t)geom_.grid * fused_fpart_per_block(geom_.variant) : 0;
     const int64_t n_part = std::max<int64_t>(nsplit_, use_fused_ ? geom_.I : 1);
     if ((int64_t)partial_.size() < n_part * ld_) partial_.resize(n_part * ld_);
-    const int64_t nF = std::max<int64_t>({forward_num_blocks(Pp_), nF_fused_, 1});
+    const int64_t nF = std::max<int64_t>({forward_num_blocks(Pp_), (int64_t)weights_num_blocks(Pp_), nF_fused_, 1});
     if ((int64_t)Fpart_.size() < nF) Fpart_.resize(nF);
     if (use_fused_ && (int64_t)gran_.size() < Pp_ * geom_.J) gran_.resize(Pp_ * geom_.J);
 }
 
 void DeviceRaySums::compute(const float* A, int64_t P, int64_t Pp, int64_t V, int64_t ld, Communicator* comm,
-                            const SolverParams& p, hipStream_t stream) {
+                            const SolverParams& p, hipStream_t stream, bool col_shard) {
     // rho_v = sum_p A[p, v] (fp64, all-reduced), l_p = sum_v A[p, v] (fp64, local): on the device instead of
     // the reference's host loops (sartsolver.cpp:38-56); scales with the reference's fp32 semantics
     RoctxRange r("sart::ray_sums");
@@ -144,7 +149,10 @@ void DeviceRaySums::compute(const float* A, int64_t P, int64_t Pp, int64_t V, in
         launch_reduce_partials_f64(part.get(), ld, nsplit, rho64.get(), stream);
         hip_ok(hipStreamSynchronize(stream), "ray sums");
     }
-    comm->all_reduce(rho64.get(), (size_t)ld, ReduceOp::kSum, stream);
+    if (col_shard)
+        comm->all_reduce(ell64.get(), (size_t)P, ReduceOp::kSum, stream);
+    else
+        comm->all_reduce(rho64.get(), (size_t)ld, ReduceOp::kSum, stream);
     launch_f64_to_f32(ell64.get(), ray_len.get(), Pp, stream);
     launch_density_scales(rho64.get(), V, ld, (float)p.ray_density_threshold, (float)p.relaxation, dinv.get(),
                           dscale.get(), dmask.get(), stream);
@@ -163,7 +171,7 @@ std::vector<double> DeviceRaySums::length(int64_t P) const {
     return h;
 }
 
-void Engine::ray_sums() { rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_); }
+void Engine::ray_sums() { rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_, cfg_.column_shard); }
 
 std::vector<double> Engine::ray_density() const {
     set_device();
@@ -180,6 +188,25 @@ void Engine::set_laplacian(const int64_t* row_ptr, const int32_t* col, const flo
     drop_graph();
     has_lap_ = false;
     if (nnz <= 0 || cfg_.beta_laplace <= 0) return;
+    if (cfg_.column_shard) {
+        // full L (nvoxel_total rows, global column indices): keep this shard's rows, gather x for the columns
+        const int64_t n = cfg_.nvoxel_total, r0 = cfg_.col_offset;
+        if (row_ptr[n] != nnz) throw std::invalid_argument("Laplacian CSR row pointer does not match nnz");
+        const int64_t k0 = row_ptr[r0], k1 = row_ptr[r0 + V_];
+        std::vector<int64_t> rp(V_ + 1);
+        for (int64_t i = 0; i <= V_; ++i) rp[i] = row_ptr[r0 + i] - k0;
+        lap_rp_.resize(V_ + 1);
+        hip_ok(hipMemcpy(lap_rp_.get(), rp.data(), (V_ + 1) * sizeof(int64_t), hipMemcpyHostToDevice), "H2D");
+        if (k1 > k0) {
+            lap_col_.resize(k1 - k0);
+            lap_val_.resize(k1 - k0);
+            hip_ok(hipMemcpy(lap_col_.get(), col + k0, (k1 - k0) * sizeof(int32_t), hipMemcpyHostToDevice), "H2D");
+            hip_ok(hipMemcpy(lap_val_.get(), val + k0, (k1 - k0) * sizeof(float), hipMemcpyHostToDevice), "H2D");
+        }
+        xg_.resize((size_t)(n + 63) / 64 * 64);
+        has_lap_ = true;
+        return;
+    }
     if (row_ptr[V_] != nnz) throw std::invalid_argument("Laplacian CSR row pointer does not match nnz");
     lap_rp_.resize(V_ + 1);
     lap_col_.resize(nnz);
@@ -199,9 +226,10 @@ double Engine::setup_frame(const double* g, const double* x0) {
         mx = std::max(mx, g[i]);
         if (g[i] > 0) gs += g[i] * g[i];
     }
-    double norm = comm_->host().all_reduce_scalar(mx, ReduceOp::kMax);
+    const bool cols = cfg_.column_shard;  // every rank holds every pixel: the sums are already global
+    double norm = cols ? mx : comm_->host().all_reduce_scalar(mx, ReduceOp::kMax);
     if (!(norm > 0)) norm = 1.0;
-    double G = comm_->host().all_reduce_scalar(gs, ReduceOp::kSum) / (norm * norm);
+    double G = (cols ? gs : comm_->host().all_reduce_scalar(gs, ReduceOp::kSum)) / (norm * norm);
     if (!(G > 0)) G = 1.0;
     if (P_) hip_ok(hipMemcpyAsync(g64_.get(), g, P_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D g");
     launch_prep_rows(g64_.get(), P_, Pp_, 1.0 / norm, rs_.ray_len.get(), (float)cfg_.ray_length_threshold, ghat_.get(),
@@ -211,7 +239,7 @@ double Engine::setup_frame(const double* g, const double* x0) {
         launch_backproject(A_, ld_, P_, gpos_.get(), nsplit_, partial_.get(), nullptr, stream_);
         launch_reduce_partials(partial_.get(), ld_, nsplit_, rs_.dinv.get(), comm_buf_.get(), nullptr, 0, nullptr,
                                nullptr, stream_);
-        comm_->all_reduce(comm_buf_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
+        if (!cols) comm_->all_reduce(comm_buf_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
         launch_init_solution(x_.get(), V_, ld_, comm_buf_.get(), nullptr, 1.0, stream_);
     } else {
         hip_ok(hipMemcpyAsync(x064_.get(), x0, V_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D x0");
@@ -222,7 +250,7 @@ double Engine::setup_frame(const double* g, const double* x0) {
         launch_backproject(A_, ld_, P_, wo_.get(), nsplit_, partial_.get(), nullptr, stream_);
         launch_reduce_partials(partial_.get(), ld_, nsplit_, rs_.dmask.get(), O_.get(), nullptr, 0, nullptr, nullptr,
                                stream_);
-        comm_->all_reduce(O_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
+        if (!cols) comm_->all_reduce(O_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
     }
     launch_state_begin(st_.get(), G, cfg_.conv_tolerance, cfg_.max_iterations, stream_);
     return norm;
@@ -232,6 +260,10 @@ void Engine::sweep() {
     SartState* st = st_.get();
     const float* scale = cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get();
     float* Fslot = comm_buf_.get() + ld_;
+    if (cfg_.column_shard) {
+        sweep_columns();
+        return;
+    }
     if (use_fused_) {
         if (geom_.variant == 6) hip_ok(hipMemsetAsync(xcnt_.get(), 0, 16 * sizeof(unsigned), stream_), "memset");
         launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, A_, ld_, P_, Pp_, x_.get(), ghat_.get(),
@@ -253,6 +285,40 @@ void Engine::sweep() {
         pen = pen_.get();
     }
     if (comm_->size() > 1) comm_->all_reduce(comm_buf_.get(), (size_t)ld_ + 1, ReduceOp::kSum, stream_);
+    launch_decide(st, Fslot, stream_);
+    if (cfg_.logarithmic)
+        launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_);
+    else
+        launch_update_linear(x_.get(), comm_buf_.get(), pen, V_, st, stream_);
+}
+
+void Engine::sweep_columns() {
+    // f_r = A_r x_r -> all-reduce (pixel vector) -> weights and ||f||^2 (identical on every rank) ->
+    // local back-projection, penalty (x all-gathered when there is a Laplacian), decision and update.
+    SartState* st = st_.get();
+    const float* scale = cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get();
+    float* Fslot = comm_buf_.get() + ld_;
+    launch_forward(kEpiPlain, A_, ld_, P_, Pp_, x_.get(), nullptr, nullptr, fitted_.get(), nullptr, nullptr, st,
+                   stream_);
+    if (comm_->size() > 1) comm_->all_reduce(fitted_.get(), (size_t)P_, ReduceOp::kSum, stream_);
+    launch_weights(cfg_.logarithmic, fitted_.get(), ghat_.get(), arow_.get(), P_, Pp_, w_.get(), Fpart_.get(), st,
+                   stream_);
+    launch_backproject(A_, ld_, P_, w_.get(), nsplit_, partial_.get(), st, stream_);
+    launch_reduce_partials(partial_.get(), ld_, nsplit_, scale, comm_buf_.get(), Fpart_.get(),
+                           weights_num_blocks(Pp_), Fslot, st, stream_);
+    const float* pen = nullptr;
+    if (has_lap_) {
+        const float* xfull = x_.get();
+        if (comm_->size() > 1) {
+            hip_ok(hipMemsetAsync(xg_.get(), 0, xg_.size() * sizeof(float), stream_), "memset");
+            launch_copy_slice(x_.get(), V_, xg_.get(), cfg_.col_offset, stream_);
+            comm_->all_reduce(xg_.get(), (size_t)cfg_.nvoxel_total, ReduceOp::kSum, stream_);
+            xfull = xg_.get();
+        }
+        launch_penalty(cfg_.logarithmic, lap_rp_.get(), lap_col_.get(), lap_val_.get(), V_, (float)cfg_.beta_laplace,
+                       xfull, pen_.get(), st, stream_);
+        pen = pen_.get();
+    }
     launch_decide(st, Fslot, stream_);
     if (cfg_.logarithmic)
         launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_);
@@ -383,6 +449,7 @@ void Engine::forward(const double* x, double* f) {
     hip_ok(hipMemcpyAsync(xd.get(), xf.data(), ld_ * sizeof(float), hipMemcpyHostToDevice, stream_), "H2D");
     launch_forward(kEpiPlain, A_, ld_, P_, Pp_, xd.get(), nullptr, nullptr, fitted_.get(), nullptr, nullptr, nullptr,
                    stream_);
+    if (cfg_.column_shard && comm_->size() > 1) comm_->all_reduce(fitted_.get(), (size_t)P_, ReduceOp::kSum, stream_);
     std::vector<float> fh(P_);
     if (P_) hip_ok(hipMemcpyAsync(fh.data(), fitted_.get(), P_ * sizeof(float), hipMemcpyDeviceToHost, stream_), "D2H");
     hip_ok(hipStreamSynchronize(stream_), "forward");

@@ -44,6 +44,15 @@ struct EngineConfig : SolverParams {
     int fault_inject = 0;
     // Multi-frame engine: frames per batch (16, 32 or 64; MultiFrameEngine rounds other values up).
     int mf_frames = 16;
+    // Column (voxel) shard instead of the reference's row (pixel) shard: this rank holds ALL
+    // pixel rows for voxels [col_offset, col_offset + nvoxel) of nvoxel_total, and gets the full
+    // measurement. Per sweep the partial forward projections (a pixel vector) are all-reduced instead of
+    // the corrections (a voxel vector); the back-projection and the update are local. Two-pass kernels
+    // only (the fused sweep needs complete row dots on one GPU). With a Laplacian, x is all-gathered
+    // every sweep for the penalty of the local rows.
+    bool column_shard = false;
+    int64_t col_offset = 0;
+    int64_t nvoxel_total = 0;  // 0: nvoxel
 };
 
 // roctx range (rocprofv3 --marker-trace) for the lifetime of the object.
@@ -73,8 +82,9 @@ class DeviceArray {
 // Column / row sums of the shard and the per-voxel / per-pixel scales derived from them (device, fp64
 // accumulation, global column sums all-reduced): shared by the single- and multi-frame engines.
 struct DeviceRaySums {
+    // col_shard: the shard holds all rows of some columns, so the row sums are all-reduced instead
     void compute(const float* A, int64_t P, int64_t Pp, int64_t V, int64_t ld, Communicator* comm,
-                 const SolverParams& p, hipStream_t stream);
+                 const SolverParams& p, hipStream_t stream, bool col_shard = false);
     std::vector<double> density(int64_t V) const;  // host copies
     std::vector<double> length(int64_t P) const;
     DeviceArray<double> rho64, ell64;
@@ -108,8 +118,9 @@ class Engine {
     int num_cus() const { return num_cus_; }
     int64_t nrows() const { return P_; }
     int64_t nvoxel() const { return V_; }
-    std::vector<double> ray_density() const;  // global, fp64 (nvoxel)
-    std::vector<double> ray_length() const;   // local, fp64 (nrows)
+    std::vector<double> ray_density() const;  // fp64 (nvoxel): global (row shard) / this shard's voxels (column)
+    std::vector<double> ray_length() const;   // fp64 (nrows): this shard's pixels (row shard) / global (column)
+    bool column_shard() const { return cfg_.column_shard; }
     double last_norm() const { return norm_; }
 
    private:
@@ -117,6 +128,7 @@ class Engine {
     void alloc_fused();
     double setup_frame(const double* g, const double* x0);
     void sweep();
+    void sweep_columns();
     void run_chunk(int n);
     bool fallback();  // false when nothing is left to fall back to
     void drop_graph();
@@ -141,6 +153,7 @@ class Engine {
     DeviceArray<SartState> st_;
     DeviceArray<uint64_t> gran_;
     DeviceArray<unsigned> xcnt_;
+    DeviceArray<float> xg_;  // column shard + Laplacian: all-gathered x (nvoxel_total, padded)
     DeviceArray<int64_t> lap_rp_;
     DeviceArray<int32_t> lap_col_;
     DeviceArray<float> lap_val_;

@@ -36,12 +36,22 @@ void launch_update_linear(float* x, const float* d, const float* pen, int64_t n,
 void launch_update_log(float* x, const float* O, const float* Fv, const float* pen, float alpha, int64_t n,
                        const SartState* st, hipStream_t stream);
 void launch_state_begin(SartState* st, double G, double tol, int max_iter, hipStream_t stream);
+// w = a (ghat - f) (linear) or a f (log) from a complete forward projection f; Fpart[block] = sum f^2 (fp64)
+int weights_num_blocks(int64_t nrows_pad);
+void launch_weights(bool logmode, const float* f, const float* ghat, const float* arow, int64_t nrows,
+                    int64_t nrows_pad, float* w, double* Fpart, const SartState* st, hipStream_t stream);
+// dst[offset + i] = src[i] for i < n (gather of a column shard's slice into a full-length vector)
+void launch_copy_slice(const float* src, int64_t n, float* dst, int64_t offset, hipStream_t stream);
 void launch_density_scales(const double* rho, int64_t n, int64_t n_pad, float thres, float alpha, float* dinv,
                            float* dscale, float* dmask, hipStream_t stream);
 void launch_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t stream);
 // synth.hip
 void launch_synth_matrix(float* A, int64_t ld, int64_t nrows_pad, int64_t nrows, int64_t ncols, int64_t row_offset,
                          uint64_t seed, float lo, float hi, hipStream_t stream);
+// block [row_offset, +nrows) x [col_offset, +ncols) of a global nrows_total x ncols_total synthetic matrix
+void launch_synth_matrix_block(float* A, int64_t ld, int64_t nrows_pad, int64_t nrows, int64_t ncols,
+                               int64_t row_offset, int64_t col_offset, int64_t ncols_total, uint64_t seed, float lo,
+                               float hi, hipStream_t stream);
 void launch_synth_vector(double* out, int64_t n, int64_t offset, uint64_t seed, double lo, double hi,
                          hipStream_t stream);
 // fused_sweep.hip

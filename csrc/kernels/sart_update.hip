@@ -176,7 +176,55 @@ __global__ void k_f64_to_f32(const double* __restrict__ src, float* __restrict__
     if (i < n) dst[i] = (float)src[i];
 }
 
+// Column-shard sweep (Engine with EngineConfig::column_shard): after the all-reduce of the partial forward
+// projections, every rank holds the complete f and forms the SART weight of every pixel, exactly as the
+// epilogue of k_forward does for a row shard (projection.hip): w = a (ghat - f) | a f, and the fp64 sum of
+// f^2 per block (fixed thread order -> deterministic and identical on all ranks).
+__global__ __launch_bounds__(256) void k_weights(int logmode, const float* __restrict__ f,
+                                                 const float* __restrict__ ghat, const float* __restrict__ arow,
+                                                 int64_t nrows, int64_t nrows_pad, float* __restrict__ w,
+                                                 double* __restrict__ Fpart, const SartState* __restrict__ st) {
+    if (st != nullptr && st->done) return;
+    __shared__ double red[4];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    double f2 = 0.0;
+    if (i < nrows_pad) {
+        float wv = 0.f;
+        if (i < nrows) {
+            const float fv = f[i];
+            wv = logmode ? arow[i] * fv : arow[i] * (ghat[i] - fv);
+            f2 = (double)fv * (double)fv;
+        }
+        w[i] = wv;
+    }
+    f2 = wave_sum(f2);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = f2;
+    __syncthreads();
+    if (threadIdx.x == 0) Fpart[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ __launch_bounds__(256) void k_copy_slice(const float* __restrict__ src, int64_t n, float* __restrict__ dst,
+                                                    int64_t offset) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) dst[offset + i] = src[i];
+}
+
 static inline unsigned nb(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+int weights_num_blocks(int64_t nrows_pad) { return (int)nb(nrows_pad); }
+
+void launch_weights(bool logmode, const float* f, const float* ghat, const float* arow, int64_t nrows,
+                    int64_t nrows_pad, float* w, double* Fpart, const SartState* st, hipStream_t stream) {
+    hipLaunchKernelGGL(k_weights, dim3(nb(nrows_pad)), dim3(256), 0, stream, logmode ? 1 : 0, f, ghat, arow, nrows,
+                       nrows_pad, w, Fpart, st);
+    check_launch("k_weights");
+}
+
+void launch_copy_slice(const float* src, int64_t n, float* dst, int64_t offset, hipStream_t stream) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_copy_slice, dim3(nb(n)), dim3(256), 0, stream, src, n, dst, offset);
+    check_launch("k_copy_slice");
+}
 
 void launch_density_scales(const double* rho, int64_t n, int64_t n_pad, float thres, float alpha, float* dinv,
                            float* dscale, float* dmask, hipStream_t stream) {

@@ -3,7 +3,7 @@
 // Every element is a pure function of (seed, global row, column), so a matrix generated as N row
 // shards on N GPUs is bit-identical to the one generated on one GPU: solutions can be compared
 // across GPU counts. The reference has no synthetic path (it always reads HDF5, raytransfer.cpp:27).
-#include "sart_common.hpp"
+#include "launchers.hpp"
 
 namespace sart {
 
@@ -18,9 +18,11 @@ __device__ __forceinline__ float u01(uint64_t seed, uint64_t idx) {
     return (float)(z >> 40) * (1.0f / 16777216.0f);  // [0, 1)
 }
 
-// A[r][c] = lo + (hi - lo) * U(seed, (row_offset + r) * ncols + c) on the valid block, 0 in the padding.
+// A[r][c] = lo + (hi - lo) * U(seed, (row_offset + r) * ncols_total + col_offset + c) on the valid block
+// (c < ncols), 0 in the padding: element (R, C) of one global matrix, for row or column shards alike.
 __global__ __launch_bounds__(256) void k_synth_matrix(float* __restrict__ A, int64_t ld, int64_t nrows_pad,
                                                       int64_t nrows, int64_t ncols, int64_t row_offset,
+                                                      int64_t col_offset, int64_t ncols_total,
                                                       uint64_t seed, float lo, float hi) {
     const int64_t ld4 = ld >> 2;
     const int64_t total4 = nrows_pad * ld4;
@@ -30,7 +32,7 @@ __global__ __launch_bounds__(256) void k_synth_matrix(float* __restrict__ A, int
         const int64_t c = (i - r * ld4) * 4;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (r < nrows) {
-            const uint64_t base = (uint64_t)(row_offset + r) * (uint64_t)ncols;
+            const uint64_t base = (uint64_t)(row_offset + r) * (uint64_t)ncols_total + (uint64_t)col_offset;
             if (c + 0 < ncols) v.x = lo + span * u01(seed, base + c + 0);
             if (c + 1 < ncols) v.y = lo + span * u01(seed, base + c + 1);
             if (c + 2 < ncols) v.z = lo + span * u01(seed, base + c + 2);
@@ -49,12 +51,18 @@ __global__ __launch_bounds__(256) void k_synth_vector(double* __restrict__ out, 
 
 void launch_synth_matrix(float* A, int64_t ld, int64_t nrows_pad, int64_t nrows, int64_t ncols, int64_t row_offset,
                          uint64_t seed, float lo, float hi, hipStream_t stream) {
+    launch_synth_matrix_block(A, ld, nrows_pad, nrows, ncols, row_offset, 0, ncols, seed, lo, hi, stream);
+}
+
+void launch_synth_matrix_block(float* A, int64_t ld, int64_t nrows_pad, int64_t nrows, int64_t ncols,
+                               int64_t row_offset, int64_t col_offset, int64_t ncols_total, uint64_t seed, float lo,
+                               float hi, hipStream_t stream) {
     const int64_t total4 = nrows_pad * (ld / 4);
     int64_t nblk = (total4 + 255) / 256;
     if (nblk > 65536) nblk = 65536;
     if (nblk < 1) nblk = 1;
     hipLaunchKernelGGL(k_synth_matrix, dim3((unsigned)nblk), dim3(256), 0, stream, A, ld, nrows_pad, nrows, ncols,
-                       row_offset, seed, lo, hi);
+                       row_offset, col_offset, ncols_total, seed, lo, hi);
     check_launch("k_synth_matrix");
 }
 

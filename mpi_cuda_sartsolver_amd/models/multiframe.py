@@ -33,6 +33,8 @@ class MultiFrameSARTSolver:
     def __init__(self, rtm: DenseRTM, laplacian: Optional[LaplacianCSR] = None, comm: Optional[Communicator] = None,
                  params: Optional[SolverParams] = None, logarithmic: bool = False, batch: int = NF,
                  check_interval: int = 16, allow_zero_tolerance: bool = False):
+        if getattr(rtm, "is_column_shard", False):
+            raise NotImplementedError("the multi-frame engine runs on row shards (use SARTSolver for column shards)")
         self.k = hip()
         self.rtm = rtm
         self.dev = rtm.device

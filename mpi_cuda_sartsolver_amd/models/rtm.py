@@ -94,15 +94,22 @@ def fused_geometry(ld: int, num_cus: int, variant: int = 6, rows_per_tile: Optio
 
 
 class DenseRTM:
-    """Local row shard [row_offset, row_offset + npixel) x [0, nvoxel) of the RTM on one GPU."""
+    """Local shard [row_offset, row_offset + npixel) x [col_offset, col_offset + nvoxel) of the RTM on one
+    GPU: a row shard (col_offset 0, nvoxel = all voxels; the reference layout) or a column shard (all pixel
+    rows of some voxels, ``col_offset`` / ``nvoxel_total`` set)."""
 
     def __init__(self, npixel: int, nvoxel: int, row_offset: int = 0, device: Optional[torch.device] = None,
-                 ld: Optional[int] = None, row_align: int = 64):
+                 ld: Optional[int] = None, row_align: int = 64, col_offset: int = 0,
+                 nvoxel_total: Optional[int] = None):
         if npixel <= 0 or nvoxel <= 0:
             raise ValueError("RTM shard must have npixel > 0 and nvoxel > 0")
         self.npixel = int(npixel)
         self.nvoxel = int(nvoxel)
         self.row_offset = int(row_offset)
+        self.col_offset = int(col_offset)
+        self.nvoxel_total = int(nvoxel_total) if nvoxel_total is not None else self.nvoxel
+        if self.col_offset < 0 or self.col_offset + self.nvoxel > self.nvoxel_total:
+            raise ValueError("column shard outside [0, nvoxel_total)")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.ld = int(ld) if ld is not None else choose_ld(self.nvoxel)
         if self.ld % 64 or self.ld < self.nvoxel:
@@ -125,20 +132,28 @@ class DenseRTM:
         if self.nrows_pad > self.npixel:
             self.A[self.npixel:].zero_()
 
+    @property
+    def is_column_shard(self) -> bool:
+        return self.nvoxel < self.nvoxel_total
+
     @classmethod
     def synthetic(cls, npixel: int, nvoxel: int, row_offset: int = 0, seed: int = 1234, lo: float = 0.0,
-                  hi: float = 1.0, device=None, ld=None) -> "DenseRTM":
-        """On-device random dense RTM; element (p, v) depends only on (seed, global p, v)."""
-        m = cls(npixel, nvoxel, row_offset, device=device, ld=ld)
+                  hi: float = 1.0, device=None, ld=None, col_offset: int = 0,
+                  nvoxel_total: Optional[int] = None) -> "DenseRTM":
+        """On-device random dense RTM; element (p, v) depends only on (seed, global p, global v), so row and
+        column shards of one global matrix agree bit for bit."""
+        m = cls(npixel, nvoxel, row_offset, device=device, ld=ld, col_offset=col_offset, nvoxel_total=nvoxel_total)
         hip().synth_matrix(m.A.data_ptr(), m.ld, m.nrows_pad, m.npixel, m.nvoxel, m.row_offset, int(seed), float(lo),
-                           float(hi), m.stream_handle)
+                           float(hi), m.stream_handle, m.col_offset, m.nvoxel_total)
         return m
 
     @classmethod
-    def from_dense(cls, A_local, row_offset: int = 0, device=None, ld=None) -> "DenseRTM":
+    def from_dense(cls, A_local, row_offset: int = 0, device=None, ld=None, col_offset: int = 0,
+                   nvoxel_total: Optional[int] = None) -> "DenseRTM":
         """Upload a host (numpy / torch) dense block [npixel, nvoxel]."""
         t = torch.as_tensor(A_local, dtype=torch.float32)
-        m = cls(t.shape[0], t.shape[1], row_offset, device=device, ld=ld)
+        m = cls(t.shape[0], t.shape[1], row_offset, device=device, ld=ld, col_offset=col_offset,
+                nvoxel_total=nvoxel_total)
         m.A.zero_()
         m.A[: m.npixel, : m.nvoxel].copy_(t.to(m.device, non_blocking=False))
         return m

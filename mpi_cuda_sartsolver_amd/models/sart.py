@@ -101,7 +101,7 @@ class SARTSolver:
                  logarithmic: bool = False, use_fused: bool = True, check_interval: int = 16,
                  allow_zero_tolerance: bool = False, fused_variant: Optional[int] = None,
                  fused_rows_per_tile: Optional[int] = None, use_graph: Optional[bool] = None,
-                 fused_min_bytes: float = 0.0):
+                 fused_min_bytes: float = 0.0, partition: Optional[str] = None):
         self.k = hip()
         self.rtm = rtm
         self.dev = rtm.device
@@ -110,7 +110,11 @@ class SARTSolver:
         self.params.validate(allow_zero_tolerance)
         self.log = bool(logarithmic)
         self.L = laplacian if (laplacian is not None and laplacian.nnz > 0 and self.params.beta_laplace > 0) else None
-        if self.L is not None and self.L.n != rtm.nvoxel:
+        # "rows" (reference layout) or "cols" (voxel shard); default: from the shard
+        if partition not in (None, "rows", "cols"):
+            raise ValueError("partition must be 'rows' or 'cols'")
+        self.column_shard = partition == "cols" or (partition is None and bool(getattr(rtm, "is_column_shard", False)))
+        if self.L is not None and self.L.n != getattr(rtm, "nvoxel_total", rtm.nvoxel):
             raise ValueError("Laplacian and ray-transfer matrices have different number of voxels.")
         if fused_variant is None:
             fused_variant = int(os.environ.get("SART_FUSED_VARIANT", "6"))
@@ -133,6 +137,10 @@ class SARTSolver:
             use_graph = os.environ.get("SART_GRAPH", "0") == "1"
         cfg.use_graph = bool(use_graph)
         cfg.fused_min_bytes = float(fused_min_bytes)  # smaller shards use the two-pass kernels
+        if self.column_shard:  # all pixel rows of voxels [col_offset, +nvoxel): two-pass, pixel all-reduce
+            cfg.column_shard = True
+            cfg.col_offset = int(getattr(rtm, "col_offset", 0))
+            cfg.nvoxel_total = int(getattr(rtm, "nvoxel_total", rtm.nvoxel))
         device = self.dev.index if self.dev.index is not None else 0
         self.native_comm = native_communicator(self.comm, device)
         self.engine = self.k.Engine(device, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld,
@@ -159,8 +167,9 @@ class SARTSolver:
         return self.engine.ray_length()
 
     def solve(self, measurement, solution=None) -> SolveResult:
-        """Solve one frame. ``measurement``: this rank's pixel slice (fp64); ``solution``: warm start
-        (fp64, nvoxel) or None for the default initial guess."""
+        """Solve one frame. ``measurement``: this rank's pixel slice (fp64; ALL pixels for a column shard);
+        ``solution``: warm start (fp64, this shard's voxels) or None for the default initial guess. The
+        solution holds this shard's voxels (all of them for a row shard; see ``gather_solution``)."""
         g = _host_f64(measurement)
         x0 = None if solution is None else _host_f64(solution)
         x, info = self.engine.solve(g, x0)
@@ -171,6 +180,16 @@ class SARTSolver:
         return SolveResult(solution=x, status=status, iterations=int(info["iterations"]),
                            convergence=float(info["convergence"]), used_fused=bool(info["used_fused"]),
                            elapsed_ms=float(info["ms"]))
+
+    def gather_solution(self, x_local: np.ndarray) -> np.ndarray:
+        """Full solution vector from the column shards of every rank (identity for a row shard)."""
+        if not self.column_shard:
+            return x_local
+        parts = self.comm.all_gather_object((int(getattr(self.rtm, "col_offset", 0)), np.asarray(x_local)))
+        out = np.zeros(int(getattr(self.rtm, "nvoxel_total", self.rtm.nvoxel)), dtype=np.float64)
+        for off, xs in parts:
+            out[off: off + xs.size] = xs
+        return out
 
     def forward_project(self, x_local) -> np.ndarray:
         """f = A x for this shard (utility / tests)."""

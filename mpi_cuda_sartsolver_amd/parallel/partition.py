@@ -3,7 +3,8 @@
 Same balanced 1-D block partition as the reference (reference main.cpp:67-68): the first
 ``npixel % nproc`` ranks get one extra row; every rank holds all voxels. Forward projection is then
 rank-local and the back-projection yields voxel partial sums that are all-reduced once per iteration.
-A column partition helper is provided for the (optional) voxel-sharded layout.
+``col_partition`` gives the optional voxel-sharded layout (every rank holds all pixel rows of a
+block of voxels; the per-iteration all-reduce then carries the pixel vector A.x instead).
 """
 from __future__ import annotations
 
@@ -32,6 +33,11 @@ def block_partition(n: int, nparts: int, part: int) -> Block:
 def row_partition(npixel: int, world_size: int, rank: int) -> Block:
     """Pixel rows owned by ``rank`` (reference main.cpp:67-68)."""
     return block_partition(npixel, world_size, rank)
+
+
+def col_partition(nvoxel: int, world_size: int, rank: int) -> Block:
+    """Voxel columns owned by ``rank`` in the column-shard layout (EngineConfig::column_shard)."""
+    return block_partition(nvoxel, world_size, rank)
 
 
 def all_blocks(n: int, nparts: int) -> list[Block]:

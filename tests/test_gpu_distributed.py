@@ -32,7 +32,8 @@ def _run(nproc, out, extra):
     return np.load(out + ".npy"), json.load(open(out + ".json"))
 
 
-@pytest.mark.parametrize("extra", [[], ["--logarithmic"], ["--multiframe"], ["--multiframe", "--logarithmic"]])
+@pytest.mark.parametrize("extra", [[], ["--logarithmic"], ["--multiframe"], ["--multiframe", "--logarithmic"],
+                                   ["--columns"], ["--columns", "--logarithmic"]])
 def test_gpu_solver_rank_invariance(tmp_path, extra):
     x1, m1 = _run(1, str(tmp_path / "r1"), extra)
     x2, m2 = _run(2, str(tmp_path / "r2"), extra)
@@ -41,3 +42,15 @@ def test_gpu_solver_rank_invariance(tmp_path, extra):
         assert np.linalg.norm(x - x1) / np.linalg.norm(x1) < 2e-3
         for a, b in zip(m, m1):
             assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3
+
+
+@pytest.mark.parametrize("log", [False, True])
+def test_column_shard_matches_row_shard(tmp_path, log):
+    """The voxel-sharded layout (all-reduce of A.x per sweep) solves the same problem as the reference's
+    pixel-sharded layout (all-reduce of the correction)."""
+    extra = ["--logarithmic"] if log else []
+    xr, mr = _run(1, str(tmp_path / "rows"), extra)
+    xc, mc = _run(2, str(tmp_path / "cols"), extra + ["--columns"])
+    assert np.linalg.norm(xc - xr) / np.linalg.norm(xr) < 2e-3
+    for a, b in zip(mc, mr):
+        assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--logarithmic", action="store_true")
     ap.add_argument("--fused", action="store_true")
     ap.add_argument("--multiframe", action="store_true")
+    ap.add_argument("--columns", action="store_true", help="column (voxel) shards instead of row shards")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     import numpy as np
@@ -25,13 +26,20 @@ def main():
     from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
     from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
     from mpi_cuda_sartsolver_amd.parallel.comm import init_distributed
-    from mpi_cuda_sartsolver_amd.parallel.partition import row_partition
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.parallel.partition import col_partition, row_partition
     from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
 
     comm = init_distributed(use_gpu=True)
     dev = torch.device("cuda", torch.cuda.current_device())
-    b = row_partition(a.npix, comm.world_size, comm.rank)
-    prob = make_problem(b.size, a.nvox, row_offset=b.offset, seed=7, device=dev, saturate_fraction=0.02)
+    if a.columns:  # every rank: all pixels (full measurement) and the RTM columns of its voxel block
+        cb = col_partition(a.nvox, comm.world_size, comm.rank)
+        prob = make_problem(a.npix, a.nvox, seed=7, device=dev, saturate_fraction=0.02)
+        prob.rtm = DenseRTM.synthetic(a.npix, cb.size, 0, seed=7, device=dev, col_offset=cb.offset,
+                                      nvoxel_total=a.nvox)
+    else:
+        b = row_partition(a.npix, comm.world_size, comm.rank)
+        prob = make_problem(b.size, a.nvox, row_offset=b.offset, seed=7, device=dev, saturate_fraction=0.02)
     L = LaplacianCSR.grid_3d(16, 16, 16, device=dev) if a.nvox == 4096 else None
     params = SolverParams(max_iterations=a.iters, conv_tolerance=1e-6, beta_laplace=1e-3)
     if a.multiframe:
@@ -43,10 +51,11 @@ def main():
         x = np.stack([r.solution for r in res])
         meta = [dict(status=r.status, iterations=r.iterations) for r in res]
     else:
-        s = SARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic, use_fused=a.fused)
+        s = SARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic, use_fused=a.fused,
+                       partition="cols" if a.columns else None)
         r = s.solve(prob.measurement)
         r2 = s.solve(prob.measurement, solution=r.solution)  # warm start path
-        x = np.stack([r.solution, r2.solution])
+        x = np.stack([s.gather_solution(r.solution), s.gather_solution(r2.solution)])
         meta = [dict(status=r.status, iterations=r.iterations, fused=r.used_fused),
                 dict(status=r2.status, iterations=r2.iterations)]
     if comm.rank == 0:

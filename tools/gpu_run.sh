@@ -42,6 +42,7 @@ for step in "$@"; do
     profmf) for nf in 16 32 64; do
               run rocprof_mf$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mf$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 || exit 1
             done ;;
+    benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchlap) run bench_lap 600 python bench.py --steps 5 --warmup 1 --laplacian ;;
     probe) run probe 600 python tools/probe.py ;;
     trace) run fused_trace 600 python tools/fused_trace.py ;;
