@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
 #pragma unroll
             for (int r = 0; r < T; ++r)
 #pragma unroll
-                for (int k = 0; k < K; ++k) dst[r][k] = src[r * ld4 + k * 64];
+                for (int k = 0; k < K; ++k) dst[r][k] = load_stream(src + r * ld4 + k * 64);
         };
         // prologue: tiles 0 .. AH-1
         [&]<int... Is>(std::integer_sequence<int, Is...>) {
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
 #pragma unroll
             for (int r = 0; r < T; ++r)
 #pragma unroll
-                for (int k = 0; k < K; ++k) dst[r * K + k] = src[r * ld4 + k * 64];
+                for (int k = 0; k < K; ++k) dst[r * K + k] = load_stream(src + r * ld4 + k * 64);
         };
 #pragma unroll
         for (int i = 0; i < AH; ++i)
@@ -545,7 +545,7 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
         auto load_tile = [&](float4(&dst)[KW], int64_t t) {
             const float4* src = a4 + (t_begin + t) * T * ld4;
 #pragma unroll
-            for (int k = 0; k < KW; ++k) dst[k] = src[k * 64];
+            for (int k = 0; k < KW; ++k) dst[k] = load_stream(src + k * 64);
         };
 #pragma unroll
         for (int i = 0; i < AH; ++i)
@@ -843,7 +843,7 @@ __global__ __launch_bounds__(kFused5Threads) void k_fused_sweep_rows2(
         auto load_tile = [&](float4(&dst)[KW], int64_t t) {
             const float4* src = a4 + (t_begin + t) * T * ld4;
 #pragma unroll
-            for (int k = 0; k < KW; ++k) dst[k] = src[k * 64];
+            for (int k = 0; k < KW; ++k) dst[k] = load_stream(src + k * 64);
         };
 #pragma unroll
         for (int i = 0; i < AH; ++i)

@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void k_forward(const float* __restrict__ A, in
         const float4 xv = x4[c];
         float4 av[RPB];
 #pragma unroll
-        for (int r = 0; r < RPB; ++r) av[r] = a4[r * ld4 + c];
+        for (int r = 0; r < RPB; ++r) av[r] = load_stream(a4 + r * ld4 + c);
 #pragma unroll
         for (int r = 0; r < RPB; ++r) acc[r] += dot4(av[r], xv);
     }
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void k_backproject(const float* __restrict__ A
         float4 av[UNR];
         float wv[UNR];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) av[u] = a4[(r + u) * ld4];
+        for (int u = 0; u < UNR; ++u) av[u] = load_stream(a4 + (r + u) * ld4);
 #pragma unroll
         for (int u = 0; u < UNR; ++u) wv[u] = w[r + u];
 #pragma unroll
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void k_backproject(const float* __restrict__ A
             fma4(acc1, av[u + 1], wv[u + 1]);
         }
     }
-    for (; r < r_end; ++r) fma4(acc0, a4[r * ld4], w[r]);
+    for (; r < r_end; ++r) fma4(acc0, load_stream(a4 + r * ld4), w[r]);
 
     acc0.x += acc1.x;
     acc0.y += acc1.y;

@@ -71,6 +71,21 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// Streaming read of the RTM: every byte of A is read once per sweep by one CU and never again before it
+// has left every cache, so the loads carry the non-temporal hint (MI355X_MICROARCH.md 'nt-weights').
+#ifndef SART_STREAM_NT
+#define SART_STREAM_NT 1
+#endif
+typedef float sart_f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 load_stream(const float4* p) {
+#if SART_STREAM_NT
+    const sart_f4v v = __builtin_nontemporal_load(reinterpret_cast<const sart_f4v*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+
 __device__ __forceinline__ float dot4(const float4 a, const float4 b) {
     return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
 }
