@@ -55,6 +55,11 @@ __device__ __forceinline__ void trace_stamp(int b, int64_t tile, int ev) {
         g_fused_trace[((int64_t)b * g_fused_trace_tiles + tile) * 4 + ev] = __builtin_amdgcn_s_memrealtime();
 }
 
+// LDS words polled by other waves of the workgroup (volatile, explicit local address space: ds_read /
+// ds_write, counted on lgkmcnt only).
+typedef __attribute__((address_space(3))) volatile float lds_vfloat;
+typedef __attribute__((address_space(3))) volatile int lds_vint;
+
 __device__ __forceinline__ uint64_t make_granule(int epoch, float v) {
     return ((uint64_t)(uint32_t)epoch << 32) | (uint64_t)__float_as_uint(v);
 }
@@ -103,8 +108,9 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
         }
 
         float4 buf[R][T][K];
+        const int64_t tlast = ntiles - 1 - t_begin;  // unconditional clamped loads: see k_fused_sweep_rows
         auto load_tile = [&](float4(&dst)[T][K], int64_t t) {
-            const float4* src = a4 + (t_begin + t) * T * ld4;
+            const float4* src = a4 + (t_begin + (t < tlast ? t : tlast)) * T * ld4;
 #pragma unroll
             for (int r = 0; r < T; ++r)
 #pragma unroll
@@ -112,7 +118,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
         };
         // prologue: tiles 0 .. AH-1
         [&]<int... Is>(std::integer_sequence<int, Is...>) {
-            ((Is < nt ? load_tile(buf[Is], Is) : void()), ...);
+            (load_tile(buf[Is], Is), ...);
         }(std::make_integer_sequence<int, AH>{});
 
         auto step = [&](auto bbc, int64_t t) {
@@ -138,7 +144,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
                     for (int k = 0; k < K; ++k) fma4(acc[k], buf[bp][r][k], wr);
                 }
             }
-            if (t - L + R < nt) load_tile(buf[bp], t - L + R);
+            load_tile(buf[bp], t - L + R);
         };
 
         for (int64_t t0 = 0; t0 < nsteps; t0 += R) {
@@ -288,16 +294,16 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
             acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         float4 fl[AH][TK];
+        const int64_t tlast = ntiles - 1 - t_begin;  // unconditional clamped loads: see k_fused_sweep_rows
         auto load_tile = [&](float4(&dst)[TK], int64_t t) {
-            const float4* src = a4 + (t_begin + t) * T * ld4;
+            const float4* src = a4 + (t_begin + (t < tlast ? t : tlast)) * T * ld4;
 #pragma unroll
             for (int r = 0; r < T; ++r)
 #pragma unroll
                 for (int k = 0; k < K; ++k) dst[r * K + k] = load_stream(src + r * ld4 + k * 64);
         };
 #pragma unroll
-        for (int i = 0; i < AH; ++i)
-            if (i < nt) load_tile(fl[i], i);
+        for (int i = 0; i < AH; ++i) load_tile(fl[i], i);
 
         auto step = [&](auto bbc, int64_t t) {
             constexpr int bb = decltype(bbc)::value;  // register slot of tile t (t % AH)
@@ -313,8 +319,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
                 float4* slot = ring + (int)(t % NL) * (4 * TK * 64);
 #pragma unroll
                 for (int q = 0; q < TK; ++q) slot[q * 64] = fl[bb][q];
-                if (t + AH < nt) load_tile(fl[bb], t + AH);
             }
+            load_tile(fl[bb], t + AH);
             __syncthreads();
             if (t >= L && t - L < nt) {
                 const int64_t u = t - L;
@@ -482,11 +488,14 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
     extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64]
     float4* s_xs = s_ring + NL * 4 * KW * 64;                         // [WPR][KW][64] if XS_LDS
     float* s_small = reinterpret_cast<float*>(s_xs + (XS_LDS ? WPR * KW * 64 : 0));
-    volatile float* s_part = s_small;                                      // [NS][4]
-    volatile float* s_w = s_small + NS * 4;                                 // [NS][4]
-    volatile int* s_pflag = reinterpret_cast<volatile int*>(s_small + 2 * NS * 4);  // [NS][4]
-    volatile int* s_wflag = s_pflag + NS * 4;                               // [NS]
-    volatile int* s_tick = s_wflag + NS;                                    // [2]
+    // Hand-off words: volatile through explicit LDS (address_space(3)) pointers. Through generic pointers
+    // the compiler keeps volatile accesses as FLAT instructions, which count on vmcnt too, so every flag
+    // poll waited vmcnt(0) and drained the compute waves' in-flight A tiles.
+    lds_vfloat* s_part = (lds_vfloat*)s_small;                                // [NS][4]
+    lds_vfloat* s_w = (lds_vfloat*)(s_small + NS * 4);                        // [NS][4]
+    lds_vint* s_pflag = (lds_vint*)(s_small + 2 * NS * 4);                    // [NS][4]
+    lds_vint* s_wflag = s_pflag + NS * 4;                                     // [NS]
+    lds_vint* s_tick = s_wflag + NS;                                          // [2]
 
     if (st->done) return;
     const int epoch = st->epoch;
@@ -542,14 +551,19 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
             acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         float4 fl[RS][KW];
+        // Tile loads are issued unconditionally, clamped to the last tile of the matrix (past the group's
+        // end they re-read valid rows that nobody uses). A guarded load makes the vmcnt bookkeeping depend
+        // on the path, and the compiler then waits for EVERY load in flight wherever a tile is consumed,
+        // which collapses the AH-tile pipeline to one tile.
+        const int64_t tlast = ntiles - 1 - t_begin;
         auto load_tile = [&](float4(&dst)[KW], int64_t t) {
-            const float4* src = a4 + (t_begin + t) * T * ld4;
+            const int64_t tc = t < tlast ? t : tlast;
+            const float4* src = a4 + (t_begin + tc) * T * ld4;
 #pragma unroll
             for (int k = 0; k < KW; ++k) dst[k] = load_stream(src + k * 64);
         };
 #pragma unroll
-        for (int i = 0; i < AH; ++i)
-            if (i < nt) load_tile(fl[i], i);
+        for (int i = 0; i < AH; ++i) load_tile(fl[i], i);
         bool stuck = false;
         unsigned long long stall = 0, nstall = 0;
 
@@ -580,7 +594,7 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
             }
             // park tile t - D (its LDS slot held tile t - D - NL, back-projected in step t - 1)
             if (t - D >= 0 && t - D < nt) park(fl[bp], t - D);
-            if (t + AH < nt) load_tile(fl[bp], t + AH);  // slot bp is free again
+            load_tile(fl[bp], t + AH);  // slot bp is free again
             if (t >= L && t - L < nt) {
                 const int64_t u = t - L;
                 const int ws = (int)(u & (NS - 1));
@@ -807,9 +821,9 @@ __global__ __launch_bounds__(kFused5Threads) void k_fused_sweep_rows2(
 
     extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64]
     float* s_small = reinterpret_cast<float*>(s_ring + NL * 4 * KW * 64);
-    volatile float* s_w = s_small;                                                  // [NS][4]
-    volatile int* s_pflag = reinterpret_cast<volatile int*>(s_small + NS * 4);      // [NS][4]
-    volatile int* s_wflag = s_pflag + NS * 4;                                       // [NS]
+    lds_vfloat* s_w = (lds_vfloat*)s_small;                                         // [NS][4]
+    lds_vint* s_pflag = (lds_vint*)(s_small + NS * 4);                              // [NS][4]
+    lds_vint* s_wflag = s_pflag + NS * 4;                                           // [NS]
 
     if (st->done) return;
     const int epoch = st->epoch;
@@ -840,14 +854,14 @@ __global__ __launch_bounds__(kFused5Threads) void k_fused_sweep_rows2(
             acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         float4 fl[AH][KW];
+        const int64_t tlast = ntiles - 1 - t_begin;  // unconditional clamped loads: see k_fused_sweep_rows
         auto load_tile = [&](float4(&dst)[KW], int64_t t) {
-            const float4* src = a4 + (t_begin + t) * T * ld4;
+            const float4* src = a4 + (t_begin + (t < tlast ? t : tlast)) * T * ld4;
 #pragma unroll
             for (int k = 0; k < KW; ++k) dst[k] = load_stream(src + k * 64);
         };
 #pragma unroll
-        for (int i = 0; i < AH; ++i)
-            if (i < nt) load_tile(fl[i], i);
+        for (int i = 0; i < AH; ++i) load_tile(fl[i], i);
         bool stuck = false;
 
         auto step = [&](auto bbc, int64_t t) {
@@ -866,8 +880,8 @@ __global__ __launch_bounds__(kFused5Threads) void k_fused_sweep_rows2(
                 float4* slot = ring + (int)(t % NL) * (4 * KW * 64);
 #pragma unroll
                 for (int k = 0; k < KW; ++k) slot[k * 64] = fl[bb][k];
-                if (t + AH < nt) load_tile(fl[bb], t + AH);
             }
+            load_tile(fl[bb], t + AH);
             if (t >= L && t - L < nt) {
                 const int64_t u = t - L;
                 const int ws = (int)(u & (NS - 1));
