@@ -163,13 +163,17 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
         double F = 0.0;
         uint64_t pv[2][kGatherRegs];  // poll registers, double buffered by step parity
 
+        // Polls are issued unconditionally at clamped addresses (tile in [0, ntiles), granule < n; lanes past
+        // n re-read granule n - 1 and are masked when summing), so the compiler counts the polls in flight
+        // instead of draining them (see load_tile in k_fused_sweep_rows).
+        const int64_t ulast = ntiles - 1 - t_begin;
         auto issue_poll = [&](uint64_t(&dst)[kGatherRegs], int64_t u) {
-            const uint64_t* g = gran + (t_begin + u) * (int64_t)n;
+            const int64_t uc = u < 0 ? 0 : (u < ulast ? u : ulast);
+            const uint64_t* g = gran + (t_begin + uc) * (int64_t)n;
 #pragma unroll
             for (int m = 0; m < kGatherRegs; ++m) {
                 const int idx = lane + 64 * m;
-                dst[m] = (idx < n) ? __hip_atomic_load(g + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                   : make_granule(epoch, 0.f);
+                dst[m] = __hip_atomic_load(g + (idx < n ? idx : n - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         };
 
@@ -194,7 +198,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
             float s = 0.f;
             if (!failed) {
 #pragma unroll
-                for (int m = 0; m < kGatherRegs; ++m) s += __uint_as_float((uint32_t)v[m]);
+                for (int m = 0; m < kGatherRegs; ++m)
+                    s += (lane + 64 * m < n) ? __uint_as_float((uint32_t)v[m]) : 0.f;
             }
             // lanes l and l' hold the same row iff l == l' (mod T): butterfly over the other bits
 #pragma unroll
@@ -222,7 +227,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
                 __hip_atomic_store(g, make_granule(epoch, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             const int64_t un = t - L + 2;  // tile whose gather starts now (published >= L-2 steps ago)
-            if (un >= 0 && un < nt) issue_poll(pv[p], un);
+            issue_poll(pv[p], un);
             const int64_t uc = t - L + 1;  // tile whose gather was issued last step; its w is due next step
             if (uc >= 0 && uc < nt) finish_tile(pv[p ^ 1], uc);
         };
@@ -350,13 +355,17 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
         double F = 0.0;
         uint64_t pv[2][kGatherRegs];
 
+        // Polls are issued unconditionally at clamped addresses (tile in [0, ntiles), granule < n; lanes past
+        // n re-read granule n - 1 and are masked when summing), so the compiler counts the polls in flight
+        // instead of draining them (see load_tile in k_fused_sweep_rows).
+        const int64_t ulast = ntiles - 1 - t_begin;
         auto issue_poll = [&](uint64_t(&dst)[kGatherRegs], int64_t u) {
-            const uint64_t* g = gran + (t_begin + u) * (int64_t)n;
+            const int64_t uc = u < 0 ? 0 : (u < ulast ? u : ulast);
+            const uint64_t* g = gran + (t_begin + uc) * (int64_t)n;
 #pragma unroll
             for (int m = 0; m < kGatherRegs; ++m) {
                 const int idx = lane + 64 * m;
-                dst[m] = (idx < n) ? __hip_atomic_load(g + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                   : make_granule(epoch, 0.f);
+                dst[m] = __hip_atomic_load(g + (idx < n ? idx : n - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         };
         auto finish_tile = [&](uint64_t(&v)[kGatherRegs], int64_t u) {
@@ -379,7 +388,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
             float s = 0.f;
             if (!failed) {
 #pragma unroll
-                for (int m = 0; m < kGatherRegs; ++m) s += __uint_as_float((uint32_t)v[m]);
+                for (int m = 0; m < kGatherRegs; ++m)
+                    s += (lane + 64 * m < n) ? __uint_as_float((uint32_t)v[m]) : 0.f;
             }
 #pragma unroll
             for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
@@ -409,7 +419,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
                 __hip_atomic_store(g, make_granule(epoch, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             const int64_t un = t - L + 2;
-            if (un >= 0 && un < nt) issue_poll(pv[p], un);
+            issue_poll(pv[p], un);
             const int64_t uc = t - L + 1;
             if (uc >= 0 && uc < nt) finish_tile(pv[p ^ 1], uc);
         };
@@ -690,13 +700,15 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
         double F = 0.0;
         constexpr int GR = kRowsGather / 64;  // poll registers per lane (J * T <= kRowsGather)
         uint64_t pv[PQ][GR];
+        // unconditional clamped polls (see issue_poll in k_fused_sweep): counted vmcnt, PQ polls in flight
+        const int64_t ulast = ntiles - 1 - t_begin;
         auto issue_poll = [&](uint64_t(&dst)[GR], int64_t u) {
-            const uint64_t* g = gran + (t_begin + u) * (int64_t)n;
+            const int64_t uc = u < 0 ? 0 : (u < ulast ? u : ulast);
+            const uint64_t* g = gran + (t_begin + uc) * (int64_t)n;
 #pragma unroll
             for (int m = 0; m < GR; ++m) {
                 const int idx = lane + 64 * m;
-                dst[m] = (idx < n) ? __hip_atomic_load(g + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                   : make_granule(epoch, 0.f);
+                dst[m] = __hip_atomic_load(g + (idx < n ? idx : n - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         };
         unsigned long long xwait = 0, xrepoll = 0;
@@ -727,7 +739,7 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
             float s = 0.f;
             if (!failed && !(dbg & 1)) {
 #pragma unroll
-                for (int m = 0; m < GR; ++m) s += __uint_as_float((uint32_t)v[m]);
+                for (int m = 0; m < GR; ++m) s += (lane + 64 * m < n) ? __uint_as_float((uint32_t)v[m]) : 0.f;
             }
 #pragma unroll
             for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
@@ -774,7 +786,7 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
                     if (DIAG && lane == 0 && !SPLIT) trace_stamp(b, u, 2);
                 }
             }
-            if (u >= PD && u - PD < nt && !(dbg & 1)) issue_poll(pv[p], u - PD);
+            issue_poll(pv[p], u - PD);  // (also with dbg & 1: the results are then ignored)
             const int64_t f = u - PD - PQ + 1;  // polled PQ - 1 steps ago into pv[(p + 1) % PQ]
             if (f >= 0 && f < nt) finish_tile(pv[(p + 1) % PQ], f);
         };
@@ -963,7 +975,8 @@ __global__ __launch_bounds__(kFused5Threads) void k_fused_sweep_rows2(
                     for (int m = 0; m < kGatherRegs; ++m) ok &= ((int)(v[m] >> 32) == epoch);
                     if (__all(ok)) {
 #pragma unroll
-                        for (int m = 0; m < kGatherRegs; ++m) s += __uint_as_float((uint32_t)v[m]);
+                        for (int m = 0; m < kGatherRegs; ++m)
+                    s += (lane + 64 * m < n) ? __uint_as_float((uint32_t)v[m]) : 0.f;
                         break;
                     }
                     if (++spins > kSpinLimit) {
