@@ -25,12 +25,12 @@ METRIC = "SART iterations/sec (whole node) on dense RTM; GFLOPS at 1/2/4/8 MI355
 
 # BASELINE.json configs as weak-scaling presets (rows per GPU): at N = 8 GPUs "512kx256k" is the
 # 524288 x 262144 RTM (68.7 GB per GPU) and "2tb" is 1966080 x 262144 fp32 = 2.06 TB (258 GB per GPU)
-# with the Laplacian and a 16-frame batch; "256k" fills one GPU with a 262144 x 262144 shard (275 GB).
+# with the Laplacian and a 64-frame batch; "256k" fills one GPU with a 262144 x 262144 shard (275 GB).
 PRESETS = {
     "64k": dict(npix=65536, nvox=65536, iters=100),
     "256k": dict(npix=262144, nvox=262144, iters=20),
     "512kx256k": dict(npix=65536, nvox=262144, iters=100),
-    "2tb": dict(npix=245760, nvox=262144, iters=20, frames=16, laplacian=True),
+    "2tb": dict(npix=245760, nvox=262144, iters=20, frames=64, laplacian=True),
 }
 
 

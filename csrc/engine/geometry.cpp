@@ -28,10 +28,14 @@ FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_
         rows_per_tile = (e && *e) ? std::atoi(e) : 0;
     }
     if (variant == 4 || variant == 6) {
+        // Rows per tile: the requested T, else the largest of 4, 2, 1 whose row group fits the XCD (T = 4 at
+        // ld = 64k, 2 at 128k, 1 at 256k: 6.5-6.9 TB/s, against 4.0-4.7 TB/s for variant 3 at those widths,
+        // profiles/probe_r1_fused_T.jsonl).
         const int per_xcd = num_cus / 8;
-        const int T = rows_per_tile > 0 ? rows_per_tile : 4;  // T = 4 measured fastest (fused_sweep.hip)
-        const int64_t slab = (T == 1 || T == 2 || T == 4) ? 8192 / T : 0;
-        if (slab > 0 && ld % slab == 0 && ld / slab > 0) {
+        for (const int T : {4, 2, 1}) {
+            if (rows_per_tile > 0 && T != rows_per_tile) continue;
+            const int64_t slab = 8192 / T;
+            if (ld % slab != 0 || ld / slab == 0) continue;
             const int J = (int)(ld / slab);
             if (variant == 6 && num_cus % 8 == 0 && per_xcd % J == 0) {
                 g.K = T, g.J = J, g.I = 8 * (per_xcd / J), g.grid = g.I * g.J, g.variant = 6, g.T = T;

@@ -51,9 +51,9 @@ def fused_geometry(ld: int, num_cus: int, variant: int = 6, rows_per_tile: Optio
 
     variant 6 (default): XCD-local row groups (L2 hand-offs); the four compute waves of a workgroup
     cover T rows x (4 / T) sub-slabs of 2048 columns, so a row is split over J = ld * T / 8192
-    workgroups (T = rows_per_tile or env SART_FUSED_T; default 4, the fastest on MI355X at every
-    measured shape -- profiles/probe_r1_rows_per_tile.jsonl; where T = 4 does not fit, variant 3 beats
-    T = 1/2 and is used instead). Variant 4: same kernel with blockIdx row groups.
+    workgroups (T = rows_per_tile or env SART_FUSED_T; default: the largest of 4, 2, 1 whose row group
+    fits an XCD -- 6.5-6.9 TB/s at 64k / 128k / 256k columns, profiles/probe_r1_fused_T.jsonl; variant 3
+    only beyond that). Variant 4: same kernel with blockIdx row groups.
     Variant 5: 2048-column slabs, two exchange waves. Variants 0-3: slabs of 1024*K columns, K chosen
     for <= 32 slabs (3: tiles parked in LDS). None: no fused path.
     """
@@ -61,7 +61,7 @@ def fused_geometry(ld: int, num_cus: int, variant: int = 6, rows_per_tile: Optio
         rows_per_tile = int(os.environ["SART_FUSED_T"])
     if variant in (4, 6):
         per_xcd = num_cus // 8
-        for T in ((rows_per_tile,) if rows_per_tile else (4,)):
+        for T in ((rows_per_tile,) if rows_per_tile else (4, 2, 1)):
             slab = 8192 // T
             if T not in (1, 2, 4) or ld % slab or ld // slab == 0:
                 continue

@@ -88,7 +88,10 @@ def main():
         emit(kind="kernel", op="backproject", P=P, V=V, nsplit=ns, ms=med, GBps=nbytes / med / 1e6,
              best_GBps=nbytes / best / 1e6)
 
-        cfgs = [(6, 4, 4), (6, 4, 2), (6, 4, 0), (3, None, 0)]
+        cfgs = [(6, 4, 4), (6, 2, 4), (6, 1, 4), (6, 4, 2), (6, 4, 0), (3, None, 0)]
+        if os.environ.get("PROBE_CFGS"):  # e.g. "6:4:4,6:1:4,3:0:0"
+            cfgs = [tuple((int(v) or None) if i == 1 else int(v) for i, v in enumerate(c.split(":")))
+                    for c in os.environ["PROBE_CFGS"].split(",")]
         for variant, T, sched in cfgs:
             g = fused_geometry(m.ld, int(info["multiProcessorCount"]), variant, T)
             if g is None or g.variant != variant or (T is not None and g.T != T):
