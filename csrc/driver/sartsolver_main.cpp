@@ -68,10 +68,13 @@ struct DeviceShard {
     }
 };
 
-std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0, uint64_t nrows, size_t block_bytes) {
+// col0 / ncols: keep only that voxel block of every row (--partition_voxels; the rows are read whole).
+std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0, uint64_t nrows, size_t block_bytes,
+                                               uint64_t col0 = 0, uint64_t ncols = 0) {
     auto sh = std::make_unique<DeviceShard>();
+    if (ncols == 0) ncols = in.nvoxel - col0;
     sh->nrows = (int64_t)nrows;
-    sh->nvoxel = (int64_t)in.nvoxel;
+    sh->nvoxel = (int64_t)ncols;
     sh->ld = choose_ld(sh->nvoxel);
     sh->nrows_pad = (sh->nrows + 63) / 64 * 64;
     const size_t bytes = (size_t)sh->nrows_pad * sh->ld * sizeof(float);
@@ -104,8 +107,8 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
                 next = std::async(std::launch::async, read_into, buf[nb], blocks[k + 1].first, blocks[k + 1].second);
             }
             const uint64_t r0 = blocks[k].first, nr = blocks[k].second - blocks[k].first;
-            hip_ok(hipMemcpy2DAsync(sh->A + r0 * sh->ld, sh->ld * sizeof(float), cur, V * sizeof(float),
-                                    V * sizeof(float), nr, hipMemcpyHostToDevice, s),
+            hip_ok(hipMemcpy2DAsync(sh->A + r0 * sh->ld, sh->ld * sizeof(float), cur + col0, V * sizeof(float),
+                                    ncols * sizeof(float), nr, hipMemcpyHostToDevice, s),
                    "H2D RTM block");
             hip_ok(hipEventRecord(ev[k % 2], s), "event");
             ev_used[k % 2] = true;
@@ -176,10 +179,13 @@ int main(int argc, char** argv) {
     const int rank = host->rank(), size = host->size();
 
     try {
-        const Block blk = block_partition(in.npixel, size, rank);  // reference main.cpp:67-68
-        if (blk.size == 0)
-            throw std::runtime_error("rank " + std::to_string(rank) + " owns no pixels: use at most " +
-                                     std::to_string(in.npixel) + " ranks");
+        // --partition_voxels: every rank holds all pixels of a block of voxels (EngineConfig::column_shard)
+        const bool cols = gpu && cfg.partition_voxels;
+        const Block vblk = cols ? block_partition(in.nvoxel, size, rank) : Block{0, in.nvoxel};
+        const Block blk = cols ? Block{0, in.npixel} : block_partition(in.npixel, size, rank);  // reference main.cpp:67-68
+        if (blk.size == 0 || vblk.size == 0)
+            throw std::runtime_error("rank " + std::to_string(rank) + " owns no " + (cols ? "voxels" : "pixels") +
+                                     ": use at most " + std::to_string(cols ? in.nvoxel : in.npixel) + " ranks");
         CompositeImage image(in.image_files, in.frame_masks, intervals, blk.size, blk.offset);
         image.set_max_cache_size((uint64_t)cfg.max_cached_frames);
 
@@ -202,7 +208,7 @@ int main(int argc, char** argv) {
         std::vector<float> hshard;
         auto load = [&]() {
             if (gpu)
-                dshard = load_device_shard(in, blk.offset, blk.size, (size_t)256 << 20);
+                dshard = load_device_shard(in, blk.offset, blk.size, (size_t)256 << 20, vblk.offset, vblk.size);
             else {
                 hshard.assign(blk.size * in.nvoxel, 0.f);
                 read_rtm_rows(in.rtm_files, in.rtm_name, in.nvoxel, blk.offset, blk.offset + blk.size, hshard.data(),
@@ -235,6 +241,11 @@ int main(int argc, char** argv) {
             ec.use_fused = !cfg.two_pass;
             ec.fused_min_bytes = fused_min_bytes_from_env();
             if (const char* v = std::getenv("SART_FUSED_VARIANT"); v && *v) ec.fused_variant = std::atoi(v);
+            if (cols) {
+                ec.column_shard = true;
+                ec.col_offset = (int64_t)vblk.offset;
+                ec.nvoxel_total = (int64_t)in.nvoxel;
+            }
             engine = std::make_unique<Engine>(device, dshard->A, dshard->nrows, dshard->nrows_pad, dshard->nvoxel,
                                               dshard->ld, dcomm.get(), ec);
             if (lap.nnz()) engine->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
@@ -317,7 +328,9 @@ int main(int argc, char** argv) {
             }
             frames.clear();
         }
-        std::vector<double> solution = warm, x(in.nvoxel);
+        if (cols && !warm.empty())  // this rank's voxels of the stored solution
+            warm = std::vector<double>(warm.begin() + vblk.offset, warm.begin() + vblk.offset + vblk.size);
+        std::vector<double> solution = warm, x(vblk.size), xfull(cols ? in.nvoxel : 0);
         std::future<std::vector<double>> fut;
         if (!frames.empty()) fut = std::async(std::launch::async, [&image, i = frames[0]]() { return image.frame(i); });
         for (size_t k = 0; k < frames.size(); ++k) {
@@ -332,8 +345,14 @@ int main(int argc, char** argv) {
                 std::cerr << "warning: fused sweep fell back " << info.fallbacks << " time(s)" << std::endl;
             if (info.nonfinite) std::cerr << "warning: frame " << cur << ": non-finite iterate, stopped" << std::endl;
             solution = x;
+            if (cols) {  // gather the voxel blocks (zero-filled sum over ranks)
+                std::fill(xfull.begin(), xfull.end(), 0.0);
+                std::copy(x.begin(), x.end(), xfull.begin() + vblk.offset);
+                host->all_reduce_host(xfull.data(), xfull.size(), ReduceOp::kSum);
+            }
             if (rank == 0) {
-                writer->add(x, info.status, image.frame_time(cur), image.camera_frame_time(cur), info.iterations);
+                writer->add(cols ? xfull : x, info.status, image.frame_time(cur), image.camera_frame_time(cur),
+                            info.iterations);
                 const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 std::cout << "Processed in: " << ms << " ms" << std::endl;  // reference main.cpp:132-137
                 if (profile.is_open())

@@ -2,7 +2,8 @@
 //
 // Same options, short aliases, defaults and validation as the reference CLI (reference
 // arguments.cpp:82-251, arguments.hpp:14-33), with an in-tree parser instead of p-ranav/argparse.
-// Extensions (not in the reference) are marked: --resume, --batch_frames, --two_pass, --profile.
+// Extensions (not in the reference) are marked: --resume, --batch_frames, --two_pass, --partition_voxels,
+// --profile.
 #pragma once
 
 #include <array>
@@ -34,6 +35,7 @@ struct Config {
     bool resume = false;        // append to an existing output file, skip frames already solved
     int batch_frames = 1;       // >1: solve independent frames together (MFMA multi-frame path, implies --no_guess)
     bool two_pass = false;      // disable the fused single-pass sweep
+    bool partition_voxels = false;  // GPU: shard the RTM by voxel columns (all pixels per rank) instead of pixel rows
     std::string profile_file;   // JSON timing/telemetry sidecar
     bool help = false;
 };

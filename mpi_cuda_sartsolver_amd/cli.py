@@ -11,7 +11,7 @@ Same CLI, input validation, frame loop, output file and console output as the re
 * fatal errors tear the process group down instead of leaving peers blocked in a collective.
 
 Extensions: ``--resume``, ``--batch_frames N`` (multi-frame MFMA solver), ``--two_pass``,
-``--profile FILE`` (JSON lines per frame).
+``--partition_voxels`` (voxel-column shards), ``--profile FILE`` (JSON lines per frame).
 """
 from __future__ import annotations
 
@@ -60,7 +60,7 @@ def run(cfg, intervals) -> int:
 
     n = native()
     from .parallel.comm import init_distributed
-    from .parallel.partition import row_partition
+    from .parallel.partition import col_partition, row_partition
 
     # ---- metadata validation (every rank, before the process group exists: reference main.cpp:27-59)
     try:
@@ -73,10 +73,17 @@ def run(cfg, intervals) -> int:
         _fail("No GPU available: run with --use_cpu or on an MI355X node.")
     comm = init_distributed(use_gpu=use_gpu)
     rank, world = comm.rank, comm.world_size
+    cols = bool(getattr(cfg, "partition_voxels", False)) and use_gpu
     try:
-        block = row_partition(inputs.npixel, world, rank)
-        if block.size == 0:
-            raise RuntimeError(f"rank {rank} owns no pixels: use at most {inputs.npixel} ranks")
+        if cols:  # voxel-column shards: every rank holds all pixels of its voxel block
+            vblock = col_partition(inputs.nvoxel, world, rank)
+            if vblock.size == 0:
+                raise RuntimeError(f"rank {rank} owns no voxels: use at most {inputs.nvoxel} ranks")
+            block = row_partition(inputs.npixel, 1, 0)
+        else:
+            block = row_partition(inputs.npixel, world, rank)
+            if block.size == 0:
+                raise RuntimeError(f"rank {rank} owns no pixels: use at most {inputs.npixel} ranks")
         image = hdf5.open_composite_image(inputs, intervals, block.size, block.offset, cfg.max_cached_frames)
         params = SolverParams(ray_density_threshold=cfg.ray_density_threshold,
                               ray_length_threshold=cfg.ray_length_threshold, conv_tolerance=cfg.conv_tolerance,
@@ -86,6 +93,9 @@ def run(cfg, intervals) -> int:
         laplacian = hdf5.load_laplacian(cfg.laplacian_file, inputs.nvoxel, device) if cfg.laplacian_file else None
 
         def load():
+            if cols:
+                return hdf5.load_rtm_shard(inputs, 0, inputs.npixel, device, col_offset=vblock.offset,
+                                           ncols=vblock.size)
             if use_gpu:
                 return hdf5.load_rtm_shard(inputs, block.offset, block.size, device)
             return hdf5.read_rtm_rows(inputs, block.offset, block.stop)
@@ -110,7 +120,8 @@ def run(cfg, intervals) -> int:
                 from .ops import hip
 
                 solver = SARTSolver(shard, laplacian, comm, params, logarithmic=cfg.logarithmic,
-                                    use_fused=not cfg.two_pass, fused_min_bytes=hip().fused_min_bytes_from_env())
+                                    use_fused=not cfg.two_pass, fused_min_bytes=hip().fused_min_bytes_from_env(),
+                                    partition="cols" if cols else None)
         else:
             from .models.cpu import CPUSARTSolver
 
@@ -134,6 +145,8 @@ def run(cfg, intervals) -> int:
                 print("warning:", wmsg, file=sys.stderr)
         skip_until = comm.broadcast_object(skip_until)
         warm = comm.broadcast_object(warm if not cfg.no_guess else None)
+        if cols and warm is not None:
+            warm = np.asarray(warm)[vblock.offset: vblock.stop]  # this rank's voxels
         profile = open(cfg.profile_file, "w") if (cfg.profile_file and rank == 0) else None
 
         solution = warm
@@ -153,8 +166,9 @@ def run(cfg, intervals) -> int:
                 t0 = time.perf_counter()
                 res = solver.solve(frame, None if (cfg.no_guess or solution is None) else solution)
                 solution = res.solution
+                x_full = solver.gather_solution(res.solution) if cols else res.solution  # collective
                 if rank == 0:
-                    writer.add(res.solution, int(res.status), image.frame_time(cur), list(image.camera_frame_time(cur)),
+                    writer.add(x_full, int(res.status), image.frame_time(cur), list(image.camera_frame_time(cur)),
                                int(res.iterations))
                     ms = 1e3 * (time.perf_counter() - t0)
                     print(f"Processed in: {ms} ms", flush=True)

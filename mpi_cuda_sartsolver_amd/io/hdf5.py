@@ -65,8 +65,9 @@ def read_rtm_rows(inputs: InputSet, row_begin: int, row_end: int, ld: Optional[i
 
 
 def load_rtm_shard(inputs: InputSet, row_offset: int, npixel_local: int, device, ld: Optional[int] = None,
-                   block_bytes: int = 256 << 20):
-    """Stream this rank's RTM rows into a device-resident ``DenseRTM``.
+                   block_bytes: int = 256 << 20, col_offset: int = 0, ncols: Optional[int] = None):
+    """Stream this rank's RTM rows into a device-resident ``DenseRTM``; with ``col_offset`` / ``ncols`` only
+    that voxel block of every row is kept (column shard: the rows are still read whole).
 
     Two pinned host buffers alternate: while block k is copied host->HBM (async on the current
     stream), block k+1 is read from HDF5 by a helper thread (the native reader releases the GIL).
@@ -77,9 +78,10 @@ def load_rtm_shard(inputs: InputSet, row_offset: int, npixel_local: int, device,
     from ..models.rtm import DenseRTM
 
     n = native()
-    rtm = DenseRTM(npixel_local, inputs.nvoxel, row_offset, device=device, ld=ld)
-    rtm.A.zero_()
     V = inputs.nvoxel
+    nc = V - col_offset if ncols is None else int(ncols)
+    rtm = DenseRTM(npixel_local, nc, row_offset, device=device, ld=ld, col_offset=col_offset, nvoxel_total=V)
+    rtm.A.zero_()
     rows_per_block = max(1, min(npixel_local, block_bytes // (4 * V)))
     bufs = [torch.empty((rows_per_block, V), dtype=torch.float32).pin_memory() for _ in range(2)]
     events = [None, None]
@@ -102,7 +104,7 @@ def load_rtm_shard(inputs: InputSet, row_offset: int, npixel_local: int, device,
                 events[(k + 1) % 2].synchronize()  # the copy that last used this buffer is done
             reader = threading.Thread(target=read_into, args=(nxt, *blocks[k + 1]))
             reader.start()
-        rtm.A[r0:r1, :V].copy_(cur[: r1 - r0], non_blocking=True)
+        rtm.A[r0:r1, :nc].copy_(cur[: r1 - r0, col_offset: col_offset + nc], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(stream)
         events[k % 2] = ev

@@ -153,3 +153,52 @@ def test_native_gpu_two_ranks_one_device(tmp_path, binary):
     _, x2, s2 = n.read_solution_file(str(tmp_path / "two.h5"))
     np.testing.assert_array_equal(s1, s2)
     assert np.linalg.norm(x2 - x1) / np.linalg.norm(x1) < 2e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log", [False, True])
+def test_partition_voxels_cli(tmp_path, binary, log):
+    """--partition_voxels (voxel-column shards, all-reduce of A x): 1 and 2 ranks of the native driver and
+    2 ranks of the Python driver agree with the pixel-row run (Laplacian, warm starts, sparse camera)."""
+    case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_b",), laplacian=True, nframes=2, nvoxel=2048,
+                     grid=(16, 16, 16), shapes=((24, 32), (20, 30)))
+    base = ["-m", "40", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3", "--two_pass"] + (["-L"] if log else [])
+    r = _run_native(binary, base + ["-o", str(tmp_path / "rows.h5"), *case.files])
+    assert r.returncode == 0, r.stderr
+    outs = {}
+    env_backend = os.environ.get("SART_DIST_BACKEND")
+    os.environ["SART_DIST_BACKEND"] = "tcp"
+    try:
+        for name, nproc, runner in (("v1", 1, "native"), ("v2", 2, "native"), ("p2", 2, "python")):
+            out = str(tmp_path / f"{name}.h5")
+            args = base + ["--partition_voxels", "-o", out, *case.files]
+            if runner == "native":
+                r = _run_native(binary, args, nproc=nproc)
+            else:
+                os.environ["SART_DIST_BACKEND"] = "gloo"
+                cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+                       "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m", "mpi_cuda_sartsolver_amd",
+                       *args]
+                r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env())
+            assert r.returncode == 0, name + r.stdout[-2000:] + r.stderr[-4000:]
+            outs[name] = out
+    finally:
+        if env_backend is None:
+            os.environ.pop("SART_DIST_BACKEND", None)
+        else:
+            os.environ["SART_DIST_BACKEND"] = env_backend
+    n = native()
+    t0, x0, s0 = n.read_solution_file(str(tmp_path / "rows.h5"))
+    for name, out in outs.items():
+        t, x, s = n.read_solution_file(out)
+        np.testing.assert_array_equal(t, t0)
+        np.testing.assert_array_equal(s, s0)
+        assert np.linalg.norm(x - x0) / np.linalg.norm(x0) < 2e-3, name
+
+
+def test_partition_voxels_rejects_cpu_and_batches(tmp_path, binary):
+    case = _case(tmp_path, nframes=1)
+    r = _run_native(binary, ["--use_cpu", "--partition_voxels", *case.files])
+    assert r.returncode == 1 and "partition_voxels" in r.stderr
+    r = _run_native(binary, ["--batch_frames", "4", "--partition_voxels", *case.files])
+    assert r.returncode == 1 and "partition_voxels" in r.stderr
