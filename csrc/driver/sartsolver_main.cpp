@@ -360,7 +360,8 @@ int main(int argc, char** argv) {
                             << ", \"status\": " << info.status << ", \"iterations\": " << info.iterations
                             << ", \"ms\": " << ms << ", \"solve_ms\": " << info.ms
                             << ", \"fused\": " << (info.used_fused ? "true" : "false")
-                            << ", \"driver\": \"" << json_escape("native") << "\"}\n";
+                            << ", \"ranks\": " << size << ", \"comm\": \"" << json_escape(host->backend())
+                            << "\", \"driver\": \"" << json_escape("native") << "\"}\n";
             }
             if (cfg.no_guess) solution.clear();
         }

@@ -199,6 +199,7 @@ std::unique_ptr<HostComm> make_tcp_host_comm(int rank, int size, const std::stri
 }
 
 std::unique_ptr<HostComm> host_comm_from_env(double timeout_s) {
+    if (mpi_launch_detected()) return make_mpi_host_comm();
     const EnvWorld w = env_world();
     if (w.size <= 1) return make_local_host_comm();
     return make_tcp_host_comm(w.rank, w.size, w.master_addr, w.port, timeout_s);

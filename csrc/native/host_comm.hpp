@@ -5,7 +5,8 @@
 // 158-329; main.cpp:84). Backends here:
 //   * local -- one rank, identity;
 //   * tcp   -- TCP sockets, star through rank 0, reductions in fixed rank order (bitwise reproducible and
-//              independent of the launcher), no MPI library needed.
+//              independent of the launcher), no MPI library needed;
+//   * mpi   -- MPI_COMM_WORLD through libmpi loaded at run time (mpiexec launches, multi-node bootstrap).
 // Rendezvous follows torchrun / MPI launchers (env_world): RANK, WORLD_SIZE, LOCAL_RANK (or
 // OMPI_COMM_WORLD_*, PMI_*), MASTER_ADDR (default 127.0.0.1); the port is SART_COMM_PORT, else
 // MASTER_PORT + 17 (torchrun's own store owns MASTER_PORT).
@@ -47,7 +48,11 @@ EnvWorld env_world();
 std::unique_ptr<HostComm> make_local_host_comm();
 std::unique_ptr<HostComm> make_tcp_host_comm(int rank, int size, const std::string& host, int port,
                                              double timeout_s = 3600.0);
-// Local for one rank, TCP otherwise.
+// MPI_COMM_WORLD through a run-time loaded libmpi (MPICH ABI; host_comm_mpi.cpp).
+std::unique_ptr<HostComm> make_mpi_host_comm();
+// SART_HOST_COMM=mpi, or an MPICH-family launcher (PMI_SIZE > 1 without torchrun's RANK).
+bool mpi_launch_detected();
+// MPI when mpi_launch_detected(); else local for one rank, TCP otherwise (SART_HOST_COMM=tcp forces TCP).
 std::unique_ptr<HostComm> host_comm_from_env(double timeout_s = 3600.0);
 
 // Balanced 1-D block partition (reference main.cpp:67-68): the first n % parts parts get one more.

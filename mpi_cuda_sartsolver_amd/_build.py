@@ -114,6 +114,7 @@ def build_hip(verbose: bool = True) -> Path:
     # native engine (host C++ on the HIP runtime + RCCL): csrc/engine
     eflags = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}"]
     for src in sorted((CSRC / "engine").glob("*.cpp")) + [CSRC / "native" / "host_comm.cpp",
+                                                          CSRC / "native" / "host_comm_mpi.cpp",
                                                           CSRC / "native" / "solver_params.cpp"]:
         obj = objdir / ("engine_" + src.stem + ".o")
         jobs.append(([hipcc, *eflags, "-c", str(src), "-o", str(obj)], obj, _digest([src, *headers], eflags)))
@@ -182,7 +183,7 @@ def build_driver(verbose: bool = True) -> Path:
                   verbose)
     hip_objs = [o for o in sorted((BUILDDIR / "hip").glob("*.o")) if o.name != "hip_module.o"]
     native_objs = [o for o in sorted((BUILDDIR / "native").glob("*.o"))
-                   if o.name not in ("native_module.o", "host_comm.o", "solver_params.o")]
+                   if o.name not in ("native_module.o", "host_comm.o", "host_comm_mpi.o", "solver_params.o")]
     objs = [dobj, *hip_objs, *native_objs]
     libdir = LIBDIR / "hdf5"  # private RUNPATH entry: only libhdf5
     libdir.mkdir(parents=True, exist_ok=True)
@@ -194,7 +195,7 @@ def build_driver(verbose: bool = True) -> Path:
     out = LIBDIR / "sartsolver"
     # libhdf5 by path, not -L: a -L/opt/conda/lib would also resolve libstdc++ to conda's older copy
     _link([hipcc, f"--offload-arch={ARCH}", *map(str, objs), f"-L{ROCM / 'lib'}", "-lrccl",
-           "-lrocprofiler-sdk-roctx", str(HDF5_PREFIX / "lib" / "libhdf5.so"), "-lgomp", "-lpthread",
+           "-lrocprofiler-sdk-roctx", str(HDF5_PREFIX / "lib" / "libhdf5.so"), "-lgomp", "-lpthread", "-ldl",
            "-Wl,-rpath,$ORIGIN/hdf5", f"-Wl,-rpath,{ROCM / 'lib'}", "-o", str(out)], out, objs, verbose)
     return out
 

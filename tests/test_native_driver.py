@@ -99,6 +99,37 @@ def test_native_cpu_ranks_invariance_and_resume(tmp_path, binary):
     np.testing.assert_allclose(x3, x1, rtol=1e-10)
 
 
+MPIEXEC = "/opt/conda/bin/mpiexec"
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="MPICH mpiexec not installed")
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_native_cpu_under_mpiexec(tmp_path, binary, nproc):
+    """The reference's own launch (mpiexec, host MPI collectives on MPI_COMM_WORLD): the MPI host
+    communicator (host_comm_mpi.cpp, libmpi loaded at run time) gives the single-rank solution."""
+    case = _case(tmp_path)
+    base = ["--use_cpu", "-m", "60", "-c", "1e-7", "-l", case.laplacian_file, "-b", "1e-3"]
+    one = str(tmp_path / "one.h5")
+    r = _run_native(binary, base + ["-o", one, *case.files])
+    assert r.returncode == 0, r.stderr
+    out, prof = str(tmp_path / "mpi.h5"), str(tmp_path / "mpi.jsonl")
+    env = {k: v for k, v in _env().items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([MPIEXEC, "-n", str(nproc), binary, *base, "--profile", prof, "-o", out, *case.files],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.count("Processed in:") == 3  # rank 0 only
+    import json
+
+    lines = [json.loads(s) for s in open(prof)]
+    assert lines and all(d["comm"] == "mpi" and d["ranks"] == nproc for d in lines)
+    n = native()
+    t1, x1, s1 = n.read_solution_file(one)
+    t2, x2, s2 = n.read_solution_file(out)
+    np.testing.assert_array_equal(t1, t2)
+    np.testing.assert_array_equal(s1, s2)
+    np.testing.assert_allclose(x2, x1, rtol=1e-8, atol=1e-12)
+
+
 def test_native_cli_errors(tmp_path, binary):
     case = _case(tmp_path, nframes=1)
     r = _run_native(binary, ["--use_cpu", "-R", "3", *case.files])
