@@ -50,6 +50,8 @@ static void bind_engine(py::module_& m) {
         .def_property_readonly("rank", [](sart::Communicator& c) { return c.rank(); })
         .def_property_readonly("size", [](sart::Communicator& c) { return c.size(); })
         .def_property_readonly("backend", &sart::Communicator::backend)
+        .def_property_readonly("describe", &sart::Communicator::describe)
+        .def("check", &sart::Communicator::check)
         .def("barrier", [](sart::Communicator& c) { c.host().barrier(); }, py::call_guard<py::gil_scoped_release>())
         .def("abort", &sart::Communicator::abort)
         .def("all_reduce_host",
@@ -102,6 +104,12 @@ static void bind_engine(py::module_& m) {
               return std::shared_ptr<sart::Communicator>(
                   sart::make_rccl_comm(device, id, sart::make_tcp_host_comm(rank, size, host, port)));
           });
+    m.def("p2p_comm",
+          [](int device, std::shared_ptr<sart::Communicator> base) {
+              py::gil_scoped_release rel;
+              return std::shared_ptr<sart::Communicator>(sart::make_p2p_comm(device, std::move(base)));
+          },
+          py::arg("device"), py::arg("base"));
     m.def("comm_from_env", [](int device) {
         py::gil_scoped_release rel;
         return std::shared_ptr<sart::Communicator>(sart::comm_from_env(device));

@@ -1,12 +1,20 @@
 #include "comm.hpp"
 
 #include <rccl/rccl.h>
+#include <unistd.h>
 
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <vector>
+
+#include "../kernels/launchers.hpp"
 
 namespace sart {
 
@@ -90,6 +98,244 @@ class RcclComm final : public Communicator {
     ncclComm_t comm_ = nullptr;
 };
 
+
+// ---- p2p: one-shot push all-reduce through IPC-mapped peer buffers (csrc/kernels/p2p_allreduce.hip) ----
+double env_double(const char* name, double dflt) {
+    const char* e = std::getenv(name);
+    return (e && *e) ? std::atof(e) : dflt;
+}
+
+class P2pComm final : public Communicator {
+   public:
+    P2pComm(int device, std::shared_ptr<Communicator> base) : base_(std::move(base)), device_(device) {
+        HostComm& h = base_->host();
+        rank_ = h.rank();
+        n_ = h.size();
+        const char* m = std::getenv("SART_P2P");
+        const std::string mode = (m && *m) ? m : "auto";
+        cap_ = std::max<int64_t>(1024, (int64_t)(env_double("SART_P2P_MAX_BYTES", 2.0 * 1024 * 1024) / 4) / 4 * 4);
+        timeout_s_ = env_double("SART_P2P_TIMEOUT_S", 600.0);
+        if (mode == "0" || mode == "off") {
+            finish(false, "p2p off (SART_P2P=0)");
+            return;
+        }
+        if (n_ < 2 || n_ > kP2pMaxRanks) {
+            finish(false, "p2p needs 2.." + std::to_string(kP2pMaxRanks) + " ranks");
+            return;
+        }
+        if (!agree(same_host())) {
+            finish(false, "p2p off: ranks span several hosts");
+            return;
+        }
+        hip_ok(hipSetDevice(device_), "hipSetDevice");
+        hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+        if (!agree(map_peers())) {
+            finish(false, "p2p off: IPC mapping failed (" + err_msg_ + ")");
+            return;
+        }
+        if (!agree(self_test())) {
+            finish(false, "p2p off: self-test failed (" + (err_msg_.empty() ? "on another rank" : err_msg_) + ")");
+            return;
+        }
+        if (mode == "1" || mode == "on") {
+            finish(true, "p2p (forced, self-test ok)");
+            return;
+        }
+        // auto: rank 0 times both at the engine's typical message (64k voxels + the piggy-backed scalar)
+        const int64_t nprobe = std::min<int64_t>(cap_, 65537);
+        const double tp = time_us([&](float* b) { p2p(b, nprobe, 0, stream_); }, nprobe);
+        const double tb = time_us([&](float* b) { base_->all_reduce(b, (size_t)nprobe, ReduceOp::kSum, stream_); },
+                                  nprobe);
+        double pick[3] = {tp < tb ? 1.0 : 0.0, tp, tb};
+        h.broadcast_host(pick, sizeof(pick), 0);
+        char buf[160];
+        std::snprintf(buf, sizeof(buf), "%s (auto: p2p %.1f us vs %s %.1f us at %lld floats, rank 0)",
+                      pick[0] > 0 ? "p2p" : base_->backend(), pick[1], base_->backend(), pick[2], (long long)nprobe);
+        finish(pick[0] > 0, buf);
+    }
+    ~P2pComm() override {
+        (void)hipSetDevice(device_);
+        if (stream_) (void)hipStreamSynchronize(stream_);
+        for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+        if (mem_) (void)hipFree(mem_);
+        if (stream_) (void)hipStreamDestroy(stream_);
+    }
+    HostComm& host() override { return base_->host(); }
+    const char* backend() const override { return active_ ? "p2p" : base_->backend(); }
+    std::string describe() const override { return why_; }
+    void all_reduce(float* dev, size_t n, ReduceOp op, hipStream_t stream) override {
+        if (active_ && n > 0 && (int64_t)n <= cap_ && reinterpret_cast<uintptr_t>(dev) % 16 == 0)
+            p2p(dev, (int64_t)n, op == ReduceOp::kSum ? 0 : 1, stream);
+        else
+            base_->all_reduce(dev, n, op, stream);
+    }
+    void all_reduce(double* dev, size_t n, ReduceOp op, hipStream_t stream) override {
+        base_->all_reduce(dev, n, op, stream);
+    }
+    bool graph_capturable() const override { return !active_ && base_->graph_capturable(); }  // epoch is an argument
+    void abort() override { base_->abort(); }
+    void check() override {
+        if (!err_) return;
+        unsigned e = 0;
+        hip_ok(hipMemcpy(&e, err_, sizeof(e), hipMemcpyDeviceToHost), "p2p error word");
+        if (e) throw std::runtime_error("p2p all-reduce: a peer did not arrive within SART_P2P_TIMEOUT_S");
+        base_->check();
+    }
+
+   private:
+    void finish(bool active, const std::string& why) {
+        active_ = active;
+        why_ = why;
+    }
+    bool agree(bool ok) {  // every rank learns whether all succeeded
+        double bad = ok ? 0.0 : 1.0;
+        base_->host().all_reduce_host(&bad, 1, ReduceOp::kMax);
+        return bad == 0.0;
+    }
+    bool same_host() {
+        char mine[256] = {0};
+        (void)gethostname(mine, sizeof(mine) - 1);
+        bool same = true;
+        for (int r = 0; r < n_; ++r) {
+            char other[256];
+            std::memcpy(other, mine, sizeof(mine));
+            base_->host().broadcast_host(other, sizeof(other), r);
+            same = same && std::memcmp(other, mine, sizeof(mine)) == 0;
+        }
+        return same;
+    }
+    bool map_peers() {
+        const size_t recv_bytes = (size_t)2 * kP2pMaxRanks * (size_t)cap_ * sizeof(float);
+        const size_t flag_bytes = (size_t)kP2pMaxRanks * kP2pMaxBlocks * sizeof(unsigned);
+        hipIpcMemHandle_t hdl;
+        std::memset(&hdl, 0, sizeof(hdl));
+        bool ok = true;
+        try {
+            hip_ok(hipExtMallocWithFlags(&mem_, recv_bytes + flag_bytes + 256, hipDeviceMallocUncached),
+                   "hipExtMallocWithFlags(uncached)");
+            hip_ok(hipMemset(mem_, 0, recv_bytes + flag_bytes + 256), "hipMemset");
+            hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
+            err_ = reinterpret_cast<unsigned*>(static_cast<char*>(mem_) + recv_bytes + flag_bytes);
+            hip_ok(hipIpcGetMemHandle(&hdl, mem_), "hipIpcGetMemHandle");
+        } catch (const std::exception& e) {
+            ok = false;
+            err_msg_ = e.what();
+        }
+        for (int r = 0; r < n_; ++r) {  // every rank takes part in every broadcast, even after a failure
+            hipIpcMemHandle_t h = hdl;
+            base_->host().broadcast_host(&h, sizeof(h), r);
+            if (!ok) continue;
+            void* p = mem_;
+            if (r != rank_) {
+                if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                    (void)hipGetLastError();
+                    ok = false;
+                    err_msg_ = "hipIpcOpenMemHandle of rank " + std::to_string(r);
+                    continue;
+                }
+                opened_.push_back(p);
+            }
+            args_.recv[r] = static_cast<float*>(p);
+            args_.flags[r] = reinterpret_cast<unsigned*>(static_cast<char*>(p) + recv_bytes);
+        }
+        return ok;  // the caller's agree() is also the barrier: every flag array is zeroed before any push
+    }
+    void p2p(float* dev, int64_t n, int op, hipStream_t stream, double timeout_s = -1) {
+        launch_p2p_allreduce(dev, dev, n, args_, rank_, n_, ++epoch_, cap_, op, err_,
+                             timeout_s > 0 ? timeout_s : timeout_s_, stream);
+    }
+    // Exact checks: integer-valued sums / maxima, and random fp32 data against the rank-order sum (the
+    // kernel's result must be bitwise identical to ((v0 + v1) + v2) + ... on every rank), both parities.
+    bool self_test() {
+        float* d = nullptr;
+        if (!agree(hipMalloc(reinterpret_cast<void**>(&d), (size_t)cap_ * sizeof(float)) == hipSuccess)) {
+            (void)hipGetLastError();
+            if (d) (void)hipFree(d);
+            err_msg_ = "hipMalloc";
+            return false;
+        }
+        const int64_t sizes[] = {1, 5, 1024, 4099, std::min<int64_t>(cap_, 65537)};
+        int call = 0;
+        for (int64_t n : sizes) {
+            for (int kind = 0; kind < 3; ++kind, ++call) {  // 0 integer sum, 1 integer max, 2 random fp32 sum
+                bool good = true;
+                try {
+                    std::vector<float> mine((size_t)n), want((size_t)n), got((size_t)n);
+                    for (int64_t i = 0; i < n; ++i) {
+                        float acc = 0.f;
+                        for (int r = 0; r < n_; ++r) {
+                            const float v = value(kind, r, i, call);
+                            if (r == rank_) mine[(size_t)i] = v;
+                            acc = r == 0 ? v : (kind == 1 ? std::max(acc, v) : acc + v);
+                        }
+                        want[(size_t)i] = acc;
+                    }
+                    hip_ok(hipMemcpy(d, mine.data(), (size_t)n * sizeof(float), hipMemcpyHostToDevice), "H2D");
+                    p2p(d, n, kind == 1 ? 1 : 0, stream_, std::min(timeout_s_, 30.0));
+                    hip_ok(hipStreamSynchronize(stream_), "p2p self-test");
+                    hip_ok(hipMemcpy(got.data(), d, (size_t)n * sizeof(float), hipMemcpyDeviceToHost), "D2H");
+                    unsigned e = 0;
+                    hip_ok(hipMemcpy(&e, err_, sizeof(e), hipMemcpyDeviceToHost), "D2H");
+                    if (e) throw std::runtime_error("peer timeout");
+                    if (std::memcmp(got.data(), want.data(), (size_t)n * sizeof(float)) != 0)
+                        throw std::runtime_error("mismatch at n=" + std::to_string(n) + " kind " + std::to_string(kind));
+                } catch (const std::exception& ex) {
+                    good = false;
+                    err_msg_ = ex.what();
+                }
+                if (!agree(good)) {  // every rank leaves the test at the same call
+                    (void)hipFree(d);
+                    return false;
+                }
+            }
+        }
+        (void)hipFree(d);
+        return true;
+    }
+    static float value(int kind, int r, int64_t i, int call) {
+        if (kind < 2) return (float)((r + 1) * ((i * 7 + call) % 251));
+        uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + (uint64_t)(r + 1) * 0xBF58476D1CE4E5B9ull + (uint64_t)call;
+        z = (z ^ (z >> 31)) * 0x94D049BB133111EBull;
+        return (float)((double)(z >> 40) / (double)(1ull << 24) * 2.0 - 1.0);
+    }
+    // mean microseconds per call over 20 calls after 3 warm-up calls (host barrier before timing)
+    double time_us(const std::function<void(float*)>& f, int64_t n) {
+        float* d = nullptr;
+        hip_ok(hipMalloc(reinterpret_cast<void**>(&d), (size_t)n * sizeof(float)), "hipMalloc");
+        hip_ok(hipMemset(d, 0, (size_t)n * sizeof(float)), "hipMemset");
+        hip_ok(hipDeviceSynchronize(), "sync");
+        for (int i = 0; i < 3; ++i) f(d);
+        hip_ok(hipStreamSynchronize(stream_), "sync");
+        base_->host().barrier();
+        hipEvent_t e0, e1;
+        hip_ok(hipEventCreate(&e0), "event");
+        hip_ok(hipEventCreate(&e1), "event");
+        hip_ok(hipEventRecord(e0, stream_), "event");
+        for (int i = 0; i < 20; ++i) f(d);
+        hip_ok(hipEventRecord(e1, stream_), "event");
+        hip_ok(hipEventSynchronize(e1), "event");
+        float ms = 0.f;
+        hip_ok(hipEventElapsedTime(&ms, e0, e1), "event");
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        (void)hipFree(d);
+        return 1e3 * ms / 20.0;
+    }
+
+    std::shared_ptr<Communicator> base_;
+    int device_ = 0, rank_ = 0, n_ = 1;
+    int64_t cap_ = 0;
+    double timeout_s_ = 600.0;
+    bool active_ = false;
+    std::string why_, err_msg_;
+    hipStream_t stream_ = nullptr;
+    void* mem_ = nullptr;
+    unsigned* err_ = nullptr;
+    std::vector<void*> opened_;
+    P2pArgs args_{};
+    unsigned epoch_ = 0;
+};
+
 }  // namespace
 
 std::unique_ptr<Communicator> make_local_comm() { return std::make_unique<LocalComm>(); }
@@ -112,11 +358,20 @@ std::unique_ptr<Communicator> comm_from_env(int device) {
     auto host = host_comm_from_env();
     if (host->size() <= 1) return make_local_comm();
     const char* be = std::getenv("SART_DIST_BACKEND");
-    if (be && (std::string(be) == "tcp" || std::string(be) == "gloo")) return make_staged_comm(std::move(host));
+    const char* p2p = std::getenv("SART_P2P");
+    if (be && (std::string(be) == "tcp" || std::string(be) == "gloo")) {
+        auto staged = make_staged_comm(std::move(host));
+        if (p2p && std::string(p2p) == "1") return make_p2p_comm(device, std::move(staged));  // tests on one GPU
+        return staged;
+    }
     std::string uid(128, '\0');
     if (host->rank() == 0) uid = rccl_unique_id();
     host->broadcast_host(uid.data(), uid.size(), 0);
-    return make_rccl_comm(device, uid, std::move(host));
+    return make_p2p_comm(device, make_rccl_comm(device, uid, std::move(host)));
+}
+
+std::unique_ptr<Communicator> make_p2p_comm(int device, std::shared_ptr<Communicator> base) {
+    return std::make_unique<P2pComm>(device, std::move(base));
 }
 
 }  // namespace sart

@@ -7,6 +7,11 @@
 //               sharing one GPU in tests, hosts without RCCL).
 //   * rccl   -- RCCL (NCCL API) on device buffers over xGMI, ordered on the caller's HIP stream and
 //               capturable into HIP graphs; host collectives ride on its TCP bootstrap HostComm.
+//   * p2p    -- one-shot push all-reduce through IPC-mapped peer buffers over all xGMI links at once
+//               (csrc/kernels/p2p_allreduce.hip) for fp32 vectors up to SART_P2P_MAX_BYTES, wrapping a
+//               base communicator (RCCL in production) that serves everything else. Enabled after an
+//               exact self-test on every rank; SART_P2P=0 off, 1 on, auto (default) on when it beats the
+//               base at the engine's message size.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -32,6 +37,10 @@ class Communicator {
     virtual bool graph_capturable() const { return false; }
     // Tear down after a fatal error so that peers blocked in a collective fail instead of hanging.
     virtual void abort() { host().abort(); }
+    // Throws when a device collective reported a failure (p2p: a peer never arrived). Call after a sync.
+    virtual void check() {}
+    // Human-readable selection (backend and why), e.g. for benchmark logs.
+    virtual std::string describe() const { return backend(); }
     int rank() { return host().rank(); }
     int size() { return host().size(); }
 };
@@ -41,8 +50,12 @@ std::unique_ptr<Communicator> make_staged_comm(std::unique_ptr<HostComm> host);
 std::string rccl_unique_id();  // NCCL_UNIQUE_ID_BYTES opaque bytes (call on one rank)
 // `bootstrap` carries the host collectives; `uid` must be the same bytes on every rank.
 std::unique_ptr<Communicator> make_rccl_comm(int device, const std::string& uid, std::unique_ptr<HostComm> bootstrap);
-// From the launcher environment: local for one rank; else RCCL over a TCP bootstrap, or staged when
-// SART_DIST_BACKEND is "tcp"/"gloo".
+// One-shot P2P all-reduce over `base` (which keeps serving doubles, large vectors and host collectives).
+// Collective: every rank of base calls it. Falls back to plain `base` behaviour (backend() == base's) when
+// the ranks span several hosts, IPC mapping or the self-test fails, or SART_P2P=0.
+std::unique_ptr<Communicator> make_p2p_comm(int device, std::shared_ptr<Communicator> base);
+// From the launcher environment: local for one rank; else RCCL (with the P2P all-reduce, SART_P2P) over a
+// TCP or MPI bootstrap, or staged when SART_DIST_BACKEND is "tcp"/"gloo".
 std::unique_ptr<Communicator> comm_from_env(int device);
 
 }  // namespace sart

@@ -419,6 +419,7 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
             if (s.done || (checked == issued && enqueued >= max_sweeps)) break;
         }
         hip_ok(hipStreamSynchronize(stream_), "solve");
+        comm_->check();
         if (error) {
             ++info.fallbacks;
             if (!fallback()) throw std::runtime_error("SART engine: persistent sweep failed without fallback");

@@ -156,6 +156,7 @@ void MultiFrameEngine::solve_group(const double* g, int B, double* x_out, SolveI
     hip_ok(hipMemcpyAsync(xh.data(), X_.get(), xh.size() * sizeof(float), hipMemcpyDeviceToHost, stream_), "D2H X");
     hip_ok(hipMemcpyAsync(hstate_, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
     hip_ok(hipStreamSynchronize(stream_), "mf solve");
+    comm_->check();
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (int f = 0; f < B; ++f) {
         for (int64_t v = 0; v < V_; ++v) x_out[(int64_t)f * V_ + v] = (double)xh[(size_t)f * ld_ + v] * norm[f];

@@ -67,6 +67,18 @@ std::vector<unsigned long long> fused_debug_stats(int nblocks);
 void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                         const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                         uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream);
+// p2p_allreduce.hip: one-shot push all-reduce through IPC-mapped peer buffers (at most 8 ranks, fp32).
+// Receive buffer of every rank: [2 parities][kP2pMaxRanks sources][cap] floats; flags: [sources][blocks].
+constexpr int kP2pMaxRanks = 8;
+constexpr int kP2pMaxBlocks = 1024;
+struct P2pArgs {
+    float* recv[kP2pMaxRanks];      // rank j's receive buffer as mapped in this process
+    unsigned* flags[kP2pMaxRanks];  // rank j's flag array as mapped in this process
+};
+int64_t p2p_chunk(int64_t n);  // elements per workgroup
+// op: 0 sum, 1 max. `epoch` strictly increases by one per call on every rank (starts at 1).
+void launch_p2p_allreduce(const float* in, float* out, int64_t n, const P2pArgs& a, int rank, int nranks,
+                          unsigned epoch, int64_t cap, int op, unsigned* err, double timeout_s, hipStream_t stream);
 // multiframe.hip (nf = frames per batch: 16, 32 or 64)
 int mf_forward_num_splits(int64_t ld, int64_t nrows_pad);
 int mf_backproject_num_splits(int64_t ld, int64_t nrows);

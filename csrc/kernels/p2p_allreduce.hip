@@ -1,0 +1,129 @@
+// One-shot peer-to-peer all-reduce over xGMI. The reference reduces the
+// per-iteration correction through host memory (D2H, MPI_Allreduce, H2D: reference
+// sartsolver_cuda.cpp:242-244); RCCL rings over xGMI use one link per direction and 2(N-1) latency steps.
+// Here every rank PUSHES its vector into a per-source slot of every peer's receive buffer (IPC-mapped,
+// all 7 links at once), raises one epoch flag per chunk in each peer, then waits for the N-1 flags of its
+// chunk and sums the N slots locally in rank order 0..N-1 -- the same order on every rank, so the result
+// is bitwise identical everywhere (the replicated solution x never drifts between GPUs).
+//
+// Buffer reuse: slots alternate with the call parity. A peer can be at most one call ahead of this
+// rank (it needs this rank's flags of call k to finish call k), so it writes the other parity's slots
+// while this rank still reads call k; flags hold monotonically increasing epochs (compared with >=).
+//
+// Memory: receive buffers and flags are uncached device memory (hipDeviceMallocUncached). Producer:
+// every pushing wave waits for its stores, then (behind a barrier) each flag lane issues a system-scope
+// release, waits again (cdna_hip_programming.md Guideline 16 Pitfall 12) and stores the flag. Consumer:
+// relaxed system-scope polls, one acquire + wait per polling lane, a barrier, then plain loads. Polls
+// are bounded (s_memrealtime, 100 MHz): on timeout the chunk is filled with NaN (the engine's
+// non-finite guard stops the frame) and *err is raised for the host.
+#include "launchers.hpp"
+
+#include <stdexcept>
+#include <string>
+
+namespace sart {
+
+namespace {
+
+__device__ inline float red(float a, float b, int op) { return op == 0 ? a + b : fmaxf(a, b); }
+
+// `in` may alias `out` (in place): each element is read in phase 1 and written in phase 2 by one thread.
+__global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* out, int64_t n, int64_t chunk,
+                                                       P2pArgs a, int rank, int nranks, unsigned epoch, int parity,
+                                                       int64_t cap, int op, unsigned* err, uint64_t timeout_ticks) {
+    const int64_t c0 = (int64_t)blockIdx.x * chunk;
+    const int64_t c1 = c0 + chunk < n ? c0 + chunk : n;
+    const int64_t mine = (int64_t)(parity * kP2pMaxRanks + rank) * cap;  // my slot in every receive buffer
+
+    // phase 1: push this chunk into slot [parity][rank] of every rank's receive buffer (self included)
+    for (int64_t i = c0 + 4 * (int64_t)threadIdx.x; i < c1; i += 4 * (int64_t)blockDim.x) {
+        if (i + 4 <= c1) {
+            const float4 v = *reinterpret_cast<const float4*>(in + i);
+            for (int j = 0; j < nranks; ++j) *reinterpret_cast<float4*>(a.recv[j] + mine + i) = v;
+        } else {
+            for (int64_t k = i; k < c1; ++k) {
+                const float v = in[k];
+                for (int j = 0; j < nranks; ++j) a.recv[j][mine + k] = v;
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int timed_out;
+    if (threadIdx.x == 0) timed_out = 0;
+    __syncthreads();
+    if ((int)threadIdx.x < nranks && (int)threadIdx.x != rank) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the pushed bytes reach every peer
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.flags[threadIdx.x] + rank * kP2pMaxBlocks + blockIdx.x, epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+
+    // phase 2: wait for this chunk from every peer, then reduce the N local slots in rank order
+    if ((int)threadIdx.x < nranks && (int)threadIdx.x != rank) {
+        const unsigned* f = a.flags[rank] + threadIdx.x * kP2pMaxBlocks + blockIdx.x;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+                timed_out = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const float* base = a.recv[rank] + (int64_t)parity * kP2pMaxRanks * cap;
+    if (timed_out) {
+        if (threadIdx.x == 0) atomicOr(err, 1u);
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) out[i] = __builtin_nanf("");
+        return;
+    }
+    for (int64_t i = c0 + 4 * (int64_t)threadIdx.x; i < c1; i += 4 * (int64_t)blockDim.x) {
+        if (i + 4 <= c1) {
+            float4 s = *reinterpret_cast<const float4*>(base + i);
+            for (int r = 1; r < nranks; ++r) {
+                const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)r * cap + i);
+                s.x = red(s.x, v.x, op);
+                s.y = red(s.y, v.y, op);
+                s.z = red(s.z, v.z, op);
+                s.w = red(s.w, v.w, op);
+            }
+            *reinterpret_cast<float4*>(out + i) = s;
+        } else {
+            for (int64_t k = i; k < c1; ++k) {
+                float s = base[k];
+                for (int r = 1; r < nranks; ++r) s = red(s, base[(int64_t)r * cap + k], op);
+                out[k] = s;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+int64_t p2p_chunk(int64_t n) {
+    // 1024 floats per workgroup (one float4 per thread) up to kP2pMaxBlocks workgroups, then wider chunks
+    const int64_t per = 1024;
+    const int64_t groups = (n + per - 1) / per;
+    const int64_t mult = (groups + kP2pMaxBlocks - 1) / kP2pMaxBlocks;
+    return per * (mult > 0 ? mult : 1);
+}
+
+void launch_p2p_allreduce(const float* in, float* out, int64_t n, const P2pArgs& a, int rank, int nranks,
+                          unsigned epoch, int64_t cap, int op, unsigned* err, double timeout_s, hipStream_t stream) {
+    if (n <= 0) return;
+    if (nranks < 1 || nranks > kP2pMaxRanks || rank < 0 || rank >= nranks || n > cap || cap % 4 != 0 ||
+        (reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) % 16 != 0)
+        throw std::runtime_error("launch_p2p_allreduce: bad arguments (n=" + std::to_string(n) + ", cap=" +
+                                 std::to_string(cap) + ", ranks=" + std::to_string(nranks) + ", 16-B aligned buffers)");
+    const int64_t chunk = p2p_chunk(n);
+    const int64_t blocks = (n + chunk - 1) / chunk;
+    if (blocks > kP2pMaxBlocks) throw std::runtime_error("launch_p2p_allreduce: too many chunks");
+    const uint64_t ticks = (uint64_t)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
+    hipLaunchKernelGGL(k_p2p_allreduce, dim3((unsigned)blocks), dim3(256), 0, stream, in, out, n, chunk, a, rank,
+                       nranks, epoch, (int)(epoch & 1u), cap, op, err, ticks);
+    check_launch("k_p2p_allreduce");
+}
+
+}  // namespace sart

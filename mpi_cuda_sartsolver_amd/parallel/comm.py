@@ -153,7 +153,10 @@ def native_communicator(comm: Optional[Communicator], device: int = 0):
     * ``nccl`` process group -> the engine's own RCCL communicator over xGMI (unique id handed out through
       the process group) with a TCP side channel for host scalars;
     * ``gloo`` -> staged communicator (device buffers staged through the TCP host communicator,
-      reductions in fixed rank order), e.g. several ranks sharing one GPU in tests.
+      reductions in fixed rank order), e.g. several ranks sharing one GPU in tests;
+    * both wrapped in the one-shot P2P all-reduce (csrc/kernels/p2p_allreduce.hip) per ``SART_P2P``:
+      ``auto`` (default; RCCL groups only: used when faster than RCCL at the engine's message size),
+      ``1`` (forced, also over gloo), ``0`` (off). ``native.describe`` says what was chosen and why.
     """
     from ..ops import hip
 
@@ -165,11 +168,16 @@ def native_communicator(comm: Optional[Communicator], device: int = 0):
         return cached
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = comm.broadcast_object(_free_port() if comm.rank == 0 else None, src=0)
+    p2p = os.environ.get("SART_P2P", "auto")
     if getattr(comm, "backend", "gloo") == "nccl":
         uid = comm.broadcast_object(k.rccl_unique_id() if comm.rank == 0 else None, src=0)
         native = k.rccl_comm(device, uid, comm.rank, comm.world_size, host, int(port))
+        if p2p not in ("0", "off"):  # one-shot P2P all-reduce over xGMI (self-tested, timed against RCCL)
+            native = k.p2p_comm(device, native)
     else:
         native = k.staged_comm(comm.rank, comm.world_size, host, int(port))
+        if p2p in ("1", "on"):  # several ranks sharing one GPU (tests): exercise the P2P kernel path
+            native = k.p2p_comm(device, native)
     comm._native_comm = native
     return native
 

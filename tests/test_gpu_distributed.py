@@ -19,9 +19,9 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(nproc, out, extra):
-    env = dict(os.environ, PYTHONPATH=ROOT, SART_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    script = os.path.join(ROOT, "tools", "dist_check.py")
+def _run(nproc, out, extra, script="dist_check.py", **env_extra):
+    env = dict(os.environ, PYTHONPATH=ROOT, SART_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", **env_extra)
+    script = os.path.join(ROOT, "tools", script)
     if nproc == 1:
         cmd = [sys.executable, script, "--out", out, *extra]
     else:
@@ -29,6 +29,8 @@ def _run(nproc, out, extra):
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), script, "--out", out, *extra]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    if script != "dist_check.py":
+        return json.load(open(out))
     return np.load(out + ".npy"), json.load(open(out + ".json"))
 
 
@@ -54,3 +56,28 @@ def test_column_shard_matches_row_shard(tmp_path, log):
     assert np.linalg.norm(xc - xr) / np.linalg.norm(xr) < 2e-3
     for a, b in zip(mc, mr):
         assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_p2p_allreduce_bitwise(tmp_path, nproc):
+    """One-shot P2P all-reduce (csrc/kernels/p2p_allreduce.hip) through IPC-mapped buffers of several
+    processes on one GPU: bitwise equal to the rank-order sum / maximum at every size, both call parities;
+    vectors above SART_P2P_MAX_BYTES go through the base communicator."""
+    res = _run(nproc, str(tmp_path / "comm.json"), [], script="comm_check.py", SART_P2P="1")
+    assert res["backend"] == "p2p", res["describe"]
+    for r in res["results"]:
+        if r["n"] * 4 <= 2 * 1024 * 1024:
+            assert r["exact"], r
+        else:  # staged fallback: fp64 host reduction, rounded once
+            assert r["close"], r
+
+
+@pytest.mark.parametrize("extra", [[], ["--logarithmic"], ["--multiframe"]])
+def test_gpu_solver_rank_invariance_p2p(tmp_path, extra):
+    x1, m1 = _run(1, str(tmp_path / "r1"), extra)
+    for n in (2, 3):
+        x, m = _run(n, str(tmp_path / f"p{n}"), extra, SART_P2P="1")
+        assert m[0]["comm"] == "p2p"
+        assert np.linalg.norm(x - x1) / np.linalg.norm(x1) < 2e-3
+        for a, b in zip(m, m1):
+            assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3

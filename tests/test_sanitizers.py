@@ -17,7 +17,7 @@ def test_host_runtime_asan_ubsan(tmp_path):
     exe = tmp_path / "host_selftest"
     srcs = [ROOT / "csrc" / "tests" / "host_selftest.cpp"] + [
         NATIVE / f for f in ("config.cpp", "cpu_kernels.cpp", "cpu_solver.cpp", "fixtures.cpp", "frames.cpp", "h5.cpp",
-                             "host_comm.cpp", "inputs.cpp", "solver_params.cpp")]
+                             "host_comm.cpp", "host_comm_mpi.cpp", "inputs.cpp", "solver_params.cpp")]
     hdf5 = _build.HDF5_PREFIX
     libdir = tmp_path / "hdf5"
     libdir.mkdir()
@@ -26,7 +26,7 @@ def test_host_runtime_asan_ubsan(tmp_path):
             (libdir / so.name).symlink_to(so)
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
            "-fno-sanitize-recover=undefined", "-fopenmp", "-DSART_HAVE_HDF5=1", f"-isystem{hdf5 / 'include'}",
-           *map(str, srcs), str(hdf5 / "lib" / "libhdf5.so"), f"-Wl,-rpath,{libdir}", "-o", str(exe)]
+           *map(str, srcs), str(hdf5 / "lib" / "libhdf5.so"), "-ldl", f"-Wl,-rpath,{libdir}", "-o", str(exe)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
     # verify_asan_link_order=0: the environment may preload libraries ahead of the ASan runtime

@@ -49,14 +49,14 @@ def main():
         g = prob.measurement.cpu().numpy()
         res = s.solve_batch(np.stack([g, 0.5 * g, 2.0 * g]))
         x = np.stack([r.solution for r in res])
-        meta = [dict(status=r.status, iterations=r.iterations) for r in res]
+        meta = [dict(status=r.status, iterations=r.iterations, comm=s.native_comm.backend) for r in res]
     else:
         s = SARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic, use_fused=a.fused,
                        partition="cols" if a.columns else None)
         r = s.solve(prob.measurement)
         r2 = s.solve(prob.measurement, solution=r.solution)  # warm start path
         x = np.stack([s.gather_solution(r.solution), s.gather_solution(r2.solution)])
-        meta = [dict(status=r.status, iterations=r.iterations, fused=r.used_fused),
+        meta = [dict(status=r.status, iterations=r.iterations, fused=r.used_fused, comm=s.native_comm.backend),
                 dict(status=r2.status, iterations=r2.iterations)]
     if comm.rank == 0:
         np.save(a.out + ".npy", x)
