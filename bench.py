@@ -183,6 +183,8 @@ def main() -> int:
         "fused_rows_per_tile": solver.geom.T if use_fused else None,
         "fused_schedule": solver.k.fused_get_schedule() if use_fused else None,
         "frames_per_step": args.frames,
+        # per-iteration device all-reduce: RCCL, or the one-shot P2P kernel when it beat RCCL at start-up
+        "allreduce": (solver.native_comm.describe if n > 1 else "none (1 rank)"),
         "effective_hbm_TBps_per_gpu": round(bytes_per_iter * iters_per_s / 1e12, 3),
         "config": {
             "model": f"SART-{args.variant} dense RTM" + (" + Laplacian" if lap is not None else "")

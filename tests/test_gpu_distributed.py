@@ -21,12 +21,12 @@ def _port():
 
 def _run(nproc, out, extra, script="dist_check.py", **env_extra):
     env = dict(os.environ, PYTHONPATH=ROOT, SART_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", **env_extra)
-    script = os.path.join(ROOT, "tools", script)
+    path = os.path.join(ROOT, "tools", script)
     if nproc == 1:
-        cmd = [sys.executable, script, "--out", out, *extra]
+        cmd = [sys.executable, path, "--out", out, *extra]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
-               "--master-addr", "127.0.0.1", "--master-port", str(_port()), script, "--out", out, *extra]
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), path, "--out", out, *extra]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     if script != "dist_check.py":
