@@ -57,31 +57,32 @@ __device__ __forceinline__ void load_groups(float (&dst)[NG], const float* __res
 }
 
 // F[row][f] = sum_v A[row][v] X[f][v]. X is frame-major [nf][ldx] (ldx == ld), F is [rows][nf].
-// One wave: 32 rows (two 16-row tiles sharing each X fragment) x nf frames, K = the columns of its
-// split; every float4 of A feeds 4 * NG MFMAs (one per k-component and column group).
+// One wave: 16 * RT rows (RT 16-row tiles sharing each X fragment) x nf frames, K = the columns of its
+// split; every float4 of A feeds 4 * NG MFMAs (one per k-component and column group) and every X
+// fragment 4 * RT. RT = 4 halves the X operand traffic per byte of A against RT = 2 (X is L2 / MALL
+// resident, but at nf = 64 it is twice the A stream with RT = 2).
 // Split-K: blockIdx.y selects the column range [k0, k1) (multiples of 16 columns) and the kernel
 // writes Fout + blockIdx.y * nrows_pad * nf; the caller sums the splits.
-template <int NG, int DEPTH>
+template <int NG, int DEPTH, int RT>
 __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A, int64_t ld, int64_t nrows,
                                                     int64_t nrows_pad, const float* __restrict__ X,
                                                     int64_t ldx, float* __restrict__ Fout, int64_t cols_per_split) {
     constexpr int NF = 16 * NG;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * 32;
-    if (row0 >= nrows_pad) return;  // wave-uniform
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * (16 * RT);
+    if (row0 >= nrows_pad) return;  // wave-uniform; nrows_pad is a multiple of 16 * RT
     const int g = lane >> 4, r = lane & 15;
     const int64_t ld4 = ld >> 2, ldx4 = ldx >> 2;
     const int64_t c0 = (int64_t)blockIdx.y * cols_per_split;
     const int64_t c1 = (c0 + cols_per_split < ld) ? c0 + cols_per_split : ld;
     Fout += (int64_t)blockIdx.y * nrows_pad * NF;
     const float4* __restrict__ a0p = reinterpret_cast<const float4*>(A) + (row0 + r) * ld4 + g + c0 / 4;
-    const float4* __restrict__ a1p = a0p + 16 * ld4;
     const float4* __restrict__ xp = reinterpret_cast<const float4*>(X) + (int64_t)r * ldx4 + g + c0 / 4;
     const int64_t xg = 16 * ldx4;  // next column group of X
 
-    floatx4 acc[2][2][NG];  // [row tile][k half][column group]
+    floatx4 acc[RT][2][NG];  // [row tile][k half][column group]
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < RT; ++t)
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -91,13 +92,14 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
     const int64_t nst = nq / 8;                        // 8-float4 steps
     if (nst > 0) {
         constexpr int RS = DEPTH + 1;
-        float4 a[RS][2][2], x[RS][2][NG];
+        float4 a[RS][RT][2], x[RS][2][NG];
         auto load = [&](int sl, int64_t t) {
             const int64_t qq = t * 8;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                a[sl][0][h] = a0p[qq + 4 * h];  // plain loads: a row's two 64-B halves come from two
-                a[sl][1][h] = a1p[qq + 4 * h];  // instructions; non-temporal loads measured 10-18 % slower here
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)  // plain loads: a row's two 64-B halves come from two
+                    a[sl][rt][h] = a0p[rt * 16 * ld4 + qq + 4 * h];  // instructions; nt loads measured slower
 #pragma unroll
                 for (int j = 0; j < NG; ++j) x[sl][h][j] = xp[j * xg + qq + 4 * h];
             }
@@ -112,12 +114,14 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
 #pragma unroll
             for (int c = 0; c < 4; ++c)
 #pragma unroll
-                for (int j = 0; j < NG; ++j) {
-                    acc[0][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a[sl][0][0], c), comp(x[sl][0][j], c), acc[0][0][j], 0, 0, 0);
-                    acc[1][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a[sl][1][0], c), comp(x[sl][0][j], c), acc[1][0][j], 0, 0, 0);
-                    acc[0][1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a[sl][0][1], c), comp(x[sl][1][j], c), acc[0][1][j], 0, 0, 0);
-                    acc[1][1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a[sl][1][1], c), comp(x[sl][1][j], c), acc[1][1][j], 0, 0, 0);
-                }
+                for (int j = 0; j < NG; ++j)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt)
+                            acc[rt][h][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a[sl][rt][h], c),
+                                                                                comp(x[sl][h][j], c), acc[rt][h][j],
+                                                                                0, 0, 0);
         };
         for (int64_t t0 = 0; t0 < nst; t0 += RS) {
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
@@ -126,26 +130,30 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
         }
     }
     for (int64_t q = nst * 8; q < nq; q += 4) {  // 4-float4 tail of a ragged split
-        const float4 a00 = a0p[q], a10 = a1p[q];
+        float4 at[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) at[rt] = a0p[rt * 16 * ld4 + q];
 #pragma unroll
         for (int j = 0; j < NG; ++j) {
             const float4 x0 = xp[j * xg + q];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                acc[0][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a00, c), comp(x0, c), acc[0][0][j], 0, 0, 0);
-                acc[1][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a10, c), comp(x0, c), acc[1][0][j], 0, 0, 0);
-            }
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt)
+                    acc[rt][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(at[rt], c), comp(x0, c), acc[rt][0][j],
+                                                                        0, 0, 0);
         }
     }
     // D: col = frame = 16 j + (lane & 15), row = (lane >> 4) * 4 + reg
 #pragma unroll
     for (int j = 0; j < NG; ++j)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t ra = row0 + g * 4 + i, rb = ra + 16;
-            if (ra < nrows) Fout[ra * NF + 16 * j + r] = acc[0][0][j][i] + acc[0][1][j][i];
-            if (rb < nrows) Fout[rb * NF + 16 * j + r] = acc[1][0][j][i] + acc[1][1][j][i];
-        }
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t ra = row0 + rt * 16 + g * 4 + i;
+                if (ra < nrows) Fout[ra * NF + 16 * j + r] = acc[rt][0][j][i] + acc[rt][1][j][i];
+            }
 }
 
 // partial[s][v][f] = sum_{rows of split s} A[row][v] W[row][f]. W is in the back-projection layout
@@ -274,15 +282,38 @@ static int mf_depth(bool forward, int nf) {
     return nf == 16 ? 2 : (nf == 32 ? 3 : 2);
 }
 
-template <int NG>
-static void fwd(dim3 grid, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
-                int64_t nrows_pad, const float* X, int64_t ldx, float* Fout, int64_t cps) {
+// Row tiles per wave of the forward kernel: 2 (32 rows) or 4 (64 rows); SART_MF_ROWS or mf_set_rows().
+static int g_mf_rows = -1;
+void mf_set_rows(int rt) { g_mf_rows = rt; }
+static int mf_rows(int nf) {
+    if (g_mf_rows < 0) {
+        const char* e = std::getenv("SART_MF_ROWS");
+        g_mf_rows = (e && *e) ? std::atoi(e) : 0;
+    }
+    if (g_mf_rows == 2 || g_mf_rows == 4) return g_mf_rows;
+    (void)nf;
+    return 2;
+}
+
+template <int NG, int RT>
+static void fwd_rt(dim3 grid, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
+                   int64_t nrows_pad, const float* X, int64_t ldx, float* Fout, int64_t cps) {
     if (depth == 1)
-        hipLaunchKernelGGL((k_mf_forward<NG, 1>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+        hipLaunchKernelGGL((k_mf_forward<NG, 1, RT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
     else if (depth == 3)
-        hipLaunchKernelGGL((k_mf_forward<NG, 3>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+        hipLaunchKernelGGL((k_mf_forward<NG, 3, RT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
     else
-        hipLaunchKernelGGL((k_mf_forward<NG, 2>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+        hipLaunchKernelGGL((k_mf_forward<NG, 2, RT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+}
+
+template <int NG>
+static void fwd(int rt, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
+                const float* X, int64_t ldx, float* Fout, int nsplit, int64_t cps) {
+    const dim3 grid((unsigned)((nrows_pad + 64 * rt - 1) / (64 * rt)), (unsigned)nsplit);
+    if (rt == 4)
+        fwd_rt<NG, 4>(grid, depth, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+    else
+        fwd_rt<NG, 2>(grid, depth, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
 }
 
 void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ldx,
@@ -292,14 +323,14 @@ void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_
     if (nsplit < 1) throw std::runtime_error("mf_forward: nsplit must be >= 1");
     check_nf(nf, "mf_forward");
     const int64_t cps = ((ld + nsplit - 1) / nsplit + 15) / 16 * 16;
-    const dim3 grid((unsigned)((nrows_pad + 127) / 128), (unsigned)nsplit);
     const int d = mf_depth(true, nf);
+    const int rt = (nrows_pad % 64 == 0) ? mf_rows(nf) : 2;  // a wave's 16 * rt rows lie inside the padding
     if (nf == 16)
-        fwd<1>(grid, d, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+        fwd<1>(rt, d, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, nsplit, cps);
     else if (nf == 32)
-        fwd<2>(grid, d, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+        fwd<2>(rt, d, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, nsplit, cps);
     else
-        fwd<4>(grid, d, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+        fwd<4>(rt, d, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, nsplit, cps);
     check_launch("k_mf_forward");
 }
 

@@ -123,9 +123,18 @@ def test_synthetic_shard_invariance(k, dev):
     assert abs(a.mean().item() - 0.5) < 0.01
 
 
+@pytest.mark.parametrize("rows", [2, 4])  # 16-row tiles per wave of the MFMA forward kernel
 @pytest.mark.parametrize("nf", [16, 32, 64])
 @pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (64, 1024), (2048, 4096), (1000, 1088)])
-def test_multiframe_mfma(k, dev, P, V, nf):
+def test_multiframe_mfma(k, dev, P, V, nf, rows):
+    k.mf_set_rows(rows)
+    try:
+        _check_multiframe_mfma(k, dev, P, V, nf)
+    finally:
+        k.mf_set_rows(0)
+
+
+def _check_multiframe_mfma(k, dev, P, V, nf):
     A, m = _rtm(dev, P, V, seed=11)
     rng = np.random.default_rng(4)
     X = rng.random((nf, V)).astype(np.float32)  # frame-major

@@ -47,6 +47,11 @@ for step in "$@"; do
     probe) run probe 600 python tools/probe.py ;;
     trace) run fused_trace 600 python tools/fused_trace.py ;;
     probef) PROBE_FUSED_ONLY=1 run probe_fused 600 python tools/probe.py ;;
+    commcheck) for n in 2 4; do
+                 SART_DIST_BACKEND=gloo SART_P2P=1 run comm_check_p2p_n$n 300 python -m torch.distributed.run --nnodes=1 \
+                   --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n)) tools/comm_check.py \
+                   --out "$OUT/comm_check_p2p_n$n.json" || exit 1
+               done ;;
     testsel) run pytest_sel 900 python -m pytest ${SEL:-tests} -m gpu -q -p no:cacheprovider ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -28,17 +28,23 @@ def main():
         W = torch.rand((m.nrows_pad, nf), device=dev)
         nsm = k.mf_backproject_num_splits(m.ld, P)
         partm = torch.zeros((nsm, m.ld, nf), device=dev)
+        fwd_only = os.environ.get("PROBE_MF_FORWARD_ONLY") == "1"
         for depth in (1, 2, 3):
             k.mf_set_depth(depth)
-            for op, fn in (("mf_forward", lambda: k.mf_forward(m.A.data_ptr(), m.ld, P, m.nrows_pad, X.data_ptr(),
-                                                                m.ld, Fo.data_ptr(), nsf, s, nf)),
-                           ("mf_backproject", lambda: k.mf_backproject(m.A.data_ptr(), m.ld, P, W.data_ptr(), nsm,
-                                                                        partm.data_ptr(), s, nf))):
-                med, best = timeit(fn, reps=7)
-                print(json.dumps(dict(kind="kernel", op=op, nf=nf, depth=depth, P=P, V=V, ms=round(med, 4),
-                                      GBps=round(nbytes / med / 1e6, 1), TFLOPs=round(2 * nf * P * V / med / 1e9, 2))),
-                      flush=True)
+            for rt in (2, 4):  # 16-row tiles per wave of the forward kernel
+                k.mf_set_rows(rt)
+                cases = [("mf_forward", lambda: k.mf_forward(m.A.data_ptr(), m.ld, P, m.nrows_pad, X.data_ptr(),
+                                                             m.ld, Fo.data_ptr(), nsf, s, nf))]
+                if rt == 2 and not fwd_only:
+                    cases.append(("mf_backproject", lambda: k.mf_backproject(m.A.data_ptr(), m.ld, P, W.data_ptr(),
+                                                                             nsm, partm.data_ptr(), s, nf)))
+                for op, fn in cases:
+                    med, best = timeit(fn, reps=7)
+                    print(json.dumps(dict(kind="kernel", op=op, nf=nf, depth=depth, rows_per_wave=16 * rt, P=P, V=V,
+                                          ms=round(med, 4), GBps=round(nbytes / med / 1e6, 1),
+                                          TFLOPs=round(2 * nf * P * V / med / 1e9, 2))), flush=True)
         k.mf_set_depth(0)
+        k.mf_set_rows(0)
         del X, Fo, W, partm
         torch.cuda.empty_cache()
 
