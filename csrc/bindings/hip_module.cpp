@@ -367,6 +367,7 @@ PYBIND11_MODULE(_sart_hip, m) {
     m.def("mf_backproject_num_splits", &sart::mf_backproject_num_splits);
     m.def("mf_set_depth", &sart::mf_set_depth);
     m.def("mf_set_rows", &sart::mf_set_rows);
+    m.def("mf_set_vox", &sart::mf_set_vox);
     m.def("mf_forward", [](uintptr_t A, int64_t ld, int64_t nrows, int64_t nrows_pad, uintptr_t X, int64_t ldx,
                            uintptr_t Fout, int nsplit, uintptr_t stream, int nf) {
         sart::launch_mf_forward(P<const float>(A), ld, nrows, nrows_pad, P<const float>(X), ldx, P<float>(Fout),

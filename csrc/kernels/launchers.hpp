@@ -84,6 +84,7 @@ int mf_forward_num_splits(int64_t ld, int64_t nrows_pad);
 int mf_backproject_num_splits(int64_t ld, int64_t nrows);
 void mf_set_depth(int d);  // 1..3: register-ring depth of the MFMA projections; 0: default
 void mf_set_rows(int rt);  // 2 or 4: 16-row tiles per wave of the MFMA forward projection; 0: default
+void mf_set_vox(int vt);   // 1 or 2: 64-voxel tiles per wave of the MFMA back-projection; 0: default
 void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ldx,
                        float* Fout, int nsplit, int nf, hipStream_t stream);
 void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,

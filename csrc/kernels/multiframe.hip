@@ -104,13 +104,14 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
                 for (int j = 0; j < NG; ++j) x[sl][h][j] = xp[j * xg + qq + 4 * h];
             }
         };
+        // Unconditional loads, clamped to the last step: with path-independent load counts the compiler
+        // keeps DEPTH steps in flight (counted vmcnt) instead of draining the ring at every step.
 #pragma unroll
-        for (int d = 0; d < DEPTH; ++d)
-            if (d < nst) load(d, d);
+        for (int d = 0; d < DEPTH; ++d) load(d, d < nst ? d : nst - 1);
         auto step = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
+            load((sl + DEPTH) % RS, t + DEPTH < nst ? t + DEPTH : nst - 1);
             if (t >= nst) return;
-            if (t + DEPTH < nst) load((sl + DEPTH) % RS, t + DEPTH);
 #pragma unroll
             for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -159,57 +160,64 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
 // partial[s][v][f] = sum_{rows of split s} A[row][v] W[row][f]. W is in the back-projection layout
 // [rows][16][NG] (frame f = 16 j + i at position i * NG + j, mf_bp_slot in multiframe_glue.hip), so a
 // lane's NG column-group operands are one contiguous vector load. partial is [splits][ld][nf] in natural
-// frame order. One wave: 64 voxels x nf frames; a float4 of A (4 voxels of one row) feeds 4 * NG MFMAs,
-// one per output tile c (voxel set {v0 + 4 i + c : i = 0..15}) and column group j.
-template <int NG, int DEPTH>
+// frame order. One wave: 64 * VT voxels x nf frames; a float4 of A (4 voxels of one row) feeds 4 * NG
+// MFMAs, one per output tile c (voxel set {v0 + 4 i + c : i = 0..15}) and column group j, and every W
+// operand feeds 4 * VT (VT = 2 halves the W traffic per byte of A; needs ld % 128 == 0).
+template <int NG, int DEPTH, int VT>
 __global__ __launch_bounds__(256) void k_mf_backproject(const float* __restrict__ A, int64_t ld, int64_t nrows,
                                                         const float* __restrict__ W, int64_t rows_per_split,
                                                         float* __restrict__ partial) {
     constexpr int NF = 16 * NG;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t vb = (int64_t)blockIdx.x * 4 + wave;  // 64-voxel block
-    if (vb * 64 >= ld) return;
+    const int64_t vb = (int64_t)blockIdx.x * 4 + wave;  // block of 64 * VT voxels
+    if (vb * 64 * VT >= ld) return;
     const int g = lane >> 4, i16 = lane & 15;
     const int64_t ld4 = ld >> 2;
     const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
     int64_t r_end = r_begin + rows_per_split;
     if (r_end > nrows) r_end = nrows;
 
-    const float4* __restrict__ ap = reinterpret_cast<const float4*>(A) + vb * 16 + i16;
+    const float4* __restrict__ ap = reinterpret_cast<const float4*>(A) + vb * 16 * VT + i16;
     const float* __restrict__ wp = W + i16 * NG;
-    floatx4 acc[4][NG];
+    floatx4 acc[VT][4][NG];
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int vt = 0; vt < VT; ++vt)
 #pragma unroll
-        for (int j = 0; j < NG; ++j) acc[c][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int j = 0; j < NG; ++j) acc[vt][c][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
     const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 16 : 0;  // 16-row steps
     if (nst > 0) {
         constexpr int RS = DEPTH + 1;
-        float4 av[RS][4];
+        float4 av[RS][4][VT];
         float wv[RS][4][NG];
         auto load = [&](int sl, int64_t t) {
             const int64_t rr = r_begin + t * 16;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                av[sl][u] = load_stream(ap + (rr + 4 * u + g) * ld4);
+#pragma unroll
+                for (int vt = 0; vt < VT; ++vt) av[sl][u][vt] = load_stream(ap + (rr + 4 * u + g) * ld4 + vt * 16);
                 load_groups<NG>(wv[sl][u], wp + (rr + 4 * u + g) * NF);
             }
         };
+        // Unconditional loads, clamped to the last step (see k_mf_forward): counted vmcnt in the ring.
 #pragma unroll
-        for (int d = 0; d < DEPTH; ++d)
-            if (d < nst) load(d, d);
+        for (int d = 0; d < DEPTH; ++d) load(d, d < nst ? d : nst - 1);
         auto step = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
+            load((sl + DEPTH) % RS, t + DEPTH < nst ? t + DEPTH : nst - 1);
             if (t >= nst) return;
-            if (t + DEPTH < nst) load((sl + DEPTH) % RS, t + DEPTH);
 #pragma unroll
             for (int u = 0; u < 4; ++u)
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
 #pragma unroll
                     for (int j = 0; j < NG; ++j)
-                        acc[c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(av[sl][u], c), wv[sl][u][j], acc[c][j], 0, 0, 0);
+#pragma unroll
+                        for (int vt = 0; vt < VT; ++vt)
+                            acc[vt][c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(av[sl][u][vt], c), wv[sl][u][j],
+                                                                                acc[vt][c][j], 0, 0, 0);
         };
         for (int64_t t0 = 0; t0 < nst; t0 += RS) {
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
@@ -219,35 +227,44 @@ __global__ __launch_bounds__(256) void k_mf_backproject(const float* __restrict_
     }
     for (int64_t r0 = r_begin + nst * 16; r0 < r_end; r0 += 4) {  // ragged tail, 4 rows per MFMA
         const int64_t row = r0 + g;
-        float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 av[VT];
         float wv[NG];
+#pragma unroll
+        for (int vt = 0; vt < VT; ++vt) av[vt] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int j = 0; j < NG; ++j) wv[j] = 0.f;
         if (row < r_end) {
-            av = load_stream(ap + row * ld4);
+#pragma unroll
+            for (int vt = 0; vt < VT; ++vt) av[vt] = load_stream(ap + row * ld4 + vt * 16);
             load_groups<NG>(wv, wp + row * NF);
         }
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
             for (int j = 0; j < NG; ++j)
-                acc[c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(av, c), wv[j], acc[c][j], 0, 0, 0);
+#pragma unroll
+                for (int vt = 0; vt < VT; ++vt)
+                    acc[vt][c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(av[vt], c), wv[j], acc[vt][c][j], 0, 0, 0);
     }
     float* out = partial + (int64_t)blockIdx.y * ld * NF;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int vt = 0; vt < VT; ++vt)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t v = vb * 64 + 4 * (g * 4 + q) + c;
+        for (int c = 0; c < 4; ++c)
 #pragma unroll
-            for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[c][j][q];
-        }
+            for (int q = 0; q < 4; ++q) {
+                const int64_t v = (vb * VT + vt) * 64 + 4 * (g * 4 + q) + c;
+#pragma unroll
+                for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[vt][c][j][q];
+            }
 }
 
 // Split-K of the forward projection: >= ~1024 workgroups, >= 1024 columns per split. (Splitting further
 // so that a split's X chunk stays L2-resident measured 0-9 % slower at nf = 16..64, 64k x 64k.)
+static int mf_rows(int nf);
 int mf_forward_num_splits(int64_t ld, int64_t nrows_pad) {
-    const int64_t nblk = (nrows_pad + 127) / 128;
+    const int64_t rows_per_block = (nrows_pad % 64 == 0 ? mf_rows(0) : 2) * 64;  // 4 waves x 16 * rt rows
+    const int64_t nblk = (nrows_pad + rows_per_block - 1) / rows_per_block;
     int64_t s = (1024 + nblk - 1) / nblk;
     const int64_t smax = ld / 1024;
     if (s > smax) s = smax;
@@ -255,8 +272,9 @@ int mf_forward_num_splits(int64_t ld, int64_t nrows_pad) {
     return (int)s;
 }
 
+static int mf_vox(int64_t ld, int nf);
 int mf_backproject_num_splits(int64_t ld, int64_t nrows) {
-    const int64_t nblk = (ld / 64 + 3) / 4;
+    const int64_t nblk = (ld / (64 * mf_vox(ld, kMfMaxFrames)) + 3) / 4;
     int64_t s = (2048 + nblk - 1) / nblk;
     const int64_t smax = (nrows + 63) / 64;
     if (s > smax) s = smax;
@@ -269,7 +287,9 @@ static void check_nf(int nf, const char* what) {
 }
 
 // Register-ring depth (steps of loads in flight per wave). Defaults per kernel and batch width from
-// tools/probe_mf.py on 64k x 64k; SART_MF_DEPTH=1..3 or mf_set_depth() overrides them.
+// tools/probe_mf.py on 64k x 64k (profiles/probe_r1_mf_tiles.jsonl, with the default tilings below: forward
+// 64 rows per wave, back-projection 64 voxels per wave at nf = 16 and 128 at nf = 32 / 64); SART_MF_DEPTH=1..3
+// or mf_set_depth() overrides them.
 static int g_mf_depth = -1;
 void mf_set_depth(int d) { g_mf_depth = d; }
 static int mf_depth(bool forward, int nf) {
@@ -278,8 +298,20 @@ static int mf_depth(bool forward, int nf) {
         g_mf_depth = (e && *e) ? std::atoi(e) : 0;
     }
     if (g_mf_depth >= 1 && g_mf_depth <= 3) return g_mf_depth;
-    if (forward) return nf == 16 ? 2 : (nf == 32 ? 1 : 3);
-    return nf == 16 ? 2 : (nf == 32 ? 3 : 2);
+    if (forward) return nf == 64 ? 2 : 3;           // with 64-row waves (profiles/probe_r1_mf_tiles.jsonl)
+    return nf == 32 ? 1 : 2;                         // nf 16: 64-voxel waves; nf 32 / 64: 128-voxel waves
+}
+
+// 64-voxel tiles per wave of the back-projection: 1 or 2 (ld % 128 == 0); SART_MF_VOX or mf_set_vox().
+static int g_mf_vox = -1;
+void mf_set_vox(int vt) { g_mf_vox = vt; }
+static int mf_vox(int64_t ld, int nf) {
+    if (g_mf_vox < 0) {
+        const char* e = std::getenv("SART_MF_VOX");
+        g_mf_vox = (e && *e) ? std::atoi(e) : 0;
+    }
+    const int vt = (g_mf_vox == 1 || g_mf_vox == 2) ? g_mf_vox : (nf >= 32 ? 2 : 1);
+    return (vt == 2 && ld % 128 == 0) ? 2 : 1;
 }
 
 // Row tiles per wave of the forward kernel: 2 (32 rows) or 4 (64 rows); SART_MF_ROWS or mf_set_rows().
@@ -292,7 +324,7 @@ static int mf_rows(int nf) {
     }
     if (g_mf_rows == 2 || g_mf_rows == 4) return g_mf_rows;
     (void)nf;
-    return 2;
+    return 4;
 }
 
 template <int NG, int RT>
@@ -334,15 +366,25 @@ void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_
     check_launch("k_mf_forward");
 }
 
-template <int NG>
-static void bwd(dim3 grid, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows, const float* W,
-                int64_t rps, float* partial) {
+template <int NG, int VT>
+static void bwd_vt(dim3 grid, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows, const float* W,
+                   int64_t rps, float* partial) {
     if (depth == 1)
-        hipLaunchKernelGGL((k_mf_backproject<NG, 1>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
+        hipLaunchKernelGGL((k_mf_backproject<NG, 1, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
     else if (depth == 3)
-        hipLaunchKernelGGL((k_mf_backproject<NG, 3>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
+        hipLaunchKernelGGL((k_mf_backproject<NG, 3, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
     else
-        hipLaunchKernelGGL((k_mf_backproject<NG, 2>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
+        hipLaunchKernelGGL((k_mf_backproject<NG, 2, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
+}
+
+template <int NG>
+static void bwd(int vt, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows, const float* W,
+                int nsplit, int64_t rps, float* partial) {
+    const dim3 grid((unsigned)((ld / (64 * vt) + 3) / 4), (unsigned)nsplit);
+    if (vt == 2)
+        bwd_vt<NG, 2>(grid, depth, stream, A, ld, nrows, W, rps, partial);
+    else
+        bwd_vt<NG, 1>(grid, depth, stream, A, ld, nrows, W, rps, partial);
 }
 
 void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,
@@ -350,14 +392,14 @@ void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const floa
     if (ld % 64 != 0) throw std::runtime_error("mf_backproject: ld must be a multiple of 64");
     check_nf(nf, "mf_backproject");
     const int64_t rps = ((nrows + nsplit - 1) / nsplit + 15) / 16 * 16;
-    const dim3 grid((unsigned)((ld / 64 + 3) / 4), (unsigned)nsplit);
     const int d = mf_depth(false, nf);
+    const int vt = mf_vox(ld, nf);
     if (nf == 16)
-        bwd<1>(grid, d, stream, A, ld, nrows, W, rps, partial);
+        bwd<1>(vt, d, stream, A, ld, nrows, W, nsplit, rps, partial);
     else if (nf == 32)
-        bwd<2>(grid, d, stream, A, ld, nrows, W, rps, partial);
+        bwd<2>(vt, d, stream, A, ld, nrows, W, nsplit, rps, partial);
     else
-        bwd<4>(grid, d, stream, A, ld, nrows, W, rps, partial);
+        bwd<4>(vt, d, stream, A, ld, nrows, W, nsplit, rps, partial);
     check_launch("k_mf_backproject");
 }
 

@@ -128,10 +128,12 @@ def test_synthetic_shard_invariance(k, dev):
 @pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (64, 1024), (2048, 4096), (1000, 1088)])
 def test_multiframe_mfma(k, dev, P, V, nf, rows):
     k.mf_set_rows(rows)
+    k.mf_set_vox(rows // 2)  # 64-voxel tiles per wave of the back-projection: 1 or 2
     try:
         _check_multiframe_mfma(k, dev, P, V, nf)
     finally:
         k.mf_set_rows(0)
+        k.mf_set_vox(0)
 
 
 def _check_multiframe_mfma(k, dev, P, V, nf):

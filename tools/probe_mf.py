@@ -23,28 +23,32 @@ def main():
     nbytes = m.nbytes
     for nf in (16, 32, 64):
         X = torch.rand((nf, m.ld), device=dev)
-        nsf = k.mf_forward_num_splits(m.ld, m.nrows_pad)
-        Fo = torch.zeros((nsf, m.nrows_pad, nf), device=dev)
+        Fo = torch.zeros((16, m.nrows_pad, nf), device=dev)  # room for the split counts of either row tiling
         W = torch.rand((m.nrows_pad, nf), device=dev)
-        nsm = k.mf_backproject_num_splits(m.ld, P)
-        partm = torch.zeros((nsm, m.ld, nf), device=dev)
+        partm = torch.zeros((16, m.ld, nf), device=dev)  # room for the split counts of either voxel tiling
         fwd_only = os.environ.get("PROBE_MF_FORWARD_ONLY") == "1"
         for depth in (1, 2, 3):
             k.mf_set_depth(depth)
             for rt in (2, 4):  # 16-row tiles per wave of the forward kernel
                 k.mf_set_rows(rt)
+                nsf = k.mf_forward_num_splits(m.ld, m.nrows_pad)
+                assert nsf <= 16
                 cases = [("mf_forward", lambda: k.mf_forward(m.A.data_ptr(), m.ld, P, m.nrows_pad, X.data_ptr(),
                                                              m.ld, Fo.data_ptr(), nsf, s, nf))]
-                if rt == 2 and not fwd_only:
+                if not fwd_only:  # rt selects the voxel tiles of the back-projection: 1 (rt 2) or 2 (rt 4)
+                    k.mf_set_vox(rt // 2)
+                    nsm = k.mf_backproject_num_splits(m.ld, P)
+                    assert nsm <= 16
                     cases.append(("mf_backproject", lambda: k.mf_backproject(m.A.data_ptr(), m.ld, P, W.data_ptr(),
                                                                              nsm, partm.data_ptr(), s, nf)))
                 for op, fn in cases:
                     med, best = timeit(fn, reps=7)
-                    print(json.dumps(dict(kind="kernel", op=op, nf=nf, depth=depth, rows_per_wave=16 * rt, P=P, V=V,
+                    print(json.dumps(dict(kind="kernel", op=op, nf=nf, depth=depth, tile=(16 * rt if op == "mf_forward" else 32 * rt), P=P, V=V,
                                           ms=round(med, 4), GBps=round(nbytes / med / 1e6, 1),
                                           TFLOPs=round(2 * nf * P * V / med / 1e9, 2))), flush=True)
         k.mf_set_depth(0)
         k.mf_set_rows(0)
+        k.mf_set_vox(0)
         del X, Fo, W, partm
         torch.cuda.empty_cache()
 
