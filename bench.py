@@ -132,9 +132,10 @@ def main() -> int:
 
         runner = _Batch(solver)
     else:
+        # time_collectives (N > 1): timing events around each per-iteration all-reduce (GPU-side only)
         solver = SARTSolver(prob.rtm, lap, comm, params, logarithmic=args.variant == "log",
                             use_fused=not args.no_fused, check_interval=32, allow_zero_tolerance=True,
-                            partition=args.partition)
+                            partition=args.partition, time_collectives=n > 1)
         g = prob.measurement
         runner = solver
     multi = args.frames > 1
@@ -146,10 +147,12 @@ def main() -> int:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     iters = 0
+    comm_ms = 0.0
     res = None
     for _ in range(args.steps):
         res = runner.solve(g)
         iters += res.iterations
+        comm_ms += max(getattr(res, "comm_ms", -1.0), 0.0)
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
@@ -185,6 +188,8 @@ def main() -> int:
         "frames_per_step": args.frames,
         # per-iteration device all-reduce: RCCL, or the one-shot P2P kernel when it beat RCCL at start-up
         "allreduce": (solver.native_comm.describe if n > 1 else "none (1 rank)"),
+        # rank 0's GPU time inside the all-reduces per SART iteration (includes waiting for slower ranks)
+        "allreduce_us_per_iter": (round(1e3 * comm_ms / max(iters, 1), 2) if n > 1 and not multi else None),
         "effective_hbm_TBps_per_gpu": round(bytes_per_iter * iters_per_s / 1e12, 3),
         "config": {
             "model": f"SART-{args.variant} dense RTM" + (" + Laplacian" if lap is not None else "")

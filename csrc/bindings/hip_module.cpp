@@ -41,6 +41,8 @@ static py::dict solve_info(const sart::SolveInfo& i) {
     d["fallbacks"] = i.fallbacks;
     d["nonfinite"] = i.nonfinite;
     d["ms"] = i.ms;
+    d["sweeps"] = i.sweeps;
+    d["comm_ms"] = i.comm_ms;
     return d;
 }
 
@@ -148,6 +150,7 @@ static void bind_engine(py::module_& m) {
         .def_readwrite("rows_per_tile", &sart::EngineConfig::rows_per_tile)
         .def_readwrite("fused_schedule", &sart::EngineConfig::fused_schedule)
         .def_readwrite("use_graph", &sart::EngineConfig::use_graph)
+        .def_readwrite("time_collectives", &sart::EngineConfig::time_collectives)
         .def_readwrite("fault_inject", &sart::EngineConfig::fault_inject);
     m.def("validate_config", [](const sart::EngineConfig& c) {
         try {

@@ -5,15 +5,17 @@
 //     MASTER_PORT (torchrun --no-python, mpirun via OMPI_COMM_WORLD_*, or bin/sartsolver); one process
 //     runs without any launcher. Rank -> GPU = LOCAL_RANK % device count (reference: rank % count,
 //     sartsolver_cuda.cpp:96-98).
-//   * per-iteration reductions with RCCL over xGMI on device buffers (csrc/engine/comm.cpp), host
-//     scalars over the TCP bootstrap; the --use_cpu path uses the TCP host communicator.
+//   * per-iteration reductions on device buffers (csrc/engine/comm.cpp): the one-shot P2P all-reduce over
+//     xGMI or RCCL; host scalars over the TCP or MPI bootstrap (mpiexec launches use MPI_COMM_WORLD); the
+//     --use_cpu path uses the host communicator alone.
 //   * every rank streams only its pixel rows from HDF5 straight into HBM through two pinned staging
 //     buffers (the reference keeps the whole shard in host RAM, raytransfer.hpp:20); with
 //     --parallel_read all ranks read at once, otherwise in turn (reference main.cpp:78-86).
 //   * the next composite frame is read on a helper thread while the current one is solved.
 //   * a fatal error on any rank aborts the communicators instead of leaving peers blocked in a
 //     collective (the reference calls std::exit on one rank).
-// Extensions: --resume, --two_pass, --profile FILE (JSON lines per frame), --batch_frames N (N independent
+// Extensions: --resume, --two_pass, --profile FILE (JSON lines per frame: iterations, convergence, it/s,
+// GFLOPS, RTM GB/s, GPU time in the all-reduces, communicators), --batch_frames N (N independent
 // frames solved together by the multi-frame MFMA engine, cold-started like --no_guess).
 #include <hip/hip_runtime.h>
 
@@ -241,6 +243,7 @@ int main(int argc, char** argv) {
             ec.use_fused = !cfg.two_pass;
             ec.fused_min_bytes = fused_min_bytes_from_env();
             if (const char* v = std::getenv("SART_FUSED_VARIANT"); v && *v) ec.fused_variant = std::atoi(v);
+            ec.time_collectives = !cfg.profile_file.empty();  // --profile: GPU time in the all-reduces per frame
             if (cols) {
                 ec.column_shard = true;
                 ec.col_offset = (int64_t)vblk.offset;
@@ -356,12 +359,24 @@ int main(int argc, char** argv) {
                 const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 std::cout << "Processed in: " << ms << " ms" << std::endl;  // reference main.cpp:132-137
                 if (profile.is_open())
+                {
+                    // throughput of the solve (4 P V flop and one or two reads of every rank's shard per sweep)
+                    const double sweeps = gpu ? (double)info.sweeps : (double)info.iterations;
+                    const double secs = info.ms > 0 ? 1e-3 * info.ms : 1e-3 * ms;
+                    const double pv = (double)in.npixel * (double)in.nvoxel;
+                    const double reads = gpu && info.used_fused ? 1.0 : 2.0;
                     profile << "{\"frame\": " << cur << ", \"time\": " << image.frame_time(cur)
                             << ", \"status\": " << info.status << ", \"iterations\": " << info.iterations
+                            << ", \"convergence\": " << info.convergence << ", \"sweeps\": " << sweeps
+                            << ", \"iters_per_s\": " << sweeps / secs << ", \"gflops\": " << 4.0 * pv * sweeps / secs / 1e9
+                            << ", \"rtm_GBps\": " << reads * 4.0 * pv * sweeps / secs / 1e9
+                            << ", \"comm_ms\": " << info.comm_ms
                             << ", \"ms\": " << ms << ", \"solve_ms\": " << info.ms
                             << ", \"fused\": " << (info.used_fused ? "true" : "false")
                             << ", \"ranks\": " << size << ", \"comm\": \"" << json_escape(host->backend())
+                            << "\", \"device_comm\": \"" << json_escape(dcomm ? dcomm->describe() : "none")
                             << "\", \"driver\": \"" << json_escape("native") << "\"}\n";
+                }
             }
             if (cfg.no_guess) solution.clear();
         }

@@ -111,6 +111,8 @@ Engine::~Engine() {
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
+    for (auto& pool : cev_)
+        for (auto& e : pool) (void)hipEventDestroy(e);
     if (hstate_) (void)hipHostFree(hstate_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
@@ -284,7 +286,11 @@ void Engine::sweep() {
                        x_.get(), pen_.get(), st, stream_);
         pen = pen_.get();
     }
-    if (comm_->size() > 1) comm_->all_reduce(comm_buf_.get(), (size_t)ld_ + 1, ReduceOp::kSum, stream_);
+    if (comm_->size() > 1) {
+        comm_begin();
+        comm_->all_reduce(comm_buf_.get(), (size_t)ld_ + 1, ReduceOp::kSum, stream_);
+        comm_end();
+    }
     launch_decide(st, Fslot, stream_);
     if (cfg_.logarithmic)
         launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_);
@@ -300,7 +306,11 @@ void Engine::sweep_columns() {
     float* Fslot = comm_buf_.get() + ld_;
     launch_forward(kEpiPlain, A_, ld_, P_, Pp_, x_.get(), nullptr, nullptr, fitted_.get(), nullptr, nullptr, st,
                    stream_);
-    if (comm_->size() > 1) comm_->all_reduce(fitted_.get(), (size_t)P_, ReduceOp::kSum, stream_);
+    if (comm_->size() > 1) {
+        comm_begin();
+        comm_->all_reduce(fitted_.get(), (size_t)P_, ReduceOp::kSum, stream_);
+        comm_end();
+    }
     launch_weights(cfg_.logarithmic, fitted_.get(), ghat_.get(), arow_.get(), P_, Pp_, w_.get(), Fpart_.get(), st,
                    stream_);
     launch_backproject(A_, ld_, P_, w_.get(), nsplit_, partial_.get(), st, stream_);
@@ -312,7 +322,9 @@ void Engine::sweep_columns() {
         if (comm_->size() > 1) {
             hip_ok(hipMemsetAsync(xg_.get(), 0, xg_.size() * sizeof(float), stream_), "memset");
             launch_copy_slice(x_.get(), V_, xg_.get(), cfg_.col_offset, stream_);
+            comm_begin();
             comm_->all_reduce(xg_.get(), (size_t)cfg_.nvoxel_total, ReduceOp::kSum, stream_);
+            comm_end();
             xfull = xg_.get();
         }
         launch_penalty(cfg_.logarithmic, lap_rp_.get(), lap_col_.get(), lap_val_.get(), V_, (float)cfg_.beta_laplace,
@@ -324,6 +336,35 @@ void Engine::sweep_columns() {
         launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_);
     else
         launch_update_linear(x_.get(), comm_buf_.get(), pen, V_, st, stream_);
+}
+
+bool Engine::timing_collectives() const { return cfg_.time_collectives && !cfg_.use_graph && comm_->size() > 1; }
+
+void Engine::comm_begin() {
+    if (!timing_collectives()) return;
+    auto& pool = cev_[cur_slot_];
+    const size_t k = (size_t)cev_used_[cur_slot_] * 2;
+    while (pool.size() < k + 2) {
+        hipEvent_t e;
+        hip_ok(hipEventCreate(&e), "hipEventCreate");
+        pool.push_back(e);
+    }
+    hip_ok(hipEventRecord(pool[k], stream_), "hipEventRecord");
+}
+
+void Engine::comm_end() {
+    if (!timing_collectives()) return;
+    const size_t k = (size_t)cev_used_[cur_slot_] * 2;
+    hip_ok(hipEventRecord(cev_[cur_slot_][k + 1], stream_), "hipEventRecord");
+    ++cev_used_[cur_slot_];
+}
+
+void Engine::collect_comm(int slot) {  // the chunk of `slot` has completed
+    for (int i = 0; i < cev_used_[slot]; ++i) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, cev_[slot][2 * i], cev_[slot][2 * i + 1]) == hipSuccess) comm_ms_ += ms;
+    }
+    cev_used_[slot] = 0;
 }
 
 void Engine::run_chunk(int n) {
@@ -391,8 +432,11 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
         norm_ = setup_frame(g, x0);
         int enqueued = 0, issued = 0, checked = 0;
         bool error = false;
+        comm_ms_ = 0.0;
+        cev_used_[0] = cev_used_[1] = 0;
         auto issue = [&]() {
             const int n = std::min(cfg_.check_interval, max_sweeps - enqueued);
+            cur_slot_ = issued & 1;
             run_chunk(n);
             enqueued += n;
             const int slot = issued & 1;
@@ -406,6 +450,7 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
             if (enqueued < max_sweeps) issue();  // keep the GPU busy while the previous chunk is checked
             const int slot = checked & 1;
             hip_ok(hipEventSynchronize(ev_[slot]), "event sync");
+            collect_comm(slot);
             SartState s = hstate_[slot];
             ++checked;
             if (use_fused_ && injected_ < cfg_.fault_inject && checked == 1) {  // fault injection (tests)
@@ -419,6 +464,8 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
             if (s.done || (checked == issued && enqueued >= max_sweeps)) break;
         }
         hip_ok(hipStreamSynchronize(stream_), "solve");
+        collect_comm(0);  // chunks issued after the last check
+        collect_comm(1);
         comm_->check();
         if (error) {
             ++info.fallbacks;
@@ -438,6 +485,8 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
     info.nonfinite = (s.flags & 1) != 0;
     info.used_fused = use_fused_;
     info.fused_variant = use_fused_ ? geom_.variant : -1;
+    info.sweeps = s.sweep;
+    info.comm_ms = timing_collectives() ? comm_ms_ : -1.0;
     info.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return info;
 }

@@ -53,6 +53,9 @@ struct EngineConfig : SolverParams {
     bool column_shard = false;
     int64_t col_offset = 0;
     int64_t nvoxel_total = 0;  // 0: nvoxel
+    // Observability: bracket every per-sweep all-reduce with timing events and report the GPU
+    // time spent in collectives (SolveInfo::comm_ms). Eager chunks only (ignored with use_graph).
+    bool time_collectives = false;
 };
 
 // roctx range (rocprofv3 --marker-trace) for the lifetime of the object.
@@ -158,6 +161,16 @@ class Engine {
     DeviceArray<int32_t> lap_col_;
     DeviceArray<float> lap_val_;
     bool has_lap_ = false;
+
+    // time_collectives: event pairs around the all-reduces of the chunk in each pipeline slot
+    std::vector<hipEvent_t> cev_[2];
+    int cev_used_[2] = {0, 0};
+    int cur_slot_ = 0;
+    double comm_ms_ = 0.0;
+    bool timing_collectives() const;
+    void comm_begin();
+    void comm_end();
+    void collect_comm(int slot);
 
     SartState* hstate_ = nullptr;  // pinned [2]
     hipEvent_t ev_[2] = {nullptr, nullptr};

@@ -63,7 +63,7 @@ __device__ __forceinline__ void load_groups(float (&dst)[NG], const float* __res
 // resident, but at nf = 64 it is twice the A stream with RT = 2).
 // Split-K: blockIdx.y selects the column range [k0, k1) (multiples of 16 columns) and the kernel
 // writes Fout + blockIdx.y * nrows_pad * nf; the caller sums the splits.
-template <int NG, int DEPTH, int RT>
+template <int NG, int DEPTH, int RT, bool NT>
 __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A, int64_t ld, int64_t nrows,
                                                     int64_t nrows_pad, const float* __restrict__ X,
                                                     int64_t ldx, float* __restrict__ Fout, int64_t cols_per_split) {
@@ -99,7 +99,8 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
             for (int h = 0; h < 2; ++h) {
 #pragma unroll
                 for (int rt = 0; rt < RT; ++rt)  // plain loads: a row's two 64-B halves come from two
-                    a[sl][rt][h] = a0p[rt * 16 * ld4 + qq + 4 * h];  // instructions; nt loads measured slower
+                    a[sl][rt][h] = NT ? load_stream(a0p + rt * 16 * ld4 + qq + 4 * h)  // SART_MF_NT=1
+                                      : a0p[rt * 16 * ld4 + qq + 4 * h];  // instructions; nt measured slower
 #pragma unroll
                 for (int j = 0; j < NG; ++j) x[sl][h][j] = xp[j * xg + qq + 4 * h];
             }
@@ -327,15 +328,34 @@ static int mf_rows(int nf) {
     return 4;
 }
 
+template <int NG, int RT, bool NT>
+static void fwd_rt_nt(dim3 grid, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
+                      int64_t nrows_pad, const float* X, int64_t ldx, float* Fout, int64_t cps) {
+    if (depth == 1)
+        hipLaunchKernelGGL((k_mf_forward<NG, 1, RT, NT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+    else if (depth == 3)
+        hipLaunchKernelGGL((k_mf_forward<NG, 3, RT, NT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+    else
+        hipLaunchKernelGGL((k_mf_forward<NG, 2, RT, NT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+}
+
+// Non-temporal A loads in the MFMA forward (experiment knob, SART_MF_NT=1; default plain loads).
+static int mf_nt() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = std::getenv("SART_MF_NT");
+        v = (e && *e) ? std::atoi(e) : 0;
+    }
+    return v;
+}
+
 template <int NG, int RT>
 static void fwd_rt(dim3 grid, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
                    int64_t nrows_pad, const float* X, int64_t ldx, float* Fout, int64_t cps) {
-    if (depth == 1)
-        hipLaunchKernelGGL((k_mf_forward<NG, 1, RT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
-    else if (depth == 3)
-        hipLaunchKernelGGL((k_mf_forward<NG, 3, RT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+    if (mf_nt() == 1)
+        fwd_rt_nt<NG, RT, true>(grid, depth, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
     else
-        hipLaunchKernelGGL((k_mf_forward<NG, 2, RT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+        fwd_rt_nt<NG, RT, false>(grid, depth, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
 }
 
 template <int NG>

@@ -30,6 +30,8 @@ struct SolveInfo {
     int fallbacks = 0;        // persistent-kernel protocol timeouts survived during this solve
     bool nonfinite = false;   // the iteration produced NaN/Inf and was stopped
     double ms = 0.0;
+    int sweeps = 0;           // sweeps executed on the device (iterations + the final decision sweep)
+    double comm_ms = -1.0;    // GPU time inside the per-sweep all-reduces (EngineConfig::time_collectives; else -1)
 };
 
 // CSR over n rows (row_ptr int64, col int32, val fp32), from the reference's sorted-flat-index COO

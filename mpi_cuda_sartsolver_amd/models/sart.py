@@ -81,6 +81,7 @@ class SolveResult:
     convergence: float
     used_fused: bool
     elapsed_ms: float = 0.0
+    comm_ms: float = -1.0  # GPU time in the per-sweep all-reduces (time_collectives=True), else -1
 
 
 def _host_f64(v) -> np.ndarray:
@@ -101,7 +102,7 @@ class SARTSolver:
                  logarithmic: bool = False, use_fused: bool = True, check_interval: int = 16,
                  allow_zero_tolerance: bool = False, fused_variant: Optional[int] = None,
                  fused_rows_per_tile: Optional[int] = None, use_graph: Optional[bool] = None,
-                 fused_min_bytes: float = 0.0, partition: Optional[str] = None):
+                 fused_min_bytes: float = 0.0, partition: Optional[str] = None, time_collectives: bool = False):
         self.k = hip()
         self.rtm = rtm
         self.dev = rtm.device
@@ -137,6 +138,7 @@ class SARTSolver:
             use_graph = os.environ.get("SART_GRAPH", "0") == "1"
         cfg.use_graph = bool(use_graph)
         cfg.fused_min_bytes = float(fused_min_bytes)  # smaller shards use the two-pass kernels
+        cfg.time_collectives = bool(time_collectives)  # SolveResult.comm_ms (events around each all-reduce)
         if self.column_shard:  # all pixel rows of voxels [col_offset, +nvoxel): two-pass, pixel all-reduce
             cfg.column_shard = True
             cfg.col_offset = int(getattr(rtm, "col_offset", 0))
@@ -179,7 +181,7 @@ class SARTSolver:
         status = SUCCESS if info["status"] == SUCCESS else MAX_ITERATIONS_EXCEEDED
         return SolveResult(solution=x, status=status, iterations=int(info["iterations"]),
                            convergence=float(info["convergence"]), used_fused=bool(info["used_fused"]),
-                           elapsed_ms=float(info["ms"]))
+                           elapsed_ms=float(info["ms"]), comm_ms=float(info["comm_ms"]))
 
     def gather_solution(self, x_local: np.ndarray) -> np.ndarray:
         """Full solution vector from the column shards of every rank (identity for a row shard)."""

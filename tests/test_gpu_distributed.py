@@ -78,6 +78,8 @@ def test_gpu_solver_rank_invariance_p2p(tmp_path, extra):
     for n in (2, 3):
         x, m = _run(n, str(tmp_path / f"p{n}"), extra, SART_P2P="1")
         assert m[0]["comm"] == "p2p"
+        if "--multiframe" not in extra:
+            assert m[0]["comm_ms"] > 0  # time_collectives: events around every per-sweep all-reduce
         assert np.linalg.norm(x - x1) / np.linalg.norm(x1) < 2e-3
         for a, b in zip(m, m1):
             assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3

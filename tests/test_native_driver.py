@@ -162,23 +162,33 @@ def test_native_gpu_matches_python_driver(tmp_path, binary, log, extra):
 
 
 @pytest.mark.gpu
-def test_native_gpu_two_ranks_one_device(tmp_path, binary):
-    """Two ranks on the box's single GPU, staged (TCP) reductions: equals the one-rank run."""
+@pytest.mark.parametrize("p2p", ["0", "1"])
+def test_native_gpu_two_ranks_one_device(tmp_path, binary, p2p):
+    """Two ranks on the box's single GPU, staged (TCP) reductions or the one-shot P2P all-reduce through
+    IPC-mapped buffers: equals the one-rank run; --profile reports the GPU time in the all-reduces."""
     case = make_case(str(tmp_path / "c"), laplacian=True, nframes=2, nvoxel=2048, grid=(16, 16, 16),
                      shapes=((24, 32), (20, 30)))
     base = ["-m", "40", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3", "--two_pass"]
     r = _run_native(binary, base + ["-o", str(tmp_path / "one.h5"), *case.files])
     assert r.returncode == 0, r.stderr
-    env_backend = os.environ.get("SART_DIST_BACKEND")
+    saved = {k: os.environ.get(k) for k in ("SART_DIST_BACKEND", "SART_P2P")}
     os.environ["SART_DIST_BACKEND"] = "tcp"
+    os.environ["SART_P2P"] = p2p
+    prof = str(tmp_path / "prof.jsonl")
     try:
-        r = _run_native(binary, base + ["-o", str(tmp_path / "two.h5"), *case.files], nproc=2)
+        r = _run_native(binary, base + ["--profile", prof, "-o", str(tmp_path / "two.h5"), *case.files], nproc=2)
     finally:
-        if env_backend is None:
-            os.environ.pop("SART_DIST_BACKEND")
-        else:
-            os.environ["SART_DIST_BACKEND"] = env_backend
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    import json
+
+    lines = [json.loads(x) for x in open(prof)]
+    assert len(lines) == 2 and all(d["ranks"] == 2 and d["comm_ms"] >= 0 and d["sweeps"] >= 1 for d in lines)
+    assert lines[0]["device_comm"].startswith("p2p" if p2p == "1" else "staged"), lines[0]["device_comm"]
     n = native()
     _, x1, s1 = n.read_solution_file(str(tmp_path / "one.h5"))
     _, x2, s2 = n.read_solution_file(str(tmp_path / "two.h5"))

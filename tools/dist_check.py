@@ -52,11 +52,12 @@ def main():
         meta = [dict(status=r.status, iterations=r.iterations, comm=s.native_comm.backend) for r in res]
     else:
         s = SARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic, use_fused=a.fused,
-                       partition="cols" if a.columns else None)
+                       partition="cols" if a.columns else None, time_collectives=True)
         r = s.solve(prob.measurement)
         r2 = s.solve(prob.measurement, solution=r.solution)  # warm start path
         x = np.stack([s.gather_solution(r.solution), s.gather_solution(r2.solution)])
-        meta = [dict(status=r.status, iterations=r.iterations, fused=r.used_fused, comm=s.native_comm.backend),
+        meta = [dict(status=r.status, iterations=r.iterations, fused=r.used_fused, comm=s.native_comm.backend,
+                     comm_ms=r.comm_ms),
                 dict(status=r2.status, iterations=r2.iterations)]
     if comm.rank == 0:
         np.save(a.out + ".npy", x)
