@@ -141,17 +141,32 @@ class P2pComm final : public Communicator {
             finish(true, "p2p (forced, self-test ok)");
             return;
         }
-        // auto: rank 0 times both at the engine's typical message (64k voxels + the piggy-backed scalar)
-        const int64_t nprobe = std::min<int64_t>(cap_, 65537);
-        const double tp = time_us([&](float* b) { p2p(b, nprobe, 0, stream_); }, nprobe);
-        const double tb = time_us([&](float* b) { base_->all_reduce(b, (size_t)nprobe, ReduceOp::kSum, stream_); },
-                                  nprobe);
-        double pick[3] = {tp < tb ? 1.0 : 0.0, tp, tb};
+        // auto: rank 0 times both at message sizes around the engine's (V + 1 floats: 64k .. 256k voxels);
+        // the P2P path serves vectors up to the largest probed size at which it won (rank 0 decides)
+        const int64_t probes[] = {4097, 65537, 262145, 524288};
+        double pick[1 + 2 * 4] = {0.0};
+        std::string table;
+        for (int i = 0; i < 4; ++i) {
+            const int64_t n = probes[i];
+            if (n > cap_) break;
+            const double tp = time_us([&](float* b) { p2p(b, n, 0, stream_); }, n);
+            const double tb = time_us([&](float* b) { base_->all_reduce(b, (size_t)n, ReduceOp::kSum, stream_); }, n);
+            pick[1 + 2 * i] = tp;
+            pick[2 + 2 * i] = tb;
+            if (tp < tb) pick[0] = (double)n;
+        }
         h.broadcast_host(pick, sizeof(pick), 0);
-        char buf[160];
-        std::snprintf(buf, sizeof(buf), "%s (auto: p2p %.1f us vs %s %.1f us at %lld floats, rank 0)",
-                      pick[0] > 0 ? "p2p" : base_->backend(), pick[1], base_->backend(), pick[2], (long long)nprobe);
-        finish(pick[0] > 0, buf);
+        for (int i = 0; i < 4 && probes[i] <= cap_; ++i) {
+            char cell[96];
+            std::snprintf(cell, sizeof(cell), "%s%lld: %.1f/%.1f", i ? ", " : "", (long long)probes[i], pick[1 + 2 * i],
+                          pick[2 + 2 * i]);
+            table += cell;
+        }
+        max_n_ = (int64_t)pick[0];
+        char buf[96];
+        std::snprintf(buf, sizeof(buf), "p2p up to %lld floats, %s above", (long long)max_n_, base_->backend());
+        finish(max_n_ > 0, (max_n_ > 0 ? std::string(buf) : std::string(base_->backend())) +
+                               " (auto, rank 0, us p2p/" + base_->backend() + " at floats " + table + ")");
     }
     ~P2pComm() override {
         (void)hipSetDevice(device_);
@@ -164,7 +179,7 @@ class P2pComm final : public Communicator {
     const char* backend() const override { return active_ ? "p2p" : base_->backend(); }
     std::string describe() const override { return why_; }
     void all_reduce(float* dev, size_t n, ReduceOp op, hipStream_t stream) override {
-        if (active_ && n > 0 && (int64_t)n <= cap_ && reinterpret_cast<uintptr_t>(dev) % 16 == 0)
+        if (active_ && n > 0 && (int64_t)n <= max_n_ && reinterpret_cast<uintptr_t>(dev) % 16 == 0)
             p2p(dev, (int64_t)n, op == ReduceOp::kSum ? 0 : 1, stream);
         else
             base_->all_reduce(dev, n, op, stream);
@@ -186,6 +201,7 @@ class P2pComm final : public Communicator {
     void finish(bool active, const std::string& why) {
         active_ = active;
         why_ = why;
+        if (active && max_n_ == 0) max_n_ = cap_;  // forced on: every vector that fits the slots
     }
     bool agree(bool ok) {  // every rank learns whether all succeeded
         double bad = ok ? 0.0 : 1.0;
@@ -325,6 +341,7 @@ class P2pComm final : public Communicator {
     std::shared_ptr<Communicator> base_;
     int device_ = 0, rank_ = 0, n_ = 1;
     int64_t cap_ = 0;
+    int64_t max_n_ = 0;  // P2P for n <= max_n_ (auto: largest probed size at which it beat the base)
     double timeout_s_ = 600.0;
     bool active_ = false;
     std::string why_, err_msg_;
@@ -361,7 +378,9 @@ std::unique_ptr<Communicator> comm_from_env(int device) {
     const char* p2p = std::getenv("SART_P2P");
     if (be && (std::string(be) == "tcp" || std::string(be) == "gloo")) {
         auto staged = make_staged_comm(std::move(host));
-        if (p2p && std::string(p2p) == "1") return make_p2p_comm(device, std::move(staged));  // tests on one GPU
+        const char* wrap = std::getenv("SART_P2P_WRAP_STAGED");  // tests on one GPU
+        if ((p2p && std::string(p2p) == "1") || (wrap && std::string(wrap) == "1"))
+            return make_p2p_comm(device, std::move(staged));
         return staged;
     }
     std::string uid(128, '\0');

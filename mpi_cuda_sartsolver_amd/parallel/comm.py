@@ -176,7 +176,9 @@ def native_communicator(comm: Optional[Communicator], device: int = 0):
             native = k.p2p_comm(device, native)
     else:
         native = k.staged_comm(comm.rank, comm.world_size, host, int(port))
-        if p2p in ("1", "on"):  # several ranks sharing one GPU (tests): exercise the P2P kernel path
+        # several ranks sharing one GPU (tests): exercise the P2P kernel path (SART_P2P_WRAP_STAGED=1 also
+        # runs the auto selection against the staged base)
+        if p2p in ("1", "on") or os.environ.get("SART_P2P_WRAP_STAGED") == "1":
             native = k.p2p_comm(device, native)
     comm._native_comm = native
     return native

@@ -72,6 +72,15 @@ def test_p2p_allreduce_bitwise(tmp_path, nproc):
             assert r["close"], r
 
 
+def test_p2p_auto_selection(tmp_path):
+    """SART_P2P=auto times the P2P kernel against the base communicator at 4k .. 512k floats on rank 0 and
+    serves vectors up to the largest size at which P2P won (here against the host-staged base)."""
+    res = _run(2, str(tmp_path / "comm.json"), ["--sizes", "1,4097,65537,524288"], script="comm_check.py",
+               SART_P2P="auto", SART_P2P_WRAP_STAGED="1")
+    assert res["backend"] == "p2p" and res["describe"].startswith("p2p up to"), res["describe"]
+    assert all(r["exact"] for r in res["results"] if r["n"] <= 4097)
+
+
 @pytest.mark.parametrize("extra", [[], ["--logarithmic"], ["--multiframe"]])
 def test_gpu_solver_rank_invariance_p2p(tmp_path, extra):
     x1, m1 = _run(1, str(tmp_path / "r1"), extra)
