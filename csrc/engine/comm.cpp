@@ -188,12 +188,19 @@ class P2pComm final : public Communicator {
         base_->all_reduce(dev, n, op, stream);
     }
     bool graph_capturable() const override { return !active_ && base_->graph_capturable(); }  // epoch is an argument
-    void abort() override { base_->abort(); }
+    void abort() override {
+        // tell every peer: their P2P kernels stop polling for this rank at once instead of at the timeout
+        const unsigned one = 1;
+        for (int r = 0; r < n_; ++r)
+            if (r != rank_ && tail_[r]) (void)hipMemcpy(tail_[r] + 1, &one, sizeof(one), hipMemcpyHostToDevice);
+        base_->abort();
+    }
     void check() override {
         if (!err_) return;
-        unsigned e = 0;
-        hip_ok(hipMemcpy(&e, err_, sizeof(e), hipMemcpyDeviceToHost), "p2p error word");
-        if (e) throw std::runtime_error("p2p all-reduce: a peer did not arrive within SART_P2P_TIMEOUT_S");
+        unsigned e[2] = {0, 0};
+        hip_ok(hipMemcpy(e, err_, sizeof(e), hipMemcpyDeviceToHost), "p2p error word");
+        if (e[1]) throw std::runtime_error("p2p all-reduce: a peer aborted");
+        if (e[0]) throw std::runtime_error("p2p all-reduce: a peer did not arrive within SART_P2P_TIMEOUT_S");
         base_->check();
     }
 
@@ -232,6 +239,7 @@ class P2pComm final : public Communicator {
             hip_ok(hipMemset(mem_, 0, recv_bytes + flag_bytes + 256), "hipMemset");
             hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
             err_ = reinterpret_cast<unsigned*>(static_cast<char*>(mem_) + recv_bytes + flag_bytes);
+            args_.abort_word = err_ + 1;
             hip_ok(hipIpcGetMemHandle(&hdl, mem_), "hipIpcGetMemHandle");
         } catch (const std::exception& e) {
             ok = false;
@@ -253,6 +261,7 @@ class P2pComm final : public Communicator {
             }
             args_.recv[r] = static_cast<float*>(p);
             args_.flags[r] = reinterpret_cast<unsigned*>(static_cast<char*>(p) + recv_bytes);
+            tail_[r] = reinterpret_cast<unsigned*>(static_cast<char*>(p) + recv_bytes + flag_bytes);  // {err, abort}
         }
         return ok;  // the caller's agree() is also the barrier: every flag array is zeroed before any push
     }
@@ -350,6 +359,7 @@ class P2pComm final : public Communicator {
     unsigned* err_ = nullptr;
     std::vector<void*> opened_;
     P2pArgs args_{};
+    unsigned* tail_[kP2pMaxRanks] = {};  // {err, abort} words of every rank as mapped here
     unsigned epoch_ = 0;
 };
 

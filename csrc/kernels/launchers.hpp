@@ -74,6 +74,7 @@ constexpr int kP2pMaxBlocks = 1024;
 struct P2pArgs {
     float* recv[kP2pMaxRanks];      // rank j's receive buffer as mapped in this process
     unsigned* flags[kP2pMaxRanks];  // rank j's flag array as mapped in this process
+    const unsigned* abort_word;     // this rank's abort word: set remotely by a peer that aborts
 };
 int64_t p2p_chunk(int64_t n);  // elements per workgroup
 // op: 0 sum, 1 max. `epoch` strictly increases by one per call on every rank (starts at 1).

@@ -14,8 +14,9 @@
 // every pushing wave waits for its stores, then (behind a barrier) each flag lane issues a system-scope
 // release, waits again (cdna_hip_programming.md Guideline 16 Pitfall 12) and stores the flag. Consumer:
 // relaxed system-scope polls, one acquire + wait per polling lane, a barrier, then plain loads. Polls
-// are bounded (s_memrealtime, 100 MHz): on timeout the chunk is filled with NaN (the engine's
-// non-finite guard stops the frame) and *err is raised for the host.
+// are bounded (s_memrealtime, 100 MHz) and also end when a peer that aborts sets this rank's abort
+// word: the chunk is then filled with NaN (the engine's non-finite guard stops the frame) and *err is
+// raised for the host.
 #include "launchers.hpp"
 
 #include <stdexcept>
@@ -63,8 +64,9 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
         const unsigned* f = a.flags[rank] + threadIdx.x * kP2pMaxBlocks + blockIdx.x;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
-                timed_out = 1;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks ||
+                __hip_atomic_load(a.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+                timed_out = 1;  // a peer is gone (timeout) or told us it aborted
                 break;
             }
             __builtin_amdgcn_s_sleep(1);

@@ -92,3 +92,15 @@ def test_gpu_solver_rank_invariance_p2p(tmp_path, extra):
         assert np.linalg.norm(x - x1) / np.linalg.norm(x1) < 2e-3
         for a, b in zip(m, m1):
             assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3
+
+
+def test_p2p_peer_abort_fails_fast(tmp_path):
+    """A rank that aborts writes the abort word of every peer: a peer waiting in the P2P all-reduce stops
+    within seconds (NaN output, check() raises) instead of polling until SART_P2P_TIMEOUT_S (120 s here)."""
+    out = str(tmp_path / "abort.json")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "p2p_abort_check.py"), "--out", out],
+                       capture_output=True, text=True, timeout=400, env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.load(open(out))
+    assert res["backend"] == "p2p" and res["first_ok"]
+    assert "aborted" in res["error"] and res["nan"] and res["seconds"] < 30, res
