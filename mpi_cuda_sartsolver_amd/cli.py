@@ -121,7 +121,7 @@ def run(cfg, intervals) -> int:
 
                 solver = SARTSolver(shard, laplacian, comm, params, logarithmic=cfg.logarithmic,
                                     use_fused=not cfg.two_pass, fused_min_bytes=hip().fused_min_bytes_from_env(),
-                                    partition="cols" if cols else None)
+                                    partition="cols" if cols else None, time_collectives=bool(cfg.profile_file))
         else:
             from .models.cpu import CPUSARTSolver
 
@@ -174,8 +174,14 @@ def run(cfg, intervals) -> int:
                     print(f"Processed in: {ms} ms", flush=True)
                     if profile:
                         profile.write(json.dumps({"frame": cur, "time": image.frame_time(cur), "status": res.status,
-                                                  "iterations": res.iterations, "ms": ms,
-                                                  "fused": bool(getattr(res, "used_fused", False))}) + "\n")
+                                                  "iterations": res.iterations, "convergence": res.convergence,
+                                                  "ms": ms, "solve_ms": getattr(res, "elapsed_ms", ms),
+                                                  "comm_ms": getattr(res, "comm_ms", -1.0),
+                                                  "fused": bool(getattr(res, "used_fused", False)),
+                                                  "ranks": comm.world_size,
+                                                  "device_comm": getattr(getattr(solver, "native_comm", None),
+                                                                         "describe", "none"),
+                                                  "driver": "python"}) + "\n")
                 if cfg.no_guess:
                     solution = None
         pool.shutdown()
