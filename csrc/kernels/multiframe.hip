@@ -274,9 +274,13 @@ int mf_forward_num_splits(int64_t ld, int64_t nrows_pad) {
 }
 
 static int mf_vox(int64_t ld, int nf);
+// Split-K of the back-projection: ~512 workgroups. The kernel time is flat from 4 to 32 splits at
+// 64k x 64k (profiles/probe_r1_mf_splits.jsonl) while k_mf_collect reads nsplit partial slices.
 int mf_backproject_num_splits(int64_t ld, int64_t nrows) {
     const int64_t nblk = (ld / (64 * mf_vox(ld, kMfMaxFrames)) + 3) / 4;
-    int64_t s = (2048 + nblk - 1) / nblk;
+    const char* e = std::getenv("SART_MF_BP_BLOCKS");  // target workgroups (tuning knob)
+    const int64_t target = (e && *e) ? std::atoll(e) : 512;
+    int64_t s = (target + nblk - 1) / nblk;
     const int64_t smax = (nrows + 63) / 64;
     if (s > smax) s = smax;
     if (s < 1) s = 1;

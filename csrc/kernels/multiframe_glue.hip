@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void k_mf_prep(const double* __restrict__ g, i
 // F = sum_s Fsplit[s] (fixed order); W = a F (log) or a (ghat - F) (linear), written in the
 // back-projection layout (mf_bp_slot); per-block, per-frame partial sums of F^2 in fp64 (deterministic:
 // fixed thread-to-row assignment, fixed tree).
-constexpr int kWRows = 256;  // rows per block
+constexpr int kWRows = 64;  // rows per block (>= 1024 blocks at 64k rows: the kernel is latency-bound)
 __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs, int nsplit, int64_t nrows_pad,
                                                     const float* __restrict__ ghat, const float* __restrict__ arow,
                                                     int logmode, float* __restrict__ W, double* __restrict__ F2part,
@@ -97,10 +97,18 @@ __global__ __launch_bounds__(256) void k_mf_collect(const float* __restrict__ pa
         const int64_t v = v0 + vv;
         if (v < ld) D[(int64_t)f * ld + v] = tile[f][vv];
     }
-    if (F2part && blockIdx.x == 0 && threadIdx.x < nf) {
+    if (F2part && blockIdx.x == 0) {  // block-uniform branch: all 256 threads, 256 / nf per frame
+        __shared__ double f2[256];
+        const int f = threadIdx.x % nf, q = threadIdx.x / nf, nq = 256 / nf;
         double s = 0.0;
-        for (int b = 0; b < nF2; ++b) s += F2part[(int64_t)b * nf + threadIdx.x];
-        F2out[threadIdx.x] = (float)s;
+        for (int b = q; b < nF2; b += nq) s += F2part[(int64_t)b * nf + f];
+        f2[threadIdx.x] = s;
+        __syncthreads();
+        if (threadIdx.x < nf) {  // fixed order over the 256 / nf partial sums: deterministic
+            double t = 0.0;
+            for (int k = 0; k < nq; ++k) t += f2[k * nf + threadIdx.x];
+            F2out[threadIdx.x] = (float)t;
+        }
     }
 }
 
