@@ -179,7 +179,8 @@ class P2pComm final : public Communicator {
     const char* backend() const override { return active_ ? "p2p" : base_->backend(); }
     std::string describe() const override { return why_; }
     void all_reduce(float* dev, size_t n, ReduceOp op, hipStream_t stream) override {
-        if (active_ && n > 0 && (int64_t)n <= max_n_ && reinterpret_cast<uintptr_t>(dev) % 16 == 0)
+        // the choice depends only on n (identical on every rank), never on this rank's pointer alignment
+        if (active_ && n > 0 && (int64_t)n <= max_n_)
             p2p(dev, (int64_t)n, op == ReduceOp::kSum ? 0 : 1, stream);
         else
             base_->all_reduce(dev, n, op, stream);

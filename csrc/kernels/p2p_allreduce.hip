@@ -31,7 +31,8 @@ __device__ inline float red(float a, float b, int op) { return op == 0 ? a + b :
 // `in` may alias `out` (in place): each element is read in phase 1 and written in phase 2 by one thread.
 __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* out, int64_t n, int64_t chunk,
                                                        P2pArgs a, int rank, int nranks, unsigned epoch, int parity,
-                                                       int64_t cap, int op, unsigned* err, uint64_t timeout_ticks) {
+                                                       int64_t cap, int op, unsigned* err, uint64_t timeout_ticks,
+                                                       int vec_io) {
     const int64_t c0 = (int64_t)blockIdx.x * chunk;
     const int64_t c1 = c0 + chunk < n ? c0 + chunk : n;
     const int64_t mine = (int64_t)(parity * kP2pMaxRanks + rank) * cap;  // my slot in every receive buffer
@@ -39,7 +40,8 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
     // phase 1: push this chunk into slot [parity][rank] of every rank's receive buffer (self included)
     for (int64_t i = c0 + 4 * (int64_t)threadIdx.x; i < c1; i += 4 * (int64_t)blockDim.x) {
         if (i + 4 <= c1) {
-            const float4 v = *reinterpret_cast<const float4*>(in + i);
+            const float4 v = vec_io ? *reinterpret_cast<const float4*>(in + i)
+                                    : make_float4(in[i], in[i + 1], in[i + 2], in[i + 3]);  // unaligned caller buffer
             for (int j = 0; j < nranks; ++j) *reinterpret_cast<float4*>(a.recv[j] + mine + i) = v;
         } else {
             for (int64_t k = i; k < c1; ++k) {
@@ -91,7 +93,11 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
                 s.z = red(s.z, v.z, op);
                 s.w = red(s.w, v.w, op);
             }
-            *reinterpret_cast<float4*>(out + i) = s;
+            if (vec_io) {
+                *reinterpret_cast<float4*>(out + i) = s;
+            } else {
+                out[i] = s.x, out[i + 1] = s.y, out[i + 2] = s.z, out[i + 3] = s.w;
+            }
         } else {
             for (int64_t k = i; k < c1; ++k) {
                 float s = base[k];
@@ -115,16 +121,17 @@ int64_t p2p_chunk(int64_t n) {
 void launch_p2p_allreduce(const float* in, float* out, int64_t n, const P2pArgs& a, int rank, int nranks,
                           unsigned epoch, int64_t cap, int op, unsigned* err, double timeout_s, hipStream_t stream) {
     if (n <= 0) return;
-    if (nranks < 1 || nranks > kP2pMaxRanks || rank < 0 || rank >= nranks || n > cap || cap % 4 != 0 ||
-        (reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) % 16 != 0)
+    if (nranks < 1 || nranks > kP2pMaxRanks || rank < 0 || rank >= nranks || n > cap || cap % 4 != 0)
         throw std::runtime_error("launch_p2p_allreduce: bad arguments (n=" + std::to_string(n) + ", cap=" +
-                                 std::to_string(cap) + ", ranks=" + std::to_string(nranks) + ", 16-B aligned buffers)");
+                                 std::to_string(cap) + ", ranks=" + std::to_string(nranks) + ")");
+    // the receive slots are always 16-B aligned; the caller's buffer may not be (4-B element accesses then)
+    const int vec_io = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) % 16) == 0;
     const int64_t chunk = p2p_chunk(n);
     const int64_t blocks = (n + chunk - 1) / chunk;
     if (blocks > kP2pMaxBlocks) throw std::runtime_error("launch_p2p_allreduce: too many chunks");
     const uint64_t ticks = (uint64_t)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
     hipLaunchKernelGGL(k_p2p_allreduce, dim3((unsigned)blocks), dim3(256), 0, stream, in, out, n, chunk, a, rank,
-                       nranks, epoch, (int)(epoch & 1u), cap, op, err, ticks);
+                       nranks, epoch, (int)(epoch & 1u), cap, op, err, ticks, vec_io);
     check_launch("k_p2p_allreduce");
 }
 

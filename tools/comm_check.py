@@ -30,20 +30,23 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     W, R = comm.world_size, comm.rank
     results = []
-    for n in [int(s) for s in a.sizes.split(",")]:
-        for op in ("sum", "max"):
-            data = [torch.randn(n, generator=torch.Generator().manual_seed(1000 * r + n), dtype=torch.float32)
-                    for r in range(W)]
-            want = data[0].clone()
-            for r in range(1, W):
-                want = want + data[r] if op == "sum" else torch.maximum(want, data[r])
-            buf = data[R].to(dev)
-            torch.cuda.synchronize()
-            k.all_reduce_device(buf.data_ptr(), n, False, ops.SUM if op == "sum" else ops.MAX, stream)
-            torch.cuda.synchronize()
-            got = buf.cpu()
-            results.append(dict(n=n, op=op, exact=bool(torch.equal(got, want)),
-                                close=bool(torch.allclose(got, want, rtol=1e-5, atol=1e-5))))
+    cases = [(int(s), op, 0) for s in a.sizes.split(",") for op in ("sum", "max")]
+    cases += [(n, "sum", 1) for n in (5, 4097)]  # buffer offset by one element: not 16-B aligned
+    for n, op, off in cases:
+        data = [torch.randn(n, generator=torch.Generator().manual_seed(1000 * r + n), dtype=torch.float32)
+                for r in range(W)]
+        want = data[0].clone()
+        for r in range(1, W):
+            want = want + data[r] if op == "sum" else torch.maximum(want, data[r])
+        store = torch.zeros(n + off, device=dev)
+        buf = store[off:]
+        buf.copy_(data[R].to(dev))
+        torch.cuda.synchronize()
+        k.all_reduce_device(buf.data_ptr(), n, False, ops.SUM if op == "sum" else ops.MAX, stream)
+        torch.cuda.synchronize()
+        got = buf.cpu()
+        results.append(dict(n=n, op=op, offset=off, exact=bool(torch.equal(got, want)),
+                            close=bool(torch.allclose(got, want, rtol=1e-5, atol=1e-5))))
     k.check()
     # latency at the engine's message size (64k voxels + the piggy-backed scalar)
     buf = torch.zeros(a.time_n, device=dev)
