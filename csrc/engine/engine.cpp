@@ -255,6 +255,8 @@ double Engine::setup_frame(const double* g, const double* x0) {
         if (!cols) comm_->all_reduce(O_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
     }
     launch_state_begin(st_.get(), G, cfg_.conv_tolerance, cfg_.max_iterations, stream_);
+    // per-XCD tickets of the first fused sweep (variant 6); later sweeps get them zeroed by the update kernel
+    if (use_fused_ && geom_.variant == 6) hip_ok(hipMemsetAsync(xcnt_.get(), 0, 16 * sizeof(unsigned), stream_), "memset");
     return norm;
 }
 
@@ -266,8 +268,8 @@ void Engine::sweep() {
         sweep_columns();
         return;
     }
+    unsigned* xcnt = (use_fused_ && geom_.variant == 6) ? xcnt_.get() : nullptr;  // zeroed by setup / update
     if (use_fused_) {
-        if (geom_.variant == 6) hip_ok(hipMemsetAsync(xcnt_.get(), 0, 16 * sizeof(unsigned), stream_), "memset");
         launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, A_, ld_, P_, Pp_, x_.get(), ghat_.get(),
                            arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I, geom_.J, st, xcnt_.get(),
                            stream_);
@@ -293,9 +295,9 @@ void Engine::sweep() {
     }
     launch_decide(st, Fslot, stream_);
     if (cfg_.logarithmic)
-        launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_);
+        launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_, xcnt);
     else
-        launch_update_linear(x_.get(), comm_buf_.get(), pen, V_, st, stream_);
+        launch_update_linear(x_.get(), comm_buf_.get(), pen, V_, st, stream_, xcnt);
 }
 
 void Engine::sweep_columns() {

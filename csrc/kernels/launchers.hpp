@@ -31,10 +31,11 @@ void launch_init_solution(float* x, int64_t n, int64_t n_pad, const float* src_f
 void launch_penalty(bool logx, const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta,
                     const float* x, float* pen, const SartState* st, hipStream_t stream);
 void launch_decide(SartState* st, const float* Fslot, hipStream_t stream);
+// xcnt (optional): fused-sweep ticket counters to zero for the next sweep
 void launch_update_linear(float* x, const float* d, const float* pen, int64_t n, const SartState* st,
-                          hipStream_t stream);
+                          hipStream_t stream, unsigned* xcnt = nullptr);
 void launch_update_log(float* x, const float* O, const float* Fv, const float* pen, float alpha, int64_t n,
-                       const SartState* st, hipStream_t stream);
+                       const SartState* st, hipStream_t stream, unsigned* xcnt = nullptr);
 void launch_state_begin(SartState* st, double G, double tol, int max_iter, hipStream_t stream);
 // w = a (ghat - f) (linear) or a f (log) from a complete forward projection f; Fpart[block] = sum f^2 (fp64)
 int weights_num_blocks(int64_t nrows_pad);

@@ -115,9 +115,12 @@ __global__ void k_decide(SartState* __restrict__ st, const float* __restrict__ F
 }
 
 // x = max(x + d - pen, 0)
+// xcnt (optional): the per-XCD ticket counters of the next fused sweep (variant 6), zeroed here so the
+// sweep loop needs no separate memset launch per iteration (the sweep that used them has completed).
 __global__ __launch_bounds__(256) void k_update_linear(float* __restrict__ x, const float* __restrict__ d,
                                                        const float* __restrict__ pen, int64_t n,
-                                                       const SartState* __restrict__ st) {
+                                                       const SartState* __restrict__ st, unsigned* __restrict__ xcnt) {
+    if (xcnt && blockIdx.x == 0 && threadIdx.x < 16) xcnt[threadIdx.x] = 0u;
     if (st->done) return;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
@@ -129,7 +132,9 @@ __global__ __launch_bounds__(256) void k_update_linear(float* __restrict__ x, co
 // x *= ((O + eps) / (Fv + eps))^alpha * exp(-pen)
 __global__ __launch_bounds__(256) void k_update_log(float* __restrict__ x, const float* __restrict__ O,
                                                     const float* __restrict__ Fv, const float* __restrict__ pen,
-                                                    float alpha, int64_t n, const SartState* __restrict__ st) {
+                                                    float alpha, int64_t n, const SartState* __restrict__ st,
+                                                    unsigned* __restrict__ xcnt) {
+    if (xcnt && blockIdx.x == 0 && threadIdx.x < 16) xcnt[threadIdx.x] = 0u;  // see k_update_linear
     if (st->done) return;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
@@ -269,14 +274,14 @@ void launch_decide(SartState* st, const float* Fslot, hipStream_t stream) {
 }
 
 void launch_update_linear(float* x, const float* d, const float* pen, int64_t n, const SartState* st,
-                          hipStream_t stream) {
-    hipLaunchKernelGGL(k_update_linear, dim3(nb(n)), dim3(256), 0, stream, x, d, pen, n, st);
+                          hipStream_t stream, unsigned* xcnt) {
+    hipLaunchKernelGGL(k_update_linear, dim3(nb(n)), dim3(256), 0, stream, x, d, pen, n, st, xcnt);
     check_launch("k_update_linear");
 }
 
 void launch_update_log(float* x, const float* O, const float* Fv, const float* pen, float alpha, int64_t n,
-                       const SartState* st, hipStream_t stream) {
-    hipLaunchKernelGGL(k_update_log, dim3(nb(n)), dim3(256), 0, stream, x, O, Fv, pen, alpha, n, st);
+                       const SartState* st, hipStream_t stream, unsigned* xcnt) {
+    hipLaunchKernelGGL(k_update_log, dim3(nb(n)), dim3(256), 0, stream, x, O, Fv, pen, alpha, n, st, xcnt);
     check_launch("k_update_log");
 }
 
