@@ -68,12 +68,17 @@ def main() -> int:
                          "pixels of --nvox voxels (two-pass kernels, all-reduce of A.x)")
     ap.add_argument("--laplacian", action="store_true",
                     help="add the 7-point grid Laplacian regulariser (beta 1e-2, the reference default)")
+    ap.add_argument("--rtm-dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="RTM storage precision; bf16 is opt-in (half the bytes per sweep, fp32 products and sums, "
+                         "two-pass kernels); the BASELINE headline is fp32")
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
                     help="BASELINE.json configuration preset (sets npix / nvox / iters / frames / laplacian)")
     args = ap.parse_args()
     if args.config:
         for k, v in PRESETS[args.config].items():
             setattr(args, k, v)
+    if args.rtm_dtype == "bf16" and (args.frames > 1 or args.partition == "cols"):
+        ap.error("--rtm-dtype bf16 runs single-frame row shards (two-pass kernels)")
     if args.partition == "cols" and args.frames > 1:
         ap.error("--partition cols solves single frames (the multi-frame engine uses row shards)")
 
@@ -103,7 +108,8 @@ def main() -> int:
     else:
         npix_total = args.npix * n if args.scaling == "weak" else args.npix
         blk = row_partition(npix_total, n, comm.rank)
-        prob = make_problem(blk.size, args.nvox, row_offset=blk.offset, seed=args.seed, device=dev)
+        prob = make_problem(blk.size, args.nvox, row_offset=blk.offset, seed=args.seed, device=dev,
+                            storage=args.rtm_dtype)
     params = SolverParams(max_iterations=args.iters, conv_tolerance=0.0)  # fixed iteration count
     lap = None
     if args.laplacian:
@@ -176,7 +182,7 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32" if args.rtm_dtype == "fp32" else "bf16 RTM storage, fp32 compute",
         "data": "synthetic (on-device random dense RTM, random phantom; no HDF5)",
         "iters_per_s": round(iters_per_s, 3),
         "sart_iterations_per_step": args.iters,
@@ -202,6 +208,7 @@ def main() -> int:
             "parallelism": (f"{'col' if cols else 'row'}-shard dp{n}" if n > 1 else "single"),
             "partition": args.partition,
             "rtm_GB_per_gpu": round(prob.rtm.nbytes / 1e9, 2),
+            "rtm_storage": args.rtm_dtype,
         },
     }
     if comm.rank == 0:

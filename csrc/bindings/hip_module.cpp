@@ -151,6 +151,7 @@ static void bind_engine(py::module_& m) {
         .def_readwrite("fused_schedule", &sart::EngineConfig::fused_schedule)
         .def_readwrite("use_graph", &sart::EngineConfig::use_graph)
         .def_readwrite("time_collectives", &sart::EngineConfig::time_collectives)
+        .def_readwrite("rtm_bf16", &sart::EngineConfig::rtm_bf16)
         .def_readwrite("fault_inject", &sart::EngineConfig::fault_inject);
     m.def("validate_config", [](const sart::EngineConfig& c) {
         try {
@@ -276,24 +277,49 @@ PYBIND11_MODULE(_sart_hip, m) {
     });
 
     m.def("forward_num_blocks", &sart::forward_num_blocks);
+    // bf16: A holds bf16 bit patterns (opt-in storage precision)
     m.def("forward", [](int epi, uintptr_t A, int64_t ld, int64_t nrows, int64_t nrows_pad, uintptr_t x,
                         uintptr_t ghat, uintptr_t arow, uintptr_t out_f, uintptr_t out_w, uintptr_t Fpart,
-                        uintptr_t st, uintptr_t stream) {
-        sart::launch_forward(epi, P<const float>(A), ld, nrows, nrows_pad, P<const float>(x), P<const float>(ghat),
-                             P<const float>(arow), P<float>(out_f), P<float>(out_w), P<double>(Fpart),
-                             P<const sart::SartState>(st), S(stream));
-    });
-    m.def("rowsum_f64", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t out, uintptr_t stream) {
-        sart::launch_rowsum_f64(P<const float>(A), ld, nrows, P<double>(out), S(stream));
-    });
-    m.def("backproject_num_splits", &sart::backproject_num_splits);
-    m.def("backproject", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t w, int nsplit, uintptr_t partial,
-                            uintptr_t st, uintptr_t stream) {
-        sart::launch_backproject(P<const float>(A), ld, nrows, P<const float>(w), nsplit, P<float>(partial),
+                        uintptr_t st, uintptr_t stream, bool bf16) {
+        if (bf16)
+            sart::launch_forward(epi, P<const sart::bf16_t>(A), ld, nrows, nrows_pad, P<const float>(x),
+                                 P<const float>(ghat), P<const float>(arow), P<float>(out_f), P<float>(out_w),
+                                 P<double>(Fpart), P<const sart::SartState>(st), S(stream));
+        else
+            sart::launch_forward(epi, P<const float>(A), ld, nrows, nrows_pad, P<const float>(x), P<const float>(ghat),
+                                 P<const float>(arow), P<float>(out_f), P<float>(out_w), P<double>(Fpart),
                                  P<const sart::SartState>(st), S(stream));
-    });
-    m.def("colsum_f64", [](uintptr_t A, int64_t ld, int64_t nrows, int nsplit, uintptr_t partial, uintptr_t stream) {
-        sart::launch_colsum_f64(P<const float>(A), ld, nrows, nsplit, P<double>(partial), S(stream));
+    }, py::arg("epi"), py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("nrows_pad"), py::arg("x"),
+       py::arg("ghat"), py::arg("arow"), py::arg("out_f"), py::arg("out_w"), py::arg("Fpart"), py::arg("st"),
+       py::arg("stream"), py::arg("bf16") = false);
+    m.def("rowsum_f64", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t out, uintptr_t stream, bool bf16) {
+        if (bf16)
+            sart::launch_rowsum_f64(P<const sart::bf16_t>(A), ld, nrows, P<double>(out), S(stream));
+        else
+            sart::launch_rowsum_f64(P<const float>(A), ld, nrows, P<double>(out), S(stream));
+    }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("out"), py::arg("stream"), py::arg("bf16") = false);
+    m.def("backproject_num_splits", &sart::backproject_num_splits, py::arg("ld"), py::arg("nrows"),
+          py::arg("elem_bytes") = 4);
+    m.def("backproject", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t w, int nsplit, uintptr_t partial,
+                            uintptr_t st, uintptr_t stream, bool bf16) {
+        if (bf16)
+            sart::launch_backproject(P<const sart::bf16_t>(A), ld, nrows, P<const float>(w), nsplit,
+                                     P<float>(partial), P<const sart::SartState>(st), S(stream));
+        else
+            sart::launch_backproject(P<const float>(A), ld, nrows, P<const float>(w), nsplit, P<float>(partial),
+                                     P<const sart::SartState>(st), S(stream));
+    }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("w"), py::arg("nsplit"), py::arg("partial"),
+       py::arg("st"), py::arg("stream"), py::arg("bf16") = false);
+    m.def("colsum_f64", [](uintptr_t A, int64_t ld, int64_t nrows, int nsplit, uintptr_t partial, uintptr_t stream,
+                           bool bf16) {
+        if (bf16)
+            sart::launch_colsum_f64(P<const sart::bf16_t>(A), ld, nrows, nsplit, P<double>(partial), S(stream));
+        else
+            sart::launch_colsum_f64(P<const float>(A), ld, nrows, nsplit, P<double>(partial), S(stream));
+    }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("nsplit"), py::arg("partial"), py::arg("stream"),
+       py::arg("bf16") = false);
+    m.def("f32_to_bf16", [](uintptr_t src, int64_t n, uintptr_t dst, uintptr_t stream) {
+        sart::launch_f32_to_bf16(P<const float>(src), n, P<sart::bf16_t>(dst), S(stream));
     });
     m.def("reduce_partials", [](uintptr_t partial, int64_t ld, int nsplit, uintptr_t scale, uintptr_t out,
                                 uintptr_t Fpart, int64_t nF, uintptr_t Fout, uintptr_t st, uintptr_t stream) {

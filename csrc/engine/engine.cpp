@@ -61,7 +61,7 @@ template class DeviceArray<unsigned>;
 template class DeviceArray<int64_t>;
 template class DeviceArray<int32_t>;
 
-Engine::Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
+Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
                Communicator* comm, const EngineConfig& cfg)
     : device_(device), A_(A), P_(nrows), Pp_(nrows_pad), V_(nvoxel), ld_(ld), comm_(comm), cfg_(cfg) {
     validate_params(cfg_);
@@ -86,7 +86,7 @@ Engine::Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int
     if (const char* fi = std::getenv("SART_FAULT_INJECT"); fi && *fi && cfg_.fault_inject == 0)
         cfg_.fault_inject = std::atoi(fi);
 
-    nsplit_ = backproject_num_splits(ld_, Pp_);
+    nsplit_ = backproject_num_splits(ld_, Pp_, cfg_.rtm_bf16 ? 2 : 4);
     comm_buf_.resize(ld_ + 64);  // [0, ld) correction, [ld] ||A x||^2
     x_.resize(ld_);
     pen_.resize(ld_);
@@ -97,7 +97,8 @@ Engine::Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int
     st_.resize(1);
     xcnt_.resize(16);
     use_fused_ = false;
-    if (cfg_.use_fused && !cfg_.column_shard && (double)Pp_ * (double)ld_ * sizeof(float) >= cfg_.fused_min_bytes) {
+    // bf16 storage: two-pass kernels (the fused sweep streams fp32 tiles)
+    if (cfg_.use_fused && !cfg_.column_shard && !cfg_.rtm_bf16 && (double)Pp_ * (double)ld_ * sizeof(float) >= cfg_.fused_min_bytes) {
         geom_ = fused_geometry(ld_, num_cus_, cfg_.fused_variant, cfg_.rows_per_tile);
         use_fused_ = geom_.valid();
     }
@@ -134,8 +135,8 @@ void Engine::alloc_fused() {
     if (use_fused_ && (int64_t)gran_.size() < Pp_ * geom_.J) gran_.resize(Pp_ * geom_.J);
 }
 
-void DeviceRaySums::compute(const float* A, int64_t P, int64_t Pp, int64_t V, int64_t ld, Communicator* comm,
-                            const SolverParams& p, hipStream_t stream, bool col_shard) {
+void DeviceRaySums::compute(const void* A, int64_t P, int64_t Pp, int64_t V, int64_t ld, Communicator* comm,
+                            const SolverParams& p, hipStream_t stream, bool col_shard, bool a_bf16) {
     // rho_v = sum_p A[p, v] (fp64, all-reduced), l_p = sum_v A[p, v] (fp64, local): on the device instead of
     // the reference's host loops (sartsolver.cpp:38-56); scales with the reference's fp32 semantics
     RoctxRange r("sart::ray_sums");
@@ -143,11 +144,16 @@ void DeviceRaySums::compute(const float* A, int64_t P, int64_t Pp, int64_t V, in
     rho64.resize(ld);
     ray_len.resize(Pp);
     for (auto* b : {&dinv, &dscale, &dmask}) b->resize(ld);
-    launch_rowsum_f64(A, ld, P, ell64.get(), stream);
-    const int nsplit = backproject_num_splits(ld, Pp);
+    const int nsplit = backproject_num_splits(ld, Pp, a_bf16 ? 2 : 4);
     {
         DeviceArray<double> part((size_t)nsplit * ld);
-        launch_colsum_f64(A, ld, P, nsplit, part.get(), stream);
+        if (a_bf16) {
+            launch_rowsum_f64(static_cast<const bf16_t*>(A), ld, P, ell64.get(), stream);
+            launch_colsum_f64(static_cast<const bf16_t*>(A), ld, P, nsplit, part.get(), stream);
+        } else {
+            launch_rowsum_f64(static_cast<const float*>(A), ld, P, ell64.get(), stream);
+            launch_colsum_f64(static_cast<const float*>(A), ld, P, nsplit, part.get(), stream);
+        }
         launch_reduce_partials_f64(part.get(), ld, nsplit, rho64.get(), stream);
         hip_ok(hipStreamSynchronize(stream), "ray sums");
     }
@@ -173,7 +179,25 @@ std::vector<double> DeviceRaySums::length(int64_t P) const {
     return h;
 }
 
-void Engine::ray_sums() { rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_, cfg_.column_shard); }
+void Engine::ray_sums() { rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_, cfg_.column_shard, cfg_.rtm_bf16); }
+
+void Engine::fwd(int epi, const float* x, float* out_f, float* out_w, double* Fpart, const SartState* st) {
+    const float* ghat = epi == kEpiPlain ? nullptr : ghat_.get();
+    const float* arow = epi == kEpiPlain ? nullptr : arow_.get();
+    if (cfg_.rtm_bf16)
+        launch_forward(epi, static_cast<const bf16_t*>(A_), ld_, P_, Pp_, x, ghat, arow, out_f, out_w, Fpart, st,
+                       stream_);
+    else
+        launch_forward(epi, static_cast<const float*>(A_), ld_, P_, Pp_, x, ghat, arow, out_f, out_w, Fpart, st,
+                       stream_);
+}
+
+void Engine::bwd(const float* w, const SartState* st) {
+    if (cfg_.rtm_bf16)
+        launch_backproject(static_cast<const bf16_t*>(A_), ld_, P_, w, nsplit_, partial_.get(), st, stream_);
+    else
+        launch_backproject(static_cast<const float*>(A_), ld_, P_, w, nsplit_, partial_.get(), st, stream_);
+}
 
 std::vector<double> Engine::ray_density() const {
     set_device();
@@ -238,7 +262,7 @@ double Engine::setup_frame(const double* g, const double* x0) {
                      arow_.get(), gpos_.get(), wo_.get(), stream_);
     if (!x0) {
         // cold start x0 = [rho > tau] A^T max(ghat, 0) / rho (reference sart_kernels.cu:22-60)
-        launch_backproject(A_, ld_, P_, gpos_.get(), nsplit_, partial_.get(), nullptr, stream_);
+        bwd(gpos_.get(), nullptr);
         launch_reduce_partials(partial_.get(), ld_, nsplit_, rs_.dinv.get(), comm_buf_.get(), nullptr, 0, nullptr,
                                nullptr, stream_);
         if (!cols) comm_->all_reduce(comm_buf_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
@@ -249,7 +273,7 @@ double Engine::setup_frame(const double* g, const double* x0) {
     }
     if (cfg_.logarithmic) {
         // frame-constant observed back-projection O = [rho > tau] A^T (a ghat), reduced once per frame
-        launch_backproject(A_, ld_, P_, wo_.get(), nsplit_, partial_.get(), nullptr, stream_);
+        bwd(wo_.get(), nullptr);
         launch_reduce_partials(partial_.get(), ld_, nsplit_, rs_.dmask.get(), O_.get(), nullptr, 0, nullptr, nullptr,
                                stream_);
         if (!cols) comm_->all_reduce(O_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
@@ -270,15 +294,14 @@ void Engine::sweep() {
     }
     unsigned* xcnt = (use_fused_ && geom_.variant == 6) ? xcnt_.get() : nullptr;  // zeroed by setup / update
     if (use_fused_) {
-        launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, A_, ld_, P_, Pp_, x_.get(), ghat_.get(),
+        launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, static_cast<const float*>(A_), ld_, P_, Pp_, x_.get(), ghat_.get(),
                            arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I, geom_.J, st, xcnt_.get(),
                            stream_);
         launch_reduce_partials(partial_.get(), ld_, geom_.I, scale, comm_buf_.get(), Fpart_.get(), nF_fused_, Fslot,
                                st, stream_);
     } else {
-        launch_forward(cfg_.logarithmic ? kEpiLog : kEpiLinear, A_, ld_, P_, Pp_, x_.get(), ghat_.get(), arow_.get(),
-                       nullptr, w_.get(), Fpart_.get(), st, stream_);
-        launch_backproject(A_, ld_, P_, w_.get(), nsplit_, partial_.get(), st, stream_);
+        fwd(cfg_.logarithmic ? kEpiLog : kEpiLinear, x_.get(), nullptr, w_.get(), Fpart_.get(), st);
+        bwd(w_.get(), st);
         launch_reduce_partials(partial_.get(), ld_, nsplit_, scale, comm_buf_.get(), Fpart_.get(),
                                forward_num_blocks(Pp_), Fslot, st, stream_);
     }
@@ -306,8 +329,7 @@ void Engine::sweep_columns() {
     SartState* st = st_.get();
     const float* scale = cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get();
     float* Fslot = comm_buf_.get() + ld_;
-    launch_forward(kEpiPlain, A_, ld_, P_, Pp_, x_.get(), nullptr, nullptr, fitted_.get(), nullptr, nullptr, st,
-                   stream_);
+    fwd(kEpiPlain, x_.get(), fitted_.get(), nullptr, nullptr, st);
     if (comm_->size() > 1) {
         comm_begin();
         comm_->all_reduce(fitted_.get(), (size_t)P_, ReduceOp::kSum, stream_);
@@ -315,7 +337,7 @@ void Engine::sweep_columns() {
     }
     launch_weights(cfg_.logarithmic, fitted_.get(), ghat_.get(), arow_.get(), P_, Pp_, w_.get(), Fpart_.get(), st,
                    stream_);
-    launch_backproject(A_, ld_, P_, w_.get(), nsplit_, partial_.get(), st, stream_);
+    bwd(w_.get(), st);
     launch_reduce_partials(partial_.get(), ld_, nsplit_, scale, comm_buf_.get(), Fpart_.get(),
                            weights_num_blocks(Pp_), Fslot, st, stream_);
     const float* pen = nullptr;
@@ -499,8 +521,7 @@ void Engine::forward(const double* x, double* f) {
     for (int64_t i = 0; i < V_; ++i) xf[i] = (float)x[i];
     DeviceArray<float> xd(ld_);
     hip_ok(hipMemcpyAsync(xd.get(), xf.data(), ld_ * sizeof(float), hipMemcpyHostToDevice, stream_), "H2D");
-    launch_forward(kEpiPlain, A_, ld_, P_, Pp_, xd.get(), nullptr, nullptr, fitted_.get(), nullptr, nullptr, nullptr,
-                   stream_);
+    fwd(kEpiPlain, xd.get(), fitted_.get(), nullptr, nullptr, nullptr);
     if (cfg_.column_shard && comm_->size() > 1) comm_->all_reduce(fitted_.get(), (size_t)P_, ReduceOp::kSum, stream_);
     std::vector<float> fh(P_);
     if (P_) hip_ok(hipMemcpyAsync(fh.data(), fitted_.get(), P_ * sizeof(float), hipMemcpyDeviceToHost, stream_), "D2H");

@@ -56,6 +56,11 @@ struct EngineConfig : SolverParams {
     // Observability: bracket every per-sweep all-reduce with timing events and report the GPU
     // time spent in collectives (SolveInfo::comm_ms). Eager chunks only (ignored with use_graph).
     bool time_collectives = false;
+    // Storage precision of the shard: A holds bf16 bit patterns instead of fp32 (half the
+    // HBM bytes per sweep, twice the matrix per GPU); products, sums and every vector stay fp32 / fp64. Ray
+    // sums are taken over the stored (rounded) values, so the solve is exact SART for the bf16 matrix.
+    // Two-pass kernels (the fused sweep and the multi-frame engine are fp32-only).
+    bool rtm_bf16 = false;
 };
 
 // roctx range (rocprofv3 --marker-trace) for the lifetime of the object.
@@ -86,8 +91,9 @@ class DeviceArray {
 // accumulation, global column sums all-reduced): shared by the single- and multi-frame engines.
 struct DeviceRaySums {
     // col_shard: the shard holds all rows of some columns, so the row sums are all-reduced instead
-    void compute(const float* A, int64_t P, int64_t Pp, int64_t V, int64_t ld, Communicator* comm,
-                 const SolverParams& p, hipStream_t stream, bool col_shard = false);
+    // A: fp32 shard, or bf16 bit patterns when a_bf16
+    void compute(const void* A, int64_t P, int64_t Pp, int64_t V, int64_t ld, Communicator* comm,
+                 const SolverParams& p, hipStream_t stream, bool col_shard = false, bool a_bf16 = false);
     std::vector<double> density(int64_t V) const;  // host copies
     std::vector<double> length(int64_t P) const;
     DeviceArray<double> rho64, ell64;
@@ -99,8 +105,9 @@ double fused_min_bytes_from_env();
 
 class Engine {
    public:
-    // A: device pointer to the row-major fp32 shard [nrows_pad x ld], zero padded (not owned).
-    Engine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
+    // A: device pointer to the row-major shard [nrows_pad x ld] (fp32, or bf16 with cfg.rtm_bf16), zero
+    // padded (not owned).
+    Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
            Communicator* comm, const EngineConfig& cfg);
     ~Engine();
     Engine(const Engine&) = delete;
@@ -132,13 +139,17 @@ class Engine {
     double setup_frame(const double* g, const double* x0);
     void sweep();
     void sweep_columns();
+    // two-pass kernels on the shard in its storage type: forward (epilogue epi) and split-K back-projection
+    // into partial_
+    void fwd(int epi, const float* x, float* out_f, float* out_w, double* Fpart, const SartState* st);
+    void bwd(const float* w, const SartState* st);
     void run_chunk(int n);
     bool fallback();  // false when nothing is left to fall back to
     void drop_graph();
     void set_device() const;
 
     int device_;
-    const float* A_;
+    const void* A_;
     int64_t P_, Pp_, V_, ld_;
     Communicator* comm_;
     EngineConfig cfg_;

@@ -23,6 +23,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, in
                                    int64_t ld, Communicator* comm, const EngineConfig& cfg)
     : device_(device), A_(A), P_(nrows), Pp_(nrows_pad), V_(nvoxel), ld_(ld), comm_(comm), cfg_(cfg) {
     validate_params(cfg_);
+    if (cfg_.rtm_bf16) throw std::invalid_argument("MultiFrameEngine: bf16 RTM storage is not supported (fp32 MFMA)");
     if (!comm_) throw std::invalid_argument("MultiFrameEngine: communicator required");
     if (ld_ % 64 || ld_ < V_ || Pp_ % 64 || Pp_ < P_)
         throw std::invalid_argument("MultiFrameEngine: ld and nrows_pad must be multiples of 64 covering the shard");

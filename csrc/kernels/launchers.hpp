@@ -10,16 +10,25 @@
 #include "sart_common.hpp"
 
 namespace sart {
-// projection.hip
+// projection.hip (RTM in fp32, or bf16 storage with fp32 products and sums)
 int64_t forward_num_blocks(int64_t nrows_pad);
 void launch_forward(int epi, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* x,
                     const float* ghat, const float* arow, float* out_f, float* out_w, double* Fpart,
                     const SartState* st, hipStream_t stream);
+void launch_forward(int epi, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* x,
+                    const float* ghat, const float* arow, float* out_f, float* out_w, double* Fpart,
+                    const SartState* st, hipStream_t stream);
 void launch_rowsum_f64(const float* A, int64_t ld, int64_t nrows, double* out, hipStream_t stream);
-int backproject_num_splits(int64_t ld, int64_t nrows);
+void launch_rowsum_f64(const bf16_t* A, int64_t ld, int64_t nrows, double* out, hipStream_t stream);
+int backproject_num_splits(int64_t ld, int64_t nrows, int elem_bytes = 4);
 void launch_backproject(const float* A, int64_t ld, int64_t nrows, const float* w, int nsplit, float* partial,
                         const SartState* st, hipStream_t stream);
+void launch_backproject(const bf16_t* A, int64_t ld, int64_t nrows, const float* w, int nsplit, float* partial,
+                        const SartState* st, hipStream_t stream);
 void launch_colsum_f64(const float* A, int64_t ld, int64_t nrows, int nsplit, double* partial, hipStream_t stream);
+void launch_colsum_f64(const bf16_t* A, int64_t ld, int64_t nrows, int nsplit, double* partial, hipStream_t stream);
+// fp32 -> bf16, round to nearest even (n a multiple of 4)
+void launch_f32_to_bf16(const float* src, int64_t n, bf16_t* dst, hipStream_t stream);
 void launch_reduce_partials(const float* partial, int64_t ld, int nsplit, const float* scale, float* out,
                             const double* Fpart, int64_t nF, float* Fout, const SartState* st, hipStream_t stream);
 void launch_reduce_partials_f64(const double* partial, int64_t ld, int nsplit, double* out, hipStream_t stream);

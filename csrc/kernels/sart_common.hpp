@@ -86,6 +86,42 @@ __device__ __forceinline__ float4 load_stream(const float4* p) {
 #endif
 }
 
+// RTM element access of the two-pass kernels, by storage type. fp32 (the reference's storage) or bf16 (opt-in
+// storage precision, SURVEY 7.3 8(d): half the HBM bytes per sweep and twice the matrix per GPU; products
+// and sums stay fp32). One 16-byte vector load per call: 4 fp32 or 8 bf16 columns, widened to NF4 float4.
+typedef uint16_t bf16_t;  // raw bf16 bit pattern (upper half of an fp32)
+typedef unsigned sart_u4v __attribute__((ext_vector_type(4)));
+
+template <typename AT>
+struct RtmVec;
+
+template <>
+struct RtmVec<float> {
+    static constexpr int NF4 = 1;  // float4 per 16-byte load
+    __device__ __forceinline__ static void load(const float* row, int64_t v, float4 (&o)[1]) {
+        o[0] = load_stream(reinterpret_cast<const float4*>(row) + v);
+    }
+};
+
+__device__ __forceinline__ float4 bf16x4_to_f4(unsigned lo, unsigned hi) {
+    return make_float4(__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u), __uint_as_float(hi << 16),
+                       __uint_as_float(hi & 0xffff0000u));
+}
+
+template <>
+struct RtmVec<bf16_t> {
+    static constexpr int NF4 = 2;
+    __device__ __forceinline__ static void load(const bf16_t* row, int64_t v, float4 (&o)[2]) {
+#if SART_STREAM_NT
+        const sart_u4v u = __builtin_nontemporal_load(reinterpret_cast<const sart_u4v*>(row) + v);
+#else
+        const sart_u4v u = reinterpret_cast<const sart_u4v*>(row)[v];
+#endif
+        o[0] = bf16x4_to_f4(u.x, u.y);
+        o[1] = bf16x4_to_f4(u.z, u.w);
+    }
+};
+
 __device__ __forceinline__ float dot4(const float4 a, const float4 b) {
     return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
 }

@@ -100,7 +100,7 @@ class DenseRTM:
 
     def __init__(self, npixel: int, nvoxel: int, row_offset: int = 0, device: Optional[torch.device] = None,
                  ld: Optional[int] = None, row_align: int = 64, col_offset: int = 0,
-                 nvoxel_total: Optional[int] = None):
+                 nvoxel_total: Optional[int] = None, storage: str = "fp32"):
         if npixel <= 0 or nvoxel <= 0:
             raise ValueError("RTM shard must have npixel > 0 and nvoxel > 0")
         self.npixel = int(npixel)
@@ -115,12 +115,35 @@ class DenseRTM:
         if self.ld % 64 or self.ld < self.nvoxel:
             raise ValueError("ld must be a multiple of 64 and >= nvoxel")
         self.nrows_pad = round_up(self.npixel, row_align)
-        self.A = torch.empty((self.nrows_pad, self.ld), dtype=torch.float32, device=self.device)
+        # storage precision: "fp32" (the reference's) or "bf16" (opt-in: half the HBM bytes per sweep and twice
+        # the matrix per GPU; the two-pass kernels widen to fp32 in registers, sums stay fp32 / fp64)
+        if storage not in ("fp32", "bf16"):
+            raise ValueError("storage must be 'fp32' or 'bf16'")
+        self.storage = storage
+        dt = torch.bfloat16 if storage == "bf16" else torch.float32
+        self.A = torch.empty((self.nrows_pad, self.ld), dtype=dt, device=self.device)
 
     # ------------------------------------------------------------------ construction helpers
     @property
     def nbytes(self) -> int:
-        return self.nrows_pad * self.ld * 4
+        return self.nrows_pad * self.ld * self.A.element_size()
+
+    @property
+    def is_bf16(self) -> bool:
+        return self.storage == "bf16"
+
+    # rows converted per block when an fp32 source is stored as bf16 (bounds the fp32 scratch to ~256 MiB)
+    def _block_rows(self) -> int:
+        return max(64, min(self.nrows_pad, (256 << 20) // (4 * self.ld)))
+
+    def _store_rows(self, local_row: int, src) -> None:
+        """Store a device fp32 block [n, ld] into rows [local_row, local_row + n) (native RNE conversion for bf16)."""
+        n = src.shape[0]
+        if not self.is_bf16:
+            self.A[local_row: local_row + n].copy_(src)
+            return
+        src = src.contiguous()
+        hip().f32_to_bf16(src.data_ptr(), n * self.ld, self.A[local_row].data_ptr(), self.stream_handle)
 
     @property
     def stream_handle(self) -> int:
@@ -139,30 +162,65 @@ class DenseRTM:
     @classmethod
     def synthetic(cls, npixel: int, nvoxel: int, row_offset: int = 0, seed: int = 1234, lo: float = 0.0,
                   hi: float = 1.0, device=None, ld=None, col_offset: int = 0,
-                  nvoxel_total: Optional[int] = None) -> "DenseRTM":
+                  nvoxel_total: Optional[int] = None, storage: str = "fp32") -> "DenseRTM":
         """On-device random dense RTM; element (p, v) depends only on (seed, global p, global v), so row and
         column shards of one global matrix agree bit for bit."""
-        m = cls(npixel, nvoxel, row_offset, device=device, ld=ld, col_offset=col_offset, nvoxel_total=nvoxel_total)
-        hip().synth_matrix(m.A.data_ptr(), m.ld, m.nrows_pad, m.npixel, m.nvoxel, m.row_offset, int(seed), float(lo),
-                           float(hi), m.stream_handle, m.col_offset, m.nvoxel_total)
+        m = cls(npixel, nvoxel, row_offset, device=device, ld=ld, col_offset=col_offset, nvoxel_total=nvoxel_total,
+                storage=storage)
+        if not m.is_bf16:
+            hip().synth_matrix(m.A.data_ptr(), m.ld, m.nrows_pad, m.npixel, m.nvoxel, m.row_offset, int(seed),
+                               float(lo), float(hi), m.stream_handle, m.col_offset, m.nvoxel_total)
+            return m
+        # bf16: generate fp32 row blocks of the same global matrix and round them into the shard
+        nb = m._block_rows()
+        scratch = torch.empty((nb, m.ld), dtype=torch.float32, device=m.device)
+        for r0 in range(0, m.nrows_pad, nb):
+            n = min(nb, m.nrows_pad - r0)
+            valid = max(0, min(n, m.npixel - r0))
+            hip().synth_matrix(scratch.data_ptr(), m.ld, n, valid, m.nvoxel, m.row_offset + r0, int(seed),
+                               float(lo), float(hi), m.stream_handle, m.col_offset, m.nvoxel_total)
+            m._store_rows(r0, scratch[:n])
+        torch.cuda.synchronize(m.device)
         return m
 
     @classmethod
     def from_dense(cls, A_local, row_offset: int = 0, device=None, ld=None, col_offset: int = 0,
-                   nvoxel_total: Optional[int] = None) -> "DenseRTM":
+                   nvoxel_total: Optional[int] = None, storage: str = "fp32") -> "DenseRTM":
         """Upload a host (numpy / torch) dense block [npixel, nvoxel]."""
         t = torch.as_tensor(A_local, dtype=torch.float32)
         m = cls(t.shape[0], t.shape[1], row_offset, device=device, ld=ld, col_offset=col_offset,
-                nvoxel_total=nvoxel_total)
+                nvoxel_total=nvoxel_total, storage=storage)
         m.A.zero_()
-        m.A[: m.npixel, : m.nvoxel].copy_(t.to(m.device, non_blocking=False))
+        m.fill_rows(0, t)
         return m
 
     def fill_rows(self, local_row: int, block) -> None:
         """Copy a host block of rows [local_row, local_row + len(block)) x [0, nvoxel) into HBM."""
         t = torch.as_tensor(block, dtype=torch.float32)
         n = t.shape[0]
-        self.A[local_row: local_row + n, : self.nvoxel].copy_(t, non_blocking=t.is_pinned())
+        if not self.is_bf16:
+            self.A[local_row: local_row + n, : self.nvoxel].copy_(t, non_blocking=t.is_pinned())
+            return
+        nb = self._block_rows()
+        for r0 in range(0, n, nb):
+            k = min(nb, n - r0)
+            scratch = torch.zeros((k, self.ld), dtype=torch.float32, device=self.device)
+            scratch[:, : self.nvoxel].copy_(t[r0: r0 + k])
+            self._store_rows(local_row + r0, scratch)
+        torch.cuda.synchronize(self.device)
+
+    def to_bf16(self) -> "DenseRTM":
+        """bf16-stored copy of this shard (same geometry), rounded to nearest even by the native kernel."""
+        # row_align = nrows_pad reproduces this shard's padded row count
+        m = DenseRTM(self.npixel, self.nvoxel, self.row_offset, device=self.device, ld=self.ld,
+                     row_align=self.nrows_pad, col_offset=self.col_offset, nvoxel_total=self.nvoxel_total,
+                     storage="bf16")
+        src = self.A if not self.is_bf16 else self.A.float()
+        nb = m._block_rows()
+        for r0 in range(0, self.nrows_pad, nb):
+            m._store_rows(r0, src[r0: r0 + nb])
+        torch.cuda.synchronize(self.device)
+        return m
 
     def to_host(self):
-        return self.A[: self.npixel, : self.nvoxel].cpu().numpy()
+        return self.A[: self.npixel, : self.nvoxel].float().cpu().numpy()

@@ -138,7 +138,8 @@ class SARTSolver:
             use_graph = os.environ.get("SART_GRAPH", "0") == "1"
         cfg.use_graph = bool(use_graph)
         cfg.fused_min_bytes = float(fused_min_bytes)  # smaller shards use the two-pass kernels
-        cfg.time_collectives = bool(time_collectives)  # SolveResult.comm_ms (events around each all-reduce)
+        cfg.time_collectives = bool(time_collectives)
+        cfg.rtm_bf16 = bool(getattr(rtm, "is_bf16", False))  # bf16-stored shard: two-pass kernels  # SolveResult.comm_ms (events around each all-reduce)
         if self.column_shard:  # all pixel rows of voxels [col_offset, +nvoxel): two-pass, pixel all-reduce
             cfg.column_shard = True
             cfg.col_offset = int(getattr(rtm, "col_offset", 0))

@@ -22,17 +22,19 @@ class SyntheticProblem:
 
 
 def make_problem(npixel_local: int, nvoxel: int, row_offset: int = 0, seed: int = 1234, device=None,
-                 saturate_fraction: float = 0.0, ld=None) -> SyntheticProblem:
+                 saturate_fraction: float = 0.0, ld=None, storage: str = "fp32") -> SyntheticProblem:
+    """storage "bf16": the shard is stored in bf16 and g = A x_true is taken over the stored matrix."""
     k = hip()
     dev = device or torch.device("cuda", torch.cuda.current_device())
-    rtm = DenseRTM.synthetic(npixel_local, nvoxel, row_offset, seed=seed, device=dev, ld=ld)
+    rtm = DenseRTM.synthetic(npixel_local, nvoxel, row_offset, seed=seed, device=dev, ld=ld, storage=storage)
     s = torch.cuda.current_stream(dev).cuda_stream
     x_true = torch.empty(nvoxel, dtype=torch.float64, device=dev)
     k.synth_vector(x_true.data_ptr(), nvoxel, 0, int(seed) + 17, 0.0, 1.0, s)
     xx = torch.zeros(rtm.ld, dtype=torch.float32, device=dev)
     xx[:nvoxel] = x_true.to(torch.float32)
     f = torch.zeros(rtm.nrows_pad, dtype=torch.float32, device=dev)
-    k.forward(0, rtm.A.data_ptr(), rtm.ld, rtm.npixel, rtm.nrows_pad, xx.data_ptr(), 0, 0, f.data_ptr(), 0, 0, 0, s)
+    k.forward(0, rtm.A.data_ptr(), rtm.ld, rtm.npixel, rtm.nrows_pad, xx.data_ptr(), 0, 0, f.data_ptr(), 0, 0, 0, s,
+              rtm.is_bf16)
     g = f[:npixel_local].to(torch.float64)
     if saturate_fraction > 0:
         u = torch.empty(npixel_local, dtype=torch.float64, device=dev)

@@ -43,6 +43,10 @@ for step in "$@"; do
               run rocprof_mf$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mf$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 || exit 1
             done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
+    benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
+               run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
+    benchbf16big) run bench_bf16_512kx256k 900 python bench.py --steps 2 --warmup 1 --rtm-dtype bf16 \
+                    --npix 524288 --nvox 262144 --iters 20 ;;
     benchlap) run bench_lap 600 python bench.py --steps 5 --warmup 1 --laplacian ;;
     probe) run probe 600 python tools/probe.py ;;
     trace) run fused_trace 600 python tools/fused_trace.py ;;
