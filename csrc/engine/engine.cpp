@@ -97,8 +97,10 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
     st_.resize(1);
     xcnt_.resize(16);
     use_fused_ = false;
-    // bf16 storage: two-pass kernels (the fused sweep streams fp32 tiles)
-    if (cfg_.use_fused && !cfg_.column_shard && !cfg_.rtm_bf16 && (double)Pp_ * (double)ld_ * sizeof(float) >= cfg_.fused_min_bytes) {
+    // bf16 storage: the fused sweep exists as variant 6 only (else the two-pass kernels)
+    const double abytes = (double)Pp_ * (double)ld_ * (cfg_.rtm_bf16 ? 2.0 : 4.0);
+    if (cfg_.use_fused && !cfg_.column_shard && abytes >= cfg_.fused_min_bytes &&
+        (!cfg_.rtm_bf16 || cfg_.fused_variant == 6)) {
         geom_ = fused_geometry(ld_, num_cus_, cfg_.fused_variant, cfg_.rows_per_tile);
         use_fused_ = geom_.valid();
     }
@@ -294,9 +296,14 @@ void Engine::sweep() {
     }
     unsigned* xcnt = (use_fused_ && geom_.variant == 6) ? xcnt_.get() : nullptr;  // zeroed by setup / update
     if (use_fused_) {
-        launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, static_cast<const float*>(A_), ld_, P_, Pp_, x_.get(), ghat_.get(),
-                           arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I, geom_.J, st, xcnt_.get(),
-                           stream_);
+        if (cfg_.rtm_bf16)  // variant 6, K = rows per tile
+            launch_fused_sweep_bf16(cfg_.logarithmic, geom_.K, static_cast<const bf16_t*>(A_), ld_, P_, Pp_, x_.get(),
+                                    ghat_.get(), arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I,
+                                    geom_.J, st, xcnt_.get(), stream_);
+        else
+            launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, static_cast<const float*>(A_), ld_, P_, Pp_,
+                               x_.get(), ghat_.get(), arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I,
+                               geom_.J, st, xcnt_.get(), stream_);
         launch_reduce_partials(partial_.get(), ld_, geom_.I, scale, comm_buf_.get(), Fpart_.get(), nF_fused_, Fslot,
                                st, stream_);
     } else {
@@ -429,7 +436,7 @@ bool Engine::fallback() {
     // A persistent sweep gave up waiting (SartState.error): XCD-local groups (variant 6) -> generic
     // groups (variant 3) -> two-pass kernels. The frame is re-solved from scratch.
     drop_graph();
-    if (use_fused_ && geom_.variant == 6) {
+    if (use_fused_ && geom_.variant == 6 && !cfg_.rtm_bf16) {
         const FusedGeometry g3 = fused_geometry(ld_, num_cus_, 3, 0);
         if (g3.valid()) {
             std::fprintf(stderr, "sart: fused sweep variant 6 timed out (unexpected workgroup placement); using variant 3\n");

@@ -59,7 +59,8 @@ struct EngineConfig : SolverParams {
     // Storage precision of the shard: A holds bf16 bit patterns instead of fp32 (half the
     // HBM bytes per sweep, twice the matrix per GPU); products, sums and every vector stay fp32 / fp64. Ray
     // sums are taken over the stored (rounded) values, so the solve is exact SART for the bf16 matrix.
-    // Two-pass kernels (the fused sweep and the multi-frame engine are fp32-only).
+    // Fused sweep variant 6 (bf16 register tiles, fp32 LDS ring) or the two-pass kernels; the multi-frame
+    // engine is fp32-only.
     bool rtm_bf16 = false;
 };
 

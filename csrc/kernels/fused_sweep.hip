@@ -471,9 +471,38 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
 // slower than 2: their stores join the vmcnt queue of their streaming loads.
 // (LDS x slab: T >= 2 only.) Scalar-memory (s_load glc) polls were measured and are no faster under load:
 // an s_load round trip to L2 costs ~1.2 us while the chip streams.
-template <bool LOG, bool XL, bool DIAG, int T, int SCHED>
+// Register tiles of the v4/v6 compute waves by RTM storage type. A lane owns 4 consecutive columns per
+// k-slot in both: one 16-byte fp32 load, or one 8-byte load of 4 bf16 widened to fp32 where the tile is
+// consumed (row dot and LDS park); the LDS ring, the x slab and every sum stay fp32. bf16 tiles take half
+// the VGPRs, so the bf16 kernel keeps more tiles in flight (RS below) for the same bytes in flight.
+template <typename AT>
+struct FusedTile;
+
+template <>
+struct FusedTile<float> {
+    using R = float4;
+    __device__ __forceinline__ static R load(const R* p) { return load_stream(p); }
+    __device__ __forceinline__ static float4 widen(const R v) { return v; }
+};
+
+typedef unsigned sart_u2v __attribute__((ext_vector_type(2)));
+template <>
+struct FusedTile<bf16_t> {
+    using R = uint2;
+    __device__ __forceinline__ static R load(const R* p) {
+#if SART_STREAM_NT
+        const sart_u2v v = __builtin_nontemporal_load(reinterpret_cast<const sart_u2v*>(p));
+        return make_uint2(v.x, v.y);
+#else
+        return *p;
+#endif
+    }
+    __device__ __forceinline__ static float4 widen(const R v) { return bf16x4_to_f4(v.x, v.y); }
+};
+
+template <bool LOG, bool XL, bool DIAG, int T, int SCHED, typename AT = float>
 __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
-    const float* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
+    const AT* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
     const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
     double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg,
     unsigned* __restrict__ xcnt) {
@@ -490,7 +519,12 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
     constexpr int L = 3 + D;     // back-projection lag in steps
     static_assert(L >= PD + PQ, "the weights must be ready one step before they are used");
     constexpr int NL = 4;        // LDS ring slots (32 KB each)
-    constexpr int RS = XS_LDS ? 5 : 4;  // register tile slots per wave (8 KB each): AH in flight + D held
+    // register tile slots per wave (8 KB fp32 / 4 KB bf16 each): AH in flight + D held. bf16: 7 tiles of
+    // 8-byte loads in flight with T = 1, 6 (48 loads) with the LDS x slab (7 would spill)
+    constexpr bool BF = !std::is_same<AT, float>::value;
+    constexpr int RS = XS_LDS ? (BF ? 7 : 5) : (BF ? 7 : 4);
+    using FT = FusedTile<AT>;
+    using RT = typename FT::R;
     constexpr int AH = RS - D;   // tiles in flight per wave
     static_assert(L >= PD + 2, "the weights must be ready one step before they are used");
     constexpr int NS = 8;        // LDS hand-off slots
@@ -551,7 +585,7 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
         const int64_t slab4 = (int64_t)gj * (64 * KW * WPR);                // first float4 of the slab
         const int64_t col4 = slab4 + wsub * (64 * KW) + lane;              // + k * 64
         const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
-        const float4* __restrict__ a4 = reinterpret_cast<const float4*>(A) + col4 + (int64_t)wrow * ld4;
+        const RT* __restrict__ a4 = reinterpret_cast<const RT*>(A) + col4 + (int64_t)wrow * ld4;  // 4 columns each
         float4* ring = s_ring + (wave * KW) * 64 + lane;
         float4 xs[XS_LDS ? 1 : KW], acc[KW];
         const float4* xl = s_xs + wsub * (KW * 64) + lane;
@@ -560,27 +594,27 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
             if constexpr (!XS_LDS) xs[k] = x4[col4 + k * 64];
             acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        float4 fl[RS][KW];
+        RT fl[RS][KW];
         // Tile loads are issued unconditionally, clamped to the last tile of the matrix (past the group's
         // end they re-read valid rows that nobody uses). A guarded load makes the vmcnt bookkeeping depend
         // on the path, and the compiler then waits for EVERY load in flight wherever a tile is consumed,
         // which collapses the AH-tile pipeline to one tile.
         const int64_t tlast = ntiles - 1 - t_begin;
-        auto load_tile = [&](float4(&dst)[KW], int64_t t) {
+        auto load_tile = [&](RT(&dst)[KW], int64_t t) {
             const int64_t tc = t < tlast ? t : tlast;
-            const float4* src = a4 + (t_begin + tc) * T * ld4;
+            const RT* src = a4 + (t_begin + tc) * T * ld4;
 #pragma unroll
-            for (int k = 0; k < KW; ++k) dst[k] = load_stream(src + k * 64);
+            for (int k = 0; k < KW; ++k) dst[k] = FT::load(src + k * 64);
         };
 #pragma unroll
         for (int i = 0; i < AH; ++i) load_tile(fl[i], i);
         bool stuck = false;
         unsigned long long stall = 0, nstall = 0;
 
-        auto park = [&](float4(&src)[KW], int64_t t) {
+        auto park = [&](RT(&src)[KW], int64_t t) {
             float4* slot = ring + (int)(t % NL) * (4 * KW * 64);
 #pragma unroll
-            for (int k = 0; k < KW; ++k) slot[k * 64] = src[k];
+            for (int k = 0; k < KW; ++k) slot[k * 64] = FT::widen(src[k]);
         };
         auto step = [&](auto bbc, int64_t t) {
             constexpr int bb = decltype(bbc)::value;        // register slot of tile t (t % RS)
@@ -590,9 +624,9 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
 #pragma unroll
                 for (int k = 0; k < KW; ++k) {
                     if constexpr (XS_LDS)
-                        s += dot4(fl[bb][k], xl[k * 64]);
+                        s += dot4(FT::widen(fl[bb][k]), xl[k * 64]);
                     else
-                        s += dot4(fl[bb][k], xs[k]);
+                        s += dot4(FT::widen(fl[bb][k]), xs[k]);
                 }
                 s = wave_sum(s);
                 if (lane == 0) {
@@ -1082,17 +1116,17 @@ static void launch_lds(bool logmode, dim3 grid, hipStream_t stream, const float*
                            nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
 }
 
-template <bool LG, bool X, bool D, int T, int SC>
-static void launch_rows_t(dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
+template <bool LG, bool X, bool D, int T, int SC, typename AT = float>
+static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                           const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                           uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
     static bool configured = false;
     if (!configured) {
-        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T, SC>),
+        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T, SC, AT>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds_bytes(T, SC)), "hipFuncSetAttribute");
         configured = true;
     }
-    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC>), grid, dim3(SC == 4 ? kFusedThreads + 64 : kFusedThreads),
+    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC, AT>), grid, dim3(SC == 4 ? kFusedThreads + 64 : kFusedThreads),
                        rows_lds_bytes(T, SC), stream, A, ld, nrows,
                        nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt);
 }
@@ -1239,6 +1273,32 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
             break;
     }
     check_launch("k_fused_sweep");
+}
+
+// bf16-stored RTM: variant 6 only (XCD-local row groups, same geometry and exchange as fp32), schedule 4
+// for T >= 2 and 0 for T = 1. A protocol timeout falls back to the bf16 two-pass kernels.
+void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
+                             const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
+                             uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream) {
+    if (T != 1 && T != 2 && T != 4) throw std::runtime_error("fused_sweep bf16: rows per tile must be 1, 2 or 4");
+    if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep bf16: padded rows must be a multiple of 4");
+    if (ld % (8192 / T) != 0 || ld / (8192 / T) != J) throw std::runtime_error("fused_sweep bf16: ld must equal J * slab");
+    if (J * 4 > kMaxGather || J * T > kRowsGather) throw std::runtime_error("fused_sweep bf16: too many slabs");
+    if (xcnt == nullptr || I % 8 != 0) throw std::runtime_error("fused_sweep bf16: needs ticket counters and I % 8 == 0");
+    const dim3 grid((unsigned)(I * J));
+    auto go = [&](auto lg, auto tt, auto sc) {
+        launch_rows_t<decltype(lg)::value, true, false, decltype(tt)::value, decltype(sc)::value, bf16_t>(
+            grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S4 = std::integral_constant<int, 4>;
+    auto by_t = [&](auto lg) {
+        if (T == 1) go(lg, std::integral_constant<int, 1>{}, S0{});
+        else if (T == 2) go(lg, std::integral_constant<int, 2>{}, S4{});
+        else go(lg, std::integral_constant<int, 4>{}, S4{});
+    };
+    if (logmode) by_t(std::true_type{}); else by_t(std::false_type{});
+    check_launch("k_fused_sweep_rows<bf16>");
 }
 
 }  // namespace sart
