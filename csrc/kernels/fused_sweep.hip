@@ -514,14 +514,21 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
     static_assert(!XS_LDS || T >= 2, "the LDS holds the x slab only for T >= 2");
     constexpr bool SPLIT = SCHED == 4;  // wave 4 publishes granules, wave 5 gathers (no shared vmcnt queue)
     constexpr int NTHR = SPLIT ? kFusedThreads + 64 : kFusedThreads;
-    constexpr int PD = (SCHED == 2 || SCHED == 4) ? 2 : 1;   // exchange step u polls tile u - PD
-    constexpr int PQ = SCHED == 1 ? 3 : 2;   // polls in flight (finishes tile u - PD - PQ + 1)
-    constexpr int L = 3 + D;     // back-projection lag in steps
-    static_assert(L >= PD + PQ, "the weights must be ready one step before they are used");
-    constexpr int NL = 4;        // LDS ring slots (32 KB each)
-    // register tile slots per wave (8 KB fp32 / 4 KB bf16 each): AH in flight + D held. bf16: 7 tiles of
-    // 8-byte loads in flight with T = 1, 6 (48 loads) with the LDS x slab (7 would spill)
     constexpr bool BF = !std::is_same<AT, float>::value;
+    // bf16 tiles are parked raw in the LDS ring (16 KB per slot), so 8 slots fit in the 128 KB of the fp32
+    // ring. With T = 1 (schedule 0) the bf16 sweep keeps 4 polls in flight and lags the back-projection by
+    // L = PD + PQ = 5 steps: 12.5 -> 13.2 it/s at 512k x 256k; with T = 4 (schedule 4) the deeper lag
+    // measured 3 % slower than the fp32 lag (458 vs 473 it/s at 64k x 64k), so it is kept there.
+    constexpr bool DEEP = BF && SCHED == 0;
+    constexpr int PD = (SCHED == 2 || SCHED == 4) ? 2 : 1;   // exchange step u polls tile u - PD
+    constexpr int PQ = DEEP ? 4 : (SCHED == 1 ? 3 : 2);      // polls in flight (finishes tile u - PD - PQ + 1)
+    constexpr int L = DEEP ? PD + PQ : 3 + D;                // back-projection lag in steps
+    static_assert(L >= PD + PQ, "the weights must be ready one step before they are used");
+    constexpr int NL = BF ? 8 : 4;  // LDS ring slots (32 KB fp32 / 16 KB bf16 each)
+    static_assert(L <= NL + D - 1, "a parked tile must be back-projected before its ring slot is reused");
+    // register tile slots per wave (8 KB fp32 / 4 KB bf16 each): AH in flight + D held. bf16: 6-7 tiles of
+    // 8-byte loads in flight (<= 56 loads, inside the 6-bit vmcnt range); 8 slots with the x slab in LDS
+    // measured no faster at 64k x 64k
     constexpr int RS = XS_LDS ? (BF ? 7 : 5) : (BF ? 7 : 4);
     using FT = FusedTile<AT>;
     using RT = typename FT::R;
@@ -529,8 +536,8 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
     static_assert(L >= PD + 2, "the weights must be ready one step before they are used");
     constexpr int NS = 8;        // LDS hand-off slots
 
-    extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64]
-    float4* s_xs = s_ring + NL * 4 * KW * 64;                         // [WPR][KW][64] if XS_LDS
+    extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64] of RT (128 KB)
+    float4* s_xs = s_ring + NL * 4 * KW * 64 * sizeof(RT) / sizeof(float4);  // [WPR][KW][64] if XS_LDS
     float* s_small = reinterpret_cast<float*>(s_xs + (XS_LDS ? WPR * KW * 64 : 0));
     // Hand-off words: volatile through explicit LDS (address_space(3)) pointers. Through generic pointers
     // the compiler keeps volatile accesses as FLAT instructions, which count on vmcnt too, so every flag
@@ -586,7 +593,7 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
         const int64_t col4 = slab4 + wsub * (64 * KW) + lane;              // + k * 64
         const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
         const RT* __restrict__ a4 = reinterpret_cast<const RT*>(A) + col4 + (int64_t)wrow * ld4;  // 4 columns each
-        float4* ring = s_ring + (wave * KW) * 64 + lane;
+        RT* ring = reinterpret_cast<RT*>(s_ring) + (wave * KW) * 64 + lane;  // tiles parked in storage type
         float4 xs[XS_LDS ? 1 : KW], acc[KW];
         const float4* xl = s_xs + wsub * (KW * 64) + lane;
 #pragma unroll
@@ -612,9 +619,9 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
         unsigned long long stall = 0, nstall = 0;
 
         auto park = [&](RT(&src)[KW], int64_t t) {
-            float4* slot = ring + (int)(t % NL) * (4 * KW * 64);
+            RT* slot = ring + (int)(t % NL) * (4 * KW * 64);
 #pragma unroll
-            for (int k = 0; k < KW; ++k) slot[k * 64] = FT::widen(src[k]);
+            for (int k = 0; k < KW; ++k) slot[k * 64] = src[k];
         };
         auto step = [&](auto bbc, int64_t t) {
             constexpr int bb = decltype(bbc)::value;        // register slot of tile t (t % RS)
@@ -658,9 +665,9 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
                 }
                 asm volatile("" ::: "memory");
                 const float wr = s_w[ws * 4 + wrow];
-                const float4* slot = ring + (int)(u % NL) * (4 * KW * 64);
+                const RT* slot = ring + (int)(u % NL) * (4 * KW * 64);
 #pragma unroll
-                for (int k = 0; k < KW; ++k) fma4(acc[k], slot[k * 64], wr);
+                for (int k = 0; k < KW; ++k) fma4(acc[k], FT::widen(slot[k * 64]), wr);
             }
         };
         const unsigned long long tstart = DIAG ? __builtin_amdgcn_s_memtime() : 0;
