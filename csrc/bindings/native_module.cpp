@@ -71,6 +71,7 @@ PYBIND11_MODULE(_sart_native, m) {
         .def_readwrite("batch_frames", &Config::batch_frames)
         .def_readwrite("two_pass", &Config::two_pass)
         .def_readwrite("partition_voxels", &Config::partition_voxels)
+        .def_readwrite("rtm_bf16", &Config::rtm_bf16)
         .def_readwrite("profile_file", &Config::profile_file)
         .def_readwrite("help", &Config::help);
     m.def("parse_arguments", &parse_arguments, py::arg("argv"));

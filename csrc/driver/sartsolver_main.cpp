@@ -39,6 +39,7 @@
 #include "../engine/engine.hpp"
 #include "../engine/geometry.hpp"
 #include "../engine/multiframe.hpp"
+#include "../kernels/launchers.hpp"
 #include "../native/config.hpp"
 #include "../native/cpu_solver.hpp"
 #include "../native/frames.hpp"
@@ -61,9 +62,11 @@ bool file_exists(const std::string& p) {
 }
 
 // Device-resident row shard [nrows_pad x ld] filled by streaming HDF5 row blocks through two pinned
-// buffers: block k+1 is read on a helper thread while block k is copied host -> HBM.
+// buffers: block k+1 is read on a helper thread while block k is copied host -> HBM. bf16 (--rtm_bf16):
+// each block lands in an fp32 staging buffer in HBM and is rounded into the bf16 shard on the device.
 struct DeviceShard {
-    float* A = nullptr;
+    void* A = nullptr;  // fp32, or bf16 bit patterns when bf16
+    bool bf16 = false;
     int64_t nrows = 0, nrows_pad = 0, nvoxel = 0, ld = 0;
     ~DeviceShard() {
         if (A) (void)hipFree(A);
@@ -72,21 +75,25 @@ struct DeviceShard {
 
 // col0 / ncols: keep only that voxel block of every row (--partition_voxels; the rows are read whole).
 std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0, uint64_t nrows, size_t block_bytes,
-                                               uint64_t col0 = 0, uint64_t ncols = 0) {
+                                               uint64_t col0 = 0, uint64_t ncols = 0, bool bf16 = false) {
     auto sh = std::make_unique<DeviceShard>();
+    sh->bf16 = bf16;
     if (ncols == 0) ncols = in.nvoxel - col0;
     sh->nrows = (int64_t)nrows;
     sh->nvoxel = (int64_t)ncols;
     sh->ld = choose_ld(sh->nvoxel);
     sh->nrows_pad = (sh->nrows + 63) / 64 * 64;
-    const size_t bytes = (size_t)sh->nrows_pad * sh->ld * sizeof(float);
-    hip_ok(hipMalloc(reinterpret_cast<void**>(&sh->A), bytes), "hipMalloc(RTM shard)");
+    const size_t bytes = (size_t)sh->nrows_pad * sh->ld * (bf16 ? sizeof(bf16_t) : sizeof(float));
+    hip_ok(hipMalloc(&sh->A, bytes), "hipMalloc(RTM shard)");
     hip_ok(hipMemset(sh->A, 0, bytes), "hipMemset(RTM shard)");
     hip_ok(hipDeviceSynchronize(), "hipMemset sync");
     const uint64_t V = in.nvoxel;
     const uint64_t rows_per_block = std::max<uint64_t>(1, std::min<uint64_t>(nrows, block_bytes / (4 * V)));
     float* buf[2] = {nullptr, nullptr};
     for (auto& b : buf) hip_ok(hipHostMalloc(reinterpret_cast<void**>(&b), rows_per_block * V * sizeof(float)), "hipHostMalloc");
+    // bf16: fp32 staging rows [rows_per_block x ld], padding columns zero (the 2-D copies write ncols only)
+    DeviceArray<float> stage;
+    if (bf16) stage.resize(rows_per_block * (size_t)sh->ld);
     hipStream_t s;
     hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
     hipEvent_t ev[2];
@@ -109,9 +116,12 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
                 next = std::async(std::launch::async, read_into, buf[nb], blocks[k + 1].first, blocks[k + 1].second);
             }
             const uint64_t r0 = blocks[k].first, nr = blocks[k].second - blocks[k].first;
-            hip_ok(hipMemcpy2DAsync(sh->A + r0 * sh->ld, sh->ld * sizeof(float), cur + col0, V * sizeof(float),
+            float* dst = bf16 ? stage.get() : static_cast<float*>(sh->A) + r0 * sh->ld;
+            hip_ok(hipMemcpy2DAsync(dst, sh->ld * sizeof(float), cur + col0, V * sizeof(float),
                                     ncols * sizeof(float), nr, hipMemcpyHostToDevice, s),
                    "H2D RTM block");
+            if (bf16)  // stream-ordered: the next block's copy into the staging rows waits for this conversion
+                launch_f32_to_bf16(stage.get(), (int64_t)nr * sh->ld, static_cast<bf16_t*>(sh->A) + r0 * sh->ld, s);
             hip_ok(hipEventRecord(ev[k % 2], s), "event");
             ev_used[k % 2] = true;
             if (next.valid()) next.get();
@@ -210,7 +220,8 @@ int main(int argc, char** argv) {
         std::vector<float> hshard;
         auto load = [&]() {
             if (gpu)
-                dshard = load_device_shard(in, blk.offset, blk.size, (size_t)256 << 20, vblk.offset, vblk.size);
+                dshard = load_device_shard(in, blk.offset, blk.size, (size_t)256 << 20, vblk.offset, vblk.size,
+                                           cfg.rtm_bf16);
             else {
                 hshard.assign(blk.size * in.nvoxel, 0.f);
                 read_rtm_rows(in.rtm_files, in.rtm_name, in.nvoxel, blk.offset, blk.offset + blk.size, hshard.data(),
@@ -234,8 +245,8 @@ int main(int argc, char** argv) {
             EngineConfig ec;
             static_cast<SolverParams&>(ec) = params;
             ec.mf_frames = cfg.batch_frames;  // batch width 16, 32 or 64 (rounded up, capped at 64)
-            mf = std::make_unique<MultiFrameEngine>(device, dshard->A, dshard->nrows, dshard->nrows_pad,
-                                                    dshard->nvoxel, dshard->ld, dcomm.get(), ec);
+            mf = std::make_unique<MultiFrameEngine>(device, static_cast<const float*>(dshard->A), dshard->nrows,
+                                                    dshard->nrows_pad, dshard->nvoxel, dshard->ld, dcomm.get(), ec);
             if (lap.nnz()) mf->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
         } else if (gpu) {
             EngineConfig ec;
@@ -244,6 +255,7 @@ int main(int argc, char** argv) {
             ec.fused_min_bytes = fused_min_bytes_from_env();
             if (const char* v = std::getenv("SART_FUSED_VARIANT"); v && *v) ec.fused_variant = std::atoi(v);
             ec.time_collectives = !cfg.profile_file.empty();  // --profile: GPU time in the all-reduces per frame
+            ec.rtm_bf16 = dshard->bf16;
             if (cols) {
                 ec.column_shard = true;
                 ec.col_offset = (int64_t)vblk.offset;

@@ -82,6 +82,8 @@ std::string usage() {
            "  --two_pass                  Use the two-pass projection kernels instead of the fused sweep.\n"
            "  --partition_voxels          Shard the RTM by voxel columns (every GPU holds all pixels of a voxel\n"
            "                              block; all-reduce of A x per iteration) instead of by pixel rows.\n"
+           "  --rtm_bf16                  Store the RTM in bf16 on the GPU (half the memory and bytes per sweep;\n"
+           "                              products and sums stay fp32).\n"
            "  --profile FILE              Write per-frame timing/iteration telemetry as JSON lines.\n";
 }
 
@@ -108,7 +110,7 @@ Config parse_arguments(const std::vector<std::string>& argv) {
     std::map<std::string, bool*> flags = {
         {"--logarithmic", &c.logarithmic}, {"--no_guess", &c.no_guess},   {"--use_cpu", &c.use_cpu},
         {"--parallel_read", &c.parallel_read}, {"--resume", &c.resume}, {"--two_pass", &c.two_pass},
-        {"--partition_voxels", &c.partition_voxels},
+        {"--partition_voxels", &c.partition_voxels}, {"--rtm_bf16", &c.rtm_bf16},
     };
     const std::map<std::string, std::string> alias = {
         {"-o", "--output_file"},           {"-t", "--time_range"},          {"-w", "--wavelength_threshold"},
@@ -167,6 +169,8 @@ Config parse_arguments(const std::vector<std::string>& argv) {
     if (c.batch_frames < 1) throw Error("Argument batch_frames must be >= 1.");
     if (c.partition_voxels && (c.batch_frames > 1 || c.use_cpu))
         throw Error("Argument partition_voxels applies to the single-frame GPU solver only.");
+    if (c.rtm_bf16 && (c.batch_frames > 1 || c.use_cpu))
+        throw Error("Argument rtm_bf16 applies to the single-frame GPU solver only.");
     if (c.input_files.size() < 2)
         throw Error("At least two input file, one with RTM and one with image, are required, " +
                     std::to_string(c.input_files.size()) + " given.");

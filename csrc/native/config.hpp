@@ -35,7 +35,8 @@ struct Config {
     bool resume = false;        // append to an existing output file, skip frames already solved
     int batch_frames = 1;       // >1: solve independent frames together (MFMA multi-frame path, implies --no_guess)
     bool two_pass = false;      // disable the fused single-pass sweep
-    bool partition_voxels = false;  // GPU: shard the RTM by voxel columns (all pixels per rank) instead of pixel rows
+    bool partition_voxels = false;
+    bool rtm_bf16 = false;      // GPU: store the RTM shard in bf16 (fp32 products and sums)  // GPU: shard the RTM by voxel columns (all pixels per rank) instead of pixel rows
     std::string profile_file;   // JSON timing/telemetry sidecar
     bool help = false;
 };

@@ -11,7 +11,8 @@ Same CLI, input validation, frame loop, output file and console output as the re
 * fatal errors tear the process group down instead of leaving peers blocked in a collective.
 
 Extensions: ``--resume``, ``--batch_frames N`` (multi-frame MFMA solver), ``--two_pass``,
-``--partition_voxels`` (voxel-column shards), ``--profile FILE`` (JSON lines per frame).
+``--partition_voxels`` (voxel-column shards), ``--rtm_bf16`` (bf16-stored RTM), ``--profile FILE`` (JSON lines
+per frame).
 """
 from __future__ import annotations
 
@@ -97,7 +98,9 @@ def run(cfg, intervals) -> int:
                 return hdf5.load_rtm_shard(inputs, 0, inputs.npixel, device, col_offset=vblock.offset,
                                            ncols=vblock.size)
             if use_gpu:
-                return hdf5.load_rtm_shard(inputs, block.offset, block.size, device)
+                rtm = hdf5.load_rtm_shard(inputs, block.offset, block.size, device)
+                # --rtm_bf16: bf16-stored shard (native RNE rounding; the fp32 copy is released)
+                return rtm.to_bf16() if getattr(cfg, "rtm_bf16", False) else rtm
             return hdf5.read_rtm_rows(inputs, block.offset, block.stop)
 
         if cfg.parallel_read or world == 1:

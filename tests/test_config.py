@@ -33,6 +33,8 @@ def test_short_and_long_aliases(n):
     assert c.max_cached_frames == 3 and c.max_cached_solutions == 4 and c.input_files == ["f1", "f2", "f3"]
     c2 = n.parse_arguments(["--output_file=y.h5", "--relaxation=1", "--batch_frames", "16", "--resume", "a", "b"])
     assert c2.output_file == "y.h5" and c2.batch_frames == 16 and c2.resume
+    assert not c2.rtm_bf16 and n.parse_arguments(["--rtm_bf16", "a", "b"]).rtm_bf16
+    assert "--rtm_bf16" in n.usage()
 
 
 @pytest.mark.parametrize("argv,msg", [
@@ -49,6 +51,8 @@ def test_short_and_long_aliases(n):
     (["-m", "abc", "a", "b"], "Failed to parse"),
     (["--bogus", "a", "b"], "Unknown argument"),
     (["-m"], "Too few arguments"),
+    (["--rtm_bf16", "--use_cpu", "a", "b"], "rtm_bf16 applies to the single-frame GPU solver"),
+    (["--rtm_bf16", "--batch_frames", "16", "a", "b"], "rtm_bf16 applies to the single-frame GPU solver"),
 ])
 def test_validation_errors(n, argv, msg):
     with pytest.raises(RuntimeError, match=msg.replace("(", r"\(").replace(")", r"\)").replace("]", r"\]")):

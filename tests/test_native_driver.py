@@ -237,6 +237,38 @@ def test_partition_voxels_cli(tmp_path, binary, log):
         assert np.linalg.norm(x - x0) / np.linalg.norm(x0) < 2e-3, name
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("log", [False, True])
+@pytest.mark.parametrize("two_pass", [False, True])
+def test_rtm_bf16_cli(tmp_path, binary, log, two_pass):
+    """--rtm_bf16: the native driver (HDF5 blocks rounded into a bf16 shard on the device) and the Python
+    driver (DenseRTM.to_bf16) run the same engine bit for bit, and match the fp64 oracle of the reference GPU
+    semantics on the bf16-rounded matrix."""
+    import torch
+
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+
+    case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_b",), laplacian=False, nframes=2, saturate=0.05,
+                     nvoxel=2048, grid=(16, 16, 8), shapes=((24, 32), (20, 30)))
+    base = ["-m", "40", "-c", "1e-9", "--rtm_bf16"] + (["-L"] if log else []) + (["--two_pass"] if two_pass else [])
+    r1 = _run_native(binary, base + ["-o", str(tmp_path / "n.h5"), *case.files])
+    assert r1.returncode == 0, r1.stdout + r1.stderr
+    r2 = _run_python(base + ["-o", str(tmp_path / "p.h5"), *case.files])
+    assert r2.returncode == 0, r2.stdout + r2.stderr
+    n = native()
+    t1, x1, s1 = n.read_solution_file(str(tmp_path / "n.h5"))
+    t2, x2, s2 = n.read_solution_file(str(tmp_path / "p.h5"))
+    np.testing.assert_array_equal(s1, s2)
+    np.testing.assert_array_equal(x1, x2)
+    Ar = torch.from_numpy(np.ascontiguousarray(case.A, dtype=np.float32)).to(torch.bfloat16).float().numpy()
+    prev = None
+    for k in range(2):
+        g = np.concatenate([case.frames[c][k].ravel()[case.masks[c].ravel() > 0] for c in sorted(case.masks)])
+        prev, _, _ = sart_gpu_semantics(Ar, g, None, logarithmic=log, max_iterations=40, conv_tolerance=1e-9,
+                                        x_prev=prev)
+    assert np.linalg.norm(x1 - prev) / np.linalg.norm(prev) < 1.5e-2
+
+
 def test_partition_voxels_rejects_cpu_and_batches(tmp_path, binary):
     case = _case(tmp_path, nframes=1)
     r = _run_native(binary, ["--use_cpu", "--partition_voxels", *case.files])
