@@ -60,6 +60,8 @@ for step in "$@"; do
                    --out "$OUT/comm_check_p2p_n$n.json" || exit 1
                done ;;
     testsel) run pytest_sel 900 python -m pytest ${SEL:-tests} -m gpu -q -p no:cacheprovider ;;
+    profbf16) run rocprof_bf16 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bf16" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --rtm-dtype bf16 &&
+              run rocprof_bf16_pmc 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof_bf16_pmc" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --rtm-dtype bf16 ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
