@@ -138,9 +138,19 @@ def main() -> int:
 
         runner = _Batch(solver)
     else:
+        # The fused sweep is a persistent kernel sized to fill the whole device and relies on all its
+        # workgroups being co-resident. Several ranks sharing one GPU (a one-GPU rehearsal of an N-rank
+        # run) launch such grids concurrently and can starve each other's hand-off spins, so a shared
+        # device runs the two-pass kernels. One rank per GPU (the production layout) keeps the fused sweep.
+        local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+        shared_device = local_ranks > torch.cuda.device_count()
+        if shared_device and not args.no_fused and comm.rank == 0:
+            print(f"note: {local_ranks} ranks share {torch.cuda.device_count()} GPU(s); using the two-pass "
+                  "kernels (the fused sweep needs a device to itself)", file=sys.stderr)
         # time_collectives (N > 1): timing events around each per-iteration all-reduce (GPU-side only)
         solver = SARTSolver(prob.rtm, lap, comm, params, logarithmic=args.variant == "log",
-                            use_fused=not args.no_fused, check_interval=32, allow_zero_tolerance=True,
+                            use_fused=not (args.no_fused or shared_device), check_interval=32,
+                            allow_zero_tolerance=True,
                             partition=args.partition, time_collectives=n > 1)
         g = prob.measurement
         runner = solver
