@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Headline benchmark: SART iterations/s and GFLOPS on a dense synthetic RTM (BASELINE.json).
 
-    python bench.py [--gpus N --steps K --warmup W]           # N == 1
+    python bench.py [--gpus N --steps K --warmup W]           # N ranks (self-launched when N > 1)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 One *step* = one frame solve with a cold start and exactly ``--iters`` SART iterations (100 by
@@ -10,6 +10,14 @@ every GPU holds a ``--npix x --nvox`` fp32 row shard (default 65536 x 65536 = 17
 is (65536*N) x 65536 at N GPUs. ``value`` is the whole-job GFLOPS with the repo convention of
 4*P*V flop per SART iteration; ``iters_per_s`` is the node-wide iteration rate.
 The timed region contains the complete solves (setup, every iteration, solution download).
+
+Launching: ``--gpus N`` with N > 1 and no launcher environment (WORLD_SIZE / MPI rank variables) starts
+``torch.distributed.run --nproc-per-node N`` as a child process before any GPU call and passes its JSON
+line and exit code through, like the reference's ``mpirun -np N`` (reference main.cpp:63-68). Under a
+launcher, a world size different from ``--gpus`` is an error (exit 1). A per-rank watchdog exits non-zero
+when a stage (setup, self-check, warmup, timed steps) makes no progress for ``--watchdog`` seconds.
+Before timing, a 3-iteration self-check compares the fused sweep and the two-pass kernels on the same shard
+with the device fp64 oracle (``selfcheck`` in the JSON line).
 """
 from __future__ import annotations
 
@@ -49,9 +57,71 @@ def grid_dims(n: int) -> tuple[int, int, int]:
     return best
 
 
+LAUNCHER_VARS = ("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE")
+
+
+def launched_world() -> int | None:
+    """World size set by a launcher (torchrun, mpirun), None when this process was started directly."""
+    for v in LAUNCHER_VARS:
+        if os.environ.get(v):
+            return int(os.environ[v])
+    return None
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n: int, argv: list[str], env_extra: dict) -> int:
+    """Start N ranks of this script under torch.distributed.run (one rank per GPU) and return their exit
+    code; rank 0's JSON line reaches our stdout unchanged. No GPU call happens in this process."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **env_extra)
+    return subprocess.run(cmd, env=env).returncode
+
+
+class Watchdog:
+    """Per-rank progress watchdog: exits the process (code 3) when no stage completes for `limit` seconds,
+    so a hang (e.g. in a collective or a communicator self-test) cannot hold the GPUs until an outer timeout."""
+
+    def __init__(self, limit: float, rank: int):
+        import threading
+
+        self.limit, self.rank = float(limit), rank
+        self.stage, self.t = "start", time.monotonic()
+        if self.limit > 0:
+            threading.Thread(target=self._run, daemon=True).start()
+
+    def kick(self, stage: str) -> None:
+        self.stage, self.t = stage, time.monotonic()
+
+    def _run(self) -> None:
+        while True:
+            time.sleep(min(5.0, self.limit / 4))
+            if time.monotonic() - self.t > self.limit:
+                print(f"bench watchdog: rank {self.rank} made no progress for {self.limit:.0f} s in stage "
+                      f"'{self.stage}'; exiting", file=sys.stderr, flush=True)
+                os._exit(3)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); > 1 self-launches under torchrun")
+    ap.add_argument("--share-gpus", action="store_true",
+                    help="rehearsal: allow more ranks than visible GPUs (ranks share devices, gloo host "
+                         "collectives, two-pass kernels)")
+    ap.add_argument("--watchdog", type=float, default=600.0,
+                    help="seconds without progress after which a rank exits non-zero (0: off)")
+    ap.add_argument("--no-selfcheck", action="store_true", help="skip the untimed fused-vs-two-pass check")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launch and rendezvous only (no GPU work): prints the JSON line with value null")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--npix", type=int, default=65536, help="pixel rows per GPU (weak scaling)")
@@ -82,17 +152,49 @@ def main() -> int:
     if args.partition == "cols" and args.frames > 1:
         ap.error("--partition cols solves single frames (the multi-frame engine uses row shards)")
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    world = launched_world()
+    if world is None and args.gpus > 1:
+        env_extra = {}
+        if not args.launch_check:
+            import torch  # device_count() does not initialise the GPU
+
+            ndev = torch.cuda.device_count()
+            if ndev < args.gpus and not args.share_gpus:
+                print(f"bench: --gpus {args.gpus} but only {ndev} GPU(s) visible (--share-gpus to rehearse "
+                      "on fewer devices)", file=sys.stderr)
+                return 1
+            if ndev < args.gpus:
+                env_extra["SART_DIST_BACKEND"] = "gloo"  # RCCL refuses two ranks on one device
+        return self_launch(args.gpus, sys.argv[1:], env_extra)
+    if (world or 1) != args.gpus:
+        print(f"bench: --gpus {args.gpus} but the launcher started {world or 1} rank(s)", file=sys.stderr)
+        return 1
+
     import torch
 
-    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
     from mpi_cuda_sartsolver_amd.parallel.comm import init_distributed
+
+    if args.launch_check:  # CPU rehearsal of the launch path: rendezvous, barrier, max-reduction, JSON line
+        comm = init_distributed(use_gpu=False)
+        wd = Watchdog(args.watchdog, comm.rank)
+        comm.barrier()
+        wd.kick("barrier")
+        t = comm.all_reduce_scalar(float(comm.rank), op="max")
+        if comm.rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "GFLOPS", "n_gpus": comm.world_size,
+                              "steps": args.steps, "warmup": args.warmup, "launch_check": True,
+                              "max_rank": int(t)}), flush=True)
+        return 0
+
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
     from mpi_cuda_sartsolver_amd.parallel.partition import row_partition
     from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
 
     comm = init_distributed(use_gpu=True)
     n = comm.world_size
-    if n != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {n}; using {n}", file=sys.stderr)
+    wd = Watchdog(args.watchdog, comm.rank)
     dev = torch.device("cuda", torch.cuda.current_device())
 
     cols = args.partition == "cols"
@@ -138,26 +240,46 @@ def main() -> int:
 
         runner = _Batch(solver)
     else:
-        # The fused sweep is a persistent kernel sized to fill the whole device and relies on all its
-        # workgroups being co-resident. Several ranks sharing one GPU (a one-GPU rehearsal of an N-rank
-        # run) launch such grids concurrently and can starve each other's hand-off spins, so a shared
-        # device runs the two-pass kernels. One rank per GPU (the production layout) keeps the fused sweep.
-        local_ranks = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
-        shared_device = local_ranks > torch.cuda.device_count()
-        if shared_device and not args.no_fused and comm.rank == 0:
-            print(f"note: {local_ranks} ranks share {torch.cuda.device_count()} GPU(s); using the two-pass "
-                  "kernels (the fused sweep needs a device to itself)", file=sys.stderr)
+        # The engine itself decides whether ranks share a GPU (PCI bus id on every rank) and then runs the
+        # two-pass kernels: the fused sweep is a persistent grid that needs its device to itself.
         # time_collectives (N > 1): timing events around each per-iteration all-reduce (GPU-side only)
         solver = SARTSolver(prob.rtm, lap, comm, params, logarithmic=args.variant == "log",
-                            use_fused=not (args.no_fused or shared_device), check_interval=32,
-                            allow_zero_tolerance=True,
+                            use_fused=not args.no_fused, check_interval=32, allow_zero_tolerance=True,
                             partition=args.partition, time_collectives=n > 1)
         g = prob.measurement
         runner = solver
     multi = args.frames > 1
+    wd.kick("setup")
 
-    for _ in range(args.warmup):
+    selfcheck = None
+    if not multi and solver.use_fused and not args.no_selfcheck:
+        # Untimed: 3 iterations of the fused sweep and of the two-pass kernels on this very shard and grid,
+        # both against the device fp64 oracle (models/oracle.py, all ranks). fp32 evaluations of SART drift
+        # from fp64 by ~1e-3 on dense random matrices (tests/test_gpu_solver.py), so the fused sweep must be
+        # no further from the oracle than 1.25x the two-pass kernels (validated against the host oracle).
+        import numpy as np
+
+        from mpi_cuda_sartsolver_amd.models.oracle import sart_oracle_f64
+
+        p3 = SolverParams(max_iterations=3, conv_tolerance=0.0)
+        kw = dict(logarithmic=args.variant == "log", allow_zero_tolerance=True, partition=args.partition)
+        gh = g.cpu().numpy() if hasattr(g, "cpu") else np.asarray(g)
+        xf = SARTSolver(prob.rtm, None, comm, p3, use_fused=True, **kw).solve(gh).solution
+        x2 = SARTSolver(prob.rtm, None, comm, p3, use_fused=False, **kw).solve(gh).solution
+        x64 = sart_oracle_f64(prob.rtm, gh, 3, logarithmic=args.variant == "log", comm=comm)
+        nrm = max(float(np.linalg.norm(x64)), 1e-300)
+        ef = comm.all_reduce_scalar(float(np.linalg.norm(xf - x64)) / nrm, op="max")
+        e2 = comm.all_reduce_scalar(float(np.linalg.norm(x2 - x64)) / nrm, op="max")
+        selfcheck = {"iterations": 3, "rel_fused_vs_f64": ef, "rel_two_pass_vs_f64": e2}
+        torch.cuda.empty_cache()
+        if not ef <= 1.25 * e2 + 1e-6:
+            print(f"bench: fused sweep self-check failed: {selfcheck}", file=sys.stderr, flush=True)
+            return 2
+        wd.kick("selfcheck")
+
+    for i in range(args.warmup):
         runner.solve(g)
+        wd.kick(f"warmup {i}")
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
@@ -165,10 +287,11 @@ def main() -> int:
     iters = 0
     comm_ms = 0.0
     res = None
-    for _ in range(args.steps):
+    for i in range(args.steps):
         res = runner.solve(g)
         iters += res.iterations
         comm_ms += max(getattr(res, "comm_ms", -1.0), 0.0)
+        wd.kick(f"step {i}")
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
@@ -201,6 +324,10 @@ def main() -> int:
         "fused_variant": solver.geom.variant if use_fused else None,
         "fused_rows_per_tile": solver.geom.T if use_fused else None,
         "fused_schedule": solver.k.fused_get_schedule() if use_fused else None,
+        "fused_grid": ({"J": solver.geom.J, "I": solver.geom.I, "workgroups": solver.geom.grid,
+                        "ld": solver.ld} if use_fused else None),
+        "selfcheck": selfcheck,
+        "shared_gpus": bool(getattr(solver, "shared_device", False)) if not multi else None,
         "frames_per_step": args.frames,
         # per-iteration device all-reduce: RCCL, or the one-shot P2P kernel when it beat RCCL at start-up
         "allreduce": (solver.native_comm.describe if n > 1 else "none (1 rank)"),

@@ -152,7 +152,8 @@ static void bind_engine(py::module_& m) {
         .def_readwrite("use_graph", &sart::EngineConfig::use_graph)
         .def_readwrite("time_collectives", &sart::EngineConfig::time_collectives)
         .def_readwrite("rtm_bf16", &sart::EngineConfig::rtm_bf16)
-        .def_readwrite("fault_inject", &sart::EngineConfig::fault_inject);
+        .def_readwrite("fault_inject", &sart::EngineConfig::fault_inject)
+        .def_readwrite("fault_nan_sweep", &sart::EngineConfig::fault_nan_sweep);
     m.def("validate_config", [](const sart::EngineConfig& c) {
         try {
             sart::validate_params(c);
@@ -212,6 +213,7 @@ static void bind_engine(py::module_& m) {
         .def_property_readonly("geometry", &sart::Engine::geometry)
         .def_property_readonly("num_cus", &sart::Engine::num_cus)
         .def_property_readonly("column_shard", &sart::Engine::column_shard)
+        .def_property_readonly("shared_device", &sart::Engine::shared_device)
         .def_property_readonly("nrows", &sart::Engine::nrows)
         .def_property_readonly("nvoxel", &sart::Engine::nvoxel)
         .def_property_readonly("stream", [](const sart::Engine& e) { return reinterpret_cast<uintptr_t>(e.stream()); })

@@ -390,7 +390,11 @@ int main(int argc, char** argv) {
                             << "\", \"driver\": \"" << json_escape("native") << "\"}\n";
                 }
             }
-            if (cfg.no_guess) solution.clear();
+            // --no_guess, or a frame whose iterate stayed non-finite (the NaN/Inf guard returned the last finite
+            // iterate when there was one): the next frame cold-starts instead of inheriting NaN
+            if (cfg.no_guess ||
+                (info.nonfinite && !std::all_of(x.begin(), x.end(), [](double v) { return std::isfinite(v); })))
+                solution.clear();
         }
         if (rank == 0) {
             writer->flush();

@@ -9,6 +9,8 @@
 #include <limits>
 #include <stdexcept>
 
+#include <unistd.h>
+
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "../kernels/launchers.hpp"
@@ -23,7 +25,33 @@ void hip_ok(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Rank of this process among the ranks that asked for fault injection (SART_FAULT_RANK: only that rank
+// injects; unset: every rank).
+bool fault_rank_selected(int rank) {
+    const char* e = std::getenv("SART_FAULT_RANK");
+    return !(e && *e) || std::atoi(e) == rank;
+}
+
 }  // namespace
+
+bool device_shared_across_ranks(Communicator* comm, int device) {
+    const int n = comm->size();
+    if (n <= 1) return false;
+    // identity of the physical GPU: host name + PCI bus id (device ordinals differ under per-rank
+    // HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES and LOCAL_WORLD_SIZE is launcher-specific)
+    char bus[64] = {0};
+    hip_ok(hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, device), "hipDeviceGetPCIBusId");
+    char host[256] = {0};
+    (void)gethostname(host, sizeof(host) - 1);
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over "host/bus"
+    for (const char* p : {static_cast<const char*>(host), "/", static_cast<const char*>(bus)})
+        for (; *p; ++p) h = (h ^ (unsigned char)*p) * 1099511628211ull;
+    std::vector<double> keys((size_t)n, 0.0);
+    keys[(size_t)comm->rank()] = (double)(h >> 12) + 1.0;  // < 2^53: exact in fp64; one nonzero slot per rank
+    comm->host().all_reduce_host(keys.data(), keys.size(), ReduceOp::kSum);
+    std::sort(keys.begin(), keys.end());
+    return std::adjacent_find(keys.begin(), keys.end()) != keys.end();
+}
 
 double fused_min_bytes_from_env() {
     const char* e = std::getenv("SART_FUSED_MIN_MB");
@@ -85,6 +113,8 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
     if (cfg_.fused_schedule >= 0) fused_set_schedule(cfg_.fused_schedule);
     if (const char* fi = std::getenv("SART_FAULT_INJECT"); fi && *fi && cfg_.fault_inject == 0)
         cfg_.fault_inject = std::atoi(fi);
+    if (const char* fn = std::getenv("SART_FAULT_NAN"); fn && *fn && cfg_.fault_nan_sweep < 0)
+        cfg_.fault_nan_sweep = std::atoi(fn);
 
     nsplit_ = backproject_num_splits(ld_, Pp_, cfg_.rtm_bf16 ? 2 : 4);
     comm_buf_.resize(ld_ + 64);  // [0, ld) correction, [ld] ||A x||^2
@@ -96,13 +126,24 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
     x064_.resize(std::max<int64_t>(V_, 1));
     st_.resize(1);
     xcnt_.resize(16);
+    xprev_.resize(ld_);
     use_fused_ = false;
+    // The fused sweep is a persistent grid that needs every CU of its GPU co-resident: ranks sharing one
+    // GPU (one-GPU rehearsals of an N-rank run) would starve each other's hand-offs, so they use the
+    // two-pass kernels (SART_FUSED_SHARED=1 keeps the fused sweep; the collective fallback then recovers
+    // from protocol timeouts). Decided from device identity, identically on every rank of the group.
+    shared_device_ = !cfg_.column_shard && device_shared_across_ranks(comm_, device_);
+    const char* fs = std::getenv("SART_FUSED_SHARED");
+    const bool fused_ok_shared = fs && std::string(fs) == "1";
+    if (shared_device_ && cfg_.use_fused && !fused_ok_shared && comm_->rank() == 0)
+        std::fprintf(stderr, "sart: %d ranks share GPUs; using the two-pass kernels (the fused sweep needs a device "
+                             "to itself)\n", comm_->size());
     // bf16 storage: the fused sweep exists as variant 6 only (else the two-pass kernels)
     const double abytes = (double)Pp_ * (double)ld_ * (cfg_.rtm_bf16 ? 2.0 : 4.0);
     if (cfg_.use_fused && !cfg_.column_shard && abytes >= cfg_.fused_min_bytes &&
-        (!cfg_.rtm_bf16 || cfg_.fused_variant == 6)) {
+        (!shared_device_ || fused_ok_shared) && (!cfg_.rtm_bf16 || cfg_.fused_variant == 6)) {
         geom_ = fused_geometry(ld_, num_cus_, cfg_.fused_variant, cfg_.rows_per_tile);
-        use_fused_ = geom_.valid();
+        use_fused_ = geom_.valid() && (!cfg_.rtm_bf16 || geom_.variant == 6);
     }
     alloc_fused();
     ray_sums();
@@ -251,6 +292,7 @@ double Engine::setup_frame(const double* g, const double* x0) {
     // the reference divides by zero when every pixel is <= 0, we keep norm = 1 then.
     double mx = -std::numeric_limits<double>::infinity(), gs = 0.0;
     for (int64_t i = 0; i < P_; ++i) {
+        if (!std::isfinite(g[i])) continue;  // masked like a saturated pixel (k_prep_rows)
         mx = std::max(mx, g[i]);
         if (g[i] > 0) gs += g[i] * g[i];
     }
@@ -318,16 +360,20 @@ void Engine::sweep() {
                        x_.get(), pen_.get(), st, stream_);
         pen = pen_.get();
     }
-    if (comm_->size() > 1) {
+    if (comm_->size() > 1) {  // [0, ld) corrections, [ld] ||A x||^2, [ld + 1] error word: one collective
         comm_begin();
-        comm_->all_reduce(comm_buf_.get(), (size_t)ld_ + 1, ReduceOp::kSum, stream_);
+        comm_->all_reduce(comm_buf_.get(), (size_t)ld_ + 2, ReduceOp::kSum, stream_);
         comm_end();
     }
     launch_decide(st, Fslot, stream_);
     if (cfg_.logarithmic)
-        launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_, xcnt);
+        launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_, xcnt,
+                          xprev_.get());
     else
-        launch_update_linear(x_.get(), comm_buf_.get(), pen, V_, st, stream_, xcnt);
+        launch_update_linear(x_.get(), comm_buf_.get(), pen, V_, st, stream_, xcnt, xprev_.get());
+    if (cfg_.fault_nan_sweep >= 0 && host_sweep_ == cfg_.fault_nan_sweep)  // fault injection (tests)
+        hip_ok(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(x_.get()), 0x7fc00000, 1, stream_), "inject NaN");
+    ++host_sweep_;
 }
 
 void Engine::sweep_columns() {
@@ -364,9 +410,10 @@ void Engine::sweep_columns() {
     }
     launch_decide(st, Fslot, stream_);
     if (cfg_.logarithmic)
-        launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_);
+        launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_, nullptr,
+                          xprev_.get());
     else
-        launch_update_linear(x_.get(), comm_buf_.get(), pen, V_, st, stream_);
+        launch_update_linear(x_.get(), comm_buf_.get(), pen, V_, st, stream_, nullptr, xprev_.get());
 }
 
 bool Engine::timing_collectives() const { return cfg_.time_collectives && !cfg_.use_graph && comm_->size() > 1; }
@@ -461,6 +508,13 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
     const int max_sweeps = cfg_.max_iterations + 1;
     while (true) {
         norm_ = setup_frame(g, x0);
+        host_sweep_ = 0;
+        // Fault injection (tests): report a protocol timeout from the device in the first sweep of this solve,
+        // through the same path as a real one (error word -> all-reduce -> k_decide on every rank).
+        if (use_fused_ && injected_ < cfg_.fault_inject && fault_rank_selected(comm_->rank())) {
+            ++injected_;
+            hip_ok(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&st_.get()->error), 16, 1, stream_), "inject");
+        }
         int enqueued = 0, issued = 0, checked = 0;
         bool error = false;
         comm_ms_ = 0.0;
@@ -484,11 +538,7 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
             collect_comm(slot);
             SartState s = hstate_[slot];
             ++checked;
-            if (use_fused_ && injected_ < cfg_.fault_inject && checked == 1) {  // fault injection (tests)
-                ++injected_;
-                s.error = 1;
-            }
-            if (s.error) {
+            if (s.error) {  // bit 8 (collective) is set on every rank in the same sweep
                 error = true;
                 break;
             }
@@ -507,8 +557,13 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
     }
     SartState s;
     hip_ok(hipMemcpy(&s, st_.get(), sizeof(SartState), hipMemcpyDeviceToHost), "D2H state");
+    // NaN/Inf guard: x of the failing sweep is non-finite; return the last finite iterate (saved by the update
+    // of the previous sweep), unless the very first sweep failed (no update yet: nothing better to return)
+    const bool rollback = (s.flags & 1) != 0 && s.sweep >= 2;
     std::vector<float> xh(V_);
-    if (V_) hip_ok(hipMemcpy(xh.data(), x_.get(), V_ * sizeof(float), hipMemcpyDeviceToHost), "D2H x");
+    if (V_)
+        hip_ok(hipMemcpy(xh.data(), rollback ? xprev_.get() : x_.get(), V_ * sizeof(float), hipMemcpyDeviceToHost),
+               "D2H x");
     for (int64_t i = 0; i < V_; ++i) x_out[i] = (double)xh[i] * norm_;  // reference sartsolver_cuda.cpp:264-265
     info.status = s.status == kSuccess ? kSuccess : kMaxIterationsExceeded;
     info.iterations = s.iterations;

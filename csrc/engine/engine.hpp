@@ -42,6 +42,9 @@ struct EngineConfig : SolverParams {
     // Fault injection (tests; env SART_FAULT_INJECT=N): report a persistent-sweep protocol timeout in the
     // first N solves, exercising the v6 -> v3 -> two-pass fallback chain end to end.
     int fault_inject = 0;
+    // Fault injection (tests; env SART_FAULT_NAN=k): write NaN into x after sweep k of every solve (eager
+    // chunks), exercising the NaN/Inf guard's rollback to the last finite iterate. -1: off.
+    int fault_nan_sweep = -1;
     // Multi-frame engine: frames per batch (16, 32 or 64; MultiFrameEngine rounds other values up).
     int mf_frames = 16;
     // Column (voxel) shard instead of the reference's row (pixel) shard: this rank holds ALL
@@ -101,6 +104,9 @@ struct DeviceRaySums {
     DeviceArray<float> ray_len, dinv, dscale, dmask;
 };
 
+// True when two ranks of `comm` drive the same physical GPU (host name + PCI bus id). Collective.
+bool device_shared_across_ranks(Communicator* comm, int device);
+
 // SART_FUSED_MIN_MB (default 128): the drivers' threshold for EngineConfig::fused_min_bytes.
 double fused_min_bytes_from_env();
 
@@ -132,6 +138,7 @@ class Engine {
     std::vector<double> ray_density() const;  // fp64 (nvoxel): global (row shard) / this shard's voxels (column)
     std::vector<double> ray_length() const;   // fp64 (nrows): this shard's pixels (row shard) / global (column)
     bool column_shard() const { return cfg_.column_shard; }
+    bool shared_device() const { return shared_device_; }
     double last_norm() const { return norm_; }
 
    private:
@@ -163,6 +170,8 @@ class Engine {
     double norm_ = 1.0;
 
     DeviceArray<float> partial_, comm_buf_, x_, pen_, O_, ghat_, arow_, gpos_, wo_, w_, fitted_;
+    DeviceArray<float> xprev_;  // x before the last update (NaN/Inf guard rollback)
+    bool shared_device_ = false;
     DeviceArray<double> Fpart_, g64_, x064_;
     DeviceRaySums rs_;
     DeviceArray<SartState> st_;
@@ -190,6 +199,7 @@ class Engine {
     bool graph_failed_ = false;
     bool warm_ = false;  // an eager chunk ran with the current kernels
     int injected_ = 0;
+    int host_sweep_ = 0;  // sweeps enqueued in the current solve (fault_nan_sweep)
 };
 
 }  // namespace sart

@@ -5,17 +5,52 @@
 
 namespace sart {
 
+namespace {
+
+// Variant 6 geometry for a padded width `ld` at T rows per tile: J = ld / slab workgroups per row (slab =
+// 8192 / T columns: the four compute waves cover T rows x 4 / T sub-slabs of 2048 columns), G = per_xcd / J
+// row groups per XCD (the XCD's remaining per_xcd - G * J CUs stay idle). cost = slab / G is the time per
+// matrix row relative to the other candidates (each CU streams slab columns of P / (8 G) rows).
+struct V6Candidate {
+    int T = 0, J = 0, G = 0;
+    double cost = 0.0;
+};
+
+V6Candidate v6_candidate(int64_t ld, int T, int per_xcd) {
+    V6Candidate c;
+    const int64_t slab = 8192 / T;
+    if (ld % slab != 0) return c;
+    const int64_t J = ld / slab;
+    if (J < 1 || J > per_xcd || J * T > 256 /* exchange gather registers */) return c;
+    c.T = T, c.J = (int)J, c.G = per_xcd / (int)J;
+    c.cost = (double)slab / c.G;
+    return c;
+}
+
+}  // namespace
+
 int64_t choose_ld(int64_t nvoxel, double max_waste) {
+    // Widths the fused sweep (variant 6) can split into whole slabs, J <= 32 per row group: at each T the
+    // smallest multiple of the slab covering nvoxel. Take the one with the lowest time per row (ties: less
+    // padding, then the larger T, measured fastest at equal cost), if it pads by at most max_waste.
     if (nvoxel >= 1024) {
-        for (int K = 1; K <= 8; K *= 2) {
-            const int64_t wc = 1024 * (int64_t)K;
-            const int64_t J = (nvoxel + wc - 1) / wc;
-            if (J <= 32 || K == 8) {
-                const int64_t ld = J * wc;
-                if ((double)(ld - nvoxel) <= max_waste * (double)nvoxel) return ld;
-                break;
+        constexpr int kPerXcd = 32;  // MI355X: 256 CUs in 8 XCDs
+        int64_t best_ld = 0;
+        double best_cost = 0.0;
+        for (const int T : {4, 2, 1}) {
+            const int64_t slab = 8192 / T;
+            const int64_t ld = (nvoxel + slab - 1) / slab * slab;
+            const V6Candidate c = v6_candidate(ld, T, kPerXcd);
+            if (c.G == 0 || (double)(ld - nvoxel) > max_waste * (double)nvoxel) continue;
+            if (best_ld == 0 || c.cost < best_cost || (c.cost == best_cost && ld < best_ld)) {
+                best_ld = ld;
+                best_cost = c.cost;
             }
         }
+        if (best_ld) return best_ld;
+        // wider than 32 slabs of 8192: a multiple of 8192 keeps the variant 3 fallback (K = 8) available
+        const int64_t ld = (nvoxel + 8191) / 8192 * 8192;
+        if ((double)(ld - nvoxel) <= max_waste * (double)nvoxel) return ld;
     }
     const int64_t n = std::max<int64_t>(nvoxel, 64);
     return (n + 63) / 64 * 64;
@@ -27,44 +62,32 @@ FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_
         const char* e = std::getenv("SART_FUSED_T");
         rows_per_tile = (e && *e) ? std::atoi(e) : 0;
     }
-    if (variant == 4 || variant == 6) {
-        // Rows per tile: the requested T, else the largest of 4, 2, 1 whose row group fits the XCD (T = 4 at
-        // ld = 64k, 2 at 128k, 1 at 256k: 6.5-6.9 TB/s, against 4.0-4.7 TB/s for variant 3 at those widths,
-        // profiles/probe_r1_fused_T.jsonl).
-        const int per_xcd = num_cus / 8;
+    if (variant == 6 && num_cus % 8 == 0) {
+        // Rows per tile: the requested T, else the candidate with the lowest time per row (ties: the larger T;
+        // T = 4 at ld = 64k, 2 at 128k, 1 at 256k measured 6.5-6.9 TB/s, against 4.0-4.7 TB/s for variant 3,
+        // profiles/probe_r1_fused_T.jsonl). Widths whose J does not divide the XCD's CU count run
+        // G = per_xcd / J row groups per XCD and leave the remaining CUs idle.
+        V6Candidate best;
         for (const int T : {4, 2, 1}) {
             if (rows_per_tile > 0 && T != rows_per_tile) continue;
-            const int64_t slab = 8192 / T;
-            if (ld % slab != 0 || ld / slab == 0) continue;
-            const int J = (int)(ld / slab);
-            if (variant == 6 && num_cus % 8 == 0 && per_xcd % J == 0) {
-                g.K = T, g.J = J, g.I = 8 * (per_xcd / J), g.grid = g.I * g.J, g.variant = 6, g.T = T;
-                return g;
-            }
-            if (variant == 4 && J <= std::min(64, num_cus)) {
-                g.K = T, g.J = J, g.I = std::max(1, num_cus / J), g.grid = g.I * g.J, g.variant = 4, g.T = T;
-                return g;
-            }
+            const V6Candidate c = v6_candidate(ld, T, num_cus / 8);
+            if (c.G > 0 && (best.G == 0 || c.cost < best.cost)) best = c;
         }
-        variant = 3;
-    }
-    if (variant == 5) {
-        if (ld % 2048 == 0 && ld / 2048 > 0 && ld / 2048 <= std::min(64, num_cus)) {
-            g.K = 8, g.J = (int)(ld / 2048), g.I = std::max(1, num_cus / g.J), g.grid = g.I * g.J, g.variant = 5,
-            g.T = 4;
+        if (best.G > 0) {
+            g.K = best.T, g.J = best.J, g.I = 8 * best.G, g.grid = g.I * g.J, g.variant = 6, g.T = best.T;
             return g;
         }
-        variant = 3;
     }
+    // Variant 3 (generic fallback): slabs of 1024 * K columns, K the smallest power of two giving <= 32
+    // slabs (any count at K = 8), T = 8 / K rows per tile, num_cus / J row groups.
     for (int K = 1; K <= 8; K *= 2) {
         const int64_t wc = 1024 * (int64_t)K;
         if (ld % wc) continue;
         const int64_t J = ld / wc;
         if (J <= 32 || K == 8) {
-            const int v = (variant != 2 || K <= 4) ? variant : 3;
-            const int T = v == 2 ? 4 / K : 8 / K;
+            const int T = 8 / K;
             if (J > num_cus || J * T > 512) return g;
-            g.K = K, g.J = (int)J, g.I = std::max(1, num_cus / (int)J), g.grid = g.I * g.J, g.variant = v, g.T = T;
+            g.K = K, g.J = (int)J, g.I = std::max(1, num_cus / (int)J), g.grid = g.I * g.J, g.variant = 3, g.T = T;
             return g;
         }
     }

@@ -7,21 +7,22 @@
 namespace sart {
 
 struct FusedGeometry {
-    int K = 0;        // variants 0-3: float4 per lane per row slab / 256; variants 4, 6: rows per tile
+    int K = 0;        // variant 3: float4 per lane per row slab / 256 (slab 1024 * K); variant 6: rows per tile
     int J = 0;        // workgroups per row (column slabs)
     int I = 0;        // row groups
     int grid = 0;     // I * J persistent workgroups
-    int variant = -1; // -1: no fused path for this width
+    int variant = -1; // 6 (XCD-local row groups), 3 (generic fallback), -1: no fused path for this width
     int T = 0;        // rows per tile
     bool valid() const { return variant >= 0; }
 };
 
-// Padded row length of a dense shard: a width the fused sweep can split into slabs when that wastes at
-// most max_waste of the row, else the next multiple of 64 floats (256 B rows).
+// Padded row length of a dense shard: the variant 6 width (J slabs of 8192 / T columns, J <= 32) with the
+// lowest estimated time per row when that wastes at most max_waste of the row, else a multiple of 8192
+// (variant 3), else the next multiple of 64 floats (256 B rows).
 int64_t choose_ld(int64_t nvoxel, double max_waste = 0.10);
 
-// Geometry for `variant` (6 default; 4/5/3/0-2 supported), falling back to variant 3 when the width
-// does not fit. rows_per_tile = 0: SART_FUSED_T or the measured default (4).
+// Geometry for `variant` (6 default, or 3), falling back to variant 3 when variant 6 cannot split the
+// width. rows_per_tile = 0: SART_FUSED_T or the lowest-cost T.
 FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_tile);
 
 }  // namespace sart

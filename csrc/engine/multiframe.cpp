@@ -110,7 +110,8 @@ void MultiFrameEngine::solve_group(const double* g, int B, double* x_out, SolveI
     for (int f = 0; f < NF; ++f) mx[f] = -std::numeric_limits<double>::infinity(), gs[f] = 0.0;
     for (int64_t p = 0; p < P_; ++p)
         for (int f = 0; f < NF; ++f) {
-            const double v = f < B ? g[(int64_t)f * P_ + p] : 0.0;
+            double v = f < B ? g[(int64_t)f * P_ + p] : 0.0;
+            if (!std::isfinite(v)) v = -1.0;  // non-finite pixel: masked like a saturated one
             hg_[p * NF + f] = v;
             if (f < B) {
                 mx[f] = std::max(mx[f], v);

@@ -40,7 +40,7 @@ constexpr int kFusedThreads = 320;  // 4 compute waves + 1 exchange wave
 constexpr unsigned kSpinLimit = 1u << 20;
 constexpr int kMaxGather = 512;     // J*T granules per tile
 constexpr int kGatherRegs = kMaxGather / 64;
-constexpr int kRowsGather = 256;    // J*T granules per tile, rows kernel (variants 4 and 6)
+constexpr int kRowsGather = 256;    // J*T granules per tile, rows kernel (variant 6)
 
 // diagnostics (dbg & 2): per-workgroup cycle counters, read with fused_debug_stats()
 __device__ unsigned long long g_fused_stats[1024 * 8];
@@ -64,190 +64,13 @@ __device__ __forceinline__ uint64_t make_granule(int epoch, float v) {
     return ((uint64_t)(uint32_t)epoch << 32) | (uint64_t)__float_as_uint(v);
 }
 
-template <int K, int TK, int R, int L, bool LOG>
-__global__ __launch_bounds__(kFusedThreads) void k_fused_sweep(
-    const float* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
-    const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
-    double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st) {
-    constexpr int T = TK / K;   // rows per tile
-    constexpr int AH = R - L;   // tiles loaded ahead: at step t tiles t+1 .. t+AH-1 are in flight
-    static_assert(T * K == TK && T >= 1, "tile must be whole rows");
-    static_assert(L >= 2 && AH >= 2, "need lag >= 2 and >= 1 tile in flight");
-
-    __shared__ float s_part[4][4][8];  // [tile % 4][compute wave][row]
-    __shared__ float s_w[4][8];        // [tile % 4][row]
-
-    if (st->done) return;
-    const int epoch = st->epoch;
-
-    const int b = blockIdx.x;
-    const int gi = b % I;  // row group (blocks b, b+8, ... share an XCD when I == 8: speed only)
-    const int gj = b / I;  // column slab
-    const int64_t ntiles = nrows_pad / T;
-    const int64_t t_begin = ntiles * gi / I;
-    const int64_t nt = ntiles * (gi + 1) / I - t_begin;
-    // The last L steps only drain the back-projection. Both wave roles execute exactly nsteps
-    // barriers (a multiple of 2R so both unrolled loops end together).
-    const int64_t nsteps = (nt + L + 2 * R - 1) / (2 * R) * (2 * R);
-
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    const int64_t ld4 = ld >> 2;
-
-    if (wave < 4) {
-        // ------------------------------ compute waves ------------------------------
-        const int64_t col4 = (int64_t)gj * (256 * K) + wave * (64 * K) + lane;
-        const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
-        const float4* __restrict__ a4 = reinterpret_cast<const float4*>(A) + col4;
-
-        float4 xs[K], acc[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            xs[k] = x4[col4 + k * 64];
-            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-
-        float4 buf[R][T][K];
-        const int64_t tlast = ntiles - 1 - t_begin;  // unconditional clamped loads: see k_fused_sweep_rows
-        auto load_tile = [&](float4(&dst)[T][K], int64_t t) {
-            const float4* src = a4 + (t_begin + (t < tlast ? t : tlast)) * T * ld4;
-#pragma unroll
-            for (int r = 0; r < T; ++r)
-#pragma unroll
-                for (int k = 0; k < K; ++k) dst[r][k] = load_stream(src + r * ld4 + k * 64);
-        };
-        // prologue: tiles 0 .. AH-1
-        [&]<int... Is>(std::integer_sequence<int, Is...>) {
-            (load_tile(buf[Is], Is), ...);
-        }(std::make_integer_sequence<int, AH>{});
-
-        auto step = [&](auto bbc, int64_t t) {
-            constexpr int bb = decltype(bbc)::value;      // slot of tile t
-            constexpr int bp = (bb + R - L) % R;          // slot of tile t-L == slot of tile t-L+R
-            if (t < nt) {
-#pragma unroll
-                for (int r = 0; r < T; ++r) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int k = 0; k < K; ++k) s += dot4(buf[bb][r][k], xs[k]);
-                    s = wave_sum(s);
-                    if (lane == 0) s_part[t & 3][wave][r] = s;
-                }
-            }
-            __syncthreads();
-            if (t >= L && t - L < nt) {
-                const int ws = (int)((t - L) & 3);
-#pragma unroll
-                for (int r = 0; r < T; ++r) {
-                    const float wr = s_w[ws][r];
-#pragma unroll
-                    for (int k = 0; k < K; ++k) fma4(acc[k], buf[bp][r][k], wr);
-                }
-            }
-            load_tile(buf[bp], t - L + R);
-        };
-
-        for (int64_t t0 = 0; t0 < nsteps; t0 += R) {
-            [&]<int... Is>(std::integer_sequence<int, Is...>) {
-                (step(std::integral_constant<int, Is>{}, t0 + Is), ...);
-            }(std::make_integer_sequence<int, R>{});
-        }
-
-        float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld) + col4;
-#pragma unroll
-        for (int k = 0; k < K; ++k) out[k * 64] = acc[k];
-    } else {
-        // ------------------------------ exchange wave ------------------------------
-        const int n = J * T;
-        bool failed = false;
-        double F = 0.0;
-        uint64_t pv[2][kGatherRegs];  // poll registers, double buffered by step parity
-
-        // Polls are issued unconditionally at clamped addresses (tile in [0, ntiles), granule < n; lanes past
-        // n re-read granule n - 1 and are masked when summing), so the compiler counts the polls in flight
-        // instead of draining them (see load_tile in k_fused_sweep_rows).
-        const int64_t ulast = ntiles - 1 - t_begin;
-        auto issue_poll = [&](uint64_t(&dst)[kGatherRegs], int64_t u) {
-            const int64_t uc = u < 0 ? 0 : (u < ulast ? u : ulast);
-            const uint64_t* g = gran + (t_begin + uc) * (int64_t)n;
-#pragma unroll
-            for (int m = 0; m < kGatherRegs; ++m) {
-                const int idx = lane + 64 * m;
-                dst[m] = __hip_atomic_load(g + (idx < n ? idx : n - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        };
-
-        // consume tile u from poll registers (re-poll synchronously if a granule is not ready yet)
-        auto finish_tile = [&](uint64_t(&v)[kGatherRegs], int64_t u) {
-            if (!failed) {
-                unsigned spins = 0;
-                while (true) {
-                    bool ok = true;
-#pragma unroll
-                    for (int m = 0; m < kGatherRegs; ++m) ok &= ((int)(v[m] >> 32) == epoch);
-                    if (__all(ok)) break;
-                    if (++spins > kSpinLimit) {
-                        failed = true;
-                        if (lane == 0) atomicOr(&st->error, 1);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    issue_poll(v, u);
-                }
-            }
-            float s = 0.f;
-            if (!failed) {
-#pragma unroll
-                for (int m = 0; m < kGatherRegs; ++m)
-                    s += (lane + 64 * m < n) ? __uint_as_float((uint32_t)v[m]) : 0.f;
-            }
-            // lanes l and l' hold the same row iff l == l' (mod T): butterfly over the other bits
-#pragma unroll
-            for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
-            if (lane < T) {
-                const int64_t row = (t_begin + u) * T + lane;
-                float w = 0.f;
-                if (row < nrows) {
-                    const float a = arow[row];
-                    w = LOG ? a * s : a * (ghat[row] - s);
-                    if (gj == 0) F += (double)s * (double)s;
-                }
-                s_w[u & 3][lane] = w;
-            }
-        };
-
-        auto xstep = [&](auto pc, int64_t t) {
-            constexpr int p = decltype(pc)::value;  // parity: pv[p] receives tile t-L+2
-            __syncthreads();
-            if (t < nt && lane < T) {
-                const int ps = (int)(t & 3);
-                const float s = ((s_part[ps][0][lane] + s_part[ps][1][lane]) + s_part[ps][2][lane]) +
-                                s_part[ps][3][lane];
-                uint64_t* g = gran + ((t_begin + t) * J + gj) * T + lane;
-                __hip_atomic_store(g, make_granule(epoch, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            const int64_t un = t - L + 2;  // tile whose gather starts now (published >= L-2 steps ago)
-            issue_poll(pv[p], un);
-            const int64_t uc = t - L + 1;  // tile whose gather was issued last step; its w is due next step
-            if (uc >= 0 && uc < nt) finish_tile(pv[p ^ 1], uc);
-        };
-
-        for (int64_t t0 = 0; t0 < nsteps; t0 += 2) {
-            xstep(std::integral_constant<int, 0>{}, t0);
-            xstep(std::integral_constant<int, 1>{}, t0 + 1);
-        }
-        F = wave_sum(F);
-        if (lane == 0) Fpart[b] = F;
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
-// Variant 3 (default): in-flight tiles in registers, held tiles in LDS.
+// Variant 3 (fallback for widths variant 6 cannot split): in-flight tiles in registers, held tiles in LDS.
 //
 // Little's law sizing: at ~24.6 GB/s per CU (6.3 TB/s over 256 CUs) and a loaded HBM latency of
 // 2-4 us a CU needs ~100 KB of loads in flight. Holding the L tiles that wait for their SART weights
 // in registers (variants 0-2) leaves room for only ~2 tiles (64 KB) in flight and caps the sweep at
-// ~4 TB/s. Here each compute wave keeps AH = 4 tiles (4 x 8 KB) of loads in flight in VGPRs; once a
+// ~4 TB/s (the removed variants 0-2). Here each compute wave keeps AH = 4 tiles (4 x 8 KB) of loads in flight in VGPRs; once a
 // tile's row partials are reduced it is parked in an LDS ring (NL = L + 1 slots x 32 KB, each wave
 // only touches its own 8 KB per slot, so no barrier guards the ring) and read back L steps later for
 // the back-projection. 128 KB of loads in flight per CU, 128 KB of LDS.
@@ -433,14 +256,14 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Variant 4 (default for ld % 2048 == 0): "split rows" + barrier-free LDS hand-offs.
+// Variant 6 (default): "split rows" + barrier-free LDS hand-offs + XCD-local row groups.
 //
 // Measured on MI355X (tools/probe.py, exchange disabled): the register/LDS pipeline of variant 3
 // streams at the HBM roof (6.2 TB/s) only when each wave performs ONE full-wave reduction per step;
 // with T rows per wave per step the T dependent shuffle reductions dominate. Here every compute wave
 // owns a different row of the 4-row tile over the same 2048-column slab (8 float4 per lane), so a
 // step costs one reduction per wave and no cross-wave partial sum.
-// The per-step __syncthreads of variants 0-3 coupled the compute waves to every jitter of the
+// The per-step __syncthreads of variant 3 (and the removed 0-2) coupled the compute waves to every jitter of the
 // inter-workgroup exchange; here compute and exchange waves hand off through LDS words tagged with
 // the tile index (written data-then-flag by one wave; LDS serves a wave's requests in order), so the
 // compute waves block only when the weight they need at step t (tile t - L) is not there yet.
@@ -741,7 +564,7 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
         double F = 0.0;
         constexpr int GR = kRowsGather / 64;  // poll registers per lane (J * T <= kRowsGather)
         uint64_t pv[PQ][GR];
-        // unconditional clamped polls (see issue_poll in k_fused_sweep): counted vmcnt, PQ polls in flight
+        // unconditional clamped polls (see issue_poll in k_fused_sweep_lds): counted vmcnt, PQ polls in flight
         const int64_t ulast = ntiles - 1 - t_begin;
         auto issue_poll = [&](uint64_t(&dst)[GR], int64_t u) {
             const int64_t uc = u < 0 ? 0 : (u < ulast ? u : ulast);
@@ -852,204 +675,6 @@ constexpr size_t rows_lds_bytes(int T, int sched) {
            (8 * 4 * 3 + 8 + 4) * sizeof(float);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Variant 5 (default): variant 4 + compute waves publish their own granules + two exchange waves.
-//
-// A granule hand-off under full HBM streaming load takes 2-3.5 us (MI355X_MICROARCH.md price list,
-// 'handoff-1to1'), two to three 32 KB steps. With one exchange wave serving every tile, the poll of
-// tile u could only be issued one step after the tile was published and had to be consumed one step
-// later; every late peer stalled the sweep. Here the compute wave that owns row r of a tile stores
-// that row's granule itself (one sc1 store from lane 0 right after its reduction), and two exchange
-// waves take alternate tiles: exchange wave e polls tile u (u % 2 == e) once its own workgroup has
-// produced tile u + 1 and may block on that poll for two steps before the weights are due.
-// ---------------------------------------------------------------------------------------------
-constexpr int kFused5Threads = 384;  // 4 compute waves + 2 exchange waves
-
-template <bool LOG>
-__global__ __launch_bounds__(kFused5Threads) void k_fused_sweep_rows2(
-    const float* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
-    const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
-    double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg) {
-    constexpr int KW = 8, T = 4, L = 3, NL = L + 1, AH = 4, NS = 8;
-
-    extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64]
-    float* s_small = reinterpret_cast<float*>(s_ring + NL * 4 * KW * 64);
-    lds_vfloat* s_w = (lds_vfloat*)s_small;                                         // [NS][4]
-    lds_vint* s_pflag = (lds_vint*)(s_small + NS * 4);                              // [NS][4]
-    lds_vint* s_wflag = s_pflag + NS * 4;                                           // [NS]
-
-    if (st->done) return;
-    const int epoch = st->epoch;
-    const int b = blockIdx.x;
-    const int gi = b % I;
-    const int gj = b / I;
-    const int64_t ntiles = nrows_pad / T;
-    const int64_t t_begin = ntiles * gi / I;
-    const int64_t nt = ntiles * (gi + 1) / I - t_begin;
-    const int wave = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    const int64_t ld4 = ld >> 2;
-    const bool exchange = !(dbg & 1);
-
-    for (int i = threadIdx.x; i < NS * 4 + NS; i += kFused5Threads) s_pflag[i] = -1;
-    __syncthreads();
-
-    if (wave < 4) {
-        const int64_t col4 = (int64_t)gj * (64 * KW) + lane;
-        const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
-        const float4* __restrict__ a4 = reinterpret_cast<const float4*>(A) + col4 + (int64_t)wave * ld4;
-        float4* ring = s_ring + (wave * KW) * 64 + lane;
-        uint64_t* gmine = gran + (int64_t)gj * T + wave;  // + tile * J * T
-        float4 xs[KW], acc[KW];
-#pragma unroll
-        for (int k = 0; k < KW; ++k) {
-            xs[k] = x4[col4 + k * 64];
-            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        float4 fl[AH][KW];
-        const int64_t tlast = ntiles - 1 - t_begin;  // unconditional clamped loads: see k_fused_sweep_rows
-        auto load_tile = [&](float4(&dst)[KW], int64_t t) {
-            const float4* src = a4 + (t_begin + (t < tlast ? t : tlast)) * T * ld4;
-#pragma unroll
-            for (int k = 0; k < KW; ++k) dst[k] = load_stream(src + k * 64);
-        };
-#pragma unroll
-        for (int i = 0; i < AH; ++i) load_tile(fl[i], i);
-        bool stuck = false;
-
-        auto step = [&](auto bbc, int64_t t) {
-            constexpr int bb = decltype(bbc)::value;
-            if (t < nt) {
-                float s = 0.f;
-#pragma unroll
-                for (int k = 0; k < KW; ++k) s += dot4(fl[bb][k], xs[k]);
-                s = wave_sum(s);
-                if (lane == 0) {
-                    if (exchange)
-                        __hip_atomic_store(gmine + (t_begin + t) * J * T, make_granule(epoch, s), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                    s_pflag[(t & (NS - 1)) * 4 + wave] = (int)t;
-                }
-                float4* slot = ring + (int)(t % NL) * (4 * KW * 64);
-#pragma unroll
-                for (int k = 0; k < KW; ++k) slot[k * 64] = fl[bb][k];
-            }
-            load_tile(fl[bb], t + AH);
-            if (t >= L && t - L < nt) {
-                const int64_t u = t - L;
-                const int ws = (int)(u & (NS - 1));
-                unsigned spins = 0;
-                while (s_wflag[ws] != (int)u && !stuck) {
-                    if (++spins > kSpinLimit) {
-                        stuck = true;
-                        if (lane == 0) atomicOr(&st->error, 2);
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                asm volatile("" ::: "memory");
-                const float wr = s_w[ws * 4 + wave];
-                const float4* slot = ring + (int)(u % NL) * (4 * KW * 64);
-#pragma unroll
-                for (int k = 0; k < KW; ++k) fma4(acc[k], slot[k * 64], wr);
-            }
-        };
-        for (int64_t t0 = 0; t0 < nt + L; t0 += AH) {
-            step(std::integral_constant<int, 0>{}, t0 + 0);
-            step(std::integral_constant<int, 1>{}, t0 + 1);
-            step(std::integral_constant<int, 2>{}, t0 + 2);
-            step(std::integral_constant<int, 3>{}, t0 + 3);
-        }
-        __syncthreads();
-        float4* red = s_ring + (wave * KW) * 64 + lane;
-#pragma unroll
-        for (int k = 0; k < KW; ++k) red[k * 64] = acc[k];
-        __syncthreads();
-        float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld) + col4;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const int k = wave * 2 + kk;
-            float4 v = s_ring[(0 * KW + k) * 64 + lane];
-#pragma unroll
-            for (int ww = 1; ww < 4; ++ww) {
-                const float4 o = s_ring[(ww * KW + k) * 64 + lane];
-                v.x += o.x;
-                v.y += o.y;
-                v.z += o.z;
-                v.w += o.w;
-            }
-            out[k * 64] = v;
-        }
-    } else {
-        const int e = wave - 4;  // this exchange wave serves tiles u % 2 == e
-        const int n = J * T;
-        bool failed = false;
-        double F = 0.0;
-        for (int64_t u = e; u < nt; u += 2) {
-            // trigger: this workgroup has reduced tile u + 1 (tile u itself for the last tile)
-            const int64_t trig = (u + 1 < nt) ? u + 1 : u;
-            const int tsl = (int)(trig & (NS - 1));
-            if (lane < 4) {
-                unsigned spins = 0;
-                while (s_pflag[tsl * 4 + lane] < (int)trig) {
-                    if (++spins > kSpinLimit) break;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            const int64_t row = (t_begin + u) * T + (lane & 3);
-            const float a = (lane < T && row < nrows) ? arow[row] : 0.f;
-            const float gh = (lane < T && row < nrows) ? ghat[row] : 0.f;
-            float s = 0.f;
-            if (exchange) {
-                const uint64_t* g = gran + (t_begin + u) * (int64_t)n;
-                uint64_t v[kGatherRegs];
-                unsigned spins = 0;
-                while (!failed) {
-                    bool ok = true;
-#pragma unroll
-                    for (int m = 0; m < kGatherRegs; ++m) {
-                        const int idx = lane + 64 * m;
-                        v[m] = (idx < n) ? __hip_atomic_load(g + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                         : make_granule(epoch, 0.f);
-                    }
-#pragma unroll
-                    for (int m = 0; m < kGatherRegs; ++m) ok &= ((int)(v[m] >> 32) == epoch);
-                    if (__all(ok)) {
-#pragma unroll
-                        for (int m = 0; m < kGatherRegs; ++m)
-                    s += (lane + 64 * m < n) ? __uint_as_float((uint32_t)v[m]) : 0.f;
-                        break;
-                    }
-                    if (++spins > kSpinLimit) {
-                        failed = true;
-                        if (lane == 0) atomicOr(&st->error, 1);
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-#pragma unroll
-            for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
-            const int ws = (int)(u & (NS - 1));
-            if (lane < T) {
-                float w = 0.f;
-                if (row < nrows) {
-                    w = LOG ? a * s : a * (gh - s);
-                    if (gj == 0) F += (double)s * (double)s;
-                }
-                s_w[ws * 4 + lane] = w;
-            }
-            asm volatile("" ::: "memory");
-            if (lane == 0) s_wflag[ws] = (int)u;
-        }
-        F = wave_sum(F);
-        if (lane == 0) Fpart[2 * b + e] = F;
-        __syncthreads();
-        __syncthreads();
-    }
-}
-
-constexpr size_t kRows2LdsBytes = 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (8 * 4 * 2 + 8) * sizeof(float);
-
 static int g_fused_dbg = 0;    // diagnostics only (set through fused_set_debug)
 static int g_fused_sched = 4;  // variant 6 pipeline schedule (k_fused_sweep_rows SCHED)
 void fused_set_debug(int flags) { g_fused_dbg = flags; }
@@ -1074,34 +699,8 @@ std::vector<unsigned long long> fused_debug_stats(int nblocks) {
     return out;
 }
 
+
 constexpr size_t kLdsRingBytes = 4 /*NL*/ * 4 /*waves*/ * 8 /*TK*/ * 64 * sizeof(float4) + 160 * sizeof(float);
-
-// ---------------------------------------------------------------------------------------------
-// Host side. Variants trade register ring depth (latency hiding) against occupancy:
-//   variant 0: TK=8, R=5, L=3      (default)
-//   variant 1: TK=8, R=4, L=2      (shallow ring)
-//   variant 2: TK=4, R=8, L=4      (small tiles, deep ring; K <= 4)
-// ---------------------------------------------------------------------------------------------
-int fused_pick_k(int64_t ld) {
-    for (int K = 1; K <= 8; K *= 2) {
-        const int64_t wc = 1024 * (int64_t)K;
-        if (ld % wc != 0) return K > 1 ? K / 2 : 0;
-        if (ld / wc <= 32) return K;
-    }
-    return 8;
-}
-
-template <int K, int TK, int R, int L>
-static void launch_cfg(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
-                       int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
-                       double* Fpart, uint64_t* gran, int I, int J, SartState* st) {
-    if (logmode)
-        hipLaunchKernelGGL((k_fused_sweep<K, TK, R, L, true>), grid, dim3(kFusedThreads), 0, stream, A, ld, nrows,
-                           nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st);
-    else
-        hipLaunchKernelGGL((k_fused_sweep<K, TK, R, L, false>), grid, dim3(kFusedThreads), 0, stream, A, ld, nrows,
-                           nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st);
-}
 
 template <int K>
 static void launch_lds(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
@@ -1139,16 +738,16 @@ static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld
 }
 
 template <int T>
-static void launch_rows(bool logmode, bool xl, dim3 grid, hipStream_t stream, const float* A, int64_t ld,
-                        int64_t nrows, int64_t nrows_pad, const float* x_, const float* ghat, const float* arow,
-                        float* partial, double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
+static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
+                        int64_t nrows_pad, const float* x_, const float* ghat, const float* arow, float* partial,
+                        double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
     const bool diag = (g_fused_dbg & 2) != 0;  // instrumented build only when asked (timing diagnostics)
-    // g_fused_sched: pipeline schedule of variant 6 (k_fused_sweep_rows SCHED); schedules 1-3 hold the x
-    // slab in LDS, which has room for it only when T >= 2. Instrumented builds: schedules 0 and 2.
-    int sched = xl && T >= 2 ? g_fused_sched : 0;
+    // g_fused_sched: pipeline schedule (k_fused_sweep_rows SCHED); schedules 1-4 hold the x slab in LDS,
+    // which has room for it only when T >= 2. Instrumented builds: schedules 0, 2 and 4.
+    int sched = T >= 2 ? g_fused_sched : 0;
     if (diag && sched != 2 && sched != 4) sched = 0;
-    auto go = [&](auto lg, auto x, auto d, auto sc) {
-        launch_rows_t<decltype(lg)::value, decltype(x)::value, decltype(d)::value, T, decltype(sc)::value>(
+    auto go = [&](auto lg, auto d, auto sc) {
+        launch_rows_t<decltype(lg)::value, true, decltype(d)::value, T, decltype(sc)::value>(
             grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
     };
     using TT = std::true_type;
@@ -1158,128 +757,75 @@ static void launch_rows(bool logmode, bool xl, dim3 grid, hipStream_t stream, co
     using S2 = std::integral_constant<int, (T >= 2 ? 2 : 0)>;
     using S3 = std::integral_constant<int, (T >= 2 ? 3 : 0)>;
     using S4 = std::integral_constant<int, (T >= 2 ? 4 : 0)>;
-
-    auto by_log = [&](auto x, auto d, auto sc) {
-        if (logmode) go(TT{}, x, d, sc); else go(FF{}, x, d, sc);
+    auto by_log = [&](auto d, auto sc) {
+        if (logmode) go(TT{}, d, sc); else go(FF{}, d, sc);
     };
-    if (!xl) {
-        if (diag) by_log(FF{}, TT{}, S0{}); else by_log(FF{}, FF{}, S0{});
-    } else if (diag) {
-        if (sched == 2) by_log(TT{}, TT{}, S2{});
-        else if (sched == 4) by_log(TT{}, TT{}, S4{});
-        else by_log(TT{}, TT{}, S0{});
-    } else {
-        switch (sched) {
-            case 1: by_log(TT{}, FF{}, S1{}); break;
-            case 2: by_log(TT{}, FF{}, S2{}); break;
-            case 3: by_log(TT{}, FF{}, S3{}); break;
-            case 4: by_log(TT{}, FF{}, S4{}); break;
-            default: by_log(TT{}, FF{}, S0{}); break;
-        }
+    if (diag) {
+        if (sched == 2) by_log(TT{}, S2{});
+        else if (sched == 4) by_log(TT{}, S4{});
+        else by_log(TT{}, S0{});
+        return;
+    }
+    switch (sched) {
+        case 1: by_log(FF{}, S1{}); break;
+        case 2: by_log(FF{}, S2{}); break;
+        case 3: by_log(FF{}, S3{}); break;
+        case 4: by_log(FF{}, S4{}); break;
+        default: by_log(FF{}, S0{}); break;
     }
 }
 
-static void launch_rows2(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
-                         int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
-                         double* Fpart, uint64_t* gran, int I, int J, SartState* st) {
-    static bool configured = false;
-    if (!configured) {
-        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows2<true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRows2LdsBytes), "hipFuncSetAttribute");
-        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows2<false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kRows2LdsBytes), "hipFuncSetAttribute");
-        configured = true;
+// Variant 3 slab width: 1024 * K columns, K the smallest power of two <= 8 giving at most 32 slabs.
+int fused_pick_k(int64_t ld) {
+    for (int K = 1; K <= 8; K *= 2) {
+        const int64_t wc = 1024 * (int64_t)K;
+        if (ld % wc != 0) return K > 1 ? K / 2 : 0;
+        if (ld / wc <= 32) return K;
     }
-    if (logmode)
-        hipLaunchKernelGGL((k_fused_sweep_rows2<true>), grid, dim3(kFused5Threads), kRows2LdsBytes, stream, A, ld,
-                           nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
-    else
-        hipLaunchKernelGGL((k_fused_sweep_rows2<false>), grid, dim3(kFused5Threads), kRows2LdsBytes, stream, A, ld,
-                           nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
+    return 8;
 }
 
-template <int K>
-static void launch_k(int variant, bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld,
-                     int64_t nrows, int64_t nrows_pad, const float* x, const float* ghat, const float* arow,
-                     float* partial, double* Fpart, uint64_t* gran, int I, int J, SartState* st) {
-    if (variant == 3)
-        launch_lds<K>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st);
-    else if (variant == 1)
-        launch_cfg<K, 8, 4, 2>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I,
-                               J, st);
-    else if (variant == 2 && K <= 4) {
-        if constexpr (K <= 4)
-            launch_cfg<K, 4, 8, 4>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart,
-                                   gran, I, J, st);
-    } else
-        launch_cfg<K, 8, 5, 3>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I,
-                               J, st);
+int fused_fpart_per_block(int variant) {
+    (void)variant;
+    return 1;
 }
-
-int fused_fpart_per_block(int variant) { return variant == 5 ? 2 : 1; }
 
 int fused_tile_rows(int K, int variant) {
-    if (variant == 4 || variant == 6) return K;  // K carries the rows per tile for variants 4 and 6
-    if (variant >= 4) return 4;
-    return (variant == 2 && K <= 4) ? 4 / K : 8 / K;
+    return variant == 6 ? K : 8 / K;  // variant 6: K carries the rows per tile; variant 3: 8 float4 per lane
 }
 
 void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows,
                         int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
                         double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt,
                         hipStream_t stream) {
-    if (variant < 4) {
-        if (K != 1 && K != 2 && K != 4 && K != 8) throw std::runtime_error("fused_sweep: K must be 1, 2, 4 or 8");
-        if (ld % (1024 * K) != 0 || ld / (1024 * K) != J)
-            throw std::runtime_error("fused_sweep: ld must equal J * 1024 * K");
-    }
-    const int T = fused_tile_rows(K, variant);
-    if (nrows_pad % T != 0) throw std::runtime_error("fused_sweep: padded rows must be a multiple of the tile");
-    if (J * T > kMaxGather) throw std::runtime_error("fused_sweep: too many slabs for the gather registers");
+    if (variant != 3 && variant != 6) throw std::runtime_error("fused_sweep: variant must be 6 or 3");
     const dim3 grid((unsigned)(I * J));
-    if (variant == 4 || variant == 5 || variant == 6) {
-        if (variant != 5 && T != 1 && T != 2 && T != 4)
-            throw std::runtime_error("fused_sweep v4/v6: rows per tile (K) must be 1, 2 or 4");
-        const int64_t slab = variant == 5 ? 2048 : 8192 / T;  // columns per workgroup
-        if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep v4-6: ld must equal J * slab");
-        if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v4-6: padded rows must be a multiple of 4");
-        if (J * 4 > kMaxGather) throw std::runtime_error("fused_sweep v4-6: too many slabs");
-        if (variant != 5 && J * T > kRowsGather) throw std::runtime_error("fused_sweep v4/v6: J * T > 256");
-        if (variant == 6 && (xcnt == nullptr || I % 8 != 0 || (I / 8) * J * 8 != I * J))
-            throw std::runtime_error("fused_sweep v6: needs the per-XCD ticket counters and I % 8 == 0");
-        if (variant == 4 || variant == 6) {
-#define SART_RT(TT)                                                                                              \
-    launch_rows<TT>(logmode, variant == 6, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, \
-                    gran, I, J, st, xcnt)
-            if (T == 1) SART_RT(1);
-            else if (T == 2) SART_RT(2);
-            else SART_RT(4);
-#undef SART_RT
-        } else
-            launch_rows2(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J,
-                         st);
+    if (variant == 6) {
+        const int T = K;
+        if (T != 1 && T != 2 && T != 4) throw std::runtime_error("fused_sweep v6: rows per tile (K) must be 1, 2 or 4");
+        const int64_t slab = 8192 / T;  // columns per workgroup
+        if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep v6: ld must equal J * slab");
+        if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v6: padded rows must be a multiple of 4");
+        if (J * T > kRowsGather) throw std::runtime_error("fused_sweep v6: J * T > 256");
+        if (xcnt == nullptr || I % 8 != 0) throw std::runtime_error("fused_sweep v6: needs the per-XCD ticket counters and I % 8 == 0");
+        if (T == 1) launch_rows<1>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
+        else if (T == 2) launch_rows<2>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
+        else launch_rows<4>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
         check_launch("k_fused_sweep_rows");
         return;
     }
+    if (K != 1 && K != 2 && K != 4 && K != 8) throw std::runtime_error("fused_sweep v3: K must be 1, 2, 4 or 8");
+    if (ld % (1024 * K) != 0 || ld / (1024 * K) != J) throw std::runtime_error("fused_sweep v3: ld must equal J * 1024 * K");
+    const int T = 8 / K;
+    if (nrows_pad % T != 0) throw std::runtime_error("fused_sweep v3: padded rows must be a multiple of the tile");
+    if (J * T > kMaxGather) throw std::runtime_error("fused_sweep v3: too many slabs for the gather registers");
     switch (K) {
-        case 1:
-            launch_k<1>(variant, logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
-                        I, J, st);
-            break;
-        case 2:
-            launch_k<2>(variant, logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
-                        I, J, st);
-            break;
-        case 4:
-            launch_k<4>(variant, logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
-                        I, J, st);
-            break;
-        case 8:
-            launch_k<8>(variant, logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
-                        I, J, st);
-            break;
+        case 1: launch_lds<1>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st); break;
+        case 2: launch_lds<2>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st); break;
+        case 4: launch_lds<4>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st); break;
+        default: launch_lds<8>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st); break;
     }
-    check_launch("k_fused_sweep");
+    check_launch("k_fused_sweep_lds");
 }
 
 // bf16-stored RTM: variant 6 only (XCD-local row groups, same geometry and exchange as fp32), schedule 4

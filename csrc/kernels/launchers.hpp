@@ -29,6 +29,7 @@ void launch_colsum_f64(const float* A, int64_t ld, int64_t nrows, int nsplit, do
 void launch_colsum_f64(const bf16_t* A, int64_t ld, int64_t nrows, int nsplit, double* partial, hipStream_t stream);
 // fp32 -> bf16, round to nearest even (n a multiple of 4)
 void launch_f32_to_bf16(const float* src, int64_t n, bf16_t* dst, hipStream_t stream);
+// Fout (optional): Fout[0] = sum of Fpart (fp32), Fout[1] = st->error (the sweep's error word, reduced with it)
 void launch_reduce_partials(const float* partial, int64_t ld, int nsplit, const float* scale, float* out,
                             const double* Fpart, int64_t nF, float* Fout, const SartState* st, hipStream_t stream);
 void launch_reduce_partials_f64(const double* partial, int64_t ld, int nsplit, double* out, hipStream_t stream);
@@ -40,11 +41,12 @@ void launch_init_solution(float* x, int64_t n, int64_t n_pad, const float* src_f
 void launch_penalty(bool logx, const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta,
                     const float* x, float* pen, const SartState* st, hipStream_t stream);
 void launch_decide(SartState* st, const float* Fslot, hipStream_t stream);
-// xcnt (optional): fused-sweep ticket counters to zero for the next sweep
+// xcnt (optional): fused-sweep ticket counters to zero for the next sweep; xprev (optional): receives x
+// before the update (rollback point of the NaN/Inf guard)
 void launch_update_linear(float* x, const float* d, const float* pen, int64_t n, const SartState* st,
-                          hipStream_t stream, unsigned* xcnt = nullptr);
+                          hipStream_t stream, unsigned* xcnt = nullptr, float* xprev = nullptr);
 void launch_update_log(float* x, const float* O, const float* Fv, const float* pen, float alpha, int64_t n,
-                       const SartState* st, hipStream_t stream, unsigned* xcnt = nullptr);
+                       const SartState* st, hipStream_t stream, unsigned* xcnt = nullptr, float* xprev = nullptr);
 void launch_state_begin(SartState* st, double G, double tol, int max_iter, hipStream_t stream);
 // w = a (ghat - f) (linear) or a f (log) from a complete forward projection f; Fpart[block] = sum f^2 (fp64)
 int weights_num_blocks(int64_t nrows_pad);

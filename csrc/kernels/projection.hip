@@ -243,8 +243,9 @@ __global__ __launch_bounds__(256) void k_f32_to_bf16(const float* __restrict__ s
 }
 
 // out[c] = scale[c] * sum_s partial[s][c]   (fixed summation order -> deterministic)
-// scale == nullptr means 1. Optionally also writes the sum of Fpart[0:nF] (fp64) to *Fout as
-// fp32, the value that is all-reduced with the correction vector (piggyback, one collective).
+// scale == nullptr means 1. Optionally also writes the sum of Fpart[0:nF] (fp64) to Fout[0] as
+// fp32, the value that is all-reduced with the correction vector (piggyback, one collective), and the
+// sweep's error word st->error to Fout[1] (so a protocol timeout on one rank reaches every rank's k_decide).
 __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ partial, int64_t ld, int nsplit,
                                                          const float* __restrict__ scale, float* __restrict__ out,
                                                          const double* __restrict__ Fpart, int64_t nF,
@@ -279,7 +280,10 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict
         acc = wave_sum(acc);
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
         __syncthreads();
-        if (threadIdx.x == 0) *Fout = (float)(((red[0] + red[1]) + red[2]) + red[3]);
+        if (threadIdx.x == 0) {
+            Fout[0] = (float)(((red[0] + red[1]) + red[2]) + red[3]);
+            Fout[1] = st != nullptr ? (float)st->error : 0.f;  // error word, all-reduced with ||A x||^2
+        }
     }
 }
 

@@ -22,6 +22,8 @@ namespace sart {
 constexpr float kEpsLog = 1e-7f;  // reference EPSILON_LOG_CUDA (sart_kernels.cu:17-19)
 
 // ghat = fp32(g / s); a = [ghat >= 0][len > tau_l] / len; gpos = max(ghat, 0); wo = a * ghat
+// A non-finite pixel (NaN / Inf from a broken detector channel) is masked like a saturated one (g < 0):
+// with a = 0 it contributes nothing; unmasked, 0 * NaN would turn every correction into NaN.
 __global__ __launch_bounds__(256) void k_prep_rows(const double* __restrict__ g, int64_t nrows, int64_t nrows_pad,
                                                    double inv_s, const float* __restrict__ ray_length,
                                                    float len_thres, float* __restrict__ ghat, float* __restrict__ arow,
@@ -30,7 +32,8 @@ __global__ __launch_bounds__(256) void k_prep_rows(const double* __restrict__ g,
     if (i >= nrows_pad) return;
     float gh = 0.f, a = 0.f;
     if (i < nrows) {
-        gh = (float)(g[i] * inv_s);
+        const double gv = g[i];
+        gh = isfinite(gv) ? (float)(gv * inv_s) : -1.f;
         const float len = ray_length[i];
         const float inv_len = (len > len_thres) ? 1.f / len : 0.f;
         a = (gh >= 0.f) ? inv_len : 0.f;
@@ -77,17 +80,31 @@ __global__ __launch_bounds__(256) void k_penalty_csr(const int64_t* __restrict__
 
 // Single lane. Consumes ||A x_s||^2 of sweep s and decides, exactly as the reference loop does
 // at its iteration s-1 (its forward projection after the update is our next sweep's forward).
+// Fslot[1] is the error word of the sweep, summed over the ranks by the same collective that carries
+// ||A x||^2 (k_reduce_partials writes the local SartState::error there): when ANY rank's persistent sweep
+// gave up, every rank stops the frame at this sweep and sees error bit 8, so the fallback decision is
+// identical on all ranks (a rank-local decision would leave its peers waiting in the next collective).
 __global__ void k_decide(SartState* __restrict__ st, const float* __restrict__ Fslot) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     if (st->done) return;
     const int s = st->sweep;
-    const double F = (double)(*Fslot);
+    const double F = (double)Fslot[0];
     st->F_last = F;
     int done = 0;
     int status = kRunning;
-    if (!isfinite(F)) {  // NaN/Inf guard: stop with the last finite iterate's status
+    if (Fslot[1] != 0.f) {
+        st->error |= 8;
+        st->sweep = s + 1;
+        st->status = kMaxIterationsExceeded;
+        st->done = 1;
+        st->epoch = st->epoch + 1;
+        return;
+    }
+    if (!isfinite(F)) {
+        // NaN/Inf guard: x_s produced a non-finite ||A x||^2. Stop; the engine returns the
+        // last finite iterate x_{s-1}, which the update kernels saved in xprev, so s - 1 updates count.
         st->flags |= 1;
-        st->iterations = s;
+        st->iterations = s > 0 ? s - 1 : 0;
         st->sweep = s + 1;
         st->status = kMaxIterationsExceeded;
         st->done = 1;
@@ -117,14 +134,19 @@ __global__ void k_decide(SartState* __restrict__ st, const float* __restrict__ F
 // x = max(x + d - pen, 0)
 // xcnt (optional): the per-XCD ticket counters of the next fused sweep (variant 6), zeroed here so the
 // sweep loop needs no separate memset launch per iteration (the sweep that used them has completed).
+// xprev (optional): receives the iterate before the update (the rollback point of the NaN/Inf guard);
+// one extra vector store per voxel, against a full pass over the shard per sweep.
 __global__ __launch_bounds__(256) void k_update_linear(float* __restrict__ x, const float* __restrict__ d,
                                                        const float* __restrict__ pen, int64_t n,
-                                                       const SartState* __restrict__ st, unsigned* __restrict__ xcnt) {
+                                                       const SartState* __restrict__ st, unsigned* __restrict__ xcnt,
+                                                       float* __restrict__ xprev) {
     if (xcnt && blockIdx.x == 0 && threadIdx.x < 16) xcnt[threadIdx.x] = 0u;
     if (st->done) return;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    float v = x[i] + d[i];
+    const float x0 = x[i];
+    if (xprev) xprev[i] = x0;
+    float v = x0 + d[i];
     if (pen) v -= pen[i];
     x[i] = (v > 0.f) ? v : 0.f;
 }
@@ -133,14 +155,16 @@ __global__ __launch_bounds__(256) void k_update_linear(float* __restrict__ x, co
 __global__ __launch_bounds__(256) void k_update_log(float* __restrict__ x, const float* __restrict__ O,
                                                     const float* __restrict__ Fv, const float* __restrict__ pen,
                                                     float alpha, int64_t n, const SartState* __restrict__ st,
-                                                    unsigned* __restrict__ xcnt) {
+                                                    unsigned* __restrict__ xcnt, float* __restrict__ xprev) {
     if (xcnt && blockIdx.x == 0 && threadIdx.x < 16) xcnt[threadIdx.x] = 0u;  // see k_update_linear
     if (st->done) return;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     float r = powf((O[i] + kEpsLog) / (Fv[i] + kEpsLog), alpha);
     if (pen) r *= expf(-pen[i]);
-    x[i] *= r;
+    const float x0 = x[i];
+    if (xprev) xprev[i] = x0;
+    x[i] = x0 * r;
 }
 
 // Device-side state initialisation for a new frame (keeps the epoch counter monotonic).
@@ -274,14 +298,14 @@ void launch_decide(SartState* st, const float* Fslot, hipStream_t stream) {
 }
 
 void launch_update_linear(float* x, const float* d, const float* pen, int64_t n, const SartState* st,
-                          hipStream_t stream, unsigned* xcnt) {
-    hipLaunchKernelGGL(k_update_linear, dim3(nb(n)), dim3(256), 0, stream, x, d, pen, n, st, xcnt);
+                          hipStream_t stream, unsigned* xcnt, float* xprev) {
+    hipLaunchKernelGGL(k_update_linear, dim3(nb(n)), dim3(256), 0, stream, x, d, pen, n, st, xcnt, xprev);
     check_launch("k_update_linear");
 }
 
 void launch_update_log(float* x, const float* O, const float* Fv, const float* pen, float alpha, int64_t n,
-                       const SartState* st, hipStream_t stream, unsigned* xcnt) {
-    hipLaunchKernelGGL(k_update_log, dim3(nb(n)), dim3(256), 0, stream, x, O, Fv, pen, alpha, n, st, xcnt);
+                       const SartState* st, hipStream_t stream, unsigned* xcnt, float* xprev) {
+    hipLaunchKernelGGL(k_update_log, dim3(nb(n)), dim3(256), 0, stream, x, O, Fv, pen, alpha, n, st, xcnt, xprev);
     check_launch("k_update_log");
 }
 

@@ -185,8 +185,8 @@ def run(cfg, intervals) -> int:
                                                   "device_comm": getattr(getattr(solver, "native_comm", None),
                                                                          "describe", "none"),
                                                   "driver": "python"}) + "\n")
-                if cfg.no_guess:
-                    solution = None
+                if cfg.no_guess or (getattr(res, "nonfinite", False) and not np.all(np.isfinite(solution))):
+                    solution = None  # cold start after a frame whose iterate stayed non-finite
         pool.shutdown()
         if rank == 0:
             writer.flush()

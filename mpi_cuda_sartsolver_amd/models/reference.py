@@ -6,7 +6,11 @@
   normalisation, the cold start uses the raw measurement including negative pixels, no clamp in the
   linear variant, 1e-100 clamp / epsilon in the logarithmic one.
 
-Both return (solution fp64, status, iterations) where iterations counts the updates applied.
+* :func:`sart_fp32_emulation` -- the GPU semantics evaluated in fp32 with numpy/BLAS sums: what an fp32
+  solver such as the reference's (cuBLAS Sgemv + fp32 atomics) produces up to summation order. Its distance
+  to the fp64 oracle is the inherent fp32 error of a problem; tests bound ours by a small multiple of it.
+
+All return (solution fp64, status, iterations) where iterations counts the updates applied.
 """
 from __future__ import annotations
 
@@ -103,3 +107,40 @@ def sart_cpu_semantics(A, g, L=None, *, logarithmic=False, ray_density_threshold
             return x, SUCCESS, it + 1
         conv_prev = conv
     return x, MAX_ITERATIONS_EXCEEDED, max_iterations
+
+
+def sart_fp32_emulation(A, g, L=None, *, logarithmic=False, ray_density_threshold=1e-6, ray_length_threshold=1e-6,
+                        beta_laplace=1e-2, relaxation=1.0, max_iterations=10, x_prev: Optional[np.ndarray] = None):
+    """Fixed-iteration GPU semantics with fp32 vectors and fp32 matrix products (no convergence test)."""
+    f32 = np.float32
+    A32 = np.asarray(A, dtype=f32)
+    g = np.asarray(g, dtype=np.float64)
+    norm = g.max()
+    if not norm > 0:
+        norm = 1.0
+    ghat = (g / norm).astype(f32)
+    rho = A32.astype(np.float64).sum(axis=0).astype(f32)
+    ell = A32.astype(np.float64).sum(axis=1).astype(f32)
+    dvalid = rho > f32(ray_density_threshold)
+    rho_s = np.where(dvalid, rho, f32(1))
+    inv_len = np.where(ell > f32(ray_length_threshold), f32(1) / np.where(ell > 0, ell, f32(1)), f32(0)).astype(f32)
+    a = np.where(ghat >= 0, inv_len, f32(0)).astype(f32)
+    scale = np.where(dvalid, f32(relaxation) / rho_s, f32(0)).astype(f32)
+    if x_prev is None:
+        x = np.where(dvalid, (A32.T @ np.maximum(ghat, f32(0))) / rho_s, f32(0)).astype(f32)
+    else:
+        x = (np.asarray(x_prev, dtype=np.float64) / norm).astype(f32)
+    x = np.maximum(x, f32(1e-7))
+    eps = f32(1e-7)
+    O = np.where(dvalid, A32.T @ (a * ghat), f32(0)).astype(f32) if logarithmic else None
+    for _ in range(max_iterations):
+        f = (A32 @ x).astype(f32)
+        if logarithmic:
+            pen = _penalty(L, x.astype(np.float64), beta_laplace, True).astype(f32)
+            Fv = np.where(dvalid, A32.T @ (a * f), f32(0)).astype(f32)
+            x = (x * ((O + eps) / (Fv + eps)) ** f32(relaxation) * np.exp(-pen)).astype(f32)
+        else:
+            pen = _penalty(L, x.astype(np.float64), beta_laplace, False).astype(f32)
+            d = (scale * (A32.T @ (a * (ghat - f)))).astype(f32)
+            x = np.maximum(x + d - pen, f32(0)).astype(f32)
+    return x.astype(np.float64) * norm, MAX_ITERATIONS_EXCEEDED, max_iterations

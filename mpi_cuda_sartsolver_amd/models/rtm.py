@@ -6,12 +6,11 @@ freed. Here the shard lives only in HBM: it is filled either on the device (synt
 streaming row blocks from HDF5 through a pinned staging buffer (``fill_rows``), so a 275 GB shard
 needs no 275 GB of host RAM.
 
-Layout: row-major fp32, ``nrows_pad x ld`` with zero padding. ``ld`` is chosen so the fused sweep can
-split the columns into J slabs of 1024*K floats (``fused_layout``); otherwise it is a multiple of 64.
+Layout: row-major fp32 (or bf16), ``nrows_pad x ld`` with zero padding. ``ld`` is chosen so the fused
+sweep can split the columns into slabs (``choose_ld``); otherwise it is a multiple of 64.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -32,65 +31,26 @@ class FusedGeometry:
 
 
 def choose_ld(nvoxel: int, max_waste: float = 0.10) -> int:
-    """Padded row length. Prefer a width that admits the fused-sweep slab geometry."""
-    if nvoxel >= 1024:
-        for K in (1, 2, 4, 8):
-            wc = 1024 * K
-            J = -(-nvoxel // wc)
-            if J <= 32 or K == 8:
-                ld = J * wc
-                if (ld - nvoxel) <= max_waste * nvoxel:
-                    return ld
-                break
-    return round_up(max(nvoxel, 64), 64)
+    """Padded row length (native ``sart::choose_ld``, csrc/engine/geometry.cpp: the single source of truth
+    for the engine, both drivers and this package): the variant 6 width with the lowest estimated time per
+    row, else a multiple of 8192 (variant 3), else the next multiple of 64."""
+    return int(hip().choose_ld(int(nvoxel), float(max_waste)))
 
 
 def fused_geometry(ld: int, num_cus: int, variant: int = 6, rows_per_tile: Optional[int] = None
                    ) -> Optional[FusedGeometry]:
-    """Persistent-grid geometry of the fused sweep (csrc/kernels/fused_sweep.hip).
+    """Persistent-grid geometry of the fused sweep (native ``sart::fused_geometry``).
 
     variant 6 (default): XCD-local row groups (L2 hand-offs); the four compute waves of a workgroup
     cover T rows x (4 / T) sub-slabs of 2048 columns, so a row is split over J = ld * T / 8192
-    workgroups (T = rows_per_tile or env SART_FUSED_T; default: the largest of 4, 2, 1 whose row group
-    fits an XCD -- 6.5-6.9 TB/s at 64k / 128k / 256k columns, profiles/probe_r1_fused_T.jsonl; variant 3
-    only beyond that). Variant 4: same kernel with blockIdx row groups.
-    Variant 5: 2048-column slabs, two exchange waves. Variants 0-3: slabs of 1024*K columns, K chosen
-    for <= 32 slabs (3: tiles parked in LDS). None: no fused path.
+    workgroups and each XCD runs G = (CUs per XCD) // J row groups (T = rows_per_tile or env
+    SART_FUSED_T, else the T with the lowest time per row). Variant 3: slabs of 1024*K columns, K chosen
+    for <= 32 slabs (the fallback). None: no fused path.
     """
-    if rows_per_tile is None and os.environ.get("SART_FUSED_T"):
-        rows_per_tile = int(os.environ["SART_FUSED_T"])
-    if variant in (4, 6):
-        per_xcd = num_cus // 8
-        for T in ((rows_per_tile,) if rows_per_tile else (4, 2, 1)):
-            slab = 8192 // T
-            if T not in (1, 2, 4) or ld % slab or ld // slab == 0:
-                continue
-            J = ld // slab
-            if variant == 6 and num_cus % 8 == 0 and per_xcd % J == 0:
-                I = 8 * (per_xcd // J)
-                return FusedGeometry(K=T, J=J, I=I, grid=I * J, variant=6, T=T)
-            if variant == 4 and J <= min(64, num_cus):
-                return FusedGeometry(K=T, J=J, I=max(1, num_cus // J), grid=max(1, num_cus // J) * J, variant=4, T=T)
-        variant = 3
-    if variant == 5:
-        if ld % 2048 == 0 and 0 < ld // 2048 <= min(64, num_cus):
-            J = ld // 2048
-            I = max(1, num_cus // J)
-            return FusedGeometry(K=8, J=J, I=I, grid=I * J, variant=variant, T=4)
-        variant = 3
-    for K in (1, 2, 4, 8):
-        wc = 1024 * K
-        if ld % wc:
-            continue
-        J = ld // wc
-        if J <= 32 or K == 8:
-            v = variant if (variant != 2 or K <= 4) else 3
-            T = (4 // K) if v == 2 else (8 // K)
-            if J > num_cus or J * T > 512:
-                return None
-            I = max(1, num_cus // J)
-            return FusedGeometry(K=K, J=J, I=I, grid=I * J, variant=v, T=T)
-    return None
+    g = hip().fused_geometry(int(ld), int(num_cus), int(variant), int(rows_per_tile or 0))
+    if not g.valid():
+        return None
+    return FusedGeometry(K=g.K, J=g.J, I=g.I, grid=g.grid, variant=g.variant, T=g.T)
 
 
 class DenseRTM:

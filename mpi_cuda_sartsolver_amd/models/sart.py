@@ -82,6 +82,9 @@ class SolveResult:
     used_fused: bool
     elapsed_ms: float = 0.0
     comm_ms: float = -1.0  # GPU time in the per-sweep all-reduces (time_collectives=True), else -1
+    fallbacks: int = 0      # persistent-sweep timeouts recovered in this solve (identical on every rank)
+    fused_variant: int = -1  # fused sweep variant that produced the result (-1: two-pass kernels)
+    nonfinite: bool = False  # stopped by the NaN/Inf guard: ``solution`` is the last finite iterate
 
 
 def _host_f64(v) -> np.ndarray:
@@ -158,6 +161,11 @@ class SARTSolver:
         return self.engine.use_fused
 
     @property
+    def shared_device(self) -> bool:
+        """Another rank of the group drives the same physical GPU (then the two-pass kernels are used)."""
+        return self.engine.shared_device
+
+    @property
     def geom(self):
         return self.engine.geometry if self.engine.use_fused else None
 
@@ -182,7 +190,9 @@ class SARTSolver:
         status = SUCCESS if info["status"] == SUCCESS else MAX_ITERATIONS_EXCEEDED
         return SolveResult(solution=x, status=status, iterations=int(info["iterations"]),
                            convergence=float(info["convergence"]), used_fused=bool(info["used_fused"]),
-                           elapsed_ms=float(info["ms"]), comm_ms=float(info["comm_ms"]))
+                           elapsed_ms=float(info["ms"]), comm_ms=float(info["comm_ms"]),
+                           fallbacks=int(info["fallbacks"]), fused_variant=int(info["fused_variant"]),
+                           nonfinite=bool(info["nonfinite"]))
 
     def gather_solution(self, x_local: np.ndarray) -> np.ndarray:
         """Full solution vector from the column shards of every rank (identity for a row shard)."""

@@ -1,0 +1,68 @@
+"""Fused-sweep geometry (csrc/engine/geometry.cpp) on the CPU: padded widths and persistent grids.
+
+The reference's kernels run at any voxel count (grid ceil(V/256), reference sart_kernels.cu:269-283;
+cublasSgemv takes any V, sartsolver_cuda.cpp:248-249). The fused sweep's fast variant 6 must therefore
+cover every width a real voxel grid produces, not only powers of two.
+"""
+import pytest
+
+from mpi_cuda_sartsolver_amd.models import rtm
+from mpi_cuda_sartsolver_amd.ops import hip
+
+CUS = 256  # MI355X: 8 XCDs x 32 CUs
+
+
+def _check_v6(ld, g):
+    assert g is not None and g.variant == 6
+    slab = 8192 // g.T
+    assert g.T in (1, 2, 4) and ld % slab == 0 and ld // slab == g.J
+    assert g.J <= CUS // 8 and g.J * g.T <= 256
+    assert g.I % 8 == 0 and g.grid == g.I * g.J <= CUS
+    assert g.I // 8 == (CUS // 8) // g.J  # as many row groups per XCD as fit
+
+
+@pytest.mark.parametrize("nvox", [20480, 30000, 60000, 61440, 65536, 70000, 100000, 131072, 150000, 200000,
+                                  229376, 262144])
+def test_every_width_gets_variant6(nvox):
+    ld = rtm.choose_ld(nvox)
+    assert nvox <= ld <= 1.10 * nvox
+    _check_v6(ld, rtm.fused_geometry(ld, CUS, 6))
+
+
+def test_width_sweep_variant6_and_waste():
+    for nvox in range(20480, 262145, 997):
+        ld = rtm.choose_ld(nvox)
+        assert ld % 64 == 0 and nvox <= ld <= 1.10 * nvox, nvox
+        _check_v6(ld, rtm.fused_geometry(ld, CUS, 6))
+
+
+@pytest.mark.parametrize("ld,T,J,I", [(65536, 4, 32, 8), (131072, 2, 32, 8), (262144, 1, 32, 8),
+                                      (61440, 4, 30, 8), (16384, 4, 8, 32)])
+def test_production_geometries(ld, T, J, I):
+    g = rtm.fused_geometry(ld, CUS, 6)
+    assert (g.T, g.J, g.I) == (T, J, I)
+
+
+def test_lowest_cost_rows_per_tile():
+    # 70000 columns: T = 2 needs J = 18 (one group per XCD, 18 of 32 CUs); T = 1 gives J = 9 and three
+    # groups per XCD (27 CUs), a lower time per row
+    ld = rtm.choose_ld(70000)
+    g = rtm.fused_geometry(ld, CUS, 6)
+    assert (ld, g.T, g.J, g.I) == (73728, 1, 9, 24)
+
+
+def test_forced_rows_per_tile_and_fallback():
+    g = rtm.fused_geometry(65536, CUS, 6, 1)
+    assert (g.T, g.J, g.I) == (1, 8, 32)
+    # wider than 32 slabs of 8192: variant 3 (K = 8)
+    g3 = rtm.fused_geometry(1 << 20, CUS, 6)
+    assert g3.variant == 3 and g3.K == 8 and g3.J == 128
+    assert rtm.fused_geometry(65536, CUS, 3).variant == 3
+    # not a multiple of 1024: no fused path
+    assert rtm.fused_geometry(64 * 1001, CUS, 6) is None
+
+
+def test_python_is_native():
+    k = hip()
+    for n in (1, 63, 64, 1000, 1024, 5000, 60000, 65536, 100000, 250000, 1 << 20):
+        assert rtm.choose_ld(n) == k.choose_ld(n)

@@ -104,3 +104,30 @@ def test_p2p_peer_abort_fails_fast(tmp_path):
     res = json.load(open(out))
     assert res["backend"] == "p2p" and res["first_ok"]
     assert "aborted" in res["error"] and res["nan"] and res["seconds"] < 30, res
+
+
+def test_shared_device_detected_from_identity(tmp_path):
+    """Ranks on one physical GPU are detected from the PCI bus id (not LOCAL_WORLD_SIZE, which only torchrun
+    sets) on every rank, and use the two-pass kernels even when the fused sweep is requested."""
+    x, m = _run(2, str(tmp_path / "s2"), ["--fused"], LOCAL_WORLD_SIZE="1")
+    assert all(r["shared"] and not r["fused"] for r in m[0]["ranks"]), m[0]["ranks"]
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_fused_timeout_on_one_rank_falls_back_on_all(tmp_path, nproc):
+    """A persistent-sweep timeout reported by ONE rank (device-side fault injection on rank 1) reaches every
+    rank through the error word of the per-sweep all-reduce: all ranks stop the frame at the same sweep,
+    fall back together (v6 -> v3 ...), re-solve, and the result matches the 1-rank solve. A rank-local
+    decision would leave the peers blocked in the next collective (round-1 advisor finding)."""
+    x1, m1 = _run(1, str(tmp_path / "r1"), ["--fused"])
+    assert m1[0]["fused"] and m1[0]["fallbacks"] == 0
+    x, m = _run(nproc, str(tmp_path / f"f{nproc}"), ["--fused"], SART_FUSED_SHARED="1", SART_FAULT_INJECT="1",
+                SART_FAULT_RANK="1")
+    ranks = m[0]["ranks"]
+    assert len(ranks) == nproc
+    assert ranks[0]["fallbacks"] >= 1, ranks
+    assert all((r["fallbacks"], r["variant"], r["fused"]) == (ranks[0]["fallbacks"], ranks[0]["variant"],
+                                                              ranks[0]["fused"]) for r in ranks), ranks
+    assert np.linalg.norm(x - x1) / np.linalg.norm(x1) < 2e-3
+    for a, b in zip(m, m1):
+        assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3

@@ -55,24 +55,3 @@ def test_tcp_comm_collectives(world):
         np.testing.assert_allclose(s, expect, rtol=1e-15)
         assert m == [world - 1.0, 0.0]
         assert b == b"hello from 1"
-
-
-def test_native_geometry_matches_python():
-    from mpi_cuda_sartsolver_amd.models import rtm
-    from mpi_cuda_sartsolver_amd.ops import hip
-
-    k = hip()
-    widths = [64, 1024, 2048, 4096, 6144, 8192, 16384, 24576, 32768, 61440, 65536, 131072, 262144, 1 << 20]
-    for ld in widths:
-        for cus in (256, 240, 304, 80):
-            for variant in (0, 1, 2, 3, 4, 5, 6):
-                for T in (None, 1, 2, 4):
-                    gp = rtm.fused_geometry(ld, cus, variant, T)
-                    gc = k.fused_geometry(ld, cus, variant, T or 0)
-                    if gp is None:
-                        assert not gc.valid(), (ld, cus, variant, T)
-                        continue
-                    assert (gc.K, gc.J, gc.I, gc.grid, gc.variant, gc.T) == (gp.K, gp.J, gp.I, gp.grid, gp.variant,
-                                                                            gp.T), (ld, cus, variant, T)
-    for n in (1, 63, 64, 1000, 1024, 5000, 60000, 65536, 100000, 250000):
-        assert k.choose_ld(n) == rtm.choose_ld(n), n

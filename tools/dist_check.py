@@ -57,8 +57,11 @@ def main():
         r2 = s.solve(prob.measurement, solution=r.solution)  # warm start path
         x = np.stack([s.gather_solution(r.solution), s.gather_solution(r2.solution)])
         meta = [dict(status=r.status, iterations=r.iterations, fused=r.used_fused, comm=s.native_comm.backend,
-                     comm_ms=r.comm_ms),
-                dict(status=r2.status, iterations=r2.iterations)]
+                     comm_ms=r.comm_ms, fallbacks=r.fallbacks, variant=r.fused_variant),
+                dict(status=r2.status, iterations=r2.iterations, fallbacks=r2.fallbacks)]
+        # every rank's fallback history: a persistent-sweep timeout must be handled identically everywhere
+        meta[0]["ranks"] = comm.all_gather_object(dict(fallbacks=r.fallbacks, variant=r.fused_variant,
+                                                       fused=r.used_fused, shared=s.shared_device))
     if comm.rank == 0:
         np.save(a.out + ".npy", x)
         with open(a.out + ".json", "w") as f:

@@ -32,13 +32,14 @@ def main():
         Fp = torch.zeros(2 * g.grid, dtype=torch.float64, device=dev)
         gran = torch.zeros(m.nrows_pad * g.J, dtype=torch.int64, device=dev)
         st = new_state(dev)
+        Fslot = torch.zeros(64, dtype=torch.float32, device=dev)  # [F, error word] read by decide
         xcnt = torch.zeros(16, dtype=torch.int32, device=dev)
         for flags in (2, 3):
             k.fused_set_debug(flags)
             times = []
             for rep in range(4):
                 k.state_begin(st.data_ptr(), 1.0, 0.0, 100, s)
-                k.decide(st.data_ptr(), Fp.data_ptr(), s)
+                k.decide(st.data_ptr(), Fslot.data_ptr(), s)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
                 xcnt.zero_()

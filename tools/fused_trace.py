@@ -41,6 +41,7 @@ def main():
     ghat = torch.rand(m.nrows_pad, device=dev)
     arow = torch.rand(m.nrows_pad, device=dev) * 1e-4
     st = new_state(dev)
+    Fslot = torch.zeros(64, dtype=torch.float32, device=dev)  # [F, error word] read by decide
     xcnt = torch.zeros(16, dtype=torch.int32, device=dev)
     for T, sched in ((4, 2), (4, 4)):
         g = fused_geometry(m.ld, ncu, 6, T)
@@ -58,7 +59,7 @@ def main():
         for rep in range(3):
             tr.zero_()
             k.state_begin(st.data_ptr(), 1.0, 0.0, 100, s)
-            k.decide(st.data_ptr(), Fp.data_ptr(), s)
+            k.decide(st.data_ptr(), Fslot.data_ptr(), s)
             xcnt.zero_()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()

@@ -52,14 +52,20 @@ for step in "$@"; do
                     --npix 524288 --nvox 262144 --iters 20 ;;
     benchlap) run bench_lap 600 python bench.py --steps 5 --warmup 1 --laplacian ;;
     probe) run probe 600 python tools/probe.py ;;
+    numerics) run numerics 600 python tools/numerics_check.py ;;
+    benchw) for v in 65536 60000 100000 200000 70000; do
+              run bench_w$v 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
+            done ;;
     trace) run fused_trace 600 python tools/fused_trace.py ;;
     probef) PROBE_FUSED_ONLY=1 run probe_fused 600 python tools/probe.py ;;
+    probew) PROBE_FUSED_ONLY=1 PROBE_CFGS=${PROBE_CFGS:-6:0:4,3:0:0} run probe_widths 600 python tools/probe.py \
+              16384x65536 16384x61440 16384x73728 8192x131072 8192x102400 4096x262144 4096x204800 ;;
     commcheck) for n in 2 4; do
                  SART_DIST_BACKEND=gloo SART_P2P=1 run comm_check_p2p_n$n 300 python -m torch.distributed.run --nnodes=1 \
                    --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29600 + n)) tools/comm_check.py \
                    --out "$OUT/comm_check_p2p_n$n.json" || exit 1
                done ;;
-    testsel) run pytest_sel 900 python -m pytest ${SEL:-tests} -m gpu -q -p no:cacheprovider ;;
+    testsel) run pytest_sel 900 python -u -m pytest ${SEL:-tests} -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     profbf16) run rocprof_bf16 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bf16" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --rtm-dtype bf16 &&
               run rocprof_bf16_pmc 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof_bf16_pmc" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --rtm-dtype bf16 ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 ;;

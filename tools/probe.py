@@ -69,6 +69,7 @@ def main():
         nb = k.forward_num_blocks(m.nrows_pad)
         Fp = torch.zeros(max(nb, 8192), dtype=torch.float64, device=dev)
         st = new_state(dev)
+        Fslot = torch.zeros(64, dtype=torch.float32, device=dev)  # [F, error word] read by decide
         k.state_begin(st.data_ptr(), 1.0, 0.0, 100, s)
 
         def fwd():
@@ -105,7 +106,7 @@ def main():
                 k.fused_set_schedule(sched if sched is not None else 4)
                 xcnt.zero_()
                 k.state_begin(st.data_ptr(), 1.0, 0.0, 100, s)
-                k.decide(st.data_ptr(), Fp.data_ptr(), s)  # sweep 0 -> epoch+1, not done
+                k.decide(st.data_ptr(), Fslot.data_ptr(), s)  # sweep 0 -> epoch+1, not done
                 k.fused_sweep(False, g.K, g.variant, m.A.data_ptr(), m.ld, P, m.nrows_pad, x.data_ptr(),
                               ghat.data_ptr(), arow.data_ptr(), part.data_ptr(), Fp.data_ptr(), gran.data_ptr(),
                               g.I, g.J, st.data_ptr(), xcnt.data_ptr(), s)
