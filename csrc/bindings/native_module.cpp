@@ -123,6 +123,27 @@ PYBIND11_MODULE(_sart_native, m) {
         },
         "Fill a caller-owned (e.g. pinned) host buffer", py::arg("sorted_files"), py::arg("rtm_name"),
         py::arg("nvoxel"), py::arg("row_begin"), py::arg("row_end"), py::arg("ptr"), py::arg("ld"));
+    py::class_<RtmReader>(m, "RtmReader")
+        .def(py::init<SortedRtmFiles, std::string, uint64_t, uint64_t, uint64_t>(), py::arg("sorted_files"),
+             py::arg("rtm_name"), py::arg("nvoxel"), py::arg("col_begin") = 0, py::arg("col_end") = 0)
+        .def_property_readonly("ncols", &RtmReader::ncols)
+        .def(
+            "read_ptr",
+            [](RtmReader& r, uint64_t r0, uint64_t r1, uintptr_t ptr, uint64_t ld) {
+                py::gil_scoped_release nogil;
+                r.read(r0, r1, reinterpret_cast<float*>(ptr), ld);
+            },
+            "Rows [r0, r1) x the column window into a caller-owned (e.g. pinned) host buffer", py::arg("row_begin"),
+            py::arg("row_end"), py::arg("ptr"), py::arg("ld"))
+        .def("read", [](RtmReader& r, uint64_t r0, uint64_t r1, py::array_t<float, py::array::c_style> out) {
+            auto bi = out.request(true);
+            if (bi.ndim != 2 || (uint64_t)bi.shape[0] < r1 - r0 || (uint64_t)bi.shape[1] < r.ncols())
+                throw std::invalid_argument("out must be float32 [rows, ld >= ncols]");
+            float* ptr = static_cast<float*>(bi.ptr);
+            const uint64_t ld = bi.shape[1];
+            py::gil_scoped_release nogil;
+            r.read(r0, r1, ptr, ld);
+        });
     m.def("read_laplacian", [](const std::string& path, uint64_t nvoxel) {
         LaplacianCOO L = read_laplacian(path, nvoxel);
         return py::make_tuple(arr(L.i), arr(L.j), arr(L.value));
@@ -342,8 +363,23 @@ PYBIND11_MODULE(_sart_native, m) {
                 c.all_reduce_host(p, n, op);
             }
             return out;
+        })
+        .def("all_reduce_host_f32", [](HostComm& c, py::array_t<float, py::array::c_style | py::array::forcecast> v,
+                                       ReduceOp op) {
+            py::array_t<float> out(v.size());
+            std::copy(v.data(), v.data() + v.size(), out.mutable_data());
+            float* p = out.mutable_data();
+            const size_t n = (size_t)v.size();
+            {
+                py::gil_scoped_release rel;
+                c.all_reduce_host(p, n, op);
+            }
+            return out;
         });
     m.def("local_host_comm", []() { return std::shared_ptr<HostComm>(make_local_host_comm()); });
+    m.def("mpi_host_comm", []() { return std::shared_ptr<HostComm>(make_mpi_host_comm()); });
+    m.def("mpi_library_version", &mpi_library_version);
+    m.def("mpi_launch_detected", &mpi_launch_detected);
     m.def("tcp_host_comm",
           [](int rank, int size, const std::string& host, int port, double timeout_s) {
               py::gil_scoped_release rel;

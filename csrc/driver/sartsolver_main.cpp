@@ -73,7 +73,7 @@ struct DeviceShard {
     }
 };
 
-// col0 / ncols: keep only that voxel block of every row (--partition_voxels; the rows are read whole).
+// col0 / ncols: only that voxel block of every row (--partition_voxels), read as a column hyperslab.
 std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0, uint64_t nrows, size_t block_bytes,
                                                uint64_t col0 = 0, uint64_t ncols = 0, bool bf16 = false) {
     auto sh = std::make_unique<DeviceShard>();
@@ -87,7 +87,8 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
     hip_ok(hipMalloc(&sh->A, bytes), "hipMalloc(RTM shard)");
     hip_ok(hipMemset(sh->A, 0, bytes), "hipMemset(RTM shard)");
     hip_ok(hipDeviceSynchronize(), "hipMemset sync");
-    const uint64_t V = in.nvoxel;
+    const uint64_t V = ncols;  // staging row length: the column window only
+    RtmReader reader(in.rtm_files, in.rtm_name, in.nvoxel, col0, col0 + ncols);
     const uint64_t rows_per_block = std::max<uint64_t>(1, std::min<uint64_t>(nrows, block_bytes / (4 * V)));
     float* buf[2] = {nullptr, nullptr};
     for (auto& b : buf) hip_ok(hipHostMalloc(reinterpret_cast<void**>(&b), rows_per_block * V * sizeof(float)), "hipHostMalloc");
@@ -101,7 +102,7 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
     bool ev_used[2] = {false, false};
     auto read_into = [&](float* b, uint64_t r0, uint64_t r1) {
         std::memset(b, 0, (r1 - r0) * V * sizeof(float));  // sparse COO rows are scattered into zeros
-        read_rtm_rows(in.rtm_files, in.rtm_name, V, row0 + r0, row0 + r1, b, V);
+        reader.read(row0 + r0, row0 + r1, b, V);  // one reader: sparse arrays are read once per shard
     };
     std::vector<std::pair<uint64_t, uint64_t>> blocks;
     for (uint64_t r = 0; r < nrows; r += rows_per_block) blocks.emplace_back(r, std::min(nrows, r + rows_per_block));
@@ -117,8 +118,8 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
             }
             const uint64_t r0 = blocks[k].first, nr = blocks[k].second - blocks[k].first;
             float* dst = bf16 ? stage.get() : static_cast<float*>(sh->A) + r0 * sh->ld;
-            hip_ok(hipMemcpy2DAsync(dst, sh->ld * sizeof(float), cur + col0, V * sizeof(float),
-                                    ncols * sizeof(float), nr, hipMemcpyHostToDevice, s),
+            hip_ok(hipMemcpy2DAsync(dst, sh->ld * sizeof(float), cur, V * sizeof(float), ncols * sizeof(float), nr,
+                                    hipMemcpyHostToDevice, s),
                    "H2D RTM block");
             if (bf16)  // stream-ordered: the next block's copy into the staging rows waits for this conversion
                 launch_f32_to_bf16(stage.get(), (int64_t)nr * sh->ld, static_cast<bf16_t*>(sh->A) + r0 * sh->ld, s);
@@ -224,8 +225,8 @@ int main(int argc, char** argv) {
                                            cfg.rtm_bf16);
             else {
                 hshard.assign(blk.size * in.nvoxel, 0.f);
-                read_rtm_rows(in.rtm_files, in.rtm_name, in.nvoxel, blk.offset, blk.offset + blk.size, hshard.data(),
-                              in.nvoxel);
+                RtmReader(in.rtm_files, in.rtm_name, in.nvoxel)
+                    .read(blk.offset, blk.offset + blk.size, hshard.data(), in.nvoxel);
             }
         };
         if (cfg.parallel_read || size == 1) {

@@ -173,9 +173,14 @@ std::vector<int32_t> h5_read_i32(hid_t loc, const std::string& path) { return re
 
 void h5_read_rows_f32(hid_t dset, uint64_t row0, uint64_t nrows, uint64_t ncols, float* out, uint64_t ld,
                       uint64_t col0) {
-    if (nrows == 0) return;
+    h5_read_block_f32(dset, row0, nrows, 0, ncols, out, ld, col0);
+}
+
+void h5_read_block_f32(hid_t dset, uint64_t row0, uint64_t nrows, uint64_t fcol0, uint64_t ncols, float* out,
+                       uint64_t ld, uint64_t col0) {
+    if (nrows == 0 || ncols == 0) return;
     H5Id fsp(H5Dget_space(dset), H5Id::kSpace);
-    hsize_t foff[2] = {row0, 0}, fcnt[2] = {nrows, ncols};
+    hsize_t foff[2] = {row0, fcol0}, fcnt[2] = {nrows, ncols};
     check(H5Sselect_hyperslab(fsp, H5S_SELECT_SET, foff, nullptr, fcnt, nullptr), "selecting RTM rows");
     hsize_t mdims[2] = {nrows, ld};
     H5Id msp(H5Screate_simple(2, mdims, nullptr), H5Id::kSpace);

@@ -83,6 +83,10 @@ std::vector<int32_t> h5_read_i32(hid_t loc, const std::string& path);
 // column offset col0 inside each output row).
 void h5_read_rows_f32(hid_t dset, uint64_t row0, uint64_t nrows, uint64_t ncols, float* out, uint64_t ld,
                       uint64_t col0);
+// Rows [row0, +nrows) x file columns [fcol0, +ncols) of a 2-D float dataset into out (row stride ld, at
+// memory column col0): one hyperslab per call.
+void h5_read_block_f32(hid_t dset, uint64_t row0, uint64_t nrows, uint64_t fcol0, uint64_t ncols, float* out,
+                       uint64_t ld, uint64_t col0);
 // One [1, H, W] slab of a 3-D dataset as doubles.
 void h5_read_frame_f64(hid_t dset, uint64_t index, double* out, uint64_t frame_size);
 

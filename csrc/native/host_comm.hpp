@@ -48,9 +48,11 @@ EnvWorld env_world();
 std::unique_ptr<HostComm> make_local_host_comm();
 std::unique_ptr<HostComm> make_tcp_host_comm(int rank, int size, const std::string& host, int port,
                                              double timeout_s = 3600.0);
-// MPI_COMM_WORLD through a run-time loaded libmpi (MPICH ABI; host_comm_mpi.cpp).
+// MPI_COMM_WORLD through a run-time loaded libmpi (MPICH or Open MPI ABI, detected; host_comm_mpi.cpp).
 std::unique_ptr<HostComm> make_mpi_host_comm();
-// SART_HOST_COMM=mpi, or an MPICH-family launcher (PMI_SIZE > 1 without torchrun's RANK).
+// MPI_Get_library_version of the loaded libmpi (loads it).
+std::string mpi_library_version();
+// SART_HOST_COMM=mpi, or an MPI launcher (PMI_SIZE or OMPI_COMM_WORLD_SIZE > 1 without torchrun's RANK).
 bool mpi_launch_detected();
 // MPI when mpi_launch_detected(); else local for one rank, TCP otherwise (SART_HOST_COMM=tcp forces TCP).
 std::unique_ptr<HostComm> host_comm_from_env(double timeout_s = 3600.0);

@@ -265,14 +265,50 @@ bool rtm_has_sparse(const SortedRtmFiles& sorted, const std::string& rtm_name) {
     return false;
 }
 
-void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, uint64_t nvoxel, uint64_t row_begin,
-                   uint64_t row_end, float* out, uint64_t ld) {
+RtmReader::RtmReader(SortedRtmFiles sorted, std::string rtm_name, uint64_t nvoxel, uint64_t col_begin,
+                     uint64_t col_end)
+    : sorted_(std::move(sorted)), name_(std::move(rtm_name)), nvoxel_(nvoxel), c0_(col_begin),
+      c1_(col_end == 0 ? nvoxel : col_end) {
+    if (c0_ > c1_ || c1_ > nvoxel_) throw Error("RtmReader: column window outside [0, nvoxel)");
+}
+
+const RtmReader::SparseSegment& RtmReader::sparse_segment(int64_t f, const std::string& path, uint64_t nvox_seg) {
+    auto it = sparse_.find(path);
+    if (it != sparse_.end()) return it->second;
+    // read the COO arrays of this segment ONCE and order them by pixel, so every row block finds its
+    // entries with a binary search (the reference re-reads and filters the whole arrays per shard,
+    // raytransfer.cpp:67-91; a per-block re-read would cost O(blocks x nnz))
+    const std::string grp = "rtm/" + name_;
+    const auto pix = h5_read_u64(f, grp + "/pixel_index");
+    const auto vox = h5_read_u64(f, grp + "/voxel_index");
+    const auto val = h5_read_f32(f, grp + "/value");
+    if (pix.size() != val.size() || vox.size() != val.size())
+        throw Error("Inconsistent sparse RTM arrays in " + path + ".");
+    std::vector<size_t> order(val.size());
+    for (size_t n = 0; n < order.size(); ++n) {
+        if (vox[n] >= nvox_seg) throw Error("Sparse RTM voxel index out of range in " + path + ".");
+        order[n] = n;
+    }
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return pix[a] < pix[b]; });
+    SparseSegment seg;
+    seg.pix.reserve(order.size());
+    seg.vox.reserve(order.size());
+    seg.val.reserve(order.size());
+    for (size_t n : order) {
+        seg.pix.push_back(pix[n]);
+        seg.vox.push_back(vox[n]);
+        seg.val.push_back(val[n]);
+    }
+    return sparse_.emplace(path, std::move(seg)).first->second;
+}
+
+void RtmReader::read(uint64_t row_begin, uint64_t row_end, float* out, uint64_t ld) {
     SART_H5_LOCK;
     if (row_end <= row_begin) return;
-    if (ld < nvoxel) throw Error("read_rtm_rows: ld < nvoxel");
-    const std::string grp = "rtm/" + rtm_name;
+    if (ld < c1_ - c0_) throw Error("read_rtm_rows: ld smaller than the column window");
+    const std::string grp = "rtm/" + name_;
     uint64_t start_pixel = 0;
-    for (const auto& [cam, files] : sorted) {
+    for (const auto& [cam, files] : sorted_) {
         uint64_t npix;
         {
             H5Id f0 = h5_open_file(files.front());
@@ -286,31 +322,37 @@ void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, ui
             for (const auto& path : files) {
                 H5Id f = h5_open_file(path);
                 const uint64_t nvox_seg = h5_attr_u64(f, "rtm", "nvoxel");
-                if (start_voxel + nvox_seg > nvoxel) throw Error("RTM segments exceed the total number of voxels.");
-                const int64_t sparse = h5_attr_i64(f, grp, "is_sparse");
-                if (sparse) {
-                    const auto pix = h5_read_u64(f, grp + "/pixel_index");
-                    const auto vox = h5_read_u64(f, grp + "/voxel_index");
-                    const auto val = h5_read_f32(f, grp + "/value");
-                    if (pix.size() != val.size() || vox.size() != val.size())
-                        throw Error("Inconsistent sparse RTM arrays in " + path + ".");
-                    for (size_t n = 0; n < val.size(); ++n) {
-                        if (pix[n] < lr0 || pix[n] >= lr1) continue;
-                        if (vox[n] >= nvox_seg) throw Error("Sparse RTM voxel index out of range in " + path + ".");
-                        const uint64_t row = start_pixel + pix[n] - row_begin;
-                        out[row * ld + start_voxel + vox[n]] = val[n];
-                    }
-                } else {
-                    H5Id d = h5_open_dataset(f, grp + "/value");
-                    const auto dims = h5_dims(d);
-                    if (dims.size() != 2 || dims[0] != npix || dims[1] != nvox_seg)
-                        throw Error("Dense RTM dataset in " + path + " has unexpected shape.");
-                    // row blocks of <= 64 MiB per hyperslab read (the reference reads one row per call,
-                    // raytransfer.cpp:103-109)
-                    const uint64_t rows_per_read = std::max<uint64_t>(1, (64ull << 20) / (4 * std::max<uint64_t>(1, nvox_seg)));
-                    for (uint64_t r = lr0; r < lr1; r += rows_per_read) {
-                        const uint64_t n = std::min(rows_per_read, lr1 - r);
-                        h5_read_rows_f32(d, r, n, nvox_seg, out + (start_pixel + r - row_begin) * ld, ld, start_voxel);
+                if (start_voxel + nvox_seg > nvoxel_) throw Error("RTM segments exceed the total number of voxels.");
+                // this segment's columns inside the window [c0, c1): segment-local [s0, s1)
+                const uint64_t s0 = std::max(c0_, start_voxel) - start_voxel;
+                const uint64_t s1 = std::min(c1_, start_voxel + nvox_seg) > start_voxel
+                                        ? std::min(c1_, start_voxel + nvox_seg) - start_voxel
+                                        : 0;
+                if (s1 > s0) {
+                    const uint64_t ocol = start_voxel + s0 - c0_;  // output column of segment column s0
+                    if (h5_attr_i64(f, grp, "is_sparse")) {
+                        const SparseSegment& seg = sparse_segment(f, path, nvox_seg);
+                        auto lo = std::lower_bound(seg.pix.begin(), seg.pix.end(), lr0);
+                        auto hi = std::lower_bound(lo, seg.pix.end(), lr1);
+                        for (size_t n = (size_t)(lo - seg.pix.begin()); n < (size_t)(hi - seg.pix.begin()); ++n) {
+                            const uint64_t v = seg.vox[n];
+                            if (v < s0 || v >= s1) continue;
+                            const uint64_t row = start_pixel + seg.pix[n] - row_begin;
+                            out[row * ld + ocol + (v - s0)] = seg.val[n];
+                        }
+                    } else {
+                        H5Id d = h5_open_dataset(f, grp + "/value");
+                        const auto dims = h5_dims(d);
+                        if (dims.size() != 2 || dims[0] != npix || dims[1] != nvox_seg)
+                            throw Error("Dense RTM dataset in " + path + " has unexpected shape.");
+                        // row blocks of <= 64 MiB per hyperslab read, only the window's columns (the reference
+                        // reads one whole row per call, raytransfer.cpp:103-109)
+                        const uint64_t nc = s1 - s0;
+                        const uint64_t rows_per_read = std::max<uint64_t>(1, (64ull << 20) / (4 * nc));
+                        for (uint64_t r = lr0; r < lr1; r += rows_per_read) {
+                            const uint64_t n = std::min(rows_per_read, lr1 - r);
+                            h5_read_block_f32(d, r, n, s0, nc, out + (start_pixel + r - row_begin) * ld, ld, ocol);
+                        }
                     }
                 }
                 start_voxel += nvox_seg;
@@ -319,6 +361,11 @@ void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, ui
         start_pixel = cam_end;
         if (start_pixel >= row_end) break;
     }
+}
+
+void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, uint64_t nvoxel, uint64_t row_begin,
+                   uint64_t row_end, float* out, uint64_t ld) {
+    RtmReader(sorted, rtm_name, nvoxel).read(row_begin, row_end, out, ld);
 }
 
 LaplacianCOO read_laplacian(const std::string& path, uint64_t expected_nvoxel) {
@@ -391,6 +438,8 @@ std::map<std::string, std::pair<uint64_t, uint64_t>> read_rtm_frame_shapes(const
 SortedImageFiles sort_image_files(const std::vector<std::string>&) { nohdf5(); }
 void check_rtm_image_consistency(const SortedRtmFiles&, const SortedImageFiles&, const std::string&, double) { nohdf5(); }
 std::pair<uint64_t, uint64_t> get_total_rtm_size(const SortedRtmFiles&) { nohdf5(); }
+RtmReader::RtmReader(SortedRtmFiles, std::string, uint64_t, uint64_t, uint64_t) { nohdf5(); }
+void RtmReader::read(uint64_t, uint64_t, float*, uint64_t) { nohdf5(); }
 void read_rtm_rows(const SortedRtmFiles&, const std::string&, uint64_t, uint64_t, uint64_t, float*, uint64_t) { nohdf5(); }
 bool rtm_has_sparse(const SortedRtmFiles&, const std::string&) { nohdf5(); }
 LaplacianCOO read_laplacian(const std::string&, uint64_t) { nohdf5(); }

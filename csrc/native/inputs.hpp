@@ -35,10 +35,31 @@ void check_rtm_image_consistency(const SortedRtmFiles& rtm, const SortedImageFil
                                  const std::string& rtm_name, double wavelength_threshold);
 std::pair<uint64_t, uint64_t> get_total_rtm_size(const SortedRtmFiles& sorted);
 
-// Reads global RTM rows [row_begin, row_end) (cameras concatenated in name order, voxel segments
-// concatenated along the columns) into out[(r - row_begin) * ld + v]. Dense datasets are read as
-// row blocks with one hyperslab per block, sparse (COO) datasets are scattered. Rows of `out` must
-// be zero-initialised by the caller when sparse data is present.
+// Streaming reader of the global RTM (cameras concatenated in name order along the rows, voxel segments
+// concatenated along the columns), restricted to the column window [col_begin, col_end) (a voxel-column
+// shard reads only its block; col_end 0 = nvoxel). read(r0, r1, out, ld) writes rows [r0, r1) x the window
+// into out[(r - r0) * ld + (v - col_begin)]: dense datasets as row blocks with one hyperslab per block (only
+// the window's columns), sparse (COO) datasets scattered from arrays read ONCE per segment and kept sorted
+// by pixel. Rows of `out` must be zero-initialised by the caller when sparse data is present.
+class RtmReader {
+   public:
+    RtmReader(SortedRtmFiles sorted, std::string rtm_name, uint64_t nvoxel, uint64_t col_begin = 0,
+              uint64_t col_end = 0);
+    void read(uint64_t row_begin, uint64_t row_end, float* out, uint64_t ld);
+    uint64_t ncols() const { return c1_ - c0_; }
+
+   private:
+    struct SparseSegment {
+        std::vector<uint64_t> pix, vox;
+        std::vector<float> val;
+    };
+    const SparseSegment& sparse_segment(int64_t f, const std::string& path, uint64_t nvox_seg);  // f: hid_t
+    SortedRtmFiles sorted_;
+    std::string name_;
+    uint64_t nvoxel_ = 0, c0_ = 0, c1_ = 0;
+    std::map<std::string, SparseSegment> sparse_;
+};
+// One-shot read of whole rows (all columns).
 void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, uint64_t nvoxel, uint64_t row_begin,
                    uint64_t row_end, float* out, uint64_t ld);
 bool rtm_has_sparse(const SortedRtmFiles& sorted, const std::string& rtm_name);

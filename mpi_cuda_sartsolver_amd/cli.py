@@ -98,9 +98,9 @@ def run(cfg, intervals) -> int:
                 return hdf5.load_rtm_shard(inputs, 0, inputs.npixel, device, col_offset=vblock.offset,
                                            ncols=vblock.size)
             if use_gpu:
-                rtm = hdf5.load_rtm_shard(inputs, block.offset, block.size, device)
-                # --rtm_bf16: bf16-stored shard (native RNE rounding; the fp32 copy is released)
-                return rtm.to_bf16() if getattr(cfg, "rtm_bf16", False) else rtm
+                # --rtm_bf16: each streamed block is rounded into the bf16 shard (native RNE conversion)
+                return hdf5.load_rtm_shard(inputs, block.offset, block.size, device,
+                                           storage="bf16" if getattr(cfg, "rtm_bf16", False) else "fp32")
             return hdf5.read_rtm_rows(inputs, block.offset, block.stop)
 
         if cfg.parallel_read or world == 1:

@@ -56,22 +56,28 @@ def validate_inputs(input_files, rtm_name: str = "with_reflections", wavelength_
                     has_sparse=bool(n.rtm_has_sparse(sorted_rtm, rtm_name)))
 
 
-def read_rtm_rows(inputs: InputSet, row_begin: int, row_end: int, ld: Optional[int] = None) -> np.ndarray:
-    """Host copy of global RTM rows [row_begin, row_end) (tests, CPU path)."""
-    ld = ld or inputs.nvoxel
+def read_rtm_rows(inputs: InputSet, row_begin: int, row_end: int, ld: Optional[int] = None, col_begin: int = 0,
+                  col_end: Optional[int] = None) -> np.ndarray:
+    """Host copy of global RTM rows [row_begin, row_end) x columns [col_begin, col_end) (tests, CPU path)."""
+    col_end = inputs.nvoxel if col_end is None else int(col_end)
+    ld = ld or (col_end - col_begin)
     out = np.zeros((row_end - row_begin, ld), dtype=np.float32)
-    native().read_rtm_rows(inputs.rtm_files, inputs.rtm_name, inputs.nvoxel, row_begin, row_end, out)
+    native().RtmReader(inputs.rtm_files, inputs.rtm_name, inputs.nvoxel, col_begin, col_end).read(row_begin, row_end,
+                                                                                                  out)
     return out
 
 
 def load_rtm_shard(inputs: InputSet, row_offset: int, npixel_local: int, device, ld: Optional[int] = None,
-                   block_bytes: int = 256 << 20, col_offset: int = 0, ncols: Optional[int] = None):
+                   block_bytes: int = 256 << 20, col_offset: int = 0, ncols: Optional[int] = None,
+                   storage: str = "fp32"):
     """Stream this rank's RTM rows into a device-resident ``DenseRTM``; with ``col_offset`` / ``ncols`` only
-    that voxel block of every row is kept (column shard: the rows are still read whole).
+    that voxel block of every row is read (column hyperslabs: a column shard reads 1/N of the file).
 
-    Two pinned host buffers alternate: while block k is copied host->HBM (async on the current
-    stream), block k+1 is read from HDF5 by a helper thread (the native reader releases the GIL).
-    Peak host memory is 2 * block_bytes regardless of the shard size.
+    Two pinned host buffers alternate: while block k is copied host->HBM (async on the current stream),
+    block k+1 is read from HDF5 by a helper thread (the native reader releases the GIL; sparse segments are
+    read once per shard). Peak host memory is 2 * block_bytes regardless of the shard size. ``storage``
+    "bf16": each block is rounded into the bf16 shard on the device through an fp32 staging block, so peak
+    HBM is the bf16 shard plus one block (never the fp32 shard).
     """
     import torch
 
@@ -80,16 +86,19 @@ def load_rtm_shard(inputs: InputSet, row_offset: int, npixel_local: int, device,
     n = native()
     V = inputs.nvoxel
     nc = V - col_offset if ncols is None else int(ncols)
-    rtm = DenseRTM(npixel_local, nc, row_offset, device=device, ld=ld, col_offset=col_offset, nvoxel_total=V)
+    reader = n.RtmReader(inputs.rtm_files, inputs.rtm_name, V, col_offset, col_offset + nc)
+    rtm = DenseRTM(npixel_local, nc, row_offset, device=device, ld=ld, col_offset=col_offset, nvoxel_total=V,
+                   storage=storage)
     rtm.A.zero_()
-    rows_per_block = max(1, min(npixel_local, block_bytes // (4 * V)))
-    bufs = [torch.empty((rows_per_block, V), dtype=torch.float32).pin_memory() for _ in range(2)]
+    rows_per_block = max(1, min(npixel_local, block_bytes // (4 * nc)))
+    bufs = [torch.empty((rows_per_block, nc), dtype=torch.float32).pin_memory() for _ in range(2)]
+    stage = (torch.zeros((rows_per_block, rtm.ld), dtype=torch.float32, device=device) if rtm.is_bf16 else None)
     events = [None, None]
     stream = torch.cuda.current_stream(device)
 
     def read_into(buf, r0, r1):
         buf[: r1 - r0].zero_()
-        n.read_rtm_rows_ptr(inputs.rtm_files, inputs.rtm_name, V, row_offset + r0, row_offset + r1, buf.data_ptr(), V)
+        reader.read_ptr(row_offset + r0, row_offset + r1, buf.data_ptr(), nc)
 
     blocks = [(r, min(npixel_local, r + rows_per_block)) for r in range(0, npixel_local, rows_per_block)]
     if not blocks:
@@ -97,19 +106,23 @@ def load_rtm_shard(inputs: InputSet, row_offset: int, npixel_local: int, device,
     read_into(bufs[0], *blocks[0])
     for k, (r0, r1) in enumerate(blocks):
         cur = bufs[k % 2]
-        reader = None
+        reader_thread = None
         if k + 1 < len(blocks):
             nxt = bufs[(k + 1) % 2]
             if events[(k + 1) % 2] is not None:
                 events[(k + 1) % 2].synchronize()  # the copy that last used this buffer is done
-            reader = threading.Thread(target=read_into, args=(nxt, *blocks[k + 1]))
-            reader.start()
-        rtm.A[r0:r1, :nc].copy_(cur[: r1 - r0, col_offset: col_offset + nc], non_blocking=True)
+            reader_thread = threading.Thread(target=read_into, args=(nxt, *blocks[k + 1]))
+            reader_thread.start()
+        if stage is None:
+            rtm.A[r0:r1, :nc].copy_(cur[: r1 - r0], non_blocking=True)
+        else:  # stream-ordered: the next block's copy into the staging rows waits for this conversion
+            stage[: r1 - r0, :nc].copy_(cur[: r1 - r0], non_blocking=True)
+            rtm._store_rows(r0, stage[: r1 - r0])
         ev = torch.cuda.Event()
         ev.record(stream)
         events[k % 2] = ev
-        if reader is not None:
-            reader.join()
+        if reader_thread is not None:
+            reader_thread.join()
     torch.cuda.synchronize(device)
     return rtm
 
