@@ -238,22 +238,29 @@ static void bind_engine(py::module_& m) {
                 py::array_t<float, py::array::c_style | py::array::forcecast> val) {
                  e.set_laplacian(rp.data(), col.data(), val.data(), (int64_t)val.size());
              })
-        .def("solve_batch", [](sart::MultiFrameEngine& e, f64arr g) {
+        .def("solve_batch", [](sart::MultiFrameEngine& e, f64arr g, py::object x0, bool chain) {
             if (g.ndim() != 2 || g.shape(1) != e.nrows())
                 throw py::value_error("measurements must be [nframes, nrows of the local shard]");
             const int nf = (int)g.shape(0);
+            f64arr x0a;
+            const double* x0p = nullptr;
+            if (!x0.is_none()) {
+                x0a = x0.cast<f64arr>();
+                if ((int64_t)x0a.size() != e.nvoxel()) throw py::value_error("x0 must have nvoxel elements");
+                x0p = x0a.data();
+            }
             py::array_t<double> x({(py::ssize_t)nf, (py::ssize_t)e.nvoxel()});
             double* xp = x.mutable_data();
             const double* gp = g.data();
             std::vector<sart::SolveInfo> infos;
             {
                 py::gil_scoped_release rel;
-                infos = e.solve_batch(gp, nf, xp);
+                infos = e.solve_batch(gp, nf, xp, x0p, chain);
             }
             py::list li;
             for (const auto& i : infos) li.append(solve_info(i));
             return py::make_tuple(x, li);
-        });
+        }, py::arg("g"), py::arg("x0") = py::none(), py::arg("chain") = false);
 }
 
 PYBIND11_MODULE(_sart_hip, m) {

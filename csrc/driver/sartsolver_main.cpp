@@ -15,8 +15,8 @@
 //   * a fatal error on any rank aborts the communicators instead of leaving peers blocked in a
 //     collective (the reference calls std::exit on one rank).
 // Extensions: --resume, --two_pass, --profile FILE (JSON lines per frame: iterations, convergence, it/s,
-// GFLOPS, RTM GB/s, GPU time in the all-reduces, communicators), --batch_frames N (N independent
-// frames solved together by the multi-frame MFMA engine, cold-started like --no_guess).
+// GFLOPS, RTM GB/s, GPU time in the all-reduces, communicators), --batch_frames N (N
+// frames solved together by the multi-frame MFMA engine; batches warm-start from the previous batch).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -307,8 +307,11 @@ int main(int argc, char** argv) {
         for (uint64_t i = 0; i < image.nframe(); ++i)
             if (image.frame_time(i) > skip_until + 1e-12) frames.push_back(i);
         if (batched) {
-            // --batch_frames N: independent frames solved together (cold start each, like --no_guess)
+            // --batch_frames N: N frames solved together on the matrix cores. Without --no_guess the batches form
+            // a warm-started time series (every frame of batch k + 1 starts from batch k's last solution, the first
+            // batch from the resumed solution or cold); with --no_guess every frame cold-starts.
             const size_t nb = (size_t)cfg.batch_frames;
+            std::vector<double> bwarm = cfg.no_guess ? std::vector<double>() : warm;
             auto read_chunk = [&image, &frames, nb, P = blk.size](size_t c0) {
                 std::vector<double> g;
                 for (size_t k = c0; k < std::min(frames.size(), c0 + nb); ++k) {
@@ -326,7 +329,13 @@ int main(int argc, char** argv) {
                 const int B = (int)std::min(nb, frames.size() - c0);
                 std::vector<double> xb((size_t)B * in.nvoxel);
                 const auto t0 = std::chrono::steady_clock::now();
-                const std::vector<SolveInfo> infos = mf->solve_batch(g.data(), B, xb.data());
+                const std::vector<SolveInfo> infos =
+                    mf->solve_batch(g.data(), B, xb.data(), bwarm.empty() ? nullptr : bwarm.data());
+                if (!cfg.no_guess) {
+                    bwarm.assign(xb.end() - (std::ptrdiff_t)in.nvoxel, xb.end());
+                    if (!std::all_of(bwarm.begin(), bwarm.end(), [](double v) { return std::isfinite(v); }))
+                        bwarm.clear();
+                }
                 const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 if (rank == 0) {
                     for (int f = 0; f < B; ++f) {

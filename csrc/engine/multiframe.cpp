@@ -33,13 +33,15 @@ MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, in
     set_device();
     hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
     hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hstate_), sizeof(MfState)), "hipHostMalloc");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hstate_), 2 * sizeof(MfState)), "hipHostMalloc");
+    for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hg_), std::max<int64_t>(P_, 1) * NF * sizeof(double)),
            "hipHostMalloc");
     nsf_ = mf_forward_num_splits(ld_, Pp_);
     nsb_ = mf_backproject_num_splits(ld_, P_);
     nwb_ = mf_weights_num_blocks(Pp_);
     X_.resize((size_t)NF * ld_);
+    Xprev_.resize((size_t)NF * ld_);
     Fs_.resize((size_t)nsf_ * Pp_ * NF);
     W_.resize((size_t)Pp_ * NF);
     part_.resize((size_t)nsb_ * ld_ * NF);
@@ -58,6 +60,8 @@ MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, in
 MultiFrameEngine::~MultiFrameEngine() {
     set_device();
     if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto& e : ev_)
+        if (e) (void)hipEventDestroy(e);
     if (hstate_) (void)hipHostFree(hstate_);
     if (hg_) (void)hipHostFree(hg_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -98,10 +102,11 @@ void MultiFrameEngine::sweep() {
     }
     if (comm_->size() > 1) comm_->all_reduce(buf_.get(), (size_t)NF * ld_ + NF, ReduceOp::kSum, stream_);
     launch_mf_decide(st, F2, stream_);
-    launch_mf_update(X_.get(), D, O_.get(), pen, (float)cfg_.relaxation, cfg_.logarithmic, V_, ld_, st, NF, stream_);
+    launch_mf_update(X_.get(), D, O_.get(), pen, (float)cfg_.relaxation, cfg_.logarithmic, V_, ld_, st, NF, stream_,
+                     Xprev_.get());
 }
 
-void MultiFrameEngine::solve_group(const double* g, int B, double* x_out, SolveInfo* info) {
+void MultiFrameEngine::solve_group(const double* g, int B, double* x_out, SolveInfo* info, const double* x0) {
     RoctxRange range("sart::mf_solve");
     const int NF = nf_;
     const auto t0 = std::chrono::steady_clock::now();
@@ -131,37 +136,61 @@ void MultiFrameEngine::solve_group(const double* g, int B, double* x_out, SolveI
     hip_ok(hipMemcpyAsync(G64_.get(), G, NF * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D G");
     launch_mf_prep(g64_.get(), P_, Pp_, norm64_.get(), rs_.ray_len.get(), (float)cfg_.ray_length_threshold,
                    ghat_.get(), arow_.get(), gpos_.get(), wo_.get(), NF, stream_);
-    // cold start x0 = max([rho > tau] A^T max(ghat, 0) / rho, 1e-7) per frame (reference sart_kernels.cu:22-60)
-    launch_mf_backproject(A_, ld_, P_, gpos_.get(), nsb_, part_.get(), NF, stream_);
-    launch_mf_collect(part_.get(), nsb_, ld_, nullptr, buf_.get(), nullptr, 0, nullptr, NF, stream_);
-    comm_->all_reduce(buf_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
-    launch_mf_init(X_.get(), buf_.get(), rs_.dinv.get(), V_, ld_, B, NF, stream_);
+    if (x0) {  // warm start: x_prev / s per frame, clamped (reference sartsolver_cuda.cpp:176-180)
+        if ((int64_t)x064_.size() < V_) x064_.resize(std::max<int64_t>(V_, 1));
+        if (V_) hip_ok(hipMemcpyAsync(x064_.get(), x0, V_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D x0");
+        launch_mf_init_warm(X_.get(), x064_.get(), norm64_.get(), V_, ld_, B, NF, stream_);
+    } else {
+        // cold start x0 = max([rho > tau] A^T max(ghat, 0) / rho, 1e-7) per frame (reference sart_kernels.cu:22-60)
+        launch_mf_backproject(A_, ld_, P_, gpos_.get(), nsb_, part_.get(), NF, stream_);
+        launch_mf_collect(part_.get(), nsb_, ld_, nullptr, buf_.get(), nullptr, 0, nullptr, NF, stream_);
+        comm_->all_reduce(buf_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
+        launch_mf_init(X_.get(), buf_.get(), rs_.dinv.get(), V_, ld_, B, NF, stream_);
+    }
     if (cfg_.logarithmic) {  // frame-constant observed back-projection, reduced once per batch
         launch_mf_backproject(A_, ld_, P_, wo_.get(), nsb_, part_.get(), NF, stream_);
         launch_mf_collect(part_.get(), nsb_, ld_, rs_.dmask.get(), O_.get(), nullptr, 0, nullptr, NF, stream_);
         comm_->all_reduce(O_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
     }
     launch_mf_state_begin(st_.get(), G64_.get(), B, cfg_.conv_tolerance, cfg_.max_iterations, NF, stream_);
+    // Chunks of check_interval sweeps, pipelined like Engine::solve: chunk c + 1 is queued before the state
+    // after chunk c is read, so the GPU never drains between chunks (sweeps after all_done are no-ops).
     const int max_sweeps = cfg_.max_iterations + 1;
-    for (int done_sweeps = 0; done_sweeps < max_sweeps;) {
-        const int n = std::min(cfg_.check_interval, max_sweeps - done_sweeps);
+    int enqueued = 0, issued = 0, checked = 0;
+    auto issue = [&]() {
+        const int n = std::min(cfg_.check_interval, max_sweeps - enqueued);
         {
             RoctxRange r("sart::mf_chunk");
             for (int i = 0; i < n; ++i) sweep();
         }
-        done_sweeps += n;
-        hip_ok(hipMemcpyAsync(hstate_, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
-        hip_ok(hipStreamSynchronize(stream_), "mf chunk");
-        if (hstate_->all_done) break;
+        enqueued += n;
+        const int slot = issued & 1;
+        hip_ok(hipMemcpyAsync(hstate_ + slot, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
+        hip_ok(hipEventRecord(ev_[slot], stream_), "event");
+        ++issued;
+    };
+    issue();
+    while (true) {
+        if (enqueued < max_sweeps) issue();
+        const int slot = checked & 1;
+        hip_ok(hipEventSynchronize(ev_[slot]), "mf chunk");
+        ++checked;
+        if (hstate_[slot].all_done || (checked == issued && enqueued >= max_sweeps)) break;
     }
-    std::vector<float> xh((size_t)NF * ld_);
+    std::vector<float> xh((size_t)NF * ld_), xp;
     hip_ok(hipMemcpyAsync(xh.data(), X_.get(), xh.size() * sizeof(float), hipMemcpyDeviceToHost, stream_), "D2H X");
     hip_ok(hipMemcpyAsync(hstate_, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
     hip_ok(hipStreamSynchronize(stream_), "mf solve");
+    if (hstate_->flags) {  // NaN/Inf guard: frames that stopped on a non-finite iterate return the last finite one
+        xp.resize(xh.size());
+        hip_ok(hipMemcpy(xp.data(), Xprev_.get(), xp.size() * sizeof(float), hipMemcpyDeviceToHost), "D2H Xprev");
+    }
     comm_->check();
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (int f = 0; f < B; ++f) {
-        for (int64_t v = 0; v < V_; ++v) x_out[(int64_t)f * V_ + v] = (double)xh[(size_t)f * ld_ + v] * norm[f];
+        const bool rollback = (hstate_->rollback >> f) & 1;
+        const float* src = rollback ? xp.data() : xh.data();
+        for (int64_t v = 0; v < V_; ++v) x_out[(int64_t)f * V_ + v] = (double)src[(size_t)f * ld_ + v] * norm[f];
         info[f].status = hstate_->status[f] == kSuccess ? kSuccess : kMaxIterationsExceeded;
         info[f].iterations = hstate_->iters[f];
         info[f].convergence = hstate_->conv[f];
@@ -171,12 +200,17 @@ void MultiFrameEngine::solve_group(const double* g, int B, double* x_out, SolveI
     }
 }
 
-std::vector<SolveInfo> MultiFrameEngine::solve_batch(const double* g, int nframes, double* x_out) {
+std::vector<SolveInfo> MultiFrameEngine::solve_batch(const double* g, int nframes, double* x_out, const double* x0,
+                                                     bool chain) {
     set_device();
     std::vector<SolveInfo> out(std::max(nframes, 0));
+    const double* warm = x0;
     for (int b0 = 0; b0 < nframes; b0 += nf_) {
         const int B = std::min(nf_, nframes - b0);
-        solve_group(g + (int64_t)b0 * P_, B, x_out + (int64_t)b0 * V_, out.data() + b0);
+        solve_group(g + (int64_t)b0 * P_, B, x_out + (int64_t)b0 * V_, out.data() + b0, warm);
+        // time-series warm start: the next group starts from this group's last solution (if it is finite)
+        const double* last = x_out + (int64_t)(b0 + B - 1) * V_;
+        warm = chain && std::all_of(last, last + V_, [](double v) { return std::isfinite(v); }) ? last : nullptr;
     }
     return out;
 }

@@ -3,7 +3,9 @@
 // frame by frame (reference main.cpp:131-140), streaming the RTM twice per iteration per frame; batching
 // turns A.x and A^T.w into skinny GEMMs (nf right-hand sides) that reuse every byte of A nf times. Every frame
 // keeps its own normalisation, saturation mask, convergence history, status and iteration count; frames
-// that finish are frozen while the others continue. Batched frames are cold-started (like --no_guess).
+// that finish are frozen while the others continue. Groups are cold-started (like --no_guess), or warm-
+// started as a time series: group k + 1 starts from the solution of group k's last frame (the reference's
+// frame-to-frame warm start, main.cpp:127-139, applied per group of batch_frames() frames).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -28,7 +30,11 @@ class MultiFrameEngine {
 
     void set_laplacian(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t nnz);
     // g: nframes x nrows (host fp64, frame-major); x_out: nframes x nvoxel. Solved batch_frames() at a time.
-    std::vector<SolveInfo> solve_batch(const double* g, int nframes, double* x_out);
+    // x0 (optional, nvoxel, de-normalised like a solution): warm start of the first group (null: cold start).
+    // chain: every later group starts from the solution of the previous group's last frame (time series);
+    // otherwise every later group cold-starts.
+    std::vector<SolveInfo> solve_batch(const double* g, int nframes, double* x_out, const double* x0 = nullptr,
+                                       bool chain = false);
     int64_t nrows() const { return P_; }
     int64_t nvoxel() const { return V_; }
     int batch_frames() const { return nf_; }
@@ -36,7 +42,7 @@ class MultiFrameEngine {
     static int batch_width(int frames);
 
    private:
-    void solve_group(const double* g, int B, double* x_out, SolveInfo* info);
+    void solve_group(const double* g, int B, double* x_out, SolveInfo* info, const double* x0);
     void sweep();
     void set_device() const;
 
@@ -49,14 +55,15 @@ class MultiFrameEngine {
     int nf_ = 16;
     int nsf_ = 1, nsb_ = 1, nwb_ = 1;
     DeviceRaySums rs_;
-    DeviceArray<float> X_, Fs_, W_, part_, buf_, pen_, O_, ghat_, arow_, gpos_, wo_;
-    DeviceArray<double> g64_, norm64_, G64_, F2part_;
+    DeviceArray<float> X_, Xprev_, Fs_, W_, part_, buf_, pen_, O_, ghat_, arow_, gpos_, wo_;
+    DeviceArray<double> g64_, norm64_, G64_, F2part_, x064_;
     DeviceArray<MfState> st_;
     DeviceArray<int64_t> lap_rp_;
     DeviceArray<int32_t> lap_col_;
     DeviceArray<float> lap_val_;
     bool has_lap_ = false;
-    MfState* hstate_ = nullptr;  // pinned
+    MfState* hstate_ = nullptr;  // pinned [2]: state after each of the two chunks in flight
+    hipEvent_t ev_[2] = {nullptr, nullptr};
     double* hg_ = nullptr;       // pinned [rows][nf] staging of a batch
 };
 

@@ -119,8 +119,12 @@ void launch_mf_init(float* X, const float* D0, const float* dinv, int64_t nvox, 
 void launch_mf_penalty(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta, bool logx,
                        const float* X, int64_t ld, float* pen, const MfState* st, int nf, hipStream_t stream);
 void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream);
+// X[f][v] = max(x0[v] / norm[f], 1e-7) for the nused frames (one warm start shared by the batch)
+void launch_mf_init_warm(float* X, const double* x0, const double* norm, int64_t nvox, int64_t ld, int nused, int nf,
+                         hipStream_t stream);
+// Xprev (optional): receives X before the update (NaN/Inf guard rollback)
 void launch_mf_update(float* X, const float* D, const float* O, const float* pen, float alpha, bool logmode,
-                      int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream);
+                      int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream, float* Xprev = nullptr);
 void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, int max_iter, int nf,
                            hipStream_t stream);
 }  // namespace sart

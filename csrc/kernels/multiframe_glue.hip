@@ -128,6 +128,23 @@ __global__ __launch_bounds__(256) void k_mf_init(float* __restrict__ X, const fl
     X[i] = x;
 }
 
+// Warm start of every used frame from one solution x0 (fp64, nvox): X[f][v] = max(x0[v] / norm[f], 1e-7)
+// (reference sartsolver_cuda.cpp:176-180: x = x_prev / s, then the clamp); padding and unused frames 0.
+__global__ __launch_bounds__(256) void k_mf_init_warm(float* __restrict__ X, const double* __restrict__ x0,
+                                                      const double* __restrict__ norm, int64_t nvox, int64_t ld,
+                                                      int nused, int nf) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)nf * ld) return;
+    const int f = (int)(i / ld);
+    const int64_t v = i % ld;
+    float x = 0.f;
+    if (f < nused && v < nvox) {
+        x = (float)(x0[v] / norm[f]);
+        x = x > 1e-7f ? x : 1e-7f;
+    }
+    X[i] = x;
+}
+
 // pen[f][v] = beta * sum_j L[v, j] x[f][j] (or log x), one thread per (row, frame), fixed order.
 __global__ __launch_bounds__(256) void k_mf_penalty(const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
                                                     const float* __restrict__ val, int64_t n, float beta, int logx,
@@ -162,9 +179,10 @@ __global__ void k_mf_decide(MfState* __restrict__ st, const float* __restrict__ 
         const double F = (double)F2[f];
         int done = st->done[f];
         if (!isfinite(F)) {
-            if (!done) {
+            if (!done) {  // NaN/Inf guard: the frame stops; its last finite iterate (s - 1 updates) is in Xprev
                 atomicOr(&st->flags, 1ull << f);
-                st->iters[f] = s;
+                if (s > 0) atomicOr(&st->rollback, 1ull << f);
+                st->iters[f] = s > 0 ? s - 1 : 0;
                 done = 1;
             }
         } else if (s >= 1) {
@@ -188,11 +206,12 @@ __global__ void k_mf_decide(MfState* __restrict__ st, const float* __restrict__ 
     }
 }
 
-// Update of the frames that are still running (after the decision of this sweep).
+// Update of the frames that are still running (after the decision of this sweep). Xprev (optional) receives
+// the iterate before the update: the rollback point of the NaN/Inf guard.
 __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const float* __restrict__ D,
                                                    const float* __restrict__ O, const float* __restrict__ pen,
                                                    float alpha, int logmode, int64_t nvox, int64_t ld,
-                                                   const MfState* __restrict__ st) {
+                                                   const MfState* __restrict__ st, float* __restrict__ Xprev) {
     if (st->all_done) return;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (int64_t)st->nf * ld) return;
@@ -200,13 +219,15 @@ __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const 
     const int64_t v = i % ld;
     if (v >= nvox || st->done[f]) return;
     const float p = pen ? pen[i] : 0.f;
+    const float x0 = X[i];
+    if (Xprev) Xprev[i] = x0;
     if (logmode) {
         const float eps = 1e-7f;  // reference EPSILON_LOG_CUDA (sart_kernels.cu:17-19)
         float r = powf((O[i] + eps) / (D[i] + eps), alpha);
         if (pen) r *= expf(-p);
-        X[i] = X[i] * r;
+        X[i] = x0 * r;
     } else {
-        const float x = X[i] + D[i] - p;
+        const float x = x0 + D[i] - p;
         X[i] = x > 0.f ? x : 0.f;
     }
 }
@@ -229,6 +250,7 @@ __global__ void k_mf_state_begin(MfState* __restrict__ st, const double* __restr
         st->all_done = nused > 0 ? 0 : 1;
         st->nf = nf;
         st->flags = 0;
+        st->rollback = 0;
         st->tol = tol;
     }
 }
@@ -286,11 +308,19 @@ void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream) {
     check_launch("k_mf_decide");
 }
 
+void launch_mf_init_warm(float* X, const double* x0, const double* norm, int64_t nvox, int64_t ld, int nused, int nf,
+                         hipStream_t stream) {
+    check_nf(nf, "mf_init_warm");
+    hipLaunchKernelGGL(k_mf_init_warm, dim3(nb((int64_t)nf * ld)), dim3(256), 0, stream, X, x0, norm, nvox, ld, nused,
+                       nf);
+    check_launch("k_mf_init_warm");
+}
+
 void launch_mf_update(float* X, const float* D, const float* O, const float* pen, float alpha, bool logmode,
-                      int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream) {
+                      int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream, float* Xprev) {
     check_nf(nf, "mf_update");
     hipLaunchKernelGGL(k_mf_update, dim3(nb((int64_t)nf * ld)), dim3(256), 0, stream, X, D, O, pen, alpha,
-                       logmode ? 1 : 0, nvox, ld, st);
+                       logmode ? 1 : 0, nvox, ld, st, Xprev);
     check_launch("k_mf_update");
 }
 

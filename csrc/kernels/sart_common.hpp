@@ -57,6 +57,7 @@ struct alignas(16) MfState {
     int32_t nf;                      // frames per batch (columns in use by the kernels)
     unsigned long long flags;        // bit f: frame f produced a non-finite ||A x||^2
     double tol;
+    unsigned long long rollback;     // bit f: frame f stopped at sweep >= 1 (its last finite iterate is in Xprev)
 };
 
 __device__ __forceinline__ float wave_sum(float v) {

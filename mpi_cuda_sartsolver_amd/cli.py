@@ -157,7 +157,7 @@ def run(cfg, intervals) -> int:
         nframes = image.nframe
         frames = (i for i in range(nframes) if image.frame_time(i) > skip_until + 1e-12)
         if cfg.batch_frames > 1 and use_gpu:
-            _run_batched(cfg, solver, image, frames, pool, writer, profile, rank)
+            _run_batched(cfg, solver, image, frames, pool, writer, profile, rank, solution)
         else:
             idx = next(frames, None)
             fut = pool.submit(image.frame, idx) if idx is not None else None
@@ -213,16 +213,21 @@ def run(cfg, intervals) -> int:
     return 0
 
 
-def _run_batched(cfg, solver, image, frames, pool, writer, profile, rank) -> None:
-    """--batch_frames N: independent frames solved together (cold start each, like --no_guess)."""
+def _run_batched(cfg, solver, image, frames, pool, writer, profile, rank, warm=None) -> None:
+    """--batch_frames N: N frames solved together on the matrix cores. Without --no_guess the batches form a
+    warm-started time series (every frame of batch k + 1 starts from batch k's last solution; the first batch
+    from the resumed solution, or cold); with --no_guess every frame cold-starts (reference main.cpp:127-139)."""
     import numpy as np
 
     idxs = list(frames)
+    warm = None if cfg.no_guess else warm
     for b0 in range(0, len(idxs), cfg.batch_frames):
         chunk = idxs[b0: b0 + cfg.batch_frames]
         batch = np.stack(list(pool.map(image.frame, chunk)))
         t0 = time.perf_counter()
-        results = solver.solve_batch(batch)
+        results = solver.solve_batch(batch, x0=warm)
+        last = results[-1].solution
+        warm = None if (cfg.no_guess or not np.all(np.isfinite(last))) else last
         ms = 1e3 * (time.perf_counter() - t0)
         if rank == 0:
             for i, res in zip(chunk, results):

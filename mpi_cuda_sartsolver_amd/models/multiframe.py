@@ -4,9 +4,11 @@ The reference solves the time series strictly frame by frame (reference main.cpp
 the RTM twice per iteration per frame. For throughput on long time series (BASELINE.json config 5),
 frames can be batched: the forward and back projections become skinny GEMMs ``A.X`` / ``A^T.W`` with
 16, 32 or 64 right-hand sides (csrc/kernels/multiframe.hip, ``v_mfma_f32_16x16x4_f32`` on 1, 2 or 4
-column groups), reading A twice per iteration for the whole batch. Every frame keeps its own normalisation, saturation mask, convergence
-history and status; frames that converge are frozen while the others continue. Batched frames are
-cold-started (no warm start chain between them), like ``--no_guess``.
+column groups), reading A twice per iteration for the whole batch. Every frame keeps its own normalisation,
+saturation mask, convergence history and status; frames that converge are frozen while the others
+continue. Batches are cold-started (``--no_guess``), or warm-started as a time series: every frame of batch
+k + 1 starts from the solution of batch k's last frame (``solve_batch(g, x0=...)``; the reference warm-starts
+frame by frame, main.cpp:127-139). A frame whose iterate turns non-finite returns its last finite iterate.
 
 The solver runs in the native engine (csrc/engine/multiframe.cpp, ``sart::MultiFrameEngine``; glue
 kernels in csrc/kernels/multiframe_glue.hip); this class is its Python face.
@@ -68,19 +70,25 @@ class MultiFrameSARTSolver:
         self.P, self.Pp, self.V, self.ld = rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld
         self.batch_width = int(self.engine.batch_frames)  # 16, 32 or 64 columns on the matrix cores
 
-    def solve_batch(self, measurements) -> List[SolveResult]:
+    def solve_batch(self, measurements, x0=None, chain: bool = False) -> List[SolveResult]:
+        """Frames [nframes, local pixels] in batches of ``self.batch``. ``x0`` (nvoxel, optional): warm start of
+        the first batch (None: cold). ``chain``: each later batch starts from the previous batch's last
+        solution (time series); otherwise later batches cold-start."""
         g_all = np.asarray(measurements, dtype=np.float64)
         if g_all.ndim == 1:
             g_all = g_all[None]
+        warm = None if x0 is None else _host_f64(x0)
         out: List[SolveResult] = []
         for b0 in range(0, g_all.shape[0], self.batch):
-            x, infos = self.engine.solve_batch(np.ascontiguousarray(g_all[b0: b0 + self.batch]))
+            x, infos = self.engine.solve_batch(np.ascontiguousarray(g_all[b0: b0 + self.batch]), warm)
             for f, info in enumerate(infos):
                 status = SUCCESS if info["status"] == SUCCESS else MAX_ITERATIONS_EXCEEDED
                 out.append(SolveResult(solution=x[f], status=status, iterations=int(info["iterations"]),
                                        convergence=float(info["convergence"]), used_fused=False,
-                                       elapsed_ms=float(info["ms"])))
+                                       elapsed_ms=float(info["ms"]), nonfinite=bool(info["nonfinite"])))
+            last = x[len(infos) - 1]
+            warm = last if (chain and np.all(np.isfinite(last))) else None
         return out
 
     def solve(self, measurement, solution=None) -> SolveResult:
-        return self.solve_batch(_host_f64(measurement)[None])[0]
+        return self.solve_batch(_host_f64(measurement)[None], x0=solution)[0]

@@ -108,3 +108,42 @@ def test_cli_gpu_matches_gpu_semantics(tmp_path, capsys, log, extra):
     assert len(t) == 4
     # fp32 vs fp64 iterates of a tolerance-stopped warm-start chain drift apart by ~1e-3..1e-2
     assert np.linalg.norm(last - xs[-1]) / np.linalg.norm(xs[-1]) < (5e-3 if batched else 1.5e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log", [False, True])
+def test_cli_batched_time_series_warm_start(tmp_path, capsys, log):
+    """--batch_frames keeps the reference's warm-started time series (main.cpp:127-139) at MFMA throughput:
+    every frame of batch k + 1 starts from batch k's last solution. 3 cameras, 64 frames, batches of 16,
+    against the sequential warm-start oracle: the same status for every frame, and the batched run solves
+    the series faster than the frame-by-frame engine."""
+    import json
+    import time
+
+    case = make_case(str(tmp_path / "c"), cameras=("cam_a", "cam_b", "cam_c"), shapes=((12, 16), (10, 14), (9, 12)),
+                     laplacian=True, nframes=64, saturate=0.02, nvoxel=1024, grid=(16, 8, 8), seed=11)
+    kw = ["-m", "400", "-c", "1e-4", "-l", case.laplacian_file, "-b", "1e-3"] + (["-L"] if log else [])
+    okw = dict(logarithmic=log, max_iterations=400, conv_tolerance=1e-4, beta_laplace=1e-3)
+    xs, sts, its = _expected(case, sart_gpu_semantics, warm=True, **okw)
+    # the batched chain's own oracle: frame 16 k + j starts from frame 16 k - 1 (the underdetermined problem's
+    # tolerance-stopped answer depends on the initial guess, so the two chains end at different iterates)
+    frames, L = _frames(case), _laplacian(case)
+    prev, xb = None, None
+    for k in range(4):
+        for j in range(16):
+            xb, _, _ = sart_gpu_semantics(case.A, frames[16 * k + j], L, x_prev=prev, **okw)
+            if j == 15:
+                prev = xb
+    walls = {}
+    for mode, extra, ref in (("batched", ["--batch_frames", "16"], xb), ("sequential", [], xs[-1])):
+        out, prof = str(tmp_path / f"{mode}.h5"), str(tmp_path / f"{mode}.jsonl")
+        t0 = time.perf_counter()
+        assert cli.main(kw + extra + ["--profile", prof, "-o", out] + case.files) == 0
+        walls[mode] = time.perf_counter() - t0
+        assert capsys.readouterr().out.count("Processed in:") == 64
+        t, last, st = native().read_solution_file(out)
+        assert len(t) == 64
+        np.testing.assert_array_equal(st, sts)  # same status per frame as the sequential warm-start series
+        assert np.linalg.norm(last - ref) / np.linalg.norm(ref) < 2e-2
+        walls[mode + "_solve_ms"] = sum(json.loads(ln)["ms"] for ln in open(prof))
+    assert walls["batched_solve_ms"] < walls["sequential_solve_ms"], walls

@@ -42,6 +42,7 @@ for step in "$@"; do
     profmf) for nf in 16 32 64; do
               run rocprof_mf$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mf$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 || exit 1
             done ;;
+    benchshare) run bench_share2 600 python bench.py --gpus 2 --share-gpus --steps 3 --warmup 1 ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
