@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <stdexcept>
@@ -55,13 +56,40 @@ MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, in
     F2part_.resize((size_t)nwb_ * NF);
     st_.resize(1);
     rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_);
+    // chunks of the overlapped back-projection / all-reduce pipeline (several ranks only): SART_MF_CHUNKS
+    // (default 4) voxel ranges aligned to the back-projection's voxel tile, each >= 1 MiB of corrections
+    int nchunks = 1;
+    if (comm_->size() > 1) {
+        const char* e = std::getenv("SART_MF_CHUNKS");
+        nchunks = (e && *e) ? std::max(1, std::atoi(e)) : 4;
+        const int64_t min_vox = std::max<int64_t>(1, (1 << 20) / (4 * NF));
+        nchunks = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, ld_ / min_vox));
+    }
+    const int64_t align = mf_backproject_vox_align(ld_, NF);
+    chunks_.assign(1, 0);
+    for (int c = 1; c < nchunks; ++c) {
+        const int64_t v = (ld_ * c / nchunks) / align * align;
+        if (v > chunks_.back() && v < ld_) chunks_.push_back(v);
+    }
+    chunks_.push_back(ld_);
+    if (chunks_.size() > 2) {
+        hip_ok(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking), "hipStreamCreate");
+        cev_.resize(chunks_.size() - 1);
+        for (auto& e : cev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        hip_ok(hipEventCreateWithFlags(&comm_done_, hipEventDisableTiming), "hipEventCreate");
+    }
 }
 
 MultiFrameEngine::~MultiFrameEngine() {
     set_device();
     if (stream_) (void)hipStreamSynchronize(stream_);
+    if (comm_stream_) (void)hipStreamSynchronize(comm_stream_);
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : cev_)
+        if (e) (void)hipEventDestroy(e);
+    if (comm_done_) (void)hipEventDestroy(comm_done_);
+    if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
     if (hstate_) (void)hipHostFree(hstate_);
     if (hg_) (void)hipHostFree(hg_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -86,21 +114,46 @@ void MultiFrameEngine::set_laplacian(const int64_t* row_ptr, const int32_t* col,
 void MultiFrameEngine::sweep() {
     const int NF = nf_;
     MfState* st = st_.get();
-    float* D = buf_.get();
-    float* F2 = buf_.get() + (int64_t)NF * ld_;
+    float* D = buf_.get();                     // [ld][nf] voxel-major corrections
+    float* F2 = buf_.get() + (int64_t)NF * ld_;  // [nf] ||A x||^2, all-reduced with the last chunk
+    const float* scale = cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get();
     launch_mf_forward(A_, ld_, P_, Pp_, X_.get(), ld_, Fs_.get(), nsf_, NF, stream_);
     launch_mf_weights(Fs_.get(), nsf_, Pp_, ghat_.get(), arow_.get(), cfg_.logarithmic, W_.get(), F2part_.get(),
                       NF, stream_);
-    launch_mf_backproject(A_, ld_, P_, W_.get(), nsb_, part_.get(), NF, stream_);
-    launch_mf_collect(part_.get(), nsb_, ld_, cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get(), D,
-                      F2part_.get(), nwb_, F2, NF, stream_);
+    const int nc = (int)chunks_.size() - 1;
+    if (comm_->size() > 1 && nc > 1) {
+        // Overlap: the back-projection runs chunk by chunk over the voxel axis on the compute
+        // stream; the all-reduce of chunk c (a contiguous [v0, v1) x nf slice of the voxel-major corrections)
+        // runs on the comm stream as soon as its collect has finished, next to the back-projection of the later
+        // chunks. All compute chunks are queued first so that a host-staged all-reduce, which blocks this thread,
+        // still overlaps with them.
+        for (int c = 0; c < nc; ++c) {
+            const int64_t v0 = chunks_[c], v1 = chunks_[c + 1];
+            launch_mf_backproject(A_, ld_, P_, W_.get(), nsb_, part_.get(), NF, stream_, v0, v1);
+            const bool last = c == nc - 1;
+            launch_mf_collect(part_.get(), nsb_, ld_, v0, v1, scale, D, last ? F2part_.get() : nullptr, nwb_,
+                              last ? F2 : nullptr, NF, stream_);
+            hip_ok(hipEventRecord(cev_[c], stream_), "event");
+        }
+        for (int c = 0; c < nc; ++c) {
+            const int64_t v0 = chunks_[c], v1 = chunks_[c + 1];
+            hip_ok(hipStreamWaitEvent(comm_stream_, cev_[c], 0), "wait chunk");
+            const size_t n = (size_t)(v1 - v0) * NF + (c == nc - 1 ? (size_t)NF : 0);
+            comm_->all_reduce(D + v0 * NF, n, ReduceOp::kSum, comm_stream_);
+        }
+        hip_ok(hipEventRecord(comm_done_, comm_stream_), "event");
+    } else {
+        launch_mf_backproject(A_, ld_, P_, W_.get(), nsb_, part_.get(), NF, stream_);
+        launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, scale, D, F2part_.get(), nwb_, F2, NF, stream_);
+        if (comm_->size() > 1) comm_->all_reduce(buf_.get(), (size_t)NF * ld_ + NF, ReduceOp::kSum, stream_);
+    }
     const float* pen = nullptr;
-    if (has_lap_) {
+    if (has_lap_) {  // needs X only: runs while the last chunks are being reduced
         launch_mf_penalty(lap_rp_.get(), lap_col_.get(), lap_val_.get(), V_, (float)cfg_.beta_laplace,
                           cfg_.logarithmic, X_.get(), ld_, pen_.get(), st, NF, stream_);
         pen = pen_.get();
     }
-    if (comm_->size() > 1) comm_->all_reduce(buf_.get(), (size_t)NF * ld_ + NF, ReduceOp::kSum, stream_);
+    if (comm_->size() > 1 && nc > 1) hip_ok(hipStreamWaitEvent(stream_, comm_done_, 0), "wait all-reduce");
     launch_mf_decide(st, F2, stream_);
     launch_mf_update(X_.get(), D, O_.get(), pen, (float)cfg_.relaxation, cfg_.logarithmic, V_, ld_, st, NF, stream_,
                      Xprev_.get());
@@ -143,13 +196,13 @@ void MultiFrameEngine::solve_group(const double* g, int B, double* x_out, SolveI
     } else {
         // cold start x0 = max([rho > tau] A^T max(ghat, 0) / rho, 1e-7) per frame (reference sart_kernels.cu:22-60)
         launch_mf_backproject(A_, ld_, P_, gpos_.get(), nsb_, part_.get(), NF, stream_);
-        launch_mf_collect(part_.get(), nsb_, ld_, nullptr, buf_.get(), nullptr, 0, nullptr, NF, stream_);
+        launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, nullptr, buf_.get(), nullptr, 0, nullptr, NF, stream_);
         comm_->all_reduce(buf_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
         launch_mf_init(X_.get(), buf_.get(), rs_.dinv.get(), V_, ld_, B, NF, stream_);
     }
     if (cfg_.logarithmic) {  // frame-constant observed back-projection, reduced once per batch
         launch_mf_backproject(A_, ld_, P_, wo_.get(), nsb_, part_.get(), NF, stream_);
-        launch_mf_collect(part_.get(), nsb_, ld_, rs_.dmask.get(), O_.get(), nullptr, 0, nullptr, NF, stream_);
+        launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, rs_.dmask.get(), O_.get(), nullptr, 0, nullptr, NF, stream_);
         comm_->all_reduce(O_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
     }
     launch_mf_state_begin(st_.get(), G64_.get(), B, cfg_.conv_tolerance, cfg_.max_iterations, NF, stream_);

@@ -62,6 +62,11 @@ class MultiFrameEngine {
     DeviceArray<int32_t> lap_col_;
     DeviceArray<float> lap_val_;
     bool has_lap_ = false;
+    // overlapped back-projection / all-reduce (several ranks): voxel chunk bounds, comm stream, events
+    std::vector<int64_t> chunks_;
+    hipStream_t comm_stream_ = nullptr;
+    std::vector<hipEvent_t> cev_;
+    hipEvent_t comm_done_ = nullptr;
     MfState* hstate_ = nullptr;  // pinned [2]: state after each of the two chunks in flight
     hipEvent_t ev_[2] = {nullptr, nullptr};
     double* hg_ = nullptr;       // pinned [rows][nf] staging of a batch

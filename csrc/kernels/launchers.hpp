@@ -104,16 +104,19 @@ void mf_set_rows(int rt);  // 2 or 4: 16-row tiles per wave of the MFMA forward 
 void mf_set_vox(int vt);   // 1 or 2: 64-voxel tiles per wave of the MFMA back-projection; 0: default
 void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ldx,
                        float* Fout, int nsplit, int nf, hipStream_t stream);
+// voxel range [v0, v1) (default: the whole row), aligned to mf_backproject_vox_align
+int mf_backproject_vox_align(int64_t ld, int nf);
 void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,
-                           int nf, hipStream_t stream);
+                           int nf, hipStream_t stream, int64_t v0 = 0, int64_t v1 = -1);
 // multiframe_glue.hip
 void launch_mf_prep(const double* g, int64_t nrows, int64_t nrows_pad, const double* norm, const float* ray_length,
                     float len_thres, float* ghat, float* arow, float* gpos, float* wo, int nf, hipStream_t stream);
 int mf_weights_num_blocks(int64_t nrows_pad);
 void launch_mf_weights(const float* Fs, int nsplit, int64_t nrows_pad, const float* ghat, const float* arow,
                        bool logmode, float* W, double* F2part, int nf, hipStream_t stream);
-void launch_mf_collect(const float* part, int nsplit, int64_t ld, const float* scale, float* D, const double* F2part,
-                       int nF2, float* F2out, int nf, hipStream_t stream);
+// D[v][f] (voxel-major) for v in [v0, v1); F2out (optional) = per-frame sums of F2part
+void launch_mf_collect(const float* part, int nsplit, int64_t ld, int64_t v0, int64_t v1, const float* scale, float* D,
+                       const double* F2part, int nF2, float* F2out, int nf, hipStream_t stream);
 void launch_mf_init(float* X, const float* D0, const float* dinv, int64_t nvox, int64_t ld, int nused, int nf,
                     hipStream_t stream);
 void launch_mf_penalty(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta, bool logx,

@@ -164,14 +164,16 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
 // frame order. One wave: 64 * VT voxels x nf frames; a float4 of A (4 voxels of one row) feeds 4 * NG
 // MFMAs, one per output tile c (voxel set {v0 + 4 i + c : i = 0..15}) and column group j, and every W
 // operand feeds 4 * VT (VT = 2 halves the W traffic per byte of A; needs ld % 128 == 0).
+// Voxel range: the blocks of 64 * VT voxels from vb0 (blockIdx.x = 0) up to voxel vend (the chunks of the
+// engine's all-reduce pipeline; the whole row is vb0 = 0, vend = ld).
 template <int NG, int DEPTH, int VT>
 __global__ __launch_bounds__(256) void k_mf_backproject(const float* __restrict__ A, int64_t ld, int64_t nrows,
                                                         const float* __restrict__ W, int64_t rows_per_split,
-                                                        float* __restrict__ partial) {
+                                                        float* __restrict__ partial, int64_t vb0, int64_t vend) {
     constexpr int NF = 16 * NG;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t vb = (int64_t)blockIdx.x * 4 + wave;  // block of 64 * VT voxels
-    if (vb * 64 * VT >= ld) return;
+    const int64_t vb = vb0 + (int64_t)blockIdx.x * 4 + wave;  // block of 64 * VT voxels
+    if (vb * 64 * VT >= vend) return;
     const int g = lane >> 4, i16 = lane & 15;
     const int64_t ld4 = ld >> 2;
     const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
@@ -392,38 +394,47 @@ void launch_mf_forward(const float* A, int64_t ld, int64_t nrows, int64_t nrows_
 
 template <int NG, int VT>
 static void bwd_vt(dim3 grid, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows, const float* W,
-                   int64_t rps, float* partial) {
+                   int64_t rps, float* partial, int64_t vb0, int64_t vend) {
     if (depth == 1)
-        hipLaunchKernelGGL((k_mf_backproject<NG, 1, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
+        hipLaunchKernelGGL((k_mf_backproject<NG, 1, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial,
+                           vb0, vend);
     else if (depth == 3)
-        hipLaunchKernelGGL((k_mf_backproject<NG, 3, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
+        hipLaunchKernelGGL((k_mf_backproject<NG, 3, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial,
+                           vb0, vend);
     else
-        hipLaunchKernelGGL((k_mf_backproject<NG, 2, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial);
+        hipLaunchKernelGGL((k_mf_backproject<NG, 2, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial,
+                           vb0, vend);
 }
 
 template <int NG>
 static void bwd(int vt, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows, const float* W,
-                int nsplit, int64_t rps, float* partial) {
-    const dim3 grid((unsigned)((ld / (64 * vt) + 3) / 4), (unsigned)nsplit);
+                int nsplit, int64_t rps, float* partial, int64_t v0, int64_t v1) {
+    const int64_t vb0 = v0 / (64 * vt), nvb = (v1 - v0 + 64 * vt - 1) / (64 * vt);
+    const dim3 grid((unsigned)((nvb + 3) / 4), (unsigned)nsplit);
     if (vt == 2)
-        bwd_vt<NG, 2>(grid, depth, stream, A, ld, nrows, W, rps, partial);
+        bwd_vt<NG, 2>(grid, depth, stream, A, ld, nrows, W, rps, partial, vb0, v1);
     else
-        bwd_vt<NG, 1>(grid, depth, stream, A, ld, nrows, W, rps, partial);
+        bwd_vt<NG, 1>(grid, depth, stream, A, ld, nrows, W, rps, partial, vb0, v1);
 }
 
+int mf_backproject_vox_align(int64_t ld, int nf) { return 64 * mf_vox(ld, nf); }
+
 void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,
-                           int nf, hipStream_t stream) {
+                           int nf, hipStream_t stream, int64_t v0, int64_t v1) {
     if (ld % 64 != 0) throw std::runtime_error("mf_backproject: ld must be a multiple of 64");
     check_nf(nf, "mf_backproject");
+    if (v1 < 0) v1 = ld;
+    const int vt = mf_vox(ld, nf);
+    if (v0 < 0 || v1 > ld || v0 >= v1 || v0 % (64 * vt) != 0 || (v1 != ld && v1 % (64 * vt) != 0))
+        throw std::runtime_error("mf_backproject: voxel range must be aligned to the wave's voxel tile");
     const int64_t rps = ((nrows + nsplit - 1) / nsplit + 15) / 16 * 16;
     const int d = mf_depth(false, nf);
-    const int vt = mf_vox(ld, nf);
     if (nf == 16)
-        bwd<1>(vt, d, stream, A, ld, nrows, W, nsplit, rps, partial);
+        bwd<1>(vt, d, stream, A, ld, nrows, W, nsplit, rps, partial, v0, v1);
     else if (nf == 32)
-        bwd<2>(vt, d, stream, A, ld, nrows, W, nsplit, rps, partial);
+        bwd<2>(vt, d, stream, A, ld, nrows, W, nsplit, rps, partial, v0, v1);
     else
-        bwd<4>(vt, d, stream, A, ld, nrows, W, nsplit, rps, partial);
+        bwd<4>(vt, d, stream, A, ld, nrows, W, nsplit, rps, partial, v0, v1);
     check_launch("k_mf_backproject");
 }
 

@@ -1,7 +1,9 @@
 // Element-wise and reduction kernels of the multi-frame solver (nf = 16, 32 or 64 frames as the N columns
 // of the MFMA projections in multiframe.hip). Layouts: pixel-major [rows][nf] for measurements, weights and
-// forward projections (the MFMA B/D fragments), frame-major [nf][ld] for solutions and corrections (the
-// MFMA A operand of the forward projection), so each frame's solution row is contiguous.
+// forward projections (the MFMA B/D fragments), frame-major [nf][ld] for solutions and penalties (the MFMA A
+// operand of the forward projection), voxel-major [ld][nf] for the reduced corrections (the back-projection
+// partials' layout): a voxel range of every frame is one contiguous chunk, so the per-sweep all-reduce can
+// run chunk by chunk next to the back-projection of the following chunks.
 //
 // Per-frame semantics are those of the single-frame solver (sart_update.hip) and the reference GPU path
 // (reference sartsolver_cuda.cpp:138-354): every frame has its own normalisation, saturation mask,
@@ -9,6 +11,8 @@
 #include "sart_common.hpp"
 
 #include <math.h>
+
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -74,28 +78,18 @@ __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs
     if (threadIdx.x < nf) F2part[(int64_t)blockIdx.x * nf + threadIdx.x] = red[threadIdx.x];
 }
 
-// D[f][v] = scale[v] * sum_s part[s][v][f] (transpose through LDS); block 0 also writes
-// F2out[f] = (float) sum_b F2part[b][f] when F2part is given.
-__global__ __launch_bounds__(256) void k_mf_collect(const float* __restrict__ part, int nsplit, int64_t ld,
-                                                    const float* __restrict__ scale, float* __restrict__ D,
+// D[v][f] = scale[v] * sum_s part[s][v][f] for v in [v0, v1) (voxel-major, contiguous; fixed summation
+// order); block 0 also writes F2out[f] = (float) sum_b F2part[b][f] when F2part is given.
+__global__ __launch_bounds__(256) void k_mf_collect(const float* __restrict__ part, int nsplit, int64_t ld, int64_t v0,
+                                                    int64_t v1, const float* __restrict__ scale, float* __restrict__ D,
                                                     const double* __restrict__ F2part, int nF2, float* __restrict__ F2out,
                                                     int nf) {
-    __shared__ float tile[kMaxNF][64 + 1];
-    const int64_t v0 = (int64_t)blockIdx.x * 64;
-    // load: the contiguous [64][nf] block, 256 elements per pass
-    for (int e = threadIdx.x; e < 64 * nf; e += 256) {
-        const int64_t v = v0 + e / nf;
-        const int f = e % nf;
+    const int64_t i = v0 * nf + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < v1 * nf) {
+        const int64_t v = i / nf;
         float acc = 0.f;
-        if (v < ld)
-            for (int s = 0; s < nsplit; ++s) acc += part[((int64_t)s * ld + v) * nf + f];
-        tile[f][e / nf] = (v < ld && scale) ? acc * scale[v] : acc;
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 64 * nf; e += 256) {
-        const int f = e / 64, vv = e % 64;
-        const int64_t v = v0 + vv;
-        if (v < ld) D[(int64_t)f * ld + v] = tile[f][vv];
+        for (int s = 0; s < nsplit; ++s) acc += part[(int64_t)s * ld * nf + i];
+        D[i] = scale ? acc * scale[v] : acc;
     }
     if (F2part && blockIdx.x == 0) {  // block-uniform branch: all 256 threads, 256 / nf per frame
         __shared__ double f2[256];
@@ -112,7 +106,7 @@ __global__ __launch_bounds__(256) void k_mf_collect(const float* __restrict__ pa
     }
 }
 
-// X[f][v] = max(D0[f][v] * dinv[v], 1e-7) for real voxels of used frames, 0 elsewhere.
+// X[f][v] = max(D0[v][f] * dinv[v], 1e-7) for real voxels of used frames, 0 elsewhere (D0 voxel-major).
 __global__ __launch_bounds__(256) void k_mf_init(float* __restrict__ X, const float* __restrict__ D0,
                                                  const float* __restrict__ dinv, int64_t nvox, int64_t ld, int nused,
                                                  int nf) {
@@ -122,7 +116,7 @@ __global__ __launch_bounds__(256) void k_mf_init(float* __restrict__ X, const fl
     const int64_t v = i % ld;
     float x = 0.f;
     if (f < nused && v < nvox) {
-        x = D0[i] * dinv[v];
+        x = D0[v * nf + f] * dinv[v];
         x = x > 1e-7f ? x : 1e-7f;
     }
     X[i] = x;
@@ -206,29 +200,43 @@ __global__ void k_mf_decide(MfState* __restrict__ st, const float* __restrict__ 
     }
 }
 
-// Update of the frames that are still running (after the decision of this sweep). Xprev (optional) receives
-// the iterate before the update: the rollback point of the NaN/Inf guard.
+// Update of the frames that are still running (after the decision of this sweep). D and O are voxel-major
+// [ld][nf] (the reduced back-projections), X / pen / Xprev frame-major [nf][ld]: a block transposes a
+// 64-voxel tile of D (and O) through LDS so both sides stay coalesced. Xprev (optional) receives the
+// iterate before the update: the rollback point of the NaN/Inf guard.
 __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const float* __restrict__ D,
                                                    const float* __restrict__ O, const float* __restrict__ pen,
                                                    float alpha, int logmode, int64_t nvox, int64_t ld,
                                                    const MfState* __restrict__ st, float* __restrict__ Xprev) {
+    __shared__ float dt[64][kMaxNF + 1];
+    __shared__ float ot[64][kMaxNF + 1];
     if (st->all_done) return;
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)st->nf * ld) return;
-    const int f = (int)(i / ld);
-    const int64_t v = i % ld;
-    if (v >= nvox || st->done[f]) return;
-    const float p = pen ? pen[i] : 0.f;
-    const float x0 = X[i];
-    if (Xprev) Xprev[i] = x0;
-    if (logmode) {
-        const float eps = 1e-7f;  // reference EPSILON_LOG_CUDA (sart_kernels.cu:17-19)
-        float r = powf((O[i] + eps) / (D[i] + eps), alpha);
-        if (pen) r *= expf(-p);
-        X[i] = x0 * r;
-    } else {
-        const float x = x0 + D[i] - p;
-        X[i] = x > 0.f ? x : 0.f;
+    const int nf = st->nf;
+    const int64_t v0 = (int64_t)blockIdx.x * 64;
+    for (int e = threadIdx.x; e < 64 * nf; e += 256) {
+        const int64_t v = v0 + e / nf;
+        const int f = e % nf;
+        dt[e / nf][f] = v < ld ? D[v * nf + f] : 0.f;
+        if (logmode) ot[e / nf][f] = v < ld ? O[v * nf + f] : 0.f;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * nf; e += 256) {
+        const int f = e / 64, vv = e % 64;
+        const int64_t v = v0 + vv;
+        if (v >= nvox || st->done[f]) continue;
+        const int64_t i = (int64_t)f * ld + v;
+        const float p = pen ? pen[i] : 0.f;
+        const float x0 = X[i];
+        if (Xprev) Xprev[i] = x0;
+        if (logmode) {
+            const float eps = 1e-7f;  // reference EPSILON_LOG_CUDA (sart_kernels.cu:17-19)
+            float r = powf((ot[vv][f] + eps) / (dt[vv][f] + eps), alpha);
+            if (pen) r *= expf(-p);
+            X[i] = x0 * r;
+        } else {
+            const float x = x0 + dt[vv][f] - p;
+            X[i] = x > 0.f ? x : 0.f;
+        }
     }
 }
 
@@ -279,11 +287,13 @@ void launch_mf_weights(const float* Fs, int nsplit, int64_t nrows_pad, const flo
     check_launch("k_mf_weights");
 }
 
-void launch_mf_collect(const float* part, int nsplit, int64_t ld, const float* scale, float* D, const double* F2part,
-                       int nF2, float* F2out, int nf, hipStream_t stream) {
+void launch_mf_collect(const float* part, int nsplit, int64_t ld, int64_t v0, int64_t v1, const float* scale,
+                       float* D, const double* F2part, int nF2, float* F2out, int nf, hipStream_t stream) {
     check_nf(nf, "mf_collect");
-    hipLaunchKernelGGL(k_mf_collect, dim3((unsigned)((ld + 63) / 64)), dim3(256), 0, stream, part, nsplit, ld, scale,
-                       D, F2part, nF2, F2out, nf);
+    if (v0 < 0 || v1 > ld || v1 < v0) throw std::runtime_error("mf_collect: voxel range outside [0, ld)");
+    const int64_t n = (v1 - v0) * nf;
+    hipLaunchKernelGGL(k_mf_collect, dim3(std::max<unsigned>(1, nb(n))), dim3(256), 0, stream, part, nsplit, ld, v0, v1,
+                       scale, D, F2part, nF2, F2out, nf);
     check_launch("k_mf_collect");
 }
 
@@ -319,7 +329,7 @@ void launch_mf_init_warm(float* X, const double* x0, const double* norm, int64_t
 void launch_mf_update(float* X, const float* D, const float* O, const float* pen, float alpha, bool logmode,
                       int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream, float* Xprev) {
     check_nf(nf, "mf_update");
-    hipLaunchKernelGGL(k_mf_update, dim3(nb((int64_t)nf * ld)), dim3(256), 0, stream, X, D, O, pen, alpha,
+    hipLaunchKernelGGL(k_mf_update, dim3((unsigned)((ld + 63) / 64)), dim3(256), 0, stream, X, D, O, pen, alpha,
                        logmode ? 1 : 0, nvox, ld, st, Xprev);
     check_launch("k_mf_update");
 }

@@ -81,15 +81,21 @@ def test_p2p_auto_selection(tmp_path):
     assert all(r["exact"] for r in res["results"] if r["n"] <= 4097)
 
 
-@pytest.mark.parametrize("extra", [[], ["--logarithmic"], ["--multiframe"]])
+@pytest.mark.parametrize("extra", [[], ["--logarithmic"], ["--multiframe"],
+                                   ["--multiframe", "--npix", "1024", "--nvox", "65536", "--iters", "12"]])
 def test_gpu_solver_rank_invariance_p2p(tmp_path, extra):
+    """(The last case has 4 MB of corrections per sweep: the multi-frame engine reduces them in 4 voxel chunks
+    on its comm stream, overlapped with the back-projection of the following chunks.)"""
     x1, m1 = _run(1, str(tmp_path / "r1"), extra)
+    # different row partitions sum in different orders: fp32 drift grows with the width (3e-3 measured at
+    # 65536 voxels x 12 iterations; profiles/numerics_r2.jsonl)
+    tol = 6e-3 if "65536" in extra else 2e-3
     for n in (2, 3):
         x, m = _run(n, str(tmp_path / f"p{n}"), extra, SART_P2P="1")
         assert m[0]["comm"] == "p2p"
         if "--multiframe" not in extra:
             assert m[0]["comm_ms"] > 0  # time_collectives: events around every per-sweep all-reduce
-        assert np.linalg.norm(x - x1) / np.linalg.norm(x1) < 2e-3
+        assert np.linalg.norm(x - x1) / np.linalg.norm(x1) < tol
         for a, b in zip(m, m1):
             assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3
 

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--logarithmic", action="store_true")
     ap.add_argument("--fused", action="store_true")
     ap.add_argument("--multiframe", action="store_true")
+    ap.add_argument("--batch", type=int, default=16, help="multi-frame batch width (16, 32, 64)")
     ap.add_argument("--columns", action="store_true", help="column (voxel) shards instead of row shards")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
@@ -45,7 +46,7 @@ def main():
     if a.multiframe:
         from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
 
-        s = MultiFrameSARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic)
+        s = MultiFrameSARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic, batch=a.batch)
         g = prob.measurement.cpu().numpy()
         res = s.solve_batch(np.stack([g, 0.5 * g, 2.0 * g]))
         x = np.stack([r.solution for r in res])

@@ -42,6 +42,25 @@ for step in "$@"; do
     profmf) for nf in 16 32 64; do
               run rocprof_mf$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mf$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 || exit 1
             done ;;
+    mfoverlap)  # 2 ranks on one GPU, each under its own rocprofv3 (no launcher between profiler and python)
+      port=$(python -c 'import socket; s = socket.socket(); s.bind(("127.0.0.1", 0)); print(s.getsockname()[1])')
+      echo "=== mfoverlap ($(date +%T))" | tee -a "$OUT/session.log"
+      pids=()
+      for r in 0 1; do
+        MASTER_ADDR=127.0.0.1 MASTER_PORT=$port RANK=$r WORLD_SIZE=2 LOCAL_RANK=$r LOCAL_WORLD_SIZE=2 \
+          SART_DIST_BACKEND=gloo SART_P2P=1 timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/mfov_r$r" -o run \
+          --output-format csv -- python3 tools/dist_check.py --multiframe --batch 32 --npix 8192 --nvox 65536 \
+          --iters 20 --out "$OUT/mfov" > "$OUT/mfov_r$r.log" 2>&1 &
+        pids+=($!)
+      done
+      rc=0
+      for p in "${pids[@]}"; do wait "$p" || rc=$?; done
+      echo "=== mfoverlap rc=$rc" | tee -a "$OUT/session.log"
+      [ $rc -eq 0 ] || { tail -n 20 "$OUT"/mfov_r*.log; exit $rc; }
+      for r in 0 1; do
+        python tools/overlap_report.py "$(ls "$OUT"/mfov_r$r/*/run_kernel_trace.csv "$OUT"/mfov_r$r/run_kernel_trace.csv 2>/dev/null | head -n 1)" \
+          --out "$OUT/mfov_report_r$r.json" || true
+      done ;;
     benchshare) run bench_share2 600 python bench.py --gpus 2 --share-gpus --steps 3 --warmup 1 ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
