@@ -143,6 +143,13 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
     if (cfg_.use_fused && !cfg_.column_shard && abytes >= cfg_.fused_min_bytes &&
         (!shared_device_ || fused_ok_shared) && (!cfg_.rtm_bf16 || cfg_.fused_variant == 6)) {
         geom_ = fused_geometry(ld_, num_cus_, cfg_.fused_variant, cfg_.rows_per_tile);
+        if (cfg_.rtm_bf16 && (cfg_.rows_per_tile == 0 || cfg_.rows_per_tile == 4)) {
+            // wide bf16 tiles (8 KB per wave per step, like fp32) where the width allows; SART_BF16_WIDE=0 keeps
+            // the narrow tiles
+            const char* w = std::getenv("SART_BF16_WIDE");
+            const FusedGeometry gw = fused_geometry_bf16_wide(ld_, num_cus_);
+            if (gw.valid() && !(w && std::string(w) == "0")) geom_ = gw;
+        }
         use_fused_ = geom_.valid() && (!cfg_.rtm_bf16 || geom_.variant == 6);
     }
     alloc_fused();
@@ -341,7 +348,7 @@ void Engine::sweep() {
         if (cfg_.rtm_bf16)  // variant 6, K = rows per tile
             launch_fused_sweep_bf16(cfg_.logarithmic, geom_.K, static_cast<const bf16_t*>(A_), ld_, P_, Pp_, x_.get(),
                                     ghat_.get(), arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I,
-                                    geom_.J, st, xcnt_.get(), stream_);
+                                    geom_.J, st, xcnt_.get(), stream_, geom_.cpl);
         else
             launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, static_cast<const float*>(A_), ld_, P_, Pp_,
                                x_.get(), ghat_.get(), arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I,

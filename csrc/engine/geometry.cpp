@@ -94,4 +94,14 @@ FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_
     return g;
 }
 
+FusedGeometry fused_geometry_bf16_wide(int64_t ld, int num_cus) {
+    FusedGeometry g;
+    if (num_cus % 8 != 0 || ld % 4096 != 0) return g;
+    const int per_xcd = num_cus / 8;
+    const int64_t J = ld / 4096;
+    if (J < 1 || J > per_xcd) return g;
+    g.K = 4, g.T = 4, g.cpl = 8, g.J = (int)J, g.I = 8 * (per_xcd / (int)J), g.grid = g.I * g.J, g.variant = 6;
+    return g;
+}
+
 }  // namespace sart

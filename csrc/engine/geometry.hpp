@@ -13,6 +13,7 @@ struct FusedGeometry {
     int grid = 0;     // I * J persistent workgroups
     int variant = -1; // 6 (XCD-local row groups), 3 (generic fallback), -1: no fused path for this width
     int T = 0;        // rows per tile
+    int cpl = 4;      // variant 6: columns per lane per k-slot (8: wide bf16 tiles, slab 16384 / T)
     bool valid() const { return variant >= 0; }
 };
 
@@ -24,5 +25,8 @@ int64_t choose_ld(int64_t nvoxel, double max_waste = 0.10);
 // Geometry for `variant` (6 default, or 3), falling back to variant 3 when variant 6 cannot split the
 // width. rows_per_tile = 0: SART_FUSED_T or the lowest-cost T.
 FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_tile);
+// Variant 6 geometry of the wide bf16 tiles (16-byte loads of 8 bf16 per lane, T = 4, slab 4096 columns); invalid
+// when the width does not split into J <= 32 such slabs.
+FusedGeometry fused_geometry_bf16_wide(int64_t ld, int num_cus);
 
 }  // namespace sart

@@ -294,24 +294,29 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
 // slower than 2: their stores join the vmcnt queue of their streaming loads.
 // (LDS x slab: T >= 2 only.) Scalar-memory (s_load glc) polls were measured and are no faster under load:
 // an s_load round trip to L2 costs ~1.2 us while the chip streams.
-// Register tiles of the v4/v6 compute waves by RTM storage type. A lane owns 4 consecutive columns per
-// k-slot in both: one 16-byte fp32 load, or one 8-byte load of 4 bf16 widened to fp32 where the tile is
-// consumed (row dot and LDS park); the LDS ring, the x slab and every sum stay fp32. bf16 tiles take half
-// the VGPRs, so the bf16 kernel keeps more tiles in flight (RS below) for the same bytes in flight.
-template <typename AT>
+// Register tiles of the v6 compute waves by RTM storage type and lane width. A lane owns CPL consecutive
+// columns per k-slot: one 16-byte fp32 load (CPL 4), one 8-byte load of 4 bf16 (CPL 4), or one 16-byte load
+// of 8 bf16 (CPL 8, "wide"), widened to H = CPL / 4 float4 where the tile is consumed (row dot and
+// back-projection); the LDS ring parks the raw storage type, the x slab and every sum stay fp32.
+// Narrow bf16 tiles carry half the bytes of an fp32 tile per instruction and per pipeline step, so at the
+// fp32 kernel's step rate they stream half the bytes (487 it/s = 4.2 TB/s at 64k x 64k); wide bf16 tiles
+// carry the fp32 tile's 8 KB per wave per step (twice the columns per workgroup: slab 16384 / T).
+template <typename AT, int CPL = 4>
 struct FusedTile;
 
 template <>
-struct FusedTile<float> {
+struct FusedTile<float, 4> {
     using R = float4;
+    static constexpr int H = 1;
     __device__ __forceinline__ static R load(const R* p) { return load_stream(p); }
-    __device__ __forceinline__ static float4 widen(const R v) { return v; }
+    __device__ __forceinline__ static void widen(const R v, float4 (&o)[1]) { o[0] = v; }
 };
 
 typedef unsigned sart_u2v __attribute__((ext_vector_type(2)));
 template <>
-struct FusedTile<bf16_t> {
+struct FusedTile<bf16_t, 4> {
     using R = uint2;
+    static constexpr int H = 1;
     __device__ __forceinline__ static R load(const R* p) {
 #if SART_STREAM_NT
         const sart_u2v v = __builtin_nontemporal_load(reinterpret_cast<const sart_u2v*>(p));
@@ -320,10 +325,28 @@ struct FusedTile<bf16_t> {
         return *p;
 #endif
     }
-    __device__ __forceinline__ static float4 widen(const R v) { return bf16x4_to_f4(v.x, v.y); }
+    __device__ __forceinline__ static void widen(const R v, float4 (&o)[1]) { o[0] = bf16x4_to_f4(v.x, v.y); }
 };
 
-template <bool LOG, bool XL, bool DIAG, int T, int SCHED, typename AT = float>
+template <>
+struct FusedTile<bf16_t, 8> {
+    using R = uint4;
+    static constexpr int H = 2;
+    __device__ __forceinline__ static R load(const R* p) {
+#if SART_STREAM_NT
+        const sart_u4v v = __builtin_nontemporal_load(reinterpret_cast<const sart_u4v*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+#else
+        return *p;
+#endif
+    }
+    __device__ __forceinline__ static void widen(const R v, float4 (&o)[2]) {
+        o[0] = bf16x4_to_f4(v.x, v.y);
+        o[1] = bf16x4_to_f4(v.z, v.w);
+    }
+};
+
+template <bool LOG, bool XL, bool DIAG, int T, int SCHED, typename AT = float, int CPL = 4>
 __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
     const AT* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
     const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
@@ -338,6 +361,8 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
     constexpr bool SPLIT = SCHED == 4;  // wave 4 publishes granules, wave 5 gathers (no shared vmcnt queue)
     constexpr int NTHR = SPLIT ? kFusedThreads + 64 : kFusedThreads;
     constexpr bool BF = !std::is_same<AT, float>::value;
+    constexpr int H = CPL / 4;  // float4 per lane per k-slot (2: wide bf16 tiles)
+    static_assert(CPL == 4 || (BF && CPL == 8 && XS_LDS), "wide tiles: bf16 storage, x slab in LDS");
     // bf16 tiles are parked raw in the LDS ring (16 KB per slot), so 8 slots fit in the 128 KB of the fp32
     // ring. With T = 1 (schedule 0) the bf16 sweep keeps 4 polls in flight and lags the back-projection by
     // L = PD + PQ = 5 steps: 12.5 -> 13.2 it/s at 512k x 256k; with T = 4 (schedule 4) the deeper lag
@@ -347,21 +372,22 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
     constexpr int PQ = DEEP ? 4 : (SCHED == 1 ? 3 : 2);      // polls in flight (finishes tile u - PD - PQ + 1)
     constexpr int L = DEEP ? PD + PQ : 3 + D;                // back-projection lag in steps
     static_assert(L >= PD + PQ, "the weights must be ready one step before they are used");
-    constexpr int NL = BF ? 8 : 4;  // LDS ring slots (32 KB fp32 / 16 KB bf16 each)
+    constexpr int NL = (BF && CPL == 4) ? 8 : 4;  // LDS ring slots (32 KB fp32 or wide bf16 / 16 KB narrow bf16)
     static_assert(L <= NL + D - 1, "a parked tile must be back-projected before its ring slot is reused");
     // register tile slots per wave (8 KB fp32 / 4 KB bf16 each): AH in flight + D held. bf16: 6-7 tiles of
     // 8-byte loads in flight (<= 56 loads, inside the 6-bit vmcnt range); 8 slots with the x slab in LDS
     // measured no faster at 64k x 64k
-    constexpr int RS = XS_LDS ? (BF ? 7 : 5) : (BF ? 7 : 4);
-    using FT = FusedTile<AT>;
+    // wide bf16 tiles: 8 KB per wave like fp32, 5 slots (4 in flight + 1 held), accumulators 2 x 32 VGPRs
+    constexpr int RS = XS_LDS ? ((BF && CPL == 4) ? 7 : 5) : (BF ? 7 : 4);
+    using FT = FusedTile<AT, CPL>;
     using RT = typename FT::R;
     constexpr int AH = RS - D;   // tiles in flight per wave
     static_assert(L >= PD + 2, "the weights must be ready one step before they are used");
     constexpr int NS = 8;        // LDS hand-off slots
 
     extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64] of RT (128 KB)
-    float4* s_xs = s_ring + NL * 4 * KW * 64 * sizeof(RT) / sizeof(float4);  // [WPR][KW][64] if XS_LDS
-    float* s_small = reinterpret_cast<float*>(s_xs + (XS_LDS ? WPR * KW * 64 : 0));
+    float4* s_xs = s_ring + NL * 4 * KW * 64 * sizeof(RT) / sizeof(float4);  // [WPR][KW][H][64] if XS_LDS
+    float* s_small = reinterpret_cast<float*>(s_xs + (XS_LDS ? WPR * KW * H * 64 : 0));
     // Hand-off words: volatile through explicit LDS (address_space(3)) pointers. Through generic pointers
     // the compiler keeps volatile accesses as FLAT instructions, which count on vmcnt too, so every flag
     // poll waited vmcnt(0) and drained the compute waves' in-flight A tiles.
@@ -400,29 +426,39 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
     const int64_t nt = ntiles * (gi + 1) / I - t_begin;
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const int64_t ld4 = ld >> 2;
+    const int64_t ld4 = ld >> (CPL == 8 ? 3 : 2);  // row length in tile vectors (RT)
     if (DIAG && threadIdx.x == 0 && b < 1024) g_fused_map[b] = gi * 1024 + gj;
 
     for (int i = threadIdx.x; i < NS * 4 + NS; i += NTHR) s_pflag[i] = -1;
     if constexpr (XS_LDS) {
-        const float4* xsrc = reinterpret_cast<const float4*>(x) + (int64_t)gj * (64 * KW * WPR);
-        for (int i = threadIdx.x; i < WPR * KW * 64; i += NTHR) s_xs[i] = xsrc[i];
+        // global float4 i of the slab = lane-vector i / H, half i % H; LDS [(sub * KW + k) * H + h][lane] so a
+        // wave reads 64 consecutive float4 per (k, h)
+        const float4* xsrc = reinterpret_cast<const float4*>(x) + (int64_t)gj * (64 * KW * WPR) * H;
+        if constexpr (H == 1) {
+            for (int i = threadIdx.x; i < WPR * KW * 64; i += NTHR) s_xs[i] = xsrc[i];
+        } else {
+            for (int i = threadIdx.x; i < WPR * KW * 64 * H; i += NTHR) {
+                const int lv = i / H, h = i % H;  // lv = (sub * KW + k) * 64 + lane
+                s_xs[((lv >> 6) * H + h) * 64 + (lv & 63)] = xsrc[i];
+            }
+        }
     }
     __syncthreads();
 
     if (wave < 4) {
         const int wrow = wave / WPR, wsub = wave % WPR;
-        const int64_t slab4 = (int64_t)gj * (64 * KW * WPR);                // first float4 of the slab
-        const int64_t col4 = slab4 + wsub * (64 * KW) + lane;              // + k * 64
+        const int64_t slab4 = (int64_t)gj * (64 * KW * WPR);                // first lane-vector of the slab
+        const int64_t col4 = slab4 + wsub * (64 * KW) + lane;              // + k * 64 (CPL columns each)
         const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
-        const RT* __restrict__ a4 = reinterpret_cast<const RT*>(A) + col4 + (int64_t)wrow * ld4;  // 4 columns each
+        const RT* __restrict__ a4 = reinterpret_cast<const RT*>(A) + col4 + (int64_t)wrow * ld4;
         RT* ring = reinterpret_cast<RT*>(s_ring) + (wave * KW) * 64 + lane;  // tiles parked in storage type
-        float4 xs[XS_LDS ? 1 : KW], acc[KW];
-        const float4* xl = s_xs + wsub * (KW * 64) + lane;
+        float4 xs[XS_LDS ? 1 : KW], acc[KW][H];
+        const float4* xl = s_xs + wsub * (KW * H * 64) + lane;             // + (k * H + h) * 64
 #pragma unroll
         for (int k = 0; k < KW; ++k) {
             if constexpr (!XS_LDS) xs[k] = x4[col4 + k * 64];
-            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int h = 0; h < H; ++h) acc[k][h] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         RT fl[RS][KW];
         // Tile loads are issued unconditionally, clamped to the last tile of the matrix (past the group's
@@ -453,10 +489,15 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
                 float s = 0.f;
 #pragma unroll
                 for (int k = 0; k < KW; ++k) {
-                    if constexpr (XS_LDS)
-                        s += dot4(FT::widen(fl[bb][k]), xl[k * 64]);
-                    else
-                        s += dot4(FT::widen(fl[bb][k]), xs[k]);
+                    float4 w[H];
+                    FT::widen(fl[bb][k], w);
+#pragma unroll
+                    for (int h = 0; h < H; ++h) {
+                        if constexpr (XS_LDS)
+                            s += dot4(w[h], xl[(k * H + h) * 64]);
+                        else
+                            s += dot4(w[h], xs[k]);
+                    }
                 }
                 s = wave_sum(s);
                 if (lane == 0) {
@@ -490,7 +531,12 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
                 const float wr = s_w[ws * 4 + wrow];
                 const RT* slot = ring + (int)(u % NL) * (4 * KW * 64);
 #pragma unroll
-                for (int k = 0; k < KW; ++k) fma4(acc[k], FT::widen(slot[k * 64]), wr);
+                for (int k = 0; k < KW; ++k) {
+                    float4 w[H];
+                    FT::widen(slot[k * 64], w);
+#pragma unroll
+                    for (int h = 0; h < H; ++h) fma4(acc[k][h], w[h], wr);
+                }
             }
         };
         const unsigned long long tstart = DIAG ? __builtin_amdgcn_s_memtime() : 0;
@@ -504,27 +550,33 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
             if (wave == 0) g_fused_stats[b * 8 + 4] = __builtin_amdgcn_s_memtime() - tstart;  // loop cycles
             if (wave == 1) g_fused_stats[b * 8 + 5] = nstall;          // steps that waited
         }
-        // the T waves of a sub-slab hold partial sums of the same 2048 columns: combine through LDS
+        // the T waves of a sub-slab hold partial sums of the same columns: combine through LDS
         __syncthreads();
-        float4* red = s_ring + (wave * KW) * 64 + lane;
+        float4* red = s_ring + (wave * KW * H) * 64 + lane;
 #pragma unroll
-        for (int k = 0; k < KW; ++k) red[k * 64] = acc[k];
+        for (int k = 0; k < KW; ++k)
+#pragma unroll
+            for (int h = 0; h < H; ++h) red[(k * H + h) * 64] = acc[k][h];
         __syncthreads();
-        float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld) + slab4 + lane;
+        float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld);
+        if constexpr (H == 1) out += slab4 + lane;  // (fp32 / narrow bf16: the original addressing)
 #pragma unroll
-        for (int i = 0; i < 2 * WPR; ++i) {  // q = sub * KW + k, spread over the four waves
+        for (int i = 0; i < 2 * WPR * H; ++i) {  // q = (sub * KW + k) * H + h, spread over the four waves
             const int q = wave + 4 * i;
-            const int sub = q / KW, k = q % KW;
-            float4 v = s_ring[(sub * KW + k) * 64 + lane];  // wave (row 0, sub)
+            const int sub = q / (KW * H), k = (q / H) % KW, h = q % H;
+            float4 v = s_ring[q * 64 + lane];  // wave (row 0, sub)
 #pragma unroll
             for (int rr = 1; rr < T; ++rr) {
-                const float4 o = s_ring[((rr * WPR + sub) * KW + k) * 64 + lane];
+                const float4 o = s_ring[(((rr * WPR + sub) * KW + k) * H + h) * 64 + lane];
                 v.x += o.x;
                 v.y += o.y;
                 v.z += o.z;
                 v.w += o.w;
             }
-            out[q * 64] = v;
+            if constexpr (H == 1)
+                out[q * 64] = v;
+            else
+                out[(slab4 + (sub * KW + k) * 64 + lane) * H + h] = v;
         }
     } else if (SPLIT && wave == 4) {
         // Publisher wave (schedule 4): stores this workgroup's row partials as soon as the compute waves
@@ -670,10 +722,11 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
     }
 }
 
-constexpr size_t rows_lds_bytes(int T, int sched) {
-    return 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (sched >= 1 ? (4 / T) * 8 * 64 * sizeof(float4) : 0) +
+constexpr size_t rows_lds_bytes(int T, int sched, int H = 1) {
+    return 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (sched >= 1 ? (4 / T) * 8 * 64 * H * sizeof(float4) : 0) +
            (8 * 4 * 3 + 8 + 4) * sizeof(float);
 }
+static_assert(rows_lds_bytes(4, 4, 2) <= 160 * 1024, "wide bf16 tiles: T = 4 fits the LDS");
 
 static int g_fused_dbg = 0;    // diagnostics only (set through fused_set_debug)
 static int g_fused_sched = 4;  // variant 6 pipeline schedule (k_fused_sweep_rows SCHED)
@@ -722,19 +775,20 @@ static void launch_lds(bool logmode, dim3 grid, hipStream_t stream, const float*
                            nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
 }
 
-template <bool LG, bool X, bool D, int T, int SC, typename AT = float>
+template <bool LG, bool X, bool D, int T, int SC, typename AT = float, int CPL = 4>
 static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                           const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                           uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
+    constexpr size_t lds = rows_lds_bytes(T, SC, CPL / 4);
     static bool configured = false;
     if (!configured) {
-        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T, SC, AT>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds_bytes(T, SC)), "hipFuncSetAttribute");
+        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T, SC, AT, CPL>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "hipFuncSetAttribute");
         configured = true;
     }
-    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC, AT>), grid, dim3(SC == 4 ? kFusedThreads + 64 : kFusedThreads),
-                       rows_lds_bytes(T, SC), stream, A, ld, nrows,
-                       nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt);
+    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC, AT, CPL>), grid,
+                       dim3(SC == 4 ? kFusedThreads + 64 : kFusedThreads), lds, stream, A, ld, nrows, nrows_pad, x,
+                       ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt);
 }
 
 template <int T>
@@ -828,27 +882,35 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
     check_launch("k_fused_sweep_lds");
 }
 
-// bf16-stored RTM: variant 6 only (XCD-local row groups, same geometry and exchange as fp32), schedule 4
-// for T >= 2 and 0 for T = 1. A protocol timeout falls back to the bf16 two-pass kernels.
+// bf16-stored RTM: variant 6 only (XCD-local row groups, same exchange as fp32). cpl 8 ("wide": 16-byte loads of
+// 8 bf16 per lane, slab 16384 / T columns) needs T = 4 (schedule 4, x slab in LDS); cpl 4 ("narrow": 8-byte
+// loads, slab 8192 / T) runs schedule 4 for T >= 2 and 0 for T = 1. A protocol timeout falls back to the bf16
+// two-pass kernels.
 void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                              const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
-                             uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream) {
+                             uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream, int cpl) {
     if (T != 1 && T != 2 && T != 4) throw std::runtime_error("fused_sweep bf16: rows per tile must be 1, 2 or 4");
+    if (cpl != 4 && !(cpl == 8 && T == 4)) throw std::runtime_error("fused_sweep bf16: wide tiles need T = 4");
     if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep bf16: padded rows must be a multiple of 4");
-    if (ld % (8192 / T) != 0 || ld / (8192 / T) != J) throw std::runtime_error("fused_sweep bf16: ld must equal J * slab");
+    const int64_t slab = 2048 * cpl / T;
+    if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep bf16: ld must equal J * slab");
     if (J * 4 > kMaxGather || J * T > kRowsGather) throw std::runtime_error("fused_sweep bf16: too many slabs");
     if (xcnt == nullptr || I % 8 != 0) throw std::runtime_error("fused_sweep bf16: needs ticket counters and I % 8 == 0");
     const dim3 grid((unsigned)(I * J));
-    auto go = [&](auto lg, auto tt, auto sc) {
-        launch_rows_t<decltype(lg)::value, true, false, decltype(tt)::value, decltype(sc)::value, bf16_t>(
-            grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
+    auto go = [&](auto lg, auto tt, auto sc, auto cp) {
+        launch_rows_t<decltype(lg)::value, true, false, decltype(tt)::value, decltype(sc)::value, bf16_t,
+                      decltype(cp)::value>(grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
+                                           I, J, st, xcnt);
     };
     using S0 = std::integral_constant<int, 0>;
     using S4 = std::integral_constant<int, 4>;
+    using C4 = std::integral_constant<int, 4>;
+    using C8 = std::integral_constant<int, 8>;
     auto by_t = [&](auto lg) {
-        if (T == 1) go(lg, std::integral_constant<int, 1>{}, S0{});
-        else if (T == 2) go(lg, std::integral_constant<int, 2>{}, S4{});
-        else go(lg, std::integral_constant<int, 4>{}, S4{});
+        if (cpl == 8) go(lg, std::integral_constant<int, 4>{}, S4{}, C8{});
+        else if (T == 1) go(lg, std::integral_constant<int, 1>{}, S0{}, C4{});
+        else if (T == 2) go(lg, std::integral_constant<int, 2>{}, S4{}, C4{});
+        else go(lg, std::integral_constant<int, 4>{}, S4{}, C4{});
     };
     if (logmode) by_t(std::true_type{}); else by_t(std::false_type{});
     check_launch("k_fused_sweep_rows<bf16>");

@@ -216,3 +216,33 @@ def test_bf16_fused_rows_per_tile(dev, T, log):
     # 32768-term fp32 row dots in another summation order, amplified by 12 linear SART updates: both sit within
     # 2e-3 of the fp64 oracle, so they agree to a few 1e-3 (fp32 fused vs two-pass: test_fused_matches_two_pass)
     assert np.linalg.norm(r1.solution - rt.solution) / np.linalg.norm(rt.solution) < 3e-3
+
+
+@pytest.mark.parametrize("nvox,J,I", [(4096, 1, 256), (65536, 16, 16), (131072, 32, 8), (100000, 25, 8)])
+@pytest.mark.parametrize("log", [False, True])
+def test_bf16_wide_tiles(dev, monkeypatch, nvox, J, I, log):
+    """Wide bf16 tiles (16-byte loads of 8 bf16 per lane, slab 4096 columns at T = 4) against the narrow bf16
+    tiles (SART_BF16_WIDE=0) and the device fp64 oracle on the stored (rounded) matrix."""
+    from mpi_cuda_sartsolver_amd.models.oracle import sart_oracle_f64
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+    from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
+
+    prob = make_problem(2048, nvox, seed=nvox % 89, device=dev, saturate_fraction=0.02, storage="bf16")
+    g = prob.measurement.cpu().numpy()
+    p = dict(max_iterations=10, conv_tolerance=0.0)
+    sw = SARTSolver(prob.rtm, None, None, SolverParams(**p), logarithmic=log, allow_zero_tolerance=True)
+    assert sw.use_fused and (sw.geom.cpl, sw.geom.T, sw.geom.J, sw.geom.I) == (8, 4, J, I)
+    rw = sw.solve(g)
+    assert rw.used_fused and rw.fallbacks == 0
+    np.testing.assert_array_equal(rw.solution, sw.solve(g).solution)  # bitwise reproducible
+    del sw
+    monkeypatch.setenv("SART_BF16_WIDE", "0")
+    sn = SARTSolver(prob.rtm, None, None, SolverParams(**p), logarithmic=log, allow_zero_tolerance=True)
+    assert sn.use_fused and sn.geom.cpl == 4
+    rn = sn.solve(g)
+    del sn
+    x64 = sart_oracle_f64(prob.rtm, g, 10, logarithmic=log)
+    ew = np.linalg.norm(rw.solution - x64) / np.linalg.norm(x64)
+    en = np.linalg.norm(rn.solution - x64) / np.linalg.norm(x64)
+    # summation-order differences only (measured 1.27x at 4096 columns, <= 1.1x at >= 64k)
+    assert ew <= 1.5 * en + 1e-7, (ew, en)

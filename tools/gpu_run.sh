@@ -65,6 +65,7 @@ for step in "$@"; do
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
+    benchbf16n) SART_BF16_WIDE=0 run bench_bf16_narrow 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 ;;
     benchbf16t) for t in 1 2 4; do
                   SART_FUSED_T=$t run bench_bf16_T$t 300 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 || exit 1
                 done ;;
