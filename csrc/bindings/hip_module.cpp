@@ -129,6 +129,7 @@ static void bind_engine(py::module_& m) {
     m.def("fused_geometry", &sart::fused_geometry, py::arg("ld"), py::arg("num_cus"), py::arg("variant") = 6,
           py::arg("rows_per_tile") = 0);
     m.def("fused_geometry_bf16_wide", &sart::fused_geometry_bf16_wide, py::arg("ld"), py::arg("num_cus"));
+    m.def("fused_fold_tiles", &sart::fused_fold_tiles, py::arg("geometry"), py::arg("nrows_pad"));
     m.def("choose_ld", &sart::choose_ld, py::arg("nvoxel"), py::arg("max_waste") = 0.10);
 
     py::class_<sart::EngineConfig>(m, "EngineConfig")

@@ -167,6 +167,7 @@ class Engine {
     FusedGeometry geom_;
     int nsplit_ = 0;
     int64_t nF_fused_ = 0;
+    int64_t fold_tiles_ = 0;  // T = 1 fused sweep: back-projection fold period (tiles), 0 = off
     double norm_ = 1.0;
 
     DeviceArray<float> partial_, comm_buf_, x_, pen_, O_, ghat_, arow_, gpos_, wo_, w_, fitted_;

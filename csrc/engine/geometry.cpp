@@ -1,6 +1,7 @@
 #include "geometry.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 namespace sart {
@@ -23,7 +24,9 @@ V6Candidate v6_candidate(int64_t ld, int T, int per_xcd) {
     const int64_t J = ld / slab;
     if (J < 1 || J > per_xcd || J * T > 256 /* exchange gather registers */) return c;
     c.T = T, c.J = (int)J, c.G = per_xcd / (int)J;
-    c.cost = (double)slab / c.G;
+    // T = 2 (schedule 4) measured 4-10 % slower per byte than T = 1 (schedule 5) at equal slab / G
+    // (131072 / 106496 columns, profiles/probe_r2_t1_sched5.jsonl); T = 4 and T = 1 tie at 65536
+    c.cost = (double)slab / c.G * (T == 2 ? 1.08 : 1.0);
     return c;
 }
 
@@ -102,6 +105,13 @@ FusedGeometry fused_geometry_bf16_wide(int64_t ld, int num_cus) {
     if (J < 1 || J > per_xcd) return g;
     g.K = 4, g.T = 4, g.cpl = 8, g.J = (int)J, g.I = 8 * (per_xcd / (int)J), g.grid = g.I * g.J, g.variant = 6;
     return g;
+}
+
+int64_t fused_fold_tiles(const FusedGeometry& g, int64_t nrows_pad) {
+    if (g.variant != 6 || g.K != 1 || g.I <= 0) return 0;
+    if (const char* e = std::getenv("SART_FUSED_FOLD")) return std::max<int64_t>(0, std::atoll(e));
+    const int64_t per_group = (nrows_pad + g.I - 1) / g.I;  // tiles (= rows at T = 1) of the longest group
+    return std::max<int64_t>(16, (int64_t)std::ceil(std::sqrt((double)per_group)));
 }
 
 }  // namespace sart

@@ -28,5 +28,8 @@ FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_
 // Variant 6 geometry of the wide bf16 tiles (16-byte loads of 8 bf16 per lane, T = 4, slab 4096 columns); invalid
 // when the width does not split into J <= 32 such slabs.
 FusedGeometry fused_geometry_bf16_wide(int64_t ld, int num_cus);
+// Fold period of the T = 1 sweep's two-level back-projection sums (variant 6): ~sqrt(tiles per row group), so
+// no fp32 chain exceeds ~2 sqrt(P / I) terms (SART_FUSED_FOLD overrides; 0 = one chain per group). 0 for T >= 2.
+int64_t fused_fold_tiles(const FusedGeometry& g, int64_t nrows_pad);
 
 }  // namespace sart

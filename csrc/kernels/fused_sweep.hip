@@ -347,18 +347,20 @@ struct FusedTile<bf16_t, 8> {
 };
 
 template <bool LOG, bool XL, bool DIAG, int T, int SCHED, typename AT = float, int CPL = 4>
-__global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
+__global__ __launch_bounds__((SCHED == 4 || SCHED == 5) ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
     const AT* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
     const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
     double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg,
-    unsigned* __restrict__ xcnt) {
+    unsigned* __restrict__ xcnt, int64_t fold_tiles) {
     static_assert(T == 1 || T == 2 || T == 4, "rows per tile");
     constexpr int KW = 8;        // float4 per lane per row: one wave covers 2048 columns
     constexpr int WPR = 4 / T;   // compute waves per row (each on its own 2048-column sub-slab)
     constexpr int D = (SCHED == 1 || SCHED == 2 || SCHED == 4) ? 1 : 0;  // steps a reduced tile stays in VGPRs
-    constexpr bool XS_LDS = SCHED >= 1;                       // x slab in LDS instead of VGPRs
+    constexpr bool XS_LDS = SCHED >= 1 && SCHED <= 4;         // x slab in LDS instead of VGPRs
     static_assert(!XS_LDS || T >= 2, "the LDS holds the x slab only for T >= 2");
-    constexpr bool SPLIT = SCHED == 4;  // wave 4 publishes granules, wave 5 gathers (no shared vmcnt queue)
+    // wave 4 publishes granules, wave 5 gathers (no shared vmcnt queue); schedule 5 = the split exchange with
+    // the x slab in VGPRs and schedule 0's lag (T = 1, whose x slab does not fit the LDS next to the ring)
+    constexpr bool SPLIT = SCHED == 4 || SCHED == 5;
     constexpr int NTHR = SPLIT ? kFusedThreads + 64 : kFusedThreads;
     constexpr bool BF = !std::is_same<AT, float>::value;
     constexpr int H = CPL / 4;  // float4 per lane per k-slot (2: wide bf16 tiles)
@@ -384,6 +386,14 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
     constexpr int AH = RS - D;   // tiles in flight per wave
     static_assert(L >= PD + 2, "the weights must be ready one step before they are used");
     constexpr int NS = 8;        // LDS hand-off slots
+    // Two-level back-projection sums (T = 1): with T = 1 every wave owns its own columns, so a lane's
+    // accumulators would sum ALL P / I rows of its group in one fp32 chain (T >= 2 split a group's rows over T
+    // waves). Measured at 65536 x 262144 bf16: 2.4x the two-pass kernels' error after one iteration, 26x at
+    // 524288 rows. Every ~fold_tiles tiles (host: ~sqrt of the group's tiles) the chain is folded into a second
+    // register set acc2 and restarts, so no chain is longer than ~2 sqrt(P / I) terms. (Splitting the group
+    // into separately drained segments deadlocks: the exchange wave finishes tile u only after the compute
+    // waves published u + PD + PQ - 1.)
+    constexpr bool FOLD = (T == 1);
 
     extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64] of RT (128 KB)
     float4* s_xs = s_ring + NL * 4 * KW * 64 * sizeof(RT) / sizeof(float4);  // [WPR][KW][H][64] if XS_LDS
@@ -452,13 +462,14 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
         const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x);
         const RT* __restrict__ a4 = reinterpret_cast<const RT*>(A) + col4 + (int64_t)wrow * ld4;
         RT* ring = reinterpret_cast<RT*>(s_ring) + (wave * KW) * 64 + lane;  // tiles parked in storage type
-        float4 xs[XS_LDS ? 1 : KW], acc[KW][H];
+        float4 xs[XS_LDS ? 1 : KW], acc[KW][H], acc2[FOLD ? KW : 1];
         const float4* xl = s_xs + wsub * (KW * H * 64) + lane;             // + (k * H + h) * 64
 #pragma unroll
         for (int k = 0; k < KW; ++k) {
             if constexpr (!XS_LDS) xs[k] = x4[col4 + k * 64];
 #pragma unroll
             for (int h = 0; h < H; ++h) acc[k][h] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (FOLD) acc2[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         RT fl[RS][KW];
         // Tile loads are issued unconditionally, clamped to the last tile of the matrix (past the group's
@@ -540,10 +551,27 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
             }
         };
         const unsigned long long tstart = DIAG ? __builtin_amdgcn_s_memtime() : 0;
+        // fold period in RS-step passes (FOLD: at most ~fold_tiles rows per chain before it joins acc2)
+        const int64_t fpass = FOLD && fold_tiles > 0 ? (fold_tiles + RS - 1) / RS : (int64_t)1 << 62;
+        int64_t fcount = 0;
         for (int64_t t0 = 0; t0 < nt + L; t0 += RS) {  // RS steps per pass: register slots are static
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
                 (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
             }(std::make_integer_sequence<int, RS>{});
+            if constexpr (FOLD) {
+                if (++fcount == fpass) {  // registers only: no memory operation joins the vmcnt pipeline
+                    fcount = 0;
+#pragma unroll
+                    for (int k = 0; k < KW; ++k) {
+                        add4(acc2[k], acc[k][0]);
+                        acc[k][0] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
+            }
+        }
+        if constexpr (FOLD) {
+#pragma unroll
+            for (int k = 0; k < KW; ++k) add4(acc[k][0], acc2[k]);
         }
         if (DIAG && lane == 0) {
             g_fused_stats[b * 8 + wave] = stall;                       // [0..3] stall cycles per wave
@@ -723,7 +751,8 @@ __global__ __launch_bounds__(SCHED == 4 ? kFusedThreads + 64 : kFusedThreads) vo
 }
 
 constexpr size_t rows_lds_bytes(int T, int sched, int H = 1) {
-    return 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) + (sched >= 1 ? (4 / T) * 8 * 64 * H * sizeof(float4) : 0) +
+    return 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) +
+           ((sched >= 1 && sched <= 4) ? (4 / T) * 8 * 64 * H * sizeof(float4) : 0) +  // x slab in LDS
            (8 * 4 * 3 + 8 + 4) * sizeof(float);
 }
 static_assert(rows_lds_bytes(4, 4, 2) <= 160 * 1024, "wide bf16 tiles: T = 4 fits the LDS");
@@ -732,7 +761,7 @@ static int g_fused_dbg = 0;    // diagnostics only (set through fused_set_debug)
 static int g_fused_sched = 4;  // variant 6 pipeline schedule (k_fused_sweep_rows SCHED)
 void fused_set_debug(int flags) { g_fused_dbg = flags; }
 void fused_set_schedule(int sched) {
-    if (sched < 0 || sched > 4) throw std::runtime_error("fused_set_schedule: 0 .. 4");
+    if (sched < 0 || sched > 5) throw std::runtime_error("fused_set_schedule: 0 .. 5");
     g_fused_sched = sched;
 }
 int fused_get_schedule() { return g_fused_sched; }
@@ -778,7 +807,7 @@ static void launch_lds(bool logmode, dim3 grid, hipStream_t stream, const float*
 template <bool LG, bool X, bool D, int T, int SC, typename AT = float, int CPL = 4>
 static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                           const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
-                          uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
+                          uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, int64_t fold_tiles) {
     constexpr size_t lds = rows_lds_bytes(T, SC, CPL / 4);
     static bool configured = false;
     if (!configured) {
@@ -787,22 +816,27 @@ static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld
         configured = true;
     }
     hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC, AT, CPL>), grid,
-                       dim3(SC == 4 ? kFusedThreads + 64 : kFusedThreads), lds, stream, A, ld, nrows, nrows_pad, x,
-                       ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt);
+                       dim3((SC == 4 || SC == 5) ? kFusedThreads + 64 : kFusedThreads), lds, stream, A, ld, nrows,
+                       nrows_pad, x,
+                       ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt, T == 1 ? fold_tiles : 0);
 }
 
 template <int T>
 static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
                         int64_t nrows_pad, const float* x_, const float* ghat, const float* arow, float* partial,
-                        double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt) {
+                        double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt,
+                        int64_t fold_tiles) {
     const bool diag = (g_fused_dbg & 2) != 0;  // instrumented build only when asked (timing diagnostics)
     // g_fused_sched: pipeline schedule (k_fused_sweep_rows SCHED); schedules 1-4 hold the x slab in LDS,
-    // which has room for it only when T >= 2. Instrumented builds: schedules 0, 2 and 4.
-    int sched = T >= 2 ? g_fused_sched : 0;
+    // which has room for it only when T >= 2. T = 1 runs schedule 5 (the split exchange with the x slab in
+    // VGPRs) under the default schedule 4 (or 5): +10-14 % over schedule 0 at 73k-262k columns, with and
+    // without idle CUs (profiles/probe_r2_t1_sched5.jsonl); schedules 0-3 select schedule 0 for T = 1.
+    // Instrumented builds: schedules 0, 2 and 4.
+    int sched = T >= 2 ? (g_fused_sched == 5 ? 4 : g_fused_sched) : (g_fused_sched >= 4 ? 5 : 0);
     if (diag && sched != 2 && sched != 4) sched = 0;
     auto go = [&](auto lg, auto d, auto sc) {
         launch_rows_t<decltype(lg)::value, true, decltype(d)::value, T, decltype(sc)::value>(
-            grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
+            grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt, fold_tiles);
     };
     using TT = std::true_type;
     using FF = std::false_type;
@@ -811,6 +845,7 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
     using S2 = std::integral_constant<int, (T >= 2 ? 2 : 0)>;
     using S3 = std::integral_constant<int, (T >= 2 ? 3 : 0)>;
     using S4 = std::integral_constant<int, (T >= 2 ? 4 : 0)>;
+    using S5 = std::integral_constant<int, (T == 1 ? 5 : 4)>;
     auto by_log = [&](auto d, auto sc) {
         if (logmode) go(TT{}, d, sc); else go(FF{}, d, sc);
     };
@@ -825,6 +860,7 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
         case 2: by_log(FF{}, S2{}); break;
         case 3: by_log(FF{}, S3{}); break;
         case 4: by_log(FF{}, S4{}); break;
+        case 5: by_log(FF{}, S5{}); break;
         default: by_log(FF{}, S0{}); break;
     }
 }
@@ -851,7 +887,7 @@ int fused_tile_rows(int K, int variant) {
 void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows,
                         int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
                         double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt,
-                        hipStream_t stream) {
+                        hipStream_t stream, int64_t fold_tiles) {
     if (variant != 3 && variant != 6) throw std::runtime_error("fused_sweep: variant must be 6 or 3");
     const dim3 grid((unsigned)(I * J));
     if (variant == 6) {
@@ -862,9 +898,12 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
         if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v6: padded rows must be a multiple of 4");
         if (J * T > kRowsGather) throw std::runtime_error("fused_sweep v6: J * T > 256");
         if (xcnt == nullptr || I % 8 != 0) throw std::runtime_error("fused_sweep v6: needs the per-XCD ticket counters and I % 8 == 0");
-        if (T == 1) launch_rows<1>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
-        else if (T == 2) launch_rows<2>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
-        else launch_rows<4>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt);
+        if (T == 1) launch_rows<1>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
+                        fold_tiles);
+        else if (T == 2) launch_rows<2>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
+                        fold_tiles);
+        else launch_rows<4>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
+                        fold_tiles);
         check_launch("k_fused_sweep_rows");
         return;
     }
@@ -884,11 +923,12 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
 
 // bf16-stored RTM: variant 6 only (XCD-local row groups, same exchange as fp32). cpl 8 ("wide": 16-byte loads of
 // 8 bf16 per lane, slab 16384 / T columns) needs T = 4 (schedule 4, x slab in LDS); cpl 4 ("narrow": 8-byte
-// loads, slab 8192 / T) runs schedule 4 for T >= 2 and 0 for T = 1. A protocol timeout falls back to the bf16
-// two-pass kernels.
+// loads, slab 8192 / T) runs schedule 4 for T >= 2 and for T = 1 schedule 0 with the deep bf16 lag (or 5 when
+// selected). A protocol timeout falls back to the bf16 two-pass kernels.
 void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                              const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
-                             uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream, int cpl) {
+                             uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream, int cpl,
+                             int64_t fold_tiles) {
     if (T != 1 && T != 2 && T != 4) throw std::runtime_error("fused_sweep bf16: rows per tile must be 1, 2 or 4");
     if (cpl != 4 && !(cpl == 8 && T == 4)) throw std::runtime_error("fused_sweep bf16: wide tiles need T = 4");
     if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep bf16: padded rows must be a multiple of 4");
@@ -900,14 +940,16 @@ void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, i
     auto go = [&](auto lg, auto tt, auto sc, auto cp) {
         launch_rows_t<decltype(lg)::value, true, false, decltype(tt)::value, decltype(sc)::value, bf16_t,
                       decltype(cp)::value>(grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
-                                           I, J, st, xcnt);
+                                           I, J, st, xcnt, fold_tiles);
     };
     using S0 = std::integral_constant<int, 0>;
     using S4 = std::integral_constant<int, 4>;
+    using S5 = std::integral_constant<int, 5>;
     using C4 = std::integral_constant<int, 4>;
     using C8 = std::integral_constant<int, 8>;
     auto by_t = [&](auto lg) {
         if (cpl == 8) go(lg, std::integral_constant<int, 4>{}, S4{}, C8{});
+        else if (T == 1 && g_fused_sched == 5) go(lg, std::integral_constant<int, 1>{}, S5{}, C4{});
         else if (T == 1) go(lg, std::integral_constant<int, 1>{}, S0{}, C4{});
         else if (T == 2) go(lg, std::integral_constant<int, 2>{}, S4{}, C4{});
         else go(lg, std::integral_constant<int, 4>{}, S4{}, C4{});

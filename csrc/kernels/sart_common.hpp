@@ -134,6 +134,13 @@ __device__ __forceinline__ void fma4(float4& acc, const float4 a, const float s)
     acc.w = fmaf(a.w, s, acc.w);
 }
 
+__device__ __forceinline__ void add4(float4& acc, const float4 a) {
+    acc.x += a.x;
+    acc.y += a.y;
+    acc.z += a.z;
+    acc.w += a.w;
+}
+
 // Launch-time error check used by every host launcher.
 void check_launch(const char* what);
 // Checked HIP runtime call (throws std::runtime_error with `what` and the HIP error string).

@@ -36,8 +36,8 @@ def test_width_sweep_variant6_and_waste():
         _check_v6(ld, rtm.fused_geometry(ld, CUS, 6))
 
 
-@pytest.mark.parametrize("ld,T,J,I", [(65536, 4, 32, 8), (131072, 2, 32, 8), (262144, 1, 32, 8),
-                                      (61440, 4, 30, 8), (16384, 4, 8, 32)])
+@pytest.mark.parametrize("ld,T,J,I", [(65536, 4, 32, 8), (131072, 1, 16, 16), (262144, 1, 32, 8),
+                                      (61440, 4, 30, 8), (16384, 4, 8, 32), (106496, 1, 13, 16)])
 def test_production_geometries(ld, T, J, I):
     g = rtm.fused_geometry(ld, CUS, 6)
     assert (g.T, g.J, g.I) == (T, J, I)
@@ -51,6 +51,14 @@ def test_lowest_cost_rows_per_tile():
     assert (ld, g.T, g.J, g.I) == (73728, 1, 9, 24)
 
 
+def test_t2_penalty_prefers_t1():
+    # 100000 columns: T = 2 at ld 102400 (J = 25, one group per XCD) against T = 1 at ld 106496 (J = 13, two
+    # groups per XCD): equal slab / G, T = 2 measured slower per byte (profiles/probe_r2_t1_sched5.jsonl)
+    assert rtm.choose_ld(100000) == 106496
+    g2 = rtm.fused_geometry(131072, CUS, 6, 2)
+    assert (g2.T, g2.J, g2.I) == (2, 32, 8)  # still available when forced
+
+
 def test_forced_rows_per_tile_and_fallback():
     g = rtm.fused_geometry(65536, CUS, 6, 1)
     assert (g.T, g.J, g.I) == (1, 8, 32)
@@ -60,6 +68,23 @@ def test_forced_rows_per_tile_and_fallback():
     assert rtm.fused_geometry(65536, CUS, 3).variant == 3
     # not a multiple of 1024: no fused path
     assert rtm.fused_geometry(64 * 1001, CUS, 6) is None
+
+
+def test_t1_fold_period(monkeypatch):
+    """T = 1 sweeps fold their back-projection chains every ~sqrt(rows per group) tiles (two-level sums: the
+    single-chain version measured 26x the two-pass error at 524288 rows); T >= 2 and variant 3 never fold."""
+    k = hip()
+    monkeypatch.delenv("SART_FUSED_FOLD", raising=False)
+    g1 = k.fused_geometry(262144, CUS, 6, 1)
+    assert g1.T == 1
+    for rows in (4096, 65536, 524288):
+        f = k.fused_fold_tiles(g1, rows)
+        per_group = -(-rows // g1.I)
+        assert 16 <= f and (f - 1) ** 2 < max(per_group, 256) <= f * f + 2 * f
+    assert k.fused_fold_tiles(k.fused_geometry(65536, CUS, 6, 4), 65536) == 0
+    assert k.fused_fold_tiles(k.fused_geometry(65536, CUS, 3, 0), 65536) == 0
+    monkeypatch.setenv("SART_FUSED_FOLD", "0")
+    assert k.fused_fold_tiles(g1, 65536) == 0
 
 
 def test_python_is_native():

@@ -218,7 +218,7 @@ def test_bf16_fused_rows_per_tile(dev, T, log):
     assert np.linalg.norm(r1.solution - rt.solution) / np.linalg.norm(rt.solution) < 3e-3
 
 
-@pytest.mark.parametrize("nvox,J,I", [(4096, 1, 256), (65536, 16, 16), (131072, 32, 8), (100000, 25, 8)])
+@pytest.mark.parametrize("nvox,J,I", [(4096, 1, 256), (65536, 16, 16), (131072, 32, 8), (100000, 26, 8)])
 @pytest.mark.parametrize("log", [False, True])
 def test_bf16_wide_tiles(dev, monkeypatch, nvox, J, I, log):
     """Wide bf16 tiles (16-byte loads of 8 bf16 per lane, slab 4096 columns at T = 4) against the narrow bf16

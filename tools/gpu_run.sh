@@ -71,14 +71,34 @@ for step in "$@"; do
                 done ;;
     benchbf16big) run bench_bf16_512kx256k 900 python bench.py --steps 2 --warmup 1 --rtm-dtype bf16 \
                     --npix 524288 --nvox 262144 --iters 20 ;;
+    benchbf16big5) SART_FUSED_SCHEDULE=5 run bench_bf16_512kx256k_s5 900 python bench.py --steps 2 --warmup 1 \
+                     --rtm-dtype bf16 --npix 524288 --nvox 262144 --iters 20 ;;
     benchlap) run bench_lap 600 python bench.py --steps 5 --warmup 1 --laplacian ;;
     probe) run probe 600 python tools/probe.py ;;
+    fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
+            SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
+            run fcheck_fp32 600 python tools/fused_check.py 8192x262144 65536x262144 16384x65536 ;;
+    foldsmall) SART_FUSED_FOLD=0 run fcheck_small_nofold 150 python tools/fused_check.py 16384x262144 &&
+              run fcheck_small_fold 150 python tools/fused_check.py 16384x262144 &&
+              SART_FUSED_FOLD=8 run fcheck_small_fold8 150 python tools/fused_check.py --dtype bf16 8192x131072 ;;
+    foldperf) for v in 200000 100000 262144; do
+                run bench_w${v}_fold 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck &&
+                SART_FUSED_FOLD=0 run bench_w${v}_nofold 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
+              done ;;
+    foldcheck) run fcheck_fold_bf16 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
+              SART_FUSED_FOLD=0 run fcheck_nofold_bf16 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
+              SART_FUSED_FOLD=64 run fcheck_fold64_bf16 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
+              run fcheck_fold_fp32 600 python tools/fused_check.py 65536x262144 8192x204800 &&
+              run bench_w200000 300 python bench.py --steps 3 --warmup 1 --nvox 200000 &&
+              SART_FUSED_FOLD=0 run bench_w200000_nofold 300 python bench.py --steps 3 --warmup 1 --nvox 200000 ;;
     numerics) run numerics 600 python tools/numerics_check.py ;;
     benchw) for v in 65536 60000 100000 200000 70000; do
               run bench_w$v 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
             done ;;
     trace) run fused_trace 600 python tools/fused_trace.py ;;
     probef) PROBE_FUSED_ONLY=1 run probe_fused 600 python tools/probe.py ;;
+    probet1) PROBE_FUSED_ONLY=1 PROBE_CFGS=6:1:0,6:1:5,6:0:4 run probe_t1 600 python tools/probe.py \
+              4096x262144 4096x204800 16384x73728 8192x106496 16384x65536 8192x131072 ;;
     probew) PROBE_FUSED_ONLY=1 PROBE_CFGS=${PROBE_CFGS:-6:0:4,3:0:0} run probe_widths 600 python tools/probe.py \
               16384x65536 16384x61440 16384x73728 8192x131072 8192x102400 4096x262144 4096x204800 ;;
     commcheck) for n in 2 4; do
