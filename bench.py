@@ -139,16 +139,17 @@ def main() -> int:
     ap.add_argument("--laplacian", action="store_true",
                     help="add the 7-point grid Laplacian regulariser (beta 1e-2, the reference default)")
     ap.add_argument("--rtm-dtype", choices=["fp32", "bf16"], default="fp32",
-                    help="RTM storage precision; bf16 is opt-in (half the bytes per sweep, fp32 products and sums, "
-                         "two-pass kernels); the BASELINE headline is fp32")
+                    help="RTM storage precision; bf16 is opt-in (half the bytes per sweep; fp32 products and sums in "
+                         "the single-frame kernels, bf16 MFMA with hi+lo split X / W and fp32 accumulation with "
+                         "--frames); the BASELINE headline is fp32")
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
                     help="BASELINE.json configuration preset (sets npix / nvox / iters / frames / laplacian)")
     args = ap.parse_args()
     if args.config:
         for k, v in PRESETS[args.config].items():
             setattr(args, k, v)
-    if args.rtm_dtype == "bf16" and (args.frames > 1 or args.partition == "cols"):
-        ap.error("--rtm-dtype bf16 runs single-frame row shards (two-pass kernels)")
+    if args.rtm_dtype == "bf16" and args.partition == "cols":
+        ap.error("--rtm-dtype bf16 runs row shards")
     if args.partition == "cols" and args.frames > 1:
         ap.error("--partition cols solves single frames (the multi-frame engine uses row shards)")
 
@@ -316,7 +317,9 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "fp32" if args.rtm_dtype == "fp32" else "bf16 RTM storage, fp32 compute",
+        "dtype": "fp32" if args.rtm_dtype == "fp32" else (
+            "bf16 RTM storage, bf16 MFMA with hi+lo bf16 split of X / W, fp32 accumulation" if multi
+            else "bf16 RTM storage, fp32 compute"),
         "data": "synthetic (on-device random dense RTM, random phantom; no HDF5)",
         "iters_per_s": round(iters_per_s, 3),
         "sart_iterations_per_step": args.iters,

@@ -227,7 +227,7 @@ static void bind_engine(py::module_& m) {
         .def(py::init([](int device, uintptr_t A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
                          std::shared_ptr<sart::Communicator> comm, const sart::EngineConfig& cfg) {
                  try {
-                     return new sart::MultiFrameEngine(device, P<const float>(A), nrows, nrows_pad, nvoxel, ld,
+                     return new sart::MultiFrameEngine(device, P<const void>(A), nrows, nrows_pad, nvoxel, ld,
                                                        comm.get(), cfg);
                  } catch (const std::invalid_argument& e) {
                      throw py::value_error(e.what());
@@ -415,6 +415,27 @@ PYBIND11_MODULE(_sart_hip, m) {
                                 nsplit, nf, S(stream));
     }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("nrows_pad"), py::arg("X"), py::arg("ldx"),
        py::arg("Fout"), py::arg("nsplit"), py::arg("stream"), py::arg("nf") = 16);
+    m.def("mf_backproject_b16_num_splits", &sart::mf_backproject_b16_num_splits);
+    m.def("mf_split_x", [](uintptr_t X, int64_t n, uintptr_t hi, uintptr_t lo, uintptr_t stream) {
+        sart::launch_mf_split_x(P<const float>(X), n, P<sart::bf16_t>(hi), P<sart::bf16_t>(lo), S(stream));
+    });
+    m.def("mf_split_w", [](uintptr_t W, int64_t nrows_pad, int nf, int64_t ldw, uintptr_t hi, uintptr_t lo,
+                           uintptr_t stream) {
+        sart::launch_mf_split_w(P<const float>(W), nrows_pad, nf, ldw, P<sart::bf16_t>(hi), P<sart::bf16_t>(lo),
+                                S(stream));
+    });
+    m.def("mf_forward_b16", [](uintptr_t A, int64_t ld, int64_t nrows, int64_t nrows_pad, uintptr_t Xh, uintptr_t Xl,
+                               uintptr_t Fout, int nsplit, uintptr_t stream, int nf) {
+        sart::launch_mf_forward_b16(P<const sart::bf16_t>(A), ld, nrows, nrows_pad, P<const sart::bf16_t>(Xh),
+                                    P<const sart::bf16_t>(Xl), P<float>(Fout), nsplit, nf, S(stream));
+    });
+    m.def("mf_backproject_b16", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t Wh, uintptr_t Wl, int64_t ldw,
+                                   int nsplit, uintptr_t partial, uintptr_t stream, int nf, int64_t v0, int64_t v1) {
+        sart::launch_mf_backproject_b16(P<const sart::bf16_t>(A), ld, nrows, P<const sart::bf16_t>(Wh),
+                                        P<const sart::bf16_t>(Wl), ldw, nsplit, P<float>(partial), nf, S(stream), v0,
+                                        v1);
+    }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("Wh"), py::arg("Wl"), py::arg("ldw"), py::arg("nsplit"),
+       py::arg("partial"), py::arg("stream"), py::arg("nf") = 16, py::arg("v0") = 0, py::arg("v1") = -1);
     m.def("mf_backproject", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t W, int nsplit, uintptr_t partial,
                                uintptr_t stream, int nf) {
         sart::launch_mf_backproject(P<const float>(A), ld, nrows, P<const float>(W), nsplit, P<float>(partial), nf,

@@ -246,7 +246,8 @@ int main(int argc, char** argv) {
             EngineConfig ec;
             static_cast<SolverParams&>(ec) = params;
             ec.mf_frames = cfg.batch_frames;  // batch width 16, 32 or 64 (rounded up, capped at 64)
-            mf = std::make_unique<MultiFrameEngine>(device, static_cast<const float*>(dshard->A), dshard->nrows,
+            ec.rtm_bf16 = dshard->bf16;       // bf16 MFMA projections
+            mf = std::make_unique<MultiFrameEngine>(device, dshard->A, dshard->nrows,
                                                     dshard->nrows_pad, dshard->nvoxel, dshard->ld, dcomm.get(), ec);
             if (lap.nnz()) mf->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
         } else if (gpu) {

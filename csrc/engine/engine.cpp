@@ -88,6 +88,7 @@ template class DeviceArray<uint64_t>;
 template class DeviceArray<unsigned>;
 template class DeviceArray<int64_t>;
 template class DeviceArray<int32_t>;
+template class DeviceArray<bf16_t>;
 
 Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
                Communicator* comm, const EngineConfig& cfg)

@@ -20,11 +20,11 @@ void hip_ok(hipError_t e, const char* what) {
 
 int MultiFrameEngine::batch_width(int frames) { return frames <= 16 ? 16 : (frames <= 32 ? 32 : 64); }
 
-MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel,
+MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel,
                                    int64_t ld, Communicator* comm, const EngineConfig& cfg)
-    : device_(device), A_(A), P_(nrows), Pp_(nrows_pad), V_(nvoxel), ld_(ld), comm_(comm), cfg_(cfg) {
+    : device_(device), A_(A), bf16_(cfg.rtm_bf16), P_(nrows), Pp_(nrows_pad), V_(nvoxel), ld_(ld), comm_(comm),
+      cfg_(cfg) {
     validate_params(cfg_);
-    if (cfg_.rtm_bf16) throw std::invalid_argument("MultiFrameEngine: bf16 RTM storage is not supported (fp32 MFMA)");
     if (!comm_) throw std::invalid_argument("MultiFrameEngine: communicator required");
     if (ld_ % 64 || ld_ < V_ || Pp_ % 64 || Pp_ < P_)
         throw std::invalid_argument("MultiFrameEngine: ld and nrows_pad must be multiples of 64 covering the shard");
@@ -39,7 +39,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, in
     hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hg_), std::max<int64_t>(P_, 1) * NF * sizeof(double)),
            "hipHostMalloc");
     nsf_ = mf_forward_num_splits(ld_, Pp_);
-    nsb_ = mf_backproject_num_splits(ld_, P_);
+    nsb_ = bf16_ ? mf_backproject_b16_num_splits(ld_, P_) : mf_backproject_num_splits(ld_, P_);
     nwb_ = mf_weights_num_blocks(Pp_);
     X_.resize((size_t)NF * ld_);
     Xprev_.resize((size_t)NF * ld_);
@@ -55,7 +55,11 @@ MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, in
     G64_.resize(NF);
     F2part_.resize((size_t)nwb_ * NF);
     st_.resize(1);
-    rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_);
+    if (bf16_) {
+        for (auto* b : {&Xh_, &Xl_}) b->resize((size_t)NF * ld_);
+        for (auto* b : {&Wh_, &Wl_}) b->resize((size_t)NF * Pp_);
+    }
+    rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_, false, bf16_);
     // chunks of the overlapped back-projection / all-reduce pipeline (several ranks only): SART_MF_CHUNKS
     // (default 4) voxel ranges aligned to the back-projection's voxel tile, each >= 1 MiB of corrections
     int nchunks = 1;
@@ -65,7 +69,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const float* A, int64_t nrows, in
         const int64_t min_vox = std::max<int64_t>(1, (1 << 20) / (4 * NF));
         nchunks = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, ld_ / min_vox));
     }
-    const int64_t align = mf_backproject_vox_align(ld_, NF);
+    const int64_t align = bf16_ ? mf_backproject_b16_vox_align(ld_) : mf_backproject_vox_align(ld_, NF);
     chunks_.assign(1, 0);
     for (int c = 1; c < nchunks; ++c) {
         const int64_t v = (ld_ * c / nchunks) / align * align;
@@ -111,13 +115,33 @@ void MultiFrameEngine::set_laplacian(const int64_t* row_ptr, const int32_t* col,
     has_lap_ = true;
 }
 
+void MultiFrameEngine::forward() {
+    if (bf16_) {
+        launch_mf_split_x(X_.get(), (int64_t)nf_ * ld_, Xh_.get(), Xl_.get(), stream_);
+        launch_mf_forward_b16(static_cast<const bf16_t*>(A_), ld_, P_, Pp_, Xh_.get(), Xl_.get(), Fs_.get(), nsf_, nf_,
+                              stream_);
+    } else {
+        launch_mf_forward(static_cast<const float*>(A_), ld_, P_, Pp_, X_.get(), ld_, Fs_.get(), nsf_, nf_, stream_);
+    }
+}
+
+void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int64_t v1) {
+    if (bf16_) {
+        if (split_w) launch_mf_split_w(W, Pp_, nf_, Pp_, Wh_.get(), Wl_.get(), stream_);
+        launch_mf_backproject_b16(static_cast<const bf16_t*>(A_), ld_, P_, Wh_.get(), Wl_.get(), Pp_, nsb_,
+                                  part_.get(), nf_, stream_, v0, v1);
+    } else {
+        launch_mf_backproject(static_cast<const float*>(A_), ld_, P_, W, nsb_, part_.get(), nf_, stream_, v0, v1);
+    }
+}
+
 void MultiFrameEngine::sweep() {
     const int NF = nf_;
     MfState* st = st_.get();
     float* D = buf_.get();                     // [ld][nf] voxel-major corrections
     float* F2 = buf_.get() + (int64_t)NF * ld_;  // [nf] ||A x||^2, all-reduced with the last chunk
     const float* scale = cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get();
-    launch_mf_forward(A_, ld_, P_, Pp_, X_.get(), ld_, Fs_.get(), nsf_, NF, stream_);
+    forward();
     launch_mf_weights(Fs_.get(), nsf_, Pp_, ghat_.get(), arow_.get(), cfg_.logarithmic, W_.get(), F2part_.get(),
                       NF, stream_);
     const int nc = (int)chunks_.size() - 1;
@@ -129,7 +153,7 @@ void MultiFrameEngine::sweep() {
         // still overlaps with them.
         for (int c = 0; c < nc; ++c) {
             const int64_t v0 = chunks_[c], v1 = chunks_[c + 1];
-            launch_mf_backproject(A_, ld_, P_, W_.get(), nsb_, part_.get(), NF, stream_, v0, v1);
+            backproject(W_.get(), c == 0, v0, v1);
             const bool last = c == nc - 1;
             launch_mf_collect(part_.get(), nsb_, ld_, v0, v1, scale, D, last ? F2part_.get() : nullptr, nwb_,
                               last ? F2 : nullptr, NF, stream_);
@@ -143,7 +167,7 @@ void MultiFrameEngine::sweep() {
         }
         hip_ok(hipEventRecord(comm_done_, comm_stream_), "event");
     } else {
-        launch_mf_backproject(A_, ld_, P_, W_.get(), nsb_, part_.get(), NF, stream_);
+        backproject(W_.get(), true, 0, ld_);
         launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, scale, D, F2part_.get(), nwb_, F2, NF, stream_);
         if (comm_->size() > 1) comm_->all_reduce(buf_.get(), (size_t)NF * ld_ + NF, ReduceOp::kSum, stream_);
     }
@@ -195,13 +219,13 @@ void MultiFrameEngine::solve_group(const double* g, int B, double* x_out, SolveI
         launch_mf_init_warm(X_.get(), x064_.get(), norm64_.get(), V_, ld_, B, NF, stream_);
     } else {
         // cold start x0 = max([rho > tau] A^T max(ghat, 0) / rho, 1e-7) per frame (reference sart_kernels.cu:22-60)
-        launch_mf_backproject(A_, ld_, P_, gpos_.get(), nsb_, part_.get(), NF, stream_);
+        backproject(gpos_.get(), true, 0, ld_);
         launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, nullptr, buf_.get(), nullptr, 0, nullptr, NF, stream_);
         comm_->all_reduce(buf_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
         launch_mf_init(X_.get(), buf_.get(), rs_.dinv.get(), V_, ld_, B, NF, stream_);
     }
     if (cfg_.logarithmic) {  // frame-constant observed back-projection, reduced once per batch
-        launch_mf_backproject(A_, ld_, P_, wo_.get(), nsb_, part_.get(), NF, stream_);
+        backproject(wo_.get(), true, 0, ld_);
         launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, rs_.dmask.get(), O_.get(), nullptr, 0, nullptr, NF, stream_);
         comm_->all_reduce(O_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
     }

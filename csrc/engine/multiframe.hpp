@@ -22,7 +22,8 @@ namespace sart {
 
 class MultiFrameEngine {
    public:
-    MultiFrameEngine(int device, const float* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
+    // A: fp32 [nrows_pad][ld], or bf16 when cfg.rtm_bf16 (bf16 MFMA projections, multiframe_bf16.hip)
+    MultiFrameEngine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
                      Communicator* comm, const EngineConfig& cfg);
     ~MultiFrameEngine();
     MultiFrameEngine(const MultiFrameEngine&) = delete;
@@ -45,9 +46,15 @@ class MultiFrameEngine {
     void solve_group(const double* g, int B, double* x_out, SolveInfo* info, const double* x0);
     void sweep();
     void set_device() const;
+    // F = A X (Fs_ split-K partials); the bf16 engine first writes the X planes
+    void forward();
+    // part_ = A^T W for voxels [v0, v1) (W in the back-projection layout); the bf16 engine reads the W planes,
+    // written from W when split_w
+    void backproject(const float* W, bool split_w, int64_t v0, int64_t v1);
 
     int device_;
-    const float* A_;
+    const void* A_;
+    bool bf16_ = false;
     int64_t P_, Pp_, V_, ld_;
     Communicator* comm_;
     EngineConfig cfg_;
@@ -57,6 +64,7 @@ class MultiFrameEngine {
     DeviceRaySums rs_;
     DeviceArray<float> X_, Xprev_, Fs_, W_, part_, buf_, pen_, O_, ghat_, arow_, gpos_, wo_;
     DeviceArray<double> g64_, norm64_, G64_, F2part_, x064_;
+    DeviceArray<bf16_t> Xh_, Xl_, Wh_, Wl_;  // bf16 engine: hi / lo operand planes
     DeviceArray<MfState> st_;
     DeviceArray<int64_t> lap_rp_;
     DeviceArray<int32_t> lap_col_;

@@ -114,6 +114,19 @@ int mf_backproject_vox_align(int64_t ld, int nf);
 void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,
                            int nf, hipStream_t stream, int64_t v0 = 0, int64_t v1 = -1);
 // multiframe_glue.hip
+// bf16-stored RTM (multiframe_bf16.hip): the same projections on v_mfma_f32_16x16x32_bf16 with the fp32
+// operand (X or W) split into hi + lo bf16 planes (k_mf_split_x: X [nf][ld] -> planes [nf][ld]; k_mf_split_w:
+// W [rows][16][nf / 16] -> frame-major planes [nf][ldw], ldw >= rows rounded up to 32).
+void launch_mf_forward_b16(const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const bf16_t* Xh,
+                           const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream);
+int mf_backproject_b16_num_splits(int64_t ld, int64_t nrows);
+int mf_backproject_b16_vox_align(int64_t ld);  // voxel-range alignment of launch_mf_backproject_b16
+void launch_mf_backproject_b16(const bf16_t* A, int64_t ld, int64_t nrows, const bf16_t* Wh, const bf16_t* Wl,
+                               int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0 = 0,
+                               int64_t v1 = -1);
+void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStream_t stream);
+void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, bf16_t* hi, bf16_t* lo,
+                       hipStream_t stream);
 void launch_mf_prep(const double* g, int64_t nrows, int64_t nrows_pad, const double* norm, const float* ray_length,
                     float len_thres, float* ghat, float* arow, float* gpos, float* wo, int nf, hipStream_t stream);
 int mf_weights_num_blocks(int64_t nrows_pad);

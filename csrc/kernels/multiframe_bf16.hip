@@ -1,0 +1,379 @@
+// Multi-frame projections of a bf16-stored RTM on the bf16 matrix cores of gfx950 (v_mfma_f32_16x16x32_bf16:
+// 16x the fp32 MFMA rate, so the skinny GEMMs of the multi-frame solver stay HBM-bound at 64 frames, where the
+// fp32 engine is matrix-core-bound; multiframe.hip).
+//
+// Numerics. The matrix is bf16 by choice of storage (--rtm_bf16: every element is exact in the operand).
+// The other operand (the solutions X of the forward projection, the SART weights W of the back-projection) is
+// fp32 state; it enters as two bf16 planes, hi = rne(x) and lo = rne(x - hi), and every product runs twice
+// (A hi + A lo) into the same fp32 accumulator: |x - hi - lo| <= 2^-17 |x|, below the storage rounding of
+// A itself (2^-9) by a factor 256, with fp32 accumulation as in the fp32 engine. The planes are written once
+// per sweep by k_mf_split_x / k_mf_split_w (multiframe_glue.hip).
+//
+// Fragment maps (cdna_hip_programming.md section 3, 16x16x32 bf16): lane l holds A[i = l & 15][k = 8 (l >> 4) + j]
+// and B[k = 8 (l >> 4) + j][n = l & 15] in element j = 0..7; C/D: n = l & 15, i = (l >> 4) * 4 + reg.
+//
+// Forward F[row][f] = sum_v A[row][v] X[f][v]: M = 16 rows, N = 16 frames, K = 32 voxels. A lane's eight k
+// are eight consecutive voxels of one row, so one 16-byte load of A and one of each X plane per 32 voxels;
+// a wave owns 16 * RT rows and reuses each X fragment RT times.
+//
+// Back-projection D[v][f] = sum_row A[row][v] W[row][f]: M = 16 voxels, N = 16 frames, K = 32 rows. A lane's
+// eight k must be eight ROWS of one voxel, while a row of A is contiguous: each lane loads 8 bytes (4 voxels)
+// of 8 rows (16 lanes x 8 B = one 128-B line per row and instruction) and regroups them with v_perm_b32 into
+// four fragments, one per voxel phase p (voxels 4 i + p of the 64-voxel block), no LDS round trip. The W
+// planes are stored frame-major [nf][rows] so a lane's eight rows are one 16-byte load.
+//
+// Ring loads are unconditional (clamped to the last step) like the fp32 kernels: the compiler then keeps
+// DEPTH steps of loads in flight with counted vmcnt waits.
+#include "sart_common.hpp"
+
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <utility>
+
+namespace sart {
+
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ floatx4 mfma_b16(const uint4 a, const uint4 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+}
+
+// Fragment of voxel phase P from the eight 8-byte row loads: element j = bf16 P of row load j.
+template <int P>
+__device__ __forceinline__ uint4 phase_frag(const uint2 (&v)[8]) {
+    constexpr unsigned sel = (P & 1) ? 0x07060302u : 0x05040100u;  // high / low halves of (S1, S0)
+    auto d = [&](int m) {
+        const unsigned a = (P >> 1) ? v[2 * m].y : v[2 * m].x;
+        const unsigned b = (P >> 1) ? v[2 * m + 1].y : v[2 * m + 1].x;
+        return __builtin_amdgcn_perm(b, a, sel);  // bytes 0-3 select from a (S1), 4-7 from b (S0)
+    };
+    return make_uint4(d(0), d(1), d(2), d(3));
+}
+
+}  // namespace
+
+// Split-K over columns: blockIdx.y selects [c0, c1) (multiples of 64); Fout + blockIdx.y * nrows_pad * nf.
+// A step covers KB blocks of 32 voxels; with KB = 2 the two loads of a row are the two halves of one 128-byte
+// line, issued back to back.
+template <int NG, int DEPTH, int RT, int KB>
+__global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict__ A, int64_t ld, int64_t nrows,
+                                                        int64_t nrows_pad, const bf16_t* __restrict__ Xh,
+                                                        const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
+                                                        int64_t cols_per_split) {
+    constexpr int NF = 16 * NG;
+    constexpr int RS = DEPTH + 1;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * (16 * RT);
+    if (row0 >= nrows_pad) return;  // wave-uniform; nrows_pad is a multiple of 16 * RT
+    const int g = lane >> 4, r = lane & 15;
+    const int64_t c0 = (int64_t)blockIdx.y * cols_per_split;
+    const int64_t c1 = (c0 + cols_per_split < ld) ? c0 + cols_per_split : ld;
+    Fout += (int64_t)blockIdx.y * nrows_pad * NF;
+    const bf16_t* __restrict__ ap = A + (row0 + r) * ld + c0 + 8 * g;
+    const int64_t xo = (int64_t)r * ld + c0 + 8 * g;  // frame r of column group 0; group j: + 16 j ld
+
+    floatx4 acc[RT][NG];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int j = 0; j < NG; ++j) acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int64_t nst = c1 > c0 ? (c1 - c0) / (32 * KB) : 0;
+    if (nst > 0) {
+        uint4 a[RS][RT][KB], xh[RS][NG][KB], xl[RS][NG][KB];
+        auto load = [&](int sl, int64_t t) {
+            const int64_t q = t * 32 * KB;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int kb = 0; kb < KB; ++kb)
+                    a[sl][rt][kb] = *reinterpret_cast<const uint4*>(ap + rt * 16 * ld + q + 32 * kb);
+#pragma unroll
+            for (int j = 0; j < NG; ++j)
+#pragma unroll
+                for (int kb = 0; kb < KB; ++kb) {
+                    xh[sl][j][kb] = *reinterpret_cast<const uint4*>(Xh + xo + (int64_t)j * 16 * ld + q + 32 * kb);
+                    xl[sl][j][kb] = *reinterpret_cast<const uint4*>(Xl + xo + (int64_t)j * 16 * ld + q + 32 * kb);
+                }
+        };
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) load(d, d < nst ? d : nst - 1);
+        auto step = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            load((sl + DEPTH) % RS, t + DEPTH < nst ? t + DEPTH : nst - 1);
+            if (t >= nst) return;
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+                for (int j = 0; j < NG; ++j)
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt) {
+                        acc[rt][j] = mfma_b16(a[sl][rt][kb], xh[sl][j][kb], acc[rt][j]);
+                        acc[rt][j] = mfma_b16(a[sl][rt][kb], xl[sl][j][kb], acc[rt][j]);
+                    }
+        };
+        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+            }(std::make_integer_sequence<int, RS>{});
+        }
+    }
+    // D: n = frame 16 j + (lane & 15), i = (lane >> 4) * 4 + reg = row within the 16-row tile
+#pragma unroll
+    for (int j = 0; j < NG; ++j)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t ra = row0 + rt * 16 + g * 4 + i;
+                if (ra < nrows) Fout[ra * NF + 16 * j + r] = acc[rt][j][i];
+            }
+}
+
+// partial[s][v][f] = sum_{rows of split s} A[row][v] W[row][f] for the 64-voxel blocks from vb0 up to voxel
+// vend; W planes [nf][ldw] (frame-major). Rows are processed up to nrows32 (rows rounded up to 32: the padding
+// rows of A and W are zero). One wave: VT blocks of 64 voxels x nf frames (each W fragment feeds 4 VT MFMAs).
+template <int NG, int DEPTH, int VT>
+__global__ __launch_bounds__(256) void k_mf_backproject_b16(const bf16_t* __restrict__ A, int64_t ld,
+                                                            int64_t nrows32, const bf16_t* __restrict__ Wh,
+                                                            const bf16_t* __restrict__ Wl, int64_t ldw,
+                                                            int64_t rows_per_split, float* __restrict__ partial,
+                                                            int64_t vb0, int64_t vend) {
+    constexpr int NF = 16 * NG;
+    constexpr int RS = DEPTH + 1;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t vb = (vb0 + (int64_t)blockIdx.x * 4 + wave) * VT;  // first block of 64 voxels
+    if (vb * 64 >= vend) return;  // (the range is a multiple of 64 * VT voxels)
+    const int g = lane >> 4, i16 = lane & 15;
+    const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
+    int64_t r_end = r_begin + rows_per_split;
+    if (r_end > nrows32) r_end = nrows32;
+    const bf16_t* __restrict__ ap = A + (r_begin + 8 * g) * ld + vb * 64 + 4 * i16;  // + (32 t + j) ld
+    const int64_t wo = (int64_t)i16 * ldw + r_begin + 8 * g;                        // + 16 j ldw + 32 t
+
+    floatx4 acc[VT][4][NG];
+#pragma unroll
+    for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int j = 0; j < NG; ++j) acc[vt][p][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 32 : 0;
+    if (nst > 0) {
+        uint2 av[RS][VT][8];
+        uint4 wh[RS][NG], wl[RS][NG];
+        auto load = [&](int sl, int64_t t) {
+            const bf16_t* at = ap + t * 32 * ld;
+#pragma unroll
+            for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    av[sl][vt][j] = load_stream(reinterpret_cast<const uint2*>(at + j * ld + vt * 64));
+#pragma unroll
+            for (int j = 0; j < NG; ++j) {
+                wh[sl][j] = *reinterpret_cast<const uint4*>(Wh + wo + (int64_t)j * 16 * ldw + t * 32);
+                wl[sl][j] = *reinterpret_cast<const uint4*>(Wl + wo + (int64_t)j * 16 * ldw + t * 32);
+            }
+        };
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) load(d, d < nst ? d : nst - 1);
+        auto step = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            load((sl + DEPTH) % RS, t + DEPTH < nst ? t + DEPTH : nst - 1);
+            if (t >= nst) return;
+#pragma unroll
+            for (int vt = 0; vt < VT; ++vt) {
+                const uint4 fr[4] = {phase_frag<0>(av[sl][vt]), phase_frag<1>(av[sl][vt]), phase_frag<2>(av[sl][vt]),
+                                     phase_frag<3>(av[sl][vt])};
+#pragma unroll
+                for (int j = 0; j < NG; ++j)
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        acc[vt][p][j] = mfma_b16(fr[p], wh[sl][j], acc[vt][p][j]);
+                        acc[vt][p][j] = mfma_b16(fr[p], wl[sl][j], acc[vt][p][j]);
+                    }
+            }
+        };
+        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+            }(std::make_integer_sequence<int, RS>{});
+        }
+    }
+    // D: n = frame 16 j + i16, i = (lane >> 4) * 4 + q = voxel slot -> voxel 64 vb + 4 i + p
+    float* out = partial + (int64_t)blockIdx.y * ld * NF;
+#pragma unroll
+    for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t v = (vb + vt) * 64 + 4 * (g * 4 + q) + p;
+#pragma unroll
+                for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[vt][p][j][q];
+            }
+}
+
+// ---------------------------------------------------------------------------------------------- launchers
+
+static void check_nf_b16(int nf, const char* what) {
+    if (nf != 16 && nf != 32 && nf != 64) throw std::runtime_error(std::string(what) + ": nf must be 16, 32 or 64");
+}
+
+// Tunables (tools/probe_mf_b16.py): register-ring depth (SART_MF_DEPTH 1..3), forward tile (SART_MF_B16_FWD =
+// "RT,KB": 16-row tiles per wave and 32-voxel blocks per step) and back-projection voxel blocks per wave
+// (SART_MF_B16_VT 1 or 2). Defaults below from the probe at 64k x 64k (profiles/probe_r2_mf_b16.jsonl).
+static int env_int(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return (e && *e) ? std::atoi(e) : dflt;
+}
+
+static int mf_b16_depth(bool forward, int nf) {
+    const int d = env_int("SART_MF_DEPTH", 0);
+    if (d >= 1 && d <= 3) return d;
+    return forward && nf < 64 ? 3 : 2;
+}
+
+struct FwdTile {
+    int rt, kb;
+};
+static FwdTile mf_b16_fwd_tile(int nf) {
+    const char* e = std::getenv("SART_MF_B16_FWD");
+    if (e && *e) {
+        const FwdTile t{std::atoi(e), std::strchr(e, ',') ? std::atoi(std::strchr(e, ',') + 1) : 1};
+        if ((t.rt == 2 || t.rt == 4 || t.rt == 8) && (t.kb == 1 || t.kb == 2)) return t;
+    }
+    return nf == 64 ? FwdTile{8, 1} : FwdTile{4, 2};  // profiles/probe_r2_mf_b16.jsonl
+}
+
+static int mf_b16_vt(int64_t ld, int nf) {
+    const int v = env_int("SART_MF_B16_VT", 0);
+    (void)nf;
+    const int vt = (v == 1 || v == 2) ? v : 2;
+    return (vt == 2 && ld % 128 == 0) ? 2 : 1;
+}
+
+template <int NG, int DEPTH, int RT, int KB>
+static void fwd_b16_t(dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
+                      const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
+    hipLaunchKernelGGL((k_mf_forward_b16<NG, DEPTH, RT, KB>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, Xh,
+                       Xl, Fout, cps);
+}
+
+template <int NG, int DEPTH>
+static void fwd_b16_d(FwdTile tl, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows,
+                      int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
+    if (tl.rt == 2 && tl.kb == 2)
+        fwd_b16_t<NG, DEPTH, 2, 2>(grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+    else if (tl.rt == 4 && tl.kb == 2)
+        fwd_b16_t<NG, DEPTH, 4, 2>(grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+    else if (tl.rt == 8)
+        fwd_b16_t<NG, DEPTH, 8, 1>(grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+    else
+        fwd_b16_t<NG, DEPTH, 4, 1>(grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+}
+
+template <int NG>
+static void fwd_b16(int depth, FwdTile tl, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows,
+                    int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
+    if (depth == 1)
+        fwd_b16_d<NG, 1>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+    else if (depth == 2)
+        fwd_b16_d<NG, 2>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+    else
+        fwd_b16_d<NG, 3>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+}
+
+void launch_mf_forward_b16(const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const bf16_t* Xh,
+                           const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream) {
+    if (ld % 64 != 0) throw std::runtime_error("mf_forward_b16: ld must be a multiple of 64");
+    if (nsplit < 1) throw std::runtime_error("mf_forward_b16: nsplit must be >= 1");
+    check_nf_b16(nf, "mf_forward_b16");
+    FwdTile tl = mf_b16_fwd_tile(nf);
+    if (nrows_pad % (16 * tl.rt) != 0) tl = FwdTile{2, 1};  // a wave's rows must lie inside the padding
+    if (nrows_pad % 32 != 0) throw std::runtime_error("mf_forward_b16: padded rows must be a multiple of 32");
+    const int64_t cps = ((ld + nsplit - 1) / nsplit + 63) / 64 * 64;
+    const int64_t rows_per_block = 64 * tl.rt;
+    const dim3 grid((unsigned)((nrows_pad + rows_per_block - 1) / rows_per_block), (unsigned)nsplit);
+    const int d = mf_b16_depth(true, nf);
+    if (nf == 16)
+        fwd_b16<1>(d, tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+    else if (nf == 32)
+        fwd_b16<2>(d, tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+    else
+        fwd_b16<4>(d, tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+    check_launch("k_mf_forward_b16");
+}
+
+// Split-K of the bf16 back-projection: ~1024 workgroups (4 waves x 64 VT voxels each), >= 64 rows per split.
+int mf_backproject_b16_num_splits(int64_t ld, int64_t nrows) {
+    const int64_t nblk = (ld / (64 * mf_b16_vt(ld, 0)) + 3) / 4;
+    const int64_t target = env_int("SART_MF_BP_BLOCKS", 1024);
+    int64_t s = (target + nblk - 1) / nblk;
+    const int64_t smax = (nrows + 63) / 64;
+    if (s > smax) s = smax;
+    if (s < 1) s = 1;
+    return (int)s;
+}
+
+int mf_backproject_b16_vox_align(int64_t ld) { return 64 * mf_b16_vt(ld, 0); }
+
+template <int NG, int DEPTH>
+static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows32,
+                      const bf16_t* Wh, const bf16_t* Wl, int64_t ldw, int64_t rps, float* partial, int64_t vb0,
+                      int64_t vend) {
+    if (vt == 2)
+        hipLaunchKernelGGL((k_mf_backproject_b16<NG, DEPTH, 2>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
+                           ldw, rps, partial, vb0, vend);
+    else
+        hipLaunchKernelGGL((k_mf_backproject_b16<NG, DEPTH, 1>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
+                           ldw, rps, partial, vb0, vend);
+}
+
+template <int NG>
+static void bwd_b16(int depth, int vt, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows32,
+                    const bf16_t* Wh, const bf16_t* Wl, int64_t ldw, int64_t rps, float* partial, int64_t vb0,
+                    int64_t vend) {
+    if (depth == 1)
+        bwd_b16_d<NG, 1>(vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend);
+    else if (depth == 2)
+        bwd_b16_d<NG, 2>(vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend);
+    else
+        bwd_b16_d<NG, 3>(vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend);
+}
+
+void launch_mf_backproject_b16(const bf16_t* A, int64_t ld, int64_t nrows, const bf16_t* Wh, const bf16_t* Wl,
+                               int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0,
+                               int64_t v1) {
+    if (ld % 64 != 0) throw std::runtime_error("mf_backproject_b16: ld must be a multiple of 64");
+    check_nf_b16(nf, "mf_backproject_b16");
+    const int64_t nrows32 = (nrows + 31) / 32 * 32;
+    if (ldw < nrows32 || ldw % 8 != 0)
+        throw std::runtime_error("mf_backproject_b16: W planes must hold the rows rounded up to 32 (ldw % 8 == 0)");
+    if (v1 < 0) v1 = ld;
+    const int vt = mf_b16_vt(ld, nf);
+    const int64_t align = 64 * vt;
+    if (v0 < 0 || v1 > ld || v0 >= v1 || v0 % align != 0 || v1 % align != 0)
+        throw std::runtime_error("mf_backproject_b16: voxel range must be aligned to the wave's voxel tile");
+    if (nsplit < 1) throw std::runtime_error("mf_backproject_b16: nsplit must be >= 1");
+    const int64_t rps = ((nrows32 + nsplit - 1) / nsplit + 31) / 32 * 32;
+    const int64_t vw0 = v0 / align, nvw = (v1 - v0) / align;  // wave tiles
+    const dim3 grid((unsigned)((nvw + 3) / 4), (unsigned)nsplit);
+    const int d = mf_b16_depth(false, nf);
+    if (nf == 16)
+        bwd_b16<1>(d, vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vw0, v1);
+    else if (nf == 32)
+        bwd_b16<2>(d, vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vw0, v1);
+    else
+        bwd_b16<4>(d, vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vw0, v1);
+    check_launch("k_mf_backproject_b16");
+}
+
+}  // namespace sart

@@ -263,6 +263,50 @@ __global__ void k_mf_state_begin(MfState* __restrict__ st, const double* __restr
     }
 }
 
+// bf16 operand planes of the bf16 MFMA projections (multiframe_bf16.hip): hi = rne(x), lo = rne(x - hi).
+__device__ __forceinline__ void split_bf16(float x, bf16_t& hi, bf16_t& lo) {
+    const __bf16 h = (__bf16)x;
+    const __bf16 l = (__bf16)(x - (float)h);
+    hi = __builtin_bit_cast(bf16_t, h);
+    lo = __builtin_bit_cast(bf16_t, l);
+}
+
+// X [nf][ld] fp32 -> planes of the same layout (n % 4 == 0).
+__global__ __launch_bounds__(256) void k_mf_split_x(const float* __restrict__ X, int64_t n4, bf16_t* __restrict__ hi,
+                                                    bf16_t* __restrict__ lo) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const float4 v = reinterpret_cast<const float4*>(X)[i];
+    bf16_t h[4], l[4];
+    split_bf16(v.x, h[0], l[0]);
+    split_bf16(v.y, h[1], l[1]);
+    split_bf16(v.z, h[2], l[2]);
+    split_bf16(v.w, h[3], l[3]);
+    reinterpret_cast<uint2*>(hi)[i] = make_uint2(h[0] | (unsigned)h[1] << 16, h[2] | (unsigned)h[3] << 16);
+    reinterpret_cast<uint2*>(lo)[i] = make_uint2(l[0] | (unsigned)l[1] << 16, l[2] | (unsigned)l[3] << 16);
+}
+
+// W [rows][16][nf / 16] (back-projection layout, mf_bp_slot) -> frame-major planes [nf][ldw]: 64 rows per block
+// through an LDS tile, so both the reads and the 128-byte plane writes are coalesced.
+__global__ __launch_bounds__(256) void k_mf_split_w(const float* __restrict__ W, int64_t nrows_pad, int nf,
+                                                    int64_t ldw, bf16_t* __restrict__ hi, bf16_t* __restrict__ lo) {
+    __shared__ float tile[64][kMaxNF + 1];
+    const int64_t r0 = (int64_t)blockIdx.x * 64;
+    for (int i = threadIdx.x; i < 64 * nf; i += 256) {
+        const int rr = i / nf, s = i % nf;
+        tile[rr][s] = (r0 + rr < nrows_pad) ? W[(r0 + rr) * nf + s] : 0.f;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * nf; i += 256) {
+        const int f = i / 64, rr = i % 64;
+        if (r0 + rr >= ldw) continue;
+        bf16_t h, l;
+        split_bf16(tile[rr][mf_bp_slot(f, nf)], h, l);
+        hi[(int64_t)f * ldw + r0 + rr] = h;
+        lo[(int64_t)f * ldw + r0 + rr] = l;
+    }
+}
+
 static inline unsigned nb(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 static void check_nf(int nf, const char* what) {
@@ -340,6 +384,21 @@ void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, 
     if (nused > nf) throw std::runtime_error("mf_state_begin: more frames than the batch holds");
     hipLaunchKernelGGL(k_mf_state_begin, dim3(1), dim3(kMaxNF), 0, stream, st, G, nused, tol, max_iter, nf);
     check_launch("k_mf_state_begin");
+}
+
+void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStream_t stream) {
+    if (n % 4 != 0) throw std::runtime_error("mf_split_x: length must be a multiple of 4");
+    hipLaunchKernelGGL(k_mf_split_x, dim3(std::max<unsigned>(1, nb(n / 4))), dim3(256), 0, stream, X, n / 4, hi, lo);
+    check_launch("k_mf_split_x");
+}
+
+void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, bf16_t* hi, bf16_t* lo,
+                       hipStream_t stream) {
+    check_nf(nf, "mf_split_w");
+    if (ldw > nrows_pad) throw std::runtime_error("mf_split_w: plane stride exceeds the padded rows");
+    hipLaunchKernelGGL(k_mf_split_w, dim3((unsigned)((ldw + 63) / 64)), dim3(256), 0, stream, W, nrows_pad, nf, ldw,
+                       hi, lo);
+    check_launch("k_mf_split_w");
 }
 
 }  // namespace sart

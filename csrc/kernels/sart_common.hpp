@@ -87,6 +87,16 @@ __device__ __forceinline__ float4 load_stream(const float4* p) {
 #endif
 }
 
+__device__ __forceinline__ uint2 load_stream(const uint2* p) {
+#if SART_STREAM_NT
+    typedef unsigned sart_u2v __attribute__((ext_vector_type(2)));
+    const sart_u2v v = __builtin_nontemporal_load(reinterpret_cast<const sart_u2v*>(p));
+    return make_uint2(v.x, v.y);
+#else
+    return *p;
+#endif
+}
+
 // RTM element access of the two-pass kernels, by storage type. fp32 (the reference's storage) or bf16 (opt-in
 // storage precision, SURVEY 7.3 8(d): half the HBM bytes per sweep and twice the matrix per GPU; products
 // and sums stay fp32). One 16-byte vector load per call: 4 fp32 or 8 bf16 columns, widened to NF4 float4.

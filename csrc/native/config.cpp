@@ -170,8 +170,8 @@ Config parse_arguments(const std::vector<std::string>& argv) {
     if (c.batch_frames < 1) throw Error("Argument batch_frames must be >= 1.");
     if (c.partition_voxels && (c.batch_frames > 1 || c.use_cpu))
         throw Error("Argument partition_voxels applies to the single-frame GPU solver only.");
-    if (c.rtm_bf16 && (c.batch_frames > 1 || c.use_cpu))
-        throw Error("Argument rtm_bf16 applies to the single-frame GPU solver only.");
+    if (c.rtm_bf16 && (c.use_cpu || c.partition_voxels))
+        throw Error("Argument rtm_bf16 applies to the GPU solvers with pixel-row shards only.");
     if (c.input_files.size() < 2)
         throw Error("At least two input file, one with RTM and one with image, are required, " +
                     std::to_string(c.input_files.size()) + " given.");

@@ -60,7 +60,7 @@ class MultiFrameSARTSolver:
         cfg.allow_zero_tolerance = bool(allow_zero_tolerance)
         cfg.check_interval = max(1, int(check_interval))
         cfg.mf_frames = self.batch
-        cfg.rtm_bf16 = bool(getattr(rtm, "is_bf16", False))  # rejected by the fp32 MFMA engine
+        cfg.rtm_bf16 = bool(getattr(rtm, "is_bf16", False))  # bf16 storage: bf16 MFMA projections
         device = self.dev.index if self.dev.index is not None else 0
         self.native_comm = native_communicator(self.comm, device)
         self.engine = self.k.MultiFrameEngine(device, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld,

@@ -51,8 +51,8 @@ def test_short_and_long_aliases(n):
     (["-m", "abc", "a", "b"], "Failed to parse"),
     (["--bogus", "a", "b"], "Unknown argument"),
     (["-m"], "Too few arguments"),
-    (["--rtm_bf16", "--use_cpu", "a", "b"], "rtm_bf16 applies to the single-frame GPU solver"),
-    (["--rtm_bf16", "--batch_frames", "16", "a", "b"], "rtm_bf16 applies to the single-frame GPU solver"),
+    (["--rtm_bf16", "--use_cpu", "a", "b"], "rtm_bf16 applies to the GPU solvers with pixel-row shards"),
+    (["--rtm_bf16", "--partition_voxels", "a", "b"], "rtm_bf16 applies to the GPU solvers with pixel-row shards"),
 ])
 def test_validation_errors(n, argv, msg):
     with pytest.raises(RuntimeError, match=msg.replace("(", r"\(").replace(")", r"\)").replace("]", r"\]")):

@@ -33,12 +33,19 @@ for step in "$@"; do
     presets) run bench_512kx256k 600 python bench.py --config 512kx256k --steps 3 --warmup 1 &&
              run bench_2tb 900 python bench.py --config 2tb --steps 2 --warmup 1 &&
              run bench_256k 900 python bench.py --config 256k --steps 2 --warmup 1 ;;
+    probemfb) run probe_mfb16 900 python tools/probe_mf_b16.py ;;
+    benchmfb) run bench_mfb16 600 python bench.py --steps 3 --warmup 1 --frames 16 --rtm-dtype bf16 &&
+              run bench_mfb32 600 python bench.py --steps 3 --warmup 1 --frames 32 --rtm-dtype bf16 &&
+              run bench_mfb64 600 python bench.py --steps 3 --warmup 1 --frames 64 --rtm-dtype bf16 ;;
     benchmf) run bench_mf16 600 python bench.py --steps 3 --warmup 1 --frames 16 &&
              run bench_mf32 600 python bench.py --steps 3 --warmup 1 --frames 32 &&
              run bench_mf64 600 python bench.py --steps 3 --warmup 1 --frames 64 ;;
     mfdepth) for d in 1 2 3; do for nf in 16 32 64; do
                SART_MF_DEPTH=$d run bench_mf${nf}_d$d 300 python bench.py --steps 2 --warmup 1 --frames $nf --iters 50 || exit 1
              done; done ;;
+    profmfb) for nf in 16 64; do
+              run rocprof_mfb$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 --rtm-dtype bf16 || exit 1
+            done ;;
     profmf) for nf in 16 32 64; do
               run rocprof_mf$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mf$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 || exit 1
             done ;;
