@@ -38,8 +38,13 @@ namespace {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // a first-class 16-byte value (no struct memcpy)
 
 __device__ __forceinline__ floatx4 mfma_b16(const uint4 a, const uint4 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+}
+__device__ __forceinline__ floatx4 mfma_b16(const uint4 a, const u32x4 b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
                                                    c, 0, 0, 0);
 }
@@ -136,6 +141,109 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
             }
 }
 
+// The forward with X shared through LDS: the four waves of a workgroup own different rows of the same column
+// range, so they need the same X fragments. Per step the X tile ([KB][hi, lo][NG][16 frames][32 voxels], 1 KiB
+// per (kb, plane, group)) is loaded once per workgroup, each wave loading a quarter into registers and writing
+// it to one of two LDS stages; every wave then reads its fragments from LDS (contiguous 1 KiB per fragment
+// instruction: conflict-free). X bytes through the vector memory path per byte of A drop 4x (2 N / R with
+// R = 64 RT rows per wave -> per workgroup), which is what bounds the register-operand forward at 32 / 64
+// frames (profiles/probe_r2_mf_b16.jsonl). One barrier per step; waves past the padded rows clamp to the last
+// row tile (they take part in the X staging and barriers, and store nothing).
+template <int NG, int DEPTH, int RT, int KB>
+__global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const bf16_t* __restrict__ A, int64_t ld, int64_t nrows,
+                                                            int64_t nrows_pad, const bf16_t* __restrict__ Xh,
+                                                            const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
+                                                            int64_t cols_per_split) {
+    constexpr int NF = 16 * NG;
+    constexpr int RS = DEPTH + 1;
+    constexpr int C = KB * 2 * NG;             // 1 KiB X pieces per step
+    constexpr int XQ = C >= 4 ? C / 4 : 1;     // pieces per wave (C = 2: two waves load each piece)
+    __shared__ __attribute__((aligned(16))) u32x4 s_x[2][C][64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * (16 * RT);
+    const bool live = row0 < nrows_pad;
+    if (!live) row0 = nrows_pad - 16 * RT;  // nrows_pad is a multiple of 16 * RT
+    const int g = lane >> 4, r = lane & 15;
+    const int64_t c0 = (int64_t)blockIdx.y * cols_per_split;
+    const int64_t c1 = (c0 + cols_per_split < ld) ? c0 + cols_per_split : ld;
+    Fout += (int64_t)blockIdx.y * nrows_pad * NF;
+    const bf16_t* __restrict__ ap = A + (row0 + r) * ld + c0 + 8 * g;
+    const int64_t xo = (int64_t)r * ld + c0 + 8 * g;
+    const int lofs = r * 4 + g;  // uint4 slot of (frame r, voxels 8 g..) inside a 1 KiB piece
+
+    floatx4 acc[RT][NG];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int j = 0; j < NG; ++j) acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int64_t nst = c1 > c0 ? (c1 - c0) / (32 * KB) : 0;  // uniform for the workgroup
+    if (nst > 0) {
+        uint4 a[RS][RT][KB];
+        u32x4 xq[RS][XQ];
+        auto piece = [&](int i) { return (C >= 4 ? wave * XQ + i : wave % C); };  // piece = (kb * 2 + plane) * NG + j
+        auto load = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            const int64_t q = t * 32 * KB;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int kb = 0; kb < KB; ++kb)
+                    a[sl][rt][kb] = *reinterpret_cast<const uint4*>(ap + rt * 16 * ld + q + 32 * kb);
+#pragma unroll
+            for (int i = 0; i < XQ; ++i) {
+                const int pc = piece(i), j = pc % NG, plane = (pc / NG) & 1, kb = pc / (2 * NG);
+                xq[sl][i] = *reinterpret_cast<const u32x4*>((plane ? Xl : Xh) + xo + (int64_t)j * 16 * ld + q + 32 * kb);
+            }
+        };
+        auto stage = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+#pragma unroll
+            for (int i = 0; i < XQ; ++i) s_x[t & 1][piece(i)][lofs] = xq[sl][i];
+        };
+        [&]<int... Q>(std::integer_sequence<int, Q...>) {
+            (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
+        }(std::make_integer_sequence<int, DEPTH>{});
+        stage(std::integral_constant<int, 0>{}, 0);
+        __syncthreads();
+        auto step = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
+            if (t >= nst) return;  // uniform for the workgroup
+            stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);  // X of step t + 1 into the other stage (its readers passed the last barrier)
+            const u32x4* xs = s_x[t & 1][0] + lofs;
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    const u32x4 xh = xs[((kb * 2 + 0) * NG + j) * 64];
+                    const u32x4 xl = xs[((kb * 2 + 1) * NG + j) * 64];
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt) {
+                        acc[rt][j] = mfma_b16(a[sl][rt][kb], xh, acc[rt][j]);
+                        acc[rt][j] = mfma_b16(a[sl][rt][kb], xl, acc[rt][j]);
+                    }
+                }
+            __syncthreads();
+        };
+        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+            }(std::make_integer_sequence<int, RS>{});
+        }
+    }
+    if (!live) return;
+#pragma unroll
+    for (int j = 0; j < NG; ++j)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t ra = row0 + rt * 16 + g * 4 + i;
+                if (ra < nrows) Fout[ra * NF + 16 * j + r] = acc[rt][j][i];
+            }
+}
+
 // partial[s][v][f] = sum_{rows of split s} A[row][v] W[row][f] for the 64-voxel blocks from vb0 up to voxel
 // vend; W planes [nf][ldw] (frame-major). Rows are processed up to nrows32 (rows rounded up to 32: the padding
 // rows of A and W are zero). One wave: VT blocks of 64 voxels x nf frames (each W fragment feeds 4 VT MFMAs).
@@ -221,6 +329,112 @@ __global__ __launch_bounds__(256) void k_mf_backproject_b16(const bf16_t* __rest
             }
 }
 
+// The back-projection with W shared through LDS: the four waves of a workgroup own different voxels of the
+// same rows, so they need the same W fragments ([hi, lo][NG][16 frames][32 rows] per step, 1 KiB pieces), loaded
+// once per workgroup and staged through two LDS stages like k_mf_forward_b16_lds. Waves past the voxel range
+// clamp to the last wave tile of the range (they stage W, take the barriers and store nothing).
+template <int NG, int DEPTH, int VT>
+__global__ __launch_bounds__(256) void k_mf_backproject_b16_lds(const bf16_t* __restrict__ A, int64_t ld,
+                                                                int64_t nrows32, const bf16_t* __restrict__ Wh,
+                                                                const bf16_t* __restrict__ Wl, int64_t ldw,
+                                                                int64_t rows_per_split, float* __restrict__ partial,
+                                                                int64_t vb0, int64_t vend) {
+    constexpr int NF = 16 * NG;
+    constexpr int RS = DEPTH + 1;
+    constexpr int C = 2 * NG;
+    constexpr int XQ = C >= 4 ? C / 4 : 1;
+    __shared__ __attribute__((aligned(16))) u32x4 s_w[2][C][64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int64_t vb = (vb0 + (int64_t)blockIdx.x * 4 + wave) * VT;
+    const bool live = vb * 64 < vend;
+    if (!live) vb = vend / 64 - VT;  // vend is a multiple of 64 * VT
+    const int g = lane >> 4, i16 = lane & 15;
+    const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
+    int64_t r_end = r_begin + rows_per_split;
+    if (r_end > nrows32) r_end = nrows32;
+    const bf16_t* __restrict__ ap = A + (r_begin + 8 * g) * ld + vb * 64 + 4 * i16;
+    const int64_t wo = (int64_t)i16 * ldw + r_begin + 8 * g;
+    const int lofs = i16 * 4 + g;
+
+    floatx4 acc[VT][4][NG];
+#pragma unroll
+    for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int j = 0; j < NG; ++j) acc[vt][p][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 32 : 0;  // uniform for the workgroup
+    if (nst > 0) {
+        uint2 av[RS][VT][8];
+        u32x4 wq[RS][XQ];
+        auto piece = [&](int i) { return (C >= 4 ? wave * XQ + i : wave % C); };  // piece = plane * NG + j
+        auto load = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            const bf16_t* at = ap + t * 32 * ld;
+#pragma unroll
+            for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    av[sl][vt][j] = load_stream(reinterpret_cast<const uint2*>(at + j * ld + vt * 64));
+#pragma unroll
+            for (int i = 0; i < XQ; ++i) {
+                const int pc = piece(i), j = pc % NG, plane = pc / NG;
+                wq[sl][i] = *reinterpret_cast<const u32x4*>((plane ? Wl : Wh) + wo + (int64_t)j * 16 * ldw + t * 32);
+            }
+        };
+        auto stage = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+#pragma unroll
+            for (int i = 0; i < XQ; ++i) s_w[t & 1][piece(i)][lofs] = wq[sl][i];
+        };
+        [&]<int... Q>(std::integer_sequence<int, Q...>) {
+            (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
+        }(std::make_integer_sequence<int, DEPTH>{});
+        stage(std::integral_constant<int, 0>{}, 0);
+        __syncthreads();
+        auto step = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
+            if (t >= nst) return;  // uniform for the workgroup
+            stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);
+            const u32x4* ws = s_w[t & 1][0] + lofs;
+#pragma unroll
+            for (int vt = 0; vt < VT; ++vt) {
+                const uint4 fr[4] = {phase_frag<0>(av[sl][vt]), phase_frag<1>(av[sl][vt]), phase_frag<2>(av[sl][vt]),
+                                     phase_frag<3>(av[sl][vt])};
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    const u32x4 wh = ws[j * 64], wl = ws[(NG + j) * 64];
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) {
+                        acc[vt][p][j] = mfma_b16(fr[p], wh, acc[vt][p][j]);
+                        acc[vt][p][j] = mfma_b16(fr[p], wl, acc[vt][p][j]);
+                    }
+                }
+            }
+            __syncthreads();
+        };
+        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+            }(std::make_integer_sequence<int, RS>{});
+        }
+    }
+    if (!live) return;
+    float* out = partial + (int64_t)blockIdx.y * ld * NF;
+#pragma unroll
+    for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t v = (vb + vt) * 64 + 4 * (g * 4 + q) + p;
+#pragma unroll
+                for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[vt][p][j][q];
+            }
+}
+
 // ---------------------------------------------------------------------------------------------- launchers
 
 static void check_nf_b16(int nf, const char* what) {
@@ -238,19 +452,24 @@ static int env_int(const char* name, int dflt) {
 static int mf_b16_depth(bool forward, int nf) {
     const int d = env_int("SART_MF_DEPTH", 0);
     if (d >= 1 && d <= 3) return d;
-    return forward && nf < 64 ? 3 : 2;
+    (void)forward;
+    (void)nf;
+    return 3;  // profiles/probe_r2_mf_b16_bwd.jsonl
 }
 
 struct FwdTile {
     int rt, kb;
+    bool lds = false;  // X shared through LDS (k_mf_forward_b16_lds)
 };
 static FwdTile mf_b16_fwd_tile(int nf) {
     const char* e = std::getenv("SART_MF_B16_FWD");
     if (e && *e) {
-        const FwdTile t{std::atoi(e), std::strchr(e, ',') ? std::atoi(std::strchr(e, ',') + 1) : 1};
+        // "RT,KB" or "RT,KB,lds"
+        FwdTile t{std::atoi(e), std::strchr(e, ',') ? std::atoi(std::strchr(e, ',') + 1) : 1};
+        t.lds = std::strstr(e, "lds") != nullptr;
         if ((t.rt == 2 || t.rt == 4 || t.rt == 8) && (t.kb == 1 || t.kb == 2)) return t;
     }
-    return nf == 64 ? FwdTile{8, 1} : FwdTile{4, 2};  // profiles/probe_r2_mf_b16.jsonl
+    return nf == 16 ? FwdTile{2, 2, true} : FwdTile{4, 2, true};  // profiles/probe_r2_mf_b16_lds.jsonl
 }
 
 static int mf_b16_vt(int64_t ld, int nf) {
@@ -260,24 +479,37 @@ static int mf_b16_vt(int64_t ld, int nf) {
     return (vt == 2 && ld % 128 == 0) ? 2 : 1;
 }
 
+// W shared through LDS in the back-projection (k_mf_backproject_b16_lds): SART_MF_B16_VT = "VT,lds" / "VT,reg"
+static bool mf_b16_bwd_lds(int nf) {
+    const char* e = std::getenv("SART_MF_B16_VT");
+    if (e && std::strstr(e, "lds")) return true;
+    if (e && std::strstr(e, "reg")) return false;
+    (void)nf;
+    return true;
+}
+
 template <int NG, int DEPTH, int RT, int KB>
-static void fwd_b16_t(dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
-                      const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
-    hipLaunchKernelGGL((k_mf_forward_b16<NG, DEPTH, RT, KB>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, Xh,
-                       Xl, Fout, cps);
+static void fwd_b16_t(bool lds, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows,
+                      int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
+    if (lds)
+        hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB>), grid, dim3(256), 0, stream, A, ld, nrows,
+                           nrows_pad, Xh, Xl, Fout, cps);
+    else
+        hipLaunchKernelGGL((k_mf_forward_b16<NG, DEPTH, RT, KB>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad,
+                           Xh, Xl, Fout, cps);
 }
 
 template <int NG, int DEPTH>
 static void fwd_b16_d(FwdTile tl, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows,
                       int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
     if (tl.rt == 2 && tl.kb == 2)
-        fwd_b16_t<NG, DEPTH, 2, 2>(grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+        fwd_b16_t<NG, DEPTH, 2, 2>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else if (tl.rt == 4 && tl.kb == 2)
-        fwd_b16_t<NG, DEPTH, 4, 2>(grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+        fwd_b16_t<NG, DEPTH, 4, 2>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else if (tl.rt == 8)
-        fwd_b16_t<NG, DEPTH, 8, 1>(grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+        fwd_b16_t<NG, DEPTH, 8, 1>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else
-        fwd_b16_t<NG, DEPTH, 4, 1>(grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+        fwd_b16_t<NG, DEPTH, 4, 1>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
 }
 
 template <int NG>
@@ -297,7 +529,7 @@ void launch_mf_forward_b16(const bf16_t* A, int64_t ld, int64_t nrows, int64_t n
     if (nsplit < 1) throw std::runtime_error("mf_forward_b16: nsplit must be >= 1");
     check_nf_b16(nf, "mf_forward_b16");
     FwdTile tl = mf_b16_fwd_tile(nf);
-    if (nrows_pad % (16 * tl.rt) != 0) tl = FwdTile{2, 1};  // a wave's rows must lie inside the padding
+    if (nrows_pad % (16 * tl.rt) != 0) tl = FwdTile{2, 1, tl.lds};  // a wave's rows must lie inside the padding
     if (nrows_pad % 32 != 0) throw std::runtime_error("mf_forward_b16: padded rows must be a multiple of 32");
     const int64_t cps = ((ld + nsplit - 1) / nsplit + 63) / 64 * 64;
     const int64_t rows_per_block = 64 * tl.rt;
@@ -329,6 +561,15 @@ template <int NG, int DEPTH>
 static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows32,
                       const bf16_t* Wh, const bf16_t* Wl, int64_t ldw, int64_t rps, float* partial, int64_t vb0,
                       int64_t vend) {
+    if (mf_b16_bwd_lds(16 * NG)) {
+        if (vt == 2)
+            hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2>), grid, dim3(256), 0, stream, A, ld, nrows32,
+                               Wh, Wl, ldw, rps, partial, vb0, vend);
+        else
+            hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1>), grid, dim3(256), 0, stream, A, ld, nrows32,
+                               Wh, Wl, ldw, rps, partial, vb0, vend);
+        return;
+    }
     if (vt == 2)
         hipLaunchKernelGGL((k_mf_backproject_b16<NG, DEPTH, 2>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
                            ldw, rps, partial, vb0, vend);

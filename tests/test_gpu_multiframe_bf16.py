@@ -60,9 +60,16 @@ def test_split_planes(k, dev):
                                    rtol=2.0 ** -16)
 
 
+# (SART_MF_B16_FWD, SART_MF_B16_VT) tiles: register-operand and LDS-shared variants of both kernels
+@pytest.mark.parametrize("fwd,bwd", [("", ""), ("4,1", "1,reg"), ("8,1", "2,reg"), ("4,2,lds", "1,lds"),
+                                     ("8,1,lds", "2,lds"), ("2,2,lds", "2,lds")])
 @pytest.mark.parametrize("nf", [16, 32, 64])
 @pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (64, 1024), (2048, 4096), (1000, 1088)])
-def test_bf16_mfma_projections(k, dev, P, V, nf):
+def test_bf16_mfma_projections(k, dev, P, V, nf, fwd, bwd, monkeypatch):
+    if fwd:
+        monkeypatch.setenv("SART_MF_B16_FWD", fwd)
+    if bwd:
+        monkeypatch.setenv("SART_MF_B16_VT", bwd)
     m, Ab = _bf16_rtm(dev, P, V, seed=P + V)
     rng = np.random.default_rng(nf)
     X = rng.random((nf, V)).astype(np.float32)

@@ -34,6 +34,9 @@ for step in "$@"; do
              run bench_2tb 900 python bench.py --config 2tb --steps 2 --warmup 1 &&
              run bench_256k 900 python bench.py --config 256k --steps 2 --warmup 1 ;;
     probemfb) run probe_mfb16 900 python tools/probe_mf_b16.py ;;
+    probemfbv) PROBE_DEPTH=2,3 PROBE_FWD="2,2,lds;4,2,lds" run probe_mfb_bwd 900 python tools/probe_mf_b16.py ;;
+    probemfbl) PROBE_BWD=0 PROBE_DEPTH=2,3 PROBE_FWD="4,2;8,1;4,1,lds;4,2,lds;8,1,lds;2,2,lds" \
+                 run probe_mfb_lds 900 python tools/probe_mf_b16.py ;;
     benchmfb) run bench_mfb16 600 python bench.py --steps 3 --warmup 1 --frames 16 --rtm-dtype bf16 &&
               run bench_mfb32 600 python bench.py --steps 3 --warmup 1 --frames 32 --rtm-dtype bf16 &&
               run bench_mfb64 600 python bench.py --steps 3 --warmup 1 --frames 64 --rtm-dtype bf16 ;;

@@ -23,7 +23,7 @@ def main():
     m = DenseRTM.synthetic(P, V, 0, seed=1, device=dev, storage="bf16")
     nbytes = m.nbytes
     nfs = [int(v) for v in os.environ.get("PROBE_NF", "16,32,64").split(",")]
-    fwd_tiles = os.environ.get("PROBE_FWD", "4,1;2,2;4,2;8,1").split(";")
+    fwd_tiles = os.environ.get("PROBE_FWD", "4,1;2,2;4,2;8,1;4,1,lds;4,2,lds;8,1,lds;2,2,lds").split(";")
     for nf in nfs:
         Xh = torch.rand((nf, m.ld), device=dev).bfloat16()
         Xl = (torch.rand((nf, m.ld), device=dev) * 1e-3).bfloat16()
@@ -31,7 +31,7 @@ def main():
         Wh = torch.rand((nf, m.nrows_pad), device=dev).bfloat16()
         Wl = (torch.rand((nf, m.nrows_pad), device=dev) * 1e-3).bfloat16()
         part = torch.zeros((64, m.ld, nf), device=dev)
-        for depth in (1, 2, 3):
+        for depth in [int(v) for v in os.environ.get("PROBE_DEPTH", "1,2,3").split(",")]:
             os.environ["SART_MF_DEPTH"] = str(depth)
             for tile in fwd_tiles:
                 os.environ["SART_MF_B16_FWD"] = tile
@@ -41,7 +41,8 @@ def main():
                 print(json.dumps(dict(op="mf_forward_b16", nf=nf, depth=depth, tile=tile, nsplit=nsf, P=P, V=V,
                                       ms=round(med, 4), GBps=round(nbytes / med / 1e6, 1),
                                       TFLOPs=round(4 * nf * P * V / med / 1e9, 1))), flush=True)
-            for vt in (1, 2):
+            for vt in (os.environ.get("PROBE_VT", "1,reg;2,reg;1,lds;2,lds").split(";")
+                       if os.environ.get("PROBE_BWD", "1") == "1" else ()):
                 os.environ["SART_MF_B16_VT"] = str(vt)
                 ns = k.mf_backproject_b16_num_splits(m.ld, P)
                 assert ns <= 64
