@@ -130,6 +130,11 @@ static void bind_engine(py::module_& m) {
           py::arg("rows_per_tile") = 0);
     m.def("fused_geometry_bf16_wide", &sart::fused_geometry_bf16_wide, py::arg("ld"), py::arg("num_cus"));
     m.def("fused_fold_tiles", &sart::fused_fold_tiles, py::arg("geometry"), py::arg("nrows_pad"));
+    m.def("fused_chain_plan", [](const sart::FusedGeometry& g, int64_t nrows_pad, bool split) {
+        const auto p = sart::fused_chain_plan(g, nrows_pad, split);
+        return py::make_tuple(p.chain_tiles, p.blocks);
+    }, py::arg("geometry"), py::arg("nrows_pad"), py::arg("split_schedule"));
+    m.def("fused_split_schedule", &sart::fused_split_schedule, py::arg("T"), py::arg("bf16"));
     m.def("choose_ld", &sart::choose_ld, py::arg("nvoxel"), py::arg("max_waste") = 0.10);
 
     py::class_<sart::EngineConfig>(m, "EngineConfig")

@@ -179,8 +179,11 @@ void Engine::drop_graph() {
 
 void Engine::alloc_fused() {
     nF_fused_ = use_fused_ ? (int64_t)geom_.grid * fused_fpart_per_block(geom_.variant) : 0;
-    fold_tiles_ = use_fused_ ? fused_fold_tiles(geom_, Pp_) : 0;
-    const int64_t n_part = std::max<int64_t>(nsplit_, use_fused_ ? geom_.I : 1);
+    const ChainPlan plan = use_fused_ ? fused_chain_plan(geom_, Pp_, fused_split_schedule(geom_.K, cfg_.rtm_bf16))
+                                      : ChainPlan{};
+    fold_tiles_ = plan.chain_tiles;
+    fused_blocks_ = use_fused_ ? plan.blocks : 0;
+    const int64_t n_part = std::max<int64_t>(nsplit_, use_fused_ ? fused_blocks_ : 1);
     if ((int64_t)partial_.size() < n_part * ld_) partial_.resize(n_part * ld_);
     const int64_t nF = std::max<int64_t>({forward_num_blocks(Pp_), (int64_t)weights_num_blocks(Pp_), nF_fused_, 1});
     if ((int64_t)Fpart_.size() < nF) Fpart_.resize(nF);
@@ -355,7 +358,7 @@ void Engine::sweep() {
             launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, static_cast<const float*>(A_), ld_, P_, Pp_,
                                x_.get(), ghat_.get(), arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I,
                                geom_.J, st, xcnt_.get(), stream_, fold_tiles_);
-        launch_reduce_partials(partial_.get(), ld_, geom_.I, scale, comm_buf_.get(), Fpart_.get(), nF_fused_, Fslot,
+        launch_reduce_partials(partial_.get(), ld_, (int)fused_blocks_, scale, comm_buf_.get(), Fpart_.get(), nF_fused_, Fslot,
                                st, stream_);
     } else {
         fwd(cfg_.logarithmic ? kEpiLog : kEpiLinear, x_.get(), nullptr, w_.get(), Fpart_.get(), st);

@@ -167,7 +167,8 @@ class Engine {
     FusedGeometry geom_;
     int nsplit_ = 0;
     int64_t nF_fused_ = 0;
-    int64_t fold_tiles_ = 0;  // T = 1 fused sweep: back-projection fold period (tiles), 0 = off
+    int64_t fold_tiles_ = 0;     // fused sweep chain_tiles (T = 1 fold period / T >= 2 segment length), 0 = off
+    int64_t fused_blocks_ = 0;   // partial-sum rows written by the fused sweep (I, or I * T * segments)
     double norm_ = 1.0;
 
     DeviceArray<float> partial_, comm_buf_, x_, pen_, O_, ghat_, arow_, gpos_, wo_, w_, fitted_;

@@ -99,11 +99,22 @@ FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_
 
 FusedGeometry fused_geometry_bf16_wide(int64_t ld, int num_cus) {
     FusedGeometry g;
-    if (num_cus % 8 != 0 || ld % 4096 != 0) return g;
+    if (num_cus % 8 != 0) return g;
     const int per_xcd = num_cus / 8;
-    const int64_t J = ld / 4096;
-    if (J < 1 || J > per_xcd) return g;
-    g.K = 4, g.T = 4, g.cpl = 8, g.J = (int)J, g.I = 8 * (per_xcd / (int)J), g.grid = g.I * g.J, g.variant = 6;
+    // T = 4 (slab 4096, schedule 4) or T = 2 (slab 8192, schedule 6: 3-slot ring, lag 3); the lower cost
+    // slab / G wins, T = 4 on ties (the deeper lag measured faster at 64k x 64k)
+    int64_t best_cost = 0;
+    for (const int T : {4, 2}) {
+        const int64_t slab = 16384 / T;
+        if (ld % slab != 0) continue;
+        const int64_t J = ld / slab;
+        if (J < 1 || J > per_xcd) continue;
+        const int G = per_xcd / (int)J;
+        const int64_t cost = slab / G;
+        if (g.valid() && cost >= best_cost) continue;
+        best_cost = cost;
+        g.K = T, g.T = T, g.cpl = 8, g.J = (int)J, g.I = 8 * G, g.grid = g.I * g.J, g.variant = 6;
+    }
     return g;
 }
 
@@ -112,6 +123,26 @@ int64_t fused_fold_tiles(const FusedGeometry& g, int64_t nrows_pad) {
     if (const char* e = std::getenv("SART_FUSED_FOLD")) return std::max<int64_t>(0, std::atoll(e));
     const int64_t per_group = (nrows_pad + g.I - 1) / g.I;  // tiles (= rows at T = 1) of the longest group
     return std::max<int64_t>(16, (int64_t)std::ceil(std::sqrt((double)per_group)));
+}
+
+ChainPlan fused_chain_plan(const FusedGeometry& g, int64_t nrows_pad, bool split_schedule) {
+    ChainPlan p;
+    p.blocks = g.I;
+    if (g.variant != 6 || g.I <= 0) return p;
+    if (g.K == 1) {
+        p.chain_tiles = fused_fold_tiles(g, nrows_pad);
+        return p;
+    }
+    if (!split_schedule) return p;
+    int64_t seg = 2240;  // > the 2048 tiles per group of the 64k x 64k headline: one chain there
+    if (const char* e = std::getenv("SART_FUSED_SEG")) seg = std::max<int64_t>(0, std::atoll(e));
+    if (seg <= 0) return p;
+    seg = (seg + 139) / 140 * 140;
+    const int64_t per_group = (nrows_pad / g.K + g.I - 1) / g.I;  // tiles of the longest row group
+    if (per_group <= seg) return p;
+    p.chain_tiles = seg;
+    p.blocks = (int64_t)g.I * g.K * ((per_group + seg - 1) / seg);
+    return p;
 }
 
 }  // namespace sart

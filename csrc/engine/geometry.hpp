@@ -25,11 +25,19 @@ int64_t choose_ld(int64_t nvoxel, double max_waste = 0.10);
 // Geometry for `variant` (6 default, or 3), falling back to variant 3 when variant 6 cannot split the
 // width. rows_per_tile = 0: SART_FUSED_T or the lowest-cost T.
 FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_tile);
-// Variant 6 geometry of the wide bf16 tiles (16-byte loads of 8 bf16 per lane, T = 4, slab 4096 columns); invalid
-// when the width does not split into J <= 32 such slabs.
+// Variant 6 geometry of the wide bf16 tiles (16-byte loads of 8 bf16 per lane: T = 4 with slab 4096 columns, or
+// T = 2 with slab 8192); invalid when the width does not split into J <= 32 such slabs.
 FusedGeometry fused_geometry_bf16_wide(int64_t ld, int num_cus);
 // Fold period of the T = 1 sweep's two-level back-projection sums (variant 6): ~sqrt(tiles per row group), so
 // no fp32 chain exceeds ~2 sqrt(P / I) terms (SART_FUSED_FOLD overrides; 0 = one chain per group). 0 for T >= 2.
 int64_t fused_fold_tiles(const FusedGeometry& g, int64_t nrows_pad);
+// Back-projection chain plan of the fused sweep (launch_fused_sweep's chain_tiles): T = 1 folds (above);
+// T >= 2 with a split schedule runs segments of 2240 tiles (SART_FUSED_SEG, rounded up to a multiple of 140)
+// when a row group has more tiles than that. blocks = partial-sum rows (of ld floats) the sweep writes.
+struct ChainPlan {
+    int64_t chain_tiles = 0;
+    int64_t blocks = 0;
+};
+ChainPlan fused_chain_plan(const FusedGeometry& g, int64_t nrows_pad, bool split_schedule);
 
 }  // namespace sart

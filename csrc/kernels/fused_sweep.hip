@@ -28,6 +28,7 @@
 // tagged with this sweep's epoch, every spin is bounded, and a timeout sets SartState::error so
 // the host falls back to the two-pass kernels (no hang, no silent wrong answer).
 #include "sart_common.hpp"
+#include "launchers.hpp"
 
 #include <stdexcept>
 #include <type_traits>
@@ -346,21 +347,26 @@ struct FusedTile<bf16_t, 8> {
     }
 };
 
+// Schedules with a separate publisher wave (the split exchange)
+constexpr bool sched_split(int sched) { return sched == 4 || sched == 5 || sched == 6; }
+
 template <bool LOG, bool XL, bool DIAG, int T, int SCHED, typename AT = float, int CPL = 4>
-__global__ __launch_bounds__((SCHED == 4 || SCHED == 5) ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
+__global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
     const AT* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
     const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
     double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg,
-    unsigned* __restrict__ xcnt, int64_t fold_tiles) {
+    unsigned* __restrict__ xcnt, int64_t chain_tiles) {
     static_assert(T == 1 || T == 2 || T == 4, "rows per tile");
     constexpr int KW = 8;        // float4 per lane per row: one wave covers 2048 columns
     constexpr int WPR = 4 / T;   // compute waves per row (each on its own 2048-column sub-slab)
-    constexpr int D = (SCHED == 1 || SCHED == 2 || SCHED == 4) ? 1 : 0;  // steps a reduced tile stays in VGPRs
-    constexpr bool XS_LDS = SCHED >= 1 && SCHED <= 4;         // x slab in LDS instead of VGPRs
+    constexpr int D = (SCHED == 1 || SCHED == 2 || SCHED == 4 || SCHED == 6) ? 1 : 0;  // steps a reduced tile stays in VGPRs
+    constexpr bool XS_LDS = (SCHED >= 1 && SCHED <= 4) || SCHED == 6;  // x slab in LDS instead of VGPRs
     static_assert(!XS_LDS || T >= 2, "the LDS holds the x slab only for T >= 2");
     // wave 4 publishes granules, wave 5 gathers (no shared vmcnt queue); schedule 5 = the split exchange with
     // the x slab in VGPRs and schedule 0's lag (T = 1, whose x slab does not fit the LDS next to the ring)
-    constexpr bool SPLIT = SCHED == 4 || SCHED == 5;
+    // schedule 6 = the split exchange for wide bf16 tiles at T = 2 (x slab in LDS, 3-slot ring, L = 3: a 4-slot
+    // ring and the 32 KB x slab of two sub-slabs would exceed the 160 KB of LDS by the hand-off words)
+    constexpr bool SPLIT = sched_split(SCHED);
     constexpr int NTHR = SPLIT ? kFusedThreads + 64 : kFusedThreads;
     constexpr bool BF = !std::is_same<AT, float>::value;
     constexpr int H = CPL / 4;  // float4 per lane per k-slot (2: wide bf16 tiles)
@@ -372,9 +378,9 @@ __global__ __launch_bounds__((SCHED == 4 || SCHED == 5) ? kFusedThreads + 64 : k
     constexpr bool DEEP = BF && SCHED == 0;
     constexpr int PD = (SCHED == 2 || SCHED == 4) ? 2 : 1;   // exchange step u polls tile u - PD
     constexpr int PQ = DEEP ? 4 : (SCHED == 1 ? 3 : 2);      // polls in flight (finishes tile u - PD - PQ + 1)
-    constexpr int L = DEEP ? PD + PQ : 3 + D;                // back-projection lag in steps
+    constexpr int L = DEEP ? PD + PQ : (SCHED == 6 ? 3 : 3 + D);  // back-projection lag in steps
     static_assert(L >= PD + PQ, "the weights must be ready one step before they are used");
-    constexpr int NL = (BF && CPL == 4) ? 8 : 4;  // LDS ring slots (32 KB fp32 or wide bf16 / 16 KB narrow bf16)
+    constexpr int NL = (BF && CPL == 4) ? 8 : (SCHED == 6 ? 3 : 4);  // LDS ring slots (32 KB fp32 or wide bf16 / 16 KB narrow bf16)
     static_assert(L <= NL + D - 1, "a parked tile must be back-projected before its ring slot is reused");
     // register tile slots per wave (8 KB fp32 / 4 KB bf16 each): AH in flight + D held. bf16: 6-7 tiles of
     // 8-byte loads in flight (<= 56 loads, inside the 6-bit vmcnt range); 8 slots with the x slab in LDS
@@ -389,11 +395,20 @@ __global__ __launch_bounds__((SCHED == 4 || SCHED == 5) ? kFusedThreads + 64 : k
     // Two-level back-projection sums (T = 1): with T = 1 every wave owns its own columns, so a lane's
     // accumulators would sum ALL P / I rows of its group in one fp32 chain (T >= 2 split a group's rows over T
     // waves). Measured at 65536 x 262144 bf16: 2.4x the two-pass kernels' error after one iteration, 26x at
-    // 524288 rows. Every ~fold_tiles tiles (host: ~sqrt of the group's tiles) the chain is folded into a second
+    // 524288 rows. Every ~chain_tiles tiles (host: ~sqrt of the group's tiles) the chain is folded into a second
     // register set acc2 and restarts, so no chain is longer than ~2 sqrt(P / I) terms. (Splitting the group
     // into separately drained segments deadlocks: the exchange wave finishes tile u only after the compute
     // waves published u + PD + PQ - 1.)
     constexpr bool FOLD = (T == 1);
+    // Segmented back-projection sums (split schedules, T >= 2): a wave's chain sums one row per tile, P / (T I)
+    // rows per group (32768 at 512k x 256k with wide bf16 tiles at T = 2, whose registers have no room for a
+    // fold set). With chain_tiles > 0 the group's tiles run in segments of chain_tiles (a multiple of RS): at
+    // a segment's end the pipeline drains, every wave stores its sums to its own partial block
+    // ((seg * T + row) * I + gi) and the chain restarts. Only split schedules: their gatherer does not need the
+    // compute waves' next tiles to finish the current ones (it skips its pacing wait on a segment's first
+    // PD + PQ - 1 tiles), so the drain cannot deadlock. chain_tiles = 0: one chain, LDS combine of the T rows.
+    constexpr bool SEG = SPLIT && T >= 2;
+    const bool seg_on = SEG && chain_tiles > 0;
 
     extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64] of RT (128 KB)
     float4* s_xs = s_ring + NL * 4 * KW * 64 * sizeof(RT) / sizeof(float4);  // [WPR][KW][H][64] if XS_LDS
@@ -477,6 +492,7 @@ __global__ __launch_bounds__((SCHED == 4 || SCHED == 5) ? kFusedThreads + 64 : k
         // on the path, and the compiler then waits for EVERY load in flight wherever a tile is consumed,
         // which collapses the AH-tile pipeline to one tile.
         const int64_t tlast = ntiles - 1 - t_begin;
+        int64_t lo = 0, hi = nt;  // tiles of the current segment (SEG) or of the whole group
         auto load_tile = [&](RT(&dst)[KW], int64_t t) {
             const int64_t tc = t < tlast ? t : tlast;
             const RT* src = a4 + (t_begin + tc) * T * ld4;
@@ -496,7 +512,7 @@ __global__ __launch_bounds__((SCHED == 4 || SCHED == 5) ? kFusedThreads + 64 : k
         auto step = [&](auto bbc, int64_t t) {
             constexpr int bb = decltype(bbc)::value;        // register slot of tile t (t % RS)
             constexpr int bp = (bb + RS - D) % RS;          // register slot of tile t - D
-            if (t < nt) {
+            if (t < hi) {
                 float s = 0.f;
 #pragma unroll
                 for (int k = 0; k < KW; ++k) {
@@ -519,9 +535,9 @@ __global__ __launch_bounds__((SCHED == 4 || SCHED == 5) ? kFusedThreads + 64 : k
                 }
             }
             // park tile t - D (its LDS slot held tile t - D - NL, back-projected in step t - 1)
-            if (t - D >= 0 && t - D < nt) park(fl[bp], t - D);
+            if (t - D >= lo && t - D < hi) park(fl[bp], t - D);
             load_tile(fl[bp], t + AH);  // slot bp is free again
-            if (t >= L && t - L < nt) {
+            if (t - L >= lo && t - L < hi) {
                 const int64_t u = t - L;
                 const int ws = (int)(u & (NS - 1));
                 unsigned spins = 0;
@@ -551,23 +567,47 @@ __global__ __launch_bounds__((SCHED == 4 || SCHED == 5) ? kFusedThreads + 64 : k
             }
         };
         const unsigned long long tstart = DIAG ? __builtin_amdgcn_s_memtime() : 0;
-        // fold period in RS-step passes (FOLD: at most ~fold_tiles rows per chain before it joins acc2)
-        const int64_t fpass = FOLD && fold_tiles > 0 ? (fold_tiles + RS - 1) / RS : (int64_t)1 << 62;
-        int64_t fcount = 0;
-        for (int64_t t0 = 0; t0 < nt + L; t0 += RS) {  // RS steps per pass: register slots are static
-            [&]<int... Q>(std::integer_sequence<int, Q...>) {
-                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
-            }(std::make_integer_sequence<int, RS>{});
-            if constexpr (FOLD) {
-                if (++fcount == fpass) {  // registers only: no memory operation joins the vmcnt pipeline
-                    fcount = 0;
+        // One pipeline loop for every mode: segments of chain_tiles tiles (SEG with chain_tiles > 0) or a single
+        // segment of the whole group; FOLD folds the T = 1 chain every fpass passes.
+        const int64_t F = seg_on ? chain_tiles : nt;
+        const int64_t fpass = FOLD && chain_tiles > 0 ? (chain_tiles + RS - 1) / RS : (int64_t)1 << 62;
+        int64_t fcount = 0, seg = 0;
+        for (lo = 0; lo < nt; lo += F, ++seg) {
+            hi = lo + F < nt ? lo + F : nt;
+            if (SEG && lo > 0) {  // refill the pipeline (segment 0's prologue ran above)
 #pragma unroll
-                    for (int k = 0; k < KW; ++k) {
-                        add4(acc2[k], acc[k][0]);
-                        acc[k][0] = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int i = 0; i < AH; ++i) load_tile(fl[i], lo + i);
+            }
+            for (int64_t t0 = lo; t0 < hi + L; t0 += RS) {  // RS steps per pass: register slots are static
+                [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                    (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+                }(std::make_integer_sequence<int, RS>{});
+                if constexpr (FOLD) {
+                    if (++fcount == fpass) {  // registers only: no memory operation joins the vmcnt pipeline
+                        fcount = 0;
+#pragma unroll
+                        for (int k = 0; k < KW; ++k) {
+                            add4(acc2[k], acc[k][0]);
+                            acc[k][0] = make_float4(0.f, 0.f, 0.f, 0.f);
+                        }
                     }
                 }
             }
+            if (SEG && seg_on) {  // this wave's sums of the segment: own partial block, then restart the chain
+                float4* out = reinterpret_cast<float4*>(partial + (((int64_t)seg * T + wrow) * I + gi) * ld);
+#pragma unroll
+                for (int k = 0; k < KW; ++k)
+#pragma unroll
+                    for (int h = 0; h < H; ++h) {
+                        out[(col4 + k * 64) * H + h] = acc[k][h];
+                        acc[k][h] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+            }
+        }
+        if (SEG && seg_on) {
+            __syncthreads();  // the exchange waves' two end barriers
+            __syncthreads();
+            return;
         }
         if constexpr (FOLD) {
 #pragma unroll
@@ -704,7 +744,10 @@ __global__ __launch_bounds__((SCHED == 4 || SCHED == 5) ? kFusedThreads + 64 : k
         };
         auto xiter = [&](auto pc, int64_t u) {
             constexpr int p = decltype(pc)::value;  // pv[p] receives tile u - PD
-            if (u < nt) {
+            // pacing: wait for the local row partials of tile u, except on a segment's first PD + PQ - 1 tiles,
+            // while the compute waves drain the previous segment (split schedules only use the wait to pace)
+            const bool pace = !(SEG && seg_on && u % chain_tiles < PD + PQ - 1);
+            if (u < nt && pace) {
                 const int ps = (int)(u & (NS - 1));
                 if (lane < T) {
                     float sv = 0.f;
@@ -751,11 +794,13 @@ __global__ __launch_bounds__((SCHED == 4 || SCHED == 5) ? kFusedThreads + 64 : k
 }
 
 constexpr size_t rows_lds_bytes(int T, int sched, int H = 1) {
-    return 4 /*NL*/ * 4 * 8 * 64 * sizeof(float4) +
-           ((sched >= 1 && sched <= 4) ? (4 / T) * 8 * 64 * H * sizeof(float4) : 0) +  // x slab in LDS
+    return (sched == 6 ? 3 : 4) /*NL x 32 KB*/ * 4 * 8 * 64 * sizeof(float4) +
+           (((sched >= 1 && sched <= 4) || sched == 6) ? (4 / T) * 8 * 64 * H * sizeof(float4) : 0) +  // x slab
            (8 * 4 * 3 + 8 + 4) * sizeof(float);
 }
 static_assert(rows_lds_bytes(4, 4, 2) <= 160 * 1024, "wide bf16 tiles: T = 4 fits the LDS");
+static_assert(rows_lds_bytes(2, 6, 2) <= 160 * 1024, "wide bf16 tiles: T = 2 (schedule 6) fits the LDS");
+static_assert(rows_lds_bytes(2, 4, 2) > 160 * 1024, "schedule 6 exists because the 4-slot ring does not fit");
 
 static int g_fused_dbg = 0;    // diagnostics only (set through fused_set_debug)
 static int g_fused_sched = 4;  // variant 6 pipeline schedule (k_fused_sweep_rows SCHED)
@@ -765,6 +810,10 @@ void fused_set_schedule(int sched) {
     g_fused_sched = sched;
 }
 int fused_get_schedule() { return g_fused_sched; }
+bool fused_split_schedule(int T, bool bf16) {  // mirrors the schedule choice of launch_rows / launch_fused_sweep_bf16
+    if (bf16) return T >= 2 || g_fused_sched == 5;
+    return g_fused_sched >= 4;  // T = 1: 4 and 5 both run schedule 5; T >= 2: 5 runs 4
+}
 std::vector<int> fused_debug_map(int nblocks) {
     std::vector<int> out((size_t)nblocks);
     hip_call(hipMemcpyFromSymbol(out.data(), HIP_SYMBOL(g_fused_map), out.size() * sizeof(int), 0, hipMemcpyDeviceToHost), "hipMemcpyFromSymbol");
@@ -807,7 +856,7 @@ static void launch_lds(bool logmode, dim3 grid, hipStream_t stream, const float*
 template <bool LG, bool X, bool D, int T, int SC, typename AT = float, int CPL = 4>
 static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                           const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
-                          uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, int64_t fold_tiles) {
+                          uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, int64_t chain_tiles) {
     constexpr size_t lds = rows_lds_bytes(T, SC, CPL / 4);
     static bool configured = false;
     if (!configured) {
@@ -816,16 +865,16 @@ static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld
         configured = true;
     }
     hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC, AT, CPL>), grid,
-                       dim3((SC == 4 || SC == 5) ? kFusedThreads + 64 : kFusedThreads), lds, stream, A, ld, nrows,
+                       dim3(sched_split(SC) ? kFusedThreads + 64 : kFusedThreads), lds, stream, A, ld, nrows,
                        nrows_pad, x,
-                       ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt, T == 1 ? fold_tiles : 0);
+                       ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt, chain_tiles);
 }
 
 template <int T>
 static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
                         int64_t nrows_pad, const float* x_, const float* ghat, const float* arow, float* partial,
                         double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt,
-                        int64_t fold_tiles) {
+                        int64_t chain_tiles) {
     const bool diag = (g_fused_dbg & 2) != 0;  // instrumented build only when asked (timing diagnostics)
     // g_fused_sched: pipeline schedule (k_fused_sweep_rows SCHED); schedules 1-4 hold the x slab in LDS,
     // which has room for it only when T >= 2. T = 1 runs schedule 5 (the split exchange with the x slab in
@@ -836,7 +885,7 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
     if (diag && sched != 2 && sched != 4) sched = 0;
     auto go = [&](auto lg, auto d, auto sc) {
         launch_rows_t<decltype(lg)::value, true, decltype(d)::value, T, decltype(sc)::value>(
-            grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt, fold_tiles);
+            grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt, chain_tiles);
     };
     using TT = std::true_type;
     using FF = std::false_type;
@@ -887,11 +936,13 @@ int fused_tile_rows(int K, int variant) {
 void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows,
                         int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
                         double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt,
-                        hipStream_t stream, int64_t fold_tiles) {
+                        hipStream_t stream, int64_t chain_tiles) {
     if (variant != 3 && variant != 6) throw std::runtime_error("fused_sweep: variant must be 6 or 3");
     const dim3 grid((unsigned)(I * J));
     if (variant == 6) {
         const int T = K;
+        if (T >= 2 && chain_tiles % kChainAlign != 0)
+            throw std::runtime_error("fused_sweep v6: segment length must be a multiple of 140 tiles");
         if (T != 1 && T != 2 && T != 4) throw std::runtime_error("fused_sweep v6: rows per tile (K) must be 1, 2 or 4");
         const int64_t slab = 8192 / T;  // columns per workgroup
         if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep v6: ld must equal J * slab");
@@ -899,11 +950,11 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
         if (J * T > kRowsGather) throw std::runtime_error("fused_sweep v6: J * T > 256");
         if (xcnt == nullptr || I % 8 != 0) throw std::runtime_error("fused_sweep v6: needs the per-XCD ticket counters and I % 8 == 0");
         if (T == 1) launch_rows<1>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
-                        fold_tiles);
+                        chain_tiles);
         else if (T == 2) launch_rows<2>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
-                        fold_tiles);
+                        chain_tiles);
         else launch_rows<4>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
-                        fold_tiles);
+                        chain_tiles);
         check_launch("k_fused_sweep_rows");
         return;
     }
@@ -922,16 +973,20 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
 }
 
 // bf16-stored RTM: variant 6 only (XCD-local row groups, same exchange as fp32). cpl 8 ("wide": 16-byte loads of
-// 8 bf16 per lane, slab 16384 / T columns) needs T = 4 (schedule 4, x slab in LDS); cpl 4 ("narrow": 8-byte
+// 8 bf16 per lane, slab 16384 / T columns) needs T = 4 (schedule 4, x slab in LDS) or T = 2 (schedule 6: a
+// 3-slot ring next to the two sub-slabs' x slab); cpl 4 ("narrow": 8-byte
 // loads, slab 8192 / T) runs schedule 4 for T >= 2 and for T = 1 schedule 0 with the deep bf16 lag (or 5 when
 // selected). A protocol timeout falls back to the bf16 two-pass kernels.
 void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                              const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                              uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream, int cpl,
-                             int64_t fold_tiles) {
+                             int64_t chain_tiles) {
     if (T != 1 && T != 2 && T != 4) throw std::runtime_error("fused_sweep bf16: rows per tile must be 1, 2 or 4");
-    if (cpl != 4 && !(cpl == 8 && T == 4)) throw std::runtime_error("fused_sweep bf16: wide tiles need T = 4");
+    if (cpl != 4 && !(cpl == 8 && (T == 4 || T == 2)))
+        throw std::runtime_error("fused_sweep bf16: wide tiles need T = 4 or 2");
     if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep bf16: padded rows must be a multiple of 4");
+    if (T >= 2 && chain_tiles % kChainAlign != 0)
+        throw std::runtime_error("fused_sweep bf16: segment length must be a multiple of 140 tiles");
     const int64_t slab = 2048 * cpl / T;
     if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep bf16: ld must equal J * slab");
     if (J * 4 > kMaxGather || J * T > kRowsGather) throw std::runtime_error("fused_sweep bf16: too many slabs");
@@ -940,15 +995,17 @@ void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, i
     auto go = [&](auto lg, auto tt, auto sc, auto cp) {
         launch_rows_t<decltype(lg)::value, true, false, decltype(tt)::value, decltype(sc)::value, bf16_t,
                       decltype(cp)::value>(grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
-                                           I, J, st, xcnt, fold_tiles);
+                                           I, J, st, xcnt, chain_tiles);
     };
     using S0 = std::integral_constant<int, 0>;
     using S4 = std::integral_constant<int, 4>;
     using S5 = std::integral_constant<int, 5>;
+    using S6 = std::integral_constant<int, 6>;
     using C4 = std::integral_constant<int, 4>;
     using C8 = std::integral_constant<int, 8>;
     auto by_t = [&](auto lg) {
-        if (cpl == 8) go(lg, std::integral_constant<int, 4>{}, S4{}, C8{});
+        if (cpl == 8 && T == 2) go(lg, std::integral_constant<int, 2>{}, S6{}, C8{});
+        else if (cpl == 8) go(lg, std::integral_constant<int, 4>{}, S4{}, C8{});
         else if (T == 1 && g_fused_sched == 5) go(lg, std::integral_constant<int, 1>{}, S5{}, C4{});
         else if (T == 1) go(lg, std::integral_constant<int, 1>{}, S0{}, C4{});
         else if (T == 2) go(lg, std::integral_constant<int, 2>{}, S4{}, C4{});

@@ -79,15 +79,19 @@ std::vector<unsigned long long> fused_debug_stats(int nblocks);
 void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                         const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                         uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream,
-                        int64_t fold_tiles = 0);
-// fold_tiles (variant 6 with T = 1 only, 0 = off): every ~fold_tiles tiles a compute wave folds its fp32
-// back-projection chain into a second accumulator set and restarts it (two-level sums; see fused_fold_tiles).
+                        int64_t chain_tiles = 0);
+// chain_tiles (variant 6; 0 = off): T = 1: every ~chain_tiles tiles a compute wave folds its fp32 back-projection
+// chain into a second register set (two-level sums). T >= 2 with a split schedule (fused_split_schedule): the
+// row groups run in segments of chain_tiles tiles (a multiple of kChainAlign); segment s writes the partial
+// blocks (s * T + row) * I + gi, so partial must hold I * T * segments rows of ld floats (fused_chain_plan).
+constexpr int64_t kChainAlign = 140;  // lcm of the register-slot counts RS (4, 5, 7) of the T >= 2 pipelines
+bool fused_split_schedule(int T, bool bf16);
 // bf16-stored RTM: the variant 6 sweep with bf16 tiles (T = rows per tile of the variant 6 geometry; cpl = bf16
 // columns per lane per k-slot: 4 (8-byte loads, slab 8192 / T) or 8 (16-byte loads, slab 16384 / T, T = 4 only))
 void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                              const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                              uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream,
-                             int cpl = 4, int64_t fold_tiles = 0);
+                             int cpl = 4, int64_t chain_tiles = 0);
 // p2p_allreduce.hip: one-shot push all-reduce through IPC-mapped peer buffers (at most 8 ranks, fp32).
 // Receive buffer of every rank: [2 parities][kP2pMaxRanks sources][cap] floats; flags: [sources][blocks].
 constexpr int kP2pMaxRanks = 8;

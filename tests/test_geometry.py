@@ -70,6 +70,15 @@ def test_forced_rows_per_tile_and_fallback():
     assert rtm.fused_geometry(64 * 1001, CUS, 6) is None
 
 
+@pytest.mark.parametrize("ld,T,J,I", [(65536, 4, 16, 16), (131072, 4, 32, 8), (262144, 2, 32, 8), (204800, 2, 25, 8),
+                                      (4096, 4, 1, 256)])
+def test_bf16_wide_geometry(ld, T, J, I):
+    """Wide bf16 tiles: T = 4 (slab 4096) where it fits an XCD, else T = 2 (slab 8192, schedule 6)."""
+    g = hip().fused_geometry_bf16_wide(ld, CUS)
+    assert g.valid() and (g.cpl, g.T, g.J, g.I) == (8, T, J, I)
+    assert not hip().fused_geometry_bf16_wide(524288, CUS).valid()
+
+
 def test_t1_fold_period(monkeypatch):
     """T = 1 sweeps fold their back-projection chains every ~sqrt(rows per group) tiles (two-level sums: the
     single-chain version measured 26x the two-pass error at 524288 rows); T >= 2 and variant 3 never fold."""
@@ -85,6 +94,23 @@ def test_t1_fold_period(monkeypatch):
     assert k.fused_fold_tiles(k.fused_geometry(65536, CUS, 3, 0), 65536) == 0
     monkeypatch.setenv("SART_FUSED_FOLD", "0")
     assert k.fused_fold_tiles(g1, 65536) == 0
+
+
+def test_segment_plan(monkeypatch):
+    """T >= 2 split schedules run row groups longer than 2240 tiles in segments, one partial block per segment
+    and tile row; shorter groups (the 64k x 64k headline: 2048 tiles per group) keep one chain."""
+    k = hip()
+    monkeypatch.delenv("SART_FUSED_SEG", raising=False)
+    g4 = k.fused_geometry(65536, CUS, 6, 4)
+    assert k.fused_chain_plan(g4, 65536, True) == (0, g4.I)
+    gw = k.fused_geometry_bf16_wide(262144, CUS)  # T = 2, I = 8: 32768 tiles per group at 512k rows
+    assert k.fused_chain_plan(gw, 524288, True) == (2240, 8 * 2 * 15)
+    assert k.fused_chain_plan(gw, 524288, False) == (0, 8)  # non-split schedules keep one chain
+    monkeypatch.setenv("SART_FUSED_SEG", "1000")  # rounded up to a multiple of 140
+    assert k.fused_chain_plan(gw, 524288, True) == (1120, 8 * 2 * 30)
+    monkeypatch.setenv("SART_FUSED_SEG", "0")
+    assert k.fused_chain_plan(gw, 524288, True) == (0, 8)
+    assert k.fused_split_schedule(2, True) and k.fused_split_schedule(4, False)
 
 
 def test_python_is_native():

@@ -177,14 +177,15 @@ def test_bf16_synthetic_bench_problem_converges(dev):
     assert np.linalg.norm(f - g) / np.linalg.norm(g) < 2e-2
 
 
-def test_bf16_rejected_by_multiframe(dev):
+def test_bf16_accepted_by_multiframe(dev):
+    """bf16 shards run in the multi-frame engine on the bf16 matrix cores (tests/test_gpu_multiframe_bf16.py)."""
     from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
     from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
     from mpi_cuda_sartsolver_amd.models.sart import SolverParams
 
     m = DenseRTM.synthetic(256, 512, device=dev, storage="bf16")
-    with pytest.raises(Exception, match="bf16"):
-        MultiFrameSARTSolver(m, None, None, SolverParams(max_iterations=4))
+    s = MultiFrameSARTSolver(m, None, None, SolverParams(max_iterations=4))
+    assert s.batch_width == 16
 
 
 @pytest.mark.parametrize("T", [1, 2, 4])
@@ -218,11 +219,13 @@ def test_bf16_fused_rows_per_tile(dev, T, log):
     assert np.linalg.norm(r1.solution - rt.solution) / np.linalg.norm(rt.solution) < 3e-3
 
 
-@pytest.mark.parametrize("nvox,J,I", [(4096, 1, 256), (65536, 16, 16), (131072, 32, 8), (100000, 26, 8)])
+@pytest.mark.parametrize("nvox,T,J,I", [(4096, 4, 1, 256), (65536, 4, 16, 16), (131072, 4, 32, 8), (100000, 4, 26, 8),
+                                        (262144, 2, 32, 8), (200000, 2, 25, 8)])
 @pytest.mark.parametrize("log", [False, True])
-def test_bf16_wide_tiles(dev, monkeypatch, nvox, J, I, log):
-    """Wide bf16 tiles (16-byte loads of 8 bf16 per lane, slab 4096 columns at T = 4) against the narrow bf16
-    tiles (SART_BF16_WIDE=0) and the device fp64 oracle on the stored (rounded) matrix."""
+def test_bf16_wide_tiles(dev, monkeypatch, nvox, T, J, I, log):
+    """Wide bf16 tiles (16-byte loads of 8 bf16 per lane: slab 4096 columns at T = 4, or 8192 at T = 2 with the
+    3-slot ring of schedule 6) against the narrow bf16 tiles (SART_BF16_WIDE=0) and the device fp64 oracle on
+    the stored (rounded) matrix."""
     from mpi_cuda_sartsolver_amd.models.oracle import sart_oracle_f64
     from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
     from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
@@ -231,7 +234,7 @@ def test_bf16_wide_tiles(dev, monkeypatch, nvox, J, I, log):
     g = prob.measurement.cpu().numpy()
     p = dict(max_iterations=10, conv_tolerance=0.0)
     sw = SARTSolver(prob.rtm, None, None, SolverParams(**p), logarithmic=log, allow_zero_tolerance=True)
-    assert sw.use_fused and (sw.geom.cpl, sw.geom.T, sw.geom.J, sw.geom.I) == (8, 4, J, I)
+    assert sw.use_fused and (sw.geom.cpl, sw.geom.T, sw.geom.J, sw.geom.I) == (8, T, J, I)
     rw = sw.solve(g)
     assert rw.used_fused and rw.fallbacks == 0
     np.testing.assert_array_equal(rw.solution, sw.solve(g).solution)  # bitwise reproducible
