@@ -119,6 +119,9 @@ for step in "$@"; do
     testsel) run pytest_sel 900 python -u -m pytest ${SEL:-tests} -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     profbf16) run rocprof_bf16 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bf16" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --rtm-dtype bf16 &&
               run rocprof_bf16_pmc 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/prof_bf16_pmc" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --iters 20 --rtm-dtype bf16 ;;
+    profr2) run rocprof_r2_fp32 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_r2_fp32" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 &&
+            run rocprof_r2_bf16_big 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_r2_bf16_big" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --rtm-dtype bf16 --npix 524288 --nvox 262144 --iters 20 &&
+            run rocprof_r2_mfb64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_r2_mfb64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --rtm-dtype bf16 ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
