@@ -347,6 +347,32 @@ struct FusedTile<bf16_t, 8> {
     }
 };
 
+// bf16 row dots on v_dot2c_f32_bf16: the x slab is held in LDS as hi = rne(x) and lo ~ x - hi bf16 pairs (the
+// fp32 slab's bytes), so a dword of the tile (two bf16) meets its two x columns in two dot2 instructions with no
+// conversion: 1 VALU op per element instead of a shift / mask plus half a packed FMA. Products of bf16 are exact
+// in fp32 (dot2 measured unbiased, <= 0.75 ulp: tools/dot2_probe.hip).
+// hi + lo holds x to 2^-17. With lo rounded to nearest, that representation error is a deterministic function of
+// x, so equal or clustered x values (a clamped cold start) bias the row dot coherently: 2^-18 of F, which the
+// cancellation in ghat - F amplified to 3x the fp32 self-check error at 512k x 256k. lo is therefore rounded
+// stochastically (a hash of the element index picks the rounding point; deterministic, zero mean, independent
+// across columns), which makes the dot's x error average out like fp32 rounding.
+typedef __bf16 sart_bf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float dot2_bf16(unsigned a, unsigned b, float c) {
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(sart_bf2, a), __builtin_bit_cast(sart_bf2, b), c, false);
+}
+__device__ __forceinline__ unsigned sr_bf16_bits(float r, uint32_t key) {  // stochastic rounding of |r| to bf16
+    uint32_t h = key * 0x9E3779B1u;
+    h ^= h >> 15;
+    h *= 0x85EBCA77u;
+    h ^= h >> 13;
+    return (__float_as_uint(r) + (h & 0xffffu)) >> 16;  // magnitude rounds up with probability = the dropped part
+}
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t key, unsigned& hi, unsigned& lo) {
+    const __bf16 ha = (__bf16)a, hb = (__bf16)b;
+    hi = (unsigned)__builtin_bit_cast(unsigned short, ha) | ((unsigned)__builtin_bit_cast(unsigned short, hb) << 16);
+    lo = sr_bf16_bits(a - (float)ha, key) | (sr_bf16_bits(b - (float)hb, key + 1) << 16);
+}
+
 // Schedules with a separate publisher wave (the split exchange)
 constexpr bool sched_split(int sched) { return sched == 4 || sched == 5 || sched == 6; }
 
@@ -370,6 +396,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     constexpr int NTHR = SPLIT ? kFusedThreads + 64 : kFusedThreads;
     constexpr bool BF = !std::is_same<AT, float>::value;
     constexpr int H = CPL / 4;  // float4 per lane per k-slot (2: wide bf16 tiles)
+    constexpr bool DOT2 = BF && XS_LDS;  // bf16 row dots on dot2 with the x slab as hi / lo bf16 pairs in LDS
     static_assert(CPL == 4 || (BF && CPL == 8 && XS_LDS), "wide tiles: bf16 storage, x slab in LDS");
     // bf16 tiles are parked raw in the LDS ring (16 KB per slot), so 8 slots fit in the 128 KB of the fp32
     // ring. With T = 1 (schedule 0) the bf16 sweep keeps 4 polls in flight and lags the back-projection by
@@ -455,7 +482,28 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     if (DIAG && threadIdx.x == 0 && b < 1024) g_fused_map[b] = gi * 1024 + gj;
 
     for (int i = threadIdx.x; i < NS * 4 + NS; i += NTHR) s_pflag[i] = -1;
-    if constexpr (XS_LDS) {
+    if constexpr (DOT2) {
+        // lane-vector lv = (sub * KW + k) * 64 + lane holds CPL columns; LDS: H = 2: [(sub KW + k) 2 + {hi, lo}]
+        // [lane] of uint4 (8 bf16 each); H = 1: [(sub KW + k)][lane] of uint4 {hi (4 bf16), lo (4 bf16)}
+        const float4* xsrc = reinterpret_cast<const float4*>(x) + (int64_t)gj * (64 * KW * WPR) * H;
+        uint4* xd = reinterpret_cast<uint4*>(s_xs);
+        for (int lv = threadIdx.x; lv < WPR * KW * 64; lv += NTHR) {
+            unsigned hi[2 * H], lo[2 * H];
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                const float4 v = xsrc[lv * H + h];
+                const uint32_t key = (uint32_t)(((int64_t)gj * (WPR * KW * 64) + lv) * CPL + 4 * h);  // column
+                split_pair(v.x, v.y, key, hi[2 * h], lo[2 * h]);
+                split_pair(v.z, v.w, key + 2, hi[2 * h + 1], lo[2 * h + 1]);
+            }
+            if constexpr (H == 2) {
+                xd[((lv >> 6) * 2 + 0) * 64 + (lv & 63)] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+                xd[((lv >> 6) * 2 + 1) * 64 + (lv & 63)] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+            } else {
+                xd[lv] = make_uint4(hi[0], hi[1], lo[0], lo[1]);
+            }
+        }
+    } else if constexpr (XS_LDS) {
         // global float4 i of the slab = lane-vector i / H, half i % H; LDS [(sub * KW + k) * H + h][lane] so a
         // wave reads 64 consecutive float4 per (k, h)
         const float4* xsrc = reinterpret_cast<const float4*>(x) + (int64_t)gj * (64 * KW * WPR) * H;
@@ -514,16 +562,37 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
             constexpr int bp = (bb + RS - D) % RS;          // register slot of tile t - D
             if (t < hi) {
                 float s = 0.f;
+                if constexpr (DOT2) {
+                    const uint4* xb = reinterpret_cast<const uint4*>(xl);
+                    float sh = 0.f, sl = 0.f;  // hi and lo chains
 #pragma unroll
-                for (int k = 0; k < KW; ++k) {
-                    float4 w[H];
-                    FT::widen(fl[bb][k], w);
+                    for (int k = 0; k < KW; ++k) {
+                        const RT a = fl[bb][k];
+                        if constexpr (H == 2) {
+                            const uint4 xh = xb[(k * 2 + 0) * 64], xo = xb[(k * 2 + 1) * 64];
+                            sh = dot2_bf16(a.x, xh.x, sh), sl = dot2_bf16(a.x, xo.x, sl);
+                            sh = dot2_bf16(a.y, xh.y, sh), sl = dot2_bf16(a.y, xo.y, sl);
+                            sh = dot2_bf16(a.z, xh.z, sh), sl = dot2_bf16(a.z, xo.z, sl);
+                            sh = dot2_bf16(a.w, xh.w, sh), sl = dot2_bf16(a.w, xo.w, sl);
+                        } else {
+                            const uint4 v = xb[k * 64];  // {hi pair 0, hi pair 1, lo pair 0, lo pair 1}
+                            sh = dot2_bf16(a.x, v.x, sh), sl = dot2_bf16(a.x, v.z, sl);
+                            sh = dot2_bf16(a.y, v.y, sh), sl = dot2_bf16(a.y, v.w, sl);
+                        }
+                    }
+                    s = sh + sl;
+                } else {
 #pragma unroll
-                    for (int h = 0; h < H; ++h) {
-                        if constexpr (XS_LDS)
-                            s += dot4(w[h], xl[(k * H + h) * 64]);
-                        else
-                            s += dot4(w[h], xs[k]);
+                    for (int k = 0; k < KW; ++k) {
+                        float4 w[H];
+                        FT::widen(fl[bb][k], w);
+#pragma unroll
+                        for (int h = 0; h < H; ++h) {
+                            if constexpr (XS_LDS)
+                                s += dot4(w[h], xl[(k * H + h) * 64]);
+                            else
+                                s += dot4(w[h], xs[k]);
+                        }
                     }
                 }
                 s = wave_sum(s);

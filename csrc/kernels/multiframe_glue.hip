@@ -263,12 +263,18 @@ __global__ void k_mf_state_begin(MfState* __restrict__ st, const double* __restr
     }
 }
 
-// bf16 operand planes of the bf16 MFMA projections (multiframe_bf16.hip): hi = rne(x), lo = rne(x - hi).
-__device__ __forceinline__ void split_bf16(float x, bf16_t& hi, bf16_t& lo) {
+// bf16 operand planes of the bf16 MFMA projections (multiframe_bf16.hip): hi = rne(x) and lo = x - hi rounded
+// stochastically to bf16 (a hash of the element index picks the rounding point: deterministic, zero mean and
+// independent across elements), so the 2^-17 representation error of hi + lo does not bias sums over equal or
+// clustered values (the same reasoning and measurement as the fused sweep's bf16 x slab, fused_sweep.hip).
+__device__ __forceinline__ void split_bf16(float x, uint32_t key, bf16_t& hi, bf16_t& lo) {
     const __bf16 h = (__bf16)x;
-    const __bf16 l = (__bf16)(x - (float)h);
     hi = __builtin_bit_cast(bf16_t, h);
-    lo = __builtin_bit_cast(bf16_t, l);
+    uint32_t r = key * 0x9E3779B1u;
+    r ^= r >> 15;
+    r *= 0x85EBCA77u;
+    r ^= r >> 13;
+    lo = (bf16_t)((__float_as_uint(x - (float)h) + (r & 0xffffu)) >> 16);
 }
 
 // X [nf][ld] fp32 -> planes of the same layout (n % 4 == 0).
@@ -278,10 +284,11 @@ __global__ __launch_bounds__(256) void k_mf_split_x(const float* __restrict__ X,
     if (i >= n4) return;
     const float4 v = reinterpret_cast<const float4*>(X)[i];
     bf16_t h[4], l[4];
-    split_bf16(v.x, h[0], l[0]);
-    split_bf16(v.y, h[1], l[1]);
-    split_bf16(v.z, h[2], l[2]);
-    split_bf16(v.w, h[3], l[3]);
+    const uint32_t key = (uint32_t)(4 * i);
+    split_bf16(v.x, key, h[0], l[0]);
+    split_bf16(v.y, key + 1, h[1], l[1]);
+    split_bf16(v.z, key + 2, h[2], l[2]);
+    split_bf16(v.w, key + 3, h[3], l[3]);
     reinterpret_cast<uint2*>(hi)[i] = make_uint2(h[0] | (unsigned)h[1] << 16, h[2] | (unsigned)h[3] << 16);
     reinterpret_cast<uint2*>(lo)[i] = make_uint2(l[0] | (unsigned)l[1] << 16, l[2] | (unsigned)l[3] << 16);
 }
@@ -301,7 +308,7 @@ __global__ __launch_bounds__(256) void k_mf_split_w(const float* __restrict__ W,
         const int f = i / 64, rr = i % 64;
         if (r0 + rr >= ldw) continue;
         bf16_t h, l;
-        split_bf16(tile[rr][mf_bp_slot(f, nf)], h, l);
+        split_bf16(tile[rr][mf_bp_slot(f, nf)], (uint32_t)((int64_t)f * ldw + r0 + rr), h, l);
         hi[(int64_t)f * ldw + r0 + rr] = h;
         lo[(int64_t)f * ldw + r0 + rr] = l;
     }

@@ -35,7 +35,8 @@ def _bf16_rtm(dev, P, V, seed):
 
 
 def test_split_planes(k, dev):
-    """hi = rne(x), lo = rne(x - hi): hi + lo reproduces x to 2^-16 relative; W planes are frame-major."""
+    """hi = rne(x), lo = x - hi rounded stochastically: hi + lo reproduces x to 2^-16 relative, without bias over
+    equal values; W planes are frame-major."""
     rng = np.random.default_rng(5)
     x = torch.from_numpy((rng.standard_normal(4096) * 10.0 ** rng.uniform(-6, 6, 4096)).astype(np.float32)).to(dev)
     hi = torch.empty(4096, dtype=torch.bfloat16, device=dev)
@@ -45,6 +46,13 @@ def test_split_planes(k, dev):
     assert torch.equal(hi, x.bfloat16())
     rec = hi.double() + lo.double()
     assert ((rec - x.double()).abs() <= 2.0 ** -16 * x.double().abs()).all()
+    # 4096 copies of one value: round-to-nearest lo would repeat one error 4096 times; the stochastic lo's
+    # errors average out (mean relative error << the 2^-18 bound of a single element)
+    same = torch.full((4096,), 1.2345678, dtype=torch.float32, device=dev)
+    k.mf_split_x(same.data_ptr(), 4096, hi.data_ptr(), lo.data_ptr(), _stream(dev))
+    torch.cuda.synchronize()
+    err = (hi.double() + lo.double() - same.double()).mean().item() / 1.2345678
+    assert abs(err) < 2.0 ** -22, err
 
     nf, rows, ldw = 32, 192, 160
     W = torch.from_numpy(rng.random((rows, nf)).astype(np.float32)).to(dev)  # [rows][16][nf / 16] layout
