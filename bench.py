@@ -319,7 +319,8 @@ def main() -> int:
         "vs_baseline": None,
         "dtype": "fp32" if args.rtm_dtype == "fp32" else (
             "bf16 RTM storage, bf16 MFMA with hi+lo bf16 split of X / W, fp32 accumulation" if multi
-            else "bf16 RTM storage, fp32 compute"),
+            else "bf16 RTM storage; fused row dots on bf16 dot2 with hi+lo split x, fp32 sums"
+            if solver.use_fused else "bf16 RTM storage, fp32 compute"),
         "data": "synthetic (on-device random dense RTM, random phantom; no HDF5)",
         "iters_per_s": round(iters_per_s, 3),
         "sart_iterations_per_step": args.iters,
