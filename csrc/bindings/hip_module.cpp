@@ -43,6 +43,7 @@ static py::dict solve_info(const sart::SolveInfo& i) {
     d["ms"] = i.ms;
     d["sweeps"] = i.sweeps;
     d["comm_ms"] = i.comm_ms;
+    d["warm_from"] = i.warm_from;
     return d;
 }
 

@@ -308,10 +308,12 @@ int main(int argc, char** argv) {
         for (uint64_t i = 0; i < image.nframe(); ++i)
             if (image.frame_time(i) > skip_until + 1e-12) frames.push_back(i);
         if (batched) {
-            // --batch_frames N: N frames solved together on the matrix cores. Without --no_guess the batches form
-            // a warm-started time series (every frame of batch k + 1 starts from batch k's last solution, the first
-            // batch from the resumed solution or cold); with --no_guess every frame cold-starts.
-            const size_t nb = (size_t)cfg.batch_frames;
+            // --batch_frames N: N slots on the matrix cores with continuous batching (a finished frame's slot takes
+            // the next frame between two sweeps). Frames are read in windows of 4 N; without --no_guess they form a
+            // warm-started time series (the window's first N frames start from the previous window's last solution
+            // or the resumed one, later frames from the latest finished frame); with --no_guess every frame
+            // cold-starts.
+            const size_t nb = (size_t)cfg.batch_frames * 4;
             std::vector<double> bwarm = cfg.no_guess ? std::vector<double>() : warm;
             auto read_chunk = [&image, &frames, nb, P = blk.size](size_t c0) {
                 std::vector<double> g;
@@ -330,8 +332,9 @@ int main(int argc, char** argv) {
                 const int B = (int)std::min(nb, frames.size() - c0);
                 std::vector<double> xb((size_t)B * in.nvoxel);
                 const auto t0 = std::chrono::steady_clock::now();
+                const int64_t first_warm = (c0 > 0 && !bwarm.empty()) ? (int64_t)frames[c0 - 1] : -1;
                 const std::vector<SolveInfo> infos =
-                    mf->solve_batch(g.data(), B, xb.data(), bwarm.empty() ? nullptr : bwarm.data());
+                    mf->solve_batch(g.data(), B, xb.data(), bwarm.empty() ? nullptr : bwarm.data(), !cfg.no_guess);
                 if (!cfg.no_guess) {
                     bwarm.assign(xb.end() - (std::ptrdiff_t)in.nvoxel, xb.end());
                     if (!std::all_of(bwarm.begin(), bwarm.end(), [](double v) { return std::isfinite(v); }))
@@ -348,7 +351,9 @@ int main(int argc, char** argv) {
                         if (profile.is_open())
                             profile << "{\"frame\": " << cur << ", \"time\": " << image.frame_time(cur)
                                     << ", \"status\": " << infos[f].status << ", \"iterations\": " << infos[f].iterations
-                                    << ", \"ms\": " << ms / B << ", \"batch\": " << B << ", \"driver\": \"native\"}\n";
+                                    << ", \"ms\": " << ms / B << ", \"batch\": " << cfg.batch_frames << ", \"warm_from\": "
+                                    << (infos[f].warm_from >= 0 ? (int64_t)frames[c0 + infos[f].warm_from] : first_warm)
+                                    << ", \"driver\": \"native\"}\n";
                     }
                 }
             }

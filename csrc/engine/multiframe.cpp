@@ -38,6 +38,8 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hg_), std::max<int64_t>(P_, 1) * NF * sizeof(double)),
            "hipHostMalloc");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hx_), (size_t)NF * ld_ * sizeof(float)), "hipHostMalloc");
+    hip_ok(hipEventCreateWithFlags(&ev_copy_, hipEventDisableTiming), "hipEventCreate");
     nsf_ = mf_forward_num_splits(ld_, Pp_);
     nsb_ = bf16_ ? mf_backproject_b16_num_splits(ld_, P_) : mf_backproject_num_splits(ld_, P_);
     nwb_ = mf_weights_num_blocks(Pp_);
@@ -51,7 +53,6 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     if (cfg_.logarithmic) O_.resize((size_t)NF * ld_);
     for (auto* b : {&ghat_, &arow_, &gpos_, &wo_}) b->resize((size_t)Pp_ * NF);
     g64_.resize((size_t)Pp_ * NF);
-    norm64_.resize(NF);
     G64_.resize(NF);
     F2part_.resize((size_t)nwb_ * NF);
     st_.resize(1);
@@ -96,6 +97,8 @@ MultiFrameEngine::~MultiFrameEngine() {
     if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
     if (hstate_) (void)hipHostFree(hstate_);
     if (hg_) (void)hipHostFree(hg_);
+    if (hx_) (void)hipHostFree(hx_);
+    if (ev_copy_) (void)hipEventDestroy(ev_copy_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -138,6 +141,7 @@ void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int
 void MultiFrameEngine::sweep() {
     const int NF = nf_;
     MfState* st = st_.get();
+    const MfSkipScope skip(&st->all_done);  // every slot done: the sweep's heavy kernels return at once
     float* D = buf_.get();                     // [ld][nf] voxel-major corrections
     float* F2 = buf_.get() + (int64_t)NF * ld_;  // [nf] ||A x||^2, all-reduced with the last chunk
     const float* scale = cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get();
@@ -183,112 +187,222 @@ void MultiFrameEngine::sweep() {
                      Xprev_.get());
 }
 
-void MultiFrameEngine::solve_group(const double* g, int B, double* x_out, SolveInfo* info, const double* x0) {
-    RoctxRange range("sart::mf_solve");
+// Continuous batching. The batch's nf columns are slots: every slot holds one frame, and a slot whose frame has
+// finished (converged, non-finite, or max_iter) is refilled with the next frame between two sweeps, so no
+// sweep works on finished frames while frames are waiting (the former group-by-group solve ran every group
+// as long as its slowest frame). All ranks see the same device state (it follows all-reduced sums), so they
+// admit the same frames at the same chunk.
+// Start values: the first frames start from x0 (or cold); later frames of a time series (chain) from the
+// solution of the latest frame finished before them (SolveInfo::warm_from), otherwise cold (--no_guess).
+// The chunks of check_interval sweeps stay pipelined: chunk c + 1 is queued before the state after chunk c
+// is read, so a refill decided on chunk c's state is queued after chunk c + 1 and the slot's new frame is
+// visible in the states from chunk c + 2 on.
+void MultiFrameEngine::admit(const double* g, const std::vector<int>& slots, const std::vector<int>& frames,
+                             const double* warm, const float* dev_src, double src_norm,
+                             std::vector<double>& slot_norm) {
     const int NF = nf_;
-    const auto t0 = std::chrono::steady_clock::now();
-    // host: layout [rows][nf], per-frame maxima and sums of squares (reference sartsolver_cuda.cpp:146-157)
+    const int k = (int)slots.size();
+    if (k == 0) return;
+    // per-frame maxima and positive sums of squares over all ranks' pixels (reference sartsolver_cuda.cpp:146-157)
     double mx[kMfMaxFrames], gs[kMfMaxFrames];
-    for (int f = 0; f < NF; ++f) mx[f] = -std::numeric_limits<double>::infinity(), gs[f] = 0.0;
-    for (int64_t p = 0; p < P_; ++p)
-        for (int f = 0; f < NF; ++f) {
-            double v = f < B ? g[(int64_t)f * P_ + p] : 0.0;
+    for (int q = 0; q < k; ++q) {
+        mx[q] = -std::numeric_limits<double>::infinity(), gs[q] = 0.0;
+        const double* gq = g + (int64_t)frames[q] * P_;
+        double* hq = hg_ + (int64_t)q * P_;
+        for (int64_t p = 0; p < P_; ++p) {
+            double v = gq[p];
             if (!std::isfinite(v)) v = -1.0;  // non-finite pixel: masked like a saturated one
-            hg_[p * NF + f] = v;
-            if (f < B) {
-                mx[f] = std::max(mx[f], v);
-                if (v > 0) gs[f] += v * v;
-            }
+            hq[p] = v;
+            mx[q] = std::max(mx[q], v);
+            if (v > 0) gs[q] += v * v;
         }
-    comm_->host().all_reduce_host(mx, NF, ReduceOp::kMax);
-    comm_->host().all_reduce_host(gs, NF, ReduceOp::kSum);
-    double norm[kMfMaxFrames], G[kMfMaxFrames];
-    for (int f = 0; f < NF; ++f) {
-        norm[f] = (f < B && mx[f] > 0) ? mx[f] : 1.0;
-        G[f] = gs[f] / (norm[f] * norm[f]);
-        if (!(G[f] > 0)) G[f] = 1.0;
     }
-    if (P_) hip_ok(hipMemcpyAsync(g64_.get(), hg_, P_ * NF * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D g");
-    hip_ok(hipMemcpyAsync(norm64_.get(), norm, NF * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D norm");
-    hip_ok(hipMemcpyAsync(G64_.get(), G, NF * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D G");
-    launch_mf_prep(g64_.get(), P_, Pp_, norm64_.get(), rs_.ray_len.get(), (float)cfg_.ray_length_threshold,
-                   ghat_.get(), arow_.get(), gpos_.get(), wo_.get(), NF, stream_);
-    if (x0) {  // warm start: x_prev / s per frame, clamped (reference sartsolver_cuda.cpp:176-180)
-        if ((int64_t)x064_.size() < V_) x064_.resize(std::max<int64_t>(V_, 1));
-        if (V_) hip_ok(hipMemcpyAsync(x064_.get(), x0, V_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D x0");
-        launch_mf_init_warm(X_.get(), x064_.get(), norm64_.get(), V_, ld_, B, NF, stream_);
-    } else {
-        // cold start x0 = max([rho > tau] A^T max(ghat, 0) / rho, 1e-7) per frame (reference sart_kernels.cu:22-60)
+    comm_->host().all_reduce_host(mx, k, ReduceOp::kMax);
+    comm_->host().all_reduce_host(gs, k, ReduceOp::kSum);
+    MfSlots sl{};
+    sl.n = k;
+    for (int q = 0; q < k; ++q) {
+        sl.slot[q] = slots[q];
+        sl.norm[q] = mx[q] > 0 ? mx[q] : 1.0;
+        sl.G[q] = gs[q] / (sl.norm[q] * sl.norm[q]);
+        if (!(sl.G[q] > 0)) sl.G[q] = 1.0;
+        slot_norm[slots[q]] = sl.norm[q];
+    }
+    if (P_) hip_ok(hipMemcpyAsync(g64_.get(), hg_, (size_t)k * P_ * sizeof(double), hipMemcpyHostToDevice, stream_),
+                   "H2D g");
+    launch_mf_prep_slots(g64_.get(), P_, Pp_, sl, rs_.ray_len.get(), (float)cfg_.ray_length_threshold, ghat_.get(),
+                         arow_.get(), gpos_.get(), wo_.get(), NF, stream_);
+    if (warm) {  // x = x_prev / s, clamped (reference sartsolver_cuda.cpp:176-180)
+        if (V_) hip_ok(hipMemcpyAsync(x064_.get(), warm, V_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D x0");
+        launch_mf_init_slots_warm(X_.get(), x064_.get(), sl, V_, ld_, stream_);
+    } else if (dev_src) {  // copied first: a new frame may enter the source's own slot
+        if (V_) hip_ok(hipMemcpyAsync(xsrc_.get(), dev_src, V_ * sizeof(float), hipMemcpyDeviceToDevice, stream_), "D2D");
+        launch_mf_init_slots_scaled(X_.get(), xsrc_.get(), src_norm, sl, V_, ld_, stream_);
+    } else {  // x0 = max([rho > tau] A^T max(ghat, 0) / rho, 1e-7) (reference sart_kernels.cu:22-60)
         backproject(gpos_.get(), true, 0, ld_);
         launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, nullptr, buf_.get(), nullptr, 0, nullptr, NF, stream_);
         comm_->all_reduce(buf_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
-        launch_mf_init(X_.get(), buf_.get(), rs_.dinv.get(), V_, ld_, B, NF, stream_);
+        launch_mf_init_slots_cold(X_.get(), buf_.get(), rs_.dinv.get(), sl, V_, ld_, NF, stream_);
     }
-    if (cfg_.logarithmic) {  // frame-constant observed back-projection, reduced once per batch
+    if (cfg_.logarithmic) {  // frame-constant observed back-projection of the new frames
         backproject(wo_.get(), true, 0, ld_);
-        launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, rs_.dmask.get(), O_.get(), nullptr, 0, nullptr, NF, stream_);
-        comm_->all_reduce(O_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
+        launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, rs_.dmask.get(), Otmp_.get(), nullptr, 0, nullptr, NF,
+                          stream_);
+        comm_->all_reduce(Otmp_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
+        launch_mf_copy_slots(O_.get(), Otmp_.get(), sl, ld_, NF, stream_);
     }
-    launch_mf_state_begin(st_.get(), G64_.get(), B, cfg_.conv_tolerance, cfg_.max_iterations, NF, stream_);
-    // Chunks of check_interval sweeps, pipelined like Engine::solve: chunk c + 1 is queued before the state
-    // after chunk c is read, so the GPU never drains between chunks (sweeps after all_done are no-ops).
-    const int max_sweeps = cfg_.max_iterations + 1;
-    int enqueued = 0, issued = 0, checked = 0;
-    auto issue = [&]() {
-        const int n = std::min(cfg_.check_interval, max_sweeps - enqueued);
-        {
-            RoctxRange r("sart::mf_chunk");
-            for (int i = 0; i < n; ++i) sweep();
-        }
-        enqueued += n;
-        const int slot = issued & 1;
-        hip_ok(hipMemcpyAsync(hstate_ + slot, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
-        hip_ok(hipEventRecord(ev_[slot], stream_), "event");
-        ++issued;
-    };
-    issue();
-    while (true) {
-        if (enqueued < max_sweeps) issue();
-        const int slot = checked & 1;
-        hip_ok(hipEventSynchronize(ev_[slot]), "mf chunk");
-        ++checked;
-        if (hstate_[slot].all_done || (checked == issued && enqueued >= max_sweeps)) break;
-    }
-    std::vector<float> xh((size_t)NF * ld_), xp;
-    hip_ok(hipMemcpyAsync(xh.data(), X_.get(), xh.size() * sizeof(float), hipMemcpyDeviceToHost, stream_), "D2H X");
-    hip_ok(hipMemcpyAsync(hstate_, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
-    hip_ok(hipStreamSynchronize(stream_), "mf solve");
-    if (hstate_->flags) {  // NaN/Inf guard: frames that stopped on a non-finite iterate return the last finite one
-        xp.resize(xh.size());
-        hip_ok(hipMemcpy(xp.data(), Xprev_.get(), xp.size() * sizeof(float), hipMemcpyDeviceToHost), "D2H Xprev");
-    }
-    comm_->check();
-    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    for (int f = 0; f < B; ++f) {
-        const bool rollback = (hstate_->rollback >> f) & 1;
-        const float* src = rollback ? xp.data() : xh.data();
-        for (int64_t v = 0; v < V_; ++v) x_out[(int64_t)f * V_ + v] = (double)src[(size_t)f * ld_ + v] * norm[f];
-        info[f].status = hstate_->status[f] == kSuccess ? kSuccess : kMaxIterationsExceeded;
-        info[f].iterations = hstate_->iters[f];
-        info[f].convergence = hstate_->conv[f];
-        info[f].nonfinite = (hstate_->flags >> f) & 1;
-        info[f].used_fused = false;
-        info[f].ms = ms / B;
-    }
+    launch_mf_slot_reset(st_.get(), sl, stream_);
 }
 
 std::vector<SolveInfo> MultiFrameEngine::solve_batch(const double* g, int nframes, double* x_out, const double* x0,
                                                      bool chain) {
     set_device();
+    RoctxRange range("sart::mf_solve");
+    const int NF = nf_;
     std::vector<SolveInfo> out(std::max(nframes, 0));
-    const double* warm = x0;
-    for (int b0 = 0; b0 < nframes; b0 += nf_) {
-        const int B = std::min(nf_, nframes - b0);
-        solve_group(g + (int64_t)b0 * P_, B, x_out + (int64_t)b0 * V_, out.data() + b0, warm);
-        // time-series warm start: the next group starts from this group's last solution (if it is finite)
-        const double* last = x_out + (int64_t)(b0 + B - 1) * V_;
-        warm = chain && std::all_of(last, last + V_, [](double v) { return std::isfinite(v); }) ? last : nullptr;
+    if (nframes <= 0) return out;
+    const auto t0 = std::chrono::steady_clock::now();
+    if ((int64_t)x064_.size() < V_) x064_.resize(std::max<int64_t>(V_, 1));
+    if (cfg_.logarithmic && (int64_t)Otmp_.size() < (int64_t)NF * ld_) Otmp_.resize((size_t)NF * ld_);
+    if ((int64_t)xsrc_.size() < ld_) xsrc_.resize(ld_);
+    // every slot starts empty (done) with finite zero columns
+    for (auto* b : {&X_, &Xprev_, &ghat_, &arow_, &gpos_, &wo_})
+        hip_ok(hipMemsetAsync(b->get(), 0, b->size() * sizeof(float), stream_), "memset");
+    if (cfg_.logarithmic) hip_ok(hipMemsetAsync(O_.get(), 0, O_.size() * sizeof(float), stream_), "memset");
+    hip_ok(hipMemsetAsync(G64_.get(), 0, G64_.size() * sizeof(double), stream_), "memset");
+    launch_mf_state_begin(st_.get(), G64_.get(), 0, cfg_.conv_tolerance, cfg_.max_iterations, NF, stream_);
+
+    std::vector<int> slot_frame(NF, -1), slot_valid(NF, 0), frame_warm(nframes, -1);
+    std::vector<double> slot_norm(NF, 1.0), frame_norm(nframes, 1.0);
+    int next = 0, finished = 0, latest = -1;  // latest: highest-index frame finished with a finite solution
+    int issued = 0, checked = 0;
+    // frames whose solution is being copied back (finalised at the next state check, after the copy)
+    struct Pending {
+        int frame, slot;
+        bool rollback;
+    };
+    std::vector<Pending> pend;
+    auto finalize = [&]() {
+        for (const Pending& pd : pend) {
+            const float* src = hx_ + (size_t)pd.slot * ld_;
+            double* dst = x_out + (int64_t)pd.frame * V_;
+            for (int64_t v = 0; v < V_; ++v) dst[v] = (double)src[v] * frame_norm[pd.frame];
+            bool finite = true;
+            for (int64_t v = 0; v < V_ && finite; ++v) finite = std::isfinite(dst[v]);
+            if (finite && pd.frame > latest) latest = pd.frame;
+            ++finished;
+        }
+        pend.clear();
+    };
+    // dev: the best finished frame whose solution is still only on the device (collected at this check)
+    struct DevSrc {
+        int frame = -1, slot = -1;
+        bool prev = false;
+    };
+    auto fill = [&](const std::vector<int>& free_slots, const DevSrc& dev) {
+        std::vector<int> slots, frames;
+        for (int f : free_slots) {
+            if (next >= nframes) break;
+            slots.push_back(f);
+            frames.push_back(next++);
+        }
+        if (slots.empty()) return;
+        const double* warm = nullptr;
+        const float* dsrc = nullptr;
+        double dnorm = 1.0;
+        int wsrc = -1;
+        if (issued == 0) {
+            warm = x0;  // the first frames: the caller's start value (or cold)
+        } else if (chain && dev.frame > latest) {
+            dsrc = (dev.prev ? Xprev_.get() : X_.get()) + (size_t)dev.slot * ld_;
+            dnorm = frame_norm[dev.frame];
+            wsrc = dev.frame;
+        } else if (chain && latest >= 0) {
+            warm = x_out + (int64_t)latest * V_;
+            wsrc = latest;
+        }
+        admit(g, slots, frames, warm, dsrc, dnorm, slot_norm);
+        for (size_t q = 0; q < slots.size(); ++q) {
+            slot_frame[slots[q]] = frames[q];
+            slot_valid[slots[q]] = issued;  // states from the next chunk on describe this frame
+            frame_warm[frames[q]] = wsrc;
+        }
+    };
+    // Sweeps are queued in chunks of at most check_interval, and never past the last sweep a running frame can
+    // need: a frame admitted after `enq` queued sweeps has made its final decision by sweep enq + max_iter + 1
+    // (its slot keeps the device sweep counter running), so a fixed-iteration batch queues exactly the sweeps
+    // it uses.
+    int64_t enq = 0;
+    std::vector<int64_t> slot_end(NF, 0);
+    auto issue = [&]() {
+        int64_t bound = 0;
+        for (int f = 0; f < NF; ++f)
+            if (slot_frame[f] >= 0) bound = std::max(bound, slot_end[f] - enq);
+        const int n = (int)std::min<int64_t>(cfg_.check_interval, bound);
+        if (n <= 0) return false;
+        {
+            RoctxRange r("sart::mf_chunk");
+            for (int i = 0; i < n; ++i) sweep();
+        }
+        enq += n;
+        const int slot = issued & 1;
+        hip_ok(hipMemcpyAsync(hstate_ + slot, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
+        hip_ok(hipEventRecord(ev_[slot], stream_), "event");
+        ++issued;
+        return true;
+    };
+    auto admitted = [&]() {  // after fill(): the end bound of the slots that just took frames
+        for (int f = 0; f < NF; ++f)
+            if (slot_frame[f] >= 0 && slot_valid[f] == issued) slot_end[f] = enq + cfg_.max_iterations + 1;
+    };
+    std::vector<int> all(NF);
+    for (int f = 0; f < NF; ++f) all[f] = f;
+    fill(all, DevSrc{});
+    admitted();
+    issue();
+    while (finished < nframes) {
+        issue();  // keep the next chunk in flight while frames run
+        if (!pend.empty()) {  // the solutions copied at the previous check
+            hip_ok(hipEventSynchronize(ev_copy_), "mf copy");
+            finalize();
+            if (finished >= nframes) break;
+        }
+        if (checked >= issued) throw std::runtime_error("MultiFrameEngine: no chunk in flight and frames unfinished");
+        const int c = checked++;
+        hip_ok(hipEventSynchronize(ev_[c & 1]), "mf chunk");
+        const MfState S = hstate_[c & 1];
+        std::vector<int> freed;
+        DevSrc best;
+        for (int f = 0; f < NF; ++f) {
+            const int fr = slot_frame[f];
+            if (fr < 0 || c < slot_valid[f] || !S.done[f]) continue;
+            const bool rollback = (S.rollback >> f) & 1;
+            SolveInfo& info = out[fr];
+            info.status = S.status[f] == kSuccess ? kSuccess : kMaxIterationsExceeded;
+            info.iterations = S.iters[f];
+            info.convergence = S.conv[f];
+            info.nonfinite = (S.flags >> f) & 1;
+            info.used_fused = false;
+            info.warm_from = frame_warm[fr];
+            frame_norm[fr] = slot_norm[f];
+            const float* src = (rollback ? Xprev_.get() : X_.get()) + (size_t)f * ld_;
+            hip_ok(hipMemcpyAsync(hx_ + (size_t)f * ld_, src, V_ * sizeof(float), hipMemcpyDeviceToHost, stream_),
+                   "D2H x");
+            pend.push_back({fr, f, rollback});
+            if (!(info.nonfinite && !rollback) && fr > best.frame) best = DevSrc{fr, f, rollback};
+            slot_frame[f] = -1;
+            freed.push_back(f);
+        }
+        if (!freed.empty()) {
+            hip_ok(hipEventRecord(ev_copy_, stream_), "event");  // the copies, before the refills' work
+            fill(freed, best);
+            admitted();
+        }
     }
+    hip_ok(hipStreamSynchronize(stream_), "mf solve");
+    comm_->check();
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (auto& info : out) info.ms = ms / nframes;
     return out;
 }
 

@@ -30,10 +30,11 @@ class MultiFrameEngine {
     MultiFrameEngine& operator=(const MultiFrameEngine&) = delete;
 
     void set_laplacian(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t nnz);
-    // g: nframes x nrows (host fp64, frame-major); x_out: nframes x nvoxel. Solved batch_frames() at a time.
-    // x0 (optional, nvoxel, de-normalised like a solution): warm start of the first group (null: cold start).
-    // chain: every later group starts from the solution of the previous group's last frame (time series);
-    // otherwise every later group cold-starts.
+    // g: nframes x nrows (host fp64, frame-major); x_out: nframes x nvoxel. batch_frames() slots, refilled with
+    // the next frame as soon as a slot's frame finishes (continuous batching). x0 (optional, nvoxel,
+    // de-normalised like a solution): start value of the first batch_frames() frames (null: cold). chain: every
+    // later frame starts from the solution of the latest frame finished before it (time series; the index is
+    // SolveInfo::warm_from); otherwise later frames cold-start.
     std::vector<SolveInfo> solve_batch(const double* g, int nframes, double* x_out, const double* x0 = nullptr,
                                        bool chain = false);
     int64_t nrows() const { return P_; }
@@ -43,7 +44,11 @@ class MultiFrameEngine {
     static int batch_width(int frames);
 
    private:
-    void solve_group(const double* g, int B, double* x_out, SolveInfo* info, const double* x0);
+    // frames[q] of g into slots[q] (normalisation, prep, start value, log observed back-projection, state)
+    // Start value: warm (host, de-normalised), else dev_src (a finished frame's normalised solution still on
+    // the device, normalisation src_norm), else cold.
+    void admit(const double* g, const std::vector<int>& slots, const std::vector<int>& frames, const double* warm,
+               const float* dev_src, double src_norm, std::vector<double>& slot_norm);
     void sweep();
     void set_device() const;
     // F = A X (Fs_ split-K partials); the bf16 engine first writes the X planes
@@ -63,7 +68,7 @@ class MultiFrameEngine {
     int nsf_ = 1, nsb_ = 1, nwb_ = 1;
     DeviceRaySums rs_;
     DeviceArray<float> X_, Xprev_, Fs_, W_, part_, buf_, pen_, O_, ghat_, arow_, gpos_, wo_;
-    DeviceArray<double> g64_, norm64_, G64_, F2part_, x064_;
+    DeviceArray<double> g64_, G64_, F2part_, x064_;
     DeviceArray<bf16_t> Xh_, Xl_, Wh_, Wl_;  // bf16 engine: hi / lo operand planes
     DeviceArray<MfState> st_;
     DeviceArray<int64_t> lap_rp_;
@@ -77,7 +82,11 @@ class MultiFrameEngine {
     hipEvent_t comm_done_ = nullptr;
     MfState* hstate_ = nullptr;  // pinned [2]: state after each of the two chunks in flight
     hipEvent_t ev_[2] = {nullptr, nullptr};
-    double* hg_ = nullptr;       // pinned [rows][nf] staging of a batch
+    double* hg_ = nullptr;       // pinned [k][rows] staging of the frames entering slots
+    float* hx_ = nullptr;        // pinned [nf][ld]: solutions of finished frames, per slot
+    hipEvent_t ev_copy_ = nullptr;
+    DeviceArray<float> Otmp_;    // log mode: observed back-projection of the frames entering slots
+    DeviceArray<float> xsrc_;    // [ld] copy of the finished frame that warm-starts a refill
 };
 
 }  // namespace sart

@@ -118,6 +118,17 @@ int mf_backproject_vox_align(int64_t ld, int nf);
 void launch_mf_backproject(const float* A, int64_t ld, int64_t nrows, const float* W, int nsplit, float* partial,
                            int nf, hipStream_t stream, int64_t v0 = 0, int64_t v1 = -1);
 // multiframe_glue.hip
+// No-op sweeps of the multi-frame engine: while a MfSkipScope is alive on the calling thread, the heavy multi-frame
+// kernels (projections, weights, collect, operand splits) launched from it return at once when *skip != 0 (the
+// device flag MfState::all_done: every slot's frame is done and the sweep would change nothing).
+extern thread_local const int* g_mf_skip;
+struct MfSkipScope {
+    explicit MfSkipScope(const int* p) : prev(g_mf_skip) { g_mf_skip = p; }
+    ~MfSkipScope() { g_mf_skip = prev; }
+    MfSkipScope(const MfSkipScope&) = delete;
+    MfSkipScope& operator=(const MfSkipScope&) = delete;
+    const int* prev;
+};
 // bf16-stored RTM (multiframe_bf16.hip): the same projections on v_mfma_f32_16x16x32_bf16 with the fp32
 // operand (X or W) split into hi + lo bf16 planes (k_mf_split_x: X [nf][ld] -> planes [nf][ld]; k_mf_split_w:
 // W [rows][16][nf / 16] -> frame-major planes [nf][ldw], ldw >= rows rounded up to 32).
@@ -131,25 +142,29 @@ void launch_mf_backproject_b16(const bf16_t* A, int64_t ld, int64_t nrows, const
 void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStream_t stream);
 void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, bf16_t* hi, bf16_t* lo,
                        hipStream_t stream);
-void launch_mf_prep(const double* g, int64_t nrows, int64_t nrows_pad, const double* norm, const float* ray_length,
-                    float len_thres, float* ghat, float* arow, float* gpos, float* wo, int nf, hipStream_t stream);
 int mf_weights_num_blocks(int64_t nrows_pad);
 void launch_mf_weights(const float* Fs, int nsplit, int64_t nrows_pad, const float* ghat, const float* arow,
                        bool logmode, float* W, double* F2part, int nf, hipStream_t stream);
 // D[v][f] (voxel-major) for v in [v0, v1); F2out (optional) = per-frame sums of F2part
 void launch_mf_collect(const float* part, int nsplit, int64_t ld, int64_t v0, int64_t v1, const float* scale, float* D,
                        const double* F2part, int nF2, float* F2out, int nf, hipStream_t stream);
-void launch_mf_init(float* X, const float* D0, const float* dinv, int64_t nvox, int64_t ld, int nused, int nf,
-                    hipStream_t stream);
 void launch_mf_penalty(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta, bool logx,
                        const float* X, int64_t ld, float* pen, const MfState* st, int nf, hipStream_t stream);
 void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream);
-// X[f][v] = max(x0[v] / norm[f], 1e-7) for the nused frames (one warm start shared by the batch)
-void launch_mf_init_warm(float* X, const double* x0, const double* norm, int64_t nvox, int64_t ld, int nused, int nf,
-                         hipStream_t stream);
 // Xprev (optional): receives X before the update (NaN/Inf guard rollback)
 void launch_mf_update(float* X, const float* D, const float* O, const float* pen, float alpha, bool logmode,
                       int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream, float* Xprev = nullptr);
+// continuous batching (multiframe_glue.hip): new frames enter the slots listed in MfSlots between sweeps
+void launch_mf_prep_slots(const double* gk, int64_t nrows, int64_t nrows_pad, const MfSlots& sl, const float* ray_length,
+                          float len_thres, float* ghat, float* arow, float* gpos, float* wo, int nf, hipStream_t stream);
+void launch_mf_init_slots_warm(float* X, const double* x0, const MfSlots& sl, int64_t nvox, int64_t ld,
+                               hipStream_t stream);
+void launch_mf_init_slots_scaled(float* X, const float* xs, double s_src, const MfSlots& sl, int64_t nvox, int64_t ld,
+                                 hipStream_t stream);
+void launch_mf_init_slots_cold(float* X, const float* D0, const float* dinv, const MfSlots& sl, int64_t nvox,
+                               int64_t ld, int nf, hipStream_t stream);
+void launch_mf_copy_slots(float* O, const float* src, const MfSlots& sl, int64_t ld, int nf, hipStream_t stream);
+void launch_mf_slot_reset(MfState* st, const MfSlots& sl, hipStream_t stream);
 void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, int max_iter, int nf,
                            hipStream_t stream);
 }  // namespace sart

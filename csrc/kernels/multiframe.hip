@@ -27,6 +27,7 @@
 //   A operand: lane l holds A[i = l & 15][k = l >> 4]; B operand: B[k = l >> 4][j = l & 15];
 //   C/D: col = l & 15, row = (l >> 4) * 4 + reg.
 #include "sart_common.hpp"
+#include "launchers.hpp"
 
 #include <cstdlib>
 #include <stdexcept>
@@ -66,7 +67,9 @@ __device__ __forceinline__ void load_groups(float (&dst)[NG], const float* __res
 template <int NG, int DEPTH, int RT, bool NT>
 __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A, int64_t ld, int64_t nrows,
                                                     int64_t nrows_pad, const float* __restrict__ X,
-                                                    int64_t ldx, float* __restrict__ Fout, int64_t cols_per_split) {
+                                                    int64_t ldx, float* __restrict__ Fout, int64_t cols_per_split,
+                                                    const int* __restrict__ skip) {
+    if (skip && *skip) return;  // every frame of the batch is done: the sweep is a no-op
     constexpr int NF = 16 * NG;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * (16 * RT);
@@ -169,7 +172,9 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
 template <int NG, int DEPTH, int VT>
 __global__ __launch_bounds__(256) void k_mf_backproject(const float* __restrict__ A, int64_t ld, int64_t nrows,
                                                         const float* __restrict__ W, int64_t rows_per_split,
-                                                        float* __restrict__ partial, int64_t vb0, int64_t vend) {
+                                                        float* __restrict__ partial, int64_t vb0, int64_t vend,
+                                                        const int* __restrict__ skip) {
+    if (skip && *skip) return;
     constexpr int NF = 16 * NG;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t vb = vb0 + (int64_t)blockIdx.x * 4 + wave;  // block of 64 * VT voxels
@@ -338,11 +343,11 @@ template <int NG, int RT, bool NT>
 static void fwd_rt_nt(dim3 grid, int depth, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
                       int64_t nrows_pad, const float* X, int64_t ldx, float* Fout, int64_t cps) {
     if (depth == 1)
-        hipLaunchKernelGGL((k_mf_forward<NG, 1, RT, NT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+        hipLaunchKernelGGL((k_mf_forward<NG, 1, RT, NT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps, g_mf_skip);
     else if (depth == 3)
-        hipLaunchKernelGGL((k_mf_forward<NG, 3, RT, NT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+        hipLaunchKernelGGL((k_mf_forward<NG, 3, RT, NT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps, g_mf_skip);
     else
-        hipLaunchKernelGGL((k_mf_forward<NG, 2, RT, NT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps);
+        hipLaunchKernelGGL((k_mf_forward<NG, 2, RT, NT>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X, ldx, Fout, cps, g_mf_skip);
 }
 
 // Non-temporal A loads in the MFMA forward (experiment knob, SART_MF_NT=1; default plain loads).
@@ -397,13 +402,13 @@ static void bwd_vt(dim3 grid, int depth, hipStream_t stream, const float* A, int
                    int64_t rps, float* partial, int64_t vb0, int64_t vend) {
     if (depth == 1)
         hipLaunchKernelGGL((k_mf_backproject<NG, 1, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial,
-                           vb0, vend);
+                           vb0, vend, g_mf_skip);
     else if (depth == 3)
         hipLaunchKernelGGL((k_mf_backproject<NG, 3, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial,
-                           vb0, vend);
+                           vb0, vend, g_mf_skip);
     else
         hipLaunchKernelGGL((k_mf_backproject<NG, 2, VT>), grid, dim3(256), 0, stream, A, ld, nrows, W, rps, partial,
-                           vb0, vend);
+                           vb0, vend, g_mf_skip);
 }
 
 template <int NG>

@@ -25,6 +25,7 @@
 // Ring loads are unconditional (clamped to the last step) like the fp32 kernels: the compiler then keeps
 // DEPTH steps of loads in flight with counted vmcnt waits.
 #include "sart_common.hpp"
+#include "launchers.hpp"
 
 #include <cstdlib>
 #include <cstring>
@@ -70,7 +71,8 @@ template <int NG, int DEPTH, int RT, int KB>
 __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict__ A, int64_t ld, int64_t nrows,
                                                         int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                         const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
-                                                        int64_t cols_per_split) {
+                                                        int64_t cols_per_split, const int* __restrict__ skip) {
+    if (skip && *skip) return;  // every frame of the batch is done: the sweep is a no-op
     constexpr int NF = 16 * NG;
     constexpr int RS = DEPTH + 1;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -153,7 +155,8 @@ template <int NG, int DEPTH, int RT, int KB>
 __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const bf16_t* __restrict__ A, int64_t ld, int64_t nrows,
                                                             int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                             const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
-                                                            int64_t cols_per_split) {
+                                                            int64_t cols_per_split, const int* __restrict__ skip) {
+    if (skip && *skip) return;
     constexpr int NF = 16 * NG;
     constexpr int RS = DEPTH + 1;
     constexpr int C = KB * 2 * NG;             // 1 KiB X pieces per step
@@ -252,7 +255,8 @@ __global__ __launch_bounds__(256) void k_mf_backproject_b16(const bf16_t* __rest
                                                             int64_t nrows32, const bf16_t* __restrict__ Wh,
                                                             const bf16_t* __restrict__ Wl, int64_t ldw,
                                                             int64_t rows_per_split, float* __restrict__ partial,
-                                                            int64_t vb0, int64_t vend) {
+                                                            int64_t vb0, int64_t vend, const int* __restrict__ skip) {
+    if (skip && *skip) return;
     constexpr int NF = 16 * NG;
     constexpr int RS = DEPTH + 1;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -338,7 +342,8 @@ __global__ __launch_bounds__(256) void k_mf_backproject_b16_lds(const bf16_t* __
                                                                 int64_t nrows32, const bf16_t* __restrict__ Wh,
                                                                 const bf16_t* __restrict__ Wl, int64_t ldw,
                                                                 int64_t rows_per_split, float* __restrict__ partial,
-                                                                int64_t vb0, int64_t vend) {
+                                                                int64_t vb0, int64_t vend, const int* __restrict__ skip) {
+    if (skip && *skip) return;
     constexpr int NF = 16 * NG;
     constexpr int RS = DEPTH + 1;
     constexpr int C = 2 * NG;
@@ -493,10 +498,10 @@ static void fwd_b16_t(bool lds, dim3 grid, hipStream_t stream, const bf16_t* A, 
                       int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
     if (lds)
         hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB>), grid, dim3(256), 0, stream, A, ld, nrows,
-                           nrows_pad, Xh, Xl, Fout, cps);
+                           nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
     else
         hipLaunchKernelGGL((k_mf_forward_b16<NG, DEPTH, RT, KB>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad,
-                           Xh, Xl, Fout, cps);
+                           Xh, Xl, Fout, cps, g_mf_skip);
 }
 
 template <int NG, int DEPTH>
@@ -564,18 +569,18 @@ static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const bf16_t* A, in
     if (mf_b16_bwd_lds(16 * NG)) {
         if (vt == 2)
             hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2>), grid, dim3(256), 0, stream, A, ld, nrows32,
-                               Wh, Wl, ldw, rps, partial, vb0, vend);
+                               Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
         else
             hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1>), grid, dim3(256), 0, stream, A, ld, nrows32,
-                               Wh, Wl, ldw, rps, partial, vb0, vend);
+                               Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
         return;
     }
     if (vt == 2)
         hipLaunchKernelGGL((k_mf_backproject_b16<NG, DEPTH, 2>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
-                           ldw, rps, partial, vb0, vend);
+                           ldw, rps, partial, vb0, vend, g_mf_skip);
     else
         hipLaunchKernelGGL((k_mf_backproject_b16<NG, DEPTH, 1>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
-                           ldw, rps, partial, vb0, vend);
+                           ldw, rps, partial, vb0, vend, g_mf_skip);
 }
 
 template <int NG>

@@ -9,6 +9,7 @@
 // (reference sartsolver_cuda.cpp:138-354): every frame has its own normalisation, saturation mask,
 // convergence history, status and iteration count; finished frames are frozen.
 #include "sart_common.hpp"
+#include "launchers.hpp"
 
 #include <math.h>
 
@@ -20,33 +21,11 @@ namespace sart {
 
 constexpr int kMaxNF = kMfMaxFrames;
 
+thread_local const int* g_mf_skip = nullptr;
+
 // Position of frame f inside a row of a back-projection operand ([rows][16][nf / 16], multiframe.hip
 // k_mf_backproject): frame f = 16 j + i sits at i * (nf / 16) + j, so a lane's column groups are adjacent.
 __device__ __forceinline__ int mf_bp_slot(int f, int nf) { return (f & 15) * (nf >> 4) + (f >> 4); }
-
-// ghat = fp32(g / s_f); a = [ghat >= 0][len > tau_l] / len; gpos = max(ghat, 0); wo = a * ghat.
-// ghat and a are [rows][nf]; gpos and wo feed the back-projection and use its layout (mf_bp_slot).
-__global__ __launch_bounds__(256) void k_mf_prep(const double* __restrict__ g, int64_t nrows, int64_t nrows_pad,
-                                                 const double* __restrict__ norm, const float* __restrict__ ray_length,
-                                                 float len_thres, float* __restrict__ ghat, float* __restrict__ arow,
-                                                 float* __restrict__ gpos, float* __restrict__ wo, int nf) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // element of [rows_pad][nf]
-    if (i >= nrows_pad * nf) return;
-    const int64_t row = i / nf;
-    const int f = (int)(i % nf);
-    float gh = 0.f, a = 0.f;
-    if (row < nrows) {
-        gh = (float)(g[i] / norm[f]);
-        const float len = ray_length[row];
-        const float inv_len = (len > len_thres) ? 1.f / len : 0.f;
-        a = (gh >= 0.f) ? inv_len : 0.f;
-    }
-    ghat[i] = gh;
-    arow[i] = a;
-    const int64_t ib = row * nf + mf_bp_slot(f, nf);
-    gpos[ib] = gh > 0.f ? gh : 0.f;
-    wo[ib] = a * gh;
-}
 
 // F = sum_s Fsplit[s] (fixed order); W = a F (log) or a (ghat - F) (linear), written in the
 // back-projection layout (mf_bp_slot); per-block, per-frame partial sums of F^2 in fp64 (deterministic:
@@ -55,7 +34,8 @@ constexpr int kWRows = 64;  // rows per block (>= 1024 blocks at 64k rows: the k
 __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs, int nsplit, int64_t nrows_pad,
                                                     const float* __restrict__ ghat, const float* __restrict__ arow,
                                                     int logmode, float* __restrict__ W, double* __restrict__ F2part,
-                                                    int nf) {
+                                                    int nf, const int* __restrict__ skip) {
+    if (skip && *skip) return;
     __shared__ double red[256];
     const int f = threadIdx.x % nf, rsub = threadIdx.x / nf, rstep = 256 / nf;  // rstep rows x nf frames per pass
     const int64_t r0 = (int64_t)blockIdx.x * kWRows;
@@ -83,7 +63,8 @@ __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs
 __global__ __launch_bounds__(256) void k_mf_collect(const float* __restrict__ part, int nsplit, int64_t ld, int64_t v0,
                                                     int64_t v1, const float* __restrict__ scale, float* __restrict__ D,
                                                     const double* __restrict__ F2part, int nF2, float* __restrict__ F2out,
-                                                    int nf) {
+                                                    int nf, const int* __restrict__ skip) {
+    if (skip && *skip) return;
     const int64_t i = v0 * nf + (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < v1 * nf) {
         const int64_t v = i / nf;
@@ -104,39 +85,6 @@ __global__ __launch_bounds__(256) void k_mf_collect(const float* __restrict__ pa
             F2out[threadIdx.x] = (float)t;
         }
     }
-}
-
-// X[f][v] = max(D0[v][f] * dinv[v], 1e-7) for real voxels of used frames, 0 elsewhere (D0 voxel-major).
-__global__ __launch_bounds__(256) void k_mf_init(float* __restrict__ X, const float* __restrict__ D0,
-                                                 const float* __restrict__ dinv, int64_t nvox, int64_t ld, int nused,
-                                                 int nf) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)nf * ld) return;
-    const int f = (int)(i / ld);
-    const int64_t v = i % ld;
-    float x = 0.f;
-    if (f < nused && v < nvox) {
-        x = D0[v * nf + f] * dinv[v];
-        x = x > 1e-7f ? x : 1e-7f;
-    }
-    X[i] = x;
-}
-
-// Warm start of every used frame from one solution x0 (fp64, nvox): X[f][v] = max(x0[v] / norm[f], 1e-7)
-// (reference sartsolver_cuda.cpp:176-180: x = x_prev / s, then the clamp); padding and unused frames 0.
-__global__ __launch_bounds__(256) void k_mf_init_warm(float* __restrict__ X, const double* __restrict__ x0,
-                                                      const double* __restrict__ norm, int64_t nvox, int64_t ld,
-                                                      int nused, int nf) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)nf * ld) return;
-    const int f = (int)(i / ld);
-    const int64_t v = i % ld;
-    float x = 0.f;
-    if (f < nused && v < nvox) {
-        x = (float)(x0[v] / norm[f]);
-        x = x > 1e-7f ? x : 1e-7f;
-    }
-    X[i] = x;
 }
 
 // pen[f][v] = beta * sum_j L[v, j] x[f][j] (or log x), one thread per (row, frame), fixed order.
@@ -171,31 +119,33 @@ __global__ void k_mf_decide(MfState* __restrict__ st, const float* __restrict__ 
     __syncthreads();
     if (f < st->nf) {
         const double F = (double)F2[f];
+        const int sf = s - st->sweep0[f];  // this frame's own sweep (continuous batching refills slots)
         int done = st->done[f];
         if (!isfinite(F)) {
-            if (!done) {  // NaN/Inf guard: the frame stops; its last finite iterate (s - 1 updates) is in Xprev
+            if (!done) {  // NaN/Inf guard: the frame stops; its last finite iterate (sf - 1 updates) is in Xprev
                 atomicOr(&st->flags, 1ull << f);
-                if (s > 0) atomicOr(&st->rollback, 1ull << f);
-                st->iters[f] = s > 0 ? s - 1 : 0;
+                if (sf > 0) atomicOr(&st->rollback, 1ull << f);
+                st->iters[f] = sf > 0 ? sf - 1 : 0;
                 done = 1;
             }
-        } else if (s >= 1) {
+        } else if (sf >= 1) {
             const double conv = (st->G[f] - F) / st->G[f];
-            const bool newly = !done && s >= 2 && fabs(conv - st->conv_prev[f]) < st->tol;
+            const bool newly = !done && sf >= 2 && fabs(conv - st->conv_prev[f]) < st->tol;
             if (newly) {
                 st->status[f] = kSuccess;
-                st->iters[f] = s;
+                st->iters[f] = sf;
             }
             if (!(done && !newly)) st->conv_prev[f] = conv;
             st->conv[f] = conv;
             done = done || newly;
         }
+        if (sf >= st->max_iter) done = 1;  // max_iter updates applied: status stays MAX_ITERATIONS_EXCEEDED
         st->done[f] = done;
         if (!done) atomicAnd(&alld, 0);
     }
     __syncthreads();
     if (f == 0) {
-        st->all_done = (alld || s >= st->max_iter) ? 1 : 0;
+        st->all_done = alld ? 1 : 0;
         st->sweep = s + 1;
     }
 }
@@ -251,6 +201,7 @@ __global__ void k_mf_state_begin(MfState* __restrict__ st, const double* __restr
         st->done[f] = f < nused ? 0 : 1;
         st->status[f] = kMaxIterationsExceeded;
         st->iters[f] = max_iter;
+        st->sweep0[f] = 0;
     }
     if (f == 0) {
         st->sweep = 0;
@@ -279,7 +230,8 @@ __device__ __forceinline__ void split_bf16(float x, uint32_t key, bf16_t& hi, bf
 
 // X [nf][ld] fp32 -> planes of the same layout (n % 4 == 0).
 __global__ __launch_bounds__(256) void k_mf_split_x(const float* __restrict__ X, int64_t n4, bf16_t* __restrict__ hi,
-                                                    bf16_t* __restrict__ lo) {
+                                                    bf16_t* __restrict__ lo, const int* __restrict__ skip) {
+    if (skip && *skip) return;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n4) return;
     const float4 v = reinterpret_cast<const float4*>(X)[i];
@@ -296,7 +248,9 @@ __global__ __launch_bounds__(256) void k_mf_split_x(const float* __restrict__ X,
 // W [rows][16][nf / 16] (back-projection layout, mf_bp_slot) -> frame-major planes [nf][ldw]: 64 rows per block
 // through an LDS tile, so both the reads and the 128-byte plane writes are coalesced.
 __global__ __launch_bounds__(256) void k_mf_split_w(const float* __restrict__ W, int64_t nrows_pad, int nf,
-                                                    int64_t ldw, bf16_t* __restrict__ hi, bf16_t* __restrict__ lo) {
+                                                    int64_t ldw, bf16_t* __restrict__ hi, bf16_t* __restrict__ lo,
+                                                    const int* __restrict__ skip) {
+    if (skip && *skip) return;
     __shared__ float tile[64][kMaxNF + 1];
     const int64_t r0 = (int64_t)blockIdx.x * 64;
     for (int i = threadIdx.x; i < 64 * nf; i += 256) {
@@ -314,18 +268,116 @@ __global__ __launch_bounds__(256) void k_mf_split_w(const float* __restrict__ W,
     }
 }
 
+// ---- continuous batching: frames enter freed slots between sweeps (MultiFrameEngine::solve_batch)
+
+// Per-slot prep of k new frames from a compact frame-major staging gk [k][rows] (non-finite pixels already
+// -1): the columns `slot` of ghat / arow ([rows][nf]) and of gpos / wo (back-projection layout).
+__global__ __launch_bounds__(256) void k_mf_prep_slots(const double* __restrict__ gk, int64_t nrows, int64_t nrows_pad,
+                                                       MfSlots sl, const float* __restrict__ ray_length,
+                                                       float len_thres, float* __restrict__ ghat,
+                                                       float* __restrict__ arow, float* __restrict__ gpos,
+                                                       float* __restrict__ wo, int nf) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // element of [k][rows_pad]
+    if (i >= (int64_t)sl.n * nrows_pad) return;
+    const int q = (int)(i / nrows_pad);
+    const int64_t row = i % nrows_pad;
+    const int f = sl.slot[q];
+    float gh = 0.f, a = 0.f;
+    if (row < nrows) {
+        gh = (float)(gk[(int64_t)q * nrows + row] / sl.norm[q]);
+        const float len = ray_length[row];
+        const float inv_len = (len > len_thres) ? 1.f / len : 0.f;
+        a = (gh >= 0.f) ? inv_len : 0.f;
+    }
+    ghat[row * nf + f] = gh;
+    arow[row * nf + f] = a;
+    const int64_t ib = row * nf + mf_bp_slot(f, nf);
+    gpos[ib] = gh > 0.f ? gh : 0.f;
+    wo[ib] = a * gh;
+}
+
+// Warm start of the new frames from one (de-normalised, fp64) solution x0: X[slot][v] = max(x0[v] / s, 1e-7).
+__global__ __launch_bounds__(256) void k_mf_init_slots_warm(float* __restrict__ X, const double* __restrict__ x0,
+                                                            MfSlots sl, int64_t nvox, int64_t ld) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)sl.n * ld) return;
+    const int q = (int)(i / ld);
+    const int64_t v = i % ld;
+    float x = 0.f;
+    if (v < nvox) {
+        x = (float)(x0[v] / sl.norm[q]);
+        x = x > 1e-7f ? x : 1e-7f;
+    }
+    X[(int64_t)sl.slot[q] * ld + v] = x;
+}
+
+// Warm start of the new frames from the normalised solution xs of a frame that just finished in another slot
+// (still on the device): x_prev = xs * s_src, then X[slot][v] = max(x_prev / s, 1e-7) -- the same fp64
+// arithmetic as the host path (solution = X * s, then x0 / s).
+__global__ __launch_bounds__(256) void k_mf_init_slots_scaled(float* __restrict__ X, const float* __restrict__ xs,
+                                                              double s_src, MfSlots sl, int64_t nvox, int64_t ld) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)sl.n * ld) return;
+    const int q = (int)(i / ld);
+    const int64_t v = i % ld;
+    float x = 0.f;
+    if (v < nvox) {
+        x = (float)((double)xs[v] * s_src / sl.norm[q]);
+        x = x > 1e-7f ? x : 1e-7f;
+    }
+    X[(int64_t)sl.slot[q] * ld + v] = x;
+}
+
+// Cold start of the new frames: X[slot][v] = max(D0[v][slot] * dinv[v], 1e-7) (D0 voxel-major, reduced).
+__global__ __launch_bounds__(256) void k_mf_init_slots_cold(float* __restrict__ X, const float* __restrict__ D0,
+                                                            const float* __restrict__ dinv, MfSlots sl, int64_t nvox,
+                                                            int64_t ld, int nf) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)sl.n * ld) return;
+    const int q = (int)(i / ld);
+    const int64_t v = i % ld;
+    const int f = sl.slot[q];
+    float x = 0.f;
+    if (v < nvox) {
+        x = D0[v * nf + f] * dinv[v];
+        x = x > 1e-7f ? x : 1e-7f;
+    }
+    X[(int64_t)f * ld + v] = x;
+}
+
+// O[v][slot] = src[v][slot] for the new frames' columns (the frame-constant observed back-projection, log mode).
+__global__ __launch_bounds__(256) void k_mf_copy_slots(float* __restrict__ O, const float* __restrict__ src, MfSlots sl,
+                                                       int64_t ld, int nf) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)sl.n * ld) return;
+    const int f = sl.slot[(int)(i / ld)];
+    const int64_t v = i % ld;
+    O[v * nf + f] = src[v * nf + f];
+}
+
+// The new frames' state: fresh convergence history, sweep count from the current sweep.
+__global__ void k_mf_slot_reset(MfState* __restrict__ st, MfSlots sl) {
+    const int q = threadIdx.x;
+    if (q < sl.n) {
+        const int f = sl.slot[q];
+        st->G[f] = sl.G[q];
+        st->conv_prev[f] = 0.0;
+        st->conv[f] = 0.0;
+        st->done[f] = 0;
+        st->status[f] = kMaxIterationsExceeded;
+        st->iters[f] = st->max_iter;
+        st->sweep0[f] = st->sweep;
+        atomicAnd(&st->flags, ~(1ull << f));
+        atomicAnd(&st->rollback, ~(1ull << f));
+    }
+    __syncthreads();
+    if (q == 0 && sl.n > 0) st->all_done = 0;
+}
+
 static inline unsigned nb(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 static void check_nf(int nf, const char* what) {
     if (nf != 16 && nf != 32 && nf != 64) throw std::runtime_error(std::string(what) + ": nf must be 16, 32 or 64");
-}
-
-void launch_mf_prep(const double* g, int64_t nrows, int64_t nrows_pad, const double* norm, const float* ray_length,
-                    float len_thres, float* ghat, float* arow, float* gpos, float* wo, int nf, hipStream_t stream) {
-    check_nf(nf, "mf_prep");
-    hipLaunchKernelGGL(k_mf_prep, dim3(nb(nrows_pad * nf)), dim3(256), 0, stream, g, nrows, nrows_pad, norm,
-                       ray_length, len_thres, ghat, arow, gpos, wo, nf);
-    check_launch("k_mf_prep");
 }
 
 int mf_weights_num_blocks(int64_t nrows_pad) { return (int)((nrows_pad + kWRows - 1) / kWRows); }
@@ -334,7 +386,7 @@ void launch_mf_weights(const float* Fs, int nsplit, int64_t nrows_pad, const flo
                        bool logmode, float* W, double* F2part, int nf, hipStream_t stream) {
     check_nf(nf, "mf_weights");
     hipLaunchKernelGGL(k_mf_weights, dim3((unsigned)mf_weights_num_blocks(nrows_pad)), dim3(256), 0, stream, Fs,
-                       nsplit, nrows_pad, ghat, arow, logmode ? 1 : 0, W, F2part, nf);
+                       nsplit, nrows_pad, ghat, arow, logmode ? 1 : 0, W, F2part, nf, g_mf_skip);
     check_launch("k_mf_weights");
 }
 
@@ -344,15 +396,8 @@ void launch_mf_collect(const float* part, int nsplit, int64_t ld, int64_t v0, in
     if (v0 < 0 || v1 > ld || v1 < v0) throw std::runtime_error("mf_collect: voxel range outside [0, ld)");
     const int64_t n = (v1 - v0) * nf;
     hipLaunchKernelGGL(k_mf_collect, dim3(std::max<unsigned>(1, nb(n))), dim3(256), 0, stream, part, nsplit, ld, v0, v1,
-                       scale, D, F2part, nF2, F2out, nf);
+                       scale, D, F2part, nF2, F2out, nf, g_mf_skip);
     check_launch("k_mf_collect");
-}
-
-void launch_mf_init(float* X, const float* D0, const float* dinv, int64_t nvox, int64_t ld, int nused, int nf,
-                    hipStream_t stream) {
-    check_nf(nf, "mf_init");
-    hipLaunchKernelGGL(k_mf_init, dim3(nb((int64_t)nf * ld)), dim3(256), 0, stream, X, D0, dinv, nvox, ld, nused, nf);
-    check_launch("k_mf_init");
 }
 
 // The kernels below take nf from the state (set by k_mf_state_begin): nf = frames of the engine's batch.
@@ -367,14 +412,6 @@ void launch_mf_penalty(const int64_t* row_ptr, const int32_t* col, const float* 
 void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream) {
     hipLaunchKernelGGL(k_mf_decide, dim3(1), dim3(kMaxNF), 0, stream, st, F2);
     check_launch("k_mf_decide");
-}
-
-void launch_mf_init_warm(float* X, const double* x0, const double* norm, int64_t nvox, int64_t ld, int nused, int nf,
-                         hipStream_t stream) {
-    check_nf(nf, "mf_init_warm");
-    hipLaunchKernelGGL(k_mf_init_warm, dim3(nb((int64_t)nf * ld)), dim3(256), 0, stream, X, x0, norm, nvox, ld, nused,
-                       nf);
-    check_launch("k_mf_init_warm");
 }
 
 void launch_mf_update(float* X, const float* D, const float* O, const float* pen, float alpha, bool logmode,
@@ -395,7 +432,7 @@ void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, 
 
 void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStream_t stream) {
     if (n % 4 != 0) throw std::runtime_error("mf_split_x: length must be a multiple of 4");
-    hipLaunchKernelGGL(k_mf_split_x, dim3(std::max<unsigned>(1, nb(n / 4))), dim3(256), 0, stream, X, n / 4, hi, lo);
+    hipLaunchKernelGGL(k_mf_split_x, dim3(std::max<unsigned>(1, nb(n / 4))), dim3(256), 0, stream, X, n / 4, hi, lo, g_mf_skip);
     check_launch("k_mf_split_x");
 }
 
@@ -404,8 +441,52 @@ void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, b
     check_nf(nf, "mf_split_w");
     if (ldw > nrows_pad) throw std::runtime_error("mf_split_w: plane stride exceeds the padded rows");
     hipLaunchKernelGGL(k_mf_split_w, dim3((unsigned)((ldw + 63) / 64)), dim3(256), 0, stream, W, nrows_pad, nf, ldw,
-                       hi, lo);
+                       hi, lo, g_mf_skip);
     check_launch("k_mf_split_w");
+}
+
+void launch_mf_prep_slots(const double* gk, int64_t nrows, int64_t nrows_pad, const MfSlots& sl, const float* ray_length,
+                          float len_thres, float* ghat, float* arow, float* gpos, float* wo, int nf, hipStream_t stream) {
+    check_nf(nf, "mf_prep_slots");
+    if (sl.n <= 0) return;
+    hipLaunchKernelGGL(k_mf_prep_slots, dim3(nb((int64_t)sl.n * nrows_pad)), dim3(256), 0, stream, gk, nrows, nrows_pad,
+                       sl, ray_length, len_thres, ghat, arow, gpos, wo, nf);
+    check_launch("k_mf_prep_slots");
+}
+
+void launch_mf_init_slots_warm(float* X, const double* x0, const MfSlots& sl, int64_t nvox, int64_t ld,
+                               hipStream_t stream) {
+    if (sl.n <= 0) return;
+    hipLaunchKernelGGL(k_mf_init_slots_warm, dim3(nb((int64_t)sl.n * ld)), dim3(256), 0, stream, X, x0, sl, nvox, ld);
+    check_launch("k_mf_init_slots_warm");
+}
+
+void launch_mf_init_slots_scaled(float* X, const float* xs, double s_src, const MfSlots& sl, int64_t nvox, int64_t ld,
+                                 hipStream_t stream) {
+    if (sl.n <= 0) return;
+    hipLaunchKernelGGL(k_mf_init_slots_scaled, dim3(nb((int64_t)sl.n * ld)), dim3(256), 0, stream, X, xs, s_src, sl,
+                       nvox, ld);
+    check_launch("k_mf_init_slots_scaled");
+}
+
+void launch_mf_init_slots_cold(float* X, const float* D0, const float* dinv, const MfSlots& sl, int64_t nvox,
+                               int64_t ld, int nf, hipStream_t stream) {
+    if (sl.n <= 0) return;
+    hipLaunchKernelGGL(k_mf_init_slots_cold, dim3(nb((int64_t)sl.n * ld)), dim3(256), 0, stream, X, D0, dinv, sl, nvox,
+                       ld, nf);
+    check_launch("k_mf_init_slots_cold");
+}
+
+void launch_mf_copy_slots(float* O, const float* src, const MfSlots& sl, int64_t ld, int nf, hipStream_t stream) {
+    if (sl.n <= 0) return;
+    hipLaunchKernelGGL(k_mf_copy_slots, dim3(nb((int64_t)sl.n * ld)), dim3(256), 0, stream, O, src, sl, ld, nf);
+    check_launch("k_mf_copy_slots");
+}
+
+void launch_mf_slot_reset(MfState* st, const MfSlots& sl, hipStream_t stream) {
+    if (sl.n <= 0) return;
+    hipLaunchKernelGGL(k_mf_slot_reset, dim3(1), dim3(kMaxNF), 0, stream, st, sl);
+    check_launch("k_mf_slot_reset");
 }
 
 }  // namespace sart

@@ -58,6 +58,15 @@ struct alignas(16) MfState {
     unsigned long long flags;        // bit f: frame f produced a non-finite ||A x||^2
     double tol;
     unsigned long long rollback;     // bit f: frame f stopped at sweep >= 1 (its last finite iterate is in Xprev)
+    int32_t sweep0[kMfMaxFrames];    // sweep at which the slot's current frame started (continuous batching)
+};
+
+// Slots (re)filled with new frames between two sweeps of the multi-frame engine: passed by value.
+struct MfSlots {
+    int n;
+    int slot[kMfMaxFrames];
+    double norm[kMfMaxFrames];  // the frame's normalisation s = max(g) (1 if not positive)
+    double G[kMfMaxFrames];     // sum_{g>0} g^2 / s^2
 };
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -32,6 +32,8 @@ struct SolveInfo {
     double ms = 0.0;
     int sweeps = 0;           // sweeps executed on the device (iterations + the final decision sweep)
     double comm_ms = -1.0;    // GPU time inside the per-sweep all-reduces (EngineConfig::time_collectives; else -1)
+    int warm_from = -1;       // multi-frame time series: index of the frame whose solution started this one
+                              // (-1: the caller's x0, or cold)
 };
 
 // CSR over n rows (row_ptr int64, col int32, val fp32), from the reference's sorted-flat-index COO

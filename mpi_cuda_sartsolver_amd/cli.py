@@ -214,18 +214,22 @@ def run(cfg, intervals) -> int:
 
 
 def _run_batched(cfg, solver, image, frames, pool, writer, profile, rank, warm=None) -> None:
-    """--batch_frames N: N frames solved together on the matrix cores. Without --no_guess the batches form a
-    warm-started time series (every frame of batch k + 1 starts from batch k's last solution; the first batch
-    from the resumed solution, or cold); with --no_guess every frame cold-starts (reference main.cpp:127-139)."""
+    """--batch_frames N: N slots on the matrix cores with continuous batching (a finished frame's slot takes the
+    next frame between two sweeps), frames read in windows of 4 N. Without --no_guess the frames form a
+    warm-started time series (a window's first N frames start from the previous window's last solution or the
+    resumed one, later frames from the latest finished frame); with --no_guess every frame cold-starts
+    (reference main.cpp:127-139)."""
     import numpy as np
 
     idxs = list(frames)
     warm = None if cfg.no_guess else warm
-    for b0 in range(0, len(idxs), cfg.batch_frames):
-        chunk = idxs[b0: b0 + cfg.batch_frames]
+    window = 4 * cfg.batch_frames
+    for b0 in range(0, len(idxs), window):
+        chunk = idxs[b0: b0 + window]
         batch = np.stack(list(pool.map(image.frame, chunk)))
         t0 = time.perf_counter()
-        results = solver.solve_batch(batch, x0=warm)
+        results = solver.solve_batch(batch, x0=warm, chain=not cfg.no_guess)
+        first_warm = idxs[b0 - 1] if (b0 > 0 and warm is not None) else -1  # the window's x0, as a frame
         last = results[-1].solution
         warm = None if (cfg.no_guess or not np.all(np.isfinite(last))) else last
         ms = 1e3 * (time.perf_counter() - t0)
@@ -235,9 +239,11 @@ def _run_batched(cfg, solver, image, frames, pool, writer, profile, rank, warm=N
                            int(res.iterations))
                 print(f"Processed in: {ms / len(chunk)} ms", flush=True)
                 if profile:
+                    wf = chunk[res.warm_from] if res.warm_from >= 0 else first_warm
                     profile.write(json.dumps({"frame": i, "time": image.frame_time(i), "status": res.status,
                                               "iterations": res.iterations, "ms": ms / len(chunk),
-                                              "batch": len(chunk)}) + "\n")
+                                              "batch": cfg.batch_frames, "warm_from": wf if not cfg.no_guess else -1})
+                                  + "\n")
 
 
 if __name__ == "__main__":

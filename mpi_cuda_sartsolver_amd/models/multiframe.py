@@ -1,14 +1,16 @@
-"""Multi-frame SART: up to 64 independent frames solved together on the fp32 matrix cores.
+"""Multi-frame SART: up to 64 independent frames solved together on the matrix cores (fp32, or bf16 shards).
 
 The reference solves the time series strictly frame by frame (reference main.cpp:131-140), streaming
 the RTM twice per iteration per frame. For throughput on long time series (BASELINE.json config 5),
 frames can be batched: the forward and back projections become skinny GEMMs ``A.X`` / ``A^T.W`` with
 16, 32 or 64 right-hand sides (csrc/kernels/multiframe.hip, ``v_mfma_f32_16x16x4_f32`` on 1, 2 or 4
 column groups), reading A twice per iteration for the whole batch. Every frame keeps its own normalisation,
-saturation mask, convergence history and status; frames that converge are frozen while the others
-continue. Batches are cold-started (``--no_guess``), or warm-started as a time series: every frame of batch
-k + 1 starts from the solution of batch k's last frame (``solve_batch(g, x0=...)``; the reference warm-starts
-frame by frame, main.cpp:127-139). A frame whose iterate turns non-finite returns its last finite iterate.
+saturation mask, convergence history, iteration count and status. The batch's columns are slots with
+continuous batching: as soon as a frame finishes, its slot takes the next frame between two sweeps, so no
+sweep is spent on finished frames while frames wait. Frames are cold-started (``--no_guess``), or started as a
+time series: the first batch from ``x0``, every later frame from the solution of the latest frame finished
+before it (``SolveResult.warm_from``; the reference warm-starts frame by frame, main.cpp:127-139). A frame whose
+iterate turns non-finite returns its last finite iterate.
 
 The solver runs in the native engine (csrc/engine/multiframe.cpp, ``sart::MultiFrameEngine``; glue
 kernels in csrc/kernels/multiframe_glue.hip); this class is its Python face.
@@ -71,23 +73,24 @@ class MultiFrameSARTSolver:
         self.batch_width = int(self.engine.batch_frames)  # 16, 32 or 64 columns on the matrix cores
 
     def solve_batch(self, measurements, x0=None, chain: bool = False) -> List[SolveResult]:
-        """Frames [nframes, local pixels] in batches of ``self.batch``. ``x0`` (nvoxel, optional): warm start of
-        the first batch (None: cold). ``chain``: each later batch starts from the previous batch's last
-        solution (time series); otherwise later batches cold-start."""
-        g_all = np.asarray(measurements, dtype=np.float64)
+        """Frames [nframes, local pixels] through ``batch_width`` slots with continuous batching: a slot whose
+        frame finished takes the next frame between two sweeps. ``x0`` (nvoxel, optional): start value of the
+        first ``batch_width`` frames (None: cold). ``chain``: every later frame starts from the solution of the
+        latest frame finished before it (time series; ``SolveResult.warm_from``); otherwise later frames
+        cold-start."""
+        g_all = np.ascontiguousarray(np.asarray(measurements, dtype=np.float64))
         if g_all.ndim == 1:
             g_all = g_all[None]
         warm = None if x0 is None else _host_f64(x0)
+        x, infos = self.engine.solve_batch(g_all, warm, bool(chain))
         out: List[SolveResult] = []
-        for b0 in range(0, g_all.shape[0], self.batch):
-            x, infos = self.engine.solve_batch(np.ascontiguousarray(g_all[b0: b0 + self.batch]), warm)
-            for f, info in enumerate(infos):
-                status = SUCCESS if info["status"] == SUCCESS else MAX_ITERATIONS_EXCEEDED
-                out.append(SolveResult(solution=x[f], status=status, iterations=int(info["iterations"]),
-                                       convergence=float(info["convergence"]), used_fused=False,
-                                       elapsed_ms=float(info["ms"]), nonfinite=bool(info["nonfinite"])))
-            last = x[len(infos) - 1]
-            warm = last if (chain and np.all(np.isfinite(last))) else None
+        for f, info in enumerate(infos):
+            status = SUCCESS if info["status"] == SUCCESS else MAX_ITERATIONS_EXCEEDED
+            r = SolveResult(solution=x[f], status=status, iterations=int(info["iterations"]),
+                            convergence=float(info["convergence"]), used_fused=False,
+                            elapsed_ms=float(info["ms"]), nonfinite=bool(info["nonfinite"]))
+            r.warm_from = int(info["warm_from"])
+            out.append(r)
         return out
 
     def solve(self, measurement, solution=None) -> SolveResult:

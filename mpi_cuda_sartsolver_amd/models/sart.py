@@ -85,6 +85,7 @@ class SolveResult:
     fallbacks: int = 0      # persistent-sweep timeouts recovered in this solve (identical on every rank)
     fused_variant: int = -1  # fused sweep variant that produced the result (-1: two-pass kernels)
     nonfinite: bool = False  # stopped by the NaN/Inf guard: ``solution`` is the last finite iterate
+    warm_from: int = -1      # multi-frame time series: frame whose solution started this one (-1: x0 / cold)
 
 
 def _host_f64(v) -> np.ndarray:

@@ -38,8 +38,9 @@ def test_multiframe_vs_oracle(log, nframes, batch):
 
 @pytest.mark.parametrize("log", [False, True])
 def test_multiframe_warm_chain(log):
-    """Time-series warm start: batch 0 starts from x0, batch k + 1 from batch k's last solution; each frame
-    matches the oracle warm-started from the same vector."""
+    """Time series with continuous batching: the first batch starts from x0, every later frame from the latest
+    frame finished before it (warm_from); each frame matches the oracle started from the same vector. Frames
+    converge after different iteration counts, so slots are refilled at different sweeps."""
     from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
     from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
     from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
@@ -51,7 +52,8 @@ def test_multiframe_warm_chain(log):
     P, V, nframes, batch = 600, 1000, 40, 16
     A = rng.random((P, V), dtype=np.float32)
     base = rng.random(V) + 0.1
-    X = base[None] * (1.0 + 0.02 * rng.random((nframes, V)))  # a slowly varying series
+    # a varying series: some frames close to their predecessor, some far (different iteration counts)
+    X = base[None] * (1.0 + rng.choice([0.01, 0.3], size=(nframes, 1)) * rng.random((nframes, V)))
     G = X @ A.T.astype(np.float64)
     L = LaplacianCSR.grid_3d(10, 10, 10, device=dev)
     kw = dict(max_iterations=60, conv_tolerance=1e-5, beta_laplace=1e-3)
@@ -59,15 +61,17 @@ def test_multiframe_warm_chain(log):
                              batch=batch)
     x0 = base * 1.5
     res = s.solve_batch(G, x0=x0, chain=True)
-    prev = x0
-    for b0 in range(0, nframes, batch):
-        b1 = min(nframes, b0 + batch)
-        for f in range(b0, b1):
-            x, st, it = sart_gpu_semantics(A, G[f], L, logarithmic=log, x_prev=prev, **kw)
-            assert res[f].status == st and abs(res[f].iterations - it) <= 2, (f, res[f].iterations, it)
-            assert np.linalg.norm(res[f].solution - x) / np.linalg.norm(x) < 3e-3
-        prev = res[b1 - 1].solution
-    # without chain, a later batch cold-starts even when x0 is given
+    assert all(res[f].warm_from == -1 for f in range(batch))
+    assert all(0 <= res[f].warm_from < f for f in range(batch, nframes))
+    assert len({res[f].iterations for f in range(nframes)}) > 1  # slots really refill at different sweeps
+    for f in range(nframes):
+        wf = res[f].warm_from
+        prev = x0 if wf < 0 else res[wf].solution
+        x, st, it = sart_gpu_semantics(A, G[f], L, logarithmic=log, x_prev=prev, **kw)
+        assert res[f].status == st and abs(res[f].iterations - it) <= 2, (f, res[f].iterations, it)
+        assert np.linalg.norm(res[f].solution - x) / np.linalg.norm(x) < 3e-3
+    # without chain, every frame after the first batch cold-starts even when x0 is given
     cold = s.solve_batch(G[:20], x0=None)
+    assert all(r.warm_from == -1 for r in cold)
     x, st, it = sart_gpu_semantics(A, G[17], L, logarithmic=log, **kw)
     assert cold[17].status == st and np.linalg.norm(cold[17].solution - x) / np.linalg.norm(x) < 3e-3
