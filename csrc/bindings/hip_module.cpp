@@ -126,9 +126,10 @@ static void bind_engine(py::module_& m) {
         .def_readonly("variant", &sart::FusedGeometry::variant)
         .def_readonly("T", &sart::FusedGeometry::T)
         .def_readonly("cpl", &sart::FusedGeometry::cpl)
+        .def_readonly("kw", &sart::FusedGeometry::kw)
         .def("valid", &sart::FusedGeometry::valid);
     m.def("fused_geometry", &sart::fused_geometry, py::arg("ld"), py::arg("num_cus"), py::arg("variant") = 6,
-          py::arg("rows_per_tile") = 0);
+          py::arg("rows_per_tile") = 0, py::arg("narrow_slabs") = true);
     m.def("fused_geometry_bf16_wide", &sart::fused_geometry_bf16_wide, py::arg("ld"), py::arg("num_cus"));
     m.def("fused_fold_tiles", &sart::fused_fold_tiles, py::arg("geometry"), py::arg("nrows_pad"));
     m.def("fused_chain_plan", [](const sart::FusedGeometry& g, int64_t nrows_pad, bool split) {
@@ -136,7 +137,8 @@ static void bind_engine(py::module_& m) {
         return py::make_tuple(p.chain_tiles, p.blocks);
     }, py::arg("geometry"), py::arg("nrows_pad"), py::arg("split_schedule"));
     m.def("fused_split_schedule", &sart::fused_split_schedule, py::arg("T"), py::arg("bf16"));
-    m.def("choose_ld", &sart::choose_ld, py::arg("nvoxel"), py::arg("max_waste") = 0.10);
+    m.def("choose_ld", &sart::choose_ld, py::arg("nvoxel"), py::arg("max_waste") = 0.10,
+          py::arg("narrow_slabs") = true);
 
     py::class_<sart::EngineConfig>(m, "EngineConfig")
         .def(py::init<>())

@@ -81,7 +81,7 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
     if (ncols == 0) ncols = in.nvoxel - col0;
     sh->nrows = (int64_t)nrows;
     sh->nvoxel = (int64_t)ncols;
-    sh->ld = choose_ld(sh->nvoxel);
+    sh->ld = choose_ld(sh->nvoxel, 0.10, !bf16);  // bf16 shards keep the 8-KiB slabs of their tiles
     sh->nrows_pad = (sh->nrows + 63) / 64 * 64;
     const size_t bytes = (size_t)sh->nrows_pad * sh->ld * (bf16 ? sizeof(bf16_t) : sizeof(float));
     hip_ok(hipMalloc(&sh->A, bytes), "hipMalloc(RTM shard)");

@@ -8,46 +8,55 @@ namespace sart {
 
 namespace {
 
-// Variant 6 geometry for a padded width `ld` at T rows per tile: J = ld / slab workgroups per row (slab =
-// 8192 / T columns: the four compute waves cover T rows x 4 / T sub-slabs of 2048 columns), G = per_xcd / J
-// row groups per XCD (the XCD's remaining per_xcd - G * J CUs stay idle). cost = slab / G is the time per
-// matrix row relative to the other candidates (each CU streams slab columns of P / (8 G) rows).
+// Variant 6 geometry for a padded width `ld` at T rows per tile and kw lane-vectors per lane: J = ld / slab
+// workgroups per row (slab = 1024 kw / T columns: the four compute waves cover T rows x 4 / T sub-slabs of
+// 256 kw columns), G = per_xcd / J row groups per XCD (the XCD's remaining per_xcd - G * J CUs stay idle).
+// cost = slab / G is the time per matrix row relative to the other candidates (each CU streams slab columns
+// of P / (8 G) rows).
 struct V6Candidate {
-    int T = 0, J = 0, G = 0;
+    int T = 0, J = 0, G = 0, kw = 8;
     double cost = 0.0;
 };
 
-V6Candidate v6_candidate(int64_t ld, int T, int per_xcd) {
+// kw < 8 streams fewer bytes per pipeline step for the same per-step exchange work: per CU, kw 7 measured
+// 26.4 GB/s and kw 6 23.2 GB/s against 26.6 at kw 8 (bench --nvox 200000 / 150000 / 65536,
+// profiles/bench_r2_widths_kw.jsonl)
+constexpr double narrow_slab_penalty(int kw) { return kw == 8 ? 1.0 : (kw == 7 ? 1.02 : 1.15); }
+
+V6Candidate v6_candidate(int64_t ld, int T, int kw, int per_xcd) {
     V6Candidate c;
-    const int64_t slab = 8192 / T;
+    const int64_t slab = 1024 * (int64_t)kw / T;
     if (ld % slab != 0) return c;
     const int64_t J = ld / slab;
     if (J < 1 || J > per_xcd || J * T > 256 /* exchange gather registers */) return c;
-    c.T = T, c.J = (int)J, c.G = per_xcd / (int)J;
+    c.T = T, c.J = (int)J, c.G = per_xcd / (int)J, c.kw = kw;
     // T = 2 (schedule 4) measured 4-10 % slower per byte than T = 1 (schedule 5) at equal slab / G
     // (131072 / 106496 columns, profiles/probe_r2_t1_sched5.jsonl); T = 4 and T = 1 tie at 65536
-    c.cost = (double)slab / c.G * (T == 2 ? 1.08 : 1.0);
+    c.cost = (double)slab / c.G * (T == 2 ? 1.08 : 1.0) * narrow_slab_penalty(kw);
     return c;
 }
 
 }  // namespace
 
-int64_t choose_ld(int64_t nvoxel, double max_waste) {
-    // Widths the fused sweep (variant 6) can split into whole slabs, J <= 32 per row group: at each T the
+int64_t choose_ld(int64_t nvoxel, double max_waste, bool narrow_slabs) {
+    // Widths the fused sweep (variant 6) can split into whole slabs, J <= 32 per row group: at each (T, kw) the
     // smallest multiple of the slab covering nvoxel. Take the one with the lowest time per row (ties: less
-    // padding, then the larger T, measured fastest at equal cost), if it pads by at most max_waste.
+    // padding, then the larger T and kw, measured fastest at equal cost), if it pads by at most max_waste.
     if (nvoxel >= 1024) {
         constexpr int kPerXcd = 32;  // MI355X: 256 CUs in 8 XCDs
         int64_t best_ld = 0;
         double best_cost = 0.0;
-        for (const int T : {4, 2, 1}) {
-            const int64_t slab = 8192 / T;
-            const int64_t ld = (nvoxel + slab - 1) / slab * slab;
-            const V6Candidate c = v6_candidate(ld, T, kPerXcd);
-            if (c.G == 0 || (double)(ld - nvoxel) > max_waste * (double)nvoxel) continue;
-            if (best_ld == 0 || c.cost < best_cost || (c.cost == best_cost && ld < best_ld)) {
-                best_ld = ld;
-                best_cost = c.cost;
+        for (const int kw : {8, 7, 6}) {
+            if (kw != 8 && !narrow_slabs) continue;
+            for (const int T : {4, 2, 1}) {
+                const int64_t slab = 1024 * (int64_t)kw / T;
+                const int64_t ld = (nvoxel + slab - 1) / slab * slab;
+                const V6Candidate c = v6_candidate(ld, T, kw, kPerXcd);
+                if (c.G == 0 || (double)(ld - nvoxel) > max_waste * (double)nvoxel) continue;
+                if (best_ld == 0 || c.cost < best_cost || (c.cost == best_cost && ld < best_ld)) {
+                    best_ld = ld;
+                    best_cost = c.cost;
+                }
             }
         }
         if (best_ld) return best_ld;
@@ -59,25 +68,30 @@ int64_t choose_ld(int64_t nvoxel, double max_waste) {
     return (n + 63) / 64 * 64;
 }
 
-FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_tile) {
+FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_tile, bool narrow_slabs) {
     FusedGeometry g;
     if (rows_per_tile <= 0) {
         const char* e = std::getenv("SART_FUSED_T");
         rows_per_tile = (e && *e) ? std::atoi(e) : 0;
     }
+    if (const char* e = std::getenv("SART_FUSED_KW"); e && *e && std::atoi(e) == 8) narrow_slabs = false;
     if (variant == 6 && num_cus % 8 == 0) {
-        // Rows per tile: the requested T, else the candidate with the lowest time per row (ties: the larger T;
-        // T = 4 at ld = 64k, 2 at 128k, 1 at 256k measured 6.5-6.9 TB/s, against 4.0-4.7 TB/s for variant 3,
-        // profiles/probe_r1_fused_T.jsonl). Widths whose J does not divide the XCD's CU count run
-        // G = per_xcd / J row groups per XCD and leave the remaining CUs idle.
+        // Rows per tile and slab: the requested T, else the candidate with the lowest time per row (ties: the
+        // larger T and kw; T = 4 at ld = 64k, 2 at 128k, 1 at 256k measured 6.5-6.9 TB/s, against 4.0-4.7 TB/s
+        // for variant 3, profiles/probe_r1_fused_T.jsonl). Widths whose J does not divide the XCD's CU count
+        // run G = per_xcd / J row groups per XCD and leave the remaining CUs idle.
         V6Candidate best;
-        for (const int T : {4, 2, 1}) {
-            if (rows_per_tile > 0 && T != rows_per_tile) continue;
-            const V6Candidate c = v6_candidate(ld, T, num_cus / 8);
-            if (c.G > 0 && (best.G == 0 || c.cost < best.cost)) best = c;
+        for (const int kw : {8, 7, 6}) {
+            if (kw != 8 && !narrow_slabs) continue;
+            for (const int T : {4, 2, 1}) {
+                if (rows_per_tile > 0 && T != rows_per_tile) continue;
+                const V6Candidate c = v6_candidate(ld, T, kw, num_cus / 8);
+                if (c.G > 0 && (best.G == 0 || c.cost < best.cost)) best = c;
+            }
         }
         if (best.G > 0) {
             g.K = best.T, g.J = best.J, g.I = 8 * best.G, g.grid = g.I * g.J, g.variant = 6, g.T = best.T;
+            g.kw = best.kw;
             return g;
         }
     }

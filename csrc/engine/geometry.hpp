@@ -14,17 +14,19 @@ struct FusedGeometry {
     int variant = -1; // 6 (XCD-local row groups), 3 (generic fallback), -1: no fused path for this width
     int T = 0;        // rows per tile
     int cpl = 4;      // variant 6: columns per lane per k-slot (8: wide bf16 tiles, slab 16384 / T)
+    int kw = 8;       // variant 6 fp32: lane-vectors per lane per row (slab 1024 kw / T; 7 / 6 fill more CUs)
     bool valid() const { return variant >= 0; }
 };
 
 // Padded row length of a dense shard: the variant 6 width (J slabs of 8192 / T columns, J <= 32) with the
 // lowest estimated time per row when that wastes at most max_waste of the row, else a multiple of 8192
 // (variant 3), else the next multiple of 64 floats (256 B rows).
-int64_t choose_ld(int64_t nvoxel, double max_waste = 0.10);
+// narrow_slabs: also consider fp32 slabs of 7 / 6 KiB columns (kw 7 / 6); bf16 shards keep kw = 8.
+int64_t choose_ld(int64_t nvoxel, double max_waste = 0.10, bool narrow_slabs = true);
 
 // Geometry for `variant` (6 default, or 3), falling back to variant 3 when variant 6 cannot split the
 // width. rows_per_tile = 0: SART_FUSED_T or the lowest-cost T.
-FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_tile);
+FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_tile, bool narrow_slabs = true);
 // Variant 6 geometry of the wide bf16 tiles (16-byte loads of 8 bf16 per lane: T = 4 with slab 4096 columns, or
 // T = 2 with slab 8192); invalid when the width does not split into J <= 32 such slabs.
 FusedGeometry fused_geometry_bf16_wide(int64_t ld, int num_cus);

@@ -376,14 +376,16 @@ __device__ __forceinline__ void split_pair(float a, float b, uint32_t key, unsig
 // Schedules with a separate publisher wave (the split exchange)
 constexpr bool sched_split(int sched) { return sched == 4 || sched == 5 || sched == 6; }
 
-template <bool LOG, bool XL, bool DIAG, int T, int SCHED, typename AT = float, int CPL = 4>
+template <bool LOG, bool XL, bool DIAG, int T, int SCHED, typename AT = float, int CPL = 4, int KW = 8>
 __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
     const AT* __restrict__ A, int64_t ld, int64_t nrows, int64_t nrows_pad, const float* __restrict__ x,
     const float* __restrict__ ghat, const float* __restrict__ arow, float* __restrict__ partial,
     double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg,
     unsigned* __restrict__ xcnt, int64_t chain_tiles) {
     static_assert(T == 1 || T == 2 || T == 4, "rows per tile");
-    constexpr int KW = 8;        // float4 per lane per row: one wave covers 2048 columns
+    // KW: lane-vectors per lane per row (8: one wave covers 2048 fp32 columns; 7 / 6 give slabs of 7 / 6 KiB
+    // columns, so widths whose 8-KiB slab count does not fit an XCD's 32 CUs still use most of them)
+    static_assert(KW >= 6 && KW <= 8, "lane-vectors per lane");
     constexpr int WPR = 4 / T;   // compute waves per row (each on its own 2048-column sub-slab)
     constexpr int D = (SCHED == 1 || SCHED == 2 || SCHED == 4 || SCHED == 6) ? 1 : 0;  // steps a reduced tile stays in VGPRs
     constexpr bool XS_LDS = (SCHED >= 1 && SCHED <= 4) || SCHED == 6;  // x slab in LDS instead of VGPRs
@@ -698,8 +700,9 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
         float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld);
         if constexpr (H == 1) out += slab4 + lane;  // (fp32 / narrow bf16: the original addressing)
 #pragma unroll
-        for (int i = 0; i < 2 * WPR * H; ++i) {  // q = (sub * KW + k) * H + h, spread over the four waves
+        for (int i = 0; i < (WPR * KW * H + 3) / 4; ++i) {  // q = (sub * KW + k) * H + h over the four waves
             const int q = wave + 4 * i;
+            if (q >= WPR * KW * H) break;
             const int sub = q / (KW * H), k = (q / H) % KW, h = q % H;
             float4 v = s_ring[q * 64 + lane];  // wave (row 0, sub)
 #pragma unroll
@@ -862,9 +865,9 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     }
 }
 
-constexpr size_t rows_lds_bytes(int T, int sched, int H = 1) {
-    return (sched == 6 ? 3 : 4) /*NL x 32 KB*/ * 4 * 8 * 64 * sizeof(float4) +
-           (((sched >= 1 && sched <= 4) || sched == 6) ? (4 / T) * 8 * 64 * H * sizeof(float4) : 0) +  // x slab
+constexpr size_t rows_lds_bytes(int T, int sched, int H = 1, int KW = 8) {
+    return (sched == 6 ? 3 : 4) /*NL x 4 waves x KW x 64 lanes x 16 B*/ * 4 * KW * 64 * sizeof(float4) +
+           (((sched >= 1 && sched <= 4) || sched == 6) ? (4 / T) * KW * 64 * H * sizeof(float4) : 0) +  // x slab
            (8 * 4 * 3 + 8 + 4) * sizeof(float);
 }
 static_assert(rows_lds_bytes(4, 4, 2) <= 160 * 1024, "wide bf16 tiles: T = 4 fits the LDS");
@@ -922,18 +925,18 @@ static void launch_lds(bool logmode, dim3 grid, hipStream_t stream, const float*
                            nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg);
 }
 
-template <bool LG, bool X, bool D, int T, int SC, typename AT = float, int CPL = 4>
+template <bool LG, bool X, bool D, int T, int SC, typename AT = float, int CPL = 4, int KW = 8>
 static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                           const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                           uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, int64_t chain_tiles) {
-    constexpr size_t lds = rows_lds_bytes(T, SC, CPL / 4);
+    constexpr size_t lds = rows_lds_bytes(T, SC, CPL / 4, KW);
     static bool configured = false;
     if (!configured) {
-        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T, SC, AT, CPL>),
+        hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T, SC, AT, CPL, KW>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "hipFuncSetAttribute");
         configured = true;
     }
-    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC, AT, CPL>), grid,
+    hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC, AT, CPL, KW>), grid,
                        dim3(sched_split(SC) ? kFusedThreads + 64 : kFusedThreads), lds, stream, A, ld, nrows,
                        nrows_pad, x,
                        ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt, chain_tiles);
@@ -943,7 +946,7 @@ template <int T>
 static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
                         int64_t nrows_pad, const float* x_, const float* ghat, const float* arow, float* partial,
                         double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt,
-                        int64_t chain_tiles) {
+                        int64_t chain_tiles, int kw) {
     const bool diag = (g_fused_dbg & 2) != 0;  // instrumented build only when asked (timing diagnostics)
     // g_fused_sched: pipeline schedule (k_fused_sweep_rows SCHED); schedules 1-4 hold the x slab in LDS,
     // which has room for it only when T >= 2. T = 1 runs schedule 5 (the split exchange with the x slab in
@@ -967,6 +970,20 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
     auto by_log = [&](auto d, auto sc) {
         if (logmode) go(TT{}, d, sc); else go(FF{}, d, sc);
     };
+    if (kw != 8) {  // narrower slabs: the default schedules only (4 at T >= 2, 5 at T = 1), no diagnostics
+        auto go_kw = [&](auto lg, auto k) {
+            using SD = std::integral_constant<int, (T >= 2 ? 4 : 5)>;
+            launch_rows_t<decltype(lg)::value, true, false, T, SD::value, float, 4, decltype(k)::value>(
+                grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
+                chain_tiles);
+        };
+        auto by_kw = [&](auto lg) {
+            if (kw == 7) go_kw(lg, std::integral_constant<int, 7>{});
+            else go_kw(lg, std::integral_constant<int, 6>{});
+        };
+        if (logmode) by_kw(TT{}); else by_kw(FF{});
+        return;
+    }
     if (diag) {
         if (sched == 2) by_log(TT{}, S2{});
         else if (sched == 4) by_log(TT{}, S4{});
@@ -1005,7 +1022,7 @@ int fused_tile_rows(int K, int variant) {
 void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows,
                         int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
                         double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt,
-                        hipStream_t stream, int64_t chain_tiles) {
+                        hipStream_t stream, int64_t chain_tiles, int kw) {
     if (variant != 3 && variant != 6) throw std::runtime_error("fused_sweep: variant must be 6 or 3");
     const dim3 grid((unsigned)(I * J));
     if (variant == 6) {
@@ -1013,17 +1030,18 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
         if (T >= 2 && chain_tiles % kChainAlign != 0)
             throw std::runtime_error("fused_sweep v6: segment length must be a multiple of 140 tiles");
         if (T != 1 && T != 2 && T != 4) throw std::runtime_error("fused_sweep v6: rows per tile (K) must be 1, 2 or 4");
-        const int64_t slab = 8192 / T;  // columns per workgroup
+        if (kw < 6 || kw > 8) throw std::runtime_error("fused_sweep v6: lane-vectors per lane (kw) must be 6, 7 or 8");
+        const int64_t slab = 1024 * kw / T;  // columns per workgroup
         if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep v6: ld must equal J * slab");
         if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v6: padded rows must be a multiple of 4");
         if (J * T > kRowsGather) throw std::runtime_error("fused_sweep v6: J * T > 256");
         if (xcnt == nullptr || I % 8 != 0) throw std::runtime_error("fused_sweep v6: needs the per-XCD ticket counters and I % 8 == 0");
         if (T == 1) launch_rows<1>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
-                        chain_tiles);
+                        chain_tiles, kw);
         else if (T == 2) launch_rows<2>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
-                        chain_tiles);
+                        chain_tiles, kw);
         else launch_rows<4>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
-                        chain_tiles);
+                        chain_tiles, kw);
         check_launch("k_fused_sweep_rows");
         return;
     }

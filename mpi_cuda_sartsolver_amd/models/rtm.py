@@ -28,17 +28,19 @@ class FusedGeometry:
     grid: int     # I * J persistent workgroups (<= number of CUs)
     variant: int  # register-ring configuration (csrc/kernels/fused_sweep.hip)
     T: int        # rows per tile
+    kw: int = 8   # variant 6 fp32: lane-vectors per lane per row (slab 1024 kw / T columns)
 
 
-def choose_ld(nvoxel: int, max_waste: float = 0.10) -> int:
+def choose_ld(nvoxel: int, max_waste: float = 0.10, storage: str = "fp32") -> int:
     """Padded row length (native ``sart::choose_ld``, csrc/engine/geometry.cpp: the single source of truth
     for the engine, both drivers and this package): the variant 6 width with the lowest estimated time per
-    row, else a multiple of 8192 (variant 3), else the next multiple of 64."""
-    return int(hip().choose_ld(int(nvoxel), float(max_waste)))
+    row, else a multiple of 8192 (variant 3), else the next multiple of 64. fp32 shards also consider slabs of
+    7 / 6 KiB columns (kw 7 / 6), bf16 shards keep the 8-KiB slabs of their tiles."""
+    return int(hip().choose_ld(int(nvoxel), float(max_waste), storage == "fp32"))
 
 
-def fused_geometry(ld: int, num_cus: int, variant: int = 6, rows_per_tile: Optional[int] = None
-                   ) -> Optional[FusedGeometry]:
+def fused_geometry(ld: int, num_cus: int, variant: int = 6, rows_per_tile: Optional[int] = None,
+                   narrow_slabs: bool = True) -> Optional[FusedGeometry]:
     """Persistent-grid geometry of the fused sweep (native ``sart::fused_geometry``).
 
     variant 6 (default): XCD-local row groups (L2 hand-offs); the four compute waves of a workgroup
@@ -47,10 +49,10 @@ def fused_geometry(ld: int, num_cus: int, variant: int = 6, rows_per_tile: Optio
     SART_FUSED_T, else the T with the lowest time per row). Variant 3: slabs of 1024*K columns, K chosen
     for <= 32 slabs (the fallback). None: no fused path.
     """
-    g = hip().fused_geometry(int(ld), int(num_cus), int(variant), int(rows_per_tile or 0))
+    g = hip().fused_geometry(int(ld), int(num_cus), int(variant), int(rows_per_tile or 0), bool(narrow_slabs))
     if not g.valid():
         return None
-    return FusedGeometry(K=g.K, J=g.J, I=g.I, grid=g.grid, variant=g.variant, T=g.T)
+    return FusedGeometry(K=g.K, J=g.J, I=g.I, grid=g.grid, variant=g.variant, T=g.T, kw=g.kw)
 
 
 class DenseRTM:
@@ -71,7 +73,7 @@ class DenseRTM:
         if self.col_offset < 0 or self.col_offset + self.nvoxel > self.nvoxel_total:
             raise ValueError("column shard outside [0, nvoxel_total)")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
-        self.ld = int(ld) if ld is not None else choose_ld(self.nvoxel)
+        self.ld = int(ld) if ld is not None else choose_ld(self.nvoxel, storage=storage)
         if self.ld % 64 or self.ld < self.nvoxel:
             raise ValueError("ld must be a multiple of 64 and >= nvoxel")
         self.nrows_pad = round_up(self.npixel, row_align)

@@ -13,8 +13,8 @@ CUS = 256  # MI355X: 8 XCDs x 32 CUs
 
 
 def _check_v6(ld, g):
-    assert g is not None and g.variant == 6
-    slab = 8192 // g.T
+    assert g is not None and g.variant == 6 and g.kw in (6, 7, 8)
+    slab = 1024 * g.kw // g.T
     assert g.T in (1, 2, 4) and ld % slab == 0 and ld // slab == g.J
     assert g.J <= CUS // 8 and g.J * g.T <= 256
     assert g.I % 8 == 0 and g.grid == g.I * g.J <= CUS
@@ -27,34 +27,48 @@ def test_every_width_gets_variant6(nvox):
     ld = rtm.choose_ld(nvox)
     assert nvox <= ld <= 1.10 * nvox
     _check_v6(ld, rtm.fused_geometry(ld, CUS, 6))
+    # bf16 shards keep the 8-KiB slabs (their tiles are 8 or 16 bytes of bf16 per lane)
+    ldb = rtm.choose_ld(nvox, storage="bf16")
+    gb = rtm.fused_geometry(ldb, CUS, 6, narrow_slabs=False)
+    assert nvox <= ldb <= 1.10 * nvox and gb.kw == 8
+    _check_v6(ldb, gb)
 
 
 def test_width_sweep_variant6_and_waste():
+    used = []
     for nvox in range(20480, 262145, 997):
         ld = rtm.choose_ld(nvox)
         assert ld % 64 == 0 and nvox <= ld <= 1.10 * nvox, nvox
-        _check_v6(ld, rtm.fused_geometry(ld, CUS, 6))
+        g = rtm.fused_geometry(ld, CUS, 6)
+        _check_v6(ld, g)
+        used.append(g.grid / CUS)
+    assert min(used) >= 0.65 and sum(used) / len(used) >= 0.9  # CUs in use across the sweep of widths (measured 0.69, 0.92)
 
 
-@pytest.mark.parametrize("ld,T,J,I", [(65536, 4, 32, 8), (131072, 1, 16, 16), (262144, 1, 32, 8),
-                                      (61440, 4, 30, 8), (16384, 4, 8, 32), (106496, 1, 13, 16)])
-def test_production_geometries(ld, T, J, I):
+@pytest.mark.parametrize("ld,T,kw,J,I", [(65536, 4, 8, 32, 8), (131072, 1, 8, 16, 16), (262144, 1, 8, 32, 8),
+                                         (61440, 4, 8, 30, 8), (16384, 4, 8, 8, 32), (106496, 1, 8, 13, 16),
+                                         (100352, 1, 7, 14, 16), (200704, 1, 7, 28, 8), (71680, 1, 7, 10, 24),
+                                         (153600, 1, 6, 25, 8), (229376, 1, 7, 32, 8)])
+def test_production_geometries(ld, T, kw, J, I):
     g = rtm.fused_geometry(ld, CUS, 6)
-    assert (g.T, g.J, g.I) == (T, J, I)
+    assert (g.T, g.kw, g.J, g.I) == (T, kw, J, I)
 
 
 def test_lowest_cost_rows_per_tile():
-    # 70000 columns: T = 2 needs J = 18 (one group per XCD, 18 of 32 CUs); T = 1 gives J = 9 and three
-    # groups per XCD (27 CUs), a lower time per row
+    # 70000 columns with 8-KiB slabs: T = 2 needs J = 18 (one group per XCD, 18 of 32 CUs); T = 1 gives J = 9
+    # and three groups per XCD (27 CUs), a lower time per row. 7-KiB slabs: J = 10, three groups (30 CUs).
+    ld = rtm.choose_ld(70000, storage="bf16")
+    g = rtm.fused_geometry(ld, CUS, 6, narrow_slabs=False)
+    assert (ld, g.T, g.J, g.I) == (73728, 1, 9, 24)
     ld = rtm.choose_ld(70000)
     g = rtm.fused_geometry(ld, CUS, 6)
-    assert (ld, g.T, g.J, g.I) == (73728, 1, 9, 24)
+    assert (ld, g.T, g.kw, g.J, g.I) == (71680, 1, 7, 10, 24)
 
 
 def test_t2_penalty_prefers_t1():
     # 100000 columns: T = 2 at ld 102400 (J = 25, one group per XCD) against T = 1 at ld 106496 (J = 13, two
     # groups per XCD): equal slab / G, T = 2 measured slower per byte (profiles/probe_r2_t1_sched5.jsonl)
-    assert rtm.choose_ld(100000) == 106496
+    assert rtm.choose_ld(100000, storage="bf16") == 106496
     g2 = rtm.fused_geometry(131072, CUS, 6, 2)
     assert (g2.T, g2.J, g2.I) == (2, 32, 8)  # still available when forced
 

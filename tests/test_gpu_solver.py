@@ -121,8 +121,11 @@ def test_ragged_shapes_fallback(dev):
     from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
     from mpi_cuda_sartsolver_amd.utils.synthetic import host_problem
 
-    A, g, _ = host_problem(333, 1500, seed=8)
+    # 1100 voxels: no slab width (1024 kw / T, kw 6..8) pads it by <= 10 %, so the fused sweep is unavailable and
+    # the two-pass kernels run (1500 voxels would take a 1536-column kw 6 slab)
+    A, g, _ = host_problem(333, 1100, seed=8)
     s = _solver(dev, A, True, max_iterations=20, conv_tolerance=0.0)
+    assert not s.use_fused
     r = s.solve(g)
     _check(r.solution, A, g, max_iterations=20)
 
@@ -212,7 +215,7 @@ def test_fused_v6_schedules(dev, T, sched, log):
 # groups per XCD), on 4096-row shards against the device fp64 oracle (models/oracle.py). The two-pass kernels
 # (oracle-validated above) set the fp32 error scale: the fused sweep must be no worse than 1.25x of it.
 PROD = [(65536, 4, 32, 8), (131072, 1, 16, 16), (262144, 1, 32, 8),
-        (60000, 4, 30, 8), (100000, 1, 13, 16), (200000, 1, 25, 8), (70000, 1, 9, 24)]
+        (60000, 4, 30, 8), (100000, 1, 14, 16), (200000, 1, 28, 8), (70000, 1, 10, 24), (150000, 1, 25, 8)]
 
 
 @pytest.mark.parametrize("nvox,T,J,I", PROD)
@@ -278,7 +281,7 @@ def test_segmented_chains(dev, monkeypatch, storage, nvox, T, log):
 
 
 @pytest.mark.parametrize("rows,nvox,T,J,I", [(1024, 65536, 4, 32, 8), (512, 131072, 1, 16, 16),
-                                             (256, 262144, 1, 32, 8), (512, 100000, 1, 13, 16)])
+                                             (256, 262144, 1, 32, 8), (512, 100000, 1, 14, 16)])
 @pytest.mark.parametrize("log", [False, True])
 def test_production_geometry_vs_oracle(dev, rows, nvox, T, J, I, log):
     """The production grids against the host fp64 oracle and the fp32 emulation (fewer rows)."""

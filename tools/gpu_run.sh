@@ -33,6 +33,8 @@ for step in "$@"; do
     presets) run bench_512kx256k 600 python bench.py --config 512kx256k --steps 3 --warmup 1 &&
              run bench_2tb 900 python bench.py --config 2tb --steps 2 --warmup 1 &&
              run bench_256k 900 python bench.py --config 256k --steps 2 --warmup 1 ;;
+    series) run series_fp32 600 python tools/series_bench.py --tol ${SERIES_TOL:-1e-8} &&
+            run series_bf16 600 python tools/series_bench.py --dtype bf16 --batch 32 --tol ${SERIES_TOL:-1e-8} ;;
     probemfb) run probe_mfb16 900 python tools/probe_mf_b16.py ;;
     probemfbv) PROBE_DEPTH=2,3 PROBE_FWD="2,2,lds;4,2,lds" run probe_mfb_bwd 900 python tools/probe_mf_b16.py ;;
     probemfbl) PROBE_BWD=0 PROBE_DEPTH=2,3 PROBE_FWD="4,2;8,1;4,1,lds;4,2,lds;8,1,lds;2,2,lds" \
@@ -102,7 +104,8 @@ for step in "$@"; do
               run bench_w200000 300 python bench.py --steps 3 --warmup 1 --nvox 200000 &&
               SART_FUSED_FOLD=0 run bench_w200000_nofold 300 python bench.py --steps 3 --warmup 1 --nvox 200000 ;;
     numerics) run numerics 600 python tools/numerics_check.py ;;
-    benchw) for v in 65536 60000 100000 200000 70000; do
+    kwcheck) run fcheck_kw 600 python tools/fused_check.py 8192x70000 8192x100000 8192x150000 8192x200000 4096x229376 ;;
+    benchw) for v in 65536 60000 100000 200000 70000 150000; do
               run bench_w$v 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
             done ;;
     trace) run fused_trace 600 python tools/fused_trace.py ;;
