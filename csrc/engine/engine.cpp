@@ -181,7 +181,7 @@ void Engine::alloc_fused() {
     nF_fused_ = use_fused_ ? (int64_t)geom_.grid * fused_fpart_per_block(geom_.variant) : 0;
     const ChainPlan plan = use_fused_ ? fused_chain_plan(geom_, Pp_, fused_split_schedule(geom_.K, cfg_.rtm_bf16))
                                       : ChainPlan{};
-    fold_tiles_ = plan.chain_tiles;
+    chain_tiles_ = plan.chain_tiles;
     fused_blocks_ = use_fused_ ? plan.blocks : 0;
     const int64_t n_part = std::max<int64_t>(nsplit_, use_fused_ ? fused_blocks_ : 1);
     if ((int64_t)partial_.size() < n_part * ld_) partial_.resize(n_part * ld_);
@@ -353,11 +353,11 @@ void Engine::sweep() {
         if (cfg_.rtm_bf16)  // variant 6, K = rows per tile
             launch_fused_sweep_bf16(cfg_.logarithmic, geom_.K, static_cast<const bf16_t*>(A_), ld_, P_, Pp_, x_.get(),
                                     ghat_.get(), arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I,
-                                    geom_.J, st, xcnt_.get(), stream_, geom_.cpl, fold_tiles_);
+                                    geom_.J, st, xcnt_.get(), stream_, geom_.cpl, chain_tiles_);
         else
             launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, static_cast<const float*>(A_), ld_, P_, Pp_,
                                x_.get(), ghat_.get(), arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I,
-                               geom_.J, st, xcnt_.get(), stream_, fold_tiles_, geom_.kw);
+                               geom_.J, st, xcnt_.get(), stream_, chain_tiles_, geom_.kw);
         launch_reduce_partials(partial_.get(), ld_, (int)fused_blocks_, scale, comm_buf_.get(), Fpart_.get(), nF_fused_, Fslot,
                                st, stream_);
     } else {

@@ -167,7 +167,7 @@ class Engine {
     FusedGeometry geom_;
     int nsplit_ = 0;
     int64_t nF_fused_ = 0;
-    int64_t fold_tiles_ = 0;     // fused sweep chain_tiles (T = 1 fold period / T >= 2 segment length), 0 = off
+    int64_t chain_tiles_ = 0;     // fused sweep chain_tiles (T = 1 fold period / T >= 2 segment length), 0 = off
     int64_t fused_blocks_ = 0;   // partial-sum rows written by the fused sweep (I, or I * T * segments)
     double norm_ = 1.0;
 
