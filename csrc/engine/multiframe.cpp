@@ -25,6 +25,8 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     : device_(device), A_(A), bf16_(cfg.rtm_bf16), P_(nrows), Pp_(nrows_pad), V_(nvoxel), ld_(ld), comm_(comm),
       cfg_(cfg) {
     validate_params(cfg_);
+    if (const char* fn = std::getenv("SART_FAULT_NAN"); fn && *fn && cfg_.fault_nan_sweep < 0)
+        cfg_.fault_nan_sweep = std::atoi(fn);
     if (!comm_) throw std::invalid_argument("MultiFrameEngine: communicator required");
     if (ld_ % 64 || ld_ < V_ || Pp_ % 64 || Pp_ < P_)
         throw std::invalid_argument("MultiFrameEngine: ld and nrows_pad must be multiples of 64 covering the shard");
@@ -185,6 +187,9 @@ void MultiFrameEngine::sweep() {
     launch_mf_decide(st, F2, stream_);
     launch_mf_update(X_.get(), D, O_.get(), pen, (float)cfg_.relaxation, cfg_.logarithmic, V_, ld_, st, NF, stream_,
                      Xprev_.get());
+    if (cfg_.fault_nan_sweep >= 0 && host_sweep_ == cfg_.fault_nan_sweep)  // fault injection (tests): slot 0
+        hip_ok(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(X_.get()), 0x7fc00000, 1, stream_), "inject NaN");
+    ++host_sweep_;
 }
 
 // Continuous batching. The batch's nf columns are slots: every slot holds one frame, and a slot whose frame has
@@ -262,6 +267,7 @@ std::vector<SolveInfo> MultiFrameEngine::solve_batch(const double* g, int nframe
     std::vector<SolveInfo> out(std::max(nframes, 0));
     if (nframes <= 0) return out;
     const auto t0 = std::chrono::steady_clock::now();
+    host_sweep_ = 0;
     if ((int64_t)x064_.size() < V_) x064_.resize(std::max<int64_t>(V_, 1));
     if (cfg_.logarithmic && (int64_t)Otmp_.size() < (int64_t)NF * ld_) Otmp_.resize((size_t)NF * ld_);
     if ((int64_t)xsrc_.size() < ld_) xsrc_.resize(ld_);

@@ -85,6 +85,7 @@ class MultiFrameEngine {
     double* hg_ = nullptr;       // pinned [k][rows] staging of the frames entering slots
     float* hx_ = nullptr;        // pinned [nf][ld]: solutions of finished frames, per slot
     hipEvent_t ev_copy_ = nullptr;
+    int host_sweep_ = 0;         // sweeps queued in the current solve_batch (EngineConfig::fault_nan_sweep)
     DeviceArray<float> Otmp_;    // log mode: observed back-projection of the frames entering slots
     DeviceArray<float> xsrc_;    // [ld] copy of the finished frame that warm-starts a refill
 };

@@ -75,3 +75,33 @@ def test_multiframe_warm_chain(log):
     assert all(r.warm_from == -1 for r in cold)
     x, st, it = sart_gpu_semantics(A, G[17], L, logarithmic=log, **kw)
     assert cold[17].status == st and np.linalg.norm(cold[17].solution - x) / np.linalg.norm(x) < 3e-3
+
+
+@pytest.mark.parametrize("log", [False, True])
+def test_multiframe_nonfinite_slot_is_rolled_back_and_refilled(monkeypatch, log):
+    """A NaN injected into slot 0's iterate after sweep 5 (SART_FAULT_NAN) stops that frame at the next sweep:
+    it returns its last finite iterate (5 updates, flagged non-finite) while the other frames continue, and the
+    slot takes the next frame of the queue, which solves normally."""
+    from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SolverParams
+
+    monkeypatch.setenv("SART_FAULT_NAN", "5")
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    P, V, nframes = 500, 800, 20
+    A = rng.random((P, V), dtype=np.float32)
+    G = (rng.random((nframes, V)) + 0.05) @ A.T.astype(np.float64)
+    kw = dict(max_iterations=30, conv_tolerance=0.0)  # every frame runs 30 sweeps: slot 0 is live at sweep 5
+    s = MultiFrameSARTSolver(DenseRTM.from_dense(A, device=dev), None, None, SolverParams(**kw), logarithmic=log,
+                             batch=16, allow_zero_tolerance=True)
+    res = s.solve_batch(G)
+    assert res[0].nonfinite and res[0].iterations == 5 and np.all(np.isfinite(res[0].solution))
+    x, _, _ = sart_gpu_semantics(A, G[0], None, logarithmic=log, max_iterations=5, conv_tolerance=0.0)
+    assert np.linalg.norm(res[0].solution - x) / np.linalg.norm(x) < 3e-3
+    for f in range(1, nframes):
+        assert not res[f].nonfinite
+        x, st, it = sart_gpu_semantics(A, G[f], None, logarithmic=log, **kw)
+        assert res[f].status == st and abs(res[f].iterations - it) <= 2, (f, res[f].iterations, it)
+        assert np.linalg.norm(res[f].solution - x) / np.linalg.norm(x) < 3e-3
