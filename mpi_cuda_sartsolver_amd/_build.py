@@ -25,7 +25,11 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "csrc"
 LIBDIR = Path(__file__).resolve().parent / "_lib"
-BUILDDIR = ROOT / "build"
+# SART_BUILD_DEBUG=1: kernels and engine with -O1 -g (device line info for rocprofv3 / printf debugging, with
+# HIP_LAUNCH_BLOCKING=1 AMD_SERIALIZE_KERNEL=3 at run time), objects under build-debug/. The
+# modules land in the same _lib/ as the optimised build: rebuild without the variable afterwards.
+DEBUG = os.environ.get("SART_BUILD_DEBUG") == "1"
+BUILDDIR = ROOT / ("build-debug" if DEBUG else "build")
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("SART_OFFLOAD_ARCH", "gfx950")
 
@@ -84,8 +88,12 @@ def _compile_many(jobs: list[tuple[list[str], Path, str]], verbose: bool) -> Non
 
 
 def _link(cmd: list[str], out: Path, objs: list[Path], verbose: bool) -> None:
+    # relink when an object is newer than the output or the output came from another object set (the debug
+    # build writes the same modules from build-debug/)
     newest = max(o.stat().st_mtime for o in objs)
-    if out.exists() and out.stat().st_mtime >= newest:
+    stamp = out.with_name(out.name + ".objs")
+    key = "\n".join(str(o) for o in objs)
+    if out.exists() and out.stat().st_mtime >= newest and stamp.exists() and stamp.read_text() == key:
         return
     if verbose:
         print("[link]", out.name, flush=True)
@@ -94,6 +102,7 @@ def _link(cmd: list[str], out: Path, objs: list[Path], verbose: bool) -> None:
     if res.returncode != 0:
         raise RuntimeError(f"link failed for {out.name}:\n{' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
     os.replace(tmp, out)
+    stamp.write_text(key)
 
 
 def build_hip(verbose: bool = True) -> Path:
@@ -103,7 +112,8 @@ def build_hip(verbose: bool = True) -> Path:
     LIBDIR.mkdir(parents=True, exist_ok=True)
     headers = (sorted((CSRC / "kernels").glob("*.hpp")) + sorted((CSRC / "engine").glob("*.hpp")) +
                sorted((CSRC / "native").glob("*.hpp")))
-    common = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
+    common = ["-O1" if DEBUG else "-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
+              "-Wno-unused-function"] + (["-g", "-DSART_DEBUG=1"] if DEBUG else [])
     jobs = []
     objs = []
     for src in sorted((CSRC / "kernels").glob("*.hip")):
@@ -112,7 +122,8 @@ def build_hip(verbose: bool = True) -> Path:
         jobs.append(([hipcc, *flags, "-c", str(src), "-o", str(obj)], obj, _digest([src, *headers], flags)))
         objs.append(obj)
     # native engine (host C++ on the HIP runtime + RCCL): csrc/engine
-    eflags = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}"]
+    eflags = ["-O0" if DEBUG else "-O2", "-std=c++17", "-fPIC", "-Wall", "-D__HIP_PLATFORM_AMD__",
+              f"-I{ROCM / 'include'}"] + (["-g"] if DEBUG else [])
     for src in sorted((CSRC / "engine").glob("*.cpp")) + [CSRC / "native" / "host_comm.cpp",
                                                           CSRC / "native" / "host_comm_mpi.cpp",
                                                           CSRC / "native" / "solver_params.cpp"]:
