@@ -131,6 +131,9 @@ def main() -> int:
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-fused", action="store_true", help="use the two-pass kernels instead of the fused sweep")
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--mf-split-a", choices=["auto", "on", "off"], default="auto",
+                    help="multi-frame fp32 shards: split A into hi + lo bf16 for the bf16 matrix cores (auto: at "
+                         "32 / 64 frames) or fp32 MFMA")
     ap.add_argument("--frames", type=int, default=1,
                     help="frames per step; > 1 solves them together with the multi-frame MFMA engine (up to 64 per batch)")
     ap.add_argument("--partition", choices=["rows", "cols"], default="rows",
@@ -225,7 +228,8 @@ def main() -> int:
         from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
 
         solver = MultiFrameSARTSolver(prob.rtm, lap, comm, params, logarithmic=args.variant == "log",
-                                      batch=min(64, args.frames), check_interval=32, allow_zero_tolerance=True)
+                                      batch=min(64, args.frames), check_interval=32, allow_zero_tolerance=True,
+                                      split_a={"auto": None, "on": True, "off": False}[args.mf_split_a])
         g1 = prob.measurement.cpu().numpy()
         g = np.stack([g1 * (1.0 + 0.05 * f) for f in range(args.frames)])  # distinct frames of one problem
 
@@ -317,7 +321,8 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": "fp32" if args.rtm_dtype == "fp32" else (
+        "dtype": ("fp32 RTM; bf16 MFMA on A and X / W split into hi + lo bf16 (3 products), fp32 accumulation"
+                  if multi and solver.split_a else "fp32") if args.rtm_dtype == "fp32" else (
             "bf16 RTM storage, bf16 MFMA with hi+lo bf16 split of X / W, fp32 accumulation" if multi
             else "bf16 RTM storage; fused row dots on bf16 dot2 with hi+lo split x, fp32 sums"
             if solver.use_fused else "bf16 RTM storage, fp32 compute"),

@@ -62,9 +62,14 @@ struct EngineConfig : SolverParams {
     // Storage precision of the shard: A holds bf16 bit patterns instead of fp32 (half the
     // HBM bytes per sweep, twice the matrix per GPU); products, sums and every vector stay fp32 / fp64. Ray
     // sums are taken over the stored (rounded) values, so the solve is exact SART for the bf16 matrix.
-    // Fused sweep variant 6 (bf16 register tiles, fp32 LDS ring) or the two-pass kernels; the multi-frame
-    // engine is fp32-only.
+    // Fused sweep variant 6 (bf16 register tiles, fp32 LDS ring), the two-pass kernels, or the bf16 MFMA
+    // multi-frame kernels.
     bool rtm_bf16 = false;
+    // Multi-frame engine with an fp32 shard: run the projections on the bf16 matrix cores with A split into
+    // hi + lo bf16 in registers (three products per element; multiframe_bf16.hip, "split-A") instead of fp32
+    // MFMA. 1: on, 0: off, -1: env SART_MF_X3 (0 / 1), else on for batches of 32 and 64 frames (where fp32
+    // MFMA bounds the sweep; at 16 frames both paths are HBM-bound).
+    int mf_split_a = -1;
 };
 
 // roctx range (rocprofv3 --marker-trace) for the lifetime of the object.

@@ -33,6 +33,15 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     cfg_.check_interval = std::max(1, cfg_.check_interval);
     nf_ = batch_width(cfg_.mf_frames);
     const int NF = nf_;
+    if (!bf16_) {
+        int m = cfg_.mf_split_a;
+        if (m < 0) {
+            const char* e = std::getenv("SART_MF_X3");
+            m = (e && *e) ? (std::atoi(e) != 0) : (NF >= 32);
+        }
+        x3_ = m != 0;
+    }
+    split_ = bf16_ || x3_;
     set_device();
     hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
     hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -43,7 +52,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hx_), (size_t)NF * ld_ * sizeof(float)), "hipHostMalloc");
     hip_ok(hipEventCreateWithFlags(&ev_copy_, hipEventDisableTiming), "hipEventCreate");
     nsf_ = mf_forward_num_splits(ld_, Pp_);
-    nsb_ = bf16_ ? mf_backproject_b16_num_splits(ld_, P_) : mf_backproject_num_splits(ld_, P_);
+    nsb_ = split_ ? mf_backproject_b16_num_splits(ld_, P_, x3_) : mf_backproject_num_splits(ld_, P_);
     nwb_ = mf_weights_num_blocks(Pp_);
     X_.resize((size_t)NF * ld_);
     Xprev_.resize((size_t)NF * ld_);
@@ -58,9 +67,10 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     G64_.resize(NF);
     F2part_.resize((size_t)nwb_ * NF);
     st_.resize(1);
-    if (bf16_) {
+    if (split_) {
         for (auto* b : {&Xh_, &Xl_}) b->resize((size_t)NF * ld_);
-        for (auto* b : {&Wh_, &Wl_}) b->resize((size_t)NF * Pp_);
+        Wh_.resize((size_t)(x3_ ? 2 : 1) * NF * Pp_);  // split-A: hi and mid planes
+        Wl_.resize((size_t)NF * Pp_);
     }
     rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_, false, bf16_);
     // chunks of the overlapped back-projection / all-reduce pipeline (several ranks only): SART_MF_CHUNKS
@@ -72,7 +82,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
         const int64_t min_vox = std::max<int64_t>(1, (1 << 20) / (4 * NF));
         nchunks = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, ld_ / min_vox));
     }
-    const int64_t align = bf16_ ? mf_backproject_b16_vox_align(ld_) : mf_backproject_vox_align(ld_, NF);
+    const int64_t align = split_ ? mf_backproject_b16_vox_align(ld_, x3_) : mf_backproject_vox_align(ld_, NF);
     chunks_.assign(1, 0);
     for (int c = 1; c < nchunks; ++c) {
         const int64_t v = (ld_ * c / nchunks) / align * align;
@@ -121,20 +131,28 @@ void MultiFrameEngine::set_laplacian(const int64_t* row_ptr, const int32_t* col,
 }
 
 void MultiFrameEngine::forward() {
-    if (bf16_) {
-        launch_mf_split_x(X_.get(), (int64_t)nf_ * ld_, Xh_.get(), Xl_.get(), stream_);
-        launch_mf_forward_b16(static_cast<const bf16_t*>(A_), ld_, P_, Pp_, Xh_.get(), Xl_.get(), Fs_.get(), nsf_, nf_,
-                              stream_);
+    if (split_) {
+        launch_mf_split_x(X_.get(), (int64_t)nf_ * ld_, Xh_.get(), Xl_.get(), stream_, x3_);
+        if (bf16_)
+            launch_mf_forward_b16(static_cast<const bf16_t*>(A_), ld_, P_, Pp_, Xh_.get(), Xl_.get(), Fs_.get(), nsf_,
+                                  nf_, stream_);
+        else
+            launch_mf_forward_x3(static_cast<const float*>(A_), ld_, P_, Pp_, Xh_.get(), Xl_.get(), Fs_.get(), nsf_,
+                                 nf_, stream_);
     } else {
         launch_mf_forward(static_cast<const float*>(A_), ld_, P_, Pp_, X_.get(), ld_, Fs_.get(), nsf_, nf_, stream_);
     }
 }
 
 void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int64_t v1) {
-    if (bf16_) {
-        if (split_w) launch_mf_split_w(W, Pp_, nf_, Pp_, Wh_.get(), Wl_.get(), stream_);
-        launch_mf_backproject_b16(static_cast<const bf16_t*>(A_), ld_, P_, Wh_.get(), Wl_.get(), Pp_, nsb_,
-                                  part_.get(), nf_, stream_, v0, v1);
+    if (split_) {
+        if (split_w) launch_mf_split_w(W, Pp_, nf_, Pp_, Wh_.get(), Wl_.get(), stream_, x3_);
+        if (bf16_)
+            launch_mf_backproject_b16(static_cast<const bf16_t*>(A_), ld_, P_, Wh_.get(), Wl_.get(), Pp_, nsb_,
+                                      part_.get(), nf_, stream_, v0, v1);
+        else
+            launch_mf_backproject_x3(static_cast<const float*>(A_), ld_, P_, Wh_.get(), Wl_.get(), Pp_, nsb_,
+                                     part_.get(), nf_, stream_, v0, v1);
     } else {
         launch_mf_backproject(static_cast<const float*>(A_), ld_, P_, W, nsb_, part_.get(), nf_, stream_, v0, v1);
     }

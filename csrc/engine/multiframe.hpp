@@ -22,7 +22,8 @@ namespace sart {
 
 class MultiFrameEngine {
    public:
-    // A: fp32 [nrows_pad][ld], or bf16 when cfg.rtm_bf16 (bf16 MFMA projections, multiframe_bf16.hip)
+    // A: fp32 [nrows_pad][ld], or bf16 when cfg.rtm_bf16 (bf16 MFMA projections, multiframe_bf16.hip); fp32
+    // shards run on fp32 MFMA (multiframe.hip) or split into bf16 on the bf16 matrix cores (cfg.mf_split_a)
     MultiFrameEngine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
                      Communicator* comm, const EngineConfig& cfg);
     ~MultiFrameEngine();
@@ -40,6 +41,7 @@ class MultiFrameEngine {
     int64_t nrows() const { return P_; }
     int64_t nvoxel() const { return V_; }
     int batch_frames() const { return nf_; }
+    bool split_a() const { return x3_; }  // fp32 shard on the bf16 matrix cores
     // 16, 32 or 64: the smallest batch width that holds `frames` (64 for anything larger)
     static int batch_width(int frames);
 
@@ -60,6 +62,8 @@ class MultiFrameEngine {
     int device_;
     const void* A_;
     bool bf16_ = false;
+    bool x3_ = false;     // fp32 shard on the bf16 matrix cores (EngineConfig::mf_split_a)
+    bool split_ = false;  // X / W enter as hi + lo bf16 planes (bf16_ || x3_)
     int64_t P_, Pp_, V_, ld_;
     Communicator* comm_;
     EngineConfig cfg_;
@@ -69,7 +73,7 @@ class MultiFrameEngine {
     DeviceRaySums rs_;
     DeviceArray<float> X_, Xprev_, Fs_, W_, part_, buf_, pen_, O_, ghat_, arow_, gpos_, wo_;
     DeviceArray<double> g64_, G64_, F2part_, x064_;
-    DeviceArray<bf16_t> Xh_, Xl_, Wh_, Wl_;  // bf16 engine: hi / lo operand planes
+    DeviceArray<bf16_t> Xh_, Xl_, Wh_, Wl_;  // bf16 / split-A engine: hi / lo operand planes
     DeviceArray<MfState> st_;
     DeviceArray<int64_t> lap_rp_;
     DeviceArray<int32_t> lap_col_;

@@ -24,6 +24,19 @@
 //
 // Ring loads are unconditional (clamped to the last step) like the fp32 kernels: the compiler then keeps
 // DEPTH steps of loads in flight with counted vmcnt waits.
+//
+// Split-A mode (AT = float: an fp32-stored RTM on the bf16 matrix cores). The fp32 engine (multiframe.hip) is
+// matrix-core bound at 32 / 64 frames: fp32 MFMA runs at 1/16 of the bf16 rate. The LDS kernels below also take
+// an fp32 A, split each element in registers as it is consumed, hi = rne(a), lo = rne(a - hi)
+// (|a - hi - lo| <= 2^-18 |a|, below the fp32 accumulation error of a 64k-long dot), and run three products
+// A_hi X_hi + A_hi X_lo + A_lo X_hi into the fp32 accumulator (the dropped A_lo X_lo is ~2^-17 of the product;
+// A and X are non-negative, so the forward sums do not cancel and these errors stay at 2^-17 / sqrt(K) of F:
+// fp32 level, tools/x3_accuracy.py). The back-projection's weights are residuals of both signs whose sum cancels:
+// there a representation error of 2^-18 of each term shows at full size in A^T W (measured 4e-6 against fp32's
+// 1.4e-7), so A and W enter as three pieces each (hi + mid + lo to 2^-27) and six products (every pair of
+// combined weight >= 2^-16). Three / six bf16 MFMAs cost 3/16 / 6/16 of one fp32 MFMA of the same K; the splits
+// are 3 / 5 VALU operations per element of A, which overlap the stream. The stored matrix, the fp32 state and the
+// fp32 sums are those of the fp32 engine.
 #include "sart_common.hpp"
 #include "launchers.hpp"
 
@@ -31,6 +44,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <utility>
 
 namespace sart {
@@ -49,6 +63,63 @@ __device__ __forceinline__ floatx4 mfma_b16(const uint4 a, const u32x4 b, floatx
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
                                                    c, 0, 0, 0);
 }
+
+typedef unsigned u32x8 __attribute__((ext_vector_type(8)));  // eight fp32 of A (a split-A forward fragment)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ floatx4 mfma_b16(const u32x4 a, const u32x4 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+}
+
+// Split two fp32 (bit patterns x = element 2m, y = element 2m + 1) into packed bf16 hi = rne and lo = rne of
+// the remainder.
+__device__ __forceinline__ void split_a2(unsigned x, unsigned y, unsigned& hi, unsigned& lo) {
+    const float a = __uint_as_float(x), b = __uint_as_float(y);
+    const bf16x2_t h = bf16x2_t{(__bf16)a, (__bf16)b};
+    hi = __builtin_bit_cast(unsigned, h);
+    const float ra = a - __uint_as_float(hi << 16), rb = b - __uint_as_float(hi & 0xffff0000u);
+    lo = __builtin_bit_cast(unsigned, bf16x2_t{(__bf16)ra, (__bf16)rb});
+}
+
+// Forward fragment of a split-A wave: eight consecutive fp32 of one row -> hi / lo bf16 fragments.
+__device__ __forceinline__ void split_a8(const u32x8 v, u32x4& hi, u32x4& lo) {
+    unsigned h0, h1, h2, h3, l0, l1, l2, l3;
+    split_a2(v[0], v[1], h0, l0);
+    split_a2(v[2], v[3], h1, l1);
+    split_a2(v[4], v[5], h2, l2);
+    split_a2(v[6], v[7], h3, l3);
+    hi = u32x4{h0, h1, h2, h3};
+    lo = u32x4{l0, l1, l2, l3};
+}
+
+// Three pieces: hi + mid + lo = a to 2^-27 (the back-projection, whose signed weights cancel in the sum).
+__device__ __forceinline__ void split_a2_3(unsigned x, unsigned y, unsigned& hi, unsigned& mid, unsigned& lo) {
+    const float a = __uint_as_float(x), b = __uint_as_float(y);
+    hi = __builtin_bit_cast(unsigned, bf16x2_t{(__bf16)a, (__bf16)b});
+    const float ra = a - __uint_as_float(hi << 16), rb = b - __uint_as_float(hi & 0xffff0000u);
+    mid = __builtin_bit_cast(unsigned, bf16x2_t{(__bf16)ra, (__bf16)rb});
+    const float sa = ra - __uint_as_float(mid << 16), sb = rb - __uint_as_float(mid & 0xffff0000u);
+    lo = __builtin_bit_cast(unsigned, bf16x2_t{(__bf16)sa, (__bf16)sb});
+}
+
+// Back-projection fragment of voxel phase P from eight 16-byte fp32 row loads (4 voxels each): element j = the
+// fp32 of voxel P in row load j, split into hi / mid / lo.
+template <int P>
+__device__ __forceinline__ void split_phase3(const u32x4 (&v)[8], u32x4& hi, u32x4& mid, u32x4& lo) {
+    unsigned h[4], m[4], l[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) split_a2_3(v[2 * q][P], v[2 * q + 1][P], h[q], m[q], l[q]);
+    hi = u32x4{h[0], h[1], h[2], h[3]};
+    mid = u32x4{m[0], m[1], m[2], m[3]};
+    lo = u32x4{l[0], l[1], l[2], l[3]};
+}
+
+// Raw A storage of one fragment: 16 bytes of bf16 or 32 bytes of fp32 (forward); 8 or 16 bytes of one row's
+// four voxels (back-projection).
+template <typename AT> struct ARaw;
+template <> struct ARaw<bf16_t> { typedef uint4 fwd; typedef uint2 bwd; };
+template <> struct ARaw<float> { typedef u32x8 fwd; typedef u32x4 bwd; };
 
 // Fragment of voxel phase P from the eight 8-byte row loads: element j = bf16 P of row load j.
 template <int P>
@@ -151,8 +222,8 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
 // R = 64 RT rows per wave -> per workgroup), which is what bounds the register-operand forward at 32 / 64
 // frames (profiles/probe_r2_mf_b16.jsonl). One barrier per step; waves past the padded rows clamp to the last
 // row tile (they take part in the X staging and barriers, and store nothing).
-template <int NG, int DEPTH, int RT, int KB>
-__global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const bf16_t* __restrict__ A, int64_t ld, int64_t nrows,
+template <int NG, int DEPTH, int RT, int KB, typename AT = bf16_t>
+__global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const AT* __restrict__ A, int64_t ld, int64_t nrows,
                                                             int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                             const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
                                                             int64_t cols_per_split, const int* __restrict__ skip) {
@@ -170,9 +241,14 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const bf16_t* __rest
     const int64_t c0 = (int64_t)blockIdx.y * cols_per_split;
     const int64_t c1 = (c0 + cols_per_split < ld) ? c0 + cols_per_split : ld;
     Fout += (int64_t)blockIdx.y * nrows_pad * NF;
-    const bf16_t* __restrict__ ap = A + (row0 + r) * ld + c0 + 8 * g;
+    constexpr bool A32 = std::is_same<AT, float>::value;
+    // split-A: lane (r, g) loads voxels 4 g .. 4 g + 3 and 16 + 4 g .. of each 32-voxel block (two contiguous
+    // 64-byte halves of a row per instruction instead of four 16-byte pieces); the X planes hold the same k order
+    // (k_mf_split_x with perm)
+    const AT* __restrict__ ap = A + (row0 + r) * ld + c0 + (A32 ? 4 : 8) * g;
     const int64_t xo = (int64_t)r * ld + c0 + 8 * g;
     const int lofs = r * 4 + g;  // uint4 slot of (frame r, voxels 8 g..) inside a 1 KiB piece
+    typedef typename ARaw<AT>::fwd AF;
 
     floatx4 acc[RT][NG];
 #pragma unroll
@@ -182,7 +258,7 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const bf16_t* __rest
 
     const int64_t nst = c1 > c0 ? (c1 - c0) / (32 * KB) : 0;  // uniform for the workgroup
     if (nst > 0) {
-        uint4 a[RS][RT][KB];
+        AF a[RS][RT][KB];
         u32x4 xq[RS][XQ];
         auto piece = [&](int i) { return (C >= 4 ? wave * XQ + i : wave % C); };  // piece = (kb * 2 + plane) * NG + j
         auto load = [&](auto slc, int64_t t) {
@@ -191,8 +267,16 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const bf16_t* __rest
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-                for (int kb = 0; kb < KB; ++kb)
-                    a[sl][rt][kb] = *reinterpret_cast<const uint4*>(ap + rt * 16 * ld + q + 32 * kb);
+                for (int kb = 0; kb < KB; ++kb) {
+                    if constexpr (A32) {
+                        const AT* p = ap + rt * 16 * ld + q + 32 * kb;
+                        const u32x4 h0 = *reinterpret_cast<const u32x4*>(p);
+                        const u32x4 h1 = *reinterpret_cast<const u32x4*>(p + 16);
+                        a[sl][rt][kb] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+                    } else {
+                        a[sl][rt][kb] = *reinterpret_cast<const AF*>(ap + rt * 16 * ld + q + 32 * kb);
+                    }
+                }
 #pragma unroll
             for (int i = 0; i < XQ; ++i) {
                 const int pc = piece(i), j = pc % NG, plane = (pc / NG) & 1, kb = pc / (2 * NG);
@@ -216,17 +300,43 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const bf16_t* __rest
             stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);  // X of step t + 1 into the other stage (its readers passed the last barrier)
             const u32x4* xs = s_x[t & 1][0] + lofs;
 #pragma unroll
-            for (int kb = 0; kb < KB; ++kb)
+            for (int kb = 0; kb < KB; ++kb) {
+                if constexpr (A32) {
+                    u32x4 ah[RT], al[RT];
 #pragma unroll
-                for (int j = 0; j < NG; ++j) {
-                    const u32x4 xh = xs[((kb * 2 + 0) * NG + j) * 64];
-                    const u32x4 xl = xs[((kb * 2 + 1) * NG + j) * 64];
+                    for (int rt = 0; rt < RT; ++rt) split_a8(a[sl][rt][kb], ah[rt], al[rt]);
+                    u32x4 xh[NG], xl[NG];
 #pragma unroll
-                    for (int rt = 0; rt < RT; ++rt) {
-                        acc[rt][j] = mfma_b16(a[sl][rt][kb], xh, acc[rt][j]);
-                        acc[rt][j] = mfma_b16(a[sl][rt][kb], xl, acc[rt][j]);
+                    for (int j = 0; j < NG; ++j) {
+                        xh[j] = xs[((kb * 2 + 0) * NG + j) * 64];
+                        xl[j] = xs[((kb * 2 + 1) * NG + j) * 64];
+                    }
+                    // product-major: consecutive MFMAs write different accumulators (no dependent chains)
+#pragma unroll
+                    for (int j = 0; j < NG; ++j)
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(al[rt], xh[j], acc[rt][j]);
+#pragma unroll
+                    for (int j = 0; j < NG; ++j)
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(ah[rt], xl[j], acc[rt][j]);
+#pragma unroll
+                    for (int j = 0; j < NG; ++j)
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(ah[rt], xh[j], acc[rt][j]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < NG; ++j) {
+                        const u32x4 xh = xs[((kb * 2 + 0) * NG + j) * 64];
+                        const u32x4 xl = xs[((kb * 2 + 1) * NG + j) * 64];
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt) {
+                            acc[rt][j] = mfma_b16(a[sl][rt][kb], xh, acc[rt][j]);
+                            acc[rt][j] = mfma_b16(a[sl][rt][kb], xl, acc[rt][j]);
+                        }
                     }
                 }
+            }
             __syncthreads();
         };
         for (int64_t t0 = 0; t0 < nst; t0 += RS) {
@@ -337,8 +447,13 @@ __global__ __launch_bounds__(256) void k_mf_backproject_b16(const bf16_t* __rest
 // same rows, so they need the same W fragments ([hi, lo][NG][16 frames][32 rows] per step, 1 KiB pieces), loaded
 // once per workgroup and staged through two LDS stages like k_mf_forward_b16_lds. Waves past the voxel range
 // clamp to the last wave tile of the range (they stage W, take the barriers and store nothing).
-template <int NG, int DEPTH, int VT>
-__global__ __launch_bounds__(256) void k_mf_backproject_b16_lds(const bf16_t* __restrict__ A, int64_t ld,
+// Split-A occupancy: the six-product body takes ~260 registers at NG = 4 (one wave per SIMD); asking for two
+// waves per SIMD makes the compiler fit it (tools/probe_mf_x3.py).
+template <typename AT, int VT>
+constexpr int mf_bwd_min_waves() { return (std::is_same<AT, float>::value && VT == 1) ? 2 : 1; }
+
+template <int NG, int DEPTH, int VT, typename AT = bf16_t>
+__global__ __launch_bounds__(256, (mf_bwd_min_waves<AT, VT>())) void k_mf_backproject_b16_lds(const AT* __restrict__ A, int64_t ld,
                                                                 int64_t nrows32, const bf16_t* __restrict__ Wh,
                                                                 const bf16_t* __restrict__ Wl, int64_t ldw,
                                                                 int64_t rows_per_split, float* __restrict__ partial,
@@ -346,8 +461,10 @@ __global__ __launch_bounds__(256) void k_mf_backproject_b16_lds(const bf16_t* __
     if (skip && *skip) return;
     constexpr int NF = 16 * NG;
     constexpr int RS = DEPTH + 1;
-    constexpr int C = 2 * NG;
-    constexpr int XQ = C >= 4 ? C / 4 : 1;
+    constexpr bool A32 = std::is_same<AT, float>::value;
+    constexpr int NPL = A32 ? 3 : 2;              // W planes: hi, (mid,) lo
+    constexpr int C = NPL * NG;                   // 1 KiB W pieces per step
+    constexpr int XQ = C >= 4 ? (C + 3) / 4 : 1;  // pieces per wave (clamped: a duplicate load writes equal data)
     __shared__ __attribute__((aligned(16))) u32x4 s_w[2][C][64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int64_t vb = (vb0 + (int64_t)blockIdx.x * 4 + wave) * VT;
@@ -357,9 +474,12 @@ __global__ __launch_bounds__(256) void k_mf_backproject_b16_lds(const bf16_t* __
     const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
     int64_t r_end = r_begin + rows_per_split;
     if (r_end > nrows32) r_end = nrows32;
-    const bf16_t* __restrict__ ap = A + (r_begin + 8 * g) * ld + vb * 64 + 4 * i16;
+    const AT* __restrict__ ap = A + (r_begin + 8 * g) * ld + vb * 64 + 4 * i16;
     const int64_t wo = (int64_t)i16 * ldw + r_begin + 8 * g;
     const int lofs = i16 * 4 + g;
+    typedef typename ARaw<AT>::bwd AB;
+    // plane pl of frame group j: hi, mid (split-A: stored after hi in Wh), lo
+    auto plane_ptr = [&](int pl) { return pl == NPL - 1 ? Wl : Wh + (int64_t)pl * NF * ldw; };
 
     floatx4 acc[VT][4][NG];
 #pragma unroll
@@ -371,21 +491,27 @@ __global__ __launch_bounds__(256) void k_mf_backproject_b16_lds(const bf16_t* __
 
     const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 32 : 0;  // uniform for the workgroup
     if (nst > 0) {
-        uint2 av[RS][VT][8];
+        AB av[RS][VT][8];
         u32x4 wq[RS][XQ];
-        auto piece = [&](int i) { return (C >= 4 ? wave * XQ + i : wave % C); };  // piece = plane * NG + j
+        auto piece = [&](int i) {  // piece = plane * NG + j
+            return C >= 4 ? (wave * XQ + i < C ? wave * XQ + i : C - 1) : wave % C;
+        };
         auto load = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
-            const bf16_t* at = ap + t * 32 * ld;
+            const AT* at = ap + t * 32 * ld;
 #pragma unroll
             for (int vt = 0; vt < VT; ++vt)
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    av[sl][vt][j] = load_stream(reinterpret_cast<const uint2*>(at + j * ld + vt * 64));
+                for (int j = 0; j < 8; ++j) {
+                    if constexpr (A32)
+                        av[sl][vt][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(at + j * ld + vt * 64));
+                    else
+                        av[sl][vt][j] = load_stream(reinterpret_cast<const uint2*>(at + j * ld + vt * 64));
+                }
 #pragma unroll
             for (int i = 0; i < XQ; ++i) {
                 const int pc = piece(i), j = pc % NG, plane = pc / NG;
-                wq[sl][i] = *reinterpret_cast<const u32x4*>((plane ? Wl : Wh) + wo + (int64_t)j * 16 * ldw + t * 32);
+                wq[sl][i] = *reinterpret_cast<const u32x4*>(plane_ptr(plane) + wo + (int64_t)j * 16 * ldw + t * 32);
             }
         };
         auto stage = [&](auto slc, int64_t t) {
@@ -406,15 +532,43 @@ __global__ __launch_bounds__(256) void k_mf_backproject_b16_lds(const bf16_t* __
             const u32x4* ws = s_w[t & 1][0] + lofs;
 #pragma unroll
             for (int vt = 0; vt < VT; ++vt) {
-                const uint4 fr[4] = {phase_frag<0>(av[sl][vt]), phase_frag<1>(av[sl][vt]), phase_frag<2>(av[sl][vt]),
-                                     phase_frag<3>(av[sl][vt])};
+                if constexpr (A32) {
+                    // six products: every piece pair of combined weight >= 2^-16 (hi, mid, lo of A and of W),
+                    // smallest first into the accumulator
+                    u32x4 fh[4], fm[4], fl[4];
+                    split_phase3<0>(av[sl][vt], fh[0], fm[0], fl[0]);
+                    split_phase3<1>(av[sl][vt], fh[1], fm[1], fl[1]);
+                    split_phase3<2>(av[sl][vt], fh[2], fm[2], fl[2]);
+                    split_phase3<3>(av[sl][vt], fh[3], fm[3], fl[3]);
+                    u32x4 wv[3][NG];
 #pragma unroll
-                for (int j = 0; j < NG; ++j) {
-                    const u32x4 wh = ws[j * 64], wl = ws[(NG + j) * 64];
+                    for (int j = 0; j < NG; ++j)
 #pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        acc[vt][p][j] = mfma_b16(fr[p], wh, acc[vt][p][j]);
-                        acc[vt][p][j] = mfma_b16(fr[p], wl, acc[vt][p][j]);
+                        for (int pl = 0; pl < 3; ++pl) wv[pl][j] = ws[(pl * NG + j) * 64];
+                    // product-major: consecutive MFMAs write different accumulators (no dependent chains)
+                    auto prod = [&](const u32x4(&fa)[4], int pl) {
+#pragma unroll
+                        for (int j = 0; j < NG; ++j)
+#pragma unroll
+                            for (int p = 0; p < 4; ++p) acc[vt][p][j] = mfma_b16(fa[p], wv[pl][j], acc[vt][p][j]);
+                    };
+                    prod(fh, 2);
+                    prod(fm, 1);
+                    prod(fl, 0);
+                    prod(fh, 1);
+                    prod(fm, 0);
+                    prod(fh, 0);
+                } else {
+                    const uint4 fr[4] = {phase_frag<0>(av[sl][vt]), phase_frag<1>(av[sl][vt]),
+                                         phase_frag<2>(av[sl][vt]), phase_frag<3>(av[sl][vt])};
+#pragma unroll
+                    for (int j = 0; j < NG; ++j) {
+                        const u32x4 wh = ws[j * 64], wl = ws[(NG + j) * 64];
+#pragma unroll
+                        for (int p = 0; p < 4; ++p) {
+                            acc[vt][p][j] = mfma_b16(fr[p], wh, acc[vt][p][j]);
+                            acc[vt][p][j] = mfma_b16(fr[p], wl, acc[vt][p][j]);
+                        }
                     }
                 }
             }
@@ -493,65 +647,114 @@ static bool mf_b16_bwd_lds(int nf) {
     return true;
 }
 
-template <int NG, int DEPTH, int RT, int KB>
-static void fwd_b16_t(bool lds, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows,
+template <int NG, int DEPTH, int RT, int KB, typename AT>
+static void fwd_b16_t(bool lds, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows,
                       int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
-    if (lds)
+    if constexpr (std::is_same<AT, float>::value) {
+        (void)lds;  // split-A: the LDS kernels only
+        hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB, float>), grid, dim3(256), 0, stream, A, ld, nrows,
+                           nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
+    } else if (lds) {
         hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB>), grid, dim3(256), 0, stream, A, ld, nrows,
                            nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
-    else
+    } else {
         hipLaunchKernelGGL((k_mf_forward_b16<NG, DEPTH, RT, KB>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad,
                            Xh, Xl, Fout, cps, g_mf_skip);
+    }
 }
 
-template <int NG, int DEPTH>
-static void fwd_b16_d(FwdTile tl, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows,
+template <int NG, int DEPTH, typename AT>
+static void fwd_b16_d(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows,
                       int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
     if (tl.rt == 2 && tl.kb == 2)
         fwd_b16_t<NG, DEPTH, 2, 2>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else if (tl.rt == 4 && tl.kb == 2)
         fwd_b16_t<NG, DEPTH, 4, 2>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
-    else if (tl.rt == 8)
-        fwd_b16_t<NG, DEPTH, 8, 1>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
-    else
+    else if (tl.rt == 2)
+        fwd_b16_t<NG, DEPTH, 2, 1>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+    else if constexpr (!std::is_same<AT, float>::value) {
+        if (tl.rt == 8)
+            fwd_b16_t<NG, DEPTH, 8, 1>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+        else
+            fwd_b16_t<NG, DEPTH, 4, 1>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+    } else {
         fwd_b16_t<NG, DEPTH, 4, 1>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+    }
 }
 
-template <int NG>
-static void fwd_b16(int depth, FwdTile tl, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows,
+template <int NG, typename AT>
+static void fwd_b16(int depth, FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows,
                     int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
-    if (depth == 1)
-        fwd_b16_d<NG, 1>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
-    else if (depth == 2)
+    if constexpr (!std::is_same<AT, float>::value) {
+        if (depth == 1) {
+            fwd_b16_d<NG, 1>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+            return;
+        }
+    }
+    if (depth <= 2)
         fwd_b16_d<NG, 2>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else
         fwd_b16_d<NG, 3>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
 }
 
-void launch_mf_forward_b16(const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const bf16_t* Xh,
-                           const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream) {
-    if (ld % 64 != 0) throw std::runtime_error("mf_forward_b16: ld must be a multiple of 64");
-    if (nsplit < 1) throw std::runtime_error("mf_forward_b16: nsplit must be >= 1");
-    check_nf_b16(nf, "mf_forward_b16");
-    FwdTile tl = mf_b16_fwd_tile(nf);
+// Split-A tunables (fp32 A on the bf16 matrix cores): SART_MF_X3_FWD = "RT,KB", SART_MF_X3_VT = VT (1 or 2),
+// SART_MF_X3_DEPTH (2 or 3). Twice the bytes of A per fragment as bf16 storage, so smaller register tiles.
+static FwdTile mf_x3_fwd_tile(int nf) {
+    const char* e = std::getenv("SART_MF_X3_FWD");
+    if (e && *e) {
+        FwdTile t{std::atoi(e), std::strchr(e, ',') ? std::atoi(std::strchr(e, ',') + 1) : 1, true};
+        if ((t.rt == 2 || t.rt == 4) && (t.kb == 1 || t.kb == 2)) return t;
+    }
+    return nf == 64 ? FwdTile{4, 1, true} : FwdTile{2, 2, true};  // profiles/probe_r2_mf_x3.jsonl
+}
+static int mf_x3_depth(bool forward) {
+    const int d = env_int("SART_MF_X3_DEPTH", 0);
+    return (d == 2 || d == 3) ? d : (forward ? 3 : 2);
+}
+static int mf_x3_vt(int64_t ld) {
+    const int v = env_int("SART_MF_X3_VT", 0);
+    const int vt = (v == 1 || v == 2) ? v : 1;
+    return (vt == 2 && ld % 128 == 0) ? 2 : 1;
+}
+
+template <typename AT>
+static void launch_mf_forward_split(const AT* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const bf16_t* Xh,
+                                    const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream) {
+    constexpr bool A32 = std::is_same<AT, float>::value;
+    const char* what = A32 ? "mf_forward_x3" : "mf_forward_b16";
+    if (ld % 64 != 0) throw std::runtime_error(std::string(what) + ": ld must be a multiple of 64");
+    if (nsplit < 1) throw std::runtime_error(std::string(what) + ": nsplit must be >= 1");
+    check_nf_b16(nf, what);
+    if (nrows_pad % 32 != 0) throw std::runtime_error(std::string(what) + ": padded rows must be a multiple of 32");
+    FwdTile tl = A32 ? mf_x3_fwd_tile(nf) : mf_b16_fwd_tile(nf);
     if (nrows_pad % (16 * tl.rt) != 0) tl = FwdTile{2, 1, tl.lds};  // a wave's rows must lie inside the padding
-    if (nrows_pad % 32 != 0) throw std::runtime_error("mf_forward_b16: padded rows must be a multiple of 32");
     const int64_t cps = ((ld + nsplit - 1) / nsplit + 63) / 64 * 64;
     const int64_t rows_per_block = 64 * tl.rt;
     const dim3 grid((unsigned)((nrows_pad + rows_per_block - 1) / rows_per_block), (unsigned)nsplit);
-    const int d = mf_b16_depth(true, nf);
+    const int d = A32 ? mf_x3_depth(true) : mf_b16_depth(true, nf);
     if (nf == 16)
         fwd_b16<1>(d, tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else if (nf == 32)
         fwd_b16<2>(d, tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else
         fwd_b16<4>(d, tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
-    check_launch("k_mf_forward_b16");
+    check_launch(A32 ? "k_mf_forward_x3" : "k_mf_forward_b16");
 }
 
-// Split-K of the bf16 back-projection: ~1024 workgroups (4 waves x 64 VT voxels each), >= 64 rows per split.
-int mf_backproject_b16_num_splits(int64_t ld, int64_t nrows) {
-    const int64_t nblk = (ld / (64 * mf_b16_vt(ld, 0)) + 3) / 4;
+void launch_mf_forward_b16(const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const bf16_t* Xh,
+                           const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream) {
+    launch_mf_forward_split(A, ld, nrows, nrows_pad, Xh, Xl, Fout, nsplit, nf, stream);
+}
+
+void launch_mf_forward_x3(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const bf16_t* Xh,
+                          const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream) {
+    launch_mf_forward_split(A, ld, nrows, nrows_pad, Xh, Xl, Fout, nsplit, nf, stream);
+}
+
+// Split-K of the bf16 / split-A back-projection: ~1024 workgroups (4 waves x 64 VT voxels each), >= 64 rows per
+// split.
+int mf_backproject_b16_num_splits(int64_t ld, int64_t nrows, bool a32) {
+    const int64_t nblk = (ld / (64 * (a32 ? mf_x3_vt(ld) : mf_b16_vt(ld, 0))) + 3) / 4;
     const int64_t target = env_int("SART_MF_BP_BLOCKS", 1024);
     int64_t s = (target + nblk - 1) / nblk;
     const int64_t smax = (nrows + 63) / 64;
@@ -560,66 +763,87 @@ int mf_backproject_b16_num_splits(int64_t ld, int64_t nrows) {
     return (int)s;
 }
 
-int mf_backproject_b16_vox_align(int64_t ld) { return 64 * mf_b16_vt(ld, 0); }
+int mf_backproject_b16_vox_align(int64_t ld, bool a32) { return 64 * (a32 ? mf_x3_vt(ld) : mf_b16_vt(ld, 0)); }
 
-template <int NG, int DEPTH>
-static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows32,
+template <int NG, int DEPTH, typename AT>
+static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows32,
                       const bf16_t* Wh, const bf16_t* Wl, int64_t ldw, int64_t rps, float* partial, int64_t vb0,
                       int64_t vend) {
-    if (mf_b16_bwd_lds(16 * NG)) {
+    if (std::is_same<AT, float>::value || mf_b16_bwd_lds(16 * NG)) {
         if (vt == 2)
-            hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2>), grid, dim3(256), 0, stream, A, ld, nrows32,
-                               Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+            hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2, AT>), grid, dim3(256), 0, stream, A, ld,
+                               nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
         else
-            hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1>), grid, dim3(256), 0, stream, A, ld, nrows32,
-                               Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+            hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1, AT>), grid, dim3(256), 0, stream, A, ld,
+                               nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
         return;
     }
-    if (vt == 2)
-        hipLaunchKernelGGL((k_mf_backproject_b16<NG, DEPTH, 2>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
-                           ldw, rps, partial, vb0, vend, g_mf_skip);
-    else
-        hipLaunchKernelGGL((k_mf_backproject_b16<NG, DEPTH, 1>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
-                           ldw, rps, partial, vb0, vend, g_mf_skip);
+    if constexpr (!std::is_same<AT, float>::value) {
+        if (vt == 2)
+            hipLaunchKernelGGL((k_mf_backproject_b16<NG, DEPTH, 2>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh,
+                               Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+        else
+            hipLaunchKernelGGL((k_mf_backproject_b16<NG, DEPTH, 1>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh,
+                               Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+    }
 }
 
-template <int NG>
-static void bwd_b16(int depth, int vt, dim3 grid, hipStream_t stream, const bf16_t* A, int64_t ld, int64_t nrows32,
+template <int NG, typename AT>
+static void bwd_b16(int depth, int vt, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows32,
                     const bf16_t* Wh, const bf16_t* Wl, int64_t ldw, int64_t rps, float* partial, int64_t vb0,
                     int64_t vend) {
-    if (depth == 1)
-        bwd_b16_d<NG, 1>(vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend);
-    else if (depth == 2)
+    if constexpr (!std::is_same<AT, float>::value) {
+        if (depth == 1) {
+            bwd_b16_d<NG, 1>(vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend);
+            return;
+        }
+    }
+    if (depth <= 2)
         bwd_b16_d<NG, 2>(vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend);
     else
         bwd_b16_d<NG, 3>(vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend);
 }
 
-void launch_mf_backproject_b16(const bf16_t* A, int64_t ld, int64_t nrows, const bf16_t* Wh, const bf16_t* Wl,
-                               int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0,
-                               int64_t v1) {
-    if (ld % 64 != 0) throw std::runtime_error("mf_backproject_b16: ld must be a multiple of 64");
-    check_nf_b16(nf, "mf_backproject_b16");
+template <typename AT>
+static void launch_mf_backproject_split(const AT* A, int64_t ld, int64_t nrows, const bf16_t* Wh, const bf16_t* Wl,
+                                        int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream,
+                                        int64_t v0, int64_t v1) {
+    constexpr bool A32 = std::is_same<AT, float>::value;
+    const std::string what = A32 ? "mf_backproject_x3" : "mf_backproject_b16";
+    if (ld % 64 != 0) throw std::runtime_error(what + ": ld must be a multiple of 64");
+    check_nf_b16(nf, what.c_str());
     const int64_t nrows32 = (nrows + 31) / 32 * 32;
     if (ldw < nrows32 || ldw % 8 != 0)
-        throw std::runtime_error("mf_backproject_b16: W planes must hold the rows rounded up to 32 (ldw % 8 == 0)");
+        throw std::runtime_error(what + ": W planes must hold the rows rounded up to 32 (ldw % 8 == 0)");
     if (v1 < 0) v1 = ld;
-    const int vt = mf_b16_vt(ld, nf);
+    const int vt = A32 ? mf_x3_vt(ld) : mf_b16_vt(ld, nf);
     const int64_t align = 64 * vt;
     if (v0 < 0 || v1 > ld || v0 >= v1 || v0 % align != 0 || v1 % align != 0)
-        throw std::runtime_error("mf_backproject_b16: voxel range must be aligned to the wave's voxel tile");
-    if (nsplit < 1) throw std::runtime_error("mf_backproject_b16: nsplit must be >= 1");
+        throw std::runtime_error(what + ": voxel range must be aligned to the wave's voxel tile");
+    if (nsplit < 1) throw std::runtime_error(what + ": nsplit must be >= 1");
     const int64_t rps = ((nrows32 + nsplit - 1) / nsplit + 31) / 32 * 32;
     const int64_t vw0 = v0 / align, nvw = (v1 - v0) / align;  // wave tiles
     const dim3 grid((unsigned)((nvw + 3) / 4), (unsigned)nsplit);
-    const int d = mf_b16_depth(false, nf);
+    const int d = A32 ? mf_x3_depth(false) : mf_b16_depth(false, nf);
     if (nf == 16)
         bwd_b16<1>(d, vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vw0, v1);
     else if (nf == 32)
         bwd_b16<2>(d, vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vw0, v1);
     else
         bwd_b16<4>(d, vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vw0, v1);
-    check_launch("k_mf_backproject_b16");
+    check_launch(A32 ? "k_mf_backproject_x3" : "k_mf_backproject_b16");
+}
+
+void launch_mf_backproject_b16(const bf16_t* A, int64_t ld, int64_t nrows, const bf16_t* Wh, const bf16_t* Wl,
+                               int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0,
+                               int64_t v1) {
+    launch_mf_backproject_split(A, ld, nrows, Wh, Wl, ldw, nsplit, partial, nf, stream, v0, v1);
+}
+
+void launch_mf_backproject_x3(const float* A, int64_t ld, int64_t nrows, const bf16_t* Wh, const bf16_t* Wl,
+                              int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0,
+                              int64_t v1) {
+    launch_mf_backproject_split(A, ld, nrows, Wh, Wl, ldw, nsplit, partial, nf, stream, v0, v1);
 }
 
 }  // namespace sart

@@ -228,9 +228,11 @@ __device__ __forceinline__ void split_bf16(float x, uint32_t key, bf16_t& hi, bf
     lo = (bf16_t)((__float_as_uint(x - (float)h) + (r & 0xffffu)) >> 16);
 }
 
-// X [nf][ld] fp32 -> planes of the same layout (n % 4 == 0).
+// X [nf][ld] fp32 -> planes of the same layout (n % 4 == 0). perm (the split-A forward, multiframe_bf16.hip):
+// within every block of 32 voxels, plane position 8 g + j holds voxel 4 g + j (j < 4) or 16 + 4 g + j - 4, the
+// k order in which that kernel's lanes load A as two contiguous 64-byte halves of a row.
 __global__ __launch_bounds__(256) void k_mf_split_x(const float* __restrict__ X, int64_t n4, bf16_t* __restrict__ hi,
-                                                    bf16_t* __restrict__ lo, const int* __restrict__ skip) {
+                                                    bf16_t* __restrict__ lo, const int* __restrict__ skip, int perm) {
     if (skip && *skip) return;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n4) return;
@@ -241,15 +243,19 @@ __global__ __launch_bounds__(256) void k_mf_split_x(const float* __restrict__ X,
     split_bf16(v.y, key + 1, h[1], l[1]);
     split_bf16(v.z, key + 2, h[2], l[2]);
     split_bf16(v.w, key + 3, h[3], l[3]);
-    reinterpret_cast<uint2*>(hi)[i] = make_uint2(h[0] | (unsigned)h[1] << 16, h[2] | (unsigned)h[3] << 16);
-    reinterpret_cast<uint2*>(lo)[i] = make_uint2(l[0] | (unsigned)l[1] << 16, l[2] | (unsigned)l[3] << 16);
+    const int64_t o = perm ? ((i & ~(int64_t)7) | ((i & 3) << 1) | ((i >> 2) & 1)) : i;
+    reinterpret_cast<uint2*>(hi)[o] = make_uint2(h[0] | (unsigned)h[1] << 16, h[2] | (unsigned)h[3] << 16);
+    reinterpret_cast<uint2*>(lo)[o] = make_uint2(l[0] | (unsigned)l[1] << 16, l[2] | (unsigned)l[3] << 16);
 }
 
 // W [rows][16][nf / 16] (back-projection layout, mf_bp_slot) -> frame-major planes [nf][ldw]: 64 rows per block
 // through an LDS tile, so both the reads and the 128-byte plane writes are coalesced.
+// three (the split-A back-projection): hi, mid = rne(w - hi) at hi + nf * ldw and lo = rne(w - hi - mid), so
+// hi + mid + lo holds w to 2^-27: the weights are residuals of both signs whose back-projection cancels, and the
+// 2^-17 of a two-piece split would show at full size in A^T W (fp32 keeps w exact).
 __global__ __launch_bounds__(256) void k_mf_split_w(const float* __restrict__ W, int64_t nrows_pad, int nf,
                                                     int64_t ldw, bf16_t* __restrict__ hi, bf16_t* __restrict__ lo,
-                                                    const int* __restrict__ skip) {
+                                                    const int* __restrict__ skip, int three) {
     if (skip && *skip) return;
     __shared__ float tile[64][kMaxNF + 1];
     const int64_t r0 = (int64_t)blockIdx.x * 64;
@@ -261,8 +267,19 @@ __global__ __launch_bounds__(256) void k_mf_split_w(const float* __restrict__ W,
     for (int i = threadIdx.x; i < 64 * nf; i += 256) {
         const int f = i / 64, rr = i % 64;
         if (r0 + rr >= ldw) continue;
+        const float w = tile[rr][mf_bp_slot(f, nf)];
         bf16_t h, l;
-        split_bf16(tile[rr][mf_bp_slot(f, nf)], (uint32_t)((int64_t)f * ldw + r0 + rr), h, l);
+        if (three) {
+            const __bf16 h1 = (__bf16)w;
+            const float r1 = w - (float)h1;
+            const __bf16 m1 = (__bf16)r1;
+            const __bf16 l1 = (__bf16)(r1 - (float)m1);
+            h = __builtin_bit_cast(bf16_t, h1);
+            l = __builtin_bit_cast(bf16_t, l1);
+            hi[(int64_t)(nf + f) * ldw + r0 + rr] = __builtin_bit_cast(bf16_t, m1);
+        } else {
+            split_bf16(w, (uint32_t)((int64_t)f * ldw + r0 + rr), h, l);
+        }
         hi[(int64_t)f * ldw + r0 + rr] = h;
         lo[(int64_t)f * ldw + r0 + rr] = l;
     }
@@ -430,18 +447,19 @@ void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, 
     check_launch("k_mf_state_begin");
 }
 
-void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStream_t stream) {
-    if (n % 4 != 0) throw std::runtime_error("mf_split_x: length must be a multiple of 4");
-    hipLaunchKernelGGL(k_mf_split_x, dim3(std::max<unsigned>(1, nb(n / 4))), dim3(256), 0, stream, X, n / 4, hi, lo, g_mf_skip);
+void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStream_t stream, bool perm) {
+    if (n % (perm ? 32 : 4) != 0) throw std::runtime_error("mf_split_x: length must be a multiple of 4 (32 permuted)");
+    hipLaunchKernelGGL(k_mf_split_x, dim3(std::max<unsigned>(1, nb(n / 4))), dim3(256), 0, stream, X, n / 4, hi, lo, g_mf_skip,
+                       (int)perm);
     check_launch("k_mf_split_x");
 }
 
 void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, bf16_t* hi, bf16_t* lo,
-                       hipStream_t stream) {
+                       hipStream_t stream, bool three) {
     check_nf(nf, "mf_split_w");
     if (ldw > nrows_pad) throw std::runtime_error("mf_split_w: plane stride exceeds the padded rows");
     hipLaunchKernelGGL(k_mf_split_w, dim3((unsigned)((ldw + 63) / 64)), dim3(256), 0, stream, W, nrows_pad, nf, ldw,
-                       hi, lo, g_mf_skip);
+                       hi, lo, g_mf_skip, (int)three);
     check_launch("k_mf_split_w");
 }
 

@@ -4,7 +4,8 @@ The reference solves the time series strictly frame by frame (reference main.cpp
 the RTM twice per iteration per frame. For throughput on long time series (BASELINE.json config 5),
 frames can be batched: the forward and back projections become skinny GEMMs ``A.X`` / ``A^T.W`` with
 16, 32 or 64 right-hand sides (csrc/kernels/multiframe.hip, ``v_mfma_f32_16x16x4_f32`` on 1, 2 or 4
-column groups), reading A twice per iteration for the whole batch. Every frame keeps its own normalisation,
+column groups; at 32 / 64 frames A is split into hi + lo bf16 in registers for the bf16 matrix cores,
+csrc/kernels/multiframe_bf16.hip), reading A twice per iteration for the whole batch. Every frame keeps its own normalisation,
 saturation mask, convergence history, iteration count and status. The batch's columns are slots with
 continuous batching: as soon as a frame finishes, its slot takes the next frame between two sweeps, so no
 sweep is spent on finished frames while frames wait. Frames are cold-started (``--no_guess``), or started as a
@@ -36,7 +37,7 @@ MAX_BATCH = 64  # widest batch: 4 column groups
 class MultiFrameSARTSolver:
     def __init__(self, rtm: DenseRTM, laplacian: Optional[LaplacianCSR] = None, comm: Optional[Communicator] = None,
                  params: Optional[SolverParams] = None, logarithmic: bool = False, batch: int = NF,
-                 check_interval: int = 16, allow_zero_tolerance: bool = False):
+                 check_interval: int = 16, allow_zero_tolerance: bool = False, split_a: Optional[bool] = None):
         if getattr(rtm, "is_column_shard", False):
             raise NotImplementedError("the multi-frame engine runs on row shards (use SARTSolver for column shards)")
         self.k = hip()
@@ -63,6 +64,9 @@ class MultiFrameSARTSolver:
         cfg.check_interval = max(1, int(check_interval))
         cfg.mf_frames = self.batch
         cfg.rtm_bf16 = bool(getattr(rtm, "is_bf16", False))  # bf16 storage: bf16 MFMA projections
+        # fp32 storage: fp32 MFMA, or A split into hi + lo bf16 on the bf16 matrix cores (None: the engine's
+        # default, on for batches of 32 / 64 frames, env SART_MF_X3)
+        cfg.mf_split_a = -1 if split_a is None else int(bool(split_a))
         device = self.dev.index if self.dev.index is not None else 0
         self.native_comm = native_communicator(self.comm, device)
         self.engine = self.k.MultiFrameEngine(device, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld,
@@ -71,6 +75,7 @@ class MultiFrameSARTSolver:
             self.engine.set_laplacian(self.L.row_ptr_host, self.L.col_host, self.L.val_host)
         self.P, self.Pp, self.V, self.ld = rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld
         self.batch_width = int(self.engine.batch_frames)  # 16, 32 or 64 columns on the matrix cores
+        self.split_a = bool(self.engine.split_a)
 
     def solve_batch(self, measurements, x0=None, chain: bool = False) -> List[SolveResult]:
         """Frames [nframes, local pixels] through ``batch_width`` slots with continuous batching: a slot whose

@@ -54,6 +54,15 @@ def test_split_planes(k, dev):
     err = (hi.double() + lo.double() - same.double()).mean().item() / 1.2345678
     assert abs(err) < 2.0 ** -22, err
 
+    # the split-A k order: position 8 g + j of every 32-block holds element 4 g + j (j < 4) or 16 + 4 g + j - 4
+    hp, lp = torch.empty_like(hi), torch.empty_like(lo)
+    k.mf_split_x(x.data_ptr(), 4096, hi.data_ptr(), lo.data_ptr(), _stream(dev))
+    k.mf_split_x(x.data_ptr(), 4096, hp.data_ptr(), lp.data_ptr(), _stream(dev), True)
+    torch.cuda.synchronize()
+    src = np.array([32 * b + (4 * (p // 8) + p % 8 if p % 8 < 4 else 16 + 4 * (p // 8) + p % 8 - 4)
+                    for b in range(128) for p in range(32)])
+    assert torch.equal(hp.cpu(), hi.cpu()[src]) and torch.equal(lp.cpu(), lo.cpu()[src])
+
     nf, rows, ldw = 32, 192, 160
     W = torch.from_numpy(rng.random((rows, nf)).astype(np.float32)).to(dev)  # [rows][16][nf / 16] layout
     wh = torch.zeros((nf, ldw), dtype=torch.bfloat16, device=dev)
@@ -166,3 +175,91 @@ def test_multiframe_bf16_matches_fp32_engine_on_rounded_matrix():
         xs.append(np.stack([r.solution for r in s.solve_batch(G)]))
     rel = np.linalg.norm(xs[1] - xs[0]) / np.linalg.norm(xs[0])
     assert rel < 1e-3, rel  # fp32 summation-order noise over 30 iterations (measured 2.6e-4)
+
+
+# ------------------------------------------------------------------ split-A: fp32 A on the bf16 matrix cores
+@pytest.mark.parametrize("fwd,vt,depth", [("", "", ""), ("2,1", "1", "3"), ("2,2", "2", "2"), ("4,2", "2", "3")])
+@pytest.mark.parametrize("nf", [16, 32, 64])
+@pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (64, 1024), (2048, 4096), (1000, 1088)])
+def test_split_a_projections(k, dev, P, V, nf, fwd, vt, depth, monkeypatch):
+    """fp32 A split in registers into bf16 pieces (forward: hi + lo, three products; back-projection: hi + mid +
+    lo, six products) against fp64 products of the fp32 matrix: fp32 MFMA accuracy, unlike bf16 storage (whose
+    tests compare against the rounded matrix)."""
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+
+    for name, val in (("SART_MF_X3_FWD", fwd), ("SART_MF_X3_VT", vt), ("SART_MF_X3_DEPTH", depth)):
+        if val:
+            monkeypatch.setenv(name, val)
+    rng = np.random.default_rng(P * 7 + V)
+    A = rng.random((P, V), dtype=np.float32)
+    m = DenseRTM.from_dense(A, device=dev)
+    Ad = A.astype(np.float64)
+    X = rng.random((nf, V)).astype(np.float32)
+    Xd = torch.zeros((nf, m.ld), device=dev)
+    Xd[:, :V] = torch.from_numpy(X)
+    Xh = torch.empty((nf, m.ld), dtype=torch.bfloat16, device=dev)
+    Xl = torch.empty_like(Xh)
+    k.mf_split_x(Xd.data_ptr(), nf * m.ld, Xh.data_ptr(), Xl.data_ptr(), _stream(dev), True)  # the x3 k order
+    nsf = 3 if m.ld > 1024 else 1
+    Fo3 = torch.zeros((nsf, m.nrows_pad, nf), device=dev)
+    k.mf_forward_x3(m.A.data_ptr(), m.ld, P, m.nrows_pad, Xh.data_ptr(), Xl.data_ptr(), Fo3.data_ptr(), nsf,
+                    _stream(dev), nf)
+    W = (rng.random((P, nf)) - 0.5).astype(np.float32)
+    Wd = torch.zeros((m.nrows_pad, nf), device=dev)
+    Wd[:P] = torch.from_numpy(np.ascontiguousarray(W.reshape(P, nf // 16, 16).transpose(0, 2, 1).reshape(P, nf)))
+    Wh = torch.zeros((2, nf, m.nrows_pad), dtype=torch.bfloat16, device=dev)  # hi, mid
+    Wl = torch.zeros((nf, m.nrows_pad), dtype=torch.bfloat16, device=dev)
+    k.mf_split_w(Wd.data_ptr(), m.nrows_pad, nf, m.nrows_pad, Wh.data_ptr(), Wl.data_ptr(), _stream(dev), True)
+    ns = 3
+    part = torch.zeros((ns, m.ld, nf), device=dev)
+    align = k.mf_backproject_b16_vox_align(m.ld, True)
+    vmid = (m.ld // 2) // align * align
+    chunks = ((0, vmid), (vmid, m.ld)) if vmid > 0 else ((0, m.ld),)
+    for v0, v1 in chunks:
+        k.mf_backproject_x3(m.A.data_ptr(), m.ld, P, Wh.data_ptr(), Wl.data_ptr(), m.nrows_pad, ns, part.data_ptr(),
+                            _stream(dev), nf, v0, v1)
+    torch.cuda.synchronize()
+    F_ref = Ad @ X.T.astype(np.float64)
+    F = Fo3.sum(0)[:P].double().cpu().numpy()
+    assert np.linalg.norm(F - F_ref) / np.linalg.norm(F_ref) < 2e-6
+    np.testing.assert_allclose(F, F_ref, rtol=2e-5, atol=2e-4)
+    B_ref = Ad.T @ W.astype(np.float64)
+    B = part.sum(0)[:V].double().cpu().numpy()
+    # signed weights cancel in A^T W: three-piece A and W keep the error at fp32 level (measured ~2e-7)
+    assert np.linalg.norm(B - B_ref) / np.linalg.norm(B_ref) < 1e-6
+    np.testing.assert_allclose(B, B_ref, rtol=1e-4, atol=5e-5)
+
+
+@pytest.mark.parametrize("batch", [32, 64])
+@pytest.mark.parametrize("iters", [1, 20])
+def test_split_a_engine_matches_fp32_mfma(batch, iters):
+    """The same fp32 shard through fp32 MFMA and through split-A bf16 MFMA, both against the fp64 oracle: the
+    split-A error is that of the fp32 engine (after 1 iteration: the kernels; after 20: the fp32 drift of an
+    ill-conditioned dense random matrix, which differs between summation orders by ~3e-4 either way). The split-A
+    engine is the default at 32 / 64 frames."""
+    from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SolverParams
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(batch + iters)
+    P, V, nframes = 1024, 2048, batch
+    A = rng.random((P, V), dtype=np.float32)
+    rf = DenseRTM.from_dense(A, device=dev)
+    G = (rng.random((nframes, V)) + 0.1) @ A.T.astype(np.float64)
+    kw = dict(max_iterations=iters, conv_tolerance=0.0)
+    xs = {}
+    for split in (False, True):
+        s = MultiFrameSARTSolver(rf, None, None, SolverParams(**kw), batch=batch, allow_zero_tolerance=True,
+                                 split_a=split)
+        assert s.split_a == split
+        xs[split] = np.stack([r.solution for r in s.solve_batch(G)])
+    assert MultiFrameSARTSolver(rf, None, None, SolverParams(**kw), batch=batch, allow_zero_tolerance=True).split_a
+    assert not MultiFrameSARTSolver(rf, None, None, SolverParams(**kw), batch=16, allow_zero_tolerance=True).split_a
+    frames = (0, 1, nframes // 2, nframes - 1)
+    ref = np.stack([sart_gpu_semantics(A, G[f], None, logarithmic=False, **kw)[0]
+                    for f in frames])
+    err = {k: np.linalg.norm(v[list(frames)] - ref) / np.linalg.norm(ref) for k, v in xs.items()}
+    print("rel vs fp64 oracle: fp32 MFMA %.3g, split-A %.3g" % (err[False], err[True]))
+    assert err[True] <= 1.5 * err[False] + 1e-6, err

@@ -36,6 +36,10 @@ for step in "$@"; do
     series) run series_fp32 600 python tools/series_bench.py --tol ${SERIES_TOL:-1e-8} &&
             run series_bf16 600 python tools/series_bench.py --dtype bf16 --batch 32 --tol ${SERIES_TOL:-1e-8} ;;
     probemfb) run probe_mfb16 900 python tools/probe_mf_b16.py ;;
+    probemfx3) run probe_mfx3 900 python tools/probe_mf_x3.py ;;
+    benchmfx3) run bench_mfx32 600 python bench.py --steps 3 --warmup 1 --frames 32 &&
+               run bench_mfx64 600 python bench.py --steps 3 --warmup 1 --frames 64 &&
+               run bench_mff64 600 python bench.py --steps 3 --warmup 1 --frames 64 --mf-split-a off ;;
     probemfbv) PROBE_DEPTH=2,3 PROBE_FWD="2,2,lds;4,2,lds" run probe_mfb_bwd 900 python tools/probe_mf_b16.py ;;
     probemfbl) PROBE_BWD=0 PROBE_DEPTH=2,3 PROBE_FWD="4,2;8,1;4,1,lds;4,2,lds;8,1,lds;2,2,lds" \
                  run probe_mfb_lds 900 python tools/probe_mf_b16.py ;;
