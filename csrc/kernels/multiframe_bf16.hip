@@ -222,7 +222,14 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
 // R = 64 RT rows per wave -> per workgroup), which is what bounds the register-operand forward at 32 / 64
 // frames (profiles/probe_r2_mf_b16.jsonl). One barrier per step; waves past the padded rows clamp to the last
 // row tile (they take part in the X staging and barriers, and store nothing).
-template <int NG, int DEPTH, int RT, int KB, typename AT = bf16_t>
+//
+// AS (A staged): a fragment-shaped load (lane (r, g) = 16 B of row r) touches 16 rows x 64 B per instruction,
+// half lines, twice the address-path work per byte of the back-projection's row loads. With AS each wave loads
+// its A tile in full 128-B row segments (R16 lanes per row, 64 / R16 rows per instruction), writes it to a
+// wave-private LDS image with the 16-B slot XOR-swizzled by (row & 7) (slot row * R16 + (seg ^ (row & 7)): the
+// 16 lanes that read one fragment column hit 8 different bank groups), and reads the fragments back with
+// ds_read_b128. Same in-order LDS queue for the write and the read of one wave: no barrier.
+template <int NG, int DEPTH, int RT, int KB, typename AT = bf16_t, bool AS = false>
 __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const AT* __restrict__ A, int64_t ld, int64_t nrows,
                                                             int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                             const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
@@ -249,6 +256,12 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const AT* __restrict
     const int64_t xo = (int64_t)r * ld + c0 + 8 * g;
     const int lofs = r * 4 + g;  // uint4 slot of (frame r, voxels 8 g..) inside a 1 KiB piece
     typedef typename ARaw<AT>::fwd AF;
+    constexpr int R16 = 32 * KB * (int)sizeof(AT) / 16;  // 16-B slots per row and step (AS)
+    constexpr int RPI = 64 / R16;                         // rows per staging load instruction
+    constexpr int NI = 16 * RT / RPI;                     // staging loads per step and wave
+    static_assert(!AS || R16 >= 8, "A staging needs full 128-B row segments");
+    __shared__ __attribute__((aligned(16))) u32x4 s_a[AS ? 4 : 1][AS ? 16 * RT * R16 : 1];
+    const AT* __restrict__ asp = A + (row0 + lane / R16) * ld + c0 + (lane % R16) * (16 / (int)sizeof(AT));
 
     floatx4 acc[RT][NG];
 #pragma unroll
@@ -258,12 +271,18 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const AT* __restrict
 
     const int64_t nst = c1 > c0 ? (c1 - c0) / (32 * KB) : 0;  // uniform for the workgroup
     if (nst > 0) {
-        AF a[RS][RT][KB];
+        AF a[AS ? 1 : RS][RT][KB];
+        u32x4 as_[AS ? RS : 1][NI];
         u32x4 xq[RS][XQ];
         auto piece = [&](int i) { return (C >= 4 ? wave * XQ + i : wave % C); };  // piece = (kb * 2 + plane) * NG + j
         auto load = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
             const int64_t q = t * 32 * KB;
+            if constexpr (AS) {
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+                    as_[sl][i] = *reinterpret_cast<const u32x4*>(asp + (int64_t)i * RPI * ld + q);
+            } else {
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -277,6 +296,7 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const AT* __restrict
                         a[sl][rt][kb] = *reinterpret_cast<const AF*>(ap + rt * 16 * ld + q + 32 * kb);
                     }
                 }
+            }
 #pragma unroll
             for (int i = 0; i < XQ; ++i) {
                 const int pc = piece(i), j = pc % NG, plane = (pc / NG) & 1, kb = pc / (2 * NG);
@@ -299,12 +319,30 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const AT* __restrict
             if (t >= nst) return;  // uniform for the workgroup
             stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);  // X of step t + 1 into the other stage (its readers passed the last barrier)
             const u32x4* xs = s_x[t & 1][0] + lofs;
+            u32x4* img = s_a[AS ? wave : 0];
+            if constexpr (AS) {  // this wave's tile into its LDS image (swizzled slots)
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    const int row = i * RPI + lane / R16;
+                    img[row * R16 + ((lane % R16) ^ (row & 7))] = as_[sl][i];
+                }
+            }
+            // fragment of tile row block rt, k block kb: (bf16) 8 consecutive voxels; (fp32) the two 16-B halves
+            // of the permuted k order
+            auto frag16 = [&](int rt, int seg) { return img[(rt * 16 + r) * R16 + (seg ^ (r & 7))]; };
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb) {
                 if constexpr (A32) {
                     u32x4 ah[RT], al[RT];
 #pragma unroll
-                    for (int rt = 0; rt < RT; ++rt) split_a8(a[sl][rt][kb], ah[rt], al[rt]);
+                    for (int rt = 0; rt < RT; ++rt) {
+                        if constexpr (AS)
+                            split_a8(__builtin_shufflevector(frag16(rt, kb * 8 + g), frag16(rt, kb * 8 + 4 + g), 0, 1,
+                                                             2, 3, 4, 5, 6, 7),
+                                     ah[rt], al[rt]);
+                        else
+                            split_a8(a[sl][rt][kb], ah[rt], al[rt]);
+                    }
                     u32x4 xh[NG], xl[NG];
 #pragma unroll
                     for (int j = 0; j < NG; ++j) {
@@ -324,6 +362,20 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const AT* __restrict
                     for (int j = 0; j < NG; ++j)
 #pragma unroll
                         for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(ah[rt], xh[j], acc[rt][j]);
+                } else if constexpr (AS) {
+                    u32x4 af[RT];
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt) af[rt] = frag16(rt, kb * 4 + g);
+#pragma unroll
+                    for (int j = 0; j < NG; ++j) {
+                        const u32x4 xh = xs[((kb * 2 + 0) * NG + j) * 64];
+                        const u32x4 xl = xs[((kb * 2 + 1) * NG + j) * 64];
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt) {
+                            acc[rt][j] = mfma_b16(af[rt], xh, acc[rt][j]);
+                            acc[rt][j] = mfma_b16(af[rt], xl, acc[rt][j]);
+                        }
+                    }
                 } else {
 #pragma unroll
                     for (int j = 0; j < NG; ++j) {
@@ -619,6 +671,7 @@ static int mf_b16_depth(bool forward, int nf) {
 struct FwdTile {
     int rt, kb;
     bool lds = false;  // X shared through LDS (k_mf_forward_b16_lds)
+    bool as = false;   // A staged through LDS in full row segments (LDS kernel, 128-B rows: bf16 KB = 2, fp32)
 };
 static FwdTile mf_b16_fwd_tile(int nf) {
     const char* e = std::getenv("SART_MF_B16_FWD");
@@ -626,9 +679,12 @@ static FwdTile mf_b16_fwd_tile(int nf) {
         // "RT,KB" or "RT,KB,lds"
         FwdTile t{std::atoi(e), std::strchr(e, ',') ? std::atoi(std::strchr(e, ',') + 1) : 1};
         t.lds = std::strstr(e, "lds") != nullptr;
+        t.as = std::strstr(e, "as") != nullptr;  // "RT,2,lds,as": A staged through LDS (KB = 2 only)
         if ((t.rt == 2 || t.rt == 4 || t.rt == 8) && (t.kb == 1 || t.kb == 2)) return t;
     }
-    return nf == 16 ? FwdTile{2, 2, true} : FwdTile{4, 2, true};  // profiles/probe_r2_mf_b16_lds.jsonl
+    // profiles/probe_r2_mf_b16_lds.jsonl, profiles/probe_r2_mf_as.jsonl (A staged: +9 % at 32 frames, a tie at 16 / 64)
+    if (nf == 32) return FwdTile{2, 2, true, true};
+    return nf == 16 ? FwdTile{2, 2, true} : FwdTile{4, 2, true};
 }
 
 static int mf_b16_vt(int64_t ld, int nf) {
@@ -648,16 +704,21 @@ static bool mf_b16_bwd_lds(int nf) {
 }
 
 template <int NG, int DEPTH, int RT, int KB, typename AT>
-static void fwd_b16_t(bool lds, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows,
+static void fwd_b16_t(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows,
                       int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
-    if constexpr (std::is_same<AT, float>::value) {
-        (void)lds;  // split-A: the LDS kernels only
-        hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB, float>), grid, dim3(256), 0, stream, A, ld, nrows,
+    constexpr bool A32 = std::is_same<AT, float>::value;
+    constexpr bool CAN_AS = A32 || KB == 2;  // full 128-B row segments per step
+    if constexpr (CAN_AS) {
+        if (tl.as) {
+            hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB, AT, true>), grid, dim3(256), 0, stream, A, ld,
+                               nrows, nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
+            return;
+        }
+    }
+    if (A32 || tl.lds) {  // split-A: the LDS kernels only
+        hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB, AT>), grid, dim3(256), 0, stream, A, ld, nrows,
                            nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
-    } else if (lds) {
-        hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB>), grid, dim3(256), 0, stream, A, ld, nrows,
-                           nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
-    } else {
+    } else if constexpr (!A32) {
         hipLaunchKernelGGL((k_mf_forward_b16<NG, DEPTH, RT, KB>), grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad,
                            Xh, Xl, Fout, cps, g_mf_skip);
     }
@@ -667,18 +728,18 @@ template <int NG, int DEPTH, typename AT>
 static void fwd_b16_d(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows,
                       int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
     if (tl.rt == 2 && tl.kb == 2)
-        fwd_b16_t<NG, DEPTH, 2, 2>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+        fwd_b16_t<NG, DEPTH, 2, 2>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else if (tl.rt == 4 && tl.kb == 2)
-        fwd_b16_t<NG, DEPTH, 4, 2>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+        fwd_b16_t<NG, DEPTH, 4, 2>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else if (tl.rt == 2)
-        fwd_b16_t<NG, DEPTH, 2, 1>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+        fwd_b16_t<NG, DEPTH, 2, 1>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else if constexpr (!std::is_same<AT, float>::value) {
         if (tl.rt == 8)
-            fwd_b16_t<NG, DEPTH, 8, 1>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+            fwd_b16_t<NG, DEPTH, 8, 1>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
         else
-            fwd_b16_t<NG, DEPTH, 4, 1>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+            fwd_b16_t<NG, DEPTH, 4, 1>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     } else {
-        fwd_b16_t<NG, DEPTH, 4, 1>(tl.lds, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
+        fwd_b16_t<NG, DEPTH, 4, 1>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     }
 }
 
@@ -703,9 +764,11 @@ static FwdTile mf_x3_fwd_tile(int nf) {
     const char* e = std::getenv("SART_MF_X3_FWD");
     if (e && *e) {
         FwdTile t{std::atoi(e), std::strchr(e, ',') ? std::atoi(std::strchr(e, ',') + 1) : 1, true};
+        t.as = std::strstr(e, "as") != nullptr;  // "RT,KB,as": A staged through LDS
         if ((t.rt == 2 || t.rt == 4) && (t.kb == 1 || t.kb == 2)) return t;
     }
-    return nf == 64 ? FwdTile{4, 1, true} : FwdTile{2, 2, true};  // profiles/probe_r2_mf_x3.jsonl
+    // profiles/probe_r2_mf_x3.jsonl, profiles/probe_r2_mf_as.jsonl
+    return nf == 64 ? FwdTile{2, 1, true, true} : FwdTile{2, 2, true};
 }
 static int mf_x3_depth(bool forward) {
     const int d = env_int("SART_MF_X3_DEPTH", 0);
@@ -727,7 +790,7 @@ static void launch_mf_forward_split(const AT* A, int64_t ld, int64_t nrows, int6
     check_nf_b16(nf, what);
     if (nrows_pad % 32 != 0) throw std::runtime_error(std::string(what) + ": padded rows must be a multiple of 32");
     FwdTile tl = A32 ? mf_x3_fwd_tile(nf) : mf_b16_fwd_tile(nf);
-    if (nrows_pad % (16 * tl.rt) != 0) tl = FwdTile{2, 1, tl.lds};  // a wave's rows must lie inside the padding
+    if (nrows_pad % (16 * tl.rt) != 0) tl = FwdTile{2, 1, tl.lds, A32 && tl.as};  // a wave's rows inside the padding
     const int64_t cps = ((ld + nsplit - 1) / nsplit + 63) / 64 * 64;
     const int64_t rows_per_block = 64 * tl.rt;
     const dim3 grid((unsigned)((nrows_pad + rows_per_block - 1) / rows_per_block), (unsigned)nsplit);

@@ -79,7 +79,8 @@ def test_split_planes(k, dev):
 
 # (SART_MF_B16_FWD, SART_MF_B16_VT) tiles: register-operand and LDS-shared variants of both kernels
 @pytest.mark.parametrize("fwd,bwd", [("", ""), ("4,1", "1,reg"), ("8,1", "2,reg"), ("4,2,lds", "1,lds"),
-                                     ("8,1,lds", "2,lds"), ("2,2,lds", "2,lds")])
+                                     ("8,1,lds", "2,lds"), ("2,2,lds", "2,lds"), ("4,2,lds,as", "2,lds"),
+                                     ("2,2,lds,as", "1,lds")])
 @pytest.mark.parametrize("nf", [16, 32, 64])
 @pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (64, 1024), (2048, 4096), (1000, 1088)])
 def test_bf16_mfma_projections(k, dev, P, V, nf, fwd, bwd, monkeypatch):
@@ -178,7 +179,8 @@ def test_multiframe_bf16_matches_fp32_engine_on_rounded_matrix():
 
 
 # ------------------------------------------------------------------ split-A: fp32 A on the bf16 matrix cores
-@pytest.mark.parametrize("fwd,vt,depth", [("", "", ""), ("2,1", "1", "3"), ("2,2", "2", "2"), ("4,2", "2", "3")])
+@pytest.mark.parametrize("fwd,vt,depth", [("", "", ""), ("2,1", "1", "3"), ("2,2", "2", "2"), ("4,2", "2", "3"),
+                                           ("4,1,as", "1", "2"), ("2,2,as", "1", "3"), ("2,1,as", "2", "2")])
 @pytest.mark.parametrize("nf", [16, 32, 64])
 @pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (64, 1024), (2048, 4096), (1000, 1088)])
 def test_split_a_projections(k, dev, P, V, nf, fwd, vt, depth, monkeypatch):

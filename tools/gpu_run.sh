@@ -37,6 +37,10 @@ for step in "$@"; do
             run series_bf16 600 python tools/series_bench.py --dtype bf16 --batch 32 --tol ${SERIES_TOL:-1e-8} ;;
     probemfb) run probe_mfb16 900 python tools/probe_mf_b16.py ;;
     probemfx3) run probe_mfx3 900 python tools/probe_mf_x3.py ;;
+    probeas) PROBE_DEPTH=2,3 PROBE_BWD=0 PROBE_FWD="2,2,lds;4,2,lds;2,2,lds,as;4,2,lds,as" \
+               run probe_mfb_as 900 python tools/probe_mf_b16.py &&
+             PROBE_FP32=0 PROBE_VT=1 PROBE_FWD="4,1;2,2;4,1,as;2,2,as;2,1,as;4,2,as" \
+               run probe_mfx3_as 900 python tools/probe_mf_x3.py ;;
     benchmfx3) run bench_mfx32 600 python bench.py --steps 3 --warmup 1 --frames 32 &&
                run bench_mfx64 600 python bench.py --steps 3 --warmup 1 --frames 64 &&
                run bench_mff64 600 python bench.py --steps 3 --warmup 1 --frames 64 --mf-split-a off ;;
