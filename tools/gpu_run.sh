@@ -56,6 +56,8 @@ for step in "$@"; do
     mfdepth) for d in 1 2 3; do for nf in 16 32 64; do
                SART_MF_DEPTH=$d run bench_mf${nf}_d$d 300 python bench.py --steps 2 --warmup 1 --frames $nf --iters 50 || exit 1
              done; done ;;
+    profx3) run rocprof_x3_64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_x3_64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 &&
+            run rocprof_x3_32 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_x3_32" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 32 --iters 20 ;;
     profmfb) for nf in 16 64; do
               run rocprof_mfb$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 --rtm-dtype bf16 || exit 1
             done ;;
