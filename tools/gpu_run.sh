@@ -97,6 +97,7 @@ for step in "$@"; do
                      --rtm-dtype bf16 --npix 524288 --nvox 262144 --iters 20 ;;
     benchlap) run bench_lap 600 python bench.py --steps 5 --warmup 1 --laplacian ;;
     probe) run probe 600 python tools/probe.py ;;
+    probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
             run fcheck_fp32 600 python tools/fused_check.py 8192x262144 65536x262144 16384x65536 ;;
