@@ -30,6 +30,7 @@
 #include "sart_common.hpp"
 #include "launchers.hpp"
 
+#include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
 #include <utility>
@@ -374,7 +375,7 @@ __device__ __forceinline__ void split_pair(float a, float b, uint32_t key, unsig
 }
 
 // Schedules with a separate publisher wave (the split exchange)
-constexpr bool sched_split(int sched) { return sched == 4 || sched == 5 || sched == 6; }
+constexpr bool sched_split(int sched) { return sched == 4 || sched == 5 || sched == 6 || sched == 7; }
 
 template <bool LOG, bool XL, bool DIAG, int T, int SCHED, typename AT = float, int CPL = 4, int KW = 8>
 __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
@@ -387,13 +388,17 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     // columns, so widths whose 8-KiB slab count does not fit an XCD's 32 CUs still use most of them)
     static_assert(KW >= 6 && KW <= 8, "lane-vectors per lane");
     constexpr int WPR = 4 / T;   // compute waves per row (each on its own 2048-column sub-slab)
-    constexpr int D = (SCHED == 1 || SCHED == 2 || SCHED == 4 || SCHED == 6) ? 1 : 0;  // steps a reduced tile stays in VGPRs
-    constexpr bool XS_LDS = (SCHED >= 1 && SCHED <= 4) || SCHED == 6;  // x slab in LDS instead of VGPRs
+    constexpr int D = SCHED == 7 ? 2 : ((SCHED == 1 || SCHED == 2 || SCHED == 4 || SCHED == 6) ? 1 : 0);  // steps a reduced tile stays in VGPRs
+    constexpr bool XS_LDS = (SCHED >= 1 && SCHED <= 4) || SCHED >= 6;  // x slab in LDS instead of VGPRs
     static_assert(!XS_LDS || T >= 2, "the LDS holds the x slab only for T >= 2");
     // wave 4 publishes granules, wave 5 gathers (no shared vmcnt queue); schedule 5 = the split exchange with
     // the x slab in VGPRs and schedule 0's lag (T = 1, whose x slab does not fit the LDS next to the ring)
     // schedule 6 = the split exchange for wide bf16 tiles at T = 2 (x slab in LDS, 3-slot ring, L = 3: a 4-slot
     // ring and the 32 KB x slab of two sub-slabs would exceed the 160 KB of LDS by the hand-off words)
+    // schedule 7 = schedule 6 with the lag of schedule 4 (L = 4, PD = PQ = 2) in the same 3-slot ring: a reduced
+    // tile stays in VGPRs two steps before parking (D = 2), so 3 of the 5 register slots are in flight. At
+    // 65536 x 262144 bf16 schedule 6 spent 14 % of its sweep on the hand-off (exchange-off ablation, L = 3)
+    // and 3 tiles x 8 KB per wave still cover the HBM latency (tools/fused_ablation.py)
     constexpr bool SPLIT = sched_split(SCHED);
     constexpr int NTHR = SPLIT ? kFusedThreads + 64 : kFusedThreads;
     constexpr bool BF = !std::is_same<AT, float>::value;
@@ -405,11 +410,11 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     // L = PD + PQ = 5 steps: 12.5 -> 13.2 it/s at 512k x 256k; with T = 4 (schedule 4) the deeper lag
     // measured 3 % slower than the fp32 lag (458 vs 473 it/s at 64k x 64k), so it is kept there.
     constexpr bool DEEP = BF && SCHED == 0;
-    constexpr int PD = (SCHED == 2 || SCHED == 4) ? 2 : 1;   // exchange step u polls tile u - PD
+    constexpr int PD = (SCHED == 2 || SCHED == 4 || SCHED == 7) ? 2 : 1;   // exchange step u polls tile u - PD
     constexpr int PQ = DEEP ? 4 : (SCHED == 1 ? 3 : 2);      // polls in flight (finishes tile u - PD - PQ + 1)
-    constexpr int L = DEEP ? PD + PQ : (SCHED == 6 ? 3 : 3 + D);  // back-projection lag in steps
+    constexpr int L = DEEP ? PD + PQ : (SCHED == 6 ? 3 : (SCHED == 7 ? 4 : 3 + D));  // back-projection lag in steps
     static_assert(L >= PD + PQ, "the weights must be ready one step before they are used");
-    constexpr int NL = (BF && CPL == 4) ? 8 : (SCHED == 6 ? 3 : 4);  // LDS ring slots (32 KB fp32 or wide bf16 / 16 KB narrow bf16)
+    constexpr int NL = (BF && CPL == 4) ? 8 : (SCHED >= 6 ? 3 : 4);  // LDS ring slots (32 KB fp32 or wide bf16 / 16 KB narrow bf16)
     static_assert(L <= NL + D - 1, "a parked tile must be back-projected before its ring slot is reused");
     // register tile slots per wave (8 KB fp32 / 4 KB bf16 each): AH in flight + D held. bf16: 6-7 tiles of
     // 8-byte loads in flight (<= 56 loads, inside the 6-bit vmcnt range); 8 slots with the x slab in LDS
@@ -866,12 +871,13 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
 }
 
 constexpr size_t rows_lds_bytes(int T, int sched, int H = 1, int KW = 8) {
-    return (sched == 6 ? 3 : 4) /*NL x 4 waves x KW x 64 lanes x 16 B*/ * 4 * KW * 64 * sizeof(float4) +
-           (((sched >= 1 && sched <= 4) || sched == 6) ? (4 / T) * KW * 64 * H * sizeof(float4) : 0) +  // x slab
+    return (sched >= 6 ? 3 : 4) /*NL x 4 waves x KW x 64 lanes x 16 B*/ * 4 * KW * 64 * sizeof(float4) +
+           (((sched >= 1 && sched <= 4) || sched >= 6) ? (4 / T) * KW * 64 * H * sizeof(float4) : 0) +  // x slab
            (8 * 4 * 3 + 8 + 4) * sizeof(float);
 }
 static_assert(rows_lds_bytes(4, 4, 2) <= 160 * 1024, "wide bf16 tiles: T = 4 fits the LDS");
 static_assert(rows_lds_bytes(2, 6, 2) <= 160 * 1024, "wide bf16 tiles: T = 2 (schedule 6) fits the LDS");
+static_assert(rows_lds_bytes(2, 7, 2) <= 160 * 1024, "wide bf16 tiles: T = 2 (schedule 7) fits the LDS");
 static_assert(rows_lds_bytes(2, 4, 2) > 160 * 1024, "schedule 6 exists because the 4-slot ring does not fit");
 
 static int g_fused_dbg = 0;    // diagnostics only (set through fused_set_debug)
@@ -1088,10 +1094,16 @@ void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, i
     using S4 = std::integral_constant<int, 4>;
     using S5 = std::integral_constant<int, 5>;
     using S6 = std::integral_constant<int, 6>;
+    using S7 = std::integral_constant<int, 7>;
+    static const bool t2_sched6 = [] {  // wide tiles at T = 2: schedule 7 (L = 4) unless SART_BF16_T2_SCHED=6
+        const char* e = std::getenv("SART_BF16_T2_SCHED");
+        return e && std::atoi(e) == 6;
+    }();
     using C4 = std::integral_constant<int, 4>;
     using C8 = std::integral_constant<int, 8>;
     auto by_t = [&](auto lg) {
-        if (cpl == 8 && T == 2) go(lg, std::integral_constant<int, 2>{}, S6{}, C8{});
+        if (cpl == 8 && T == 2 && t2_sched6) go(lg, std::integral_constant<int, 2>{}, S6{}, C8{});
+        else if (cpl == 8 && T == 2) go(lg, std::integral_constant<int, 2>{}, S7{}, C8{});
         else if (cpl == 8) go(lg, std::integral_constant<int, 4>{}, S4{}, C8{});
         else if (T == 1 && g_fused_sched == 5) go(lg, std::integral_constant<int, 1>{}, S5{}, C4{});
         else if (T == 1) go(lg, std::integral_constant<int, 1>{}, S0{}, C4{});

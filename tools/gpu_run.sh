@@ -97,6 +97,12 @@ for step in "$@"; do
                      --rtm-dtype bf16 --npix 524288 --nvox 262144 --iters 20 ;;
     benchlap) run bench_lap 600 python bench.py --steps 5 --warmup 1 --laplacian ;;
     probe) run probe 600 python tools/probe.py ;;
+    ablation) run ablation_bf16 600 python tools/fused_ablation.py --dtype bf16 65536x262144 65536x65536 &&
+              run ablation_fp32 600 python tools/fused_ablation.py --dtype fp32 65536x262144 65536x65536 65536x100000 ;;
+    sched7) SEL="tests/test_gpu_bf16.py tests/test_gpu_solver.py" run pytest_sched7 900 python -u -m pytest tests/test_gpu_bf16.py tests/test_gpu_solver.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
+            run ablation_s7 600 python tools/fused_ablation.py --dtype bf16 65536x262144 &&
+            SART_BF16_T2_SCHED=6 run ablation_s6 600 python tools/fused_ablation.py --dtype bf16 65536x262144 &&
+            run fcheck_s7 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
