@@ -374,6 +374,34 @@ __device__ __forceinline__ void split_pair(float a, float b, uint32_t key, unsig
     lo = sr_bf16_bits(a - (float)ha, key) | (sr_bf16_bits(b - (float)hb, key + 1) << 16);
 }
 
+// Row-dot reductions on DPP instead of ds_bpermute (__shfl_xor): the 6 bpermutes of a full-wave sum are LDS
+// round trips that queue behind the ring's LDS traffic, once per tile in every compute wave and in the gatherer.
+// Within each 16-lane row: quad_perm xor 1 / xor 2, then row_ror 4 / 8 (rotations keep lane % 4), so every lane
+// holds the sum of its row's lanes of the same class lane % T; the four rows are added through v_readlane.
+// Fixed order: bitwise reproducible. The result is valid in lanes < T.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int T>
+__device__ __forceinline__ float class_sum_dpp(float v, int lane) {
+    static_assert(T == 1 || T == 2 || T == 4, "lane classes");
+    if constexpr (T == 1) v += dpp_f<0xB1>(v);  // quad_perm [1, 0, 3, 2]
+    if constexpr (T <= 2) v += dpp_f<0x4E>(v);  // quad_perm [2, 3, 0, 1]
+    v += dpp_f<0x124>(v);                       // row_ror 4
+    v += dpp_f<0x128>(v);                       // row_ror 8
+    float r = 0.f;
+#pragma unroll
+    for (int c = 0; c < T; ++c) {
+        const float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), c)) +
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), c + 16)) +
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), c + 32)) +
+                        __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), c + 48));
+        r = lane == c ? t : r;
+    }
+    return r;
+}
+
 // Schedules with a separate publisher wave (the split exchange)
 constexpr bool sched_split(int sched) { return sched >= 4 && sched <= 8; }
 
@@ -604,7 +632,12 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
                         }
                     }
                 }
-                s = wave_sum(s);
+                // lane 0 publishes. DPP for bf16 tiles (-9 % sweep time at 65536 x 262144, -10 % at 100000 columns);
+                // fp32 tiles keep the LDS bpermutes, measured 1-4 % faster there (profiles/ab_r2_dpp_reductions.jsonl)
+                if constexpr (BF)
+                    s = class_sum_dpp<1>(s, lane);
+                else
+                    s = wave_sum(s);
                 if (lane == 0) {
                     s_part[(t & (NS - 1)) * 4 + wave] = s;
                     asm volatile("" ::: "memory");
@@ -813,8 +846,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
 #pragma unroll
                 for (int m = 0; m < GR; ++m) s += (lane + 64 * m < n) ? __uint_as_float((uint32_t)v[m]) : 0.f;
             }
-#pragma unroll
-            for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
+            s = class_sum_dpp<T>(s, lane);  // lane r < T: row r of the tile (fp32 200000 columns: -6 %)
             const int ws = (int)(u & (NS - 1));
             if (lane < T) {
                 const int64_t row = (t_begin + u) * T + lane;

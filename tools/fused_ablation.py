@@ -51,11 +51,12 @@ def main():
                                   use_fused=True, check_interval=32, allow_zero_tolerance=True)
         s1, sn = mk(1), mk(a.iters)
         for dbg, mode in ((0, "full"), (1, "no_exchange")):
-            k.fused_set_debug(dbg)
+            k.fused_set_debug(dbg | int(os.environ.get("SART_FUSED_DBG_EXTRA", "0")))
             solve_ms(s1, g, reps=1)  # warm
             t1, tn = solve_ms(s1, g), solve_ms(sn, g)
             ms = (tn - t1) / (a.iters - 1)
             print(json.dumps({"shape": shape, "dtype": a.dtype, "mode": mode, "T": sn.geom.T,
+                              "dbg_extra": int(os.environ.get("SART_FUSED_DBG_EXTRA", "0")),
                               "schedule": (int(os.environ.get("SART_BF16_T2_SCHED", "7"))
                                            if a.dtype == "bf16" and sn.geom.T == 2 else sn.k.fused_get_schedule()),
                               "J": sn.geom.J, "I": sn.geom.I,

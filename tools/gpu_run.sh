@@ -115,6 +115,20 @@ for step in "$@"; do
           run ab_new_$i 300 python tools/fused_ablation.py --dtype fp32 ${AB_SHAPES:-65536x100000 65536x200000 65536x262144 65536x65536} &&
           run ab_old_$i 300 python .abold/tools/fused_ablation.py --dtype fp32 ${AB_SHAPES:-65536x100000 65536x200000 65536x262144 65536x65536} || exit 1
         done ;;
+    abtests) run pytest_ab 900 python -u -m pytest tests/test_gpu_bf16.py tests/test_gpu_solver.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
+             run fcheck_ab 600 python tools/fused_check.py 8192x100000 8192x200000 65536x262144 16384x65536 &&
+             run fcheck_ab_bf16 600 python tools/fused_check.py --dtype bf16 65536x262144 16384x65536 ;;
+    abbf16) for i in 1 2; do
+              run abb_new_$i 300 python tools/fused_ablation.py --dtype bf16 65536x262144 65536x65536 65536x100000 &&
+              run abb_old_$i 300 python .abold/tools/fused_ablation.py --dtype bf16 65536x262144 65536x65536 65536x100000 || exit 1
+            done ;;
+    abdpp) for x in 0 16 32 48; do
+             SART_FUSED_DBG_EXTRA=$x run abdpp_$x 300 python tools/fused_ablation.py --dtype fp32 65536x200000 65536x100000 65536x70000 || exit 1
+           done ;;
+    abdpp2) for x in 0 16 32 48; do
+             SART_FUSED_DBG_EXTRA=$x run abdpp2_$x 300 python tools/fused_ablation.py --dtype bf16 65536x262144 65536x65536 65536x100000 &&
+             SART_FUSED_DBG_EXTRA=$x run abdpp3_$x 300 python tools/fused_ablation.py --dtype fp32 65536x65536 65536x262144 65536x200000 || exit 1
+           done ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
