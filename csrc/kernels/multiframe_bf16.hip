@@ -93,14 +93,23 @@ __device__ __forceinline__ void split_a8(const u32x8 v, u32x4& hi, u32x4& lo) {
     lo = u32x4{l0, l1, l2, l3};
 }
 
-// Three pieces: hi + mid + lo = a to 2^-27 (the back-projection, whose signed weights cancel in the sum).
+// Three pieces, exact: hi + mid + lo = a (the back-projection, whose signed weights cancel in the sum). Truncation
+// splits: hi = the top 16 bits of a, r = a - hi is exact (same sign and exponent, <= 16 significant bits), mid = the
+// top 16 bits of r, lo = r - mid exact with <= 8 significant bits, i.e. a bf16 value. Per pair of elements: 4 v_and,
+// 2 packed fp32 subtractions and 3 v_perm (upper halves) = 4.5 VALU operations per element, against 5.5 for the
+// round-to-nearest split (cvt_pk, widen, subtract twice), with no representation error left at all.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split_a2_3(unsigned x, unsigned y, unsigned& hi, unsigned& mid, unsigned& lo) {
-    const float a = __uint_as_float(x), b = __uint_as_float(y);
-    hi = __builtin_bit_cast(unsigned, bf16x2_t{(__bf16)a, (__bf16)b});
-    const float ra = a - __uint_as_float(hi << 16), rb = b - __uint_as_float(hi & 0xffff0000u);
-    mid = __builtin_bit_cast(unsigned, bf16x2_t{(__bf16)ra, (__bf16)rb});
-    const float sa = ra - __uint_as_float(mid << 16), sb = rb - __uint_as_float(mid & 0xffff0000u);
-    lo = __builtin_bit_cast(unsigned, bf16x2_t{(__bf16)sa, (__bf16)sb});
+    const f32x2 a = {__uint_as_float(x), __uint_as_float(y)};
+    const f32x2 h = {__uint_as_float(x & 0xffff0000u), __uint_as_float(y & 0xffff0000u)};
+    const f32x2 r = a - h;
+    const unsigned rx = __float_as_uint(r.x), ry = __float_as_uint(r.y);
+    const f32x2 m = {__uint_as_float(rx & 0xffff0000u), __uint_as_float(ry & 0xffff0000u)};
+    const f32x2 l = r - m;
+    constexpr unsigned kUpper = 0x07060302u;  // bytes 2-3 of S1 (x: element 2m), then bytes 2-3 of S0 (y)
+    hi = __builtin_amdgcn_perm(y, x, kUpper);
+    mid = __builtin_amdgcn_perm(ry, rx, kUpper);
+    lo = __builtin_amdgcn_perm(__float_as_uint(l.y), __float_as_uint(l.x), kUpper);
 }
 
 // Back-projection fragment of voxel phase P from eight 16-byte fp32 row loads (4 voxels each): element j = the

@@ -129,6 +129,14 @@ for step in "$@"; do
              SART_FUSED_DBG_EXTRA=$x run abdpp2_$x 300 python tools/fused_ablation.py --dtype bf16 65536x262144 65536x65536 65536x100000 &&
              SART_FUSED_DBG_EXTRA=$x run abdpp3_$x 300 python tools/fused_ablation.py --dtype fp32 65536x65536 65536x262144 65536x200000 || exit 1
            done ;;
+    abmf) run pytest_mf 900 python -u -m pytest tests/test_gpu_multiframe.py tests/test_gpu_multiframe_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
+          run x3acc 300 python tools/x3_accuracy.py &&
+          for i in 1 2; do
+            run abmf_new64_$i 300 python bench.py --steps 3 --warmup 1 --frames 64 &&
+            run abmf_old64_$i 300 python .abold/bench.py --steps 3 --warmup 1 --frames 64 &&
+            run abmf_new32_$i 300 python bench.py --steps 3 --warmup 1 --frames 32 &&
+            run abmf_old32_$i 300 python .abold/bench.py --steps 3 --warmup 1 --frames 32 || exit 1
+          done ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
