@@ -96,16 +96,18 @@ __device__ __forceinline__ void split_a8(const u32x8 v, u32x4& hi, u32x4& lo) {
 // Three pieces, exact: hi + mid + lo = a (the back-projection, whose signed weights cancel in the sum). Truncation
 // splits: hi = the top 16 bits of a, r = a - hi is exact (same sign and exponent, <= 16 significant bits), mid = the
 // top 16 bits of r, lo = r - mid exact with <= 8 significant bits, i.e. a bf16 value. Per pair of elements: 4 v_and,
-// 2 packed fp32 subtractions and 3 v_perm (upper halves) = 4.5 VALU operations per element, against 5.5 for the
-// round-to-nearest split (cvt_pk, widen, subtract twice), with no representation error left at all.
+// 4 subtractions and 3 v_perm (upper halves), against 2 cvt_pk, 4 widenings and 4 subtractions for the
+// round-to-nearest split, with no representation error left at all.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split_a2_3(unsigned x, unsigned y, unsigned& hi, unsigned& mid, unsigned& lo) {
     const f32x2 a = {__uint_as_float(x), __uint_as_float(y)};
     const f32x2 h = {__uint_as_float(x & 0xffff0000u), __uint_as_float(y & 0xffff0000u)};
-    const f32x2 r = a - h;
+    // one subtraction and one fma per pair, not two isomorphic subtractions: the compiler would pack those into
+    // v_pk_add_f32, which costs more than two plain operations beside MFMAs (MI355X_MICROARCH.md, filler prices)
+    const f32x2 r = {a.x - h.x, __builtin_fmaf(h.y, -1.0f, a.y)};
     const unsigned rx = __float_as_uint(r.x), ry = __float_as_uint(r.y);
     const f32x2 m = {__uint_as_float(rx & 0xffff0000u), __uint_as_float(ry & 0xffff0000u)};
-    const f32x2 l = r - m;
+    const f32x2 l = {r.x - m.x, __builtin_fmaf(m.y, -1.0f, r.y)};
     constexpr unsigned kUpper = 0x07060302u;  // bytes 2-3 of S1 (x: element 2m), then bytes 2-3 of S0 (y)
     hi = __builtin_amdgcn_perm(y, x, kUpper);
     mid = __builtin_amdgcn_perm(ry, rx, kUpper);

@@ -137,6 +137,12 @@ for step in "$@"; do
             run abmf_new32_$i 300 python bench.py --steps 3 --warmup 1 --frames 32 &&
             run abmf_old32_$i 300 python .abold/bench.py --steps 3 --warmup 1 --frames 32 || exit 1
           done ;;
+    abmf2) for i in 1 2; do
+            run abmf2_new64_$i 300 python bench.py --steps 3 --warmup 1 --frames 64 &&
+            run abmf2_old64_$i 300 python .abold/bench.py --steps 3 --warmup 1 --frames 64 &&
+            run abmf2_new32_$i 300 python bench.py --steps 3 --warmup 1 --frames 32 &&
+            run abmf2_old32_$i 300 python .abold/bench.py --steps 3 --warmup 1 --frames 32 || exit 1
+          done && run x3acc2 300 python tools/x3_accuracy.py ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
