@@ -96,8 +96,9 @@ __device__ __forceinline__ void split_a8(const u32x8 v, u32x4& hi, u32x4& lo) {
 // Three pieces, exact: hi + mid + lo = a (the back-projection, whose signed weights cancel in the sum). Truncation
 // splits: hi = the top 16 bits of a, r = a - hi is exact (same sign and exponent, <= 16 significant bits), mid = the
 // top 16 bits of r, lo = r - mid exact with <= 8 significant bits, i.e. a bf16 value. Per pair of elements: 4 v_and,
-// 4 subtractions and 3 v_perm (upper halves), against 2 cvt_pk, 4 widenings and 4 subtractions for the
-// round-to-nearest split, with no representation error left at all.
+// 4 subtractions and 3 v_perm (upper halves), as many operations as the round-to-nearest split (3 cvt_pk, 4
+// widenings, 4 subtractions) but cheaper ones beside the MFMAs (+1.5-3 % at 32 / 64 frames,
+// profiles/ab_r2_mf_trunc_split.jsonl), and no representation error left at all.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split_a2_3(unsigned x, unsigned y, unsigned& hi, unsigned& mid, unsigned& lo) {
     const f32x2 a = {__uint_as_float(x), __uint_as_float(y)};

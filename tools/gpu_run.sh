@@ -143,6 +143,10 @@ for step in "$@"; do
             run abmf2_new32_$i 300 python bench.py --steps 3 --warmup 1 --frames 32 &&
             run abmf2_old32_$i 300 python .abold/bench.py --steps 3 --warmup 1 --frames 32 || exit 1
           done && run x3acc2 300 python tools/x3_accuracy.py ;;
+    pmcmf) echo "=== pmcmf" >> "$OUT/session.log"
+           timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
+             -d "$OUT/pmc_mf64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 5 --npix 16384 --no-selfcheck > "$OUT/pmc_mf64.log" 2>&1
+           rc=$?; echo "=== pmcmf rc=$rc" >> "$OUT/session.log"; tail -5 "$OUT/pmc_mf64.log"; [ $rc -eq 0 ] || exit $rc ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
