@@ -147,6 +147,10 @@ for step in "$@"; do
            timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
              -d "$OUT/pmc_mf64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 5 --npix 16384 --no-selfcheck > "$OUT/pmc_mf64.log" 2>&1
            rc=$?; echo "=== pmcmf rc=$rc" >> "$OUT/session.log"; tail -5 "$OUT/pmc_mf64.log"; [ $rc -eq 0 ] || exit $rc ;;
+    abpreset) for i in 1 2; do
+            run abp_new_$i 300 python bench.py --config 512kx256k --steps 3 --warmup 1 --no-selfcheck &&
+            run abp_old_$i 300 python .abold/bench.py --config 512kx256k --steps 3 --warmup 1 --no-selfcheck || exit 1
+          done ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
