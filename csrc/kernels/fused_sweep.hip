@@ -403,7 +403,7 @@ __device__ __forceinline__ float class_sum_dpp(float v, int lane) {
 }
 
 // Schedules with a separate publisher wave (the split exchange)
-constexpr bool sched_split(int sched) { return sched >= 4 && sched <= 8; }
+constexpr bool sched_split(int sched) { return sched >= 4 && sched <= 7; }
 
 template <bool LOG, bool XL, bool DIAG, int T, int SCHED, typename AT = float, int CPL = 4, int KW = 8>
 __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
@@ -416,7 +416,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     // columns, so widths whose 8-KiB slab count does not fit an XCD's 32 CUs still use most of them)
     static_assert(KW >= 6 && KW <= 8, "lane-vectors per lane");
     constexpr int WPR = 4 / T;   // compute waves per row (each on its own 2048-column sub-slab)
-    constexpr int D = SCHED == 7 ? 2 : ((SCHED == 1 || SCHED == 2 || SCHED == 4 || SCHED == 6 || SCHED == 8) ? 1 : 0);  // steps a reduced tile stays in VGPRs
+    constexpr int D = SCHED == 7 ? 2 : ((SCHED == 1 || SCHED == 2 || SCHED == 4 || SCHED == 6) ? 1 : 0);  // steps a reduced tile stays in VGPRs
     constexpr bool XS_LDS = (SCHED >= 1 && SCHED <= 4) || SCHED == 6 || SCHED == 7;  // x slab in LDS instead of VGPRs
     static_assert(!XS_LDS || T >= 2, "the LDS holds the x slab only for T >= 2");
     // wave 4 publishes granules, wave 5 gathers (no shared vmcnt queue); schedule 5 = the split exchange with
@@ -427,8 +427,8 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     // tile stays in VGPRs two steps before parking (D = 2), so 3 of the 5 register slots are in flight. At
     // 65536 x 262144 bf16 schedule 6 spent 14 % of its sweep on the hand-off (exchange-off ablation, L = 3)
     // and 3 tiles x 8 KB per wave still cover the HBM latency (tools/fused_ablation.py)
-    // schedule 8 = schedule 5 (T = 1, x slab in VGPRs) with the same trade: a reduced tile stays one step in
-    // VGPRs (D = 1, 3 tiles in flight), so the 4-slot ring allows L = 4 (PD = PQ = 2) instead of 3
+    // (the same trade at T = 1, L = 4 in schedule 5's 4-slot ring with D = 1, measured equal to schedule 5 at
+    // 70000 ... 262144 columns and was removed: profiles/ablation_r2_t1_sched5_vs_8.jsonl)
     constexpr bool SPLIT = sched_split(SCHED);
     constexpr int NTHR = SPLIT ? kFusedThreads + 64 : kFusedThreads;
     constexpr bool BF = !std::is_same<AT, float>::value;
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     // L = PD + PQ = 5 steps: 12.5 -> 13.2 it/s at 512k x 256k; with T = 4 (schedule 4) the deeper lag
     // measured 3 % slower than the fp32 lag (458 vs 473 it/s at 64k x 64k), so it is kept there.
     constexpr bool DEEP = BF && SCHED == 0;
-    constexpr int PD = (SCHED == 2 || SCHED == 4 || SCHED == 7 || SCHED == 8) ? 2 : 1;   // exchange step u polls tile u - PD
+    constexpr int PD = (SCHED == 2 || SCHED == 4 || SCHED == 7) ? 2 : 1;   // exchange step u polls tile u - PD
     constexpr int PQ = DEEP ? 4 : (SCHED == 1 ? 3 : 2);      // polls in flight (finishes tile u - PD - PQ + 1)
     constexpr int L = DEEP ? PD + PQ : (SCHED == 6 ? 3 : (SCHED == 7 ? 4 : 3 + D));  // back-projection lag in steps
     static_assert(L >= PD + PQ, "the weights must be ready one step before they are used");
@@ -927,8 +927,7 @@ static int g_fused_dbg = 0;    // diagnostics only (set through fused_set_debug)
 static int g_fused_sched = 4;  // variant 6 pipeline schedule (k_fused_sweep_rows SCHED)
 void fused_set_debug(int flags) { g_fused_dbg = flags; }
 void fused_set_schedule(int sched) {
-    if (sched < 0 || sched > 8 || sched == 6 || sched == 7)
-        throw std::runtime_error("fused_set_schedule: 0 .. 5 or 8");
+    if (sched < 0 || sched > 5) throw std::runtime_error("fused_set_schedule: 0 .. 5");
     g_fused_sched = sched;
 }
 int fused_get_schedule() { return g_fused_sched; }
@@ -1003,7 +1002,7 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
     // VGPRs) under the default schedule 4 (or 5): +10-14 % over schedule 0 at 73k-262k columns, with and
     // without idle CUs (profiles/probe_r2_t1_sched5.jsonl); schedules 0-3 select schedule 0 for T = 1.
     // Instrumented builds: schedules 0, 2 and 4.
-    int sched = T >= 2 ? (g_fused_sched >= 5 ? 4 : g_fused_sched) : (g_fused_sched == 8 ? 8 : g_fused_sched >= 4 ? 5 : 0);
+    int sched = T >= 2 ? (g_fused_sched == 5 ? 4 : g_fused_sched) : (g_fused_sched >= 4 ? 5 : 0);
     if (diag && sched != 2 && sched != 4) sched = 0;
     auto go = [&](auto lg, auto d, auto sc) {
         launch_rows_t<decltype(lg)::value, true, decltype(d)::value, T, decltype(sc)::value>(
@@ -1017,22 +1016,15 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
     using S3 = std::integral_constant<int, (T >= 2 ? 3 : 0)>;
     using S4 = std::integral_constant<int, (T >= 2 ? 4 : 0)>;
     using S5 = std::integral_constant<int, (T == 1 ? 5 : 4)>;
-    using S8 = std::integral_constant<int, (T == 1 ? 8 : 4)>;
     auto by_log = [&](auto d, auto sc) {
         if (logmode) go(TT{}, d, sc); else go(FF{}, d, sc);
     };
     if (kw != 8) {  // narrower slabs: the default schedules only (4 at T >= 2, 5 at T = 1), no diagnostics
         auto go_kw = [&](auto lg, auto k) {
             using SD = std::integral_constant<int, (T >= 2 ? 4 : 5)>;
-            using SE = std::integral_constant<int, (T >= 2 ? 4 : 8)>;
-            if (sched == 8)
-                launch_rows_t<decltype(lg)::value, true, false, T, SE::value, float, 4, decltype(k)::value>(
-                    grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
-                    chain_tiles);
-            else
-                launch_rows_t<decltype(lg)::value, true, false, T, SD::value, float, 4, decltype(k)::value>(
-                    grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
-                    chain_tiles);
+            launch_rows_t<decltype(lg)::value, true, false, T, SD::value, float, 4, decltype(k)::value>(
+                grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
+                chain_tiles);
         };
         auto by_kw = [&](auto lg) {
             if (kw == 7) go_kw(lg, std::integral_constant<int, 7>{});
@@ -1053,7 +1045,6 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
         case 3: by_log(FF{}, S3{}); break;
         case 4: by_log(FF{}, S4{}); break;
         case 5: by_log(FF{}, S5{}); break;
-        case 8: by_log(FF{}, S8{}); break;
         default: by_log(FF{}, S0{}); break;
     }
 }
