@@ -103,9 +103,6 @@ for step in "$@"; do
             run ablation_s7 600 python tools/fused_ablation.py --dtype bf16 65536x262144 &&
             SART_BF16_T2_SCHED=6 run ablation_s6 600 python tools/fused_ablation.py --dtype bf16 65536x262144 &&
             run fcheck_s7 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 ;;
-    sched8) run ablation_t1_s5 600 python tools/fused_ablation.py --dtype fp32 65536x100000 65536x200000 65536x70000 65536x262144 &&
-            SART_FUSED_SCHEDULE=8 run ablation_t1_s8 600 python tools/fused_ablation.py --dtype fp32 65536x100000 65536x200000 65536x70000 65536x262144 &&
-            SART_FUSED_SCHEDULE=8 run fcheck_s8 600 python tools/fused_check.py 8192x100000 8192x200000 65536x262144 16384x131072 ;;
     prefetch) run pytest_prefetch 900 python -u -m pytest tests/test_gpu_bf16.py tests/test_gpu_solver.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
               run ablation_pf_fp32 600 python tools/fused_ablation.py --dtype fp32 65536x100000 65536x200000 65536x70000 65536x262144 65536x65536 &&
               run ablation_pf_bf16 600 python tools/fused_ablation.py --dtype bf16 65536x262144 65536x65536 65536x100000 &&
