@@ -1138,10 +1138,9 @@ void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, i
     using S5 = std::integral_constant<int, 5>;
     using S6 = std::integral_constant<int, 6>;
     using S7 = std::integral_constant<int, 7>;
-    static const bool t2_sched6 = [] {  // wide tiles at T = 2: schedule 7 (L = 4) unless SART_BF16_T2_SCHED=6
-        const char* e = std::getenv("SART_BF16_T2_SCHED");
-        return e && std::atoi(e) == 6;
-    }();
+    // wide tiles at T = 2: schedule 7 (L = 4) unless SART_BF16_T2_SCHED=6 (read per launch: tests switch it)
+    const char* t2e = std::getenv("SART_BF16_T2_SCHED");
+    const bool t2_sched6 = t2e && std::atoi(t2e) == 6;
     using C4 = std::integral_constant<int, 4>;
     using C8 = std::integral_constant<int, 8>;
     auto by_t = [&](auto lg) {

@@ -224,7 +224,7 @@ def test_bf16_fused_rows_per_tile(dev, T, log):
 @pytest.mark.parametrize("log", [False, True])
 def test_bf16_wide_tiles(dev, monkeypatch, nvox, T, J, I, log):
     """Wide bf16 tiles (16-byte loads of 8 bf16 per lane: slab 4096 columns at T = 4, or 8192 at T = 2 with the
-    3-slot ring of schedule 6) against the narrow bf16 tiles (SART_BF16_WIDE=0) and the device fp64 oracle on
+    3-slot ring of schedule 7) against the narrow bf16 tiles (SART_BF16_WIDE=0) and the device fp64 oracle on
     the stored (rounded) matrix."""
     from mpi_cuda_sartsolver_amd.models.oracle import sart_oracle_f64
     from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
@@ -249,3 +249,35 @@ def test_bf16_wide_tiles(dev, monkeypatch, nvox, T, J, I, log):
     en = np.linalg.norm(rn.solution - x64) / np.linalg.norm(x64)
     # summation-order differences only (measured 1.27x at 4096 columns, <= 1.1x at >= 64k)
     assert ew <= 1.5 * en + 1e-7, (ew, en)
+
+
+@pytest.mark.parametrize("log", [False, True])
+def test_bf16_wide_t2_schedules_agree(dev, monkeypatch, log):
+    """Wide bf16 tiles at T = 2: schedule 7 (4-step lag, the default) and schedule 6 (3-step lag,
+    SART_BF16_T2_SCHED=6) run the same arithmetic in the same order, so their iterates are bitwise equal; both are
+    fused (no fallback) and match the device fp64 oracle on the stored matrix."""
+    from mpi_cuda_sartsolver_amd.models.oracle import sart_oracle_f64
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+    from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
+
+    prob = make_problem(4096, 262144, seed=7, device=dev, saturate_fraction=0.02, storage="bf16")
+    g = prob.measurement.cpu().numpy()
+    p = SolverParams(max_iterations=8, conv_tolerance=0.0)
+    out = {}
+    for sched in ("7", "6"):
+        monkeypatch.setenv("SART_BF16_T2_SCHED", sched)
+        s = SARTSolver(prob.rtm, None, None, p, logarithmic=log, allow_zero_tolerance=True)
+        assert s.use_fused and (s.geom.cpl, s.geom.T) == (8, 2)
+        r = s.solve(g)
+        assert r.used_fused and r.fallbacks == 0
+        out[sched] = r.solution
+        del s
+    np.testing.assert_array_equal(out["7"], out["6"])
+    # fp32 drift of 8 iterations on a 262144-wide random matrix is ~7e-3 for any summation order: compare with
+    # the bf16 two-pass kernels' distance to the oracle, not with a fixed bound
+    t = SARTSolver(prob.rtm, None, None, p, logarithmic=log, allow_zero_tolerance=True, use_fused=False)
+    r2 = t.solve(g)
+    x64 = sart_oracle_f64(prob.rtm, g, 8, logarithmic=log)
+    e7 = np.linalg.norm(out["7"] - x64) / np.linalg.norm(x64)
+    e2 = np.linalg.norm(r2.solution - x64) / np.linalg.norm(x64)
+    assert e7 <= max(1.5 * e2, 1e-5), (e7, e2)

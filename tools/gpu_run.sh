@@ -148,6 +148,11 @@ for step in "$@"; do
             run abp_new_$i 300 python bench.py --config 512kx256k --steps 3 --warmup 1 --no-selfcheck &&
             run abp_old_$i 300 python .abold/bench.py --config 512kx256k --steps 3 --warmup 1 --no-selfcheck || exit 1
           done ;;
+    abgraph) for i in 1 2; do
+            run abg_def_$i 300 python bench.py --steps 5 --warmup 1 --no-selfcheck &&
+            SART_GRAPH=1 run abg_graph_$i 300 python bench.py --steps 5 --warmup 1 --no-selfcheck || exit 1
+          done ;;
+    testsrest) run pytest_gpu_rest 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
