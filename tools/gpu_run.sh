@@ -153,6 +153,9 @@ for step in "$@"; do
             SART_GRAPH=1 run abg_graph_$i 300 python bench.py --steps 5 --warmup 1 --no-selfcheck || exit 1
           done ;;
     testsrest) run pytest_gpu_rest 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    rehearse8) SART_DIST_BACKEND=gloo SART_P2P=1 SART_P2P_TIMEOUT_S=60 run comm_check_p2p_n8 300 python -m torch.distributed.run --nnodes=1 \
+                 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29608 tools/comm_check.py --out "$OUT/comm_check_p2p_n8.json" &&
+               SART_P2P=1 SART_P2P_TIMEOUT_S=60 run bench_share8_p2p 400 python bench.py --gpus 8 --share-gpus --npix 4096 --steps 2 --warmup 1 --iters 20 --watchdog 200 ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
