@@ -156,6 +156,20 @@ for step in "$@"; do
     rehearse8) SART_DIST_BACKEND=gloo SART_P2P=1 SART_P2P_TIMEOUT_S=60 run comm_check_p2p_n8 300 python -m torch.distributed.run --nnodes=1 \
                  --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29608 tools/comm_check.py --out "$OUT/comm_check_p2p_n8.json" &&
                SART_P2P=1 SART_P2P_TIMEOUT_S=60 run bench_share8_p2p 400 python bench.py --gpus 8 --share-gpus --npix 4096 --steps 2 --warmup 1 --iters 20 --watchdog 200 ;;
+    mf16sweep) run rocprof_mf16 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mf16" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 16 --iters 20 &&
+               for kv in DEF=0 SART_MF_DEPTH=1 SART_MF_DEPTH=2 SART_MF_DEPTH=3 SART_MF_ROWS=2 SART_MF_VOX=2 SART_MF_NT=1 SART_MF_BP_BLOCKS=1024 SART_MF_BP_BLOCKS=256 DEF=1; do
+                 env "$kv" timeout -k 10 300 python bench.py --steps 2 --warmup 1 --frames 16 --iters 50 > "$OUT/mf16_$kv.log" 2>&1 || { echo "FATAL $kv"; exit 1; }
+                 echo "=== mf16 $kv $(grep -h '^{' "$OUT/mf16_$kv.log" | python -c 'import sys,json; print(json.loads(sys.stdin.readline())["iters_per_s"])')" | tee -a "$OUT/session.log"
+               done ;;
+    mf16x3) for i in 1 2; do
+              run mf16_x3on_$i 300 python bench.py --steps 2 --warmup 1 --frames 16 --iters 50 --mf-split-a on &&
+              run mf16_x3off_$i 300 python bench.py --steps 2 --warmup 1 --frames 16 --iters 50 --mf-split-a off || exit 1
+            done &&
+            run rocprof_mf16x3 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mf16x3" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 16 --iters 20 --mf-split-a on ;;
+    mf16as) for kv in SART_MF_X3_FWD=2,2 SART_MF_X3_FWD=2,2,as SART_MF_X3_FWD=2,1,as SART_MF_X3_FWD=4,1,as SART_MF_X3_FWD=4,2,as SART_MF_X3_FWD=4,1 SART_MF_X3_DEPTH=2; do
+              env "$kv" timeout -k 10 300 python bench.py --steps 2 --warmup 1 --frames 16 --iters 50 --mf-split-a on > "$OUT/mf16as_$kv.log" 2>&1 || { echo "FATAL $kv"; exit 1; }
+              echo "=== mf16as $kv $(grep -h '^{' "$OUT/mf16as_$kv.log" | python -c 'import sys,json; print(json.loads(sys.stdin.readline())["iters_per_s"])')" | tee -a "$OUT/session.log"
+            done ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
