@@ -170,6 +170,11 @@ for step in "$@"; do
               env "$kv" timeout -k 10 300 python bench.py --steps 2 --warmup 1 --frames 16 --iters 50 --mf-split-a on > "$OUT/mf16as_$kv.log" 2>&1 || { echo "FATAL $kv"; exit 1; }
               echo "=== mf16as $kv $(grep -h '^{' "$OUT/mf16as_$kv.log" | python -c 'import sys,json; print(json.loads(sys.stdin.readline())["iters_per_s"])')" | tee -a "$OUT/session.log"
             done ;;
+    finalmatrix) for spec in "default|" "log|--variant log" "lap|--laplacian" "twopass|--no-fused" "cols|--partition cols" "bf16|--rtm-dtype bf16" "bf16log|--rtm-dtype bf16 --variant log" "mf16|--frames 16" "mf32|--frames 32" "mf64|--frames 64" "mfb16|--frames 16 --rtm-dtype bf16" "mfb32|--frames 32 --rtm-dtype bf16" "mfb64|--frames 64 --rtm-dtype bf16"; do
+                   name=${spec%%|*}; args=${spec#*|}
+                   timeout -k 10 300 python bench.py --steps 3 --warmup 1 $args > "$OUT/final_$name.log" 2>&1 || { echo "FATAL $name"; exit 1; }
+                   echo "=== final $name $(grep -h '^{' "$OUT/final_$name.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+                 done ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
