@@ -609,7 +609,9 @@ __global__ __launch_bounds__(256, (mf_bwd_min_waves<AT, VT>())) void k_mf_backpr
                     for (int j = 0; j < NG; ++j)
 #pragma unroll
                         for (int pl = 0; pl < 3; ++pl) wv[pl][j] = ws[(pl * NG + j) * 64];
-                    // product-major: consecutive MFMAs write different accumulators (no dependent chains)
+                    // product-major: consecutive MFMAs write different accumulators (no dependent chains); a
+                    // phase-major order (split one phase, then its 6 x NG MFMAs) measured 0.6-1 % slower
+                    // (profiles/ab_r2_mf_phase_major_negative.jsonl)
                     auto prod = [&](const u32x4(&fa)[4], int pl) {
 #pragma unroll
                         for (int j = 0; j < NG; ++j)
