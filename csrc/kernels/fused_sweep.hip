@@ -846,7 +846,11 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
 #pragma unroll
                 for (int m = 0; m < GR; ++m) s += (lane + 64 * m < n) ? __uint_as_float((uint32_t)v[m]) : 0.f;
             }
-            s = class_sum_dpp<T>(s, lane);  // lane r < T: row r of the tile (fp32 200000 columns: -6 %)
+            if constexpr (T == 1 && !BF && KW == 8) {  // (A/B: the 8-KiB-slab fp32 T = 1 gatherer on bpermutes)
+                for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
+            } else {
+                s = class_sum_dpp<T>(s, lane);  // lane r < T: row r of the tile (fp32 200000 columns: -6 %)
+            }
             const int ws = (int)(u & (NS - 1));
             if (lane < T) {
                 const int64_t row = (t_begin + u) * T + lane;

@@ -175,6 +175,11 @@ for step in "$@"; do
                    timeout -k 10 300 python bench.py --steps 3 --warmup 1 $args > "$OUT/final_$name.log" 2>&1 || { echo "FATAL $name"; exit 1; }
                    echo "=== final $name $(grep -h '^{' "$OUT/final_$name.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
                  done ;;
+    abkw8) for i in 1 2; do
+            run abk_new_$i 300 python bench.py --config 512kx256k --steps 3 --warmup 1 --no-selfcheck &&
+            run abk_old_$i 300 python .abold/bench.py --config 512kx256k --steps 3 --warmup 1 --no-selfcheck || exit 1
+          done &&
+          run abk_fc 300 python tools/fused_check.py 65536x262144 ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
