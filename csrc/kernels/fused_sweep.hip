@@ -846,7 +846,9 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
 #pragma unroll
                 for (int m = 0; m < GR; ++m) s += (lane + 64 * m < n) ? __uint_as_float((uint32_t)v[m]) : 0.f;
             }
-            if constexpr (T == 1 && !BF && KW == 8) {  // (A/B: the 8-KiB-slab fp32 T = 1 gatherer on bpermutes)
+            // 8-KiB fp32 slabs keep the bpermutes: same-box A/B, 512kx256k preset shard (T = 1) 93.8 -> 102.1 it/s,
+            // 64k x 64k (T = 4) +0.2 % (profiles/ab_r2_kw8_t1_gatherer.jsonl, ab_r2_kw8_t4_gatherer.jsonl)
+            if constexpr (!BF && KW == 8) {
                 for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
             } else {
                 s = class_sum_dpp<T>(s, lane);  // lane r < T: row r of the tile (fp32 200000 columns: -6 %)

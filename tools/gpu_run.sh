@@ -180,6 +180,10 @@ for step in "$@"; do
             run abk_old_$i 300 python .abold/bench.py --config 512kx256k --steps 3 --warmup 1 --no-selfcheck || exit 1
           done &&
           run abk_fc 300 python tools/fused_check.py 65536x262144 ;;
+    abt4) for i in 1 2; do
+            run abt4_new_$i 300 python bench.py --steps 5 --warmup 1 --no-selfcheck &&
+            run abt4_old_$i 300 python .abold/bench.py --steps 5 --warmup 1 --no-selfcheck || exit 1
+          done ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
