@@ -632,9 +632,10 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
                         }
                     }
                 }
-                // lane 0 publishes. DPP for bf16 tiles (-9 % sweep time at 65536 x 262144, -10 % at 100000 columns);
-                // fp32 tiles keep the LDS bpermutes, measured 1-4 % faster there (profiles/ab_r2_dpp_reductions.jsonl)
-                if constexpr (BF)
+                // lane 0 publishes. DPP for bf16 tiles at T = 4 (bench A/B at 64k x 64k: 772 vs 756 it/s); bf16 at
+                // T = 2 (512k x 256k: 20.9 vs 21.3 it/s) and fp32 tiles keep the LDS bpermutes
+                // (profiles/ab_r2_bf16_dpp_bench.jsonl, profiles/ab_r2_dpp_reductions.jsonl)
+                if constexpr (BF && T == 4)
                     s = class_sum_dpp<1>(s, lane);
                 else
                     s = wave_sum(s);
@@ -848,7 +849,8 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
             }
             // 8-KiB fp32 slabs keep the bpermutes: same-box A/B, 512kx256k preset shard (T = 1) 93.8 -> 102.1 it/s,
             // 64k x 64k (T = 4) +0.2 % (profiles/ab_r2_kw8_t1_gatherer.jsonl, ab_r2_kw8_t4_gatherer.jsonl)
-            if constexpr (!BF && KW == 8) {
+            // (and bf16 at T = 2 like its compute waves; bf16 T = 4 and 6 / 7-KiB fp32 slabs use DPP)
+            if constexpr (KW == 8 && !(BF && T == 4)) {
                 for (int off = T; off < 64; off <<= 1) s += __shfl_xor(s, off, kWave);
             } else {
                 s = class_sum_dpp<T>(s, lane);  // lane r < T: row r of the tile (fp32 200000 columns: -6 %)

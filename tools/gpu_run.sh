@@ -184,6 +184,16 @@ for step in "$@"; do
             run abt4_new_$i 300 python bench.py --steps 5 --warmup 1 --no-selfcheck &&
             run abt4_old_$i 300 python .abold/bench.py --steps 5 --warmup 1 --no-selfcheck || exit 1
           done ;;
+    abbf) for i in 1 2; do
+            run abbf_dpp_$i 300 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --no-selfcheck &&
+            run abbf_shfl_$i 300 python .abold/bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --no-selfcheck || exit 1
+          done &&
+          run abbfbig_dpp 600 python bench.py --steps 2 --warmup 1 --rtm-dtype bf16 --npix 524288 --nvox 262144 --iters 20 --no-selfcheck &&
+          run abbfbig_shfl 600 python .abold/bench.py --steps 2 --warmup 1 --rtm-dtype bf16 --npix 524288 --nvox 262144 --iters 20 --no-selfcheck ;;
+    bf16final) run pytest_bf16f 900 python -u -m pytest tests/test_gpu_bf16.py tests/test_gpu_solver.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
+               run bench_bf16f 300 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
+               run bench_bf16bigf 600 python bench.py --steps 2 --warmup 1 --rtm-dtype bf16 --npix 524288 --nvox 262144 --iters 20 &&
+               run bench_f 300 python bench.py --steps 5 --warmup 1 ;;
     probemall) run probe_mall 600 python tools/probe_mall.py ;;
     fcheck) run fcheck_bf16 600 python tools/fused_check.py --dtype bf16 8192x262144 65536x262144 &&
             SART_FUSED_SCHEDULE=5 run fcheck_bf16_s5 600 python tools/fused_check.py --dtype bf16 65536x262144 &&
