@@ -76,6 +76,33 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def visible_gpu_count() -> int:
+    """GPUs this process may use, counted without initialising HIP (a launcher must start from a process that has
+    not touched the GPU): HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES, else the GPU nodes
+    of the KFD topology (nodes with SIMDs), else torch's count."""
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        e = os.environ.get(v)
+        if e is not None:
+            return len([t for t in e.split(",") if t.strip() != ""])
+    nodes = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        n = 0
+        for d in os.listdir(nodes):
+            try:
+                with open(os.path.join(nodes, d, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+                n += int(props.get("simd_count", "0")) > 0
+            except (OSError, ValueError):
+                pass
+        if n:
+            return n
+    except OSError:
+        pass
+    import torch
+
+    return torch.cuda.device_count()
+
+
 def self_launch(n: int, argv: list[str], env_extra: dict) -> int:
     """Start N ranks of this script under torch.distributed.run (one rank per GPU) and return their exit
     code; rank 0's JSON line reaches our stdout unchanged. No GPU call happens in this process."""
@@ -162,19 +189,22 @@ def main() -> int:
     if world is None and args.gpus > 1:
         env_extra = {}
         if not args.launch_check:
-            import torch  # device_count() does not initialise the GPU
-
-            ndev = torch.cuda.device_count()
+            ndev = visible_gpu_count()
             if ndev < args.gpus and not args.share_gpus:
                 print(f"bench: --gpus {args.gpus} but only {ndev} GPU(s) visible (--share-gpus to rehearse "
                       "on fewer devices)", file=sys.stderr)
                 return 1
             if ndev < args.gpus:
-                env_extra["SART_DIST_BACKEND"] = "gloo"  # RCCL refuses two ranks on one device
+                # RCCL refuses two ranks on one device: gloo host collectives under the one-shot P2P all-reduce
+                # (auto-selected against the staged base), and the fused sweep on each rank's share of the CUs
+                env_extra.update(SART_DIST_BACKEND="gloo", SART_P2P_WRAP_STAGED="1", SART_FUSED_SHARED="1")
         return self_launch(args.gpus, sys.argv[1:], env_extra)
     if (world or 1) != args.gpus:
         print(f"bench: --gpus {args.gpus} but the launcher started {world or 1} rank(s)", file=sys.stderr)
         return 1
+    # A device all-reduce that waits this long for a peer gives up; the engine then re-solves the frame on the base
+    # communicator (RCCL), so a stalled P2P path costs one timeout instead of the watchdog's limit.
+    os.environ.setdefault("SART_P2P_TIMEOUT_S", "30")
 
     import torch
 
@@ -196,6 +226,7 @@ def main() -> int:
     from mpi_cuda_sartsolver_amd.parallel.partition import row_partition
     from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
 
+    t_setup = time.perf_counter()
     comm = init_distributed(use_gpu=True)
     n = comm.world_size
     wd = Watchdog(args.watchdog, comm.rank)
@@ -254,6 +285,7 @@ def main() -> int:
         g = prob.measurement
         runner = solver
     multi = args.frames > 1
+    startup = {"setup_s": round(time.perf_counter() - t_setup, 2)}  # process group, shard, engine, comm self-tests
     wd.kick("setup")
 
     selfcheck = None
@@ -267,6 +299,7 @@ def main() -> int:
 
         from mpi_cuda_sartsolver_amd.models.oracle import sart_oracle_f64
 
+        t_check = time.perf_counter()
         p1 = SolverParams(max_iterations=1, conv_tolerance=0.0)
         kw = dict(logarithmic=args.variant == "log", allow_zero_tolerance=True, partition=args.partition)
         gh = g.cpu().numpy() if hasattr(g, "cpu") else np.asarray(g)
@@ -278,7 +311,9 @@ def main() -> int:
         e2 = comm.all_reduce_scalar(float(np.linalg.norm(x2 - x64)) / nrm, op="max")
         selfcheck = {"iterations": 1, "rel_fused_vs_f64": ef, "rel_two_pass_vs_f64": e2}
         torch.cuda.empty_cache()
-        if not ef <= max(1.5 * e2, 1e-5):
+        startup["selfcheck_s"] = round(time.perf_counter() - t_check, 2)
+        # the same bound as the GPU tests (tests/test_gpu_solver.py: fused <= 1.25x the two-pass error)
+        if not ef <= max(1.25 * e2, 1e-5):
             print(f"bench: fused sweep self-check failed: {selfcheck}", file=sys.stderr, flush=True)
             return 2
         wd.kick("selfcheck")
@@ -292,11 +327,13 @@ def main() -> int:
     t0 = time.perf_counter()
     iters = 0
     comm_ms = 0.0
+    comm_fallbacks = 0
     res = None
     for i in range(args.steps):
         res = runner.solve(g)
         iters += res.iterations
         comm_ms += max(getattr(res, "comm_ms", -1.0), 0.0)
+        comm_fallbacks += int(getattr(res, "comm_fallbacks", 0))
         wd.kick(f"step {i}")
     torch.cuda.synchronize()
     comm.barrier()
@@ -338,9 +375,12 @@ def main() -> int:
                         "ld": solver.ld} if use_fused else None),
         "selfcheck": selfcheck,
         "shared_gpus": bool(getattr(solver, "shared_device", False)) if not multi else None,
+        "fused_plan_cus": solver.plan_cus if use_fused else None,
+        "startup": startup,
         "frames_per_step": args.frames,
         # per-iteration device all-reduce: RCCL, or the one-shot P2P kernel when it beat RCCL at start-up
         "allreduce": (solver.native_comm.describe if n > 1 else "none (1 rank)"),
+        "allreduce_fallbacks": comm_fallbacks,  # timed steps re-solved after a device all-reduce timeout
         # rank 0's GPU time inside the all-reduces per SART iteration (includes waiting for slower ranks)
         "allreduce_us_per_iter": (round(1e3 * comm_ms / max(iters, 1), 2) if n > 1 and not multi else None),
         "effective_hbm_TBps_per_gpu": round(bytes_per_iter * iters_per_s / 1e12, 3),

@@ -39,6 +39,8 @@ static py::dict solve_info(const sart::SolveInfo& i) {
     d["used_fused"] = i.used_fused;
     d["fused_variant"] = i.fused_variant;
     d["fallbacks"] = i.fallbacks;
+    d["comm_fallbacks"] = i.comm_fallbacks;
+    d["comm"] = std::string(i.comm ? i.comm : "");
     d["nonfinite"] = i.nonfinite;
     d["ms"] = i.ms;
     d["sweeps"] = i.sweeps;
@@ -55,6 +57,9 @@ static void bind_engine(py::module_& m) {
         .def_property_readonly("backend", &sart::Communicator::backend)
         .def_property_readonly("describe", &sart::Communicator::describe)
         .def("check", &sart::Communicator::check)
+        .def("device_failed", &sart::Communicator::device_failed)
+        .def_property_readonly("degradable", &sart::Communicator::degradable)
+        .def("degrade", &sart::Communicator::degrade)
         .def("barrier", [](sart::Communicator& c) { c.host().barrier(); }, py::call_guard<py::gil_scoped_release>())
         .def("abort", &sart::Communicator::abort)
         .def("all_reduce_host",
@@ -165,7 +170,8 @@ static void bind_engine(py::module_& m) {
         .def_readwrite("rtm_bf16", &sart::EngineConfig::rtm_bf16)
         .def_readwrite("mf_split_a", &sart::EngineConfig::mf_split_a)
         .def_readwrite("fault_inject", &sart::EngineConfig::fault_inject)
-        .def_readwrite("fault_nan_sweep", &sart::EngineConfig::fault_nan_sweep);
+        .def_readwrite("fault_nan_sweep", &sart::EngineConfig::fault_nan_sweep)
+        .def_readwrite("fused_max_cus", &sart::EngineConfig::fused_max_cus);
     m.def("validate_config", [](const sart::EngineConfig& c) {
         try {
             sart::validate_params(c);
@@ -226,6 +232,8 @@ static void bind_engine(py::module_& m) {
         .def_property_readonly("num_cus", &sart::Engine::num_cus)
         .def_property_readonly("column_shard", &sart::Engine::column_shard)
         .def_property_readonly("shared_device", &sart::Engine::shared_device)
+        .def_property_readonly("ranks_per_device", &sart::Engine::ranks_per_device)
+        .def_property_readonly("plan_cus", &sart::Engine::plan_cus)
         .def_property_readonly("nrows", &sart::Engine::nrows)
         .def_property_readonly("nvoxel", &sart::Engine::nvoxel)
         .def_property_readonly("stream", [](const sart::Engine& e) { return reinterpret_cast<uintptr_t>(e.stream()); })

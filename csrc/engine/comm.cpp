@@ -4,6 +4,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -12,6 +13,7 @@
 #include <functional>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../kernels/launchers.hpp"
@@ -108,13 +110,21 @@ double env_double(const char* name, double dflt) {
 class P2pComm final : public Communicator {
    public:
     P2pComm(int device, std::shared_ptr<Communicator> base) : base_(std::move(base)), device_(device) {
+        t_start_ = std::chrono::steady_clock::now();
         HostComm& h = base_->host();
         rank_ = h.rank();
         n_ = h.size();
         const char* m = std::getenv("SART_P2P");
         const std::string mode = (m && *m) ? m : "auto";
         cap_ = std::max<int64_t>(1024, (int64_t)(env_double("SART_P2P_MAX_BYTES", 2.0 * 1024 * 1024) / 4) / 4 * 4);
-        timeout_s_ = env_double("SART_P2P_TIMEOUT_S", 600.0);
+        // a healthy peer is at most a few sweeps behind (the host collectives of every frame's setup align the
+        // ranks first), so a P2P wait this long means the peer is gone or stuck: the engines then switch to the
+        // base communicator and re-solve the frame (device_failed / degrade)
+        timeout_s_ = env_double("SART_P2P_TIMEOUT_S", 60.0);
+        if (const char* f = std::getenv("SART_FAULT_P2P"); f && *f) {
+            const char* fr = std::getenv("SART_FAULT_RANK");
+            if (!(fr && *fr) || std::atoi(fr) == rank_) fault_call_ = std::atoll(f);
+        }
         if (mode == "0" || mode == "off") {
             finish(false, "p2p off (SART_P2P=0)");
             return;
@@ -180,9 +190,12 @@ class P2pComm final : public Communicator {
     std::string describe() const override { return why_; }
     void all_reduce(float* dev, size_t n, ReduceOp op, hipStream_t stream) override {
         // the choice depends only on n (identical on every rank), never on this rank's pointer alignment
-        if (active_ && n > 0 && (int64_t)n <= max_n_)
-            p2p(dev, (int64_t)n, op == ReduceOp::kSum ? 0 : 1, stream);
-        else
+        if (active_ && n > 0 && (int64_t)n <= max_n_) {
+            // SART_FAULT_P2P=k (tests): the k-th P2P all-reduce of this process raises no flags (a peer that never
+            // arrives), only on SART_FAULT_RANK when that is set
+            const bool skip = fault_call_ > 0 && ++calls_ == fault_call_;
+            p2p(dev, (int64_t)n, op == ReduceOp::kSum ? 0 : 1, stream, -1.0, skip);
+        } else
             base_->all_reduce(dev, n, op, stream);
     }
     void all_reduce(double* dev, size_t n, ReduceOp op, hipStream_t stream) override {
@@ -197,18 +210,39 @@ class P2pComm final : public Communicator {
         base_->abort();
     }
     void check() override {
-        if (!err_) return;
-        unsigned e[2] = {0, 0};
-        hip_ok(hipMemcpy(e, err_, sizeof(e), hipMemcpyDeviceToHost), "p2p error word");
-        if (e[1]) throw std::runtime_error("p2p all-reduce: a peer aborted");
-        if (e[0]) throw std::runtime_error("p2p all-reduce: a peer did not arrive within SART_P2P_TIMEOUT_S");
+        if (err_ && active_) {
+            const auto e = err_words();
+            if (e.second) throw std::runtime_error("p2p all-reduce: a peer aborted");
+            if (e.first) throw std::runtime_error("p2p all-reduce: a peer did not arrive within SART_P2P_TIMEOUT_S");
+        }
         base_->check();
+    }
+    bool device_failed() override {
+        if (!err_ || !active_) return false;
+        const auto e = err_words();
+        return e.first != 0 && e.second == 0;  // a timeout; a peer's abort is fatal (check() throws)
+    }
+    bool degradable() const override { return active_; }
+    bool degrade() override {
+        if (!active_) return false;
+        active_ = false;
+        why_ = std::string(base_->backend()) + " (p2p disabled after a p2p all-reduce timeout; was: " + why_ + ")";
+        return true;
     }
 
    private:
+    std::pair<unsigned, unsigned> err_words() {  // {timeout, abort}
+        unsigned e[2] = {0, 0};
+        hip_ok(hipMemcpy(e, err_, sizeof(e), hipMemcpyDeviceToHost), "p2p error word");
+        return {e[0], e[1]};
+    }
     void finish(bool active, const std::string& why) {
         active_ = active;
-        why_ = why;
+        // start-up cost (IPC mapping, self-test, auto probe) on this rank, reported with the selection
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start_).count();
+        char buf[64];
+        std::snprintf(buf, sizeof(buf), " [p2p setup %.0f ms]", ms);
+        why_ = why + buf;
         if (active && max_n_ == 0) max_n_ = cap_;  // forced on: every vector that fits the slots
     }
     bool agree(bool ok) {  // every rank learns whether all succeeded
@@ -266,9 +300,9 @@ class P2pComm final : public Communicator {
         }
         return ok;  // the caller's agree() is also the barrier: every flag array is zeroed before any push
     }
-    void p2p(float* dev, int64_t n, int op, hipStream_t stream, double timeout_s = -1) {
+    void p2p(float* dev, int64_t n, int op, hipStream_t stream, double timeout_s = -1, bool skip_flags = false) {
         launch_p2p_allreduce(dev, dev, n, args_, rank_, n_, ++epoch_, cap_, op, err_,
-                             timeout_s > 0 ? timeout_s : timeout_s_, stream);
+                             timeout_s > 0 ? timeout_s : timeout_s_, stream, skip_flags);
     }
     // Exact checks: integer-valued sums / maxima, and random fp32 data against the rank-order sum (the
     // kernel's result must be bitwise identical to ((v0 + v1) + v2) + ... on every rank), both parities.
@@ -352,7 +386,9 @@ class P2pComm final : public Communicator {
     int device_ = 0, rank_ = 0, n_ = 1;
     int64_t cap_ = 0;
     int64_t max_n_ = 0;  // P2P for n <= max_n_ (auto: largest probed size at which it beat the base)
-    double timeout_s_ = 600.0;
+    double timeout_s_ = 60.0;
+    int64_t fault_call_ = 0, calls_ = 0;  // SART_FAULT_P2P
+    std::chrono::steady_clock::time_point t_start_;
     bool active_ = false;
     std::string why_, err_msg_;
     hipStream_t stream_ = nullptr;

@@ -37,8 +37,18 @@ class Communicator {
     virtual bool graph_capturable() const { return false; }
     // Tear down after a fatal error so that peers blocked in a collective fail instead of hanging.
     virtual void abort() { host().abort(); }
-    // Throws when a device collective reported a failure (p2p: a peer never arrived). Call after a sync.
+    // Throws when a device collective reported a failure (p2p: a peer aborted, or never arrived while the
+    // p2p path is still active). Call after a sync.
     virtual void check() {}
+    // Recoverable device-collective failure on THIS rank since construction (p2p: a peer did not arrive within
+    // SART_P2P_TIMEOUT_S; the call's output is NaN). Call after a sync; the engines agree on it over the host
+    // communicator, then every rank calls degrade() and re-solves.
+    virtual bool device_failed() { return false; }
+    // True while degrade() has something to switch to (the engines agree on failures only then).
+    virtual bool degradable() const { return false; }
+    // Serve every device collective from the base path from now on (p2p -> RCCL / staged). Collective in the
+    // sense that every rank must call it after the same solve.
+    virtual bool degrade() { return false; }
     // Human-readable selection (backend and why), e.g. for benchmark logs.
     virtual std::string describe() const { return backend(); }
     int rank() { return host().rank(); }

@@ -34,24 +34,39 @@ bool fault_rank_selected(int rank) {
 
 }  // namespace
 
-bool device_shared_across_ranks(Communicator* comm, int device) {
+int ranks_sharing_device(Communicator* comm, int device) {
     const int n = comm->size();
-    if (n <= 1) return false;
-    // identity of the physical GPU: host name + PCI bus id (device ordinals differ under per-rank
-    // HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES and LOCAL_WORLD_SIZE is launcher-specific)
+    if (n <= 1) return 1;
+    // identity of the physical GPU: boot id + host name + PCI bus id (device ordinals differ under per-rank
+    // HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES and LOCAL_WORLD_SIZE is launcher-specific; containers on
+    // different nodes can share a host name and bus ids, but not the kernel's boot id)
     char bus[64] = {0};
     hip_ok(hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, device), "hipDeviceGetPCIBusId");
     char host[256] = {0};
     (void)gethostname(host, sizeof(host) - 1);
-    uint64_t h = 1469598103934665603ull;  // FNV-1a over "host/bus"
-    for (const char* p : {static_cast<const char*>(host), "/", static_cast<const char*>(bus)})
+    char boot[64] = {0};
+    if (FILE* f = std::fopen("/proc/sys/kernel/random/boot_id", "r")) {
+        if (!std::fgets(boot, sizeof(boot), f)) boot[0] = 0;
+        std::fclose(f);
+    }
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over "boot/host/bus"
+    for (const char* p : {static_cast<const char*>(boot), "/", static_cast<const char*>(host), "/",
+                          static_cast<const char*>(bus)})
         for (; *p; ++p) h = (h ^ (unsigned char)*p) * 1099511628211ull;
     std::vector<double> keys((size_t)n, 0.0);
     keys[(size_t)comm->rank()] = (double)(h >> 12) + 1.0;  // < 2^53: exact in fp64; one nonzero slot per rank
     comm->host().all_reduce_host(keys.data(), keys.size(), ReduceOp::kSum);
     std::sort(keys.begin(), keys.end());
-    return std::adjacent_find(keys.begin(), keys.end()) != keys.end();
+    int most = 1;  // the largest number of ranks on one GPU (identical on every rank)
+    for (size_t i = 0, j = 0; i < keys.size(); i = j) {
+        for (j = i; j < keys.size() && keys[j] == keys[i]; ++j) {
+        }
+        most = std::max(most, (int)(j - i));
+    }
+    return most;
 }
+
+bool device_shared_across_ranks(Communicator* comm, int device) { return ranks_sharing_device(comm, device) > 1; }
 
 double fused_min_bytes_from_env() {
     const char* e = std::getenv("SART_FUSED_MIN_MB");
@@ -129,29 +144,47 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
     xcnt_.resize(16);
     xprev_.resize(ld_);
     use_fused_ = false;
-    // The fused sweep is a persistent grid that needs every CU of its GPU co-resident: ranks sharing one
-    // GPU (one-GPU rehearsals of an N-rank run) would starve each other's hand-offs, so they use the
-    // two-pass kernels (SART_FUSED_SHARED=1 keeps the fused sweep; the collective fallback then recovers
-    // from protocol timeouts). Decided from device identity, identically on every rank of the group.
-    shared_device_ = !cfg_.column_shard && device_shared_across_ranks(comm_, device_);
+    // The fused sweep is a persistent grid whose workgroups must all be co-resident. Ranks sharing one GPU
+    // (one-GPU rehearsals of an N-rank run) therefore plan their grids on disjoint shares of the CUs: with
+    // SART_FUSED_SHARED=1 each rank's geometry targets num_cus / (ranks per GPU) CUs (8 XCDs x CUs per XCD,
+    // every workgroup one CU by its LDS), so the grids of all ranks fit side by side; without it ranks that share
+    // a GPU use the two-pass kernels. EngineConfig::fused_max_cus / SART_FUSED_CUS caps the plan explicitly.
+    // Decided from device identity, identically on every rank of the group.
+    ranks_per_device_ = cfg_.column_shard ? 1 : ranks_sharing_device(comm_, device_);
+    shared_device_ = ranks_per_device_ > 1;
     const char* fs = std::getenv("SART_FUSED_SHARED");
     const bool fused_ok_shared = fs && std::string(fs) == "1";
     if (shared_device_ && cfg_.use_fused && !fused_ok_shared && comm_->rank() == 0)
-        std::fprintf(stderr, "sart: %d ranks share GPUs; using the two-pass kernels (the fused sweep needs a device "
-                             "to itself)\n", comm_->size());
+        std::fprintf(stderr, "sart: %d ranks share GPUs; using the two-pass kernels (SART_FUSED_SHARED=1 splits the "
+                             "CUs between their fused sweeps)\n", comm_->size());
+    plan_cus_ = num_cus_;
+    if (shared_device_) plan_cus_ = num_cus_ / ranks_per_device_;
+    if (const char* c = std::getenv("SART_FUSED_CUS"); c && *c && cfg_.fused_max_cus <= 0) cfg_.fused_max_cus = std::atoi(c);
+    if (cfg_.fused_max_cus > 0) plan_cus_ = std::min(plan_cus_, cfg_.fused_max_cus);
+    plan_cus_ = plan_cus_ / 8 * 8;  // whole CUs per XCD
     // bf16 storage: the fused sweep exists as variant 6 only (else the two-pass kernels)
     const double abytes = (double)Pp_ * (double)ld_ * (cfg_.rtm_bf16 ? 2.0 : 4.0);
-    if (cfg_.use_fused && !cfg_.column_shard && abytes >= cfg_.fused_min_bytes &&
+    if (cfg_.use_fused && !cfg_.column_shard && abytes >= cfg_.fused_min_bytes && plan_cus_ >= 8 &&
         (!shared_device_ || fused_ok_shared) && (!cfg_.rtm_bf16 || cfg_.fused_variant == 6)) {
-        geom_ = fused_geometry(ld_, num_cus_, cfg_.fused_variant, cfg_.rows_per_tile, !cfg_.rtm_bf16);
+        geom_ = fused_geometry(ld_, plan_cus_, cfg_.fused_variant, cfg_.rows_per_tile, !cfg_.rtm_bf16);
         if (cfg_.rtm_bf16 && (cfg_.rows_per_tile == 0 || cfg_.rows_per_tile == 4)) {
             // wide bf16 tiles (8 KB per wave per step, like fp32) where the width allows; SART_BF16_WIDE=0 keeps
             // the narrow tiles
             const char* w = std::getenv("SART_BF16_WIDE");
-            const FusedGeometry gw = fused_geometry_bf16_wide(ld_, num_cus_);
+            const FusedGeometry gw = fused_geometry_bf16_wide(ld_, plan_cus_);
             if (gw.valid() && !(w && std::string(w) == "0")) geom_ = gw;
         }
         use_fused_ = geom_.valid() && (!cfg_.rtm_bf16 || geom_.variant == 6);
+    }
+    // Every rank runs the fused sweep or none does: shards of different heights can land on both sides of
+    // fused_min_bytes, and a rank on the two-pass kernels would then see its peers' protocol errors (the error
+    // word rides in the all-reduce) without a fused sweep of its own to fall back from.
+    if (comm_->size() > 1 && !cfg_.column_shard) {
+        const double off = comm_->host().all_reduce_scalar(use_fused_ ? 0.0 : 1.0, ReduceOp::kMax);
+        if (off > 0.0 && use_fused_) {
+            use_fused_ = false;
+            geom_ = FusedGeometry{};
+        }
     }
     alloc_fused();
     ray_sums();
@@ -492,11 +525,13 @@ void Engine::run_chunk(int n) {
 
 bool Engine::fallback() {
     RoctxRange r("sart::fallback");
-    // A persistent sweep gave up waiting (SartState.error): XCD-local groups (variant 6) -> generic
-    // groups (variant 3) -> two-pass kernels. The frame is re-solved from scratch.
+    // A persistent sweep gave up waiting (SartState.error, set on every rank by the all-reduced error word):
+    // XCD-local groups (variant 6) -> generic groups (variant 3) -> two-pass kernels. The frame is re-solved from
+    // scratch. A rank whose own kernels are already the two-pass ones re-solves on them: its peers step down
+    // their chains and re-solve too, so every rank enters the same number of collectives.
     drop_graph();
     if (use_fused_ && geom_.variant == 6 && !cfg_.rtm_bf16) {
-        const FusedGeometry g3 = fused_geometry(ld_, num_cus_, 3, 0);
+        const FusedGeometry g3 = fused_geometry(ld_, plan_cus_, 3, 0);
         if (g3.valid()) {
             std::fprintf(stderr, "sart: fused sweep variant 6 timed out (unexpected workgroup placement); using variant 3\n");
             geom_ = g3;
@@ -507,10 +542,20 @@ bool Engine::fallback() {
     if (use_fused_) {
         std::fprintf(stderr, "sart: fused sweep protocol timeout; switching to the two-pass kernels\n");
         use_fused_ = false;
-        return true;
     }
-    return false;
+    return true;
 }
+
+bool device_comm_failed_anywhere(Communicator* comm) {
+    // The P2P all-reduce of one rank can time out while its peers complete the same call (they received every
+    // flag), so whether a frame must be re-solved is agreed over the host communicator after every solve, while
+    // a degradable device path is active (one host scalar per frame).
+    if (comm->size() <= 1 || !comm->degradable()) return false;
+    const bool mine = comm->device_failed();
+    return comm->host().all_reduce_scalar(mine ? 1.0 : 0.0, ReduceOp::kMax) > 0.0;
+}
+
+bool Engine::comm_failed_anywhere() { return device_comm_failed_anywhere(comm_); }
 
 SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
     RoctxRange range("sart::solve");
@@ -559,10 +604,22 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
         hip_ok(hipStreamSynchronize(stream_), "solve");
         collect_comm(0);  // chunks issued after the last check
         collect_comm(1);
+        if (comm_failed_anywhere()) {
+            // a device all-reduce timed out somewhere (its output is NaN there): every rank switches to the base
+            // communicator and re-solves the frame; a second failure on the base path is fatal
+            ++info.comm_fallbacks;
+            const bool had = comm_->degrade();
+            if (comm_->rank() == 0)
+                std::fprintf(stderr, "sart: device all-reduce timed out; re-solving on %s\n", comm_->backend());
+            if (!had || info.comm_fallbacks > 1) throw std::runtime_error("SART engine: device all-reduce failed");
+            drop_graph();
+            continue;
+        }
         comm_->check();
         if (error) {
             ++info.fallbacks;
-            if (!fallback()) throw std::runtime_error("SART engine: persistent sweep failed without fallback");
+            if (info.fallbacks > 4 || !fallback())
+                throw std::runtime_error("SART engine: persistent sweep failed without fallback");
             continue;
         }
         break;
@@ -582,6 +639,7 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
     info.convergence = s.conv_last;
     info.nonfinite = (s.flags & 1) != 0;
     info.used_fused = use_fused_;
+    info.comm = comm_->backend();
     info.fused_variant = use_fused_ ? geom_.variant : -1;
     info.sweeps = s.sweep;
     info.comm_ms = timing_collectives() ? comm_ms_ : -1.0;

@@ -70,6 +70,9 @@ struct EngineConfig : SolverParams {
     // MFMA. 1: on, 0: off, -1: env SART_MF_X3 (0 / 1), else on for batches of 32 and 64 frames (where fp32
     // MFMA bounds the sweep; at 16 frames both paths are HBM-bound).
     int mf_split_a = -1;
+    // Fused sweep: plan the persistent grid for at most this many CUs (0: all; env SART_FUSED_CUS). Ranks that
+    // share a GPU (SART_FUSED_SHARED=1) plan for num_cus / (ranks per GPU) each.
+    int fused_max_cus = 0;
 };
 
 // roctx range (rocprofv3 --marker-trace) for the lifetime of the object.
@@ -109,8 +112,14 @@ struct DeviceRaySums {
     DeviceArray<float> ray_len, dinv, dscale, dmask;
 };
 
-// True when two ranks of `comm` drive the same physical GPU (host name + PCI bus id). Collective.
-bool device_shared_across_ranks(Communicator* comm, int device);
+// The largest number of ranks of `comm` that drive one physical GPU (boot id + host name + PCI bus id), identical
+// on every rank; 1 when every rank has a GPU of its own. Collective.
+int ranks_sharing_device(Communicator* comm, int device);
+bool device_shared_across_ranks(Communicator* comm, int device);  // ranks_sharing_device(...) > 1
+
+// Collective, after a synchronised solve: true on every rank when a degradable device all-reduce (P2P) failed on
+// some rank (then every rank calls comm->degrade() and re-solves). One host scalar while P2P is active, else free.
+bool device_comm_failed_anywhere(Communicator* comm);
 
 // SART_FUSED_MIN_MB (default 128): the drivers' threshold for EngineConfig::fused_min_bytes.
 double fused_min_bytes_from_env();
@@ -144,6 +153,8 @@ class Engine {
     std::vector<double> ray_length() const;   // fp64 (nrows): this shard's pixels (row shard) / global (column)
     bool column_shard() const { return cfg_.column_shard; }
     bool shared_device() const { return shared_device_; }
+    int ranks_per_device() const { return ranks_per_device_; }
+    int plan_cus() const { return plan_cus_; }  // CUs the fused geometry was planned for
     double last_norm() const { return norm_; }
 
    private:
@@ -157,7 +168,8 @@ class Engine {
     void fwd(int epi, const float* x, float* out_f, float* out_w, double* Fpart, const SartState* st);
     void bwd(const float* w, const SartState* st);
     void run_chunk(int n);
-    bool fallback();  // false when nothing is left to fall back to
+    bool fallback();  // steps the fused-sweep fallback chain (re-solve on the current kernels at its end)
+    bool comm_failed_anywhere();  // collective: a degradable device all-reduce failed on some rank
     void drop_graph();
     void set_device() const;
 
@@ -179,6 +191,8 @@ class Engine {
     DeviceArray<float> partial_, comm_buf_, x_, pen_, O_, ghat_, arow_, gpos_, wo_, w_, fitted_;
     DeviceArray<float> xprev_;  // x before the last update (NaN/Inf guard rollback)
     bool shared_device_ = false;
+    int ranks_per_device_ = 1;
+    int plan_cus_ = 0;
     DeviceArray<double> Fpart_, g64_, x064_;
     DeviceRaySums rs_;
     DeviceArray<SartState> st_;

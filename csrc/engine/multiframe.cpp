@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -279,6 +280,27 @@ void MultiFrameEngine::admit(const double* g, const std::vector<int>& slots, con
 
 std::vector<SolveInfo> MultiFrameEngine::solve_batch(const double* g, int nframes, double* x_out, const double* x0,
                                                      bool chain) {
+    // a device all-reduce that timed out on some rank (P2P: a peer never arrived) is agreed over the host
+    // communicator; every rank then switches to the base communicator and re-solves the batch once
+    for (int attempt = 0;; ++attempt) {
+        std::vector<SolveInfo> out = solve_batch_once(g, nframes, x_out, x0, chain);
+        if (!device_comm_failed_anywhere(comm_)) {
+            comm_->check();
+            for (auto& info : out) {
+                info.comm_fallbacks = attempt;
+                info.comm = comm_->backend();
+            }
+            return out;
+        }
+        const bool had = comm_->degrade();
+        if (comm_->rank() == 0)
+            std::fprintf(stderr, "sart: device all-reduce timed out; re-solving the batch on %s\n", comm_->backend());
+        if (!had || attempt >= 1) throw std::runtime_error("MultiFrameEngine: device all-reduce failed");
+    }
+}
+
+std::vector<SolveInfo> MultiFrameEngine::solve_batch_once(const double* g, int nframes, double* x_out,
+                                                          const double* x0, bool chain) {
     set_device();
     RoctxRange range("sart::mf_solve");
     const int NF = nf_;
@@ -424,7 +446,7 @@ std::vector<SolveInfo> MultiFrameEngine::solve_batch(const double* g, int nframe
         }
     }
     hip_ok(hipStreamSynchronize(stream_), "mf solve");
-    comm_->check();
+    if (comm_stream_) hip_ok(hipStreamSynchronize(comm_stream_), "mf comm");
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (auto& info : out) info.ms = ms / nframes;
     return out;

@@ -46,6 +46,7 @@ class MultiFrameEngine {
     static int batch_width(int frames);
 
    private:
+    std::vector<SolveInfo> solve_batch_once(const double* g, int nframes, double* x_out, const double* x0, bool chain);
     // frames[q] of g into slots[q] (normalisation, prep, start value, log observed back-projection, state)
     // Start value: warm (host, de-normalised), else dev_src (a finished frame's normalised solution still on
     // the device, normalisation src_norm), else cold.

@@ -105,8 +105,10 @@ struct P2pArgs {
 };
 int64_t p2p_chunk(int64_t n);  // elements per workgroup
 // op: 0 sum, 1 max. `epoch` strictly increases by one per call on every rank (starts at 1).
+// skip_flags (fault injection, tests): push the data but raise no flag, so the peers time out in this call.
 void launch_p2p_allreduce(const float* in, float* out, int64_t n, const P2pArgs& a, int rank, int nranks,
-                          unsigned epoch, int64_t cap, int op, unsigned* err, double timeout_s, hipStream_t stream);
+                          unsigned epoch, int64_t cap, int op, unsigned* err, double timeout_s, hipStream_t stream,
+                          bool skip_flags = false);
 // multiframe.hip (nf = frames per batch: 16, 32 or 64)
 int mf_forward_num_splits(int64_t ld, int64_t nrows_pad);
 int mf_backproject_num_splits(int64_t ld, int64_t nrows);

@@ -32,9 +32,16 @@ __device__ inline float red(float a, float b, int op) { return op == 0 ? a + b :
 __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* out, int64_t n, int64_t chunk,
                                                        P2pArgs a, int rank, int nranks, unsigned epoch, int parity,
                                                        int64_t cap, int op, unsigned* err, uint64_t timeout_ticks,
-                                                       int vec_io) {
+                                                       int vec_io, int skip_flags) {
     const int64_t c0 = (int64_t)blockIdx.x * chunk;
     const int64_t c1 = c0 + chunk < n ? c0 + chunk : n;
+    // After a timeout on this rank the device path is being abandoned (the engines agree on it after the solve and
+    // switch to the base communicator): later calls fail at once, without pushing or raising flags, so a solve
+    // pays one timeout per rank instead of one per queued sweep.
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+        for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) out[i] = __builtin_nanf("");
+        return;
+    }
     const int64_t mine = (int64_t)(parity * kP2pMaxRanks + rank) * cap;  // my slot in every receive buffer
 
     // phase 1: push this chunk into slot [parity][rank] of every rank's receive buffer (self included)
@@ -54,7 +61,7 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
     __shared__ int timed_out;
     if (threadIdx.x == 0) timed_out = 0;
     __syncthreads();
-    if ((int)threadIdx.x < nranks && (int)threadIdx.x != rank) {
+    if ((int)threadIdx.x < nranks && (int)threadIdx.x != rank && !skip_flags) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: the pushed bytes reach every peer
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(a.flags[threadIdx.x] + rank * kP2pMaxBlocks + blockIdx.x, epoch, __ATOMIC_RELAXED,
@@ -119,7 +126,8 @@ int64_t p2p_chunk(int64_t n) {
 }
 
 void launch_p2p_allreduce(const float* in, float* out, int64_t n, const P2pArgs& a, int rank, int nranks,
-                          unsigned epoch, int64_t cap, int op, unsigned* err, double timeout_s, hipStream_t stream) {
+                          unsigned epoch, int64_t cap, int op, unsigned* err, double timeout_s, hipStream_t stream,
+                          bool skip_flags) {
     if (n <= 0) return;
     if (nranks < 1 || nranks > kP2pMaxRanks || rank < 0 || rank >= nranks || n > cap || cap % 4 != 0)
         throw std::runtime_error("launch_p2p_allreduce: bad arguments (n=" + std::to_string(n) + ", cap=" +
@@ -131,7 +139,7 @@ void launch_p2p_allreduce(const float* in, float* out, int64_t n, const P2pArgs&
     if (blocks > kP2pMaxBlocks) throw std::runtime_error("launch_p2p_allreduce: too many chunks");
     const uint64_t ticks = (uint64_t)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
     hipLaunchKernelGGL(k_p2p_allreduce, dim3((unsigned)blocks), dim3(256), 0, stream, in, out, n, chunk, a, rank,
-                       nranks, epoch, (int)(epoch & 1u), cap, op, err, ticks, vec_io);
+                       nranks, epoch, (int)(epoch & 1u), cap, op, err, ticks, vec_io, skip_flags ? 1 : 0);
     check_launch("k_p2p_allreduce");
 }
 

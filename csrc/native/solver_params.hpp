@@ -28,6 +28,8 @@ struct SolveInfo {
     bool used_fused = false;
     int fused_variant = -1;
     int fallbacks = 0;        // persistent-kernel protocol timeouts survived during this solve
+    int comm_fallbacks = 0;   // device all-reduce timeouts survived (the frame re-solved on the base communicator)
+    const char* comm = "";    // device communicator that produced the result (static string)
     bool nonfinite = false;   // the iteration produced NaN/Inf and was stopped
     double ms = 0.0;
     int sweeps = 0;           // sweeps executed on the device (iterations + the final decision sweep)

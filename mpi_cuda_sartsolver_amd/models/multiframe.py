@@ -93,7 +93,8 @@ class MultiFrameSARTSolver:
             status = SUCCESS if info["status"] == SUCCESS else MAX_ITERATIONS_EXCEEDED
             r = SolveResult(solution=x[f], status=status, iterations=int(info["iterations"]),
                             convergence=float(info["convergence"]), used_fused=False,
-                            elapsed_ms=float(info["ms"]), nonfinite=bool(info["nonfinite"]))
+                            elapsed_ms=float(info["ms"]), nonfinite=bool(info["nonfinite"]),
+                            comm_fallbacks=int(info["comm_fallbacks"]), comm=str(info["comm"]))
             r.warm_from = int(info["warm_from"])
             out.append(r)
         return out

@@ -83,6 +83,8 @@ class SolveResult:
     elapsed_ms: float = 0.0
     comm_ms: float = -1.0  # GPU time in the per-sweep all-reduces (time_collectives=True), else -1
     fallbacks: int = 0      # persistent-sweep timeouts recovered in this solve (identical on every rank)
+    comm_fallbacks: int = 0  # device all-reduce timeouts recovered (re-solved on the base communicator)
+    comm: str = ""           # device communicator that produced the result (p2p / rccl / staged / local)
     fused_variant: int = -1  # fused sweep variant that produced the result (-1: two-pass kernels)
     nonfinite: bool = False  # stopped by the NaN/Inf guard: ``solution`` is the last finite iterate
     warm_from: int = -1      # multi-frame time series: frame whose solution started this one (-1: x0 / cold)
@@ -163,8 +165,18 @@ class SARTSolver:
 
     @property
     def shared_device(self) -> bool:
-        """Another rank of the group drives the same physical GPU (then the two-pass kernels are used)."""
+        """Another rank of the group drives the same physical GPU (two-pass kernels, or the fused sweep on a
+        share of the CUs with SART_FUSED_SHARED=1)."""
         return self.engine.shared_device
+
+    @property
+    def ranks_per_device(self) -> int:
+        return self.engine.ranks_per_device
+
+    @property
+    def plan_cus(self) -> int:
+        """CUs the fused geometry was planned for (all of them, or a share when ranks share the GPU)."""
+        return self.engine.plan_cus
 
     @property
     def geom(self):
@@ -193,7 +205,8 @@ class SARTSolver:
                            convergence=float(info["convergence"]), used_fused=bool(info["used_fused"]),
                            elapsed_ms=float(info["ms"]), comm_ms=float(info["comm_ms"]),
                            fallbacks=int(info["fallbacks"]), fused_variant=int(info["fused_variant"]),
-                           nonfinite=bool(info["nonfinite"]))
+                           nonfinite=bool(info["nonfinite"]), comm_fallbacks=int(info["comm_fallbacks"]),
+                           comm=str(info["comm"]))
 
     def gather_solution(self, x_local: np.ndarray) -> np.ndarray:
         """Full solution vector from the column shards of every rank (identity for a row shard)."""

@@ -34,16 +34,51 @@ def _run(nproc, out, extra, script="dist_check.py", **env_extra):
     return np.load(out + ".npy"), json.load(open(out + ".json"))
 
 
+def _laplacian(nvox):
+    from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+
+    return LaplacianCSR.grid_3d(16, 16, 16) if nvox == 4096 else None  # as tools/dist_check.py
+
+
+def _oracle_rel(tmp_path, xs, extra, iters):
+    """Rel. errors of the solutions xs (frame 0) against the fp64 oracle of the 1-rank problem (saved by
+    dist_check --save-problem), and the fp32 emulation's error on the same problem (the inherent fp32 error)."""
+    from mpi_cuda_sartsolver_amd.models.reference import sart_fp32_emulation, sart_gpu_semantics
+
+    A = np.load(str(tmp_path / "r1.A.npy"))
+    g = np.load(str(tmp_path / "r1.g.npy"))
+    L = _laplacian(A.shape[1])
+    kw = dict(max_iterations=iters, beta_laplace=1e-3, logarithmic="--logarithmic" in extra)
+    x64, _, _ = sart_gpu_semantics(A, g, L, conv_tolerance=0.0, **kw)
+    x32, _, _ = sart_fp32_emulation(A, g, L, **kw)
+    rel = lambda a: float(np.linalg.norm(a - x64) / np.linalg.norm(x64))  # noqa: E731
+    return [rel(x) for x in xs], rel(x32)
+
+
+# Multi-rank solutions are fp32 evaluations in another summation order (row blocks per rank, the all-reduce): every
+# one must stay within the fp32 emulation's distance of the fp64 oracle (single-GPU kernels: 0.42-0.63x of it).
+RANK_FACTOR = 1.0
+
+
 @pytest.mark.parametrize("extra", [[], ["--logarithmic"], ["--multiframe"], ["--multiframe", "--logarithmic"],
                                    ["--columns"], ["--columns", "--logarithmic"]])
 def test_gpu_solver_rank_invariance(tmp_path, extra):
-    x1, m1 = _run(1, str(tmp_path / "r1"), extra)
-    x2, m2 = _run(2, str(tmp_path / "r2"), extra)
-    x3, m3 = _run(3, str(tmp_path / "r3"), extra)
-    for x, m in ((x2, m2), (x3, m3)):
-        assert np.linalg.norm(x - x1) / np.linalg.norm(x1) < 2e-3
+    fixed = extra + ["--tol", "0", "--iters", "20"]
+    x1, m1 = _run(1, str(tmp_path / "r1"), fixed + ["--save-problem"])
+    x2, m2 = _run(2, str(tmp_path / "r2"), fixed)
+    x3, m3 = _run(3, str(tmp_path / "r3"), fixed)
+    (e1, e2, e3), e32 = _oracle_rel(tmp_path, [x1[0], x2[0], x3[0]], extra, 20)
+    assert max(e1, e2, e3) <= RANK_FACTOR * e32 + 1e-7, (e1, e2, e3, e32)
+    for m in (m2, m3):
         for a, b in zip(m, m1):
-            assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3
+            assert a["status"] == b["status"] and a["iterations"] == b["iterations"]
+    if "--multiframe" in extra:
+        return
+    # with the convergence test: the same statuses and (within 3) iteration counts at every rank count
+    c1 = _run(1, str(tmp_path / "c1"), extra)[1]
+    c3 = _run(3, str(tmp_path / "c3"), extra)[1]
+    for a, b in zip(c3, c1):
+        assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3
 
 
 @pytest.mark.parametrize("log", [False, True])
@@ -51,11 +86,13 @@ def test_column_shard_matches_row_shard(tmp_path, log):
     """The voxel-sharded layout (all-reduce of A.x per sweep) solves the same problem as the reference's
     pixel-sharded layout (all-reduce of the correction)."""
     extra = ["--logarithmic"] if log else []
-    xr, mr = _run(1, str(tmp_path / "rows"), extra)
-    xc, mc = _run(2, str(tmp_path / "cols"), extra + ["--columns"])
-    assert np.linalg.norm(xc - xr) / np.linalg.norm(xr) < 2e-3
+    fixed = extra + ["--tol", "0", "--iters", "20"]
+    xr, mr = _run(1, str(tmp_path / "r1"), fixed + ["--save-problem"])
+    xc, mc = _run(2, str(tmp_path / "cols"), fixed + ["--columns"])
+    (er, ec), e32 = _oracle_rel(tmp_path, [xr[0], xc[0]], extra, 20)
+    assert max(er, ec) <= RANK_FACTOR * e32 + 1e-7, (er, ec, e32)
     for a, b in zip(mc, mr):
-        assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3
+        assert a["status"] == b["status"] and a["iterations"] == b["iterations"]
 
 
 @pytest.mark.parametrize("nproc", [2, 3])
@@ -86,18 +123,21 @@ def test_p2p_auto_selection(tmp_path):
 def test_gpu_solver_rank_invariance_p2p(tmp_path, extra):
     """(The last case has 4 MB of corrections per sweep: the multi-frame engine reduces them in 4 voxel chunks
     on its comm stream, overlapped with the back-projection of the following chunks.)"""
-    x1, m1 = _run(1, str(tmp_path / "r1"), extra)
-    # different row partitions sum in different orders: fp32 drift grows with the width (3e-3 measured at
-    # 65536 voxels x 12 iterations; profiles/numerics_r2.jsonl)
-    tol = 6e-3 if "65536" in extra else 2e-3
+    iters = 12 if "--iters" in extra else 20
+    fixed = [e for e in extra] + ["--tol", "0"] + ([] if "--iters" in extra else ["--iters", "20"])
+    x1, m1 = _run(1, str(tmp_path / "r1"), fixed + ["--save-problem"])
+    xs = []
     for n in (2, 3):
-        x, m = _run(n, str(tmp_path / f"p{n}"), extra, SART_P2P="1")
+        x, m = _run(n, str(tmp_path / f"p{n}"), fixed, SART_P2P="1")
         assert m[0]["comm"] == "p2p"
         if "--multiframe" not in extra:
             assert m[0]["comm_ms"] > 0  # time_collectives: events around every per-sweep all-reduce
-        assert np.linalg.norm(x - x1) / np.linalg.norm(x1) < tol
+            assert m[0]["x_bitwise_equal"]
         for a, b in zip(m, m1):
-            assert a["status"] == b["status"] and abs(a["iterations"] - b["iterations"]) <= 3
+            assert a["status"] == b["status"] and a["iterations"] == b["iterations"]
+        xs.append(x[0])
+    errs, e32 = _oracle_rel(tmp_path, [x1[0]] + xs, extra, iters)
+    assert max(errs) <= RANK_FACTOR * e32 + 1e-7, (errs, e32)
 
 
 def test_p2p_peer_abort_fails_fast(tmp_path):
@@ -113,10 +153,62 @@ def test_p2p_peer_abort_fails_fast(tmp_path):
 
 
 def test_shared_device_detected_from_identity(tmp_path):
-    """Ranks on one physical GPU are detected from the PCI bus id (not LOCAL_WORLD_SIZE, which only torchrun
-    sets) on every rank, and use the two-pass kernels even when the fused sweep is requested."""
+    """Ranks on one physical GPU are detected from the device identity (boot id + host + PCI bus id, not
+    LOCAL_WORLD_SIZE, which only torchrun sets) on every rank, and use the two-pass kernels when the fused sweep is
+    requested without SART_FUSED_SHARED=1."""
     x, m = _run(2, str(tmp_path / "s2"), ["--fused"], LOCAL_WORLD_SIZE="1")
-    assert all(r["shared"] and not r["fused"] for r in m[0]["ranks"]), m[0]["ranks"]
+    assert all(r["shared"] and not r["fused"] and r["ranks_per_device"] == 2 for r in m[0]["ranks"]), m[0]["ranks"]
+
+
+FUSED_SHAPE = ["--fused", "--npix", "8192", "--nvox", "32768", "--iters", "20", "--tol", "0"]
+
+
+def test_fused_sweep_on_shared_gpu_two_ranks(tmp_path):
+    """The production multi-rank path on ONE GPU: 2 ranks, each running the fused sweep (variant 6) on its own half
+    of the CUs (SART_FUSED_SHARED=1: persistent grids planned for 128 CUs, side by side), with the one-shot P2P
+    all-reduce of the corrections every sweep. Every rank reports fused, no fallback and comm p2p; the replicated x
+    is bitwise identical on both ranks; both the 1-rank and the 2-rank solutions are within the fp32 emulation's
+    error of the fp64 oracle (reference loop: sartsolver_cuda.cpp:231-262)."""
+    x1, m1 = _run(1, str(tmp_path / "r1"), FUSED_SHAPE + ["--save-problem"])
+    assert m1[0]["fused"] and m1[0]["ranks"][0]["plan_cus"] >= 128
+    x2, m2 = _run(2, str(tmp_path / "p2"), FUSED_SHAPE, SART_FUSED_SHARED="1", SART_P2P="1")
+    ranks = m2[0]["ranks"]
+    for r in ranks:
+        assert r["fused"] and r["variant"] == 6 and r["fallbacks"] == 0 and r["fallbacks2"] == 0, ranks
+        assert r["comm"] == "p2p" and r["comm_fallbacks"] == 0 and r["ranks_per_device"] == 2, ranks
+        assert r["plan_cus"] * 2 <= m1[0]["ranks"][0]["plan_cus"] and r["grid"]["workgroups"] <= r["plan_cus"], ranks
+    assert m2[0]["x_bitwise_equal"]
+    for a, b in zip(m2, m1):
+        assert a["status"] == b["status"] == -1 and a["iterations"] == b["iterations"] == 20
+    (e1, e2), e32 = _oracle_rel(tmp_path, [x1[0], x2[0]], [], 20)
+    assert max(e1, e2) <= RANK_FACTOR * e32 + 1e-7, (e1, e2, e32)
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_p2p_timeout_degrades_to_base_on_every_rank(tmp_path, fused):
+    """A P2P all-reduce that times out on some rank mid-solve (SART_FAULT_P2P: rank 1 never raises its flags in
+    its 3rd call, so rank 0 waits SART_P2P_TIMEOUT_S) is agreed on after the solve: EVERY rank switches to the
+    base communicator (staged here, RCCL in production) and re-solves the frame; the result matches the 1-rank
+    solve and later frames stay on the base path. A stall costs about one timeout, not one per queued sweep."""
+    import time
+
+    extra = FUSED_SHAPE if fused else ["--iters", "20", "--tol", "0"]
+    x1, m1 = _run(1, str(tmp_path / "r1"), extra + ["--save-problem"])
+    env = dict(SART_P2P="1", SART_FAULT_P2P="3", SART_FAULT_RANK="1", SART_P2P_TIMEOUT_S="4")
+    if fused:
+        env["SART_FUSED_SHARED"] = "1"
+    t0 = time.monotonic()
+    x, m = _run(2, str(tmp_path / "f2"), extra, **env)
+    wall = time.monotonic() - t0
+    ranks = m[0]["ranks"]
+    for r in ranks:
+        assert r["comm_fallbacks"] == 1 and r["comm"] == "staged", ranks
+        assert r["comm_fallbacks2"] == 0 and r["comm2"] == "staged", ranks
+        assert r["fused"] == fused and r["fallbacks"] == 0, ranks
+    assert m[0]["x_bitwise_equal"]
+    assert wall < 120, wall
+    (e1, e2), e32 = _oracle_rel(tmp_path, [x1[0], x[0]], [], 20)
+    assert max(e1, e2) <= RANK_FACTOR * e32 + 1e-7, (e1, e2, e32)
 
 
 @pytest.mark.parametrize("nproc", [2, 3])

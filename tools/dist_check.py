@@ -14,11 +14,14 @@ def main():
     ap.add_argument("--npix", type=int, default=3000)
     ap.add_argument("--nvox", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--tol", type=float, default=1e-6, help="convergence tolerance (0: exactly --iters iterations)")
     ap.add_argument("--logarithmic", action="store_true")
     ap.add_argument("--fused", action="store_true")
     ap.add_argument("--multiframe", action="store_true")
     ap.add_argument("--batch", type=int, default=16, help="multi-frame batch width (16, 32, 64)")
     ap.add_argument("--columns", action="store_true", help="column (voxel) shards instead of row shards")
+    ap.add_argument("--save-problem", action="store_true",
+                    help="(1 rank) also save the global A and g as <out>.A.npy / <out>.g.npy for host oracles")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     import numpy as np
@@ -42,7 +45,10 @@ def main():
         b = row_partition(a.npix, comm.world_size, comm.rank)
         prob = make_problem(b.size, a.nvox, row_offset=b.offset, seed=7, device=dev, saturate_fraction=0.02)
     L = LaplacianCSR.grid_3d(16, 16, 16, device=dev) if a.nvox == 4096 else None
-    params = SolverParams(max_iterations=a.iters, conv_tolerance=1e-6, beta_laplace=1e-3)
+    if a.save_problem and comm.world_size == 1:  # the global problem (a 1-rank shard holds all of it)
+        np.save(a.out + ".A.npy", prob.rtm.to_host())
+        np.save(a.out + ".g.npy", prob.measurement.cpu().numpy())
+    params = SolverParams(max_iterations=a.iters, conv_tolerance=a.tol, beta_laplace=1e-3)
     if a.multiframe:
         from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
 
@@ -53,16 +59,27 @@ def main():
         meta = [dict(status=r.status, iterations=r.iterations, comm=s.native_comm.backend) for r in res]
     else:
         s = SARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic, use_fused=a.fused,
-                       partition="cols" if a.columns else None, time_collectives=True)
+                       partition="cols" if a.columns else None, time_collectives=True,
+                       allow_zero_tolerance=a.tol == 0)
         r = s.solve(prob.measurement)
         r2 = s.solve(prob.measurement, solution=r.solution)  # warm start path
         x = np.stack([s.gather_solution(r.solution), s.gather_solution(r2.solution)])
-        meta = [dict(status=r.status, iterations=r.iterations, fused=r.used_fused, comm=s.native_comm.backend,
-                     comm_ms=r.comm_ms, fallbacks=r.fallbacks, variant=r.fused_variant),
-                dict(status=r2.status, iterations=r2.iterations, fallbacks=r2.fallbacks)]
+        meta = [dict(status=r.status, iterations=r.iterations, fused=r.used_fused, comm=r.comm or s.native_comm.backend,
+                     comm_ms=r.comm_ms, fallbacks=r.fallbacks, comm_fallbacks=r.comm_fallbacks, variant=r.fused_variant,
+                     describe=s.native_comm.describe),
+                dict(status=r2.status, iterations=r2.iterations, fallbacks=r2.fallbacks, comm=r2.comm,
+                     comm_fallbacks=r2.comm_fallbacks)]
         # every rank's fallback history: a persistent-sweep timeout must be handled identically everywhere
-        meta[0]["ranks"] = comm.all_gather_object(dict(fallbacks=r.fallbacks, variant=r.fused_variant,
-                                                       fused=r.used_fused, shared=s.shared_device))
+        g = s.geom
+        meta[0]["ranks"] = comm.all_gather_object(dict(
+            fallbacks=r.fallbacks, variant=r.fused_variant, fused=r.used_fused, shared=s.shared_device,
+            comm=r.comm, comm_fallbacks=r.comm_fallbacks, comm2=r2.comm, fallbacks2=r2.fallbacks,
+            comm_fallbacks2=r2.comm_fallbacks, plan_cus=s.plan_cus, ranks_per_device=s.ranks_per_device,
+            grid=(dict(J=g.J, I=g.I, T=g.T, kw=g.kw, workgroups=g.grid) if g is not None else None)))
+        if not a.columns:  # the replicated solution must be bitwise identical on every rank
+            xs = comm.all_gather_object(x)
+            meta[0]["x_bitwise_equal"] = all(np.array_equal(xs[0], xi) for xi in xs)
+
     if comm.rank == 0:
         np.save(a.out + ".npy", x)
         with open(a.out + ".json", "w") as f:
