@@ -372,7 +372,7 @@ def main() -> int:
         "fused_rows_per_tile": solver.geom.T if use_fused else None,
         "fused_schedule": solver.k.fused_get_schedule() if use_fused else None,
         "fused_grid": ({"J": solver.geom.J, "I": solver.geom.I, "workgroups": solver.geom.grid,
-                        "ld": solver.ld} if use_fused else None),
+                        "ld": solver.ld, "kw": solver.geom.kw, "xcd_local": solver.geom.xl} if use_fused else None),
         "selfcheck": selfcheck,
         "shared_gpus": bool(getattr(solver, "shared_device", False)) if not multi else None,
         "fused_plan_cus": solver.plan_cus if use_fused else None,

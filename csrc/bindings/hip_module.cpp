@@ -132,9 +132,10 @@ static void bind_engine(py::module_& m) {
         .def_readonly("T", &sart::FusedGeometry::T)
         .def_readonly("cpl", &sart::FusedGeometry::cpl)
         .def_readonly("kw", &sart::FusedGeometry::kw)
+        .def_readonly("xl", &sart::FusedGeometry::xl)
         .def("valid", &sart::FusedGeometry::valid);
     m.def("fused_geometry", &sart::fused_geometry, py::arg("ld"), py::arg("num_cus"), py::arg("variant") = 6,
-          py::arg("rows_per_tile") = 0, py::arg("narrow_slabs") = true);
+          py::arg("rows_per_tile") = 0, py::arg("narrow_slabs") = true, py::arg("chip_wide") = true);
     m.def("fused_geometry_bf16_wide", &sart::fused_geometry_bf16_wide, py::arg("ld"), py::arg("num_cus"));
     m.def("fused_fold_tiles", &sart::fused_fold_tiles, py::arg("geometry"), py::arg("nrows_pad"));
     m.def("fused_chain_plan", [](const sart::FusedGeometry& g, int64_t nrows_pad, bool split) {

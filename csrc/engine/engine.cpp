@@ -166,7 +166,7 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
     const double abytes = (double)Pp_ * (double)ld_ * (cfg_.rtm_bf16 ? 2.0 : 4.0);
     if (cfg_.use_fused && !cfg_.column_shard && abytes >= cfg_.fused_min_bytes && plan_cus_ >= 8 &&
         (!shared_device_ || fused_ok_shared) && (!cfg_.rtm_bf16 || cfg_.fused_variant == 6)) {
-        geom_ = fused_geometry(ld_, plan_cus_, cfg_.fused_variant, cfg_.rows_per_tile, !cfg_.rtm_bf16);
+        geom_ = fused_geometry(ld_, plan_cus_, cfg_.fused_variant, cfg_.rows_per_tile, !cfg_.rtm_bf16, !cfg_.rtm_bf16);
         if (cfg_.rtm_bf16 && (cfg_.rows_per_tile == 0 || cfg_.rows_per_tile == 4)) {
             // wide bf16 tiles (8 KB per wave per step, like fp32) where the width allows; SART_BF16_WIDE=0 keeps
             // the narrow tiles
@@ -390,7 +390,7 @@ void Engine::sweep() {
         else
             launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, static_cast<const float*>(A_), ld_, P_, Pp_,
                                x_.get(), ghat_.get(), arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I,
-                               geom_.J, st, xcnt_.get(), stream_, chain_tiles_, geom_.kw);
+                               geom_.J, st, xcnt_.get(), stream_, chain_tiles_, geom_.kw, geom_.xl);
         launch_reduce_partials(partial_.get(), ld_, (int)fused_blocks_, scale, comm_buf_.get(), Fpart_.get(), nF_fused_, Fslot,
                                st, stream_);
     } else {

@@ -10,11 +10,14 @@ namespace {
 
 // Variant 6 geometry for a padded width `ld` at T rows per tile and kw lane-vectors per lane: J = ld / slab
 // workgroups per row (slab = 1024 kw / T columns: the four compute waves cover T rows x 4 / T sub-slabs of
-// 256 kw columns), G = per_xcd / J row groups per XCD (the XCD's remaining per_xcd - G * J CUs stay idle).
-// cost = slab / G is the time per matrix row relative to the other candidates (each CU streams slab columns
-// of P / (8 G) rows).
+// 256 kw columns).
+//   XCD-local (xl): G = per_xcd / J row groups per XCD, I = 8 G (the XCD's remaining per_xcd - G J CUs idle).
+//   chip-wide (!xl, T = 1 only): I = num_cus / J row groups of any J <= num_cus, granules through memory.
+// cost = slab / I is the time per matrix row relative to the other candidates (each CU streams slab columns of
+// P / I rows), times the measured per-CU rate penalties.
 struct V6Candidate {
-    int T = 0, J = 0, G = 0, kw = 8;
+    int T = 0, J = 0, I = 0, kw = 8;
+    bool xl = true;
     double cost = 0.0;
 };
 
@@ -23,27 +26,70 @@ struct V6Candidate {
 // profiles/bench_r2_widths_kw.jsonl)
 constexpr double narrow_slab_penalty(int kw) { return kw == 8 ? 1.0 : (kw == 7 ? 1.02 : 1.15); }
 
-V6Candidate v6_candidate(int64_t ld, int T, int kw, int per_xcd) {
+// Chip-wide row groups hand granules off through memory instead of the XCD's L2 (handoff-1to1: cross-XCD
+// +0.1-0.3 us of ~3 us under streaming load). SART_FUSED_XL=0 / 1 forces one kind where both exist.
+constexpr double kChipWidePenalty = 1.05;
+
+int xl_mode() {
+    const char* e = std::getenv("SART_FUSED_XL");
+    return (e && *e) ? std::atoi(e) : -1;  // -1 auto, 0 chip-wide only, 1 XCD-local only
+}
+
+V6Candidate v6_candidate(int64_t ld, int T, int kw, int num_cus, bool xl) {
     V6Candidate c;
+    const int per_xcd = num_cus / 8;
     const int64_t slab = 1024 * (int64_t)kw / T;
     if (ld % slab != 0) return c;
     const int64_t J = ld / slab;
-    if (J < 1 || J > per_xcd || J * T > 256 /* exchange gather registers */) return c;
-    c.T = T, c.J = (int)J, c.G = per_xcd / (int)J, c.kw = kw;
+    if (J < 1 || J * T > 256 /* exchange gather registers */) return c;
+    if (xl) {
+        if (J > per_xcd) return c;
+        c.I = 8 * (per_xcd / (int)J);
+    } else {
+        if (T != 1 || J > num_cus) return c;
+        c.I = num_cus / (int)J;
+    }
+    c.T = T, c.J = (int)J, c.kw = kw, c.xl = xl;
     // T = 2 (schedule 4) measured 4-10 % slower per byte than T = 1 (schedule 5) at equal slab / G
     // (131072 / 106496 columns, profiles/probe_r2_t1_sched5.jsonl); T = 4 and T = 1 tie at 65536
-    c.cost = (double)slab / c.G * (T == 2 ? 1.08 : 1.0) * narrow_slab_penalty(kw);
+    c.cost = (double)slab / c.I * (T == 2 ? 1.08 : 1.0) * narrow_slab_penalty(kw) * (xl ? 1.0 : kChipWidePenalty);
     return c;
+}
+
+// The lower-cost row-group kind at (ld, T, kw) (I == 0: none), per SART_FUSED_XL and chip_wide.
+V6Candidate best_kind(int64_t ld, int T, int kw, int num_cus, bool chip_wide) {
+    V6Candidate best;
+    const int xm = xl_mode();
+    for (const bool xl : {true, false}) {
+        if ((xm == 0 && xl) || (xm == 1 && !xl) || (!xl && !chip_wide)) continue;
+        const V6Candidate c = v6_candidate(ld, T, kw, num_cus, xl);
+        if (c.I > 0 && (best.I == 0 || c.cost < best.cost)) best = c;
+    }
+    return best;
+}
+
+// The lowest-cost candidate over (kw, T, kind) for width ld (I == 0: none). rows_per_tile > 0 fixes T.
+V6Candidate best_v6(int64_t ld, int num_cus, int rows_per_tile, bool narrow_slabs, bool chip_wide) {
+    V6Candidate best;
+    for (const int kw : {8, 7, 6}) {
+        if (kw != 8 && !narrow_slabs) continue;
+        for (const int T : {4, 2, 1}) {
+            if (rows_per_tile > 0 && T != rows_per_tile) continue;
+            const V6Candidate c = best_kind(ld, T, kw, num_cus, chip_wide);
+            if (c.I > 0 && (best.I == 0 || c.cost < best.cost)) best = c;
+        }
+    }
+    return best;
 }
 
 }  // namespace
 
 int64_t choose_ld(int64_t nvoxel, double max_waste, bool narrow_slabs) {
-    // Widths the fused sweep (variant 6) can split into whole slabs, J <= 32 per row group: at each (T, kw) the
-    // smallest multiple of the slab covering nvoxel. Take the one with the lowest time per row (ties: less
-    // padding, then the larger T and kw, measured fastest at equal cost), if it pads by at most max_waste.
+    // Widths the fused sweep (variant 6) can split into whole slabs: at each (T, kw) the smallest multiple of the
+    // slab covering nvoxel. Take the one with the lowest time per row (ties: less padding, then the larger T and
+    // kw, measured fastest at equal cost), if it pads by at most max_waste.
     if (nvoxel >= 1024) {
-        constexpr int kPerXcd = 32;  // MI355X: 256 CUs in 8 XCDs
+        constexpr int kCus = 256;  // MI355X: 256 CUs in 8 XCDs
         int64_t best_ld = 0;
         double best_cost = 0.0;
         for (const int kw : {8, 7, 6}) {
@@ -51,8 +97,9 @@ int64_t choose_ld(int64_t nvoxel, double max_waste, bool narrow_slabs) {
             for (const int T : {4, 2, 1}) {
                 const int64_t slab = 1024 * (int64_t)kw / T;
                 const int64_t ld = (nvoxel + slab - 1) / slab * slab;
-                const V6Candidate c = v6_candidate(ld, T, kw, kPerXcd);
-                if (c.G == 0 || (double)(ld - nvoxel) > max_waste * (double)nvoxel) continue;
+                if ((double)(ld - nvoxel) > max_waste * (double)nvoxel) continue;
+                const V6Candidate c = best_kind(ld, T, kw, kCus, narrow_slabs);  // bf16 (!narrow): XCD-local only
+                if (c.I == 0) continue;
                 if (best_ld == 0 || c.cost < best_cost || (c.cost == best_cost && ld < best_ld)) {
                     best_ld = ld;
                     best_cost = c.cost;
@@ -60,7 +107,7 @@ int64_t choose_ld(int64_t nvoxel, double max_waste, bool narrow_slabs) {
             }
         }
         if (best_ld) return best_ld;
-        // wider than 32 slabs of 8192: a multiple of 8192 keeps the variant 3 fallback (K = 8) available
+        // wider than 256 slabs of 8192: a multiple of 8192 keeps the variant 3 fallback (K = 8) available
         const int64_t ld = (nvoxel + 8191) / 8192 * 8192;
         if ((double)(ld - nvoxel) <= max_waste * (double)nvoxel) return ld;
     }
@@ -68,7 +115,8 @@ int64_t choose_ld(int64_t nvoxel, double max_waste, bool narrow_slabs) {
     return (n + 63) / 64 * 64;
 }
 
-FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_tile, bool narrow_slabs) {
+FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_tile, bool narrow_slabs,
+                             bool chip_wide) {
     FusedGeometry g;
     if (rows_per_tile <= 0) {
         const char* e = std::getenv("SART_FUSED_T");
@@ -76,22 +124,15 @@ FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_
     }
     if (const char* e = std::getenv("SART_FUSED_KW"); e && *e && std::atoi(e) == 8) narrow_slabs = false;
     if (variant == 6 && num_cus % 8 == 0) {
-        // Rows per tile and slab: the requested T, else the candidate with the lowest time per row (ties: the
-        // larger T and kw; T = 4 at ld = 64k, 2 at 128k, 1 at 256k measured 6.5-6.9 TB/s, against 4.0-4.7 TB/s
-        // for variant 3, profiles/probe_r1_fused_T.jsonl). Widths whose J does not divide the XCD's CU count
-        // run G = per_xcd / J row groups per XCD and leave the remaining CUs idle.
-        V6Candidate best;
-        for (const int kw : {8, 7, 6}) {
-            if (kw != 8 && !narrow_slabs) continue;
-            for (const int T : {4, 2, 1}) {
-                if (rows_per_tile > 0 && T != rows_per_tile) continue;
-                const V6Candidate c = v6_candidate(ld, T, kw, num_cus / 8);
-                if (c.G > 0 && (best.G == 0 || c.cost < best.cost)) best = c;
-            }
-        }
-        if (best.G > 0) {
-            g.K = best.T, g.J = best.J, g.I = 8 * best.G, g.grid = g.I * g.J, g.variant = 6, g.T = best.T;
+        // Rows per tile, slab and row-group kind: the requested T, else the candidate with the lowest time per row
+        // (ties: the larger T and kw, XCD-local; T = 4 at ld = 64k, 2 at 128k, 1 at 256k measured 6.5-6.9 TB/s,
+        // against 4.0-4.7 TB/s for variant 3, profiles/probe_r1_fused_T.jsonl). Rows wider than 32 slabs, and
+        // widths whose J leaves CUs of every XCD idle, use chip-wide row groups of I = num_cus / J.
+        const V6Candidate best = best_v6(ld, num_cus, rows_per_tile, narrow_slabs, chip_wide);
+        if (best.I > 0) {
+            g.K = best.T, g.J = best.J, g.I = best.I, g.grid = g.I * g.J, g.variant = 6, g.T = best.T;
             g.kw = best.kw;
+            g.xl = best.xl;
             return g;
         }
     }

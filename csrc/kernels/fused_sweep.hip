@@ -1003,7 +1003,26 @@ template <int T>
 static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
                         int64_t nrows_pad, const float* x_, const float* ghat, const float* arow, float* partial,
                         double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt,
-                        int64_t chain_tiles, int kw) {
+                        int64_t chain_tiles, int kw, bool xl) {
+    if (!xl) {
+        // chip-wide row groups (T = 1, schedule 5): workgroup b is (b % I, b / I), granules written through to
+        // memory (agent scope), so a group may span XCDs: J up to the CU count, I = CUs / J of any value
+        if constexpr (T == 1) {
+            auto go_cw = [&](auto lg, auto k) {
+                launch_rows_t<decltype(lg)::value, false, false, 1, 5, float, 4, decltype(k)::value>(
+                    grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
+                    chain_tiles);
+            };
+            auto by_kw = [&](auto lg) {
+                if (kw == 8) go_cw(lg, std::integral_constant<int, 8>{});
+                else if (kw == 7) go_cw(lg, std::integral_constant<int, 7>{});
+                else go_cw(lg, std::integral_constant<int, 6>{});
+            };
+            if (logmode) by_kw(std::true_type{}); else by_kw(std::false_type{});
+            return;
+        }
+        throw std::runtime_error("fused_sweep v6: chip-wide row groups need T = 1");
+    }
     const bool diag = (g_fused_dbg & 2) != 0;  // instrumented build only when asked (timing diagnostics)
     // g_fused_sched: pipeline schedule (k_fused_sweep_rows SCHED); schedules 1-4 hold the x slab in LDS,
     // which has room for it only when T >= 2. T = 1 runs schedule 5 (the split exchange with the x slab in
@@ -1079,7 +1098,7 @@ int fused_tile_rows(int K, int variant) {
 void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows,
                         int64_t nrows_pad, const float* x, const float* ghat, const float* arow, float* partial,
                         double* Fpart, uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt,
-                        hipStream_t stream, int64_t chain_tiles, int kw) {
+                        hipStream_t stream, int64_t chain_tiles, int kw, bool xl) {
     if (variant != 3 && variant != 6) throw std::runtime_error("fused_sweep: variant must be 6 or 3");
     const dim3 grid((unsigned)(I * J));
     if (variant == 6) {
@@ -1092,13 +1111,16 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
         if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep v6: ld must equal J * slab");
         if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v6: padded rows must be a multiple of 4");
         if (J * T > kRowsGather) throw std::runtime_error("fused_sweep v6: J * T > 256");
-        if (xcnt == nullptr || I % 8 != 0) throw std::runtime_error("fused_sweep v6: needs the per-XCD ticket counters and I % 8 == 0");
+        if (xl && (xcnt == nullptr || I % 8 != 0))
+            throw std::runtime_error("fused_sweep v6: XCD-local groups need the per-XCD ticket counters and I % 8 == 0");
+        if (!xl && T != 1) throw std::runtime_error("fused_sweep v6: chip-wide row groups need T = 1");
+        if (I < 1) throw std::runtime_error("fused_sweep v6: no row groups");
         if (T == 1) launch_rows<1>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
-                        chain_tiles, kw);
+                        chain_tiles, kw, xl);
         else if (T == 2) launch_rows<2>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
-                        chain_tiles, kw);
+                        chain_tiles, kw, xl);
         else launch_rows<4>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
-                        chain_tiles, kw);
+                        chain_tiles, kw, xl);
         check_launch("k_fused_sweep_rows");
         return;
     }

@@ -79,7 +79,7 @@ std::vector<unsigned long long> fused_debug_stats(int nblocks);
 void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                         const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                         uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream,
-                        int64_t chain_tiles = 0, int kw = 8);
+                        int64_t chain_tiles = 0, int kw = 8, bool xl = true);
 // kw (variant 6): lane-vectors per lane per row, slab = 1024 kw / T columns (8, or 7 / 6 at the default
 // schedules: widths whose 8-KiB-slab count leaves CUs idle; FusedGeometry::kw).
 // chain_tiles (variant 6; 0 = off): T = 1: every ~chain_tiles tiles a compute wave folds its fp32 back-projection

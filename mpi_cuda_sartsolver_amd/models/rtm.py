@@ -29,6 +29,7 @@ class FusedGeometry:
     variant: int  # register-ring configuration (csrc/kernels/fused_sweep.hip)
     T: int        # rows per tile
     kw: int = 8   # variant 6 fp32: lane-vectors per lane per row (slab 1024 kw / T columns)
+    xl: bool = True  # variant 6: XCD-local row groups (else chip-wide groups of I = CUs // J, granules via memory)
 
 
 def choose_ld(nvoxel: int, max_waste: float = 0.10, storage: str = "fp32") -> int:
@@ -40,19 +41,22 @@ def choose_ld(nvoxel: int, max_waste: float = 0.10, storage: str = "fp32") -> in
 
 
 def fused_geometry(ld: int, num_cus: int, variant: int = 6, rows_per_tile: Optional[int] = None,
-                   narrow_slabs: bool = True) -> Optional[FusedGeometry]:
+                   narrow_slabs: bool = True, chip_wide: bool = True) -> Optional[FusedGeometry]:
     """Persistent-grid geometry of the fused sweep (native ``sart::fused_geometry``).
 
     variant 6 (default): XCD-local row groups (L2 hand-offs); the four compute waves of a workgroup
     cover T rows x (4 / T) sub-slabs of 2048 columns, so a row is split over J = ld * T / 8192
     workgroups and each XCD runs G = (CUs per XCD) // J row groups (T = rows_per_tile or env
-    SART_FUSED_T, else the T with the lowest time per row). Variant 3: slabs of 1024*K columns, K chosen
-    for <= 32 slabs (the fallback). None: no fused path.
+    SART_FUSED_T, else the T with the lowest time per row). Rows wider than an XCD's 32 slabs, and widths whose
+    J leaves CUs of every XCD idle, use chip-wide row groups instead (T = 1, I = CUs // J, ``xl=False``;
+    chip_wide=False excludes them). Variant 3: slabs of 1024*K columns, K chosen for <= 32 slabs (the
+    fallback). None: no fused path.
     """
-    g = hip().fused_geometry(int(ld), int(num_cus), int(variant), int(rows_per_tile or 0), bool(narrow_slabs))
+    g = hip().fused_geometry(int(ld), int(num_cus), int(variant), int(rows_per_tile or 0), bool(narrow_slabs),
+                             bool(chip_wide))
     if not g.valid():
         return None
-    return FusedGeometry(K=g.K, J=g.J, I=g.I, grid=g.grid, variant=g.variant, T=g.T, kw=g.kw)
+    return FusedGeometry(K=g.K, J=g.J, I=g.I, grid=g.grid, variant=g.variant, T=g.T, kw=g.kw, xl=g.xl)
 
 
 class DenseRTM:

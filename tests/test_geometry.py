@@ -16,49 +16,69 @@ def _check_v6(ld, g):
     assert g is not None and g.variant == 6 and g.kw in (6, 7, 8)
     slab = 1024 * g.kw // g.T
     assert g.T in (1, 2, 4) and ld % slab == 0 and ld // slab == g.J
-    assert g.J <= CUS // 8 and g.J * g.T <= 256
-    assert g.I % 8 == 0 and g.grid == g.I * g.J <= CUS
-    assert g.I // 8 == (CUS // 8) // g.J  # as many row groups per XCD as fit
+    assert g.J * g.T <= 256 and g.grid == g.I * g.J <= CUS
+    if g.xl:  # XCD-local row groups: as many per XCD as fit
+        assert g.J <= CUS // 8 and g.I % 8 == 0 and g.I // 8 == (CUS // 8) // g.J
+    else:  # chip-wide row groups (T = 1): as many as fit the chip
+        assert g.T == 1 and g.J <= CUS and g.I == CUS // g.J
 
 
 @pytest.mark.parametrize("nvox", [20480, 30000, 60000, 61440, 65536, 70000, 100000, 131072, 150000, 200000,
-                                  229376, 262144])
+                                  229376, 262144, 300000, 524288, 1000000, 1048576])
 def test_every_width_gets_variant6(nvox):
     ld = rtm.choose_ld(nvox)
     assert nvox <= ld <= 1.10 * nvox
     _check_v6(ld, rtm.fused_geometry(ld, CUS, 6))
+    if nvox > 262144:
+        return  # bf16 tiles: XCD-local row groups only (at most 32 slabs of 8192)
     # bf16 shards keep the 8-KiB slabs (their tiles are 8 or 16 bytes of bf16 per lane)
     ldb = rtm.choose_ld(nvox, storage="bf16")
-    gb = rtm.fused_geometry(ldb, CUS, 6, narrow_slabs=False)
-    assert nvox <= ldb <= 1.10 * nvox and gb.kw == 8
+    gb = rtm.fused_geometry(ldb, CUS, 6, narrow_slabs=False, chip_wide=False)
+    assert nvox <= ldb <= 1.10 * nvox and gb.kw == 8 and gb.xl
     _check_v6(ldb, gb)
 
 
 def test_width_sweep_variant6_and_waste():
+    """Every width from 20k to 1M voxels gets variant 6 with at most 10 % padding; chip-wide row groups keep at
+    least 85 % of the CUs busy where XCD-local groups left whole CUs of every XCD idle (round 2: min 0.69)."""
     used = []
-    for nvox in range(20480, 262145, 997):
+    for nvox in list(range(20480, 262145, 997)) + list(range(262144, 1048577, 8191)):
         ld = rtm.choose_ld(nvox)
         assert ld % 64 == 0 and nvox <= ld <= 1.10 * nvox, nvox
         g = rtm.fused_geometry(ld, CUS, 6)
         _check_v6(ld, g)
         used.append(g.grid / CUS)
-    assert min(used) >= 0.65 and sum(used) / len(used) >= 0.9  # CUs in use across the sweep of widths (measured 0.69, 0.92)
+    assert min(used) >= 0.85 and sum(used) / len(used) >= 0.95, (min(used), sum(used) / len(used))
 
 
-@pytest.mark.parametrize("ld,T,kw,J,I", [(65536, 4, 8, 32, 8), (131072, 1, 8, 16, 16), (262144, 1, 8, 32, 8),
-                                         (61440, 4, 8, 30, 8), (16384, 4, 8, 8, 32), (106496, 1, 8, 13, 16),
-                                         (100352, 1, 7, 14, 16), (200704, 1, 7, 28, 8), (71680, 1, 7, 10, 24),
-                                         (153600, 1, 6, 25, 8), (229376, 1, 7, 32, 8)])
-def test_production_geometries(ld, T, kw, J, I):
+@pytest.mark.parametrize("ld,T,kw,J,I,xl", [(65536, 4, 8, 32, 8, True), (131072, 1, 8, 16, 16, True),
+                                            (262144, 1, 8, 32, 8, True), (61440, 4, 8, 30, 8, True),
+                                            (16384, 4, 8, 8, 32, True), (106496, 1, 8, 13, 19, False),
+                                            (100352, 1, 7, 14, 18, False), (200704, 1, 7, 28, 9, False),
+                                            (71680, 1, 7, 10, 24, True), (150528, 1, 7, 21, 12, False),
+                                            (229376, 1, 7, 32, 8, True), (524288, 1, 8, 64, 4, False),
+                                            (1048576, 1, 8, 128, 2, False), (301056, 1, 7, 42, 6, False)])
+def test_production_geometries(ld, T, kw, J, I, xl):
     g = rtm.fused_geometry(ld, CUS, 6)
-    assert (g.T, g.kw, g.J, g.I) == (T, kw, J, I)
+    assert (g.T, g.kw, g.J, g.I, g.xl) == (T, kw, J, I, xl)
+
+
+def test_xl_override(monkeypatch):
+    """SART_FUSED_XL=1 keeps XCD-local groups only (wider rows then fall back to variant 3), 0 chip-wide only."""
+    monkeypatch.setenv("SART_FUSED_XL", "1")
+    g = rtm.fused_geometry(200704, CUS, 6)
+    assert g.xl and (g.J, g.I) == (28, 8)
+    assert rtm.fused_geometry(524288, CUS, 6).variant == 3
+    monkeypatch.setenv("SART_FUSED_XL", "0")
+    g = rtm.fused_geometry(65536, CUS, 6)
+    assert not g.xl and (g.T, g.J, g.I) == (1, 8, 32)
 
 
 def test_lowest_cost_rows_per_tile():
     # 70000 columns with 8-KiB slabs: T = 2 needs J = 18 (one group per XCD, 18 of 32 CUs); T = 1 gives J = 9
     # and three groups per XCD (27 CUs), a lower time per row. 7-KiB slabs: J = 10, three groups (30 CUs).
     ld = rtm.choose_ld(70000, storage="bf16")
-    g = rtm.fused_geometry(ld, CUS, 6, narrow_slabs=False)
+    g = rtm.fused_geometry(ld, CUS, 6, narrow_slabs=False, chip_wide=False)
     assert (ld, g.T, g.J, g.I) == (73728, 1, 9, 24)
     ld = rtm.choose_ld(70000)
     g = rtm.fused_geometry(ld, CUS, 6)
@@ -76,8 +96,10 @@ def test_t2_penalty_prefers_t1():
 def test_forced_rows_per_tile_and_fallback():
     g = rtm.fused_geometry(65536, CUS, 6, 1)
     assert (g.T, g.J, g.I) == (1, 8, 32)
-    # wider than 32 slabs of 8192: variant 3 (K = 8)
-    g3 = rtm.fused_geometry(1 << 20, CUS, 6)
+    # wider than 32 slabs of 8192: chip-wide variant 6; without chip-wide groups variant 3 (K = 8)
+    g6 = rtm.fused_geometry(1 << 20, CUS, 6)
+    assert g6.variant == 6 and not g6.xl and (g6.J, g6.I) == (128, 2)
+    g3 = rtm.fused_geometry(1 << 20, CUS, 6, chip_wide=False)
     assert g3.variant == 3 and g3.K == 8 and g3.J == 128
     assert rtm.fused_geometry(65536, CUS, 3).variant == 3
     # not a multiple of 1024: no fused path
