@@ -142,6 +142,7 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
     x064_.resize(std::max<int64_t>(V_, 1));
     st_.resize(1);
     xcnt_.resize(16);
+    ticket_.resize(1);
     xprev_.resize(ld_);
     use_fused_ = false;
     // The fused sweep is a persistent grid whose workgroups must all be co-resident. Ranks sharing one GPU
@@ -410,12 +411,8 @@ void Engine::sweep() {
         comm_->all_reduce(comm_buf_.get(), (size_t)ld_ + 2, ReduceOp::kSum, stream_);
         comm_end();
     }
-    launch_decide(st, Fslot, stream_);
-    if (cfg_.logarithmic)
-        launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_, xcnt,
-                          xprev_.get());
-    else
-        launch_update_linear(x_.get(), comm_buf_.get(), pen, V_, st, stream_, xcnt, xprev_.get());
+    launch_decide_update(cfg_.logarithmic, st, Fslot, x_.get(), comm_buf_.get(), O_.get(), pen, (float)cfg_.relaxation,
+                         V_, xcnt, xprev_.get(), ticket_.get(), stream_);
     if (cfg_.fault_nan_sweep >= 0 && host_sweep_ == cfg_.fault_nan_sweep)  // fault injection (tests)
         hip_ok(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(x_.get()), 0x7fc00000, 1, stream_), "inject NaN");
     ++host_sweep_;
@@ -453,12 +450,8 @@ void Engine::sweep_columns() {
                        xfull, pen_.get(), st, stream_);
         pen = pen_.get();
     }
-    launch_decide(st, Fslot, stream_);
-    if (cfg_.logarithmic)
-        launch_update_log(x_.get(), O_.get(), comm_buf_.get(), pen, (float)cfg_.relaxation, V_, st, stream_, nullptr,
-                          xprev_.get());
-    else
-        launch_update_linear(x_.get(), comm_buf_.get(), pen, V_, st, stream_, nullptr, xprev_.get());
+    launch_decide_update(cfg_.logarithmic, st, Fslot, x_.get(), comm_buf_.get(), O_.get(), pen, (float)cfg_.relaxation,
+                         V_, nullptr, xprev_.get(), ticket_.get(), stream_);
 }
 
 bool Engine::timing_collectives() const { return cfg_.time_collectives && !cfg_.use_graph && comm_->size() > 1; }

@@ -198,6 +198,7 @@ class Engine {
     DeviceArray<SartState> st_;
     DeviceArray<uint64_t> gran_;
     DeviceArray<unsigned> xcnt_;
+    DeviceArray<unsigned> ticket_;  // k_decide_update's arrival ticket (0 between sweeps)
     DeviceArray<float> xg_;  // column shard + Laplacian: all-gathered x (nvoxel_total, padded)
     DeviceArray<int64_t> lap_rp_;
     DeviceArray<int32_t> lap_col_;

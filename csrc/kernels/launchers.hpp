@@ -41,6 +41,11 @@ void launch_init_solution(float* x, int64_t n, int64_t n_pad, const float* src_f
 void launch_penalty(bool logx, const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta,
                     const float* x, float* pen, const SartState* st, hipStream_t stream);
 void launch_decide(SartState* st, const float* Fslot, hipStream_t stream);
+// launch_decide + launch_update_{linear,log} in one kernel (d = the reduced corrections, or Fv for log with O the
+// observed back-projection); ticket: one device word, 0 between launches (re-armed by the kernel itself).
+void launch_decide_update(bool logmode, SartState* st, const float* Fslot, float* x, const float* d, const float* O,
+                          const float* pen, float alpha, int64_t n, unsigned* xcnt, float* xprev, unsigned* ticket,
+                          hipStream_t stream);
 // xcnt (optional): fused-sweep ticket counters to zero for the next sweep; xprev (optional): receives x
 // before the update (rollback point of the NaN/Inf guard)
 void launch_update_linear(float* x, const float* d, const float* pen, int64_t n, const SartState* st,

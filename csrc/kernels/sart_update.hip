@@ -84,51 +84,102 @@ __global__ __launch_bounds__(256) void k_penalty_csr(const int64_t* __restrict__
 // ||A x||^2 (k_reduce_partials writes the local SartState::error there): when ANY rank's persistent sweep
 // gave up, every rank stops the frame at this sweep and sees error bit 8, so the fallback decision is
 // identical on all ranks (a rank-local decision would leave its peers waiting in the next collective).
-__global__ void k_decide(SartState* __restrict__ st, const float* __restrict__ Fslot) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    if (st->done) return;
-    const int s = st->sweep;
+// The decision on a copy of the state (shared by k_decide and k_decide_update): a pure function of the state
+// before the sweep and of the sweep's reduced Fslot, so every workgroup that evaluates it gets the same answer.
+__device__ void decide_next(SartState& st, const float* __restrict__ Fslot) {
+    if (st.done) return;
+    const int s = st.sweep;
     const double F = (double)Fslot[0];
-    st->F_last = F;
+    st.F_last = F;
     int done = 0;
     int status = kRunning;
     if (Fslot[1] != 0.f) {
-        st->error |= 8;
-        st->sweep = s + 1;
-        st->status = kMaxIterationsExceeded;
-        st->done = 1;
-        st->epoch = st->epoch + 1;
+        st.error |= 8;
+        st.sweep = s + 1;
+        st.status = kMaxIterationsExceeded;
+        st.done = 1;
+        st.epoch = st.epoch + 1;
         return;
     }
     if (!isfinite(F)) {
         // NaN/Inf guard: x_s produced a non-finite ||A x||^2. Stop; the engine returns the
         // last finite iterate x_{s-1}, which the update kernels saved in xprev, so s - 1 updates count.
-        st->flags |= 1;
-        st->iterations = s > 0 ? s - 1 : 0;
-        st->sweep = s + 1;
-        st->status = kMaxIterationsExceeded;
-        st->done = 1;
-        st->epoch = st->epoch + 1;
+        st.flags |= 1;
+        st.iterations = s > 0 ? s - 1 : 0;
+        st.sweep = s + 1;
+        st.status = kMaxIterationsExceeded;
+        st.done = 1;
+        st.epoch = st.epoch + 1;
         return;
     }
     if (s >= 1) {
-        const double conv = (st->G - F) / st->G;
-        if (s >= 2 && fabs(conv - st->conv_prev) < st->tol) {
+        const double conv = (st.G - F) / st.G;
+        if (s >= 2 && fabs(conv - st.conv_prev) < st.tol) {
             done = 1;
             status = kSuccess;
         }
-        st->conv_prev = conv;
-        st->conv_last = conv;
+        st.conv_prev = conv;
+        st.conv_last = conv;
     }
-    if (!done && s >= st->max_iter) {
+    if (!done && s >= st.max_iter) {
         done = 1;
         status = kMaxIterationsExceeded;
     }
-    st->iterations = done ? s : s + 1;
-    st->sweep = s + 1;
-    st->status = status;
-    st->done = done;
-    st->epoch = st->epoch + 1;
+    st.iterations = done ? s : s + 1;
+    st.sweep = s + 1;
+    st.status = status;
+    st.done = done;
+    st.epoch = st.epoch + 1;
+}
+
+__global__ void k_decide(SartState* __restrict__ st, const float* __restrict__ Fslot) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    SartState s = *st;
+    decide_next(s, Fslot);
+    *st = s;
+}
+
+// k_decide and k_update_linear / k_update_log in ONE launch (one kernel boundary less per SART iteration): every
+// workgroup evaluates the decision itself from the state before it, applies the update to its voxels when the
+// frame continues, then takes a ticket; the last workgroup to arrive writes the new state (every other one has
+// read the old state before its ticket) and re-arms the ticket for the next sweep.
+template <bool LOGV>
+__global__ __launch_bounds__(256) void k_decide_update(SartState* __restrict__ st, const float* __restrict__ Fslot,
+                                                       float* __restrict__ x, const float* __restrict__ d,
+                                                       const float* __restrict__ O, const float* __restrict__ pen,
+                                                       float alpha, int64_t n, unsigned* __restrict__ xcnt,
+                                                       float* __restrict__ xprev, unsigned* __restrict__ ticket) {
+    __shared__ SartState s_next;
+    __shared__ int s_apply;
+    if (threadIdx.x == 0) {
+        SartState s = *st;
+        decide_next(s, Fslot);
+        s_next = s;
+        s_apply = !s.done;
+    }
+    if (xcnt && blockIdx.x == 0 && threadIdx.x < 16) xcnt[threadIdx.x] = 0u;  // see k_update_linear
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s_apply && i < n) {
+        const float x0 = x[i];
+        if (xprev) xprev[i] = x0;
+        if constexpr (LOGV) {
+            float r = powf((O[i] + kEpsLog) / (d[i] + kEpsLog), alpha);
+            if (pen) r *= expf(-pen[i]);
+            x[i] = x0 * r;
+        } else {
+            float v = x0 + d[i];
+            if (pen) v -= pen[i];
+            x[i] = (v > 0.f) ? v : 0.f;
+        }
+    }
+    if (threadIdx.x == 0) {
+        const unsigned t = atomicAdd(ticket, 1u);  // after this workgroup's read of *st (its value is consumed above)
+        if (t == gridDim.x - 1) {
+            *st = s_next;
+            *ticket = 0u;
+        }
+    }
 }
 
 // x = max(x + d - pen, 0)
@@ -295,6 +346,19 @@ void launch_penalty(bool logx, const int64_t* row_ptr, const int32_t* col, const
 void launch_decide(SartState* st, const float* Fslot, hipStream_t stream) {
     hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, stream, st, Fslot);
     check_launch("k_decide");
+}
+
+void launch_decide_update(bool logmode, SartState* st, const float* Fslot, float* x, const float* d, const float* O,
+                          const float* pen, float alpha, int64_t n, unsigned* xcnt, float* xprev, unsigned* ticket,
+                          hipStream_t stream) {
+    const unsigned blocks = nb(n > 0 ? n : 1);
+    if (logmode)
+        hipLaunchKernelGGL(k_decide_update<true>, dim3(blocks), dim3(256), 0, stream, st, Fslot, x, d, O, pen, alpha, n,
+                           xcnt, xprev, ticket);
+    else
+        hipLaunchKernelGGL(k_decide_update<false>, dim3(blocks), dim3(256), 0, stream, st, Fslot, x, d, O, pen, alpha,
+                           n, xcnt, xprev, ticket);
+    check_launch("k_decide_update");
 }
 
 void launch_update_linear(float* x, const float* d, const float* pen, int64_t n, const SartState* st,

@@ -84,6 +84,12 @@ for step in "$@"; do
           --out "$OUT/mfov_report_r$r.json" || true
       done ;;
     benchshare) run bench_share2 600 python bench.py --gpus 2 --share-gpus --steps 3 --warmup 1 ;;
+    widths3) for v in 150000 200000 100000 300000 524288; do
+               run bench_w3_$v 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck &&
+               SART_FUSED_XL=1 run bench_w3xl_$v 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
+             done &&
+             run bench_w3_1m 300 python bench.py --steps 3 --warmup 1 --nvox 1048576 --npix 16384 --no-selfcheck &&
+             SART_FUSED_XL=1 run bench_w3xl_1m 300 python bench.py --steps 3 --warmup 1 --nvox 1048576 --npix 16384 --no-selfcheck ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
