@@ -96,8 +96,15 @@ struct MpiApi {
     void load() {
         std::string tried;
         const char* env = std::getenv("SART_MPI_LIB");
-        for (const char* cand : {env, "libmpi.so.12", "libmpi.so.40", "/opt/conda/lib/libmpi.so.12",
-                                 "/opt/conda/lib/libmpi.so.40", "libmpi.so"}) {
+        // the launcher names the ABI to try first: Open MPI's mpirun exports OMPI_*, the MPICH family PMI_*
+        // (a singleton MPI_Init of the other library would make every process rank 0 of 1)
+        const char* ompi = std::getenv("OMPI_COMM_WORLD_SIZE");
+        const bool open_mpi_first = ompi && *ompi;
+        const char* first = open_mpi_first ? "libmpi.so.40" : "libmpi.so.12";
+        const char* second = open_mpi_first ? "libmpi.so.12" : "libmpi.so.40";
+        const char* first_c = open_mpi_first ? "/opt/conda/lib/libmpi.so.40" : "/opt/conda/lib/libmpi.so.12";
+        const char* second_c = open_mpi_first ? "/opt/conda/lib/libmpi.so.12" : "/opt/conda/lib/libmpi.so.40";
+        for (const char* cand : {env, first, first_c, second, second_c, "libmpi.so"}) {
             if (!cand || !*cand) continue;
             lib = dlopen(cand, RTLD_NOW | RTLD_GLOBAL);
             if (lib) break;
@@ -160,6 +167,14 @@ class MpiHostComm final : public HostComm {
         }
         mpi_ok(api_.comm_rank(&rank_), "MPI_Comm_rank");
         mpi_ok(api_.comm_size(&size_), "MPI_Comm_size");
+        // the world must be the launcher's: a library of the other MPI family initialises as a singleton
+        for (const char* var : {"OMPI_COMM_WORLD_SIZE", "PMI_SIZE"}) {
+            const char* v = std::getenv(var);
+            if (v && *v && std::atoi(v) != size_)
+                throw std::runtime_error(std::string("mpi host comm: MPI_Comm_size is ") + std::to_string(size_) +
+                                         " but the launcher set " + var + "=" + v + " (" + api_.version.substr(0, 60) +
+                                         "): point SART_MPI_LIB at the launcher's libmpi");
+        }
     }
     ~MpiHostComm() override {
         int fin = 0;

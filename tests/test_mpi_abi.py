@@ -57,3 +57,22 @@ def test_launcher_detection():
         env = dict(base, PYTHONPATH=ROOT, **extra)
         r = subprocess.run([sys.executable, "-c", probe], env=env, capture_output=True, text=True, timeout=60)
         assert r.stdout.strip() == expect, (extra, r.stdout, r.stderr)
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_mpi_world_must_match_launcher(tmp_path):
+    """A libmpi of the other family initialises as a singleton (every process rank 0 of 1) instead of joining the
+    launcher's world: the world size is checked against OMPI_COMM_WORLD_SIZE / PMI_SIZE and a mismatch is an error
+    naming SART_MPI_LIB (the fake library reports a world of 2)."""
+    lib = tmp_path / "libfake_openmpi.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-O1", "-DOMPI_ABI", "-o", str(lib), SRC], check=True)
+    base = {k: v for k, v in os.environ.items() if k not in ("RANK", "PMI_SIZE", "OMPI_COMM_WORLD_SIZE")}
+    probe = "from mpi_cuda_sartsolver_amd.ops import native; c = native().mpi_host_comm(); print(c.size)"
+    for extra, ok in (({"OMPI_COMM_WORLD_SIZE": "2"}, True), ({"OMPI_COMM_WORLD_SIZE": "4"}, False),
+                      ({"PMI_SIZE": "3"}, False)):
+        env = dict(base, PYTHONPATH=ROOT, SART_MPI_LIB=str(lib), **extra)
+        r = subprocess.run([sys.executable, "-c", probe], env=env, capture_output=True, text=True, timeout=120)
+        if ok:
+            assert r.returncode == 0 and r.stdout.strip() == "2", r.stderr[-2000:]
+        else:
+            assert r.returncode != 0 and "SART_MPI_LIB" in r.stderr, (extra, r.stderr[-2000:])
