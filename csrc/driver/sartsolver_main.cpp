@@ -393,12 +393,13 @@ int main(int argc, char** argv) {
                     const double secs = info.ms > 0 ? 1e-3 * info.ms : 1e-3 * ms;
                     const double pv = (double)in.npixel * (double)in.nvoxel;
                     const double reads = gpu && info.used_fused ? 1.0 : 2.0;
+                    const double elem = gpu && cfg.rtm_bf16 ? 2.0 : 4.0;  // bytes per stored RTM element
                     profile << "{\"frame\": " << cur << ", \"time\": " << image.frame_time(cur)
                             << ", \"status\": " << info.status << ", \"iterations\": " << info.iterations
                             << ", \"convergence\": " << info.convergence << ", \"sweeps\": " << sweeps
                             << ", \"iters_per_s\": " << sweeps / secs << ", \"gflops\": " << 4.0 * pv * sweeps / secs / 1e9
-                            << ", \"rtm_GBps\": " << reads * 4.0 * pv * sweeps / secs / 1e9
-                            << ", \"comm_ms\": " << info.comm_ms
+                            << ", \"rtm_GBps\": " << reads * elem * pv * sweeps / secs / 1e9
+                            << ", \"comm_ms\": " << info.comm_ms << ", \"comm_fallbacks\": " << info.comm_fallbacks
                             << ", \"ms\": " << ms << ", \"solve_ms\": " << info.ms
                             << ", \"fused\": " << (info.used_fused ? "true" : "false")
                             << ", \"ranks\": " << size << ", \"comm\": \"" << json_escape(host->backend())

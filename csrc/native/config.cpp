@@ -77,9 +77,11 @@ std::string usage() {
            "  --parallel_read             Read RTM data in a parallel way (high-IOPS storage optimization).\n"
            "Extensions:\n"
            "  --resume                    Append to an existing output file and skip frames already solved.\n"
-           "  --batch_frames N            Solve N frames together on the matrix cores; each batch warm-starts\n"
-           "                              from the previous batch's last solution (cold with --no_guess).\n"
-           "                              [default: 1]\n"
+           "  --batch_frames N            Solve N frames together on the matrix cores (continuous batching: a\n"
+           "                              finished frame's slot takes the next frame, warm-started from the\n"
+           "                              latest frame finished before it; cold with --no_guess). This is NOT\n"
+           "                              the reference's frame k-1 -> k warm-start chain, so results depend\n"
+           "                              on N; N = 1 keeps the reference semantics. [default: 1]\n"
            "  --two_pass                  Use the two-pass projection kernels instead of the fused sweep.\n"
            "  --partition_voxels          Shard the RTM by voxel columns (every GPU holds all pixels of a voxel\n"
            "                              block; all-reduce of A x per iteration) instead of by pixel rows.\n"

@@ -1,4 +1,5 @@
-"""End-to-end CLI runs on generated HDF5 cases: output file vs the fp64 oracle frame by frame."""
+"""End-to-end CLI runs on generated HDF5 cases: output file vs the fp64 oracle frame by frame. ``cli.main`` runs the
+native driver as a child process, so its console output is captured at the file-descriptor level (capfd)."""
 import math
 import os
 
@@ -49,13 +50,13 @@ def _read_all(path):
 
 @pytest.mark.parametrize("log", [False, True])
 @pytest.mark.parametrize("no_guess", [False, True])
-def test_cli_cpu_matches_reference_cpu_semantics(tmp_path, capsys, log, no_guess):
+def test_cli_cpu_matches_reference_cpu_semantics(tmp_path, capfd, log, no_guess):
     case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_a",), laplacian=True, nframes=3, saturate=0.05)
     out = str(tmp_path / "out.h5")
     argv = ["--use_cpu", "-m", "120", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3", "-o", out]
     argv += (["-L"] if log else []) + (["--no_guess"] if no_guess else []) + case.files
     assert cli.main(argv) == 0
-    assert capsys.readouterr().out.count("Processed in:") == 3
+    assert capfd.readouterr().out.count("Processed in:") == 3
     xs, sts, its = _expected(case, sart_cpu_semantics, warm=not no_guess, logarithmic=log, max_iterations=120,
                              conv_tolerance=1e-6, beta_laplace=1e-3)
     t, last, st, _ = _read_all(out)
@@ -64,37 +65,36 @@ def test_cli_cpu_matches_reference_cpu_semantics(tmp_path, capsys, log, no_guess
     np.testing.assert_allclose(last, xs[-1], rtol=1e-7, atol=1e-12 * np.abs(xs[-1]).max())
 
 
-def test_cli_time_range_and_resume(tmp_path, capsys):
+def test_cli_time_range_and_resume(tmp_path, capfd):
     case = make_case(str(tmp_path / "c"), nframes=6, dt=0.1)
     out = str(tmp_path / "out.h5")
     base = ["--use_cpu", "-m", "50", "-o", out]
     assert cli.main(base + ["-t", "0:0.25"] + case.files) == 0
     t, _, _ = native().read_solution_file(out)
     np.testing.assert_allclose(t, [0.0, 0.1, 0.2], atol=1e-12)
-    capsys.readouterr()
+    capfd.readouterr()
     assert cli.main(base + ["--resume"] + case.files) == 0
-    assert capsys.readouterr().out.count("Processed in:") == 3  # only the frames after t = 0.2
+    assert capfd.readouterr().out.count("Processed in:") == 3  # only the frames after t = 0.2
     t, last, _ = native().read_solution_file(out)
     np.testing.assert_allclose(t, 0.1 * np.arange(6), atol=1e-12)
     xs, _, _ = _expected(case, sart_cpu_semantics, max_iterations=50, conv_tolerance=1e-5, beta_laplace=2e-2)
     np.testing.assert_allclose(last, xs[-1], rtol=1e-7)
 
 
-def test_cli_errors(tmp_path, capsys):
+def test_cli_errors(tmp_path, capfd):
     case = make_case(str(tmp_path / "c"), nframes=2)
-    with pytest.raises(SystemExit):
-        cli.main(["--use_cpu", "-R", "3"] + case.files)
-    assert "relaxation" in capsys.readouterr().err
-    with pytest.raises(SystemExit):
-        cli.main(["--use_cpu", "-t", "100:200"] + case.files)
-    assert "No composite images" in capsys.readouterr().err
+    assert cli.main(["--use_cpu", "-R", "3"] + case.files) == 1
+    assert "relaxation" in capfd.readouterr().err
+    assert cli.main(["--use_cpu", "-t", "100:200"] + case.files) == 1
+    assert "No composite images" in capfd.readouterr().err
     assert cli.main(["--help"]) == 0
+    assert "Usage: sartsolver" in capfd.readouterr().out
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("log", [False, True])
 @pytest.mark.parametrize("extra", [[], ["--two_pass"], ["--batch_frames", "4"]])
-def test_cli_gpu_matches_gpu_semantics(tmp_path, capsys, log, extra):
+def test_cli_gpu_matches_gpu_semantics(tmp_path, capfd, log, extra):
     case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_b",), laplacian=True, nframes=4, saturate=0.05,
                      nvoxel=2048, grid=(16, 16, 16), shapes=((24, 32), (20, 30)))
     out = str(tmp_path / "out.h5")
@@ -112,7 +112,7 @@ def test_cli_gpu_matches_gpu_semantics(tmp_path, capsys, log, extra):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("log", [False, True])
-def test_cli_batched_time_series_warm_start(tmp_path, capsys, log):
+def test_cli_batched_time_series_warm_start(tmp_path, capfd, log):
     """--batch_frames keeps a warm-started time series (reference main.cpp:127-139) at MFMA throughput with
     continuous batching: 16 slots, a finished frame's slot takes the next frame, every frame after the first
     16 starts from the latest finished frame (reported as warm_from in --profile). 3 cameras, 64 frames: the
@@ -133,7 +133,7 @@ def test_cli_batched_time_series_warm_start(tmp_path, capsys, log):
         t0 = time.perf_counter()
         assert cli.main(kw + extra + ["--profile", prof, "-o", out] + case.files) == 0
         walls[mode] = time.perf_counter() - t0
-        assert capsys.readouterr().out.count("Processed in:") == 64
+        assert capfd.readouterr().out.count("Processed in:") == 64
         t, last, st = native().read_solution_file(out)
         assert len(t) == 64
         np.testing.assert_array_equal(st, sts)  # same status per frame as the sequential warm-start series

@@ -1,5 +1,7 @@
-"""The native ``sartsolver`` executable (csrc/driver/sartsolver_main.cpp) against the Python driver and the
-fp64 oracle: same CLI, same output file, multi-rank runs under torchrun --no-python."""
+"""The native ``sartsolver`` executable (csrc/driver/sartsolver_main.cpp) against the fp64 oracle, and the Python
+entry point ``python -m mpi_cuda_sartsolver_amd`` (a launcher of that executable, cli.py): same arguments, same
+output file bit for bit, multi-rank runs under torchrun (--no-python for the executable itself) and mpiexec."""
+import json
 import os
 import socket
 import subprocess
@@ -149,8 +151,13 @@ def test_native_gpu_matches_python_driver(tmp_path, binary, log, extra):
     case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_b",), laplacian=True, nframes=3, saturate=0.05,
                      nvoxel=2048, grid=(16, 16, 16), shapes=((24, 32), (20, 30)))
     base = ["-m", "60", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3"] + (["-L"] if log else []) + extra
-    r1 = _run_native(binary, base + ["-o", str(tmp_path / "n.h5"), *case.files])
+    prof = str(tmp_path / "n.jsonl")
+    r1 = _run_native(binary, base + ["--profile", prof, "-o", str(tmp_path / "n.h5"), *case.files])
     assert r1.returncode == 0, r1.stdout + r1.stderr
+    for line in open(prof):  # bytes of the fp32 shard: 4 per element, one (fused) or two reads per sweep
+        rec = json.loads(line)
+        if "rtm_GBps" in rec:  # (batched frames report per-frame times only)
+            assert abs(rec["rtm_GBps"] / rec["gflops"] - (1 if rec["fused"] else 2)) < 1e-6, rec
     r2 = _run_python(base + ["-o", str(tmp_path / "p.h5"), *case.files])
     assert r2.returncode == 0, r2.stdout + r2.stderr
     n = native()
@@ -251,8 +258,13 @@ def test_rtm_bf16_cli(tmp_path, binary, log, two_pass):
     case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_b",), laplacian=False, nframes=2, saturate=0.05,
                      nvoxel=2048, grid=(16, 16, 8), shapes=((24, 32), (20, 30)))
     base = ["-m", "40", "-c", "1e-9", "--rtm_bf16"] + (["-L"] if log else []) + (["--two_pass"] if two_pass else [])
-    r1 = _run_native(binary, base + ["-o", str(tmp_path / "n.h5"), *case.files])
+    prof = str(tmp_path / "n.jsonl")
+    r1 = _run_native(binary, base + ["--profile", prof, "-o", str(tmp_path / "n.h5"), *case.files])
     assert r1.returncode == 0, r1.stdout + r1.stderr
+    for line in open(prof):  # bytes of the bf16 shard: 2 per element, one (fused) or two reads per sweep
+        rec = json.loads(line)
+        reads = 1 if rec["fused"] else 2
+        assert abs(rec["rtm_GBps"] / rec["gflops"] - reads * 2 / 4) < 1e-6, rec
     r2 = _run_python(base + ["-o", str(tmp_path / "p.h5"), *case.files])
     assert r2.returncode == 0, r2.stdout + r2.stderr
     n = native()
