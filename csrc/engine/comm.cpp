@@ -191,9 +191,10 @@ class P2pComm final : public Communicator {
     void all_reduce(float* dev, size_t n, ReduceOp op, hipStream_t stream) override {
         // the choice depends only on n (identical on every rank), never on this rank's pointer alignment
         if (active_ && n > 0 && (int64_t)n <= max_n_) {
-            // SART_FAULT_P2P=k (tests): the k-th P2P all-reduce of this process raises no flags (a peer that never
-            // arrives), only on SART_FAULT_RANK when that is set
-            const bool skip = fault_call_ > 0 && ++calls_ == fault_call_;
+            // SART_FAULT_P2P=k (tests): from its k-th P2P all-reduce on, this process raises no flags (a peer whose
+            // device path stopped; a single missing flag would heal at the next call, flags being monotonic), only
+            // on SART_FAULT_RANK when that is set
+            const bool skip = fault_call_ > 0 && ++calls_ >= fault_call_;
             p2p(dev, (int64_t)n, op == ReduceOp::kSum ? 0 : 1, stream, -1.0, skip);
         } else
             base_->all_reduce(dev, n, op, stream);

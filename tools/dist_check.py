@@ -52,7 +52,8 @@ def main():
     if a.multiframe:
         from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
 
-        s = MultiFrameSARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic, batch=a.batch)
+        s = MultiFrameSARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic, batch=a.batch,
+                                 allow_zero_tolerance=a.tol == 0)
         g = prob.measurement.cpu().numpy()
         res = s.solve_batch(np.stack([g, 0.5 * g, 2.0 * g]))
         x = np.stack([r.solution for r in res])
