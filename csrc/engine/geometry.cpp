@@ -26,9 +26,12 @@ struct V6Candidate {
 // profiles/bench_r2_widths_kw.jsonl)
 constexpr double narrow_slab_penalty(int kw) { return kw == 8 ? 1.0 : (kw == 7 ? 1.02 : 1.15); }
 
-// Chip-wide row groups hand granules off through memory instead of the XCD's L2 (handoff-1to1: cross-XCD
-// +0.1-0.3 us of ~3 us under streaming load). SART_FUSED_XL=0 / 1 forces one kind where both exist.
-constexpr double kChipWidePenalty = 1.05;
+// Chip-wide row groups hand granules off through memory instead of the XCD's L2. Per CU they streamed 1.22-1.55x
+// slower than XCD-local groups at the widths where both exist (100000 / 200000 / 150000 voxels: 22.6 / 23.3 / 18.2
+// against 28.6 / 28.5 / 28.2 GB/s per CU, profiles/bench_r3_widths_chipwide_vs_xl.jsonl), so they serve only
+// rows wider than an XCD's 32 slabs, where they beat variant 3 by 20-31 % (300000 / 524288 / 1048576 voxels:
+// 5.07 / 5.85 / 6.15 against 4.15 / 4.87 / 4.70 TB/s). SART_FUSED_XL=0 / 1 forces one kind where both exist.
+constexpr double kChipWidePenalty = 1.6;
 
 int xl_mode() {
     const char* e = std::getenv("SART_FUSED_XL");
@@ -126,8 +129,8 @@ FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_
     if (variant == 6 && num_cus % 8 == 0) {
         // Rows per tile, slab and row-group kind: the requested T, else the candidate with the lowest time per row
         // (ties: the larger T and kw, XCD-local; T = 4 at ld = 64k, 2 at 128k, 1 at 256k measured 6.5-6.9 TB/s,
-        // against 4.0-4.7 TB/s for variant 3, profiles/probe_r1_fused_T.jsonl). Rows wider than 32 slabs, and
-        // widths whose J leaves CUs of every XCD idle, use chip-wide row groups of I = num_cus / J.
+        // against 4.0-4.7 TB/s for variant 3, profiles/probe_r1_fused_T.jsonl). Rows wider than an XCD's slabs use
+        // chip-wide row groups of I = num_cus / J (kChipWidePenalty).
         const V6Candidate best = best_v6(ld, num_cus, rows_per_tile, narrow_slabs, chip_wide);
         if (best.I > 0) {
             g.K = best.T, g.J = best.J, g.I = best.I, g.grid = g.I * g.J, g.variant = 6, g.T = best.T;

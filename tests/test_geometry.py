@@ -39,8 +39,8 @@ def test_every_width_gets_variant6(nvox):
 
 
 def test_width_sweep_variant6_and_waste():
-    """Every width from 20k to 1M voxels gets variant 6 with at most 10 % padding; chip-wide row groups keep at
-    least 85 % of the CUs busy where XCD-local groups left whole CUs of every XCD idle (round 2: min 0.69)."""
+    """Every width from 20k to 1M voxels gets variant 6 with at most 10 % padding (XCD-local row groups up to 32
+    slabs, chip-wide ones beyond: measured 1.2-1.55x slower per CU where both exist)."""
     used = []
     for nvox in list(range(20480, 262145, 997)) + list(range(262144, 1048577, 8191)):
         ld = rtm.choose_ld(nvox)
@@ -48,14 +48,14 @@ def test_width_sweep_variant6_and_waste():
         g = rtm.fused_geometry(ld, CUS, 6)
         _check_v6(ld, g)
         used.append(g.grid / CUS)
-    assert min(used) >= 0.85 and sum(used) / len(used) >= 0.95, (min(used), sum(used) / len(used))
+    assert min(used) >= 0.65 and sum(used) / len(used) >= 0.9, (min(used), sum(used) / len(used))
 
 
 @pytest.mark.parametrize("ld,T,kw,J,I,xl", [(65536, 4, 8, 32, 8, True), (131072, 1, 8, 16, 16, True),
                                             (262144, 1, 8, 32, 8, True), (61440, 4, 8, 30, 8, True),
-                                            (16384, 4, 8, 8, 32, True), (106496, 1, 8, 13, 19, False),
-                                            (100352, 1, 7, 14, 18, False), (200704, 1, 7, 28, 9, False),
-                                            (71680, 1, 7, 10, 24, True), (150528, 1, 7, 21, 12, False),
+                                            (16384, 4, 8, 8, 32, True), (106496, 1, 8, 13, 16, True),
+                                            (100352, 1, 7, 14, 16, True), (200704, 1, 7, 28, 8, True),
+                                            (71680, 1, 7, 10, 24, True), (153600, 1, 6, 25, 8, True),
                                             (229376, 1, 7, 32, 8, True), (524288, 1, 8, 64, 4, False),
                                             (1048576, 1, 8, 128, 2, False), (301056, 1, 7, 42, 6, False)])
 def test_production_geometries(ld, T, kw, J, I, xl):
@@ -68,6 +68,10 @@ def test_xl_override(monkeypatch):
     monkeypatch.setenv("SART_FUSED_XL", "1")
     g = rtm.fused_geometry(200704, CUS, 6)
     assert g.xl and (g.J, g.I) == (28, 8)
+    monkeypatch.setenv("SART_FUSED_XL", "0")
+    g = rtm.fused_geometry(200704, CUS, 6)
+    assert not g.xl and (g.J, g.I) == (28, 9)
+    monkeypatch.setenv("SART_FUSED_XL", "1")
     assert rtm.fused_geometry(524288, CUS, 6).variant == 3
     monkeypatch.setenv("SART_FUSED_XL", "0")
     g = rtm.fused_geometry(65536, CUS, 6)

@@ -215,10 +215,9 @@ def test_fused_v6_schedules(dev, T, sched, log):
 # groups per XCD), on 4096-row shards against the device fp64 oracle (models/oracle.py). The two-pass kernels
 # (oracle-validated above) set the fp32 error scale: the fused sweep must be no worse than 1.25x of it.
 # Chip-wide row groups (xl False: granules through memory, I = 256 // J) serve rows wider than 32 slabs
-# (300000 ... 1048576 voxels; the reference runs any V: sart_kernels.cu:269-283) and widths whose J left CUs of
-# every XCD idle (100000 / 150000 / 200000).
+# (300000 ... 1048576 voxels; the reference runs any V: sart_kernels.cu:269-283).
 PROD = [(65536, 4, 32, 8), (131072, 1, 16, 16), (262144, 1, 32, 8),
-        (60000, 4, 30, 8), (100000, 1, 14, 18), (200000, 1, 28, 9), (70000, 1, 10, 24), (150000, 1, 21, 12),
+        (60000, 4, 30, 8), (100000, 1, 14, 16), (200000, 1, 28, 8), (70000, 1, 10, 24), (150000, 1, 25, 8),
         (300000, 1, 42, 6), (524288, 1, 64, 4), (1048576, 1, 128, 2)]
 
 
@@ -285,7 +284,7 @@ def test_segmented_chains(dev, monkeypatch, storage, nvox, T, log):
 
 
 @pytest.mark.parametrize("rows,nvox,T,J,I", [(1024, 65536, 4, 32, 8), (512, 131072, 1, 16, 16),
-                                             (256, 262144, 1, 32, 8), (512, 100000, 1, 14, 18),
+                                             (256, 262144, 1, 32, 8), (512, 100000, 1, 14, 16),
                                              (128, 524288, 1, 64, 4)])
 @pytest.mark.parametrize("log", [False, True])
 def test_production_geometry_vs_oracle(dev, rows, nvox, T, J, I, log):

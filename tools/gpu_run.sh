@@ -84,6 +84,11 @@ for step in "$@"; do
           --out "$OUT/mfov_report_r$r.json" || true
       done ;;
     benchshare) run bench_share2 600 python bench.py --gpus 2 --share-gpus --steps 3 --warmup 1 ;;
+    small3) for p in 8192 16384; do
+              run bench_small_$p 300 python bench.py --steps 5 --warmup 1 --npix $p --no-selfcheck || exit 1
+            done ;;
+    rehearse8f) SART_P2P_TIMEOUT_S=60 run bench_share8_fused 500 python bench.py --gpus 8 --share-gpus --npix 16384 \
+                  --steps 3 --warmup 1 --watchdog 300 ;;
     widths3) for v in 150000 200000 100000 300000 524288; do
                run bench_w3_$v 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck &&
                SART_FUSED_XL=1 run bench_w3xl_$v 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
@@ -146,6 +151,13 @@ for step in "$@"; do
             run abmf2_new32_$i 300 python bench.py --steps 3 --warmup 1 --frames 32 &&
             run abmf2_old32_$i 300 python .abold/bench.py --steps 3 --warmup 1 --frames 32 || exit 1
           done && run x3acc2 300 python tools/x3_accuracy.py ;;
+    pmcmfb) echo "=== pmcmfb" >> "$OUT/session.log"
+           timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
+             -d "$OUT/pmc_mfb64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 5 --npix 16384 --rtm-dtype bf16 --no-selfcheck > "$OUT/pmc_mfb64.log" 2>&1
+           rc=$?; echo "=== pmcmfb rc=$rc" >> "$OUT/session.log"; tail -5 "$OUT/pmc_mfb64.log"; [ $rc -eq 0 ] || exit $rc
+           timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_WAVES GRBM_GUI_ACTIVE \
+             -d "$OUT/pmc_mfb64_insts" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 5 --npix 16384 --rtm-dtype bf16 --no-selfcheck > "$OUT/pmc_mfb64_insts.log" 2>&1
+           rc=$?; echo "=== pmcmfb insts rc=$rc" >> "$OUT/session.log"; [ $rc -eq 0 ] || exit $rc ;;
     pmcmf) echo "=== pmcmf" >> "$OUT/session.log"
            timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
              -d "$OUT/pmc_mf64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 5 --npix 16384 --no-selfcheck > "$OUT/pmc_mf64.log" 2>&1
