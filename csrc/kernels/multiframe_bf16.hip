@@ -266,7 +266,12 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const AT* __restrict
     // (k_mf_split_x with perm)
     const AT* __restrict__ ap = A + (row0 + r) * ld + c0 + (A32 ? 4 : 8) * g;
     const int64_t xo = (int64_t)r * ld + c0 + 8 * g;
-    const int lofs = r * 4 + g;  // uint4 slot of (frame r, voxels 8 g..) inside a 1 KiB piece
+    // uint4 slot of this lane's fragment (frame r, voxels 8 g..) inside a 1 KiB piece: the lane index itself. Every
+    // wave's lane l reads what lane l of the loading wave wrote, so any bijection works; lane-linear slots put the 16
+    // lanes of each ds_read_b128 group and the 8 of each ds_write_b128 group on distinct 16-B bank slots (the former
+    // r * 4 + g was 2-way on the reads and 4-way on the writes: PMC SQ_LDS_BANK_CONFLICT ~4x the LDS-active cycles,
+    // profiles/pmc_r3_mfb64.txt)
+    const int lofs = lane;
     typedef typename ARaw<AT>::fwd AF;
     constexpr int R16 = 32 * KB * (int)sizeof(AT) / 16;  // 16-B slots per row and step (AS)
     constexpr int RPI = 64 / R16;                         // rows per staging load instruction
@@ -540,7 +545,7 @@ __global__ __launch_bounds__(256, (mf_bwd_min_waves<AT, VT>())) void k_mf_backpr
     if (r_end > nrows32) r_end = nrows32;
     const AT* __restrict__ ap = A + (r_begin + 8 * g) * ld + vb * 64 + 4 * i16;
     const int64_t wo = (int64_t)i16 * ldw + r_begin + 8 * g;
-    const int lofs = i16 * 4 + g;
+    const int lofs = lane;  // lane-linear W slots: conflict-free (see k_mf_forward_b16_lds)
     typedef typename ARaw<AT>::bwd AB;
     // plane pl of frame group j: hi, mid (split-A: stored after hi in Wh), lo
     auto plane_ptr = [&](int pl) { return pl == NPL - 1 ? Wl : Wh + (int64_t)pl * NF * ldw; };

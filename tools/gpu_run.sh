@@ -151,6 +151,14 @@ for step in "$@"; do
             run abmf2_new32_$i 300 python bench.py --steps 3 --warmup 1 --frames 32 &&
             run abmf2_old32_$i 300 python .abold/bench.py --steps 3 --warmup 1 --frames 32 || exit 1
           done && run x3acc2 300 python tools/x3_accuracy.py ;;
+    abmfb) run pytest_mfb 900 python -u -m pytest tests/test_gpu_multiframe.py tests/test_gpu_multiframe_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
+           for i in 1 2; do
+             for spec in "b64|--frames 64 --rtm-dtype bf16" "f64|--frames 64" "b32|--frames 32 --rtm-dtype bf16" "f32|--frames 32"; do
+               name=${spec%%|*}; args=${spec#*|}
+               run abmfb_new_${name}_$i 300 python bench.py --steps 3 --warmup 1 --no-selfcheck $args &&
+               run abmfb_old_${name}_$i 300 python .abold/bench.py --steps 3 --warmup 1 --no-selfcheck $args || exit 1
+             done
+           done ;;
     pmcmfb) echo "=== pmcmfb" >> "$OUT/session.log"
            timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
              -d "$OUT/pmc_mfb64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 5 --npix 16384 --rtm-dtype bf16 --no-selfcheck > "$OUT/pmc_mfb64.log" 2>&1
