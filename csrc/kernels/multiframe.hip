@@ -273,7 +273,9 @@ static int mf_rows(int nf);
 int mf_forward_num_splits(int64_t ld, int64_t nrows_pad) {
     const int64_t rows_per_block = (nrows_pad % 64 == 0 ? mf_rows(0) : 2) * 64;  // 4 waves x 16 * rt rows
     const int64_t nblk = (nrows_pad + rows_per_block - 1) / rows_per_block;
-    int64_t s = (1024 + nblk - 1) / nblk;
+    const char* e = std::getenv("SART_MF_FWD_BLOCKS");  // target workgroups (tuning knob)
+    const int64_t target = (e && *e) ? std::atoll(e) : 1024;
+    int64_t s = (target + nblk - 1) / nblk;
     const int64_t smax = ld / 1024;
     if (s > smax) s = smax;
     if (s < 1) s = 1;

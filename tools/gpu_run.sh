@@ -159,6 +159,14 @@ for step in "$@"; do
                run abmfb_old_${name}_$i 300 python .abold/bench.py --steps 3 --warmup 1 --no-selfcheck $args || exit 1
              done
            done ;;
+    mfblocks) for kv in DEF=0 SART_MF_FWD_BLOCKS=768 SART_MF_FWD_BLOCKS=1536 SART_MF_FWD_BLOCKS=2048 SART_MF_FWD_BLOCKS=3072 \
+                      SART_MF_BP_BLOCKS=768 SART_MF_BP_BLOCKS=1536 SART_MF_BP_BLOCKS=2048 SART_MF_BP_BLOCKS=3072 DEF=1; do
+                for spec in "b64|--frames 64 --rtm-dtype bf16" "f64|--frames 64"; do
+                  name=${spec%%|*}; args=${spec#*|}
+                  env "$kv" timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck $args > "$OUT/mfblk_${name}_$kv.log" 2>&1 || { echo "FATAL $kv"; exit 1; }
+                  echo "=== mfblk $name $kv $(grep -h '^{' "$OUT/mfblk_${name}_$kv.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+                done
+              done ;;
     pmcmfb) echo "=== pmcmfb" >> "$OUT/session.log"
            timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE \
              -d "$OUT/pmc_mfb64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 5 --npix 16384 --rtm-dtype bf16 --no-selfcheck > "$OUT/pmc_mfb64.log" 2>&1
