@@ -398,6 +398,33 @@ def test_fault_injection_fallback_chain(dev, faults, expect):
     _check(x, A, g, max_iterations=12)
 
 
+@pytest.mark.parametrize("faults,expect", [(1, 3), (2, None)])
+def test_fault_injection_fallback_chain_chip_wide(dev, faults, expect):
+    """The fallback chain from chip-wide row groups (524288 voxels: J = 64 > 32 slabs per XCD) to variant 3 and the
+    two-pass kernels, each re-solve against the device fp64 oracle (fused <= 1.25x the two-pass error)."""
+    from mpi_cuda_sartsolver_amd.models.oracle import sart_oracle_f64
+    from mpi_cuda_sartsolver_amd.ops import hip
+    from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
+
+    k = hip()
+    prob = make_problem(512, 524288, seed=17, device=dev, saturate_fraction=0.02)
+    rtm, g = prob.rtm, prob.measurement.cpu().numpy()
+    cfg = k.EngineConfig()
+    cfg.max_iterations, cfg.conv_tolerance, cfg.allow_zero_tolerance = 8, 0.0, True
+    cfg.fault_inject = faults
+    e = k.Engine(dev.index or 0, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld, k.local_comm(), cfg)
+    assert e.use_fused and e.geometry.variant == 6 and not e.geometry.xl and e.geometry.J == 64
+    x, info = e.solve(g, None)
+    assert info["fallbacks"] == faults and info["used_fused"] == (expect is not None)
+    if expect is not None:
+        assert info["fused_variant"] == expect
+    cfg.fault_inject, cfg.use_fused = 0, False
+    e2 = k.Engine(dev.index or 0, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld, k.local_comm(), cfg)
+    x2, _ = e2.solve(g, None)
+    x64 = sart_oracle_f64(rtm, g, 8)
+    assert _rel(x, x64) <= 1.25 * _rel(x2, x64) + 1e-7
+
+
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("log", [False, True])
 def test_hip_graph_chunks_match_eager(dev, fused, log):
