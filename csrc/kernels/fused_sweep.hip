@@ -403,7 +403,7 @@ __device__ __forceinline__ float class_sum_dpp(float v, int lane) {
 }
 
 // Schedules with a separate publisher wave (the split exchange)
-constexpr bool sched_split(int sched) { return sched >= 4 && sched <= 7; }
+constexpr bool sched_split(int sched) { return sched >= 4 && sched <= 8; }
 
 template <bool LOG, bool XL, bool DIAG, int T, int SCHED, typename AT = float, int CPL = 4, int KW = 8>
 __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
@@ -441,10 +441,13 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     // measured 3 % slower than the fp32 lag (458 vs 473 it/s at 64k x 64k), so it is kept there.
     constexpr bool DEEP = BF && SCHED == 0;
     constexpr int PD = (SCHED == 2 || SCHED == 4 || SCHED == 7) ? 2 : 1;   // exchange step u polls tile u - PD
-    constexpr int PQ = DEEP ? 4 : (SCHED == 1 ? 3 : 2);      // polls in flight (finishes tile u - PD - PQ + 1)
-    constexpr int L = DEEP ? PD + PQ : (SCHED == 6 ? 3 : (SCHED == 7 ? 4 : 3 + D));  // back-projection lag in steps
+    // schedule 8 = schedule 5 with 3 polls in flight and a 4-step lag in a 5-slot ring (chip-wide row groups, whose
+    // granules make memory-side round trips; kw 6 / 7 only: five 32-KiB kw 8 slots do not fit the LDS)
+    constexpr int PQ = DEEP ? 4 : ((SCHED == 1 || SCHED == 8) ? 3 : 2);  // polls in flight (finishes tile u - PD - PQ + 1)
+    constexpr int L = DEEP ? PD + PQ : (SCHED == 6 ? 3 : ((SCHED == 7 || SCHED == 8) ? 4 : 3 + D));  // back-projection lag
+    static_assert(SCHED != 8 || (KW <= 7 && T == 1 && !BF), "schedule 8: fp32 T = 1 slabs of kw <= 7");
     static_assert(L >= PD + PQ, "the weights must be ready one step before they are used");
-    constexpr int NL = (BF && CPL == 4) ? 8 : ((SCHED == 6 || SCHED == 7) ? 3 : 4);  // LDS ring slots (32 KB fp32 or wide bf16 / 16 KB narrow bf16)
+    constexpr int NL = (BF && CPL == 4) ? 8 : ((SCHED == 6 || SCHED == 7) ? 3 : (SCHED == 8 ? 5 : 4));  // LDS ring slots (32 KB fp32 or wide bf16 / 16 KB narrow bf16)
     static_assert(L <= NL + D - 1, "a parked tile must be back-projected before its ring slot is reused");
     // register tile slots per wave (8 KB fp32 / 4 KB bf16 each): AH in flight + D held. bf16: 6-7 tiles of
     // 8-byte loads in flight (<= 56 loads, inside the 6-bit vmcnt range); 8 slots with the x slab in LDS
@@ -922,7 +925,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
 }
 
 constexpr size_t rows_lds_bytes(int T, int sched, int H = 1, int KW = 8) {
-    return (sched == 6 || sched == 7 ? 3 : 4) /*NL x 4 waves x KW x 64 lanes x 16 B*/ * 4 * KW * 64 * sizeof(float4) +
+    return (sched == 6 || sched == 7 ? 3 : (sched == 8 ? 5 : 4)) /*NL x 4 waves x KW x 64 lanes x 16 B*/ * 4 * KW * 64 * sizeof(float4) +
            (((sched >= 1 && sched <= 4) || sched == 6 || sched == 7) ? (4 / T) * KW * 64 * H * sizeof(float4) : 0) +  // x slab
            (8 * 4 * 3 + 8 + 4) * sizeof(float);
 }
@@ -930,6 +933,8 @@ static_assert(rows_lds_bytes(4, 4, 2) <= 160 * 1024, "wide bf16 tiles: T = 4 fit
 static_assert(rows_lds_bytes(2, 6, 2) <= 160 * 1024, "wide bf16 tiles: T = 2 (schedule 6) fits the LDS");
 static_assert(rows_lds_bytes(2, 7, 2) <= 160 * 1024, "wide bf16 tiles: T = 2 (schedule 7) fits the LDS");
 static_assert(rows_lds_bytes(2, 4, 2) > 160 * 1024, "schedule 6 exists because the 4-slot ring does not fit");
+static_assert(rows_lds_bytes(1, 8, 1, 7) <= 160 * 1024 && rows_lds_bytes(1, 8, 1, 8) > 160 * 1024,
+              "schedule 8: a 5-slot ring of kw 7 slabs fits, of kw 8 slabs not");
 
 static int g_fused_dbg = 0;    // diagnostics only (set through fused_set_debug)
 static int g_fused_sched = 4;  // variant 6 pipeline schedule (k_fused_sweep_rows SCHED)
@@ -1008,15 +1013,22 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
         // chip-wide row groups (T = 1, schedule 5): workgroup b is (b % I, b / I), granules written through to
         // memory (agent scope), so a group may span XCDs: J up to the CU count, I = CUs / J of any value
         if constexpr (T == 1) {
-            auto go_cw = [&](auto lg, auto k) {
-                launch_rows_t<decltype(lg)::value, false, false, 1, 5, float, 4, decltype(k)::value>(
+            auto go_cw = [&](auto lg, auto k, auto sc) {
+                launch_rows_t<decltype(lg)::value, false, false, 1, decltype(sc)::value, float, 4, decltype(k)::value>(
                     grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
                     chain_tiles);
             };
+            // SART_FUSED_CW_SCHED=8: the deeper exchange pipeline for kw 6 / 7 (read per launch: A/B runs)
+            const char* cws = std::getenv("SART_FUSED_CW_SCHED");
+            const bool deep = cws && std::atoi(cws) == 8;
+            using S5 = std::integral_constant<int, 5>;
+            using S8 = std::integral_constant<int, 8>;
             auto by_kw = [&](auto lg) {
-                if (kw == 8) go_cw(lg, std::integral_constant<int, 8>{});
-                else if (kw == 7) go_cw(lg, std::integral_constant<int, 7>{});
-                else go_cw(lg, std::integral_constant<int, 6>{});
+                if (kw == 8) go_cw(lg, std::integral_constant<int, 8>{}, S5{});
+                else if (kw == 7 && deep) go_cw(lg, std::integral_constant<int, 7>{}, S8{});
+                else if (kw == 7) go_cw(lg, std::integral_constant<int, 7>{}, S5{});
+                else if (deep) go_cw(lg, std::integral_constant<int, 6>{}, S8{});
+                else go_cw(lg, std::integral_constant<int, 6>{}, S5{});
             };
             if (logmode) by_kw(std::true_type{}); else by_kw(std::false_type{});
             return;

@@ -157,7 +157,7 @@ def test_native_gpu_matches_python_driver(tmp_path, binary, log, extra):
     for line in open(prof):  # bytes of the fp32 shard: 4 per element, one (fused) or two reads per sweep
         rec = json.loads(line)
         if "rtm_GBps" in rec:  # (batched frames report per-frame times only)
-            assert abs(rec["rtm_GBps"] / rec["gflops"] - (1 if rec["fused"] else 2)) < 1e-6, rec
+            assert abs(rec["rtm_GBps"] / rec["gflops"] - (1 if rec["fused"] else 2)) < 1e-4, rec  # 6 printed digits
     r2 = _run_python(base + ["-o", str(tmp_path / "p.h5"), *case.files])
     assert r2.returncode == 0, r2.stdout + r2.stderr
     n = native()
@@ -264,7 +264,7 @@ def test_rtm_bf16_cli(tmp_path, binary, log, two_pass):
     for line in open(prof):  # bytes of the bf16 shard: 2 per element, one (fused) or two reads per sweep
         rec = json.loads(line)
         reads = 1 if rec["fused"] else 2
-        assert abs(rec["rtm_GBps"] / rec["gflops"] - reads * 2 / 4) < 1e-6, rec
+        assert abs(rec["rtm_GBps"] / rec["gflops"] - reads * 2 / 4) < 1e-4, rec  # (6 printed digits)
     r2 = _run_python(base + ["-o", str(tmp_path / "p.h5"), *case.files])
     assert r2.returncode == 0, r2.stdout + r2.stderr
     n = native()
