@@ -1018,9 +1018,10 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
                     grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
                     chain_tiles);
             };
-            // SART_FUSED_CW_SCHED=8: the deeper exchange pipeline for kw 6 / 7 (read per launch: A/B runs)
+            // kw 6 / 7: schedule 8, the deeper exchange pipeline (+5.3 % at 300000 voxels, +2.8 % at 530432,
+            // profiles/ab_r3_cw_sched8.jsonl); SART_FUSED_CW_SCHED=5 keeps schedule 5 (read per launch: A/B runs)
             const char* cws = std::getenv("SART_FUSED_CW_SCHED");
-            const bool deep = cws && std::atoi(cws) == 8;
+            const bool deep = !(cws && std::atoi(cws) == 5);
             using S5 = std::integral_constant<int, 5>;
             using S8 = std::integral_constant<int, 8>;
             auto by_kw = [&](auto lg) {

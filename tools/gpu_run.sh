@@ -84,11 +84,11 @@ for step in "$@"; do
           --out "$OUT/mfov_report_r$r.json" || true
       done ;;
     benchshare) run bench_share2 600 python bench.py --gpus 2 --share-gpus --steps 3 --warmup 1 ;;
-    cw8) SART_FUSED_CW_SCHED=8 run fcheck_cw8 600 python tools/fused_check.py 8192x300000 4096x150528 &&
+    cw8) run fcheck_cw8 600 python tools/fused_check.py 8192x300000 4096x150528 &&
          for i in 1 2; do
            for v in 300000 530432; do
-             run bench_cw5_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck &&
-             SART_FUSED_CW_SCHED=8 run bench_cw8_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
+             SART_FUSED_CW_SCHED=5 run bench_cw5_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck &&
+             run bench_cw8_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
            done
          done ;;
     small3) for p in 8192 16384; do
