@@ -211,6 +211,21 @@ def test_p2p_timeout_degrades_to_base_on_every_rank(tmp_path, fused):
     assert max(e1, e2) <= RANK_FACTOR * e32 + 1e-7, (e1, e2, e32)
 
 
+def test_p2p_timeout_degrades_multiframe(tmp_path):
+    """The multi-frame engine's chunked all-reduce on its comm stream: a P2P stall on rank 1 (SART_FAULT_P2P) is
+    agreed on after the batch, every rank re-solves the batch on the staged base, and every frame matches the 1-rank
+    batch within the fp32 emulation's error of the oracle."""
+    extra = ["--multiframe", "--iters", "20", "--tol", "0"]
+    x1, m1 = _run(1, str(tmp_path / "r1"), extra + ["--save-problem"])
+    x, m = _run(2, str(tmp_path / "f2"), extra, SART_P2P="1", SART_FAULT_P2P="4", SART_FAULT_RANK="1",
+                SART_P2P_TIMEOUT_S="4")
+    for r in m[0]["ranks"]:
+        assert r["comm"] == "staged" and r["comm_fallbacks"] == 1, m[0]["ranks"]
+    assert all(f["comm"] == "staged" for f in m)
+    (e1, e2), e32 = _oracle_rel(tmp_path, [x1[0], x[0]], extra, 20)
+    assert max(e1, e2) <= RANK_FACTOR * e32 + 1e-7, (e1, e2, e32)
+
+
 @pytest.mark.parametrize("nproc", [2, 3])
 def test_fused_timeout_on_one_rank_falls_back_on_all(tmp_path, nproc):
     """A persistent-sweep timeout reported by ONE rank (device-side fault injection on rank 1) reaches every

@@ -57,7 +57,9 @@ def main():
         g = prob.measurement.cpu().numpy()
         res = s.solve_batch(np.stack([g, 0.5 * g, 2.0 * g]))
         x = np.stack([r.solution for r in res])
-        meta = [dict(status=r.status, iterations=r.iterations, comm=s.native_comm.backend) for r in res]
+        meta = [dict(status=r.status, iterations=r.iterations, comm=r.comm or s.native_comm.backend,
+                     comm_fallbacks=r.comm_fallbacks) for r in res]
+        meta[0]["ranks"] = comm.all_gather_object(dict(comm=res[0].comm, comm_fallbacks=res[0].comm_fallbacks))
     else:
         s = SARTSolver(prob.rtm, L, comm, params, logarithmic=a.logarithmic, use_fused=a.fused,
                        partition="cols" if a.columns else None, time_collectives=True,
