@@ -403,7 +403,7 @@ __device__ __forceinline__ float class_sum_dpp(float v, int lane) {
 }
 
 // Schedules with a separate publisher wave (the split exchange)
-constexpr bool sched_split(int sched) { return sched >= 4 && sched <= 9; }
+constexpr bool sched_split(int sched) { return sched >= 4 && sched <= 8; }
 
 template <bool LOG, bool XL, bool DIAG, int T, int SCHED, typename AT = float, int CPL = 4, int KW = 8>
 __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThreads) void k_fused_sweep_rows(
@@ -416,7 +416,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     // columns, so widths whose 8-KiB slab count does not fit an XCD's 32 CUs still use most of them)
     static_assert(KW >= 6 && KW <= 8, "lane-vectors per lane");
     constexpr int WPR = 4 / T;   // compute waves per row (each on its own 2048-column sub-slab)
-    constexpr int D = SCHED == 7 ? 2 : ((SCHED == 1 || SCHED == 2 || SCHED == 4 || SCHED == 6 || SCHED == 9) ? 1 : 0);  // steps a reduced tile stays in VGPRs
+    constexpr int D = SCHED == 7 ? 2 : ((SCHED == 1 || SCHED == 2 || SCHED == 4 || SCHED == 6) ? 1 : 0);  // steps a reduced tile stays in VGPRs
     constexpr bool XS_LDS = (SCHED >= 1 && SCHED <= 4) || SCHED == 6 || SCHED == 7;  // x slab in LDS instead of VGPRs
     static_assert(!XS_LDS || T >= 2, "the LDS holds the x slab only for T >= 2");
     // wave 4 publishes granules, wave 5 gathers (no shared vmcnt queue); schedule 5 = the split exchange with
@@ -443,12 +443,11 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     constexpr int PD = (SCHED == 2 || SCHED == 4 || SCHED == 7) ? 2 : 1;   // exchange step u polls tile u - PD
     // schedule 8 = schedule 5 with 3 polls in flight and a 4-step lag in a 5-slot ring (chip-wide row groups, whose
     // granules make memory-side round trips; kw 6 / 7 only: five 32-KiB kw 8 slots do not fit the LDS)
-    // schedule 9 = schedule 5 with 3 polls in flight and a 4-step lag in the 4-slot ring: a reduced tile stays one
-    // step in VGPRs before parking (D = 1, 3 register tiles in flight): kw 8 chip-wide row groups
-    constexpr int PQ = DEEP ? 4 : ((SCHED == 1 || SCHED == 8 || SCHED == 9) ? 3 : 2);  // polls in flight (finishes tile u - PD - PQ + 1)
-    constexpr int L = DEEP ? PD + PQ : (SCHED == 6 ? 3 : ((SCHED == 7 || SCHED == 8 || SCHED == 9) ? 4 : 3 + D));  // back-projection lag
+    // (the kw 8 analogue, a 4-step lag in the 4-slot ring with a reduced tile held one step in VGPRs, measured 4-5 %
+    // slower than schedule 5 at 524288 / 1048576 voxels: profiles/ab_r3_cw_sched9_negative.jsonl)
+    constexpr int PQ = DEEP ? 4 : ((SCHED == 1 || SCHED == 8) ? 3 : 2);  // polls in flight (finishes tile u - PD - PQ + 1)
+    constexpr int L = DEEP ? PD + PQ : (SCHED == 6 ? 3 : ((SCHED == 7 || SCHED == 8) ? 4 : 3 + D));  // back-projection lag
     static_assert(SCHED != 8 || (KW <= 7 && T == 1 && !BF), "schedule 8: fp32 T = 1 slabs of kw <= 7");
-    static_assert(SCHED != 9 || (T == 1 && !BF), "schedule 9: fp32 T = 1");
     static_assert(L >= PD + PQ, "the weights must be ready one step before they are used");
     constexpr int NL = (BF && CPL == 4) ? 8 : ((SCHED == 6 || SCHED == 7) ? 3 : (SCHED == 8 ? 5 : 4));  // LDS ring slots (32 KB fp32 or wide bf16 / 16 KB narrow bf16)
     static_assert(L <= NL + D - 1, "a parked tile must be back-projected before its ring slot is reused");
@@ -1027,12 +1026,8 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
             const bool deep = !(cws && std::atoi(cws) == 5);
             using S5 = std::integral_constant<int, 5>;
             using S8 = std::integral_constant<int, 8>;
-            // kw 8: SART_FUSED_CW_SCHED=9 selects schedule 9 (A/B)
-            using S9 = std::integral_constant<int, 9>;
-            const bool deep8 = cws && std::atoi(cws) == 9;
             auto by_kw = [&](auto lg) {
-                if (kw == 8 && deep8) go_cw(lg, std::integral_constant<int, 8>{}, S9{});
-                else if (kw == 8) go_cw(lg, std::integral_constant<int, 8>{}, S5{});
+                if (kw == 8) go_cw(lg, std::integral_constant<int, 8>{}, S5{});
                 else if (kw == 7 && deep) go_cw(lg, std::integral_constant<int, 7>{}, S8{});
                 else if (kw == 7) go_cw(lg, std::integral_constant<int, 7>{}, S5{});
                 else if (deep) go_cw(lg, std::integral_constant<int, 6>{}, S8{});

@@ -91,14 +91,6 @@ for step in "$@"; do
              run bench_cw8_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
            done
          done ;;
-    cw9) run fcheck_cw9 600 env SART_FUSED_CW_SCHED=9 python tools/fused_check.py 4096x524288 &&
-         for i in 1 2; do
-           for spec in "524288|65536" "1048576|16384"; do
-             v=${spec%%|*}; p=${spec#*|}
-             run bench_cw9base_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --npix $p --no-selfcheck &&
-             SART_FUSED_CW_SCHED=9 run bench_cw9_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --npix $p --no-selfcheck || exit 1
-           done
-         done ;;
     small3) for p in 8192 16384; do
               run bench_small_$p 300 python bench.py --steps 5 --warmup 1 --npix $p --no-selfcheck || exit 1
             done ;;
