@@ -29,8 +29,9 @@ constexpr double narrow_slab_penalty(int kw) { return kw == 8 ? 1.0 : (kw == 7 ?
 // Chip-wide row groups hand granules off through memory instead of the XCD's L2. Per CU they streamed 1.22-1.55x
 // slower than XCD-local groups at the widths where both exist (100000 / 200000 / 150000 voxels: 22.6 / 23.3 / 18.2
 // against 28.6 / 28.5 / 28.2 GB/s per CU, profiles/bench_r3_widths_chipwide_vs_xl.jsonl), so they serve only
-// rows wider than an XCD's 32 slabs, where they beat variant 3 by 20-31 % (300000 / 524288 / 1048576 voxels:
-// 5.07 / 5.85 / 6.15 against 4.15 / 4.87 / 4.70 TB/s). SART_FUSED_XL=0 / 1 forces one kind where both exist.
+// rows wider than an XCD's 32 slabs, where they beat variant 3 by 22-30 % (300000 / 524288 / 1048576 voxels:
+// 5.40 / 5.95 / 6.11 against 4.15 / 4.87 / 4.70 TB/s, kw 6 / 7 with fused schedule 8). SART_FUSED_XL=0 / 1 forces
+// one kind where both exist.
 constexpr double kChipWidePenalty = 1.6;
 
 int xl_mode() {

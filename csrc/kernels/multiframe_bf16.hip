@@ -241,8 +241,20 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
 // wave-private LDS image with the 16-B slot XOR-swizzled by (row & 7) (slot row * R16 + (seg ^ (row & 7)): the
 // 16 lanes that read one fragment column hit 8 different bank groups), and reads the fragments back with
 // ds_read_b128. Same in-order LDS queue for the write and the read of one wave: no barrier.
+// Waves per SIMD the register budget is cut for (the second __launch_bounds__ argument): SART_MF_MINW_FWD /
+// SART_MF_MINW_BWD at compile time (A/B builds); 1 lets the 64-frame bf16 kernels take 284 / 332 VGPRs (one wave per
+// SIMD, no latency hiding across waves).
+#ifndef SART_MF_MINW_FWD
+#define SART_MF_MINW_FWD 2
+#endif
+#ifndef SART_MF_MINW_BWD
+#define SART_MF_MINW_BWD 2
+#endif
+template <typename AT, int NG>
+constexpr int mf_fwd_min_waves() { return std::is_same<AT, float>::value ? 1 : (NG == 4 ? SART_MF_MINW_FWD : 1); }
+
 template <int NG, int DEPTH, int RT, int KB, typename AT = bf16_t, bool AS = false>
-__global__ __launch_bounds__(256) void k_mf_forward_b16_lds(const AT* __restrict__ A, int64_t ld, int64_t nrows,
+__global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forward_b16_lds(const AT* __restrict__ A, int64_t ld, int64_t nrows,
                                                             int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                             const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
                                                             int64_t cols_per_split, const int* __restrict__ skip) {
@@ -519,10 +531,12 @@ __global__ __launch_bounds__(256) void k_mf_backproject_b16(const bf16_t* __rest
 // Split-A occupancy: the six-product body takes ~260 registers at NG = 4 (one wave per SIMD); asking for two
 // waves per SIMD makes the compiler fit it (tools/probe_mf_x3.py).
 template <typename AT, int VT>
-constexpr int mf_bwd_min_waves() { return (std::is_same<AT, float>::value && VT == 1) ? 2 : 1; }
+constexpr int mf_bwd_min_waves() {
+    return std::is_same<AT, float>::value ? (VT == 1 ? 2 : 1) : SART_MF_MINW_BWD;
+}
 
 template <int NG, int DEPTH, int VT, typename AT = bf16_t>
-__global__ __launch_bounds__(256, (mf_bwd_min_waves<AT, VT>())) void k_mf_backproject_b16_lds(const AT* __restrict__ A, int64_t ld,
+__global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::is_same<AT, float>::value && VT == 1 ? 2 : 1))) void k_mf_backproject_b16_lds(const AT* __restrict__ A, int64_t ld,
                                                                 int64_t nrows32, const bf16_t* __restrict__ Wh,
                                                                 const bf16_t* __restrict__ Wl, int64_t ldw,
                                                                 int64_t rows_per_split, float* __restrict__ partial,

@@ -91,6 +91,15 @@ for step in "$@"; do
              run bench_cw8_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
            done
          done ;;
+    mfminw) for i in 1 2; do
+              timeout -k 10 300 python .abold/bench.py --steps 3 --warmup 1 --no-selfcheck --frames 64 --rtm-dtype bf16 > "$OUT/mfw_old_$i.log" 2>&1 || exit 1
+              echo "=== mfw old $i $(grep -h '^{' "$OUT/mfw_old_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+              for cfg in "2|4,2,lds|1,lds" "3|4,1,lds|1,lds" "3|2,2,lds|1,lds" "2|2,2,lds|1,lds" "2|4,2,lds|2,lds"; do
+                d=${cfg%%|*}; rest=${cfg#*|}; f=${rest%%|*}; v=${rest#*|}
+                SART_MF_DEPTH=$d SART_MF_B16_FWD=$f SART_MF_B16_VT=$v timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck --frames 64 --rtm-dtype bf16 > "$OUT/mfw_new_${d}_${f}_${v}_$i.log" 2>&1 || exit 1
+                echo "=== mfw new d=$d fwd=$f vt=$v $i $(grep -h '^{' "$OUT/mfw_new_${d}_${f}_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+              done
+            done ;;
     small3) for p in 8192 16384; do
               run bench_small_$p 300 python bench.py --steps 5 --warmup 1 --npix $p --no-selfcheck || exit 1
             done ;;
