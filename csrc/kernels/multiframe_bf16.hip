@@ -245,10 +245,10 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
 // SART_MF_MINW_BWD at compile time (A/B builds); 1 lets the 64-frame bf16 kernels take 284 / 332 VGPRs (one wave per
 // SIMD, no latency hiding across waves).
 #ifndef SART_MF_MINW_FWD
-#define SART_MF_MINW_FWD 2
+#define SART_MF_MINW_FWD 1
 #endif
 #ifndef SART_MF_MINW_BWD
-#define SART_MF_MINW_BWD 2
+#define SART_MF_MINW_BWD 1
 #endif
 template <typename AT, int NG>
 constexpr int mf_fwd_min_waves() { return std::is_same<AT, float>::value ? 1 : (NG == 4 ? SART_MF_MINW_FWD : 1); }
