@@ -250,6 +250,10 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
 #ifndef SART_MF_MINW_BWD
 #define SART_MF_MINW_BWD 1
 #endif
+// bf16 X / W fragments read from LDS all at once at the top of a step (A/B builds: -DSART_MF_XF_EARLY=0)
+#ifndef SART_MF_XF_EARLY
+#define SART_MF_XF_EARLY 1
+#endif
 template <typename AT, int NG>
 constexpr int mf_fwd_min_waves() { return std::is_same<AT, float>::value ? 1 : (NG == 4 ? SART_MF_MINW_FWD : 1); }
 
@@ -359,6 +363,31 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
             // fragment of tile row block rt, k block kb: (bf16) 8 consecutive voxels; (fp32) the two 16-B halves
             // of the permuted k order
             auto frag16 = [&](int rt, int seg) { return img[(rt * 16 + r) * R16 + (seg ^ (r & 7))]; };
+            if constexpr (!A32 && !AS && SART_MF_XF_EARLY) {
+                // bf16 A in registers: every X fragment of the step is read from LDS first (KB x 2 planes x NG
+                // ds_read_b128), then the MFMAs run with counted waits. Left to itself the scheduler re-used a few
+                // registers and issued each read ~4 MFMAs ahead of its use, which at one wave per SIMD exposes the
+                // LDS latency before every MFMA group. Same accumulation order: bitwise unchanged.
+                u32x4 xf[KB][2][NG];
+#pragma unroll
+                for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+                    for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+                        for (int j = 0; j < NG; ++j) xf[kb][pl][j] = xs[((kb * 2 + pl) * NG + j) * 64];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+                    for (int j = 0; j < NG; ++j)
+#pragma unroll
+                        for (int rt = 0; rt < RT; ++rt) {
+                            acc[rt][j] = mfma_b16(a[sl][rt][kb], xf[kb][0][j], acc[rt][j]);
+                            acc[rt][j] = mfma_b16(a[sl][rt][kb], xf[kb][1][j], acc[rt][j]);
+                        }
+                __syncthreads();
+                return;
+            }
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb) {
                 if constexpr (A32) {
@@ -613,6 +642,28 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
             if (t >= nst) return;  // uniform for the workgroup
             stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);
             const u32x4* ws = s_w[t & 1][0] + lofs;
+            if constexpr (!A32 && SART_MF_XF_EARLY) {
+                // bf16: the step's W fragments are read once for all VT voxel tiles (the loop below re-read them per
+                // tile), all before the MFMAs (see k_mf_forward_b16_lds). Same accumulation order.
+                u32x4 wf[2][NG];
+#pragma unroll
+                for (int j = 0; j < NG; ++j) wf[0][j] = ws[j * 64], wf[1][j] = ws[(NG + j) * 64];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int vt = 0; vt < VT; ++vt) {
+                    const uint4 fr[4] = {phase_frag<0>(av[sl][vt]), phase_frag<1>(av[sl][vt]),
+                                         phase_frag<2>(av[sl][vt]), phase_frag<3>(av[sl][vt])};
+#pragma unroll
+                    for (int j = 0; j < NG; ++j)
+#pragma unroll
+                        for (int p = 0; p < 4; ++p) {
+                            acc[vt][p][j] = mfma_b16(fr[p], wf[0][j], acc[vt][p][j]);
+                            acc[vt][p][j] = mfma_b16(fr[p], wf[1][j], acc[vt][p][j]);
+                        }
+                }
+                __syncthreads();
+                return;
+            }
 #pragma unroll
             for (int vt = 0; vt < VT; ++vt) {
                 if constexpr (A32) {
