@@ -24,7 +24,20 @@ struct V6Candidate {
 // kw < 8 streams fewer bytes per pipeline step for the same per-step exchange work: per CU, kw 7 measured
 // 26.4 GB/s and kw 6 23.2 GB/s against 26.6 at kw 8 (bench --nvox 200000 / 150000 / 65536,
 // profiles/bench_r2_widths_kw.jsonl)
-constexpr double narrow_slab_penalty(int kw) { return kw == 8 ? 1.0 : (kw == 7 ? 1.02 : 1.15); }
+constexpr double narrow_slab_penalty(int kw) { return kw == 8 ? 1.0 : (kw == 7 ? 1.02 : (kw == 6 ? 1.15 : 1.3)); }
+
+// kw candidates: 8, 7, 6 (narrow_slabs), 5 with SART_FUSED_KW5=1; forced: SART_FUSED_KW=k keeps only k for the
+// geometry of a given width (A/B runs; the width itself is chosen without it)
+bool kw_allowed(int kw, bool narrow_slabs, bool forced = true) {
+    if (const char* e = std::getenv("SART_FUSED_KW"); forced && e && *e) return kw == std::atoi(e) && (kw == 8 || narrow_slabs);
+    if (kw == 8) return true;
+    if (!narrow_slabs) return false;
+    if (kw == 5) {
+        const char* e = std::getenv("SART_FUSED_KW5");
+        return e && std::atoi(e) == 1;
+    }
+    return true;
+}
 
 // Chip-wide row groups hand granules off through memory instead of the XCD's L2. Per CU they streamed 1.22-1.55x
 // slower than XCD-local groups at the widths where both exist (100000 / 200000 / 150000 voxels: 22.6 / 23.3 / 18.2
@@ -75,9 +88,10 @@ V6Candidate best_kind(int64_t ld, int T, int kw, int num_cus, bool chip_wide) {
 // The lowest-cost candidate over (kw, T, kind) for width ld (I == 0: none). rows_per_tile > 0 fixes T.
 V6Candidate best_v6(int64_t ld, int num_cus, int rows_per_tile, bool narrow_slabs, bool chip_wide) {
     V6Candidate best;
-    for (const int kw : {8, 7, 6}) {
-        if (kw != 8 && !narrow_slabs) continue;
+    for (const int kw : {8, 7, 6, 5}) {
+        if (!kw_allowed(kw, narrow_slabs)) continue;
         for (const int T : {4, 2, 1}) {
+            if (T != 1 && kw == 5) continue;
             if (rows_per_tile > 0 && T != rows_per_tile) continue;
             const V6Candidate c = best_kind(ld, T, kw, num_cus, chip_wide);
             if (c.I > 0 && (best.I == 0 || c.cost < best.cost)) best = c;
@@ -96,9 +110,10 @@ int64_t choose_ld(int64_t nvoxel, double max_waste, bool narrow_slabs) {
         constexpr int kCus = 256;  // MI355X: 256 CUs in 8 XCDs
         int64_t best_ld = 0;
         double best_cost = 0.0;
-        for (const int kw : {8, 7, 6}) {
-            if (kw != 8 && !narrow_slabs) continue;
+        for (const int kw : {8, 7, 6, 5}) {
+            if (!kw_allowed(kw, narrow_slabs, false)) continue;
             for (const int T : {4, 2, 1}) {
+                if (T != 1 && kw == 5) continue;
                 const int64_t slab = 1024 * (int64_t)kw / T;
                 const int64_t ld = (nvoxel + slab - 1) / slab * slab;
                 if ((double)(ld - nvoxel) > max_waste * (double)nvoxel) continue;
@@ -126,7 +141,6 @@ FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_
         const char* e = std::getenv("SART_FUSED_T");
         rows_per_tile = (e && *e) ? std::atoi(e) : 0;
     }
-    if (const char* e = std::getenv("SART_FUSED_KW"); e && *e && std::atoi(e) == 8) narrow_slabs = false;
     if (variant == 6 && num_cus % 8 == 0) {
         // Rows per tile, slab and row-group kind: the requested T, else the candidate with the lowest time per row
         // (ties: the larger T and kw, XCD-local; T = 4 at ld = 64k, 2 at 128k, 1 at 256k measured 6.5-6.9 TB/s,

@@ -45,7 +45,7 @@ def main():
             progress(f"{sh}: {'fused' if fused else 'two-pass'} solve")
             r = s.solve(g)
             if fused:
-                out.update(geom=[s.geom.variant, s.geom.T, s.geom.J, s.geom.I, s.geom.cpl],
+                out.update(geom=[s.geom.variant, s.geom.T, s.geom.J, s.geom.I, s.geom.cpl], kw=s.geom.kw, xl=s.geom.xl,
                            sched=s.k.fused_get_schedule(), fallbacks=r.fallbacks, used_fused=r.used_fused)
                 r2 = s.solve(g)
                 out["fused_repeat_bitwise"] = bool(np.array_equal(r.solution, r2.solution))

@@ -91,6 +91,28 @@ for step in "$@"; do
              run bench_cw8_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
            done
          done ;;
+    kw5) SART_FUSED_KW5=1 run fcheck_kw5 600 python tools/fused_check.py 4096x150000 4096x163840 &&
+         SART_FUSED_KW5=1 SART_FUSED_XL_SCHED=8 run fcheck_kw5s8 600 python tools/fused_check.py 4096x150000 4096x200000 &&
+         for i in 1 2; do
+           for v in 147456 150000 155648 163840; do
+             run bench_kwb_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck &&
+             SART_FUSED_KW5=1 run bench_kw5_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck &&
+             SART_FUSED_KW5=1 SART_FUSED_XL_SCHED=8 run bench_kw5s8_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
+           done
+           for v in 100000 200000; do
+             run bench_kwb_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck &&
+             SART_FUSED_XL_SCHED=8 run bench_kws8_${v}_$i 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck || exit 1
+           done
+         done ;;
+    rsab) SART_FUSED_KW5=1 run fcheck_rs 600 python tools/fused_check.py 4096x150000 4096x200000 4096x100000 4096x300000 &&
+          for i in 1 2; do
+            for cfg in 150000: 150000:SART_FUSED_KW5=1 163840:SART_FUSED_KW5=1 200000: 100000: 300000: 524288: 65536:; do
+              v=${cfg%%:*}; e=${cfg#*:}; tag=${v}_${e:+kw5}
+              env $e timeout -k 10 300 python .abold/bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/rs_old_${tag}_$i.log" 2>&1 &&
+              env $e timeout -k 10 300 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/rs_new_${tag}_$i.log" 2>&1 || exit 1
+              echo "=== rs $tag $i old $(grep -o '"effective_hbm_TBps_per_gpu": [0-9.]*' "$OUT/rs_old_${tag}_$i.log") new $(grep -o '"effective_hbm_TBps_per_gpu": [0-9.]*' "$OUT/rs_new_${tag}_$i.log")" | tee -a "$OUT/session.log"
+            done
+          done ;;
     mfminw) for i in 1 2; do
               timeout -k 10 300 python .abold/bench.py --steps 3 --warmup 1 --no-selfcheck --frames 64 --rtm-dtype bf16 > "$OUT/mfw_old_$i.log" 2>&1 || exit 1
               echo "=== mfw old $i $(grep -h '^{' "$OUT/mfw_old_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
