@@ -133,6 +133,13 @@ for step in "$@"; do
              done &&
              run bench_w3_1m 300 python bench.py --steps 3 --warmup 1 --nvox 1048576 --npix 16384 --no-selfcheck &&
              SART_FUSED_XL=1 run bench_w3xl_1m 300 python bench.py --steps 3 --warmup 1 --nvox 1048576 --npix 16384 --no-selfcheck ;;
+    widthsweep)  # 65536 rows x 32768 ... 262144 voxels in steps of 8192 (one JSON line per width)
+      for v in $(seq ${WS_FROM:-32768} 8192 ${WS_TO:-262144}); do
+        timeout -k 10 200 python bench.py --steps 3 --warmup 1 --iters ${WS_ITERS:-50} --nvox $v --no-selfcheck \
+          > "$OUT/ws_$v.log" 2>&1 || { echo "FATAL width $v"; tail -n 20 "$OUT/ws_$v.log"; exit 1; }
+        grep -h '^{' "$OUT/ws_$v.log" >> "$OUT/widthsweep.jsonl"
+        echo "=== width $v $(grep -h '^{' "$OUT/ws_$v.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
+      done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
