@@ -140,6 +140,23 @@ for step in "$@"; do
         grep -h '^{' "$OUT/ws_$v.log" >> "$OUT/widthsweep.jsonl"
         echo "=== width $v $(grep -h '^{' "$OUT/ws_$v.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
       done ;;
+    mfdeep)  # bf16 64-frame ring depth A/B (3 = default, 4, 5) + the MF bf16 tests at depth 5
+      SART_MF_DEPTH=5 run pytest_mfdeep 600 python -u -m pytest tests/test_gpu_multiframe_bf16.py -m gpu -x -q \
+        -p no:cacheprovider --timeout 120 --timeout-method thread &&
+      for i in 1 2; do
+        for d in 3 4 5; do
+          SART_MF_DEPTH=$d timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck --frames 64 --rtm-dtype bf16 \
+            > "$OUT/mfd_${d}_$i.log" 2>&1 || { echo "FATAL depth $d"; tail -n 20 "$OUT/mfd_${d}_$i.log"; exit 1; }
+          echo "=== mfdeep d=$d run $i $(grep -h '^{' "$OUT/mfd_${d}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
+    pmcfetchmf)  # HBM bytes per multi-frame kernel (bf16 shard, 64 frames): is X / W re-read from memory?
+      echo "=== pmcfetchmf" >> "$OUT/session.log"
+      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_mfb64" -o run --output-format csv -- python3 bench.py \
+        --steps 1 --warmup 0 --frames 64 --iters 5 --rtm-dtype bf16 --no-selfcheck > "$OUT/pmc_fetch_mfb64.log" 2>&1
+      rc=$?; echo "=== pmcfetchmf rc=$rc" >> "$OUT/session.log"; [ $rc -eq 0 ] || exit $rc ;;
+    probes3) run probe_mf_ld 300 python tools/probe_mf_ld.py &&
+             run ablation_dips 300 python tools/fused_ablation.py --dtype fp32 65536x147456 65536x172032 65536x73728 65536x139264 ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
