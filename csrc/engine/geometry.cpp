@@ -24,10 +24,14 @@ struct V6Candidate {
 // kw < 8 streams fewer bytes per pipeline step for the same per-step exchange work: per CU, kw 7 measured
 // 26.4 GB/s and kw 6 23.2 GB/s against 26.6 at kw 8 (bench --nvox 200000 / 150000 / 65536,
 // profiles/bench_r2_widths_kw.jsonl)
-constexpr double narrow_slab_penalty(int kw) { return kw == 8 ? 1.0 : (kw == 7 ? 1.02 : (kw == 6 ? 1.15 : 1.3)); }
+// kw 9 (T = 1 only, 3 register tiles in flight): 4-10 % below kw 8's per-CU rate (70000 voxels: 344 it/s at kw 9,
+// J = 8 on 256 CUs, against 348 at kw 7, J = 10 on 240 CUs; profiles/ab_r3_kw9.jsonl)
+constexpr double narrow_slab_penalty(int kw) {
+    return kw == 8 ? 1.0 : (kw == 9 ? 1.06 : (kw == 7 ? 1.02 : (kw == 6 ? 1.15 : 1.3)));
+}
 
-// kw candidates: 8, 7, 6 (narrow_slabs), 5 with SART_FUSED_KW5=1; forced: SART_FUSED_KW=k keeps only k for the
-// geometry of a given width (A/B runs; the width itself is chosen without it)
+// kw candidates: 8, 7, 6, 9 (narrow_slabs; 9 unless SART_FUSED_KW9=0), 5 with SART_FUSED_KW5=1; forced:
+// SART_FUSED_KW=k keeps only k for the geometry of a given width (A/B runs; the width itself is chosen without it)
 bool kw_allowed(int kw, bool narrow_slabs, bool forced = true) {
     if (const char* e = std::getenv("SART_FUSED_KW"); forced && e && *e) return kw == std::atoi(e) && (kw == 8 || narrow_slabs);
     if (kw == 8) return true;
@@ -35,6 +39,10 @@ bool kw_allowed(int kw, bool narrow_slabs, bool forced = true) {
     if (kw == 5) {
         const char* e = std::getenv("SART_FUSED_KW5");
         return e && std::atoi(e) == 1;
+    }
+    if (kw == 9) {
+        const char* e = std::getenv("SART_FUSED_KW9");
+        return !(e && *e && std::atoi(e) == 0);
     }
     return true;
 }
@@ -63,7 +71,7 @@ V6Candidate v6_candidate(int64_t ld, int T, int kw, int num_cus, bool xl) {
         if (J > per_xcd) return c;
         c.I = 8 * (per_xcd / (int)J);
     } else {
-        if (T != 1 || J > num_cus) return c;
+        if (T != 1 || J > num_cus || kw == 9) return c;  // (kw 9: XCD-local groups only)
         c.I = num_cus / (int)J;
     }
     c.T = T, c.J = (int)J, c.kw = kw, c.xl = xl;
@@ -88,10 +96,10 @@ V6Candidate best_kind(int64_t ld, int T, int kw, int num_cus, bool chip_wide) {
 // The lowest-cost candidate over (kw, T, kind) for width ld (I == 0: none). rows_per_tile > 0 fixes T.
 V6Candidate best_v6(int64_t ld, int num_cus, int rows_per_tile, bool narrow_slabs, bool chip_wide) {
     V6Candidate best;
-    for (const int kw : {8, 7, 6, 5}) {
+    for (const int kw : {8, 7, 6, 5, 9}) {
         if (!kw_allowed(kw, narrow_slabs)) continue;
         for (const int T : {4, 2, 1}) {
-            if (T != 1 && kw == 5) continue;
+            if (T != 1 && (kw == 5 || kw == 9)) continue;
             if (rows_per_tile > 0 && T != rows_per_tile) continue;
             const V6Candidate c = best_kind(ld, T, kw, num_cus, chip_wide);
             if (c.I > 0 && (best.I == 0 || c.cost < best.cost)) best = c;
@@ -110,10 +118,10 @@ int64_t choose_ld(int64_t nvoxel, double max_waste, bool narrow_slabs) {
         constexpr int kCus = 256;  // MI355X: 256 CUs in 8 XCDs
         int64_t best_ld = 0;
         double best_cost = 0.0;
-        for (const int kw : {8, 7, 6, 5}) {
+        for (const int kw : {8, 7, 6, 5, 9}) {
             if (!kw_allowed(kw, narrow_slabs, false)) continue;
             for (const int T : {4, 2, 1}) {
-                if (T != 1 && kw == 5) continue;
+                if (T != 1 && (kw == 5 || kw == 9)) continue;
                 const int64_t slab = 1024 * (int64_t)kw / T;
                 const int64_t ld = (nvoxel + slab - 1) / slab * slab;
                 if ((double)(ld - nvoxel) > max_waste * (double)nvoxel) continue;

@@ -402,6 +402,12 @@ __device__ __forceinline__ float class_sum_dpp(float v, int lane) {
     return r;
 }
 
+// Register tile slots of the fp32 x-slab-in-VGPR schedules (0, 5, 8): >= 32 KiB of A in flight per wave
+// (kw 9: 3 slots, the most the 256 VGPRs of a wave hold next to the x slab and the two accumulator sets)
+constexpr int t1_reg_slots(int kw) { return kw >= 9 ? 3 : (kw == 8 ? 4 : (kw == 7 ? 5 : (kw == 6 ? 6 : 7))); }
+template <typename AT>
+constexpr bool BF_T() { return !std::is_same<AT, float>::value; }
+
 // Schedules with a separate publisher wave (the split exchange)
 constexpr bool sched_split(int sched) { return sched >= 4 && sched <= 8; }
 
@@ -414,7 +420,8 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     static_assert(T == 1 || T == 2 || T == 4, "rows per tile");
     // KW: lane-vectors per lane per row (8: one wave covers 2048 fp32 columns; 7 / 6 give slabs of 7 / 6 KiB
     // columns, so widths whose 8-KiB slab count does not fit an XCD's 32 CUs still use most of them)
-    static_assert(KW >= 6 && KW <= 8, "lane-vectors per lane");
+    static_assert(KW >= 5 && KW <= 9, "lane-vectors per lane");
+    static_assert(KW != 9 || (T == 1 && !BF_T<AT>()), "9-KiB slabs: fp32 T = 1 only (register and LDS budget)");
     constexpr int WPR = 4 / T;   // compute waves per row (each on its own 2048-column sub-slab)
     constexpr int D = SCHED == 7 ? 2 : ((SCHED == 1 || SCHED == 2 || SCHED == 4 || SCHED == 6) ? 1 : 0);  // steps a reduced tile stays in VGPRs
     constexpr bool XS_LDS = (SCHED >= 1 && SCHED <= 4) || SCHED == 6 || SCHED == 7;  // x slab in LDS instead of VGPRs
@@ -455,7 +462,11 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     // 8-byte loads in flight (<= 56 loads, inside the 6-bit vmcnt range); 8 slots with the x slab in LDS
     // measured no faster at 64k x 64k
     // wide bf16 tiles: 8 KB per wave like fp32, 5 slots (4 in flight + 1 held), accumulators 2 x 32 VGPRs
-    constexpr int RS = XS_LDS ? ((BF && CPL == 4) ? 7 : 5) : (BF ? 7 : 4);
+    // fp32 tiles with the x slab in VGPRs (T = 1): AH = RS tiles in flight, sized so that a wave keeps >= 32 KiB of A in
+    // flight at every slab width (kw 8: 4, 7: 5, 6: 6, 5: 7 tiles). With 4 tiles at every kw, narrow slabs streamed at
+    // the same ~0.88 us per step as kw 8 (loaded latency / tiles in flight), i.e. 23-28 GB/s per CU instead of ~30
+    // (Little's law; the exchange-off ablation at 147456 voxels ran only 5 % faster, profiles/ab_r3_t1_*.jsonl)
+    constexpr int RS = XS_LDS ? ((BF && CPL == 4) ? 7 : 5) : (BF ? 7 : t1_reg_slots(KW));
     using FT = FusedTile<AT, CPL>;
     using RT = typename FT::R;
     constexpr int AH = RS - D;   // tiles in flight per wave
@@ -935,6 +946,7 @@ static_assert(rows_lds_bytes(4, 4, 2) <= 160 * 1024, "wide bf16 tiles: T = 4 fit
 static_assert(rows_lds_bytes(2, 6, 2) <= 160 * 1024, "wide bf16 tiles: T = 2 (schedule 6) fits the LDS");
 static_assert(rows_lds_bytes(2, 7, 2) <= 160 * 1024, "wide bf16 tiles: T = 2 (schedule 7) fits the LDS");
 static_assert(rows_lds_bytes(2, 4, 2) > 160 * 1024, "schedule 6 exists because the 4-slot ring does not fit");
+static_assert(rows_lds_bytes(1, 5, 1, 9) <= 160 * 1024, "9-KiB slabs: T = 1 (schedule 5) fits the LDS");
 static_assert(rows_lds_bytes(1, 8, 1, 7) <= 160 * 1024 && rows_lds_bytes(1, 8, 1, 8) > 160 * 1024,
               "schedule 8: a 5-slot ring of kw 7 slabs fits, of kw 8 slabs not");
 
@@ -1030,8 +1042,9 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
                 if (kw == 8) go_cw(lg, std::integral_constant<int, 8>{}, S5{});
                 else if (kw == 7 && deep) go_cw(lg, std::integral_constant<int, 7>{}, S8{});
                 else if (kw == 7) go_cw(lg, std::integral_constant<int, 7>{}, S5{});
-                else if (deep) go_cw(lg, std::integral_constant<int, 6>{}, S8{});
-                else go_cw(lg, std::integral_constant<int, 6>{}, S5{});
+                else if (kw == 6 && deep) go_cw(lg, std::integral_constant<int, 6>{}, S8{});
+                else if (kw == 6) go_cw(lg, std::integral_constant<int, 6>{}, S5{});
+                else go_cw(lg, std::integral_constant<int, 5>{}, S5{});
             };
             if (logmode) by_kw(std::true_type{}); else by_kw(std::false_type{});
             return;
@@ -1070,7 +1083,11 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
         };
         auto by_kw = [&](auto lg) {
             if (kw == 7) go_kw(lg, std::integral_constant<int, 7>{});
-            else go_kw(lg, std::integral_constant<int, 6>{});
+            else if (kw == 6) go_kw(lg, std::integral_constant<int, 6>{});
+            else if constexpr (T == 1) {
+                if (kw == 9) go_kw(lg, std::integral_constant<int, 9>{});
+                else go_kw(lg, std::integral_constant<int, 5>{});
+            }
         };
         if (logmode) by_kw(TT{}); else by_kw(FF{});
         return;
@@ -1121,7 +1138,9 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
         if (T >= 2 && chain_tiles % kChainAlign != 0)
             throw std::runtime_error("fused_sweep v6: segment length must be a multiple of 140 tiles");
         if (T != 1 && T != 2 && T != 4) throw std::runtime_error("fused_sweep v6: rows per tile (K) must be 1, 2 or 4");
-        if (kw < 6 || kw > 8) throw std::runtime_error("fused_sweep v6: lane-vectors per lane (kw) must be 6, 7 or 8");
+        if (kw < 5 || kw > 9) throw std::runtime_error("fused_sweep v6: lane-vectors per lane (kw) must be 5 ... 9");
+        if ((kw == 5 || kw == 9) && T != 1) throw std::runtime_error("fused_sweep v6: 5- and 9-KiB slabs need T = 1");
+        if (kw == 9 && !xl) throw std::runtime_error("fused_sweep v6: 9-KiB slabs need XCD-local row groups");
         const int64_t slab = 1024 * kw / T;  // columns per workgroup
         if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep v6: ld must equal J * slab");
         if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v6: padded rows must be a multiple of 4");

@@ -13,7 +13,8 @@ CUS = 256  # MI355X: 8 XCDs x 32 CUs
 
 
 def _check_v6(ld, g):
-    assert g is not None and g.variant == 6 and g.kw in (6, 7, 8)
+    assert g is not None and g.variant == 6 and g.kw in (6, 7, 8, 9)
+    assert g.kw != 9 or (g.T == 1 and g.xl)  # 9-KiB slabs: T = 1, XCD-local groups
     slab = 1024 * g.kw // g.T
     assert g.T in (1, 2, 4) and ld % slab == 0 and ld // slab == g.J
     assert g.J * g.T <= 256 and g.grid == g.I * g.J <= CUS
@@ -57,7 +58,9 @@ def test_width_sweep_variant6_and_waste():
                                             (100352, 1, 7, 14, 16, True), (200704, 1, 7, 28, 8, True),
                                             (71680, 1, 7, 10, 24, True), (153600, 1, 6, 25, 8, True),
                                             (229376, 1, 7, 32, 8, True), (524288, 1, 8, 64, 4, False),
-                                            (1048576, 1, 8, 128, 2, False), (301056, 1, 7, 42, 6, False)])
+                                            (1048576, 1, 8, 128, 2, False), (301056, 1, 7, 42, 6, False),
+                                            (147456, 1, 9, 16, 16, True), (73728, 1, 9, 8, 32, True),
+                                            (294912, 1, 9, 32, 8, True)])
 def test_production_geometries(ld, T, kw, J, I, xl):
     g = rtm.fused_geometry(ld, CUS, 6)
     assert (g.T, g.kw, g.J, g.I, g.xl) == (T, kw, J, I, xl)
@@ -86,7 +89,10 @@ def test_lowest_cost_rows_per_tile():
     assert (ld, g.T, g.J, g.I) == (73728, 1, 9, 24)
     ld = rtm.choose_ld(70000)
     g = rtm.fused_geometry(ld, CUS, 6)
+    # 7-KiB slabs at J = 10 (30 CUs per XCD) against 9-KiB slabs at ld 73728 (J = 8, all 32 CUs, 5 % padding):
+    # measured 348 vs 344 it/s, kept 7 KiB (profiles/ab_r3_kw9.jsonl); 73728 itself takes the 9-KiB slabs
     assert (ld, g.T, g.kw, g.J, g.I) == (71680, 1, 7, 10, 24)
+    assert rtm.fused_geometry(73728, CUS, 6).kw == 9
 
 
 def test_t2_penalty_prefers_t1():
@@ -157,3 +163,11 @@ def test_python_is_native():
     k = hip()
     for n in (1, 63, 64, 1000, 1024, 5000, 60000, 65536, 100000, 250000, 1 << 20):
         assert rtm.choose_ld(n) == k.choose_ld(n)
+
+
+def test_kw9_opt_out(monkeypatch):
+    """SART_FUSED_KW9=0 removes the 9-KiB slabs: 147456 voxels then run 6-KiB slabs on 24 CUs per XCD."""
+    monkeypatch.setenv("SART_FUSED_KW9", "0")
+    g = rtm.fused_geometry(147456, CUS, 6)
+    assert (g.kw, g.J, g.I) == (6, 24, 8)
+    assert rtm.fused_geometry(73728, CUS, 6).kw == 8

@@ -157,6 +157,37 @@ for step in "$@"; do
       rc=$?; echo "=== pmcfetchmf rc=$rc" >> "$OUT/session.log"; [ $rc -eq 0 ] || exit $rc ;;
     probes3) run probe_mf_ld 300 python tools/probe_mf_ld.py &&
              run ablation_dips 300 python tools/fused_ablation.py --dtype fp32 65536x147456 65536x172032 65536x73728 65536x139264 ;;
+    abt1)  # T = 1 register-ring depth by slab width (new) vs 4 tiles at every kw (.abold), kw 5 opt-in
+      run pytest_t1 600 python -u -m pytest tests/test_gpu_solver.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread &&
+      SART_FUSED_KW5=1 run fcheck_t1kw5 300 python tools/fused_check.py 4096x150000 4096x163840 8192x147456 &&
+      for i in 1 2; do
+        for cfg in 147456: 163840: 180224: 100000: 200000: 300000: 65536: 150000:SART_FUSED_KW5=1 163840:SART_FUSED_KW5=1; do
+          v=${cfg%%:*}; e=${cfg#*:}; tag=${v}${e:+_kw5}
+          env $e timeout -k 10 200 python .abold/bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/t1_old_${tag}_$i.log" 2>&1 &&
+          env $e timeout -k 10 200 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/t1_new_${tag}_$i.log" 2>&1 || { echo "FATAL $tag"; exit 1; }
+          echo "=== t1 $tag $i old $(grep -h '^{' "$OUT/t1_old_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])') new $(grep -h '^{' "$OUT/t1_new_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
+    access) run access_probe 120 tools/access_probe 0 && run access_probe_pitch 120 tools/access_probe 256 ;;
+    abkw9)  # 9-KiB T = 1 slabs (new default where cheaper) vs SART_FUSED_KW9=0; ring depth vs .abold (4 tiles at every kw)
+      run fcheck_kw9 300 python tools/fused_check.py 4096x147456 4096x73728 4096x294912 8192x70000 &&
+      SART_FUSED_KW5=1 run fcheck_kw5b 300 python tools/fused_check.py 4096x150000 &&
+      SEL="tests/test_gpu_solver.py" run pytest_kw9 600 python -u -m pytest tests/test_gpu_solver.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread &&
+      for i in 1 2; do
+        for v in 70000 73728 90112 139264 147456 294912; do
+          timeout -k 10 200 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/k9_new_${v}_$i.log" 2>&1 &&
+          SART_FUSED_KW9=0 timeout -k 10 200 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/k9_off_${v}_$i.log" 2>&1 || { echo "FATAL $v"; exit 1; }
+          echo "=== kw9 $v $i on $(grep -h '^{' "$OUT/k9_new_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])') off $(grep -h '^{' "$OUT/k9_off_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
+        done
+        for cfg in 147456:SART_FUSED_KW9=0 163840: 200000: 65536: 150000:SART_FUSED_KW5=1; do
+          v=${cfg%%:*}; e=${cfg#*:}; tag=${v}${e:+_${e#SART_FUSED_}}
+          if [ "$e" != "SART_FUSED_KW5=1" ]; then
+            env $e timeout -k 10 200 python .abold/bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/rd_old_${tag}_$i.log" 2>&1 || { echo "FATAL old $tag"; exit 1; }
+          fi
+          env $e timeout -k 10 200 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/rd_new_${tag}_$i.log" 2>&1 || { echo "FATAL new $tag"; exit 1; }
+          echo "=== ring $tag $i old $(grep -sh '^{' "$OUT/rd_old_${tag}_$i.log" | python -c 'import sys,json; l=sys.stdin.readline(); d=json.loads(l) if l else {}; print(d.get("iters_per_s"), d.get("effective_hbm_TBps_per_gpu"))') new $(grep -h '^{' "$OUT/rd_new_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
