@@ -188,6 +188,18 @@ for step in "$@"; do
           echo "=== ring $tag $i old $(grep -sh '^{' "$OUT/rd_old_${tag}_$i.log" | python -c 'import sys,json; l=sys.stdin.readline(); d=json.loads(l) if l else {}; print(d.get("iters_per_s"), d.get("effective_hbm_TBps_per_gpu"))') new $(grep -h '^{' "$OUT/rd_new_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
         done
       done ;;
+    ablpub)  # T = 1 lane-partial publication (new) vs the wave_sum in every compute wave (.abold)
+      run fcheck_lpub 300 python tools/fused_check.py 4096x131072 4096x150000 4096x147456 4096x300000 8192x262144 &&
+      SART_FUSED_KW5=1 run fcheck_lpub5 300 python tools/fused_check.py 4096x163840 &&
+      run pytest_lpub 600 python -u -m pytest tests/test_gpu_solver.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread &&
+      for i in 1 2; do
+        for cfg in 155648: 163840: 180224: 150000: 147456: 262144: 300000: 100000: 150000:SART_FUSED_KW5=1 163840:SART_FUSED_KW5=1; do
+          v=${cfg%%:*}; e=${cfg#*:}; tag=${v}${e:+_kw5}
+          env $e timeout -k 10 200 python .abold/bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/lp_old_${tag}_$i.log" 2>&1 &&
+          env $e timeout -k 10 200 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/lp_new_${tag}_$i.log" 2>&1 || { echo "FATAL $tag"; exit 1; }
+          echo "=== lpub $tag $i old $(grep -h '^{' "$OUT/lp_old_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])') new $(grep -h '^{' "$OUT/lp_new_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
