@@ -61,6 +61,53 @@ __device__ __forceinline__ void trace_stamp(int b, int64_t tile, int ev) {
 // ds_write, counted on lgkmcnt only).
 typedef __attribute__((address_space(3))) volatile float lds_vfloat;
 typedef __attribute__((address_space(3))) volatile int lds_vint;
+typedef int sart_i4v __attribute__((ext_vector_type(4)));
+typedef float sart_f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) volatile sart_i4v lds_vi4;
+typedef __attribute__((address_space(3))) volatile sart_f4v lds_vf4;
+
+// Row partial of tile u for tile row `lane` (< T) from the compute waves' LDS slot ps: the WPR = 4 / T waves of the
+// row, summed in wave order (bitwise the same as reading them one by one). The slot's four flags and four partials are
+// each read with ONE 16-byte LDS access: polling four flags in turn put four dependent LDS round trips (queued behind
+// the A ring's traffic) into every tile of the publisher and gatherer waves, the per-tile floor of T = 1 sweeps.
+// VEC = false: the flags and partials one by one (measured faster for 8-KiB T = 1 slabs, 4.5 %, and chip-wide row
+// groups, 7-12 %, whose gatherers then poll the peers' granules later; the 16-byte reads gain 1-5.5 % for XCD-local
+// 6 / 7-KiB slabs at T = 1: 150000 voxels 141 -> 148 it/s, profiles/ab_r3_t1_flag4.jsonl)
+template <int T, bool VEC>
+__device__ __forceinline__ float local_row_partial(lds_vint* s_pflag, lds_vfloat* s_part, int ps, int u, int lane,
+                                                   unsigned spin_limit) {
+    constexpr int WPR = 4 / T;
+    if constexpr (!VEC) {
+        float sv = 0.f;
+#pragma unroll
+        for (int i = 0; i < WPR; ++i) {
+            const int wv = lane * WPR + i;
+            unsigned spins = 0;
+            while (s_pflag[ps * 4 + wv] != u) {
+                if (++spins > spin_limit) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            asm volatile("" ::: "memory");
+            sv += s_part[ps * 4 + wv];
+        }
+        return sv;
+    }
+    unsigned spins = 0;
+    while (true) {
+        const sart_i4v f = *reinterpret_cast<lds_vi4*>(s_pflag + ps * 4);
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < WPR; ++i) ok &= f[(lane * WPR + i) & 3] == u;
+        if (ok || ++spins > spin_limit) break;  // (the compute waves always publish: the limit cannot trigger)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+    const sart_f4v v = *reinterpret_cast<lds_vf4*>(s_part + ps * 4);
+    float sv = 0.f;
+#pragma unroll
+    for (int i = 0; i < WPR; ++i) sv += v[(lane * WPR + i) & 3];
+    return sv;
+}
 
 __device__ __forceinline__ uint64_t make_granule(int epoch, float v) {
     return ((uint64_t)(uint32_t)epoch << 32) | (uint64_t)__float_as_uint(v);
@@ -488,6 +535,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     // compute waves' next tiles to finish the current ones (it skips its pacing wait on a segment's first
     // PD + PQ - 1 tiles), so the drain cannot deadlock. chain_tiles = 0: one chain, LDS combine of the T rows.
     constexpr bool SEG = SPLIT && T >= 2;
+    constexpr bool FLAG4 = XL && T == 1 && !BF && KW <= 7;  // one 16-byte LDS read of a slot's flags (local_row_partial)
     const bool seg_on = SEG && chain_tiles > 0;
 
     extern __shared__ __attribute__((aligned(16))) float4 s_ring[];  // [NL][4][KW][64] of RT (128 KB)
@@ -783,18 +831,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
         for (int64_t u = 0; u < nt; ++u) {
             const int ps = (int)(u & (NS - 1));
             if (lane < T) {
-                float sv = 0.f;
-#pragma unroll
-                for (int i = 0; i < WPR; ++i) {
-                    const int wv = lane * WPR + i;
-                    unsigned spins = 0;
-                    while (s_pflag[ps * 4 + wv] != (int)u) {
-                        if (++spins > kSpinLimit) break;
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                    asm volatile("" ::: "memory");
-                    sv += s_part[ps * 4 + wv];
-                }
+                const float sv = local_row_partial<T, FLAG4>(s_pflag, s_part, ps, (int)u, lane, kSpinLimit);
                 if (!(dbg & 1)) {
                     uint64_t* g = gran + ((t_begin + u) * J + gj) * T + lane;
                     if constexpr (XL)
@@ -893,18 +930,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
             if (u < nt && pace) {
                 const int ps = (int)(u & (NS - 1));
                 if (lane < T) {
-                    float sv = 0.f;
-#pragma unroll
-                    for (int i = 0; i < WPR; ++i) {  // fixed order: bitwise reproducible row partial
-                        const int wv = lane * WPR + i;
-                        unsigned spins = 0;
-                        while (s_pflag[ps * 4 + wv] != (int)u) {
-                            if (++spins > kSpinLimit) break;  // compute waves always publish: cannot trigger
-                            __builtin_amdgcn_s_sleep(1);
-                        }
-                        asm volatile("" ::: "memory");
-                        sv += s_part[ps * 4 + wv];
-                    }
+                    const float sv = local_row_partial<T, FLAG4>(s_pflag, s_part, ps, (int)u, lane, kSpinLimit);  // fixed order
                     if (!(dbg & 1) && !SPLIT) {
                         uint64_t* g = gran + ((t_begin + u) * J + gj) * T + lane;
                         if constexpr (XL)  // plain 8-byte store: the line stays in this XCD's L2

@@ -200,6 +200,17 @@ for step in "$@"; do
           echo "=== lpub $tag $i old $(grep -h '^{' "$OUT/lp_old_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])') new $(grep -h '^{' "$OUT/lp_new_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
         done
       done ;;
+    abflag4)  # one 16-byte LDS read for a slot's four wave flags / partials (new) vs four polls in turn (.abold)
+      run fcheck_flag4 300 python tools/fused_check.py 4096x131072 4096x150000 4096x147456 4096x300000 16384x65536 &&
+      run fcheck_flag4_old 300 python .abold/tools/fused_check.py 4096x131072 4096x150000 4096x147456 4096x300000 16384x65536 &&
+      run pytest_flag4 600 python -u -m pytest tests/test_gpu_solver.py tests/test_gpu_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread &&
+      for i in 1 2; do
+        for v in 150000 163840 188416 100000 200000 262144 300000 524288 65536 98304; do
+          timeout -k 10 200 python .abold/bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/f4_old_${v}_$i.log" 2>&1 &&
+          timeout -k 10 200 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/f4_new_${v}_$i.log" 2>&1 || { echo "FATAL $v"; exit 1; }
+          echo "=== flag4 $v $i old $(grep -h '^{' "$OUT/f4_old_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])') new $(grep -h '^{' "$OUT/f4_new_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
