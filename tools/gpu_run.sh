@@ -211,6 +211,14 @@ for step in "$@"; do
           echo "=== flag4 $v $i old $(grep -h '^{' "$OUT/f4_old_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])') new $(grep -h '^{' "$OUT/f4_new_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
         done
       done ;;
+    kw5b)  # 5-KiB slabs (with the 16-byte flag reads) against the default geometry at the kw 6 widths with idle CUs
+      for i in 1 2; do
+        for v in 150000 155648 163840 147456; do
+          timeout -k 10 200 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/k5_def_${v}_$i.log" 2>&1 &&
+          SART_FUSED_KW5=1 timeout -k 10 200 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/k5_on_${v}_$i.log" 2>&1 || { echo "FATAL $v"; exit 1; }
+          echo "=== kw5b $v $i def $(grep -h '^{' "$OUT/k5_def_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])') kw5 $(grep -h '^{' "$OUT/k5_on_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
