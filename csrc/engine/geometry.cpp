@@ -30,15 +30,15 @@ constexpr double narrow_slab_penalty(int kw) {
     return kw == 8 ? 1.0 : (kw == 9 ? 1.06 : (kw == 7 ? 1.02 : (kw == 6 ? 1.15 : 1.3)));
 }
 
-// kw candidates: 8, 7, 6, 9 (narrow_slabs; 9 unless SART_FUSED_KW9=0), 5 with SART_FUSED_KW5=1; forced:
+// kw candidates: 8, 7, 6, 5, 9 (narrow_slabs; 5 / 9 unless SART_FUSED_KW5=0 / SART_FUSED_KW9=0); forced:
 // SART_FUSED_KW=k keeps only k for the geometry of a given width (A/B runs; the width itself is chosen without it)
 bool kw_allowed(int kw, bool narrow_slabs, bool forced = true) {
     if (const char* e = std::getenv("SART_FUSED_KW"); forced && e && *e) return kw == std::atoi(e) && (kw == 8 || narrow_slabs);
     if (kw == 8) return true;
     if (!narrow_slabs) return false;
-    if (kw == 5) {
+    if (kw == 5) {  // (on by default since the 16-byte flag reads: +3.6-4 % at 150000 ... 163840, profiles/ab_r3_kw5_flag4.jsonl)
         const char* e = std::getenv("SART_FUSED_KW5");
-        return e && std::atoi(e) == 1;
+        return !(e && *e && std::atoi(e) == 0);
     }
     if (kw == 9) {
         const char* e = std::getenv("SART_FUSED_KW9");

@@ -13,8 +13,8 @@ CUS = 256  # MI355X: 8 XCDs x 32 CUs
 
 
 def _check_v6(ld, g):
-    assert g is not None and g.variant == 6 and g.kw in (6, 7, 8, 9)
-    assert g.kw != 9 or (g.T == 1 and g.xl)  # 9-KiB slabs: T = 1, XCD-local groups
+    assert g is not None and g.variant == 6 and g.kw in (5, 6, 7, 8, 9)
+    assert g.kw not in (5, 9) or (g.T == 1 and g.xl)  # 5- and 9-KiB slabs: T = 1, XCD-local groups
     slab = 1024 * g.kw // g.T
     assert g.T in (1, 2, 4) and ld % slab == 0 and ld // slab == g.J
     assert g.J * g.T <= 256 and g.grid == g.I * g.J <= CUS
@@ -56,7 +56,7 @@ def test_width_sweep_variant6_and_waste():
                                             (262144, 1, 8, 32, 8, True), (61440, 4, 8, 30, 8, True),
                                             (16384, 4, 8, 8, 32, True), (106496, 1, 8, 13, 16, True),
                                             (100352, 1, 7, 14, 16, True), (200704, 1, 7, 28, 8, True),
-                                            (71680, 1, 7, 10, 24, True), (153600, 1, 6, 25, 8, True),
+                                            (71680, 1, 7, 10, 24, True), (153600, 1, 5, 30, 8, True), (163840, 1, 5, 32, 8, True),
                                             (229376, 1, 7, 32, 8, True), (524288, 1, 8, 64, 4, False),
                                             (1048576, 1, 8, 128, 2, False), (301056, 1, 7, 42, 6, False),
                                             (147456, 1, 9, 16, 16, True), (73728, 1, 9, 8, 32, True),
@@ -171,3 +171,12 @@ def test_kw9_opt_out(monkeypatch):
     g = rtm.fused_geometry(147456, CUS, 6)
     assert (g.kw, g.J, g.I) == (6, 24, 8)
     assert rtm.fused_geometry(73728, CUS, 6).kw == 8
+
+
+def test_kw5_opt_out(monkeypatch):
+    """5-KiB slabs fill the XCDs at 148480 ... 163840 voxels (150000: J = 30 instead of 6-KiB slabs at J = 25);
+    SART_FUSED_KW5=0 removes them."""
+    assert (rtm.choose_ld(150000), rtm.fused_geometry(153600, CUS, 6).kw) == (153600, 5)
+    monkeypatch.setenv("SART_FUSED_KW5", "0")
+    g = rtm.fused_geometry(153600, CUS, 6)
+    assert (g.kw, g.J, g.I) == (6, 25, 8)

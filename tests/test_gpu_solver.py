@@ -217,8 +217,8 @@ def test_fused_v6_schedules(dev, T, sched, log):
 # Chip-wide row groups (xl False: granules through memory, I = 256 // J) serve rows wider than 32 slabs
 # (300000 ... 1048576 voxels; the reference runs any V: sart_kernels.cu:269-283).
 PROD = [(65536, 4, 32, 8), (131072, 1, 16, 16), (262144, 1, 32, 8),
-        (60000, 4, 30, 8), (100000, 1, 14, 16), (200000, 1, 28, 8), (70000, 1, 10, 24), (73728, 1, 8, 32), (150000, 1, 25, 8),
-        (147456, 1, 16, 16), (294912, 1, 32, 8), (155648, 1, 26, 8),
+        (60000, 4, 30, 8), (100000, 1, 14, 16), (200000, 1, 28, 8), (70000, 1, 10, 24), (73728, 1, 8, 32), (150000, 1, 30, 8),
+        (147456, 1, 16, 16), (294912, 1, 32, 8), (155648, 1, 31, 8), (163840, 1, 32, 8),
         (300000, 1, 42, 6), (524288, 1, 64, 4), (1048576, 1, 128, 2)]
 
 
