@@ -250,6 +250,10 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
 #ifndef SART_MF_MINW_BWD
 #define SART_MF_MINW_BWD 1
 #endif
+// split-A: X / W of the next step staged into LDS after the step's MFMAs (A/B builds: -DSART_MF_STAGE_LATE=0)
+#ifndef SART_MF_STAGE_LATE
+#define SART_MF_STAGE_LATE 1
+#endif
 // bf16 X / W fragments read from LDS all at once at the top of a step (A/B builds: -DSART_MF_XF_EARLY=0)
 #ifndef SART_MF_XF_EARLY
 #define SART_MF_XF_EARLY 1
@@ -277,6 +281,7 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
     const int64_t c1 = (c0 + cols_per_split < ld) ? c0 + cols_per_split : ld;
     Fout += (int64_t)blockIdx.y * nrows_pad * NF;
     constexpr bool A32 = std::is_same<AT, float>::value;
+    constexpr bool LATE = SART_MF_STAGE_LATE && A32;  // stage_next after the MFMAs (split-A only, see below)
     // split-A: lane (r, g) loads voxels 4 g .. 4 g + 3 and 16 + 4 g .. of each 32-voxel block (two contiguous
     // 64-byte halves of a row per instruction instead of four 16-byte pieces); the X planes hold the same k order
     // (k_mf_split_x with perm)
@@ -350,7 +355,16 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
             constexpr int sl = decltype(slc)::value;
             load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
             if (t >= nst) return;  // uniform for the workgroup
-            stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);  // X of step t + 1 into the other stage (its readers passed the last barrier)
+            // X of step t + 1 goes into the other stage (its readers passed the last barrier). Split-A stages it AFTER
+            // this step's MFMAs (stage_next): its loads were issued with A of step t + 1, and the vmcnt wait the staging
+            // needs covers them, so staging first made every step wait for step t + 1's data before computing step t:
+            // +3.3 % at 64 frames (9011 -> 9304 frame-it/s); bf16 A measured -0.8 % at 64 frames and equal at 32, so it
+            // stages first (profiles/ab_r3_mf_stage_late.jsonl).
+            auto stage_next = [&] {
+                if constexpr (LATE) __builtin_amdgcn_sched_barrier(0);
+                stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);
+            };
+            if constexpr (!LATE) stage_next();
             const u32x4* xs = s_x[t & 1][0] + lofs;
             u32x4* img = s_a[AS ? wave : 0];
             if constexpr (AS) {  // this wave's tile into its LDS image (swizzled slots)
@@ -385,6 +399,7 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
                             acc[rt][j] = mfma_b16(a[sl][rt][kb], xf[kb][0][j], acc[rt][j]);
                             acc[rt][j] = mfma_b16(a[sl][rt][kb], xf[kb][1][j], acc[rt][j]);
                         }
+                if constexpr (LATE) stage_next();
                 __syncthreads();
                 return;
             }
@@ -447,6 +462,7 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
                     }
                 }
             }
+            if constexpr (LATE) stage_next();
             __syncthreads();
         };
         for (int64_t t0 = 0; t0 < nst; t0 += RS) {
@@ -574,6 +590,7 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
     constexpr int NF = 16 * NG;
     constexpr int RS = DEPTH + 1;
     constexpr bool A32 = std::is_same<AT, float>::value;
+    constexpr bool LATE = SART_MF_STAGE_LATE && A32;  // stage_next after the MFMAs (split-A only)
     constexpr int NPL = A32 ? 3 : 2;              // W planes: hi, (mid,) lo
     constexpr int C = NPL * NG;                   // 1 KiB W pieces per step
     constexpr int XQ = C >= 4 ? (C + 3) / 4 : 1;  // pieces per wave (clamped: a duplicate load writes equal data)
@@ -640,7 +657,11 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
             constexpr int sl = decltype(slc)::value;
             load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
             if (t >= nst) return;  // uniform for the workgroup
-            stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);
+            auto stage_next = [&] {  // W of step t + 1 after this step's MFMAs (see k_mf_forward_b16_lds)
+                if constexpr (LATE) __builtin_amdgcn_sched_barrier(0);
+                stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);
+            };
+            if constexpr (!LATE) stage_next();
             const u32x4* ws = s_w[t & 1][0] + lofs;
             if constexpr (!A32 && SART_MF_XF_EARLY) {
                 // bf16: the step's W fragments are read once for all VT voxel tiles (the loop below re-read them per
@@ -661,6 +682,7 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
                             acc[vt][p][j] = mfma_b16(fr[p], wf[1][j], acc[vt][p][j]);
                         }
                 }
+                if constexpr (LATE) stage_next();
                 __syncthreads();
                 return;
             }
@@ -708,6 +730,7 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
                     }
                 }
             }
+            if constexpr (LATE) stage_next();
             __syncthreads();
         };
         for (int64_t t0 = 0; t0 < nst; t0 += RS) {

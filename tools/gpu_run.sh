@@ -219,6 +219,16 @@ for step in "$@"; do
           echo "=== kw5b $v $i def $(grep -h '^{' "$OUT/k5_def_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])') kw5 $(grep -h '^{' "$OUT/k5_on_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
         done
       done ;;
+    abstage)  # multi-frame bf16 / split-A kernels: next step's X / W staged after the MFMAs (new) vs before (.abold)
+      run pytest_stage 600 python -u -m pytest tests/test_gpu_multiframe.py tests/test_gpu_multiframe_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread &&
+      for i in 1 2; do
+        for spec in "b64|--frames 64 --rtm-dtype bf16" "f64|--frames 64" "b32|--frames 32 --rtm-dtype bf16" "f32|--frames 32" "b16|--frames 16 --rtm-dtype bf16"; do
+          name=${spec%%|*}; args=${spec#*|}
+          timeout -k 10 300 python .abold/bench.py --steps 3 --warmup 1 --no-selfcheck $args > "$OUT/st_old_${name}_$i.log" 2>&1 &&
+          timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck $args > "$OUT/st_new_${name}_$i.log" 2>&1 || { echo "FATAL $name"; exit 1; }
+          echo "=== stage $name $i old $(grep -h '^{' "$OUT/st_old_${name}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])') new $(grep -h '^{' "$OUT/st_new_${name}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
