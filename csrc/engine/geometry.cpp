@@ -71,7 +71,7 @@ V6Candidate v6_candidate(int64_t ld, int T, int kw, int num_cus, bool xl) {
         if (J > per_xcd) return c;
         c.I = 8 * (per_xcd / (int)J);
     } else {
-        if (T != 1 || J > num_cus || kw == 9) return c;  // (kw 9: XCD-local groups only)
+        if (T != 1 || J > num_cus) return c;
         c.I = num_cus / (int)J;
     }
     c.T = T, c.J = (int)J, c.kw = kw, c.xl = xl;

@@ -1066,6 +1066,7 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
             using S8 = std::integral_constant<int, 8>;
             auto by_kw = [&](auto lg) {
                 if (kw == 8) go_cw(lg, std::integral_constant<int, 8>{}, S5{});
+                else if (kw == 9) go_cw(lg, std::integral_constant<int, 9>{}, S5{});
                 else if (kw == 7 && deep) go_cw(lg, std::integral_constant<int, 7>{}, S8{});
                 else if (kw == 7) go_cw(lg, std::integral_constant<int, 7>{}, S5{});
                 else if (kw == 6 && deep) go_cw(lg, std::integral_constant<int, 6>{}, S8{});
@@ -1166,7 +1167,6 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
         if (T != 1 && T != 2 && T != 4) throw std::runtime_error("fused_sweep v6: rows per tile (K) must be 1, 2 or 4");
         if (kw < 5 || kw > 9) throw std::runtime_error("fused_sweep v6: lane-vectors per lane (kw) must be 5 ... 9");
         if ((kw == 5 || kw == 9) && T != 1) throw std::runtime_error("fused_sweep v6: 5- and 9-KiB slabs need T = 1");
-        if (kw == 9 && !xl) throw std::runtime_error("fused_sweep v6: 9-KiB slabs need XCD-local row groups");
         const int64_t slab = 1024 * kw / T;  // columns per workgroup
         if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep v6: ld must equal J * slab");
         if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep v6: padded rows must be a multiple of 4");

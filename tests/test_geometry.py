@@ -14,7 +14,7 @@ CUS = 256  # MI355X: 8 XCDs x 32 CUs
 
 def _check_v6(ld, g):
     assert g is not None and g.variant == 6 and g.kw in (5, 6, 7, 8, 9)
-    assert g.kw not in (5, 9) or (g.T == 1 and g.xl)  # 5- and 9-KiB slabs: T = 1, XCD-local groups
+    assert g.kw not in (5, 9) or g.T == 1  # 5- and 9-KiB slabs: T = 1
     slab = 1024 * g.kw // g.T
     assert g.T in (1, 2, 4) and ld % slab == 0 and ld // slab == g.J
     assert g.J * g.T <= 256 and g.grid == g.I * g.J <= CUS

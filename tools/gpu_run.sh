@@ -229,6 +229,14 @@ for step in "$@"; do
           echo "=== stage $name $i old $(grep -h '^{' "$OUT/st_old_${name}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])') new $(grep -h '^{' "$OUT/st_new_${name}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
         done
       done ;;
+    prof2tb) run rocprof_2tb 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_2tb" -o run --output-format csv -- python3 bench.py --config 2tb --steps 1 --warmup 0 --no-selfcheck &&
+             run rocprof_mfx64 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx64" -o run --output-format csv -- python3 bench.py --frames 64 --steps 1 --warmup 0 --iters 20 --no-selfcheck ;;
+    finalb) run bench_bf16 300 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
+            run bench_mfb64 300 python bench.py --steps 3 --warmup 1 --frames 64 --rtm-dtype bf16 &&
+            run bench_mfx64 300 python bench.py --steps 3 --warmup 1 --frames 64 &&
+            run bench_mfx32 300 python bench.py --steps 3 --warmup 1 --frames 32 &&
+            run bench_2tb 600 python bench.py --config 2tb --steps 2 --warmup 1 &&
+            run bench_512k 600 python bench.py --config 512kx256k --steps 3 --warmup 1 ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
