@@ -60,7 +60,7 @@ def test_width_sweep_variant6_and_waste():
                                             (229376, 1, 7, 32, 8, True), (524288, 1, 8, 64, 4, False),
                                             (1048576, 1, 8, 128, 2, False), (301056, 1, 7, 42, 6, False),
                                             (147456, 1, 9, 16, 16, True), (73728, 1, 9, 8, 32, True),
-                                            (294912, 1, 9, 32, 8, True)])
+                                            (294912, 1, 9, 32, 8, True), (368640, 1, 9, 40, 6, False)])
 def test_production_geometries(ld, T, kw, J, I, xl):
     g = rtm.fused_geometry(ld, CUS, 6)
     assert (g.T, g.kw, g.J, g.I, g.xl) == (T, kw, J, I, xl)
