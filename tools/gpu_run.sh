@@ -237,6 +237,31 @@ for step in "$@"; do
             run bench_mfx32 300 python bench.py --steps 3 --warmup 1 --frames 32 &&
             run bench_2tb 600 python bench.py --config 2tb --steps 2 --warmup 1 &&
             run bench_512k 600 python bench.py --config 512kx256k --steps 3 --warmup 1 ;;
+    cw9) SART_FUSED_XL=0 run fcheck_cw9 300 python tools/fused_check.py 4096x368640 &&
+         for i in 1 2; do
+           for v in 368640 385024; do
+             timeout -k 10 200 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/cw9_on_${v}_$i.log" 2>&1 &&
+             SART_FUSED_KW9=0 timeout -k 10 200 python bench.py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/cw9_off_${v}_$i.log" 2>&1 || { echo "FATAL $v"; exit 1; }
+             echo "=== cw9 $v $i on $(grep -h '^{' "$OUT/cw9_on_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])') off $(grep -h '^{' "$OUT/cw9_off_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
+           done
+         done ;;
+    abkw8)  # 8-KiB T = 1 slabs across builds: HEAD / pre-flag4 (.abold) / round-3 start (.abr3s), same box, interleaved
+      for i in 1 2; do
+        for v in 262144 131072; do
+          for b in head old r3s; do
+            case $b in head) py=bench.py ;; old) py=.abold/bench.py ;; r3s) py=.abr3s/bench.py ;; esac
+            timeout -k 10 200 python $py --steps 3 --warmup 1 --nvox $v --no-selfcheck > "$OUT/k8_${b}_${v}_$i.log" 2>&1 || { echo "FATAL $b $v"; exit 1; }
+          done
+          echo "=== kw8 $v $i $(for b in head old r3s; do echo -n "$b "; grep -h '^{' "$OUT/k8_${b}_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], end=" ")'; done)" | tee -a "$OUT/session.log"
+        done
+      done ;;
+    mfnw)  # 64-frame bf16 kernels: 8 waves of half-size tiles (SART_MF_B16_NW=8) vs 4 waves
+      SART_MF_B16_NW=8 run pytest_mfnw 600 python -u -m pytest tests/test_gpu_multiframe_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread &&
+      for i in 1 2; do
+        timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck --frames 64 --rtm-dtype bf16 > "$OUT/nw4_$i.log" 2>&1 &&
+        SART_MF_B16_NW=8 timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck --frames 64 --rtm-dtype bf16 > "$OUT/nw8_$i.log" 2>&1 || { echo "FATAL nw"; exit 1; }
+        echo "=== mfnw $i nw4 $(grep -h '^{' "$OUT/nw4_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])') nw8 $(grep -h '^{' "$OUT/nw8_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+      done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
