@@ -262,6 +262,11 @@ for step in "$@"; do
         SART_MF_B16_NW=8 timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck --frames 64 --rtm-dtype bf16 > "$OUT/nw8_$i.log" 2>&1 || { echo "FATAL nw"; exit 1; }
         echo "=== mfnw $i nw4 $(grep -h '^{' "$OUT/nw4_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])') nw8 $(grep -h '^{' "$OUT/nw8_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
       done ;;
+    fwd2tb)  # forward split-K count at the 2tb preset shard (245760 x 262144, 64 frames split-A)
+      for kv in DEF=0 SART_MF_FWD_BLOCKS=2048 SART_MF_FWD_BLOCKS=4096 SART_MF_FWD_BLOCKS=8192; do
+        env "$kv" timeout -k 10 400 python bench.py --config 2tb --steps 1 --warmup 1 --no-selfcheck > "$OUT/f2tb_$kv.log" 2>&1 || { echo "FATAL $kv"; exit 1; }
+        echo "=== fwd2tb $kv $(grep -h '^{' "$OUT/f2tb_$kv.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+      done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
