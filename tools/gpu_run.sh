@@ -267,6 +267,14 @@ for step in "$@"; do
         env "$kv" timeout -k 10 400 python bench.py --config 2tb --steps 1 --warmup 1 --no-selfcheck > "$OUT/f2tb_$kv.log" 2>&1 || { echo "FATAL $kv"; exit 1; }
         echo "=== fwd2tb $kv $(grep -h '^{' "$OUT/f2tb_$kv.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
       done ;;
+    x3knobs)  # split-A 64-frame tile / depth knobs after the late staging
+      for i in 1 2; do
+        for kv in DEF=0 SART_MF_X3_VT=2 SART_MF_X3_DEPTH=3 "SART_MF_X3_VT=2 SART_MF_X3_DEPTH=3" SART_MF_X3_FWD=2,2,as SART_MF_X3_FWD=4,1,as SART_MF_X3_FWD=2,1 SART_MF_X3_FWD=2,2; do
+          tag=$(echo "$kv" | tr ' =,' '_-.')
+          env $kv timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck --frames 64 > "$OUT/x3k_${tag}_$i.log" 2>&1 || { echo "FATAL $kv"; exit 1; }
+          echo "=== x3k $tag $i $(grep -h '^{' "$OUT/x3k_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
