@@ -108,9 +108,45 @@ V6Candidate best_v6(int64_t ld, int num_cus, int rows_per_tile, bool narrow_slab
     return best;
 }
 
+// Wide bf16 tiles (16-byte loads of 8 bf16 per lane, x slab in LDS): T = 4 (schedule 4) or T = 2 (schedule 7), slab
+// 2048 kw / T columns of kw = 8 (16384 / T) or, so that J fills more of an XCD's 32 CUs, kw = 7 / 6 / 5 (kw 9 does
+// not fit the registers next to the wide tiles' two accumulator halves). XCD-local groups only. Cost as v6_candidate:
+// slab / G times the narrow-slab penalty; T = 4 and kw 8 first on ties. SART_BF16_KW=k keeps only k (A/B runs).
+V6Candidate bf16_wide_candidate(int64_t ld, int T, int kw, int num_cus) {
+    V6Candidate c;
+    if (const char* e = std::getenv("SART_BF16_KW"); e && *e && std::atoi(e) != kw) return c;
+    const int per_xcd = num_cus / 8;
+    const int64_t slab = 2048 * (int64_t)kw / T;
+    if (num_cus % 8 != 0 || ld % slab != 0) return c;
+    const int64_t J = ld / slab;
+    if (J < 1 || J > per_xcd) return c;
+    c.T = T, c.J = (int)J, c.kw = kw, c.xl = true;
+    c.I = 8 * (per_xcd / (int)J);
+    c.cost = (double)slab / (per_xcd / (int)J) * narrow_slab_penalty(kw);
+    return c;
+}
+
 }  // namespace
 
 int64_t choose_ld(int64_t nvoxel, double max_waste, bool narrow_slabs) {
+    if (!narrow_slabs && nvoxel >= 1024) {
+        // bf16 storage: the widths of the wide tiles first (the engine runs them wherever they are valid)
+        int64_t best_ld = 0;
+        double best_cost = 0.0;
+        for (const int kw : {8, 7, 6, 5})
+            for (const int T : {4, 2}) {
+                const int64_t slab = 2048 * (int64_t)kw / T;
+                const int64_t ld = (nvoxel + slab - 1) / slab * slab;
+                if ((double)(ld - nvoxel) > max_waste * (double)nvoxel) continue;
+                const V6Candidate c = bf16_wide_candidate(ld, T, kw, 256);
+                if (c.I == 0) continue;
+                if (best_ld == 0 || c.cost < best_cost || (c.cost == best_cost && ld < best_ld)) {
+                    best_ld = ld;
+                    best_cost = c.cost;
+                }
+            }
+        if (best_ld) return best_ld;
+    }
     // Widths the fused sweep (variant 6) can split into whole slabs: at each (T, kw) the smallest multiple of the
     // slab covering nvoxel. Take the one with the lowest time per row (ties: less padding, then the larger T and
     // kw, measured fastest at equal cost), if it pads by at most max_waste.
@@ -180,22 +216,17 @@ FusedGeometry fused_geometry(int64_t ld, int num_cus, int variant, int rows_per_
 
 FusedGeometry fused_geometry_bf16_wide(int64_t ld, int num_cus) {
     FusedGeometry g;
-    if (num_cus % 8 != 0) return g;
-    const int per_xcd = num_cus / 8;
-    // T = 4 (slab 4096, schedule 4) or T = 2 (slab 8192, schedule 6: 3-slot ring, lag 3); the lower cost
-    // slab / G wins, T = 4 on ties (the deeper lag measured faster at 64k x 64k)
-    int64_t best_cost = 0;
-    for (const int T : {4, 2}) {
-        const int64_t slab = 16384 / T;
-        if (ld % slab != 0) continue;
-        const int64_t J = ld / slab;
-        if (J < 1 || J > per_xcd) continue;
-        const int G = per_xcd / (int)J;
-        const int64_t cost = slab / G;
-        if (g.valid() && cost >= best_cost) continue;
-        best_cost = cost;
-        g.K = T, g.T = T, g.cpl = 8, g.J = (int)J, g.I = 8 * G, g.grid = g.I * g.J, g.variant = 6;
-    }
+    // T = 4 (schedule 4) or T = 2 (schedule 7: 3-slot ring, lag 4) at kw 8 ... 5 (bf16_wide_candidate); the lower
+    // cost slab / G wins, T = 4 and kw 8 on ties (the deeper lag measured faster at 64k x 64k)
+    double best_cost = 0.0;
+    for (const int kw : {8, 7, 6, 5})
+        for (const int T : {4, 2}) {
+            const V6Candidate c = bf16_wide_candidate(ld, T, kw, num_cus);
+            if (c.I == 0 || (g.valid() && c.cost >= best_cost)) continue;
+            best_cost = c.cost;
+            g.K = T, g.T = T, g.cpl = 8, g.J = c.J, g.I = c.I, g.grid = g.I * g.J, g.variant = 6, g.kw = kw;
+            g.xl = true;
+        }
     return g;
 }
 

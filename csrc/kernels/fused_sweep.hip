@@ -1206,22 +1206,32 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
 void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                              const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                              uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream, int cpl,
-                             int64_t chain_tiles) {
+                             int64_t chain_tiles, int kw) {
     if (T != 1 && T != 2 && T != 4) throw std::runtime_error("fused_sweep bf16: rows per tile must be 1, 2 or 4");
     if (cpl != 4 && !(cpl == 8 && (T == 4 || T == 2)))
         throw std::runtime_error("fused_sweep bf16: wide tiles need T = 4 or 2");
+    if (kw != 8 && !(cpl == 8 && kw >= 5 && kw <= 7))
+        throw std::runtime_error("fused_sweep bf16: kw 5 ... 7 only with wide tiles (narrow tiles: kw 8)");
     if (nrows_pad % 4 != 0) throw std::runtime_error("fused_sweep bf16: padded rows must be a multiple of 4");
     if (T >= 2 && chain_tiles % kChainAlign != 0)
         throw std::runtime_error("fused_sweep bf16: segment length must be a multiple of 140 tiles");
-    const int64_t slab = 2048 * cpl / T;
+    const int64_t slab = 256 * (int64_t)cpl * kw / T;  // 4 / T sub-slabs of 64 lanes x kw lane-vectors x cpl columns
     if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep bf16: ld must equal J * slab");
     if (J * 4 > kMaxGather || J * T > kRowsGather) throw std::runtime_error("fused_sweep bf16: too many slabs");
     if (xcnt == nullptr || I % 8 != 0) throw std::runtime_error("fused_sweep bf16: needs ticket counters and I % 8 == 0");
     const dim3 grid((unsigned)(I * J));
     auto go = [&](auto lg, auto tt, auto sc, auto cp) {
-        launch_rows_t<decltype(lg)::value, true, false, decltype(tt)::value, decltype(sc)::value, bf16_t,
-                      decltype(cp)::value>(grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran,
-                                           I, J, st, xcnt, chain_tiles);
+        constexpr int TT = decltype(tt)::value, SC = decltype(sc)::value, CP = decltype(cp)::value;
+        auto run = [&](auto k) {
+            launch_rows_t<decltype(lg)::value, true, false, TT, SC, bf16_t, CP, decltype(k)::value>(
+                grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt, chain_tiles);
+        };
+        if constexpr (CP == 8) {  // wide tiles: narrower slabs so that J fills an XCD's 32 CUs at more widths
+            if (kw == 7) return run(std::integral_constant<int, 7>{});
+            if (kw == 6) return run(std::integral_constant<int, 6>{});
+            if (kw == 5) return run(std::integral_constant<int, 5>{});
+        }
+        run(std::integral_constant<int, 8>{});
     };
     using S0 = std::integral_constant<int, 0>;
     using S4 = std::integral_constant<int, 4>;

@@ -94,11 +94,12 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
 constexpr int64_t kChainAlign = 140;  // lcm of the register-slot counts RS (4, 5, 7) of the T >= 2 pipelines
 bool fused_split_schedule(int T, bool bf16);
 // bf16-stored RTM: the variant 6 sweep with bf16 tiles (T = rows per tile of the variant 6 geometry; cpl = bf16
-// columns per lane per k-slot: 4 (8-byte loads, slab 8192 / T) or 8 (16-byte loads, slab 16384 / T, T = 4 only))
+// columns per lane per k-slot: 4 (8-byte loads, slab 8192 / T) or 8 (16-byte loads at T = 4 / 2, "wide": slab
+// 2048 kw / T with kw = 5 ... 8 lane-vectors per lane, 16384 / T at kw 8))
 void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                              const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                              uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream,
-                             int cpl = 4, int64_t chain_tiles = 0);
+                             int cpl = 4, int64_t chain_tiles = 0, int kw = 8);
 // p2p_allreduce.hip: one-shot push all-reduce through IPC-mapped peer buffers (at most 8 ranks, fp32).
 // Receive buffer of every rank: [2 parities][kP2pMaxRanks sources][cap] floats; flags: [sources][blocks].
 constexpr int kP2pMaxRanks = 8;

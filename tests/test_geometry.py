@@ -32,11 +32,12 @@ def test_every_width_gets_variant6(nvox):
     _check_v6(ld, rtm.fused_geometry(ld, CUS, 6))
     if nvox > 262144:
         return  # bf16 tiles: XCD-local row groups only (at most 32 slabs of 8192)
-    # bf16 shards keep the 8-KiB slabs (their tiles are 8 or 16 bytes of bf16 per lane)
+    # bf16 shards: the wide tiles (16 bytes of 8 bf16 per lane, T = 4 / 2, slab 2048 kw / T, kw 5 ... 8) at every
+    # width up to 32 slabs of 8192
     ldb = rtm.choose_ld(nvox, storage="bf16")
-    gb = rtm.fused_geometry(ldb, CUS, 6, narrow_slabs=False, chip_wide=False)
-    assert nvox <= ldb <= 1.10 * nvox and gb.kw == 8 and gb.xl
-    _check_v6(ldb, gb)
+    gw = hip().fused_geometry_bf16_wide(ldb, CUS)
+    assert nvox <= ldb <= 1.10 * nvox and gw.valid() and gw.cpl == 8 and gw.T in (2, 4) and 5 <= gw.kw <= 8
+    assert ldb == gw.J * 2048 * gw.kw // gw.T and gw.J <= CUS // 8 and gw.I == 8 * ((CUS // 8) // gw.J)
 
 
 def test_width_sweep_variant6_and_waste():
@@ -84,9 +85,8 @@ def test_xl_override(monkeypatch):
 def test_lowest_cost_rows_per_tile():
     # 70000 columns with 8-KiB slabs: T = 2 needs J = 18 (one group per XCD, 18 of 32 CUs); T = 1 gives J = 9
     # and three groups per XCD (27 CUs), a lower time per row. 7-KiB slabs: J = 10, three groups (30 CUs).
-    ld = rtm.choose_ld(70000, storage="bf16")
-    g = rtm.fused_geometry(ld, CUS, 6, narrow_slabs=False, chip_wide=False)
-    assert (ld, g.T, g.J, g.I) == (73728, 1, 9, 24)
+    g = rtm.fused_geometry(73728, CUS, 6, narrow_slabs=False, chip_wide=False)  # bf16 narrow tiles (kw 8)
+    assert (g.T, g.J, g.I) == (1, 9, 24)
     ld = rtm.choose_ld(70000)
     g = rtm.fused_geometry(ld, CUS, 6)
     # 7-KiB slabs at J = 10 (30 CUs per XCD) against 9-KiB slabs at ld 73728 (J = 8, all 32 CUs, 5 % padding):
@@ -98,7 +98,7 @@ def test_lowest_cost_rows_per_tile():
 def test_t2_penalty_prefers_t1():
     # 100000 columns: T = 2 at ld 102400 (J = 25, one group per XCD) against T = 1 at ld 106496 (J = 13, two
     # groups per XCD): equal slab / G, T = 2 measured slower per byte (profiles/probe_r2_t1_sched5.jsonl)
-    assert rtm.choose_ld(100000, storage="bf16") == 106496
+    assert rtm.fused_geometry(106496, CUS, 6, narrow_slabs=False, chip_wide=False).T == 1
     g2 = rtm.fused_geometry(131072, CUS, 6, 2)
     assert (g2.T, g2.J, g2.I) == (2, 32, 8)  # still available when forced
 
@@ -180,3 +180,17 @@ def test_kw5_opt_out(monkeypatch):
     monkeypatch.setenv("SART_FUSED_KW5", "0")
     g = rtm.fused_geometry(153600, CUS, 6)
     assert (g.kw, g.J, g.I) == (6, 25, 8)
+
+
+@pytest.mark.parametrize("nvox,ld,T,J,kw", [(65536, 65536, 4, 16, 8), (100000, 100352, 4, 28, 7),
+                                           (150000, 153600, 2, 30, 5), (200000, 200704, 2, 28, 7),
+                                           (262144, 262144, 2, 32, 8), (70000, 71680, 2, 10, 7)])
+def test_bf16_wide_kw(nvox, ld, T, J, kw, monkeypatch):
+    """Wide bf16 tiles take 7 / 6 / 5 lane-vectors per lane where 8-KiB-equivalent slabs leave CUs idle (150000
+    voxels: J = 30 instead of 19); SART_BF16_KW=8 keeps the 8-wide slabs."""
+    ldb = rtm.choose_ld(nvox, storage="bf16")
+    g = hip().fused_geometry_bf16_wide(ldb, CUS)
+    assert (ldb, g.T, g.J, g.kw) == (ld, T, J, kw)
+    monkeypatch.setenv("SART_BF16_KW", "8")
+    g8 = hip().fused_geometry_bf16_wide(rtm.choose_ld(nvox, storage="bf16"), CUS)
+    assert g8.kw == 8

@@ -275,6 +275,22 @@ for step in "$@"; do
           echo "=== x3k $tag $i $(grep -h '^{' "$OUT/x3k_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
         done
       done ;;
+    bf16w)  # bf16-stored shards at several widths (65536 rows)
+      for v in ${BW_LIST:-65536 73728 100000 131072 150000 200000 262144}; do
+        timeout -k 10 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --rtm-dtype bf16 --no-selfcheck > "$OUT/bw_$v.log" 2>&1 || { echo "FATAL $v"; tail -n 20 "$OUT/bw_$v.log"; exit 1; }
+        grep -h '^{' "$OUT/bw_$v.log" >> "$OUT/bf16_widths.jsonl"
+        echo "=== bf16w $v $(grep -h '^{' "$OUT/bw_$v.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"], d["fused_rows_per_tile"])')" | tee -a "$OUT/session.log"
+      done ;;
+    abbf16kw)  # wide bf16 tiles with kw 5-7 (default) vs kw 8 only (SART_BF16_KW=8)
+      run pytest_bf16kw 900 python -u -m pytest tests/test_gpu_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread &&
+      run fcheck_bf16kw 300 python tools/fused_check.py --dtype bf16 8192x150000 16384x100000 8192x200000 65536x163840 &&
+      for i in 1 2; do
+        for v in 150000 100000 200000 70000 163840 98304; do
+          timeout -k 10 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --rtm-dtype bf16 --no-selfcheck > "$OUT/bk_new_${v}_$i.log" 2>&1 &&
+          SART_BF16_KW=8 timeout -k 10 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --rtm-dtype bf16 --no-selfcheck > "$OUT/bk_old_${v}_$i.log" 2>&1 || { echo "FATAL $v"; exit 1; }
+          echo "=== bf16kw $v $i new $(grep -h '^{' "$OUT/bk_new_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"], d["fused_rows_per_tile"])') kw8 $(grep -h '^{' "$OUT/bk_old_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"], d["fused_rows_per_tile"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
