@@ -291,6 +291,15 @@ for step in "$@"; do
           echo "=== bf16kw $v $i new $(grep -h '^{' "$OUT/bk_new_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"], d["fused_rows_per_tile"])') kw8 $(grep -h '^{' "$OUT/bk_old_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"], d["fused_rows_per_tile"])')" | tee -a "$OUT/session.log"
         done
       done ;;
+    abbf16f4)  # 16-byte flag reads for wide bf16 T = 2 slabs of kw 5-7 (new) vs the one-by-one polls (.abold)
+      run pytest_bf16f4 600 python -u -m pytest tests/test_gpu_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread &&
+      for i in 1 2; do
+        for v in 150000 163840 200000 70000 262144; do
+          timeout -k 10 200 python .abold/bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --rtm-dtype bf16 --no-selfcheck > "$OUT/bf4_old_${v}_$i.log" 2>&1 &&
+          timeout -k 10 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --rtm-dtype bf16 --no-selfcheck > "$OUT/bf4_new_${v}_$i.log" 2>&1 || { echo "FATAL $v"; exit 1; }
+          echo "=== bf16f4 $v $i old $(grep -h '^{' "$OUT/bf4_old_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])') new $(grep -h '^{' "$OUT/bf4_new_${v}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], d["fused_grid"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
     benchcols) run bench_cols 600 python bench.py --steps 3 --warmup 1 --partition cols ;;
     benchbf16) run bench_bf16 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 &&
                run bench_bf16_log 600 python bench.py --steps 5 --warmup 1 --rtm-dtype bf16 --variant log ;;
