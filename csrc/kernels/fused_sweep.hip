@@ -465,8 +465,8 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     double* __restrict__ Fpart, uint64_t* __restrict__ gran, int I, int J, SartState* __restrict__ st, int dbg,
     unsigned* __restrict__ xcnt, int64_t chain_tiles) {
     static_assert(T == 1 || T == 2 || T == 4, "rows per tile");
-    // KW: lane-vectors per lane per row (8: one wave covers 2048 fp32 columns; 7 / 6 give slabs of 7 / 6 KiB
-    // columns, so widths whose 8-KiB slab count does not fit an XCD's 32 CUs still use most of them)
+    // KW: lane-vectors per lane per row (8: one wave covers 2048 fp32 columns; 9 / 7 / 6 / 5 give slabs of 9 ... 5 KiB
+    // columns, so widths whose 8-KiB slab count does not fit an XCD's 32 CUs still use most of them; 9 and 5 at T = 1)
     static_assert(KW >= 5 && KW <= 9, "lane-vectors per lane");
     static_assert(KW != 9 || (T == 1 && !BF_T<AT>()), "9-KiB slabs: fp32 T = 1 only (register and LDS budget)");
     constexpr int WPR = 4 / T;   // compute waves per row (each on its own 2048-column sub-slab)
@@ -510,9 +510,9 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     // measured no faster at 64k x 64k
     // wide bf16 tiles: 8 KB per wave like fp32, 5 slots (4 in flight + 1 held), accumulators 2 x 32 VGPRs
     // fp32 tiles with the x slab in VGPRs (T = 1): AH = RS tiles in flight, sized so that a wave keeps >= 32 KiB of A in
-    // flight at every slab width (kw 8: 4, 7: 5, 6: 6, 5: 7 tiles). With 4 tiles at every kw, narrow slabs streamed at
-    // the same ~0.88 us per step as kw 8 (loaded latency / tiles in flight), i.e. 23-28 GB/s per CU instead of ~30
-    // (Little's law; the exchange-off ablation at 147456 voxels ran only 5 % faster, profiles/ab_r3_t1_*.jsonl)
+    // flight at every slab width (kw 8: 4, 7: 5, 6: 6, 5: 7 tiles; kw 9: 3, the register limit). Against 4 tiles at every
+    // kw this measured +0.5-1.4 % (profiles/ab_r3_t1_ring_depth.jsonl): the narrow slabs' ~0.85 us step floor is the
+    // per-step hand-off chain, not loads in flight (see local_row_partial)
     constexpr int RS = XS_LDS ? ((BF && CPL == 4) ? 7 : 5) : (BF ? 7 : t1_reg_slots(KW));
     using FT = FusedTile<AT, CPL>;
     using RT = typename FT::R;
