@@ -131,6 +131,7 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
         cfg_.fault_inject = std::atoi(fi);
     if (const char* fn = std::getenv("SART_FAULT_NAN"); fn && *fn && cfg_.fault_nan_sweep < 0)
         cfg_.fault_nan_sweep = std::atoi(fn);
+    if (const char* t = std::getenv("SART_TAIL_FUSED"); t && *t) tail_fused_ = std::atoi(t) != 0;
 
     nsplit_ = backproject_num_splits(ld_, Pp_, cfg_.rtm_bf16 ? 2 : 4);
     comm_buf_.resize(ld_ + 64);  // [0, ld) correction, [ld] ||A x||^2
@@ -383,6 +384,11 @@ void Engine::sweep() {
         return;
     }
     unsigned* xcnt = (use_fused_ && geom_.variant == 6) ? xcnt_.get() : nullptr;  // zeroed by setup / update
+    const int nsplit = use_fused_ ? (int)fused_blocks_ : nsplit_;
+    const int64_t nF = use_fused_ ? nF_fused_ : forward_num_blocks(Pp_);
+    // One rank: the reduction of the partial rows, the decision and the update are one kernel (nothing to
+    // all-reduce in between); every workgroup sums the nF sweep partials, so only while nF stays small.
+    const bool one_tail = tail_fused_ && comm_->size() == 1 && nF <= 4096;
     if (use_fused_) {
         if (cfg_.rtm_bf16)  // variant 6, K = rows per tile
             launch_fused_sweep_bf16(cfg_.logarithmic, geom_.K, static_cast<const bf16_t*>(A_), ld_, P_, Pp_, x_.get(),
@@ -392,14 +398,13 @@ void Engine::sweep() {
             launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, static_cast<const float*>(A_), ld_, P_, Pp_,
                                x_.get(), ghat_.get(), arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I,
                                geom_.J, st, xcnt_.get(), stream_, chain_tiles_, geom_.kw, geom_.xl);
-        launch_reduce_partials(partial_.get(), ld_, (int)fused_blocks_, scale, comm_buf_.get(), Fpart_.get(), nF_fused_, Fslot,
-                               st, stream_);
     } else {
         fwd(cfg_.logarithmic ? kEpiLog : kEpiLinear, x_.get(), nullptr, w_.get(), Fpart_.get(), st);
         bwd(w_.get(), st);
-        launch_reduce_partials(partial_.get(), ld_, nsplit_, scale, comm_buf_.get(), Fpart_.get(),
-                               forward_num_blocks(Pp_), Fslot, st, stream_);
     }
+    if (!one_tail)
+        launch_reduce_partials(partial_.get(), ld_, nsplit, scale, comm_buf_.get(), Fpart_.get(), nF, Fslot, st,
+                               stream_);
     const float* pen = nullptr;
     if (has_lap_) {
         launch_penalty(cfg_.logarithmic, lap_rp_.get(), lap_col_.get(), lap_val_.get(), V_, (float)cfg_.beta_laplace,
@@ -411,8 +416,13 @@ void Engine::sweep() {
         comm_->all_reduce(comm_buf_.get(), (size_t)ld_ + 2, ReduceOp::kSum, stream_);
         comm_end();
     }
-    launch_decide_update(cfg_.logarithmic, st, Fslot, x_.get(), comm_buf_.get(), O_.get(), pen, (float)cfg_.relaxation,
-                         V_, xcnt, xprev_.get(), ticket_.get(), stream_);
+    if (one_tail)
+        launch_reduce_decide_update(cfg_.logarithmic, st, partial_.get(), ld_, nsplit, scale, Fpart_.get(), nF,
+                                    x_.get(), O_.get(), pen, (float)cfg_.relaxation, V_, xcnt, xprev_.get(),
+                                    ticket_.get(), stream_);
+    else
+        launch_decide_update(cfg_.logarithmic, st, Fslot, x_.get(), comm_buf_.get(), O_.get(), pen,
+                             (float)cfg_.relaxation, V_, xcnt, xprev_.get(), ticket_.get(), stream_);
     if (cfg_.fault_nan_sweep >= 0 && host_sweep_ == cfg_.fault_nan_sweep)  // fault injection (tests)
         hip_ok(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(x_.get()), 0x7fc00000, 1, stream_), "inject NaN");
     ++host_sweep_;

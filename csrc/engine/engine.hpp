@@ -219,6 +219,7 @@ class Engine {
     hipEvent_t ev_[2] = {nullptr, nullptr};
     hipGraphExec_t graph_ = nullptr;
     bool graph_failed_ = false;
+    bool tail_fused_ = true;  // one rank: reduce + decide + update in one kernel (SART_TAIL_FUSED=0: three)
     bool warm_ = false;  // an eager chunk ran with the current kernels
     int injected_ = 0;
     int host_sweep_ = 0;  // sweeps enqueued in the current solve (fault_nan_sweep)

@@ -46,6 +46,12 @@ void launch_decide(SartState* st, const float* Fslot, hipStream_t stream);
 void launch_decide_update(bool logmode, SartState* st, const float* Fslot, float* x, const float* d, const float* O,
                           const float* pen, float alpha, int64_t n, unsigned* xcnt, float* xprev, unsigned* ticket,
                           hipStream_t stream);
+// One rank: launch_reduce_partials (into registers, not d) + launch_decide_update in one kernel; x is bitwise the
+// two-launch x. nF: the Fpart partials every workgroup sums (keep it small, e.g. the fused sweep's grid).
+void launch_reduce_decide_update(bool logmode, SartState* st, const float* partial, int64_t ld, int nsplit,
+                                 const float* scale, const double* Fpart, int64_t nF, float* x, const float* O,
+                                 const float* pen, float alpha, int64_t n, unsigned* xcnt, float* xprev,
+                                 unsigned* ticket, hipStream_t stream);
 // xcnt (optional): fused-sweep ticket counters to zero for the next sweep; xprev (optional): receives x
 // before the update (rollback point of the NaN/Inf guard)
 void launch_update_linear(float* x, const float* d, const float* pen, int64_t n, const SartState* st,

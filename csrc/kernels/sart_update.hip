@@ -182,6 +182,64 @@ __global__ __launch_bounds__(256) void k_decide_update(SartState* __restrict__ s
     }
 }
 
+// One rank (nothing to all-reduce between the sweep and the update): k_reduce_partials and k_decide_update in ONE
+// launch, so a SART iteration is the sweep plus this kernel. Every workgroup sums the sweep's Fpart[0:nF] itself in
+// k_reduce_partials' order (nF is the sweep's grid, a few hundred doubles: L2 hits), evaluates the decision, sums
+// its voxels' partial rows in k_reduce_partials' order and applies k_decide_update's update. Contraction is off so
+// the correction is rounded before it is added, as when it went through memory: x is bitwise the three-kernel x.
+template <bool LOGV>
+__global__ __launch_bounds__(256) void k_reduce_decide_update(SartState* __restrict__ st,
+                                                              const float* __restrict__ partial, int64_t ld,
+                                                              int nsplit, const float* __restrict__ scale,
+                                                              const double* __restrict__ Fpart, int64_t nF,
+                                                              float* __restrict__ x, const float* __restrict__ O,
+                                                              const float* __restrict__ pen, float alpha, int64_t n,
+                                                              unsigned* __restrict__ xcnt, float* __restrict__ xprev,
+                                                              unsigned* __restrict__ ticket) {
+#pragma clang fp contract(off)
+    __shared__ double red[4];
+    __shared__ SartState s_next;
+    __shared__ int s_apply;
+    double acc = 0.0;
+    for (int64_t i = threadIdx.x; i < nF; i += 256) acc += Fpart[i];
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    if (xcnt && blockIdx.x == 0 && threadIdx.x < 16) xcnt[threadIdx.x] = 0u;  // see k_update_linear
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        SartState s = *st;
+        const float F[2] = {(float)(((red[0] + red[1]) + red[2]) + red[3]), (float)s.error};
+        decide_next(s, F);
+        s_next = s;
+        s_apply = !s.done;
+    }
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s_apply && i < n) {
+        float d = partial[i];
+        for (int k = 1; k < nsplit; ++k) d += partial[(int64_t)k * ld + i];
+        if (scale != nullptr) d *= scale[i];
+        const float x0 = x[i];
+        if (xprev) xprev[i] = x0;
+        if constexpr (LOGV) {
+            float r = powf((O[i] + kEpsLog) / (d + kEpsLog), alpha);
+            if (pen) r *= expf(-pen[i]);
+            x[i] = x0 * r;
+        } else {
+            float v = x0 + d;
+            if (pen) v -= pen[i];
+            x[i] = (v > 0.f) ? v : 0.f;
+        }
+    }
+    if (threadIdx.x == 0) {
+        const unsigned t = atomicAdd(ticket, 1u);  // after this workgroup's read of *st
+        if (t == gridDim.x - 1) {
+            *st = s_next;
+            *ticket = 0u;
+        }
+    }
+}
+
 // x = max(x + d - pen, 0)
 // xcnt (optional): the per-XCD ticket counters of the next fused sweep (variant 6), zeroed here so the
 // sweep loop needs no separate memset launch per iteration (the sweep that used them has completed).
@@ -359,6 +417,22 @@ void launch_decide_update(bool logmode, SartState* st, const float* Fslot, float
         hipLaunchKernelGGL(k_decide_update<false>, dim3(blocks), dim3(256), 0, stream, st, Fslot, x, d, O, pen, alpha,
                            n, xcnt, xprev, ticket);
     check_launch("k_decide_update");
+}
+
+void launch_reduce_decide_update(bool logmode, SartState* st, const float* partial, int64_t ld, int nsplit,
+                                 const float* scale, const double* Fpart, int64_t nF, float* x, const float* O,
+                                 const float* pen, float alpha, int64_t n, unsigned* xcnt, float* xprev,
+                                 unsigned* ticket, hipStream_t stream) {
+    if (n > ld || nsplit < 1 || nF < 0)
+        throw std::runtime_error("launch_reduce_decide_update: bad arguments (n > ld, nsplit < 1 or nF < 0)");
+    const unsigned blocks = nb(n > 0 ? n : 1);
+    if (logmode)
+        hipLaunchKernelGGL(k_reduce_decide_update<true>, dim3(blocks), dim3(256), 0, stream, st, partial, ld, nsplit,
+                           scale, Fpart, nF, x, O, pen, alpha, n, xcnt, xprev, ticket);
+    else
+        hipLaunchKernelGGL(k_reduce_decide_update<false>, dim3(blocks), dim3(256), 0, stream, st, partial, ld, nsplit,
+                           scale, Fpart, nF, x, O, pen, alpha, n, xcnt, xprev, ticket);
+    check_launch("k_reduce_decide_update");
 }
 
 void launch_update_linear(float* x, const float* d, const float* pen, int64_t n, const SartState* st,

@@ -102,6 +102,31 @@ def test_fused_is_deterministic(dev, problem):
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("log", [False, True])
+@pytest.mark.parametrize("lap", [False, True])
+def test_one_kernel_tail_is_bitwise(dev, monkeypatch, fused, log, lap):
+    """One rank: reduce + decide + update in one kernel (default) gives bitwise the x, iteration count and status
+    of the three-kernel tail (SART_TAIL_FUSED=0), including a convergence stop and the Laplacian penalty."""
+    from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+    from mpi_cuda_sartsolver_amd.utils.synthetic import host_problem
+
+    A, g, _ = host_problem(1024, 4096, seed=17)
+    L = LaplacianCSR.grid_3d(16, 16, 16, device=dev) if lap else None
+    out = []
+    for knob in ("0", "1"):
+        monkeypatch.setenv("SART_TAIL_FUSED", knob)
+        res = []
+        for tol in (0.0, 1e-4):
+            s = _solver(dev, A, fused, log=log, L=L, max_iterations=40, conv_tolerance=tol)
+            r = s.solve(g)
+            res.append((r.solution, r.iterations, r.status))
+        out.append(res)
+    for (xa, ia, sa), (xb, ib, sb) in zip(*out):
+        assert ia == ib and sa == sb
+        assert np.array_equal(xa, xb)
+
+
 @pytest.mark.parametrize("log", [False, True])
 def test_laplacian_and_warm_start(dev, log):
     from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
