@@ -107,6 +107,16 @@ double env_double(const char* name, double dflt) {
     return (e && *e) ? std::atof(e) : dflt;
 }
 
+}  // namespace
+
+void Communicator::reduce_all_reduce(const ReduceSrc& src, float* out, hipStream_t stream) {
+    launch_reduce_partials(src.partial, src.ld, src.nsplit, src.scale, out, src.Fpart, src.nF, out + src.ld, src.st,
+                           stream);
+    all_reduce(out, (size_t)src.ld + 2, ReduceOp::kSum, stream);
+}
+
+namespace {
+
 class P2pComm final : public Communicator {
    public:
     P2pComm(int device, std::shared_ptr<Communicator> base) : base_(std::move(base)), device_(device) {
@@ -121,6 +131,7 @@ class P2pComm final : public Communicator {
         // ranks first), so a P2P wait this long means the peer is gone or stuck: the engines then switch to the
         // base communicator and re-solve the frame (device_failed / degrade)
         timeout_s_ = env_double("SART_P2P_TIMEOUT_S", 60.0);
+        if (const char* f = std::getenv("SART_P2P_FUSED_REDUCE"); f && *f) fused_reduce_ = std::atoi(f) != 0;
         if (const char* f = std::getenv("SART_FAULT_P2P"); f && *f) {
             const char* fr = std::getenv("SART_FAULT_RANK");
             if (!(fr && *fr) || std::atoi(fr) == rank_) fault_call_ = std::atoll(f);
@@ -201,6 +212,15 @@ class P2pComm final : public Communicator {
     }
     void all_reduce(double* dev, size_t n, ReduceOp op, hipStream_t stream) override {
         base_->all_reduce(dev, n, op, stream);
+    }
+    void reduce_all_reduce(const ReduceSrc& src, float* out, hipStream_t stream) override {
+        // SART_P2P_FUSED_REDUCE=0: two launches (the A/B baseline); same fault injection as all_reduce
+        if (active_ && fused_reduce_ && src.ld + 2 <= max_n_) {
+            const bool skip = fault_call_ > 0 && ++calls_ >= fault_call_;
+            launch_p2p_reduce_allreduce(src, out, args_, rank_, n_, ++epoch_, cap_, err_, timeout_s_, stream, skip);
+        } else {
+            Communicator::reduce_all_reduce(src, out, stream);
+        }
     }
     bool graph_capturable() const override { return !active_ && base_->graph_capturable(); }  // epoch is an argument
     void abort() override {
@@ -399,6 +419,7 @@ class P2pComm final : public Communicator {
     P2pArgs args_{};
     unsigned* tail_[kP2pMaxRanks] = {};  // {err, abort} words of every rank as mapped here
     unsigned epoch_ = 0;
+    bool fused_reduce_ = true;  // reduce_all_reduce in one kernel
 };
 
 }  // namespace

@@ -21,6 +21,7 @@
 #include <memory>
 #include <string>
 
+#include "../kernels/launchers.hpp"
 #include "../native/host_comm.hpp"
 
 namespace sart {
@@ -33,6 +34,9 @@ class Communicator {
     // In-place reductions of device buffers, stream-ordered on `stream`.
     virtual void all_reduce(float* dev, size_t n, ReduceOp op, hipStream_t stream) = 0;
     virtual void all_reduce(double* dev, size_t n, ReduceOp op, hipStream_t stream) = 0;
+    // The single-frame engine's per-sweep collective: out[0, ld + 2) = the ReduceSrc vector (launchers.hpp), summed
+    // over the ranks. Default: launch_reduce_partials, then all_reduce; p2p: one kernel forms and pushes the vector.
+    virtual void reduce_all_reduce(const ReduceSrc& src, float* out, hipStream_t stream);
     // Device collectives may be captured into a HIP graph.
     virtual bool graph_capturable() const { return false; }
     // Tear down after a fatal error so that peers blocked in a collective fail instead of hanging.

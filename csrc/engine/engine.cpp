@@ -402,9 +402,6 @@ void Engine::sweep() {
         fwd(cfg_.logarithmic ? kEpiLog : kEpiLinear, x_.get(), nullptr, w_.get(), Fpart_.get(), st);
         bwd(w_.get(), st);
     }
-    if (!one_tail)
-        launch_reduce_partials(partial_.get(), ld_, nsplit, scale, comm_buf_.get(), Fpart_.get(), nF, Fslot, st,
-                               stream_);
     const float* pen = nullptr;
     if (has_lap_) {
         launch_penalty(cfg_.logarithmic, lap_rp_.get(), lap_col_.get(), lap_val_.get(), V_, (float)cfg_.beta_laplace,
@@ -412,9 +409,13 @@ void Engine::sweep() {
         pen = pen_.get();
     }
     if (comm_->size() > 1) {  // [0, ld) corrections, [ld] ||A x||^2, [ld + 1] error word: one collective
-        comm_begin();
-        comm_->all_reduce(comm_buf_.get(), (size_t)ld_ + 2, ReduceOp::kSum, stream_);
+        comm_begin();          // (p2p: formed from the partial rows and pushed by one kernel)
+        comm_->reduce_all_reduce(ReduceSrc{partial_.get(), ld_, nsplit, scale, Fpart_.get(), nF, st}, comm_buf_.get(),
+                                 stream_);
         comm_end();
+    } else if (!one_tail) {
+        launch_reduce_partials(partial_.get(), ld_, nsplit, scale, comm_buf_.get(), Fpart_.get(), nF, Fslot, st,
+                               stream_);
     }
     if (one_tail)
         launch_reduce_decide_update(cfg_.logarithmic, st, partial_.get(), ld_, nsplit, scale, Fpart_.get(), nF,

@@ -121,6 +121,23 @@ int64_t p2p_chunk(int64_t n);  // elements per workgroup
 void launch_p2p_allreduce(const float* in, float* out, int64_t n, const P2pArgs& a, int rank, int nranks,
                           unsigned epoch, int64_t cap, int op, unsigned* err, double timeout_s, hipStream_t stream,
                           bool skip_flags = false);
+// The per-sweep vector of the single-frame engine before its all-reduce, as launch_reduce_partials writes it:
+// v[i] = scale[i] * sum_s partial[s][i] for i < ld (scale nullptr: 1), v[ld] = sum Fpart[0:nF] (fp64 -> fp32),
+// v[ld + 1] = st->error (st nullptr: 0). partial: nsplit rows of ld floats, 16-byte aligned, ld % 64 == 0.
+struct ReduceSrc {
+    const float* partial = nullptr;
+    int64_t ld = 0;
+    int nsplit = 0;
+    const float* scale = nullptr;
+    const double* Fpart = nullptr;
+    int64_t nF = 0;
+    const SartState* st = nullptr;
+};
+// launch_reduce_partials + launch_p2p_allreduce (sum) of its ld + 2 floats in ONE kernel: each workgroup forms its
+// chunk of v in registers and pushes it. out (ld + 2 floats) receives the all-reduced v, bitwise the two-launch result.
+void launch_p2p_reduce_allreduce(const ReduceSrc& src, float* out, const P2pArgs& a, int rank, int nranks,
+                                 unsigned epoch, int64_t cap, unsigned* err, double timeout_s, hipStream_t stream,
+                                 bool skip_flags = false);
 // multiframe.hip (nf = frames per batch: 16, 32 or 64)
 int mf_forward_num_splits(int64_t ld, int64_t nrows_pad);
 int mf_backproject_num_splits(int64_t ld, int64_t nrows);

@@ -29,10 +29,12 @@ namespace {
 __device__ inline float red(float a, float b, int op) { return op == 0 ? a + b : fmaxf(a, b); }
 
 // `in` may alias `out` (in place): each element is read in phase 1 and written in phase 2 by one thread.
+// RED: there is no `in`; phase 1 forms the pushed values from src in k_reduce_partials' summation order (n = ld + 2).
+template <bool RED>
 __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* out, int64_t n, int64_t chunk,
                                                        P2pArgs a, int rank, int nranks, unsigned epoch, int parity,
                                                        int64_t cap, int op, unsigned* err, uint64_t timeout_ticks,
-                                                       int vec_io, int skip_flags) {
+                                                       int vec_io, int skip_flags, ReduceSrc src) {
     const int64_t c0 = (int64_t)blockIdx.x * chunk;
     const int64_t c1 = c0 + chunk < n ? c0 + chunk : n;
     // After a timeout on this rank the device path is being abandoned (the engines agree on it after the solve and
@@ -44,15 +46,59 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
     }
     const int64_t mine = (int64_t)(parity * kP2pMaxRanks + rank) * cap;  // my slot in every receive buffer
 
+    // RED: the chunk holding [ld] and [ld + 1] (never split: chunks are multiples of 1024, ld of 64) sums Fpart first
+    __shared__ float tailv[2];
+    if constexpr (RED) {
+        if (c0 <= src.ld && src.ld < c1) {  // uniform over the workgroup
+            __shared__ double red4[4];
+            double acc = 0.0;
+            for (int64_t i = threadIdx.x; i < src.nF; i += 256) acc += src.Fpart[i];
+            acc = wave_sum(acc);
+            if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = acc;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                tailv[0] = (float)(((red4[0] + red4[1]) + red4[2]) + red4[3]);
+                tailv[1] = src.st != nullptr ? (float)src.st->error : 0.f;
+            }
+            __syncthreads();
+        }
+    }
+    const int64_t ld4 = src.ld >> 2;
+
     // phase 1: push this chunk into slot [parity][rank] of every rank's receive buffer (self included)
     for (int64_t i = c0 + 4 * (int64_t)threadIdx.x; i < c1; i += 4 * (int64_t)blockDim.x) {
         if (i + 4 <= c1) {
-            const float4 v = vec_io ? *reinterpret_cast<const float4*>(in + i)
-                                    : make_float4(in[i], in[i + 1], in[i + 2], in[i + 3]);  // unaligned caller buffer
+            float4 v;
+            if constexpr (RED) {  // i + 4 <= ld here: only the chunk's tail [ld, ld + 2) is shorter than 4
+                const float4* __restrict__ p4 = reinterpret_cast<const float4*>(src.partial) + (i >> 2);
+                v = p4[0];
+                for (int k = 1; k < src.nsplit; ++k) {
+                    const float4 w = p4[(int64_t)k * ld4];
+                    v.x += w.x;
+                    v.y += w.y;
+                    v.z += w.z;
+                    v.w += w.w;
+                }
+                if (src.scale != nullptr) {
+                    const float4 sc = reinterpret_cast<const float4*>(src.scale)[i >> 2];
+                    v.x *= sc.x;
+                    v.y *= sc.y;
+                    v.z *= sc.z;
+                    v.w *= sc.w;
+                }
+            } else {
+                v = vec_io ? *reinterpret_cast<const float4*>(in + i)
+                           : make_float4(in[i], in[i + 1], in[i + 2], in[i + 3]);  // unaligned caller buffer
+            }
             for (int j = 0; j < nranks; ++j) *reinterpret_cast<float4*>(a.recv[j] + mine + i) = v;
         } else {
             for (int64_t k = i; k < c1; ++k) {
-                const float v = in[k];
+                float v;
+                if constexpr (RED) {
+                    v = k == src.ld ? tailv[0] : tailv[1];  // k >= ld: ld % 4 == 0 and n = ld + 2
+                } else {
+                    v = in[k];
+                }
                 for (int j = 0; j < nranks; ++j) a.recv[j][mine + k] = v;
             }
         }
@@ -138,9 +184,29 @@ void launch_p2p_allreduce(const float* in, float* out, int64_t n, const P2pArgs&
     const int64_t blocks = (n + chunk - 1) / chunk;
     if (blocks > kP2pMaxBlocks) throw std::runtime_error("launch_p2p_allreduce: too many chunks");
     const uint64_t ticks = (uint64_t)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
-    hipLaunchKernelGGL(k_p2p_allreduce, dim3((unsigned)blocks), dim3(256), 0, stream, in, out, n, chunk, a, rank,
-                       nranks, epoch, (int)(epoch & 1u), cap, op, err, ticks, vec_io, skip_flags ? 1 : 0);
+    hipLaunchKernelGGL(k_p2p_allreduce<false>, dim3((unsigned)blocks), dim3(256), 0, stream, in, out, n, chunk, a,
+                       rank, nranks, epoch, (int)(epoch & 1u), cap, op, err, ticks, vec_io, skip_flags ? 1 : 0,
+                       ReduceSrc{});
     check_launch("k_p2p_allreduce");
+}
+
+void launch_p2p_reduce_allreduce(const ReduceSrc& src, float* out, const P2pArgs& a, int rank, int nranks,
+                                 unsigned epoch, int64_t cap, unsigned* err, double timeout_s, hipStream_t stream,
+                                 bool skip_flags) {
+    const int64_t n = src.ld + 2;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src.partial) | reinterpret_cast<uintptr_t>(src.scale) |
+                           reinterpret_cast<uintptr_t>(out)) % 16) == 0;
+    if (nranks < 1 || nranks > kP2pMaxRanks || rank < 0 || rank >= nranks || n > cap || cap % 4 != 0 ||
+        src.ld <= 0 || src.ld % 64 != 0 || src.nsplit < 1 || src.nF < 0 || src.partial == nullptr || !aligned)
+        throw std::runtime_error("launch_p2p_reduce_allreduce: bad arguments (ld=" + std::to_string(src.ld) +
+                                 ", cap=" + std::to_string(cap) + ", ranks=" + std::to_string(nranks) + ")");
+    const int64_t chunk = p2p_chunk(n);
+    const int64_t blocks = (n + chunk - 1) / chunk;
+    if (blocks > kP2pMaxBlocks) throw std::runtime_error("launch_p2p_reduce_allreduce: too many chunks");
+    const uint64_t ticks = (uint64_t)(timeout_s * 1e8);
+    hipLaunchKernelGGL(k_p2p_allreduce<true>, dim3((unsigned)blocks), dim3(256), 0, stream, nullptr, out, n, chunk, a,
+                       rank, nranks, epoch, (int)(epoch & 1u), cap, 0, err, ticks, 1, skip_flags ? 1 : 0, src);
+    check_launch("k_p2p_reduce_allreduce");
 }
 
 }  // namespace sart

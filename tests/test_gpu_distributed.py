@@ -184,6 +184,21 @@ def test_fused_sweep_on_shared_gpu_two_ranks(tmp_path):
     assert max(e1, e2) <= RANK_FACTOR * e32 + 1e-7, (e1, e2, e32)
 
 
+@pytest.mark.parametrize("shape", [["--tol", "0"], FUSED_SHAPE, FUSED_SHAPE + ["--logarithmic"]])
+def test_p2p_fused_reduce_is_bitwise(tmp_path, shape):
+    """At N > 1 the P2P kernel forms the per-sweep vector from the partial rows itself (one launch instead of
+    k_reduce_partials + the all-reduce): x, status and iterations are bitwise those of the two-launch path
+    (SART_P2P_FUSED_REDUCE=0), on the two-pass and the fused sweep."""
+    env = dict(SART_P2P="1", SART_FUSED_SHARED="1")
+    xa, ma = _run(2, str(tmp_path / "a"), shape, SART_P2P_FUSED_REDUCE="0", **env)
+    xb, mb = _run(2, str(tmp_path / "b"), shape, SART_P2P_FUSED_REDUCE="1", **env)
+    for m in (ma, mb):
+        assert m[0]["comm"] == "p2p" and m[0]["x_bitwise_equal"]
+    for a, b in zip(ma, mb):
+        assert a["status"] == b["status"] and a["iterations"] == b["iterations"]
+    assert np.array_equal(xa, xb)
+
+
 @pytest.mark.parametrize("fused", [False, True])
 def test_p2p_timeout_degrades_to_base_on_every_rank(tmp_path, fused):
     """A P2P all-reduce that times out on some rank mid-solve (SART_FAULT_P2P: rank 1 never raises its flags in
