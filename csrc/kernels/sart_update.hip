@@ -15,6 +15,9 @@
 #include "sart_common.hpp"
 
 #include <math.h>
+
+#include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace sart {
@@ -187,7 +190,19 @@ __global__ __launch_bounds__(256) void k_decide_update(SartState* __restrict__ s
 // k_reduce_partials' order (nF is the sweep's grid, a few hundred doubles: L2 hits), evaluates the decision, sums
 // its voxels' partial rows in k_reduce_partials' order and applies k_decide_update's update. Contraction is off so
 // the correction is rounded before it is added, as when it went through memory: x is bitwise the three-kernel x.
-template <bool LOGV>
+template <int VEC>
+__device__ __forceinline__ void load_v(const float* __restrict__ p, float (&v)[VEC]) {
+    if constexpr (VEC == 4) {
+        const float4 t = *reinterpret_cast<const float4*>(p);
+        v[0] = t.x, v[1] = t.y, v[2] = t.z, v[3] = t.w;
+    } else {
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) v[c] = p[c];
+    }
+}
+
+// VEC consecutive voxels per thread (4: float4 accesses; every array is ld long, ld % 64 == 0, stores guarded by n).
+template <bool LOGV, int VEC>
 __global__ __launch_bounds__(256) void k_reduce_decide_update(SartState* __restrict__ st,
                                                               const float* __restrict__ partial, int64_t ld,
                                                               int nsplit, const float* __restrict__ scale,
@@ -200,6 +215,27 @@ __global__ __launch_bounds__(256) void k_reduce_decide_update(SartState* __restr
     __shared__ double red[4];
     __shared__ SartState s_next;
     __shared__ int s_apply;
+    // this thread's voxel operands first (independent of the decision; stale but finite once the frame is done),
+    // so their latency overlaps the Fpart reduction
+    const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * VEC;
+    const bool mine = i0 < n;
+    float d[VEC], x0[VEC], o[VEC], pn[VEC], t[VEC];
+    if (mine) {
+        load_v<VEC>(partial + i0, d);
+        for (int k = 1; k < nsplit; ++k) {
+            load_v<VEC>(partial + (int64_t)k * ld + i0, t);
+#pragma unroll
+            for (int c = 0; c < VEC; ++c) d[c] += t[c];
+        }
+        if (scale != nullptr) {
+            load_v<VEC>(scale + i0, t);
+#pragma unroll
+            for (int c = 0; c < VEC; ++c) d[c] *= t[c];
+        }
+        load_v<VEC>(x + i0, x0);
+        if constexpr (LOGV) load_v<VEC>(O + i0, o);
+        if (pen) load_v<VEC>(pen + i0, pn);
+    }
     double acc = 0.0;
     for (int64_t i = threadIdx.x; i < nF; i += 256) acc += Fpart[i];
     acc = wave_sum(acc);
@@ -214,26 +250,34 @@ __global__ __launch_bounds__(256) void k_reduce_decide_update(SartState* __restr
         s_apply = !s.done;
     }
     __syncthreads();
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (s_apply && i < n) {
-        float d = partial[i];
-        for (int k = 1; k < nsplit; ++k) d += partial[(int64_t)k * ld + i];
-        if (scale != nullptr) d *= scale[i];
-        const float x0 = x[i];
-        if (xprev) xprev[i] = x0;
-        if constexpr (LOGV) {
-            float r = powf((O[i] + kEpsLog) / (d + kEpsLog), alpha);
-            if (pen) r *= expf(-pen[i]);
-            x[i] = x0 * r;
+    if (s_apply && mine) {
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) {
+            float v;
+            if constexpr (LOGV) {
+                float r = powf((o[c] + kEpsLog) / (d[c] + kEpsLog), alpha);
+                if (pen) r *= expf(-pn[c]);
+                v = x0[c] * r;
+            } else {
+                v = x0[c] + d[c];
+                if (pen) v -= pn[c];
+                v = (v > 0.f) ? v : 0.f;
+            }
+            t[c] = v;
+        }
+        if (VEC == 4 && i0 + 4 <= n) {
+            if (xprev) *reinterpret_cast<float4*>(xprev + i0) = make_float4(x0[0], x0[1], x0[2], x0[3]);
+            *reinterpret_cast<float4*>(x + i0) = make_float4(t[0], t[1], t[2], t[3]);
         } else {
-            float v = x0 + d;
-            if (pen) v -= pen[i];
-            x[i] = (v > 0.f) ? v : 0.f;
+            for (int c = 0; c < VEC && i0 + c < n; ++c) {
+                if (xprev) xprev[i0 + c] = x0[c];
+                x[i0 + c] = t[c];
+            }
         }
     }
     if (threadIdx.x == 0) {
-        const unsigned t = atomicAdd(ticket, 1u);  // after this workgroup's read of *st
-        if (t == gridDim.x - 1) {
+        const unsigned tk = atomicAdd(ticket, 1u);  // after this workgroup's read of *st
+        if (tk == gridDim.x - 1) {
             *st = s_next;
             *ticket = 0u;
         }
@@ -425,13 +469,21 @@ void launch_reduce_decide_update(bool logmode, SartState* st, const float* parti
                                  unsigned* ticket, hipStream_t stream) {
     if (n > ld || nsplit < 1 || nF < 0)
         throw std::runtime_error("launch_reduce_decide_update: bad arguments (n > ld, nsplit < 1 or nF < 0)");
-    const unsigned blocks = nb(n > 0 ? n : 1);
-    if (logmode)
-        hipLaunchKernelGGL(k_reduce_decide_update<true>, dim3(blocks), dim3(256), 0, stream, st, partial, ld, nsplit,
-                           scale, Fpart, nF, x, O, pen, alpha, n, xcnt, xprev, ticket);
-    else
-        hipLaunchKernelGGL(k_reduce_decide_update<false>, dim3(blocks), dim3(256), 0, stream, st, partial, ld, nsplit,
-                           scale, Fpart, nF, x, O, pen, alpha, n, xcnt, xprev, ticket);
+    // SART_TAIL_VEC=1: one voxel per thread (A/B); default 4 (float4 accesses, a quarter of the workgroups)
+    static const int vec = [] {
+        const char* e = std::getenv("SART_TAIL_VEC");
+        return (e && *e && std::atoi(e) == 1) ? 1 : 4;
+    }();
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, (n + 256 * vec - 1) / (256 * vec));
+#define SART_RDU(L, V)                                                                                                 \
+    hipLaunchKernelGGL((k_reduce_decide_update<L, V>), dim3(blocks), dim3(256), 0, stream, st, partial, ld, nsplit,   \
+                       scale, Fpart, nF, x, O, pen, alpha, n, xcnt, xprev, ticket)
+    if (vec == 4) {
+        if (logmode) SART_RDU(true, 4); else SART_RDU(false, 4);
+    } else {
+        if (logmode) SART_RDU(true, 1); else SART_RDU(false, 1);
+    }
+#undef SART_RDU
     check_launch("k_reduce_decide_update");
 }
 
