@@ -188,31 +188,52 @@ __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const 
     __shared__ float dt[64][kMaxNF + 1];
     __shared__ float ot[64][kMaxNF + 1];
     if (st->all_done) return;
-    const int nf = st->nf;
-    const int64_t v0 = (int64_t)blockIdx.x * 64;
-    for (int e = threadIdx.x; e < 64 * nf; e += 256) {
-        const int64_t v = v0 + e / nf;
-        const int f = e % nf;
-        dt[e / nf][f] = v < ld ? D[v * nf + f] : 0.f;
-        if (logmode) ot[e / nf][f] = v < ld ? O[v * nf + f] : 0.f;
+    const int nf = st->nf;  // 16, 32 or 64: four consecutive e of a voxel-major row share one voxel
+    const int64_t v0 = (int64_t)blockIdx.x * 64;  // v0 + 63 < ld (ld % 64 == 0, grid ld / 64)
+    // float4 accesses throughout (D, O: the block's 64 nf contiguous floats; X, Xprev, pen: 4 voxels of one frame)
+    const float4* D4 = reinterpret_cast<const float4*>(D + v0 * nf);
+    const float4* O4 = logmode ? reinterpret_cast<const float4*>(O + v0 * nf) : nullptr;
+    for (int e4 = threadIdx.x; e4 < 16 * nf; e4 += 256) {
+        const int r = (4 * e4) / nf, c = (4 * e4) % nf;
+        const float4 d = D4[e4];
+        dt[r][c] = d.x, dt[r][c + 1] = d.y, dt[r][c + 2] = d.z, dt[r][c + 3] = d.w;
+        if (logmode) {
+            const float4 o = O4[e4];
+            ot[r][c] = o.x, ot[r][c + 1] = o.y, ot[r][c + 2] = o.z, ot[r][c + 3] = o.w;
+        }
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < 64 * nf; e += 256) {
-        const int f = e / 64, vv = e % 64;
-        const int64_t v = v0 + vv;
+    for (int e4 = threadIdx.x; e4 < 16 * nf; e4 += 256) {
+        const int f = e4 / 16, vq = 4 * (e4 % 16);
+        const int64_t v = v0 + vq;
         if (v >= nvox || st->done[f]) continue;
         const int64_t i = (int64_t)f * ld + v;
-        const float p = pen ? pen[i] : 0.f;
-        const float x0 = X[i];
-        if (Xprev) Xprev[i] = x0;
-        if (logmode) {
-            const float eps = 1e-7f;  // reference EPSILON_LOG_CUDA (sart_kernels.cu:17-19)
-            float r = powf((ot[vv][f] + eps) / (dt[vv][f] + eps), alpha);
-            if (pen) r *= expf(-p);
-            X[i] = x0 * r;
+        const int m = nvox - v < 4 ? (int)(nvox - v) : 4;  // voxels of this quad inside the shard
+        const float4 x4 = *reinterpret_cast<const float4*>(X + i);
+        const float4 p4 = pen ? *reinterpret_cast<const float4*>(pen + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float xs[4] = {x4.x, x4.y, x4.z, x4.w}, ps[4] = {p4.x, p4.y, p4.z, p4.w};
+        float out[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float x0 = xs[k], p = ps[k];
+            if (logmode) {
+                const float eps = 1e-7f;  // reference EPSILON_LOG_CUDA (sart_kernels.cu:17-19)
+                float r = powf((ot[vq + k][f] + eps) / (dt[vq + k][f] + eps), alpha);
+                if (pen) r *= expf(-p);
+                out[k] = x0 * r;
+            } else {
+                const float x = x0 + dt[vq + k][f] - p;
+                out[k] = x > 0.f ? x : 0.f;
+            }
+        }
+        if (m == 4) {
+            if (Xprev) *reinterpret_cast<float4*>(Xprev + i) = x4;
+            *reinterpret_cast<float4*>(X + i) = make_float4(out[0], out[1], out[2], out[3]);
         } else {
-            const float x = x0 + dt[vv][f] - p;
-            X[i] = x > 0.f ? x : 0.f;
+            for (int k = 0; k < m; ++k) {
+                if (Xprev) Xprev[i + k] = xs[k];
+                X[i + k] = out[k];
+            }
         }
     }
 }
