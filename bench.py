@@ -198,6 +198,13 @@ def main() -> int:
                 # RCCL refuses two ranks on one device: gloo host collectives under the one-shot P2P all-reduce
                 # (auto-selected against the staged base), and the fused sweep on each rank's share of the CUs
                 env_extra.update(SART_DIST_BACKEND="gloo", SART_P2P_WRAP_STAGED="1", SART_FUSED_SHARED="1")
+                # Hardware queues: the GPU maps 24 compute queues (KFD num_cp_queues); 8 ranks x HIP's default 4 = 32
+                # over-subscribe it and the scheduler time-slices the processes, so every P2P all-reduce waits out a
+                # time slice for a descheduled peer (10.3 ms per call, 83.7 it/s; with 1 queue per rank 111 us,
+                # 172.4 it/s: profiles/bench_r4_n8_rehearsal_one_gpu_q{4,1}.json). One rank per GPU is unaffected.
+                per_gpu = -(-args.gpus // max(ndev, 1))
+                if "GPU_MAX_HW_QUEUES" not in os.environ:
+                    env_extra["GPU_MAX_HW_QUEUES"] = str(max(1, min(4, 12 // per_gpu)))
         return self_launch(args.gpus, sys.argv[1:], env_extra)
     if (world or 1) != args.gpus:
         print(f"bench: --gpus {args.gpus} but the launcher started {world or 1} rank(s)", file=sys.stderr)
@@ -286,8 +293,19 @@ def main() -> int:
         runner = solver
     multi = args.frames > 1
     startup = {"setup_s": round(time.perf_counter() - t_setup, 2)}  # process group, shard, engine, comm self-tests
+    if n > 1:  # of which the device communicator's own start-up (p2p: IPC mapping, self-test, size probes)
+        startup["comm_setup_s"] = round(float(solver.native_comm.setup_seconds), 2)
     wd.kick("setup")
 
+    class _Counts:  # recoveries over the WHOLE run (self-check, warm-up and timed steps), not the timed steps only
+        def __init__(self):
+            self.comm = self.fused = 0
+
+        def add(self, r):
+            self.comm += int(getattr(r, "comm_fallbacks", 0))
+            self.fused += int(getattr(r, "fallbacks", 0))
+
+    counts = _Counts()
     selfcheck = None
     if not multi and solver.use_fused and not args.no_selfcheck:
         # Untimed: ONE iteration from the cold start (x1 = x0 + d(x0): every part of the sweep runs once) with
@@ -303,8 +321,11 @@ def main() -> int:
         p1 = SolverParams(max_iterations=1, conv_tolerance=0.0)
         kw = dict(logarithmic=args.variant == "log", allow_zero_tolerance=True, partition=args.partition)
         gh = g.cpu().numpy() if hasattr(g, "cpu") else np.asarray(g)
-        xf = SARTSolver(prob.rtm, None, comm, p1, use_fused=True, **kw).solve(gh).solution
-        x2 = SARTSolver(prob.rtm, None, comm, p1, use_fused=False, **kw).solve(gh).solution
+        rf = SARTSolver(prob.rtm, None, comm, p1, use_fused=True, **kw).solve(gh)
+        r2 = SARTSolver(prob.rtm, None, comm, p1, use_fused=False, **kw).solve(gh)
+        counts.add(rf)
+        counts.add(r2)
+        xf, x2 = rf.solution, r2.solution
         x64 = sart_oracle_f64(prob.rtm, gh, 1, logarithmic=args.variant == "log", comm=comm)
         nrm = max(float(np.linalg.norm(x64)), 1e-300)
         ef = comm.all_reduce_scalar(float(np.linalg.norm(xf - x64)) / nrm, op="max")
@@ -319,7 +340,7 @@ def main() -> int:
         wd.kick("selfcheck")
 
     for i in range(args.warmup):
-        runner.solve(g)
+        counts.add(runner.solve(g))
         wd.kick(f"warmup {i}")
     torch.cuda.synchronize()
     comm.barrier()
@@ -334,6 +355,7 @@ def main() -> int:
         iters += res.iterations
         comm_ms += max(getattr(res, "comm_ms", -1.0), 0.0)
         comm_fallbacks += int(getattr(res, "comm_fallbacks", 0))
+        counts.add(res)
         wd.kick(f"step {i}")
     torch.cuda.synchronize()
     comm.barrier()
@@ -370,7 +392,9 @@ def main() -> int:
         "fused_sweep": use_fused,
         "fused_variant": solver.geom.variant if use_fused else None,
         "fused_rows_per_tile": solver.geom.T if use_fused else None,
-        "fused_schedule": solver.k.fused_get_schedule() if use_fused else None,
+        # the pipeline schedule the sweep kernel actually ran (T, kw and chip-wide groups pick it; the global knob
+        # fused_get_schedule() is only the default), recorded by the launcher of the last sweep
+        "fused_schedule": solver.k.fused_last_schedule() if use_fused else None,
         "fused_grid": ({"J": solver.geom.J, "I": solver.geom.I, "workgroups": solver.geom.grid,
                         "ld": solver.ld, "kw": solver.geom.kw, "xcd_local": solver.geom.xl} if use_fused else None),
         "selfcheck": selfcheck,
@@ -380,7 +404,11 @@ def main() -> int:
         "frames_per_step": args.frames,
         # per-iteration device all-reduce: RCCL, or the one-shot P2P kernel when it beat RCCL at start-up
         "allreduce": (solver.native_comm.describe if n > 1 else "none (1 rank)"),
-        "allreduce_fallbacks": comm_fallbacks,  # timed steps re-solved after a device all-reduce timeout
+        # frames re-solved after a device all-reduce timeout / a persistent-sweep timeout, over the whole run
+        # (self-check + warm-up + timed steps) and within the timed steps alone
+        "allreduce_fallbacks": counts.comm,
+        "allreduce_fallbacks_timed": comm_fallbacks,
+        "fused_fallbacks": counts.fused,
         # rank 0's GPU time inside the all-reduces per SART iteration (includes waiting for slower ranks)
         "allreduce_us_per_iter": (round(1e3 * comm_ms / max(iters, 1), 2) if n > 1 and not multi else None),
         "effective_hbm_TBps_per_gpu": round(bytes_per_iter * iters_per_s / 1e12, 3),

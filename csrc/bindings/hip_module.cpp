@@ -56,6 +56,8 @@ static void bind_engine(py::module_& m) {
         .def_property_readonly("size", [](sart::Communicator& c) { return c.size(); })
         .def_property_readonly("backend", &sart::Communicator::backend)
         .def_property_readonly("describe", &sart::Communicator::describe)
+        .def_property_readonly("setup_seconds", &sart::Communicator::setup_seconds)
+        .def("prepare", &sart::Communicator::prepare, py::arg("float_sizes"), py::call_guard<py::gil_scoped_release>())
         .def("check", &sart::Communicator::check)
         .def("device_failed", &sart::Communicator::device_failed)
         .def_property_readonly("degradable", &sart::Communicator::degradable)
@@ -408,6 +410,7 @@ PYBIND11_MODULE(_sart_hip, m) {
     m.def("fused_tile_rows", &sart::fused_tile_rows);
     m.def("fused_set_schedule", &sart::fused_set_schedule);
     m.def("fused_get_schedule", &sart::fused_get_schedule);
+    m.def("fused_last_schedule", &sart::fused_last_schedule);
     m.def("fused_debug_map", &sart::fused_debug_map);
     m.def("fused_set_trace", [](uintptr_t buf, long long tiles) {
         sart::fused_set_trace(reinterpret_cast<unsigned long long*>(buf), tiles);

@@ -127,6 +127,7 @@ PYBIND11_MODULE(_sart_native, m) {
         .def(py::init<SortedRtmFiles, std::string, uint64_t, uint64_t, uint64_t>(), py::arg("sorted_files"),
              py::arg("rtm_name"), py::arg("nvoxel"), py::arg("col_begin") = 0, py::arg("col_end") = 0)
         .def_property_readonly("ncols", &RtmReader::ncols)
+        .def("set_rows_per_read", &RtmReader::set_rows_per_read, py::arg("rows"))
         .def(
             "read_ptr",
             [](RtmReader& r, uint64_t r0, uint64_t r1, uintptr_t ptr, uint64_t ld) {
@@ -203,6 +204,29 @@ PYBIND11_MODULE(_sart_native, m) {
     m.def("read_solution_file", [](const std::string& fn) {
         StoredSolutions s = read_solution_file(fn);
         return py::make_tuple(arr(s.time), arr(s.last_solution), arr(s.status));
+    });
+    // any numeric dataset as float64 with its shape (tests: every frame of solution/value, solution/iterations)
+    m.def("read_dataset_f64", [](const std::string& fn, const std::string& name) {
+#ifdef SART_HAVE_HDF5
+        std::vector<double> v;
+        std::vector<hsize_t> dims;
+        {
+            SART_H5_LOCK;
+            H5Id f = h5_open_file(fn);
+            v = h5_read_f64(f, name);
+            H5Id d = h5_open_dataset(f, name);
+            dims = h5_dims(d);
+        }
+        std::vector<py::ssize_t> shape(dims.begin(), dims.end());
+        py::array_t<double> out(shape);
+        std::copy(v.begin(), v.end(), out.mutable_data());
+        return out;
+#else
+        (void)fn;
+        (void)name;
+        throw Error("built without HDF5 support");
+        return py::array_t<double>();
+#endif
     });
 
     py::class_<VoxelGrid>(m, "VoxelGrid")
@@ -325,6 +349,21 @@ PYBIND11_MODULE(_sart_native, m) {
             write_image_file(path, camera, wavelength, vec(time), vec(frames), fb.shape[1], fb.shape[2]);
         },
         py::arg("path"), py::arg("camera_name"), py::arg("wavelength"), py::arg("time"), py::arg("frames"));
+    m.def(
+        "write_synthetic_rtm_file",
+        [](std::string path, std::string camera, double wavelength, uint64_t h, uint64_t w, uint64_t nvoxel,
+           uint64_t seed, uint64_t nnz_per_row, bool drop_cache, uint64_t block_bytes, std::string rtm_name) {
+            py::gil_scoped_release nogil;
+            return write_synthetic_rtm_file(path, camera, wavelength, h, w, nvoxel, seed, nnz_per_row, drop_cache,
+                                            block_bytes, rtm_name);
+        },
+        py::arg("path"), py::arg("camera_name"), py::arg("wavelength"), py::arg("h"), py::arg("w"), py::arg("nvoxel"),
+        py::arg("seed") = 0, py::arg("nnz_per_row") = 0, py::arg("drop_cache") = false,
+        py::arg("block_bytes") = (uint64_t)256 << 20, py::arg("rtm_name") = "with_reflections");
+    m.def("synthetic_rtm_value", &synthetic_rtm_value, py::arg("seed"), py::arg("p"), py::arg("v"));
+    m.def("synthetic_rtm_voxel", &synthetic_rtm_voxel, py::arg("p"), py::arg("k"), py::arg("nnz_per_row"),
+          py::arg("nvoxel"));
+    m.def("drop_file_cache", &drop_file_cache, py::arg("path"));
     m.def(
         "write_laplacian_file",
         [](std::string path, uint64_t nvoxel, u64arr i, u64arr j, f32arr v) {

@@ -31,7 +31,12 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <sys/prctl.h>
 #include <sys/stat.h>
+#include <unistd.h>
+
+#include <csignal>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -73,9 +78,35 @@ struct DeviceShard {
     }
 };
 
+// Load-path observability (--profile's first line): wall time of the whole load, the summed HDF5 read time of the
+// reader, the summed GPU time of the host -> HBM copies, the time the copy loop waited for a read (read-bound) and for
+// a staging buffer to drain (copy-bound), and the resident-set high-water mark before / after (the loader's own host
+// memory is the two pinned staging blocks). With the double buffer working, wall ~ max(read, h2d) + one block.
+struct LoadStats {
+    double wall_s = 0, read_s = 0, h2d_s = 0, wait_read_s = 0, wait_copy_s = 0;
+    uint64_t bytes = 0, blocks = 0, rows_per_block = 0, staging_bytes = 0, rows_per_read = 0;
+    double rss_hwm_before_mb = 0, rss_hwm_after_mb = 0;
+};
+
+double rss_hwm_mb() {  // VmHWM of this process, MiB (0 where /proc is unavailable)
+    std::ifstream f("/proc/self/status");
+    std::string line;
+    while (std::getline(f, line))
+        if (line.rfind("VmHWM:", 0) == 0) return std::atof(line.c_str() + 6) / 1024.0;
+    return 0.0;
+}
+
+double seconds_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 // col0 / ncols: only that voxel block of every row (--partition_voxels), read as a column hyperslab.
 std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0, uint64_t nrows, size_t block_bytes,
-                                               uint64_t col0 = 0, uint64_t ncols = 0, bool bf16 = false) {
+                                               uint64_t col0 = 0, uint64_t ncols = 0, bool bf16 = false,
+                                               LoadStats* stats = nullptr) {
+    LoadStats ls;
+    ls.rss_hwm_before_mb = rss_hwm_mb();
+    const auto t_load = std::chrono::steady_clock::now();
     auto sh = std::make_unique<DeviceShard>();
     sh->bf16 = bf16;
     if (ncols == 0) ncols = in.nvoxel - col0;
@@ -89,7 +120,13 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
     hip_ok(hipDeviceSynchronize(), "hipMemset sync");
     const uint64_t V = ncols;  // staging row length: the column window only
     RtmReader reader(in.rtm_files, in.rtm_name, in.nvoxel, col0, col0 + ncols);
+    if (const char* e = std::getenv("SART_RTM_ROWS_PER_READ"); e && *e) {
+        ls.rows_per_read = (uint64_t)std::max(0ll, std::atoll(e));
+        reader.set_rows_per_read(ls.rows_per_read);
+    }
     const uint64_t rows_per_block = std::max<uint64_t>(1, std::min<uint64_t>(nrows, block_bytes / (4 * V)));
+    ls.rows_per_block = rows_per_block;
+    ls.staging_bytes = 2 * rows_per_block * V * sizeof(float);
     float* buf[2] = {nullptr, nullptr};
     for (auto& b : buf) hip_ok(hipHostMalloc(reinterpret_cast<void**>(&b), rows_per_block * V * sizeof(float)), "hipHostMalloc");
     // bf16: fp32 staging rows [rows_per_block x ld], padding columns zero (the 2-D copies write ncols only)
@@ -100,42 +137,74 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
     hipEvent_t ev[2];
     for (auto& e : ev) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     bool ev_used[2] = {false, false};
-    auto read_into = [&](float* b, uint64_t r0, uint64_t r1) {
-        std::memset(b, 0, (r1 - r0) * V * sizeof(float));  // sparse COO rows are scattered into zeros
-        reader.read(row0 + r0, row0 + r1, b, V);  // one reader: sparse arrays are read once per shard
-    };
     std::vector<std::pair<uint64_t, uint64_t>> blocks;
     for (uint64_t r = 0; r < nrows; r += rows_per_block) blocks.emplace_back(r, std::min(nrows, r + rows_per_block));
+    // timing events around every block copy (GPU time of the H2D traffic)
+    std::vector<hipEvent_t> tev(2 * blocks.size(), nullptr);
+    for (auto& e : tev) hip_ok(hipEventCreate(&e), "hipEventCreate");
+    std::vector<double> read_s(blocks.size(), 0.0);  // one slot per block: written by whichever thread reads it
+    auto read_into = [&](size_t k, float* b) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const uint64_t r0 = blocks[k].first, r1 = blocks[k].second;
+        std::memset(b, 0, (r1 - r0) * V * sizeof(float));  // sparse COO rows are scattered into zeros
+        reader.read(row0 + r0, row0 + r1, b, V);  // one reader: sparse arrays are read once per shard
+        read_s[k] = seconds_since(t0);
+    };
+    auto release = [&]() {
+        for (auto& e : tev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& e : ev) (void)hipEventDestroy(e);
+        (void)hipStreamDestroy(s);
+        for (auto& b : buf) (void)hipHostFree(b);
+    };
     try {
-        if (!blocks.empty()) read_into(buf[0], blocks[0].first, blocks[0].second);
+        if (!blocks.empty()) read_into(0, buf[0]);
         for (size_t k = 0; k < blocks.size(); ++k) {
             float* cur = buf[k % 2];
             std::future<void> next;
             if (k + 1 < blocks.size()) {
                 const int nb = (k + 1) % 2;
-                if (ev_used[nb]) hip_ok(hipEventSynchronize(ev[nb]), "event sync");
-                next = std::async(std::launch::async, read_into, buf[nb], blocks[k + 1].first, blocks[k + 1].second);
+                if (ev_used[nb]) {  // the staging buffer of block k + 1 still feeds the copy of block k - 1
+                    const auto tw = std::chrono::steady_clock::now();
+                    hip_ok(hipEventSynchronize(ev[nb]), "event sync");
+                    ls.wait_copy_s += seconds_since(tw);
+                }
+                next = std::async(std::launch::async, read_into, k + 1, buf[nb]);
             }
             const uint64_t r0 = blocks[k].first, nr = blocks[k].second - blocks[k].first;
             float* dst = bf16 ? stage.get() : static_cast<float*>(sh->A) + r0 * sh->ld;
+            hip_ok(hipEventRecord(tev[2 * k], s), "event");
             hip_ok(hipMemcpy2DAsync(dst, sh->ld * sizeof(float), cur, V * sizeof(float), ncols * sizeof(float), nr,
                                     hipMemcpyHostToDevice, s),
                    "H2D RTM block");
+            hip_ok(hipEventRecord(tev[2 * k + 1], s), "event");
             if (bf16)  // stream-ordered: the next block's copy into the staging rows waits for this conversion
                 launch_f32_to_bf16(stage.get(), (int64_t)nr * sh->ld, static_cast<bf16_t*>(sh->A) + r0 * sh->ld, s);
             hip_ok(hipEventRecord(ev[k % 2], s), "event");
             ev_used[k % 2] = true;
-            if (next.valid()) next.get();
+            if (next.valid()) {
+                const auto tw = std::chrono::steady_clock::now();
+                next.get();
+                ls.wait_read_s += seconds_since(tw);
+            }
         }
         hip_ok(hipStreamSynchronize(s), "RTM upload");
     } catch (...) {
         (void)hipStreamSynchronize(s);
-        for (auto& b : buf) (void)hipHostFree(b);
+        release();
         throw;
     }
-    for (auto& e : ev) (void)hipEventDestroy(e);
-    (void)hipStreamDestroy(s);
-    for (auto& b : buf) (void)hipHostFree(b);
+    for (size_t k = 0; k < blocks.size(); ++k) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, tev[2 * k], tev[2 * k + 1]) == hipSuccess) ls.h2d_s += 1e-3 * ms;
+        ls.read_s += read_s[k];
+    }
+    release();
+    ls.blocks = blocks.size();
+    ls.bytes = nrows * V * sizeof(float);
+    ls.wall_s = seconds_since(t_load);
+    ls.rss_hwm_after_mb = rss_hwm_mb();
+    if (stats) *stats = ls;
     return sh;
 }
 
@@ -148,6 +217,13 @@ std::string json_escape(const std::string& s) {
 }  // namespace
 
 int main(int argc, char** argv) {
+    // Started by the Python entry point (cli.py sets SART_PARENT_PID): die with it. cli.py forwards SIGTERM /
+    // SIGINT / SIGHUP itself; this covers a parent killed with SIGKILL, so no orphan keeps the GPU or sits in a
+    // collective. A parent that is already gone (a race with the prctl) ends the driver at once.
+    if (const char* pp = std::getenv("SART_PARENT_PID"); pp && *pp) {
+        (void)::prctl(PR_SET_PDEATHSIG, SIGTERM);
+        if ((long)::getppid() != std::atol(pp)) return 1;
+    }
     std::vector<std::string> args(argv + 1, argv + argc);
     Config cfg;
     std::vector<std::array<double, 4>> intervals;
@@ -219,10 +295,14 @@ int main(int argc, char** argv) {
 
         std::unique_ptr<DeviceShard> dshard;
         std::vector<float> hshard;
+        LoadStats lstats;
+        size_t block_bytes = (size_t)256 << 20;  // per staging buffer (two of them)
+        if (const char* e = std::getenv("SART_RTM_BLOCK_MB"); e && *e)
+            block_bytes = (size_t)std::max(1.0, std::atof(e) * 1048576.0);
         auto load = [&]() {
             if (gpu)
-                dshard = load_device_shard(in, blk.offset, blk.size, (size_t)256 << 20, vblk.offset, vblk.size,
-                                           cfg.rtm_bf16);
+                dshard = load_device_shard(in, blk.offset, blk.size, block_bytes, vblk.offset, vblk.size,
+                                           cfg.rtm_bf16, &lstats);
             else {
                 hshard.assign(blk.size * in.nvoxel, 0.f);
                 RtmReader(in.rtm_files, in.rtm_name, in.nvoxel)
@@ -303,6 +383,28 @@ int main(int argc, char** argv) {
         }
         std::ofstream profile;
         if (rank == 0 && !cfg.profile_file.empty()) profile.open(cfg.profile_file);
+        if (gpu && !cfg.profile_file.empty()) {
+            // first profile line: the HDF5 -> HBM load (slowest rank's wall time; totals over ranks)
+            double mx[2] = {lstats.wall_s, lstats.rss_hwm_after_mb - lstats.rss_hwm_before_mb};
+            double sm[5] = {(double)lstats.bytes, lstats.read_s, lstats.h2d_s, lstats.wait_read_s, lstats.wait_copy_s};
+            host->all_reduce_host(mx, 2, ReduceOp::kMax);
+            host->all_reduce_host(sm, 5, ReduceOp::kSum);
+            if (profile.is_open())
+                profile << "{\"load\": true, \"load_s\": " << mx[0] << ", \"rtm_GB\": " << sm[0] / 1e9
+                        << ", \"load_GBps\": " << (mx[0] > 0 ? sm[0] / 1e9 / mx[0] : 0.0)
+                        << ", \"read_s\": " << sm[1] << ", \"h2d_s\": " << sm[2] << ", \"wait_read_s\": " << sm[3]
+                        << ", \"wait_copy_s\": " << sm[4] << ", \"ranks\": " << size
+                        << ", \"parallel_read\": " << ((cfg.parallel_read || size == 1) ? "true" : "false")
+                        << ", \"rank0\": {\"load_s\": " << lstats.wall_s << ", \"read_s\": " << lstats.read_s
+                        << ", \"h2d_s\": " << lstats.h2d_s << ", \"blocks\": " << lstats.blocks
+                        << ", \"rows_per_block\": " << lstats.rows_per_block
+                        << ", \"rows_per_read\": " << lstats.rows_per_read
+                        << ", \"staging_MB\": " << lstats.staging_bytes / 1048576.0
+                        << ", \"rss_hwm_before_MB\": " << lstats.rss_hwm_before_mb
+                        << ", \"rss_hwm_after_MB\": " << lstats.rss_hwm_after_mb << "}"
+                        << ", \"rss_growth_MB_max\": " << mx[1]
+                        << ", \"sparse\": " << (in.has_sparse ? "true" : "false") << ", \"driver\": \"native\"}\n";
+        }
 
         std::vector<uint64_t> frames;
         for (uint64_t i = 0; i < image.nframe(); ++i)

@@ -120,23 +120,25 @@ namespace {
 class P2pComm final : public Communicator {
    public:
     P2pComm(int device, std::shared_ptr<Communicator> base) : base_(std::move(base)), device_(device) {
-        t_start_ = std::chrono::steady_clock::now();
+        const auto t0 = std::chrono::steady_clock::now();
         HostComm& h = base_->host();
         rank_ = h.rank();
         n_ = h.size();
         const char* m = std::getenv("SART_P2P");
-        const std::string mode = (m && *m) ? m : "auto";
+        mode_ = (m && *m) ? m : "auto";
         cap_ = std::max<int64_t>(1024, (int64_t)(env_double("SART_P2P_MAX_BYTES", 2.0 * 1024 * 1024) / 4) / 4 * 4);
         // a healthy peer is at most a few sweeps behind (the host collectives of every frame's setup align the
         // ranks first), so a P2P wait this long means the peer is gone or stuck: the engines then switch to the
         // base communicator and re-solve the frame (device_failed / degrade)
         timeout_s_ = env_double("SART_P2P_TIMEOUT_S", 60.0);
+        // start-up calls (self-test, probes) give up sooner: a failure there only means "no P2P"
+        setup_timeout_s_ = std::min(timeout_s_, env_double("SART_P2P_SETUP_TIMEOUT_S", 10.0));
         if (const char* f = std::getenv("SART_P2P_FUSED_REDUCE"); f && *f) fused_reduce_ = std::atoi(f) != 0;
         if (const char* f = std::getenv("SART_FAULT_P2P"); f && *f) {
             const char* fr = std::getenv("SART_FAULT_RANK");
             if (!(fr && *fr) || std::atoi(fr) == rank_) fault_call_ = std::atoll(f);
         }
-        if (mode == "0" || mode == "off") {
+        if (mode_ == "0" || mode_ == "off") {
             finish(false, "p2p off (SART_P2P=0)");
             return;
         }
@@ -149,45 +151,43 @@ class P2pComm final : public Communicator {
             return;
         }
         hip_ok(hipSetDevice(device_), "hipSetDevice");
+        // Ranks sharing one GPU (one-GPU rehearsals): every P2P workgroup spins until its peers' chunks arrive, so
+        // the spinning workgroups of all ranks together must leave the CUs their peers' persistent sweeps need:
+        // 32 / (ranks per GPU) workgroups per call (4 at 8 ranks). One rank per GPU: up to kP2pMaxBlocks.
+        rpd_ = ranks_sharing_device(h, device_);
+        args_.max_blocks = rpd_ > 1 ? std::max(1, 32 / rpd_) : kP2pMaxBlocks;
+        if (rpd_ > 1 && rank_ == 0) {
+            // the GPU maps 24 compute queues at once (KFD num_cp_queues); more and the processes are time-sliced, and
+            // a P2P call then waits out a time slice for a descheduled peer (measured 10.3 ms instead of 111 us at 8
+            // ranks with HIP's default 4 queues per process: profiles/bench_r4_n8_rehearsal_one_gpu_q{4,1}.json)
+            const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+            const int hwq = (q && *q) ? std::atoi(q) : 4;
+            if (rpd_ * hwq > 24)
+                std::fprintf(stderr, "sart: %d ranks share one GPU with %d hardware queues each (%d > 24 mapped at once): "
+                             "processes are time-sliced; set GPU_MAX_HW_QUEUES=%d\n", rpd_, hwq, rpd_ * hwq,
+                             std::max(1, 12 / rpd_));
+        }
+        if (const char* b = std::getenv("SART_P2P_BLOCKS"); b && *b) args_.max_blocks = std::max(1, std::atoi(b));
         hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-        if (!agree(map_peers())) {
+        const bool mapped = agree(map_peers());
+        t_map_ = seconds_since(t0);
+        if (!mapped) {
             finish(false, "p2p off: IPC mapping failed (" + err_msg_ + ")");
             return;
         }
-        if (!agree(self_test())) {
+        const auto t1 = std::chrono::steady_clock::now();
+        const bool tested = self_test();
+        t_test_ = seconds_since(t1);
+        if (!tested) {
             finish(false, "p2p off: self-test failed (" + (err_msg_.empty() ? "on another rank" : err_msg_) + ")");
             return;
         }
-        if (mode == "1" || mode == "on") {
+        if (mode_ == "1" || mode_ == "on") {
             finish(true, "p2p (forced, self-test ok)");
             return;
         }
-        // auto: rank 0 times both at message sizes around the engine's (V + 1 floats: 64k .. 256k voxels);
-        // the P2P path serves vectors up to the largest probed size at which it won (rank 0 decides)
-        const int64_t probes[] = {4097, 65537, 262145, 524288};
-        double pick[1 + 2 * 4] = {0.0};
-        std::string table;
-        for (int i = 0; i < 4; ++i) {
-            const int64_t n = probes[i];
-            if (n > cap_) break;
-            const double tp = time_us([&](float* b) { p2p(b, n, 0, stream_); }, n);
-            const double tb = time_us([&](float* b) { base_->all_reduce(b, (size_t)n, ReduceOp::kSum, stream_); }, n);
-            pick[1 + 2 * i] = tp;
-            pick[2 + 2 * i] = tb;
-            if (tp < tb) pick[0] = (double)n;
-        }
-        h.broadcast_host(pick, sizeof(pick), 0);
-        for (int i = 0; i < 4 && probes[i] <= cap_; ++i) {
-            char cell[96];
-            std::snprintf(cell, sizeof(cell), "%s%lld: %.1f/%.1f", i ? ", " : "", (long long)probes[i], pick[1 + 2 * i],
-                          pick[2 + 2 * i]);
-            table += cell;
-        }
-        max_n_ = (int64_t)pick[0];
-        char buf[96];
-        std::snprintf(buf, sizeof(buf), "p2p up to %lld floats, %s above", (long long)max_n_, base_->backend());
-        finish(max_n_ > 0, (max_n_ > 0 ? std::string(buf) : std::string(base_->backend())) +
-                               " (auto, rank 0, us p2p/" + base_->backend() + " at floats " + table + ")");
+        finish(true, "p2p self-test ok; auto: sizes the engine announces are timed against " +
+                         std::string(base_->backend()));
     }
     ~P2pComm() override {
         (void)hipSetDevice(device_);
@@ -198,10 +198,63 @@ class P2pComm final : public Communicator {
     }
     HostComm& host() override { return base_->host(); }
     const char* backend() const override { return active_ ? "p2p" : base_->backend(); }
-    std::string describe() const override { return why_; }
+    std::string describe() const override {
+        char buf[160];
+        std::snprintf(buf, sizeof(buf), " [p2p setup %.0f ms: map %.0f, self-test %.0f, probes %.0f; %d ranks/GPU, %d blocks]",
+                      1e3 * setup_seconds(), 1e3 * t_map_, 1e3 * t_test_, 1e3 * t_probe_, rpd_, args_.max_blocks);
+        std::string table;
+        for (const auto& p : probes_) {
+            char cell[96];
+            std::snprintf(cell, sizeof(cell), "%s%lld: %.1f/%.1f", table.empty() ? "" : ", ", (long long)p.n, p.us_p2p,
+                          p.us_base);
+            table += cell;
+        }
+        std::string sel = why_;
+        if (active_ && auto_mode()) {
+            std::string won;
+            for (const auto& p : probes_)
+                if (p.p2p) won += (won.empty() ? "" : ",") + std::to_string(p.n);
+            sel = won.empty() ? std::string(base_->backend()) + " (auto: p2p won at no announced size)"
+                              : "p2p at floats " + won + ", " + base_->backend() + " otherwise (auto)";
+        }
+        if (!table.empty()) sel += " (rank 0, us p2p/" + std::string(base_->backend()) + " at floats " + table + ")";
+        return sel + buf;
+    }
+    double setup_seconds() const override { return t_map_ + t_test_ + t_probe_; }
+    void prepare(const std::vector<int64_t>& sizes) override {
+        if (!active_ || !auto_mode()) return;
+        std::vector<int64_t> todo;
+        for (int64_t n : sizes)
+            if (n > 0 && n <= cap_ && !probed(n) && std::find(todo.begin(), todo.end(), n) == todo.end())
+                todo.push_back(n);
+        // every rank must probe the same sizes in the same order: agree on the count (a mismatch is a caller bug)
+        double cnt[2] = {(double)todo.size(), -(double)todo.size()};
+        base_->host().all_reduce_host(cnt, 2, ReduceOp::kMax);
+        if (cnt[0] != -cnt[1]) throw std::runtime_error("p2p prepare: ranks announced different message sizes");
+        if (todo.empty()) return;
+        const auto t0 = std::chrono::steady_clock::now();
+        std::sort(todo.begin(), todo.end());
+        std::vector<double> us(2 * todo.size(), 0.0);
+        for (size_t i = 0; i < todo.size(); ++i) {
+            const int64_t n = todo[i];
+            us[2 * i] = time_us([&](float* b) { p2p(b, n, 0, stream_, setup_timeout_s_); }, n);
+            us[2 * i + 1] = time_us([&](float* b) { base_->all_reduce(b, (size_t)n, ReduceOp::kSum, stream_); }, n);
+        }
+        base_->host().broadcast_host(us.data(), us.size() * sizeof(double), 0);  // rank 0 decides
+        // a probe call that timed out on any rank leaves that rank's device path failed: P2P off everywhere
+        const bool ok = agree(err_words().first == 0);
+        for (size_t i = 0; i < todo.size(); ++i)
+            probes_.push_back(Probe{todo[i], us[2 * i], us[2 * i + 1], ok && us[2 * i] < us[2 * i + 1]});
+        std::sort(probes_.begin(), probes_.end(), [](const Probe& a, const Probe& b) { return a.n < b.n; });
+        t_probe_ += seconds_since(t0);
+        if (!ok) {
+            active_ = false;
+            why_ = std::string(base_->backend()) + " (p2p off: a probe call timed out)";
+        }
+    }
     void all_reduce(float* dev, size_t n, ReduceOp op, hipStream_t stream) override {
         // the choice depends only on n (identical on every rank), never on this rank's pointer alignment
-        if (active_ && n > 0 && (int64_t)n <= max_n_) {
+        if (use_p2p((int64_t)n)) {
             // SART_FAULT_P2P=k (tests): from its k-th P2P all-reduce on, this process raises no flags (a peer whose
             // device path stopped; a single missing flag would heal at the next call, flags being monotonic), only
             // on SART_FAULT_RANK when that is set
@@ -215,7 +268,7 @@ class P2pComm final : public Communicator {
     }
     void reduce_all_reduce(const ReduceSrc& src, float* out, hipStream_t stream) override {
         // SART_P2P_FUSED_REDUCE=0: two launches (the A/B baseline); same fault injection as all_reduce
-        if (active_ && fused_reduce_ && src.ld + 2 <= max_n_) {
+        if (fused_reduce_ && use_p2p(src.ld + 2)) {
             const bool skip = fault_call_ > 0 && ++calls_ >= fault_call_;
             launch_p2p_reduce_allreduce(src, out, args_, rank_, n_, ++epoch_, cap_, err_, timeout_s_, stream, skip);
         } else {
@@ -246,25 +299,43 @@ class P2pComm final : public Communicator {
     bool degradable() const override { return active_; }
     bool degrade() override {
         if (!active_) return false;
+        why_ = std::string(base_->backend()) + " (p2p disabled after a p2p all-reduce timeout; was: " + describe() + ")";
         active_ = false;
-        why_ = std::string(base_->backend()) + " (p2p disabled after a p2p all-reduce timeout; was: " + why_ + ")";
         return true;
     }
 
    private:
+    struct Probe {
+        int64_t n;
+        double us_p2p, us_base;
+        bool p2p;
+    };
+    static double seconds_since(std::chrono::steady_clock::time_point t0) {
+        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    bool auto_mode() const { return !(mode_ == "1" || mode_ == "on"); }
+    bool probed(int64_t n) const {
+        for (const auto& p : probes_)
+            if (p.n == n) return true;
+        return false;
+    }
+    // forced: every vector that fits the slots; auto: the decision at the smallest probed size >= n (a vector a
+    // few floats shorter than a probed one, e.g. the cold start's ld next to the sweep's ld + 2, goes the same way)
+    bool use_p2p(int64_t n) const {
+        if (!active_ || n <= 0 || n > cap_) return false;
+        if (!auto_mode()) return true;
+        for (const auto& p : probes_)  // sorted by n
+            if (p.n >= n) return p.p2p;
+        return false;
+    }
     std::pair<unsigned, unsigned> err_words() {  // {timeout, abort}
         unsigned e[2] = {0, 0};
-        hip_ok(hipMemcpy(e, err_, sizeof(e), hipMemcpyDeviceToHost), "p2p error word");
+        if (err_) hip_ok(hipMemcpy(e, err_, sizeof(e), hipMemcpyDeviceToHost), "p2p error word");
         return {e[0], e[1]};
     }
     void finish(bool active, const std::string& why) {
         active_ = active;
-        // start-up cost (IPC mapping, self-test, auto probe) on this rank, reported with the selection
-        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start_).count();
-        char buf[64];
-        std::snprintf(buf, sizeof(buf), " [p2p setup %.0f ms]", ms);
-        why_ = why + buf;
-        if (active && max_n_ == 0) max_n_ = cap_;  // forced on: every vector that fits the slots
+        why_ = why;
     }
     bool agree(bool ok) {  // every rank learns whether all succeeded
         double bad = ok ? 0.0 : 1.0;
@@ -301,17 +372,23 @@ class P2pComm final : public Communicator {
             ok = false;
             err_msg_ = e.what();
         }
-        for (int r = 0; r < n_; ++r) {  // every rank takes part in every broadcast, even after a failure
-            hipIpcMemHandle_t h = hdl;
-            base_->host().broadcast_host(&h, sizeof(h), r);
-            if (!ok) continue;
+        // every rank's handle in one gather (a sum of one nonzero slot per rank) instead of n broadcasts
+        std::vector<unsigned char> all((size_t)n_ * sizeof(hdl), 0);
+        std::memcpy(all.data() + (size_t)rank_ * sizeof(hdl), &hdl, sizeof(hdl));
+        std::vector<double> words(all.size());
+        for (size_t i = 0; i < all.size(); ++i) words[i] = all[i];
+        base_->host().all_reduce_host(words.data(), words.size(), ReduceOp::kSum);
+        for (int r = 0; r < n_ && ok; ++r) {
+            hipIpcMemHandle_t h;
+            for (size_t i = 0; i < sizeof(h); ++i)
+                reinterpret_cast<unsigned char*>(&h)[i] = (unsigned char)words[(size_t)r * sizeof(h) + i];
             void* p = mem_;
             if (r != rank_) {
                 if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
                     (void)hipGetLastError();
                     ok = false;
                     err_msg_ = "hipIpcOpenMemHandle of rank " + std::to_string(r);
-                    continue;
+                    break;
                 }
                 opened_.push_back(p);
             }
@@ -325,8 +402,10 @@ class P2pComm final : public Communicator {
         launch_p2p_allreduce(dev, dev, n, args_, rank_, n_, ++epoch_, cap_, op, err_,
                              timeout_s > 0 ? timeout_s : timeout_s_, stream, skip_flags);
     }
-    // Exact checks: integer-valued sums / maxima, and random fp32 data against the rank-order sum (the
-    // kernel's result must be bitwise identical to ((v0 + v1) + v2) + ... on every rank), both parities.
+    // Exact checks: integer-valued sums / maxima, and random fp32 data against the rank-order sum (the kernel's
+    // result must be bitwise identical to ((v0 + v1) + v2) + ... on every rank). Every rank runs every call (a
+    // failed call on one rank makes its later calls fail fast; its peers time out at most once, after
+    // setup_timeout_s_), and the ranks agree once at the end.
     bool self_test() {
         float* d = nullptr;
         if (!agree(hipMalloc(reinterpret_cast<void**>(&d), (size_t)cap_ * sizeof(float)) == hipSuccess)) {
@@ -335,11 +414,11 @@ class P2pComm final : public Communicator {
             err_msg_ = "hipMalloc";
             return false;
         }
-        const int64_t sizes[] = {1, 5, 1024, 4099, std::min<int64_t>(cap_, 65537)};
+        const int64_t sizes[] = {1, 4099, std::min<int64_t>(cap_, 65537)};
         int call = 0;
+        bool good = true;
         for (int64_t n : sizes) {
             for (int kind = 0; kind < 3; ++kind, ++call) {  // 0 integer sum, 1 integer max, 2 random fp32 sum
-                bool good = true;
                 try {
                     std::vector<float> mine((size_t)n), want((size_t)n), got((size_t)n);
                     for (int64_t i = 0; i < n; ++i) {
@@ -352,26 +431,20 @@ class P2pComm final : public Communicator {
                         want[(size_t)i] = acc;
                     }
                     hip_ok(hipMemcpy(d, mine.data(), (size_t)n * sizeof(float), hipMemcpyHostToDevice), "H2D");
-                    p2p(d, n, kind == 1 ? 1 : 0, stream_, std::min(timeout_s_, 30.0));
+                    p2p(d, n, kind == 1 ? 1 : 0, stream_, setup_timeout_s_);
                     hip_ok(hipStreamSynchronize(stream_), "p2p self-test");
                     hip_ok(hipMemcpy(got.data(), d, (size_t)n * sizeof(float), hipMemcpyDeviceToHost), "D2H");
-                    unsigned e = 0;
-                    hip_ok(hipMemcpy(&e, err_, sizeof(e), hipMemcpyDeviceToHost), "D2H");
-                    if (e) throw std::runtime_error("peer timeout");
+                    if (err_words().first) throw std::runtime_error("peer timeout");
                     if (std::memcmp(got.data(), want.data(), (size_t)n * sizeof(float)) != 0)
                         throw std::runtime_error("mismatch at n=" + std::to_string(n) + " kind " + std::to_string(kind));
                 } catch (const std::exception& ex) {
+                    if (good) err_msg_ = ex.what();
                     good = false;
-                    err_msg_ = ex.what();
-                }
-                if (!agree(good)) {  // every rank leaves the test at the same call
-                    (void)hipFree(d);
-                    return false;
                 }
             }
         }
         (void)hipFree(d);
-        return true;
+        return agree(good);
     }
     static float value(int kind, int r, int64_t i, int call) {
         if (kind < 2) return (float)((r + 1) * ((i * 7 + call) % 251));
@@ -379,20 +452,20 @@ class P2pComm final : public Communicator {
         z = (z ^ (z >> 31)) * 0x94D049BB133111EBull;
         return (float)((double)(z >> 40) / (double)(1ull << 24) * 2.0 - 1.0);
     }
-    // mean microseconds per call over 20 calls after 3 warm-up calls (host barrier before timing)
+    // mean microseconds per call over 10 calls after 2 warm-up calls (host barrier before timing)
     double time_us(const std::function<void(float*)>& f, int64_t n) {
         float* d = nullptr;
         hip_ok(hipMalloc(reinterpret_cast<void**>(&d), (size_t)n * sizeof(float)), "hipMalloc");
         hip_ok(hipMemset(d, 0, (size_t)n * sizeof(float)), "hipMemset");
         hip_ok(hipDeviceSynchronize(), "sync");
-        for (int i = 0; i < 3; ++i) f(d);
+        for (int i = 0; i < 2; ++i) f(d);
         hip_ok(hipStreamSynchronize(stream_), "sync");
         base_->host().barrier();
         hipEvent_t e0, e1;
         hip_ok(hipEventCreate(&e0), "event");
         hip_ok(hipEventCreate(&e1), "event");
         hip_ok(hipEventRecord(e0, stream_), "event");
-        for (int i = 0; i < 20; ++i) f(d);
+        for (int i = 0; i < 10; ++i) f(d);
         hip_ok(hipEventRecord(e1, stream_), "event");
         hip_ok(hipEventSynchronize(e1), "event");
         float ms = 0.f;
@@ -400,16 +473,17 @@ class P2pComm final : public Communicator {
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         (void)hipFree(d);
-        return 1e3 * ms / 20.0;
+        return 1e3 * ms / 10.0;
     }
 
     std::shared_ptr<Communicator> base_;
-    int device_ = 0, rank_ = 0, n_ = 1;
+    int device_ = 0, rank_ = 0, n_ = 1, rpd_ = 1;
+    std::string mode_;
     int64_t cap_ = 0;
-    int64_t max_n_ = 0;  // P2P for n <= max_n_ (auto: largest probed size at which it beat the base)
-    double timeout_s_ = 60.0;
+    std::vector<Probe> probes_;  // auto mode: announced sizes, sorted by n
+    double timeout_s_ = 60.0, setup_timeout_s_ = 10.0;
+    double t_map_ = 0.0, t_test_ = 0.0, t_probe_ = 0.0;
     int64_t fault_call_ = 0, calls_ = 0;  // SART_FAULT_P2P
-    std::chrono::steady_clock::time_point t_start_;
     bool active_ = false;
     std::string why_, err_msg_;
     hipStream_t stream_ = nullptr;
@@ -423,6 +497,38 @@ class P2pComm final : public Communicator {
 };
 
 }  // namespace
+
+int ranks_sharing_device(HostComm& host, int device) {
+    const int n = host.size();
+    if (n <= 1) return 1;
+    // identity of the physical GPU: boot id + host name + PCI bus id (device ordinals differ under per-rank
+    // HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES and LOCAL_WORLD_SIZE is launcher-specific; containers on
+    // different nodes can share a host name and bus ids, but not the kernel's boot id)
+    char bus[64] = {0};
+    hip_ok(hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, device), "hipDeviceGetPCIBusId");
+    char hn[256] = {0};
+    (void)gethostname(hn, sizeof(hn) - 1);
+    char boot[64] = {0};
+    if (FILE* f = std::fopen("/proc/sys/kernel/random/boot_id", "r")) {
+        if (!std::fgets(boot, sizeof(boot), f)) boot[0] = 0;
+        std::fclose(f);
+    }
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over "boot/host/bus"
+    for (const char* p : {static_cast<const char*>(boot), "/", static_cast<const char*>(hn), "/",
+                          static_cast<const char*>(bus)})
+        for (; *p; ++p) h = (h ^ (unsigned char)*p) * 1099511628211ull;
+    std::vector<double> keys((size_t)n, 0.0);
+    keys[(size_t)host.rank()] = (double)(h >> 12) + 1.0;  // < 2^53: exact in fp64; one nonzero slot per rank
+    host.all_reduce_host(keys.data(), keys.size(), ReduceOp::kSum);
+    std::sort(keys.begin(), keys.end());
+    int most = 1;  // the largest number of ranks on one GPU (identical on every rank)
+    for (size_t i = 0, j = 0; i < keys.size(); i = j) {
+        for (j = i; j < keys.size() && keys[j] == keys[i]; ++j) {
+        }
+        most = std::max(most, (int)(j - i));
+    }
+    return most;
+}
 
 std::unique_ptr<Communicator> make_local_comm() { return std::make_unique<LocalComm>(); }
 

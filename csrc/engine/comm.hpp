@@ -11,7 +11,8 @@
 //               (csrc/kernels/p2p_allreduce.hip) for fp32 vectors up to SART_P2P_MAX_BYTES, wrapping a
 //               base communicator (RCCL in production) that serves everything else. Enabled after an
 //               exact self-test on every rank; SART_P2P=0 off, 1 on, auto (default): rank 0 times both at
-//               4k .. 512k floats and P2P serves vectors up to the largest size at which it won.
+//               the message sizes the engine announces (Communicator::prepare) and P2P serves the sizes at
+//               which it won.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -20,6 +21,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "../kernels/launchers.hpp"
 #include "../native/host_comm.hpp"
@@ -53,11 +55,21 @@ class Communicator {
     // Serve every device collective from the base path from now on (p2p -> RCCL / staged). Collective in the
     // sense that every rank must call it after the same solve.
     virtual bool degrade() { return false; }
+    // The engines announce the fp32 message sizes of their collectives (collective: every rank, same sizes). The
+    // p2p communicator in auto mode times itself against its base at exactly those sizes (once per size) and
+    // serves a size from the p2p path when it won there; sizes never announced are served by the base.
+    virtual void prepare(const std::vector<int64_t>& float_sizes) { (void)float_sizes; }
+    // Host-side start-up cost of the communicator so far (p2p: IPC mapping, self-test, probes), seconds.
+    virtual double setup_seconds() const { return 0.0; }
     // Human-readable selection (backend and why), e.g. for benchmark logs.
     virtual std::string describe() const { return backend(); }
     int rank() { return host().rank(); }
     int size() { return host().size(); }
 };
+
+// The largest number of ranks of `host` that run on one physical GPU (identity: boot id + host name + PCI bus id),
+// identical on every rank. Collective over the host communicator.
+int ranks_sharing_device(HostComm& host, int device);
 
 std::unique_ptr<Communicator> make_local_comm();
 std::unique_ptr<Communicator> make_staged_comm(std::unique_ptr<HostComm> host);

@@ -34,37 +34,7 @@ bool fault_rank_selected(int rank) {
 
 }  // namespace
 
-int ranks_sharing_device(Communicator* comm, int device) {
-    const int n = comm->size();
-    if (n <= 1) return 1;
-    // identity of the physical GPU: boot id + host name + PCI bus id (device ordinals differ under per-rank
-    // HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES and LOCAL_WORLD_SIZE is launcher-specific; containers on
-    // different nodes can share a host name and bus ids, but not the kernel's boot id)
-    char bus[64] = {0};
-    hip_ok(hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, device), "hipDeviceGetPCIBusId");
-    char host[256] = {0};
-    (void)gethostname(host, sizeof(host) - 1);
-    char boot[64] = {0};
-    if (FILE* f = std::fopen("/proc/sys/kernel/random/boot_id", "r")) {
-        if (!std::fgets(boot, sizeof(boot), f)) boot[0] = 0;
-        std::fclose(f);
-    }
-    uint64_t h = 1469598103934665603ull;  // FNV-1a over "boot/host/bus"
-    for (const char* p : {static_cast<const char*>(boot), "/", static_cast<const char*>(host), "/",
-                          static_cast<const char*>(bus)})
-        for (; *p; ++p) h = (h ^ (unsigned char)*p) * 1099511628211ull;
-    std::vector<double> keys((size_t)n, 0.0);
-    keys[(size_t)comm->rank()] = (double)(h >> 12) + 1.0;  // < 2^53: exact in fp64; one nonzero slot per rank
-    comm->host().all_reduce_host(keys.data(), keys.size(), ReduceOp::kSum);
-    std::sort(keys.begin(), keys.end());
-    int most = 1;  // the largest number of ranks on one GPU (identical on every rank)
-    for (size_t i = 0, j = 0; i < keys.size(); i = j) {
-        for (j = i; j < keys.size() && keys[j] == keys[i]; ++j) {
-        }
-        most = std::max(most, (int)(j - i));
-    }
-    return most;
-}
+int ranks_sharing_device(Communicator* comm, int device) { return ranks_sharing_device(comm->host(), device); }
 
 bool device_shared_across_ranks(Communicator* comm, int device) { return ranks_sharing_device(comm, device) > 1; }
 
@@ -190,6 +160,14 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
     }
     alloc_fused();
     ray_sums();
+    // the fp32 collectives of a solve: row shards reduce the voxel correction (+ ||A x||^2 and the error word) per
+    // sweep and ld-long vectors per frame; column shards the pixel vector A x (and x when there is a Laplacian)
+    if (comm_->size() > 1) {
+        if (cfg_.column_shard)
+            comm_->prepare({P_, cfg_.nvoxel_total});
+        else
+            comm_->prepare({ld_ + 2, ld_});
+    }
 }
 
 Engine::~Engine() {
@@ -565,6 +543,10 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
     RoctxRange range("sart::solve");
     set_device();
     const auto t0 = std::chrono::steady_clock::now();
+    // Row shards align the ranks in setup_frame's host collectives; column shards have none there, so while a
+    // device path with a timeout is active a barrier keeps a rank that was busy between frames (rank 0 writing
+    // the output) from counting against its peers' first all-reduce timeout.
+    if (cfg_.column_shard && comm_->size() > 1 && comm_->degradable()) comm_->host().barrier();
     SolveInfo info;
     const int max_sweeps = cfg_.max_iterations + 1;
     while (true) {

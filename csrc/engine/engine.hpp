@@ -188,6 +188,9 @@ class Engine {
     int64_t fused_blocks_ = 0;   // partial-sum rows written by the fused sweep (I, or I * T * segments)
     double norm_ = 1.0;
 
+    // comm_buf_: [0, ld) the reduced correction, [ld] ||A x||^2, [ld + 1] the error word of the last sweep, EXCEPT
+    // after a one-rank sweep on the one-kernel tail (k_reduce_decide_update keeps them in registers): its contents
+    // are then undefined (stale). Nothing reads it after a solve; a diagnostic that does must use SART_TAIL_FUSED=0.
     DeviceArray<float> partial_, comm_buf_, x_, pen_, O_, ghat_, arow_, gpos_, wo_, w_, fitted_;
     DeviceArray<float> xprev_;  // x before the last update (NaN/Inf guard rollback)
     bool shared_device_ = false;

@@ -90,6 +90,12 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
         if (v > chunks_.back() && v < ld_) chunks_.push_back(v);
     }
     chunks_.push_back(ld_);
+    if (comm_->size() > 1) {  // the fp32 collectives of a sweep (p2p auto mode times exactly these sizes)
+        std::vector<int64_t> sizes{(int64_t)NF * ld_ + NF, (int64_t)NF * ld_};
+        for (size_t c = 0; c + 1 < chunks_.size(); ++c)
+            sizes.push_back((chunks_[c + 1] - chunks_[c]) * NF + (c + 2 == chunks_.size() ? NF : 0));
+        comm_->prepare(sizes);
+    }
     if (chunks_.size() > 2) {
         hip_ok(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking), "hipStreamCreate");
         cev_.resize(chunks_.size() - 1);

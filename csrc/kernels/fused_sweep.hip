@@ -984,6 +984,8 @@ void fused_set_schedule(int sched) {
     g_fused_sched = sched;
 }
 int fused_get_schedule() { return g_fused_sched; }
+static int g_fused_last_sched = -1;  // SCHED of the last k_fused_sweep_rows launch (variant 3: -1)
+int fused_last_schedule() { return g_fused_last_sched; }
 bool fused_split_schedule(int T, bool bf16) {  // mirrors the schedule choice of launch_rows / launch_fused_sweep_bf16
     if (bf16) return T >= 2 || g_fused_sched == 5;
     return g_fused_sched >= 4;  // T = 1: 4 and 5 both run schedule 5; T >= 2: 5 runs 4
@@ -1032,6 +1034,7 @@ static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld
                           const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                           uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, int64_t chain_tiles) {
     constexpr size_t lds = rows_lds_bytes(T, SC, CPL / 4, KW);
+    g_fused_last_sched = SC;
     static bool configured = false;
     if (!configured) {
         hip_call(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fused_sweep_rows<LG, X, D, T, SC, AT, CPL, KW>),
@@ -1189,6 +1192,7 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
     const int T = 8 / K;
     if (nrows_pad % T != 0) throw std::runtime_error("fused_sweep v3: padded rows must be a multiple of the tile");
     if (J * T > kMaxGather) throw std::runtime_error("fused_sweep v3: too many slabs for the gather registers");
+    g_fused_last_sched = -1;
     switch (K) {
         case 1: launch_lds<1>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st); break;
         case 2: launch_lds<2>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st); break;

@@ -82,6 +82,7 @@ int fused_pick_k(int64_t ld);
 int fused_tile_rows(int K, int variant);
 void fused_set_schedule(int sched);
 int fused_get_schedule();
+int fused_last_schedule();  // pipeline schedule the last variant-6 launch ran (T / kw / chip-wide pick it), -1: v3
 void fused_set_trace(unsigned long long* buf, long long tiles);
 std::vector<int> fused_debug_map(int nblocks);
 int fused_fpart_per_block(int variant);
@@ -114,8 +115,12 @@ struct P2pArgs {
     float* recv[kP2pMaxRanks];      // rank j's receive buffer as mapped in this process
     unsigned* flags[kP2pMaxRanks];  // rank j's flag array as mapped in this process
     const unsigned* abort_word;     // this rank's abort word: set remotely by a peer that aborts
+    // workgroups per call (0: kP2pMaxBlocks). Identical on every rank. Ranks sharing one GPU (one-GPU rehearsals)
+    // use few: every workgroup spins until its peers' chunks arrive, and the spinning workgroups of all ranks must
+    // leave room for the peers' persistent sweeps and their own all-reduce kernels.
+    int max_blocks;
 };
-int64_t p2p_chunk(int64_t n);  // elements per workgroup
+int64_t p2p_chunk(int64_t n, int max_blocks = kP2pMaxBlocks);  // elements per workgroup
 // op: 0 sum, 1 max. `epoch` strictly increases by one per call on every rank (starts at 1).
 // skip_flags (fault injection, tests): push the data but raise no flag, so the peers time out in this call.
 void launch_p2p_allreduce(const float* in, float* out, int64_t n, const P2pArgs& a, int rank, int nranks,

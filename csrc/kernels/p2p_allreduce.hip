@@ -39,8 +39,13 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
     const int64_t c1 = c0 + chunk < n ? c0 + chunk : n;
     // After a timeout on this rank the device path is being abandoned (the engines agree on it after the solve and
     // switch to the base communicator): later calls fail at once, without pushing or raising flags, so a solve
-    // pays one timeout per rank instead of one per queued sweep.
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+    // pays one timeout per rank instead of one per queued sweep. One load per workgroup, broadcast through LDS: the
+    // whole workgroup takes the same branch (a per-thread load could split it while another workgroup of this
+    // launch raises *err, and the threads that went on would raise flags for a partly pushed chunk).
+    __shared__ unsigned err0;
+    if (threadIdx.x == 0) err0 = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (err0 != 0) {
         for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) out[i] = __builtin_nanf("");
         return;
     }
@@ -163,11 +168,12 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
 
 }  // namespace
 
-int64_t p2p_chunk(int64_t n) {
-    // 1024 floats per workgroup (one float4 per thread) up to kP2pMaxBlocks workgroups, then wider chunks
+int64_t p2p_chunk(int64_t n, int max_blocks) {
+    // 1024 floats per workgroup (one float4 per thread) up to max_blocks workgroups, then wider chunks
     const int64_t per = 1024;
+    const int64_t mb = max_blocks > 0 && max_blocks < kP2pMaxBlocks ? max_blocks : kP2pMaxBlocks;
     const int64_t groups = (n + per - 1) / per;
-    const int64_t mult = (groups + kP2pMaxBlocks - 1) / kP2pMaxBlocks;
+    const int64_t mult = (groups + mb - 1) / mb;
     return per * (mult > 0 ? mult : 1);
 }
 
@@ -180,7 +186,7 @@ void launch_p2p_allreduce(const float* in, float* out, int64_t n, const P2pArgs&
                                  std::to_string(cap) + ", ranks=" + std::to_string(nranks) + ")");
     // the receive slots are always 16-B aligned; the caller's buffer may not be (4-B element accesses then)
     const int vec_io = ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) % 16) == 0;
-    const int64_t chunk = p2p_chunk(n);
+    const int64_t chunk = p2p_chunk(n, a.max_blocks);
     const int64_t blocks = (n + chunk - 1) / chunk;
     if (blocks > kP2pMaxBlocks) throw std::runtime_error("launch_p2p_allreduce: too many chunks");
     const uint64_t ticks = (uint64_t)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
@@ -200,7 +206,7 @@ void launch_p2p_reduce_allreduce(const ReduceSrc& src, float* out, const P2pArgs
         src.ld <= 0 || src.ld % 64 != 0 || src.nsplit < 1 || src.nF < 0 || src.partial == nullptr || !aligned)
         throw std::runtime_error("launch_p2p_reduce_allreduce: bad arguments (ld=" + std::to_string(src.ld) +
                                  ", cap=" + std::to_string(cap) + ", ranks=" + std::to_string(nranks) + ")");
-    const int64_t chunk = p2p_chunk(n);
+    const int64_t chunk = p2p_chunk(n, a.max_blocks);
     const int64_t blocks = (n + chunk - 1) / chunk;
     if (blocks > kP2pMaxBlocks) throw std::runtime_error("launch_p2p_reduce_allreduce: too many chunks");
     const uint64_t ticks = (uint64_t)(timeout_s * 1e8);

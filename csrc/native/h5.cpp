@@ -260,6 +260,27 @@ void h5_write_u8(hid_t loc, const std::string& path, const std::vector<uint64_t>
     write_ds(loc, path, dims, H5T_STD_U8LE, H5T_NATIVE_UINT8, data);
 }
 
+H5Id h5_create_dataset(hid_t loc, const std::string& path, const std::vector<uint64_t>& dims, hid_t ftype) {
+    std::vector<hsize_t> d(dims.begin(), dims.end());
+    H5Id sp(H5Screate_simple((int)d.size(), d.data(), nullptr), H5Id::kSpace);
+    H5Id ds(H5Dcreate2(loc, path.c_str(), ftype, sp, H5P_DEFAULT, H5P_DEFAULT, H5P_DEFAULT), H5Id::kDataset);
+    if (!ds.valid()) throw Error("Unable to create HDF5 dataset " + path + ".");
+    return ds;
+}
+
+void h5_write_box(hid_t dset, const std::vector<uint64_t>& off, const std::vector<uint64_t>& cnt, hid_t mtype,
+                  const void* data) {
+    if (off.size() != cnt.size() || off.empty()) throw Error("h5_write_box: bad box");
+    size_t n = 1;
+    for (auto v : cnt) n *= v;
+    if (n == 0) return;
+    std::vector<hsize_t> o(off.begin(), off.end()), c(cnt.begin(), cnt.end());
+    H5Id fsp(H5Dget_space(dset), H5Id::kSpace);
+    check(H5Sselect_hyperslab(fsp, H5S_SELECT_SET, o.data(), nullptr, c.data(), nullptr), "selecting a box");
+    H5Id msp(H5Screate_simple((int)c.size(), c.data(), nullptr), H5Id::kSpace);
+    check(H5Dwrite(dset, mtype, msp, fsp, H5P_DEFAULT, data), "writing a box");
+}
+
 #endif  // SART_HAVE_HDF5
 
 }  // namespace sart

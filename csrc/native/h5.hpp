@@ -101,6 +101,11 @@ void h5_write_f32(hid_t loc, const std::string& path, const std::vector<uint64_t
 void h5_write_u64(hid_t loc, const std::string& path, const std::vector<uint64_t>& dims, const uint64_t* data);
 void h5_write_i32(hid_t loc, const std::string& path, const std::vector<uint64_t>& dims, const int32_t* data);
 void h5_write_u8(hid_t loc, const std::string& path, const std::vector<uint64_t>& dims, const uint8_t* data);
+// Datasets written piecewise (large synthetic fixtures): create with file type `ftype`, then write the box
+// [off, off + cnt) from a dense memory block of memory type `mtype`.
+H5Id h5_create_dataset(hid_t loc, const std::string& path, const std::vector<uint64_t>& dims, hid_t ftype);
+void h5_write_box(hid_t dset, const std::vector<uint64_t>& off, const std::vector<uint64_t>& cnt, hid_t mtype,
+                  const void* data);
 
 #endif  // SART_HAVE_HDF5
 

@@ -348,7 +348,8 @@ void RtmReader::read(uint64_t row_begin, uint64_t row_end, float* out, uint64_t 
                         // row blocks of <= 64 MiB per hyperslab read, only the window's columns (the reference
                         // reads one whole row per call, raytransfer.cpp:103-109)
                         const uint64_t nc = s1 - s0;
-                        const uint64_t rows_per_read = std::max<uint64_t>(1, (64ull << 20) / (4 * nc));
+                        const uint64_t rows_per_read =
+                            rows_per_read_ ? rows_per_read_ : std::max<uint64_t>(1, (64ull << 20) / (4 * nc));
                         for (uint64_t r = lr0; r < lr1; r += rows_per_read) {
                             const uint64_t n = std::min(rows_per_read, lr1 - r);
                             h5_read_block_f32(d, r, n, s0, nc, out + (start_pixel + r - row_begin) * ld, ld, ocol);

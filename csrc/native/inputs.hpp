@@ -47,6 +47,9 @@ class RtmReader {
               uint64_t col_end = 0);
     void read(uint64_t row_begin, uint64_t row_end, float* out, uint64_t ld);
     uint64_t ncols() const { return c1_ - c0_; }
+    // Dense datasets: rows per hyperslab read (0: blocks of <= 64 MiB; 1: one row per read, the reference's
+    // pattern raytransfer.cpp:103-109, kept for load-path comparisons: SART_RTM_ROWS_PER_READ).
+    void set_rows_per_read(uint64_t n) { rows_per_read_ = n; }
 
    private:
     struct SparseSegment {
@@ -56,7 +59,7 @@ class RtmReader {
     const SparseSegment& sparse_segment(int64_t f, const std::string& path, uint64_t nvox_seg);  // f: hid_t
     SortedRtmFiles sorted_;
     std::string name_;
-    uint64_t nvoxel_ = 0, c0_ = 0, c1_ = 0;
+    uint64_t nvoxel_ = 0, c0_ = 0, c1_ = 0, rows_per_read_ = 0;
     std::map<std::string, SparseSegment> sparse_;
 };
 // One-shot read of whole rows (all columns).

@@ -12,13 +12,21 @@ MASTER_PORT) or by ``mpiexec`` (PMI_* / OMPI_* variables; the launcher's file de
 child, so PMI reaches it), like the reference's ``mpirun`` (reference main.cpp:63-68). The Python solver API
 (``models.sart.SARTSolver``, ``models.multiframe.MultiFrameSARTSolver``, ``models.cpu.CPUSARTSolver``) drives the
 same native engines for programmatic use.
+
+Signals: launchers stop their workers with SIGTERM (torchrun, mpiexec) or SIGINT / SIGHUP. This process forwards
+each of them to the driver and waits for it, so the driver never outlives its launcher holding a GPU or blocked
+in a collective; the driver also asks the kernel for SIGTERM should this process die without forwarding
+(``SART_PARENT_PID``, PR_SET_PDEATHSIG in sartsolver_main.cpp).
 """
 from __future__ import annotations
 
 import os
+import signal
 import subprocess
 import sys
 from pathlib import Path
+
+FORWARDED = (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)
 
 
 def driver_binary() -> Path:
@@ -35,9 +43,33 @@ def main(argv=None) -> int:
         return 1
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (P2P all-reduce, RCCL) on this platform
+    env["SART_PARENT_PID"] = str(os.getpid())  # the driver exits if this process is already gone at its start
     sys.stdout.flush()
     sys.stderr.flush()
-    return subprocess.run([str(binary), *argv], env=env, close_fds=False).returncode
+    proc = subprocess.Popen([str(binary), *argv], env=env, close_fds=False)
+    received: list[int] = []
+
+    def forward(signum, _frame):
+        received.append(signum)
+        try:
+            proc.send_signal(signum)
+        except ProcessLookupError:
+            pass
+
+    previous = {s: signal.signal(s, forward) for s in FORWARDED}
+    try:
+        while True:
+            try:
+                rc = proc.wait()
+                break
+            except InterruptedError:  # pragma: no cover - PEP 475 retries wait() itself
+                continue
+    finally:
+        for s, h in previous.items():
+            signal.signal(s, h)
+    if rc < 0 and received:  # killed by the forwarded signal: report it like a shell does
+        return 128 - rc
+    return rc
 
 
 if __name__ == "__main__":

@@ -58,7 +58,9 @@ def _case(tmp_path, **kw):
 
 
 @pytest.mark.parametrize("log", [False, True])
-def test_native_cpu_matches_python_driver(tmp_path, binary, log):
+def test_native_cpu_module_entry_point_forwards(tmp_path, binary, log):
+    """python -m mpi_cuda_sartsolver_amd launches the same executable (cli.py): arguments and output forwarded, the
+    file bit for bit (the CPU solver's parity with the reference CPU semantics: test_cli_e2e)."""
     case = _case(tmp_path)
     base = ["--use_cpu", "-m", "80", "-c", "1e-7", "-l", case.laplacian_file, "-b", "1e-3"] + (["-L"] if log else [])
     r1 = _run_native(binary, base + ["-o", str(tmp_path / "n.h5"), *case.files])
@@ -147,17 +149,30 @@ def test_native_cli_errors(tmp_path, binary):
 @pytest.mark.gpu
 @pytest.mark.parametrize("log", [False, True])
 @pytest.mark.parametrize("extra", [[], ["--batch_frames", "2", "--no_guess"]])
-def test_native_gpu_matches_python_driver(tmp_path, binary, log, extra):
+def test_native_gpu_vs_oracle_and_module_entry_point(tmp_path, binary, log, extra):
+    """The native driver on the GPU: every frame within the fp32 emulation's error of the fp64 oracle chain run for
+    the recorded update counts (test_cli_e2e.chain_errors: an independent parity check of the frame loop, warm
+    starts and output); --profile's first line reports the HDF5 -> HBM load, the others the solves. Then the module
+    entry point (python -m mpi_cuda_sartsolver_amd, cli.py) must forward the arguments and exit code to the same
+    executable: bitwise the same file."""
+    from test_cli_e2e import CLI_FP32_FACTOR, chain_errors
+
     case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_b",), laplacian=True, nframes=3, saturate=0.05,
                      nvoxel=2048, grid=(16, 16, 16), shapes=((24, 32), (20, 30)))
     base = ["-m", "60", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3"] + (["-L"] if log else []) + extra
     prof = str(tmp_path / "n.jsonl")
     r1 = _run_native(binary, base + ["--profile", prof, "-o", str(tmp_path / "n.h5"), *case.files])
     assert r1.returncode == 0, r1.stdout + r1.stderr
-    for line in open(prof):  # bytes of the fp32 shard: 4 per element, one (fused) or two reads per sweep
-        rec = json.loads(line)
+    recs = [json.loads(line) for line in open(prof)]
+    load = recs[0]
+    assert load.get("load") and load["rtm_GB"] > 0 and load["load_s"] > 0 and load["rank0"]["blocks"] >= 1, load
+    assert load["sparse"] is True  # cam_b is a sparse COO file
+    for rec in recs[1:]:  # bytes of the fp32 shard: 4 per element, one (fused) or two reads per sweep
+        assert "load" not in rec
         if "rtm_GBps" in rec:  # (batched frames report per-frame times only)
             assert abs(rec["rtm_GBps"] / rec["gflops"] - (1 if rec["fused"] else 2)) < 1e-4, rec  # 6 printed digits
+    e, e32 = chain_errors(case, str(tmp_path / "n.h5"), log=log, warm="--no_guess" not in extra)
+    assert np.all(e <= CLI_FP32_FACTOR * e32 + 1e-6), (e, e32)
     r2 = _run_python(base + ["-o", str(tmp_path / "p.h5"), *case.files])
     assert r2.returncode == 0, r2.stdout + r2.stderr
     n = native()
@@ -165,7 +180,7 @@ def test_native_gpu_matches_python_driver(tmp_path, binary, log, extra):
     t2, x2, s2 = n.read_solution_file(str(tmp_path / "p.h5"))
     np.testing.assert_array_equal(t1, t2)
     np.testing.assert_array_equal(s1, s2)
-    np.testing.assert_array_equal(x1, x2)  # same engine and kernels: bitwise
+    np.testing.assert_array_equal(x1, x2)  # the same executable behind both entry points: bitwise
 
 
 @pytest.mark.gpu
@@ -194,6 +209,8 @@ def test_native_gpu_two_ranks_one_device(tmp_path, binary, p2p):
     import json
 
     lines = [json.loads(x) for x in open(prof)]
+    assert lines[0]["load"] and lines[0]["ranks"] == 2  # the HDF5 -> HBM load of both ranks
+    lines = lines[1:]
     assert len(lines) == 2 and all(d["ranks"] == 2 and d["comm_ms"] >= 0 and d["sweeps"] >= 1 for d in lines)
     assert lines[0]["device_comm"].startswith("p2p" if p2p == "1" else "staged"), lines[0]["device_comm"]
     n = native()
@@ -263,6 +280,8 @@ def test_rtm_bf16_cli(tmp_path, binary, log, two_pass):
     assert r1.returncode == 0, r1.stdout + r1.stderr
     for line in open(prof):  # bytes of the bf16 shard: 2 per element, one (fused) or two reads per sweep
         rec = json.loads(line)
+        if rec.get("load"):
+            continue
         reads = 1 if rec["fused"] else 2
         assert abs(rec["rtm_GBps"] / rec["gflops"] - reads * 2 / 4) < 1e-4, rec  # (6 printed digits)
     r2 = _run_python(base + ["-o", str(tmp_path / "p.h5"), *case.files])
@@ -287,3 +306,43 @@ def test_partition_voxels_rejects_cpu_and_batches(tmp_path, binary):
     assert r.returncode == 1 and "partition_voxels" in r.stderr
     r = _run_native(binary, ["--batch_frames", "4", "--partition_voxels", *case.files])
     assert r.returncode == 1 and "partition_voxels" in r.stderr
+
+
+@pytest.mark.parametrize("sig", ["SIGTERM", "SIGKILL"])
+def test_module_entry_point_does_not_orphan_the_driver(tmp_path, binary, sig):
+    """torchrun / mpiexec stop workers with SIGTERM: cli.py forwards it to the native driver and waits (exit code
+    128 + 15); a parent killed outright (SIGKILL) takes the driver with it (PR_SET_PDEATHSIG from SART_PARENT_PID).
+    Either way no driver outlives its launcher holding a GPU or sitting in a collective."""
+    import signal
+    import time
+
+    import psutil
+
+    case = _case(tmp_path, nframes=1)
+    # rank 0 of a 2-rank world whose peer never comes: the driver blocks in the host rendezvous, like a rank whose
+    # peer has already failed
+    env = dict(_env(), RANK="0", WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    args = ["--use_cpu", "-o", str(tmp_path / "o.h5"), *case.files]
+    p = subprocess.Popen([sys.executable, "-m", "mpi_cuda_sartsolver_amd", *args], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    try:
+        child = None
+        for _ in range(300):  # the driver starts within seconds (python import + exec)
+            kids = psutil.Process(p.pid).children()
+            if kids:
+                child = kids[0]
+                break
+            time.sleep(0.1)
+        assert child is not None and child.exe().endswith("sartsolver"), "driver not started"
+        time.sleep(1.0)  # inside the rendezvous
+        assert p.poll() is None and child.is_running()
+        p.send_signal(getattr(signal, sig))
+        rc = p.wait(timeout=60)
+        if sig == "SIGTERM":
+            assert rc == 128 + signal.SIGTERM, rc  # forwarded, the driver's death reported like a shell does
+        gone, alive = psutil.wait_procs([child], timeout=30)
+        assert not alive, f"driver {child.pid} outlived its parent after {sig}"
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()

@@ -473,6 +473,29 @@ for step in "$@"; do
             run rocprof_r2_bf16_big 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_r2_bf16_big" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --rtm-dtype bf16 --npix 524288 --nvox 262144 --iters 20 &&
             run rocprof_r2_mfb64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_r2_mfb64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --rtm-dtype bf16 ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 ;;
+    r4info)  # scheduler limits that decide whether N processes' queues are all resident (no GPU work)
+      { echo "hws_max_conc_proc: $(cat /sys/module/amdgpu/parameters/hws_max_conc_proc 2>&1)";
+        echo "sched_policy: $(cat /sys/module/amdgpu/parameters/sched_policy 2>&1)";
+        echo "GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-unset}";
+        for d in /sys/class/kfd/kfd/topology/nodes/*; do
+          if grep -q "simd_count [1-9]" "$d/properties" 2>/dev/null; then
+            grep -E "num_cp_queues|num_sdma|simd_count|cu_per_simd|max_waves_per_simd|num_xcc|array_count|max_slots" "$d/properties"; fi
+        done; } > "$OUT/r4info.txt" 2>&1; cat "$OUT/r4info.txt" ;;
+    r4comm)  # P2P all-reduce at 4 and 8 processes on one GPU (forced p2p, gloo host side): bitwise + set-up time
+      for n in 4 8; do
+        SART_DIST_BACKEND=gloo SART_P2P=1 run comm_check_p2p_n$n 300 python -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29610 + n)) tools/comm_check.py \
+          --out "$OUT/comm_check_p2p_n$n.json" || exit 1
+        python -c "import json; d=json.load(open('$OUT/comm_check_p2p_n$n.json')); print('n$n', d['backend'], d['setup_s'], d['us_per_call'], all(r['exact'] or r['n']*4>2**21 for r in d['results'])); print(d['describe'])" | tee -a "$OUT/session.log"
+      done ;;
+    r4reh8)  # 8-rank one-GPU rehearsal of bench --gpus 8 (fused sweep per rank on 32 CUs + P2P auto vs staged)
+      run bench_share8_r4 300 python bench.py --gpus 8 --share-gpus --npix 16384 --steps 3 --warmup 1 --watchdog 300 ;;
+    r4reh8q1)  # the same with one hardware queue per process (8 queues in all: no queue over-subscription)
+      GPU_MAX_HW_QUEUES=1 run bench_share8_r4_q1 300 python bench.py --gpus 8 --share-gpus --npix 16384 --steps 3 --warmup 1 --watchdog 300 ;;
+    r4reh4) run bench_share4_r4 500 python bench.py --gpus 4 --share-gpus --npix 32768 --steps 3 --warmup 1 --watchdog 300 ;;
+    r4load) run load_bench 900 python tools/load_bench.py ;;
+    r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
