@@ -154,6 +154,8 @@ def main() -> int:
     ap.add_argument("--npix", type=int, default=65536, help="pixel rows per GPU (weak scaling)")
     ap.add_argument("--nvox", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=100, help="SART iterations per frame solve")
+    ap.add_argument("--ld", type=int, default=None,
+                    help="padded row length of the shard (default: choose_ld; geometry A/B runs with SART_FUSED_KW)")
     ap.add_argument("--variant", choices=["linear", "log"], default="linear")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--no-fused", action="store_true", help="use the two-pass kernels instead of the fused sweep")
@@ -253,7 +255,7 @@ def main() -> int:
         npix_total = args.npix * n if args.scaling == "weak" else args.npix
         blk = row_partition(npix_total, n, comm.rank)
         prob = make_problem(blk.size, args.nvox, row_offset=blk.offset, seed=args.seed, device=dev,
-                            storage=args.rtm_dtype)
+                            storage=args.rtm_dtype, ld=args.ld)
     params = SolverParams(max_iterations=args.iters, conv_tolerance=0.0)  # fixed iteration count
     lap = None
     if args.laplacian:

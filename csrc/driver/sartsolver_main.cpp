@@ -476,6 +476,9 @@ int main(int argc, char** argv) {
             const SolveInfo info = gpu ? engine->solve(frame.data(), x0, x.data()) : cpu->solve(frame.data(), x0, x.data());
             if (info.fallbacks)
                 std::cerr << "warning: fused sweep fell back " << info.fallbacks << " time(s)" << std::endl;
+            if (info.comm_fallbacks && rank == 0)
+                std::cerr << "warning: frame " << cur << ": device all-reduce timed out; re-solved on "
+                          << (dcomm ? dcomm->backend() : "the base communicator") << std::endl;
             if (info.nonfinite) std::cerr << "warning: frame " << cur << ": non-finite iterate, stopped" << std::endl;
             solution = x;
             if (cols) {  // gather the voxel blocks (zero-filled sum over ranks)

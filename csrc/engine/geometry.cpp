@@ -55,6 +55,11 @@ bool kw_allowed(int kw, bool narrow_slabs, bool forced = true) {
 // one kind where both exist.
 constexpr double kChipWidePenalty = 1.6;
 
+// Per-CU time of a chip-wide slab of kw lane-vectors relative to an XCD-local kw 8 slab. Chip-wide groups run
+// schedule 5 at kw 8 / 9 / 5 and schedule 8 (3 polls in flight, 4-step lag) at kw 6 / 7 (fused_sweep.hip
+// launch_rows), so their per-kw ratios differ from the XCD-local ones (narrow_slab_penalty).
+double chip_wide_penalty(int kw) { return kChipWidePenalty * narrow_slab_penalty(kw); }
+
 int xl_mode() {
     const char* e = std::getenv("SART_FUSED_XL");
     return (e && *e) ? std::atoi(e) : -1;  // -1 auto, 0 chip-wide only, 1 XCD-local only
@@ -77,7 +82,7 @@ V6Candidate v6_candidate(int64_t ld, int T, int kw, int num_cus, bool xl) {
     c.T = T, c.J = (int)J, c.kw = kw, c.xl = xl;
     // T = 2 (schedule 4) measured 4-10 % slower per byte than T = 1 (schedule 5) at equal slab / G
     // (131072 / 106496 columns, profiles/probe_r2_t1_sched5.jsonl); T = 4 and T = 1 tie at 65536
-    c.cost = (double)slab / c.I * (T == 2 ? 1.08 : 1.0) * narrow_slab_penalty(kw) * (xl ? 1.0 : kChipWidePenalty);
+    c.cost = (double)slab / c.I * (T == 2 ? 1.08 : 1.0) * (xl ? narrow_slab_penalty(kw) : chip_wide_penalty(kw));
     return c;
 }
 

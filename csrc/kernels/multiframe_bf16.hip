@@ -261,7 +261,9 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
 template <typename AT, int NG>
 constexpr int mf_fwd_min_waves() { return std::is_same<AT, float>::value ? 1 : (NG == 4 ? SART_MF_MINW_FWD : 1); }
 
-template <int NG, int DEPTH, int RT, int KB, typename AT = bf16_t, bool AS = false>
+// ABL: diagnostic ablations as in k_mf_backproject_b16_lds (bit 0 no MFMAs, bit 1 no split of A, bit 2 no X staging
+// and no barrier); 0 in every production launch.
+template <int NG, int DEPTH, int RT, int KB, typename AT = bf16_t, bool AS = false, int ABL = 0>
 __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forward_b16_lds(const AT* __restrict__ A, int64_t ld, int64_t nrows,
                                                             int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                             const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
@@ -364,8 +366,8 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
                 if constexpr (LATE) __builtin_amdgcn_sched_barrier(0);
                 stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);
             };
-            if constexpr (!LATE) stage_next();
-            const u32x4* xs = s_x[t & 1][0] + lofs;
+            if constexpr (!LATE && !(ABL & 4)) stage_next();
+            const u32x4* xs = s_x[(ABL & 4) ? 0 : (t & 1)][0] + lofs;
             u32x4* img = s_a[AS ? wave : 0];
             if constexpr (AS) {  // this wave's tile into its LDS image (swizzled slots)
 #pragma unroll
@@ -409,7 +411,10 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
                     u32x4 ah[RT], al[RT];
 #pragma unroll
                     for (int rt = 0; rt < RT; ++rt) {
-                        if constexpr (AS)
+                        if constexpr (AS && (ABL & 2)) {
+                            ah[rt] = frag16(rt, kb * 8 + g);
+                            al[rt] = frag16(rt, kb * 8 + 4 + g);
+                        } else if constexpr (AS)
                             split_a8(__builtin_shufflevector(frag16(rt, kb * 8 + g), frag16(rt, kb * 8 + 4 + g), 0, 1,
                                                              2, 3, 4, 5, 6, 7),
                                      ah[rt], al[rt]);
@@ -423,6 +428,13 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
                         xl[j] = xs[((kb * 2 + 1) * NG + j) * 64];
                     }
                     // product-major: consecutive MFMAs write different accumulators (no dependent chains)
+                    if constexpr ((ABL & 1) != 0) {
+#pragma unroll
+                        for (int j = 0; j < NG; ++j)
+#pragma unroll
+                            for (int rt = 0; rt < RT; ++rt)
+                                acc[rt][j][0] += __uint_as_float((al[rt][0] ^ ah[rt][3] ^ xh[j][1] ^ xl[j][2]) & 0x3fffffu);
+                    } else {
 #pragma unroll
                     for (int j = 0; j < NG; ++j)
 #pragma unroll
@@ -435,6 +447,7 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
                     for (int j = 0; j < NG; ++j)
 #pragma unroll
                         for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(ah[rt], xh[j], acc[rt][j]);
+                    }
                 } else if constexpr (AS) {
                     u32x4 af[RT];
 #pragma unroll
@@ -462,6 +475,7 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
                     }
                 }
             }
+            if constexpr (ABL & 4) return;
             if constexpr (LATE) stage_next();
             __syncthreads();
         };
@@ -580,7 +594,11 @@ constexpr int mf_bwd_min_waves() {
     return std::is_same<AT, float>::value ? (VT == 1 ? 2 : 1) : SART_MF_MINW_BWD;
 }
 
-template <int NG, int DEPTH, int VT, typename AT = bf16_t>
+// ABL (diagnostic ablations, tools/probe_mf_x3.py with SART_MF_ABL; 0 in every production launch): bit 0 drops the
+// MFMAs (each fragment folds into an accumulator with one VALU op, so no load is dead), bit 1 drops the split of A
+// (split-A: the raw bits stand for all three pieces), bit 2 drops the W staging (no LDS writes, no barrier: the step
+// re-reads the stage of step 0). Times of the ablated kernels locate the pipe that bounds a step.
+template <int NG, int DEPTH, int VT, typename AT = bf16_t, int ABL = 0>
 __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::is_same<AT, float>::value && VT == 1 ? 2 : 1))) void k_mf_backproject_b16_lds(const AT* __restrict__ A, int64_t ld,
                                                                 int64_t nrows32, const bf16_t* __restrict__ Wh,
                                                                 const bf16_t* __restrict__ Wl, int64_t ldw,
@@ -661,8 +679,8 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
                 if constexpr (LATE) __builtin_amdgcn_sched_barrier(0);
                 stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);
             };
-            if constexpr (!LATE) stage_next();
-            const u32x4* ws = s_w[t & 1][0] + lofs;
+            if constexpr (!LATE && !(ABL & 4)) stage_next();
+            const u32x4* ws = s_w[(ABL & 4) ? 0 : (t & 1)][0] + lofs;
             if constexpr (!A32 && SART_MF_XF_EARLY) {
                 // bf16: the step's W fragments are read once for all VT voxel tiles (the loop below re-read them per
                 // tile), all before the MFMAs (see k_mf_forward_b16_lds). Same accumulation order.
@@ -692,10 +710,18 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
                     // six products: every piece pair of combined weight >= 2^-16 (hi, mid, lo of A and of W),
                     // smallest first into the accumulator
                     u32x4 fh[4], fm[4], fl[4];
-                    split_phase3<0>(av[sl][vt], fh[0], fm[0], fl[0]);
-                    split_phase3<1>(av[sl][vt], fh[1], fm[1], fl[1]);
-                    split_phase3<2>(av[sl][vt], fh[2], fm[2], fl[2]);
-                    split_phase3<3>(av[sl][vt], fh[3], fm[3], fl[3]);
+                    if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+                        for (int p = 0; p < 4; ++p) {
+                            const u32x4 raw = {av[sl][vt][0][p], av[sl][vt][2][p], av[sl][vt][4][p], av[sl][vt][6][p]};
+                            fh[p] = raw, fm[p] = raw, fl[p] = raw;
+                        }
+                    } else {
+                        split_phase3<0>(av[sl][vt], fh[0], fm[0], fl[0]);
+                        split_phase3<1>(av[sl][vt], fh[1], fm[1], fl[1]);
+                        split_phase3<2>(av[sl][vt], fh[2], fm[2], fl[2]);
+                        split_phase3<3>(av[sl][vt], fh[3], fm[3], fl[3]);
+                    }
                     u32x4 wv[3][NG];
 #pragma unroll
                     for (int j = 0; j < NG; ++j)
@@ -708,7 +734,12 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
 #pragma unroll
                         for (int j = 0; j < NG; ++j)
 #pragma unroll
-                            for (int p = 0; p < 4; ++p) acc[vt][p][j] = mfma_b16(fa[p], wv[pl][j], acc[vt][p][j]);
+                            for (int p = 0; p < 4; ++p) {
+                                if constexpr ((ABL & 1) != 0)
+                                    acc[vt][p][j][0] += __uint_as_float((fa[p][0] ^ fa[p][3] ^ wv[pl][j][1]) & 0x3fffffu);
+                                else
+                                    acc[vt][p][j] = mfma_b16(fa[p], wv[pl][j], acc[vt][p][j]);
+                            }
                     };
                     prod(fh, 2);
                     prod(fm, 1);
@@ -730,6 +761,7 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
                     }
                 }
             }
+            if constexpr (ABL & 4) return;
             if constexpr (LATE) stage_next();
             __syncthreads();
         };
@@ -815,6 +847,25 @@ static void fwd_b16_t(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, in
                       int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
     constexpr bool A32 = std::is_same<AT, float>::value;
     constexpr bool CAN_AS = A32 || KB == 2;  // full 128-B row segments per step
+    if constexpr (A32 && NG == 4 && DEPTH == 3 && RT == 2 && KB == 1) {
+        const int abl = env_int("SART_MF_ABL", 0);  // diagnostics only (tools/probe_mf_abl.py)
+        if (abl > 0 && tl.as) {
+            auto go = [&](auto k) {
+                hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB, AT, true, decltype(k)::value>), grid,
+                                   dim3(256), 0, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
+            };
+            switch (abl & 7) {
+                case 1: go(std::integral_constant<int, 1>{}); break;
+                case 2: go(std::integral_constant<int, 2>{}); break;
+                case 3: go(std::integral_constant<int, 3>{}); break;
+                case 4: go(std::integral_constant<int, 4>{}); break;
+                case 5: go(std::integral_constant<int, 5>{}); break;
+                case 6: go(std::integral_constant<int, 6>{}); break;
+                default: go(std::integral_constant<int, 7>{}); break;
+            }
+            return;
+        }
+    }
     if constexpr (CAN_AS) {
         if (tl.as) {
             hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB, AT, true>), grid, dim3(256), 0, stream, A, ld,
@@ -939,6 +990,25 @@ template <int NG, int DEPTH, typename AT>
 static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows32,
                       const bf16_t* Wh, const bf16_t* Wl, int64_t ldw, int64_t rps, float* partial, int64_t vb0,
                       int64_t vend) {
+    if constexpr (std::is_same<AT, float>::value && NG == 4 && DEPTH == 2) {
+        const int abl = env_int("SART_MF_ABL", 0);  // diagnostics only (tools/probe_mf_abl.py; read per launch)
+        if (abl > 0 && vt == 1) {
+            auto go = [&](auto k) {
+                hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1, AT, decltype(k)::value>), grid, dim3(256), 0,
+                                   stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+            };
+            switch (abl & 7) {
+                case 1: go(std::integral_constant<int, 1>{}); break;
+                case 2: go(std::integral_constant<int, 2>{}); break;
+                case 3: go(std::integral_constant<int, 3>{}); break;
+                case 4: go(std::integral_constant<int, 4>{}); break;
+                case 5: go(std::integral_constant<int, 5>{}); break;
+                case 6: go(std::integral_constant<int, 6>{}); break;
+                default: go(std::integral_constant<int, 7>{}); break;
+            }
+            return;
+        }
+    }
     if (std::is_same<AT, float>::value || mf_b16_bwd_lds(16 * NG)) {
         if (vt == 2)
             hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2, AT>), grid, dim3(256), 0, stream, A, ld,

@@ -494,6 +494,23 @@ for step in "$@"; do
       GPU_MAX_HW_QUEUES=1 run bench_share8_r4_q1 300 python bench.py --gpus 8 --share-gpus --npix 16384 --steps 3 --warmup 1 --watchdog 300 ;;
     r4reh4) run bench_share4_r4 500 python bench.py --gpus 4 --share-gpus --npix 32768 --steps 3 --warmup 1 --watchdog 300 ;;
     r4load) run load_bench 900 python tools/load_bench.py ;;
+    r4abl) run probe_abl 300 python tools/probe_mf_abl.py &&
+           run probe_abl_2tb 300 python tools/probe_mf_abl.py 16384x262144 ;;
+    r4strong)  # strong scaling of the 64k x 64k headline over ranks sharing one GPU: 32768 / 16384 / 8192 rows per rank
+      for n in 2 4 8; do
+        timeout -k 10 300 python bench.py --gpus $n --share-gpus --scaling strong --steps 3 --warmup 1 --watchdog 240 \
+          > "$OUT/strong_n$n.log" 2>&1 || { echo "FATAL strong $n"; tail -n 30 "$OUT/strong_n$n.log"; exit 1; }
+        grep -h '^{' "$OUT/strong_n$n.log" >> "$OUT/strong.jsonl"
+        echo "=== strong n$n $(grep -h '^{' "$OUT/strong_n$n.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["allreduce_us_per_iter"], d["allreduce"][:60], d["allreduce_fallbacks"], d["fused_grid"])')" | tee -a "$OUT/session.log"
+      done ;;
+    r4cw)  # chip-wide row groups: per-CU rate by slab width kw (forced) at widths > 294912 (J must divide the width)
+      for spec in ${CW_SPECS:-8:303104 8:311296 8:327680 8:344064 7:301056 7:308224 7:315392 6:307200 6:313344 6:325632 9:304128 9:313344 9:331776 5:307200 5:327680}; do
+        k=${spec%%:*}; v=${spec#*:}
+        SART_FUSED_KW=$k timeout -k 10 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --ld $v --npix 32768 --no-selfcheck \
+          > "$OUT/cw_${k}_$v.log" 2>&1 || { echo "FATAL $spec"; tail -n 20 "$OUT/cw_${k}_$v.log"; exit 1; }
+        grep -h '^{' "$OUT/cw_${k}_$v.log" >> "$OUT/cw_kw.jsonl"
+        echo "=== cw kw$k $v $(grep -h '^{' "$OUT/cw_${k}_$v.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); g=d["fused_grid"]; print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], g, d["fused_schedule"], round(d["effective_hbm_TBps_per_gpu"]*1e3/g["workgroups"], 2), "GB/s/CU")')" | tee -a "$OUT/session.log"
+      done ;;
     r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Ablations of the split-A 64-frame back-projection (k_mf_backproject_b16_lds<4, 2, 1, float, ABL>, the 2tb preset's
+kernel): time per call with the MFMAs (1), the in-register split of A (2) and / or the W staging + barrier (4)
+removed (SART_MF_ABL = OR of the bits), on a synthetic fp32 shard (default 65536 x 65536). The bit whose removal
+moves the time names the pipe that bounds a step. One JSON line per variant."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM  # noqa: E402
+from mpi_cuda_sartsolver_amd.ops import hip  # noqa: E402
+from probe import timeit  # noqa: E402
+
+
+def main():
+    k = hip()
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream().cuda_stream
+    P, V = (int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "65536x65536").split("x"))
+    nf = 64
+    m = DenseRTM.synthetic(P, V, 0, seed=1, device=dev)
+    W = torch.rand((m.nrows_pad, nf), device=dev)
+    Wh = torch.zeros((2, nf, m.nrows_pad), dtype=torch.bfloat16, device=dev)
+    Wl = torch.zeros((nf, m.nrows_pad), dtype=torch.bfloat16, device=dev)
+    k.mf_split_w(W.data_ptr(), m.nrows_pad, nf, m.nrows_pad, Wh.data_ptr(), Wl.data_ptr(), s, True)
+    ns = k.mf_backproject_b16_num_splits(m.ld, P, True)
+    part = torch.zeros((ns, m.ld, nf), device=dev)
+    os.environ["SART_MF_X3_DEPTH"] = "2"
+    os.environ["SART_MF_X3_VT"] = "1"
+    for abl in [int(v) for v in os.environ.get("PROBE_ABL", "0,1,2,4,3,5,6,7,0").split(",")]:
+        os.environ["SART_MF_ABL"] = str(abl)
+        med, best = timeit(lambda: k.mf_backproject_x3(m.A.data_ptr(), m.ld, P, Wh.data_ptr(), Wl.data_ptr(),
+                                                       m.nrows_pad, ns, part.data_ptr(), s, nf), reps=7)
+        print(json.dumps(dict(op="mf_backproject_x3", abl=abl, no_mfma=bool(abl & 1), no_split=bool(abl & 2),
+                              no_w_lds=bool(abl & 4), nf=nf, P=P, V=V, nsplit=ns, ms=round(med, 4),
+                              GBps=round(m.nbytes / med / 1e6, 1))), flush=True)
+    # the split-A forward (k_mf_forward_b16_lds<4, 3, 2, 1, float, true, ABL>: A staged through LDS, X in LDS)
+    X = torch.rand((nf, m.ld), device=dev)
+    Xh = torch.empty((nf, m.ld), dtype=torch.bfloat16, device=dev)
+    Xl = torch.empty_like(Xh)
+    k.mf_split_x(X.data_ptr(), nf * m.ld, Xh.data_ptr(), Xl.data_ptr(), s, True)
+    nsf = k.mf_forward_num_splits(m.ld, m.nrows_pad)
+    Fo = torch.zeros((nsf, m.nrows_pad, nf), device=dev)
+    os.environ["SART_MF_X3_DEPTH"] = "3"
+    os.environ["SART_MF_X3_FWD"] = "2,1,as"
+    for abl in [int(v) for v in os.environ.get("PROBE_ABL", "0,1,2,4,3,5,6,7,0").split(",")]:
+        os.environ["SART_MF_ABL"] = str(abl)
+        med, best = timeit(lambda: k.mf_forward_x3(m.A.data_ptr(), m.ld, P, m.nrows_pad, Xh.data_ptr(), Xl.data_ptr(),
+                                                   Fo.data_ptr(), nsf, s, nf), reps=7)
+        print(json.dumps(dict(op="mf_forward_x3", abl=abl, no_mfma=bool(abl & 1), no_split=bool(abl & 2),
+                              no_x_lds=bool(abl & 4), nf=nf, P=P, V=V, nsplit=nsf, ms=round(med, 4),
+                              GBps=round(m.nbytes / med / 1e6, 1))), flush=True)
+    for key in ("SART_MF_ABL", "SART_MF_X3_DEPTH", "SART_MF_X3_FWD", "SART_MF_X3_VT"):
+        os.environ.pop(key, None)
+
+
+if __name__ == "__main__":
+    main()
