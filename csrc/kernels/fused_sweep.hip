@@ -164,12 +164,19 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
         const float4* __restrict__ a4 = reinterpret_cast<const float4*>(A) + col4;
         float4* ring = s_ring + (wave * TK) * 64 + lane;  // + slot * (4 * TK * 64) + q * 64
 
-        float4 xs[K], acc[K];
+        // Two-level back-projection sums like variant 6 at T = 1: a lane's chain would otherwise sum all nt * T rows of
+        // its group (the chip-wide fallback at 512 x 524288: 1.29x the two-pass error); folded into acc2 every fpass
+        // passes of UNR steps, ~sqrt(nt T) rows per chain
+        float4 xs[K], acc[K], acc2[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             xs[k] = x4[col4 + k * 64];
             acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            acc2[k] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
+        int64_t fpass = (int64_t)__builtin_ceilf(__builtin_sqrtf((float)(nt * T)) / (float)(UNR * T));
+        if (fpass < 1) fpass = 1;
+        int64_t fcount = 0;
         float4 fl[AH][TK];
         const int64_t tlast = ntiles - 1 - t_begin;  // unconditional clamped loads: see k_fused_sweep_rows
         auto load_tile = [&](float4(&dst)[TK], int64_t t) {
@@ -217,10 +224,21 @@ __global__ __launch_bounds__(kFusedThreads) void k_fused_sweep_lds(
             step(std::integral_constant<int, 1>{}, t0 + 1);
             step(std::integral_constant<int, 2>{}, t0 + 2);
             step(std::integral_constant<int, 3>{}, t0 + 3);
+            if (++fcount == fpass) {  // registers only
+                fcount = 0;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    add4(acc2[k], acc[k]);
+                    acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
         }
         float4* out = reinterpret_cast<float4*>(partial + (int64_t)gi * ld) + col4;
 #pragma unroll
-        for (int k = 0; k < K; ++k) out[k * 64] = acc[k];
+        for (int k = 0; k < K; ++k) {
+            add4(acc[k], acc2[k]);
+            out[k * 64] = acc[k];
+        }
     } else {
         const int n = J * T;
         bool failed = false;

@@ -785,6 +785,195 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
             }
 }
 
+// Split-A back-projection with the W fragments loaded straight into registers (no LDS, no barrier): every wave
+// runs its own pipeline. A lane's W fragment of frame group j and plane pl -- eight rows 8 g .. 8 g + 7 of frame
+// 16 j + i16 -- is one 16-byte load of the frame-major W plane, i.e. exactly the B operand of v_mfma_f32_16x16x32_bf16,
+// so the DEPTH-step register ring carries A and W alike. W bytes per step are 1.5x the A bytes of a wave (three
+// planes x NG groups x 1 KiB against 8 KiB of A), served by L2: the four waves of a workgroup read the same W
+// lines (FETCH_SIZE of the LDS kernels: W are L2 hits). MINW: waves per SIMD the register budget is cut for.
+// Same summation order per accumulator as k_mf_backproject_b16_lds<NG, DEPTH, 1, float>: bitwise equal output.
+template <int NG, int DEPTH, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_mf_backproject_x3_reg(const float* __restrict__ A, int64_t ld,
+                                                                      int64_t nrows32, const bf16_t* __restrict__ Wh,
+                                                                      const bf16_t* __restrict__ Wl, int64_t ldw,
+                                                                      int64_t rows_per_split, float* __restrict__ partial,
+                                                                      int64_t vb0, int64_t vend,
+                                                                      const int* __restrict__ skip) {
+    if (skip && *skip) return;
+    constexpr int NF = 16 * NG;
+    constexpr int RS = DEPTH + 1;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t vb = vb0 + (int64_t)blockIdx.x * 4 + wave;  // 64-voxel block of this wave
+    if (vb * 64 >= vend) return;                               // no barrier in this kernel: idle waves leave
+    const int g = lane >> 4, i16 = lane & 15;
+    const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
+    int64_t r_end = r_begin + rows_per_split;
+    if (r_end > nrows32) r_end = nrows32;
+    const float* __restrict__ ap = A + (r_begin + 8 * g) * ld + vb * 64 + 4 * i16;
+    const bf16_t* __restrict__ wp[3] = {Wh + (int64_t)i16 * ldw + r_begin + 8 * g,
+                                        Wh + (int64_t)NF * ldw + (int64_t)i16 * ldw + r_begin + 8 * g,
+                                        Wl + (int64_t)i16 * ldw + r_begin + 8 * g};  // hi, mid, lo planes
+
+    floatx4 acc[4][NG];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int j = 0; j < NG; ++j) acc[p][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 32 : 0;
+    if (nst > 0) {
+        u32x4 av[RS][8];
+        u32x4 wv[RS][3][NG];
+        auto load = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            const float* at = ap + t * 32 * ld;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                av[sl][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(at + j * ld));
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                for (int j = 0; j < NG; ++j)
+                    wv[sl][pl][j] = *reinterpret_cast<const u32x4*>(wp[pl] + (int64_t)j * 16 * ldw + t * 32);
+        };
+        [&]<int... Q>(std::integer_sequence<int, Q...>) {
+            (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
+        }(std::make_integer_sequence<int, DEPTH>{});
+        auto step = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
+            if (t >= nst) return;
+            u32x4 fh[4], fm[4], fl[4];
+            split_phase3<0>(av[sl], fh[0], fm[0], fl[0]);
+            split_phase3<1>(av[sl], fh[1], fm[1], fl[1]);
+            split_phase3<2>(av[sl], fh[2], fm[2], fl[2]);
+            split_phase3<3>(av[sl], fh[3], fm[3], fl[3]);
+            auto prod = [&](const u32x4(&fa)[4], int pl) {
+#pragma unroll
+                for (int j = 0; j < NG; ++j)
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) acc[p][j] = mfma_b16(fa[p], wv[sl][pl][j], acc[p][j]);
+            };
+            prod(fh, 2);
+            prod(fm, 1);
+            prod(fl, 0);
+            prod(fh, 1);
+            prod(fm, 0);
+            prod(fh, 0);
+        };
+        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+            }(std::make_integer_sequence<int, RS>{});
+        }
+    }
+    float* out = partial + (int64_t)blockIdx.y * ld * NF;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t v = vb * 64 + 4 * (g * 4 + q) + p;
+#pragma unroll
+            for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[p][j][q];
+        }
+}
+
+// Split-A forward with the X fragments loaded straight into registers (no LDS, no barrier), the counterpart of
+// k_mf_backproject_x3_reg: a lane's X fragment of frame group j and plane -- eight voxels (in the permuted k order of
+// k_mf_split_x with perm) of frame 16 j + r -- is one 16-byte load, the B operand as it is. A is loaded as fragments
+// (lane (r, g): the two 16-byte halves of row r's voxels 4 g .. and 16 + 4 g ..). Same products in the same order as
+// k_mf_forward_b16_lds<NG, DEPTH, RT, KB, float>: bitwise equal output.
+template <int NG, int DEPTH, int RT, int KB, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_mf_forward_x3_reg(const float* __restrict__ A, int64_t ld, int64_t nrows,
+                                                                  int64_t nrows_pad, const bf16_t* __restrict__ Xh,
+                                                                  const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
+                                                                  int64_t cols_per_split, const int* __restrict__ skip) {
+    if (skip && *skip) return;
+    constexpr int NF = 16 * NG;
+    constexpr int RS = DEPTH + 1;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * (16 * RT);
+    if (row0 >= nrows_pad) return;  // no barrier in this kernel
+    const int g = lane >> 4, r = lane & 15;
+    const int64_t c0 = (int64_t)blockIdx.y * cols_per_split;
+    const int64_t c1 = (c0 + cols_per_split < ld) ? c0 + cols_per_split : ld;
+    Fout += (int64_t)blockIdx.y * nrows_pad * NF;
+    const float* __restrict__ ap = A + (row0 + r) * ld + c0 + 4 * g;
+    const int64_t xo = (int64_t)r * ld + c0 + 8 * g;
+
+    floatx4 acc[RT][NG];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int j = 0; j < NG; ++j) acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int64_t nst = c1 > c0 ? (c1 - c0) / (32 * KB) : 0;
+    if (nst > 0) {
+        u32x8 a[RS][RT][KB];
+        u32x4 xh[RS][KB][NG], xl[RS][KB][NG];
+        auto load = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            const int64_t q = t * 32 * KB;
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int kb = 0; kb < KB; ++kb) {
+                    const float* p = ap + rt * 16 * ld + q + 32 * kb;
+                    const u32x4 h0 = *reinterpret_cast<const u32x4*>(p);
+                    const u32x4 h1 = *reinterpret_cast<const u32x4*>(p + 16);
+                    a[sl][rt][kb] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+                }
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    xh[sl][kb][j] = *reinterpret_cast<const u32x4*>(Xh + xo + (int64_t)j * 16 * ld + q + 32 * kb);
+                    xl[sl][kb][j] = *reinterpret_cast<const u32x4*>(Xl + xo + (int64_t)j * 16 * ld + q + 32 * kb);
+                }
+        };
+        [&]<int... Q>(std::integer_sequence<int, Q...>) {
+            (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
+        }(std::make_integer_sequence<int, DEPTH>{});
+        auto step = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
+            if (t >= nst) return;
+#pragma unroll
+            for (int kb = 0; kb < KB; ++kb) {
+                u32x4 ah[RT], al[RT];
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) split_a8(a[sl][rt][kb], ah[rt], al[rt]);
+#pragma unroll
+                for (int j = 0; j < NG; ++j)
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(al[rt], xh[sl][kb][j], acc[rt][j]);
+#pragma unroll
+                for (int j = 0; j < NG; ++j)
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(ah[rt], xl[sl][kb][j], acc[rt][j]);
+#pragma unroll
+                for (int j = 0; j < NG; ++j)
+#pragma unroll
+                    for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(ah[rt], xh[sl][kb][j], acc[rt][j]);
+            }
+        };
+        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+            }(std::make_integer_sequence<int, RS>{});
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NG; ++j)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t ra = row0 + rt * 16 + g * 4 + i;
+                if (ra < nrows) Fout[ra * NF + 16 * j + r] = acc[rt][j][i];
+            }
+}
+
 // ---------------------------------------------------------------------------------------------- launchers
 
 static void check_nf_b16(int nf, const char* what) {
@@ -847,6 +1036,19 @@ static void fwd_b16_t(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, in
                       int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
     constexpr bool A32 = std::is_same<AT, float>::value;
     constexpr bool CAN_AS = A32 || KB == 2;  // full 128-B row segments per step
+    if constexpr (A32) {
+        // SART_MF_X3_FWD_REG = 1 / 2: X fragments straight into registers (k_mf_forward_x3_reg), 1 or 2 waves per SIMD
+        const int reg = env_int("SART_MF_X3_FWD_REG", 0);
+        if (reg == 1 || reg == 2) {
+            if (reg == 2)
+                hipLaunchKernelGGL((k_mf_forward_x3_reg<NG, DEPTH, RT, KB, 2>), grid, dim3(256), 0, stream, A, ld, nrows,
+                                   nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
+            else
+                hipLaunchKernelGGL((k_mf_forward_x3_reg<NG, DEPTH, RT, KB, 1>), grid, dim3(256), 0, stream, A, ld, nrows,
+                                   nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
+            return;
+        }
+    }
     if constexpr (A32 && NG == 4 && DEPTH == 3 && RT == 2 && KB == 1) {
         const int abl = env_int("SART_MF_ABL", 0);  // diagnostics only (tools/probe_mf_abl.py)
         if (abl > 0 && tl.as) {
@@ -990,6 +1192,20 @@ template <int NG, int DEPTH, typename AT>
 static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows32,
                       const bf16_t* Wh, const bf16_t* Wl, int64_t ldw, int64_t rps, float* partial, int64_t vb0,
                       int64_t vend) {
+    if constexpr (std::is_same<AT, float>::value) {
+        // SART_MF_X3_BWD = reg1 / reg2: W fragments straight into registers (k_mf_backproject_x3_reg), 1 or 2 waves
+        // per SIMD (A/B against the LDS kernel; voxel tiles of 64: vt 1)
+        const char* e = std::getenv("SART_MF_X3_BWD");
+        if (e && std::strncmp(e, "reg", 3) == 0 && vt == 1) {
+            if (e[3] == '2')
+                hipLaunchKernelGGL((k_mf_backproject_x3_reg<NG, DEPTH, 2>), grid, dim3(256), 0, stream, A, ld, nrows32,
+                                   Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+            else
+                hipLaunchKernelGGL((k_mf_backproject_x3_reg<NG, DEPTH, 1>), grid, dim3(256), 0, stream, A, ld, nrows32,
+                                   Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+            return;
+        }
+    }
     if constexpr (std::is_same<AT, float>::value && NG == 4 && DEPTH == 2) {
         const int abl = env_int("SART_MF_ABL", 0);  // diagnostics only (tools/probe_mf_abl.py; read per launch)
         if (abl > 0 && vt == 1) {

@@ -448,9 +448,9 @@ def test_fault_injection_fallback_chain_chip_wide(dev, faults, expect):
     e2 = k.Engine(dev.index or 0, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld, k.local_comm(), cfg)
     x2, _ = e2.solve(g, None)
     x64 = sart_oracle_f64(rtm, g, 8)
-    # variant 3 (the emergency fallback) sums a row group's P / I rows per lane in one fp32 chain (no two-level
-    # fold): measured 1.29x the two-pass error here, the chip-wide variant 6 within the 1.25x of the other tests
-    assert _rel(x, x64) <= (1.5 if expect == 3 else 1.25) * _rel(x2, x64) + 1e-7
+    # variant 3 (the emergency fallback) folds its back-projection chains like variant 6 at T = 1 (before the fold:
+    # 1.29x the two-pass error here): the same 1.25x bound as every other fused path
+    assert _rel(x, x64) <= 1.25 * _rel(x2, x64) + 1e-7
 
 
 @pytest.mark.parametrize("fused", [True, False])

@@ -38,6 +38,21 @@ def main():
         print(json.dumps(dict(op="mf_backproject_x3", abl=abl, no_mfma=bool(abl & 1), no_split=bool(abl & 2),
                               no_w_lds=bool(abl & 4), nf=nf, P=P, V=V, nsplit=ns, ms=round(med, 4),
                               GBps=round(m.nbytes / med / 1e6, 1))), flush=True)
+    # the register-W back-projection (k_mf_backproject_x3_reg: no LDS, no barrier) against the LDS kernel
+    os.environ.pop("SART_MF_ABL", None)
+    ref = None
+    for bwd, depth in (("lds", 2), ("reg1", 2), ("reg1", 3), ("lds", 2)):
+        os.environ["SART_MF_X3_BWD"] = bwd
+        os.environ["SART_MF_X3_DEPTH"] = str(depth)
+        med, best = timeit(lambda: k.mf_backproject_x3(m.A.data_ptr(), m.ld, P, Wh.data_ptr(), Wl.data_ptr(),
+                                                       m.nrows_pad, ns, part.data_ptr(), s, nf), reps=7)
+        out = part.clone()
+        if ref is None:
+            ref = out
+        print(json.dumps(dict(op="mf_backproject_x3", variant=bwd, depth=depth, nf=nf, P=P, V=V, nsplit=ns,
+                              ms=round(med, 4), GBps=round(m.nbytes / med / 1e6, 1),
+                              bitwise_equal_lds=bool(torch.equal(out, ref)))), flush=True)
+    os.environ.pop("SART_MF_X3_BWD", None)
     # the split-A forward (k_mf_forward_b16_lds<4, 3, 2, 1, float, true, ABL>: A staged through LDS, X in LDS)
     X = torch.rand((nf, m.ld), device=dev)
     Xh = torch.empty((nf, m.ld), dtype=torch.bfloat16, device=dev)
@@ -54,7 +69,23 @@ def main():
         print(json.dumps(dict(op="mf_forward_x3", abl=abl, no_mfma=bool(abl & 1), no_split=bool(abl & 2),
                               no_x_lds=bool(abl & 4), nf=nf, P=P, V=V, nsplit=nsf, ms=round(med, 4),
                               GBps=round(m.nbytes / med / 1e6, 1))), flush=True)
-    for key in ("SART_MF_ABL", "SART_MF_X3_DEPTH", "SART_MF_X3_FWD", "SART_MF_X3_VT"):
+    # the register-X forward (k_mf_forward_x3_reg: no LDS, no barrier) against the LDS kernels
+    os.environ.pop("SART_MF_ABL", None)
+    ref = None
+    for tile, reg, depth in (("2,1,as", 0, 3), ("2,1", 1, 3), ("2,1", 2, 3), ("4,1", 1, 3), ("2,2", 1, 2),
+                             ("2,1", 1, 2), ("2,1,as", 0, 3)):
+        os.environ["SART_MF_X3_FWD"] = tile
+        os.environ["SART_MF_X3_FWD_REG"] = str(reg)
+        os.environ["SART_MF_X3_DEPTH"] = str(depth)
+        med, best = timeit(lambda: k.mf_forward_x3(m.A.data_ptr(), m.ld, P, m.nrows_pad, Xh.data_ptr(), Xl.data_ptr(),
+                                                   Fo.data_ptr(), nsf, s, nf), reps=7)
+        out = Fo.clone()
+        if ref is None:
+            ref = out
+        print(json.dumps(dict(op="mf_forward_x3", tile=tile, reg=reg, depth=depth, nf=nf, P=P, V=V, nsplit=nsf,
+                              ms=round(med, 4), GBps=round(m.nbytes / med / 1e6, 1),
+                              bitwise_equal_lds=bool(torch.equal(out, ref)))), flush=True)
+    for key in ("SART_MF_ABL", "SART_MF_X3_DEPTH", "SART_MF_X3_FWD", "SART_MF_X3_VT", "SART_MF_X3_FWD_REG"):
         os.environ.pop(key, None)
 
 
