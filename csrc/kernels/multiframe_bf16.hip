@@ -792,7 +792,10 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
 // planes x NG groups x 1 KiB against 8 KiB of A), served by L2: the four waves of a workgroup read the same W
 // lines (FETCH_SIZE of the LDS kernels: W are L2 hits). MINW: waves per SIMD the register budget is cut for.
 // Same summation order per accumulator as k_mf_backproject_b16_lds<NG, DEPTH, 1, float>: bitwise equal output.
-template <int NG, int DEPTH, int MINW>
+// PIPE: the split of step t + 1 runs beside the MFMAs of step t (one wave per SIMD: nothing else overlaps the split's
+// VALU work with the matrix pipe); its A arrived DEPTH - 1 steps earlier, so PIPE wants DEPTH >= 3.
+// WD (PIPE): W is loaded WD steps ahead in its own ring of WD + 1 slots (L2 hits: a shallower ring than A's).
+template <int NG, int DEPTH, int MINW, bool PIPE = false, int WD = DEPTH>
 __global__ __launch_bounds__(256, MINW) void k_mf_backproject_x3_reg(const float* __restrict__ A, int64_t ld,
                                                                       int64_t nrows32, const bf16_t* __restrict__ Wh,
                                                                       const bf16_t* __restrict__ Wl, int64_t ldw,
@@ -822,37 +825,49 @@ __global__ __launch_bounds__(256, MINW) void k_mf_backproject_x3_reg(const float
 
     const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 32 : 0;
     if (nst > 0) {
+        constexpr int WS = PIPE ? WD + 1 : RS;  // W ring slots
         u32x4 av[RS][8];
-        u32x4 wv[RS][3][NG];
-        auto load = [&](auto slc, int64_t t) {
-            constexpr int sl = decltype(slc)::value;
+        u32x4 wv[WS][3][NG];
+        auto load_a = [&](int sl, int64_t t) {
             const float* at = ap + t * 32 * ld;
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 av[sl][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(at + j * ld));
+        };
+        auto load_w = [&](int sl, int64_t t) {
 #pragma unroll
             for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
                 for (int j = 0; j < NG; ++j)
                     wv[sl][pl][j] = *reinterpret_cast<const u32x4*>(wp[pl] + (int64_t)j * 16 * ldw + t * 32);
         };
-        [&]<int... Q>(std::integer_sequence<int, Q...>) {
-            (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
-        }(std::make_integer_sequence<int, DEPTH>{});
-        auto step = [&](auto slc, int64_t t) {
+        auto load = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
-            load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
-            if (t >= nst) return;
-            u32x4 fh[4], fm[4], fl[4];
-            split_phase3<0>(av[sl], fh[0], fm[0], fl[0]);
-            split_phase3<1>(av[sl], fh[1], fm[1], fl[1]);
-            split_phase3<2>(av[sl], fh[2], fm[2], fl[2]);
-            split_phase3<3>(av[sl], fh[3], fm[3], fl[3]);
+            load_a(sl, t);
+            load_w(sl, t);
+        };
+        if constexpr (PIPE) {
+#pragma unroll
+            for (int d = 0; d < DEPTH; ++d) load_a(d, d < nst ? d : nst - 1);
+#pragma unroll
+            for (int d = 0; d < WD; ++d) load_w(d, d < nst ? d : nst - 1);
+        } else {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
+            }(std::make_integer_sequence<int, DEPTH>{});
+        }
+        auto split_all = [&](const u32x4(&v)[8], u32x4(&fh)[4], u32x4(&fm)[4], u32x4(&fl)[4]) {
+            split_phase3<0>(v, fh[0], fm[0], fl[0]);
+            split_phase3<1>(v, fh[1], fm[1], fl[1]);
+            split_phase3<2>(v, fh[2], fm[2], fl[2]);
+            split_phase3<3>(v, fh[3], fm[3], fl[3]);
+        };
+        auto mfmas = [&](const u32x4(&fh)[4], const u32x4(&fm)[4], const u32x4(&fl)[4], const u32x4(&w)[3][NG]) {
             auto prod = [&](const u32x4(&fa)[4], int pl) {
 #pragma unroll
                 for (int j = 0; j < NG; ++j)
 #pragma unroll
-                    for (int p = 0; p < 4; ++p) acc[p][j] = mfma_b16(fa[p], wv[sl][pl][j], acc[p][j]);
+                    for (int p = 0; p < 4; ++p) acc[p][j] = mfma_b16(fa[p], w[pl][j], acc[p][j]);
             };
             prod(fh, 2);
             prod(fm, 1);
@@ -861,10 +876,47 @@ __global__ __launch_bounds__(256, MINW) void k_mf_backproject_x3_reg(const float
             prod(fm, 0);
             prod(fh, 0);
         };
-        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
-            [&]<int... Q>(std::integer_sequence<int, Q...>) {
-                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
-            }(std::make_integer_sequence<int, RS>{});
+        if constexpr (!PIPE) {
+            auto step = [&](auto slc, int64_t t) {
+                constexpr int sl = decltype(slc)::value;
+                load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
+                if (t >= nst) return;
+                u32x4 fh[4], fm[4], fl[4];
+                split_all(av[sl], fh, fm, fl);
+                mfmas(fh, fm, fl, wv[sl]);
+            };
+            for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+                [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                    (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+                }(std::make_integer_sequence<int, RS>{});
+            }
+        } else {
+            u32x4 F[2][3][4];  // split of the current and of the next step
+            split_all(av[0], F[0][0], F[0][1], F[0][2]);
+            auto step = [&](auto qc, int64_t t) {
+                constexpr int q = decltype(qc)::value;
+                constexpr int sl = q % RS, ws = q % WS, fb = q % 2;
+                load_a((sl + DEPTH) % RS, t + DEPTH < nst ? t + DEPTH : nst - 1);
+                load_w((ws + WD) % WS, t + WD < nst ? t + WD : nst - 1);
+                if (t >= nst) return;
+                split_all(av[(sl + 1) % RS], F[fb ^ 1][0], F[fb ^ 1][1], F[fb ^ 1][2]);  // (clamped: always valid)
+                mfmas(F[fb][0], F[fb][1], F[fb][2], wv[ws]);
+                // interleave: one MFMA, then two VALU of the next step's split (176 VALU over 24 NG MFMAs)
+#pragma unroll
+                for (int i = 0; i < 24 * NG; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                }
+            };
+            constexpr auto gcd = [](int a, int b) { while (b) { const int c = a % b; a = b; b = c; } return a; };
+            constexpr int L2 = RS * WS / gcd(RS, WS);
+            constexpr int PASS = L2 % 2 == 0 ? L2 : 2 * L2;  // lcm(RS, WS, 2): static ring slots and split buffers
+            static_assert(PASS % RS == 0 && PASS % WS == 0 && PASS % 2 == 0, "static ring slots per pass");
+            for (int64_t t0 = 0; t0 < nst; t0 += PASS) {
+                [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                    (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+                }(std::make_integer_sequence<int, PASS>{});
+            }
         }
     }
     float* out = partial + (int64_t)blockIdx.y * ld * NF;
@@ -883,7 +935,9 @@ __global__ __launch_bounds__(256, MINW) void k_mf_backproject_x3_reg(const float
 // k_mf_split_x with perm) of frame 16 j + r -- is one 16-byte load, the B operand as it is. A is loaded as fragments
 // (lane (r, g): the two 16-byte halves of row r's voxels 4 g .. and 16 + 4 g ..). Same products in the same order as
 // k_mf_forward_b16_lds<NG, DEPTH, RT, KB, float>: bitwise equal output.
-template <int NG, int DEPTH, int RT, int KB, int MINW>
+// AS: A loaded in full 128-byte row segments (8 rows per instruction, the back-projection's load shape) and regrouped
+// into fragments through a wave-private LDS image (swizzled slots, as in k_mf_forward_b16_lds): still no barrier.
+template <int NG, int DEPTH, int RT, int KB, int MINW, bool AS = false>
 __global__ __launch_bounds__(256, MINW) void k_mf_forward_x3_reg(const float* __restrict__ A, int64_t ld, int64_t nrows,
                                                                   int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                                   const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
@@ -900,6 +954,13 @@ __global__ __launch_bounds__(256, MINW) void k_mf_forward_x3_reg(const float* __
     Fout += (int64_t)blockIdx.y * nrows_pad * NF;
     const float* __restrict__ ap = A + (row0 + r) * ld + c0 + 4 * g;
     const int64_t xo = (int64_t)r * ld + c0 + 8 * g;
+    constexpr int R16 = 32 * KB * 4 / 16;  // 16-B slots per row and step (AS)
+    constexpr int RPI = 64 / R16;          // rows per staging load instruction
+    constexpr int NI = 16 * RT / RPI;      // staging loads per step and wave
+    static_assert(!AS || R16 >= 8, "A staging needs full 128-B row segments");
+    __shared__ __attribute__((aligned(16))) u32x4 s_a[AS ? 4 : 1][AS ? 16 * RT * R16 : 1];
+    u32x4* img = s_a[AS ? wave : 0];
+    const float* __restrict__ asp = A + (row0 + lane / R16) * ld + c0 + (lane % R16) * 4;
 
     floatx4 acc[RT][NG];
 #pragma unroll
@@ -909,11 +970,17 @@ __global__ __launch_bounds__(256, MINW) void k_mf_forward_x3_reg(const float* __
 
     const int64_t nst = c1 > c0 ? (c1 - c0) / (32 * KB) : 0;
     if (nst > 0) {
-        u32x8 a[RS][RT][KB];
+        u32x8 a[AS ? 1 : RS][RT][KB];
+        u32x4 as_[AS ? RS : 1][NI];
         u32x4 xh[RS][KB][NG], xl[RS][KB][NG];
         auto load = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
             const int64_t q = t * 32 * KB;
+            if constexpr (AS) {
+#pragma unroll
+                for (int i = 0; i < NI; ++i)
+                    as_[sl][i] = *reinterpret_cast<const u32x4*>(asp + (int64_t)i * RPI * ld + q);
+            } else {
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -923,6 +990,7 @@ __global__ __launch_bounds__(256, MINW) void k_mf_forward_x3_reg(const float* __
                     const u32x4 h1 = *reinterpret_cast<const u32x4*>(p + 16);
                     a[sl][rt][kb] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
                 }
+            }
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
@@ -938,11 +1006,26 @@ __global__ __launch_bounds__(256, MINW) void k_mf_forward_x3_reg(const float* __
             constexpr int sl = decltype(slc)::value;
             load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
             if (t >= nst) return;
+            if constexpr (AS) {  // this wave's tile into its own LDS image (in-order LDS queue: no barrier)
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    const int row = i * RPI + lane / R16;
+                    img[row * R16 + ((lane % R16) ^ (row & 7))] = as_[sl][i];
+                }
+            }
+            auto frag16 = [&](int rt, int seg) { return img[(rt * 16 + r) * R16 + (seg ^ (r & 7))]; };
 #pragma unroll
             for (int kb = 0; kb < KB; ++kb) {
                 u32x4 ah[RT], al[RT];
 #pragma unroll
-                for (int rt = 0; rt < RT; ++rt) split_a8(a[sl][rt][kb], ah[rt], al[rt]);
+                for (int rt = 0; rt < RT; ++rt) {
+                    if constexpr (AS)
+                        split_a8(__builtin_shufflevector(frag16(rt, kb * 8 + g), frag16(rt, kb * 8 + 4 + g), 0, 1, 2, 3,
+                                                         4, 5, 6, 7),
+                                 ah[rt], al[rt]);
+                    else
+                        split_a8(a[sl][rt][kb], ah[rt], al[rt]);
+                }
 #pragma unroll
                 for (int j = 0; j < NG; ++j)
 #pragma unroll
@@ -1040,12 +1123,17 @@ static void fwd_b16_t(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, in
         // SART_MF_X3_FWD_REG = 1 / 2: X fragments straight into registers (k_mf_forward_x3_reg), 1 or 2 waves per SIMD
         const int reg = env_int("SART_MF_X3_FWD_REG", 0);
         if (reg == 1 || reg == 2) {
-            if (reg == 2)
-                hipLaunchKernelGGL((k_mf_forward_x3_reg<NG, DEPTH, RT, KB, 2>), grid, dim3(256), 0, stream, A, ld, nrows,
-                                   nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
-            else
-                hipLaunchKernelGGL((k_mf_forward_x3_reg<NG, DEPTH, RT, KB, 1>), grid, dim3(256), 0, stream, A, ld, nrows,
-                                   nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
+            auto go = [&](auto mw, auto as) {
+                hipLaunchKernelGGL((k_mf_forward_x3_reg<NG, DEPTH, RT, KB, decltype(mw)::value, decltype(as)::value>),
+                                   grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
+            };
+            using W1 = std::integral_constant<int, 1>;
+            using W2 = std::integral_constant<int, 2>;
+            if (tl.as) {
+                if (reg == 2) go(W2{}, std::true_type{}); else go(W1{}, std::true_type{});
+            } else {
+                if (reg == 2) go(W2{}, std::false_type{}); else go(W1{}, std::false_type{});
+            }
             return;
         }
     }
@@ -1195,9 +1283,16 @@ static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_
     if constexpr (std::is_same<AT, float>::value) {
         // SART_MF_X3_BWD = reg1 / reg2: W fragments straight into registers (k_mf_backproject_x3_reg), 1 or 2 waves
         // per SIMD (A/B against the LDS kernel; voxel tiles of 64: vt 1)
+        // regp: the pipelined form (the next step's split beside this step's MFMAs)
         const char* e = std::getenv("SART_MF_X3_BWD");
         if (e && std::strncmp(e, "reg", 3) == 0 && vt == 1) {
-            if (e[3] == '2')
+            if (e[3] == 'p' && e[4] == '2')  // regp2: W two steps ahead
+                hipLaunchKernelGGL((k_mf_backproject_x3_reg<NG, DEPTH, 1, true, 2>), grid, dim3(256), 0, stream, A, ld,
+                                   nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+            else if (e[3] == 'p')  // regp: W one step ahead
+                hipLaunchKernelGGL((k_mf_backproject_x3_reg<NG, DEPTH, 1, true, 1>), grid, dim3(256), 0, stream, A, ld,
+                                   nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+            else if (e[3] == '2')
                 hipLaunchKernelGGL((k_mf_backproject_x3_reg<NG, DEPTH, 2>), grid, dim3(256), 0, stream, A, ld, nrows32,
                                    Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
             else

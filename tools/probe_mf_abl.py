@@ -41,7 +41,7 @@ def main():
     # the register-W back-projection (k_mf_backproject_x3_reg: no LDS, no barrier) against the LDS kernel
     os.environ.pop("SART_MF_ABL", None)
     ref = None
-    for bwd, depth in (("lds", 2), ("reg1", 2), ("reg1", 3), ("lds", 2)):
+    for bwd, depth in (("lds", 2), ("reg1", 2), ("reg1", 3), ("regp", 3), ("regp2", 3), ("lds", 2)):
         os.environ["SART_MF_X3_BWD"] = bwd
         os.environ["SART_MF_X3_DEPTH"] = str(depth)
         med, best = timeit(lambda: k.mf_backproject_x3(m.A.data_ptr(), m.ld, P, Wh.data_ptr(), Wl.data_ptr(),
@@ -73,7 +73,7 @@ def main():
     os.environ.pop("SART_MF_ABL", None)
     ref = None
     for tile, reg, depth in (("2,1,as", 0, 3), ("2,1", 1, 3), ("2,1", 2, 3), ("4,1", 1, 3), ("2,2", 1, 2),
-                             ("2,1", 1, 2), ("2,1,as", 0, 3)):
+                             ("2,1", 1, 2), ("2,1,as", 1, 3), ("2,1,as", 2, 3), ("4,1,as", 1, 3), ("2,1,as", 0, 3)):
         os.environ["SART_MF_X3_FWD"] = tile
         os.environ["SART_MF_X3_FWD_REG"] = str(reg)
         os.environ["SART_MF_X3_DEPTH"] = str(depth)
