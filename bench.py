@@ -204,9 +204,10 @@ def main() -> int:
                 # over-subscribe it and the scheduler time-slices the processes, so every P2P all-reduce waits out a
                 # time slice for a descheduled peer (10.3 ms per call, 83.7 it/s; with 1 queue per rank 111 us,
                 # 172.4 it/s: profiles/bench_r4_n8_rehearsal_one_gpu_q{4,1}.json). One rank per GPU is unaffected.
+                # The cap is a ceiling on whatever the environment sets (the GPU boxes export HIP's default, 4).
                 per_gpu = -(-args.gpus // max(ndev, 1))
-                if "GPU_MAX_HW_QUEUES" not in os.environ:
-                    env_extra["GPU_MAX_HW_QUEUES"] = str(max(1, min(4, 12 // per_gpu)))
+                have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+                env_extra["GPU_MAX_HW_QUEUES"] = str(max(1, min(have, 12 // per_gpu)))
         return self_launch(args.gpus, sys.argv[1:], env_extra)
     if (world or 1) != args.gpus:
         print(f"bench: --gpus {args.gpus} but the launcher started {world or 1} rank(s)", file=sys.stderr)

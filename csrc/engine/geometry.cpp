@@ -57,8 +57,15 @@ constexpr double kChipWidePenalty = 1.6;
 
 // Per-CU time of a chip-wide slab of kw lane-vectors relative to an XCD-local kw 8 slab. Chip-wide groups run
 // schedule 5 at kw 8 / 9 / 5 and schedule 8 (3 polls in flight, 4-step lag) at kw 6 / 7 (fused_sweep.hip
-// launch_rows), so their per-kw ratios differ from the XCD-local ones (narrow_slab_penalty).
-double chip_wide_penalty(int kw) { return kChipWidePenalty * narrow_slab_penalty(kw); }
+// launch_rows), and every step gathers J granules through memory, so the wider slabs (fewer granules per byte)
+// stream faster there than their XCD-local ratios (narrow_slab_penalty) say. Measured per CU at 301056 ... 344064
+// voxels (profiles/cw_r4_kw.jsonl, forced kw): kw 9 23.3-24.1, kw 7 23.5-23.7 (I = 5), kw 8 21.3-21.8, kw 6
+// 20.7-20.9, kw 5 15.4-20.0 GB/s; scaled so that kw 8 keeps kChipWidePenalty against XCD-local slabs.
+// Grids of 248 or more chip-wide workgroups measured 3-12 % slower per CU (kw 7 / 8 / 9 at 252: 20.6 / 20.1 / 23.3).
+double chip_wide_penalty(int kw, int workgroups) {
+    const double per_kw = kw == 9 ? 0.90 : (kw == 7 ? 0.91 : (kw == 8 ? 1.0 : (kw == 6 ? 1.03 : 1.2)));
+    return kChipWidePenalty * per_kw * (workgroups >= 248 ? 1.08 : 1.0);
+}
 
 int xl_mode() {
     const char* e = std::getenv("SART_FUSED_XL");
@@ -82,7 +89,7 @@ V6Candidate v6_candidate(int64_t ld, int T, int kw, int num_cus, bool xl) {
     c.T = T, c.J = (int)J, c.kw = kw, c.xl = xl;
     // T = 2 (schedule 4) measured 4-10 % slower per byte than T = 1 (schedule 5) at equal slab / G
     // (131072 / 106496 columns, profiles/probe_r2_t1_sched5.jsonl); T = 4 and T = 1 tie at 65536
-    c.cost = (double)slab / c.I * (T == 2 ? 1.08 : 1.0) * (xl ? narrow_slab_penalty(kw) : chip_wide_penalty(kw));
+    c.cost = (double)slab / c.I * (T == 2 ? 1.08 : 1.0) * (xl ? narrow_slab_penalty(kw) : chip_wide_penalty(kw, c.I * c.J));
     return c;
 }
 

@@ -1057,6 +1057,129 @@ __global__ __launch_bounds__(256, MINW) void k_mf_forward_x3_reg(const float* __
             }
 }
 
+// Split-A back-projection, software-pipelined: the split of step t + 1's A (VALU) is issued between the MFMAs of step t,
+// at one wave per SIMD. The LDS kernel (k_mf_backproject_b16_lds, two waves per SIMD) runs the split and the MFMAs of a
+// step back to back, and ablations show they barely overlap: 64 frames, 64k x 64k, 3.32 ms per call, 2.30 ms without
+// the split, 1.72 ms without the MFMAs (profiles/ablation_r4_mf64_split_a.jsonl). W is staged through two LDS stages
+// as there (one barrier per step: the four waves share W). Same products in the same order per accumulator: bitwise
+// the LDS kernel's output.
+template <int NG, int DEPTH>
+__global__ __launch_bounds__(256, 1) void k_mf_backproject_x3_pipe(const float* __restrict__ A, int64_t ld,
+                                                                    int64_t nrows32, const bf16_t* __restrict__ Wh,
+                                                                    const bf16_t* __restrict__ Wl, int64_t ldw,
+                                                                    int64_t rows_per_split, float* __restrict__ partial,
+                                                                    int64_t vb0, int64_t vend,
+                                                                    const int* __restrict__ skip) {
+    if (skip && *skip) return;
+    constexpr int NF = 16 * NG;
+    constexpr int RS = DEPTH + 1;
+    constexpr int C = 3 * NG;            // 1 KiB W pieces per step (hi, mid, lo planes x NG groups)
+    constexpr int XQ = (C + 3) / 4;      // pieces per wave (clamped: a duplicate load writes equal data)
+    __shared__ __attribute__((aligned(16))) u32x4 s_w[2][C][64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int64_t vb = vb0 + (int64_t)blockIdx.x * 4 + wave;
+    const bool live = vb * 64 < vend;
+    if (!live) vb = vend / 64 - 1;  // stages W and takes the barriers, stores nothing
+    const int g = lane >> 4, i16 = lane & 15;
+    const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
+    int64_t r_end = r_begin + rows_per_split;
+    if (r_end > nrows32) r_end = nrows32;
+    const float* __restrict__ ap = A + (r_begin + 8 * g) * ld + vb * 64 + 4 * i16;
+    const int64_t wo = (int64_t)i16 * ldw + r_begin + 8 * g;
+    auto plane_ptr = [&](int pl) { return pl == 2 ? Wl : Wh + (int64_t)pl * NF * ldw; };
+
+    floatx4 acc[4][NG];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int j = 0; j < NG; ++j) acc[p][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 32 : 0;  // uniform for the workgroup
+    if (nst > 0) {
+        u32x4 av[RS][8];
+        u32x4 wq[RS][XQ];
+        auto piece = [&](int i) { return wave * XQ + i < C ? wave * XQ + i : C - 1; };  // piece = plane * NG + j
+        auto load = [&](int sl, int64_t t) {
+            const float* at = ap + t * 32 * ld;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                av[sl][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(at + j * ld));
+#pragma unroll
+            for (int i = 0; i < XQ; ++i) {
+                const int pc = piece(i), j = pc % NG, plane = pc / NG;
+                wq[sl][i] = *reinterpret_cast<const u32x4*>(plane_ptr(plane) + wo + (int64_t)j * 16 * ldw + t * 32);
+            }
+        };
+        auto stage = [&](int sl, int64_t t) {
+#pragma unroll
+            for (int i = 0; i < XQ; ++i) s_w[t & 1][piece(i)][lane] = wq[sl][i];
+        };
+        auto split_all = [&](const u32x4(&v)[8], u32x4(&F)[3][4]) {
+            split_phase3<0>(v, F[0][0], F[1][0], F[2][0]);
+            split_phase3<1>(v, F[0][1], F[1][1], F[2][1]);
+            split_phase3<2>(v, F[0][2], F[1][2], F[2][2]);
+            split_phase3<3>(v, F[0][3], F[1][3], F[2][3]);
+        };
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) load(d, d < nst ? d : nst - 1);
+        stage(0, 0);
+        __syncthreads();
+        u32x4 F[2][3][4];  // [buffer][hi, mid, lo][phase]: the split of this step and of the next
+        split_all(av[0], F[0]);
+        auto step = [&](auto qc, int64_t t) {
+            constexpr int q = decltype(qc)::value;
+            constexpr int sl = q % RS, fb = q % 2;
+            load((sl + DEPTH) % RS, t + DEPTH < nst ? t + DEPTH : nst - 1);
+            if (t >= nst) return;  // uniform for the workgroup
+            const u32x4* ws = s_w[t & 1][0] + lane;
+            u32x4 wv[3][NG];
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+                for (int j = 0; j < NG; ++j) wv[pl][j] = ws[(pl * NG + j) * 64];
+            split_all(av[(sl + 1) % RS], F[fb ^ 1]);  // the next step's A (clamped loads: always valid data)
+            auto prod = [&](int pa, int pl) {
+#pragma unroll
+                for (int j = 0; j < NG; ++j)
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) acc[p][j] = mfma_b16(F[fb][pa][p], wv[pl][j], acc[p][j]);
+            };
+            prod(0, 2);  // (hi, lo), (mid, mid), (lo, hi), (hi, mid), (mid, hi), (hi, hi): smallest first
+            prod(1, 1);
+            prod(2, 0);
+            prod(0, 1);
+            prod(1, 0);
+            prod(0, 0);
+            // the step's W fragment reads first, then one MFMA / two VALU of the next step's split in turn
+            __builtin_amdgcn_sched_group_barrier(0x100, 3 * NG, 0);
+#pragma unroll
+            for (int i = 0; i < 24 * NG; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            stage((sl + 1) % RS, t + 1);  // W of step t + 1 into the other stage (its readers passed the last barrier)
+            __syncthreads();
+        };
+        constexpr int PASS = RS % 2 == 0 ? RS : 2 * RS;  // static ring slots and split buffers per pass
+        for (int64_t t0 = 0; t0 < nst; t0 += PASS) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+            }(std::make_integer_sequence<int, PASS>{});
+        }
+    }
+    if (!live) return;
+    float* out = partial + (int64_t)blockIdx.y * ld * NF;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+            const int64_t v = vb * 64 + 4 * (g * 4 + qq) + p;
+#pragma unroll
+            for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[p][j][qq];
+        }
+}
+
 // ---------------------------------------------------------------------------------------------- launchers
 
 static void check_nf_b16(int nf, const char* what) {
@@ -1285,6 +1408,15 @@ static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_
         // per SIMD (A/B against the LDS kernel; voxel tiles of 64: vt 1)
         // regp: the pipelined form (the next step's split beside this step's MFMAs)
         const char* e = std::getenv("SART_MF_X3_BWD");
+        if (e && std::strncmp(e, "pipe", 4) == 0 && vt == 1) {  // pipe2 / pipe3: ring depth 2 / 3
+            if (e[4] == '3')
+                hipLaunchKernelGGL((k_mf_backproject_x3_pipe<NG, 3>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
+                                   ldw, rps, partial, vb0, vend, g_mf_skip);
+            else
+                hipLaunchKernelGGL((k_mf_backproject_x3_pipe<NG, 2>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
+                                   ldw, rps, partial, vb0, vend, g_mf_skip);
+            return;
+        }
         if (e && std::strncmp(e, "reg", 3) == 0 && vt == 1) {
             if (e[3] == 'p' && e[4] == '2')  // regp2: W two steps ahead
                 hipLaunchKernelGGL((k_mf_backproject_x3_reg<NG, DEPTH, 1, true, 2>), grid, dim3(256), 0, stream, A, ld,

@@ -21,8 +21,9 @@ def _port():
 
 def _run(nproc, out, extra, script="dist_check.py", **env_extra):
     env = dict(os.environ, PYTHONPATH=ROOT, SART_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", **env_extra)
-    if nproc > 2 and "GPU_MAX_HW_QUEUES" not in os.environ:  # N ranks x queues within the 24 the GPU maps (bench.py)
-        env["GPU_MAX_HW_QUEUES"] = str(max(1, min(4, 12 // nproc)))
+    if nproc > 2:  # N ranks x queues within the 24 the GPU maps (a ceiling on the box's default 4, as bench.py)
+        have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+        env["GPU_MAX_HW_QUEUES"] = str(max(1, min(have, 12 // nproc)))
     path = os.path.join(ROOT, "tools", script)
     if nproc == 1:
         cmd = [sys.executable, path, "--out", out, *extra]

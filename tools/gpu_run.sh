@@ -512,6 +512,7 @@ for step in "$@"; do
         echo "=== cw kw$k $v $(grep -h '^{' "$OUT/cw_${k}_$v.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); g=d["fused_grid"]; print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], g, d["fused_schedule"], round(d["effective_hbm_TBps_per_gpu"]*1e3/g["workgroups"], 2), "GB/s/CU")')" | tee -a "$OUT/session.log"
       done ;;
     r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    r4bench) run bench_r4 300 python bench.py --steps 20 --warmup 5 ;;
     r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

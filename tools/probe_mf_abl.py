@@ -41,9 +41,11 @@ def main():
     # the register-W back-projection (k_mf_backproject_x3_reg: no LDS, no barrier) against the LDS kernel
     os.environ.pop("SART_MF_ABL", None)
     ref = None
-    for bwd, depth in (("lds", 2), ("reg1", 2), ("reg1", 3), ("regp", 3), ("regp2", 3), ("lds", 2)):
+    for bwd, depth in [tuple(v.split(":")) for v in os.environ.get(
+            "PROBE_BWD", "lds:2,pipe2:2,pipe3:2,reg1:2,lds:2").split(",")]:
         os.environ["SART_MF_X3_BWD"] = bwd
         os.environ["SART_MF_X3_DEPTH"] = str(depth)
+        part.zero_()
         med, best = timeit(lambda: k.mf_backproject_x3(m.A.data_ptr(), m.ld, P, Wh.data_ptr(), Wl.data_ptr(),
                                                        m.nrows_pad, ns, part.data_ptr(), s, nf), reps=7)
         out = part.clone()
