@@ -441,19 +441,22 @@ PYBIND11_MODULE(_sart_hip, m) {
           py::arg("a32") = false);
     m.def("mf_backproject_b16_vox_align", &sart::mf_backproject_b16_vox_align, py::arg("ld"), py::arg("a32") = false);
     m.def("mf_forward_x3", [](uintptr_t A, int64_t ld, int64_t nrows, int64_t nrows_pad, uintptr_t Xh, uintptr_t Xl,
-                              uintptr_t Fout, int nsplit, uintptr_t stream, int nf) {
+                              uintptr_t Fout, int nsplit, uintptr_t stream, int nf, bool xblk) {
         sart::launch_mf_forward_x3(P<const float>(A), ld, nrows, nrows_pad, P<const sart::bf16_t>(Xh),
-                                   P<const sart::bf16_t>(Xl), P<float>(Fout), nsplit, nf, S(stream));
-    });
+                                   P<const sart::bf16_t>(Xl), P<float>(Fout), nsplit, nf, S(stream), xblk);
+    }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("nrows_pad"), py::arg("Xh"), py::arg("Xl"),
+       py::arg("Fout"), py::arg("nsplit"), py::arg("stream"), py::arg("nf"), py::arg("xblk") = false);
     m.def("mf_backproject_x3", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t Wh, uintptr_t Wl, int64_t ldw,
                                   int nsplit, uintptr_t partial, uintptr_t stream, int nf, int64_t v0, int64_t v1) {
         sart::launch_mf_backproject_x3(P<const float>(A), ld, nrows, P<const sart::bf16_t>(Wh),
                                        P<const sart::bf16_t>(Wl), ldw, nsplit, P<float>(partial), nf, S(stream), v0, v1);
     }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("Wh"), py::arg("Wl"), py::arg("ldw"), py::arg("nsplit"),
        py::arg("partial"), py::arg("stream"), py::arg("nf") = 16, py::arg("v0") = 0, py::arg("v1") = -1);
-    m.def("mf_split_x", [](uintptr_t X, int64_t n, uintptr_t hi, uintptr_t lo, uintptr_t stream, bool perm) {
-        sart::launch_mf_split_x(P<const float>(X), n, P<sart::bf16_t>(hi), P<sart::bf16_t>(lo), S(stream), perm);
-    }, py::arg("X"), py::arg("n"), py::arg("hi"), py::arg("lo"), py::arg("stream"), py::arg("perm") = false);
+    m.def("mf_split_x", [](uintptr_t X, int64_t n, uintptr_t hi, uintptr_t lo, uintptr_t stream, bool perm,
+                           int64_t ld) {
+        sart::launch_mf_split_x(P<const float>(X), n, P<sart::bf16_t>(hi), P<sart::bf16_t>(lo), S(stream), perm, ld);
+    }, py::arg("X"), py::arg("n"), py::arg("hi"), py::arg("lo"), py::arg("stream"), py::arg("perm") = false,
+       py::arg("ld") = 0);
     m.def("mf_split_w", [](uintptr_t W, int64_t nrows_pad, int nf, int64_t ldw, uintptr_t hi, uintptr_t lo,
                            uintptr_t stream, bool three) {
         sart::launch_mf_split_w(P<const float>(W), nrows_pad, nf, ldw, P<sart::bf16_t>(hi), P<sart::bf16_t>(lo),
@@ -461,10 +464,11 @@ PYBIND11_MODULE(_sart_hip, m) {
     }, py::arg("W"), py::arg("nrows_pad"), py::arg("nf"), py::arg("ldw"), py::arg("hi"), py::arg("lo"),
        py::arg("stream"), py::arg("three") = false);
     m.def("mf_forward_b16", [](uintptr_t A, int64_t ld, int64_t nrows, int64_t nrows_pad, uintptr_t Xh, uintptr_t Xl,
-                               uintptr_t Fout, int nsplit, uintptr_t stream, int nf) {
+                               uintptr_t Fout, int nsplit, uintptr_t stream, int nf, bool xblk) {
         sart::launch_mf_forward_b16(P<const sart::bf16_t>(A), ld, nrows, nrows_pad, P<const sart::bf16_t>(Xh),
-                                    P<const sart::bf16_t>(Xl), P<float>(Fout), nsplit, nf, S(stream));
-    });
+                                    P<const sart::bf16_t>(Xl), P<float>(Fout), nsplit, nf, S(stream), xblk);
+    }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("nrows_pad"), py::arg("Xh"), py::arg("Xl"),
+       py::arg("Fout"), py::arg("nsplit"), py::arg("stream"), py::arg("nf"), py::arg("xblk") = false);
     m.def("mf_backproject_b16", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t Wh, uintptr_t Wl, int64_t ldw,
                                    int nsplit, uintptr_t partial, uintptr_t stream, int nf, int64_t v0, int64_t v1) {
         sart::launch_mf_backproject_b16(P<const sart::bf16_t>(A), ld, nrows, P<const sart::bf16_t>(Wh),

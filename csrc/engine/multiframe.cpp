@@ -43,6 +43,10 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
         x3_ = m != 0;
     }
     split_ = bf16_ || x3_;
+    if (split_) {  // X planes blocked [ld / 32][nf][32] for the forward (SART_MF_XBLK=0: frame-major, A/B runs)
+        const char* e = std::getenv("SART_MF_XBLK");
+        xblk_ = !(e && *e && std::atoi(e) == 0);
+    }
     set_device();
     hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
     hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -139,13 +143,13 @@ void MultiFrameEngine::set_laplacian(const int64_t* row_ptr, const int32_t* col,
 
 void MultiFrameEngine::forward() {
     if (split_) {
-        launch_mf_split_x(X_.get(), (int64_t)nf_ * ld_, Xh_.get(), Xl_.get(), stream_, x3_);
+        launch_mf_split_x(X_.get(), (int64_t)nf_ * ld_, Xh_.get(), Xl_.get(), stream_, x3_, xblk_ ? ld_ : 0);
         if (bf16_)
             launch_mf_forward_b16(static_cast<const bf16_t*>(A_), ld_, P_, Pp_, Xh_.get(), Xl_.get(), Fs_.get(), nsf_,
-                                  nf_, stream_);
+                                  nf_, stream_, xblk_);
         else
             launch_mf_forward_x3(static_cast<const float*>(A_), ld_, P_, Pp_, Xh_.get(), Xl_.get(), Fs_.get(), nsf_,
-                                 nf_, stream_);
+                                 nf_, stream_, xblk_);
     } else {
         launch_mf_forward(static_cast<const float*>(A_), ld_, P_, Pp_, X_.get(), ld_, Fs_.get(), nsf_, nf_, stream_);
     }

@@ -65,6 +65,7 @@ class MultiFrameEngine {
     bool bf16_ = false;
     bool x3_ = false;     // fp32 shard on the bf16 matrix cores (EngineConfig::mf_split_a)
     bool split_ = false;  // X / W enter as hi + lo bf16 planes (bf16_ || x3_)
+    bool xblk_ = false;   // X planes blocked [ld / 32][nf][32] (launch_mf_split_x / forward xblk)
     int64_t P_, Pp_, V_, ld_;
     Communicator* comm_;
     EngineConfig cfg_;

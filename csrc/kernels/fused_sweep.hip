@@ -573,6 +573,19 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     const int b = blockIdx.x;
     int gi = b % I;
     int gj = b / I;
+    if constexpr (!XL) {
+        // Chip-wide groups: the dispatcher deals workgroups to the XCDs round-robin (b % 8), so with gi = b % I a
+        // group lived on gcd(I, 8) ... 8 / gcd(I, 8) XCDs: I = 4 put each group of J = 57 ... 61 slabs on 2 XCDs
+        // (4.3-4.5 TB/s), I = 6 on 4 (4.9-5.3), odd I on all 8 (5.5-6.2 TB/s, profiles/cw_r4_sweep.jsonl). Number
+        // the workgroups XCD by XCD (p = the workgroups of lower XCDs + b / 8) and deal p round-robin to the groups:
+        // every group gets ~J / 8 slabs on every XCD whatever I is. (dbg & 8: the old b % I map, A/B runs.)
+        if (!(dbg & 8)) {
+            const int grid = I * J, x = b & 7;
+            const int p = x * (grid >> 3) + (x < (grid & 7) ? x : (grid & 7)) + (b >> 3);
+            gi = p % I;
+            gj = p / I;
+        }
+    }
     if constexpr (XL) {
         if (threadIdx.x == 0) {
             unsigned xcc;
@@ -1059,10 +1072,15 @@ static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), "hipFuncSetAttribute");
         configured = true;
     }
+    int dbg = g_fused_dbg;
+    if constexpr (!X) {  // SART_FUSED_CW_MAP=0: chip-wide groups keep the b % I map (read per launch: A/B runs)
+        const char* e = std::getenv("SART_FUSED_CW_MAP");
+        if (e && *e && std::atoi(e) == 0) dbg |= 8;
+    }
     hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC, AT, CPL, KW>), grid,
                        dim3(sched_split(SC) ? kFusedThreads + 64 : kFusedThreads), lds, stream, A, ld, nrows,
                        nrows_pad, x,
-                       ghat, arow, partial, Fpart, gran, I, J, st, g_fused_dbg, xcnt, chain_tiles);
+                       ghat, arow, partial, Fpart, gran, I, J, st, dbg, xcnt, chain_tiles);
 }
 
 template <int T>

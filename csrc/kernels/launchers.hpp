@@ -170,8 +170,9 @@ struct MfSkipScope {
 // bf16-stored RTM (multiframe_bf16.hip): the same projections on v_mfma_f32_16x16x32_bf16 with the fp32
 // operand (X or W) split into hi + lo bf16 planes (k_mf_split_x: X [nf][ld] -> planes [nf][ld]; k_mf_split_w:
 // W [rows][16][nf / 16] -> frame-major planes [nf][ldw], ldw >= rows rounded up to 32).
+// xblk: X planes in the blocked layout [ld / 32][nf][32] (launch_mf_split_x with ld > 0), else frame-major [nf][ld]
 void launch_mf_forward_b16(const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const bf16_t* Xh,
-                           const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream);
+                           const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream, bool xblk = false);
 // a32: the split-A kernels (fp32 A split into hi + lo bf16 in registers, three products; launch_mf_*_x3)
 int mf_backproject_b16_num_splits(int64_t ld, int64_t nrows, bool a32 = false);
 int mf_backproject_b16_vox_align(int64_t ld, bool a32 = false);  // voxel-range alignment of the launchers below
@@ -179,13 +180,15 @@ void launch_mf_backproject_b16(const bf16_t* A, int64_t ld, int64_t nrows, const
                                int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0 = 0,
                                int64_t v1 = -1);
 void launch_mf_forward_x3(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const bf16_t* Xh,
-                          const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream);
+                          const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream, bool xblk = false);
 // Wh: hi and mid planes ([2][nf][ldw], launch_mf_split_w with three), Wl: lo plane
 void launch_mf_backproject_x3(const float* A, int64_t ld, int64_t nrows, const bf16_t* Wh, const bf16_t* Wl,
                               int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0 = 0,
                               int64_t v1 = -1);
-// perm: the split-A forward's k order (launch_mf_forward_x3 reads planes written with perm = true)
-void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStream_t stream, bool perm = false);
+// perm: the split-A forward's k order (launch_mf_forward_x3 reads planes written with perm = true). ld > 0: X is
+// [nf = n / ld][ld] and the planes are written blocked, [ld / 32][nf][32] (the forward's xblk layout)
+void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStream_t stream, bool perm = false,
+                       int64_t ld = 0);
 // three: hi [nf][ldw] then mid [nf][ldw] in `hi` (2 nf ldw elements), lo: the split-A back-projection's planes
 void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, bf16_t* hi, bf16_t* lo,
                        hipStream_t stream, bool three = false);

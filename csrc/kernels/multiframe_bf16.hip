@@ -147,6 +147,14 @@ __device__ __forceinline__ uint4 phase_frag(const uint2 (&v)[8]) {
 
 }  // namespace
 
+// Column range and X plane layout of a forward launch: element (frame f, voxel c) of a plane sits at
+// f * xfs + (c / 32) * xbs + c % 32. Frame-major planes [nf][ld]: xfs = ld, xbs = 32. Blocked planes
+// [ld / 32][nf][32] (launch_mf_split_x with ld > 0): xfs = 32, xbs = 32 nf, so the X tile of a step (nf frames of
+// 32 voxels) is one contiguous 2 nf * 32 bytes per plane instead of nf 64-byte pieces ld * 2 bytes apart.
+struct FwdCols {
+    int64_t cps, xfs, xbs;
+};
+
 // Split-K over columns: blockIdx.y selects [c0, c1) (multiples of 64); Fout + blockIdx.y * nrows_pad * nf.
 // A step covers KB blocks of 32 voxels; with KB = 2 the two loads of a row are the two halves of one 128-byte
 // line, issued back to back.
@@ -154,7 +162,8 @@ template <int NG, int DEPTH, int RT, int KB>
 __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict__ A, int64_t ld, int64_t nrows,
                                                         int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                         const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
-                                                        int64_t cols_per_split, const int* __restrict__ skip) {
+                                                        FwdCols fc, const int* __restrict__ skip) {
+    const int64_t cols_per_split = fc.cps, xfs = fc.xfs, xbs = fc.xbs;
     if (skip && *skip) return;  // every frame of the batch is done: the sweep is a no-op
     constexpr int NF = 16 * NG;
     constexpr int RS = DEPTH + 1;
@@ -166,7 +175,7 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
     const int64_t c1 = (c0 + cols_per_split < ld) ? c0 + cols_per_split : ld;
     Fout += (int64_t)blockIdx.y * nrows_pad * NF;
     const bf16_t* __restrict__ ap = A + (row0 + r) * ld + c0 + 8 * g;
-    const int64_t xo = (int64_t)r * ld + c0 + 8 * g;  // frame r of column group 0; group j: + 16 j ld
+    const int64_t xo = (int64_t)r * xfs + (c0 >> 5) * xbs + 8 * g;  // frame r of column group 0; group j: + 16 j xfs
 
     floatx4 acc[RT][NG];
 #pragma unroll
@@ -188,8 +197,8 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
             for (int j = 0; j < NG; ++j)
 #pragma unroll
                 for (int kb = 0; kb < KB; ++kb) {
-                    xh[sl][j][kb] = *reinterpret_cast<const uint4*>(Xh + xo + (int64_t)j * 16 * ld + q + 32 * kb);
-                    xl[sl][j][kb] = *reinterpret_cast<const uint4*>(Xl + xo + (int64_t)j * 16 * ld + q + 32 * kb);
+                    xh[sl][j][kb] = *reinterpret_cast<const uint4*>(Xh + xo + (int64_t)j * 16 * xfs + (t * KB + kb) * xbs);
+                    xl[sl][j][kb] = *reinterpret_cast<const uint4*>(Xl + xo + (int64_t)j * 16 * xfs + (t * KB + kb) * xbs);
                 }
         };
 #pragma unroll
@@ -267,7 +276,8 @@ template <int NG, int DEPTH, int RT, int KB, typename AT = bf16_t, bool AS = fal
 __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forward_b16_lds(const AT* __restrict__ A, int64_t ld, int64_t nrows,
                                                             int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                             const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
-                                                            int64_t cols_per_split, const int* __restrict__ skip) {
+                                                            FwdCols fc, const int* __restrict__ skip) {
+    const int64_t cols_per_split = fc.cps, xfs = fc.xfs, xbs = fc.xbs;
     if (skip && *skip) return;
     constexpr int NF = 16 * NG;
     constexpr int RS = DEPTH + 1;
@@ -288,7 +298,7 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
     // 64-byte halves of a row per instruction instead of four 16-byte pieces); the X planes hold the same k order
     // (k_mf_split_x with perm)
     const AT* __restrict__ ap = A + (row0 + r) * ld + c0 + (A32 ? 4 : 8) * g;
-    const int64_t xo = (int64_t)r * ld + c0 + 8 * g;
+    const int64_t xo = (int64_t)r * xfs + (c0 >> 5) * xbs + 8 * g;
     // uint4 slot of this lane's fragment (frame r, voxels 8 g..) inside a 1 KiB piece: the lane index itself. Every
     // wave's lane l reads what lane l of the loading wave wrote, so any bijection works; lane-linear slots put the 16
     // lanes of each ds_read_b128 group and the 8 of each ds_write_b128 group on distinct 16-B bank slots (the former
@@ -340,7 +350,7 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
 #pragma unroll
             for (int i = 0; i < XQ; ++i) {
                 const int pc = piece(i), j = pc % NG, plane = (pc / NG) & 1, kb = pc / (2 * NG);
-                xq[sl][i] = *reinterpret_cast<const u32x4*>((plane ? Xl : Xh) + xo + (int64_t)j * 16 * ld + q + 32 * kb);
+                xq[sl][i] = *reinterpret_cast<const u32x4*>((plane ? Xl : Xh) + xo + (int64_t)j * 16 * xfs + (t * KB + kb) * xbs);
             }
         };
         auto stage = [&](auto slc, int64_t t) {
@@ -941,7 +951,8 @@ template <int NG, int DEPTH, int RT, int KB, int MINW, bool AS = false>
 __global__ __launch_bounds__(256, MINW) void k_mf_forward_x3_reg(const float* __restrict__ A, int64_t ld, int64_t nrows,
                                                                   int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                                   const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
-                                                                  int64_t cols_per_split, const int* __restrict__ skip) {
+                                                                  FwdCols fc, const int* __restrict__ skip) {
+    const int64_t cols_per_split = fc.cps, xfs = fc.xfs, xbs = fc.xbs;
     if (skip && *skip) return;
     constexpr int NF = 16 * NG;
     constexpr int RS = DEPTH + 1;
@@ -953,7 +964,7 @@ __global__ __launch_bounds__(256, MINW) void k_mf_forward_x3_reg(const float* __
     const int64_t c1 = (c0 + cols_per_split < ld) ? c0 + cols_per_split : ld;
     Fout += (int64_t)blockIdx.y * nrows_pad * NF;
     const float* __restrict__ ap = A + (row0 + r) * ld + c0 + 4 * g;
-    const int64_t xo = (int64_t)r * ld + c0 + 8 * g;
+    const int64_t xo = (int64_t)r * xfs + (c0 >> 5) * xbs + 8 * g;
     constexpr int R16 = 32 * KB * 4 / 16;  // 16-B slots per row and step (AS)
     constexpr int RPI = 64 / R16;          // rows per staging load instruction
     constexpr int NI = 16 * RT / RPI;      // staging loads per step and wave
@@ -995,8 +1006,8 @@ __global__ __launch_bounds__(256, MINW) void k_mf_forward_x3_reg(const float* __
             for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
                 for (int j = 0; j < NG; ++j) {
-                    xh[sl][kb][j] = *reinterpret_cast<const u32x4*>(Xh + xo + (int64_t)j * 16 * ld + q + 32 * kb);
-                    xl[sl][kb][j] = *reinterpret_cast<const u32x4*>(Xl + xo + (int64_t)j * 16 * ld + q + 32 * kb);
+                    xh[sl][kb][j] = *reinterpret_cast<const u32x4*>(Xh + xo + (int64_t)j * 16 * xfs + (t * KB + kb) * xbs);
+                    xl[sl][kb][j] = *reinterpret_cast<const u32x4*>(Xl + xo + (int64_t)j * 16 * xfs + (t * KB + kb) * xbs);
                 }
         };
         [&]<int... Q>(std::integer_sequence<int, Q...>) {
@@ -1239,7 +1250,7 @@ static bool mf_b16_bwd_lds(int nf) {
 
 template <int NG, int DEPTH, int RT, int KB, typename AT>
 static void fwd_b16_t(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows,
-                      int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
+                      int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, FwdCols cps) {
     constexpr bool A32 = std::is_same<AT, float>::value;
     constexpr bool CAN_AS = A32 || KB == 2;  // full 128-B row segments per step
     if constexpr (A32) {
@@ -1297,7 +1308,7 @@ static void fwd_b16_t(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, in
 
 template <int NG, int DEPTH, typename AT>
 static void fwd_b16_d(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows,
-                      int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
+                      int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, FwdCols cps) {
     if (tl.rt == 2 && tl.kb == 2)
         fwd_b16_t<NG, DEPTH, 2, 2>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else if (tl.rt == 4 && tl.kb == 2)
@@ -1316,7 +1327,7 @@ static void fwd_b16_d(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, in
 
 template <int NG, typename AT>
 static void fwd_b16(int depth, FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows,
-                    int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, int64_t cps) {
+                    int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, FwdCols cps) {
     if constexpr (!std::is_same<AT, float>::value) {
         if (depth == 1) {
             fwd_b16_d<NG, 1>(tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
@@ -1353,7 +1364,8 @@ static int mf_x3_vt(int64_t ld) {
 
 template <typename AT>
 static void launch_mf_forward_split(const AT* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const bf16_t* Xh,
-                                    const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream) {
+                                    const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream,
+                                    bool xblk) {
     constexpr bool A32 = std::is_same<AT, float>::value;
     const char* what = A32 ? "mf_forward_x3" : "mf_forward_b16";
     if (ld % 64 != 0) throw std::runtime_error(std::string(what) + ": ld must be a multiple of 64");
@@ -1362,7 +1374,7 @@ static void launch_mf_forward_split(const AT* A, int64_t ld, int64_t nrows, int6
     if (nrows_pad % 32 != 0) throw std::runtime_error(std::string(what) + ": padded rows must be a multiple of 32");
     FwdTile tl = A32 ? mf_x3_fwd_tile(nf) : mf_b16_fwd_tile(nf);
     if (nrows_pad % (16 * tl.rt) != 0) tl = FwdTile{2, 1, tl.lds, A32 && tl.as};  // a wave's rows inside the padding
-    const int64_t cps = ((ld + nsplit - 1) / nsplit + 63) / 64 * 64;
+    const FwdCols cps{((ld + nsplit - 1) / nsplit + 63) / 64 * 64, xblk ? 32 : ld, xblk ? 32 * (int64_t)nf : 32};
     const int64_t rows_per_block = 64 * tl.rt;
     const dim3 grid((unsigned)((nrows_pad + rows_per_block - 1) / rows_per_block), (unsigned)nsplit);
     const int d = A32 ? mf_x3_depth(true) : mf_b16_depth(true, nf);
@@ -1376,13 +1388,13 @@ static void launch_mf_forward_split(const AT* A, int64_t ld, int64_t nrows, int6
 }
 
 void launch_mf_forward_b16(const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const bf16_t* Xh,
-                           const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream) {
-    launch_mf_forward_split(A, ld, nrows, nrows_pad, Xh, Xl, Fout, nsplit, nf, stream);
+                           const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream, bool xblk) {
+    launch_mf_forward_split(A, ld, nrows, nrows_pad, Xh, Xl, Fout, nsplit, nf, stream, xblk);
 }
 
 void launch_mf_forward_x3(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const bf16_t* Xh,
-                          const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream) {
-    launch_mf_forward_split(A, ld, nrows, nrows_pad, Xh, Xl, Fout, nsplit, nf, stream);
+                          const bf16_t* Xl, float* Fout, int nsplit, int nf, hipStream_t stream, bool xblk) {
+    launch_mf_forward_split(A, ld, nrows, nrows_pad, Xh, Xl, Fout, nsplit, nf, stream, xblk);
 }
 
 // Split-K of the bf16 / split-A back-projection: ~1024 workgroups (4 waves x 64 VT voxels each), >= 64 rows per

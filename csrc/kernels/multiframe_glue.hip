@@ -280,7 +280,8 @@ __device__ __forceinline__ void split_bf16(float x, uint32_t key, bf16_t& hi, bf
 // within every block of 32 voxels, plane position 8 g + j holds voxel 4 g + j (j < 4) or 16 + 4 g + j - 4, the
 // k order in which that kernel's lanes load A as two contiguous 64-byte halves of a row.
 __global__ __launch_bounds__(256) void k_mf_split_x(const float* __restrict__ X, int64_t n4, bf16_t* __restrict__ hi,
-                                                    bf16_t* __restrict__ lo, const int* __restrict__ skip, int perm) {
+                                                    bf16_t* __restrict__ lo, const int* __restrict__ skip, int perm,
+                                                    int64_t ld, int64_t nf) {
     if (skip && *skip) return;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n4) return;
@@ -291,7 +292,12 @@ __global__ __launch_bounds__(256) void k_mf_split_x(const float* __restrict__ X,
     split_bf16(v.y, key + 1, h[1], l[1]);
     split_bf16(v.z, key + 2, h[2], l[2]);
     split_bf16(v.w, key + 3, h[3], l[3]);
-    const int64_t o = perm ? ((i & ~(int64_t)7) | ((i & 3) << 1) | ((i >> 2) & 1)) : i;
+    int64_t o = i;  // 4-element unit: frame-major, or blocked [ld / 32][nf][32] (8 units per 32 voxels)
+    if (ld > 0) {
+        const int64_t f = (4 * i) / ld, c = (4 * i) % ld;
+        o = ((c >> 5) * nf + f) * 8 + ((c & 31) >> 2);
+    }
+    if (perm) o = (o & ~(int64_t)7) | ((o & 3) << 1) | ((o >> 2) & 1);
     reinterpret_cast<uint2*>(hi)[o] = make_uint2(h[0] | (unsigned)h[1] << 16, h[2] | (unsigned)h[3] << 16);
     reinterpret_cast<uint2*>(lo)[o] = make_uint2(l[0] | (unsigned)l[1] << 16, l[2] | (unsigned)l[3] << 16);
 }
@@ -495,10 +501,13 @@ void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, 
     check_launch("k_mf_state_begin");
 }
 
-void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStream_t stream, bool perm) {
+void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStream_t stream, bool perm,
+                       int64_t ld) {
     if (n % (perm ? 32 : 4) != 0) throw std::runtime_error("mf_split_x: length must be a multiple of 4 (32 permuted)");
+    if (ld > 0 && (ld % 32 != 0 || n % ld != 0))
+        throw std::runtime_error("mf_split_x: blocked planes need ld a multiple of 32 dividing the length");
     hipLaunchKernelGGL(k_mf_split_x, dim3(std::max<unsigned>(1, nb(n / 4))), dim3(256), 0, stream, X, n / 4, hi, lo, g_mf_skip,
-                       (int)perm);
+                       (int)perm, ld, ld > 0 ? n / ld : (int64_t)0);
     check_launch("k_mf_split_x");
 }
 

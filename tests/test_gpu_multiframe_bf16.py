@@ -265,3 +265,38 @@ def test_split_a_engine_matches_fp32_mfma(batch, iters):
     err = {k: np.linalg.norm(v[list(frames)] - ref) / np.linalg.norm(ref) for k, v in xs.items()}
     print("rel vs fp64 oracle: fp32 MFMA %.3g, split-A %.3g" % (err[False], err[True]))
     assert err[True] <= 1.5 * err[False] + 1e-6, err
+
+
+# ------------------------------------------------------------------ blocked X planes ([ld / 32][nf][32])
+@pytest.mark.parametrize("storage,fwd", [("fp32", ""), ("fp32", "2,2"), ("fp32", "4,1,as"), ("bf16", ""),
+                                         ("bf16", "4,1"), ("bf16", "8,1,lds"), ("bf16", "2,2,lds,as")])
+@pytest.mark.parametrize("nf", [16, 32, 64])
+@pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (1000, 1088)])
+def test_forward_blocked_x_planes_bitwise(k, dev, P, V, nf, storage, fwd, monkeypatch):
+    """The forwards read blocked X planes (launch_mf_split_x with ld) at the same k order and MFMA sequence as
+    frame-major ones: identical sums bit for bit, over ragged column splits and every forward tile."""
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+
+    a32 = storage == "fp32"
+    if fwd:
+        monkeypatch.setenv("SART_MF_X3_FWD" if a32 else "SART_MF_B16_FWD", fwd)
+    rng = np.random.default_rng(P + V + nf)
+    m = DenseRTM.from_dense(rng.random((P, V), dtype=np.float32), device=dev, storage=storage)
+    Xd = torch.zeros((nf, m.ld), device=dev)
+    Xd[:, :V] = torch.from_numpy(rng.random((nf, V)).astype(np.float32))
+    nsf = 3 if m.ld > 1024 else 1
+    fwd_op = k.mf_forward_x3 if a32 else k.mf_forward_b16
+    outs = []
+    for blk in (False, True):
+        Xh = torch.empty((nf, m.ld), dtype=torch.bfloat16, device=dev)
+        Xl = torch.empty_like(Xh)
+        k.mf_split_x(Xd.data_ptr(), nf * m.ld, Xh.data_ptr(), Xl.data_ptr(), _stream(dev), a32, m.ld if blk else 0)
+        if blk:  # element (f, c) of the blocked plane sits at (c / 32, f, c % 32)
+            perm = Xh.view(m.ld // 32, nf, 32).permute(1, 0, 2).reshape(nf, m.ld)
+            torch.testing.assert_close(perm, outs[0][1], rtol=0, atol=0)
+        Fo = torch.zeros((nsf, m.nrows_pad, nf), device=dev)
+        fwd_op(m.A.data_ptr(), m.ld, P, m.nrows_pad, Xh.data_ptr(), Xl.data_ptr(), Fo.data_ptr(), nsf, _stream(dev),
+               nf, blk)
+        torch.cuda.synchronize()
+        outs.append((Fo, Xh))
+    assert torch.equal(outs[0][0], outs[1][0])

@@ -244,7 +244,7 @@ def test_fused_v6_schedules(dev, T, sched, log):
 PROD = [(65536, 4, 32, 8), (131072, 1, 16, 16), (262144, 1, 32, 8),
         (60000, 4, 30, 8), (100000, 1, 14, 16), (200000, 1, 28, 8), (70000, 1, 10, 24), (73728, 1, 8, 32), (150000, 1, 30, 8),
         (147456, 1, 16, 16), (294912, 1, 32, 8), (155648, 1, 31, 8), (163840, 1, 32, 8),
-        (300000, 1, 42, 6), (524288, 1, 64, 4), (1048576, 1, 128, 2)]
+        (300000, 1, 42, 6), (303104, 1, 33, 7), (327680, 1, 36, 7), (524288, 1, 57, 4), (1048576, 1, 114, 2)]
 
 
 @pytest.mark.parametrize("nvox,T,J,I", PROD)

@@ -511,6 +511,18 @@ for step in "$@"; do
         grep -h '^{' "$OUT/cw_${k}_$v.log" >> "$OUT/cw_kw.jsonl"
         echo "=== cw kw$k $v $(grep -h '^{' "$OUT/cw_${k}_$v.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); g=d["fused_grid"]; print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], g, d["fused_schedule"], round(d["effective_hbm_TBps_per_gpu"]*1e3/g["workgroups"], 2), "GB/s/CU")')" | tee -a "$OUT/session.log"
       done ;;
+    r4cwsweep)  # default geometry at 294912 ... 557056 voxels in steps of 8192 (chip-wide row groups above 294912)
+      : > "$OUT/cw_sweep.jsonl"
+      for v in $(seq ${CWS_FROM:-294912} 8192 ${CWS_TO:-557056}); do
+        timeout -k 10 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --npix 32768 --no-selfcheck \
+          > "$OUT/cws_$v.log" 2>&1 || { echo "FATAL $v"; tail -n 20 "$OUT/cws_$v.log"; exit 1; }
+        grep -h '^{' "$OUT/cws_$v.log" >> "$OUT/cw_sweep.jsonl"
+        echo "=== cws $v $(grep -h '^{' "$OUT/cws_$v.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); g=d["fused_grid"]; print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], g["ld"], g["kw"], g["J"], g["I"], g["xcd_local"], d["fused_schedule"])')" | tee -a "$OUT/session.log"
+        rm -f "$OUT/cws_$v.log"
+      done ;;
+    r4xblk) run probe_xblk 400 python tools/probe_mf_xblk.py ;;
+    r4mftest) run pytest_mf 600 python -u -m pytest tests/test_gpu_multiframe_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "blocked or split_a or vs_oracle" ;;
+    r4cwtest) run pytest_cw 600 python -u -m pytest tests/test_gpu_solver.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "production_geometry or chip_wide" ;;
     r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r4bench) run bench_r4 300 python bench.py --steps 20 --warmup 5 ;;
     r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
