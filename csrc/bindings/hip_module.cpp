@@ -410,6 +410,7 @@ PYBIND11_MODULE(_sart_hip, m) {
     m.def("fused_tile_rows", &sart::fused_tile_rows);
     m.def("fused_set_schedule", &sart::fused_set_schedule);
     m.def("fused_get_schedule", &sart::fused_get_schedule);
+    m.def("fused_granules", &sart::fused_granules, py::arg("nrows_pad"), py::arg("J"), py::arg("xl") = true);
     m.def("fused_last_schedule", &sart::fused_last_schedule);
     m.def("fused_debug_map", &sart::fused_debug_map);
     m.def("fused_set_trace", [](uintptr_t buf, long long tiles) {

@@ -200,7 +200,10 @@ void Engine::alloc_fused() {
     if ((int64_t)partial_.size() < n_part * ld_) partial_.resize(n_part * ld_);
     const int64_t nF = std::max<int64_t>({forward_num_blocks(Pp_), (int64_t)weights_num_blocks(Pp_), nF_fused_, 1});
     if ((int64_t)Fpart_.size() < nF) Fpart_.resize(nF);
-    if (use_fused_ && (int64_t)gran_.size() < Pp_ * geom_.J) gran_.resize(Pp_ * geom_.J);
+    if (use_fused_) {
+        const int64_t ng = std::max<int64_t>(Pp_ * geom_.J, fused_granules(Pp_, geom_.J, geom_.xl));
+        if ((int64_t)gran_.size() < ng) gran_.resize(ng);
+    }
 }
 
 void DeviceRaySums::compute(const void* A, int64_t P, int64_t Pp, int64_t V, int64_t ld, Communicator* comm,

@@ -611,6 +611,11 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int64_t ld4 = ld >> (CPL == 8 ? 3 : 2);  // row length in tile vectors (RT)
+    // Granule row of a tile: J entries (T = 1 for chip-wide groups), padded there to whole 128-byte lines (16
+    // granules) so that no line holds granules of two tiles: the J writers of tile u + 1 (other XCDs) then never
+    // store into a line the gatherers of tile u are still re-polling through memory (fused_granules sizes the
+    // buffer; dbg & 16: unpadded, A/B runs).
+    const int Jg = (XL || (dbg & 16)) ? J : ((J + 15) & ~15);
     if (DIAG && threadIdx.x == 0 && b < 1024) g_fused_map[b] = gi * 1024 + gj;
 
     for (int i = threadIdx.x; i < NS * 4 + NS; i += NTHR) s_pflag[i] = -1;
@@ -864,7 +869,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
             if (lane < T) {
                 const float sv = local_row_partial<T, FLAG4>(s_pflag, s_part, ps, (int)u, lane, kSpinLimit);
                 if (!(dbg & 1)) {
-                    uint64_t* g = gran + ((t_begin + u) * J + gj) * T + lane;
+                    uint64_t* g = gran + ((t_begin + u) * Jg + gj) * T + lane;
                     if constexpr (XL)
                         __hip_atomic_store(g, make_granule(epoch, sv), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     else
@@ -894,7 +899,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
         };
         auto issue_poll = [&](uint64_t(&dst)[GR], int64_t u) {
             const int64_t uc = u < 0 ? 0 : (u < ulast ? u : ulast);
-            const uint64_t* g = gran + (t_begin + uc) * (int64_t)n;
+            const uint64_t* g = gran + (t_begin + uc) * (int64_t)Jg * T;
 #pragma unroll
             for (int m = 0; m < GR; ++m) {
                 const int idx = lane + 64 * m;
@@ -963,7 +968,7 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
                 if (lane < T) {
                     const float sv = local_row_partial<T, FLAG4>(s_pflag, s_part, ps, (int)u, lane, kSpinLimit);  // fixed order
                     if (!(dbg & 1) && !SPLIT) {
-                        uint64_t* g = gran + ((t_begin + u) * J + gj) * T + lane;
+                        uint64_t* g = gran + ((t_begin + u) * Jg + gj) * T + lane;
                         if constexpr (XL)  // plain 8-byte store: the line stays in this XCD's L2
                             __hip_atomic_store(g, make_granule(epoch, sv), __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1017,6 +1022,8 @@ void fused_set_schedule(int sched) {
 int fused_get_schedule() { return g_fused_sched; }
 static int g_fused_last_sched = -1;  // SCHED of the last k_fused_sweep_rows launch (variant 3: -1)
 int fused_last_schedule() { return g_fused_last_sched; }
+
+int64_t fused_granules(int64_t nrows_pad, int J, bool xl) { return nrows_pad * (xl ? J : ((J + 15) & ~15)); }
 bool fused_split_schedule(int T, bool bf16) {  // mirrors the schedule choice of launch_rows / launch_fused_sweep_bf16
     if (bf16) return T >= 2 || g_fused_sched == 5;
     return g_fused_sched >= 4;  // T = 1: 4 and 5 both run schedule 5; T >= 2: 5 runs 4
@@ -1073,9 +1080,14 @@ static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld
         configured = true;
     }
     int dbg = g_fused_dbg;
-    if constexpr (!X) {  // SART_FUSED_CW_MAP=0: chip-wide groups keep the b % I map (read per launch: A/B runs)
+    if constexpr (!X) {
+        // group map (SART_FUSED_CW_MAP: 0 = b % I, 1 = XCD-balanced, default: balanced for even I only) and granule
+        // padding (SART_FUSED_GPAD=0: unpadded), read per launch (A/B runs)
         const char* e = std::getenv("SART_FUSED_CW_MAP");
-        if (e && *e && std::atoi(e) == 0) dbg |= 8;
+        const int map = (e && *e) ? std::atoi(e) : 2;
+        if (map == 0 || (map == 2 && I % 2 == 1)) dbg |= 8;
+        const char* gp = std::getenv("SART_FUSED_GPAD");
+        if (gp && *gp && std::atoi(gp) == 0) dbg |= 16;
     }
     hipLaunchKernelGGL((k_fused_sweep_rows<LG, X, D, T, SC, AT, CPL, KW>), grid,
                        dim3(sched_split(SC) ? kFusedThreads + 64 : kFusedThreads), lds, stream, A, ld, nrows,

@@ -82,7 +82,9 @@ int fused_pick_k(int64_t ld);
 int fused_tile_rows(int K, int variant);
 void fused_set_schedule(int sched);
 int fused_get_schedule();
-int fused_last_schedule();  // pipeline schedule the last variant-6 launch ran (T / kw / chip-wide pick it), -1: v3
+int fused_last_schedule();
+// granule buffer entries (uint64) of a variant-6 sweep: chip-wide groups pad each tile's row to 16 granules
+int64_t fused_granules(int64_t nrows_pad, int J, bool xl);  // pipeline schedule the last variant-6 launch ran (T / kw / chip-wide pick it), -1: v3
 void fused_set_trace(unsigned long long* buf, long long tiles);
 std::vector<int> fused_debug_map(int nblocks);
 int fused_fpart_per_block(int variant);

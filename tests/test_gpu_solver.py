@@ -311,7 +311,7 @@ def test_segmented_chains(dev, monkeypatch, storage, nvox, T, log):
 
 @pytest.mark.parametrize("rows,nvox,T,J,I", [(1024, 65536, 4, 32, 8), (512, 131072, 1, 16, 16),
                                              (256, 262144, 1, 32, 8), (512, 100000, 1, 14, 16),
-                                             (128, 524288, 1, 64, 4)])
+                                             (128, 524288, 1, 57, 4)])
 @pytest.mark.parametrize("log", [False, True])
 def test_production_geometry_vs_oracle(dev, rows, nvox, T, J, I, log):
     """The production grids against the host fp64 oracle and the fp32 emulation (fewer rows)."""
@@ -424,22 +424,25 @@ def test_fault_injection_fallback_chain(dev, faults, expect):
     _check(x, A, g, max_iterations=12)
 
 
-@pytest.mark.parametrize("faults,expect", [(1, 3), (2, None)])
-def test_fault_injection_fallback_chain_chip_wide(dev, faults, expect):
-    """The fallback chain from chip-wide row groups (524288 voxels: J = 64 > 32 slabs per XCD) to variant 3 and the
-    two-pass kernels, each re-solve against the device fp64 oracle (fused <= 1.25x the two-pass error)."""
+@pytest.mark.parametrize("ld,faults,expect", [(524288, 1, 3), (524288, 2, None), (None, 1, None)])
+def test_fault_injection_fallback_chain_chip_wide(dev, ld, faults, expect):
+    """The fallback chain from chip-wide row groups (524288 voxels: J > 32 slabs per XCD) to variant 3 and the
+    two-pass kernels, each re-solve against the device fp64 oracle (fused <= 1.25x the two-pass error). At the
+    width choose_ld picks (525312 = 57 slabs of 9216, granule rows padded to 64) variant 3 has no valid slab
+    (513 slabs of 1024), so the first fault goes straight to the two-pass kernels."""
     from mpi_cuda_sartsolver_amd.models.oracle import sart_oracle_f64
     from mpi_cuda_sartsolver_amd.ops import hip
     from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
 
     k = hip()
-    prob = make_problem(512, 524288, seed=17, device=dev, saturate_fraction=0.02)
+    prob = make_problem(512, 524288, seed=17, device=dev, saturate_fraction=0.02, ld=ld)
     rtm, g = prob.rtm, prob.measurement.cpu().numpy()
     cfg = k.EngineConfig()
     cfg.max_iterations, cfg.conv_tolerance, cfg.allow_zero_tolerance = 8, 0.0, True
     cfg.fault_inject = faults
     e = k.Engine(dev.index or 0, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld, k.local_comm(), cfg)
-    assert e.use_fused and e.geometry.variant == 6 and not e.geometry.xl and e.geometry.J == 64
+    assert e.use_fused and e.geometry.variant == 6 and not e.geometry.xl
+    assert (e.geometry.J, e.geometry.kw) == ((64, 8) if ld else (57, 9))
     x, info = e.solve(g, None)
     assert info["fallbacks"] == faults and info["used_fused"] == (expect is not None)
     if expect is not None:

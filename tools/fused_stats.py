@@ -30,7 +30,7 @@ def main():
         arow = torch.rand(m.nrows_pad, device=dev) * 1e-4
         part = torch.zeros(g.I * m.ld, device=dev)
         Fp = torch.zeros(2 * g.grid, dtype=torch.float64, device=dev)
-        gran = torch.zeros(m.nrows_pad * g.J, dtype=torch.int64, device=dev)
+        gran = torch.zeros(k.fused_granules(m.nrows_pad, g.J, g.xl), dtype=torch.int64, device=dev)
         st = new_state(dev)
         Fslot = torch.zeros(64, dtype=torch.float32, device=dev)  # [F, error word] read by decide
         xcnt = torch.zeros(16, dtype=torch.int32, device=dev)

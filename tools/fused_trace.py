@@ -50,7 +50,7 @@ def main():
         nt = ntile // g.I
         part = torch.zeros(g.I * m.ld, device=dev)
         Fp = torch.zeros(2 * g.grid, dtype=torch.float64, device=dev)
-        gran = torch.zeros(m.nrows_pad * g.J, dtype=torch.int64, device=dev)
+        gran = torch.zeros(k.fused_granules(m.nrows_pad, g.J, g.xl), dtype=torch.int64, device=dev)
         tr = torch.zeros(g.grid * nt * 4, dtype=torch.int64, device=dev)
         k.fused_set_schedule(sched)
         k.fused_set_debug(2)

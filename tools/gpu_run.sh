@@ -523,6 +523,21 @@ for step in "$@"; do
     r4xblk) run probe_xblk 400 python tools/probe_mf_xblk.py ;;
     r4mftest) run pytest_mf 600 python -u -m pytest tests/test_gpu_multiframe_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "blocked or split_a or vs_oracle" ;;
     r4cwtest) run pytest_cw 600 python -u -m pytest tests/test_gpu_solver.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "production_geometry or chip_wide" ;;
+    r4cwab)  # A/B of chip-wide settings: for each width, every "NAME=VAL[,NAME=VAL]" setting of CWAB_SETS (":" = defaults)
+      : > "$OUT/cw_ab.jsonl"
+      for v in ${CWAB_WIDTHS:-303104 327680 360448 393216 450560 458752 524288 557056}; do
+        for set in ${CWAB_SETS:-: SART_FUSED_GPAD=0}; do
+          envs=(); [ "$set" != ":" ] && IFS=, read -ra envs <<< "$set"
+          env "${envs[@]}" timeout -k 10 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --npix 32768 --no-selfcheck \
+            > "$OUT/cwab.log" 2>&1 || { echo "FATAL $v $set"; tail -n 20 "$OUT/cwab.log"; exit 1; }
+          grep -h '^{' "$OUT/cwab.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); d["ab_set"]=sys.argv[1]; print(json.dumps(d))' "$set" >> "$OUT/cw_ab.jsonl"
+          echo "=== cwab $v $set $(tail -n 1 "$OUT/cw_ab.jsonl" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); g=d["fused_grid"]; print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], g["ld"], g["kw"], g["J"], g["I"], g["xcd_local"], d["fused_schedule"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
+    r4mf) run bench_mfx64_blk 600 python bench.py --steps 3 --warmup 1 --frames 64 &&
+          SART_MF_XBLK=0 run bench_mfx64_fm 600 python bench.py --steps 3 --warmup 1 --frames 64 &&
+          run bench_mfb64_blk 600 python bench.py --steps 3 --warmup 1 --frames 64 --rtm-dtype bf16 &&
+          run bench_2tb_blk 900 python bench.py --config 2tb --steps 2 --warmup 1 ;;
     r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r4bench) run bench_r4 300 python bench.py --steps 20 --warmup 5 ;;
     r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;

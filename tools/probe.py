@@ -97,7 +97,7 @@ def main():
             g = fused_geometry(m.ld, int(info["multiProcessorCount"]), variant, T)
             if g is None or g.variant != variant or (T is not None and g.T != T):
                 continue
-            gran = torch.zeros(m.nrows_pad * g.J, dtype=torch.int64, device=dev)
+            gran = torch.zeros(k.fused_granules(m.nrows_pad, g.J, g.xl), dtype=torch.int64, device=dev)
             xcnt = torch.zeros(16, dtype=torch.int32, device=dev)
             if part.numel() < g.I * m.ld:
                 part = torch.zeros(g.I * m.ld, device=dev)
