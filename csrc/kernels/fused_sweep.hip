@@ -615,7 +615,8 @@ __global__ __launch_bounds__(sched_split(SCHED) ? kFusedThreads + 64 : kFusedThr
     // granules) so that no line holds granules of two tiles: the J writers of tile u + 1 (other XCDs) then never
     // store into a line the gatherers of tile u are still re-polling through memory (fused_granules sizes the
     // buffer; dbg & 16: unpadded, A/B runs).
-    const int Jg = (XL || (dbg & 16)) ? J : ((J + 15) & ~15);
+    // XCD-local groups keep unpadded rows unless dbg & 32 (A/B runs: SART_FUSED_GPAD=2).
+    const int Jg = ((XL && !(dbg & 32)) || (dbg & 16)) ? J : ((J + 15) & ~15);
     if (DIAG && threadIdx.x == 0 && b < 1024) g_fused_map[b] = gi * 1024 + gj;
 
     for (int i = threadIdx.x; i < NS * 4 + NS; i += NTHR) s_pflag[i] = -1;
@@ -1023,7 +1024,10 @@ int fused_get_schedule() { return g_fused_sched; }
 static int g_fused_last_sched = -1;  // SCHED of the last k_fused_sweep_rows launch (variant 3: -1)
 int fused_last_schedule() { return g_fused_last_sched; }
 
-int64_t fused_granules(int64_t nrows_pad, int J, bool xl) { return nrows_pad * (xl ? J : ((J + 15) & ~15)); }
+int64_t fused_granules(int64_t nrows_pad, int J, bool xl) {
+    (void)xl;  // (XCD-local rows are padded too under SART_FUSED_GPAD=2)
+    return nrows_pad * ((J + 15) & ~15);
+}
 bool fused_split_schedule(int T, bool bf16) {  // mirrors the schedule choice of launch_rows / launch_fused_sweep_bf16
     if (bf16) return T >= 2 || g_fused_sched == 5;
     return g_fused_sched >= 4;  // T = 1: 4 and 5 both run schedule 5; T >= 2: 5 runs 4
@@ -1080,7 +1084,10 @@ static void launch_rows_t(dim3 grid, hipStream_t stream, const AT* A, int64_t ld
         configured = true;
     }
     int dbg = g_fused_dbg;
-    if constexpr (!X) {
+    if constexpr (X) {
+        const char* gp = std::getenv("SART_FUSED_GPAD");
+        if (gp && *gp && std::atoi(gp) == 2) dbg |= 32;
+    } else {
         // group map (SART_FUSED_CW_MAP: 0 = b % I, 1 = XCD-balanced, default: balanced for even I only) and granule
         // padding (SART_FUSED_GPAD=0: unpadded), read per launch (A/B runs)
         const char* e = std::getenv("SART_FUSED_CW_MAP");
