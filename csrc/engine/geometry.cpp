@@ -47,24 +47,26 @@ bool kw_allowed(int kw, bool narrow_slabs, bool forced = true) {
     return true;
 }
 
-// Chip-wide row groups hand granules off through memory instead of the XCD's L2. Per CU they streamed 1.22-1.55x
-// slower than XCD-local groups at the widths where both exist (100000 / 200000 / 150000 voxels: 22.6 / 23.3 / 18.2
-// against 28.6 / 28.5 / 28.2 GB/s per CU, profiles/bench_r3_widths_chipwide_vs_xl.jsonl), so they serve only
-// rows wider than an XCD's 32 slabs, where they beat variant 3 by 22-30 % (300000 / 524288 / 1048576 voxels:
-// 5.40 / 5.95 / 6.11 against 4.15 / 4.87 / 4.70 TB/s, kw 6 / 7 with fused schedule 8). SART_FUSED_XL=0 / 1 forces
-// one kind where both exist.
-constexpr double kChipWidePenalty = 1.6;
+// Chip-wide row groups hand granules off through memory instead of the XCD's L2. Until round 4 they streamed
+// 1.22-1.55x slower per CU than XCD-local groups: a tile's J 8-byte granules shared 128-byte lines with the next
+// tile's, so the J writers of tile u + 1 (on other XCDs) stored into lines the gatherers of tile u were still
+// re-polling through memory. With every tile's granule row padded to whole lines (fused_sweep.hip, fused_granules)
+// they stream at the XCD-local rate: 24.2-27.3 GB/s per CU at kw 6 ... 9 (kw 5: 21.0-21.4) at 301056 ... 344064
+// voxels (profiles/cw_r4_kw_padded.txt), 5.9-6.3 TB/s at 303104 ... 557056 (profiles/cw_r4_granule_pad_ab.jsonl,
+// unpadded 4.6-5.8). kChipWidePenalty is fitted where both kinds exist (profiles/cw_r4_xl_vs_cw.txt): chip-wide
+// groups win at 150000 ... 172032 voxels (6.56-6.78 against 6.21-6.57 TB/s: wider slabs on more CUs than the kw 5 / 6
+// XCD-local grids) and lose at 100000 and 180224 ... 245760 (-1 ... -6 %; profiles/width_r4_sweep_default_vs_xl_box1.jsonl:
+// 180224 / 188416 by 1-2 % at 1.16), which 1.19 reproduces.
+// SART_FUSED_XL=0 / 1 forces one kind where both exist.
+constexpr double kChipWidePenalty = 1.19;
 
-// Per-CU time of a chip-wide slab of kw lane-vectors relative to an XCD-local kw 8 slab. Chip-wide groups run
-// schedule 5 at kw 8 / 9 / 5 and schedule 8 (3 polls in flight, 4-step lag) at kw 6 / 7 (fused_sweep.hip
-// launch_rows), and every step gathers J granules through memory, so the wider slabs (fewer granules per byte)
-// stream faster there than their XCD-local ratios (narrow_slab_penalty) say. Measured per CU at 301056 ... 344064
-// voxels (profiles/cw_r4_kw.jsonl, forced kw): kw 9 23.3-24.1, kw 7 23.5-23.7 (I = 5), kw 8 21.3-21.8, kw 6
-// 20.7-20.9, kw 5 15.4-20.0 GB/s; scaled so that kw 8 keeps kChipWidePenalty against XCD-local slabs.
-// Grids of 248 or more chip-wide workgroups measured 3-12 % slower per CU (kw 7 / 8 / 9 at 252: 20.6 / 20.1 / 23.3).
-double chip_wide_penalty(int kw, int workgroups) {
-    const double per_kw = kw == 9 ? 0.90 : (kw == 7 ? 0.91 : (kw == 8 ? 1.0 : (kw == 6 ? 1.03 : 1.2)));
-    return kChipWidePenalty * per_kw * (workgroups >= 248 ? 1.08 : 1.0);
+// Per-CU time of a chip-wide slab of kw lane-vectors relative to an XCD-local kw 8 slab (chip-wide groups run schedule
+// 5 at kw 8 / 9 / 5 and schedule 8 at kw 6 / 7, fused_sweep.hip launch_rows). (The grid size showed no consistent
+// effect once the granule rows were padded: kw 7 at 252 workgroups 24.6 GB/s per CU at 301056 voxels, 26.4 at 150528.)
+double chip_wide_penalty(int kw) {
+    // kw 7 (schedule 8) as kw 8 / 9: 150528 voxels at kw 7 (J = 21) 337 it/s against 310 at kw 9 (J = 17, ld 156672)
+    const double per_kw = kw >= 7 ? 1.0 : (kw == 6 ? 1.08 : 1.26);
+    return kChipWidePenalty * per_kw;
 }
 
 int xl_mode() {
@@ -89,7 +91,7 @@ V6Candidate v6_candidate(int64_t ld, int T, int kw, int num_cus, bool xl) {
     c.T = T, c.J = (int)J, c.kw = kw, c.xl = xl;
     // T = 2 (schedule 4) measured 4-10 % slower per byte than T = 1 (schedule 5) at equal slab / G
     // (131072 / 106496 columns, profiles/probe_r2_t1_sched5.jsonl); T = 4 and T = 1 tie at 65536
-    c.cost = (double)slab / c.I * (T == 2 ? 1.08 : 1.0) * (xl ? narrow_slab_penalty(kw) : chip_wide_penalty(kw, c.I * c.J));
+    c.cost = (double)slab / c.I * (T == 2 ? 1.08 : 1.0) * (xl ? narrow_slab_penalty(kw) : chip_wide_penalty(kw));
     return c;
 }
 

@@ -57,7 +57,8 @@ def test_width_sweep_variant6_and_waste():
                                             (262144, 1, 8, 32, 8, True), (61440, 4, 8, 30, 8, True),
                                             (16384, 4, 8, 8, 32, True), (106496, 1, 8, 13, 16, True),
                                             (100352, 1, 7, 14, 16, True), (200704, 1, 7, 28, 8, True),
-                                            (71680, 1, 7, 10, 24, True), (153600, 1, 5, 30, 8, True), (163840, 1, 5, 32, 8, True),
+                                            (71680, 1, 7, 10, 24, True), (153600, 1, 6, 25, 10, False), (163840, 1, 8, 20, 12, False),
+                                            (150528, 1, 7, 21, 12, False),
                                             (229376, 1, 7, 32, 8, True), (524288, 1, 8, 64, 4, False),
                                             (1048576, 1, 8, 128, 2, False), (301056, 1, 7, 42, 6, False),
                                             (147456, 1, 9, 16, 16, True), (73728, 1, 9, 8, 32, True),
@@ -166,17 +167,22 @@ def test_python_is_native():
 
 
 def test_kw9_opt_out(monkeypatch):
-    """SART_FUSED_KW9=0 removes the 9-KiB slabs: 147456 voxels then run 6-KiB slabs on 24 CUs per XCD."""
+    """SART_FUSED_KW9=0 removes the 9-KiB slabs: 147456 voxels then run 6-KiB slabs on 24 CUs per XCD (XCD-local
+    groups, SART_FUSED_XL=1)."""
     monkeypatch.setenv("SART_FUSED_KW9", "0")
+    monkeypatch.setenv("SART_FUSED_XL", "1")
     g = rtm.fused_geometry(147456, CUS, 6)
     assert (g.kw, g.J, g.I) == (6, 24, 8)
     assert rtm.fused_geometry(73728, CUS, 6).kw == 8
 
 
 def test_kw5_opt_out(monkeypatch):
-    """5-KiB slabs fill the XCDs at 148480 ... 163840 voxels (150000: J = 30 instead of 6-KiB slabs at J = 25);
-    SART_FUSED_KW5=0 removes them."""
-    assert (rtm.choose_ld(150000), rtm.fused_geometry(153600, CUS, 6).kw) == (153600, 5)
+    """With XCD-local groups only (SART_FUSED_XL=1), 5-KiB slabs fill the XCDs at 148480 ... 163840 voxels (150000:
+    J = 30 instead of 6-KiB slabs at J = 25); SART_FUSED_KW5=0 removes them. (By default 150000 voxels take chip-wide
+    groups of 7-KiB slabs on 252 CUs: 337 against 308 it/s, profiles/cw_r4_xl_vs_cw.txt.)"""
+    assert (rtm.choose_ld(150000), rtm.fused_geometry(150528, CUS, 6).kw) == (150528, 7)
+    monkeypatch.setenv("SART_FUSED_XL", "1")
+    assert rtm.fused_geometry(153600, CUS, 6).kw == 5
     monkeypatch.setenv("SART_FUSED_KW5", "0")
     g = rtm.fused_geometry(153600, CUS, 6)
     assert (g.kw, g.J, g.I) == (6, 25, 8)

@@ -242,9 +242,9 @@ def test_fused_v6_schedules(dev, T, sched, log):
 # Chip-wide row groups (xl False: granules through memory, I = 256 // J) serve rows wider than 32 slabs
 # (300000 ... 1048576 voxels; the reference runs any V: sart_kernels.cu:269-283).
 PROD = [(65536, 4, 32, 8), (131072, 1, 16, 16), (262144, 1, 32, 8),
-        (60000, 4, 30, 8), (100000, 1, 14, 16), (200000, 1, 28, 8), (70000, 1, 10, 24), (73728, 1, 8, 32), (150000, 1, 30, 8),
-        (147456, 1, 16, 16), (294912, 1, 32, 8), (155648, 1, 31, 8), (163840, 1, 32, 8),
-        (300000, 1, 42, 6), (303104, 1, 33, 7), (327680, 1, 36, 7), (524288, 1, 57, 4), (1048576, 1, 114, 2)]
+        (60000, 4, 30, 8), (100000, 1, 14, 16), (200000, 1, 28, 8), (70000, 1, 10, 24), (73728, 1, 8, 32), (150000, 1, 21, 12),
+        (147456, 1, 16, 16), (294912, 1, 32, 8), (155648, 1, 17, 15), (163840, 1, 23, 11),
+        (300000, 1, 42, 6), (303104, 1, 33, 7), (327680, 1, 36, 7), (524288, 1, 64, 4), (1048576, 1, 128, 2)]
 
 
 @pytest.mark.parametrize("nvox,T,J,I", PROD)
@@ -311,7 +311,7 @@ def test_segmented_chains(dev, monkeypatch, storage, nvox, T, log):
 
 @pytest.mark.parametrize("rows,nvox,T,J,I", [(1024, 65536, 4, 32, 8), (512, 131072, 1, 16, 16),
                                              (256, 262144, 1, 32, 8), (512, 100000, 1, 14, 16),
-                                             (128, 524288, 1, 57, 4)])
+                                             (128, 524288, 1, 64, 4)])
 @pytest.mark.parametrize("log", [False, True])
 def test_production_geometry_vs_oracle(dev, rows, nvox, T, J, I, log):
     """The production grids against the host fp64 oracle and the fp32 emulation (fewer rows)."""
@@ -424,11 +424,11 @@ def test_fault_injection_fallback_chain(dev, faults, expect):
     _check(x, A, g, max_iterations=12)
 
 
-@pytest.mark.parametrize("ld,faults,expect", [(524288, 1, 3), (524288, 2, None), (None, 1, None)])
+@pytest.mark.parametrize("ld,faults,expect", [(524288, 1, 3), (524288, 2, None), (525312, 1, None)])
 def test_fault_injection_fallback_chain_chip_wide(dev, ld, faults, expect):
     """The fallback chain from chip-wide row groups (524288 voxels: J > 32 slabs per XCD) to variant 3 and the
-    two-pass kernels, each re-solve against the device fp64 oracle (fused <= 1.25x the two-pass error). At the
-    width choose_ld picks (525312 = 57 slabs of 9216, granule rows padded to 64) variant 3 has no valid slab
+    two-pass kernels, each re-solve against the device fp64 oracle (fused <= 1.25x the two-pass error). At
+    525312 (57 slabs of 9216, granule rows padded to 64) variant 3 has no valid slab
     (513 slabs of 1024), so the first fault goes straight to the two-pass kernels."""
     from mpi_cuda_sartsolver_amd.models.oracle import sart_oracle_f64
     from mpi_cuda_sartsolver_amd.ops import hip
@@ -442,7 +442,7 @@ def test_fault_injection_fallback_chain_chip_wide(dev, ld, faults, expect):
     cfg.fault_inject = faults
     e = k.Engine(dev.index or 0, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld, k.local_comm(), cfg)
     assert e.use_fused and e.geometry.variant == 6 and not e.geometry.xl
-    assert (e.geometry.J, e.geometry.kw) == ((64, 8) if ld else (57, 9))
+    assert (e.geometry.J, e.geometry.kw) == ((64, 8) if ld == 524288 else (57, 9))
     x, info = e.solve(g, None)
     assert info["fallbacks"] == faults and info["used_fused"] == (expect is not None)
     if expect is not None:

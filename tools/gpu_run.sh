@@ -538,6 +538,9 @@ for step in "$@"; do
           SART_MF_XBLK=0 run bench_mfx64_fm 600 python bench.py --steps 3 --warmup 1 --frames 64 &&
           run bench_mfb64_blk 600 python bench.py --steps 3 --warmup 1 --frames 64 --rtm-dtype bf16 &&
           run bench_2tb_blk 900 python bench.py --config 2tb --steps 2 --warmup 1 ;;
+    r4tiles) PROBE_STORAGE=fp32 PROBE_TILES="2,1,as:3;2,1,as:2;4,1,as:3;4,1,as:2;2,2,as:2;2,2,as:3;4,1:3;2,2:2;4,2,as:2" \
+               run probe_tiles 600 python tools/probe_mf_xblk.py ;;
+    r4profmf) run rocprof_mfx64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --no-selfcheck ;;
     r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r4bench) run bench_r4 300 python bench.py --steps 20 --warmup 5 ;;
     r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;

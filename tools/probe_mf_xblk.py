@@ -35,7 +35,7 @@ def main():
                 planes[blk] = (Xh, Xl)
             nsf0 = k.mf_forward_num_splits(m.ld, m.nrows_pad)
             fwd = k.mf_forward_x3 if a32 else k.mf_forward_b16
-            for nsf in sorted({nsf0, 1, 2, 4, 8, 16} & set(range(1, 4 * nsf0 + 1)) | {nsf0}):
+            for nsf in ([] if os.environ.get("PROBE_TILES") else sorted({nsf0, 1, 2, 4, 8, 16} & set(range(1, 4 * nsf0 + 1)) | {nsf0})):
                 Fo = {}
                 for blk in (False, True, False, True):
                     Xh, Xl = planes[blk]
@@ -47,6 +47,25 @@ def main():
                                           nsplit=nsf, default_nsplit=nsf == nsf0, xblk=blk, ms=round(med, 4),
                                           GBps=round(m.nbytes / med / 1e6, 1),
                                           bitwise_equal=bool(torch.equal(Fo[False], out)))), flush=True)
+            # forward tiles / ring depths on blocked planes (PROBE_TILES="RT,KB[,as]:depth;..."), default split count
+            tiles = os.environ.get("PROBE_TILES", "")
+            tenv = "SART_MF_X3_FWD" if a32 else "SART_MF_B16_FWD"
+            denv = "SART_MF_X3_DEPTH" if a32 else "SART_MF_DEPTH"
+            ref = None
+            for spec in [t for t in tiles.split(";") if t]:
+                tile, depth = spec.split(":")
+                os.environ[tenv], os.environ[denv] = tile, depth
+                Xh, Xl = planes[True]
+                out = torch.zeros((nsf0, m.nrows_pad, nf), device=dev)
+                med, _ = timeit(lambda: fwd(m.A.data_ptr(), m.ld, P, m.nrows_pad, Xh.data_ptr(), Xl.data_ptr(),
+                                            out.data_ptr(), nsf0, s, nf, True), reps=7)
+                ref = out if ref is None else ref
+                print(json.dumps(dict(op="mf_forward_x3" if a32 else "mf_forward_b16", P=P, V=V, nf=nf, nsplit=nsf0,
+                                      xblk=True, tile=tile, depth=int(depth), ms=round(med, 4),
+                                      GBps=round(m.nbytes / med / 1e6, 1),
+                                      bitwise_equal_first=bool(torch.equal(ref, out)))), flush=True)
+            for key in (tenv, denv):
+                os.environ.pop(key, None)
             del m, X, planes
             torch.cuda.empty_cache()
 
