@@ -513,7 +513,7 @@ for step in "$@"; do
       done ;;
     r4cwsweep)  # default geometry at 294912 ... 557056 voxels in steps of 8192 (chip-wide row groups above 294912)
       : > "$OUT/cw_sweep.jsonl"
-      for v in $(seq ${CWS_FROM:-294912} 8192 ${CWS_TO:-557056}); do
+      for v in $(seq ${CWS_FROM:-294912} 8192 ${CWS_TO:-557056}) ${CWS_EXTRA:-}; do
         timeout -k 10 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --npix 32768 --no-selfcheck \
           > "$OUT/cws_$v.log" 2>&1 || { echo "FATAL $v"; tail -n 20 "$OUT/cws_$v.log"; exit 1; }
         grep -h '^{' "$OUT/cws_$v.log" >> "$OUT/cw_sweep.jsonl"
