@@ -83,7 +83,8 @@ struct DeviceShard {
 // a staging buffer to drain (copy-bound), and the resident-set high-water mark before / after (the loader's own host
 // memory is the two pinned staging blocks). With the double buffer working, wall ~ max(read, h2d) + one block.
 struct LoadStats {
-    double wall_s = 0, read_s = 0, h2d_s = 0, wait_read_s = 0, wait_copy_s = 0;
+    // setup_s: device allocation, pinned staging and opening the files (before the first block read)
+    double wall_s = 0, setup_s = 0, read_s = 0, h2d_s = 0, wait_read_s = 0, wait_copy_s = 0;
     uint64_t bytes = 0, blocks = 0, rows_per_block = 0, staging_bytes = 0, rows_per_read = 0;
     double rss_hwm_before_mb = 0, rss_hwm_after_mb = 0;
 };
@@ -105,6 +106,7 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
                                                uint64_t col0 = 0, uint64_t ncols = 0, bool bf16 = false,
                                                LoadStats* stats = nullptr) {
     LoadStats ls;
+    hip_ok(hipFree(nullptr), "hipFree");  // the HIP runtime's own footprint is not the loader's
     ls.rss_hwm_before_mb = rss_hwm_mb();
     const auto t_load = std::chrono::steady_clock::now();
     auto sh = std::make_unique<DeviceShard>();
@@ -157,6 +159,7 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
         (void)hipStreamDestroy(s);
         for (auto& b : buf) (void)hipHostFree(b);
     };
+    ls.setup_s = seconds_since(t_load);
     try {
         if (!blocks.empty()) read_into(0, buf[0]);
         for (size_t k = 0; k < blocks.size(); ++k) {
@@ -385,17 +388,19 @@ int main(int argc, char** argv) {
         if (rank == 0 && !cfg.profile_file.empty()) profile.open(cfg.profile_file);
         if (gpu && !cfg.profile_file.empty()) {
             // first profile line: the HDF5 -> HBM load (slowest rank's wall time; totals over ranks)
-            double mx[2] = {lstats.wall_s, lstats.rss_hwm_after_mb - lstats.rss_hwm_before_mb};
+            double mx[3] = {lstats.wall_s, lstats.rss_hwm_after_mb - lstats.rss_hwm_before_mb, lstats.setup_s};
             double sm[5] = {(double)lstats.bytes, lstats.read_s, lstats.h2d_s, lstats.wait_read_s, lstats.wait_copy_s};
-            host->all_reduce_host(mx, 2, ReduceOp::kMax);
+            host->all_reduce_host(mx, 3, ReduceOp::kMax);
             host->all_reduce_host(sm, 5, ReduceOp::kSum);
             if (profile.is_open())
                 profile << "{\"load\": true, \"load_s\": " << mx[0] << ", \"rtm_GB\": " << sm[0] / 1e9
                         << ", \"load_GBps\": " << (mx[0] > 0 ? sm[0] / 1e9 / mx[0] : 0.0)
+                        << ", \"setup_s\": " << mx[2]
                         << ", \"read_s\": " << sm[1] << ", \"h2d_s\": " << sm[2] << ", \"wait_read_s\": " << sm[3]
                         << ", \"wait_copy_s\": " << sm[4] << ", \"ranks\": " << size
                         << ", \"parallel_read\": " << ((cfg.parallel_read || size == 1) ? "true" : "false")
-                        << ", \"rank0\": {\"load_s\": " << lstats.wall_s << ", \"read_s\": " << lstats.read_s
+                        << ", \"rank0\": {\"load_s\": " << lstats.wall_s << ", \"setup_s\": " << lstats.setup_s
+                        << ", \"read_s\": " << lstats.read_s
                         << ", \"h2d_s\": " << lstats.h2d_s << ", \"blocks\": " << lstats.blocks
                         << ", \"rows_per_block\": " << lstats.rows_per_block
                         << ", \"rows_per_read\": " << lstats.rows_per_read

@@ -374,7 +374,7 @@ void Engine::sweep() {
         if (cfg_.rtm_bf16)  // variant 6, K = rows per tile
             launch_fused_sweep_bf16(cfg_.logarithmic, geom_.K, static_cast<const bf16_t*>(A_), ld_, P_, Pp_, x_.get(),
                                     ghat_.get(), arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I,
-                                    geom_.J, st, xcnt_.get(), stream_, geom_.cpl, chain_tiles_, geom_.kw);
+                                    geom_.J, st, xcnt_.get(), stream_, geom_.cpl, chain_tiles_, geom_.kw, geom_.xl);
         else
             launch_fused_sweep(cfg_.logarithmic, geom_.K, geom_.variant, static_cast<const float*>(A_), ld_, P_, Pp_,
                                x_.get(), ghat_.get(), arow_.get(), partial_.get(), Fpart_.get(), gran_.get(), geom_.I,

@@ -129,6 +129,7 @@ V6Candidate best_v6(int64_t ld, int num_cus, int rows_per_tile, bool narrow_slab
 V6Candidate bf16_wide_candidate(int64_t ld, int T, int kw, int num_cus) {
     V6Candidate c;
     if (const char* e = std::getenv("SART_BF16_KW"); e && *e && std::atoi(e) != kw) return c;
+    if (const char* e = std::getenv("SART_BF16_T"); e && *e && std::atoi(e) != T) return c;  // A/B runs
     const int per_xcd = num_cus / 8;
     const int64_t slab = 2048 * (int64_t)kw / T;
     if (num_cus % 8 != 0 || ld % slab != 0) return c;
@@ -138,6 +139,31 @@ V6Candidate bf16_wide_candidate(int64_t ld, int T, int kw, int num_cus) {
     c.I = 8 * (per_xcd / (int)J);
     c.cost = (double)slab / (per_xcd / (int)J) * narrow_slab_penalty(kw);
     return c;
+}
+
+// Wide bf16 tiles in chip-wide row groups (I = num_cus / J groups of any J <= 128, granules through memory): for rows
+// of more than an XCD's 32 slabs at T = 4, or where the XCD-local grid leaves CUs idle. Same cost scale as
+// bf16_wide_candidate (slab / groups per XCD, I / 8 here) times chip_wide_penalty. Opt-in (SART_BF16_XL=0: chip-wide
+// only, 2: both kinds by cost; unset / 1: XCD-local only): the first GPU run (150000 voxels, T = 4, J = 42) missed the
+// bench self-check, 1.40x the two-pass error where XCD-local bf16 sweeps measure 0.86-0.88x.
+V6Candidate bf16_wide_cw_candidate(int64_t ld, int T, int kw, int num_cus) {
+    V6Candidate c;
+    if (const char* e = std::getenv("SART_BF16_KW"); e && *e && std::atoi(e) != kw) return c;
+    if (const char* e = std::getenv("SART_BF16_T"); e && *e && std::atoi(e) != T) return c;
+    if (const char* e = std::getenv("SART_BF16_XL"); !(e && *e && (std::atoi(e) == 0 || std::atoi(e) == 2))) return c;
+    const int64_t slab = 2048 * (int64_t)kw / T;
+    if (ld % slab != 0) return c;
+    const int64_t J = ld / slab;
+    if (J < 2 || J > 128 || J > num_cus) return c;
+    c.T = T, c.J = (int)J, c.kw = kw, c.xl = false;
+    c.I = num_cus / (int)J;
+    c.cost = (double)slab / (c.I / 8.0) * narrow_slab_penalty(kw) * chip_wide_penalty(8);
+    return c;
+}
+
+bool bf16_xl_allowed() {
+    const char* e = std::getenv("SART_BF16_XL");
+    return !(e && *e && std::atoi(e) == 0);
 }
 
 }  // namespace
@@ -152,11 +178,13 @@ int64_t choose_ld(int64_t nvoxel, double max_waste, bool narrow_slabs) {
                 const int64_t slab = 2048 * (int64_t)kw / T;
                 const int64_t ld = (nvoxel + slab - 1) / slab * slab;
                 if ((double)(ld - nvoxel) > max_waste * (double)nvoxel) continue;
-                const V6Candidate c = bf16_wide_candidate(ld, T, kw, 256);
-                if (c.I == 0) continue;
-                if (best_ld == 0 || c.cost < best_cost || (c.cost == best_cost && ld < best_ld)) {
-                    best_ld = ld;
-                    best_cost = c.cost;
+                for (const V6Candidate& c : {bf16_xl_allowed() ? bf16_wide_candidate(ld, T, kw, 256) : V6Candidate{},
+                                             bf16_wide_cw_candidate(ld, T, kw, 256)}) {
+                    if (c.I == 0) continue;
+                    if (best_ld == 0 || c.cost < best_cost || (c.cost == best_cost && ld < best_ld)) {
+                        best_ld = ld;
+                        best_cost = c.cost;
+                    }
                 }
             }
         if (best_ld) return best_ld;
@@ -234,13 +262,15 @@ FusedGeometry fused_geometry_bf16_wide(int64_t ld, int num_cus) {
     // cost slab / G wins, T = 4 and kw 8 on ties (the deeper lag measured faster at 64k x 64k)
     double best_cost = 0.0;
     for (const int kw : {8, 7, 6, 5})
-        for (const int T : {4, 2}) {
-            const V6Candidate c = bf16_wide_candidate(ld, T, kw, num_cus);
-            if (c.I == 0 || (g.valid() && c.cost >= best_cost)) continue;
-            best_cost = c.cost;
-            g.K = T, g.T = T, g.cpl = 8, g.J = c.J, g.I = c.I, g.grid = g.I * g.J, g.variant = 6, g.kw = kw;
-            g.xl = true;
-        }
+        for (const int T : {4, 2})
+            for (const V6Candidate& c : {(bf16_xl_allowed() && num_cus % 8 == 0) ? bf16_wide_candidate(ld, T, kw, num_cus)
+                                                                             : V6Candidate{},
+                                         bf16_wide_cw_candidate(ld, T, kw, num_cus)}) {
+                if (c.I == 0 || (g.valid() && c.cost >= best_cost)) continue;
+                best_cost = c.cost;
+                g.K = T, g.T = T, g.cpl = 8, g.J = c.J, g.I = c.I, g.grid = g.I * g.J, g.variant = 6, g.kw = kw;
+                g.xl = c.xl;
+            }
     return g;
 }
 

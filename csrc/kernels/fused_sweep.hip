@@ -1265,7 +1265,7 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
 void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                              const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                              uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream, int cpl,
-                             int64_t chain_tiles, int kw) {
+                             int64_t chain_tiles, int kw, bool xl) {
     if (T != 1 && T != 2 && T != 4) throw std::runtime_error("fused_sweep bf16: rows per tile must be 1, 2 or 4");
     if (cpl != 4 && !(cpl == 8 && (T == 4 || T == 2)))
         throw std::runtime_error("fused_sweep bf16: wide tiles need T = 4 or 2");
@@ -1277,11 +1277,24 @@ void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, i
     const int64_t slab = 256 * (int64_t)cpl * kw / T;  // 4 / T sub-slabs of 64 lanes x kw lane-vectors x cpl columns
     if (ld % slab != 0 || ld / slab != J) throw std::runtime_error("fused_sweep bf16: ld must equal J * slab");
     if (J * 4 > kMaxGather || J * T > kRowsGather) throw std::runtime_error("fused_sweep bf16: too many slabs");
-    if (xcnt == nullptr || I % 8 != 0) throw std::runtime_error("fused_sweep bf16: needs ticket counters and I % 8 == 0");
+    if (xl && (xcnt == nullptr || I % 8 != 0))
+        throw std::runtime_error("fused_sweep bf16: XCD-local groups need ticket counters and I % 8 == 0");
+    if (!xl && cpl != 8) throw std::runtime_error("fused_sweep bf16: chip-wide row groups take the wide tiles only");
+    if (I < 1) throw std::runtime_error("fused_sweep bf16: no row groups");
     const dim3 grid((unsigned)(I * J));
+    // chip-wide row groups (xl false, wide tiles only): the fp32 chip-wide protocol (granules through memory in
+    // padded rows, the XCD-balanced map) at T = 4 / 2, where a row of 32 wide slabs does not fit one XCD
     auto go = [&](auto lg, auto tt, auto sc, auto cp) {
         constexpr int TT = decltype(tt)::value, SC = decltype(sc)::value, CP = decltype(cp)::value;
         auto run = [&](auto k) {
+            if constexpr (CP == 8) {
+                if (!xl) {
+                    launch_rows_t<decltype(lg)::value, false, false, TT, SC, bf16_t, CP, decltype(k)::value>(
+                        grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
+                        chain_tiles);
+                    return;
+                }
+            }
             launch_rows_t<decltype(lg)::value, true, false, TT, SC, bf16_t, CP, decltype(k)::value>(
                 grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt, chain_tiles);
         };

@@ -108,7 +108,7 @@ bool fused_split_schedule(int T, bool bf16);
 void launch_fused_sweep_bf16(bool logmode, int T, const bf16_t* A, int64_t ld, int64_t nrows, int64_t nrows_pad,
                              const float* x, const float* ghat, const float* arow, float* partial, double* Fpart,
                              uint64_t* gran, int I, int J, SartState* st, unsigned* xcnt, hipStream_t stream,
-                             int cpl = 4, int64_t chain_tiles = 0, int kw = 8);
+                             int cpl = 4, int64_t chain_tiles = 0, int kw = 8, bool xl = true);
 // p2p_allreduce.hip: one-shot push all-reduce through IPC-mapped peer buffers (at most 8 ranks, fp32).
 // Receive buffer of every rank: [2 parities][kP2pMaxRanks sources][cap] floats; flags: [sources][blocks].
 constexpr int kP2pMaxRanks = 8;

@@ -1342,19 +1342,25 @@ static void fwd_b16(int depth, FwdTile tl, dim3 grid, hipStream_t stream, const 
 
 // Split-A tunables (fp32 A on the bf16 matrix cores): SART_MF_X3_FWD = "RT,KB", SART_MF_X3_VT = VT (1 or 2),
 // SART_MF_X3_DEPTH (2 or 3). Twice the bytes of A per fragment as bf16 storage, so smaller register tiles.
-static FwdTile mf_x3_fwd_tile(int nf) {
+static FwdTile mf_x3_fwd_tile(int nf, int64_t ld) {
     const char* e = std::getenv("SART_MF_X3_FWD");
     if (e && *e) {
         FwdTile t{std::atoi(e), std::strchr(e, ',') ? std::atoi(std::strchr(e, ',') + 1) : 1, true};
         t.as = std::strstr(e, "as") != nullptr;  // "RT,KB,as": A staged through LDS
         if ((t.rt == 2 || t.rt == 4) && (t.kb == 1 || t.kb == 2)) return t;
     }
-    // profiles/probe_r2_mf_x3.jsonl, profiles/probe_r2_mf_as.jsonl
-    return nf == 64 ? FwdTile{2, 1, true, true} : FwdTile{2, 2, true};
+    // profiles/probe_r2_mf_x3.jsonl, profiles/probe_r2_mf_as.jsonl; with blocked X planes (round 4,
+    // profiles/probe_r4_mf_x3_fwd_tiles_xblk.jsonl) 64 frames on rows of >= 128k columns take two 32-voxel blocks per
+    // step (16384 x 262144: 3.08 against 3.21 ms; 64k x 64k: 2.96 against 2.90, so narrower rows keep one)
+    if (nf == 64) return ld >= 131072 ? FwdTile{2, 2, true, true} : FwdTile{2, 1, true, true};
+    return FwdTile{2, 2, true};
 }
 static int mf_x3_depth(bool forward) {
+    // the forward's ring: 2 steps ahead on blocked X planes (64k x 64k: 2.90 against 2.98 ms at 3, 16384 x 262144
+    // equal; profiles/probe_r4_mf_x3_fwd_tiles_xblk.jsonl)
+    (void)forward;
     const int d = env_int("SART_MF_X3_DEPTH", 0);
-    return (d == 2 || d == 3) ? d : (forward ? 3 : 2);
+    return (d == 2 || d == 3) ? d : 2;
 }
 static int mf_x3_vt(int64_t ld) {
     const int v = env_int("SART_MF_X3_VT", 0);
@@ -1372,7 +1378,7 @@ static void launch_mf_forward_split(const AT* A, int64_t ld, int64_t nrows, int6
     if (nsplit < 1) throw std::runtime_error(std::string(what) + ": nsplit must be >= 1");
     check_nf_b16(nf, what);
     if (nrows_pad % 32 != 0) throw std::runtime_error(std::string(what) + ": padded rows must be a multiple of 32");
-    FwdTile tl = A32 ? mf_x3_fwd_tile(nf) : mf_b16_fwd_tile(nf);
+    FwdTile tl = A32 ? mf_x3_fwd_tile(nf, ld) : mf_b16_fwd_tile(nf);
     if (nrows_pad % (16 * tl.rt) != 0) tl = FwdTile{2, 1, tl.lds, A32 && tl.as};  // a wave's rows inside the padding
     const FwdCols cps{((ld + nsplit - 1) / nsplit + 63) / 64 * 64, xblk ? 32 : ld, xblk ? 32 * (int64_t)nf : 32};
     const int64_t rows_per_block = 64 * tl.rt;

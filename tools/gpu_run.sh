@@ -528,7 +528,7 @@ for step in "$@"; do
       for v in ${CWAB_WIDTHS:-303104 327680 360448 393216 450560 458752 524288 557056}; do
         for set in ${CWAB_SETS:-: SART_FUSED_GPAD=0}; do
           envs=(); [ "$set" != ":" ] && IFS=, read -ra envs <<< "$set"
-          env "${envs[@]}" timeout -k 10 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --npix 32768 --no-selfcheck \
+          env "${envs[@]}" timeout -k 10 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --npix 32768 ${CWAB_ARGS:---no-selfcheck} \
             > "$OUT/cwab.log" 2>&1 || { echo "FATAL $v $set"; tail -n 20 "$OUT/cwab.log"; exit 1; }
           grep -h '^{' "$OUT/cwab.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); d["ab_set"]=sys.argv[1]; print(json.dumps(d))' "$set" >> "$OUT/cw_ab.jsonl"
           echo "=== cwab $v $set $(tail -n 1 "$OUT/cw_ab.jsonl" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); g=d["fused_grid"]; print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"], g["ld"], g["kw"], g["J"], g["I"], g["xcd_local"], d["fused_schedule"])')" | tee -a "$OUT/session.log"

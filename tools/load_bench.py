@@ -104,9 +104,12 @@ def main() -> int:
         recs = [json.loads(x) for x in open(prof)]
         load = recs[0]
         rec = {"case": case, "process_wall_s": round(wall, 2), **load}
-        rec["overlap"] = {  # a working double buffer: load_s ~ max(read_s, h2d_s) + one block
+        # a working double buffer: load_s ~ setup_s + max(read_s, h2d_s) + one block's copy
+        blk = load["h2d_s"] / max(1, load["rank0"]["blocks"])
+        rec["overlap"] = {
             "max_read_h2d_s": round(max(load["read_s"], load["h2d_s"]), 3),
             "sum_read_h2d_s": round(load["read_s"] + load["h2d_s"], 3),
+            "setup_plus_max_plus_block_s": round(load.get("setup_s", 0.0) + max(load["read_s"], load["h2d_s"]) + blk, 3),
         }
         rec["solve"] = {k: recs[1].get(k) for k in ("iterations", "solve_ms", "fused", "rtm_GBps")} if len(recs) > 1 else None
         emit(rec)
