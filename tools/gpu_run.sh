@@ -541,6 +541,9 @@ for step in "$@"; do
     r4tiles) PROBE_STORAGE=fp32 PROBE_TILES="2,1,as:3;2,1,as:2;4,1,as:3;4,1,as:2;2,2,as:2;2,2,as:3;4,1:3;2,2:2;4,2,as:2" \
                run probe_tiles 600 python tools/probe_mf_xblk.py ;;
     r4profmf) run rocprof_mfx64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --no-selfcheck ;;
+    r4m32) PROBE_ABL=0 PROBE_BWD="${M32_SET:-lds:2,m32:2,m32d3:2,lds:2}" run probe_m32 300 python tools/probe_mf_abl.py &&
+           PROBE_ABL=0 PROBE_BWD="${M32_SET:-lds:2,m32:2,m32d3:2}" run probe_m32_2tb 300 python tools/probe_mf_abl.py 16384x262144 ;;
+    r4m32test) run pytest_m32 600 python -u -m pytest tests/test_gpu_multiframe_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "split_a_projections and m32" ;;
     r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r4bench) run bench_r4 300 python bench.py --steps 20 --warmup 5 ;;
     r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
