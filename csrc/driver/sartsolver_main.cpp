@@ -86,7 +86,7 @@ struct LoadStats {
     // setup_s: device allocation, pinned staging and opening the files (before the first block read)
     double wall_s = 0, setup_s = 0, read_s = 0, h2d_s = 0, wait_read_s = 0, wait_copy_s = 0;
     uint64_t bytes = 0, blocks = 0, rows_per_block = 0, staging_bytes = 0, rows_per_read = 0;
-    double rss_hwm_before_mb = 0, rss_hwm_after_mb = 0;
+    double rss_hwm_before_mb = 0, rss_hwm_after_mb = 0, rss_after_setup_mb = 0, rss_after_first_read_mb = 0;
 };
 
 double rss_hwm_mb() {  // VmHWM of this process, MiB (0 where /proc is unavailable)
@@ -160,8 +160,10 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
         for (auto& b : buf) (void)hipHostFree(b);
     };
     ls.setup_s = seconds_since(t_load);
+    ls.rss_after_setup_mb = rss_hwm_mb();
     try {
         if (!blocks.empty()) read_into(0, buf[0]);
+        ls.rss_after_first_read_mb = rss_hwm_mb();
         for (size_t k = 0; k < blocks.size(); ++k) {
             float* cur = buf[k % 2];
             std::future<void> next;
@@ -406,6 +408,8 @@ int main(int argc, char** argv) {
                         << ", \"rows_per_read\": " << lstats.rows_per_read
                         << ", \"staging_MB\": " << lstats.staging_bytes / 1048576.0
                         << ", \"rss_hwm_before_MB\": " << lstats.rss_hwm_before_mb
+                        << ", \"rss_hwm_after_setup_MB\": " << lstats.rss_after_setup_mb
+                        << ", \"rss_hwm_after_first_read_MB\": " << lstats.rss_after_first_read_mb
                         << ", \"rss_hwm_after_MB\": " << lstats.rss_hwm_after_mb << "}"
                         << ", \"rss_growth_MB_max\": " << mx[1]
                         << ", \"sparse\": " << (in.has_sparse ? "true" : "false") << ", \"driver\": \"native\"}\n";

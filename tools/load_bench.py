@@ -86,6 +86,8 @@ def main() -> int:
         env = dict(env0)
         if case == "dense_row":
             env["SART_RTM_ROWS_PER_READ"] = "1"
+        if case == "dense_small":  # 64 MiB blocks (128 MiB of pinned staging): what the RSS growth scales with
+            env["SART_RTM_BLOCK_MB"] = "64"
         if case == "dense_warm":  # read once to pull the file into the page cache
             with open(path, "rb") as f:
                 while f.read(64 << 20):
