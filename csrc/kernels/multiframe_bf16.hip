@@ -278,7 +278,8 @@ constexpr int mf_fwd_min_waves() { return std::is_same<AT, float>::value ? 1 : (
 
 // ABL: diagnostic ablations as in k_mf_backproject_b16_lds (bit 0 no MFMAs, bit 1 no split of A, bit 2 no X staging
 // and no barrier); 0 in every production launch.
-template <int NG, int DEPTH, int RT, int KB, typename AT = bf16_t, bool AS = false, int ABL = 0>
+// EX (early X): X of step u is loaded at step u - DEPTH - 1, ahead of A's batch (see EW of k_mf_backproject_b16_lds).
+template <int NG, int DEPTH, int RT, int KB, typename AT = bf16_t, bool AS = false, int ABL = 0, bool EX = false>
 __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forward_b16_lds(const AT* __restrict__ A, int64_t ld, int64_t nrows,
                                                             int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                             const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
@@ -331,6 +332,14 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
         u32x4 as_[AS ? RS : 1][NI];
         u32x4 xq[RS][XQ];
         auto piece = [&](int i) { return (C >= 4 ? wave * XQ + i : wave % C); };  // piece = (kb * 2 + plane) * NG + j
+        auto load_x = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+#pragma unroll
+            for (int i = 0; i < XQ; ++i) {
+                const int pc = piece(i), j = pc % NG, plane = (pc / NG) & 1, kb = pc / (2 * NG);
+                xq[sl][i] = *reinterpret_cast<const u32x4*>((plane ? Xl : Xh) + xo + (int64_t)j * 16 * xfs + (t * KB + kb) * xbs);
+            }
+        };
         auto load = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
             const int64_t q = t * 32 * KB;
@@ -353,17 +362,18 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
                     }
                 }
             }
-#pragma unroll
-            for (int i = 0; i < XQ; ++i) {
-                const int pc = piece(i), j = pc % NG, plane = (pc / NG) & 1, kb = pc / (2 * NG);
-                xq[sl][i] = *reinterpret_cast<const u32x4*>((plane ? Xl : Xh) + xo + (int64_t)j * 16 * xfs + (t * KB + kb) * xbs);
-            }
+            if constexpr (!EX) load_x(slc, t);
         };
         auto stage = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
 #pragma unroll
             for (int i = 0; i < XQ; ++i) s_x[t & 1][piece(i)][lofs] = xq[sl][i];
         };
+        if constexpr (EX) {  // X of steps 0 .. DEPTH into slots 0 .. DEPTH, ahead of A's prologue
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (load_x(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
+            }(std::make_integer_sequence<int, RS>{});
+        }
         [&]<int... Q>(std::integer_sequence<int, Q...>) {
             (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
         }(std::make_integer_sequence<int, DEPTH>{});
@@ -371,6 +381,8 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
         __syncthreads();
         auto step = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
+            // EX: X of step t + DEPTH + 1 into this step's slot (X of step t was staged the step before)
+            if constexpr (EX) load_x(slc, t + DEPTH + 1 < nst ? t + DEPTH + 1 : nst - 1);
             load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
             if (t >= nst) return;  // uniform for the workgroup
             // X of step t + 1 goes into the other stage (its readers passed the last barrier). Split-A stages it AFTER
@@ -614,7 +626,11 @@ constexpr int mf_bwd_min_waves() {
 // MFMAs (each fragment folds into an accumulator with one VALU op, so no load is dead), bit 1 drops the split of A
 // (split-A: the raw bits stand for all three pieces), bit 2 drops the W staging (no LDS writes, no barrier: the step
 // re-reads the stage of step 0). Times of the ablated kernels locate the pipe that bounds a step.
-template <int NG, int DEPTH, int VT, typename AT = bf16_t, int ABL = 0>
+// EW (early W): W of step u is loaded one step before A of step u's batch would be (at step u - DEPTH - 1, into ring
+// slot u % RS, whose previous W was staged the step before). The wait that staging step t + 1's W needs then covers
+// only loads issued at step t - DEPTH or earlier; loaded in one batch with A of step t + 1 (EW false), that wait also
+// held every wave until A of step t + 1 had arrived, i.e. one step ahead instead of DEPTH (in-order vmcnt).
+template <int NG, int DEPTH, int VT, typename AT = bf16_t, int ABL = 0, bool EW = false>
 __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::is_same<AT, float>::value && VT == 1 ? 2 : 1))) void k_mf_backproject_b16_lds(const AT* __restrict__ A, int64_t ld,
                                                                 int64_t nrows32, const bf16_t* __restrict__ Wh,
                                                                 const bf16_t* __restrict__ Wl, int64_t ldw,
@@ -659,7 +675,7 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
         auto piece = [&](int i) {  // piece = plane * NG + j
             return C >= 4 ? (wave * XQ + i < C ? wave * XQ + i : C - 1) : wave % C;
         };
-        auto load = [&](auto slc, int64_t t) {
+        auto load_a = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
             const AT* at = ap + t * 32 * ld;
 #pragma unroll
@@ -671,17 +687,29 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
                     else
                         av[sl][vt][j] = load_stream(reinterpret_cast<const uint2*>(at + j * ld + vt * 64));
                 }
+        };
+        auto load_w = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
 #pragma unroll
             for (int i = 0; i < XQ; ++i) {
                 const int pc = piece(i), j = pc % NG, plane = pc / NG;
                 wq[sl][i] = *reinterpret_cast<const u32x4*>(plane_ptr(plane) + wo + (int64_t)j * 16 * ldw + t * 32);
             }
         };
+        auto load = [&](auto slc, int64_t t) {
+            load_a(slc, t);
+            if constexpr (!EW) load_w(slc, t);
+        };
         auto stage = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
 #pragma unroll
             for (int i = 0; i < XQ; ++i) s_w[t & 1][piece(i)][lofs] = wq[sl][i];
         };
+        if constexpr (EW) {  // W of steps 0 .. DEPTH into slots 0 .. DEPTH, ahead of A's prologue
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (load_w(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
+            }(std::make_integer_sequence<int, RS>{});
+        }
         [&]<int... Q>(std::integer_sequence<int, Q...>) {
             (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
         }(std::make_integer_sequence<int, DEPTH>{});
@@ -689,6 +717,8 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
         __syncthreads();
         auto step = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
+            // EW: W of step t + DEPTH + 1 into this step's slot (W of step t was staged the step before)
+            if constexpr (EW) load_w(slc, t + DEPTH + 1 < nst ? t + DEPTH + 1 : nst - 1);
             load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
             if (t >= nst) return;  // uniform for the workgroup
             auto stage_next = [&] {  // W of step t + 1 after this step's MFMAs (see k_mf_forward_b16_lds)
@@ -1441,14 +1471,22 @@ static void fwd_b16_t(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, in
             return;
         }
     }
+    const bool ex = env_int("SART_MF_XEARLY", 1) != 0;  // SART_MF_XEARLY=0: X loaded with A (A/B runs)
     if constexpr (CAN_AS) {
         if (tl.as) {
-            hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB, AT, true>), grid, dim3(256), 0, stream, A, ld,
-                               nrows, nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
+            if (ex)
+                hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB, AT, true, 0, true>), grid, dim3(256), 0,
+                                   stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
+            else
+                hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB, AT, true>), grid, dim3(256), 0, stream, A,
+                                   ld, nrows, nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
             return;
         }
     }
-    if (A32 || tl.lds) {  // split-A: the LDS kernels only
+    if ((A32 || tl.lds) && ex) {
+        hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB, AT, false, 0, true>), grid, dim3(256), 0, stream, A,
+                           ld, nrows, nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
+    } else if (A32 || tl.lds) {  // split-A: the LDS kernels only
         hipLaunchKernelGGL((k_mf_forward_b16_lds<NG, DEPTH, RT, KB, AT>), grid, dim3(256), 0, stream, A, ld, nrows,
                            nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
     } else if constexpr (!A32) {
@@ -1645,6 +1683,17 @@ static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_
         }
     }
     if (std::is_same<AT, float>::value || mf_b16_bwd_lds(16 * NG)) {
+        // SART_MF_WEARLY=0 / 1: W loaded in one batch with A / one step earlier (A/B runs; read per launch). Default
+        // on for bf16 storage; off for split-A, whose two-waves-per-SIMD budget spills 40 VGPRs with the extra W slot
+        if (env_int("SART_MF_WEARLY", std::is_same<AT, float>::value ? 0 : 1) != 0) {
+            if (vt == 2)
+                hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2, AT, 0, true>), grid, dim3(256), 0, stream, A,
+                                   ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+            else
+                hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1, AT, 0, true>), grid, dim3(256), 0, stream, A,
+                                   ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+            return;
+        }
         if (vt == 2)
             hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2, AT>), grid, dim3(256), 0, stream, A, ld,
                                nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);

@@ -544,6 +544,30 @@ for step in "$@"; do
     r4m32) PROBE_ABL=0 PROBE_BWD="${M32_SET:-lds:2,m32:2,m32d3:2,lds:2}" run probe_m32 300 python tools/probe_mf_abl.py &&
            PROBE_ABL=0 PROBE_BWD="${M32_SET:-lds:2,m32:2,m32d3:2}" run probe_m32_2tb 300 python tools/probe_mf_abl.py 16384x262144 ;;
     r4m32test) run pytest_m32 600 python -u -m pytest tests/test_gpu_multiframe_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "split_a_projections and m32" ;;
+    r4bf16cw)  # wide bf16 tiles, XCD-local vs chip-wide groups, self-check on (rc 1 = self-check failed: keep going)
+      for spec in "131072:1:" "131072:0:" "150000:0:4" "150000:0:2" "163840:0:" "150000:1:"; do
+        IFS=: read -r v xl t <<< "$spec"
+        SART_BF16_XL=$xl SART_BF16_T=$t run bf16cw_${v}_${xl}_${t} 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox $v --npix 32768 --rtm-dtype bf16 || exit 1
+        grep -h '^{' "$OUT/bf16cw_${v}_${xl}_${t}.log" >> "$OUT/bf16cw.jsonl" || true
+        grep -h "self-check" "$OUT/bf16cw_${v}_${xl}_${t}.log" | tail -1 || true
+      done ;;
+    r4mfab)  # multi-frame A/B over env settings (MFAB_SETS, "," joins variables; ":" = defaults), 64 frames, both storages
+      : > "$OUT/mf_ab.jsonl"
+      for args in "--frames 64" "--frames 64 --rtm-dtype bf16" ${MFAB_EXTRA:-}; do
+        for set in ${MFAB_SETS:-: SART_MF_WEARLY=0 SART_MF_WEARLY=1 SART_MF_XEARLY=0}; do
+          envs=(); [ "$set" != ":" ] && IFS=, read -ra envs <<< "$set"
+          env "${envs[@]}" timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck $args > "$OUT/mfab.log" 2>&1 \
+            || { echo "FATAL $args $set"; tail -n 20 "$OUT/mfab.log"; exit 1; }
+          grep -h '^{' "$OUT/mfab.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); d["ab_set"]=sys.argv[1]; d["ab_args"]=sys.argv[2]; print(json.dumps(d))' "$set" "$args" >> "$OUT/mf_ab.jsonl"
+          echo "=== mfab [$args] $set $(tail -n 1 "$OUT/mf_ab.jsonl" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
+    r4bf16seg)  # chip-wide bf16 at 150000 voxels: does a shorter back-projection chain (segments) fix the self-check?
+      for seg in 280 700; do
+        SART_BF16_XL=0 SART_BF16_T=4 SART_FUSED_SEG=$seg run bf16seg_$seg 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox 150000 --npix 32768 --rtm-dtype bf16 || true
+        grep -h "self-check\|^{" "$OUT/bf16seg_$seg.log" | cut -c1-300 | tail -2 || true
+      done
+      SART_BF16_XL=1 run bf16seg_xl 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox 150000 --npix 32768 --rtm-dtype bf16 || true ;;
     r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r4bench) run bench_r4 300 python bench.py --steps 20 --warmup 5 ;;
     r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
