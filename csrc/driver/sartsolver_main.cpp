@@ -322,6 +322,9 @@ int main(int argc, char** argv) {
                 host->barrier();
             }
         }
+        if (gpu && rank == 0)  // the HDF5 -> HBM load of this rank's shard (all ranks: the --profile load line)
+            std::cout << "RTM loaded in: " << lstats.wall_s << " s (" << lstats.bytes / 1e9 << " GB, "
+                      << (lstats.wall_s > 0 ? lstats.bytes / 1e9 / lstats.wall_s : 0.0) << " GB/s)" << std::endl;
 
         std::unique_ptr<Engine> engine;
         std::unique_ptr<MultiFrameEngine> mf;

@@ -143,14 +143,15 @@ V6Candidate bf16_wide_candidate(int64_t ld, int T, int kw, int num_cus) {
 
 // Wide bf16 tiles in chip-wide row groups (I = num_cus / J groups of any J <= 128, granules through memory): for rows
 // of more than an XCD's 32 slabs at T = 4, or where the XCD-local grid leaves CUs idle. Same cost scale as
-// bf16_wide_candidate (slab / groups per XCD, I / 8 here) times chip_wide_penalty. Opt-in (SART_BF16_XL=0: chip-wide
-// only, 2: both kinds by cost; unset / 1: XCD-local only): the first GPU run (150000 voxels, T = 4, J = 42) missed the
-// bench self-check, 1.40x the two-pass error where XCD-local bf16 sweeps measure 0.86-0.88x.
+// bf16_wide_candidate (slab / groups per XCD, I / 8 here) times chip_wide_penalty. SART_BF16_XL=0 / 1 keeps only
+// chip-wide / XCD-local groups. Chip-wide and XCD-local sweeps of the same grid give the same iterate (131072 voxels,
+// J = 32: self-check 1.195x the two-pass error both); 32768 x 150000 voxels run at 6.54 TB/s chip-wide (T = 4, J = 42,
+// 700-tile segments) against 4.64 XCD-local in round 3.
 V6Candidate bf16_wide_cw_candidate(int64_t ld, int T, int kw, int num_cus) {
     V6Candidate c;
     if (const char* e = std::getenv("SART_BF16_KW"); e && *e && std::atoi(e) != kw) return c;
     if (const char* e = std::getenv("SART_BF16_T"); e && *e && std::atoi(e) != T) return c;
-    if (const char* e = std::getenv("SART_BF16_XL"); !(e && *e && (std::atoi(e) == 0 || std::atoi(e) == 2))) return c;
+    if (const char* e = std::getenv("SART_BF16_XL"); e && *e && std::atoi(e) == 1) return c;
     const int64_t slab = 2048 * (int64_t)kw / T;
     if (ld % slab != 0) return c;
     const int64_t J = ld / slab;
@@ -290,7 +291,10 @@ ChainPlan fused_chain_plan(const FusedGeometry& g, int64_t nrows_pad, bool split
         return p;
     }
     if (!split_schedule) return p;
-    int64_t seg = 2240;  // > the 2048 tiles per group of the 64k x 64k headline: one chain there
+    // fp32: 2240 tiles (> the 2048 tiles per group of the 64k x 64k headline: one chain there). Wide bf16 tiles: 700
+    // (32768 x 150000 voxels, chip-wide T = 4, 1365 tiles per group: one chain measured 1.40x the two-pass error in the
+    // bench self-check, segments of 700 / 280 tiles 1.16x / 1.24x, and the XCD-local T = 2 grid in one chain 1.59x)
+    int64_t seg = g.cpl == 8 ? 700 : 2240;
     if (const char* e = std::getenv("SART_FUSED_SEG")) seg = std::max<int64_t>(0, std::atoll(e));
     if (seg <= 0) return p;
     seg = (seg + 139) / 140 * 140;

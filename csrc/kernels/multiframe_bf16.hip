@@ -1471,7 +1471,9 @@ static void fwd_b16_t(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, in
             return;
         }
     }
-    const bool ex = env_int("SART_MF_XEARLY", 1) != 0;  // SART_MF_XEARLY=0: X loaded with A (A/B runs)
+    // SART_MF_XEARLY=0 / 1: X loaded with A / a step earlier (A/B runs). Default: split-A only (+0.3 %; bf16 storage
+    // -2.7 %, profiles/ab_r4_mf_early_operands.jsonl)
+    const bool ex = env_int("SART_MF_XEARLY", A32 ? 1 : 0) != 0;
     if constexpr (CAN_AS) {
         if (tl.as) {
             if (ex)
@@ -1684,7 +1686,8 @@ static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_
     }
     if (std::is_same<AT, float>::value || mf_b16_bwd_lds(16 * NG)) {
         // SART_MF_WEARLY=0 / 1: W loaded in one batch with A / one step earlier (A/B runs; read per launch). Default
-        // on for bf16 storage; off for split-A, whose two-waves-per-SIMD budget spills 40 VGPRs with the extra W slot
+        // on for bf16 storage (+0.9 %); off for split-A, whose two-waves-per-SIMD budget spills 40 VGPRs with the extra
+        // W slot (-12 %, profiles/ab_r4_mf_early_operands.jsonl)
         if (env_int("SART_MF_WEARLY", std::is_same<AT, float>::value ? 0 : 1) != 0) {
             if (vt == 2)
                 hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2, AT, 0, true>), grid, dim3(256), 0, stream, A,

@@ -30,14 +30,16 @@ def test_every_width_gets_variant6(nvox):
     ld = rtm.choose_ld(nvox)
     assert nvox <= ld <= 1.10 * nvox
     _check_v6(ld, rtm.fused_geometry(ld, CUS, 6))
-    if nvox > 262144:
-        return  # bf16 tiles: XCD-local row groups only (at most 32 slabs of 8192)
     # bf16 shards: the wide tiles (16 bytes of 8 bf16 per lane, T = 4 / 2, slab 2048 kw / T, kw 5 ... 8) at every
-    # width up to 32 slabs of 8192
+    # width, in XCD-local row groups (J <= 32) or chip-wide ones (J <= 128, I = CUs // J)
     ldb = rtm.choose_ld(nvox, storage="bf16")
     gw = hip().fused_geometry_bf16_wide(ldb, CUS)
     assert nvox <= ldb <= 1.10 * nvox and gw.valid() and gw.cpl == 8 and gw.T in (2, 4) and 5 <= gw.kw <= 8
-    assert ldb == gw.J * 2048 * gw.kw // gw.T and gw.J <= CUS // 8 and gw.I == 8 * ((CUS // 8) // gw.J)
+    assert ldb == gw.J * 2048 * gw.kw // gw.T
+    if gw.xl:
+        assert gw.J <= CUS // 8 and gw.I == 8 * ((CUS // 8) // gw.J)
+    else:
+        assert gw.J <= 128 and gw.I == CUS // gw.J
 
 
 def test_width_sweep_variant6_and_waste():
@@ -117,13 +119,17 @@ def test_forced_rows_per_tile_and_fallback():
     assert rtm.fused_geometry(64 * 1001, CUS, 6) is None
 
 
-@pytest.mark.parametrize("ld,T,J,I", [(65536, 4, 16, 16), (131072, 4, 32, 8), (262144, 2, 32, 8), (204800, 2, 25, 8),
-                                      (4096, 4, 1, 256)])
-def test_bf16_wide_geometry(ld, T, J, I):
-    """Wide bf16 tiles: T = 4 (slab 4096) where it fits an XCD, else T = 2 (slab 8192, schedule 6)."""
+@pytest.mark.parametrize("ld,T,J,I,xl", [(65536, 4, 16, 16, True), (131072, 4, 32, 8, True), (262144, 2, 32, 8, True),
+                                         (204800, 4, 50, 5, False), (4096, 4, 1, 256, True), (524288, 4, 128, 2, False)])
+def test_bf16_wide_geometry(ld, T, J, I, xl, monkeypatch):
+    """Wide bf16 tiles: T = 4 (slab 4096) where it fits an XCD, else T = 2 (slab 8192, schedule 7), or chip-wide row
+    groups where those cost less (204800: J = 50 at T = 4 on 250 CUs instead of 25 slabs at T = 2 on 200). With
+    XCD-local groups only (SART_BF16_XL=1) rows of more than 32 slabs have no fused geometry."""
     g = hip().fused_geometry_bf16_wide(ld, CUS)
-    assert g.valid() and (g.cpl, g.T, g.J, g.I) == (8, T, J, I)
+    assert g.valid() and (g.cpl, g.T, g.J, g.I, g.xl) == (8, T, J, I, xl)
+    monkeypatch.setenv("SART_BF16_XL", "1")
     assert not hip().fused_geometry_bf16_wide(524288, CUS).valid()
+    assert hip().fused_geometry_bf16_wide(204800, CUS).T == 2
 
 
 def test_t1_fold_period(monkeypatch):
@@ -144,14 +150,15 @@ def test_t1_fold_period(monkeypatch):
 
 
 def test_segment_plan(monkeypatch):
-    """T >= 2 split schedules run row groups longer than 2240 tiles in segments, one partial block per segment
-    and tile row; shorter groups (the 64k x 64k headline: 2048 tiles per group) keep one chain."""
+    """T >= 2 split schedules run row groups longer than 2240 tiles (wide bf16 tiles: 700) in segments, one partial
+    block per segment and tile row; shorter groups (the 64k x 64k fp32 headline: 2048 tiles per group) keep one
+    chain."""
     k = hip()
     monkeypatch.delenv("SART_FUSED_SEG", raising=False)
     g4 = k.fused_geometry(65536, CUS, 6, 4)
     assert k.fused_chain_plan(g4, 65536, True) == (0, g4.I)
     gw = k.fused_geometry_bf16_wide(262144, CUS)  # T = 2, I = 8: 32768 tiles per group at 512k rows
-    assert k.fused_chain_plan(gw, 524288, True) == (2240, 8 * 2 * 15)
+    assert k.fused_chain_plan(gw, 524288, True) == (700, 8 * 2 * 47)
     assert k.fused_chain_plan(gw, 524288, False) == (0, 8)  # non-split schedules keep one chain
     monkeypatch.setenv("SART_FUSED_SEG", "1000")  # rounded up to a multiple of 140
     assert k.fused_chain_plan(gw, 524288, True) == (1120, 8 * 2 * 30)
@@ -189,11 +196,11 @@ def test_kw5_opt_out(monkeypatch):
 
 
 @pytest.mark.parametrize("nvox,ld,T,J,kw", [(65536, 65536, 4, 16, 8), (100000, 100352, 4, 28, 7),
-                                           (150000, 153600, 2, 30, 5), (200000, 200704, 2, 28, 7),
+                                           (150000, 150528, 4, 42, 7), (200000, 200704, 2, 28, 7),
                                            (262144, 262144, 2, 32, 8), (70000, 71680, 2, 10, 7)])
 def test_bf16_wide_kw(nvox, ld, T, J, kw, monkeypatch):
     """Wide bf16 tiles take 7 / 6 / 5 lane-vectors per lane where 8-KiB-equivalent slabs leave CUs idle (150000
-    voxels: J = 30 instead of 19); SART_BF16_KW=8 keeps the 8-wide slabs."""
+    voxels: chip-wide J = 42 at T = 4); SART_BF16_KW=8 keeps the 8-wide slabs."""
     ldb = rtm.choose_ld(nvox, storage="bf16")
     g = hip().fused_geometry_bf16_wide(ldb, CUS)
     assert (ldb, g.T, g.J, g.kw) == (ld, T, J, kw)

@@ -221,14 +221,14 @@ def test_bf16_fused_rows_per_tile(dev, T, log):
 
 @pytest.mark.parametrize("nvox,T,J,I,kw", [(4096, 4, 1, 256, 8), (65536, 4, 16, 16, 8), (131072, 4, 32, 8, 8),
                                            (100000, 4, 28, 8, 7), (262144, 2, 32, 8, 8), (200000, 2, 28, 8, 7),
-                                           (150000, 2, 30, 8, 5), (70000, 2, 10, 24, 7), (163840, 2, 32, 8, 5),
-                                           (98304, 4, 32, 8, 6)])
+                                           (150000, 4, 42, 6, 7), (70000, 2, 10, 24, 7), (163840, 2, 23, 11, 7),
+                                           (98304, 4, 32, 8, 6), (300000, 4, 84, 3, 7)])
 @pytest.mark.parametrize("log", [False, True])
 def test_bf16_wide_tiles(dev, monkeypatch, nvox, T, J, I, kw, log):
     """Wide bf16 tiles (16-byte loads of 8 bf16 per lane: slab 2048 kw / T columns, T = 4, or T = 2 with the 3-slot
-    ring of schedule 7; kw 7 / 6 / 5 where 8 would leave CUs idle) against the narrow bf16 tiles (SART_BF16_WIDE=0)
-    where the width allows them, else the two-pass kernels, and the device fp64 oracle on the stored (rounded)
-    matrix."""
+    ring of schedule 7; kw 7 / 6 / 5 where 8 would leave CUs idle; chip-wide row groups at 150000 / 163840 / 300000
+    voxels) against the narrow bf16 tiles (SART_BF16_WIDE=0) where the width allows them, else the two-pass kernels,
+    and the device fp64 oracle on the stored (rounded) matrix."""
     from mpi_cuda_sartsolver_amd.models.oracle import sart_oracle_f64
     from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
     from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem

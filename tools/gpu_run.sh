@@ -568,6 +568,7 @@ for step in "$@"; do
         grep -h "self-check\|^{" "$OUT/bf16seg_$seg.log" | cut -c1-300 | tail -2 || true
       done
       SART_BF16_XL=1 run bf16seg_xl 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox 150000 --npix 32768 --rtm-dtype bf16 || true ;;
+    r4bf16test) run pytest_bf16 900 python -u -m pytest tests/test_gpu_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r4bench) run bench_r4 300 python bench.py --steps 20 --warmup 5 ;;
     r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
