@@ -155,7 +155,7 @@ V6Candidate bf16_wide_cw_candidate(int64_t ld, int T, int kw, int num_cus) {
     const int64_t slab = 2048 * (int64_t)kw / T;
     if (ld % slab != 0) return c;
     const int64_t J = ld / slab;
-    if (J < 2 || J > 128 || J > num_cus) return c;
+    if (J < 2 || J * T > 256 || J > num_cus) return c;  // the gatherer's J T granules per tile (kRowsGather)
     c.T = T, c.J = (int)J, c.kw = kw, c.xl = false;
     c.I = num_cus / (int)J;
     c.cost = (double)slab / (c.I / 8.0) * narrow_slab_penalty(kw) * chip_wide_penalty(8);

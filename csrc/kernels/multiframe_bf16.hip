@@ -630,8 +630,10 @@ constexpr int mf_bwd_min_waves() {
 // slot u % RS, whose previous W was staged the step before). The wait that staging step t + 1's W needs then covers
 // only loads issued at step t - DEPTH or earlier; loaded in one batch with A of step t + 1 (EW false), that wait also
 // held every wave until A of step t + 1 had arrived, i.e. one step ahead instead of DEPTH (in-order vmcnt).
-template <int NG, int DEPTH, int VT, typename AT = bf16_t, int ABL = 0, bool EW = false>
-__global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::is_same<AT, float>::value && VT == 1 ? 2 : 1))) void k_mf_backproject_b16_lds(const AT* __restrict__ A, int64_t ld,
+// MW > 0: waves per SIMD the register budget is cut for, instead of the default (A/B builds: SART_MF_X3_BWD=w1 / w1d3
+// runs the split-A VT = 1 kernel with one wave per SIMD, 512 registers, ring depth 2 / 3).
+template <int NG, int DEPTH, int VT, typename AT = bf16_t, int ABL = 0, bool EW = false, int MW = 0>
+__global__ __launch_bounds__(256, (MW > 0 ? MW : (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::is_same<AT, float>::value && VT == 1 ? 2 : 1)))) void k_mf_backproject_b16_lds(const AT* __restrict__ A, int64_t ld,
                                                                 int64_t nrows32, const bf16_t* __restrict__ Wh,
                                                                 const bf16_t* __restrict__ Wl, int64_t ldw,
                                                                 int64_t rows_per_split, float* __restrict__ partial,
@@ -1619,6 +1621,25 @@ static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_
                       const bf16_t* Wh, const bf16_t* Wl, int64_t ldw, int64_t rps, float* partial, int64_t vb0,
                       int64_t vend) {
     if constexpr (std::is_same<AT, float>::value) {
+        if (const char* w = std::getenv("SART_MF_X3_BWD"); w && w[0] == 'w' && w[1] == '1' && vt == 1) {
+            const bool ew = env_int("SART_MF_WEARLY", 0) != 0;
+            if (std::strcmp(w, "w1d3") == 0) {
+                if (ew)
+                    hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 3, 1, AT, 0, true, 1>), grid, dim3(256), 0, stream, A,
+                                       ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+                else
+                    hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 3, 1, AT, 0, false, 1>), grid, dim3(256), 0, stream,
+                                       A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+            } else {
+                if (ew)
+                    hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 2, 1, AT, 0, true, 1>), grid, dim3(256), 0, stream, A,
+                                       ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+                else
+                    hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 2, 1, AT, 0, false, 1>), grid, dim3(256), 0, stream,
+                                       A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+            }
+            return;
+        }
         if (mf_x3_m32() && vt == 2 && (NG == 2 || NG == 4)) {  // 32x32x16 MFMAs, 128 voxels per wave
             const char* e = std::getenv("SART_MF_X3_BWD");
             constexpr int NT = NG / 2 > 0 ? NG / 2 : 1;

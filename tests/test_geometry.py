@@ -120,7 +120,7 @@ def test_forced_rows_per_tile_and_fallback():
 
 
 @pytest.mark.parametrize("ld,T,J,I,xl", [(65536, 4, 16, 16, True), (131072, 4, 32, 8, True), (262144, 2, 32, 8, True),
-                                         (204800, 4, 50, 5, False), (4096, 4, 1, 256, True), (524288, 4, 128, 2, False)])
+                                         (204800, 4, 50, 5, False), (4096, 4, 1, 256, True), (524288, 2, 64, 4, False)])
 def test_bf16_wide_geometry(ld, T, J, I, xl, monkeypatch):
     """Wide bf16 tiles: T = 4 (slab 4096) where it fits an XCD, else T = 2 (slab 8192, schedule 7), or chip-wide row
     groups where those cost less (204800: J = 50 at T = 4 on 250 CUs instead of 25 slabs at T = 2 on 200). With

@@ -222,7 +222,7 @@ def test_bf16_fused_rows_per_tile(dev, T, log):
 @pytest.mark.parametrize("nvox,T,J,I,kw", [(4096, 4, 1, 256, 8), (65536, 4, 16, 16, 8), (131072, 4, 32, 8, 8),
                                            (100000, 4, 28, 8, 7), (262144, 2, 32, 8, 8), (200000, 2, 28, 8, 7),
                                            (150000, 4, 42, 6, 7), (70000, 2, 10, 24, 7), (163840, 2, 23, 11, 7),
-                                           (98304, 4, 32, 8, 6), (300000, 4, 84, 3, 7)])
+                                           (98304, 4, 32, 8, 6), (300000, 2, 42, 6, 7)])
 @pytest.mark.parametrize("log", [False, True])
 def test_bf16_wide_tiles(dev, monkeypatch, nvox, T, J, I, kw, log):
     """Wide bf16 tiles (16-byte loads of 8 bf16 per lane: slab 2048 kw / T columns, T = 4, or T = 2 with the 3-slot
