@@ -43,9 +43,11 @@ def main():
     ref = None
     for bwd, depth in [tuple(v.split(":")) for v in os.environ.get(
             "PROBE_BWD", "lds:2,pipe2:2,pipe3:2,reg1:2,lds:2").split(",")]:
-        os.environ["SART_MF_X3_BWD"] = bwd
+        # "<variant>_vt2": the same kernel with two 64-voxel tiles per wave (SART_MF_X3_VT=2)
+        os.environ["SART_MF_X3_VT"] = "2" if bwd.endswith("_vt2") else "1"
+        os.environ["SART_MF_X3_BWD"] = bwd[:-4] if bwd.endswith("_vt2") else bwd
         os.environ["SART_MF_X3_DEPTH"] = str(depth)
-        nsv = k.mf_backproject_b16_num_splits(m.ld, P, True)  # m32: 128 voxels per wave, its own split count
+        nsv = k.mf_backproject_b16_num_splits(m.ld, P, True)  # m32 / vt 2: 128 voxels per wave, its own split count
         pv = torch.zeros((nsv, m.ld, nf), device=dev)
         med, best = timeit(lambda: k.mf_backproject_x3(m.A.data_ptr(), m.ld, P, Wh.data_ptr(), Wl.data_ptr(),
                                                        m.nrows_pad, nsv, pv.data_ptr(), s, nf), reps=7)
@@ -58,6 +60,7 @@ def main():
                               rel_vs_first=rel, bitwise_equal_first=bool(rel == 0.0))), flush=True)
         del pv
     os.environ.pop("SART_MF_X3_BWD", None)
+    os.environ["SART_MF_X3_VT"] = "1"
     # the split-A forward (k_mf_forward_b16_lds<4, 3, 2, 1, float, true, ABL>: A staged through LDS, X in LDS)
     X = torch.rand((nf, m.ld), device=dev)
     Xh = torch.empty((nf, m.ld), dtype=torch.bfloat16, device=dev)
