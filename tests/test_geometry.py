@@ -207,3 +207,29 @@ def test_bf16_wide_kw(nvox, ld, T, J, kw, monkeypatch):
     monkeypatch.setenv("SART_BF16_KW", "8")
     g8 = hip().fused_geometry_bf16_wide(rtm.choose_ld(nvox, storage="bf16"), CUS)
     assert g8.kw == 8
+
+
+def test_granule_rows_padded_to_lines():
+    """Chip-wide row groups pad every tile's granule row to whole 128-byte lines (16 granules), so no line holds the
+    granules of two tiles (round 4: 303104 ... 557056 voxels 4.3-5.8 -> 6.0-6.7 TB/s); the buffer covers it."""
+    k = hip()
+    assert k.fused_granules(4096, 33, False) == 4096 * 48
+    assert k.fused_granules(4096, 64, False) == 4096 * 64
+    assert k.fused_granules(4096, 30, True) >= 4096 * 30
+
+
+def test_chip_wide_group_map_is_balanced():
+    """The XCD-balanced map of chip-wide workgroups (fused_sweep.hip: p = workgroups of lower XCDs + b / 8, group
+    p % I): a bijection for every grid, and with I even every group gets J / 8 (+-1) workgroups on every XCD."""
+    for I, J in [(4, 57), (6, 40), (4, 64), (5, 49), (2, 128), (12, 21)]:
+        grid = I * J
+        seen, per = set(), {}
+        for b in range(grid):
+            x = b & 7
+            p = x * (grid >> 3) + min(x, grid & 7) + (b >> 3)
+            seen.add(p)
+            per.setdefault((p % I, x), 0)
+            per[(p % I, x)] += 1
+        assert seen == set(range(grid))
+        counts = [per.get((g, x), 0) for g in range(I) for x in range(8)]
+        assert max(counts) - min(counts) <= 2 and min(counts) >= J // 8 - 1
