@@ -126,6 +126,10 @@ V6Candidate best_v6(int64_t ld, int num_cus, int rows_per_tile, bool narrow_slab
 // 2048 kw / T columns of kw = 8 (16384 / T) or, so that J fills more of an XCD's 32 CUs, kw = 7 / 6 / 5 (kw 9 does
 // not fit the registers next to the wide tiles' two accumulator halves). XCD-local groups only. Cost as v6_candidate:
 // slab / G times the narrow-slab penalty; T = 4 and kw 8 first on ties. SART_BF16_KW=k keeps only k (A/B runs).
+// Wide bf16 tiles at T = 2 (schedule 7) stream ~12 % slower per CU than at T = 4 (200000 voxels, T = 2: 23.2 GB/s per CU;
+// 150000 chip-wide at T = 4: 26.1; profiles/bf16_r4_widths_cw_vs_xl.jsonl).
+double bf16_t2_penalty(int T) { return T == 2 ? 1.12 : 1.0; }
+
 V6Candidate bf16_wide_candidate(int64_t ld, int T, int kw, int num_cus) {
     V6Candidate c;
     if (const char* e = std::getenv("SART_BF16_KW"); e && *e && std::atoi(e) != kw) return c;
@@ -137,7 +141,7 @@ V6Candidate bf16_wide_candidate(int64_t ld, int T, int kw, int num_cus) {
     if (J < 1 || J > per_xcd) return c;
     c.T = T, c.J = (int)J, c.kw = kw, c.xl = true;
     c.I = 8 * (per_xcd / (int)J);
-    c.cost = (double)slab / (per_xcd / (int)J) * narrow_slab_penalty(kw);
+    c.cost = (double)slab / (per_xcd / (int)J) * narrow_slab_penalty(kw) * bf16_t2_penalty(T);
     return c;
 }
 
@@ -158,7 +162,9 @@ V6Candidate bf16_wide_cw_candidate(int64_t ld, int T, int kw, int num_cus) {
     if (J < 2 || J * T > 256 || J > num_cus) return c;  // the gatherer's J T granules per tile (kRowsGather)
     c.T = T, c.J = (int)J, c.kw = kw, c.xl = false;
     c.I = num_cus / (int)J;
-    c.cost = (double)slab / (c.I / 8.0) * narrow_slab_penalty(kw) * chip_wide_penalty(8);
+    // priced like XCD-local wide tiles: chip-wide and XCD-local grids of the same J stream alike (131072 voxels: 781
+    // against 778 it/s, profiles/bf16_r4_widths_cw_vs_xl.jsonl)
+    c.cost = (double)slab / (c.I / 8.0) * narrow_slab_penalty(kw) * bf16_t2_penalty(T);
     return c;
 }
 

@@ -119,7 +119,7 @@ def test_forced_rows_per_tile_and_fallback():
     assert rtm.fused_geometry(64 * 1001, CUS, 6) is None
 
 
-@pytest.mark.parametrize("ld,T,J,I,xl", [(65536, 4, 16, 16, True), (131072, 4, 32, 8, True), (262144, 2, 32, 8, True),
+@pytest.mark.parametrize("ld,T,J,I,xl", [(65536, 4, 16, 16, True), (131072, 4, 32, 8, True), (262144, 4, 64, 4, False),
                                          (204800, 4, 50, 5, False), (4096, 4, 1, 256, True), (524288, 2, 64, 4, False)])
 def test_bf16_wide_geometry(ld, T, J, I, xl, monkeypatch):
     """Wide bf16 tiles: T = 4 (slab 4096) where it fits an XCD, else T = 2 (slab 8192, schedule 7), or chip-wide row
@@ -130,6 +130,8 @@ def test_bf16_wide_geometry(ld, T, J, I, xl, monkeypatch):
     monkeypatch.setenv("SART_BF16_XL", "1")
     assert not hip().fused_geometry_bf16_wide(524288, CUS).valid()
     assert hip().fused_geometry_bf16_wide(204800, CUS).T == 2
+    g2 = hip().fused_geometry_bf16_wide(262144, CUS)
+    assert (g2.T, g2.J, g2.I, g2.xl) == (2, 32, 8, True)
 
 
 def test_t1_fold_period(monkeypatch):
@@ -157,7 +159,8 @@ def test_segment_plan(monkeypatch):
     monkeypatch.delenv("SART_FUSED_SEG", raising=False)
     g4 = k.fused_geometry(65536, CUS, 6, 4)
     assert k.fused_chain_plan(g4, 65536, True) == (0, g4.I)
-    gw = k.fused_geometry_bf16_wide(262144, CUS)  # T = 2, I = 8: 32768 tiles per group at 512k rows
+    monkeypatch.setenv("SART_BF16_XL", "1")
+    gw = k.fused_geometry_bf16_wide(262144, CUS)  # XCD-local T = 2, I = 8: 32768 tiles per group at 512k rows
     assert k.fused_chain_plan(gw, 524288, True) == (700, 8 * 2 * 47)
     assert k.fused_chain_plan(gw, 524288, False) == (0, 8)  # non-split schedules keep one chain
     monkeypatch.setenv("SART_FUSED_SEG", "1000")  # rounded up to a multiple of 140
@@ -196,8 +199,8 @@ def test_kw5_opt_out(monkeypatch):
 
 
 @pytest.mark.parametrize("nvox,ld,T,J,kw", [(65536, 65536, 4, 16, 8), (100000, 100352, 4, 28, 7),
-                                           (150000, 150528, 4, 42, 7), (200000, 200704, 2, 28, 7),
-                                           (262144, 262144, 2, 32, 8), (70000, 71680, 2, 10, 7)])
+                                           (150000, 150528, 4, 42, 7), (200000, 200704, 4, 49, 8),
+                                           (262144, 262144, 4, 64, 8), (70000, 73728, 4, 18, 8)])
 def test_bf16_wide_kw(nvox, ld, T, J, kw, monkeypatch):
     """Wide bf16 tiles take 7 / 6 / 5 lane-vectors per lane where 8-KiB-equivalent slabs leave CUs idle (150000
     voxels: chip-wide J = 42 at T = 4); SART_BF16_KW=8 keeps the 8-wide slabs."""

@@ -220,9 +220,9 @@ def test_bf16_fused_rows_per_tile(dev, T, log):
 
 
 @pytest.mark.parametrize("nvox,T,J,I,kw", [(4096, 4, 1, 256, 8), (65536, 4, 16, 16, 8), (131072, 4, 32, 8, 8),
-                                           (100000, 4, 28, 8, 7), (262144, 2, 32, 8, 8), (200000, 2, 28, 8, 7),
-                                           (150000, 4, 42, 6, 7), (70000, 2, 10, 24, 7), (163840, 2, 23, 11, 7),
-                                           (98304, 4, 32, 8, 6), (300000, 2, 42, 6, 7)])
+                                           (100000, 4, 28, 9, 7), (262144, 4, 64, 4, 8), (200000, 4, 49, 5, 8),
+                                           (150000, 4, 42, 6, 7), (70000, 4, 18, 14, 8), (163840, 4, 40, 6, 8),
+                                           (98304, 4, 28, 9, 7), (300000, 2, 42, 6, 7)])
 @pytest.mark.parametrize("log", [False, True])
 def test_bf16_wide_tiles(dev, monkeypatch, nvox, T, J, I, kw, log):
     """Wide bf16 tiles (16-byte loads of 8 bf16 per lane: slab 2048 kw / T columns, T = 4, or T = 2 with the 3-slot
@@ -268,6 +268,7 @@ def test_bf16_wide_t2_schedules_agree(dev, monkeypatch, log):
     from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
     from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
 
+    monkeypatch.setenv("SART_BF16_XL", "1")  # XCD-local groups: 262144 voxels at T = 2 (by default chip-wide at T = 4)
     prob = make_problem(4096, 262144, seed=7, device=dev, saturate_fraction=0.02, storage="bf16")
     g = prob.measurement.cpu().numpy()
     p = SolverParams(max_iterations=8, conv_tolerance=0.0)

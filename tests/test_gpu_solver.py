@@ -275,7 +275,7 @@ def test_production_geometry_vs_f64_oracle(dev, nvox, T, J, I, log):
 
 
 @pytest.mark.parametrize("storage,nvox,T", [("fp32", 65536, 4), ("fp32", 60000, 4), ("fp32", 131072, 1),
-                                            ("bf16", 262144, 2), ("bf16", 131072, 4)])
+                                            ("bf16", 262144, 4), ("bf16", 300000, 2), ("bf16", 131072, 4)])
 @pytest.mark.parametrize("log", [False, True])
 def test_segmented_chains(dev, monkeypatch, storage, nvox, T, log):
     """Row groups longer than SART_FUSED_SEG tiles run in segments (split schedules, T >= 2; T = 1 folds in
