@@ -85,7 +85,11 @@ V6Candidate v6_candidate(int64_t ld, int T, int kw, int num_cus, bool xl) {
         if (J > per_xcd) return c;
         c.I = 8 * (per_xcd / (int)J);
     } else {
-        if (T != 1 || J > num_cus) return c;
+        // chip-wide: T = 1 (schedule 5 / 8) at any kw, T = 2 / 4 (schedule 4) at kw 6 ... 8 (SART_FUSED_CW_T=1: T = 1
+        // only, A/B runs)
+        const char* e = std::getenv("SART_FUSED_CW_T");
+        const int tmax = (e && *e) ? std::atoi(e) : 4;
+        if (J > num_cus || T > tmax || (T != 1 && (kw < 6 || kw > 8))) return c;
         c.I = num_cus / (int)J;
     }
     c.T = T, c.J = (int)J, c.kw = kw, c.xl = xl;

@@ -1133,8 +1133,22 @@ static void launch_rows(bool logmode, dim3 grid, hipStream_t stream, const float
             };
             if (logmode) by_kw(std::true_type{}); else by_kw(std::false_type{});
             return;
+        } else {
+            // T = 2 / 4 (schedule 4, x slab in LDS): rows of more than an XCD's 32 slabs of 2048 / 4096 columns
+            auto go_cw = [&](auto lg, auto k) {
+                launch_rows_t<decltype(lg)::value, false, false, T, 4, float, 4, decltype(k)::value>(
+                    grid, stream, A, ld, nrows, nrows_pad, x_, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
+                    chain_tiles);
+            };
+            auto by_kw = [&](auto lg) {
+                if (kw == 8) go_cw(lg, std::integral_constant<int, 8>{});
+                else if (kw == 7) go_cw(lg, std::integral_constant<int, 7>{});
+                else if (kw == 6) go_cw(lg, std::integral_constant<int, 6>{});
+                else throw std::runtime_error("fused_sweep v6: chip-wide T >= 2 needs kw 6 ... 8");
+            };
+            if (logmode) by_kw(std::true_type{}); else by_kw(std::false_type{});
+            return;
         }
-        throw std::runtime_error("fused_sweep v6: chip-wide row groups need T = 1");
     }
     const bool diag = (g_fused_dbg & 2) != 0;  // instrumented build only when asked (timing diagnostics)
     // g_fused_sched: pipeline schedule (k_fused_sweep_rows SCHED); schedules 1-4 hold the x slab in LDS,
@@ -1231,7 +1245,8 @@ void launch_fused_sweep(bool logmode, int K, int variant, const float* A, int64_
         if (J * T > kRowsGather) throw std::runtime_error("fused_sweep v6: J * T > 256");
         if (xl && (xcnt == nullptr || I % 8 != 0))
             throw std::runtime_error("fused_sweep v6: XCD-local groups need the per-XCD ticket counters and I % 8 == 0");
-        if (!xl && T != 1) throw std::runtime_error("fused_sweep v6: chip-wide row groups need T = 1");
+        if (!xl && T != 1 && (kw < 6 || kw > 8))
+            throw std::runtime_error("fused_sweep v6: chip-wide row groups at T >= 2 need kw 6 ... 8");
         if (I < 1) throw std::runtime_error("fused_sweep v6: no row groups");
         if (T == 1) launch_rows<1>(logmode, grid, stream, A, ld, nrows, nrows_pad, x, ghat, arow, partial, Fpart, gran, I, J, st, xcnt,
                         chain_tiles, kw, xl);

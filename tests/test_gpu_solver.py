@@ -274,6 +274,31 @@ def test_production_geometry_vs_f64_oracle(dev, nvox, T, J, I, log):
     assert ef <= 1.25 * e2 + 1e-7, f"fused {ef:.3e} vs two-pass {e2:.3e}"
 
 
+@pytest.mark.parametrize("nvox,T", [(131072, 4), (100000, 4), (303104, 2), (524288, 2)])
+@pytest.mark.parametrize("log", [False, True])
+def test_chip_wide_multirow_tiles_vs_f64_oracle(dev, monkeypatch, nvox, T, log):
+    """fp32 chip-wide row groups at T = 2 / 4 (schedule 4, x slab in LDS; SART_FUSED_XL=0, SART_FUSED_T forced)
+    against the device fp64 oracle, within 1.25x the two-pass kernels' error."""
+    from mpi_cuda_sartsolver_amd.models.oracle import sart_oracle_f64
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+    from mpi_cuda_sartsolver_amd.utils.synthetic import make_problem
+
+    monkeypatch.setenv("SART_FUSED_XL", "0")
+    monkeypatch.setenv("SART_FUSED_T", str(T))
+    prob = make_problem(4096, nvox, seed=nvox % 97, device=dev, saturate_fraction=0.02)
+    g = prob.measurement.cpu().numpy()
+    p = dict(max_iterations=10, conv_tolerance=0.0)
+    sf = SARTSolver(prob.rtm, None, None, SolverParams(**p), logarithmic=log, allow_zero_tolerance=True)
+    assert sf.use_fused and (sf.geom.variant, sf.geom.T, sf.geom.xl) == (6, T, False)
+    rf = sf.solve(g)
+    assert rf.used_fused and rf.fallbacks == 0 and rf.iterations == 10
+    del sf
+    r2 = SARTSolver(prob.rtm, None, None, SolverParams(**p), logarithmic=log, use_fused=False,
+                    allow_zero_tolerance=True).solve(g)
+    x64 = sart_oracle_f64(prob.rtm, g, 10, logarithmic=log)
+    assert _rel(rf.solution, x64) <= 1.25 * _rel(r2.solution, x64) + 1e-7
+
+
 @pytest.mark.parametrize("storage,nvox,T", [("fp32", 65536, 4), ("fp32", 60000, 4), ("fp32", 131072, 1),
                                             ("bf16", 262144, 4), ("bf16", 300000, 2), ("bf16", 131072, 4)])
 @pytest.mark.parametrize("log", [False, True])
