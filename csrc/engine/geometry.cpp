@@ -85,10 +85,11 @@ V6Candidate v6_candidate(int64_t ld, int T, int kw, int num_cus, bool xl) {
         if (J > per_xcd) return c;
         c.I = 8 * (per_xcd / (int)J);
     } else {
-        // chip-wide: T = 1 (schedule 5 / 8) at any kw, T = 2 / 4 (schedule 4) at kw 6 ... 8 (SART_FUSED_CW_T=1: T = 1
-        // only, A/B runs)
+        // chip-wide: T = 1 (schedule 5 / 8) at any kw; T = 2 / 4 (schedule 4, kw 6 ... 8) only with SART_FUSED_CW_T=2 / 4:
+        // no faster than T = 1 where measured (100000 / 150000 / 393216 / 524288 voxels: -1 ... -20 %, 303104 equal;
+        // profiles/cw_r4_multirow_t_ab.jsonl) and T = 2 at 303104 voxels missed the 1.25x error bound (1.58x)
         const char* e = std::getenv("SART_FUSED_CW_T");
-        const int tmax = (e && *e) ? std::atoi(e) : 4;
+        const int tmax = (e && *e) ? std::atoi(e) : 1;
         if (J > num_cus || T > tmax || (T != 1 && (kw < 6 || kw > 8))) return c;
         c.I = num_cus / (int)J;
     }
