@@ -637,8 +637,14 @@ __global__ __launch_bounds__(256, (MW > 0 ? MW : (NG == 4 ? mf_bwd_min_waves<AT,
                                                                 int64_t nrows32, const bf16_t* __restrict__ Wh,
                                                                 const bf16_t* __restrict__ Wl, int64_t ldw,
                                                                 int64_t rows_per_split, float* __restrict__ partial,
-                                                                int64_t vb0, int64_t vend, const int* __restrict__ skip) {
+                                                                int64_t vb0, int64_t vend, const int* __restrict__ skip,
+                                                                int stagger) {
     if (skip && *skip) return;
+    // stagger (A/B runs, SART_MF_STAGGER=n): workgroups of odd 256-block rounds (the second workgroup a CU receives)
+    // start n x 1024 cycles late, so the two workgroups sharing a CU's SIMDs are not in lockstep (MI355X_MICROARCH.md,
+    // 'try a stagger')
+    if (stagger > 0 && (((blockIdx.x + blockIdx.y * gridDim.x) >> 8) & 1))
+        for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(16);
     constexpr int NF = 16 * NG;
     constexpr int RS = DEPTH + 1;
     constexpr bool A32 = std::is_same<AT, float>::value;
@@ -1376,6 +1382,11 @@ __global__ __launch_bounds__(256, 1) void k_mf_backproject_x3_m32(const float* _
             }
 }
 
+static int mf_stagger() {
+    const char* e = std::getenv("SART_MF_STAGGER");
+    return (e && *e) ? std::atoi(e) : 0;
+}
+
 static void check_nf_b16(int nf, const char* what) {
     if (nf != 16 && nf != 32 && nf != 64) throw std::runtime_error(std::string(what) + ": nf must be 16, 32 or 64");
 }
@@ -1626,17 +1637,17 @@ static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_
             if (std::strcmp(w, "w1d3") == 0) {
                 if (ew)
                     hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 3, 1, AT, 0, true, 1>), grid, dim3(256), 0, stream, A,
-                                       ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+                                       ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
                 else
                     hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 3, 1, AT, 0, false, 1>), grid, dim3(256), 0, stream,
-                                       A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+                                       A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
             } else {
                 if (ew)
                     hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 2, 1, AT, 0, true, 1>), grid, dim3(256), 0, stream, A,
-                                       ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+                                       ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
                 else
                     hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 2, 1, AT, 0, false, 1>), grid, dim3(256), 0, stream,
-                                       A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+                                       A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
             }
             return;
         }
@@ -1691,7 +1702,7 @@ static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_
         if (abl > 0 && vt == 1) {
             auto go = [&](auto k) {
                 hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1, AT, decltype(k)::value>), grid, dim3(256), 0,
-                                   stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+                                   stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
             };
             switch (abl & 7) {
                 case 1: go(std::integral_constant<int, 1>{}); break;
@@ -1712,18 +1723,18 @@ static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_
         if (env_int("SART_MF_WEARLY", std::is_same<AT, float>::value ? 0 : 1) != 0) {
             if (vt == 2)
                 hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2, AT, 0, true>), grid, dim3(256), 0, stream, A,
-                                   ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+                                   ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
             else
                 hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1, AT, 0, true>), grid, dim3(256), 0, stream, A,
-                                   ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+                                   ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
             return;
         }
         if (vt == 2)
             hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2, AT>), grid, dim3(256), 0, stream, A, ld,
-                               nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+                               nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
         else
             hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1, AT>), grid, dim3(256), 0, stream, A, ld,
-                               nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
+                               nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
         return;
     }
     if constexpr (!std::is_same<AT, float>::value) {

@@ -569,6 +569,9 @@ for step in "$@"; do
       done
       SART_BF16_XL=1 run bf16seg_xl 200 python bench.py --steps 3 --warmup 1 --iters 50 --nvox 150000 --npix 32768 --rtm-dtype bf16 || true ;;
     r4bf16test) run pytest_bf16 900 python -u -m pytest tests/test_gpu_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    r4pmcbwd)  # PMC of the split-A 64-frame back-projection (probe, default kernel): issue / co-execution counters
+      PROBE_ABL=0 PROBE_BWD="lds:2" timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE \
+        -d "$OUT/pmc_bwd" -o run --output-format csv -- python3 tools/probe_mf_abl.py > "$OUT/pmc_bwd.log" 2>&1 || { echo "FATAL pmc"; tail -n 20 "$OUT/pmc_bwd.log"; exit 1; } ;;
     r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r4bench) run bench_r4 300 python bench.py --steps 20 --warmup 5 ;;
     r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;

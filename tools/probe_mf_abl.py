@@ -43,7 +43,10 @@ def main():
     ref = None
     for bwd, depth in [tuple(v.split(":")) for v in os.environ.get(
             "PROBE_BWD", "lds:2,pipe2:2,pipe3:2,reg1:2,lds:2").split(",")]:
-        # "<variant>_vt2": the same kernel with two 64-voxel tiles per wave (SART_MF_X3_VT=2)
+        # "<variant>@n": SART_MF_STAGGER=n; "<variant>_vt2": two 64-voxel tiles per wave (SART_MF_X3_VT=2)
+        name = bwd
+        bwd, _, stg = bwd.partition("@")
+        os.environ["SART_MF_STAGGER"] = stg or "0"
         os.environ["SART_MF_X3_VT"] = "2" if bwd.endswith("_vt2") else "1"
         os.environ["SART_MF_X3_BWD"] = bwd[:-4] if bwd.endswith("_vt2") else bwd
         os.environ["SART_MF_X3_DEPTH"] = str(depth)
@@ -55,7 +58,7 @@ def main():
         if ref is None:
             ref = out
         rel = float((out - ref).norm() / ref.norm())
-        print(json.dumps(dict(op="mf_backproject_x3", variant=bwd, depth=depth, nf=nf, P=P, V=V, nsplit=nsv,
+        print(json.dumps(dict(op="mf_backproject_x3", variant=name, depth=depth, nf=nf, P=P, V=V, nsplit=nsv,
                               ms=round(med, 4), GBps=round(m.nbytes / med / 1e6, 1),
                               rel_vs_first=rel, bitwise_equal_first=bool(rel == 0.0))), flush=True)
         del pv
