@@ -458,6 +458,23 @@ PYBIND11_MODULE(_sart_hip, m) {
         sart::launch_mf_split_x(P<const float>(X), n, P<sart::bf16_t>(hi), P<sart::bf16_t>(lo), S(stream), perm, ld);
     }, py::arg("X"), py::arg("n"), py::arg("hi"), py::arg("lo"), py::arg("stream"), py::arg("perm") = false,
        py::arg("ld") = 0);
+    m.def("mf_split_w16", [](uintptr_t W, int64_t nrows_pad, int nf, int64_t ldw, uintptr_t w1, uintptr_t w2,
+                             uintptr_t wmax, float a_scale, uintptr_t inv_scale, uintptr_t stream) {
+        sart::launch_mf_split_w16(P<const float>(W), nrows_pad, nf, ldw, P<uint16_t>(w1), P<uint16_t>(w2),
+                                  P<unsigned>(wmax), a_scale, P<float>(inv_scale), S(stream));
+    });
+    m.def("absmax_pow2_scale", [](uintptr_t A, int64_t n, uintptr_t scratch, uintptr_t stream) {
+        return sart::absmax_pow2_scale(P<const float>(A), n, P<unsigned>(scratch), S(stream));
+    });
+    m.def("mf_backproject_h16", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t W1, uintptr_t W2, int64_t ldw,
+                                   int nsplit, uintptr_t partial, uintptr_t stream, int nf, int64_t v0, int64_t v1,
+                                   float a_scale, uintptr_t inv_scale) {
+        sart::launch_mf_backproject_h16(P<const float>(A), ld, nrows, P<const uint16_t>(W1), P<const uint16_t>(W2), ldw,
+                                        nsplit, P<float>(partial), nf, S(stream), v0, v1, a_scale,
+                                        P<const float>(inv_scale));
+    }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("W1"), py::arg("W2"), py::arg("ldw"), py::arg("nsplit"),
+       py::arg("partial"), py::arg("stream"), py::arg("nf"), py::arg("v0"), py::arg("v1"), py::arg("a_scale"),
+       py::arg("inv_scale"));
     m.def("mf_split_w", [](uintptr_t W, int64_t nrows_pad, int nf, int64_t ldw, uintptr_t hi, uintptr_t lo,
                            uintptr_t stream, bool three) {
         sart::launch_mf_split_w(P<const float>(W), nrows_pad, nf, ldw, P<sart::bf16_t>(hi), P<sart::bf16_t>(lo),

@@ -74,8 +74,18 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     st_.resize(1);
     if (split_) {
         for (auto* b : {&Xh_, &Xl_}) b->resize((size_t)NF * ld_);
-        Wh_.resize((size_t)(x3_ ? 2 : 1) * NF * Pp_);  // split-A: hi and mid planes
-        Wl_.resize((size_t)NF * Pp_);
+        // split-A back-projection: f16 pairs (three products) unless SART_MF_BWD16=0 (bf16 hi + mid + lo, six)
+        const char* e = std::getenv("SART_MF_BWD16");
+        h16_ = x3_ && !(e && *e && std::atoi(e) == 0);
+        if (h16_) {
+            W16_.resize((size_t)2 * NF * Pp_);
+            wmax_.resize(NF);
+            wscale_.resize(NF);
+            a_scale_ = absmax_pow2_scale(static_cast<const float*>(A_), Pp_ * ld_, wmax_.get(), stream_);
+        } else {
+            Wh_.resize((size_t)(x3_ ? 2 : 1) * NF * Pp_);  // split-A: hi and mid planes
+            Wl_.resize((size_t)NF * Pp_);
+        }
     }
     rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_, false, bf16_);
     // chunks of the overlapped back-projection / all-reduce pipeline (several ranks only): SART_MF_CHUNKS
@@ -156,7 +166,13 @@ void MultiFrameEngine::forward() {
 }
 
 void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int64_t v1) {
-    if (split_) {
+    if (h16_) {
+        uint16_t* w1 = W16_.get();
+        uint16_t* w2 = W16_.get() + (size_t)nf_ * Pp_;
+        if (split_w) launch_mf_split_w16(W, Pp_, nf_, Pp_, w1, w2, wmax_.get(), a_scale_, wscale_.get(), stream_);
+        launch_mf_backproject_h16(static_cast<const float*>(A_), ld_, P_, w1, w2, Pp_, nsb_, part_.get(), nf_, stream_,
+                                  v0, v1, a_scale_, wscale_.get());
+    } else if (split_) {
         if (split_w) launch_mf_split_w(W, Pp_, nf_, Pp_, Wh_.get(), Wl_.get(), stream_, x3_);
         if (bf16_)
             launch_mf_backproject_b16(static_cast<const bf16_t*>(A_), ld_, P_, Wh_.get(), Wl_.get(), Pp_, nsb_,

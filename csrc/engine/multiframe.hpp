@@ -76,6 +76,13 @@ class MultiFrameEngine {
     DeviceArray<float> X_, Xprev_, Fs_, W_, part_, buf_, pen_, O_, ghat_, arow_, gpos_, wo_;
     DeviceArray<double> g64_, G64_, F2part_, x064_;
     DeviceArray<bf16_t> Xh_, Xl_, Wh_, Wl_;  // bf16 / split-A engine: hi / lo operand planes
+    // split-A back-projection on f16 pairs (launch_mf_backproject_h16): planes w1 | w2 ([2][nf][Pp] f16 bits),
+    // per-frame max scratch and 1 / (a_scale s_f), and the shard's power-of-two scale
+    bool h16_ = false;
+    float a_scale_ = 1.f;
+    DeviceArray<bf16_t> W16_;
+    DeviceArray<unsigned> wmax_;
+    DeviceArray<float> wscale_;
     DeviceArray<MfState> st_;
     DeviceArray<int64_t> lap_rp_;
     DeviceArray<int32_t> lap_col_;

@@ -191,6 +191,17 @@ void launch_mf_backproject_x3(const float* A, int64_t ld, int64_t nrows, const b
 // [nf = n / ld][ld] and the planes are written blocked, [ld / 32][nf][32] (the forward's xblk layout)
 void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStream_t stream, bool perm = false,
                        int64_t ld = 0);
+// fp16-pair back-projection operands: frame-major planes w1, w2 ([nf][ldw] of f16 bits) of w s_f with a per-frame
+// power-of-two scale s_f (from the frame's max |w|, wmax: nf words of scratch), inv_scale[f] = 1 / (a_scale s_f)
+void launch_mf_split_w16(const float* W, int64_t nrows_pad, int nf, int64_t ldw, uint16_t* w1, uint16_t* w2,
+                         unsigned* wmax, float a_scale, float* inv_scale, hipStream_t stream);
+// power-of-two scale 2^(14 - e) for max |A| = m 2^e over n floats (1 if A is zero); synchronises the stream
+float absmax_pow2_scale(const float* A, int64_t n, unsigned* scratch, hipStream_t stream);
+// split-A back-projection on f16 pairs (two pieces of A s_A and of W s_f, three v_mfma_f32_16x16x32_f16 products,
+// fp32 accumulation, the output scaled by inv_scale per frame): W1 / W2 from launch_mf_split_w16
+void launch_mf_backproject_h16(const float* A, int64_t ld, int64_t nrows, const uint16_t* W1, const uint16_t* W2,
+                               int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0,
+                               int64_t v1, float a_scale, const float* inv_scale);
 // three: hi [nf][ldw] then mid [nf][ldw] in `hi` (2 nf ldw elements), lo: the split-A back-projection's planes
 void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, bf16_t* hi, bf16_t* lo,
                        hipStream_t stream, bool three = false);

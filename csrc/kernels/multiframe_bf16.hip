@@ -1382,6 +1382,140 @@ __global__ __launch_bounds__(256, 1) void k_mf_backproject_x3_m32(const float* _
             }
 }
 
+// ----------------------------------------------------------------------------------------------------------------
+// Split-A back-projection on f16 pairs (SART_MF_BWD16, default for fp32 shards at 32 / 64 frames). fp16 has 11
+// significant bits, so two rne pieces hold a scaled fp32 value to 2^-24 (|a s - a1 - a2| <= 2^-12 |a s - a1| <=
+// 2^-24 |a s|), i.e. at fp32 rounding, where bf16 (8 bits) needs three. Two pieces of A s_A and of W s_f make
+// three products (a2 w1, a1 w2, a1 w1: the dropped a2 w2 is 2^-24 of a term) instead of the six of the bf16 split,
+// and the split is 3 VALU operations per element (scale, convert, residual) instead of 5.5. The scales are powers
+// of two (s_A from max |A| once per shard, absmax_pow2_scale; s_f per frame and sweep, launch_mf_split_w16) that
+// keep every scaled value below 2^14 and values down to 2^-16 of the maximum normal in both pieces; the epilogue
+// multiplies by inv_scale[f] = 1 / (s_A s_f), exactly. Layout and staging as k_mf_backproject_b16_lds (VT = 1).
+typedef _Float16 halfx8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ floatx4 mfma_h16(const u32x4 a, const u32x4 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8_t, a), __builtin_bit_cast(halfx8_t, b),
+                                                  c, 0, 0, 0);
+}
+__device__ __forceinline__ void split_h2(unsigned x, unsigned y, float s, unsigned& p1, unsigned& p2) {
+    const float a = __uint_as_float(x) * s, b = __uint_as_float(y) * s;
+    const halfx2_t h = {(_Float16)a, (_Float16)b};
+    p1 = __builtin_bit_cast(unsigned, h);
+    const halfx2_t l = {(_Float16)(a - (float)h.x), (_Float16)(b - (float)h.y)};
+    p2 = __builtin_bit_cast(unsigned, l);
+}
+template <int P>
+__device__ __forceinline__ void split_phase_h(const u32x4 (&v)[8], float s, u32x4& h1, u32x4& h2) {
+    unsigned a[4], b[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) split_h2(v[2 * q][P], v[2 * q + 1][P], s, a[q], b[q]);
+    h1 = u32x4{a[0], a[1], a[2], a[3]};
+    h2 = u32x4{b[0], b[1], b[2], b[3]};
+}
+
+template <int NG, int DEPTH>
+__global__ __launch_bounds__(256, 2) void k_mf_backproject_h16(const float* __restrict__ A, int64_t ld, int64_t nrows32,
+                                                               const uint16_t* __restrict__ W1,
+                                                               const uint16_t* __restrict__ W2, int64_t ldw,
+                                                               int64_t rows_per_split, float* __restrict__ partial,
+                                                               int64_t vb0, int64_t vend, float a_scale,
+                                                               const float* __restrict__ inv_scale,
+                                                               const int* __restrict__ skip) {
+    if (skip && *skip) return;
+    constexpr int NF = 16 * NG;
+    constexpr int RS = DEPTH + 1;
+    constexpr int C = 2 * NG;                     // 1 KiB W pieces per step: (plane, frame group)
+    constexpr int XQ = C >= 4 ? (C + 3) / 4 : 1;  // pieces per wave
+    __shared__ __attribute__((aligned(16))) u32x4 s_w[2][C][64];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int64_t vb = vb0 + (int64_t)blockIdx.x * 4 + wave;
+    const bool live = vb * 64 < vend;
+    if (!live) vb = vend / 64 - 1;  // vend is a multiple of 64
+    const int g = lane >> 4, i16 = lane & 15;
+    const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
+    int64_t r_end = r_begin + rows_per_split;
+    if (r_end > nrows32) r_end = nrows32;
+    const float* __restrict__ ap = A + (r_begin + 8 * g) * ld + vb * 64 + 4 * i16;
+    const int64_t wo = (int64_t)i16 * ldw + r_begin + 8 * g;
+    floatx4 acc[4][NG];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int j = 0; j < NG; ++j) acc[p][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 32 : 0;  // uniform for the workgroup
+    if (nst > 0) {
+        u32x4 av[RS][8];
+        u32x4 wq[RS][XQ];
+        auto piece = [&](int i) { return C >= 4 ? (wave * XQ + i < C ? wave * XQ + i : C - 1) : wave % C; };
+        auto load = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            const float* at = ap + t * 32 * ld;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                av[sl][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(at + j * ld));
+#pragma unroll
+            for (int i = 0; i < XQ; ++i) {
+                const int pc = piece(i), j = pc % NG, plane = pc / NG;
+                wq[sl][i] = *reinterpret_cast<const u32x4*>((plane ? W2 : W1) + wo + (int64_t)j * 16 * ldw + t * 32);
+            }
+        };
+        auto stage = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+#pragma unroll
+            for (int i = 0; i < XQ; ++i) s_w[t & 1][piece(i)][lane] = wq[sl][i];
+        };
+        [&]<int... Q>(std::integer_sequence<int, Q...>) {
+            (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
+        }(std::make_integer_sequence<int, DEPTH>{});
+        stage(std::integral_constant<int, 0>{}, 0);
+        __syncthreads();
+        auto step = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
+            if (t >= nst) return;  // uniform for the workgroup
+            const u32x4* ws = s_w[t & 1][0] + lane;
+            u32x4 h1[4], h2[4];
+            split_phase_h<0>(av[sl], a_scale, h1[0], h2[0]);
+            split_phase_h<1>(av[sl], a_scale, h1[1], h2[1]);
+            split_phase_h<2>(av[sl], a_scale, h1[2], h2[2]);
+            split_phase_h<3>(av[sl], a_scale, h1[3], h2[3]);
+            u32x4 wv[2][NG];
+#pragma unroll
+            for (int j = 0; j < NG; ++j) wv[0][j] = ws[j * 64], wv[1][j] = ws[(NG + j) * 64];
+            auto prod = [&](const u32x4(&fa)[4], int pl) {
+#pragma unroll
+                for (int j = 0; j < NG; ++j)
+#pragma unroll
+                    for (int p = 0; p < 4; ++p) acc[p][j] = mfma_h16(fa[p], wv[pl][j], acc[p][j]);
+            };
+            prod(h2, 0);  // smallest first: a2 w1, a1 w2, a1 w1
+            prod(h1, 1);
+            prod(h1, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);
+            __syncthreads();
+        };
+        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+            }(std::make_integer_sequence<int, RS>{});
+        }
+    }
+    if (!live) return;
+    float* out = partial + (int64_t)blockIdx.y * ld * NF;
+    float isc[NG];
+#pragma unroll
+    for (int j = 0; j < NG; ++j) isc[j] = inv_scale[16 * j + i16];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t v = vb * 64 + 4 * (g * 4 + q) + p;
+#pragma unroll
+            for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[p][j][q] * isc[j];
+        }
+}
+
 static int mf_stagger() {
     const char* e = std::getenv("SART_MF_STAGGER");
     return (e && *e) ? std::atoi(e) : 0;
@@ -1797,6 +1931,41 @@ void launch_mf_backproject_b16(const bf16_t* A, int64_t ld, int64_t nrows, const
                                int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0,
                                int64_t v1) {
     launch_mf_backproject_split(A, ld, nrows, Wh, Wl, ldw, nsplit, partial, nf, stream, v0, v1);
+}
+
+void launch_mf_backproject_h16(const float* A, int64_t ld, int64_t nrows, const uint16_t* W1, const uint16_t* W2,
+                               int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0,
+                               int64_t v1, float a_scale, const float* inv_scale) {
+    const std::string what = "mf_backproject_h16";
+    if (ld % 64 != 0) throw std::runtime_error(what + ": ld must be a multiple of 64");
+    check_nf_b16(nf, what.c_str());
+    const int64_t nrows32 = (nrows + 31) / 32 * 32;
+    if (ldw < nrows32 || ldw % 8 != 0)
+        throw std::runtime_error(what + ": W planes must hold the rows rounded up to 32 (ldw % 8 == 0)");
+    if (v1 < 0) v1 = ld;
+    if (v0 < 0 || v1 > ld || v0 >= v1 || v0 % 64 != 0 || v1 % 64 != 0)
+        throw std::runtime_error(what + ": voxel range must be aligned to 64");
+    if (nsplit < 1) throw std::runtime_error(what + ": nsplit must be >= 1");
+    const int64_t rps = ((nrows32 + nsplit - 1) / nsplit + 31) / 32 * 32;
+    const int64_t vw0 = v0 / 64, nvw = (v1 - v0) / 64;
+    const dim3 grid((unsigned)((nvw + 3) / 4), (unsigned)nsplit);
+    const int d = mf_x3_depth(false);
+    auto go = [&](auto ng) {
+        constexpr int NG = decltype(ng)::value;
+        if (d == 3)
+            hipLaunchKernelGGL((k_mf_backproject_h16<NG, 3>), grid, dim3(256), 0, stream, A, ld, nrows32, W1, W2, ldw,
+                               rps, partial, vw0, v1, a_scale, inv_scale, g_mf_skip);
+        else
+            hipLaunchKernelGGL((k_mf_backproject_h16<NG, 2>), grid, dim3(256), 0, stream, A, ld, nrows32, W1, W2, ldw,
+                               rps, partial, vw0, v1, a_scale, inv_scale, g_mf_skip);
+    };
+    if (nf == 16)
+        go(std::integral_constant<int, 1>{});
+    else if (nf == 32)
+        go(std::integral_constant<int, 2>{});
+    else
+        go(std::integral_constant<int, 4>{});
+    check_launch("k_mf_backproject_h16");
 }
 
 void launch_mf_backproject_x3(const float* A, int64_t ld, int64_t nrows, const bf16_t* Wh, const bf16_t* Wl,

@@ -511,6 +511,122 @@ void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStr
     check_launch("k_mf_split_x");
 }
 
+// fp16-pair back-projection operands (launch_mf_backproject_h16). Per-frame max |w| over the rows (non-negative
+// floats order like their bit patterns: an unsigned atomic max), then w s_f = w1 + w2 + e with w1 = rne_f16(w s_f),
+// w2 = rne_f16(w s_f - w1), |e| <= 2^-24 |w s_f|, s_f = 2^(14 - e_f) for max |w| = m 2^e_f (m in [0.5, 1)): the
+// scaled frame stays below 2^14 (f16 max 65504) and its values down to 2^-16 of the frame's max keep both pieces
+// normal. inv_scale[f] = 1 / (a_scale s_f) (exact: powers of two) undoes both scalings in the back-projection.
+__global__ __launch_bounds__(256) void k_mf_wmax(const float* __restrict__ W, int64_t nrows_pad, int nf,
+                                                 unsigned* __restrict__ wmax, const int* __restrict__ skip) {
+    if (skip && *skip) return;
+    __shared__ unsigned m[kMaxNF];
+    for (int i = threadIdx.x; i < nf; i += 256) m[i] = 0u;
+    __syncthreads();
+    const int64_t r0 = (int64_t)blockIdx.x * 64;
+    for (int i = threadIdx.x; i < 64 * nf; i += 256) {
+        const int rr = i / nf, sl = i % nf;
+        if (r0 + rr < nrows_pad) {
+            const float w = fabsf(W[(r0 + rr) * nf + sl]);
+            if (w > 0.f && w <= 3.0e38f) atomicMax(&m[sl], __float_as_uint(w));  // (LDS) slot sl: finite values only
+        }
+    }
+    __syncthreads();
+    for (int sl = threadIdx.x; sl < nf; sl += 256) {
+        const int f = (sl % (nf >> 4)) * 16 + sl / (nf >> 4);  // inverse of mf_bp_slot
+        if (m[sl]) atomicMax(&wmax[f], m[sl]);
+    }
+}
+
+__device__ __forceinline__ int mf_w16_exp(unsigned mbits) {  // e with max |w| = m 2^e, m in [0.5, 1)
+    if (mbits == 0u) return 0;
+    int e;
+    (void)frexpf(__uint_as_float(mbits), &e);
+    return e;
+}
+
+__global__ __launch_bounds__(256) void k_mf_split_w16(const float* __restrict__ W, int64_t nrows_pad, int nf,
+                                                      int64_t ldw, uint16_t* __restrict__ w1, uint16_t* __restrict__ w2,
+                                                      const unsigned* __restrict__ wmax, float a_scale,
+                                                      float* __restrict__ inv_scale, const int* __restrict__ skip) {
+    if (skip && *skip) return;
+    __shared__ float tile[64][kMaxNF + 1];
+    __shared__ float sc[kMaxNF];
+    for (int f = threadIdx.x; f < nf; f += 256) {
+        const int e = mf_w16_exp(wmax[f]);
+        sc[f] = ldexpf(1.f, 14 - e);
+        if (blockIdx.x == 0) inv_scale[f] = ldexpf(1.f / a_scale, e - 14);
+    }
+    const int64_t r0 = (int64_t)blockIdx.x * 64;
+    for (int i = threadIdx.x; i < 64 * nf; i += 256) {
+        const int rr = i / nf, s = i % nf;
+        tile[rr][s] = (r0 + rr < nrows_pad) ? W[(r0 + rr) * nf + s] : 0.f;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * nf; i += 256) {
+        const int f = i / 64, rr = i % 64;
+        if (r0 + rr >= ldw) continue;
+        const float w = tile[rr][mf_bp_slot(f, nf)] * sc[f];
+        const _Float16 h1 = (_Float16)w;
+        const _Float16 h2 = (_Float16)(w - (float)h1);
+        w1[(int64_t)f * ldw + r0 + rr] = __builtin_bit_cast(uint16_t, h1);
+        w2[(int64_t)f * ldw + r0 + rr] = __builtin_bit_cast(uint16_t, h2);
+    }
+}
+
+// max |a| over n floats (unsigned atomic max of the bit patterns; non-finite values ignored)
+__global__ __launch_bounds__(256) void k_absmax_f32(const float* __restrict__ A, int64_t n, unsigned* __restrict__ out) {
+    __shared__ unsigned red[256];
+    unsigned m = 0u;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n / 4; i += (int64_t)gridDim.x * 256) {
+        const float4 v = reinterpret_cast<const float4*>(A)[i];
+        const float xs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float a = fabsf(xs[k]);
+            if (a <= 3.0e38f) m = max(m, __float_as_uint(a));
+        }
+    }
+    if (blockIdx.x == 0)
+        for (int64_t i = (n / 4) * 4 + threadIdx.x; i < n; i += 256) {
+            const float a = fabsf(A[i]);
+            if (a <= 3.0e38f) m = max(m, __float_as_uint(a));
+        }
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && red[0]) atomicMax(out, red[0]);
+}
+
+void launch_mf_split_w16(const float* W, int64_t nrows_pad, int nf, int64_t ldw, uint16_t* w1, uint16_t* w2,
+                         unsigned* wmax, float a_scale, float* inv_scale, hipStream_t stream) {
+    check_nf(nf, "mf_split_w16");
+    if (ldw > nrows_pad) throw std::runtime_error("mf_split_w16: plane stride exceeds the padded rows");
+    hip_call(hipMemsetAsync(wmax, 0, nf * sizeof(unsigned), stream), "hipMemsetAsync");
+    const unsigned nb64 = (unsigned)((nrows_pad + 63) / 64);
+    hipLaunchKernelGGL(k_mf_wmax, dim3(nb64), dim3(256), 0, stream, W, nrows_pad, nf, wmax, g_mf_skip);
+    check_launch("k_mf_wmax");
+    hipLaunchKernelGGL(k_mf_split_w16, dim3((unsigned)((ldw + 63) / 64)), dim3(256), 0, stream, W, nrows_pad, nf, ldw,
+                       w1, w2, wmax, a_scale, inv_scale, g_mf_skip);
+    check_launch("k_mf_split_w16");
+}
+
+float absmax_pow2_scale(const float* A, int64_t n, unsigned* scratch, hipStream_t stream) {
+    hip_call(hipMemsetAsync(scratch, 0, sizeof(unsigned), stream), "hipMemsetAsync");
+    const int64_t nb = std::min<int64_t>(4096, std::max<int64_t>(1, (n / 4 + 255) / 256));
+    hipLaunchKernelGGL(k_absmax_f32, dim3((unsigned)nb), dim3(256), 0, stream, A, n, scratch);
+    check_launch("k_absmax_f32");
+    unsigned bits = 0;
+    hip_call(hipMemcpyAsync(&bits, scratch, sizeof(unsigned), hipMemcpyDeviceToHost, stream), "D2H");
+    hip_call(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    if (bits == 0u) return 1.f;
+    int e;
+    (void)frexpf(__builtin_bit_cast(float, bits), &e);
+    return ldexpf(1.f, 14 - e);  // scaled max in [2^13, 2^14)
+}
+
 void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, bf16_t* hi, bf16_t* lo,
                        hipStream_t stream, bool three) {
     check_nf(nf, "mf_split_w");

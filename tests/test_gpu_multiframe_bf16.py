@@ -304,3 +304,42 @@ def test_forward_blocked_x_planes_bitwise(k, dev, P, V, nf, storage, fwd, monkey
         torch.cuda.synchronize()
         outs.append((Fo, Xh))
     assert torch.equal(outs[0][0], outs[1][0])
+
+
+# ------------------------------------------------------------------ split-A back-projection on f16 pairs
+@pytest.mark.parametrize("ascale,wscale", [(1.0, 1.0), (1e-7, 1.0), (3e4, 1e-6), (1.0, 1e5)])
+@pytest.mark.parametrize("nf", [16, 32, 64])
+@pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (2048, 4096), (1000, 1088)])
+def test_split_a_backprojection_f16_pairs(k, dev, P, V, nf, ascale, wscale):
+    """fp32 A and W each held as two f16 pieces of a power-of-two-scaled value (|x s - x1 - x2| <= 2^-24 |x s|),
+    three products, fp32 accumulation, the per-frame inverse scale applied in the epilogue: against fp64 products
+    of the fp32 operands at fp32 accuracy, also for matrices and weights far from 1 (the scales keep both pieces
+    normal), and frames of different magnitude (per-frame scales)."""
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+
+    rng = np.random.default_rng(P * 3 + V + nf)
+    A = (rng.random((P, V), dtype=np.float32) * np.float32(ascale)).astype(np.float32)
+    m = DenseRTM.from_dense(A, device=dev)
+    W = ((rng.random((P, nf)) - 0.5) * wscale * np.logspace(0, 3, nf)[None, :]).astype(np.float32)
+    Wd = torch.zeros((m.nrows_pad, nf), device=dev)
+    Wd[:P] = torch.from_numpy(np.ascontiguousarray(W.reshape(P, nf // 16, 16).transpose(0, 2, 1).reshape(P, nf)))
+    scratch = torch.zeros(nf, dtype=torch.int32, device=dev)
+    a_scale = k.absmax_pow2_scale(m.A.data_ptr(), m.nrows_pad * m.ld, scratch.data_ptr(), _stream(dev))
+    assert 2.0 ** 13 <= float(np.abs(A).max()) * a_scale < 2.0 ** 14
+    w16 = torch.zeros((2, nf, m.nrows_pad), dtype=torch.int16, device=dev)
+    inv = torch.zeros(nf, device=dev)
+    k.mf_split_w16(Wd.data_ptr(), m.nrows_pad, nf, m.nrows_pad, w16[0].data_ptr(), w16[1].data_ptr(),
+                   scratch.data_ptr(), a_scale, inv.data_ptr(), _stream(dev))
+    ns = 3
+    part = torch.zeros((ns, m.ld, nf), device=dev)
+    vmid = (m.ld // 2) // 64 * 64
+    for v0, v1 in ((0, vmid), (vmid, m.ld)):
+        k.mf_backproject_h16(m.A.data_ptr(), m.ld, P, w16[0].data_ptr(), w16[1].data_ptr(), m.nrows_pad, ns,
+                             part.data_ptr(), _stream(dev), nf, v0, v1, a_scale, inv.data_ptr())
+    torch.cuda.synchronize()
+    B_ref = A.astype(np.float64).T @ W.astype(np.float64)
+    B = part.sum(0)[:V].double().cpu().numpy()
+    # per frame (frames span three decades): the six-product bf16 split measures ~2e-7 (test_split_a_projections)
+    for f in range(nf):
+        rel = np.linalg.norm(B[:, f] - B_ref[:, f]) / np.linalg.norm(B_ref[:, f])
+        assert rel < 1e-6, (f, rel)

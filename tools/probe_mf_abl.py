@@ -52,8 +52,19 @@ def main():
         os.environ["SART_MF_X3_DEPTH"] = str(depth)
         nsv = k.mf_backproject_b16_num_splits(m.ld, P, True)  # m32 / vt 2: 128 voxels per wave, its own split count
         pv = torch.zeros((nsv, m.ld, nf), device=dev)
-        med, best = timeit(lambda: k.mf_backproject_x3(m.A.data_ptr(), m.ld, P, Wh.data_ptr(), Wl.data_ptr(),
-                                                       m.nrows_pad, nsv, pv.data_ptr(), s, nf), reps=7)
+        if bwd == "h16":  # f16 pairs, three products (launch_mf_backproject_h16)
+            scratch = torch.zeros(nf, dtype=torch.int32, device=dev)
+            a_sc = k.absmax_pow2_scale(m.A.data_ptr(), m.nrows_pad * m.ld, scratch.data_ptr(), s)
+            w16 = torch.zeros((2, nf, m.nrows_pad), dtype=torch.int16, device=dev)
+            inv = torch.zeros(nf, device=dev)
+            k.mf_split_w16(W.data_ptr(), m.nrows_pad, nf, m.nrows_pad, w16[0].data_ptr(), w16[1].data_ptr(),
+                           scratch.data_ptr(), a_sc, inv.data_ptr(), s)
+            med, best = timeit(lambda: k.mf_backproject_h16(m.A.data_ptr(), m.ld, P, w16[0].data_ptr(), w16[1].data_ptr(),
+                                                            m.nrows_pad, nsv, pv.data_ptr(), s, nf, 0, m.ld, a_sc,
+                                                            inv.data_ptr()), reps=7)
+        else:
+            med, best = timeit(lambda: k.mf_backproject_x3(m.A.data_ptr(), m.ld, P, Wh.data_ptr(), Wl.data_ptr(),
+                                                           m.nrows_pad, nsv, pv.data_ptr(), s, nf), reps=7)
         out = pv.double().sum(0)
         if ref is None:
             ref = out
