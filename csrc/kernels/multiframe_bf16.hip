@@ -1413,8 +1413,9 @@ __device__ __forceinline__ void split_phase_h(const u32x4 (&v)[8], float s, u32x
     h2 = u32x4{b[0], b[1], b[2], b[3]};
 }
 
-template <int NG, int DEPTH>
-__global__ __launch_bounds__(256, 2) void k_mf_backproject_h16(const float* __restrict__ A, int64_t ld, int64_t nrows32,
+// EW: W loaded a step ahead of A's batch (see k_mf_backproject_b16_lds); MW: waves per SIMD of the register budget
+template <int NG, int DEPTH, bool EW = false, int MW = 2>
+__global__ __launch_bounds__(256, MW) void k_mf_backproject_h16(const float* __restrict__ A, int64_t ld, int64_t nrows32,
                                                                const uint16_t* __restrict__ W1,
                                                                const uint16_t* __restrict__ W2, int64_t ldw,
                                                                int64_t rows_per_split, float* __restrict__ partial,
@@ -1447,23 +1448,32 @@ __global__ __launch_bounds__(256, 2) void k_mf_backproject_h16(const float* __re
         u32x4 av[RS][8];
         u32x4 wq[RS][XQ];
         auto piece = [&](int i) { return C >= 4 ? (wave * XQ + i < C ? wave * XQ + i : C - 1) : wave % C; };
-        auto load = [&](auto slc, int64_t t) {
+        auto load_w = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
-            const float* at = ap + t * 32 * ld;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                av[sl][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(at + j * ld));
 #pragma unroll
             for (int i = 0; i < XQ; ++i) {
                 const int pc = piece(i), j = pc % NG, plane = pc / NG;
                 wq[sl][i] = *reinterpret_cast<const u32x4*>((plane ? W2 : W1) + wo + (int64_t)j * 16 * ldw + t * 32);
             }
         };
+        auto load = [&](auto slc, int64_t t) {
+            constexpr int sl = decltype(slc)::value;
+            const float* at = ap + t * 32 * ld;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                av[sl][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(at + j * ld));
+            if constexpr (!EW) load_w(slc, t);
+        };
         auto stage = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
 #pragma unroll
             for (int i = 0; i < XQ; ++i) s_w[t & 1][piece(i)][lane] = wq[sl][i];
         };
+        if constexpr (EW) {
+            [&]<int... Q>(std::integer_sequence<int, Q...>) {
+                (load_w(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
+            }(std::make_integer_sequence<int, RS>{});
+        }
         [&]<int... Q>(std::integer_sequence<int, Q...>) {
             (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
         }(std::make_integer_sequence<int, DEPTH>{});
@@ -1471,6 +1481,7 @@ __global__ __launch_bounds__(256, 2) void k_mf_backproject_h16(const float* __re
         __syncthreads();
         auto step = [&](auto slc, int64_t t) {
             constexpr int sl = decltype(slc)::value;
+            if constexpr (EW) load_w(slc, t + DEPTH + 1 < nst ? t + DEPTH + 1 : nst - 1);
             load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
             if (t >= nst) return;  // uniform for the workgroup
             const u32x4* ws = s_w[t & 1][0] + lane;
@@ -1950,14 +1961,22 @@ void launch_mf_backproject_h16(const float* A, int64_t ld, int64_t nrows, const 
     const int64_t vw0 = v0 / 64, nvw = (v1 - v0) / 64;
     const dim3 grid((unsigned)((nvw + 3) / 4), (unsigned)nsplit);
     const int d = mf_x3_depth(false);
+    // SART_MF_H16 (A/B runs): "ew" early W loads, "w1" one wave per SIMD (512 registers), "ew,w1"
+    const char* hv = std::getenv("SART_MF_H16");
+    const bool ew = hv && std::strstr(hv, "ew"), w1 = hv && std::strstr(hv, "w1");
     auto go = [&](auto ng) {
         constexpr int NG = decltype(ng)::value;
-        if (d == 3)
-            hipLaunchKernelGGL((k_mf_backproject_h16<NG, 3>), grid, dim3(256), 0, stream, A, ld, nrows32, W1, W2, ldw,
-                               rps, partial, vw0, v1, a_scale, inv_scale, g_mf_skip);
-        else
-            hipLaunchKernelGGL((k_mf_backproject_h16<NG, 2>), grid, dim3(256), 0, stream, A, ld, nrows32, W1, W2, ldw,
-                               rps, partial, vw0, v1, a_scale, inv_scale, g_mf_skip);
+        auto run = [&](auto k) {
+            hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, A, ld, nrows32, W1, W2, ldw, rps, partial, vw0, v1,
+                               a_scale, inv_scale, g_mf_skip);
+        };
+        if (w1 && ew && d == 3) run(k_mf_backproject_h16<NG, 3, true, 1>);
+        else if (w1 && d == 3) run(k_mf_backproject_h16<NG, 3, false, 1>);
+        else if (w1 && ew) run(k_mf_backproject_h16<NG, 2, true, 1>);
+        else if (w1) run(k_mf_backproject_h16<NG, 2, false, 1>);
+        else if (ew) run(k_mf_backproject_h16<NG, 2, true, 2>);
+        else if (d == 3) run(k_mf_backproject_h16<NG, 3>);
+        else run(k_mf_backproject_h16<NG, 2>);
     };
     if (nf == 16)
         go(std::integral_constant<int, 1>{});

@@ -52,7 +52,8 @@ def main():
         os.environ["SART_MF_X3_DEPTH"] = str(depth)
         nsv = k.mf_backproject_b16_num_splits(m.ld, P, True)  # m32 / vt 2: 128 voxels per wave, its own split count
         pv = torch.zeros((nsv, m.ld, nf), device=dev)
-        if bwd == "h16":  # f16 pairs, three products (launch_mf_backproject_h16)
+        if bwd.startswith("h16"):  # f16 pairs, three products (launch_mf_backproject_h16); "h16+ew,w1": SART_MF_H16
+            os.environ["SART_MF_H16"] = bwd[4:]
             scratch = torch.zeros(nf, dtype=torch.int32, device=dev)
             a_sc = k.absmax_pow2_scale(m.A.data_ptr(), m.nrows_pad * m.ld, scratch.data_ptr(), s)
             w16 = torch.zeros((2, nf, m.nrows_pad), dtype=torch.int16, device=dev)
