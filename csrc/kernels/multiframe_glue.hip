@@ -102,9 +102,16 @@ __global__ __launch_bounds__(256) void k_mf_collect(const float* __restrict__ pa
     if (F2part && blockIdx.x == 0) {  // block-uniform branch: all 256 threads, 256 / nf per frame
         __shared__ double f2[256];
         const int f = threadIdx.x % nf, q = threadIdx.x / nf, nq = 256 / nf;
-        double s = 0.0;
-        for (int b = q; b < nF2; b += nq) s += F2part[(int64_t)b * nf + f];
-        f2[threadIdx.x] = s;
+        // eight independent partial sums per thread (fixed assignment and combination order: deterministic): one
+        // dependent chain of nF2 / nq loads made this block the kernel's tail (78 us per 64-frame sweep at 64k rows,
+        // profiles/rocprof_r4_mfx64_kernel_stats.csv)
+        double sp[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        int b = q;
+        for (; b + 7 * nq < nF2; b += 8 * nq)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sp[k] += F2part[(int64_t)(b + k * nq) * nf + f];
+        for (; b < nF2; b += nq) sp[0] += F2part[(int64_t)b * nf + f];
+        f2[threadIdx.x] = ((sp[0] + sp[1]) + (sp[2] + sp[3])) + ((sp[4] + sp[5]) + (sp[6] + sp[7]));
         __syncthreads();
         if (threadIdx.x < nf) {  // fixed order over the 256 / nf partial sums: deterministic
             double t = 0.0;
