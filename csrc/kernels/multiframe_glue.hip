@@ -526,21 +526,23 @@ void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStr
 __global__ __launch_bounds__(256) void k_mf_wmax(const float* __restrict__ W, int64_t nrows_pad, int nf,
                                                  unsigned* __restrict__ wmax, const int* __restrict__ skip) {
     if (skip && *skip) return;
-    __shared__ unsigned m[kMaxNF];
-    for (int i = threadIdx.x; i < nf; i += 256) m[i] = 0u;
-    __syncthreads();
+    // thread (slot sl, row class q): a register max over the block's rows of its class (coalesced: consecutive threads
+    // read consecutive slots), then the nq classes of a slot combined through LDS; one global atomic per slot
+    __shared__ unsigned red[256];
+    const int sl = threadIdx.x % nf, q = threadIdx.x / nf, nq = 256 / nf;
     const int64_t r0 = (int64_t)blockIdx.x * 64;
-    for (int i = threadIdx.x; i < 64 * nf; i += 256) {
-        const int rr = i / nf, sl = i % nf;
+    unsigned m = 0u;
+    for (int rr = q; rr < 64; rr += nq)
         if (r0 + rr < nrows_pad) {
             const float w = fabsf(W[(r0 + rr) * nf + sl]);
-            if (w > 0.f && w <= 3.0e38f) atomicMax(&m[sl], __float_as_uint(w));  // (LDS) slot sl: finite values only
+            if (w <= 3.0e38f) m = max(m, __float_as_uint(w));  // finite values only
         }
-    }
+    red[threadIdx.x] = m;
     __syncthreads();
-    for (int sl = threadIdx.x; sl < nf; sl += 256) {
+    if (q == 0) {
+        for (int k = 1; k < nq; ++k) m = max(m, red[k * nf + sl]);
         const int f = (sl % (nf >> 4)) * 16 + sl / (nf >> 4);  // inverse of mf_bp_slot
-        if (m[sl]) atomicMax(&wmax[f], m[sl]);
+        if (m) atomicMax(&wmax[f], m);
     }
 }
 
