@@ -64,12 +64,6 @@ __device__ __forceinline__ floatx4 mfma_b16(const uint4 a, const u32x4 b, floatx
                                                    c, 0, 0, 0);
 }
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-__device__ __forceinline__ f32x16 mfma32_b16(const u32x4 a, const u32x4 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
-}
-
 typedef unsigned u32x8 __attribute__((ext_vector_type(8)));  // eight fp32 of A (a split-A forward fragment)
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
@@ -630,21 +624,13 @@ constexpr int mf_bwd_min_waves() {
 // slot u % RS, whose previous W was staged the step before). The wait that staging step t + 1's W needs then covers
 // only loads issued at step t - DEPTH or earlier; loaded in one batch with A of step t + 1 (EW false), that wait also
 // held every wave until A of step t + 1 had arrived, i.e. one step ahead instead of DEPTH (in-order vmcnt).
-// MW > 0: waves per SIMD the register budget is cut for, instead of the default (A/B builds: SART_MF_X3_BWD=w1 / w1d3
-// runs the split-A VT = 1 kernel with one wave per SIMD, 512 registers, ring depth 2 / 3).
-template <int NG, int DEPTH, int VT, typename AT = bf16_t, int ABL = 0, bool EW = false, int MW = 0>
-__global__ __launch_bounds__(256, (MW > 0 ? MW : (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::is_same<AT, float>::value && VT == 1 ? 2 : 1)))) void k_mf_backproject_b16_lds(const AT* __restrict__ A, int64_t ld,
+template <int NG, int DEPTH, int VT, typename AT = bf16_t, int ABL = 0, bool EW = false>
+__global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::is_same<AT, float>::value && VT == 1 ? 2 : 1))) void k_mf_backproject_b16_lds(const AT* __restrict__ A, int64_t ld,
                                                                 int64_t nrows32, const bf16_t* __restrict__ Wh,
                                                                 const bf16_t* __restrict__ Wl, int64_t ldw,
                                                                 int64_t rows_per_split, float* __restrict__ partial,
-                                                                int64_t vb0, int64_t vend, const int* __restrict__ skip,
-                                                                int stagger) {
+                                                                int64_t vb0, int64_t vend, const int* __restrict__ skip) {
     if (skip && *skip) return;
-    // stagger (A/B runs, SART_MF_STAGGER=n): workgroups of odd 256-block rounds (the second workgroup a CU receives)
-    // start n x 1024 cycles late, so the two workgroups sharing a CU's SIMDs are not in lockstep (MI355X_MICROARCH.md,
-    // 'try a stagger')
-    if (stagger > 0 && (((blockIdx.x + blockIdx.y * gridDim.x) >> 8) & 1))
-        for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(16);
     constexpr int NF = 16 * NG;
     constexpr int RS = DEPTH + 1;
     constexpr bool A32 = std::is_same<AT, float>::value;
@@ -839,548 +825,7 @@ __global__ __launch_bounds__(256, (MW > 0 ? MW : (NG == 4 ? mf_bwd_min_waves<AT,
             }
 }
 
-// Split-A back-projection with the W fragments loaded straight into registers (no LDS, no barrier): every wave
-// runs its own pipeline. A lane's W fragment of frame group j and plane pl -- eight rows 8 g .. 8 g + 7 of frame
-// 16 j + i16 -- is one 16-byte load of the frame-major W plane, i.e. exactly the B operand of v_mfma_f32_16x16x32_bf16,
-// so the DEPTH-step register ring carries A and W alike. W bytes per step are 1.5x the A bytes of a wave (three
-// planes x NG groups x 1 KiB against 8 KiB of A), served by L2: the four waves of a workgroup read the same W
-// lines (FETCH_SIZE of the LDS kernels: W are L2 hits). MINW: waves per SIMD the register budget is cut for.
-// Same summation order per accumulator as k_mf_backproject_b16_lds<NG, DEPTH, 1, float>: bitwise equal output.
-// PIPE: the split of step t + 1 runs beside the MFMAs of step t (one wave per SIMD: nothing else overlaps the split's
-// VALU work with the matrix pipe); its A arrived DEPTH - 1 steps earlier, so PIPE wants DEPTH >= 3.
-// WD (PIPE): W is loaded WD steps ahead in its own ring of WD + 1 slots (L2 hits: a shallower ring than A's).
-template <int NG, int DEPTH, int MINW, bool PIPE = false, int WD = DEPTH>
-__global__ __launch_bounds__(256, MINW) void k_mf_backproject_x3_reg(const float* __restrict__ A, int64_t ld,
-                                                                      int64_t nrows32, const bf16_t* __restrict__ Wh,
-                                                                      const bf16_t* __restrict__ Wl, int64_t ldw,
-                                                                      int64_t rows_per_split, float* __restrict__ partial,
-                                                                      int64_t vb0, int64_t vend,
-                                                                      const int* __restrict__ skip) {
-    if (skip && *skip) return;
-    constexpr int NF = 16 * NG;
-    constexpr int RS = DEPTH + 1;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t vb = vb0 + (int64_t)blockIdx.x * 4 + wave;  // 64-voxel block of this wave
-    if (vb * 64 >= vend) return;                               // no barrier in this kernel: idle waves leave
-    const int g = lane >> 4, i16 = lane & 15;
-    const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
-    int64_t r_end = r_begin + rows_per_split;
-    if (r_end > nrows32) r_end = nrows32;
-    const float* __restrict__ ap = A + (r_begin + 8 * g) * ld + vb * 64 + 4 * i16;
-    const bf16_t* __restrict__ wp[3] = {Wh + (int64_t)i16 * ldw + r_begin + 8 * g,
-                                        Wh + (int64_t)NF * ldw + (int64_t)i16 * ldw + r_begin + 8 * g,
-                                        Wl + (int64_t)i16 * ldw + r_begin + 8 * g};  // hi, mid, lo planes
-
-    floatx4 acc[4][NG];
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int j = 0; j < NG; ++j) acc[p][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-    const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 32 : 0;
-    if (nst > 0) {
-        constexpr int WS = PIPE ? WD + 1 : RS;  // W ring slots
-        u32x4 av[RS][8];
-        u32x4 wv[WS][3][NG];
-        auto load_a = [&](int sl, int64_t t) {
-            const float* at = ap + t * 32 * ld;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                av[sl][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(at + j * ld));
-        };
-        auto load_w = [&](int sl, int64_t t) {
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-                for (int j = 0; j < NG; ++j)
-                    wv[sl][pl][j] = *reinterpret_cast<const u32x4*>(wp[pl] + (int64_t)j * 16 * ldw + t * 32);
-        };
-        auto load = [&](auto slc, int64_t t) {
-            constexpr int sl = decltype(slc)::value;
-            load_a(sl, t);
-            load_w(sl, t);
-        };
-        if constexpr (PIPE) {
-#pragma unroll
-            for (int d = 0; d < DEPTH; ++d) load_a(d, d < nst ? d : nst - 1);
-#pragma unroll
-            for (int d = 0; d < WD; ++d) load_w(d, d < nst ? d : nst - 1);
-        } else {
-            [&]<int... Q>(std::integer_sequence<int, Q...>) {
-                (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
-            }(std::make_integer_sequence<int, DEPTH>{});
-        }
-        auto split_all = [&](const u32x4(&v)[8], u32x4(&fh)[4], u32x4(&fm)[4], u32x4(&fl)[4]) {
-            split_phase3<0>(v, fh[0], fm[0], fl[0]);
-            split_phase3<1>(v, fh[1], fm[1], fl[1]);
-            split_phase3<2>(v, fh[2], fm[2], fl[2]);
-            split_phase3<3>(v, fh[3], fm[3], fl[3]);
-        };
-        auto mfmas = [&](const u32x4(&fh)[4], const u32x4(&fm)[4], const u32x4(&fl)[4], const u32x4(&w)[3][NG]) {
-            auto prod = [&](const u32x4(&fa)[4], int pl) {
-#pragma unroll
-                for (int j = 0; j < NG; ++j)
-#pragma unroll
-                    for (int p = 0; p < 4; ++p) acc[p][j] = mfma_b16(fa[p], w[pl][j], acc[p][j]);
-            };
-            prod(fh, 2);
-            prod(fm, 1);
-            prod(fl, 0);
-            prod(fh, 1);
-            prod(fm, 0);
-            prod(fh, 0);
-        };
-        if constexpr (!PIPE) {
-            auto step = [&](auto slc, int64_t t) {
-                constexpr int sl = decltype(slc)::value;
-                load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
-                if (t >= nst) return;
-                u32x4 fh[4], fm[4], fl[4];
-                split_all(av[sl], fh, fm, fl);
-                mfmas(fh, fm, fl, wv[sl]);
-            };
-            for (int64_t t0 = 0; t0 < nst; t0 += RS) {
-                [&]<int... Q>(std::integer_sequence<int, Q...>) {
-                    (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
-                }(std::make_integer_sequence<int, RS>{});
-            }
-        } else {
-            u32x4 F[2][3][4];  // split of the current and of the next step
-            split_all(av[0], F[0][0], F[0][1], F[0][2]);
-            auto step = [&](auto qc, int64_t t) {
-                constexpr int q = decltype(qc)::value;
-                constexpr int sl = q % RS, ws = q % WS, fb = q % 2;
-                load_a((sl + DEPTH) % RS, t + DEPTH < nst ? t + DEPTH : nst - 1);
-                load_w((ws + WD) % WS, t + WD < nst ? t + WD : nst - 1);
-                if (t >= nst) return;
-                split_all(av[(sl + 1) % RS], F[fb ^ 1][0], F[fb ^ 1][1], F[fb ^ 1][2]);  // (clamped: always valid)
-                mfmas(F[fb][0], F[fb][1], F[fb][2], wv[ws]);
-                // interleave: one MFMA, then two VALU of the next step's split (176 VALU over 24 NG MFMAs)
-#pragma unroll
-                for (int i = 0; i < 24 * NG; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-                }
-            };
-            constexpr auto gcd = [](int a, int b) { while (b) { const int c = a % b; a = b; b = c; } return a; };
-            constexpr int L2 = RS * WS / gcd(RS, WS);
-            constexpr int PASS = L2 % 2 == 0 ? L2 : 2 * L2;  // lcm(RS, WS, 2): static ring slots and split buffers
-            static_assert(PASS % RS == 0 && PASS % WS == 0 && PASS % 2 == 0, "static ring slots per pass");
-            for (int64_t t0 = 0; t0 < nst; t0 += PASS) {
-                [&]<int... Q>(std::integer_sequence<int, Q...>) {
-                    (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
-                }(std::make_integer_sequence<int, PASS>{});
-            }
-        }
-    }
-    float* out = partial + (int64_t)blockIdx.y * ld * NF;
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t v = vb * 64 + 4 * (g * 4 + q) + p;
-#pragma unroll
-            for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[p][j][q];
-        }
-}
-
-// Split-A forward with the X fragments loaded straight into registers (no LDS, no barrier), the counterpart of
-// k_mf_backproject_x3_reg: a lane's X fragment of frame group j and plane -- eight voxels (in the permuted k order of
-// k_mf_split_x with perm) of frame 16 j + r -- is one 16-byte load, the B operand as it is. A is loaded as fragments
-// (lane (r, g): the two 16-byte halves of row r's voxels 4 g .. and 16 + 4 g ..). Same products in the same order as
-// k_mf_forward_b16_lds<NG, DEPTH, RT, KB, float>: bitwise equal output.
-// AS: A loaded in full 128-byte row segments (8 rows per instruction, the back-projection's load shape) and regrouped
-// into fragments through a wave-private LDS image (swizzled slots, as in k_mf_forward_b16_lds): still no barrier.
-template <int NG, int DEPTH, int RT, int KB, int MINW, bool AS = false>
-__global__ __launch_bounds__(256, MINW) void k_mf_forward_x3_reg(const float* __restrict__ A, int64_t ld, int64_t nrows,
-                                                                  int64_t nrows_pad, const bf16_t* __restrict__ Xh,
-                                                                  const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
-                                                                  FwdCols fc, const int* __restrict__ skip) {
-    const int64_t cols_per_split = fc.cps, xfs = fc.xfs, xbs = fc.xbs;
-    if (skip && *skip) return;
-    constexpr int NF = 16 * NG;
-    constexpr int RS = DEPTH + 1;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t row0 = ((int64_t)blockIdx.x * 4 + wave) * (16 * RT);
-    if (row0 >= nrows_pad) return;  // no barrier in this kernel
-    const int g = lane >> 4, r = lane & 15;
-    const int64_t c0 = (int64_t)blockIdx.y * cols_per_split;
-    const int64_t c1 = (c0 + cols_per_split < ld) ? c0 + cols_per_split : ld;
-    Fout += (int64_t)blockIdx.y * nrows_pad * NF;
-    const float* __restrict__ ap = A + (row0 + r) * ld + c0 + 4 * g;
-    const int64_t xo = (int64_t)r * xfs + (c0 >> 5) * xbs + 8 * g;
-    constexpr int R16 = 32 * KB * 4 / 16;  // 16-B slots per row and step (AS)
-    constexpr int RPI = 64 / R16;          // rows per staging load instruction
-    constexpr int NI = 16 * RT / RPI;      // staging loads per step and wave
-    static_assert(!AS || R16 >= 8, "A staging needs full 128-B row segments");
-    __shared__ __attribute__((aligned(16))) u32x4 s_a[AS ? 4 : 1][AS ? 16 * RT * R16 : 1];
-    u32x4* img = s_a[AS ? wave : 0];
-    const float* __restrict__ asp = A + (row0 + lane / R16) * ld + c0 + (lane % R16) * 4;
-
-    floatx4 acc[RT][NG];
-#pragma unroll
-    for (int t = 0; t < RT; ++t)
-#pragma unroll
-        for (int j = 0; j < NG; ++j) acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-    const int64_t nst = c1 > c0 ? (c1 - c0) / (32 * KB) : 0;
-    if (nst > 0) {
-        u32x8 a[AS ? 1 : RS][RT][KB];
-        u32x4 as_[AS ? RS : 1][NI];
-        u32x4 xh[RS][KB][NG], xl[RS][KB][NG];
-        auto load = [&](auto slc, int64_t t) {
-            constexpr int sl = decltype(slc)::value;
-            const int64_t q = t * 32 * KB;
-            if constexpr (AS) {
-#pragma unroll
-                for (int i = 0; i < NI; ++i)
-                    as_[sl][i] = *reinterpret_cast<const u32x4*>(asp + (int64_t)i * RPI * ld + q);
-            } else {
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-                for (int kb = 0; kb < KB; ++kb) {
-                    const float* p = ap + rt * 16 * ld + q + 32 * kb;
-                    const u32x4 h0 = *reinterpret_cast<const u32x4*>(p);
-                    const u32x4 h1 = *reinterpret_cast<const u32x4*>(p + 16);
-                    a[sl][rt][kb] = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-                }
-            }
-#pragma unroll
-            for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-                for (int j = 0; j < NG; ++j) {
-                    xh[sl][kb][j] = *reinterpret_cast<const u32x4*>(Xh + xo + (int64_t)j * 16 * xfs + (t * KB + kb) * xbs);
-                    xl[sl][kb][j] = *reinterpret_cast<const u32x4*>(Xl + xo + (int64_t)j * 16 * xfs + (t * KB + kb) * xbs);
-                }
-        };
-        [&]<int... Q>(std::integer_sequence<int, Q...>) {
-            (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
-        }(std::make_integer_sequence<int, DEPTH>{});
-        auto step = [&](auto slc, int64_t t) {
-            constexpr int sl = decltype(slc)::value;
-            load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
-            if (t >= nst) return;
-            if constexpr (AS) {  // this wave's tile into its own LDS image (in-order LDS queue: no barrier)
-#pragma unroll
-                for (int i = 0; i < NI; ++i) {
-                    const int row = i * RPI + lane / R16;
-                    img[row * R16 + ((lane % R16) ^ (row & 7))] = as_[sl][i];
-                }
-            }
-            auto frag16 = [&](int rt, int seg) { return img[(rt * 16 + r) * R16 + (seg ^ (r & 7))]; };
-#pragma unroll
-            for (int kb = 0; kb < KB; ++kb) {
-                u32x4 ah[RT], al[RT];
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt) {
-                    if constexpr (AS)
-                        split_a8(__builtin_shufflevector(frag16(rt, kb * 8 + g), frag16(rt, kb * 8 + 4 + g), 0, 1, 2, 3,
-                                                         4, 5, 6, 7),
-                                 ah[rt], al[rt]);
-                    else
-                        split_a8(a[sl][rt][kb], ah[rt], al[rt]);
-                }
-#pragma unroll
-                for (int j = 0; j < NG; ++j)
-#pragma unroll
-                    for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(al[rt], xh[sl][kb][j], acc[rt][j]);
-#pragma unroll
-                for (int j = 0; j < NG; ++j)
-#pragma unroll
-                    for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(ah[rt], xl[sl][kb][j], acc[rt][j]);
-#pragma unroll
-                for (int j = 0; j < NG; ++j)
-#pragma unroll
-                    for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(ah[rt], xh[sl][kb][j], acc[rt][j]);
-            }
-        };
-        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
-            [&]<int... Q>(std::integer_sequence<int, Q...>) {
-                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
-            }(std::make_integer_sequence<int, RS>{});
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < NG; ++j)
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int64_t ra = row0 + rt * 16 + g * 4 + i;
-                if (ra < nrows) Fout[ra * NF + 16 * j + r] = acc[rt][j][i];
-            }
-}
-
-// Split-A back-projection, software-pipelined: the split of step t + 1's A (VALU) is issued between the MFMAs of step t,
-// at one wave per SIMD. The LDS kernel (k_mf_backproject_b16_lds, two waves per SIMD) runs the split and the MFMAs of a
-// step back to back, and ablations show they barely overlap: 64 frames, 64k x 64k, 3.32 ms per call, 2.30 ms without
-// the split, 1.72 ms without the MFMAs (profiles/ablation_r4_mf64_split_a.jsonl). W is staged through two LDS stages
-// as there (one barrier per step: the four waves share W). Same products in the same order per accumulator: bitwise
-// the LDS kernel's output.
-template <int NG, int DEPTH>
-__global__ __launch_bounds__(256, 1) void k_mf_backproject_x3_pipe(const float* __restrict__ A, int64_t ld,
-                                                                    int64_t nrows32, const bf16_t* __restrict__ Wh,
-                                                                    const bf16_t* __restrict__ Wl, int64_t ldw,
-                                                                    int64_t rows_per_split, float* __restrict__ partial,
-                                                                    int64_t vb0, int64_t vend,
-                                                                    const int* __restrict__ skip) {
-    if (skip && *skip) return;
-    constexpr int NF = 16 * NG;
-    constexpr int RS = DEPTH + 1;
-    constexpr int C = 3 * NG;            // 1 KiB W pieces per step (hi, mid, lo planes x NG groups)
-    constexpr int XQ = (C + 3) / 4;      // pieces per wave (clamped: a duplicate load writes equal data)
-    __shared__ __attribute__((aligned(16))) u32x4 s_w[2][C][64];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int64_t vb = vb0 + (int64_t)blockIdx.x * 4 + wave;
-    const bool live = vb * 64 < vend;
-    if (!live) vb = vend / 64 - 1;  // stages W and takes the barriers, stores nothing
-    const int g = lane >> 4, i16 = lane & 15;
-    const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
-    int64_t r_end = r_begin + rows_per_split;
-    if (r_end > nrows32) r_end = nrows32;
-    const float* __restrict__ ap = A + (r_begin + 8 * g) * ld + vb * 64 + 4 * i16;
-    const int64_t wo = (int64_t)i16 * ldw + r_begin + 8 * g;
-    auto plane_ptr = [&](int pl) { return pl == 2 ? Wl : Wh + (int64_t)pl * NF * ldw; };
-
-    floatx4 acc[4][NG];
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int j = 0; j < NG; ++j) acc[p][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-    const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 32 : 0;  // uniform for the workgroup
-    if (nst > 0) {
-        u32x4 av[RS][8];
-        u32x4 wq[RS][XQ];
-        auto piece = [&](int i) { return wave * XQ + i < C ? wave * XQ + i : C - 1; };  // piece = plane * NG + j
-        auto load = [&](int sl, int64_t t) {
-            const float* at = ap + t * 32 * ld;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                av[sl][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(at + j * ld));
-#pragma unroll
-            for (int i = 0; i < XQ; ++i) {
-                const int pc = piece(i), j = pc % NG, plane = pc / NG;
-                wq[sl][i] = *reinterpret_cast<const u32x4*>(plane_ptr(plane) + wo + (int64_t)j * 16 * ldw + t * 32);
-            }
-        };
-        auto stage = [&](int sl, int64_t t) {
-#pragma unroll
-            for (int i = 0; i < XQ; ++i) s_w[t & 1][piece(i)][lane] = wq[sl][i];
-        };
-        auto split_all = [&](const u32x4(&v)[8], u32x4(&F)[3][4]) {
-            split_phase3<0>(v, F[0][0], F[1][0], F[2][0]);
-            split_phase3<1>(v, F[0][1], F[1][1], F[2][1]);
-            split_phase3<2>(v, F[0][2], F[1][2], F[2][2]);
-            split_phase3<3>(v, F[0][3], F[1][3], F[2][3]);
-        };
-#pragma unroll
-        for (int d = 0; d < DEPTH; ++d) load(d, d < nst ? d : nst - 1);
-        stage(0, 0);
-        __syncthreads();
-        u32x4 F[2][3][4];  // [buffer][hi, mid, lo][phase]: the split of this step and of the next
-        split_all(av[0], F[0]);
-        auto step = [&](auto qc, int64_t t) {
-            constexpr int q = decltype(qc)::value;
-            constexpr int sl = q % RS, fb = q % 2;
-            load((sl + DEPTH) % RS, t + DEPTH < nst ? t + DEPTH : nst - 1);
-            if (t >= nst) return;  // uniform for the workgroup
-            const u32x4* ws = s_w[t & 1][0] + lane;
-            u32x4 wv[3][NG];
-#pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-                for (int j = 0; j < NG; ++j) wv[pl][j] = ws[(pl * NG + j) * 64];
-            split_all(av[(sl + 1) % RS], F[fb ^ 1]);  // the next step's A (clamped loads: always valid data)
-            auto prod = [&](int pa, int pl) {
-#pragma unroll
-                for (int j = 0; j < NG; ++j)
-#pragma unroll
-                    for (int p = 0; p < 4; ++p) acc[p][j] = mfma_b16(F[fb][pa][p], wv[pl][j], acc[p][j]);
-            };
-            prod(0, 2);  // (hi, lo), (mid, mid), (lo, hi), (hi, mid), (mid, hi), (hi, hi): smallest first
-            prod(1, 1);
-            prod(2, 0);
-            prod(0, 1);
-            prod(1, 0);
-            prod(0, 0);
-            // the step's W fragment reads first, then one MFMA / two VALU of the next step's split in turn
-            __builtin_amdgcn_sched_group_barrier(0x100, 3 * NG, 0);
-#pragma unroll
-            for (int i = 0; i < 24 * NG; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            stage((sl + 1) % RS, t + 1);  // W of step t + 1 into the other stage (its readers passed the last barrier)
-            __syncthreads();
-        };
-        constexpr int PASS = RS % 2 == 0 ? RS : 2 * RS;  // static ring slots and split buffers per pass
-        for (int64_t t0 = 0; t0 < nst; t0 += PASS) {
-            [&]<int... Q>(std::integer_sequence<int, Q...>) {
-                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
-            }(std::make_integer_sequence<int, PASS>{});
-        }
-    }
-    if (!live) return;
-    float* out = partial + (int64_t)blockIdx.y * ld * NF;
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-            const int64_t v = vb * 64 + 4 * (g * 4 + qq) + p;
-#pragma unroll
-            for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[p][j][qq];
-        }
-}
-
 // ---------------------------------------------------------------------------------------------- launchers
-
-// Split-A back-projection on v_mfma_f32_32x32x16_bf16 (SART_MF_X3_BWD=m32 / m32d3; 32 / 64 frames). A 16x16x32 MFMA
-// holds the SIMD's vector issue for 8 of its 16 cycles, a 32x32x16 MFMA (the same cycles per flop) for 8 of 32
-// (MI355X_MICROARCH.md, vector-instruction issue cost): the split of A (176 VALU operations per step and wave) then
-// fits in the MFMAs' shadow instead of being added to them (16x16x32 ablations: MFMAs alone 2.30 ms, split alone
-// 1.72, both 3.32 per 64k x 64k call, profiles/ablation_r4_mf64_split_a.jsonl). A wave owns 128 voxels: lane
-// (r = l & 31, h = l >> 5) loads 16 bytes (voxels 4 r .. 4 r + 3) of rows 8 h .. 8 h + 7 of each 16-row step, i.e.
-// the A operand A^T[voxel 4 r + p][row 8 h + j] of the four voxel phases p (split_phase3, as the 16x16x32 kernel);
-// the B operand W[row 8 h + j][frame 32 n + r] is one 16-byte load of the frame-major plane (L2 hits: the four waves
-// read the same lines), carried in the same DEPTH-step ring, so there is no LDS staging and no barrier. Six products
-// per (phase, frame tile), smallest first. Accumulators: 4 phases x NT frame tiles x 16 (one wave per SIMD).
-// WL: the W fragments staged through LDS like k_mf_backproject_b16_lds (one load per workgroup instead of per wave,
-// two stages, one barrier per step): the per-wave W loads are 6 KB per 8 KB of A and miss L2 at 64k rows (25 MB of
-// W planes).
-template <int NT, int DEPTH, bool WL = false>
-__global__ __launch_bounds__(256, 1) void k_mf_backproject_x3_m32(const float* __restrict__ A, int64_t ld,
-                                                                  int64_t nrows32, const bf16_t* __restrict__ Wh,
-                                                                  const bf16_t* __restrict__ Wl, int64_t ldw,
-                                                                  int64_t rows_per_split, float* __restrict__ partial,
-                                                                  int64_t vw0, int64_t vend,
-                                                                  const int* __restrict__ skip) {
-    if (skip && *skip) return;
-    constexpr int NF = 32 * NT;
-    constexpr int RS = DEPTH + 1;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r = lane & 31, h = lane >> 5;
-    int64_t v0 = (vw0 + (int64_t)blockIdx.x * 4 + wave) * 128;
-    const bool live = v0 < vend;
-    if (!live) v0 = vend - 128;  // vend is a multiple of 128: clamped waves load valid voxels and store nothing
-    const int64_t r_begin = (int64_t)blockIdx.y * rows_per_split;
-    int64_t r_end = r_begin + rows_per_split;
-    if (r_end > nrows32) r_end = nrows32;
-    const float* __restrict__ ap = A + (r_begin + 8 * h) * ld + v0 + 4 * r;
-    const int64_t wo = (int64_t)r * ldw + r_begin + 8 * h;
-    const bf16_t* __restrict__ wpl[3] = {Wh + wo, Wh + (int64_t)NF * ldw + wo, Wl + wo};  // hi, mid, lo planes
-
-    f32x16 acc[4][NT];
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int n = 0; n < NT; ++n)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) acc[p][n][i] = 0.f;
-
-    constexpr int C = 3 * NT;                   // 1 KiB W pieces per step: (plane, frame tile)
-    constexpr int XQ = (C + 3) / 4;             // pieces per wave (clamped: a duplicate load writes equal data)
-    __shared__ __attribute__((aligned(16))) u32x4 s_w[WL ? 2 : 1][WL ? C : 1][64];
-    auto piece = [&](int i) { return wave * XQ + i < C ? wave * XQ + i : C - 1; };
-    const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 16 : 0;
-    if (nst > 0) {
-        u32x4 av[RS][8];
-        u32x4 wv[RS][WL ? XQ : 3][WL ? 1 : NT];
-        auto load = [&](auto slc, int64_t t) {
-            constexpr int sl = decltype(slc)::value;
-            const float* at = ap + t * 16 * ld;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                av[sl][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(at + j * ld));
-            if constexpr (WL) {
-#pragma unroll
-                for (int i = 0; i < XQ; ++i) {
-                    const int pc = piece(i), pl = pc / NT, n = pc % NT;
-                    wv[sl][i][0] = *reinterpret_cast<const u32x4*>(wpl[pl] + (int64_t)n * 32 * ldw + t * 16);
-                }
-            } else {
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-                    for (int n = 0; n < NT; ++n)
-                        wv[sl][pl][n] = *reinterpret_cast<const u32x4*>(wpl[pl] + (int64_t)n * 32 * ldw + t * 16);
-            }
-        };
-        auto stage = [&](auto slc, int64_t t) {  // WL: this wave's pieces of step t into stage t & 1
-            constexpr int sl = decltype(slc)::value;
-            if constexpr (WL) {
-#pragma unroll
-                for (int i = 0; i < XQ; ++i) s_w[t & 1][piece(i)][lane] = wv[sl][i][0];
-            }
-        };
-        [&]<int... Q>(std::integer_sequence<int, Q...>) {
-            (load(std::integral_constant<int, Q>{}, Q < nst ? Q : nst - 1), ...);
-        }(std::make_integer_sequence<int, DEPTH>{});
-        if constexpr (WL) {
-            stage(std::integral_constant<int, 0>{}, 0);
-            __syncthreads();
-        }
-        auto step = [&](auto slc, int64_t t) {
-            constexpr int sl = decltype(slc)::value;
-            load(std::integral_constant<int, (sl + DEPTH) % RS>{}, t + DEPTH < nst ? t + DEPTH : nst - 1);
-            if (t >= nst) return;
-            u32x4 wf[3][NT];
-            if constexpr (WL) {
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-                    for (int n = 0; n < NT; ++n) wf[pl][n] = s_w[t & 1][pl * NT + n][lane];
-            } else {
-#pragma unroll
-                for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-                    for (int n = 0; n < NT; ++n) wf[pl][n] = wv[sl][pl][n];
-            }
-            u32x4 fh[4], fm[4], fl[4];
-            split_phase3<0>(av[sl], fh[0], fm[0], fl[0]);
-            split_phase3<1>(av[sl], fh[1], fm[1], fl[1]);
-            split_phase3<2>(av[sl], fh[2], fm[2], fl[2]);
-            split_phase3<3>(av[sl], fh[3], fm[3], fl[3]);
-            auto prod = [&](const u32x4(&fa)[4], int pl) {
-#pragma unroll
-                for (int n = 0; n < NT; ++n)
-#pragma unroll
-                    for (int p = 0; p < 4; ++p) acc[p][n] = mfma32_b16(fa[p], wf[pl][n], acc[p][n]);
-            };
-            prod(fh, 2);
-            prod(fm, 1);
-            prod(fl, 0);
-            prod(fh, 1);
-            prod(fm, 0);
-            prod(fh, 0);
-            if constexpr (WL) {  // W of step t + 1 into the other stage (its readers passed the last barrier)
-                __builtin_amdgcn_sched_barrier(0);
-                stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);
-                __syncthreads();
-            }
-        };
-        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
-            [&]<int... Q>(std::integer_sequence<int, Q...>) {
-                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
-            }(std::make_integer_sequence<int, RS>{});
-        }
-    }
-    if (!live) return;
-    // D of (phase p, frame tile n): column = lane & 31 (frame 32 n + r), row m = (i & 3) + 8 (i >> 2) + 4 h
-    // (voxel v0 + 4 m + p); 32 lanes store 128 contiguous bytes of one voxel's frames
-    float* out = partial + (int64_t)blockIdx.y * ld * NF;
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int n = 0; n < NT; ++n)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
-                out[(v0 + 4 * m + p) * NF + 32 * n + r] = acc[p][n][i];
-            }
-}
 
 // ----------------------------------------------------------------------------------------------------------------
 // Split-A back-projection on f16 pairs (SART_MF_BWD16, default for fp32 shards at 32 / 64 frames). fp16 has 11
@@ -1527,11 +972,6 @@ __global__ __launch_bounds__(256, MW) void k_mf_backproject_h16(const float* __r
         }
 }
 
-static int mf_stagger() {
-    const char* e = std::getenv("SART_MF_STAGGER");
-    return (e && *e) ? std::atoi(e) : 0;
-}
-
 static void check_nf_b16(int nf, const char* what) {
     if (nf != 16 && nf != 32 && nf != 64) throw std::runtime_error(std::string(what) + ": nf must be 16, 32 or 64");
 }
@@ -1592,24 +1032,6 @@ static void fwd_b16_t(FwdTile tl, dim3 grid, hipStream_t stream, const AT* A, in
                       int64_t nrows_pad, const bf16_t* Xh, const bf16_t* Xl, float* Fout, FwdCols cps) {
     constexpr bool A32 = std::is_same<AT, float>::value;
     constexpr bool CAN_AS = A32 || KB == 2;  // full 128-B row segments per step
-    if constexpr (A32) {
-        // SART_MF_X3_FWD_REG = 1 / 2: X fragments straight into registers (k_mf_forward_x3_reg), 1 or 2 waves per SIMD
-        const int reg = env_int("SART_MF_X3_FWD_REG", 0);
-        if (reg == 1 || reg == 2) {
-            auto go = [&](auto mw, auto as) {
-                hipLaunchKernelGGL((k_mf_forward_x3_reg<NG, DEPTH, RT, KB, decltype(mw)::value, decltype(as)::value>),
-                                   grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps, g_mf_skip);
-            };
-            using W1 = std::integral_constant<int, 1>;
-            using W2 = std::integral_constant<int, 2>;
-            if (tl.as) {
-                if (reg == 2) go(W2{}, std::true_type{}); else go(W1{}, std::true_type{});
-            } else {
-                if (reg == 2) go(W2{}, std::false_type{}); else go(W1{}, std::false_type{});
-            }
-            return;
-        }
-    }
     if constexpr (A32 && NG == 4 && DEPTH == 3 && RT == 2 && KB == 1) {
         const int abl = env_int("SART_MF_ABL", 0);  // diagnostics only (tools/probe_mf_abl.py)
         if (abl > 0 && tl.as) {
@@ -1711,13 +1133,7 @@ static int mf_x3_depth(bool forward) {
     const int d = env_int("SART_MF_X3_DEPTH", 0);
     return (d == 2 || d == 3) ? d : 2;
 }
-// SART_MF_X3_BWD=m32 / m32d3: the 32x32x16 back-projection (k_mf_backproject_x3_m32, 128 voxels per wave: vt 2)
-static bool mf_x3_m32() {
-    const char* e = std::getenv("SART_MF_X3_BWD");
-    return e && std::strncmp(e, "m32", 3) == 0;
-}
 static int mf_x3_vt(int64_t ld) {
-    if (mf_x3_m32() && ld % 128 == 0) return 2;
     const int v = env_int("SART_MF_X3_VT", 0);
     const int vt = (v == 1 || v == 2) ? v : 1;
     return (vt == 2 && ld % 128 == 0) ? 2 : 1;
@@ -1776,78 +1192,12 @@ template <int NG, int DEPTH, typename AT>
 static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_t ld, int64_t nrows32,
                       const bf16_t* Wh, const bf16_t* Wl, int64_t ldw, int64_t rps, float* partial, int64_t vb0,
                       int64_t vend) {
-    if constexpr (std::is_same<AT, float>::value) {
-        if (const char* w = std::getenv("SART_MF_X3_BWD"); w && w[0] == 'w' && w[1] == '1' && vt == 1) {
-            const bool ew = env_int("SART_MF_WEARLY", 0) != 0;
-            if (std::strcmp(w, "w1d3") == 0) {
-                if (ew)
-                    hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 3, 1, AT, 0, true, 1>), grid, dim3(256), 0, stream, A,
-                                       ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
-                else
-                    hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 3, 1, AT, 0, false, 1>), grid, dim3(256), 0, stream,
-                                       A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
-            } else {
-                if (ew)
-                    hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 2, 1, AT, 0, true, 1>), grid, dim3(256), 0, stream, A,
-                                       ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
-                else
-                    hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, 2, 1, AT, 0, false, 1>), grid, dim3(256), 0, stream,
-                                       A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
-            }
-            return;
-        }
-        if (mf_x3_m32() && vt == 2 && (NG == 2 || NG == 4)) {  // 32x32x16 MFMAs, 128 voxels per wave
-            const char* e = std::getenv("SART_MF_X3_BWD");
-            constexpr int NT = NG / 2 > 0 ? NG / 2 : 1;
-            if (std::strcmp(e, "m32d3") == 0)
-                hipLaunchKernelGGL((k_mf_backproject_x3_m32<NT, 3>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
-                                   ldw, rps, partial, vb0, vend, g_mf_skip);
-            else if (std::strcmp(e, "m32l") == 0)
-                hipLaunchKernelGGL((k_mf_backproject_x3_m32<NT, 2, true>), grid, dim3(256), 0, stream, A, ld, nrows32,
-                                   Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
-            else if (std::strcmp(e, "m32ld3") == 0)
-                hipLaunchKernelGGL((k_mf_backproject_x3_m32<NT, 3, true>), grid, dim3(256), 0, stream, A, ld, nrows32,
-                                   Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
-            else
-                hipLaunchKernelGGL((k_mf_backproject_x3_m32<NT, 2>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
-                                   ldw, rps, partial, vb0, vend, g_mf_skip);
-            return;
-        }
-        // SART_MF_X3_BWD = reg1 / reg2: W fragments straight into registers (k_mf_backproject_x3_reg), 1 or 2 waves
-        // per SIMD (A/B against the LDS kernel; voxel tiles of 64: vt 1)
-        // regp: the pipelined form (the next step's split beside this step's MFMAs)
-        const char* e = std::getenv("SART_MF_X3_BWD");
-        if (e && std::strncmp(e, "pipe", 4) == 0 && vt == 1) {  // pipe2 / pipe3: ring depth 2 / 3
-            if (e[4] == '3')
-                hipLaunchKernelGGL((k_mf_backproject_x3_pipe<NG, 3>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
-                                   ldw, rps, partial, vb0, vend, g_mf_skip);
-            else
-                hipLaunchKernelGGL((k_mf_backproject_x3_pipe<NG, 2>), grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl,
-                                   ldw, rps, partial, vb0, vend, g_mf_skip);
-            return;
-        }
-        if (e && std::strncmp(e, "reg", 3) == 0 && vt == 1) {
-            if (e[3] == 'p' && e[4] == '2')  // regp2: W two steps ahead
-                hipLaunchKernelGGL((k_mf_backproject_x3_reg<NG, DEPTH, 1, true, 2>), grid, dim3(256), 0, stream, A, ld,
-                                   nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
-            else if (e[3] == 'p')  // regp: W one step ahead
-                hipLaunchKernelGGL((k_mf_backproject_x3_reg<NG, DEPTH, 1, true, 1>), grid, dim3(256), 0, stream, A, ld,
-                                   nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
-            else if (e[3] == '2')
-                hipLaunchKernelGGL((k_mf_backproject_x3_reg<NG, DEPTH, 2>), grid, dim3(256), 0, stream, A, ld, nrows32,
-                                   Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
-            else
-                hipLaunchKernelGGL((k_mf_backproject_x3_reg<NG, DEPTH, 1>), grid, dim3(256), 0, stream, A, ld, nrows32,
-                                   Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
-            return;
-        }
-    }
     if constexpr (std::is_same<AT, float>::value && NG == 4 && DEPTH == 2) {
         const int abl = env_int("SART_MF_ABL", 0);  // diagnostics only (tools/probe_mf_abl.py; read per launch)
         if (abl > 0 && vt == 1) {
             auto go = [&](auto k) {
                 hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1, AT, decltype(k)::value>), grid, dim3(256), 0,
-                                   stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
+                                   stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
             };
             switch (abl & 7) {
                 case 1: go(std::integral_constant<int, 1>{}); break;
@@ -1868,18 +1218,18 @@ static void bwd_b16_d(int vt, dim3 grid, hipStream_t stream, const AT* A, int64_
         if (env_int("SART_MF_WEARLY", std::is_same<AT, float>::value ? 0 : 1) != 0) {
             if (vt == 2)
                 hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2, AT, 0, true>), grid, dim3(256), 0, stream, A,
-                                   ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
+                                   ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
             else
                 hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1, AT, 0, true>), grid, dim3(256), 0, stream, A,
-                                   ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
+                                   ld, nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
             return;
         }
         if (vt == 2)
             hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 2, AT>), grid, dim3(256), 0, stream, A, ld,
-                               nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
+                               nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
         else
             hipLaunchKernelGGL((k_mf_backproject_b16_lds<NG, DEPTH, 1, AT>), grid, dim3(256), 0, stream, A, ld,
-                               nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip, mf_stagger());
+                               nrows32, Wh, Wl, ldw, rps, partial, vb0, vend, g_mf_skip);
         return;
     }
     if constexpr (!std::is_same<AT, float>::value) {

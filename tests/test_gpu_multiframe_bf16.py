@@ -180,8 +180,7 @@ def test_multiframe_bf16_matches_fp32_engine_on_rounded_matrix():
 
 # ------------------------------------------------------------------ split-A: fp32 A on the bf16 matrix cores
 @pytest.mark.parametrize("fwd,vt,depth", [("", "", ""), ("2,1", "1", "3"), ("2,2", "2", "2"), ("4,2", "2", "3"),
-                                           ("4,1,as", "1", "2"), ("2,2,as", "1", "3"), ("2,1,as", "2", "2"),
-                                           ("", "m32", ""), ("2,2,as", "m32d3", "")])
+                                           ("4,1,as", "1", "2"), ("2,2,as", "1", "3"), ("2,1,as", "2", "2")])
 @pytest.mark.parametrize("nf", [16, 32, 64])
 @pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (64, 1024), (2048, 4096), (1000, 1088)])
 def test_split_a_projections(k, dev, P, V, nf, fwd, vt, depth, monkeypatch):
@@ -190,10 +189,7 @@ def test_split_a_projections(k, dev, P, V, nf, fwd, vt, depth, monkeypatch):
     tests compare against the rounded matrix)."""
     from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
 
-    # vt "m32" / "m32d3": the 32x32x16 back-projection (k_mf_backproject_x3_m32, 128 voxels per wave)
-    bwd = vt if vt.startswith("m32") else ""
-    for name, val in (("SART_MF_X3_FWD", fwd), ("SART_MF_X3_VT", "" if bwd else vt), ("SART_MF_X3_DEPTH", depth),
-                      ("SART_MF_X3_BWD", bwd)):
+    for name, val in (("SART_MF_X3_FWD", fwd), ("SART_MF_X3_VT", vt), ("SART_MF_X3_DEPTH", depth)):
         if val:
             monkeypatch.setenv(name, val)
     rng = np.random.default_rng(P * 7 + V)

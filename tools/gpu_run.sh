@@ -541,9 +541,8 @@ for step in "$@"; do
     r4tiles) PROBE_STORAGE=fp32 PROBE_TILES="2,1,as:3;2,1,as:2;4,1,as:3;4,1,as:2;2,2,as:2;2,2,as:3;4,1:3;2,2:2;4,2,as:2" \
                run probe_tiles 600 python tools/probe_mf_xblk.py ;;
     r4profmf) run rocprof_mfx64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --no-selfcheck ;;
-    r4m32) PROBE_ABL=0 PROBE_BWD="${M32_SET:-lds:2,m32:2,m32d3:2,lds:2}" run probe_m32 300 python tools/probe_mf_abl.py &&
-           PROBE_ABL=0 PROBE_BWD="${M32_SET:-lds:2,m32:2,m32d3:2}" run probe_m32_2tb 300 python tools/probe_mf_abl.py 16384x262144 ;;
-    r4m32test) run pytest_m32 600 python -u -m pytest tests/test_gpu_multiframe_bf16.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "split_a_projections and m32" ;;
+    r4m32) PROBE_ABL=0 PROBE_BWD="${M32_SET:-lds:2,h16:2,lds:2,h16:2}" run probe_m32 300 python tools/probe_mf_abl.py &&
+           PROBE_ABL=0 PROBE_BWD="${M32_SET:-lds:2,h16:2,lds:2,h16:2}" run probe_m32_2tb 300 python tools/probe_mf_abl.py 16384x262144 ;;
     r4bf16cw)  # wide bf16 tiles, XCD-local vs chip-wide groups, self-check on (rc 1 = self-check failed: keep going)
       for spec in "131072:1:" "131072:0:" "150000:0:4" "150000:0:2" "163840:0:" "150000:1:"; do
         IFS=: read -r v xl t <<< "$spec"

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Ablations of the split-A 64-frame back-projection (k_mf_backproject_b16_lds<4, 2, 1, float, ABL>, the 2tb preset's
-kernel): time per call with the MFMAs (1), the in-register split of A (2) and / or the W staging + barrier (4)
-removed (SART_MF_ABL = OR of the bits), on a synthetic fp32 shard (default 65536 x 65536). The bit whose removal
-moves the time names the pipe that bounds a step. One JSON line per variant."""
+"""Ablations of the split-A 64-frame back-projection (k_mf_backproject_b16_lds<4, 2, 1, float, ABL>, the bf16
+three-piece form): time per call with the MFMAs (1), the in-register split of A (2) and / or the W staging + barrier
+(4) removed (SART_MF_ABL = OR of the bits), on a synthetic fp32 shard (default 65536 x 65536); the bit whose removal
+moves the time names the pipe that bounds a step. Then back-projection variants (PROBE_BWD, "lds" = the bf16 form,
+"h16[+ew|w1]" = the f16-pair kernel, "_vt2" two voxel tiles per wave) against the first, and the split-A forward's
+ablations. One JSON line per variant."""
 import json
 import os
 import sys
@@ -42,13 +44,10 @@ def main():
     os.environ.pop("SART_MF_ABL", None)
     ref = None
     for bwd, depth in [tuple(v.split(":")) for v in os.environ.get(
-            "PROBE_BWD", "lds:2,pipe2:2,pipe3:2,reg1:2,lds:2").split(",")]:
-        # "<variant>@n": SART_MF_STAGGER=n; "<variant>_vt2": two 64-voxel tiles per wave (SART_MF_X3_VT=2)
+            "PROBE_BWD", "lds:2,h16:2,lds:2,h16:2").split(";" if ";" in os.environ.get("PROBE_BWD", "") else ",")]:
+        # "<variant>_vt2": two 64-voxel tiles per wave (SART_MF_X3_VT=2); "h16[+opts]": the f16-pair kernel
         name = bwd
-        bwd, _, stg = bwd.partition("@")
-        os.environ["SART_MF_STAGGER"] = stg or "0"
         os.environ["SART_MF_X3_VT"] = "2" if bwd.endswith("_vt2") else "1"
-        os.environ["SART_MF_X3_BWD"] = bwd[:-4] if bwd.endswith("_vt2") else bwd
         os.environ["SART_MF_X3_DEPTH"] = str(depth)
         nsv = k.mf_backproject_b16_num_splits(m.ld, P, True)  # m32 / vt 2: 128 voxels per wave, its own split count
         pv = torch.zeros((nsv, m.ld, nf), device=dev)
@@ -74,7 +73,6 @@ def main():
                               ms=round(med, 4), GBps=round(m.nbytes / med / 1e6, 1),
                               rel_vs_first=rel, bitwise_equal_first=bool(rel == 0.0))), flush=True)
         del pv
-    os.environ.pop("SART_MF_X3_BWD", None)
     os.environ["SART_MF_X3_VT"] = "1"
     # the split-A forward (k_mf_forward_b16_lds<4, 3, 2, 1, float, true, ABL>: A staged through LDS, X in LDS)
     X = torch.rand((nf, m.ld), device=dev)
@@ -92,23 +90,7 @@ def main():
         print(json.dumps(dict(op="mf_forward_x3", abl=abl, no_mfma=bool(abl & 1), no_split=bool(abl & 2),
                               no_x_lds=bool(abl & 4), nf=nf, P=P, V=V, nsplit=nsf, ms=round(med, 4),
                               GBps=round(m.nbytes / med / 1e6, 1))), flush=True)
-    # the register-X forward (k_mf_forward_x3_reg: no LDS, no barrier) against the LDS kernels
-    os.environ.pop("SART_MF_ABL", None)
-    ref = None
-    for tile, reg, depth in (("2,1,as", 0, 3), ("2,1", 1, 3), ("2,1", 2, 3), ("4,1", 1, 3), ("2,2", 1, 2),
-                             ("2,1", 1, 2), ("2,1,as", 1, 3), ("2,1,as", 2, 3), ("4,1,as", 1, 3), ("2,1,as", 0, 3)):
-        os.environ["SART_MF_X3_FWD"] = tile
-        os.environ["SART_MF_X3_FWD_REG"] = str(reg)
-        os.environ["SART_MF_X3_DEPTH"] = str(depth)
-        med, best = timeit(lambda: k.mf_forward_x3(m.A.data_ptr(), m.ld, P, m.nrows_pad, Xh.data_ptr(), Xl.data_ptr(),
-                                                   Fo.data_ptr(), nsf, s, nf), reps=7)
-        out = Fo.clone()
-        if ref is None:
-            ref = out
-        print(json.dumps(dict(op="mf_forward_x3", tile=tile, reg=reg, depth=depth, nf=nf, P=P, V=V, nsplit=nsf,
-                              ms=round(med, 4), GBps=round(m.nbytes / med / 1e6, 1),
-                              bitwise_equal_lds=bool(torch.equal(out, ref)))), flush=True)
-    for key in ("SART_MF_ABL", "SART_MF_X3_DEPTH", "SART_MF_X3_FWD", "SART_MF_X3_VT", "SART_MF_X3_FWD_REG"):
+    for key in ("SART_MF_ABL", "SART_MF_X3_DEPTH", "SART_MF_X3_FWD", "SART_MF_X3_VT", "SART_MF_H16"):
         os.environ.pop(key, None)
 
 
