@@ -388,7 +388,9 @@ def main() -> int:
         "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": ("fp32 RTM; forward: bf16 MFMA on A and X split into hi + lo bf16 (3 products); back-projection: "
-                  "f16 MFMA on A and W split into two scaled f16 pieces (3 products, exact to 2^-24); fp32 accumulation"
+                  + ("f16 MFMA on A and W split into two scaled f16 pieces (3 products, exact to 2^-24)"
+                     if os.environ.get("SART_MF_BWD16", "1") != "0" else
+                     "bf16 MFMA on A and W split into hi + mid + lo bf16 (6 products)") + "; fp32 accumulation"
                   if multi and solver.split_a else "fp32") if args.rtm_dtype == "fp32" else (
             "bf16 RTM storage, bf16 MFMA with hi+lo bf16 split of X / W, fp32 accumulation" if multi
             else "bf16 RTM storage; fused row dots on bf16 dot2 with hi+lo split x, fp32 sums"

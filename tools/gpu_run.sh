@@ -550,11 +550,11 @@ for step in "$@"; do
         grep -h '^{' "$OUT/bf16cw_${v}_${xl}_${t}.log" >> "$OUT/bf16cw.jsonl" || true
         grep -h "self-check" "$OUT/bf16cw_${v}_${xl}_${t}.log" | tail -1 || true
       done ;;
-    r4mfab)  # multi-frame A/B over env settings (MFAB_SETS, "," joins variables; ":" = defaults), 64 frames, both storages
+    r4mfab)  # multi-frame A/B over env settings (MFAB_SETS, "+" joins variables; ":" = defaults), 64 frames, both storages
       : > "$OUT/mf_ab.jsonl"
       for args in "--frames 64" "--frames 64 --rtm-dtype bf16" ${MFAB_EXTRA:-}; do
         for set in ${MFAB_SETS:-: SART_MF_WEARLY=0 SART_MF_WEARLY=1 SART_MF_XEARLY=0}; do
-          envs=(); [ "$set" != ":" ] && IFS=, read -ra envs <<< "$set"
+          envs=(); [ "$set" != ":" ] && IFS=+ read -ra envs <<< "$set"
           env "${envs[@]}" timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck $args > "$OUT/mfab.log" 2>&1 \
             || { echo "FATAL $args $set"; tail -n 20 "$OUT/mfab.log"; exit 1; }
           grep -h '^{' "$OUT/mfab.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); d["ab_set"]=sys.argv[1]; d["ab_args"]=sys.argv[2]; print(json.dumps(d))' "$set" "$args" >> "$OUT/mf_ab.jsonl"
