@@ -8,6 +8,7 @@
 #include <cstring>
 #include <limits>
 #include <stdexcept>
+#include <thread>
 
 #include "../kernels/launchers.hpp"
 
@@ -47,6 +48,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
         const char* e = std::getenv("SART_MF_XBLK");
         xblk_ = !(e && *e && std::atoi(e) == 0);
     }
+    if (const char* e = std::getenv("SART_MF_LAST_BWD"); e && *e) skip_last_bwd_ = std::atoi(e) == 0;
     set_device();
     hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
     hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
@@ -105,7 +107,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     }
     chunks_.push_back(ld_);
     if (comm_->size() > 1) {  // the fp32 collectives of a sweep (p2p auto mode times exactly these sizes)
-        std::vector<int64_t> sizes{(int64_t)NF * ld_ + NF, (int64_t)NF * ld_};
+        std::vector<int64_t> sizes{(int64_t)NF * ld_ + NF, (int64_t)NF * ld_, (int64_t)NF};
         for (size_t c = 0; c + 1 < chunks_.size(); ++c)
             sizes.push_back((chunks_[c + 1] - chunks_[c]) * NF + (c + 2 == chunks_.size() ? NF : 0));
         comm_->prepare(sizes);
@@ -185,7 +187,7 @@ void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int
     }
 }
 
-void MultiFrameEngine::sweep() {
+void MultiFrameEngine::sweep(bool last) {
     const int NF = nf_;
     MfState* st = st_.get();
     const MfSkipScope skip(&st->all_done);  // every slot done: the sweep's heavy kernels return at once
@@ -195,6 +197,14 @@ void MultiFrameEngine::sweep() {
     forward();
     launch_mf_weights(Fs_.get(), nsf_, Pp_, ghat_.get(), arow_.get(), cfg_.logarithmic, W_.get(), F2part_.get(),
                       NF, stream_);
+    if (last && skip_last_bwd_) {
+        // every running frame is decided at max_iter here (its update is skipped on all_done): ||A x||^2 only
+        launch_mf_collect(part_.get(), nsb_, ld_, 0, 0, scale, D, F2part_.get(), nwb_, F2, NF, stream_);
+        if (comm_->size() > 1) comm_->all_reduce(F2, (size_t)NF, ReduceOp::kSum, stream_);
+        launch_mf_decide(st, F2, stream_);
+        ++host_sweep_;
+        return;
+    }
     const int nc = (int)chunks_.size() - 1;
     if (comm_->size() > 1 && nc > 1) {
         // Overlap: the back-projection runs chunk by chunk over the voxel axis on the compute
@@ -255,17 +265,30 @@ void MultiFrameEngine::admit(const double* g, const std::vector<int>& slots, con
     if (k == 0) return;
     // per-frame maxima and positive sums of squares over all ranks' pixels (reference sartsolver_cuda.cpp:146-157)
     double mx[kMfMaxFrames], gs[kMfMaxFrames];
-    for (int q = 0; q < k; ++q) {
-        mx[q] = -std::numeric_limits<double>::infinity(), gs[q] = 0.0;
+    auto scan = [&](int q) {  // one frame, pixels in order (the sum is deterministic whatever thread runs it)
+        double m = -std::numeric_limits<double>::infinity(), s = 0.0;
         const double* gq = g + (int64_t)frames[q] * P_;
         double* hq = hg_ + (int64_t)q * P_;
         for (int64_t p = 0; p < P_; ++p) {
             double v = gq[p];
             if (!std::isfinite(v)) v = -1.0;  // non-finite pixel: masked like a saturated one
             hq[p] = v;
-            mx[q] = std::max(mx[q], v);
-            if (v > 0) gs[q] += v * v;
+            m = std::max(m, v);
+            if (v > 0) s += v * v;
         }
+        mx[q] = m, gs[q] = s;
+    };
+    // frames on host threads when the batch is large (64 frames x 245760 pixels: 12 ms on one thread per solve)
+    const int nth = (int)std::min<int64_t>({k, 8, std::max<int64_t>(1, (int64_t)k * P_ / (1 << 20))});
+    if (nth > 1) {
+        std::vector<std::thread> pool;
+        for (int t = 0; t < nth; ++t)
+            pool.emplace_back([&, t] {
+                for (int q = t; q < k; q += nth) scan(q);
+            });
+        for (auto& th : pool) th.join();
+    } else {
+        for (int q = 0; q < k; ++q) scan(q);
     }
     comm_->host().all_reduce_host(mx, k, ReduceOp::kMax);
     comm_->host().all_reduce_host(gs, k, ReduceOp::kSum);
@@ -414,7 +437,8 @@ std::vector<SolveInfo> MultiFrameEngine::solve_batch_once(const double* g, int n
         if (n <= 0) return false;
         {
             RoctxRange r("sart::mf_chunk");
-            for (int i = 0; i < n; ++i) sweep();
+            // the chunk that reaches the bound ends with the batch's final sweep (its frames are all decided there)
+            for (int i = 0; i < n; ++i) sweep(i == bound - 1);
         }
         enq += n;
         const int slot = issued & 1;

@@ -52,7 +52,10 @@ class MultiFrameEngine {
     // the device, normalisation src_norm), else cold.
     void admit(const double* g, const std::vector<int>& slots, const std::vector<int>& frames, const double* warm,
                const float* dev_src, double src_norm, std::vector<double>& slot_norm);
-    void sweep();
+    // last: the batch's final sweep (every running frame reaches max_iter at its decision): forward, ||A x||^2 and
+    // the decision only; its back-projection and update would be discarded (reference sartsolver_cuda.cpp:231-262
+    // runs max_iter back-projections after the initial guess)
+    void sweep(bool last = false);
     void set_device() const;
     // F = A X (Fs_ split-K partials); the bf16 engine first writes the X planes
     void forward();
@@ -98,6 +101,7 @@ class MultiFrameEngine {
     double* hg_ = nullptr;       // pinned [k][rows] staging of the frames entering slots
     float* hx_ = nullptr;        // pinned [nf][ld]: solutions of finished frames, per slot
     hipEvent_t ev_copy_ = nullptr;
+    bool skip_last_bwd_ = true;  // SART_MF_LAST_BWD=1: run the final sweep's back-projection anyway (A/B)
     int host_sweep_ = 0;         // sweeps queued in the current solve_batch (EngineConfig::fault_nan_sweep)
     DeviceArray<float> Otmp_;    // log mode: observed back-projection of the frames entering slots
     DeviceArray<float> xsrc_;    // [ld] copy of the finished frame that warm-starts a refill

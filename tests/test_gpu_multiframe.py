@@ -105,3 +105,36 @@ def test_multiframe_nonfinite_slot_is_rolled_back_and_refilled(monkeypatch, log)
         x, st, it = sart_gpu_semantics(A, G[f], None, logarithmic=log, **kw)
         assert res[f].status == st and abs(res[f].iterations - it) <= 2, (f, res[f].iterations, it)
         assert np.linalg.norm(res[f].solution - x) / np.linalg.norm(x) < 3e-3
+
+
+@pytest.mark.parametrize("log", [False, True])
+@pytest.mark.parametrize("tol", [0.0, 1e-4])
+def test_final_sweep_skips_backprojection_bitwise(monkeypatch, log, tol):
+    """The batch's final sweep (every running frame decided at max_iter) runs the forward and the decision only;
+    its back-projection and update would be discarded. Solutions, iteration counts, statuses and convergence
+    values equal those of SART_MF_LAST_BWD=1 (the full final sweep) bit for bit, with slots refilled across chunk
+    boundaries (40 frames through 16 slots, chunks of 5 sweeps)."""
+    from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+    from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SolverParams
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(11)
+    P, V, nframes = 600, 1000, 40
+    A = rng.random((P, V), dtype=np.float32)
+    G = (rng.random((nframes, V)) + 0.05) @ A.T.astype(np.float64)
+    L = LaplacianCSR.grid_3d(10, 10, 10, device=dev)
+    rtm = DenseRTM.from_dense(A, device=dev)
+    out = {}
+    for full in ("1", "0"):
+        monkeypatch.setenv("SART_MF_LAST_BWD", full)
+        s = MultiFrameSARTSolver(rtm, L, None, SolverParams(max_iterations=12, conv_tolerance=tol, beta_laplace=1e-3),
+                                 logarithmic=log, batch=16, check_interval=5, allow_zero_tolerance=True)
+        out[full] = s.solve_batch(G)
+        del s
+    for a, b in zip(out["1"], out["0"]):
+        assert (a.status, a.iterations, a.convergence, a.nonfinite) == (b.status, b.iterations, b.convergence,
+                                                                        b.nonfinite)
+        assert np.array_equal(a.solution, b.solution)
+    assert max(r.iterations for r in out["0"]) == 12

@@ -540,6 +540,14 @@ for step in "$@"; do
           run bench_2tb_blk 900 python bench.py --config 2tb --steps 2 --warmup 1 ;;
     r4tiles) PROBE_STORAGE=fp32 PROBE_TILES="2,1,as:3;2,1,as:2;4,1,as:3;4,1,as:2;2,2,as:2;2,2,as:3;4,1:3;2,2:2;4,2,as:2" \
                run probe_tiles 600 python tools/probe_mf_xblk.py ;;
+    r4lastbwd)  # final-sweep back-projection skipped (default) vs run (SART_MF_LAST_BWD=1)
+              run pytest_mf 600 python -u -m pytest tests/test_gpu_multiframe.py tests/test_gpu_multiframe_bf16.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider &&
+              run bench_2tb_skip 600 python bench.py --config 2tb --steps 2 --warmup 1 &&
+              SART_MF_LAST_BWD=1 run bench_2tb_full 600 python bench.py --config 2tb --steps 2 --warmup 1 &&
+              run bench_mfx64_skip 300 python bench.py --steps 3 --warmup 1 --frames 64 &&
+              run bench_mfb64_skip 300 python bench.py --steps 3 --warmup 1 --frames 64 --rtm-dtype bf16 ;;
+    r4prof2tb) run rocprof_2tb 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_2tb" -o run --output-format csv -- python3 bench.py --config 2tb --steps 1 --warmup 0 --no-selfcheck &&
+               run rocprof_mfb64 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --rtm-dtype bf16 --no-selfcheck ;;
     r4profmf) run rocprof_mfx64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --no-selfcheck ;;
     r4m32) PROBE_ABL=0 PROBE_BWD="${M32_SET:-lds:2,h16:2,lds:2,h16:2}" run probe_m32 300 python tools/probe_mf_abl.py &&
            PROBE_ABL=0 PROBE_BWD="${M32_SET:-lds:2,h16:2,lds:2,h16:2}" run probe_m32_2tb 300 python tools/probe_mf_abl.py 16384x262144 ;;
