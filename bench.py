@@ -164,7 +164,7 @@ def main() -> int:
                     help="multi-frame fp32 shards: split A into hi + lo bf16 for the bf16 matrix cores (auto: at "
                          "32 / 64 frames) or fp32 MFMA")
     ap.add_argument("--frames", type=int, default=1,
-                    help="frames per step; > 1 solves them together with the multi-frame MFMA engine (up to 64 per batch)")
+                    help="frames per step; > 1 solves them together with the multi-frame MFMA engine (up to 128 per batch on fp32 shards (split-A), 64 on bf16 shards)")
     ap.add_argument("--partition", choices=["rows", "cols"], default="rows",
                     help="rows: the reference's pixel shards (default); cols: voxel shards, each GPU holds all "
                          "pixels of --nvox voxels (two-pass kernels, all-reduce of A.x)")
@@ -269,7 +269,7 @@ def main() -> int:
         from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
 
         solver = MultiFrameSARTSolver(prob.rtm, lap, comm, params, logarithmic=args.variant == "log",
-                                      batch=min(64, args.frames), check_interval=32, allow_zero_tolerance=True,
+                                      batch=min(128, args.frames), check_interval=32, allow_zero_tolerance=True,
                                       split_a={"auto": None, "on": True, "off": False}[args.mf_split_a])
         g1 = prob.measurement.cpu().numpy()
         g = np.stack([g1 * (1.0 + 0.05 * f) for f in range(args.frames)])  # distinct frames of one problem
@@ -375,7 +375,7 @@ def main() -> int:
     gflops = flop_per_iter * iters_per_s / 1e9
     use_fused = (not multi) and solver.use_fused
     # bytes of A per SART iteration of ONE frame: fused 1 read, two-pass 2 reads, multi-frame 2 reads per batch
-    bytes_per_iter = prob.rtm.nbytes * (2.0 / min(64, args.frames) if multi else (1 if use_fused else 2))
+    bytes_per_iter = prob.rtm.nbytes * (2.0 / min(solver.batch_width, args.frames) if multi else (1 if use_fused else 2))
     out = {
         "metric": METRIC,
         "value": round(gflops, 2),

@@ -20,7 +20,9 @@ void hip_ok(hipError_t e, const char* what) {
 }
 }  // namespace
 
-int MultiFrameEngine::batch_width(int frames) { return frames <= 16 ? 16 : (frames <= 32 ? 32 : 64); }
+int MultiFrameEngine::batch_width(int frames) {
+    return frames <= 16 ? 16 : (frames <= 32 ? 32 : (frames <= 64 ? 64 : 128));
+}
 
 MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel,
                                    int64_t ld, Communicator* comm, const EngineConfig& cfg)
@@ -34,15 +36,20 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
         throw std::invalid_argument("MultiFrameEngine: ld and nrows_pad must be multiples of 64 covering the shard");
     cfg_.check_interval = std::max(1, cfg_.check_interval);
     nf_ = batch_width(cfg_.mf_frames);
-    const int NF = nf_;
     if (!bf16_) {
         int m = cfg_.mf_split_a;
         if (m < 0) {
             const char* e = std::getenv("SART_MF_X3");
-            m = (e && *e) ? (std::atoi(e) != 0) : (NF >= 32);
+            m = (e && *e) ? (std::atoi(e) != 0) : (nf_ >= 32);
         }
         x3_ = m != 0;
     }
+    // split-A back-projection: f16 pairs (three products) unless SART_MF_BWD16=0 (bf16 hi + mid + lo, six)
+    if (const char* e = std::getenv("SART_MF_BWD16"); x3_) h16_ = !(e && *e && std::atoi(e) == 0);
+    // 128 columns (8 MFMA column groups) exist for the split-A forward and the f16-pair back-projection only; other
+    // paths take 64-frame batches
+    if (nf_ == 128 && !(x3_ && h16_)) nf_ = 64;
+    const int NF = nf_;
     split_ = bf16_ || x3_;
     if (split_) {  // X planes blocked [ld / 32][nf][32] for the forward (SART_MF_XBLK=0: frame-major, A/B runs)
         const char* e = std::getenv("SART_MF_XBLK");
@@ -76,9 +83,6 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     st_.resize(1);
     if (split_) {
         for (auto* b : {&Xh_, &Xl_}) b->resize((size_t)NF * ld_);
-        // split-A back-projection: f16 pairs (three products) unless SART_MF_BWD16=0 (bf16 hi + mid + lo, six)
-        const char* e = std::getenv("SART_MF_BWD16");
-        h16_ = x3_ && !(e && *e && std::atoi(e) == 0);
         if (h16_) {
             W16_.resize((size_t)2 * NF * Pp_);
             wmax_.resize(NF);
@@ -472,12 +476,12 @@ std::vector<SolveInfo> MultiFrameEngine::solve_batch_once(const double* g, int n
         for (int f = 0; f < NF; ++f) {
             const int fr = slot_frame[f];
             if (fr < 0 || c < slot_valid[f] || !S.done[f]) continue;
-            const bool rollback = (S.rollback >> f) & 1;
+            const bool rollback = (S.rollback[f >> 6] >> (f & 63)) & 1;
             SolveInfo& info = out[fr];
             info.status = S.status[f] == kSuccess ? kSuccess : kMaxIterationsExceeded;
             info.iterations = S.iters[f];
             info.convergence = S.conv[f];
-            info.nonfinite = (S.flags >> f) & 1;
+            info.nonfinite = (S.flags[f >> 6] >> (f & 63)) & 1;
             info.used_fused = false;
             info.warm_from = frame_warm[fr];
             frame_norm[fr] = slot_norm[f];

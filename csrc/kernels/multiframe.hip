@@ -286,7 +286,7 @@ static int mf_vox(int64_t ld, int nf);
 // Split-K of the back-projection: ~512 workgroups. The kernel time is flat from 4 to 32 splits at
 // 64k x 64k (profiles/probe_r1_mf_splits.jsonl) while k_mf_collect reads nsplit partial slices.
 int mf_backproject_num_splits(int64_t ld, int64_t nrows) {
-    const int64_t nblk = (ld / (64 * mf_vox(ld, kMfMaxFrames)) + 3) / 4;
+    const int64_t nblk = (ld / (64 * mf_vox(ld, 64)) + 3) / 4;  // the fp32 kernels' widest batch
     const char* e = std::getenv("SART_MF_BP_BLOCKS");  // target workgroups (tuning knob)
     const int64_t target = (e && *e) ? std::atoll(e) : 512;
     int64_t s = (target + nblk - 1) / nblk;

@@ -972,8 +972,11 @@ __global__ __launch_bounds__(256, MW) void k_mf_backproject_h16(const float* __r
         }
 }
 
-static void check_nf_b16(int nf, const char* what) {
-    if (nf != 16 && nf != 32 && nf != 64) throw std::runtime_error(std::string(what) + ": nf must be 16, 32 or 64");
+// split128: the split-A forward and the f16-pair back-projection also take 128 frames (8 column groups)
+static void check_nf_b16(int nf, const char* what, bool split128 = false) {
+    if (nf == 128 && split128) return;
+    if (nf != 16 && nf != 32 && nf != 64)
+        throw std::runtime_error(std::string(what) + (split128 ? ": nf must be 16, 32, 64 or 128" : ": nf must be 16, 32 or 64"));
 }
 
 // Tunables (tools/probe_mf_b16.py): register-ring depth (SART_MF_DEPTH 1..3), forward tile (SART_MF_B16_FWD =
@@ -1124,6 +1127,7 @@ static FwdTile mf_x3_fwd_tile(int nf, int64_t ld) {
     // profiles/probe_r4_mf_x3_fwd_tiles_xblk.jsonl) 64 frames on rows of >= 128k columns take two 32-voxel blocks per
     // step (16384 x 262144: 3.08 against 3.21 ms; 64k x 64k: 2.96 against 2.90, so narrower rows keep one)
     if (nf == 64) return ld >= 131072 ? FwdTile{2, 2, true, true} : FwdTile{2, 1, true, true};
+    if (nf == 128) return FwdTile{2, 1, true, true};  // 128 frames: one 32-voxel block per step (registers)
     return FwdTile{2, 2, true};
 }
 static int mf_x3_depth(bool forward) {
@@ -1147,14 +1151,29 @@ static void launch_mf_forward_split(const AT* A, int64_t ld, int64_t nrows, int6
     const char* what = A32 ? "mf_forward_x3" : "mf_forward_b16";
     if (ld % 64 != 0) throw std::runtime_error(std::string(what) + ": ld must be a multiple of 64");
     if (nsplit < 1) throw std::runtime_error(std::string(what) + ": nsplit must be >= 1");
-    check_nf_b16(nf, what);
+    check_nf_b16(nf, what, A32);
     if (nrows_pad % 32 != 0) throw std::runtime_error(std::string(what) + ": padded rows must be a multiple of 32");
     FwdTile tl = A32 ? mf_x3_fwd_tile(nf, ld) : mf_b16_fwd_tile(nf);
     if (nrows_pad % (16 * tl.rt) != 0) tl = FwdTile{2, 1, tl.lds, A32 && tl.as};  // a wave's rows inside the padding
+    if (A32 && nf == 128) tl.rt = 2, tl.as = true;  // the one 128-frame tiling (see below)
     const FwdCols cps{((ld + nsplit - 1) / nsplit + 63) / 64 * 64, xblk ? 32 : ld, xblk ? 32 * (int64_t)nf : 32};
     const int64_t rows_per_block = 64 * tl.rt;
     const dim3 grid((unsigned)((nrows_pad + rows_per_block - 1) / rows_per_block), (unsigned)nsplit);
     const int d = A32 ? mf_x3_depth(true) : mf_b16_depth(true, nf);
+    if constexpr (A32) {
+        if (nf == 128) {  // 8 column groups (64 accumulator registers at RT = 2): A staged, X early
+            auto run = [&](auto kern) {
+                hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps,
+                                   g_mf_skip);
+            };
+            if (tl.kb == 2 && d == 3) run(k_mf_forward_b16_lds<8, 3, 2, 2, float, true, 0, true>);
+            else if (tl.kb == 2) run(k_mf_forward_b16_lds<8, 2, 2, 2, float, true, 0, true>);
+            else if (d == 3) run(k_mf_forward_b16_lds<8, 3, 2, 1, float, true, 0, true>);
+            else run(k_mf_forward_b16_lds<8, 2, 2, 1, float, true, 0, true>);
+            check_launch("k_mf_forward_x3");
+            return;
+        }
+    }
     if (nf == 16)
         fwd_b16<1>(d, tl, grid, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps);
     else if (nf == 32)
@@ -1299,7 +1318,7 @@ void launch_mf_backproject_h16(const float* A, int64_t ld, int64_t nrows, const 
                                int64_t v1, float a_scale, const float* inv_scale) {
     const std::string what = "mf_backproject_h16";
     if (ld % 64 != 0) throw std::runtime_error(what + ": ld must be a multiple of 64");
-    check_nf_b16(nf, what.c_str());
+    check_nf_b16(nf, what.c_str(), true);
     const int64_t nrows32 = (nrows + 31) / 32 * 32;
     if (ldw < nrows32 || ldw % 8 != 0)
         throw std::runtime_error(what + ": W planes must hold the rows rounded up to 32 (ldw % 8 == 0)");
@@ -1332,8 +1351,18 @@ void launch_mf_backproject_h16(const float* A, int64_t ld, int64_t nrows, const 
         go(std::integral_constant<int, 1>{});
     else if (nf == 32)
         go(std::integral_constant<int, 2>{});
-    else
+    else if (nf == 64)
         go(std::integral_constant<int, 4>{});
+    else {  // 128 frames: 8 column groups, one wave per SIMD (128 accumulator registers)
+        auto run = [&](auto kern) {
+            hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, A, ld, nrows32, W1, W2, ldw, rps, partial, vw0, v1,
+                               a_scale, inv_scale, g_mf_skip);
+        };
+        if (ew && d == 3) run(k_mf_backproject_h16<8, 3, true, 1>);
+        else if (ew) run(k_mf_backproject_h16<8, 2, true, 1>);
+        else if (d == 3) run(k_mf_backproject_h16<8, 3, false, 1>);
+        else run(k_mf_backproject_h16<8, 2, false, 1>);
+    }
     check_launch("k_mf_backproject_h16");
 }
 

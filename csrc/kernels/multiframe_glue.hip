@@ -1,4 +1,4 @@
-// Element-wise and reduction kernels of the multi-frame solver (nf = 16, 32 or 64 frames as the N columns
+// Element-wise and reduction kernels of the multi-frame solver (nf = 16, 32, 64 or 128 frames as the N columns
 // of the MFMA projections in multiframe.hip). Layouts: pixel-major [rows][nf] for measurements, weights and
 // forward projections (the MFMA B/D fragments), frame-major [nf][ld] for solutions and penalties (the MFMA A
 // operand of the forward projection), voxel-major [ld][nf] for the reduced corrections (the back-projection
@@ -121,18 +121,18 @@ __global__ __launch_bounds__(256) void k_mf_collect(const float* __restrict__ pa
     }
 }
 
-// pen[f][v] = beta * sum_j L[v, j] x[f][j] (or log x), one thread per (row, frame), fixed order.
+// pen[f][v] = beta * sum_j L[v, j] x[f][j] (or log x), one thread per (row, frame), fixed order. Frame f is
+// blockIdx.y: a wave reads 64 consecutive CSR rows and the x / pen entries of one frame row (coalesced; with the
+// frame index fastest, every lane read a different frame row: 566 us per 64-frame sweep at 262144 voxels,
+// profiles/rocprof_r4_2tb_kernel_stats.csv), and a finished frame's blocks return at once.
 __global__ __launch_bounds__(256) void k_mf_penalty(const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
                                                     const float* __restrict__ val, int64_t n, float beta, int logx,
                                                     const float* __restrict__ X, int64_t ld, float* __restrict__ pen,
                                                     const MfState* __restrict__ st) {
     if (st->all_done) return;
-    const int nf = st->nf;
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n * nf) return;
-    const int f = (int)(i % nf);
-    const int64_t r = i / nf;
-    if (st->done[f]) return;
+    const int f = blockIdx.y;
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= n || st->done[f]) return;
     const float* x = X + (int64_t)f * ld;
     float s = 0.f;  // same arithmetic as k_penalty_csr (sart_update.hip)
     for (int64_t k = row_ptr[r]; k < row_ptr[r + 1]; ++k) {
@@ -157,8 +157,8 @@ __global__ void k_mf_decide(MfState* __restrict__ st, const float* __restrict__ 
         int done = st->done[f];
         if (!isfinite(F)) {
             if (!done) {  // NaN/Inf guard: the frame stops; its last finite iterate (sf - 1 updates) is in Xprev
-                atomicOr(&st->flags, 1ull << f);
-                if (sf > 0) atomicOr(&st->rollback, 1ull << f);
+                atomicOr(&st->flags[f >> 6], 1ull << (f & 63));
+                if (sf > 0) atomicOr(&st->rollback[f >> 6], 1ull << (f & 63));
                 st->iters[f] = sf > 0 ? sf - 1 : 0;
                 done = 1;
             }
@@ -188,14 +188,16 @@ __global__ void k_mf_decide(MfState* __restrict__ st, const float* __restrict__ 
 // [ld][nf] (the reduced back-projections), X / pen / Xprev frame-major [nf][ld]: a block transposes a
 // 64-voxel tile of D (and O) through LDS so both sides stay coalesced. Xprev (optional) receives the
 // iterate before the update: the rollback point of the NaN/Inf guard.
+// TN: LDS tile columns (64, or 128 for 128-frame batches; the narrower tile keeps 4 blocks per CU at <= 64 frames)
+template <int TN>
 __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const float* __restrict__ D,
                                                    const float* __restrict__ O, const float* __restrict__ pen,
                                                    float alpha, int logmode, int64_t nvox, int64_t ld,
                                                    const MfState* __restrict__ st, float* __restrict__ Xprev) {
-    __shared__ float dt[64][kMaxNF + 1];
-    __shared__ float ot[64][kMaxNF + 1];
+    __shared__ float dt[64][TN + 1];
+    __shared__ float ot[64][TN + 1];
     if (st->all_done) return;
-    const int nf = st->nf;  // 16, 32 or 64: four consecutive e of a voxel-major row share one voxel
+    const int nf = st->nf;  // 16 .. 128 (<= TN): four consecutive e of a voxel-major row share one voxel
     const int64_t v0 = (int64_t)blockIdx.x * 64;  // v0 + 63 < ld (ld % 64 == 0, grid ld / 64)
     // float4 accesses throughout (D, O: the block's 64 nf contiguous floats; X, Xprev, pen: 4 voxels of one frame)
     const float4* D4 = reinterpret_cast<const float4*>(D + v0 * nf);
@@ -263,8 +265,7 @@ __global__ void k_mf_state_begin(MfState* __restrict__ st, const double* __restr
         st->max_iter = max_iter;
         st->all_done = nused > 0 ? 0 : 1;
         st->nf = nf;
-        st->flags = 0;
-        st->rollback = 0;
+        for (int w = 0; w < kMfMaxFrames / 64; ++w) st->flags[w] = 0, st->rollback[w] = 0;
         st->tol = tol;
     }
 }
@@ -314,11 +315,12 @@ __global__ __launch_bounds__(256) void k_mf_split_x(const float* __restrict__ X,
 // three (the split-A back-projection): hi, mid = rne(w - hi) at hi + nf * ldw and lo = rne(w - hi - mid), so
 // hi + mid + lo holds w to 2^-27: the weights are residuals of both signs whose back-projection cancels, and the
 // 2^-17 of a two-piece split would show at full size in A^T W (fp32 keeps w exact).
+template <int TN>
 __global__ __launch_bounds__(256) void k_mf_split_w(const float* __restrict__ W, int64_t nrows_pad, int nf,
                                                     int64_t ldw, bf16_t* __restrict__ hi, bf16_t* __restrict__ lo,
                                                     const int* __restrict__ skip, int three) {
     if (skip && *skip) return;
-    __shared__ float tile[64][kMaxNF + 1];
+    __shared__ float tile[64][TN + 1];
     const int64_t r0 = (int64_t)blockIdx.x * 64;
     for (int i = threadIdx.x; i < 64 * nf; i += 256) {
         const int rr = i / nf, s = i % nf;
@@ -445,8 +447,8 @@ __global__ void k_mf_slot_reset(MfState* __restrict__ st, MfSlots sl) {
         st->status[f] = kMaxIterationsExceeded;
         st->iters[f] = st->max_iter;
         st->sweep0[f] = st->sweep;
-        atomicAnd(&st->flags, ~(1ull << f));
-        atomicAnd(&st->rollback, ~(1ull << f));
+        atomicAnd(&st->flags[f >> 6], ~(1ull << (f & 63)));
+        atomicAnd(&st->rollback[f >> 6], ~(1ull << (f & 63)));
     }
     __syncthreads();
     if (q == 0 && sl.n > 0) st->all_done = 0;
@@ -455,7 +457,8 @@ __global__ void k_mf_slot_reset(MfState* __restrict__ st, MfSlots sl) {
 static inline unsigned nb(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 static void check_nf(int nf, const char* what) {
-    if (nf != 16 && nf != 32 && nf != 64) throw std::runtime_error(std::string(what) + ": nf must be 16, 32 or 64");
+    if (nf != 16 && nf != 32 && nf != 64 && nf != 128)
+        throw std::runtime_error(std::string(what) + ": nf must be 16, 32, 64 or 128");
 }
 
 int mf_weights_num_blocks(int64_t nrows_pad) { return (int)((nrows_pad + kWRows - 1) / kWRows); }
@@ -482,7 +485,7 @@ void launch_mf_collect(const float* part, int nsplit, int64_t ld, int64_t v0, in
 void launch_mf_penalty(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta, bool logx,
                        const float* X, int64_t ld, float* pen, const MfState* st, int nf, hipStream_t stream) {
     check_nf(nf, "mf_penalty");
-    hipLaunchKernelGGL(k_mf_penalty, dim3(nb(n * nf)), dim3(256), 0, stream, row_ptr, col, val, n, beta,
+    hipLaunchKernelGGL(k_mf_penalty, dim3(nb(n), nf), dim3(256), 0, stream, row_ptr, col, val, n, beta,
                        logx ? 1 : 0, X, ld, pen, st);
     check_launch("k_mf_penalty");
 }
@@ -495,7 +498,8 @@ void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream) {
 void launch_mf_update(float* X, const float* D, const float* O, const float* pen, float alpha, bool logmode,
                       int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream, float* Xprev) {
     check_nf(nf, "mf_update");
-    hipLaunchKernelGGL(k_mf_update, dim3((unsigned)((ld + 63) / 64)), dim3(256), 0, stream, X, D, O, pen, alpha,
+    hipLaunchKernelGGL((nf > 64 ? k_mf_update<128> : k_mf_update<64>), dim3((unsigned)((ld + 63) / 64)), dim3(256), 0,
+                       stream, X, D, O, pen, alpha,
                        logmode ? 1 : 0, nvox, ld, st, Xprev);
     check_launch("k_mf_update");
 }
@@ -553,13 +557,14 @@ __device__ __forceinline__ int mf_w16_exp(unsigned mbits) {  // e with max |w| =
     return e;
 }
 
+template <int TN>
 __global__ __launch_bounds__(256) void k_mf_split_w16(const float* __restrict__ W, int64_t nrows_pad, int nf,
                                                       int64_t ldw, uint16_t* __restrict__ w1, uint16_t* __restrict__ w2,
                                                       const unsigned* __restrict__ wmax, float a_scale,
                                                       float* __restrict__ inv_scale, const int* __restrict__ skip) {
     if (skip && *skip) return;
-    __shared__ float tile[64][kMaxNF + 1];
-    __shared__ float sc[kMaxNF];
+    __shared__ float tile[64][TN + 1];
+    __shared__ float sc[TN];
     for (int f = threadIdx.x; f < nf; f += 256) {
         const int e = mf_w16_exp(wmax[f]);
         sc[f] = ldexpf(1.f, 14 - e);
@@ -617,7 +622,8 @@ void launch_mf_split_w16(const float* W, int64_t nrows_pad, int nf, int64_t ldw,
     const unsigned nb64 = (unsigned)((nrows_pad + 63) / 64);
     hipLaunchKernelGGL(k_mf_wmax, dim3(nb64), dim3(256), 0, stream, W, nrows_pad, nf, wmax, g_mf_skip);
     check_launch("k_mf_wmax");
-    hipLaunchKernelGGL(k_mf_split_w16, dim3((unsigned)((ldw + 63) / 64)), dim3(256), 0, stream, W, nrows_pad, nf, ldw,
+    hipLaunchKernelGGL((nf > 64 ? k_mf_split_w16<128> : k_mf_split_w16<64>), dim3((unsigned)((ldw + 63) / 64)), dim3(256),
+                       0, stream, W, nrows_pad, nf, ldw,
                        w1, w2, wmax, a_scale, inv_scale, g_mf_skip);
     check_launch("k_mf_split_w16");
 }
@@ -640,7 +646,8 @@ void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, b
                        hipStream_t stream, bool three) {
     check_nf(nf, "mf_split_w");
     if (ldw > nrows_pad) throw std::runtime_error("mf_split_w: plane stride exceeds the padded rows");
-    hipLaunchKernelGGL(k_mf_split_w, dim3((unsigned)((ldw + 63) / 64)), dim3(256), 0, stream, W, nrows_pad, nf, ldw,
+    hipLaunchKernelGGL((nf > 64 ? k_mf_split_w<128> : k_mf_split_w<64>), dim3((unsigned)((ldw + 63) / 64)), dim3(256), 0,
+                       stream, W, nrows_pad, nf, ldw,
                        hi, lo, g_mf_skip, (int)three);
     check_launch("k_mf_split_w");
 }

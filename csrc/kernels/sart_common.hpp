@@ -42,8 +42,9 @@ static_assert(sizeof(SartState) == 128, "SartState must be 128 bytes");
 enum Status : int32_t { kSuccess = 0, kMaxIterationsExceeded = -1, kRunning = -2 };
 
 // Device-resident convergence state of a multi-frame batch (multi-frame solver): one column per frame.
-// A batch holds nf = 16, 32 or 64 frames (the MFMA N dimension is 16; 32 and 64 use 2 or 4 column groups).
-constexpr int kMfMaxFrames = 64;
+// A batch holds nf = 16, 32, 64 or 128 frames (the MFMA N dimension is 16; 32 .. 128 use 2 .. 8 column groups;
+// 128 on the split-A path only).
+constexpr int kMfMaxFrames = 128;
 struct alignas(16) MfState {
     double G[kMfMaxFrames];          // sum_{g>0} g^2 / s^2 per frame
     double conv_prev[kMfMaxFrames];
@@ -55,9 +56,9 @@ struct alignas(16) MfState {
     int32_t max_iter;
     int32_t all_done;                // every frame done, or max_iter reached (no further update)
     int32_t nf;                      // frames per batch (columns in use by the kernels)
-    unsigned long long flags;        // bit f: frame f produced a non-finite ||A x||^2
+    unsigned long long flags[kMfMaxFrames / 64];     // bit f % 64 of word f / 64: frame f produced a non-finite ||A x||^2
     double tol;
-    unsigned long long rollback;     // bit f: frame f stopped at sweep >= 1 (its last finite iterate is in Xprev)
+    unsigned long long rollback[kMfMaxFrames / 64];  // frame f stopped at sweep >= 1 (last finite iterate in Xprev)
     int32_t sweep0[kMfMaxFrames];    // sweep at which the slot's current frame started (continuous batching)
 };
 

@@ -1,11 +1,12 @@
-"""Multi-frame SART: up to 64 independent frames solved together on the matrix cores (fp32, or bf16 shards).
+"""Multi-frame SART: up to 128 independent frames solved together on the matrix cores (fp32, or bf16 shards).
 
 The reference solves the time series strictly frame by frame (reference main.cpp:131-140), streaming
 the RTM twice per iteration per frame. For throughput on long time series (BASELINE.json config 5),
 frames can be batched: the forward and back projections become skinny GEMMs ``A.X`` / ``A^T.W`` with
-16, 32 or 64 right-hand sides (csrc/kernels/multiframe.hip, ``v_mfma_f32_16x16x4_f32`` on 1, 2 or 4
-column groups; at 32 / 64 frames A is split into hi + lo bf16 in registers for the bf16 matrix cores,
-csrc/kernels/multiframe_bf16.hip), reading A twice per iteration for the whole batch. Every frame keeps its own normalisation,
+16, 32, 64 or 128 right-hand sides (csrc/kernels/multiframe.hip, ``v_mfma_f32_16x16x4_f32`` on 1, 2 or 4
+column groups; from 32 frames on A is split into hi + lo bf16 (forward) / two scaled f16 pieces (back-projection)
+in registers for the 16-bit matrix cores, csrc/kernels/multiframe_bf16.hip, which also take 128 frames on 8
+column groups), reading A twice per iteration for the whole batch. Every frame keeps its own normalisation,
 saturation mask, convergence history, iteration count and status. The batch's columns are slots with
 continuous batching: as soon as a frame finishes, its slot takes the next frame between two sweeps, so no
 sweep is spent on finished frames while frames wait. Frames are cold-started (``--no_guess``), or started as a
@@ -31,7 +32,7 @@ from .rtm import DenseRTM
 from .sart import SolveResult, SolverParams, _host_f64
 
 NF = 16        # MFMA column group (frames per 16-wide N tile)
-MAX_BATCH = 64  # widest batch: 4 column groups
+MAX_BATCH = 128  # widest batch: 8 column groups (split-A fp32 shards; other paths take 64)
 
 
 class MultiFrameSARTSolver:
@@ -74,7 +75,7 @@ class MultiFrameSARTSolver:
         if self.L is not None:
             self.engine.set_laplacian(self.L.row_ptr_host, self.L.col_host, self.L.val_host)
         self.P, self.Pp, self.V, self.ld = rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld
-        self.batch_width = int(self.engine.batch_frames)  # 16, 32 or 64 columns on the matrix cores
+        self.batch_width = int(self.engine.batch_frames)  # 16, 32, 64 or 128 columns on the matrix cores
         self.split_a = bool(self.engine.split_a)
 
     def solve_batch(self, measurements, x0=None, chain: bool = False) -> List[SolveResult]:

@@ -137,4 +137,5 @@ def test_final_sweep_skips_backprojection_bitwise(monkeypatch, log, tol):
         assert (a.status, a.iterations, a.convergence, a.nonfinite) == (b.status, b.iterations, b.convergence,
                                                                         b.nonfinite)
         assert np.array_equal(a.solution, b.solution)
-    assert max(r.iterations for r in out["0"]) == 12
+    if tol == 0.0:  # fixed iteration count: every frame reaches the final-sweep decision
+        assert all(r.iterations == 12 for r in out["0"])

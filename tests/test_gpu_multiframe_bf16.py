@@ -339,3 +339,92 @@ def test_split_a_backprojection_f16_pairs(k, dev, P, V, nf, ascale, wscale):
     for f in range(nf):
         rel = np.linalg.norm(B[:, f] - B_ref[:, f]) / np.linalg.norm(B_ref[:, f])
         assert rel < 1e-6, (f, rel)
+
+
+# ------------------------------------------------------------------ 128 frames (split-A: 8 MFMA column groups)
+@pytest.mark.parametrize("fwd", ["", "2,2,as"])
+@pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (64, 1024), (2048, 4096), (1000, 1088)])
+def test_split_a_128_frames(k, dev, P, V, fwd, monkeypatch):
+    """The 128-frame split-A kernels (forward: hi + lo bf16, three products; back-projection: f16 pairs) against
+    fp64 products of the fp32 operands, with the forward's blocked and frame-major X planes bitwise equal."""
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+
+    if fwd:
+        monkeypatch.setenv("SART_MF_X3_FWD", fwd)
+    nf = 128
+    rng = np.random.default_rng(P * 5 + V)
+    A = rng.random((P, V), dtype=np.float32)
+    m = DenseRTM.from_dense(A, device=dev)
+    Ad = A.astype(np.float64)
+    X = rng.random((nf, V)).astype(np.float32)
+    Xd = torch.zeros((nf, m.ld), device=dev)
+    Xd[:, :V] = torch.from_numpy(X)
+    nsf = 3 if m.ld > 1024 else 1
+    outs = []
+    for blk in (False, True):
+        Xh = torch.empty((nf, m.ld), dtype=torch.bfloat16, device=dev)
+        Xl = torch.empty_like(Xh)
+        k.mf_split_x(Xd.data_ptr(), nf * m.ld, Xh.data_ptr(), Xl.data_ptr(), _stream(dev), True, m.ld if blk else 0)
+        Fo = torch.zeros((nsf, m.nrows_pad, nf), device=dev)
+        k.mf_forward_x3(m.A.data_ptr(), m.ld, P, m.nrows_pad, Xh.data_ptr(), Xl.data_ptr(), Fo.data_ptr(), nsf,
+                        _stream(dev), nf, blk)
+        torch.cuda.synchronize()
+        outs.append(Fo)
+    assert torch.equal(outs[0], outs[1])
+    F_ref = Ad @ X.T.astype(np.float64)
+    F = outs[1].sum(0)[:P].double().cpu().numpy()
+    assert np.linalg.norm(F - F_ref) / np.linalg.norm(F_ref) < 2e-6
+    np.testing.assert_allclose(F, F_ref, rtol=2e-5, atol=2e-4)
+    W = ((rng.random((P, nf)) - 0.5) * np.logspace(0, 3, nf)[None, :]).astype(np.float32)
+    Wd = torch.zeros((m.nrows_pad, nf), device=dev)
+    Wd[:P] = torch.from_numpy(np.ascontiguousarray(W.reshape(P, nf // 16, 16).transpose(0, 2, 1).reshape(P, nf)))
+    scratch = torch.zeros(nf, dtype=torch.int32, device=dev)
+    a_scale = k.absmax_pow2_scale(m.A.data_ptr(), m.nrows_pad * m.ld, scratch.data_ptr(), _stream(dev))
+    w16 = torch.zeros((2, nf, m.nrows_pad), dtype=torch.int16, device=dev)
+    inv = torch.zeros(nf, device=dev)
+    k.mf_split_w16(Wd.data_ptr(), m.nrows_pad, nf, m.nrows_pad, w16[0].data_ptr(), w16[1].data_ptr(),
+                   scratch.data_ptr(), a_scale, inv.data_ptr(), _stream(dev))
+    ns = 3
+    part = torch.zeros((ns, m.ld, nf), device=dev)
+    vmid = (m.ld // 2) // 64 * 64
+    for v0, v1 in ((0, vmid), (vmid, m.ld)):
+        k.mf_backproject_h16(m.A.data_ptr(), m.ld, P, w16[0].data_ptr(), w16[1].data_ptr(), m.nrows_pad, ns,
+                             part.data_ptr(), _stream(dev), nf, v0, v1, a_scale, inv.data_ptr())
+    torch.cuda.synchronize()
+    B_ref = Ad.T @ W.astype(np.float64)
+    B = part.sum(0)[:V].double().cpu().numpy()
+    for f in range(nf):
+        rel = np.linalg.norm(B[:, f] - B_ref[:, f]) / np.linalg.norm(B_ref[:, f])
+        assert rel < 1e-6, (f, rel)
+
+
+@pytest.mark.parametrize("log", [False, True])
+def test_split_a_engine_128_frames_vs_oracle(log):
+    """A 128-frame batch (8 column groups) through the split-A engine with continuous batching (150 frames: 22
+    slots refilled) against the fp64 oracle per frame; a bf16 shard asked for 128 takes 64-frame batches."""
+    from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+    from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SolverParams
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(128)
+    P, V, nframes = 700, 1000, 150
+    A = rng.random((P, V), dtype=np.float32)
+    X = rng.random((nframes, V)) + 0.05
+    G = X @ A.T.astype(np.float64)
+    G[rng.random(G.shape) < 0.03] = -1.0
+    L = LaplacianCSR.grid_3d(10, 10, 10, device=dev)
+    kw = dict(max_iterations=30, conv_tolerance=1e-4, beta_laplace=1e-3)
+    s = MultiFrameSARTSolver(DenseRTM.from_dense(A, device=dev), L, None, SolverParams(**kw), logarithmic=log,
+                             batch=128)
+    assert s.batch_width == 128 and s.split_a
+    res = s.solve_batch(G)
+    for f in list(range(0, nframes, 7)) + [127, 128, nframes - 1]:
+        x, st, it = sart_gpu_semantics(A, G[f], L, logarithmic=log, **kw)
+        assert res[f].status == st and abs(res[f].iterations - it) <= 2, (f, res[f].iterations, it)
+        assert np.linalg.norm(res[f].solution - x) / np.linalg.norm(x) < 3e-3
+    sb = MultiFrameSARTSolver(DenseRTM.from_dense(A, device=dev, storage="bf16"), None, None, SolverParams(**kw),
+                              batch=128)
+    assert sb.batch_width == 64

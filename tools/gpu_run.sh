@@ -546,6 +546,13 @@ for step in "$@"; do
               SART_MF_LAST_BWD=1 run bench_2tb_full 600 python bench.py --config 2tb --steps 2 --warmup 1 &&
               run bench_mfx64_skip 300 python bench.py --steps 3 --warmup 1 --frames 64 &&
               run bench_mfb64_skip 300 python bench.py --steps 3 --warmup 1 --frames 64 --rtm-dtype bf16 ;;
+    r4mf128)  # 128-frame split-A batches: kernels + engine tests, then 64 / 128-frame benches
+              run pytest_mf128 600 python -u -m pytest tests/test_gpu_multiframe_bf16.py -k "128" -x -q --timeout 300 --timeout-method thread -p no:cacheprovider &&
+              run pytest_mf 900 python -u -m pytest tests/test_gpu_multiframe.py tests/test_gpu_multiframe_bf16.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider &&
+              run bench_mfx64 300 python bench.py --steps 3 --warmup 1 --frames 64 &&
+              run bench_mfx128 300 python bench.py --steps 3 --warmup 1 --frames 128 &&
+              run bench_mfb64 300 python bench.py --steps 3 --warmup 1 --frames 64 --rtm-dtype bf16 &&
+              run rocprof_mfx128 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx128" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 128 --iters 20 --no-selfcheck ;;
     r4prof2tb) run rocprof_2tb 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_2tb" -o run --output-format csv -- python3 bench.py --config 2tb --steps 1 --warmup 0 --no-selfcheck &&
                run rocprof_mfb64 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --rtm-dtype bf16 --no-selfcheck ;;
     r4profmf) run rocprof_mfx64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --no-selfcheck ;;
@@ -568,6 +575,15 @@ for step in "$@"; do
           grep -h '^{' "$OUT/mfab.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); d["ab_set"]=sys.argv[1]; d["ab_args"]=sys.argv[2]; print(json.dumps(d))' "$set" "$args" >> "$OUT/mf_ab.jsonl"
           echo "=== mfab [$args] $set $(tail -n 1 "$OUT/mf_ab.jsonl" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
         done
+      done ;;
+    r4mf128ab)  # 128-frame split-A A/B over env settings (MFAB_SETS as r4mfab)
+      : > "$OUT/mf128_ab.jsonl"
+      for set in ${MFAB_SETS:-: SART_MF_X3_FWD=2,2,as SART_MF_X3_DEPTH=3 SART_MF_H16=ew SART_MF_H16=ew+SART_MF_X3_DEPTH=3}; do
+        envs=(); [ "$set" != ":" ] && IFS=+ read -ra envs <<< "$set"
+        env "${envs[@]}" timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck --frames 128 > "$OUT/mfab.log" 2>&1 \
+          || { echo "FATAL $set"; tail -n 20 "$OUT/mfab.log"; exit 1; }
+        grep -h '^{' "$OUT/mfab.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); d["ab_set"]=sys.argv[1]; print(json.dumps(d))' "$set" >> "$OUT/mf128_ab.jsonl"
+        echo "=== mf128ab $set $(tail -n 1 "$OUT/mf128_ab.jsonl" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
       done ;;
     r4bf16seg)  # chip-wide bf16 at 150000 voxels: does a shorter back-projection chain (segments) fix the self-check?
       for seg in 280 700; do
