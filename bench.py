@@ -177,9 +177,11 @@ def main() -> int:
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
                     help="BASELINE.json configuration preset (sets npix / nvox / iters / frames / laplacian)")
     args = ap.parse_args()
-    if args.config:
+    if args.config:  # the preset's values, except flags given explicitly (e.g. --config 2tb --frames 128)
+        given = {a.split("=")[0] for a in sys.argv[1:] if a.startswith("--")}
         for k, v in PRESETS[args.config].items():
-            setattr(args, k, v)
+            if "--" + k.replace("_", "-") not in given:
+                setattr(args, k, v)
     if args.rtm_dtype == "bf16" and args.partition == "cols":
         ap.error("--rtm-dtype bf16 runs row shards")
     if args.partition == "cols" and args.frames > 1:
