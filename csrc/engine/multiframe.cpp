@@ -46,9 +46,9 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     }
     // split-A back-projection: f16 pairs (three products) unless SART_MF_BWD16=0 (bf16 hi + mid + lo, six)
     if (const char* e = std::getenv("SART_MF_BWD16"); x3_) h16_ = !(e && *e && std::atoi(e) == 0);
-    // 128 columns (8 MFMA column groups) exist for the split-A forward and the f16-pair back-projection only; other
-    // paths take 64-frame batches
-    if (nf_ == 128 && !(x3_ && h16_)) nf_ = 64;
+    // 128 columns (8 MFMA column groups) exist for bf16 storage and for split-A with the f16-pair back-projection;
+    // the fp32 MFMA and three-piece bf16 back-projection paths take 64-frame batches
+    if (nf_ == 128 && !(bf16_ || (x3_ && h16_))) nf_ = 64;
     const int NF = nf_;
     split_ = bf16_ || x3_;
     if (split_) {  // X planes blocked [ld / 32][nf][32] for the forward (SART_MF_XBLK=0: frame-major, A/B runs)

@@ -1015,8 +1015,8 @@ static FwdTile mf_b16_fwd_tile(int nf) {
 }
 
 static int mf_b16_vt(int64_t ld, int nf) {
+    if (nf == 128) return 1;  // 8 column groups: one 64-voxel tile per wave
     const int v = env_int("SART_MF_B16_VT", 0);
-    (void)nf;
     const int vt = (v == 1 || v == 2) ? v : 2;
     return (vt == 2 && ld % 128 == 0) ? 2 : 1;
 }
@@ -1151,11 +1151,12 @@ static void launch_mf_forward_split(const AT* A, int64_t ld, int64_t nrows, int6
     const char* what = A32 ? "mf_forward_x3" : "mf_forward_b16";
     if (ld % 64 != 0) throw std::runtime_error(std::string(what) + ": ld must be a multiple of 64");
     if (nsplit < 1) throw std::runtime_error(std::string(what) + ": nsplit must be >= 1");
-    check_nf_b16(nf, what, A32);
+    check_nf_b16(nf, what, true);
     if (nrows_pad % 32 != 0) throw std::runtime_error(std::string(what) + ": padded rows must be a multiple of 32");
     FwdTile tl = A32 ? mf_x3_fwd_tile(nf, ld) : mf_b16_fwd_tile(nf);
     if (nrows_pad % (16 * tl.rt) != 0) tl = FwdTile{2, 1, tl.lds, A32 && tl.as};  // a wave's rows inside the padding
-    if (A32 && nf == 128) tl.rt = 2, tl.as = true;  // the one 128-frame tiling (see below)
+    // the 128-frame tilings (see below); bf16 storage stages A through LDS (+3.8 %, profiles/ab_r4_mfb128_variants.jsonl)
+    if (nf == 128) tl = FwdTile{2, A32 ? tl.kb : 2, true, true};
     const FwdCols cps{((ld + nsplit - 1) / nsplit + 63) / 64 * 64, xblk ? 32 : ld, xblk ? 32 * (int64_t)nf : 32};
     const int64_t rows_per_block = 64 * tl.rt;
     const dim3 grid((unsigned)((nrows_pad + rows_per_block - 1) / rows_per_block), (unsigned)nsplit);
@@ -1171,6 +1172,20 @@ static void launch_mf_forward_split(const AT* A, int64_t ld, int64_t nrows, int6
             else if (d == 3) run(k_mf_forward_b16_lds<8, 3, 2, 1, float, true, 0, true>);
             else run(k_mf_forward_b16_lds<8, 2, 2, 1, float, true, 0, true>);
             check_launch("k_mf_forward_x3");
+            return;
+        }
+    }
+    if constexpr (!A32) {
+        if (nf == 128) {  // bf16 storage, 128 frames: 8 column groups, RT = 2, two 32-voxel blocks per step, X in LDS
+            auto run = [&](auto kern) {
+                hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, Xh, Xl, Fout, cps,
+                                   g_mf_skip);
+            };
+            if (tl.as && d >= 3) run(k_mf_forward_b16_lds<8, 3, 2, 2, bf16_t, true>);
+            else if (tl.as) run(k_mf_forward_b16_lds<8, 2, 2, 2, bf16_t, true>);
+            else if (d >= 3) run(k_mf_forward_b16_lds<8, 3, 2, 2, bf16_t>);
+            else run(k_mf_forward_b16_lds<8, 2, 2, 2, bf16_t>);
+            check_launch("k_mf_forward_b16");
             return;
         }
     }
@@ -1284,7 +1299,7 @@ static void launch_mf_backproject_split(const AT* A, int64_t ld, int64_t nrows, 
     constexpr bool A32 = std::is_same<AT, float>::value;
     const std::string what = A32 ? "mf_backproject_x3" : "mf_backproject_b16";
     if (ld % 64 != 0) throw std::runtime_error(what + ": ld must be a multiple of 64");
-    check_nf_b16(nf, what.c_str());
+    check_nf_b16(nf, what.c_str(), !A32);  // 128 frames: bf16 storage (split-A takes launch_mf_backproject_h16)
     const int64_t nrows32 = (nrows + 31) / 32 * 32;
     if (ldw < nrows32 || ldw % 8 != 0)
         throw std::runtime_error(what + ": W planes must hold the rows rounded up to 32 (ldw % 8 == 0)");
@@ -1298,6 +1313,18 @@ static void launch_mf_backproject_split(const AT* A, int64_t ld, int64_t nrows, 
     const int64_t vw0 = v0 / align, nvw = (v1 - v0) / align;  // wave tiles
     const dim3 grid((unsigned)((nvw + 3) / 4), (unsigned)nsplit);
     const int d = A32 ? mf_x3_depth(false) : mf_b16_depth(false, nf);
+    if constexpr (!A32) {
+        if (nf == 128) {  // 8 column groups, one 64-voxel tile per wave (VT = 1), W in LDS, W loaded early
+            auto run = [&](auto kern) {
+                hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vw0, v1,
+                                   g_mf_skip);
+            };
+            if (d >= 3) run(k_mf_backproject_b16_lds<8, 3, 1, bf16_t, 0, true>);
+            else run(k_mf_backproject_b16_lds<8, 2, 1, bf16_t, 0, true>);
+            check_launch("k_mf_backproject_b16");
+            return;
+        }
+    }
     if (nf == 16)
         bwd_b16<1>(d, vt, grid, stream, A, ld, nrows32, Wh, Wl, ldw, rps, partial, vw0, v1);
     else if (nf == 32)

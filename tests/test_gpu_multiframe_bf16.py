@@ -81,7 +81,7 @@ def test_split_planes(k, dev):
 @pytest.mark.parametrize("fwd,bwd", [("", ""), ("4,1", "1,reg"), ("8,1", "2,reg"), ("4,2,lds", "1,lds"),
                                      ("8,1,lds", "2,lds"), ("2,2,lds", "2,lds"), ("4,2,lds,as", "2,lds"),
                                      ("2,2,lds,as", "1,lds")])
-@pytest.mark.parametrize("nf", [16, 32, 64])
+@pytest.mark.parametrize("nf", [16, 32, 64, 128])  # 128: one tiling whatever the knobs say
 @pytest.mark.parametrize("P,V", [(512, 1024), (1000, 2048), (64, 1024), (2048, 4096), (1000, 1088)])
 def test_bf16_mfma_projections(k, dev, P, V, nf, fwd, bwd, monkeypatch):
     if fwd:
@@ -125,7 +125,7 @@ def test_bf16_mfma_projections(k, dev, P, V, nf, fwd, bwd, monkeypatch):
 
 
 @pytest.mark.parametrize("log", [False, True])
-@pytest.mark.parametrize("nframes,batch", [(5, 16), (27, 32), (40, 64)])
+@pytest.mark.parametrize("nframes,batch", [(5, 16), (27, 32), (40, 64), (140, 128)])
 def test_multiframe_bf16_vs_oracle(log, nframes, batch):
     """The batched solver on a bf16-stored shard follows the fp64 oracle run on the same bf16-rounded matrix."""
     from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
@@ -146,6 +146,7 @@ def test_multiframe_bf16_vs_oracle(log, nframes, batch):
     L = LaplacianCSR.grid_3d(10, 10, 10, device=dev)
     kw = dict(max_iterations=40, conv_tolerance=1e-4, beta_laplace=1e-3)
     s = MultiFrameSARTSolver(rtm, L, None, SolverParams(**kw), logarithmic=log, batch=batch)
+    assert s.batch_width == batch
     res = s.solve_batch(G)
     for f in range(nframes):
         x, st, it = sart_gpu_semantics(Ab, G[f], L, logarithmic=log, **kw)
@@ -401,7 +402,7 @@ def test_split_a_128_frames(k, dev, P, V, fwd, monkeypatch):
 @pytest.mark.parametrize("log", [False, True])
 def test_split_a_engine_128_frames_vs_oracle(log):
     """A 128-frame batch (8 column groups) through the split-A engine with continuous batching (150 frames: 22
-    slots refilled) against the fp64 oracle per frame; a bf16 shard asked for 128 takes 64-frame batches."""
+    slots refilled) against the fp64 oracle per frame; the fp32 MFMA path (split-A off) takes 64-frame batches."""
     from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
     from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
     from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
@@ -425,6 +426,6 @@ def test_split_a_engine_128_frames_vs_oracle(log):
         x, st, it = sart_gpu_semantics(A, G[f], L, logarithmic=log, **kw)
         assert res[f].status == st and abs(res[f].iterations - it) <= 2, (f, res[f].iterations, it)
         assert np.linalg.norm(res[f].solution - x) / np.linalg.norm(x) < 3e-3
-    sb = MultiFrameSARTSolver(DenseRTM.from_dense(A, device=dev, storage="bf16"), None, None, SolverParams(**kw),
-                              batch=128)
-    assert sb.batch_width == 64
+    sf = MultiFrameSARTSolver(DenseRTM.from_dense(A, device=dev), None, None, SolverParams(**kw), batch=128,
+                              split_a=False)
+    assert sf.batch_width == 64

@@ -553,6 +553,16 @@ for step in "$@"; do
               run bench_mfx128 300 python bench.py --steps 3 --warmup 1 --frames 128 &&
               run bench_mfb64 300 python bench.py --steps 3 --warmup 1 --frames 64 --rtm-dtype bf16 &&
               run rocprof_mfx128 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx128" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 128 --iters 20 --no-selfcheck ;;
+    r4mfb128)  # 128-frame bf16-storage batches: tests, bench, kernel trace
+              run pytest_mfb128 600 python -u -m pytest tests/test_gpu_multiframe_bf16.py -k "128" -x -q --timeout 300 --timeout-method thread -p no:cacheprovider &&
+              run bench_mfb128 300 python bench.py --steps 3 --warmup 1 --frames 128 --rtm-dtype bf16 &&
+              run rocprof_mfb128 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb128" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 128 --iters 20 --rtm-dtype bf16 --no-selfcheck ;;
+    r4mffinal)  # multi-frame suites and the 64 / 128-frame benches of both storages
+              run pytest_mf 900 python -u -m pytest tests/test_gpu_multiframe.py tests/test_gpu_multiframe_bf16.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider &&
+              for a in "--frames 64" "--frames 128" "--frames 64 --rtm-dtype bf16" "--frames 128 --rtm-dtype bf16"; do
+                run bench_mf 300 python bench.py --steps 3 --warmup 1 $a || exit 1
+                grep -h '^{' "$OUT/bench_mf.log" >> "$OUT/mf_final.jsonl"
+              done ;;
     r4prof2tb) run rocprof_2tb 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_2tb" -o run --output-format csv -- python3 bench.py --config 2tb --steps 1 --warmup 0 --no-selfcheck &&
                run rocprof_mfb64 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --rtm-dtype bf16 --no-selfcheck ;;
     r4profmf) run rocprof_mfx64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --no-selfcheck ;;
@@ -580,7 +590,7 @@ for step in "$@"; do
       : > "$OUT/mf128_ab.jsonl"
       for set in ${MFAB_SETS:-: SART_MF_X3_FWD=2,2,as SART_MF_X3_DEPTH=3 SART_MF_H16=ew SART_MF_H16=ew+SART_MF_X3_DEPTH=3}; do
         envs=(); [ "$set" != ":" ] && IFS=+ read -ra envs <<< "$set"
-        env "${envs[@]}" timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck --frames 128 > "$OUT/mfab.log" 2>&1 \
+        env "${envs[@]}" timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-selfcheck --frames 128 ${MF128_ARGS:-} > "$OUT/mfab.log" 2>&1 \
           || { echo "FATAL $set"; tail -n 20 "$OUT/mfab.log"; exit 1; }
         grep -h '^{' "$OUT/mfab.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); d["ab_set"]=sys.argv[1]; print(json.dumps(d))' "$set" >> "$OUT/mf128_ab.jsonl"
         echo "=== mf128ab $set $(tail -n 1 "$OUT/mf128_ab.jsonl" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
