@@ -171,11 +171,12 @@ void MultiFrameEngine::forward() {
     }
 }
 
-void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int64_t v1) {
+void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int64_t v1, bool have_max) {
     if (h16_) {
         uint16_t* w1 = W16_.get();
         uint16_t* w2 = W16_.get() + (size_t)nf_ * Pp_;
-        if (split_w) launch_mf_split_w16(W, Pp_, nf_, Pp_, w1, w2, wmax_.get(), a_scale_, wscale_.get(), stream_);
+        if (split_w)
+            launch_mf_split_w16(W, Pp_, nf_, Pp_, w1, w2, wmax_.get(), a_scale_, wscale_.get(), stream_, have_max);
         launch_mf_backproject_h16(static_cast<const float*>(A_), ld_, P_, w1, w2, Pp_, nsb_, part_.get(), nf_, stream_,
                                   v0, v1, a_scale_, wscale_.get());
     } else if (split_) {
@@ -199,8 +200,9 @@ void MultiFrameEngine::sweep(bool last) {
     float* F2 = buf_.get() + (int64_t)NF * ld_;  // [nf] ||A x||^2, all-reduced with the last chunk
     const float* scale = cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get();
     forward();
+    // f16-pair back-projection: the weights kernel also leaves each frame's max |w| (its f16 scale) in wmax_
     launch_mf_weights(Fs_.get(), nsf_, Pp_, ghat_.get(), arow_.get(), cfg_.logarithmic, W_.get(), F2part_.get(),
-                      NF, stream_);
+                      NF, stream_, h16_ ? wmax_.get() : nullptr);
     if (last && skip_last_bwd_) {
         // every running frame is decided at max_iter here (its update is skipped on all_done): ||A x||^2 only
         launch_mf_collect(part_.get(), nsb_, ld_, 0, 0, scale, D, F2part_.get(), nwb_, F2, NF, stream_);
@@ -218,7 +220,7 @@ void MultiFrameEngine::sweep(bool last) {
         // still overlaps with them.
         for (int c = 0; c < nc; ++c) {
             const int64_t v0 = chunks_[c], v1 = chunks_[c + 1];
-            backproject(W_.get(), c == 0, v0, v1);
+            backproject(W_.get(), c == 0, v0, v1, true);
             const bool last = c == nc - 1;
             launch_mf_collect(part_.get(), nsb_, ld_, v0, v1, scale, D, last ? F2part_.get() : nullptr, nwb_,
                               last ? F2 : nullptr, NF, stream_);
@@ -232,7 +234,7 @@ void MultiFrameEngine::sweep(bool last) {
         }
         hip_ok(hipEventRecord(comm_done_, comm_stream_), "event");
     } else {
-        backproject(W_.get(), true, 0, ld_);
+        backproject(W_.get(), true, 0, ld_, true);
         launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, scale, D, F2part_.get(), nwb_, F2, NF, stream_);
         if (comm_->size() > 1) comm_->all_reduce(buf_.get(), (size_t)NF * ld_ + NF, ReduceOp::kSum, stream_);
     }

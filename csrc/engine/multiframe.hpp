@@ -61,7 +61,8 @@ class MultiFrameEngine {
     void forward();
     // part_ = A^T W for voxels [v0, v1) (W in the back-projection layout); the bf16 engine reads the W planes,
     // written from W when split_w
-    void backproject(const float* W, bool split_w, int64_t v0, int64_t v1);
+    // have_max: wmax_ already holds the max |w| per frame (the weights kernel of this sweep)
+    void backproject(const float* W, bool split_w, int64_t v0, int64_t v1, bool have_max = false);
 
     int device_;
     const void* A_;

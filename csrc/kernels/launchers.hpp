@@ -193,8 +193,9 @@ void launch_mf_split_x(const float* X, int64_t n, bf16_t* hi, bf16_t* lo, hipStr
                        int64_t ld = 0);
 // fp16-pair back-projection operands: frame-major planes w1, w2 ([nf][ldw] of f16 bits) of w s_f with a per-frame
 // power-of-two scale s_f (from the frame's max |w|, wmax: nf words of scratch), inv_scale[f] = 1 / (a_scale s_f)
+// have_max: wmax already holds the frames' max |w| (launch_mf_weights with wmax), else it is computed here
 void launch_mf_split_w16(const float* W, int64_t nrows_pad, int nf, int64_t ldw, uint16_t* w1, uint16_t* w2,
-                         unsigned* wmax, float a_scale, float* inv_scale, hipStream_t stream);
+                         unsigned* wmax, float a_scale, float* inv_scale, hipStream_t stream, bool have_max = false);
 // power-of-two scale 2^(14 - e) for max |A| = m 2^e over n floats (1 if A is zero); synchronises the stream
 float absmax_pow2_scale(const float* A, int64_t n, unsigned* scratch, hipStream_t stream);
 // split-A back-projection on f16 pairs (two pieces of A s_A and of W s_f, three v_mfma_f32_16x16x32_f16 products,
@@ -206,8 +207,9 @@ void launch_mf_backproject_h16(const float* A, int64_t ld, int64_t nrows, const 
 void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, bf16_t* hi, bf16_t* lo,
                        hipStream_t stream, bool three = false);
 int mf_weights_num_blocks(int64_t nrows_pad);
+// wmax (optional, nf words): also the per-frame max |w| over finite weights (zeroed here first; as k_mf_wmax)
 void launch_mf_weights(const float* Fs, int nsplit, int64_t nrows_pad, const float* ghat, const float* arow,
-                       bool logmode, float* W, double* F2part, int nf, hipStream_t stream);
+                       bool logmode, float* W, double* F2part, int nf, hipStream_t stream, unsigned* wmax = nullptr);
 // D[v][f] (voxel-major) for v in [v0, v1); F2out (optional) = per-frame sums of F2part
 void launch_mf_collect(const float* part, int nsplit, int64_t ld, int64_t v0, int64_t v1, const float* scale, float* D,
                        const double* F2part, int nF2, float* F2out, int nf, hipStream_t stream);

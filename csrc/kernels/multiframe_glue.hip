@@ -34,7 +34,8 @@ constexpr int kWRows = 64;  // rows per block (>= 1024 blocks at 64k rows: the k
 __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs, int nsplit, int64_t nrows_pad,
                                                     const float* __restrict__ ghat, const float* __restrict__ arow,
                                                     int logmode, float* __restrict__ W, double* __restrict__ F2part,
-                                                    int nf, const int* __restrict__ skip) {
+                                                    int nf, const int* __restrict__ skip,
+                                                    unsigned* __restrict__ wmax) {
     if (skip && *skip) return;
     __shared__ double red[1024];
     // four consecutive frames of one row per thread (16-byte loads of every split, in split order); q threads per
@@ -43,6 +44,7 @@ __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs
     const int f0 = fq * 4;
     const int64_t r0 = (int64_t)blockIdx.x * kWRows;
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    unsigned wm[4] = {0u, 0u, 0u, 0u};  // max |w| bits per frame (finite values only, as k_mf_wmax)
     for (int rr = rsub; rr < kWRows; rr += rstep) {
         const int64_t row = r0 + rr;
         if (row >= nrows_pad) break;
@@ -61,7 +63,9 @@ __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            W[row * nf + mf_bp_slot(f0 + k, nf)] = logmode ? av[k] * Fv[k] : av[k] * (gv[k] - Fv[k]);
+            const float w = logmode ? av[k] * Fv[k] : av[k] * (gv[k] - Fv[k]);
+            W[row * nf + mf_bp_slot(f0 + k, nf)] = w;
+            if (fabsf(w) <= 3.0e38f) wm[k] = max(wm[k], __float_as_uint(fabsf(w)));
             acc[k] += (double)Fv[k] * (double)Fv[k];
         }
     }
@@ -73,6 +77,19 @@ __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs
         double t = 0.0;
         for (int r = 0; r < rstep; ++r) t += red[(r * q + f / 4) * 4 + (f & 3)];
         F2part[(int64_t)blockIdx.x * nf + f] = t;
+    }
+    if (wmax) {  // the block's max |w| per frame, then one atomic per frame (the max is order-free)
+        __syncthreads();
+        unsigned* redu = reinterpret_cast<unsigned*>(red);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) redu[threadIdx.x * 4 + k] = wm[k];
+        __syncthreads();
+        if (threadIdx.x < nf) {
+            const int f = threadIdx.x;
+            unsigned m = 0u;
+            for (int r = 0; r < rstep; ++r) m = max(m, redu[(r * q + f / 4) * 4 + (f & 3)]);
+            if (m) atomicMax(&wmax[f], m);
+        }
     }
 }
 
@@ -464,10 +481,11 @@ static void check_nf(int nf, const char* what) {
 int mf_weights_num_blocks(int64_t nrows_pad) { return (int)((nrows_pad + kWRows - 1) / kWRows); }
 
 void launch_mf_weights(const float* Fs, int nsplit, int64_t nrows_pad, const float* ghat, const float* arow,
-                       bool logmode, float* W, double* F2part, int nf, hipStream_t stream) {
+                       bool logmode, float* W, double* F2part, int nf, hipStream_t stream, unsigned* wmax) {
     check_nf(nf, "mf_weights");
+    if (wmax) hip_call(hipMemsetAsync(wmax, 0, nf * sizeof(unsigned), stream), "hipMemsetAsync");
     hipLaunchKernelGGL(k_mf_weights, dim3((unsigned)mf_weights_num_blocks(nrows_pad)), dim3(256), 0, stream, Fs,
-                       nsplit, nrows_pad, ghat, arow, logmode ? 1 : 0, W, F2part, nf, g_mf_skip);
+                       nsplit, nrows_pad, ghat, arow, logmode ? 1 : 0, W, F2part, nf, g_mf_skip, wmax);
     check_launch("k_mf_weights");
 }
 
@@ -615,13 +633,15 @@ __global__ __launch_bounds__(256) void k_absmax_f32(const float* __restrict__ A,
 }
 
 void launch_mf_split_w16(const float* W, int64_t nrows_pad, int nf, int64_t ldw, uint16_t* w1, uint16_t* w2,
-                         unsigned* wmax, float a_scale, float* inv_scale, hipStream_t stream) {
+                         unsigned* wmax, float a_scale, float* inv_scale, hipStream_t stream, bool have_max) {
     check_nf(nf, "mf_split_w16");
     if (ldw > nrows_pad) throw std::runtime_error("mf_split_w16: plane stride exceeds the padded rows");
-    hip_call(hipMemsetAsync(wmax, 0, nf * sizeof(unsigned), stream), "hipMemsetAsync");
-    const unsigned nb64 = (unsigned)((nrows_pad + 63) / 64);
-    hipLaunchKernelGGL(k_mf_wmax, dim3(nb64), dim3(256), 0, stream, W, nrows_pad, nf, wmax, g_mf_skip);
-    check_launch("k_mf_wmax");
+    if (!have_max) {
+        hip_call(hipMemsetAsync(wmax, 0, nf * sizeof(unsigned), stream), "hipMemsetAsync");
+        const unsigned nb64 = (unsigned)((nrows_pad + 63) / 64);
+        hipLaunchKernelGGL(k_mf_wmax, dim3(nb64), dim3(256), 0, stream, W, nrows_pad, nf, wmax, g_mf_skip);
+        check_launch("k_mf_wmax");
+    }
     hipLaunchKernelGGL((nf > 64 ? k_mf_split_w16<128> : k_mf_split_w16<64>), dim3((unsigned)((ldw + 63) / 64)), dim3(256),
                        0, stream, W, nrows_pad, nf, ldw,
                        w1, w2, wmax, a_scale, inv_scale, g_mf_skip);
