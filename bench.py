@@ -42,6 +42,22 @@ PRESETS = {
 }
 
 
+def shared_gpu_env(ranks: int, ndev: int) -> dict:
+    """Environment of a rehearsal with more ranks than GPUs (--share-gpus)."""
+    # RCCL refuses two ranks on one device: gloo host collectives under the one-shot P2P all-reduce (auto-selected
+    # against the staged base), and the fused sweep on each rank's share of the CUs
+    env = dict(SART_DIST_BACKEND="gloo", SART_P2P_WRAP_STAGED="1", SART_FUSED_SHARED="1")
+    # Hardware queues: the GPU maps 24 compute queues (KFD num_cp_queues); 8 ranks x HIP's default 4 = 32
+    # over-subscribe it and the scheduler time-slices the processes, so every P2P all-reduce waits out a time slice
+    # for a descheduled peer (10.3 ms per call, 83.7 it/s; with 1 queue per rank 111 us, 172.4 it/s:
+    # profiles/bench_r4_n8_rehearsal_one_gpu_q{4,1}.json). One rank per GPU is unaffected. The cap is a ceiling on
+    # whatever the environment sets (the GPU boxes export HIP's default, 4).
+    per_gpu = -(-ranks // max(ndev, 1))
+    have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    env["GPU_MAX_HW_QUEUES"] = str(max(1, min(have, 12 // per_gpu)))
+    return env
+
+
 def grid_dims(n: int) -> tuple[int, int, int]:
     """nx * ny * nz == n with the factors as close to a cube as possible (synthetic voxel grid)."""
     best = (n, 1, 1)
@@ -199,21 +215,15 @@ def main() -> int:
                       "on fewer devices)", file=sys.stderr)
                 return 1
             if ndev < args.gpus:
-                # RCCL refuses two ranks on one device: gloo host collectives under the one-shot P2P all-reduce
-                # (auto-selected against the staged base), and the fused sweep on each rank's share of the CUs
-                env_extra.update(SART_DIST_BACKEND="gloo", SART_P2P_WRAP_STAGED="1", SART_FUSED_SHARED="1")
-                # Hardware queues: the GPU maps 24 compute queues (KFD num_cp_queues); 8 ranks x HIP's default 4 = 32
-                # over-subscribe it and the scheduler time-slices the processes, so every P2P all-reduce waits out a
-                # time slice for a descheduled peer (10.3 ms per call, 83.7 it/s; with 1 queue per rank 111 us,
-                # 172.4 it/s: profiles/bench_r4_n8_rehearsal_one_gpu_q{4,1}.json). One rank per GPU is unaffected.
-                # The cap is a ceiling on whatever the environment sets (the GPU boxes export HIP's default, 4).
-                per_gpu = -(-args.gpus // max(ndev, 1))
-                have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
-                env_extra["GPU_MAX_HW_QUEUES"] = str(max(1, min(have, 12 // per_gpu)))
+                env_extra.update(shared_gpu_env(args.gpus, ndev))
         return self_launch(args.gpus, sys.argv[1:], env_extra)
     if (world or 1) != args.gpus:
         print(f"bench: --gpus {args.gpus} but the launcher started {world or 1} rank(s)", file=sys.stderr)
         return 1
+    if world and world > 1 and args.share_gpus and not args.launch_check:
+        ndev = visible_gpu_count()
+        if ndev < world:  # an external launcher (torchrun) with ranks sharing GPUs: the same set-up, before HIP starts
+            os.environ.update(shared_gpu_env(world, ndev))
     # A device all-reduce that waits this long for a peer gives up; the engine then re-solves the frame on the base
     # communicator (RCCL), so a stalled P2P path costs one timeout instead of the watchdog's limit.
     os.environ.setdefault("SART_P2P_TIMEOUT_S", "30")
