@@ -557,6 +557,15 @@ for step in "$@"; do
               run pytest_mfb128 600 python -u -m pytest tests/test_gpu_multiframe_bf16.py -k "128" -x -q --timeout 300 --timeout-method thread -p no:cacheprovider &&
               run bench_mfb128 300 python bench.py --steps 3 --warmup 1 --frames 128 --rtm-dtype bf16 &&
               run rocprof_mfb128 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb128" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 128 --iters 20 --rtm-dtype bf16 --no-selfcheck ;;
+    r4tbab)  # 2tb preset (64 frames) A/B over env settings (MFAB_SETS as r4mfab)
+      : > "$OUT/tb_ab.jsonl"
+      for set in ${MFAB_SETS:-: SART_MF_X3_FWD=2,1,as SART_MF_FWD_BLOCKS=512 SART_MF_FWD_BLOCKS=2048}; do
+        envs=(); [ "$set" != ":" ] && IFS=+ read -ra envs <<< "$set"
+        env "${envs[@]}" timeout -k 10 400 python bench.py --config 2tb --steps 2 --warmup 1 > "$OUT/tbab.log" 2>&1 \
+          || { echo "FATAL $set"; tail -n 20 "$OUT/tbab.log"; exit 1; }
+        grep -h '^{' "$OUT/tbab.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); d["ab_set"]=sys.argv[1]; print(json.dumps(d))' "$set" >> "$OUT/tb_ab.jsonl"
+        echo "=== tbab $set $(tail -n 1 "$OUT/tb_ab.jsonl" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+      done ;;
     r4mffinal)  # multi-frame suites and the 64 / 128-frame benches of both storages
               run pytest_mf 900 python -u -m pytest tests/test_gpu_multiframe.py tests/test_gpu_multiframe_bf16.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider &&
               for a in "--frames 64" "--frames 128" "--frames 64 --rtm-dtype bf16" "--frames 128 --rtm-dtype bf16"; do
