@@ -45,7 +45,7 @@ struct EngineConfig : SolverParams {
     // Fault injection (tests; env SART_FAULT_NAN=k): write NaN into x after sweep k of every solve (eager
     // chunks), exercising the NaN/Inf guard's rollback to the last finite iterate. -1: off.
     int fault_nan_sweep = -1;
-    // Multi-frame engine: frames per batch (16, 32 or 64; MultiFrameEngine rounds other values up).
+    // Multi-frame engine: frames per batch (16, 32, 64 or 128; MultiFrameEngine rounds other values up).
     int mf_frames = 16;
     // Column (voxel) shard instead of the reference's row (pixel) shard: this rank holds ALL
     // pixel rows for voxels [col_offset, col_offset + nvoxel) of nvoxel_total, and gets the full

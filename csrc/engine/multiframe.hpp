@@ -1,5 +1,5 @@
-// Native multi-frame engine: up to nf = 16, 32 or 64 independent frames solved together on the fp32 matrix
-// cores (csrc/kernels/multiframe.hip, multiframe_glue.hip). The reference solves a time series strictly
+// Native multi-frame engine: up to nf = 16, 32, 64 or 128 independent frames solved together on the matrix cores
+// (csrc/kernels/multiframe.hip, multiframe_bf16.hip, multiframe_glue.hip; 128 on the 16-bit paths only). The reference solves a time series strictly
 // frame by frame (reference main.cpp:131-140), streaming the RTM twice per iteration per frame; batching
 // turns A.x and A^T.w into skinny GEMMs (nf right-hand sides) that reuse every byte of A nf times. Every frame
 // keeps its own normalisation, saturation mask, convergence history, status and iteration count; frames
@@ -42,7 +42,8 @@ class MultiFrameEngine {
     int64_t nvoxel() const { return V_; }
     int batch_frames() const { return nf_; }
     bool split_a() const { return x3_; }  // fp32 shard on the bf16 matrix cores
-    // 16, 32 or 64: the smallest batch width that holds `frames` (64 for anything larger)
+    // 16, 32, 64 or 128: the smallest batch width that holds `frames` (128 for anything larger; the constructor
+    // takes 64 where the path has no 128-column kernels)
     static int batch_width(int frames);
 
    private:

@@ -145,7 +145,7 @@ struct ReduceSrc {
 void launch_p2p_reduce_allreduce(const ReduceSrc& src, float* out, const P2pArgs& a, int rank, int nranks,
                                  unsigned epoch, int64_t cap, unsigned* err, double timeout_s, hipStream_t stream,
                                  bool skip_flags = false);
-// multiframe.hip (nf = frames per batch: 16, 32 or 64)
+// multiframe.hip (nf = frames per batch: 16, 32 or 64; the 16-bit kernels of multiframe_bf16.hip also take 128)
 int mf_forward_num_splits(int64_t ld, int64_t nrows_pad);
 int mf_backproject_num_splits(int64_t ld, int64_t nrows);
 void mf_set_depth(int d);  // 1..3: register-ring depth of the MFMA projections; 0: default

@@ -493,7 +493,7 @@ void launch_mf_collect(const float* part, int nsplit, int64_t ld, int64_t v0, in
                        float* D, const double* F2part, int nF2, float* F2out, int nf, hipStream_t stream) {
     check_nf(nf, "mf_collect");
     if (v0 < 0 || v1 > ld || v1 < v0) throw std::runtime_error("mf_collect: voxel range outside [0, ld)");
-    const int64_t n = (v1 - v0) * nf;  // a multiple of 4 (nf is 16, 32 or 64): 4 elements per thread
+    const int64_t n = (v1 - v0) * nf;  // a multiple of 4 (nf is 16 .. 128): 4 elements per thread
     hipLaunchKernelGGL(k_mf_collect, dim3(std::max<unsigned>(1, nb(n / 4))), dim3(256), 0, stream, part, nsplit, ld, v0, v1,
                        scale, D, F2part, nF2, F2out, nf, g_mf_skip);
     check_launch("k_mf_collect");
