@@ -427,7 +427,7 @@ PYBIND11_MODULE(_sart_hip, m) {
                                  P<uint64_t>(gran), I, J, P<sart::SartState>(st), P<unsigned>(xcnt), S(stream));
     });
     m.def("fused_min_bytes_from_env", &sart::fused_min_bytes_from_env);
-    m.def("mf_forward_num_splits", &sart::mf_forward_num_splits);
+    m.def("mf_forward_num_splits", &sart::mf_forward_num_splits, py::arg("ld"), py::arg("nrows_pad"), py::arg("target") = 0);
     m.def("mf_backproject_num_splits", &sart::mf_backproject_num_splits);
     m.def("mf_set_depth", &sart::mf_set_depth);
     m.def("mf_set_rows", &sart::mf_set_rows);

@@ -65,7 +65,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
            "hipHostMalloc");
     hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hx_), (size_t)NF * ld_ * sizeof(float)), "hipHostMalloc");
     hip_ok(hipEventCreateWithFlags(&ev_copy_, hipEventDisableTiming), "hipEventCreate");
-    nsf_ = mf_forward_num_splits(ld_, Pp_);
+    nsf_ = mf_forward_num_splits(ld_, Pp_, bf16_ ? 512 : 0);  // bf16 storage: ~512 workgroups (see the back-projection)
     nsb_ = split_ ? mf_backproject_b16_num_splits(ld_, P_, x3_) : mf_backproject_num_splits(ld_, P_);
     nwb_ = mf_weights_num_blocks(Pp_);
     X_.resize((size_t)NF * ld_);

@@ -146,7 +146,8 @@ void launch_p2p_reduce_allreduce(const ReduceSrc& src, float* out, const P2pArgs
                                  unsigned epoch, int64_t cap, unsigned* err, double timeout_s, hipStream_t stream,
                                  bool skip_flags = false);
 // multiframe.hip (nf = frames per batch: 16, 32 or 64; the 16-bit kernels of multiframe_bf16.hip also take 128)
-int mf_forward_num_splits(int64_t ld, int64_t nrows_pad);
+// target: workgroups to aim for (0: 1024, or SART_MF_FWD_BLOCKS)
+int mf_forward_num_splits(int64_t ld, int64_t nrows_pad, int target = 0);
 int mf_backproject_num_splits(int64_t ld, int64_t nrows);
 void mf_set_depth(int d);  // 1..3: register-ring depth of the MFMA projections; 0: default
 void mf_set_rows(int rt);  // 2 or 4: 16-row tiles per wave of the MFMA forward projection; 0: default

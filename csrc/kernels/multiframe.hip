@@ -270,11 +270,11 @@ __global__ __launch_bounds__(256) void k_mf_backproject(const float* __restrict_
 // Split-K of the forward projection: >= ~1024 workgroups, >= 1024 columns per split. (Splitting further
 // so that a split's X chunk stays L2-resident measured 0-9 % slower at nf = 16..64, 64k x 64k.)
 static int mf_rows(int nf);
-int mf_forward_num_splits(int64_t ld, int64_t nrows_pad) {
+int mf_forward_num_splits(int64_t ld, int64_t nrows_pad, int target_blocks) {
     const int64_t rows_per_block = (nrows_pad % 64 == 0 ? mf_rows(0) : 2) * 64;  // 4 waves x 16 * rt rows
     const int64_t nblk = (nrows_pad + rows_per_block - 1) / rows_per_block;
     const char* e = std::getenv("SART_MF_FWD_BLOCKS");  // target workgroups (tuning knob)
-    const int64_t target = (e && *e) ? std::atoll(e) : 1024;
+    const int64_t target = (e && *e) ? std::atoll(e) : (target_blocks > 0 ? target_blocks : 1024);
     int64_t s = (target + nblk - 1) / nblk;
     const int64_t smax = ld / 1024;
     if (s > smax) s = smax;

@@ -1212,7 +1212,9 @@ void launch_mf_forward_x3(const float* A, int64_t ld, int64_t nrows, int64_t nro
 // split.
 int mf_backproject_b16_num_splits(int64_t ld, int64_t nrows, bool a32) {
     const int64_t nblk = (ld / (64 * (a32 ? mf_x3_vt(ld) : mf_b16_vt(ld, 0))) + 3) / 4;
-    const int64_t target = env_int("SART_MF_BP_BLOCKS", 1024);
+    // bf16 storage: ~512 (fewer partial slices for k_mf_collect: +1.3 % with 512-block forwards at 64 frames,
+    // profiles/ab_r4_mf_split_blocks_low.jsonl); split-A ~1024 (256: -5 %)
+    const int64_t target = env_int("SART_MF_BP_BLOCKS", a32 ? 1024 : 512);
     int64_t s = (target + nblk - 1) / nblk;
     const int64_t smax = (nrows + 63) / 64;
     if (s > smax) s = smax;
