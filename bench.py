@@ -154,6 +154,20 @@ class Watchdog:
                 os._exit(3)
 
 
+def _split_a_dtype(solver) -> str:
+    """The operand pieces the split-A multi-frame projections ran with (MultiFrameSARTSolver.forward_split /
+    backproject_split): f16 pairs are ~2^-22 per product (not fp32-exact: 2^-24), bf16 pairs 2^-17, bf16 triples
+    fp32-exact."""
+    desc = {"f16x2": "f16 MFMA on two f16 pieces of A (scaled per %s) and of the fp32 operand (3 products, ~2^-22 "
+                     "per product)",
+            "bf16x2": "bf16 MFMA on hi + lo bf16 pieces of A and of the fp32 operand (3 products, ~2^-17 per product)",
+            "bf16x3": "bf16 MFMA on hi + mid + lo bf16 pieces of A and W (6 products, fp32-exact)"}
+    fwd = desc.get(solver.forward_split, solver.forward_split)
+    bwd = desc.get(solver.backproject_split, solver.backproject_split)
+    return ("fp32 RTM; forward: " + (fwd % "row" if "%s" in fwd else fwd) + "; back-projection: "
+            + (bwd % "column" if "%s" in bwd else bwd) + "; fp32 accumulation")
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); > 1 self-launches under torchrun")
@@ -177,10 +191,13 @@ def main() -> int:
     ap.add_argument("--no-fused", action="store_true", help="use the two-pass kernels instead of the fused sweep")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--mf-split-a", choices=["auto", "on", "off"], default="auto",
-                    help="multi-frame fp32 shards: split A into hi + lo bf16 for the bf16 matrix cores (auto: at "
-                         "32 / 64 frames) or fp32 MFMA")
+                    help="multi-frame fp32 shards: split A in registers into two f16 pieces (scaled per row for the "
+                         "forward, per column for the back-projection) for the 16-bit matrix cores (auto: from 32 "
+                         "frames on) or fp32 MFMA")
     ap.add_argument("--frames", type=int, default=1,
-                    help="frames per step; > 1 solves them together with the multi-frame MFMA engine (up to 128 per batch on fp32 shards (split-A), 64 on bf16 shards)")
+                    help="frames per step; > 1 solves them together with the multi-frame MFMA engine (up to 128 per "
+                         "batch on bf16 storage and on split-A fp32 shards; 64 on the fp32 MFMA path and the "
+                         "six-product bf16 back-projection)")
     ap.add_argument("--partition", choices=["rows", "cols"], default="rows",
                     help="rows: the reference's pixel shards (default); cols: voxel shards, each GPU holds all "
                          "pixels of --nvox voxels (two-pass kernels, all-reduce of A.x)")
@@ -399,11 +416,7 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
-        "dtype": ("fp32 RTM; forward: bf16 MFMA on A and X split into hi + lo bf16 (3 products); back-projection: "
-                  + ("f16 MFMA on A and W split into two scaled f16 pieces (3 products, exact to 2^-24)"
-                     if os.environ.get("SART_MF_BWD16", "1") != "0" else
-                     "bf16 MFMA on A and W split into hi + mid + lo bf16 (6 products)") + "; fp32 accumulation"
-                  if multi and solver.split_a else "fp32") if args.rtm_dtype == "fp32" else (
+        "dtype": (_split_a_dtype(solver) if multi and solver.split_a else "fp32") if args.rtm_dtype == "fp32" else (
             "bf16 RTM storage, bf16 MFMA with hi+lo bf16 split of X / W, fp32 accumulation" if multi
             else "bf16 RTM storage; fused row dots on bf16 dot2 with hi+lo split x, fp32 sums"
             if solver.use_fused else "bf16 RTM storage, fp32 compute"),
@@ -424,6 +437,8 @@ def main() -> int:
         "fused_plan_cus": solver.plan_cus if use_fused else None,
         "startup": startup,
         "frames_per_step": args.frames,
+        # multi-frame operand pieces that ran (f16x2 / bf16x2 / bf16x3 / fp32 / bf16-storage)
+        "mf_split": ({"forward": solver.forward_split, "backproject": solver.backproject_split} if multi else None),
         # per-iteration device all-reduce: RCCL, or the one-shot P2P kernel when it beat RCCL at start-up
         "allreduce": (solver.native_comm.describe if n > 1 else "none (1 rank)"),
         # frames re-solved after a device all-reduce timeout / a persistent-sweep timeout, over the whole run

@@ -256,6 +256,8 @@ static void bind_engine(py::module_& m) {
              py::keep_alive<1, 8>())
         .def_property_readonly("batch_frames", &sart::MultiFrameEngine::batch_frames)
         .def_property_readonly("split_a", &sart::MultiFrameEngine::split_a)
+        .def_property_readonly("forward_split", &sart::MultiFrameEngine::forward_split)
+        .def_property_readonly("backproject_split", &sart::MultiFrameEngine::backproject_split)
         .def("set_laplacian",
              [](sart::MultiFrameEngine& e, py::array_t<int64_t, py::array::c_style | py::array::forcecast> rp,
                 py::array_t<int32_t, py::array::c_style | py::array::forcecast> col,
@@ -468,13 +470,35 @@ PYBIND11_MODULE(_sart_hip, m) {
     });
     m.def("mf_backproject_h16", [](uintptr_t A, int64_t ld, int64_t nrows, uintptr_t W1, uintptr_t W2, int64_t ldw,
                                    int nsplit, uintptr_t partial, uintptr_t stream, int nf, int64_t v0, int64_t v1,
-                                   float a_scale, uintptr_t inv_scale) {
+                                   uintptr_t csc, uintptr_t inv_scale) {
         sart::launch_mf_backproject_h16(P<const float>(A), ld, nrows, P<const uint16_t>(W1), P<const uint16_t>(W2), ldw,
-                                        nsplit, P<float>(partial), nf, S(stream), v0, v1, a_scale,
+                                        nsplit, P<float>(partial), nf, S(stream), v0, v1, P<const float>(csc),
                                         P<const float>(inv_scale));
     }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("W1"), py::arg("W2"), py::arg("ldw"), py::arg("nsplit"),
-       py::arg("partial"), py::arg("stream"), py::arg("nf"), py::arg("v0"), py::arg("v1"), py::arg("a_scale"),
+       py::arg("partial"), py::arg("stream"), py::arg("nf"), py::arg("v0"), py::arg("v1"), py::arg("csc"),
        py::arg("inv_scale"));
+    m.def("mf_row_scales", [](uintptr_t A, int64_t ld, int64_t nrows_pad, uintptr_t rsc, uintptr_t stream) {
+        sart::launch_mf_row_scales(P<const float>(A), ld, nrows_pad, P<float>(rsc), S(stream));
+    });
+    m.def("mf_col_scales", [](uintptr_t A, int64_t ld, int64_t nrows_pad, uintptr_t scratch, uintptr_t csc,
+                              uintptr_t stream) {
+        sart::launch_mf_col_scales(P<const float>(A), ld, nrows_pad, P<unsigned>(scratch), P<float>(csc), S(stream));
+    });
+    m.def("mf_split_x16", [](uintptr_t X, int64_t ld, int nf, uintptr_t x1, uintptr_t x2, uintptr_t xmax,
+                             uintptr_t xinv, uintptr_t stream, bool perm, bool blocked) {
+        sart::launch_mf_split_x16(P<const float>(X), ld, nf, P<uint16_t>(x1), P<uint16_t>(x2), P<unsigned>(xmax),
+                                  P<float>(xinv), S(stream), perm, blocked);
+    }, py::arg("X"), py::arg("ld"), py::arg("nf"), py::arg("x1"), py::arg("x2"), py::arg("xmax"), py::arg("xinv"),
+       py::arg("stream"), py::arg("perm") = true, py::arg("blocked") = false);
+    m.def("mf_forward_h16", [](uintptr_t A, int64_t ld, int64_t nrows, int64_t nrows_pad, uintptr_t X1, uintptr_t X2,
+                               uintptr_t Fout, int nsplit, uintptr_t stream, int nf, bool xblk, uintptr_t rsc,
+                               uintptr_t xinv) {
+        sart::launch_mf_forward_h16(P<const float>(A), ld, nrows, nrows_pad, P<const uint16_t>(X1),
+                                    P<const uint16_t>(X2), P<float>(Fout), nsplit, nf, S(stream), xblk,
+                                    P<const float>(rsc), P<const float>(xinv));
+    }, py::arg("A"), py::arg("ld"), py::arg("nrows"), py::arg("nrows_pad"), py::arg("X1"), py::arg("X2"),
+       py::arg("Fout"), py::arg("nsplit"), py::arg("stream"), py::arg("nf"), py::arg("xblk"), py::arg("rsc"),
+       py::arg("xinv"));
     m.def("mf_split_w", [](uintptr_t W, int64_t nrows_pad, int nf, int64_t ldw, uintptr_t hi, uintptr_t lo,
                            uintptr_t stream, bool three) {
         sart::launch_mf_split_w(P<const float>(W), nrows_pad, nf, ldw, P<sart::bf16_t>(hi), P<sart::bf16_t>(lo),

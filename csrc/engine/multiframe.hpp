@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 #include <vector>
 
 #include "../kernels/sart_common.hpp"
@@ -42,6 +43,10 @@ class MultiFrameEngine {
     int64_t nvoxel() const { return V_; }
     int batch_frames() const { return nf_; }
     bool split_a() const { return x3_; }  // fp32 shard on the bf16 matrix cores
+    // the operand pieces of the split-A projections ("f16x2" range-safe f16 pairs, "bf16x2" / "bf16x3" bf16 pieces),
+    // "fp32" (fp32 MFMA) or "bf16-storage"
+    std::string forward_split() const;
+    std::string backproject_split() const;
     // 16, 32, 64 or 128: the smallest batch width that holds `frames` (128 for anything larger; the constructor
     // takes 64 where the path has no 128-column kernels)
     static int batch_width(int frames);
@@ -82,12 +87,16 @@ class MultiFrameEngine {
     DeviceArray<double> g64_, G64_, F2part_, x064_;
     DeviceArray<bf16_t> Xh_, Xl_, Wh_, Wl_;  // bf16 / split-A engine: hi / lo operand planes
     // split-A back-projection on f16 pairs (launch_mf_backproject_h16): planes w1 | w2 ([2][nf][Pp] f16 bits),
-    // per-frame max scratch and 1 / (a_scale s_f), and the shard's power-of-two scale
+    // per-frame max scratch and 1 / s_f, and the per-column power-of-two scales of the shard (csc_: [2][ld])
     bool h16_ = false;
-    float a_scale_ = 1.f;
     DeviceArray<bf16_t> W16_;
     DeviceArray<unsigned> wmax_;
-    DeviceArray<float> wscale_;
+    DeviceArray<float> wscale_, csc_;
+    // split-A forward on f16 pairs (launch_mf_forward_h16, default with split-A; SART_MF_FWD16=0: bf16 hi + lo
+    // pieces): X planes in Xh_ / Xl_ (f16 bits), per-row scales of the shard (rsc_: [2][Pp]), per-frame 1 / s_f
+    bool fwd16_ = false;
+    DeviceArray<float> rsc_, xinv_;
+    DeviceArray<unsigned> xmax_;
     DeviceArray<MfState> st_;
     DeviceArray<int64_t> lap_rp_;
     DeviceArray<int32_t> lap_col_;

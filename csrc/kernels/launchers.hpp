@@ -199,11 +199,26 @@ void launch_mf_split_w16(const float* W, int64_t nrows_pad, int nf, int64_t ldw,
                          unsigned* wmax, float a_scale, float* inv_scale, hipStream_t stream, bool have_max = false);
 // power-of-two scale 2^(14 - e) for max |A| = m 2^e over n floats (1 if A is zero); synchronises the stream
 float absmax_pow2_scale(const float* A, int64_t n, unsigned* scratch, hipStream_t stream);
-// split-A back-projection on f16 pairs (two pieces of A s_A and of W s_f, three v_mfma_f32_16x16x32_f16 products,
-// fp32 accumulation, the output scaled by inv_scale per frame): W1 / W2 from launch_mf_split_w16
+// split-A back-projection on f16 pairs (two pieces of A s_v and of W s_f, three v_mfma_f32_16x16x32_f16 products,
+// fp32 accumulation, the output scaled by 1 / s_v and inv_scale[f] = 1 / s_f): W1 / W2 from launch_mf_split_w16
+// (a_scale 1), csc from launch_mf_col_scales
 void launch_mf_backproject_h16(const float* A, int64_t ld, int64_t nrows, const uint16_t* W1, const uint16_t* W2,
                                int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0,
-                               int64_t v1, float a_scale, const float* inv_scale);
+                               int64_t v1, const float* csc, const float* inv_scale);
+// Range-safe f16 scales (multiframe_glue.hip): powers of two per row (rsc: [nrows_pad] scales then their inverses)
+// and per column (csc: [ld] then [ld]; scratch: ld words) of an fp32 shard
+void launch_mf_row_scales(const float* A, int64_t ld, int64_t nrows_pad, float* rsc, hipStream_t stream);
+void launch_mf_col_scales(const float* A, int64_t ld, int64_t nrows_pad, unsigned* scratch, float* csc,
+                          hipStream_t stream);
+// X [nf][ld] -> f16 pieces of X s_f (per-frame power-of-two scale from max |X[f]|; xmax: nf words of scratch,
+// xinv[f] = 1 / s_f), in the layout of launch_mf_split_x (perm; blocked = the ld > 0 layout)
+void launch_mf_split_x16(const float* X, int64_t ld, int nf, uint16_t* x1, uint16_t* x2, unsigned* xmax, float* xinv,
+                         hipStream_t stream, bool perm, bool blocked);
+// split-A forward on f16 pairs: A s_p (rsc, per row) times X s_f (launch_mf_split_x16), three f16 products, the
+// output scaled by 1 / (s_p s_f)
+void launch_mf_forward_h16(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const uint16_t* X1,
+                           const uint16_t* X2, float* Fout, int nsplit, int nf, hipStream_t stream, bool xblk,
+                           const float* rsc, const float* xinv);
 // three: hi [nf][ldw] then mid [nf][ldw] in `hi` (2 nf ldw elements), lo: the split-A back-projection's planes
 void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, bf16_t* hi, bf16_t* lo,
                        hipStream_t stream, bool three = false);

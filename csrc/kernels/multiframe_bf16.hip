@@ -93,6 +93,28 @@ __device__ __forceinline__ void split_a8(const u32x8 v, u32x4& hi, u32x4& lo) {
     lo = u32x4{l0, l1, l2, l3};
 }
 
+typedef _Float16 halfx8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 halfx2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ floatx4 mfma_h16(const u32x4 a, const u32x4 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8_t, a), __builtin_bit_cast(halfx8_t, b),
+                                                  c, 0, 0, 0);
+}
+__device__ __forceinline__ void split_h2(unsigned x, unsigned y, float s, unsigned& p1, unsigned& p2) {
+    const float a = __uint_as_float(x) * s, b = __uint_as_float(y) * s;
+    const halfx2_t h = {(_Float16)a, (_Float16)b};
+    p1 = __builtin_bit_cast(unsigned, h);
+    const halfx2_t l = {(_Float16)(a - (float)h.x), (_Float16)(b - (float)h.y)};
+    p2 = __builtin_bit_cast(unsigned, l);
+}
+// Forward fragment of an f16-pair split-A wave: eight consecutive fp32 of one row, scaled by the row's s_p
+__device__ __forceinline__ void split_h8(const u32x8 v, float s, u32x4& p1, u32x4& p2) {
+    unsigned a[4], b[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) split_h2(v[2 * q], v[2 * q + 1], s, a[q], b[q]);
+    p1 = u32x4{a[0], a[1], a[2], a[3]};
+    p2 = u32x4{b[0], b[1], b[2], b[3]};
+}
+
 // Three pieces, exact: hi + mid + lo = a (the back-projection, whose signed weights cancel in the sum). Truncation
 // splits: hi = the top 16 bits of a, r = a - hi is exact (same sign and exponent, <= 16 significant bits), mid = the
 // top 16 bits of r, lo = r - mid exact with <= 8 significant bits, i.e. a bf16 value. Per pair of elements: 4 v_and,
@@ -153,6 +175,10 @@ __device__ __forceinline__ uint4 phase_frag(const uint2 (&v)[8]) {
 // 32 voxels) is one contiguous 2 nf * 32 bytes per plane instead of nf 64-byte pieces ld * 2 bytes apart.
 struct FwdCols {
     int64_t cps, xfs, xbs;
+    // f16-pair split-A forward (H16): per-row scales of A ([nrows_pad] scales, then their inverses) and the
+    // per-frame inverse scales of the X pieces (launch_mf_split_x16)
+    const float* rsc = nullptr;
+    const float* xinv = nullptr;
 };
 
 // Split-K over columns: blockIdx.y selects [c0, c1) (multiples of 64); Fout + blockIdx.y * nrows_pad * nf.
@@ -273,7 +299,11 @@ constexpr int mf_fwd_min_waves() { return std::is_same<AT, float>::value ? 1 : (
 // ABL: diagnostic ablations as in k_mf_backproject_b16_lds (bit 0 no MFMAs, bit 1 no split of A, bit 2 no X staging
 // and no barrier); 0 in every production launch.
 // EX (early X): X of step u is loaded at step u - DEPTH - 1, ahead of A's batch (see EW of k_mf_backproject_b16_lds).
-template <int NG, int DEPTH, int RT, int KB, typename AT = bf16_t, bool AS = false, int ABL = 0, bool EX = false>
+// H16 (split-A only): A enters as two f16 pieces of A s_p (s_p per row, FwdCols::rsc) and X as two f16 pieces of
+// X s_f (launch_mf_split_x16), three v_mfma_f32_16x16x32_f16 products (a2 x1, a1 x2, a1 x1), the epilogue multiplies
+// by 1 / (s_p s_f): 2^-22 per product instead of the 2^-17 of the bf16 hi + lo pieces, at the same cost.
+template <int NG, int DEPTH, int RT, int KB, typename AT = bf16_t, bool AS = false, int ABL = 0, bool EX = false,
+          bool H16 = false>
 __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forward_b16_lds(const AT* __restrict__ A, int64_t ld, int64_t nrows,
                                                             int64_t nrows_pad, const bf16_t* __restrict__ Xh,
                                                             const bf16_t* __restrict__ Xl, float* __restrict__ Fout,
@@ -313,6 +343,10 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
     static_assert(!AS || R16 >= 8, "A staging needs full 128-B row segments");
     __shared__ __attribute__((aligned(16))) u32x4 s_a[AS ? 4 : 1][AS ? 16 * RT * R16 : 1];
     const AT* __restrict__ asp = A + (row0 + lane / R16) * ld + c0 + (lane % R16) * (16 / (int)sizeof(AT));
+    static_assert(!H16 || (A32 && ABL == 0), "the f16-pair forward is a split-A kernel");
+    float rs[RT];  // H16: this lane's row scales (row row0 + 16 rt + r of each row tile)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) rs[rt] = H16 ? fc.rsc[row0 + rt * 16 + r] : 1.f;
 
     floatx4 acc[RT][NG];
 #pragma unroll
@@ -436,12 +470,18 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
                         if constexpr (AS && (ABL & 2)) {
                             ah[rt] = frag16(rt, kb * 8 + g);
                             al[rt] = frag16(rt, kb * 8 + 4 + g);
-                        } else if constexpr (AS)
-                            split_a8(__builtin_shufflevector(frag16(rt, kb * 8 + g), frag16(rt, kb * 8 + 4 + g), 0, 1,
-                                                             2, 3, 4, 5, 6, 7),
-                                     ah[rt], al[rt]);
-                        else
-                            split_a8(a[sl][rt][kb], ah[rt], al[rt]);
+                        } else {
+                            u32x8 v;
+                            if constexpr (AS)
+                                v = __builtin_shufflevector(frag16(rt, kb * 8 + g), frag16(rt, kb * 8 + 4 + g), 0, 1, 2,
+                                                            3, 4, 5, 6, 7);
+                            else
+                                v = a[sl][rt][kb];
+                            if constexpr (H16)
+                                split_h8(v, rs[rt], ah[rt], al[rt]);
+                            else
+                                split_a8(v, ah[rt], al[rt]);
+                        }
                     }
                     u32x4 xh[NG], xl[NG];
 #pragma unroll
@@ -457,18 +497,22 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
                             for (int rt = 0; rt < RT; ++rt)
                                 acc[rt][j][0] += __uint_as_float((al[rt][0] ^ ah[rt][3] ^ xh[j][1] ^ xl[j][2]) & 0x3fffffu);
                     } else {
+                    auto mm = [](const u32x4 p, const u32x4 q, floatx4 c) {
+                        if constexpr (H16) return mfma_h16(p, q, c);
+                        else return mfma_b16(p, q, c);
+                    };
 #pragma unroll
                     for (int j = 0; j < NG; ++j)
 #pragma unroll
-                        for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(al[rt], xh[j], acc[rt][j]);
+                        for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mm(al[rt], xh[j], acc[rt][j]);
 #pragma unroll
                     for (int j = 0; j < NG; ++j)
 #pragma unroll
-                        for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(ah[rt], xl[j], acc[rt][j]);
+                        for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mm(ah[rt], xl[j], acc[rt][j]);
 #pragma unroll
                     for (int j = 0; j < NG; ++j)
 #pragma unroll
-                        for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mfma_b16(ah[rt], xh[j], acc[rt][j]);
+                        for (int rt = 0; rt < RT; ++rt) acc[rt][j] = mm(ah[rt], xh[j], acc[rt][j]);
                     }
                 } else if constexpr (AS) {
                     u32x4 af[RT];
@@ -508,6 +552,20 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
         }
     }
     if (!live) return;
+    if constexpr (H16) {  // 1 / (s_p s_f), exact (powers of two)
+#pragma unroll
+        for (int j = 0; j < NG; ++j) {
+            const float xi = fc.xinv[16 * j + r];
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int64_t ra = row0 + rt * 16 + g * 4 + i;
+                    if (ra < nrows) Fout[ra * NF + 16 * j + r] = acc[rt][j][i] * fc.rsc[nrows_pad + ra] * xi;
+                }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < NG; ++j)
 #pragma unroll
@@ -828,27 +886,15 @@ __global__ __launch_bounds__(256, (NG == 4 ? mf_bwd_min_waves<AT, VT>() : (std::
 // ---------------------------------------------------------------------------------------------- launchers
 
 // ----------------------------------------------------------------------------------------------------------------
-// Split-A back-projection on f16 pairs (SART_MF_BWD16, default for fp32 shards at 32 / 64 frames). fp16 has 11
-// significant bits, so two rne pieces hold a scaled fp32 value to 2^-24 (|a s - a1 - a2| <= 2^-12 |a s - a1| <=
-// 2^-24 |a s|), i.e. at fp32 rounding, where bf16 (8 bits) needs three. Two pieces of A s_A and of W s_f make
-// three products (a2 w1, a1 w2, a1 w1: the dropped a2 w2 is 2^-24 of a term) instead of the six of the bf16 split,
-// and the split is 3 VALU operations per element (scale, convert, residual) instead of 5.5. The scales are powers
-// of two (s_A from max |A| once per shard, absmax_pow2_scale; s_f per frame and sweep, launch_mf_split_w16) that
-// keep every scaled value below 2^14 and values down to 2^-16 of the maximum normal in both pieces; the epilogue
-// multiplies by inv_scale[f] = 1 / (s_A s_f), exactly. Layout and staging as k_mf_backproject_b16_lds (VT = 1).
-typedef _Float16 halfx8_t __attribute__((ext_vector_type(8)));
-typedef _Float16 halfx2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ floatx4 mfma_h16(const u32x4 a, const u32x4 b, floatx4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8_t, a), __builtin_bit_cast(halfx8_t, b),
-                                                  c, 0, 0, 0);
-}
-__device__ __forceinline__ void split_h2(unsigned x, unsigned y, float s, unsigned& p1, unsigned& p2) {
-    const float a = __uint_as_float(x) * s, b = __uint_as_float(y) * s;
-    const halfx2_t h = {(_Float16)a, (_Float16)b};
-    p1 = __builtin_bit_cast(unsigned, h);
-    const halfx2_t l = {(_Float16)(a - (float)h.x), (_Float16)(b - (float)h.y)};
-    p2 = __builtin_bit_cast(unsigned, l);
-}
+// Split-A back-projection on f16 pairs (SART_MF_BWD16, default for fp32 shards at 32 / 64 / 128 frames). fp16 has
+// 11 significant bits, so two rne pieces hold a scaled fp32 value to ~2^-22 (|a s - a1| <= 2^-11 |a s|, |a s - a1 -
+// a2| <= 2^-11 |a s - a1|), where bf16 (8 bits) needs three pieces for the same. Two pieces of A s_v and of W s_f
+// make three products (a2 w1, a1 w2, a1 w1; the dropped a2 w2 is ~2^-22 of a term) instead of the six of the bf16
+// split, and the split is 3 VALU operations per element (scale, convert, residual) instead of 5.5. Not fp32-exact:
+// ~2^-22 per product against fp32's 2^-24. The scales are powers of two: s_v per voxel COLUMN (max_p |A[p][v]|,
+// launch_mf_col_scales: a column's entries within 2^-16 of its own maximum keep both pieces normal, whatever the
+// range across columns; multiframe_glue.hip) and s_f per frame and sweep (launch_mf_split_w16); the epilogue
+// multiplies by inv_scale[f] = 1 / s_f and 1 / s_v, exactly. Layout and staging as k_mf_backproject_b16_lds (VT = 1).
 template <int P>
 __device__ __forceinline__ void split_phase_h(const u32x4 (&v)[8], float s, u32x4& h1, u32x4& h2) {
     unsigned a[4], b[4];
@@ -864,7 +910,8 @@ __global__ __launch_bounds__(256, MW) void k_mf_backproject_h16(const float* __r
                                                                const uint16_t* __restrict__ W1,
                                                                const uint16_t* __restrict__ W2, int64_t ldw,
                                                                int64_t rows_per_split, float* __restrict__ partial,
-                                                               int64_t vb0, int64_t vend, float a_scale,
+                                                               int64_t vb0, int64_t vend,
+                                                               const float* __restrict__ csc,
                                                                const float* __restrict__ inv_scale,
                                                                const int* __restrict__ skip) {
     if (skip && *skip) return;
@@ -883,6 +930,7 @@ __global__ __launch_bounds__(256, MW) void k_mf_backproject_h16(const float* __r
     if (r_end > nrows32) r_end = nrows32;
     const float* __restrict__ ap = A + (r_begin + 8 * g) * ld + vb * 64 + 4 * i16;
     const int64_t wo = (int64_t)i16 * ldw + r_begin + 8 * g;
+    const float4 cs4 = *reinterpret_cast<const float4*>(csc + vb * 64 + 4 * i16);  // scales of voxel phases 0..3
     floatx4 acc[4][NG];
 #pragma unroll
     for (int p = 0; p < 4; ++p)
@@ -931,10 +979,10 @@ __global__ __launch_bounds__(256, MW) void k_mf_backproject_h16(const float* __r
             if (t >= nst) return;  // uniform for the workgroup
             const u32x4* ws = s_w[t & 1][0] + lane;
             u32x4 h1[4], h2[4];
-            split_phase_h<0>(av[sl], a_scale, h1[0], h2[0]);
-            split_phase_h<1>(av[sl], a_scale, h1[1], h2[1]);
-            split_phase_h<2>(av[sl], a_scale, h1[2], h2[2]);
-            split_phase_h<3>(av[sl], a_scale, h1[3], h2[3]);
+            split_phase_h<0>(av[sl], cs4.x, h1[0], h2[0]);
+            split_phase_h<1>(av[sl], cs4.y, h1[1], h2[1]);
+            split_phase_h<2>(av[sl], cs4.z, h1[2], h2[2]);
+            split_phase_h<3>(av[sl], cs4.w, h1[3], h2[3]);
             u32x4 wv[2][NG];
 #pragma unroll
             for (int j = 0; j < NG; ++j) wv[0][j] = ws[j * 64], wv[1][j] = ws[(NG + j) * 64];
@@ -967,8 +1015,9 @@ __global__ __launch_bounds__(256, MW) void k_mf_backproject_h16(const float* __r
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t v = vb * 64 + 4 * (g * 4 + q) + p;
+            const float iv = csc[ld + v];
 #pragma unroll
-            for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[p][j][q] * isc[j];
+            for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[p][j][q] * isc[j] * iv;
         }
 }
 
@@ -1208,6 +1257,44 @@ void launch_mf_forward_x3(const float* A, int64_t ld, int64_t nrows, int64_t nro
     launch_mf_forward_split(A, ld, nrows, nrows_pad, Xh, Xl, Fout, nsplit, nf, stream, xblk);
 }
 
+// The f16-pair split-A forward (H16; default for fp32 shards at 32 / 64 / 128 frames): the x3 tilings with RT = 2 and
+// a ring two steps deep, X loaded early; planes from launch_mf_split_x16 with perm (and blocked when xblk).
+template <int NG>
+static void fwd_h16_ng(const FwdTile& tl, dim3 grid, hipStream_t stream, const float* A, int64_t ld, int64_t nrows,
+                       int64_t nrows_pad, const bf16_t* X1, const bf16_t* X2, float* Fout, FwdCols cps) {
+    auto run = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X1, X2, Fout, cps, g_mf_skip);
+    };
+    if (tl.kb == 2 && tl.as) run(k_mf_forward_b16_lds<NG, 2, 2, 2, float, true, 0, true, true>);
+    else if (tl.kb == 2) run(k_mf_forward_b16_lds<NG, 2, 2, 2, float, false, 0, true, true>);
+    else if (tl.as) run(k_mf_forward_b16_lds<NG, 2, 2, 1, float, true, 0, true, true>);
+    else run(k_mf_forward_b16_lds<NG, 2, 2, 1, float, false, 0, true, true>);
+}
+
+void launch_mf_forward_h16(const float* A, int64_t ld, int64_t nrows, int64_t nrows_pad, const uint16_t* X1,
+                           const uint16_t* X2, float* Fout, int nsplit, int nf, hipStream_t stream, bool xblk,
+                           const float* rsc, const float* xinv) {
+    const char* what = "mf_forward_h16";
+    if (ld % 64 != 0) throw std::runtime_error(std::string(what) + ": ld must be a multiple of 64");
+    if (nsplit < 1) throw std::runtime_error(std::string(what) + ": nsplit must be >= 1");
+    check_nf_b16(nf, what, true);
+    if (nrows_pad % 64 != 0) throw std::runtime_error(std::string(what) + ": padded rows must be a multiple of 64");
+    if (!rsc || !xinv) throw std::runtime_error(std::string(what) + ": row scales and frame scales required");
+    FwdTile tl = mf_x3_fwd_tile(nf, ld);
+    if (nf == 128) tl.as = true;
+    FwdCols cps{((ld + nsplit - 1) / nsplit + 63) / 64 * 64, xblk ? 32 : ld, xblk ? 32 * (int64_t)nf : 32};
+    cps.rsc = rsc;
+    cps.xinv = xinv;
+    const dim3 grid((unsigned)((nrows_pad + 127) / 128), (unsigned)nsplit);  // 4 waves x 32 rows per workgroup
+    const bf16_t* x1 = reinterpret_cast<const bf16_t*>(X1);
+    const bf16_t* x2 = reinterpret_cast<const bf16_t*>(X2);
+    if (nf == 16) fwd_h16_ng<1>(tl, grid, stream, A, ld, nrows, nrows_pad, x1, x2, Fout, cps);
+    else if (nf == 32) fwd_h16_ng<2>(tl, grid, stream, A, ld, nrows, nrows_pad, x1, x2, Fout, cps);
+    else if (nf == 64) fwd_h16_ng<4>(tl, grid, stream, A, ld, nrows, nrows_pad, x1, x2, Fout, cps);
+    else fwd_h16_ng<8>(tl, grid, stream, A, ld, nrows, nrows_pad, x1, x2, Fout, cps);
+    check_launch("k_mf_forward_h16");
+}
+
 // Split-K of the bf16 / split-A back-projection: ~1024 workgroups (4 waves x 64 VT voxels each), >= 64 rows per
 // split.
 int mf_backproject_b16_num_splits(int64_t ld, int64_t nrows, bool a32) {
@@ -1344,8 +1431,9 @@ void launch_mf_backproject_b16(const bf16_t* A, int64_t ld, int64_t nrows, const
 
 void launch_mf_backproject_h16(const float* A, int64_t ld, int64_t nrows, const uint16_t* W1, const uint16_t* W2,
                                int64_t ldw, int nsplit, float* partial, int nf, hipStream_t stream, int64_t v0,
-                               int64_t v1, float a_scale, const float* inv_scale) {
+                               int64_t v1, const float* csc, const float* inv_scale) {
     const std::string what = "mf_backproject_h16";
+    if (!csc || !inv_scale) throw std::runtime_error(what + ": column scales and frame scales required");
     if (ld % 64 != 0) throw std::runtime_error(what + ": ld must be a multiple of 64");
     check_nf_b16(nf, what.c_str(), true);
     const int64_t nrows32 = (nrows + 31) / 32 * 32;
@@ -1366,7 +1454,7 @@ void launch_mf_backproject_h16(const float* A, int64_t ld, int64_t nrows, const 
         constexpr int NG = decltype(ng)::value;
         auto run = [&](auto k) {
             hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, A, ld, nrows32, W1, W2, ldw, rps, partial, vw0, v1,
-                               a_scale, inv_scale, g_mf_skip);
+                               csc, inv_scale, g_mf_skip);
         };
         if (w1 && ew && d == 3) run(k_mf_backproject_h16<NG, 3, true, 1>);
         else if (w1 && d == 3) run(k_mf_backproject_h16<NG, 3, false, 1>);
@@ -1385,7 +1473,7 @@ void launch_mf_backproject_h16(const float* A, int64_t ld, int64_t nrows, const 
     else {  // 128 frames: 8 column groups, one wave per SIMD (128 accumulator registers)
         auto run = [&](auto kern) {
             hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, A, ld, nrows32, W1, W2, ldw, rps, partial, vw0, v1,
-                               a_scale, inv_scale, g_mf_skip);
+                               csc, inv_scale, g_mf_skip);
         };
         if (ew && d == 3) run(k_mf_backproject_h16<8, 3, true, 1>);
         else if (ew) run(k_mf_backproject_h16<8, 2, true, 1>);

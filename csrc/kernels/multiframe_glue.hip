@@ -574,6 +574,12 @@ __device__ __forceinline__ int mf_w16_exp(unsigned mbits) {  // e with max |w| =
     (void)frexpf(__uint_as_float(mbits), &e);
     return e;
 }
+// The f16 scale exponent 14 - e of a maximum m 2^e, clamped so that the scale and its inverse are both normal
+// floats (a maximum below 2^-106 would otherwise give an infinite scale, and w * inf non-finite pieces)
+__device__ __host__ __forceinline__ int mf_f16_shift(int e) {
+    const int s = 14 - e;
+    return s > 120 ? 120 : (s < -120 ? -120 : s);
+}
 
 template <int TN>
 __global__ __launch_bounds__(256) void k_mf_split_w16(const float* __restrict__ W, int64_t nrows_pad, int nf,
@@ -584,9 +590,9 @@ __global__ __launch_bounds__(256) void k_mf_split_w16(const float* __restrict__ 
     __shared__ float tile[64][TN + 1];
     __shared__ float sc[TN];
     for (int f = threadIdx.x; f < nf; f += 256) {
-        const int e = mf_w16_exp(wmax[f]);
-        sc[f] = ldexpf(1.f, 14 - e);
-        if (blockIdx.x == 0) inv_scale[f] = ldexpf(1.f / a_scale, e - 14);
+        const int s = mf_f16_shift(mf_w16_exp(wmax[f]));
+        sc[f] = ldexpf(1.f, s);
+        if (blockIdx.x == 0) inv_scale[f] = ldexpf(1.f / a_scale, -s);
     }
     const int64_t r0 = (int64_t)blockIdx.x * 64;
     for (int i = threadIdx.x; i < 64 * nf; i += 256) {
@@ -632,6 +638,161 @@ __global__ __launch_bounds__(256) void k_absmax_f32(const float* __restrict__ A,
     if (threadIdx.x == 0 && red[0]) atomicMax(out, red[0]);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Range-safe f16-pair operands of the split-A projections (multiframe_bf16.hip). An f16 piece has a 5-bit exponent,
+// so one scale for a whole shard keeps only entries within ~2^16 of the shard's max |A| at full precision; a
+// ray-transfer matrix with reflections spans 1e8 .. 1e20 (tests/test_gpu_realistic.py). Each kernel therefore
+// scales A where its sums run: the forward F[p][f] = sum_v A[p][v] X[f][v] per ROW (s_p from max_v |A[p][v]|), the
+// back-projection D[v][f] = sum_p A[p][v] W[p][f] per COLUMN (s_v from max_p |A[p][v]|), and the fp32 operand per
+// frame (X by max_v |X[f][v]|, W by max_p |W[p][f]|). Every scale is a power of two 2^mf_f16_shift(e) (scaled maxima
+// in [2^13, 2^14)); the inverse is applied to each output in the epilogue, exactly. What is left is an absolute
+// floor of ~2^-39 of the row / column / frame maximum per element (subnormal f16), against fp32's 2^-24 relative.
+// Scale arrays hold the scale at [i] and its inverse at [n + i].
+
+// max_v |A[p][v]| of every row (one wave per row, 4 rows per block) -> rsc[p] = 2^s, rsc[nrows_pad + p] = 2^-s
+__global__ __launch_bounds__(256) void k_mf_row_scales(const float* __restrict__ A, int64_t ld, int64_t nrows_pad,
+                                                       float* __restrict__ rsc) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= nrows_pad) return;
+    const float4* a = reinterpret_cast<const float4*>(A + row * ld);
+    unsigned m = 0u;
+    for (int64_t i = lane; i < ld / 4; i += 64) {
+        const float4 v = a[i];
+        const float xs[4] = {fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (xs[k] <= 3.0e38f) m = max(m, __float_as_uint(xs[k]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+    if (lane == 0) {
+        const int s = m ? mf_f16_shift(mf_w16_exp(m)) : 0;
+        rsc[row] = ldexpf(1.f, s);
+        rsc[nrows_pad + row] = ldexpf(1.f, -s);
+    }
+}
+
+// max_p |A[p][v]| over a range of rows per block (4 columns per thread, 1024 per block), combined by an unsigned
+// atomic max of the bit patterns (order-free)
+__global__ __launch_bounds__(256) void k_mf_col_max(const float* __restrict__ A, int64_t ld, int64_t nrows_pad,
+                                                    int64_t rows_per_block, unsigned* __restrict__ cmax) {
+    const int64_t c4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c4 * 4 >= ld) return;
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+    const int64_t r1 = r0 + rows_per_block < nrows_pad ? r0 + rows_per_block : nrows_pad;
+    unsigned m[4] = {0u, 0u, 0u, 0u};
+    for (int64_t r = r0; r < r1; ++r) {
+        const float4 v = reinterpret_cast<const float4*>(A + r * ld)[c4];
+        const float xs[4] = {fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (xs[k] <= 3.0e38f) m[k] = max(m[k], __float_as_uint(xs[k]));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (m[k]) atomicMax(&cmax[c4 * 4 + k], m[k]);
+}
+
+__global__ __launch_bounds__(256) void k_mf_col_scales(const unsigned* __restrict__ cmax, int64_t ld,
+                                                       float* __restrict__ csc) {
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v >= ld) return;
+    const int s = cmax[v] ? mf_f16_shift(mf_w16_exp(cmax[v])) : 0;
+    csc[v] = ldexpf(1.f, s);
+    csc[ld + v] = ldexpf(1.f, -s);
+}
+
+// per-frame max |X[f][v]| of frame-major X [nf][ld] (finite values only)
+__global__ __launch_bounds__(256) void k_mf_xmax(const float* __restrict__ X, int64_t ld, unsigned* __restrict__ xmax,
+                                                 const int* __restrict__ skip) {
+    if (skip && *skip) return;
+    __shared__ unsigned red[256];
+    const int f = blockIdx.y;
+    const float4* x = reinterpret_cast<const float4*>(X + (int64_t)f * ld);
+    unsigned m = 0u;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < ld / 4; i += (int64_t)gridDim.x * 256) {
+        const float4 v = x[i];
+        const float xs[4] = {fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (xs[k] <= 3.0e38f) m = max(m, __float_as_uint(xs[k]));
+    }
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + o]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && red[0]) atomicMax(&xmax[f], red[0]);
+}
+
+// X [nf][ld] fp32 -> f16 pieces x s_f = x1 + x2 (+ |e| <= 2^-22 |x s_f|, both rne) in the layout of k_mf_split_x
+// (perm: the split-A forward's k order; blocked: [ld / 32][nf][32]); xinv[f] = 1 / s_f
+__global__ __launch_bounds__(256) void k_mf_split_x16(const float* __restrict__ X, int64_t ld, int nf,
+                                                      uint16_t* __restrict__ x1, uint16_t* __restrict__ x2,
+                                                      const unsigned* __restrict__ xmax, float* __restrict__ xinv,
+                                                      const int* __restrict__ skip, int perm, int blocked) {
+    if (skip && *skip) return;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < nf && blockIdx.x == 0) {
+        const int f = (int)i;
+        xinv[f] = ldexpf(1.f, xmax[f] ? -mf_f16_shift(mf_w16_exp(xmax[f])) : 0);
+    }
+    if (i >= (int64_t)nf * ld / 4) return;
+    const int64_t f = (4 * i) / ld, c = (4 * i) % ld;
+    const float sc = ldexpf(1.f, xmax[f] ? mf_f16_shift(mf_w16_exp(xmax[f])) : 0);
+    const float4 v = reinterpret_cast<const float4*>(X)[i];
+    const float xs[4] = {v.x * sc, v.y * sc, v.z * sc, v.w * sc};
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const _Float16 a = (_Float16)xs[k];
+        h[k] = __builtin_bit_cast(uint16_t, a);
+        l[k] = __builtin_bit_cast(uint16_t, (_Float16)(xs[k] - (float)a));
+    }
+    int64_t o = i;
+    if (blocked) o = ((c >> 5) * nf + f) * 8 + ((c & 31) >> 2);
+    if (perm) o = (o & ~(int64_t)7) | ((o & 3) << 1) | ((o >> 2) & 1);
+    reinterpret_cast<uint2*>(x1)[o] = make_uint2(h[0] | (unsigned)h[1] << 16, h[2] | (unsigned)h[3] << 16);
+    reinterpret_cast<uint2*>(x2)[o] = make_uint2(l[0] | (unsigned)l[1] << 16, l[2] | (unsigned)l[3] << 16);
+}
+
+void launch_mf_row_scales(const float* A, int64_t ld, int64_t nrows_pad, float* rsc, hipStream_t stream) {
+    if (ld % 4 != 0) throw std::runtime_error("mf_row_scales: ld must be a multiple of 4");
+    if (nrows_pad <= 0) return;
+    hipLaunchKernelGGL(k_mf_row_scales, dim3((unsigned)((nrows_pad + 3) / 4)), dim3(256), 0, stream, A, ld, nrows_pad,
+                       rsc);
+    check_launch("k_mf_row_scales");
+}
+
+void launch_mf_col_scales(const float* A, int64_t ld, int64_t nrows_pad, unsigned* scratch, float* csc,
+                          hipStream_t stream) {
+    if (ld % 4 != 0) throw std::runtime_error("mf_col_scales: ld must be a multiple of 4");
+    hip_call(hipMemsetAsync(scratch, 0, ld * sizeof(unsigned), stream), "hipMemsetAsync");
+    const int64_t rpb = 256;
+    if (nrows_pad > 0) {
+        const dim3 grid((unsigned)((ld / 4 + 255) / 256), (unsigned)((nrows_pad + rpb - 1) / rpb));
+        hipLaunchKernelGGL(k_mf_col_max, grid, dim3(256), 0, stream, A, ld, nrows_pad, rpb, scratch);
+        check_launch("k_mf_col_max");
+    }
+    hipLaunchKernelGGL(k_mf_col_scales, dim3(nb(ld)), dim3(256), 0, stream, scratch, ld, csc);
+    check_launch("k_mf_col_scales");
+}
+
+void launch_mf_split_x16(const float* X, int64_t ld, int nf, uint16_t* x1, uint16_t* x2, unsigned* xmax, float* xinv,
+                         hipStream_t stream, bool perm, bool blocked) {
+    check_nf(nf, "mf_split_x16");
+    if (ld % 32 != 0) throw std::runtime_error("mf_split_x16: ld must be a multiple of 32");
+    hip_call(hipMemsetAsync(xmax, 0, nf * sizeof(unsigned), stream), "hipMemsetAsync");
+    const unsigned bx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(16, (ld / 4 + 1023) / 1024));
+    hipLaunchKernelGGL(k_mf_xmax, dim3(bx, (unsigned)nf), dim3(256), 0, stream, X, ld, xmax, g_mf_skip);
+    check_launch("k_mf_xmax");
+    hipLaunchKernelGGL(k_mf_split_x16, dim3(std::max<unsigned>(1, nb((int64_t)nf * ld / 4))), dim3(256), 0, stream, X,
+                       ld, nf, x1, x2, xmax, xinv, g_mf_skip, (int)perm, (int)blocked);
+    check_launch("k_mf_split_x16");
+}
+
 void launch_mf_split_w16(const float* W, int64_t nrows_pad, int nf, int64_t ldw, uint16_t* w1, uint16_t* w2,
                          unsigned* wmax, float a_scale, float* inv_scale, hipStream_t stream, bool have_max) {
     check_nf(nf, "mf_split_w16");
@@ -659,7 +820,7 @@ float absmax_pow2_scale(const float* A, int64_t n, unsigned* scratch, hipStream_
     if (bits == 0u) return 1.f;
     int e;
     (void)frexpf(__builtin_bit_cast(float, bits), &e);
-    return ldexpf(1.f, 14 - e);  // scaled max in [2^13, 2^14)
+    return ldexpf(1.f, mf_f16_shift(e));  // scaled max in [2^13, 2^14)
 }
 
 void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, bf16_t* hi, bf16_t* lo,

@@ -23,6 +23,7 @@ from __future__ import annotations
 import os
 import signal
 import subprocess
+import threading
 import sys
 from pathlib import Path
 
@@ -56,14 +57,24 @@ def main(argv=None) -> int:
         except ProcessLookupError:
             pass
 
-    previous = {s: signal.signal(s, forward) for s in FORWARDED}
+    # signal handlers can only be installed from the main thread: elsewhere (main() called from a worker thread)
+    # the driver is simply waited for; any failure while setting up kills and reaps the child instead of leaving it
+    previous = {}
     try:
+        if threading.current_thread() is threading.main_thread():
+            for s in FORWARDED:
+                previous[s] = signal.signal(s, forward)
         while True:
             try:
                 rc = proc.wait()
                 break
             except InterruptedError:  # pragma: no cover - PEP 475 retries wait() itself
                 continue
+    except BaseException:
+        if proc.poll() is None:
+            proc.kill()
+        proc.wait()
+        raise
     finally:
         for s, h in previous.items():
             signal.signal(s, h)

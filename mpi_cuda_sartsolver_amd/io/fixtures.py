@@ -4,6 +4,10 @@
 or sparse COO), a frame mask, a voxel map, an image time series generated from a known phantom with
 ``g = A x_true`` (optionally with saturated pixels), and optionally a Laplacian file. The returned
 dictionary holds the global dense matrix and phantoms so tests can compare the solver output.
+
+``raytraced=True`` takes the matrix from the ray-traced camera model with wall reflections
+(utils/raytrace.py: Siddon path lengths, 1/r^2, specular bounces and a diffuse wall term; >= 90 % zeros in
+the direct part, values over > 1e8) on every voxel of ``grid``, and a slowly varying ring phantom per frame.
 """
 from __future__ import annotations
 
@@ -39,23 +43,40 @@ def _grid_voxels(nx, ny, nz, nvoxel, rng):
 def make_case(directory: str, cameras=("cam_a", "cam_b"), shapes=((6, 8), (5, 7)), nvoxel=48, grid=(4, 4, 4),
               segments=2, sparse_cameras=(), nframes=4, dt=0.1, time_offsets=None, saturate=0.0,
               laplacian=False, wavelength=656.3, rtm_name="with_reflections", seed=0, coordinate_system="",
-              bounds=()) -> Case:
+              bounds=(), raytraced=False, mask_fraction=0.2) -> Case:
     os.makedirs(directory, exist_ok=True)
     n = native()
     rng = np.random.default_rng(seed)
     nx, ny, nz = grid
-    vi, vj, vk = _grid_voxels(nx, ny, nz, nvoxel, rng)
+    traced = None
+    if raytraced:
+        from ..utils.raytrace import Camera, default_cameras, phantom, raytraced_rtm
+
+        nvoxel = nx * ny * nz
+        flat = np.arange(nvoxel)
+        vi, vj, vk = flat // (ny * nz), (flat // nz) % ny, flat % nz
+        base = default_cameras(n=4)
+        cams = [Camera(cam, b.position, b.look_at, tuple(sh), b.field_of_view, b.up)
+                for cam, sh, b in zip(cameras, shapes, base)]
+        A_all, info = raytraced_rtm(grid=grid, cameras=cams, seed=seed)
+        traced = {cam: A_all[r0:r1] for cam, (r0, r1) in info["rows"].items()}
+        phantoms = np.stack([phantom(grid, t=float(k), seed=seed) for k in range(nframes)])
+    else:
+        vi, vj, vk = _grid_voxels(nx, ny, nz, nvoxel, rng)
+        phantoms = rng.random((nframes, nvoxel)) + 0.1
     seg_edges = np.linspace(0, nvoxel, segments + 1).astype(int)
     time_offsets = time_offsets or [0.0] * len(cameras)
-    phantoms = rng.random((nframes, nvoxel)) + 0.1
     blocks, files, rtm_files, image_files, masks = [], [], [], [], {}
     times, frames = {}, {}
     for c, (cam, (h, w)) in enumerate(zip(cameras, shapes)):
-        mask = (rng.random((h, w)) > 0.2).astype(np.uint8)
+        mask = (rng.random((h, w)) > mask_fraction).astype(np.uint8)
         mask[0, 0] = 1
         npix = int(mask.sum())
-        A_cam = rng.random((npix, nvoxel)).astype(np.float32)
-        A_cam[A_cam < 0.3] = 0.0  # some structural zeros
+        if traced is not None:
+            A_cam = np.ascontiguousarray(traced[cam][mask.ravel() > 0])
+        else:
+            A_cam = rng.random((npix, nvoxel)).astype(np.float32)
+            A_cam[A_cam < 0.3] = 0.0  # some structural zeros
         masks[cam] = mask
         for s in range(segments):
             v0, v1 = seg_edges[s], seg_edges[s + 1]
@@ -93,7 +114,8 @@ def make_case(directory: str, cameras=("cam_a", "cam_b"), shapes=((6, 8), (5, 7)
     if laplacian:
         from ..models.laplacian import LaplacianCSR
 
-        L = LaplacianCSR.grid_3d(1, 1, nvoxel)  # chain Laplacian over the voxel order
+        # chain Laplacian over the voxel order; the 3-D grid Laplacian for ray-traced cases (every voxel present)
+        L = LaplacianCSR.grid_3d(nx, ny, nz) if raytraced else LaplacianCSR.grid_3d(1, 1, nvoxel)
         rows = np.repeat(np.arange(nvoxel), np.diff(L.row_ptr_host))
         lap = os.path.join(directory, "laplacian.h5")
         n.write_laplacian_file(lap, nvoxel, rows.astype(np.uint64), L.col_host.astype(np.uint64), L.val_host)

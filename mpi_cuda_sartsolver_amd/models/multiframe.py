@@ -4,9 +4,9 @@ The reference solves the time series strictly frame by frame (reference main.cpp
 the RTM twice per iteration per frame. For throughput on long time series (BASELINE.json config 5),
 frames can be batched: the forward and back projections become skinny GEMMs ``A.X`` / ``A^T.W`` with
 16, 32, 64 or 128 right-hand sides (csrc/kernels/multiframe.hip, ``v_mfma_f32_16x16x4_f32`` on 1, 2 or 4
-column groups; from 32 frames on A is split into hi + lo bf16 (forward) / two scaled f16 pieces (back-projection)
-in registers for the 16-bit matrix cores, csrc/kernels/multiframe_bf16.hip, which also take 128 frames on 8
-column groups), reading A twice per iteration for the whole batch. Every frame keeps its own normalisation,
+column groups; from 32 frames on A is split in registers into two f16 pieces of A scaled per row (forward) / per
+column (back-projection) for the 16-bit matrix cores, csrc/kernels/multiframe_bf16.hip, which also take 128 frames
+on 8 column groups), reading A twice per iteration for the whole batch. Every frame keeps its own normalisation,
 saturation mask, convergence history, iteration count and status. The batch's columns are slots with
 continuous batching: as soon as a frame finishes, its slot takes the next frame between two sweeps, so no
 sweep is spent on finished frames while frames wait. Frames are cold-started (``--no_guess``), or started as a
@@ -32,7 +32,8 @@ from .rtm import DenseRTM
 from .sart import SolveResult, SolverParams, _host_f64
 
 NF = 16        # MFMA column group (frames per 16-wide N tile)
-MAX_BATCH = 128  # widest batch: 8 column groups (split-A fp32 shards; other paths take 64)
+MAX_BATCH = 128  # widest batch: 8 column groups (bf16 storage and split-A with f16 pairs; the fp32 MFMA and bf16
+                 # six-product back-projection paths take 64)
 
 
 class MultiFrameSARTSolver:
@@ -77,6 +78,11 @@ class MultiFrameSARTSolver:
         self.P, self.Pp, self.V, self.ld = rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld
         self.batch_width = int(self.engine.batch_frames)  # 16, 32, 64 or 128 columns on the matrix cores
         self.split_a = bool(self.engine.split_a)
+        # operand pieces of the projections: "f16x2" (split-A default: range-safe f16 pairs, per-row scales in the
+        # forward, per-column in the back-projection), "bf16x2" / "bf16x3" (SART_MF_FWD16=0 / SART_MF_BWD16=0),
+        # "fp32" (fp32 MFMA) or "bf16-storage"
+        self.forward_split = str(self.engine.forward_split)
+        self.backproject_split = str(self.engine.backproject_split)
 
     def solve_batch(self, measurements, x0=None, chain: bool = False) -> List[SolveResult]:
         """Frames [nframes, local pixels] through ``batch_width`` slots with continuous batching: a slot whose

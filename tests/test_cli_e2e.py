@@ -37,11 +37,12 @@ def _expected(case, oracle, warm=True, **kw):
     return np.array(xs), np.array(sts), its
 
 
-def chain_errors(case, out, *, log=False, warm=True, warm_from=None, beta_laplace=1e-3, A=None):
+def chain_errors(case, out, *, log=False, warm=True, warm_from=None, beta_laplace=1e-3, A=None, orders=("blas",)):
     """Every frame of a CLI output file against the fp64 oracle of the reference GPU semantics, run for the frame's
     own recorded number of SART updates (solution/iterations) and warm-started like the run (warm: from frame k - 1;
     warm_from: from the listed frame, -1 cold) from the oracle's own solutions; next to it the fp32 emulation of the
-    same chain (its inherent fp32 error). Returns (ours, fp32) relative errors per frame."""
+    same chain (its inherent fp32 error; the largest over the summation ``orders``, see sart_fp32_emulation).
+    Returns (ours, fp32) relative errors per frame."""
     from mpi_cuda_sartsolver_amd.models.reference import sart_fp32_emulation
 
     n = native()
@@ -51,16 +52,20 @@ def chain_errors(case, out, *, log=False, warm=True, warm_from=None, beta_laplac
     L = _laplacian(case)
     kw = dict(logarithmic=log, beta_laplace=beta_laplace)
     e_ours, e_32 = [], []
-    s64, s32 = {}, {}
+    s64, s32 = {}, {o: {} for o in orders}
     for k, g in enumerate(_frames(case)):
         src = (warm_from[k] if warm_from is not None else (k - 1 if warm else -1))
         x64, _, _ = sart_gpu_semantics(A, g, L, conv_tolerance=0.0, max_iterations=int(its[k]),
                                        x_prev=s64.get(src), **kw)
-        x32, _, _ = sart_fp32_emulation(A, g, L, max_iterations=int(its[k]), x_prev=s32.get(src), **kw)
         nrm = np.linalg.norm(x64)
         e_ours.append(np.linalg.norm(X[k] - x64) / nrm)
-        e_32.append(np.linalg.norm(x32 - x64) / nrm)
-        s64[k], s32[k] = x64, x32
+        e = 0.0
+        for o in orders:
+            x32, _, _ = sart_fp32_emulation(A, g, L, max_iterations=int(its[k]), x_prev=s32[o].get(src), order=o, **kw)
+            e = max(e, np.linalg.norm(x32 - x64) / nrm)
+            s32[o][k] = x32
+        e_32.append(e)
+        s64[k] = x64
     return np.array(e_ours), np.array(e_32)
 
 

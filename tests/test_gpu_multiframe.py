@@ -1,6 +1,9 @@
-"""Multi-frame MFMA solver vs the per-frame fp64 oracle of the GPU semantics."""
+"""Multi-frame MFMA solver vs the per-frame fp64 oracle of the GPU semantics: statuses and iteration counts of the
+tolerance-stopped runs, and solutions at the fp32-emulation bound (tests/fp32_bound.py: no further from the oracle,
+after the frame's own update count, than an fp32 evaluation of the same chain)."""
 import numpy as np
 import pytest
+from fp32_bound import check_fp32_bound
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -33,7 +36,8 @@ def test_multiframe_vs_oracle(log, nframes, batch):
         x, st, it = sart_gpu_semantics(A, G[f], L, logarithmic=log, **kw)
         assert res[f].status == st
         assert abs(res[f].iterations - it) <= 2
-        assert np.linalg.norm(res[f].solution - x) / np.linalg.norm(x) < 3e-3
+    for f in sorted({0, nframes // 2, nframes - 1}):
+        check_fp32_bound(res[f].solution, A, G[f], L, log=log, iterations=res[f].iterations, beta_laplace=1e-3)
 
 
 @pytest.mark.parametrize("log", [False, True])
@@ -69,12 +73,15 @@ def test_multiframe_warm_chain(log):
         prev = x0 if wf < 0 else res[wf].solution
         x, st, it = sart_gpu_semantics(A, G[f], L, logarithmic=log, x_prev=prev, **kw)
         assert res[f].status == st and abs(res[f].iterations - it) <= 2, (f, res[f].iterations, it)
-        assert np.linalg.norm(res[f].solution - x) / np.linalg.norm(x) < 3e-3
+        if f % 7 == 0 or f == nframes - 1:
+            check_fp32_bound(res[f].solution, A, G[f], L, log=log, iterations=res[f].iterations, beta_laplace=1e-3,
+                             x_prev=prev)
     # without chain, every frame after the first batch cold-starts even when x0 is given
     cold = s.solve_batch(G[:20], x0=None)
     assert all(r.warm_from == -1 for r in cold)
     x, st, it = sart_gpu_semantics(A, G[17], L, logarithmic=log, **kw)
-    assert cold[17].status == st and np.linalg.norm(cold[17].solution - x) / np.linalg.norm(x) < 3e-3
+    assert cold[17].status == st
+    check_fp32_bound(cold[17].solution, A, G[17], L, log=log, iterations=cold[17].iterations, beta_laplace=1e-3)
 
 
 @pytest.mark.parametrize("log", [False, True])
@@ -98,13 +105,13 @@ def test_multiframe_nonfinite_slot_is_rolled_back_and_refilled(monkeypatch, log)
                              batch=16, allow_zero_tolerance=True)
     res = s.solve_batch(G)
     assert res[0].nonfinite and res[0].iterations == 5 and np.all(np.isfinite(res[0].solution))
-    x, _, _ = sart_gpu_semantics(A, G[0], None, logarithmic=log, max_iterations=5, conv_tolerance=0.0)
-    assert np.linalg.norm(res[0].solution - x) / np.linalg.norm(x) < 3e-3
+    check_fp32_bound(res[0].solution, A, G[0], None, log=log, iterations=5)
     for f in range(1, nframes):
         assert not res[f].nonfinite
         x, st, it = sart_gpu_semantics(A, G[f], None, logarithmic=log, **kw)
         assert res[f].status == st and abs(res[f].iterations - it) <= 2, (f, res[f].iterations, it)
-        assert np.linalg.norm(res[f].solution - x) / np.linalg.norm(x) < 3e-3
+    for f in (1, 16, nframes - 1):  # frame 16: the refill of the rolled-back slot
+        check_fp32_bound(res[f].solution, A, G[f], None, log=log, iterations=res[f].iterations)
 
 
 @pytest.mark.parametrize("log", [False, True])

@@ -1,0 +1,251 @@
+"""Every default solver path on a ray-traced RTM with reflections (utils/raytrace.py), bounded by the fp32 emulation.
+
+The reference's production matrices (default dataset ``with_reflections``, reference arguments.cpp:135-137) are
+mostly zero, with entries over many decades, rows and columns below the thresholds, and voxels seen only through
+weak reflections; the reference multiplies their raw fp32 values with plain FMAs (sart_kernels.cu:63-110). Here
+2048 pixels (two 32 x 32 cameras) x 4096 voxels (16^3; BASELINE config 1's shape): every path's solution after a
+fixed number of SART updates against the fp64 oracle of the reference GPU semantics, at no more than the error
+of an fp32 evaluation of the same algorithm (``sart_fp32_emulation``: fp32 vectors and fp32 products, the larger
+error of BLAS sums and of the reference kernels' serial 256-term tiles) -- the bound of the single-frame solver tests
+(tests/test_gpu_solver.py) -- with FACTOR = 1.0 and an absolute slack of 2e-8 (the emulation's own error here is
+~2e-7: the matrix is well conditioned; summation order alone moves it by ~10 %).
+
+Paths: the fused sweep and the two-pass kernels (linear / log, with and without the Laplacian), the column
+shard, the multi-frame engine at 16 (fp32 MFMA), 32, 64 and 128 frames (split-A on f16 pairs with per-row /
+per-column scales) and the CLI end to end on HDF5 files of the same model.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+FACTOR = 1.0
+SLACK = 2e-8
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def realistic():
+    from mpi_cuda_sartsolver_amd.utils.raytrace import phantom, raytraced_rtm
+
+    A, info = raytraced_rtm(grid=(16, 16, 16))
+    rng = np.random.default_rng(3)
+    X = np.stack([phantom((16, 16, 16), t=float(t)) for t in range(128)])
+    G = X @ A.T.astype(np.float64)
+    G[rng.random(G.shape) < 0.02] = -1.0  # saturated pixels
+    return A, G, info
+
+
+@pytest.fixture(scope="module")
+def lap(dev):
+    from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+
+    return LaplacianCSR.grid_3d(16, 16, 16, device=dev)
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b) / np.linalg.norm(b)
+
+
+def _errors(x, A, g, L, *, log, iters, beta, x_prev=None):
+    """(ours, fp32) errors against the fp64 oracle; fp32: the larger of the two fp32 emulations' (BLAS sums and
+    the reference kernels' own serial-tile order: summation order alone moves the error by ~10 % here, and a pure
+    fp32 kernel lands anywhere in that spread)."""
+    from mpi_cuda_sartsolver_amd.models.reference import sart_fp32_emulation, sart_gpu_semantics
+
+    kw = dict(logarithmic=log, max_iterations=iters, beta_laplace=beta, x_prev=x_prev)
+    x64, _, _ = sart_gpu_semantics(A, g, L, conv_tolerance=0.0, **kw)
+    e32 = max(_rel(sart_fp32_emulation(A, g, L, order=o, **kw)[0], x64) for o in ("blas", "reference"))
+    return _rel(x, x64), e32
+
+
+def test_structure(realistic):
+    from mpi_cuda_sartsolver_amd.utils.raytrace import rtm_stats
+
+    A, _, info = realistic
+    st = rtm_stats(A, info["direct"])
+    assert st["direct_zero_fraction"] >= 0.9 and st["dynamic_range"] >= 1e8
+    assert st["rows_below"] > 0 and st["cols_below"] > 0
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("log", [False, True])
+@pytest.mark.parametrize("with_lap", [False, True])
+def test_single_frame_paths(dev, realistic, lap, fused, log, with_lap):
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+
+    A, G, _ = realistic
+    L = lap if with_lap else None
+    beta = 1e-3
+    s = SARTSolver(DenseRTM.from_dense(A, device=dev), L, None,
+                   SolverParams(max_iterations=40, conv_tolerance=0.0, beta_laplace=beta), logarithmic=log,
+                   use_fused=fused, allow_zero_tolerance=True)
+    assert s.use_fused == fused
+    for k in (0, 5):
+        r = s.solve(G[k])
+        e, e32 = _errors(r.solution, A, G[k], L, log=log, iters=40, beta=beta)
+        print(f"fused={fused} log={log} lap={with_lap} frame {k}: {e:.3e} (fp32 emulation {e32:.3e})")
+        assert e <= FACTOR * e32 + SLACK, (k, e, e32)
+
+
+@pytest.mark.parametrize("log", [False, True])
+def test_column_shard(dev, realistic, lap, log):
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+
+    A, G, _ = realistic
+    s = SARTSolver(DenseRTM.from_dense(A, device=dev), lap, None,
+                   SolverParams(max_iterations=30, conv_tolerance=0.0, beta_laplace=1e-3), logarithmic=log,
+                   allow_zero_tolerance=True, partition="cols")
+    assert s.engine.column_shard
+    r = s.solve(G[1])
+    e, e32 = _errors(r.solution, A, G[1], lap, log=log, iters=30, beta=1e-3)
+    assert e <= FACTOR * e32 + SLACK, (e, e32)
+
+
+@pytest.mark.parametrize("log", [False, True])
+@pytest.mark.parametrize("batch", [16, 32, 64, 128])
+def test_multiframe_paths(dev, realistic, lap, batch, log):
+    """The multi-frame engine's default path per batch width (16: fp32 MFMA; 32 / 64 / 128: split-A with f16-pair
+    forward and back-projection), fixed iterations, every checked frame at the fp32 emulation bound."""
+    from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SolverParams
+
+    A, G, _ = realistic
+    iters, beta = 30, 1e-3
+    s = MultiFrameSARTSolver(DenseRTM.from_dense(A, device=dev), lap, None,
+                             SolverParams(max_iterations=iters, conv_tolerance=0.0, beta_laplace=beta),
+                             logarithmic=log, batch=batch, allow_zero_tolerance=True)
+    assert s.batch_width == batch and s.split_a == (batch >= 32)
+    if batch >= 32:
+        assert s.forward_split == "f16x2" and s.backproject_split == "f16x2"
+    res = s.solve_batch(G[:batch])
+    for f in sorted({0, 1, batch // 2, batch - 1}):
+        assert res[f].iterations == iters
+        e, e32 = _errors(res[f].solution, A, G[f], lap, log=log, iters=iters, beta=beta)
+        print(f"batch={batch} log={log} frame {f}: {e:.3e} (fp32 emulation {e32:.3e})")
+        assert e <= FACTOR * e32 + SLACK, (f, e, e32)
+
+
+def test_bf16_pair_forward_is_not_fp32_grade(dev, realistic):
+    """Why the split-A forward moved to f16 pairs: the bf16 hi + lo forward (2^-17 per product, SART_MF_FWD16=0) is
+    ~10x the fp32 emulation's error on this matrix, whose rows are dominated by a few entries."""
+    import os
+
+    from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SolverParams
+
+    A, G, _ = realistic
+    os.environ["SART_MF_FWD16"] = "0"
+    try:
+        s = MultiFrameSARTSolver(DenseRTM.from_dense(A, device=dev), None, None,
+                                 SolverParams(max_iterations=10, conv_tolerance=0.0), batch=32,
+                                 allow_zero_tolerance=True)
+    finally:
+        del os.environ["SART_MF_FWD16"]
+    assert s.forward_split == "bf16x2"
+    r = s.solve_batch(G[:32])[0]
+    e, e32 = _errors(r.solution, A, G[0], None, log=False, iters=10, beta=0.0)
+    print(f"bf16 hi + lo forward: {e:.3e} (fp32 emulation {e32:.3e})")
+    assert e > 2 * e32
+
+
+def _colmajor_w(W, nf):
+    P = W.shape[0]
+    return np.ascontiguousarray(W.reshape(P, nf // 16, 16).transpose(0, 2, 1).reshape(P, nf))
+
+
+@pytest.mark.parametrize("nf", [32, 64, 128])
+def test_f16_pair_kernels_per_element(dev, realistic, nf):
+    """The f16-pair kernels on the realistic matrix, element by element against fp64: every output within a few
+    2^-22 of its own scale sum |A||x| (forward, per row) / sum |A||w| (back-projection, per column) -- relative to
+    the row's / column's own magnitudes, however small they are against the matrix's maximum."""
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+
+    from mpi_cuda_sartsolver_amd.ops import hip
+
+    k = hip()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    A, _, _ = realistic
+    P, V = A.shape
+    m = DenseRTM.from_dense(A, device=dev)
+    rng = np.random.default_rng(nf)
+    X = (rng.random((nf, V)) * np.logspace(-3, 0, nf)[:, None]).astype(np.float32)
+    Xd = torch.zeros((nf, m.ld), device=dev)
+    Xd[:, :V] = torch.from_numpy(X)
+    rsc = torch.zeros(2 * m.nrows_pad, device=dev)
+    k.mf_row_scales(m.A.data_ptr(), m.ld, m.nrows_pad, rsc.data_ptr(), st)
+    x16 = torch.zeros((2, nf * m.ld), dtype=torch.int16, device=dev)
+    xmax = torch.zeros(nf, dtype=torch.int32, device=dev)
+    xinv = torch.zeros(nf, device=dev)
+    outs = []
+    for blk in (False, True):
+        k.mf_split_x16(Xd.data_ptr(), m.ld, nf, x16[0].data_ptr(), x16[1].data_ptr(), xmax.data_ptr(), xinv.data_ptr(),
+                       st, True, blk)
+        Fo = torch.zeros((2, m.nrows_pad, nf), device=dev)
+        k.mf_forward_h16(m.A.data_ptr(), m.ld, P, m.nrows_pad, x16[0].data_ptr(), x16[1].data_ptr(), Fo.data_ptr(), 2,
+                         st, nf, blk, rsc.data_ptr(), xinv.data_ptr())
+        torch.cuda.synchronize()
+        outs.append(Fo.sum(0)[:P].double().cpu().numpy())
+    np.testing.assert_array_equal(outs[0], outs[1])  # blocked and frame-major X planes: same sums
+    A64 = A.astype(np.float64)
+    F_ref = A64 @ X.T.astype(np.float64)
+    scale = np.abs(A64) @ np.abs(X.T.astype(np.float64))
+    err = np.abs(outs[0] - F_ref)
+    # representation (~2^-22 per product) plus fp32 accumulation over V terms; a range failure (an f16 floor hit)
+    # shows as 2^-12 or worse of the row's own scale
+    tol = 8 * 2.0 ** -22 + 2.0 ** -24 * np.sqrt(V)
+    assert np.all(err <= tol * scale + 1e-30), (err / np.maximum(scale, 1e-30)).max()
+
+    W = ((rng.random((P, nf)) - 0.5) * np.logspace(0, 3, nf)[None, :]).astype(np.float32)
+    Wd = torch.zeros((m.nrows_pad, nf), device=dev)
+    Wd[:P] = torch.from_numpy(_colmajor_w(W, nf))
+    csc = torch.zeros(2 * m.ld, device=dev)
+    cmax = torch.zeros(m.ld, dtype=torch.int32, device=dev)
+    k.mf_col_scales(m.A.data_ptr(), m.ld, m.nrows_pad, cmax.data_ptr(), csc.data_ptr(), st)
+    w16 = torch.zeros((2, nf, m.nrows_pad), dtype=torch.int16, device=dev)
+    wmax = torch.zeros(nf, dtype=torch.int32, device=dev)
+    inv = torch.zeros(nf, device=dev)
+    k.mf_split_w16(Wd.data_ptr(), m.nrows_pad, nf, m.nrows_pad, w16[0].data_ptr(), w16[1].data_ptr(), wmax.data_ptr(),
+                   1.0, inv.data_ptr(), st)
+    ns = 3
+    part = torch.zeros((ns, m.ld, nf), device=dev)
+    k.mf_backproject_h16(m.A.data_ptr(), m.ld, P, w16[0].data_ptr(), w16[1].data_ptr(), m.nrows_pad, ns,
+                         part.data_ptr(), st, nf, 0, m.ld, csc.data_ptr(), inv.data_ptr())
+    torch.cuda.synchronize()
+    B = part.sum(0)[:V].double().cpu().numpy()
+    B_ref = A64.T @ W.astype(np.float64)
+    bscale = np.abs(A64).T @ np.abs(W.astype(np.float64))
+    berr = np.abs(B - B_ref)
+    tol = 8 * 2.0 ** -22 + 2.0 ** -24 * np.sqrt(P)
+    assert np.all(berr <= tol * bscale + 1e-30), (berr / np.maximum(bscale, 1e-30)).max()
+
+
+@pytest.mark.parametrize("extra", [[], ["--two_pass"], ["--batch_frames", "32"]])
+def test_cli_realistic_hdf5(tmp_path, capfd, extra):
+    """CLI end to end on HDF5 files of the ray-traced model (one camera's RTM stored sparse COO): every frame of
+    the output against the fp64 oracle of the same chain, at the fp32 emulation's error of that chain."""
+    from mpi_cuda_sartsolver_amd import cli
+    from mpi_cuda_sartsolver_amd.io.fixtures import make_case
+
+    from test_cli_e2e import chain_errors
+
+    case = make_case(str(tmp_path / "c"), shapes=((32, 32), (32, 32)), grid=(16, 16, 16), raytraced=True,
+                     sparse_cameras=("cam_b",), laplacian=True, nframes=6, saturate=0.02, mask_fraction=0.1)
+    out = str(tmp_path / "out.h5")
+    batched = "--batch_frames" in extra
+    argv = ["-m", "40", "-c", "1e-7", "-l", case.laplacian_file, "-b", "1e-3", "-o", out] + extra
+    argv += (["--no_guess"] if batched else []) + case.files
+    assert cli.main(argv) == 0
+    assert capfd.readouterr().out.count("Processed in:") == 6
+    e, e32 = chain_errors(case, out, warm=not batched, orders=("blas", "reference"))
+    print("cli", extra, e, e32)
+    assert np.all(e <= FACTOR * e32 + SLACK), (e, e32)

@@ -53,15 +53,16 @@ def main():
         pv = torch.zeros((nsv, m.ld, nf), device=dev)
         if bwd.startswith("h16"):  # f16 pairs, three products (launch_mf_backproject_h16); "h16+ew,w1": SART_MF_H16
             os.environ["SART_MF_H16"] = bwd[4:]
-            scratch = torch.zeros(nf, dtype=torch.int32, device=dev)
-            a_sc = k.absmax_pow2_scale(m.A.data_ptr(), m.nrows_pad * m.ld, scratch.data_ptr(), s)
+            scratch = torch.zeros(max(nf, m.ld), dtype=torch.int32, device=dev)
+            csc = torch.zeros(2 * m.ld, device=dev)
+            k.mf_col_scales(m.A.data_ptr(), m.ld, m.nrows_pad, scratch.data_ptr(), csc.data_ptr(), s)
             w16 = torch.zeros((2, nf, m.nrows_pad), dtype=torch.int16, device=dev)
             inv = torch.zeros(nf, device=dev)
             k.mf_split_w16(W.data_ptr(), m.nrows_pad, nf, m.nrows_pad, w16[0].data_ptr(), w16[1].data_ptr(),
-                           scratch.data_ptr(), a_sc, inv.data_ptr(), s)
+                           scratch.data_ptr(), 1.0, inv.data_ptr(), s)
             med, best = timeit(lambda: k.mf_backproject_h16(m.A.data_ptr(), m.ld, P, w16[0].data_ptr(), w16[1].data_ptr(),
-                                                            m.nrows_pad, nsv, pv.data_ptr(), s, nf, 0, m.ld, a_sc,
-                                                            inv.data_ptr()), reps=7)
+                                                            m.nrows_pad, nsv, pv.data_ptr(), s, nf, 0, m.ld,
+                                                            csc.data_ptr(), inv.data_ptr()), reps=7)
         else:
             med, best = timeit(lambda: k.mf_backproject_x3(m.A.data_ptr(), m.ld, P, Wh.data_ptr(), Wl.data_ptr(),
                                                            m.nrows_pad, nsv, pv.data_ptr(), s, nf), reps=7)
