@@ -45,9 +45,10 @@ class LocalComm final : public Communicator {
 
 class StagedComm final : public Communicator {
    public:
-    explicit StagedComm(std::unique_ptr<HostComm> h) : host_(std::move(h)) {}
+    explicit StagedComm(std::unique_ptr<HostComm> h, std::string note = "") : host_(std::move(h)), note_(std::move(note)) {}
     HostComm& host() override { return *host_; }
     const char* backend() const override { return "staged"; }
+    std::string describe() const override { return note_.empty() ? std::string("staged") : "staged (" + note_ + ")"; }
     void all_reduce(float* dev, size_t n, ReduceOp op, hipStream_t s) override { staged(dev, n, op, s); }
     void all_reduce(double* dev, size_t n, ReduceOp op, hipStream_t s) override { staged(dev, n, op, s); }
 
@@ -63,20 +64,32 @@ class StagedComm final : public Communicator {
         hip_ok(hipStreamSynchronize(stream), "staged sync");
     }
     std::unique_ptr<HostComm> host_;
+    std::string note_;
 };
 
 class RcclComm final : public Communicator {
    public:
-    RcclComm(int device, const std::string& uid, std::unique_ptr<HostComm> boot) : host_(std::move(boot)) {
-        if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("RcclComm: bad unique id");
-        ncclUniqueId id;
-        std::memcpy(&id, uid.data(), sizeof(id));
-        hip_ok(hipSetDevice(device), "hipSetDevice");
-        nccl_ok(ncclCommInitRank(&comm_, host_->size(), id, host_->rank()), "ncclCommInitRank");
+    explicit RcclComm(std::unique_ptr<HostComm> boot) : host_(std::move(boot)) {}
+    // ncclCommInitRank on this rank: "" on success, else the error (the communicator stays unusable)
+    std::string init(int device, const std::string& uid) {
+        try {
+            if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("RcclComm: bad unique id");
+            ncclUniqueId id;
+            std::memcpy(&id, uid.data(), sizeof(id));
+            hip_ok(hipSetDevice(device), "hipSetDevice");
+            nccl_ok(ncclCommInitRank(&comm_, host_->size(), id, host_->rank()), "ncclCommInitRank");
+        } catch (const std::exception& e) {
+            comm_ = nullptr;
+            return e.what();
+        }
+        return "";
     }
-    ~RcclComm() override {
+    void destroy() {
         if (comm_) (void)ncclCommDestroy(comm_);
+        comm_ = nullptr;
     }
+    std::unique_ptr<HostComm> take_host() { return std::move(host_); }
+    ~RcclComm() override { destroy(); }
     HostComm& host() override { return *host_; }
     const char* backend() const override { return "rccl"; }
     void all_reduce(float* dev, size_t n, ReduceOp op, hipStream_t stream) override {
@@ -218,6 +231,8 @@ class P2pComm final : public Communicator {
                               : "p2p at floats " + won + ", " + base_->backend() + " otherwise (auto)";
         }
         if (!table.empty()) sel += " (rank 0, us p2p/" + std::string(base_->backend()) + " at floats " + table + ")";
+        const std::string bd = base_->describe();
+        if (bd != base_->backend()) sel += "; base: " + bd;  // e.g. staged after a failed RCCL bring-up
         return sel + buf;
     }
     double setup_seconds() const override { return t_map_ + t_test_ + t_probe_; }
@@ -543,7 +558,31 @@ std::string rccl_unique_id() {
 }
 
 std::unique_ptr<Communicator> make_rccl_comm(int device, const std::string& uid, std::unique_ptr<HostComm> bootstrap) {
-    return std::make_unique<RcclComm>(device, uid, std::move(bootstrap));
+    auto rc = std::make_unique<RcclComm>(std::move(bootstrap));
+    // SART_FAULT_RCCL_INIT=1 (tests): the RCCL bring-up fails on every rank (no rank calls ncclCommInitRank), or,
+    // with SART_FAULT_RANK, on that rank only (it still takes part in the collective init, so its peers are not
+    // left waiting in it, and reports failure afterwards)
+    const char* f = std::getenv("SART_FAULT_RCCL_INIT");
+    const char* fr = std::getenv("SART_FAULT_RANK");
+    const bool inject = f && *f && std::atoi(f) != 0;
+    const bool inject_all = inject && !(fr && *fr);
+    std::string err = inject_all ? std::string("injected (SART_FAULT_RCCL_INIT)") : rc->init(device, uid);
+    if (inject && !inject_all && std::atoi(fr) == rc->host().rank()) {
+        rc->destroy();
+        err = "injected (SART_FAULT_RCCL_INIT)";
+    }
+    // every rank learns whether all brought RCCL up; if any did not, all continue on device buffers staged
+    // through the host communicator (which the P2P all-reduce then wraps: it needs only IPC), instead of a
+    // failed run. The second word carries the lowest failing rank (max of -rank).
+    double fail[2] = {err.empty() ? 0.0 : 1.0, err.empty() ? -1e9 : -(double)rc->host().rank()};
+    rc->host().all_reduce_host(fail, 2, ReduceOp::kMax);
+    if (fail[0] == 0.0) return rc;
+    rc->destroy();
+    const int first = (int)(-fail[1]);
+    std::string note = "RCCL init failed on rank " + std::to_string(first) + (err.empty() ? "" : ": " + err) +
+                       "; collectives staged through host memory";
+    if (rc->host().rank() == 0) std::fprintf(stderr, "sart: %s\n", note.c_str());
+    return std::make_unique<StagedComm>(rc->take_host(), note);
 }
 
 std::unique_ptr<Communicator> comm_from_env(int device) {

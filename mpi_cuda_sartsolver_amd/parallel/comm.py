@@ -4,8 +4,11 @@ The reference reduces the voxel correction through host memory with CUDA-unaware
 ``MPI_Allreduce``, H2D copy, plus a second scalar ``MPI_Allreduce`` every iteration
 (reference sartsolver_cuda.cpp:242-255). Here one collective per iteration runs on device buffers:
 
-* :class:`TorchDistComm` -- ``torch.distributed`` process group; backend ``nccl`` is RCCL over xGMI
-  on MI355X (one process per GPU), backend ``gloo`` is the CPU path used by the multi-process tests.
+* :class:`TorchDistComm` -- ``torch.distributed`` process group for the Python layer's host-side collectives
+  (scalars, barriers, object exchange; gloo by default). The per-iteration device collectives belong to the
+  native engine's communicator (:func:`native_communicator`): RCCL over xGMI (``device_backend == "rccl"``,
+  one process per GPU), brought up once per process by the engine -- or staged through host memory
+  (``"staged"``: several ranks sharing one GPU in the tests, or every rank after a failed RCCL bring-up).
 * :class:`SingleProcessComm` -- world size 1, every collective is the identity.
 
 The scalar ``||A x||^2`` rides in the same buffer as the correction vector (one collective, not two).
@@ -57,13 +60,16 @@ _OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp
 class TorchDistComm(Communicator):
     """Wraps an initialised torch.distributed process group."""
 
-    def __init__(self, group: Optional[dist.ProcessGroup] = None, device: Optional[torch.device] = None):
+    def __init__(self, group: Optional[dist.ProcessGroup] = None, device: Optional[torch.device] = None,
+                 device_backend: Optional[str] = None):
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed is not initialised")
         self.group = group
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
+        # the native engine's device collectives: "rccl" or "staged" (default: follow the process group)
+        self.device_backend = device_backend or ("rccl" if self.backend == "nccl" else "staged")
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
         self.device = device
@@ -117,24 +123,29 @@ def init_distributed(use_gpu: bool = True, timeout_s: float = 1800.0) -> Communi
     import datetime
 
     rank, world, local = env_world()
-    if use_gpu and torch.cuda.is_available():
+    gpu = use_gpu and torch.cuda.is_available()
+    if gpu:
         ndev = torch.cuda.device_count()
         torch.cuda.set_device(local % ndev)
     if world == 1:
         return SingleProcessComm()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
-    backend = "nccl" if (use_gpu and torch.cuda.is_available()) else "gloo"
-    # SART_DIST_BACKEND=gloo: exercise the multi-rank GPU path with several ranks on ONE GPU (tests on a
-    # single-GPU box; RCCL refuses two ranks on the same device). Production uses nccl (= RCCL).
-    backend = os.environ.get("SART_DIST_BACKEND", backend)
+    # Device collectives: the engine's own RCCL communicator (one per process, brought up by the engine; a failed
+    # bring-up on any rank leaves every rank on staged collectives + P2P, csrc/engine/comm.cpp make_rccl_comm).
+    # SART_DIST_BACKEND=gloo / tcp: staged from the start (several ranks sharing ONE GPU in the tests: RCCL refuses
+    # two ranks on one device). The process group only carries the Python layer's host-side collectives, over gloo,
+    # so RCCL is not brought up a second time by torch; SART_DIST_BACKEND=nccl puts the group on RCCL as well.
+    env = os.environ.get("SART_DIST_BACKEND", "")
+    device_backend = "staged" if (not gpu or env in ("gloo", "tcp")) else "rccl"
+    backend = "nccl" if (gpu and env == "nccl") else "gloo"
     if not dist.is_initialized():
         kwargs = dict(backend=backend, rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kwargs["device_id"] = torch.device("cuda", torch.cuda.current_device())
         dist.init_process_group(**kwargs)
-    dev = torch.device("cuda", torch.cuda.current_device()) if (use_gpu and torch.cuda.is_available()) else None
-    return TorchDistComm(device=dev)
+    dev = torch.device("cuda", torch.cuda.current_device()) if gpu else None
+    return TorchDistComm(device=dev, device_backend=device_backend)
 
 
 def _free_port() -> int:
@@ -150,9 +161,10 @@ def native_communicator(comm: Optional[Communicator], device: int = 0):
     per process group and cached on it:
 
     * world size 1 -> ``LocalComm``;
-    * ``nccl`` process group -> the engine's own RCCL communicator over xGMI (unique id handed out through
-      the process group) with a TCP side channel for host scalars;
-    * ``gloo`` -> staged communicator (device buffers staged through the TCP host communicator,
+    * ``device_backend == "rccl"`` -> the engine's own RCCL communicator over xGMI (unique id handed out through
+      the process group) with a TCP side channel for host scalars; if RCCL fails to come up on any rank, every
+      rank gets the staged communicator instead (``describe`` says so);
+    * ``"staged"`` -> staged communicator (device buffers staged through the TCP host communicator,
       reductions in fixed rank order), e.g. several ranks sharing one GPU in tests;
     * both wrapped in the one-shot P2P all-reduce (csrc/kernels/p2p_allreduce.hip) per ``SART_P2P``:
       ``auto`` (default; RCCL groups only: used when faster than RCCL at the engine's message size),
@@ -169,7 +181,8 @@ def native_communicator(comm: Optional[Communicator], device: int = 0):
     host = os.environ.get("MASTER_ADDR", "127.0.0.1")
     port = comm.broadcast_object(_free_port() if comm.rank == 0 else None, src=0)
     p2p = os.environ.get("SART_P2P", "auto")
-    if getattr(comm, "backend", "gloo") == "nccl":
+    device_backend = getattr(comm, "device_backend", "rccl" if getattr(comm, "backend", "gloo") == "nccl" else "staged")
+    if device_backend == "rccl":
         uid = comm.broadcast_object(k.rccl_unique_id() if comm.rank == 0 else None, src=0)
         native = k.rccl_comm(device, uid, comm.rank, comm.world_size, host, int(port))
         if p2p not in ("0", "off"):  # one-shot P2P all-reduce over xGMI (self-tested, timed against RCCL)

@@ -19,8 +19,9 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(nproc, out, extra, script="dist_check.py", **env_extra):
-    env = dict(os.environ, PYTHONPATH=ROOT, SART_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", **env_extra)
+def _run(nproc, out, extra, script="dist_check.py", timeout=600, **env_extra):
+    env = dict(os.environ, PYTHONPATH=ROOT, SART_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.update(env_extra)
     if nproc > 2:  # N ranks x queues within the 24 the GPU maps (a ceiling on the box's default 4, as bench.py)
         have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
         env["GPU_MAX_HW_QUEUES"] = str(max(1, min(have, 12 // nproc)))
@@ -30,7 +31,7 @@ def _run(nproc, out, extra, script="dist_check.py", **env_extra):
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), path, "--out", out, *extra]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     if script != "dist_check.py":
         return json.load(open(out))
@@ -98,18 +99,23 @@ def test_column_shard_matches_row_shard(tmp_path, log):
         assert a["status"] == b["status"] and a["iterations"] == b["iterations"]
 
 
-@pytest.mark.parametrize("nproc", [2, 3, 4, 8])
-def test_p2p_allreduce_bitwise(tmp_path, nproc):
+@pytest.mark.parametrize("nproc,blocks", [(2, 0), (3, 0), (4, 0), (8, 0), (2, 1024)])
+def test_p2p_allreduce_bitwise(tmp_path, nproc, blocks):
     """One-shot P2P all-reduce (csrc/kernels/p2p_allreduce.hip) through IPC-mapped buffers of several
     processes on one GPU: bitwise equal to the rank-order sum / maximum at every size, both call parities;
     vectors above SART_P2P_MAX_BYTES go through the base communicator. 8 processes is the production rank count
     (one per GPU of a node); sharing one GPU they run with 32 / 8 = 4 workgroups per call, and the start-up
-    (IPC mapping + self-test) stays under 10 s."""
-    res = _run(nproc, str(tmp_path / "comm.json"), [], script="comm_check.py", SART_P2P="1")
+    (IPC mapping + self-test) stays under 10 s. blocks 1024: the launch shape of one rank per GPU (up to
+    kP2pMaxBlocks = 1024 workgroups per call: 65 at the headline's 65538 floats, 512 at the 2 MiB cap) on the
+    shared GPU (SART_P2P_BLOCKS)."""
+    env = dict(SART_P2P="1", SART_P2P_TIMEOUT_S="30")
+    if blocks:
+        env["SART_P2P_BLOCKS"] = str(blocks)
+    res = _run(nproc, str(tmp_path / "comm.json"), [], script="comm_check.py", **env)
     assert res["backend"] == "p2p", res["describe"]
     assert res["setup_s"] < 10.0, res["describe"]
     if nproc > 1:
-        assert f"{nproc} ranks/GPU, {32 // nproc} blocks" in res["describe"], res["describe"]
+        assert f"{nproc} ranks/GPU, {blocks or 32 // nproc} blocks" in res["describe"], res["describe"]
     for r in res["results"]:
         if r["n"] * 4 <= 2 * 1024 * 1024:
             assert r["exact"], r
@@ -148,6 +154,47 @@ def test_gpu_solver_rank_invariance_p2p(tmp_path, extra):
             assert a["status"] == b["status"] and a["iterations"] == b["iterations"]
         xs.append(x[0])
     errs, e32 = _oracle_rel(tmp_path, [x1[0]] + xs, extra, iters)
+    assert max(errs) <= RANK_FACTOR * e32 + 1e-7, (errs, e32)
+
+
+@pytest.mark.parametrize("extra", [["--npix", "2048", "--nvox", "65536"],
+                                   ["--multiframe", "--batch", "32", "--npix", "1024", "--nvox", "65536"]])
+def test_p2p_production_launch_shape(tmp_path, extra):
+    """The P2P all-reduce at the launch shape of one rank per GPU (SART_P2P_BLOCKS=1024, as on the 8-GPU node:
+    65 workgroups for the single-frame 65538-float vector, 512 for a multi-frame chunk of 16384 voxels x 32 frames =
+    the 2 MiB cap) with two ranks on the two-pass kernels: bitwise-equal replicated solutions, the same statuses and
+    iteration counts as one rank, and the fp32-emulation bound."""
+    fixed = extra + ["--tol", "0", "--iters", "12"]
+    x1, m1 = _run(1, str(tmp_path / "r1"), fixed + ["--save-problem"])
+    x, m = _run(2, str(tmp_path / "p2"), fixed, timeout=240, SART_P2P="1", SART_P2P_BLOCKS="1024",
+                SART_P2P_TIMEOUT_S="30")
+    assert m[0]["comm"] == "p2p"
+    if "--multiframe" not in extra:
+        assert m[0]["x_bitwise_equal"] and "1024 blocks" in m[0]["describe"], m[0]
+    for a, b in zip(m, m1):
+        assert a["status"] == b["status"] and a["iterations"] == b["iterations"]
+    errs, e32 = _oracle_rel(tmp_path, [x1[0], x[0]], extra, 12)
+    assert max(errs) <= RANK_FACTOR * e32 + 1e-7, (errs, e32)
+
+
+@pytest.mark.parametrize("fault_rank", ["", "1"])
+def test_rccl_init_failure_degrades_to_staged(tmp_path, fault_rank):
+    """A failed RCCL bring-up (SART_FAULT_RCCL_INIT: on every rank, or reported by rank 1 only after the collective
+    init) is agreed on over the host communicator: every rank continues on staged collectives wrapped by the P2P
+    all-reduce instead of failing the run, ``describe`` names the failure, and a 2-rank solve matches the 1-rank one
+    at the fp32-emulation bound. (Without SART_DIST_BACKEND the ranks ask for RCCL, as on the node.)"""
+    fixed = ["--tol", "0", "--iters", "12"]
+    x1, m1 = _run(1, str(tmp_path / "r1"), fixed + ["--save-problem"])
+    env = dict(SART_DIST_BACKEND="", SART_FAULT_RCCL_INIT="1", SART_P2P="1", SART_P2P_TIMEOUT_S="30")
+    if fault_rank:
+        env["SART_FAULT_RANK"] = fault_rank
+    x, m = _run(2, str(tmp_path / "f2"), fixed, timeout=240, **env)
+    d = m[0]["describe"]
+    assert m[0]["comm"] == "p2p" and "RCCL init failed" in d and "staged" in d, d
+    assert m[0]["x_bitwise_equal"]
+    for a, b in zip(m, m1):
+        assert a["status"] == b["status"] and a["iterations"] == b["iterations"]
+    errs, e32 = _oracle_rel(tmp_path, [x1[0], x[0]], [], 12)
     assert max(errs) <= RANK_FACTOR * e32 + 1e-7, (errs, e32)
 
 
