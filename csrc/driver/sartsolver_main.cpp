@@ -421,6 +421,8 @@ int main(int argc, char** argv) {
         std::vector<uint64_t> frames;
         for (uint64_t i = 0; i < image.nframe(); ++i)
             if (image.frame_time(i) > skip_until + 1e-12) frames.push_back(i);
+        const size_t nframes_total = frames.size();
+        const auto t_loop = std::chrono::steady_clock::now();
         if (batched) {
             // --batch_frames N: N slots on the matrix cores with continuous batching (a finished frame's slot takes
             // the next frame between two sweeps). Frames are read in windows of 4 N; without --no_guess they form a
@@ -480,7 +482,9 @@ int main(int argc, char** argv) {
         if (!frames.empty()) fut = std::async(std::launch::async, [&image, i = frames[0]]() { return image.frame(i); });
         for (size_t k = 0; k < frames.size(); ++k) {
             const uint64_t cur = frames[k];
+            const auto tf = std::chrono::steady_clock::now();
             std::vector<double> frame = fut.get();
+            const double wait_frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf).count();
             if (k + 1 < frames.size())  // prefetch the next composite frame during the solve
                 fut = std::async(std::launch::async, [&image, i = frames[k + 1]]() { return image.frame(i); });
             const auto t0 = std::chrono::steady_clock::now();
@@ -499,9 +503,12 @@ int main(int argc, char** argv) {
                 host->all_reduce_host(xfull.data(), xfull.size(), ReduceOp::kSum);
             }
             if (rank == 0) {
+                const auto tw = std::chrono::steady_clock::now();
                 writer->add(cols ? xfull : x, info.status, image.frame_time(cur), image.camera_frame_time(cur),
                             info.iterations);
-                const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                const auto t1 = std::chrono::steady_clock::now();
+                const double writer_ms = std::chrono::duration<double, std::milli>(t1 - tw).count();
+                const double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
                 std::cout << "Processed in: " << ms << " ms" << std::endl;  // reference main.cpp:132-137
                 if (profile.is_open())
                 {
@@ -518,6 +525,9 @@ int main(int argc, char** argv) {
                             << ", \"rtm_GBps\": " << reads * elem * pv * sweeps / secs / 1e9
                             << ", \"comm_ms\": " << info.comm_ms << ", \"comm_fallbacks\": " << info.comm_fallbacks
                             << ", \"ms\": " << ms << ", \"solve_ms\": " << info.ms
+                            << ", \"setup_ms\": " << info.setup_ms << ", \"iterate_ms\": " << info.iterate_ms
+                            << ", \"finish_ms\": " << info.finish_ms << ", \"writer_ms\": " << writer_ms
+                            << ", \"queued_sweeps\": " << info.queued_sweeps << ", \"wait_frame_ms\": " << wait_frame_ms
                             << ", \"fused\": " << (info.used_fused ? "true" : "false")
                             << ", \"ranks\": " << size << ", \"comm\": \"" << json_escape(host->backend())
                             << "\", \"device_comm\": \"" << json_escape(dcomm ? dcomm->describe() : "none")
@@ -533,6 +543,12 @@ int main(int argc, char** argv) {
         if (rank == 0) {
             writer->flush();
             if (!appended) voxelgrid.write(cfg.output_file, "voxel_map");
+            // the whole frame loop (reads not hidden by the prefetch, solves, output, the final flush)
+            if (nframes_total) {
+                const double loop_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_loop).count();
+                std::cout << "Frames processed: " << nframes_total << " in " << loop_s << " s ("
+                          << nframes_total / loop_s << " frames/s)" << std::endl;
+            }
         }
         host->barrier();
     } catch (const std::exception& e) {

@@ -93,6 +93,9 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
     hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
     for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hstate_), 2 * sizeof(SartState)), "hipHostMalloc");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hg_), std::max<int64_t>(P_, 1) * sizeof(double)), "hipHostMalloc");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hx0_), std::max<int64_t>(V_, 1) * sizeof(double)), "hipHostMalloc");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hxo_), std::max<int64_t>(V_, 1) * sizeof(float)), "hipHostMalloc");
     hipDeviceProp_t prop;
     hip_ok(hipGetDeviceProperties(&prop, device_), "hipGetDeviceProperties");
     num_cus_ = prop.multiProcessorCount;
@@ -179,6 +182,8 @@ Engine::~Engine() {
     for (auto& pool : cev_)
         for (auto& e : pool) (void)hipEventDestroy(e);
     if (hstate_) (void)hipHostFree(hstate_);
+    for (void* p : {static_cast<void*>(hg_), static_cast<void*>(hx0_), static_cast<void*>(hxo_)})
+        if (p) (void)hipHostFree(p);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -318,18 +323,21 @@ double Engine::setup_frame(const double* g, const double* x0) {
     RoctxRange r("sart::setup_frame");
     // normalisation by the global maximum and sum_{g > 0} g^2 (reference sartsolver_cuda.cpp:146-157);
     // the reference divides by zero when every pixel is <= 0, we keep norm = 1 then.
+    // the previous frame's copies out of the pinned buffers have completed (solve() synchronises the stream)
     double mx = -std::numeric_limits<double>::infinity(), gs = 0.0;
     for (int64_t i = 0; i < P_; ++i) {
-        if (!std::isfinite(g[i])) continue;  // masked like a saturated pixel (k_prep_rows)
-        mx = std::max(mx, g[i]);
-        if (g[i] > 0) gs += g[i] * g[i];
+        const double v = g[i];
+        hg_[i] = v;  // into pinned memory in the same pass
+        if (!std::isfinite(v)) continue;  // masked like a saturated pixel (k_prep_rows)
+        mx = std::max(mx, v);
+        if (v > 0) gs += v * v;
     }
     const bool cols = cfg_.column_shard;  // every rank holds every pixel: the sums are already global
     double norm = cols ? mx : comm_->host().all_reduce_scalar(mx, ReduceOp::kMax);
     if (!(norm > 0)) norm = 1.0;
     double G = (cols ? gs : comm_->host().all_reduce_scalar(gs, ReduceOp::kSum)) / (norm * norm);
     if (!(G > 0)) G = 1.0;
-    if (P_) hip_ok(hipMemcpyAsync(g64_.get(), g, P_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D g");
+    if (P_) hip_ok(hipMemcpyAsync(g64_.get(), hg_, P_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D g");
     launch_prep_rows(g64_.get(), P_, Pp_, 1.0 / norm, rs_.ray_len.get(), (float)cfg_.ray_length_threshold, ghat_.get(),
                      arow_.get(), gpos_.get(), wo_.get(), stream_);
     if (!x0) {
@@ -340,7 +348,8 @@ double Engine::setup_frame(const double* g, const double* x0) {
         if (!cols) comm_->all_reduce(comm_buf_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
         launch_init_solution(x_.get(), V_, ld_, comm_buf_.get(), nullptr, 1.0, stream_);
     } else {
-        hip_ok(hipMemcpyAsync(x064_.get(), x0, V_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D x0");
+        std::memcpy(hx0_, x0, V_ * sizeof(double));
+        hip_ok(hipMemcpyAsync(x064_.get(), hx0_, V_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D x0");
         launch_init_solution(x_.get(), V_, ld_, nullptr, x064_.get(), 1.0 / norm, stream_);
     }
     if (cfg_.logarithmic) {
@@ -552,8 +561,14 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
     if (cfg_.column_shard && comm_->size() > 1 && comm_->degradable()) comm_->host().barrier();
     SolveInfo info;
     const int max_sweeps = cfg_.max_iterations + 1;
+    auto ms_since = [](std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+    };
+    std::chrono::steady_clock::time_point t_iter = t0;
     while (true) {
         norm_ = setup_frame(g, x0);
+        info.setup_ms = ms_since(t0);
+        t_iter = std::chrono::steady_clock::now();
         host_sweep_ = 0;
         // Fault injection (tests): report a protocol timeout from the device in the first sweep of this solve,
         // through the same path as a real one (error word -> all-reduce -> k_decide on every rank).
@@ -591,6 +606,7 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
             if (s.done || (checked == issued && enqueued >= max_sweeps)) break;
         }
         hip_ok(hipStreamSynchronize(stream_), "solve");
+        info.queued_sweeps = enqueued;
         collect_comm(0);  // chunks issued after the last check
         collect_comm(1);
         if (comm_failed_anywhere()) {
@@ -613,16 +629,20 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
         }
         break;
     }
+    info.iterate_ms = ms_since(t_iter);
+    const auto t_fin = std::chrono::steady_clock::now();
     SartState s;
     hip_ok(hipMemcpy(&s, st_.get(), sizeof(SartState), hipMemcpyDeviceToHost), "D2H state");
     // NaN/Inf guard: x of the failing sweep is non-finite; return the last finite iterate (saved by the update
     // of the previous sweep), unless the very first sweep failed (no update yet: nothing better to return)
     const bool rollback = (s.flags & 1) != 0 && s.sweep >= 2;
-    std::vector<float> xh(V_);
-    if (V_)
-        hip_ok(hipMemcpy(xh.data(), rollback ? xprev_.get() : x_.get(), V_ * sizeof(float), hipMemcpyDeviceToHost),
+    if (V_) {
+        hip_ok(hipMemcpyAsync(hxo_, rollback ? xprev_.get() : x_.get(), V_ * sizeof(float), hipMemcpyDeviceToHost,
+                              stream_),
                "D2H x");
-    for (int64_t i = 0; i < V_; ++i) x_out[i] = (double)xh[i] * norm_;  // reference sartsolver_cuda.cpp:264-265
+        hip_ok(hipStreamSynchronize(stream_), "D2H x");
+    }
+    for (int64_t i = 0; i < V_; ++i) x_out[i] = (double)hxo_[i] * norm_;  // reference sartsolver_cuda.cpp:264-265
     info.status = s.status == kSuccess ? kSuccess : kMaxIterationsExceeded;
     info.iterations = s.iterations;
     info.convergence = s.conv_last;
@@ -632,7 +652,8 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
     info.fused_variant = use_fused_ ? geom_.variant : -1;
     info.sweeps = s.sweep;
     info.comm_ms = timing_collectives() ? comm_ms_ : -1.0;
-    info.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    info.finish_ms = ms_since(t_fin);
+    info.ms = ms_since(t0);
     return info;
 }
 

@@ -219,6 +219,11 @@ class Engine {
     void collect_comm(int slot);
 
     SartState* hstate_ = nullptr;  // pinned [2]
+    // pinned per-frame staging (the frame's pixels in, x0 in, the solution out): asynchronous copies instead of
+    // the runtime's staged pageable ones (profiles/series_r5_*.jsonl: setup / finish per frame)
+    double* hg_ = nullptr;
+    double* hx0_ = nullptr;
+    float* hxo_ = nullptr;
     hipEvent_t ev_[2] = {nullptr, nullptr};
     hipGraphExec_t graph_ = nullptr;
     bool graph_failed_ = false;

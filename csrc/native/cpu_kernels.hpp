@@ -20,5 +20,11 @@ void cpu_raysums(const float* A, int64_t P, int64_t V, int64_t ld, double* rho, 
 double cpu_forward(const float* A, int64_t P, int64_t V, int64_t ld, const double* x, double* f);
 // out[v] = sum_p A[p,v] w[p]
 void cpu_backproject(const float* A, int64_t P, int64_t V, int64_t ld, const double* w, double* out);
+// One read of A per SART iteration (the CPU counterpart of the GPU fused sweep): per row, f[p] = A[p,:] x, then
+// w_p = a[p] f[p] (log) or a[p] (g[p] - f[p]) (linear) and out += A[p,:]^T w_p while the row is still in cache.
+// Returns sum_p f[p]^2. out: the back-projection of the NEXT iteration's weights (x is the iterate after this
+// iteration's update).
+double cpu_sweep(const float* A, int64_t P, int64_t V, int64_t ld, const double* x, const double* g, const double* a,
+                 bool logmode, double* f, double* out);
 
 }  // namespace sart

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <limits>
 #include <numeric>
 #include <stdexcept>
@@ -52,14 +53,18 @@ void CpuSolver::set_laplacian(const Csr& L) {
 }
 
 void CpuSolver::penalty(const std::vector<double>& x, std::vector<double>& pen) const {
-    // beta * L x (linear) or beta * L log x (log), rows in CSR order (reference sartsolver.cpp:190-199, 287-296)
+    // beta * L x (linear) or beta * L log x (log), one row per iteration of a parallel loop (each row's sum in CSR
+    // order: the result does not depend on the thread count) (reference sartsolver.cpp:190-199, 287-296)
+    const bool lg = p_.logarithmic;
+    const double beta = p_.beta_laplace;
+#pragma omp parallel for schedule(static)
     for (int64_t r = 0; r < V_; ++r) {
         double s = 0.0;
         for (int64_t k = L_.row_ptr[r]; k < L_.row_ptr[r + 1]; ++k) {
             const double xv = x[L_.col[k]];
-            s += (double)L_.val[k] * (p_.logarithmic ? std::log(xv) : xv);
+            s += (double)L_.val[k] * (lg ? std::log(xv) : xv);
         }
-        pen[r] = p_.beta_laplace * s;
+        pen[r] = beta * s;
     }
 }
 
@@ -80,7 +85,7 @@ SolveInfo CpuSolver::solve(const double* g, const double* x0, double* x_out) {
     for (int64_t q = 0; q < P_; ++q)
         if (g[q] > 0) gs += g[q] * g[q];
     const double G = comm_->all_reduce_scalar(gs, ReduceOp::kSum) / (norm * norm);
-    std::vector<double> a(P_), w(P_), f(P_), red(V_), x(V_), O, pen(V_, 0.0);
+    std::vector<double> a(P_), w(P_), f(P_), red(V_), x(V_), O, pen(V_, 0.0);  // red: one-off back-projections
     for (int64_t q = 0; q < P_; ++q) a[q] = gw[q] >= 0 ? inv_len_[q] : 0.0;
     if (!x0) {  // cold start (reference sartsolver.cpp:150-160)
         for (int64_t q = 0; q < P_; ++q) w[q] = gpu_ ? std::max(gw[q], 0.0) : gw[q];
@@ -100,30 +105,48 @@ SolveInfo CpuSolver::solve(const double* g, const double* x0, double* x_out) {
         for (int64_t v = 0; v < V_; ++v)
             if (!dvalid_[v]) O[v] = 0.0;
     }
-    cpu_forward(A_, P_, V_, ld_, x.data(), f.data());
+    // One read of A per iteration (cpu_sweep): the sweep after an update computes that iterate's forward
+    // projection (for the convergence test) and, from it, the next iteration's back-projection, as the GPU fused
+    // sweep does. red[0, V) and the sum of f^2 (red[V]) travel in one host all-reduce per iteration (the reference
+    // runs two: sartsolver.cpp:206, 222).
+    // SART_CPU_TWO_PASS=1: the forward and the back-projection as two reads of A (A/B measurements only)
+    std::vector<double> redF(V_ + 1);
+    const char* tp = std::getenv("SART_CPU_TWO_PASS");
+    const bool two_pass = tp && *tp && std::atoi(tp) != 0;
+    auto sweep = [&]() {
+        if (two_pass) {
+            redF[V_] = cpu_forward(A_, P_, V_, ld_, x.data(), f.data());
+            for (int64_t q = 0; q < P_; ++q) w[q] = lg ? a[q] * f[q] : a[q] * (gw[q] - f[q]);
+            cpu_backproject(A_, P_, V_, ld_, w.data(), redF.data());
+        } else {
+            redF[V_] = cpu_sweep(A_, P_, V_, ld_, x.data(), gw.data(), a.data(), lg, f.data(), redF.data());
+        }
+        comm_->all_reduce_host(redF.data(), (size_t)V_ + 1, ReduceOp::kSum);
+    };
+    sweep();  // the start value's forward projection and the first back-projection
     SolveInfo info;
     info.status = -1;
     info.iterations = p_.max_iterations;
     double conv_prev = 0.0, conv = 0.0;
     for (int it = 0; it < p_.max_iterations; ++it) {
         if (has_lap_) penalty(x, pen);
-        for (int64_t q = 0; q < P_; ++q) w[q] = lg ? a[q] * f[q] : a[q] * (gw[q] - f[q]);
-        cpu_backproject(A_, P_, V_, ld_, w.data(), red.data());
-        comm_->all_reduce_host(red.data(), (size_t)V_, ReduceOp::kSum);
+        const double* red_ = redF.data();
         if (lg) {
+#pragma omp parallel for schedule(static)
             for (int64_t v = 0; v < V_; ++v) {
-                const double Fv = dvalid_[v] ? red[v] : 0.0;
+                const double Fv = dvalid_[v] ? red_[v] : 0.0;
                 x[v] = x[v] * std::pow((O[v] + eps) / (Fv + eps), p_.relaxation) * std::exp(-pen[v]);
             }
         } else {
+#pragma omp parallel for schedule(static)
             for (int64_t v = 0; v < V_; ++v) {
-                const double d = (dvalid_[v] ? p_.relaxation / rho_s_[v] * red[v] : 0.0) - pen[v];
+                const double d = (dvalid_[v] ? p_.relaxation / rho_s_[v] * red_[v] : 0.0) - pen[v];
                 const double xn = x[v] + d;
                 x[v] = gpu_ ? std::max(xn, 0.0) : (std::signbit(xn) ? 0.0 : xn);
             }
         }
-        const double f2 = cpu_forward(A_, P_, V_, ld_, x.data(), f.data());
-        const double F = comm_->all_reduce_scalar(f2, ReduceOp::kSum);
+        sweep();
+        const double F = redF[V_];
         conv = G != 0 ? (G - F) / G : 0.0;
         if (!std::isfinite(conv)) {
             info.nonfinite = true;

@@ -1,6 +1,7 @@
 #include "frames.hpp"
 
 #include <algorithm>
+#include <future>
 #include <cmath>
 #include <limits>
 #include <numeric>
@@ -192,11 +193,10 @@ SolutionWriter::SolutionWriter(std::string filename, std::vector<std::string> ca
     : filename_(std::move(filename)), cams_(std::move(camera_names)), nvox_(nvoxel), first_(!append) {
     if (nvox_ == 0) throw Error("Argument nvoxel must be positive.");
     set_max_cache_size(max_cache_size);
-    cam_times_.resize(cams_.size());
+    cache_.cam_times.resize(cams_.size());
 }
 
 SolutionWriter::~SolutionWriter() {
-    SART_H5_LOCK;
     try {
         flush();
     } catch (...) {
@@ -212,12 +212,22 @@ void SolutionWriter::add(const std::vector<double>& solution, int32_t status, do
                          const std::vector<double>& camera_time, int32_t iterations) {
     if (solution.size() != nvox_) throw Error("Solution vector must contain nvoxel elements.");
     if (camera_time.size() != cams_.size()) throw Error("One time stamp per camera is required.");
-    solutions_.push_back(solution);
-    status_.push_back(status);
-    times_.push_back(time);
-    iterations_.push_back(iterations);
-    for (size_t c = 0; c < cams_.size(); ++c) cam_times_[c].push_back(camera_time[c]);
-    if (times_.size() >= max_cache_) flush();
+    cache_.solutions.push_back(solution);
+    cache_.status.push_back(status);
+    cache_.times.push_back(time);
+    cache_.iterations.push_back(iterations);
+    for (size_t c = 0; c < cams_.size(); ++c) cache_.cam_times[c].push_back(camera_time[c]);
+    if (cache_.times.size() >= max_cache_) {  // write in the background (the previous write first)
+        if (pending_.valid()) pending_.get();
+        pending_ = std::async(std::launch::async, [this, b = take()]() { write(b); });
+    }
+}
+
+SolutionWriter::Batch SolutionWriter::take() {
+    Batch b = std::move(cache_);
+    cache_ = Batch{};
+    cache_.cam_times.resize(cams_.size());
+    return b;
 }
 
 namespace {
@@ -242,11 +252,11 @@ void write_1d_at(hid_t ds, hid_t mtype, hsize_t offset, hsize_t n, const void* d
 }
 }  // namespace
 
-void SolutionWriter::create() {
+void SolutionWriter::create(uint64_t chunk) {
     SART_H5_LOCK;
     H5Id f = h5_create_file(filename_);
     H5Id g = h5_create_group(f, "solution");
-    const hsize_t n = times_.size();
+    const hsize_t n = chunk;
     {
         hsize_t dims[2] = {0, nvox_}, maxd[2] = {H5S_UNLIMITED, nvox_}, ch[2] = {1, nvox_};
         H5Id sp(H5Screate_simple(2, dims, maxd), H5Id::kSpace);
@@ -263,24 +273,24 @@ void SolutionWriter::create() {
     create_ext_1d(g, "iterations", H5T_STD_I32LE, 0, n);  // extension: SART updates per frame
 }
 
-void SolutionWriter::append() {
+void SolutionWriter::append(const Batch& b) {
     SART_H5_LOCK;
     H5Id f = h5_open_file(filename_, true);
     H5Id tds = h5_open_dataset(f, "solution/time");
     const hsize_t off = h5_dims(tds)[0];
-    const hsize_t n = times_.size();
-    write_1d_at(tds, H5T_NATIVE_DOUBLE, off, n, times_.data());
+    const hsize_t n = b.times.size();
+    write_1d_at(tds, H5T_NATIVE_DOUBLE, off, n, b.times.data());
     {
         H5Id ds = h5_open_dataset(f, "solution/status");
-        write_1d_at(ds, H5T_NATIVE_INT32, off, n, status_.data());
+        write_1d_at(ds, H5T_NATIVE_INT32, off, n, b.status.data());
     }
     if (h5_exists(f, "solution/iterations")) {
         H5Id ds = h5_open_dataset(f, "solution/iterations");
-        write_1d_at(ds, H5T_NATIVE_INT32, off, n, iterations_.data());
+        write_1d_at(ds, H5T_NATIVE_INT32, off, n, b.iterations.data());
     }
     for (size_t c = 0; c < cams_.size(); ++c) {
         H5Id ds = h5_open_dataset(f, "solution/time_" + cams_[c]);
-        write_1d_at(ds, H5T_NATIVE_DOUBLE, off, n, cam_times_[c].data());
+        write_1d_at(ds, H5T_NATIVE_DOUBLE, off, n, b.cam_times[c].data());
     }
     H5Id vds = h5_open_dataset(f, "solution/value");
     hsize_t newsize[2] = {off + n, nvox_};
@@ -291,22 +301,22 @@ void SolutionWriter::append() {
     for (hsize_t r = 0; r < n; ++r) {
         hsize_t o[2] = {off + r, 0}, c[2] = {1, nvox_};
         H5Sselect_hyperslab(fsp, H5S_SELECT_SET, o, nullptr, c, nullptr);
-        if (H5Dwrite(vds, H5T_NATIVE_DOUBLE, msp, fsp, H5P_DEFAULT, solutions_[r].data()) < 0)
+        if (H5Dwrite(vds, H5T_NATIVE_DOUBLE, msp, fsp, H5P_DEFAULT, b.solutions[r].data()) < 0)
             throw Error("Unable to write solution/value.");
     }
 }
 
-void SolutionWriter::flush() {
+void SolutionWriter::write(const Batch& b) {
     SART_H5_LOCK;
-    if (times_.empty()) return;
-    if (first_) create();
+    if (b.times.empty()) return;
+    if (first_) create(b.times.size());  // (the reference: chunk size = the first flush's size, solution.cpp:91)
     first_ = false;
-    append();
-    solutions_.clear();
-    times_.clear();
-    status_.clear();
-    iterations_.clear();
-    for (auto& v : cam_times_) v.clear();
+    append(b);
+}
+
+void SolutionWriter::flush() {
+    if (pending_.valid()) pending_.get();  // the background write first (rethrows its error)
+    write(take());
 }
 
 StoredSolutions read_solution_file(const std::string& filename) {

@@ -12,6 +12,7 @@
 #include <array>
 #include <cstdint>
 #include <map>
+#include <future>
 #include <string>
 #include <vector>
 
@@ -66,19 +67,27 @@ class SolutionWriter {
     void flush();
     uint64_t max_cache_size() const { return max_cache_; }
     void set_max_cache_size(uint64_t v);
-    uint64_t pending() const { return times_.size(); }
+    uint64_t pending() const { return cache_.times.size(); }
 
    private:
-    void create();
-    void append();
+    struct Batch {
+        std::vector<std::vector<double>> solutions;
+        std::vector<double> times;
+        std::vector<int32_t> status, iterations;
+        std::vector<std::vector<double>> cam_times;  // [camera][frame]
+    };
+    Batch take();                // the cached frames, leaving the cache empty
+    void write(const Batch& b);  // create the file on the first write, then extend the datasets
+    void create(uint64_t chunk);
+    void append(const Batch& b);
     std::string filename_;
     std::vector<std::string> cams_;
     uint64_t nvox_, max_cache_;
     bool first_;
-    std::vector<std::vector<double>> solutions_;
-    std::vector<double> times_;
-    std::vector<int32_t> status_, iterations_;
-    std::vector<std::vector<double>> cam_times_;  // [camera][frame]
+    Batch cache_;
+    // a full cache is written by a background thread (one at a time) while the frame loop continues: the
+    // max_cache_size-frame flush no longer stalls the frame that fills the cache (profiles/series_r5_*.jsonl)
+    std::future<void> pending_;
 };
 
 // (times, last solution, number of stored frames) of an existing solution file; empty if absent.

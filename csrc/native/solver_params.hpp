@@ -36,6 +36,12 @@ struct SolveInfo {
     double comm_ms = -1.0;    // GPU time inside the per-sweep all-reduces (EngineConfig::time_collectives; else -1)
     int warm_from = -1;       // multi-frame time series: index of the frame whose solution started this one
                               // (-1: the caller's x0, or cold)
+    // per-frame breakdown of ms (single-frame engine): host + device setup of the frame (normalisation, H2D of g
+    // and x0, cold-start back-projection) up to the first queued sweep, the sweep loop up to the final state
+    // check, the read-back of x (D2H and de-normalisation); sweeps queued in total (the chunks past the
+    // convergence sweep run as no-op sweeps)
+    double setup_ms = 0.0, iterate_ms = 0.0, finish_ms = 0.0;
+    int queued_sweeps = 0;
 };
 
 // CSR over n rows (row_ptr int64, col int32, val fp32), from the reference's sorted-flat-index COO

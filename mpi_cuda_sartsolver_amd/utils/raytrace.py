@@ -127,10 +127,11 @@ def pixel_rays(cam: Camera, ss: int = 2):
 
 
 def raytraced_rtm(grid=(16, 16, 16), cameras=None, ss=2, margin=0.35, bounces=3, reflectivity=(1e-5, 3e-3),
-                  diffuse=1e-6, rough_patch=(0, 0.0, 0.5), seed=0, dtype=np.float32):
+                  diffuse=1e-6, rough_patch=(0, 0.0, 0.5), seed=0, dtype=np.float32, keep_direct=True):
     """Dense [sum of camera pixels, nx * ny * nz] RTM in the reference's order (cameras in the given order, pixels
     row-major, voxels by flat grid index i * ny * nz + j * nz + k). Returns (A, info) with info: per-camera row
-    ranges, the direct-only matrix (for the sparsity statistics) and the face reflectivities."""
+    ranges, the direct-only matrix (for the sparsity statistics; keep_direct=False: None, for large matrices) and
+    the face reflectivities."""
     rng = np.random.default_rng(seed)
     cameras = cameras or default_cameras()
     n = np.asarray(grid)
@@ -146,7 +147,7 @@ def raytraced_rtm(grid=(16, 16, 16), cameras=None, ss=2, margin=0.35, bounces=3,
         H, W = cam.shape
         P = H * W
         Acam = np.zeros(P * V)
-        Adir = np.zeros(P * V)
+        Adir = np.zeros(P * V) if keep_direct else None
         O, D, pix, wt = pixel_rays(cam, ss)
         r0 = np.linalg.norm(centre - np.asarray(cam.position))
         amp = wt.copy()
@@ -159,8 +160,9 @@ def raytraced_rtm(grid=(16, 16, 16), cameras=None, ss=2, margin=0.35, bounces=3,
                 r = path_len[ray] + tm
             val = amp[ray] * seg * (r0 / np.maximum(r, 1e-3)) ** 2
             np.add.at(Acam, pix[ray] * V + flat, val)
-            if b == 0:
+            if b == 0 and keep_direct:
                 np.add.at(Adir, pix[ray] * V + flat, val)
+            if b == 0:
                 path_len = np.zeros(len(cur_O))
             tw, a, side = _wall_hit(cur_O, cur_D, lo_w, hi_w)
             face = 2 * a + side
@@ -183,13 +185,16 @@ def raytraced_rtm(grid=(16, 16, 16), cameras=None, ss=2, margin=0.35, bounces=3,
             cur_D[np.arange(len(cur_D)), a] *= -1.0
             cur_O = hitp.copy()  # nudged back inside the vessel
             cur_O[np.arange(len(cur_O)), a] -= 1e-9 * (2 * side - 1)
-        blocks.append(Acam.reshape(P, V))
-        direct_blocks.append(Adir.reshape(P, V))
+        blocks.append(Acam.reshape(P, V).astype(dtype))
+        del Acam
+        if keep_direct:
+            direct_blocks.append(Adir.reshape(P, V).astype(dtype))
         rows[cam.name] = (p0, p0 + P)
         p0 += P
-    A = np.concatenate(blocks).astype(dtype)
-    info = dict(rows=rows, direct=np.concatenate(direct_blocks).astype(dtype), reflectivity=R, grid=tuple(grid),
-                cameras=cameras)
+    A = np.concatenate(blocks) if len(blocks) > 1 else blocks[0]
+    del blocks
+    info = dict(rows=rows, direct=np.concatenate(direct_blocks) if keep_direct else None, reflectivity=R,
+                grid=tuple(grid), cameras=cameras)
     return A, info
 
 
