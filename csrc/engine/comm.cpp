@@ -147,6 +147,7 @@ class P2pComm final : public Communicator {
         // start-up calls (self-test, probes) give up sooner: a failure there only means "no P2P"
         setup_timeout_s_ = std::min(timeout_s_, env_double("SART_P2P_SETUP_TIMEOUT_S", 10.0));
         if (const char* f = std::getenv("SART_P2P_FUSED_REDUCE"); f && *f) fused_reduce_ = std::atoi(f) != 0;
+        if (const char* f = std::getenv("SART_P2P_FUSED_UPDATE"); f && *f) fused_update_ = std::atoi(f) != 0;
         if (const char* f = std::getenv("SART_FAULT_P2P"); f && *f) {
             const char* fr = std::getenv("SART_FAULT_RANK");
             if (!(fr && *fr) || std::atoi(fr) == rank_) fault_call_ = std::atoll(f);
@@ -289,6 +290,17 @@ class P2pComm final : public Communicator {
         } else {
             Communicator::reduce_all_reduce(src, out, stream);
         }
+    }
+    bool reduce_all_reduce_update(const ReduceSrc& src, float* out, const UpdateArgs& upd, hipStream_t stream) override {
+        // SART_P2P_FUSED_UPDATE=0: the update in its own launch (the A/B baseline); same fault injection as all_reduce
+        if (fused_reduce_ && fused_update_ && use_p2p(src.ld + 2)) {
+            const bool skip = fault_call_ > 0 && ++calls_ >= fault_call_;
+            launch_p2p_reduce_allreduce(src, out, args_, rank_, n_, ++epoch_, cap_, err_, timeout_s_, stream, skip,
+                                        &upd);
+            return true;
+        }
+        reduce_all_reduce(src, out, stream);
+        return false;
     }
     bool graph_capturable() const override { return !active_ && base_->graph_capturable(); }  // epoch is an argument
     void abort() override {
@@ -509,6 +521,7 @@ class P2pComm final : public Communicator {
     unsigned* tail_[kP2pMaxRanks] = {};  // {err, abort} words of every rank as mapped here
     unsigned epoch_ = 0;
     bool fused_reduce_ = true;  // reduce_all_reduce in one kernel
+    bool fused_update_ = true;  // ... with the sweep's decision and update (reduce_all_reduce_update)
 };
 
 }  // namespace

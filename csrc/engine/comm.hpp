@@ -39,6 +39,14 @@ class Communicator {
     // The single-frame engine's per-sweep collective: out[0, ld + 2) = the ReduceSrc vector (launchers.hpp), summed
     // over the ranks. Default: launch_reduce_partials, then all_reduce; p2p: one kernel forms and pushes the vector.
     virtual void reduce_all_reduce(const ReduceSrc& src, float* out, hipStream_t stream);
+    // reduce_all_reduce, and where the backend can, the decision and update of the sweep in the same launch
+    // (p2p: launch_p2p_reduce_allreduce with UpdateArgs). Returns true when the update ran; false: the caller runs
+    // launch_decide_update on out (default).
+    virtual bool reduce_all_reduce_update(const ReduceSrc& src, float* out, const UpdateArgs& upd, hipStream_t stream) {
+        (void)upd;
+        reduce_all_reduce(src, out, stream);
+        return false;
+    }
     // Device collectives may be captured into a HIP graph.
     virtual bool graph_capturable() const { return false; }
     // Tear down after a fatal error so that peers blocked in a collective fail instead of hanging.

@@ -398,16 +398,29 @@ void Engine::sweep() {
                        x_.get(), pen_.get(), st, stream_);
         pen = pen_.get();
     }
+    bool updated = false;
     if (comm_->size() > 1) {  // [0, ld) corrections, [ld] ||A x||^2, [ld + 1] error word: one collective
-        comm_begin();          // (p2p: formed from the partial rows and pushed by one kernel)
-        comm_->reduce_all_reduce(ReduceSrc{partial_.get(), ld_, nsplit, scale, Fpart_.get(), nF, st}, comm_buf_.get(),
-                                 stream_);
+        comm_begin();          // (p2p: formed from the partial rows, pushed, and the update applied by one kernel)
+        UpdateArgs u;
+        u.st = st;
+        u.x = x_.get();
+        u.O = O_.get();
+        u.pen = pen;
+        u.alpha = (float)cfg_.relaxation;
+        u.n = V_;
+        u.xcnt = xcnt;
+        u.xprev = xprev_.get();
+        u.ticket = ticket_.get();
+        u.logmode = cfg_.logarithmic;
+        updated = comm_->reduce_all_reduce_update(ReduceSrc{partial_.get(), ld_, nsplit, scale, Fpart_.get(), nF, st},
+                                                  comm_buf_.get(), u, stream_);
         comm_end();
     } else if (!one_tail) {
         launch_reduce_partials(partial_.get(), ld_, nsplit, scale, comm_buf_.get(), Fpart_.get(), nF, Fslot, st,
                                stream_);
     }
-    if (one_tail)
+    if (updated) {
+    } else if (one_tail)
         launch_reduce_decide_update(cfg_.logarithmic, st, partial_.get(), ld_, nsplit, scale, Fpart_.get(), nF,
                                     x_.get(), O_.get(), pen, (float)cfg_.relaxation, V_, xcnt, xprev_.get(),
                                     ticket_.get(), stream_);

@@ -140,11 +140,28 @@ struct ReduceSrc {
     int64_t nF = 0;
     const SartState* st = nullptr;
 };
+// The SART update after the per-sweep all-reduce (launch_decide_update's operands), for the P2P kernel's fused tail
+struct UpdateArgs {
+    SartState* st = nullptr;
+    float* x = nullptr;
+    const float* O = nullptr;    // log mode: the observed back-projection
+    const float* pen = nullptr;  // optional
+    float alpha = 1.f;
+    int64_t n = 0;               // voxels
+    unsigned* xcnt = nullptr;    // optional: per-XCD tickets of the next fused sweep, zeroed here
+    float* xprev = nullptr;      // optional: the iterate before the update (NaN/Inf rollback point)
+    unsigned* ticket = nullptr;  // the last workgroup to arrive writes the new state
+    bool logmode = false;
+};
 // launch_reduce_partials + launch_p2p_allreduce (sum) of its ld + 2 floats in ONE kernel: each workgroup forms its
 // chunk of v in registers and pushes it. out (ld + 2 floats) receives the all-reduced v, bitwise the two-launch result.
+// upd (optional): also launch_decide_update in the same kernel -- every workgroup takes ||A x||^2 and the error word
+// from the tail slots of all ranks (its own rank's tail computed locally), decides, and updates its chunk's voxels
+// (x, state and xprev bitwise those of the separate launch). At N > 1 a SART iteration is then the sweep plus this
+// one kernel, as at N = 1 (k_reduce_decide_update).
 void launch_p2p_reduce_allreduce(const ReduceSrc& src, float* out, const P2pArgs& a, int rank, int nranks,
                                  unsigned epoch, int64_t cap, unsigned* err, double timeout_s, hipStream_t stream,
-                                 bool skip_flags = false);
+                                 bool skip_flags = false, const UpdateArgs* upd = nullptr);
 // multiframe.hip (nf = frames per batch: 16, 32 or 64; the 16-bit kernels of multiframe_bf16.hip also take 128)
 // target: workgroups to aim for (0: 1024, or SART_MF_FWD_BLOCKS)
 int mf_forward_num_splits(int64_t ld, int64_t nrows_pad, int target = 0);

@@ -28,13 +28,38 @@ namespace {
 
 __device__ inline float red(float a, float b, int op) { return op == 0 ? a + b : fmaxf(a, b); }
 
+// Poll flag f (>= epoch) as one lane, bounded by the timeout and this rank's abort word; true on arrival.
+__device__ inline bool p2p_wait_flag(const unsigned* f, unsigned epoch, const unsigned* abort_word,
+                                     uint64_t timeout_ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks ||
+            __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+            return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+
 // `in` may alias `out` (in place): each element is read in phase 1 and written in phase 2 by one thread.
 // RED: there is no `in`; phase 1 forms the pushed values from src in k_reduce_partials' summation order (n = ld + 2).
-template <bool RED>
+// UPD (RED only; 1 linear, 2 log): launch_decide_update fused in (launchers.hpp UpdateArgs): the state is read
+// before anything else, ||A x||^2 and the error word of every rank come from the tail chunk's slots (this rank's own
+// computed here, in the tail workgroup's order), the decision is decide_next's, the update that of
+// k_reduce_decide_update, and the last workgroup to take the ticket writes the new state.
+template <bool RED, int UPD = 0>
 __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* out, int64_t n, int64_t chunk,
                                                        P2pArgs a, int rank, int nranks, unsigned epoch, int parity,
                                                        int64_t cap, int op, unsigned* err, uint64_t timeout_ticks,
-                                                       int vec_io, int skip_flags, ReduceSrc src) {
+                                                       int vec_io, int skip_flags, ReduceSrc src, UpdateArgs u) {
+#pragma clang fp contract(off)
+    static_assert(UPD == 0 || RED, "the fused update follows the reduce + all-reduce");
+    __shared__ SartState s_next;
+    __shared__ int s_apply;
+    if constexpr (UPD != 0) {
+        if (threadIdx.x == 0) s_next = *u.st;  // before this workgroup's ticket (taken last)
+        if (u.xcnt && blockIdx.x == 0 && threadIdx.x < 16) u.xcnt[threadIdx.x] = 0u;  // see k_update_linear
+    }
     const int64_t c0 = (int64_t)blockIdx.x * chunk;
     const int64_t c1 = c0 + chunk < n ? c0 + chunk : n;
     // After a timeout on this rank the device path is being abandoned (the engines agree on it after the solve and
@@ -47,6 +72,17 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
     __syncthreads();
     if (err0 != 0) {
         for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) out[i] = __builtin_nanf("");
+        if constexpr (UPD != 0) {  // as the separate update on this NaN output: the NaN guard stops the frame (the
+            if (threadIdx.x == 0) {  // engines re-solve it on the base communicator); state and ticket as usual
+                const float F[2] = {__builtin_nanf(""), 0.f};
+                decide_next(s_next, F);
+                const unsigned tk = atomicAdd(u.ticket, 1u);
+                if (tk == gridDim.x - 1) {
+                    *u.st = s_next;
+                    *u.ticket = 0u;
+                }
+            }
+        }
         return;
     }
     const int64_t mine = (int64_t)(parity * kP2pMaxRanks + rank) * cap;  // my slot in every receive buffer
@@ -54,7 +90,7 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
     // RED: the chunk holding [ld] and [ld + 1] (never split: chunks are multiples of 1024, ld of 64) sums Fpart first
     __shared__ float tailv[2];
     if constexpr (RED) {
-        if (c0 <= src.ld && src.ld < c1) {  // uniform over the workgroup
+        if (UPD != 0 || (c0 <= src.ld && src.ld < c1)) {  // uniform over the workgroup
             __shared__ double red4[4];
             double acc = 0.0;
             for (int64_t i = threadIdx.x; i < src.nF; i += 256) acc += src.Fpart[i];
@@ -119,18 +155,16 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
 
-    // phase 2: wait for this chunk from every peer, then reduce the N local slots in rank order
+    // phase 2: wait for this chunk from every peer, then reduce the N local slots in rank order. UPD: also for the
+    // tail chunk (||A x||^2 and the error word of every peer) when this is not the tail chunk's workgroup.
+    const int64_t tail_blk = RED ? src.ld / chunk : 0;
     if ((int)threadIdx.x < nranks && (int)threadIdx.x != rank) {
         const unsigned* f = a.flags[rank] + threadIdx.x * kP2pMaxBlocks + blockIdx.x;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks ||
-                __hip_atomic_load(a.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
-                timed_out = 1;  // a peer is gone (timeout) or told us it aborted
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
+        bool ok = p2p_wait_flag(f, epoch, a.abort_word, timeout_ticks);
+        if (UPD != 0 && ok && tail_blk != (int64_t)blockIdx.x)
+            ok = p2p_wait_flag(a.flags[rank] + threadIdx.x * kP2pMaxBlocks + tail_blk, epoch, a.abort_word,
+                               timeout_ticks);
+        if (!ok) timed_out = 1;  // a peer is gone (timeout) or told us it aborted
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -139,7 +173,32 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
     if (timed_out) {
         if (threadIdx.x == 0) atomicOr(err, 1u);
         for (int64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) out[i] = __builtin_nanf("");
+        if constexpr (UPD != 0) {  // non-finite ||A x||^2: the NaN guard stops the frame (decide_next advances the
+            if (threadIdx.x == 0) {  // sweep and epoch as on any NaN); the engines re-solve it
+                const float F[2] = {__builtin_nanf(""), 0.f};
+                decide_next(s_next, F);
+                const unsigned tk = atomicAdd(u.ticket, 1u);
+                if (tk == gridDim.x - 1) {
+                    *u.st = s_next;
+                    *u.ticket = 0u;
+                }
+            }
+        }
         return;
+    }
+    if constexpr (UPD != 0) {  // {||A x||^2, error word}: the tail slots of every rank summed in rank order
+        if (threadIdx.x == 0) {
+            float F[2];
+            for (int k = 0; k < 2; ++k) {
+                auto slot = [&](int r) { return r == rank ? tailv[k] : base[(int64_t)r * cap + src.ld + k]; };
+                float t = slot(0);
+                for (int r = 1; r < nranks; ++r) t = t + slot(r);
+                F[k] = t;
+            }
+            decide_next(s_next, F);
+            s_apply = !s_next.done;
+        }
+        __syncthreads();
     }
     for (int64_t i = c0 + 4 * (int64_t)threadIdx.x; i < c1; i += 4 * (int64_t)blockDim.x) {
         if (i + 4 <= c1) {
@@ -156,11 +215,47 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
             } else {
                 out[i] = s.x, out[i + 1] = s.y, out[i + 2] = s.z, out[i + 3] = s.w;
             }
+            if constexpr (UPD != 0) {  // i + 4 <= ld here (the chunk's short tail holds [ld, ld + 2) only)
+                if (s_apply && i < u.n) {
+                    const float dv[4] = {s.x, s.y, s.z, s.w};
+                    float x0[4], o[4] = {0.f, 0.f, 0.f, 0.f}, pn[4] = {0.f, 0.f, 0.f, 0.f}, t[4];
+                    const float4 xv = *reinterpret_cast<const float4*>(u.x + i);
+                    x0[0] = xv.x, x0[1] = xv.y, x0[2] = xv.z, x0[3] = xv.w;
+                    if constexpr (UPD == 2) {
+                        const float4 ov = *reinterpret_cast<const float4*>(u.O + i);
+                        o[0] = ov.x, o[1] = ov.y, o[2] = ov.z, o[3] = ov.w;
+                    }
+                    if (u.pen) {
+                        const float4 pv = *reinterpret_cast<const float4*>(u.pen + i);
+                        pn[0] = pv.x, pn[1] = pv.y, pn[2] = pv.z, pn[3] = pv.w;
+                    }
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) t[c] = sart_update_voxel<UPD == 2>(x0[c], dv[c], o[c], u.pen, pn[c], u.alpha);
+                    if (i + 4 <= u.n) {
+                        if (u.xprev) *reinterpret_cast<float4*>(u.xprev + i) = xv;
+                        *reinterpret_cast<float4*>(u.x + i) = make_float4(t[0], t[1], t[2], t[3]);
+                    } else {
+                        for (int c = 0; c < 4 && i + c < u.n; ++c) {
+                            if (u.xprev) u.xprev[i + c] = x0[c];
+                            u.x[i + c] = t[c];
+                        }
+                    }
+                }
+            }
         } else {
             for (int64_t k = i; k < c1; ++k) {
                 float s = base[k];
                 for (int r = 1; r < nranks; ++r) s = red(s, base[(int64_t)r * cap + k], op);
                 out[k] = s;
+            }
+        }
+    }
+    if constexpr (UPD != 0) {
+        if (threadIdx.x == 0) {
+            const unsigned tk = atomicAdd(u.ticket, 1u);  // after this workgroup's read of the state (kernel start)
+            if (tk == gridDim.x - 1) {
+                *u.st = s_next;
+                *u.ticket = 0u;
             }
         }
     }
@@ -192,13 +287,13 @@ void launch_p2p_allreduce(const float* in, float* out, int64_t n, const P2pArgs&
     const uint64_t ticks = (uint64_t)(timeout_s * 1e8);  // s_memrealtime: 100 MHz
     hipLaunchKernelGGL(k_p2p_allreduce<false>, dim3((unsigned)blocks), dim3(256), 0, stream, in, out, n, chunk, a,
                        rank, nranks, epoch, (int)(epoch & 1u), cap, op, err, ticks, vec_io, skip_flags ? 1 : 0,
-                       ReduceSrc{});
+                       ReduceSrc{}, UpdateArgs{});
     check_launch("k_p2p_allreduce");
 }
 
 void launch_p2p_reduce_allreduce(const ReduceSrc& src, float* out, const P2pArgs& a, int rank, int nranks,
                                  unsigned epoch, int64_t cap, unsigned* err, double timeout_s, hipStream_t stream,
-                                 bool skip_flags) {
+                                 bool skip_flags, const UpdateArgs* upd) {
     const int64_t n = src.ld + 2;
     const bool aligned = ((reinterpret_cast<uintptr_t>(src.partial) | reinterpret_cast<uintptr_t>(src.scale) |
                            reinterpret_cast<uintptr_t>(out)) % 16) == 0;
@@ -210,8 +305,24 @@ void launch_p2p_reduce_allreduce(const ReduceSrc& src, float* out, const P2pArgs
     const int64_t blocks = (n + chunk - 1) / chunk;
     if (blocks > kP2pMaxBlocks) throw std::runtime_error("launch_p2p_reduce_allreduce: too many chunks");
     const uint64_t ticks = (uint64_t)(timeout_s * 1e8);
+    if (upd) {
+        const UpdateArgs& u = *upd;
+        if (!u.st || !u.x || !u.ticket || (u.logmode && !u.O) || u.n > src.ld ||
+            ((reinterpret_cast<uintptr_t>(u.x) | reinterpret_cast<uintptr_t>(u.O) | reinterpret_cast<uintptr_t>(u.pen) |
+              reinterpret_cast<uintptr_t>(u.xprev)) % 16) != 0)
+            throw std::runtime_error("launch_p2p_reduce_allreduce: bad update arguments");
+        auto run = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream, nullptr, out, n, chunk, a, rank, nranks,
+                               epoch, (int)(epoch & 1u), cap, 0, err, ticks, 1, skip_flags ? 1 : 0, src, u);
+        };
+        if (u.logmode) run(k_p2p_allreduce<true, 2>);
+        else run(k_p2p_allreduce<true, 1>);
+        check_launch("k_p2p_reduce_allreduce (fused update)");
+        return;
+    }
     hipLaunchKernelGGL(k_p2p_allreduce<true>, dim3((unsigned)blocks), dim3(256), 0, stream, nullptr, out, n, chunk, a,
-                       rank, nranks, epoch, (int)(epoch & 1u), cap, 0, err, ticks, 1, skip_flags ? 1 : 0, src);
+                       rank, nranks, epoch, (int)(epoch & 1u), cap, 0, err, ticks, 1, skip_flags ? 1 : 0, src,
+                       UpdateArgs{});
     check_launch("k_p2p_reduce_allreduce");
 }
 

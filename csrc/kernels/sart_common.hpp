@@ -166,4 +166,76 @@ void check_launch(const char* what);
 // Checked HIP runtime call (throws std::runtime_error with `what` and the HIP error string).
 void hip_call(hipError_t e, const char* what);
 
+constexpr float kEpsLog = 1e-7f;  // reference EPSILON_LOG_CUDA (sart_kernels.cu:17-19)
+
+// Single lane. Consumes ||A x_s||^2 of sweep s and decides, exactly as the reference loop does
+// at its iteration s-1 (its forward projection after the update is our next sweep's forward).
+// Fslot[1] is the error word of the sweep, summed over the ranks by the same collective that carries
+// ||A x||^2 (k_reduce_partials writes the local SartState::error there): when ANY rank's persistent sweep
+// gave up, every rank stops the frame at this sweep and sees error bit 8, so the fallback decision is
+// identical on all ranks (a rank-local decision would leave its peers waiting in the next collective).
+// The decision on a copy of the state (shared by k_decide and k_decide_update): a pure function of the state
+// before the sweep and of the sweep's reduced Fslot, so every workgroup that evaluates it gets the same answer.
+__device__ inline void decide_next(SartState& st, const float* __restrict__ Fslot) {
+    if (st.done) return;
+    const int s = st.sweep;
+    const double F = (double)Fslot[0];
+    st.F_last = F;
+    int done = 0;
+    int status = kRunning;
+    if (Fslot[1] != 0.f) {
+        st.error |= 8;
+        st.sweep = s + 1;
+        st.status = kMaxIterationsExceeded;
+        st.done = 1;
+        st.epoch = st.epoch + 1;
+        return;
+    }
+    if (!isfinite(F)) {
+        // NaN/Inf guard: x_s produced a non-finite ||A x||^2. Stop; the engine returns the
+        // last finite iterate x_{s-1}, which the update kernels saved in xprev, so s - 1 updates count.
+        st.flags |= 1;
+        st.iterations = s > 0 ? s - 1 : 0;
+        st.sweep = s + 1;
+        st.status = kMaxIterationsExceeded;
+        st.done = 1;
+        st.epoch = st.epoch + 1;
+        return;
+    }
+    if (s >= 1) {
+        const double conv = (st.G - F) / st.G;
+        if (s >= 2 && fabs(conv - st.conv_prev) < st.tol) {
+            done = 1;
+            status = kSuccess;
+        }
+        st.conv_prev = conv;
+        st.conv_last = conv;
+    }
+    if (!done && s >= st.max_iter) {
+        done = 1;
+        status = kMaxIterationsExceeded;
+    }
+    st.iterations = done ? s : s + 1;
+    st.sweep = s + 1;
+    st.status = status;
+    st.done = done;
+    st.epoch = st.epoch + 1;
+}
+
+// One voxel's SART update (k_decide_update, k_reduce_decide_update, the P2P kernel's fused update: one definition, so
+// every path rounds the same way; callers compile it with contraction off)
+template <bool LOGV>
+__device__ __forceinline__ float sart_update_voxel(float x0, float d, float o, const float* pen, float pn, float alpha) {
+#pragma clang fp contract(off)
+    if constexpr (LOGV) {
+        float r = powf((o + kEpsLog) / (d + kEpsLog), alpha);
+        if (pen) r *= expf(-pn);
+        return x0 * r;
+    } else {
+        float v = x0 + d;
+        if (pen) v -= pn;
+        return (v > 0.f) ? v : 0.f;
+    }
+}
+
 }  // namespace sart

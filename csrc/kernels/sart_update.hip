@@ -22,7 +22,6 @@
 
 namespace sart {
 
-constexpr float kEpsLog = 1e-7f;  // reference EPSILON_LOG_CUDA (sart_kernels.cu:17-19)
 
 // ghat = fp32(g / s); a = [ghat >= 0][len > tau_l] / len; gpos = max(ghat, 0); wo = a * ghat
 // A non-finite pixel (NaN / Inf from a broken detector channel) is masked like a saturated one (g < 0):
@@ -81,59 +80,7 @@ __global__ __launch_bounds__(256) void k_penalty_csr(const int64_t* __restrict__
     pen[i] = beta * acc;
 }
 
-// Single lane. Consumes ||A x_s||^2 of sweep s and decides, exactly as the reference loop does
-// at its iteration s-1 (its forward projection after the update is our next sweep's forward).
-// Fslot[1] is the error word of the sweep, summed over the ranks by the same collective that carries
-// ||A x||^2 (k_reduce_partials writes the local SartState::error there): when ANY rank's persistent sweep
-// gave up, every rank stops the frame at this sweep and sees error bit 8, so the fallback decision is
-// identical on all ranks (a rank-local decision would leave its peers waiting in the next collective).
-// The decision on a copy of the state (shared by k_decide and k_decide_update): a pure function of the state
-// before the sweep and of the sweep's reduced Fslot, so every workgroup that evaluates it gets the same answer.
-__device__ void decide_next(SartState& st, const float* __restrict__ Fslot) {
-    if (st.done) return;
-    const int s = st.sweep;
-    const double F = (double)Fslot[0];
-    st.F_last = F;
-    int done = 0;
-    int status = kRunning;
-    if (Fslot[1] != 0.f) {
-        st.error |= 8;
-        st.sweep = s + 1;
-        st.status = kMaxIterationsExceeded;
-        st.done = 1;
-        st.epoch = st.epoch + 1;
-        return;
-    }
-    if (!isfinite(F)) {
-        // NaN/Inf guard: x_s produced a non-finite ||A x||^2. Stop; the engine returns the
-        // last finite iterate x_{s-1}, which the update kernels saved in xprev, so s - 1 updates count.
-        st.flags |= 1;
-        st.iterations = s > 0 ? s - 1 : 0;
-        st.sweep = s + 1;
-        st.status = kMaxIterationsExceeded;
-        st.done = 1;
-        st.epoch = st.epoch + 1;
-        return;
-    }
-    if (s >= 1) {
-        const double conv = (st.G - F) / st.G;
-        if (s >= 2 && fabs(conv - st.conv_prev) < st.tol) {
-            done = 1;
-            status = kSuccess;
-        }
-        st.conv_prev = conv;
-        st.conv_last = conv;
-    }
-    if (!done && s >= st.max_iter) {
-        done = 1;
-        status = kMaxIterationsExceeded;
-    }
-    st.iterations = done ? s : s + 1;
-    st.sweep = s + 1;
-    st.status = status;
-    st.done = done;
-    st.epoch = st.epoch + 1;
-}
+// decide_next: sart_common.hpp (shared with the P2P all-reduce's fused update, p2p_allreduce.hip)
 
 __global__ void k_decide(SartState* __restrict__ st, const float* __restrict__ Fslot) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -264,19 +211,7 @@ __global__ __launch_bounds__(256) void k_reduce_decide_update(SartState* __restr
     __syncthreads();
     if (s_apply && mine) {
 #pragma unroll
-        for (int c = 0; c < VEC; ++c) {
-            float v;
-            if constexpr (LOGV) {
-                float r = powf((o[c] + kEpsLog) / (d[c] + kEpsLog), alpha);
-                if (pen) r *= expf(-pn[c]);
-                v = x0[c] * r;
-            } else {
-                v = x0[c] + d[c];
-                if (pen) v -= pn[c];
-                v = (v > 0.f) ? v : 0.f;
-            }
-            t[c] = v;
-        }
+        for (int c = 0; c < VEC; ++c) t[c] = sart_update_voxel<LOGV>(x0[c], d[c], LOGV ? o[c] : 0.f, pen, pen ? pn[c] : 0.f, alpha);
         if (VEC == 4 && i0 + 4 <= n) {
             if (xprev) *reinterpret_cast<float4*>(xprev + i0) = make_float4(x0[0], x0[1], x0[2], x0[3]);
             *reinterpret_cast<float4*>(x + i0) = make_float4(t[0], t[1], t[2], t[3]);

@@ -246,19 +246,27 @@ def test_fused_sweep_on_shared_gpu(tmp_path, nproc):
     assert max(e1, e2) <= RANK_FACTOR * e32 + 1e-7, (e1, e2, e32)
 
 
-@pytest.mark.parametrize("shape", [["--tol", "0"], FUSED_SHAPE, FUSED_SHAPE + ["--logarithmic"]])
+@pytest.mark.parametrize("shape", [["--tol", "0"], ["--tol", "1e-5", "--logarithmic"], FUSED_SHAPE,
+                                   FUSED_SHAPE + ["--logarithmic"], ["--npix", "4096", "--nvox", "65536"]])
 def test_p2p_fused_reduce_is_bitwise(tmp_path, shape):
     """At N > 1 the P2P kernel forms the per-sweep vector from the partial rows itself (one launch instead of
-    k_reduce_partials + the all-reduce): x, status and iterations are bitwise those of the two-launch path
-    (SART_P2P_FUSED_REDUCE=0), on the two-pass and the fused sweep."""
+    k_reduce_partials + the all-reduce) and, by default, also decides and updates x (one launch instead of three:
+    every workgroup takes ||A x||^2 from the tail slots of all ranks). x, status and iterations are bitwise those of
+    the three-launch path (SART_P2P_FUSED_REDUCE=0) and of the two-launch one (SART_P2P_FUSED_UPDATE=0), on the
+    two-pass and the fused sweep, with and without the convergence test (the last case: 65 workgroups)."""
     env = dict(SART_P2P="1", SART_FUSED_SHARED="1")
-    xa, ma = _run(2, str(tmp_path / "a"), shape, SART_P2P_FUSED_REDUCE="0", **env)
-    xb, mb = _run(2, str(tmp_path / "b"), shape, SART_P2P_FUSED_REDUCE="1", **env)
-    for m in (ma, mb):
+    runs = {}
+    for tag, extra in (("three", dict(SART_P2P_FUSED_REDUCE="0")), ("two", dict(SART_P2P_FUSED_UPDATE="0")),
+                       ("one", {})):
+        runs[tag] = _run(2, str(tmp_path / tag), shape, **env, **extra)
+    for x, m in runs.values():
         assert m[0]["comm"] == "p2p" and m[0]["x_bitwise_equal"]
-    for a, b in zip(ma, mb):
-        assert a["status"] == b["status"] and a["iterations"] == b["iterations"]
-    assert np.array_equal(xa, xb)
+    xa, ma = runs["three"]
+    for tag in ("two", "one"):
+        xb, mb = runs[tag]
+        for a, b in zip(ma, mb):
+            assert a["status"] == b["status"] and a["iterations"] == b["iterations"], (tag, a, b)
+        assert np.array_equal(xa, xb), tag
 
 
 @pytest.mark.parametrize("fused", [False, True])

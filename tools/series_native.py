@@ -161,6 +161,8 @@ def main():
         load, fr, wall, loop_s, _ = drive(run, argv)
         ms = [x["ms"] for x in fr]
         rec = dict(base, run=run, process_wall_s=round(wall, 2), load_s=round(load.get("load_s", 0), 2),
+                   load_GBps=round(load.get("load_GBps", 0), 2), load_rss_growth_MB=load.get("rss_growth_MB_max"),
+                   load_staging_MB=load.get("rank0", {}).get("staging_MB"),
                    loop_s=loop_s, frames_per_s=round(len(fr) / loop_s, 2) if loop_s else None,
                    processed_ms={"mean": round(float(np.mean(ms)), 3), "p50": round(pct(ms, 50), 3),
                                  "p90": round(pct(ms, 90), 3), "p99": round(pct(ms, 99), 3),
