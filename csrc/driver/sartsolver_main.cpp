@@ -80,13 +80,16 @@ struct DeviceShard {
 
 // Load-path observability (--profile's first line): wall time of the whole load, the summed HDF5 read time of the
 // reader, the summed GPU time of the host -> HBM copies, the time the copy loop waited for a read (read-bound) and for
-// a staging buffer to drain (copy-bound), and the resident-set high-water mark before / after (the loader's own host
-// memory is the two pinned staging blocks). With the double buffer working, wall ~ max(read, h2d) + one block.
+// a staging buffer to drain (copy-bound), and the resident-set high-water mark before / after, the baseline taken after
+// the HIP runtime's one-time set-up (the loader's own host memory is the two pinned staging blocks). With the double
+// buffer working, wall ~ max(read, h2d) + one block.
 struct LoadStats {
     // setup_s: device allocation, pinned staging and opening the files (before the first block read)
     double wall_s = 0, setup_s = 0, read_s = 0, h2d_s = 0, wait_read_s = 0, wait_copy_s = 0;
     uint64_t bytes = 0, blocks = 0, rows_per_block = 0, staging_bytes = 0, rows_per_read = 0;
     double rss_hwm_before_mb = 0, rss_hwm_after_mb = 0, rss_after_setup_mb = 0, rss_after_first_read_mb = 0;
+    // setup checkpoints (VmHWM, MiB): after the device allocation, after its zero fill, after the pinned staging
+    double rss_after_malloc_mb = 0, rss_after_memset_mb = 0, rss_after_pinned_mb = 0;
 };
 
 double rss_hwm_mb() {  // VmHWM of this process, MiB (0 where /proc is unavailable)
@@ -106,7 +109,24 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
                                                uint64_t col0 = 0, uint64_t ncols = 0, bool bf16 = false,
                                                LoadStats* stats = nullptr) {
     LoadStats ls;
-    hip_ok(hipFree(nullptr), "hipFree");  // the HIP runtime's own footprint is not the loader's
+    // The HIP runtime's one-time host footprint is not the loader's: its first kernel launch (code objects, device
+    // queues: ~0.4 GB of resident memory on the MI355X box), its first pitched host -> device copy and the copy
+    // stream itself (~0.19 GB: the stream's device queue) are paid here, before the baseline is taken
+    // (profiles/load_r5_rss_checkpoints*.jsonl); what the load adds after it is the loader's own memory.
+    hip_ok(hipFree(nullptr), "hipFree");
+    hipStream_t s;
+    hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    {
+        void* d = nullptr;
+        float* h = nullptr;
+        hip_ok(hipMalloc(&d, 1 << 20), "hipMalloc(warm-up)");
+        hip_ok(hipHostMalloc(reinterpret_cast<void**>(&h), 4096), "hipHostMalloc(warm-up)");
+        hip_ok(hipMemsetAsync(d, 0, 1 << 20, s), "hipMemset(warm-up)");
+        hip_ok(hipMemcpy2DAsync(d, 4096, h, 1024, 1024, 4, hipMemcpyHostToDevice, s), "hipMemcpy2D(warm-up)");
+        hip_ok(hipStreamSynchronize(s), "warm-up sync");
+        (void)hipHostFree(h);
+        (void)hipFree(d);
+    }
     ls.rss_hwm_before_mb = rss_hwm_mb();
     const auto t_load = std::chrono::steady_clock::now();
     auto sh = std::make_unique<DeviceShard>();
@@ -118,8 +138,11 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
     sh->nrows_pad = (sh->nrows + 63) / 64 * 64;
     const size_t bytes = (size_t)sh->nrows_pad * sh->ld * (bf16 ? sizeof(bf16_t) : sizeof(float));
     hip_ok(hipMalloc(&sh->A, bytes), "hipMalloc(RTM shard)");
-    hip_ok(hipMemset(sh->A, 0, bytes), "hipMemset(RTM shard)");
-    hip_ok(hipDeviceSynchronize(), "hipMemset sync");
+    ls.rss_after_malloc_mb = rss_hwm_mb();
+    // on the copy stream: a fill on the null stream would bring up that stream's device queue (~0.19 GB resident)
+    hip_ok(hipMemsetAsync(sh->A, 0, bytes, s), "hipMemset(RTM shard)");
+    hip_ok(hipStreamSynchronize(s), "hipMemset sync");
+    ls.rss_after_memset_mb = rss_hwm_mb();
     const uint64_t V = ncols;  // staging row length: the column window only
     RtmReader reader(in.rtm_files, in.rtm_name, in.nvoxel, col0, col0 + ncols);
     if (const char* e = std::getenv("SART_RTM_ROWS_PER_READ"); e && *e) {
@@ -131,11 +154,10 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
     ls.staging_bytes = 2 * rows_per_block * V * sizeof(float);
     float* buf[2] = {nullptr, nullptr};
     for (auto& b : buf) hip_ok(hipHostMalloc(reinterpret_cast<void**>(&b), rows_per_block * V * sizeof(float)), "hipHostMalloc");
+    ls.rss_after_pinned_mb = rss_hwm_mb();
     // bf16: fp32 staging rows [rows_per_block x ld], padding columns zero (the 2-D copies write ncols only)
     DeviceArray<float> stage;
     if (bf16) stage.resize(rows_per_block * (size_t)sh->ld);
-    hipStream_t s;
-    hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
     hipEvent_t ev[2];
     for (auto& e : ev) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
     bool ev_used[2] = {false, false};
@@ -411,6 +433,9 @@ int main(int argc, char** argv) {
                         << ", \"rows_per_read\": " << lstats.rows_per_read
                         << ", \"staging_MB\": " << lstats.staging_bytes / 1048576.0
                         << ", \"rss_hwm_before_MB\": " << lstats.rss_hwm_before_mb
+                        << ", \"rss_hwm_after_malloc_MB\": " << lstats.rss_after_malloc_mb
+                        << ", \"rss_hwm_after_memset_MB\": " << lstats.rss_after_memset_mb
+                        << ", \"rss_hwm_after_pinned_MB\": " << lstats.rss_after_pinned_mb
                         << ", \"rss_hwm_after_setup_MB\": " << lstats.rss_after_setup_mb
                         << ", \"rss_hwm_after_first_read_MB\": " << lstats.rss_after_first_read_mb
                         << ", \"rss_hwm_after_MB\": " << lstats.rss_hwm_after_mb << "}"
