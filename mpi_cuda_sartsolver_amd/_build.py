@@ -153,7 +153,7 @@ def build_native(verbose: bool = True) -> Path:
     LIBDIR.mkdir(parents=True, exist_ok=True)
     srcdir = CSRC / "native"
     headers = sorted(srcdir.glob("*.hpp"))
-    flags = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-Wall", "-Wno-sign-compare",
+    flags = ["-O3", "-std=c++17", "-fPIC", "-fopenmp", "-ffp-contract=off", "-Wall", "-Wno-sign-compare",
              *[f"-I{p}" for p in _py_includes()], f"-I{srcdir}"]
     libs = ["-fopenmp"]
     if hdf5_available():

@@ -58,6 +58,13 @@ for step in "$@"; do
              done; done ;;
     profx3) run rocprof_x3_64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_x3_64" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 &&
             run rocprof_x3_32 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_x3_32" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 32 --iters 20 ;;
+    cfg1) run config1_blocked 300 python tools/cpu_config1.py --ranks 1,4 --out "$OUT/config1.jsonl" &&
+          SART_CPU_TWO_PASS=1 run config1_twopass 300 python tools/cpu_config1.py --ranks 1,4 --out "$OUT/config1_twopass.jsonl" &&
+          run config1_blocked2 300 python tools/cpu_config1.py --ranks 1,4 --gpu --out "$OUT/config1.jsonl" ;;
+    profhead) run rocprof_head 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_head" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 ;;
+    profmf128) for nf in 64 128; do
+              run rocprof_mfx$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 --no-selfcheck || exit 1
+            done ;;
     profmfb) for nf in 16 64; do
               run rocprof_mfb$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 --rtm-dtype bf16 || exit 1
             done ;;
