@@ -355,7 +355,7 @@ int main(int argc, char** argv) {
         if (batched) {
             EngineConfig ec;
             static_cast<SolverParams&>(ec) = params;
-            ec.mf_frames = cfg.batch_frames;  // batch width 16, 32, 64 or 128 (rounded up; 128: split-A fp32 only)
+            ec.mf_frames = cfg.batch_frames;  // batch width 16, 32, 64 or 128 (rounded up; 128: bf16 storage and f16-pair split-A)
             ec.rtm_bf16 = dshard->bf16;       // bf16 MFMA projections
             mf = std::make_unique<MultiFrameEngine>(device, dshard->A, dshard->nrows,
                                                     dshard->nrows_pad, dshard->nvoxel, dshard->ld, dcomm.get(), ec);

@@ -99,12 +99,19 @@ __device__ __forceinline__ floatx4 mfma_h16(const u32x4 a, const u32x4 b, floatx
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8_t, a), __builtin_bit_cast(halfx8_t, b),
                                                   c, 0, 0, 0);
 }
+// Two VALU operations per element: p1 = rne16(a s) and p2 = rne16(a s - p1) are each one v_fma_mix{lo,hi}_f16 (fp32
+// a and s, for p2 an f16 half of p1 as the negated addend; the f16 result goes into one half of the packed register).
+// a s is exact (s is a power of two inside the clamped range) and so is a s - p1 in fp32, so each single rounding to
+// f16 gives the bits of scaling, converting and subtracting separately. Written in C++ the compiler emitted the
+// scale, a v_cvt_pk_f16_f32 and the products again for the residual (7 operations per pair instead of 4), or packed
+// fp32 FMAs and conversions back, which cost more beside MFMAs (MI355X_MICROARCH.md, filler prices).
 __device__ __forceinline__ void split_h2(unsigned x, unsigned y, float s, unsigned& p1, unsigned& p2) {
-    const float a = __uint_as_float(x) * s, b = __uint_as_float(y) * s;
-    const halfx2_t h = {(_Float16)a, (_Float16)b};
-    p1 = __builtin_bit_cast(unsigned, h);
-    const halfx2_t l = {(_Float16)(a - (float)h.x), (_Float16)(b - (float)h.y)};
-    p2 = __builtin_bit_cast(unsigned, l);
+    asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+        "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+        "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(p1), "=&v"(p2)
+        : "v"(__uint_as_float(x)), "v"(__uint_as_float(y)), "v"(s));
 }
 // Forward fragment of an f16-pair split-A wave: eight consecutive fp32 of one row, scaled by the row's s_p
 __device__ __forceinline__ void split_h8(const u32x8 v, float s, u32x4& p1, u32x4& p2) {

@@ -43,7 +43,7 @@ enum Status : int32_t { kSuccess = 0, kMaxIterationsExceeded = -1, kRunning = -2
 
 // Device-resident convergence state of a multi-frame batch (multi-frame solver): one column per frame.
 // A batch holds nf = 16, 32, 64 or 128 frames (the MFMA N dimension is 16; 32 .. 128 use 2 .. 8 column groups;
-// 128 on the split-A path only).
+// 128 on bf16 storage and the f16-pair split-A path; 64 on the fp32 MFMA and bf16 six-product paths).
 constexpr int kMfMaxFrames = 128;
 struct alignas(16) MfState {
     double G[kMfMaxFrames];          // sum_{g>0} g^2 / s^2 per frame

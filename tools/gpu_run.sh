@@ -65,6 +65,27 @@ for step in "$@"; do
     profmf128) for nf in 64 128; do
               run rocprof_mfx$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 --no-selfcheck || exit 1
             done ;;
+    r5mf) for cfg in "64|fp32" "128|fp32" "64|bf16" "128|bf16" "32|fp32"; do
+            nf=${cfg%%|*}; dt=${cfg#*|}
+            run bench_r5_mf${nf}_$dt 300 python bench.py --steps 3 --warmup 1 --frames $nf --rtm-dtype $dt || exit 1
+            grep -h '^{' "$OUT/bench_r5_mf${nf}_$dt.log" >> "$OUT/bench_r5_mf.jsonl"
+          done ;;
+    r52tb) for nf in 64 128; do
+             run bench_r5_2tb_$nf 900 python bench.py --config 2tb --steps 2 --warmup 1 --frames $nf || exit 1
+             grep -h '^{' "$OUT/bench_r5_2tb_$nf.log" >> "$OUT/bench_r5_mf.jsonl"
+           done ;;
+    splitchk) run split_h2_check 120 tools/split_h2_check &&
+              run pytest_mf16 900 python -u -m pytest tests/test_gpu_realistic.py tests/test_gpu_multiframe_bf16.py -m gpu -x -q \
+                -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    abmix)  # split_h2 on v_fma_mix (new) vs the C++ split (.abold), same box, alternating
+      for i in 1 2; do
+        for cfg in "64|" "128|" "64|--config 2tb"; do
+          nf=${cfg%%|*}; ex=${cfg#*|}; tag=${nf}${ex:+_2tb}
+          timeout -k 10 600 python .abold/bench.py --steps 3 --warmup 1 --frames $nf $ex --no-selfcheck > "$OUT/abmix_old_${tag}_$i.log" 2>&1 &&
+          timeout -k 10 600 python bench.py --steps 3 --warmup 1 --frames $nf $ex --no-selfcheck > "$OUT/abmix_new_${tag}_$i.log" 2>&1 || { echo "FATAL $tag"; exit 1; }
+          echo "=== abmix $tag $i old $(grep -h '^{' "$OUT/abmix_old_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"])') new $(grep -h '^{' "$OUT/abmix_new_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
     profmfb) for nf in 16 64; do
               run rocprof_mfb$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 --rtm-dtype bf16 || exit 1
             done ;;
