@@ -292,6 +292,10 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
 #ifndef SART_MF_MINW_BWD
 #define SART_MF_MINW_BWD 1
 #endif
+// A-staged forwards (AS): non-temporal loads of the A tile (A/B builds: -DSART_MF_AS_NT=0)
+#ifndef SART_MF_AS_NT
+#define SART_MF_AS_NT 1
+#endif
 // split-A: X / W of the next step staged into LDS after the step's MFMAs (A/B builds: -DSART_MF_STAGE_LATE=0)
 #ifndef SART_MF_STAGE_LATE
 #define SART_MF_STAGE_LATE 1
@@ -332,6 +336,7 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
     Fout += (int64_t)blockIdx.y * nrows_pad * NF;
     constexpr bool A32 = std::is_same<AT, float>::value;
     constexpr bool LATE = SART_MF_STAGE_LATE && A32;  // stage_next after the MFMAs (split-A only, see below)
+    constexpr bool NT_AS = SART_MF_AS_NT != 0;
     // split-A: lane (r, g) loads voxels 4 g .. 4 g + 3 and 16 + 4 g .. of each 32-voxel block (two contiguous
     // 64-byte halves of a row per instruction instead of four 16-byte pieces); the X planes hold the same k order
     // (k_mf_split_x with perm)
@@ -379,9 +384,14 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
             constexpr int sl = decltype(slc)::value;
             const int64_t q = t * 32 * KB;
             if constexpr (AS) {
+                // full 128-B row segments, 8 rows per instruction: with the non-temporal hint this shape streams at
+                // 6.7 TB/s alone, 5.9-6.0 without (profiles/access_probe_r3.jsonl); A is read once per sweep
 #pragma unroll
-                for (int i = 0; i < NI; ++i)
-                    as_[sl][i] = *reinterpret_cast<const u32x4*>(asp + (int64_t)i * RPI * ld + q);
+                for (int i = 0; i < NI; ++i) {
+                    const u32x4* p = reinterpret_cast<const u32x4*>(asp + (int64_t)i * RPI * ld + q);
+                    if constexpr (NT_AS) as_[sl][i] = __builtin_nontemporal_load(p);
+                    else as_[sl][i] = *p;
+                }
             } else {
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
@@ -1272,6 +1282,12 @@ static void fwd_h16_ng(const FwdTile& tl, dim3 grid, hipStream_t stream, const f
     auto run = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(256), 0, stream, A, ld, nrows, nrows_pad, X1, X2, Fout, cps, g_mf_skip);
     };
+    // SART_MF_H16_FDEPTH=3: a register ring three steps deep for the A-staged tilings (A/B runs)
+    if (tl.as && env_int("SART_MF_H16_FDEPTH", 2) == 3) {
+        if (tl.kb == 2) run(k_mf_forward_b16_lds<NG, 3, 2, 2, float, true, 0, true, true>);
+        else run(k_mf_forward_b16_lds<NG, 3, 2, 1, float, true, 0, true, true>);
+        return;
+    }
     if (tl.kb == 2 && tl.as) run(k_mf_forward_b16_lds<NG, 2, 2, 2, float, true, 0, true, true>);
     else if (tl.kb == 2) run(k_mf_forward_b16_lds<NG, 2, 2, 2, float, false, 0, true, true>);
     else if (tl.as) run(k_mf_forward_b16_lds<NG, 2, 2, 1, float, true, 0, true, true>);

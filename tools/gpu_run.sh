@@ -79,11 +79,22 @@ for step in "$@"; do
                 -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     abmix)  # split_h2 on v_fma_mix (new) vs the C++ split (.abold), same box, alternating
       for i in 1 2; do
-        for cfg in "64|" "128|" "64|--config 2tb"; do
-          nf=${cfg%%|*}; ex=${cfg#*|}; tag=${nf}${ex:+_2tb}
+        for cfg in ${AB_CFGS:-64| 128| 64|--config=2tb}; do  # one token per config: frames|extra-argument
+          nf=${cfg%%|*}; ex=${cfg#*|}; tag=${nf}${ex:+_${ex##*=}}
           timeout -k 10 600 python .abold/bench.py --steps 3 --warmup 1 --frames $nf $ex --no-selfcheck > "$OUT/abmix_old_${tag}_$i.log" 2>&1 &&
           timeout -k 10 600 python bench.py --steps 3 --warmup 1 --frames $nf $ex --no-selfcheck > "$OUT/abmix_new_${tag}_$i.log" 2>&1 || { echo "FATAL $tag"; exit 1; }
           echo "=== abmix $tag $i old $(grep -h '^{' "$OUT/abmix_old_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"])') new $(grep -h '^{' "$OUT/abmix_new_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
+    abdepth)  # register-ring depth of the f16-pair kernels: forward (SART_MF_H16_FDEPTH) / back-projection (SART_MF_X3_DEPTH)
+      for i in 1 2; do
+        for nf in 64 128; do
+          for cfg in "2,2" "3,2" "2,3" "3,3"; do
+            fd=${cfg%%,*}; bd=${cfg#*,}
+            SART_MF_H16_FDEPTH=$fd SART_MF_X3_DEPTH=$bd timeout -k 10 300 python bench.py --steps 3 --warmup 1 --frames $nf --no-selfcheck \
+              > "$OUT/abd_${nf}_${fd}${bd}_$i.log" 2>&1 || { echo "FATAL $nf $cfg"; exit 1; }
+            echo "=== abdepth nf=$nf fwd=$fd bwd=$bd $i $(grep -h '^{' "$OUT/abd_${nf}_${fd}${bd}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"])')" | tee -a "$OUT/session.log"
+          done
         done
       done ;;
     profmfb) for nf in 16 64; do
