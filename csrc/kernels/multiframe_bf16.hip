@@ -1192,7 +1192,9 @@ static FwdTile mf_x3_fwd_tile(int nf, int64_t ld) {
     // profiles/probe_r2_mf_x3.jsonl, profiles/probe_r2_mf_as.jsonl; with blocked X planes (round 4,
     // profiles/probe_r4_mf_x3_fwd_tiles_xblk.jsonl) 64 frames on rows of >= 128k columns take two 32-voxel blocks per
     // step (16384 x 262144: 3.08 against 3.21 ms; 64k x 64k: 2.96 against 2.90, so narrower rows keep one)
-    if (nf == 64) return ld >= 131072 ? FwdTile{2, 2, true, true} : FwdTile{2, 1, true, true};
+    // 32 frames take the A-staged tile too since its loads are non-temporal (+3.2 % at 64k x 64k,
+    // profiles/ab_r5_mf32_as.txt)
+    if (nf == 64 || nf == 32) return ld >= 131072 ? FwdTile{2, 2, true, true} : FwdTile{2, 1, true, true};
     if (nf == 128) return FwdTile{2, 1, true, true};  // 128 frames: one 32-voxel block per step (registers)
     return FwdTile{2, 2, true};
 }

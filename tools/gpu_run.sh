@@ -97,6 +97,16 @@ for step in "$@"; do
           done
         done
       done ;;
+    abenv)  # env-knob A/B on one build: AB_RUNS = "tag|frames|extra-arg|ENV=VAL[;ENV=VAL]" tokens, two rounds
+      for i in 1 2; do
+        for r in $AB_RUNS; do
+          IFS='|' read -r tag nf ex ev <<< "$r"
+          env ${ev//;/ } timeout -k 10 300 python bench.py --steps 3 --warmup 1 --frames $nf $ex --no-selfcheck > "$OUT/abenv_${tag}_$i.log" 2>&1 || { echo "FATAL $tag"; exit 1; }
+          echo "=== abenv $tag $i $(grep -h '^{' "$OUT/abenv_${tag}_$i.log" | python -c 'import sys,json; d=json.loads(sys.stdin.readline()); print(d["iters_per_s"], d["effective_hbm_TBps_per_gpu"])')" | tee -a "$OUT/session.log"
+        done
+      done ;;
+    prof64) run rocprof_mfx64b 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx64b" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --no-selfcheck &&
+            run rocprof_2tb64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_2tb64" -o run --output-format csv -- python3 bench.py --config 2tb --steps 1 --warmup 0 --frames 64 --no-selfcheck ;;
     profmfb) for nf in 16 64; do
               run rocprof_mfb$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 --rtm-dtype bf16 || exit 1
             done ;;
