@@ -296,6 +296,25 @@ PYBIND11_MODULE(_sart_native, m) {
         return out;
     });
 
+    // one read of A per iteration (the --use_cpu sweep): returns (f, out, sum f^2)
+    m.def("cpu_sweep", [](py::array_t<float, py::array::c_style> A, int64_t P, int64_t V, f64arr x, f64arr g, f64arr a,
+                          bool logmode) {
+        auto bi = A.request();
+        check_rows(bi, P, V, bi.ndim == 2 ? bi.shape[1] : 0);
+        if (x.size() < V || g.size() < P || a.size() < P) throw std::invalid_argument("vector too short");
+        py::array_t<double> f(P), out(V);
+        const float* ap = static_cast<const float*>(bi.ptr);
+        const double *xp = x.data(), *gp = g.data(), *arow = a.data();
+        double *fp = f.mutable_data(), *op = out.mutable_data();
+        const int64_t ld = bi.shape[1];
+        double f2;
+        {
+            py::gil_scoped_release nogil;
+            f2 = cpu_sweep(ap, P, V, ld, xp, gp, arow, logmode, fp, op);
+        }
+        return py::make_tuple(f, out, f2);
+    });
+
     // ---------------------------------------------------------------- fixture writers
     m.def(
         "write_rtm_file",

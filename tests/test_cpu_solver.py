@@ -28,6 +28,27 @@ def test_native_cpu_kernels(P, V):
     np.testing.assert_allclose(n.cpu_backproject(Ald, P, V, w), A64.T @ w, rtol=1e-10, atol=1e-12)
 
 
+@pytest.mark.parametrize("P,V", [(1, 1), (5, 3), (67, 129), (300, 1001)])
+@pytest.mark.parametrize("log", [False, True])
+def test_native_cpu_sweep(P, V, log):
+    """The one-read sweep (row blocks, four rows per accumulator pass, zero-weight rows skipped) against numpy:
+    f = A x, w = a f (log) or a (g - f), out = A^T w, sum f^2; ragged shapes and scattered zero weights."""
+    n = native()
+    rng = np.random.default_rng(P + 7 * V)
+    A = rng.random((P, V), dtype=np.float32)
+    Ald = np.zeros((P, V + 3), np.float32)
+    Ald[:, :V] = A
+    A64 = A.astype(np.float64)
+    x, g = rng.random(V), rng.random(P)
+    a = np.where(rng.random(P) < 0.3, 0.0, rng.random(P))  # a = 0 rows (masked / negative pixels) in every block
+    f, out, f2 = n.cpu_sweep(Ald, P, V, x, g, a, log)
+    fr = A64 @ x
+    w = a * fr if log else a * (g - fr)
+    np.testing.assert_allclose(f, fr, rtol=1e-12)
+    assert np.isclose(f2, np.sum(fr ** 2), rtol=1e-12)
+    np.testing.assert_allclose(out, A64.T @ w, rtol=1e-10, atol=1e-12 * max(1.0, np.abs(w).sum()))
+
+
 @pytest.mark.parametrize("log", [False, True])
 @pytest.mark.parametrize("semantics", ["cpu", "gpu"])
 @pytest.mark.parametrize("lap", [False, True])
