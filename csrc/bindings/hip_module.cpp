@@ -193,6 +193,28 @@ static void bind_engine(py::module_& m) {
                  }
              }),
              py::keep_alive<1, 8>())
+        // sparse shard: device pointers of the CSR (row_ptr, col, val) and CSC (col_ptr, row, cval) arrays (not owned:
+        // the caller keeps them alive with the engine)
+        .def_static("from_sparse",
+                    [](int device, uintptr_t row_ptr, uintptr_t col, uintptr_t val, uintptr_t col_ptr, uintptr_t row,
+                       uintptr_t cval, int64_t nnz, int64_t nrows, int64_t nvoxel,
+                       std::shared_ptr<sart::Communicator> comm, const sart::EngineConfig& cfg) {
+                        sart::SparseRtm s;
+                        s.row_ptr = P<const int64_t>(row_ptr);
+                        s.col = P<const int32_t>(col);
+                        s.val = P<const float>(val);
+                        s.col_ptr = P<const int64_t>(col_ptr);
+                        s.row = P<const int32_t>(row);
+                        s.cval = P<const float>(cval);
+                        s.nnz = nnz;
+                        const int64_t pp = (nrows + 63) / 64 * 64, ld = (nvoxel + 63) / 64 * 64;
+                        try {
+                            return new sart::Engine(device, nullptr, nrows, pp, nvoxel, ld, comm.get(), cfg, &s);
+                        } catch (const std::invalid_argument& e) {
+                            throw py::value_error(e.what());
+                        }
+                    },
+                    py::keep_alive<0, 11>())
         .def("set_laplacian",
              [](sart::Engine& e, py::array_t<int64_t, py::array::c_style | py::array::forcecast> rp,
                 py::array_t<int32_t, py::array::c_style | py::array::forcecast> col,
@@ -234,6 +256,8 @@ static void bind_engine(py::module_& m) {
         .def_property_readonly("geometry", &sart::Engine::geometry)
         .def_property_readonly("num_cus", &sart::Engine::num_cus)
         .def_property_readonly("column_shard", &sart::Engine::column_shard)
+        .def_property_readonly("sparse", &sart::Engine::sparse)
+        .def_property_readonly("nnz", &sart::Engine::nnz)
         .def_property_readonly("shared_device", &sart::Engine::shared_device)
         .def_property_readonly("ranks_per_device", &sart::Engine::ranks_per_device)
         .def_property_readonly("plan_cus", &sart::Engine::plan_cus)

@@ -9,6 +9,7 @@
 #include "config.hpp"
 #include "cpu_kernels.hpp"
 #include "cpu_solver.hpp"
+#include "sparse_csr.hpp"
 #include "host_comm.hpp"
 #include "fixtures.hpp"
 #include "frames.hpp"
@@ -72,6 +73,7 @@ PYBIND11_MODULE(_sart_native, m) {
         .def_readwrite("two_pass", &Config::two_pass)
         .def_readwrite("partition_voxels", &Config::partition_voxels)
         .def_readwrite("rtm_bf16", &Config::rtm_bf16)
+        .def_readwrite("rtm_format", &Config::rtm_format)
         .def_readwrite("profile_file", &Config::profile_file)
         .def_readwrite("help", &Config::help);
     m.def("parse_arguments", &parse_arguments, py::arg("argv"));
@@ -295,6 +297,49 @@ PYBIND11_MODULE(_sart_native, m) {
         }
         return out;
     });
+
+    // host CSR of (row, col, value) entries (later duplicates win, zeros dropped) and its transpose (= CSC)
+    m.def("csr_from_entries", [](int64_t nrows, int64_t ncols, py::array_t<int64_t, py::array::c_style | py::array::forcecast> r,
+                                 py::array_t<int32_t, py::array::c_style | py::array::forcecast> c,
+                                 py::array_t<float, py::array::c_style | py::array::forcecast> v) {
+        std::vector<int64_t> rows(r.data(), r.data() + r.size());
+        std::vector<int32_t> cols(c.data(), c.data() + c.size());
+        std::vector<float> vals(v.data(), v.data() + v.size());
+        sart::HostCsr a;
+        try {
+            a = sart::csr_from_entries(nrows, ncols, rows, cols, vals);
+        } catch (const std::invalid_argument& e) {
+            throw py::value_error(e.what());
+        }
+        return py::make_tuple(py::array_t<int64_t>(a.ptr.size(), a.ptr.data()),
+                              py::array_t<int32_t>(a.idx.size(), a.idx.data()),
+                              py::array_t<float>(a.val.size(), a.val.data()));
+    });
+    m.def("csr_transpose", [](int64_t nrows, int64_t ncols, py::array_t<int64_t, py::array::c_style | py::array::forcecast> ptr,
+                              py::array_t<int32_t, py::array::c_style | py::array::forcecast> idx,
+                              py::array_t<float, py::array::c_style | py::array::forcecast> val) {
+        sart::HostCsr a;
+        a.nrows = nrows;
+        a.ncols = ncols;
+        a.ptr.assign(ptr.data(), ptr.data() + ptr.size());
+        a.idx.assign(idx.data(), idx.data() + idx.size());
+        a.val.assign(val.data(), val.data() + val.size());
+        if ((int64_t)a.ptr.size() != nrows + 1 || a.idx.size() != a.val.size() || a.ptr.back() != (int64_t)a.val.size())
+            throw py::value_error("csr_transpose: inconsistent CSR arrays");
+        const sart::HostCsr t = sart::csr_transpose(a);
+        return py::make_tuple(py::array_t<int64_t>(t.ptr.size(), t.ptr.data()),
+                              py::array_t<int32_t>(t.idx.size(), t.idx.data()),
+                              py::array_t<float>(t.val.size(), t.val.data()));
+    });
+    // the RTM rows [r0, r1) of validated inputs as CSR (RtmReader::read_csr)
+    m.def("read_rtm_csr", [](const std::vector<std::string>& files, const std::string& rtm_name, uint64_t r0, uint64_t r1) {
+        const sart::InputSet in = sart::validate_inputs(files, rtm_name, 50.0);
+        sart::RtmReader rd(in.rtm_files, rtm_name, in.nvoxel);
+        const sart::HostCsr a = rd.read_csr(r0, r1);
+        return py::make_tuple(py::array_t<int64_t>(a.ptr.size(), a.ptr.data()),
+                              py::array_t<int32_t>(a.idx.size(), a.idx.data()),
+                              py::array_t<float>(a.val.size(), a.val.data()), a.ncols);
+    }, py::arg("files"), py::arg("rtm_name") = "with_reflections", py::arg("row_begin"), py::arg("row_end"));
 
     // one read of A per iteration (the --use_cpu sweep): returns (f, out, sum f^2)
     m.def("cpu_sweep", [](py::array_t<float, py::array::c_style> A, int64_t P, int64_t V, f64arr x, f64arr g, f64arr a,

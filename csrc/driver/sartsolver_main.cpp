@@ -235,6 +235,68 @@ std::unique_ptr<DeviceShard> load_device_shard(const InputSet& in, uint64_t row0
     return sh;
 }
 
+// Sparse device shard (--rtm_format): the rows' non-zeros as CSR + CSC (csrc/kernels/sparse.hip). Read through
+// RtmReader::read_csr (COO arrays of sparse datasets, non-zeros of dense row blocks), transposed on the host, copied
+// once; host memory is the two CSR copies of the shard, freed after the upload.
+struct DeviceSparseShard {
+    DeviceArray<int64_t> rp, cp;
+    DeviceArray<int32_t> col, row;
+    DeviceArray<float> val, cval;
+    int64_t nrows = 0, nvoxel = 0, nnz = 0;
+    SparseRtm view() const {
+        SparseRtm s;
+        s.row_ptr = rp.get();
+        s.col = col.get();
+        s.val = val.get();
+        s.col_ptr = cp.get();
+        s.row = row.get();
+        s.cval = cval.get();
+        s.nnz = nnz;
+        return s;
+    }
+};
+
+std::unique_ptr<DeviceSparseShard> load_sparse_shard(const InputSet& in, uint64_t row0, uint64_t nrows,
+                                                     LoadStats* stats) {
+    LoadStats ls;
+    hip_ok(hipFree(nullptr), "hipFree");
+    ls.rss_hwm_before_mb = rss_hwm_mb();
+    const auto t0 = std::chrono::steady_clock::now();
+    RtmReader reader(in.rtm_files, in.rtm_name, in.nvoxel);
+    const HostCsr a = reader.read_csr(row0, row0 + nrows);
+    const HostCsr t = csr_transpose(a);
+    ls.read_s = seconds_since(t0);
+    auto sh = std::make_unique<DeviceSparseShard>();
+    sh->nrows = (int64_t)nrows;
+    sh->nvoxel = (int64_t)in.nvoxel;
+    sh->nnz = a.nnz();
+    const size_t n = (size_t)std::max<int64_t>(1, sh->nnz);
+    sh->rp.resize(a.ptr.size());
+    sh->cp.resize(t.ptr.size());
+    sh->col.resize(n);
+    sh->row.resize(n);
+    sh->val.resize(n);
+    sh->cval.resize(n);
+    const auto t1 = std::chrono::steady_clock::now();
+    auto up = [](void* d, const void* h, size_t bytes) {
+        if (bytes) hip_ok(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice), "H2D sparse RTM");
+    };
+    up(sh->rp.get(), a.ptr.data(), a.ptr.size() * sizeof(int64_t));
+    up(sh->cp.get(), t.ptr.data(), t.ptr.size() * sizeof(int64_t));
+    up(sh->col.get(), a.idx.data(), a.idx.size() * sizeof(int32_t));
+    up(sh->val.get(), a.val.data(), a.val.size() * sizeof(float));
+    up(sh->row.get(), t.idx.data(), t.idx.size() * sizeof(int32_t));
+    up(sh->cval.get(), t.val.data(), t.val.size() * sizeof(float));
+    ls.h2d_s = seconds_since(t1);
+    ls.blocks = 1;
+    ls.rows_per_block = nrows;
+    ls.bytes = (uint64_t)sh->nnz * 16 + (a.ptr.size() + t.ptr.size()) * sizeof(int64_t);
+    ls.wall_s = seconds_since(t0);
+    ls.rss_hwm_after_mb = rss_hwm_mb();
+    if (stats) *stats = ls;
+    return sh;
+}
+
 std::string json_escape(const std::string& s) {
     std::string o;
     for (char c : s) o += (c == '"' || c == '\\') ? std::string("\\") + c : std::string(1, c);
@@ -321,13 +383,23 @@ int main(int argc, char** argv) {
         }
 
         std::unique_ptr<DeviceShard> dshard;
+        std::unique_ptr<DeviceSparseShard> sshard;
         std::vector<float> hshard;
+        // --rtm_format: the single-frame GPU solver on pixel-row shards of fp32 values can keep a sparse RTM sparse
+        // (decided from the files' metadata: the same on every rank)
+        bool sparse = false;
+        if (gpu && !cols && cfg.batch_frames == 1 && !cfg.rtm_bf16 && cfg.rtm_format != "dense") {
+            const double dens = rtm_sparse_density(in.rtm_files, in.rtm_name, in.npixel, in.nvoxel);
+            sparse = cfg.rtm_format == "sparse" || (dens >= 0.0 && dens <= 0.25);
+        }
         LoadStats lstats;
         size_t block_bytes = (size_t)256 << 20;  // per staging buffer (two of them)
         if (const char* e = std::getenv("SART_RTM_BLOCK_MB"); e && *e)
             block_bytes = (size_t)std::max(1.0, std::atof(e) * 1048576.0);
         auto load = [&]() {
-            if (gpu)
+            if (sparse)
+                sshard = load_sparse_shard(in, blk.offset, blk.size, &lstats);
+            else if (gpu)
                 dshard = load_device_shard(in, blk.offset, blk.size, block_bytes, vblk.offset, vblk.size,
                                            cfg.rtm_bf16, &lstats);
             else {
@@ -346,7 +418,9 @@ int main(int argc, char** argv) {
         }
         if (gpu && rank == 0)  // the HDF5 -> HBM load of this rank's shard (all ranks: the --profile load line)
             std::cout << "RTM loaded in: " << lstats.wall_s << " s (" << lstats.bytes / 1e9 << " GB, "
-                      << (lstats.wall_s > 0 ? lstats.bytes / 1e9 / lstats.wall_s : 0.0) << " GB/s)" << std::endl;
+                      << (lstats.wall_s > 0 ? lstats.bytes / 1e9 / lstats.wall_s : 0.0) << " GB/s"
+                      << (sparse ? ", sparse: " + std::to_string(sshard->nnz) + " non-zeros" : std::string()) << ")"
+                      << std::endl;
 
         std::unique_ptr<Engine> engine;
         std::unique_ptr<MultiFrameEngine> mf;
@@ -367,14 +441,21 @@ int main(int argc, char** argv) {
             ec.fused_min_bytes = fused_min_bytes_from_env();
             if (const char* v = std::getenv("SART_FUSED_VARIANT"); v && *v) ec.fused_variant = std::atoi(v);
             ec.time_collectives = !cfg.profile_file.empty();  // --profile: GPU time in the all-reduces per frame
-            ec.rtm_bf16 = dshard->bf16;
             if (cols) {
                 ec.column_shard = true;
                 ec.col_offset = (int64_t)vblk.offset;
                 ec.nvoxel_total = (int64_t)in.nvoxel;
             }
-            engine = std::make_unique<Engine>(device, dshard->A, dshard->nrows, dshard->nrows_pad, dshard->nvoxel,
-                                              dshard->ld, dcomm.get(), ec);
+            if (sparse) {
+                const SparseRtm view = sshard->view();
+                engine = std::make_unique<Engine>(device, nullptr, sshard->nrows, (sshard->nrows + 63) / 64 * 64,
+                                                  sshard->nvoxel, (sshard->nvoxel + 63) / 64 * 64, dcomm.get(), ec,
+                                                  &view);
+            } else {
+                ec.rtm_bf16 = dshard->bf16;
+                engine = std::make_unique<Engine>(device, dshard->A, dshard->nrows, dshard->nrows_pad,
+                                                  dshard->nvoxel, dshard->ld, dcomm.get(), ec);
+            }
             if (lap.nnz()) engine->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
         } else {
             cpu = std::make_unique<CpuSolver>(hshard.data(), (int64_t)blk.size, (int64_t)in.nvoxel,
@@ -440,7 +521,9 @@ int main(int argc, char** argv) {
                         << ", \"rss_hwm_after_first_read_MB\": " << lstats.rss_after_first_read_mb
                         << ", \"rss_hwm_after_MB\": " << lstats.rss_hwm_after_mb << "}"
                         << ", \"rss_growth_MB_max\": " << mx[1]
-                        << ", \"sparse\": " << (in.has_sparse ? "true" : "false") << ", \"driver\": \"native\"}\n";
+                        << ", \"sparse\": " << (in.has_sparse ? "true" : "false")
+                        << ", \"rtm_format\": \"" << (sparse ? "sparse" : "dense") << "\""
+                        << ", \"nnz\": " << (sparse ? sshard->nnz : 0) << ", \"driver\": \"native\"}\n";
         }
 
         std::vector<uint64_t> frames;

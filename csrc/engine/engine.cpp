@@ -76,10 +76,20 @@ template class DeviceArray<int32_t>;
 template class DeviceArray<bf16_t>;
 
 Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
-               Communicator* comm, const EngineConfig& cfg)
+               Communicator* comm, const EngineConfig& cfg, const SparseRtm* sparse)
     : device_(device), A_(A), P_(nrows), Pp_(nrows_pad), V_(nvoxel), ld_(ld), comm_(comm), cfg_(cfg) {
     validate_params(cfg_);
     if (!comm_) throw std::invalid_argument("Engine: communicator required");
+    if (sparse) {
+        if (cfg_.column_shard || cfg_.rtm_bf16)
+            throw std::invalid_argument("Engine: a sparse shard is a row shard of fp32 values");
+        if (!sparse->row_ptr || !sparse->col_ptr)
+            throw std::invalid_argument("Engine: sparse shard needs its CSR and CSC arrays");
+        sparse_ = true;
+        sp_ = *sparse;
+    } else if (!A_) {
+        throw std::invalid_argument("Engine: dense shard pointer required");
+    }
     if (ld_ % 64 || ld_ < V_ || Pp_ % 64 || Pp_ < P_)
         throw std::invalid_argument("Engine: ld and nrows_pad must be multiples of 64 covering the shard");
     cfg_.check_interval = std::max(1, cfg_.check_interval);
@@ -106,7 +116,8 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
         cfg_.fault_nan_sweep = std::atoi(fn);
     if (const char* t = std::getenv("SART_TAIL_FUSED"); t && *t) tail_fused_ = std::atoi(t) != 0;
 
-    nsplit_ = backproject_num_splits(ld_, Pp_, cfg_.rtm_bf16 ? 2 : 4);
+    // the sparse back-projection writes complete column sums: one partial row
+    nsplit_ = sparse_ ? 1 : backproject_num_splits(ld_, Pp_, cfg_.rtm_bf16 ? 2 : 4);
     comm_buf_.resize(ld_ + 64);  // [0, ld) correction, [ld] ||A x||^2
     x_.resize(ld_);
     pen_.resize(ld_);
@@ -139,7 +150,7 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
     plan_cus_ = plan_cus_ / 8 * 8;  // whole CUs per XCD
     // bf16 storage: the fused sweep exists as variant 6 only (else the two-pass kernels)
     const double abytes = (double)Pp_ * (double)ld_ * (cfg_.rtm_bf16 ? 2.0 : 4.0);
-    if (cfg_.use_fused && !cfg_.column_shard && abytes >= cfg_.fused_min_bytes && plan_cus_ >= 8 &&
+    if (cfg_.use_fused && !sparse_ && !cfg_.column_shard && abytes >= cfg_.fused_min_bytes && plan_cus_ >= 8 &&
         (!shared_device_ || fused_ok_shared) && (!cfg_.rtm_bf16 || cfg_.fused_variant == 6)) {
         geom_ = fused_geometry(ld_, plan_cus_, cfg_.fused_variant, cfg_.rows_per_tile, !cfg_.rtm_bf16, !cfg_.rtm_bf16);
         if (cfg_.rtm_bf16 && (cfg_.rows_per_tile == 0 || cfg_.rows_per_tile == 4)) {
@@ -255,12 +266,35 @@ std::vector<double> DeviceRaySums::length(int64_t P) const {
     return h;
 }
 
-void Engine::ray_sums() { rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_, cfg_.column_shard, cfg_.rtm_bf16); }
+void DeviceRaySums::compute_sparse(const SparseRtm& s, int64_t P, int64_t Pp, int64_t V, int64_t ld,
+                                   Communicator* comm, const SolverParams& p, hipStream_t stream) {
+    RoctxRange r("sart::ray_sums");
+    ell64.resize(Pp);  // zero-filled: padded rows / columns stay 0
+    rho64.resize(ld);
+    ray_len.resize(Pp);
+    for (auto* b : {&dinv, &dscale, &dmask}) b->resize(ld);
+    launch_csr_rowsum_f64(s, P, ell64.get(), stream);
+    launch_csc_colsum_f64(s, V, rho64.get(), stream);
+    comm->all_reduce(rho64.get(), (size_t)ld, ReduceOp::kSum, stream);
+    launch_f64_to_f32(ell64.get(), ray_len.get(), Pp, stream);
+    launch_density_scales(rho64.get(), V, ld, (float)p.ray_density_threshold, (float)p.relaxation, dinv.get(),
+                          dscale.get(), dmask.get(), stream);
+    hip_ok(hipStreamSynchronize(stream), "ray sums");
+}
+
+void Engine::ray_sums() {
+    if (sparse_)
+        rs_.compute_sparse(sp_, P_, Pp_, V_, ld_, comm_, cfg_, stream_);
+    else
+        rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_, cfg_.column_shard, cfg_.rtm_bf16);
+}
 
 void Engine::fwd(int epi, const float* x, float* out_f, float* out_w, double* Fpart, const SartState* st) {
     const float* ghat = epi == kEpiPlain ? nullptr : ghat_.get();
     const float* arow = epi == kEpiPlain ? nullptr : arow_.get();
-    if (cfg_.rtm_bf16)
+    if (sparse_)
+        launch_csr_forward(epi, sp_, P_, Pp_, x, ghat, arow, out_f, out_w, Fpart, st, stream_);
+    else if (cfg_.rtm_bf16)
         launch_forward(epi, static_cast<const bf16_t*>(A_), ld_, P_, Pp_, x, ghat, arow, out_f, out_w, Fpart, st,
                        stream_);
     else
@@ -269,7 +303,9 @@ void Engine::fwd(int epi, const float* x, float* out_f, float* out_w, double* Fp
 }
 
 void Engine::bwd(const float* w, const SartState* st) {
-    if (cfg_.rtm_bf16)
+    if (sparse_)
+        launch_csc_backproject(sp_, V_, w, partial_.get(), st, stream_);  // nsplit_ == 1
+    else if (cfg_.rtm_bf16)
         launch_backproject(static_cast<const bf16_t*>(A_), ld_, P_, w, nsplit_, partial_.get(), st, stream_);
     else
         launch_backproject(static_cast<const float*>(A_), ld_, P_, w, nsplit_, partial_.get(), st, stream_);

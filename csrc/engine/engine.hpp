@@ -19,6 +19,7 @@
 #include <string>
 #include <vector>
 
+#include "../kernels/launchers.hpp"
 #include "../kernels/sart_common.hpp"
 #include "../native/solver_params.hpp"
 #include "comm.hpp"
@@ -106,6 +107,9 @@ struct DeviceRaySums {
     // A: fp32 shard, or bf16 bit patterns when a_bf16
     void compute(const void* A, int64_t P, int64_t Pp, int64_t V, int64_t ld, Communicator* comm,
                  const SolverParams& p, hipStream_t stream, bool col_shard = false, bool a_bf16 = false);
+    // the same from a sparse shard (CSR row sums, CSC column sums)
+    void compute_sparse(const SparseRtm& s, int64_t P, int64_t Pp, int64_t V, int64_t ld, Communicator* comm,
+                        const SolverParams& p, hipStream_t stream);
     std::vector<double> density(int64_t V) const;  // host copies
     std::vector<double> length(int64_t P) const;
     DeviceArray<double> rho64, ell64;
@@ -128,8 +132,10 @@ class Engine {
    public:
     // A: device pointer to the row-major shard [nrows_pad x ld] (fp32, or bf16 with cfg.rtm_bf16), zero
     // padded (not owned).
+    // sparse: the shard as device CSR + CSC arrays instead (A null; csrc/kernels/sparse.hip, not owned): the two-pass
+    // sweep on sparse kernels, row shards of fp32 values only
     Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
-           Communicator* comm, const EngineConfig& cfg);
+           Communicator* comm, const EngineConfig& cfg, const SparseRtm* sparse = nullptr);
     ~Engine();
     Engine(const Engine&) = delete;
     Engine& operator=(const Engine&) = delete;
@@ -152,6 +158,8 @@ class Engine {
     std::vector<double> ray_density() const;  // fp64 (nvoxel): global (row shard) / this shard's voxels (column)
     std::vector<double> ray_length() const;   // fp64 (nrows): this shard's pixels (row shard) / global (column)
     bool column_shard() const { return cfg_.column_shard; }
+    bool sparse() const { return sparse_; }
+    int64_t nnz() const { return sparse_ ? sp_.nnz : 0; }
     bool shared_device() const { return shared_device_; }
     int ranks_per_device() const { return ranks_per_device_; }
     int plan_cus() const { return plan_cus_; }  // CUs the fused geometry was planned for
@@ -175,6 +183,8 @@ class Engine {
 
     int device_;
     const void* A_;
+    bool sparse_ = false;
+    SparseRtm sp_{};
     int64_t P_, Pp_, V_, ld_;
     Communicator* comm_;
     EngineConfig cfg_;

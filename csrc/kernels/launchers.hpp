@@ -27,6 +27,28 @@ void launch_backproject(const bf16_t* A, int64_t ld, int64_t nrows, const float*
                         const SartState* st, hipStream_t stream);
 void launch_colsum_f64(const float* A, int64_t ld, int64_t nrows, int nsplit, double* partial, hipStream_t stream);
 void launch_colsum_f64(const bf16_t* A, int64_t ld, int64_t nrows, int nsplit, double* partial, hipStream_t stream);
+// sparse.hip: a sparse RTM shard held twice on the device, as CSR (rows: the forward projection and the row sums) and
+// CSC (columns: the back-projection and the column sums), so both projections are gathers with one writer per output
+// (no atomics: bitwise reproducible). Indices are 32-bit column / row numbers, offsets 64-bit.
+struct SparseRtm {
+    const int64_t* row_ptr = nullptr;  // [nrows + 1]
+    const int32_t* col = nullptr;      // [nnz]
+    const float* val = nullptr;        // [nnz]
+    const int64_t* col_ptr = nullptr;  // [nvoxel + 1]
+    const int32_t* row = nullptr;      // [nnz]
+    const float* cval = nullptr;       // [nnz]
+    int64_t nnz = 0;
+};
+// f = A x with the epilogues of launch_forward (kEpiPlain / kEpiLinear / kEpiLog) and the same Fpart layout:
+// forward_num_blocks(nrows_pad) fp64 partial sums of f^2
+void launch_csr_forward(int epi, const SparseRtm& s, int64_t nrows, int64_t nrows_pad, const float* x,
+                        const float* ghat, const float* arow, float* out_f, float* out_w, double* Fpart,
+                        const SartState* st, hipStream_t stream);
+// out[v] = sum_p A[p, v] w[p] for v < nvoxel (one split: out is a partial row of k_reduce_partials)
+void launch_csc_backproject(const SparseRtm& s, int64_t nvoxel, const float* w, float* out, const SartState* st,
+                            hipStream_t stream);
+void launch_csr_rowsum_f64(const SparseRtm& s, int64_t nrows, double* out, hipStream_t stream);
+void launch_csc_colsum_f64(const SparseRtm& s, int64_t nvoxel, double* out, hipStream_t stream);
 // fp32 -> bf16, round to nearest even (n a multiple of 4)
 void launch_f32_to_bf16(const float* src, int64_t n, bf16_t* dst, hipStream_t stream);
 // Fout (optional): Fout[0] = sum of Fpart (fp32), Fout[1] = st->error (the sweep's error word, reduced with it)

@@ -265,6 +265,21 @@ bool rtm_has_sparse(const SortedRtmFiles& sorted, const std::string& rtm_name) {
     return false;
 }
 
+double rtm_sparse_density(const SortedRtmFiles& sorted, const std::string& rtm_name, uint64_t npixel,
+                          uint64_t nvoxel) {
+    SART_H5_LOCK;
+    double entries = 0.0;
+    for (const auto& [cam, files] : sorted)
+        for (const auto& path : files) {
+            H5Id f = h5_open_file(path);
+            if (!h5_attr_i64(f, "rtm/" + rtm_name, "is_sparse")) return -1.0;
+            H5Id d = h5_open_dataset(f, "rtm/" + rtm_name + "/value");
+            const auto dims = h5_dims(d);
+            entries += dims.empty() ? 0.0 : (double)dims[0];
+        }
+    return npixel && nvoxel ? entries / ((double)npixel * (double)nvoxel) : -1.0;
+}
+
 RtmReader::RtmReader(SortedRtmFiles sorted, std::string rtm_name, uint64_t nvoxel, uint64_t col_begin,
                      uint64_t col_end)
     : sorted_(std::move(sorted)), name_(std::move(rtm_name)), nvoxel_(nvoxel), c0_(col_begin),
@@ -369,6 +384,78 @@ void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, ui
     RtmReader(sorted, rtm_name, nvoxel).read(row_begin, row_end, out, ld);
 }
 
+HostCsr RtmReader::read_csr(uint64_t row_begin, uint64_t row_end) {
+    SART_H5_LOCK;
+    std::vector<int64_t> rows;
+    std::vector<int32_t> cols;
+    std::vector<float> vals;
+    const uint64_t nrows = row_end > row_begin ? row_end - row_begin : 0, ncols = c1_ - c0_;
+    const std::string grp = "rtm/" + name_;
+    uint64_t start_pixel = 0;
+    for (const auto& [cam, files] : sorted_) {
+        if (nrows == 0) break;
+        uint64_t npix;
+        {
+            H5Id f0 = h5_open_file(files.front());
+            npix = h5_attr_u64(f0, "rtm", "npixel");
+        }
+        const uint64_t cam_end = start_pixel + npix;
+        if (cam_end > row_begin && start_pixel < row_end) {
+            const uint64_t lr0 = std::max(row_begin, start_pixel) - start_pixel;
+            const uint64_t lr1 = std::min(row_end, cam_end) - start_pixel;
+            uint64_t start_voxel = 0;
+            for (const auto& path : files) {
+                H5Id f = h5_open_file(path);
+                const uint64_t nvox_seg = h5_attr_u64(f, "rtm", "nvoxel");
+                if (start_voxel + nvox_seg > nvoxel_) throw Error("RTM segments exceed the total number of voxels.");
+                const uint64_t s0 = std::max(c0_, start_voxel) - start_voxel;
+                const uint64_t s1 = std::min(c1_, start_voxel + nvox_seg) > start_voxel
+                                        ? std::min(c1_, start_voxel + nvox_seg) - start_voxel
+                                        : 0;
+                if (s1 > s0) {
+                    const uint64_t ocol = start_voxel + s0 - c0_;
+                    if (h5_attr_i64(f, grp, "is_sparse")) {
+                        const SparseSegment& seg = sparse_segment(f, path, nvox_seg);
+                        auto lo = std::lower_bound(seg.pix.begin(), seg.pix.end(), lr0);
+                        auto hi = std::lower_bound(lo, seg.pix.end(), lr1);
+                        for (size_t n = (size_t)(lo - seg.pix.begin()); n < (size_t)(hi - seg.pix.begin()); ++n) {
+                            const uint64_t v = seg.vox[n];
+                            if (v < s0 || v >= s1) continue;
+                            rows.push_back((int64_t)(start_pixel + seg.pix[n] - row_begin));
+                            cols.push_back((int32_t)(ocol + (v - s0)));
+                            vals.push_back(seg.val[n]);
+                        }
+                    } else {
+                        H5Id d = h5_open_dataset(f, grp + "/value");
+                        const auto dims = h5_dims(d);
+                        if (dims.size() != 2 || dims[0] != npix || dims[1] != nvox_seg)
+                            throw Error("Dense RTM dataset in " + path + " has unexpected shape.");
+                        const uint64_t nc = s1 - s0;
+                        const uint64_t rpr = std::max<uint64_t>(1, (64ull << 20) / (4 * nc));
+                        std::vector<float> blk;
+                        for (uint64_t r = lr0; r < lr1; r += rpr) {
+                            const uint64_t n = std::min(rpr, lr1 - r);
+                            blk.assign(n * nc, 0.0f);
+                            h5_read_block_f32(d, r, n, s0, nc, blk.data(), nc, 0);
+                            for (uint64_t i = 0; i < n; ++i)
+                                for (uint64_t c = 0; c < nc; ++c)
+                                    if (blk[i * nc + c] != 0.0f) {
+                                        rows.push_back((int64_t)(start_pixel + r + i - row_begin));
+                                        cols.push_back((int32_t)(ocol + c));
+                                        vals.push_back(blk[i * nc + c]);
+                                    }
+                        }
+                    }
+                }
+                start_voxel += nvox_seg;
+            }
+        }
+        start_pixel = cam_end;
+        if (start_pixel >= row_end) break;
+    }
+    return csr_from_entries((int64_t)nrows, (int64_t)ncols, rows, cols, vals);
+}
+
 LaplacianCOO read_laplacian(const std::string& path, uint64_t expected_nvoxel) {
     SART_H5_LOCK;
     H5Id f = h5_open_file(path);
@@ -441,8 +528,10 @@ void check_rtm_image_consistency(const SortedRtmFiles&, const SortedImageFiles&,
 std::pair<uint64_t, uint64_t> get_total_rtm_size(const SortedRtmFiles&) { nohdf5(); }
 RtmReader::RtmReader(SortedRtmFiles, std::string, uint64_t, uint64_t, uint64_t) { nohdf5(); }
 void RtmReader::read(uint64_t, uint64_t, float*, uint64_t) { nohdf5(); }
+HostCsr RtmReader::read_csr(uint64_t, uint64_t) { nohdf5(); }
 void read_rtm_rows(const SortedRtmFiles&, const std::string&, uint64_t, uint64_t, uint64_t, float*, uint64_t) { nohdf5(); }
 bool rtm_has_sparse(const SortedRtmFiles&, const std::string&) { nohdf5(); }
+double rtm_sparse_density(const SortedRtmFiles&, const std::string&, uint64_t, uint64_t) { nohdf5(); }
 LaplacianCOO read_laplacian(const std::string&, uint64_t) { nohdf5(); }
 InputSet validate_inputs(const std::vector<std::string>&, const std::string&, double) { nohdf5(); }
 

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "h5.hpp"
+#include "sparse_csr.hpp"
 
 namespace sart {
 
@@ -46,6 +47,10 @@ class RtmReader {
     RtmReader(SortedRtmFiles sorted, std::string rtm_name, uint64_t nvoxel, uint64_t col_begin = 0,
               uint64_t col_end = 0);
     void read(uint64_t row_begin, uint64_t row_end, float* out, uint64_t ld);
+    // The same rows and columns as a CSR matrix of the non-zero entries (sparse datasets from their COO arrays,
+    // dense datasets from the non-zeros of row blocks): what read() would leave in a zeroed dense block, without
+    // the dense block (the sparse RTM path, csrc/kernels/sparse.hip).
+    HostCsr read_csr(uint64_t row_begin, uint64_t row_end);
     uint64_t ncols() const { return c1_ - c0_; }
     // Dense datasets: rows per hyperslab read (0: blocks of <= 64 MiB; 1: one row per read, the reference's
     // pattern raytransfer.cpp:103-109, kept for load-path comparisons: SART_RTM_ROWS_PER_READ).
@@ -66,6 +71,8 @@ class RtmReader {
 void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, uint64_t nvoxel, uint64_t row_begin,
                    uint64_t row_end, float* out, uint64_t ld);
 bool rtm_has_sparse(const SortedRtmFiles& sorted, const std::string& rtm_name);
+// Stored entries of all RTM datasets / (npixel x nvoxel) when every dataset is sparse COO; -1 when one is dense.
+double rtm_sparse_density(const SortedRtmFiles& sorted, const std::string& rtm_name, uint64_t npixel, uint64_t nvoxel);
 
 // Everything the driver needs to know about the inputs, validated with the same checks in the same order
 // as the reference (main.cpp:27-59).

@@ -1,0 +1,72 @@
+#include "sparse_csr.hpp"
+
+#include <algorithm>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+
+namespace sart {
+
+HostCsr csr_from_entries(int64_t nrows, int64_t ncols, const std::vector<int64_t>& rows,
+                         const std::vector<int32_t>& cols, const std::vector<float>& vals) {
+    if (rows.size() != cols.size() || rows.size() != vals.size())
+        throw std::invalid_argument("csr_from_entries: rows, cols and values differ in length");
+    if (ncols > INT32_MAX) throw std::invalid_argument("csr_from_entries: more than 2^31 - 1 columns");
+    const size_t n = vals.size();
+    std::vector<int64_t> count(nrows + 1, 0);
+    for (size_t t = 0; t < n; ++t) {
+        if (rows[t] < 0 || rows[t] >= nrows || cols[t] < 0 || cols[t] >= ncols)
+            throw std::invalid_argument("csr_from_entries: entry (" + std::to_string(rows[t]) + ", " +
+                                        std::to_string(cols[t]) + ") outside the matrix");
+        ++count[rows[t] + 1];
+    }
+    std::partial_sum(count.begin(), count.end(), count.begin());
+    // stable counting sort by row: the entries of a row keep their input order
+    std::vector<size_t> order(n);
+    {
+        std::vector<int64_t> next(count.begin(), count.end() - 1);
+        for (size_t t = 0; t < n; ++t) order[next[rows[t]]++] = t;
+    }
+    HostCsr a;
+    a.nrows = nrows;
+    a.ncols = ncols;
+    a.ptr.assign(nrows + 1, 0);
+    a.idx.reserve(n);
+    a.val.reserve(n);
+    std::vector<size_t> rowv;
+    for (int64_t r = 0; r < nrows; ++r) {
+        rowv.assign(order.begin() + count[r], order.begin() + count[r + 1]);
+        std::stable_sort(rowv.begin(), rowv.end(), [&](size_t p, size_t q) { return cols[p] < cols[q]; });
+        for (size_t k = 0; k < rowv.size(); ++k) {
+            if (k + 1 < rowv.size() && cols[rowv[k + 1]] == cols[rowv[k]]) continue;  // a later duplicate wins
+            const float v = vals[rowv[k]];
+            if (v == 0.0f) continue;
+            a.idx.push_back(cols[rowv[k]]);
+            a.val.push_back(v);
+        }
+        a.ptr[r + 1] = (int64_t)a.val.size();
+    }
+    return a;
+}
+
+HostCsr csr_transpose(const HostCsr& a) {
+    if (a.nrows > INT32_MAX) throw std::invalid_argument("csr_transpose: more than 2^31 - 1 rows");
+    HostCsr t;
+    t.nrows = a.ncols;
+    t.ncols = a.nrows;
+    t.ptr.assign(a.ncols + 1, 0);
+    for (int32_t c : a.idx) ++t.ptr[(int64_t)c + 1];
+    std::partial_sum(t.ptr.begin(), t.ptr.end(), t.ptr.begin());
+    t.idx.resize(a.idx.size());
+    t.val.resize(a.val.size());
+    std::vector<int64_t> next(t.ptr.begin(), t.ptr.end() - 1);
+    for (int64_t r = 0; r < a.nrows; ++r)  // rows ascending: each column's entries come out in row order
+        for (int64_t k = a.ptr[r]; k < a.ptr[r + 1]; ++k) {
+            const int64_t d = next[a.idx[k]]++;
+            t.idx[d] = (int32_t)r;
+            t.val[d] = a.val[k];
+        }
+    return t;
+}
+
+}  // namespace sart

@@ -100,6 +100,22 @@ int main(int argc, char** argv) {
     std::vector<float> rows(19 * 8, 0.f);
     read_rtm_rows(in.rtm_files, in.rtm_name, 8, 0, 19, rows.data(), 8);
     CHECK(rows == r.value);
+    {  // sparse path: CSR of the same rows (read_csr), its transpose, and the one-read CPU sweep
+        RtmReader rd(in.rtm_files, in.rtm_name, 8);
+        const HostCsr a = rd.read_csr(2, 17);
+        CHECK(a.nrows == 15 && a.ncols == 8 && (int64_t)a.ptr.size() == 16);
+        bool same = true;
+        for (int64_t i = 0; i < 15; ++i)
+            for (int64_t k = a.ptr[i]; k < a.ptr[i + 1]; ++k) same = same && a.val[k] == r.value[(i + 2) * 8 + a.idx[k]];
+        CHECK(same && a.nnz() == 15 * 8);
+        const HostCsr t = csr_transpose(a);
+        CHECK(t.nrows == 8 && t.ncols == 15 && t.nnz() == a.nnz() && t.ptr[8] == a.nnz());
+        const HostCsr d = csr_from_entries(3, 4, {2, 0, 2, 0}, {1, 3, 1, 0}, {1.f, 2.f, 5.f, 0.f});
+        CHECK(d.ptr == (std::vector<int64_t>{0, 1, 1, 2}) && d.val[1] == 5.f && d.idx[0] == 3);
+        std::vector<double> xx(8, 1.0), gg(19, 1.0), aa(19, 0.5), ff(19), oo(8);
+        const double f2 = cpu_sweep(rows.data(), 19, 8, 8, xx.data(), gg.data(), aa.data(), false, ff.data(), oo.data());
+        CHECK(std::isfinite(f2) && f2 > 0);
+    }
     CompositeImage ci(in.image_files, in.frame_masks, parse_time_intervals(""), 19, 0);
     CHECK(ci.nframe() == 3 && ci.frame(1).size() == 19);
     {

@@ -190,3 +190,73 @@ class DenseRTM:
 
     def to_host(self):
         return self.A[: self.npixel, : self.nvoxel].float().cpu().numpy()
+
+
+class SparseRTM:
+    """Device-resident sparse row shard [row_offset, row_offset + npixel) x nvoxel of the RTM: CSR (forward
+    projection, row sums) and CSC (back-projection, column sums) copies of the non-zeros, fp32 values
+    (csrc/kernels/sparse.hip). The reference scatters a sparse COO RTM into its dense shard
+    (raytransfer.cpp:67-91); a no-reflection RTM of a few MB then streams as many bytes per iteration as a dense
+    one. ``SARTSolver`` runs the two-pass sweep on these kernels (the fused sweep is dense-only)."""
+
+    is_bf16 = False
+    is_column_shard = False
+
+    def __init__(self, npixel: int, nvoxel: int, row_ptr, col, val, row_offset: int = 0,
+                 device: Optional[torch.device] = None):
+        import numpy as np
+
+        from ..ops import native
+
+        if npixel <= 0 or nvoxel <= 0:
+            raise ValueError("RTM shard must have npixel > 0 and nvoxel > 0")
+        self.npixel, self.nvoxel, self.row_offset = int(npixel), int(nvoxel), int(row_offset)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+        ci = np.ascontiguousarray(col, dtype=np.int32)
+        vv = np.ascontiguousarray(val, dtype=np.float32)
+        if rp.size != self.npixel + 1 or rp[-1] != vv.size or ci.size != vv.size:
+            raise ValueError("inconsistent CSR arrays")
+        cp, ri, cv = native().csr_transpose(self.npixel, self.nvoxel, rp, ci, vv)
+        self.nnz = int(vv.size)
+        self.nrows_pad = round_up(self.npixel, 64)
+        self.ld = round_up(self.nvoxel, 64)
+
+        def dev(a):  # at least one element: a zero-size tensor has no stable data pointer
+            t = torch.from_numpy(a if a.size else np.zeros(1, dtype=a.dtype))
+            return t.to(self.device)
+
+        self.row_ptr, self.col, self.val = dev(rp), dev(ci), dev(vv)
+        self.col_ptr, self.row, self.cval = dev(cp), dev(ri), dev(cv)
+
+    @property
+    def density(self) -> float:
+        return self.nnz / float(self.npixel * self.nvoxel)
+
+    @property
+    def nbytes(self) -> int:
+        return 2 * self.nnz * 8 + (self.npixel + self.nvoxel + 2) * 8
+
+    def pointers(self):
+        return (self.row_ptr.data_ptr(), self.col.data_ptr(), self.val.data_ptr(), self.col_ptr.data_ptr(),
+                self.row.data_ptr(), self.cval.data_ptr())
+
+    @classmethod
+    def from_entries(cls, npixel: int, nvoxel: int, rows, cols, vals, row_offset: int = 0, device=None):
+        """From (local row, column, value) entries in any order (a later duplicate wins, zeros are dropped)."""
+        import numpy as np
+
+        from ..ops import native
+
+        rp, ci, vv = native().csr_from_entries(int(npixel), int(nvoxel), np.asarray(rows, dtype=np.int64),
+                                               np.asarray(cols, dtype=np.int32), np.asarray(vals, dtype=np.float32))
+        return cls(npixel, nvoxel, rp, ci, vv, row_offset=row_offset, device=device)
+
+    @classmethod
+    def from_dense(cls, A_local, row_offset: int = 0, device=None):
+        """The non-zeros of a dense host matrix (numpy, fp32 values)."""
+        import numpy as np
+
+        A = np.asarray(A_local, dtype=np.float32)
+        r, c = np.nonzero(A)
+        return cls.from_entries(A.shape[0], A.shape[1], r, c, A[r, c], row_offset=row_offset, device=device)

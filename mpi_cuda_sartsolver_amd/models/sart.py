@@ -103,7 +103,7 @@ class SARTSolver:
     ``nccl`` process group, host TCP otherwise) and the convergence loop run in C++.
     """
 
-    def __init__(self, rtm: DenseRTM, laplacian: Optional[LaplacianCSR] = None,
+    def __init__(self, rtm, laplacian: Optional[LaplacianCSR] = None,
                  comm: Optional[Communicator] = None, params: Optional[SolverParams] = None,
                  logarithmic: bool = False, use_fused: bool = True, check_interval: int = 16,
                  allow_zero_tolerance: bool = False, fused_variant: Optional[int] = None,
@@ -152,8 +152,14 @@ class SARTSolver:
             cfg.nvoxel_total = int(getattr(rtm, "nvoxel_total", rtm.nvoxel))
         device = self.dev.index if self.dev.index is not None else 0
         self.native_comm = native_communicator(self.comm, device)
-        self.engine = self.k.Engine(device, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld,
-                                    self.native_comm, cfg)
+        if getattr(rtm, "nnz", None) is not None:  # SparseRTM: CSR / CSC kernels, two-pass sweep
+            if self.column_shard:
+                raise ValueError("a sparse RTM shard is a row shard")
+            self.engine = self.k.Engine.from_sparse(device, *rtm.pointers(), rtm.nnz, rtm.npixel, rtm.nvoxel,
+                                               self.native_comm, cfg)
+        else:
+            self.engine = self.k.Engine(device, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld,
+                                        self.native_comm, cfg)
         if self.L is not None:
             self.engine.set_laplacian(self.L.row_ptr_host, self.L.col_host, self.L.val_host)
         self.P, self.Pp, self.V, self.ld = rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld

@@ -198,6 +198,34 @@ def raytraced_rtm(grid=(16, 16, 16), cameras=None, ss=2, margin=0.35, bounces=3,
     return A, info
 
 
+def raytraced_direct_coo(grid=(16, 16, 16), cameras=None, ss=2):
+    """The direct line-of-sight part of ``raytraced_rtm`` (the no-reflection RTM: no bounces, no diffuse band) as COO
+    triplets (global pixel row, flat voxel, value fp32; one entry per (pixel, voxel), sub-rays summed) without a
+    dense matrix, so it scales to 64k x 64k and beyond. Returns (rows, cols, vals, row_ranges)."""
+    cameras = cameras or default_cameras()
+    n = np.asarray(grid)
+    V = int(np.prod(n))
+    centre = np.full(3, 0.5)
+    out_r, out_c, out_v, rows = [], [], [], {}
+    p0 = 0
+    for cam in cameras:
+        H, W = cam.shape
+        O, D, pix, wt = pixel_rays(cam, ss)
+        r0 = np.linalg.norm(centre - np.asarray(cam.position))
+        ray, flat, seg, tm = siddon(O, D, n)
+        val = wt[ray] * seg * (r0 / np.maximum(tm, 1e-3)) ** 2
+        key = pix[ray].astype(np.int64) * V + flat
+        uk, inv = np.unique(key, return_inverse=True)
+        acc = np.zeros(uk.size)
+        np.add.at(acc, inv, val)
+        out_r.append(uk // V + p0)
+        out_c.append(uk % V)
+        out_v.append(acc.astype(np.float32))
+        rows[cam.name] = (p0, p0 + H * W)
+        p0 += H * W
+    return (np.concatenate(out_r), np.concatenate(out_c).astype(np.int32), np.concatenate(out_v), rows)
+
+
 def phantom(grid=(16, 16, 16), t=0.0, seed=0):
     """Smooth emissivity: a tilted ring (torus-like shell) whose peak drifts slowly with t, on a weak background,
     plus a localized blob; values in (0, ~1.1]."""

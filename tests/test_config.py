@@ -35,6 +35,8 @@ def test_short_and_long_aliases(n):
     assert c2.output_file == "y.h5" and c2.batch_frames == 16 and c2.resume
     assert not c2.rtm_bf16 and n.parse_arguments(["--rtm_bf16", "a", "b"]).rtm_bf16
     assert "--rtm_bf16" in n.usage()
+    assert c2.rtm_format == "auto" and n.parse_arguments(["--rtm_format", "sparse", "a", "b"]).rtm_format == "sparse"
+    assert n.parse_arguments(["--rtm_format=dense", "a", "b"]).rtm_format == "dense" and "--rtm_format" in n.usage()
 
 
 @pytest.mark.parametrize("argv,msg", [
@@ -53,6 +55,9 @@ def test_short_and_long_aliases(n):
     (["-m"], "Too few arguments"),
     (["--rtm_bf16", "--use_cpu", "a", "b"], "rtm_bf16 applies to the GPU solvers with pixel-row shards"),
     (["--rtm_bf16", "--partition_voxels", "a", "b"], "rtm_bf16 applies to the GPU solvers with pixel-row shards"),
+    (["--rtm_format", "csr", "a", "b"], "rtm_format must be auto, dense or sparse"),
+    (["--rtm_format", "sparse", "--batch_frames", "16", "a", "b"], "rtm_format sparse applies to the single-frame"),
+    (["--rtm_format", "sparse", "--use_cpu", "a", "b"], "rtm_format sparse applies to the single-frame"),
 ])
 def test_validation_errors(n, argv, msg):
     with pytest.raises(RuntimeError, match=msg.replace("(", r"\(").replace(")", r"\)").replace("]", r"\]")):

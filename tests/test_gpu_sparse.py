@@ -1,0 +1,171 @@
+"""Sparse RTM path on the GPU (csrc/kernels/sparse.hip; SparseRTM + SARTSolver, Engine sparse mode).
+
+A ray-traced RTM with reflections (utils/raytrace.py, 2048 pixels x 4096 voxels: >= 90 % zeros in the direct part,
+values over >= 1e8, rows and columns below the thresholds) and its direct-only part (the no-reflection matrix,
+~1 % non-zeros) held as CSR + CSC: ray sums and the forward projection per element against fp64, and every solver
+variant (linear / log, with and without the Laplacian, cold and warm starts) against the fp64 oracle at the fp32
+emulation's error, as the dense paths in tests/test_gpu_realistic.py; plus equality with the dense engine to the
+same bound, and the CLI on sparse HDF5 files (the driver picks the sparse path, ``--rtm_format``).
+"""
+import numpy as np
+import pytest
+
+from fp32_bound import check_fp32_bound, rel
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def rtms():
+    from mpi_cuda_sartsolver_amd.utils.raytrace import phantom, raytraced_rtm
+
+    A, info = raytraced_rtm(grid=(16, 16, 16))
+    direct = np.asarray(info["direct"], dtype=np.float32)  # the direct line-of-sight part: the no-reflection RTM
+    rng = np.random.default_rng(5)
+    X = np.stack([phantom((16, 16, 16), t=float(t)) for t in range(4)])
+    out = {}
+    for name, M in (("reflections", A), ("direct", direct)):
+        G = X @ M.T.astype(np.float64)
+        G[rng.random(G.shape) < 0.02] = -1.0  # saturated pixels
+        out[name] = (M, G)
+    return out
+
+
+@pytest.fixture(scope="module")
+def lap(dev):
+    from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
+
+    return LaplacianCSR.grid_3d(16, 16, 16, device=dev)
+
+
+@pytest.mark.parametrize("which", ["reflections", "direct"])
+def test_ray_sums_and_forward(dev, rtms, which):
+    from mpi_cuda_sartsolver_amd.models.rtm import SparseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver
+
+    A, _ = rtms[which]
+    sp = SparseRTM.from_dense(A, device=dev)
+    assert sp.nnz == np.count_nonzero(A)
+    if which == "direct":
+        assert sp.density < 0.05
+    s = SARTSolver(sp)
+    assert s.engine.sparse and not s.use_fused and s.engine.nnz == sp.nnz
+    A64 = A.astype(np.float64)
+    np.testing.assert_allclose(s.ray_density64, A64.sum(0), rtol=1e-12, atol=0)
+    np.testing.assert_allclose(s.ray_length64, A64.sum(1), rtol=1e-12, atol=0)
+    x = np.random.default_rng(1).random(A.shape[1])
+    f = s.forward_project(x)
+    ref = A64 @ x
+    # fp32 products and sums: each lane sums ceil(nnz / 32) terms serially, then 5 levels of the xor tree
+    terms = np.ceil(np.count_nonzero(A, axis=1) / 32.0) + 6
+    assert np.all(np.abs(f - ref) <= terms * 2.0 ** -24 * (np.abs(A64) @ np.abs(x)) + 1e-30)
+
+
+@pytest.mark.parametrize("which", ["reflections", "direct"])
+@pytest.mark.parametrize("log", [False, True])
+@pytest.mark.parametrize("with_lap", [False, True])
+def test_solver_vs_oracle(dev, rtms, lap, which, log, with_lap):
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM, SparseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+
+    A, G = rtms[which]
+    L = lap if with_lap else None
+    beta = 1e-3
+    prm = dict(max_iterations=40, conv_tolerance=0.0, beta_laplace=beta)
+    s = SARTSolver(SparseRTM.from_dense(A, device=dev), L, None, SolverParams(**prm), logarithmic=log,
+                   allow_zero_tolerance=True)
+    d = SARTSolver(DenseRTM.from_dense(A, device=dev), L, None, SolverParams(**prm), logarithmic=log,
+                   use_fused=False, allow_zero_tolerance=True)
+    prev = None
+    for k in range(3):  # frame 0 cold, frames 1, 2 warm-started from the previous solution
+        r = s.solve(G[k], prev)
+        assert r.iterations == 40
+        e, e32 = check_fp32_bound(r.solution, A, G[k], L, log=log, iterations=40, beta_laplace=beta, x_prev=prev,
+                                  slack=2e-8)
+        rd = d.solve(G[k], prev)
+        print(f"{which} log={log} lap={with_lap} frame {k}: sparse {e:.3e}, dense two-pass "
+              f"{rel(rd.solution, r.solution):.3e} apart, fp32 emulation {e32:.3e}")
+        prev = r.solution
+
+
+def test_convergence_rule_and_status(dev, rtms):
+    """The default stopping rule: the same iteration count and status as the dense two-pass engine."""
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM, SparseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+
+    A, G = rtms["direct"]
+    p = SolverParams(max_iterations=500, conv_tolerance=1e-5)
+    rs = SARTSolver(SparseRTM.from_dense(A, device=dev), None, None, p).solve(G[0])
+    rd = SARTSolver(DenseRTM.from_dense(A, device=dev), None, None, p, use_fused=False).solve(G[0])
+    assert (rs.status, rs.iterations) == (rd.status, rd.iterations)
+    assert rel(rs.solution, rd.solution) < 1e-4
+
+
+def test_empty_rows_and_columns(dev):
+    """Rows and columns without entries (a pixel seeing nothing, a voxel seen by no ray): zero ray sums, masked
+    like the dense path; no out-of-range reads at the ends of the CSR / CSC arrays."""
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM, SparseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+
+    rng = np.random.default_rng(9)
+    A = np.where(rng.random((300, 257)) < 0.05, rng.random((300, 257)), 0.0).astype(np.float32)
+    A[:, :3] = 0.0
+    A[-5:, :] = 0.0
+    A[:7, :] = 0.0
+    g = A.astype(np.float64) @ (rng.random(257) + 0.1)
+    p = SolverParams(max_iterations=25, conv_tolerance=0.0)
+    rs = SARTSolver(SparseRTM.from_dense(A, device=dev), None, None, p, allow_zero_tolerance=True).solve(g)
+    rd = SARTSolver(DenseRTM.from_dense(A, device=dev), None, None, p, use_fused=False,
+                    allow_zero_tolerance=True).solve(g)
+    # voxels no ray sees keep the clamped start value (reference semantics, as the dense engine)
+    np.testing.assert_array_equal(rs.solution[:3], rd.solution[:3])
+    assert rel(rs.solution, rd.solution) < 1e-5
+
+
+@pytest.mark.parametrize("fmt", ["auto", "sparse"])
+@pytest.mark.parametrize("log", [False, True])
+def test_cli_sparse_hdf5(tmp_path, capfd, fmt, log):
+    """CLI end to end on sparse COO files of the ray-traced model (both cameras sparse, so ``auto`` keeps the RTM
+    sparse; ``sparse`` forces it): the driver reports the sparse shard and every frame of the output is within the
+    fp32 emulation's error of the fp64 oracle chain (as tests/test_gpu_realistic.py::test_cli_realistic_hdf5)."""
+    from mpi_cuda_sartsolver_amd import cli
+    from mpi_cuda_sartsolver_amd.io.fixtures import make_case
+
+    from test_cli_e2e import chain_errors
+
+    case = make_case(str(tmp_path / "c"), shapes=((32, 32), (32, 32)), grid=(16, 16, 16), raytraced=True,
+                     sparse_cameras=("cam_a", "cam_b"), laplacian=True, nframes=4, saturate=0.02, mask_fraction=0.1)
+    out = str(tmp_path / "out.h5")
+    argv = ["-m", "40", "-c", "1e-7", "-l", case.laplacian_file, "-b", "1e-3", "-o", out, "--rtm_format", fmt]
+    argv += (["-L"] if log else []) + case.files
+    assert cli.main(argv) == 0
+    text = capfd.readouterr().out
+    assert text.count("Processed in:") == 4
+    assert "sparse: " in text  # "RTM loaded in: ... sparse: <nnz> non-zeros"
+    e, e32 = chain_errors(case, out, warm=True, orders=("blas", "reference"), log=log)
+    print("cli sparse", fmt, log, e, e32)
+    assert np.all(e <= e32 + 2e-8), (e, e32)
+
+
+def test_cli_dense_format_on_sparse_files(tmp_path, capfd):
+    """--rtm_format dense on the same files: the dense shard (no sparse line), and the same solutions to the fp32
+    emulation's error."""
+    from mpi_cuda_sartsolver_amd import cli
+    from mpi_cuda_sartsolver_amd.io.fixtures import make_case
+
+    from test_cli_e2e import chain_errors
+
+    case = make_case(str(tmp_path / "c"), shapes=((16, 16), (16, 16)), grid=(8, 8, 8), raytraced=True,
+                     sparse_cameras=("cam_a", "cam_b"), nframes=3)
+    out = str(tmp_path / "out.h5")
+    assert cli.main(["-m", "30", "-c", "1e-7", "-o", out, "--rtm_format", "dense"] + case.files) == 0
+    text = capfd.readouterr().out
+    assert "sparse: " not in text and text.count("Processed in:") == 3
+    e, e32 = chain_errors(case, out, warm=True, orders=("blas", "reference"))
+    assert np.all(e <= e32 + 2e-8), (e, e32)

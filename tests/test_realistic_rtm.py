@@ -98,3 +98,16 @@ def test_cli_cpu_on_realistic_hdf5(tmp_path, capfd):
         prev = x
     _, last, _ = native().read_solution_file(out)
     np.testing.assert_allclose(last, xs[-1], rtol=1e-9, atol=1e-15 * np.abs(xs[-1]).max())
+
+
+def test_direct_coo_matches_dense_direct_part():
+    """raytraced_direct_coo (the no-reflection matrix without a dense array) equals the direct part of
+    raytraced_rtm entry for entry."""
+    from mpi_cuda_sartsolver_amd.utils.raytrace import raytraced_direct_coo
+
+    A, info = raytraced_rtm(grid=(8, 8, 8))
+    r, c, v, rows = raytraced_direct_coo(grid=(8, 8, 8))
+    D = np.zeros(A.shape, np.float32)
+    D[r, c] = v
+    np.testing.assert_array_equal(D, info["direct"])
+    assert rows == info["rows"] and v.dtype == np.float32 and np.all(v > 0)

@@ -17,7 +17,8 @@ def test_host_runtime_asan_ubsan(tmp_path):
     exe = tmp_path / "host_selftest"
     srcs = [ROOT / "csrc" / "tests" / "host_selftest.cpp"] + [
         NATIVE / f for f in ("config.cpp", "cpu_kernels.cpp", "cpu_solver.cpp", "fixtures.cpp", "frames.cpp", "h5.cpp",
-                             "host_comm.cpp", "host_comm_mpi.cpp", "inputs.cpp", "solver_params.cpp")]
+                             "host_comm.cpp", "host_comm_mpi.cpp", "inputs.cpp", "solver_params.cpp",
+                             "sparse_csr.cpp")]
     hdf5 = _build.HDF5_PREFIX
     libdir = tmp_path / "hdf5"
     libdir.mkdir()

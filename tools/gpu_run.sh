@@ -107,6 +107,9 @@ for step in "$@"; do
       done ;;
     prof64) run rocprof_mfx64b 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfx64b" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames 64 --iters 20 --no-selfcheck &&
             run rocprof_2tb64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_2tb64" -o run --output-format csv -- python3 bench.py --config 2tb --steps 1 --warmup 0 --frames 64 --no-selfcheck ;;
+    sparse) run pytest_sparse 900 python -u -m pytest tests/test_gpu_sparse.py tests/test_cli_e2e.py tests/test_native_driver.py \
+              -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    sparsebench) run sparse_bench 600 python tools/sparse_bench.py --out "$OUT/sparse_bench.jsonl" ;;
     profmfb) for nf in 16 64; do
               run rocprof_mfb$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 --rtm-dtype bf16 || exit 1
             done ;;
