@@ -87,6 +87,9 @@ Engine::Engine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int6
             throw std::invalid_argument("Engine: sparse shard needs its CSR and CSC arrays");
         sparse_ = true;
         sp_ = *sparse;
+        // lanes per row / column from the mean entries per row / column, fixed for the engine's life
+        if (!sp_.lanes_rows) sp_.lanes_rows = sparse_lanes(nrows_pad ? (double)sp_.nnz / (double)nrows_pad : 0.0);
+        if (!sp_.lanes_cols) sp_.lanes_cols = sparse_lanes(nvoxel ? (double)sp_.nnz / (double)nvoxel : 0.0);
     } else if (!A_) {
         throw std::invalid_argument("Engine: dense shard pointer required");
     }
@@ -411,7 +414,7 @@ void Engine::sweep() {
     }
     unsigned* xcnt = (use_fused_ && geom_.variant == 6) ? xcnt_.get() : nullptr;  // zeroed by setup / update
     const int nsplit = use_fused_ ? (int)fused_blocks_ : nsplit_;
-    const int64_t nF = use_fused_ ? nF_fused_ : forward_num_blocks(Pp_);
+    const int64_t nF = use_fused_ ? nF_fused_ : (sparse_ ? csr_forward_num_blocks(sp_, Pp_) : forward_num_blocks(Pp_));
     // One rank: the reduction of the partial rows, the decision and the update are one kernel (nothing to
     // all-reduce in between); every workgroup sums the nF sweep partials, so only while nF stays small.
     const bool one_tail = tail_fused_ && comm_->size() == 1 && nF <= 4096;

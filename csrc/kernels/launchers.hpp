@@ -38,9 +38,16 @@ struct SparseRtm {
     const int32_t* row = nullptr;      // [nnz]
     const float* cval = nullptr;       // [nnz]
     int64_t nnz = 0;
+    // lanes per row / column (4, 8, 16 or 32; 0: sparse_lanes()): one power-of-two group of a wave per row, so short
+    // rows do not leave most of a wave idle (set once per engine: the forward's Fpart layout depends on it)
+    int lanes_rows = 0, lanes_cols = 0;
 };
-// f = A x with the epilogues of launch_forward (kEpiPlain / kEpiLinear / kEpiLog) and the same Fpart layout:
-// forward_num_blocks(nrows_pad) fp64 partial sums of f^2
+// lanes per row for rows of `avg` entries on average (env SART_SPARSE_LANES overrides)
+int sparse_lanes(double avg);
+// fp64 ||f||^2 partials of launch_csr_forward: one per 256 / lanes_rows rows
+int64_t csr_forward_num_blocks(const SparseRtm& s, int64_t nrows_pad);
+// f = A x with the epilogues of launch_forward (kEpiPlain / kEpiLinear / kEpiLog); Fpart: csr_forward_num_blocks
+// fp64 partial sums of f^2
 void launch_csr_forward(int epi, const SparseRtm& s, int64_t nrows, int64_t nrows_pad, const float* x,
                         const float* ghat, const float* arow, float* out_f, float* out_w, double* Fpart,
                         const SartState* st, hipStream_t stream);

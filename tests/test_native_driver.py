@@ -346,3 +346,43 @@ def test_module_entry_point_does_not_orphan_the_driver(tmp_path, binary, sig):
         if p.poll() is None:
             p.kill()
             p.wait()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p2p", ["0", "1"])
+def test_native_sparse_two_ranks_one_device(tmp_path, binary, p2p):
+    """The sparse RTM path (--rtm_format sparse) on two ranks of the box's single GPU (row shards of the CSR, the
+    per-iteration all-reduce staged or P2P) against the one-rank sparse run and the dense run of the same files."""
+    case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_a", "cam_b"), laplacian=True, nframes=2,
+                     grid=(12, 12, 12), shapes=((24, 32), (20, 30)), raytraced=True)
+    base = ["-m", "40", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3"]
+    r = _run_native(binary, base + ["--rtm_format", "sparse", "-o", str(tmp_path / "one.h5"), *case.files])
+    assert r.returncode == 0, r.stderr
+    assert "sparse: " in r.stdout
+    r = _run_native(binary, base + ["--rtm_format", "dense", "-o", str(tmp_path / "dense.h5"), *case.files])
+    assert r.returncode == 0, r.stderr
+    saved = {k: os.environ.get(k) for k in ("SART_DIST_BACKEND", "SART_P2P")}
+    os.environ["SART_DIST_BACKEND"] = "tcp"
+    os.environ["SART_P2P"] = p2p
+    prof = str(tmp_path / "prof.jsonl")
+    try:
+        r = _run_native(binary, base + ["--rtm_format", "sparse", "--profile", prof, "-o", str(tmp_path / "two.h5"),
+                                        *case.files], nproc=2)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    import json
+
+    load = json.loads(open(prof).readline())
+    assert load["rtm_format"] == "sparse" and load["nnz"] > 0 and load["ranks"] == 2
+    n = native()
+    _, x1, s1 = n.read_solution_file(str(tmp_path / "one.h5"))
+    _, x2, s2 = n.read_solution_file(str(tmp_path / "two.h5"))
+    _, xd, sd = n.read_solution_file(str(tmp_path / "dense.h5"))
+    np.testing.assert_array_equal(s1, s2)
+    assert np.linalg.norm(x2 - x1) / np.linalg.norm(x1) < 2e-3
+    assert np.linalg.norm(xd - x1) / np.linalg.norm(x1) < 2e-3

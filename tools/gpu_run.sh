@@ -110,6 +110,11 @@ for step in "$@"; do
     sparse) run pytest_sparse 900 python -u -m pytest tests/test_gpu_sparse.py tests/test_cli_e2e.py tests/test_native_driver.py \
               -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sparsebench) run sparse_bench 600 python tools/sparse_bench.py --out "$OUT/sparse_bench.jsonl" ;;
+    sparselanes) for l in 4 8 16 32; do
+                   SART_SPARSE_LANES=$l run sparse_lanes_$l 300 python tools/sparse_bench.py --no-dense --out "$OUT/sparse_lanes_$l.jsonl" || exit 1
+                 done
+                 run sparse_lanes_auto 300 python tools/sparse_bench.py --no-dense --out "$OUT/sparse_lanes_auto.jsonl" &&
+                 run rocprof_sparse 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_sparse" -o run --output-format csv -- python3 tools/sparse_bench.py --no-dense --steps 2 ;;
     profmfb) for nf in 16 64; do
               run rocprof_mfb$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 --rtm-dtype bf16 || exit 1
             done ;;
