@@ -632,8 +632,19 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
         bool error = false;
         comm_ms_ = 0.0;
         cev_used_[0] = cev_used_[1] = 0;
+        // Chunk sizes. A warm-started frame of a time series needs about as many sweeps as the one before it, so
+        // its first chunk holds that many + 1 and the chunk queued behind it (to keep the GPU busy while the first
+        // is checked) only 2; later chunks are check_interval long. Sweeps queued past the decision return at once
+        // but still cost their launches (~3 x 3 us): with full chunks a sparse 64k x 64k frame of 8 sweeps of 33 us
+        // queued 24 of them. Results are unchanged (the decision and the update are on the device).
+        const int pred = (x0 && last_sweeps_ > 0) ? last_sweeps_ : 0;
+        auto chunk = [&](int k) {
+            if (pred && k == 0) return std::min(cfg_.check_interval, pred + 1);
+            if (pred && k == 1) return std::min(cfg_.check_interval, 2);
+            return cfg_.check_interval;
+        };
         auto issue = [&]() {
-            const int n = std::min(cfg_.check_interval, max_sweeps - enqueued);
+            const int n = std::min(chunk(issued), max_sweeps - enqueued);
             cur_slot_ = issued & 1;
             run_chunk(n);
             enqueued += n;
@@ -703,6 +714,7 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
     info.comm = comm_->backend();
     info.fused_variant = use_fused_ ? geom_.variant : -1;
     info.sweeps = s.sweep;
+    last_sweeps_ = s.sweep;
     info.comm_ms = timing_collectives() ? comm_ms_ : -1.0;
     info.finish_ms = ms_since(t_fin);
     info.ms = ms_since(t0);

@@ -197,6 +197,7 @@ class Engine {
     int64_t chain_tiles_ = 0;     // fused sweep chain_tiles (T = 1 fold period / T >= 2 segment length), 0 = off
     int64_t fused_blocks_ = 0;   // partial-sum rows written by the fused sweep (I, or I * T * segments)
     double norm_ = 1.0;
+    int last_sweeps_ = 0;  // sweeps of the previous solve: the first chunk of a warm-started one
 
     // comm_buf_: [0, ld) the reduced correction, [ld] ||A x||^2, [ld + 1] the error word of the last sweep, EXCEPT
     // after a one-rank sweep on the one-kernel tail (k_reduce_decide_update keeps them in registers): its contents

@@ -115,6 +115,8 @@ for step in "$@"; do
                  done
                  run sparse_lanes_auto 300 python tools/sparse_bench.py --no-dense --out "$OUT/sparse_lanes_auto.jsonl" &&
                  run rocprof_sparse 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_sparse" -o run --output-format csv -- python3 tools/sparse_bench.py --no-dense --steps 2 ;;
+    seriessparse) run series_sparse 900 python tools/series_native.py --sparse-direct --runs seq --out "$OUT/series_sparse.jsonl" ;;
+    seriesdense) run series_dense 900 python tools/series_native.py --runs seq --out "$OUT/series_dense.jsonl" ;;
     profmfb) for nf in 16 64; do
               run rocprof_mfb$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 --rtm-dtype bf16 || exit 1
             done ;;

@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--amp", type=float, default=0.05)
     ap.add_argument("--period", type=float, default=200.0)
     ap.add_argument("--random", action="store_true", help="uniform random RTM instead of the ray-traced one")
+    ap.add_argument("--sparse-direct", action="store_true",
+                    help="the ray-traced model's direct (no-reflection) part, written as sparse COO files: the driver "
+                         "keeps it sparse on the GPU (--rtm_format auto)")
     ap.add_argument("--tstep", type=float, default=0.1, help="phantom time step per frame (ray-traced)")
     ap.add_argument("--runs", default="seq", help="comma list: seq (frame by frame), batch<N> (--batch_frames N)")
     ap.add_argument("--extra", default="", help="extra driver arguments for every run")
@@ -92,6 +95,37 @@ def main():
         Ad = shard.A[: inp.npixel, : a.nvox]
         model = "uniform random dense (native writer)"
         phantom_desc = f"b (1 + {a.amp} sin(2 pi t / {a.period} + phase))"
+    elif a.sparse_direct:
+        from mpi_cuda_sartsolver_amd.models.rtm import SparseRTM
+        from mpi_cuda_sartsolver_amd.models.sart import SARTSolver
+        from mpi_cuda_sartsolver_amd.utils.raytrace import Camera, default_cameras, phantom, raytraced_direct_coo
+
+        grids = {4096: (16, 16, 16), 32768: (32, 32, 32), 65536: (32, 32, 64)}
+        grid = grids[a.nvox]
+        cobj = [Camera(c, bc.position, bc.look_at, (a.h, a.w), bc.field_of_view, bc.up)
+                for c, bc in zip(cams, default_cameras(n=2))]
+        r, c, v, info = raytraced_direct_coo(grid=grid, cameras=cobj)
+        flat = np.arange(a.nvox)
+        nx, ny, nz = grid
+        vi, vj, vk = flat // (ny * nz), (flat // nz) % ny, flat % nz
+        for cam, path in zip(cams, rtm):
+            r0, r1 = info[cam]
+            sel = (r >= r0) & (r < r1)
+            n.write_rtm_file(path=path, camera_name=cam, wavelength=656.3, npixel=r1 - r0, nvoxel=a.nvox,
+                             frame_mask=np.ones((a.h, a.w), np.uint8), vi=vi.astype(np.uint64), vj=vj.astype(np.uint64),
+                             vk=vk.astype(np.uint64), vvalue=np.arange(a.nvox, dtype=np.int32), nx=nx, ny=ny, nz=nz,
+                             rtm_name="with_reflections", coordinate_system="", bounds=[],
+                             pixel_index=(r[sel] - r0).astype(np.uint64), voxel_index=c[sel].astype(np.uint64),
+                             value=v[sel])
+        t_rtm = time.perf_counter() - t0
+        X = np.stack([phantom(grid, t=a.tstep * k) for k in range(a.frames)])
+        sp = SparseRTM.from_entries(2 * P1, a.nvox, r, c, v, device=dev)
+        fwd = SARTSolver(sp)
+        G = np.stack([fwd.forward_project(X[k]) for k in range(a.frames)])
+        del fwd, sp
+        model = "ray-traced direct part (no reflections), sparse COO files"
+        phantom_desc = f"utils.raytrace.phantom(t = {a.tstep} k)"
+        Xd = None
     else:
         from mpi_cuda_sartsolver_amd.utils.raytrace import Camera, default_cameras, phantom, raytraced_rtm
 
@@ -118,9 +152,10 @@ def main():
         del A
         model = "ray-traced with reflections (utils/raytrace.py)"
         phantom_desc = f"utils.raytrace.phantom(t = {a.tstep} k)"
-    Xd = torch.from_numpy(X.T.astype(np.float32)).to(dev)
-    G = (Ad @ Xd).double().cpu().numpy().T  # [frames, pixels]
-    del Ad, Xd
+    if not a.sparse_direct:
+        Xd = torch.from_numpy(X.T.astype(np.float32)).to(dev)
+        G = (Ad @ Xd).double().cpu().numpy().T  # [frames, pixels]
+        del Ad, Xd
     torch.cuda.empty_cache()
     img = [os.path.join(a.dir, f"image_{c}.h5") for c in cams]
     for k, (c, path) in enumerate(zip(cams, img)):
@@ -128,7 +163,8 @@ def main():
     fixture_s = time.perf_counter() - t0
     files = rtm + img
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-    base = {"npixel": 2 * P1, "nvoxel": a.nvox, "frames": a.frames, "cameras": 2, "rtm_GB": 2 * P1 * a.nvox * 4 / 1e9,
+    base = {"npixel": 2 * P1, "nvoxel": a.nvox, "frames": a.frames, "cameras": 2,
+            "rtm_GB": (r.size * 16 / 1e9) if a.sparse_direct else 2 * P1 * a.nvox * 4 / 1e9,
             "rtm": model, "phantom": phantom_desc, "fixture_s": round(fixture_s, 1),
             "rtm_write_s": round(t_rtm, 1), "reads": "page cache (files written by this process)"}
     extra = a.extra.split() if a.extra else []
