@@ -390,7 +390,11 @@ int main(int argc, char** argv) {
         bool sparse = false;
         if (gpu && !cols && cfg.batch_frames == 1 && !cfg.rtm_bf16 && cfg.rtm_format != "dense") {
             const double dens = rtm_sparse_density(in.rtm_files, in.rtm_name, in.npixel, in.nvoxel);
-            sparse = cfg.rtm_format == "sparse" || (dens >= 0.0 && dens <= 0.25);
+            // auto: the sparse kernels read 16 bytes per non-zero and sweep (CSR + CSC, index + value) against 4 bytes
+            // per element for the dense fused sweep; measured at 32768 x 32768 (uniform random positions): sparse /
+            // dense fused it/s 11268 / 1525 at 1 %, 3038 / 1532 at 4.9 %, 2031 / 1534 at 9.5 %, 1336 / 1531 at 18 %
+            // (profiles/sparse_r5_density_breakeven.jsonl): auto takes the sparse path up to 10 %
+            sparse = cfg.rtm_format == "sparse" || (dens >= 0.0 && dens <= 0.10);
         }
         LoadStats lstats;
         size_t block_bytes = (size_t)256 << 20;  // per staging buffer (two of them)

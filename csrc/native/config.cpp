@@ -89,7 +89,7 @@ std::string usage() {
            "                              products and sums stay fp32).\n"
            "  --rtm_format F              auto | dense | sparse: keep a sparse RTM sparse on the GPU (CSR + CSC;\n"
            "                              single-frame solver, pixel-row shards). auto: when every RTM dataset is\n"
-           "                              sparse COO with at most 25 % non-zeros. [default: auto]\n"
+           "                              sparse COO with at most 10 % non-zeros. [default: auto]\n"
            "  --profile FILE              Write per-frame timing/iteration telemetry as JSON lines.\n";
 }
 

@@ -37,7 +37,7 @@ struct Config {
     bool two_pass = false;      // disable the fused single-pass sweep
     bool partition_voxels = false;
     // GPU single-frame solver: keep the RTM sparse on the device (CSR + CSC, csrc/kernels/sparse.hip) instead of a
-    // dense shard. "auto": when every RTM dataset is sparse COO with at most 25 % non-zeros; "dense" / "sparse".
+    // dense shard. "auto": when every RTM dataset is sparse COO with at most 10 % non-zeros; "dense" / "sparse".
     std::string rtm_format = "auto";
     bool rtm_bf16 = false;      // GPU: store the RTM shard in bf16 (fp32 products and sums)  // GPU: shard the RTM by voxel columns (all pixels per rank) instead of pixel rows
     std::string profile_file;   // JSON timing/telemetry sidecar

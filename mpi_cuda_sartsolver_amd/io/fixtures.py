@@ -43,7 +43,7 @@ def _grid_voxels(nx, ny, nz, nvoxel, rng):
 def make_case(directory: str, cameras=("cam_a", "cam_b"), shapes=((6, 8), (5, 7)), nvoxel=48, grid=(4, 4, 4),
               segments=2, sparse_cameras=(), nframes=4, dt=0.1, time_offsets=None, saturate=0.0,
               laplacian=False, wavelength=656.3, rtm_name="with_reflections", seed=0, coordinate_system="",
-              bounds=(), raytraced=False, mask_fraction=0.2) -> Case:
+              bounds=(), raytraced=False, mask_fraction=0.2, direct_only=False) -> Case:
     os.makedirs(directory, exist_ok=True)
     n = native()
     rng = np.random.default_rng(seed)
@@ -59,6 +59,8 @@ def make_case(directory: str, cameras=("cam_a", "cam_b"), shapes=((6, 8), (5, 7)
         cams = [Camera(cam, b.position, b.look_at, tuple(sh), b.field_of_view, b.up)
                 for cam, sh, b in zip(cameras, shapes, base)]
         A_all, info = raytraced_rtm(grid=grid, cameras=cams, seed=seed)
+        if direct_only:  # the no-reflection matrix: the direct line-of-sight part only (~1 % non-zeros)
+            A_all = np.asarray(info["direct"], dtype=np.float32)
         traced = {cam: A_all[r0:r1] for cam, (r0, r1) in info["rows"].items()}
         phantoms = np.stack([phantom(grid, t=float(k), seed=seed) for k in range(nframes)])
     else:

@@ -131,16 +131,20 @@ def test_empty_rows_and_columns(dev):
 @pytest.mark.parametrize("fmt", ["auto", "sparse"])
 @pytest.mark.parametrize("log", [False, True])
 def test_cli_sparse_hdf5(tmp_path, capfd, fmt, log):
-    """CLI end to end on sparse COO files of the ray-traced model (both cameras sparse, so ``auto`` keeps the RTM
-    sparse; ``sparse`` forces it): the driver reports the sparse shard and every frame of the output is within the
-    fp32 emulation's error of the fp64 oracle chain (as tests/test_gpu_realistic.py::test_cli_realistic_hdf5)."""
+    """CLI end to end on sparse COO files of the ray-traced model (both cameras sparse; ``auto`` keeps the
+    no-reflection matrix sparse, ``sparse`` forces it for the matrix with reflections): the driver reports the sparse
+    shard and every frame of the output is within the fp32 emulation's error of the fp64 oracle chain (as
+    tests/test_gpu_realistic.py::test_cli_realistic_hdf5)."""
     from mpi_cuda_sartsolver_amd import cli
     from mpi_cuda_sartsolver_amd.io.fixtures import make_case
 
     from test_cli_e2e import chain_errors
 
+    # auto: the no-reflection matrix (~0.5 % non-zeros, below auto's 10 %); sparse: the matrix with reflections
+    # (~18 %: auto would keep it dense)
     case = make_case(str(tmp_path / "c"), shapes=((32, 32), (32, 32)), grid=(16, 16, 16), raytraced=True,
-                     sparse_cameras=("cam_a", "cam_b"), laplacian=True, nframes=4, saturate=0.02, mask_fraction=0.1)
+                     sparse_cameras=("cam_a", "cam_b"), laplacian=True, nframes=4, saturate=0.02, mask_fraction=0.1,
+                     direct_only=fmt == "auto")
     out = str(tmp_path / "out.h5")
     argv = ["-m", "40", "-c", "1e-7", "-l", case.laplacian_file, "-b", "1e-3", "-o", out, "--rtm_format", fmt]
     argv += (["-L"] if log else []) + case.files

@@ -117,6 +117,10 @@ for step in "$@"; do
                  run rocprof_sparse 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_sparse" -o run --output-format csv -- python3 tools/sparse_bench.py --no-dense --steps 2 ;;
     seriessparse) run series_sparse 900 python tools/series_native.py --sparse-direct --runs seq --out "$OUT/series_sparse.jsonl" ;;
     seriesdense) run series_dense 900 python tools/series_native.py --runs seq --out "$OUT/series_dense.jsonl" ;;
+    sparsedens) for d in 0.01 0.03 0.05 0.1 0.2; do
+                  run sparse_dens_$d 600 python tools/sparse_bench.py --random-density $d --shape 128,128 --grid 32,32,32 \
+                    --out "$OUT/sparse_density.jsonl" || exit 1
+                done ;;
     profmfb) for nf in 16 64; do
               run rocprof_mfb$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_mfb$nf" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --frames $nf --iters 20 --rtm-dtype bf16 || exit 1
             done ;;

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--no-dense", action="store_true")
+    ap.add_argument("--random-density", type=float, default=0.0,
+                    help="instead of the ray-traced matrix: uniform random positions at this density, --shape rows x "
+                         "--grid voxels (the break-even density of the sparse path against the dense fused sweep)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     import torch
@@ -41,11 +44,18 @@ def main():
     t0 = time.perf_counter()
     cams = [Camera(f"cam_{i}", b.position, b.look_at, (H, W), b.field_of_view, b.up)
             for i, b in enumerate(default_cameras(n=2))]
-    r, c, v, _ = raytraced_direct_coo(grid=grid, cameras=cams)
     P, V = 2 * H * W, int(np.prod(grid))
+    if a.random_density > 0:
+        rng = np.random.default_rng(7)
+        nnz = int(a.random_density * P * V)
+        flat = np.unique(rng.integers(0, P * V, size=nnz, dtype=np.int64))
+        r, c = flat // V, (flat % V).astype(np.int32)
+        v = rng.random(flat.size, dtype=np.float32) + 0.01
+    else:
+        r, c, v, _ = raytraced_direct_coo(grid=grid, cameras=cams)
     sp = SparseRTM.from_entries(P, V, r, c, v, device=dev)
     build_s = time.perf_counter() - t0
-    x_true = phantom(grid, t=1.0)
+    x_true = phantom(grid, t=1.0) if a.random_density <= 0 else np.random.default_rng(1).random(V) + 0.1
     p = SolverParams(max_iterations=a.iters, conv_tolerance=0.0)
     lines = []
 
@@ -59,7 +69,9 @@ def main():
         dt = (time.perf_counter() - t) / a.steps
         rec = dict(path=name, P=P, V=V, nnz=sp.nnz, density=round(sp.density, 6), iters=a.iters,
                    ms_per_solve=round(1e3 * dt, 3), iters_per_s=round(a.iters / dt, 1),
-                   used_fused=bool(res.used_fused), rtm="ray-traced direct (no reflections)", grid=list(grid))
+                   used_fused=bool(res.used_fused),
+                   rtm=("uniform random positions" if a.random_density > 0 else "ray-traced direct (no reflections)"),
+                   grid=list(grid))
         lines.append(rec)
         print(json.dumps(rec), flush=True)
         return res.solution
