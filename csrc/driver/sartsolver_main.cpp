@@ -590,6 +590,8 @@ int main(int argc, char** argv) {
         if (cols && !warm.empty())  // this rank's voxels of the stored solution
             warm = std::vector<double>(warm.begin() + vblk.offset, warm.begin() + vblk.offset + vblk.size);
         std::vector<double> solution = warm, x(vblk.size), xfull(cols ? in.nvoxel : 0);
+        const char* wd = std::getenv("SART_WARM_ON_DEVICE");
+        const bool warm_dev = !(wd && *wd && std::atoi(wd) == 0);
         std::future<std::vector<double>> fut;
         if (!frames.empty()) fut = std::async(std::launch::async, [&image, i = frames[0]]() { return image.frame(i); });
         for (size_t k = 0; k < frames.size(); ++k) {
@@ -601,7 +603,10 @@ int main(int argc, char** argv) {
                 fut = std::async(std::launch::async, [&image, i = frames[k + 1]]() { return image.frame(i); });
             const auto t0 = std::chrono::steady_clock::now();
             const double* x0 = (cfg.no_guess || solution.empty()) ? nullptr : solution.data();
-            const SolveInfo info = gpu ? engine->solve(frame.data(), x0, x.data()) : cpu->solve(frame.data(), x0, x.data());
+            // from frame 1 on, a warm start is the engine's own previous solution: rescaled on the device
+            // (SART_WARM_ON_DEVICE=0: through the host copy, for A/B runs)
+            const SolveInfo info = gpu ? engine->solve(frame.data(), x0, x.data(), k > 0 && x0 != nullptr && warm_dev)
+                                       : cpu->solve(frame.data(), x0, x.data());
             if (info.fallbacks)
                 std::cerr << "warning: fused sweep fell back " << info.fallbacks << " time(s)" << std::endl;
             if (info.comm_fallbacks && rank == 0)

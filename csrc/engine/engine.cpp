@@ -358,7 +358,7 @@ void Engine::set_laplacian(const int64_t* row_ptr, const int32_t* col, const flo
     has_lap_ = true;
 }
 
-double Engine::setup_frame(const double* g, const double* x0) {
+double Engine::setup_frame(const double* g, const double* x0, bool x0_on_device) {
     RoctxRange r("sart::setup_frame");
     // normalisation by the global maximum and sum_{g > 0} g^2 (reference sartsolver_cuda.cpp:146-157);
     // the reference divides by zero when every pixel is <= 0, we keep norm = 1 then.
@@ -386,6 +386,8 @@ double Engine::setup_frame(const double* g, const double* x0) {
                                nullptr, stream_);
         if (!cols) comm_->all_reduce(comm_buf_.get(), (size_t)ld_, ReduceOp::kSum, stream_);
         launch_init_solution(x_.get(), V_, ld_, comm_buf_.get(), nullptr, 1.0, stream_);
+    } else if (x0_on_device) {
+        launch_rescale_solution(x_.get(), V_, ld_, last_norm_, 1.0 / norm, stream_);
     } else {
         std::memcpy(hx0_, x0, V_ * sizeof(double));
         hip_ok(hipMemcpyAsync(x064_.get(), hx0_, V_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D x0");
@@ -603,9 +605,12 @@ bool device_comm_failed_anywhere(Communicator* comm) {
 
 bool Engine::comm_failed_anywhere() { return device_comm_failed_anywhere(comm_); }
 
-SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
+SolveInfo Engine::solve(const double* g, const double* x0, double* x_out, bool x0_is_last) {
     RoctxRange range("sart::solve");
     set_device();
+    // a re-solve (fallback, device all-reduce failure) starts from the host x0: x_ has moved by then
+    bool x0_on_device = x0 && x0_is_last && last_x_on_device_;
+    last_x_on_device_ = false;
     const auto t0 = std::chrono::steady_clock::now();
     // Row shards align the ranks in setup_frame's host collectives; column shards have none there, so while a
     // device path with a timeout is active a barrier keeps a rank that was busy between frames (rank 0 writing
@@ -618,7 +623,8 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
     };
     std::chrono::steady_clock::time_point t_iter = t0;
     while (true) {
-        norm_ = setup_frame(g, x0);
+        norm_ = setup_frame(g, x0, x0_on_device);
+        x0_on_device = false;
         info.setup_ms = ms_since(t0);
         t_iter = std::chrono::steady_clock::now();
         host_sweep_ = 0;
@@ -706,6 +712,8 @@ SolveInfo Engine::solve(const double* g, const double* x0, double* x_out) {
         hip_ok(hipStreamSynchronize(stream_), "D2H x");
     }
     for (int64_t i = 0; i < V_; ++i) x_out[i] = (double)hxo_[i] * norm_;  // reference sartsolver_cuda.cpp:264-265
+    last_x_on_device_ = !rollback;
+    last_norm_ = norm_;
     info.status = s.status == kSuccess ? kSuccess : kMaxIterationsExceeded;
     info.iterations = s.iterations;
     info.convergence = s.conv_last;

@@ -144,7 +144,9 @@ class Engine {
     void set_laplacian(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t nnz);
     // One frame: g = this rank's pixels (host fp64, nrows), x0 = warm start (host fp64, nvoxel) or null,
     // x_out = solution (host fp64, nvoxel, de-normalised).
-    SolveInfo solve(const double* g, const double* x0, double* x_out);
+    // x0_is_last: x0 is this engine's previous x_out (the reference's frame k-1 -> k warm start): the start value
+    // is rescaled from the copy still on the device (no host copy and upload; bitwise the same start value)
+    SolveInfo solve(const double* g, const double* x0, double* x_out, bool x0_is_last = false);
     // f = A x for this shard (host fp64 in/out).
     void forward(const double* x, double* f);
 
@@ -168,7 +170,7 @@ class Engine {
    private:
     void ray_sums();
     void alloc_fused();
-    double setup_frame(const double* g, const double* x0);
+    double setup_frame(const double* g, const double* x0, bool x0_on_device = false);
     void sweep();
     void sweep_columns();
     // two-pass kernels on the shard in its storage type: forward (epilogue epi) and split-K back-projection
@@ -198,6 +200,8 @@ class Engine {
     int64_t fused_blocks_ = 0;   // partial-sum rows written by the fused sweep (I, or I * T * segments)
     double norm_ = 1.0;
     int last_sweeps_ = 0;  // sweeps of the previous solve: the first chunk of a warm-started one
+    bool last_x_on_device_ = false;  // x_ holds the previous solve's returned solution (no rollback since)
+    double last_norm_ = 1.0;
 
     // comm_buf_: [0, ld) the reduced correction, [ld] ||A x||^2, [ld + 1] the error word of the last sweep, EXCEPT
     // after a one-rank sweep on the one-kernel tail (k_reduce_decide_update keeps them in registers): its contents

@@ -67,6 +67,8 @@ void launch_prep_rows(const double* g, int64_t nrows, int64_t nrows_pad, double 
                       float len_thres, float* ghat, float* arow, float* gpos, float* wo, hipStream_t stream);
 void launch_init_solution(float* x, int64_t n, int64_t n_pad, const float* src_f32, const double* src_f64,
                           double scale, hipStream_t stream);
+// x = fp32((x a) b), clamped (a warm start from the solution left on the device by the previous solve)
+void launch_rescale_solution(float* x, int64_t n, int64_t n_pad, double a, double b, hipStream_t stream);
 void launch_penalty(bool logx, const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta,
                     const float* x, float* pen, const SartState* st, hipStream_t stream);
 void launch_decide(SartState* st, const float* Fslot, hipStream_t stream);

@@ -61,6 +61,21 @@ __global__ __launch_bounds__(256) void k_init_solution(float* __restrict__ x, in
     x[i] = v;
 }
 
+// Warm start from the solution still on the device (x normalised by the previous frame's norm a): x = fp32((x a) b)
+// with b = 1 / the new norm, in double and in the order of the host path (de-normalise to the fp64 output, then
+// normalise the start value), so the bits equal a host round trip; clamped like k_init_solution.
+__global__ __launch_bounds__(256) void k_rescale_solution(float* __restrict__ x, int64_t n, int64_t n_pad, double a,
+                                                          double b) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_pad) return;
+    float v = 0.f;
+    if (i < n) {
+        v = (float)(((double)x[i] * a) * b);
+        if (v < kEpsLog) v = kEpsLog;
+    }
+    x[i] = v;
+}
+
 // pen[i] = beta * sum_k val[k] * h(x[col[k]]), h = identity (linear) or log (logarithmic SART).
 template <bool LOGX>
 __global__ __launch_bounds__(256) void k_penalty_csr(const int64_t* __restrict__ row_ptr,
@@ -379,6 +394,11 @@ void launch_init_solution(float* x, int64_t n, int64_t n_pad, const float* src_f
                           double scale, hipStream_t stream) {
     hipLaunchKernelGGL(k_init_solution, dim3(nb(n_pad)), dim3(256), 0, stream, x, n, n_pad, src_f32, src_f64, scale);
     check_launch("k_init_solution");
+}
+
+void launch_rescale_solution(float* x, int64_t n, int64_t n_pad, double a, double b, hipStream_t stream) {
+    hipLaunchKernelGGL(k_rescale_solution, dim3(nb(n_pad)), dim3(256), 0, stream, x, n, n_pad, a, b);
+    check_launch("k_rescale_solution");
 }
 
 void launch_penalty(bool logx, const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta,

@@ -386,3 +386,30 @@ def test_native_sparse_two_ranks_one_device(tmp_path, binary, p2p):
     np.testing.assert_array_equal(s1, s2)
     assert np.linalg.norm(x2 - x1) / np.linalg.norm(x1) < 2e-3
     assert np.linalg.norm(xd - x1) / np.linalg.norm(x1) < 2e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--two_pass", "-L"], ["--rtm_format", "sparse"]])
+def test_warm_start_on_device_is_bitwise(tmp_path, binary, extra):
+    """Frames 1.. start from the previous solution still on the device (rescaled there) instead of a host round trip
+    (SART_WARM_ON_DEVICE=0): the same start values, so the whole series is bitwise equal."""
+    case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_a", "cam_b"), laplacian=True, nframes=4,
+                     grid=(12, 12, 12), shapes=((24, 32), (20, 30)), raytraced=True)
+    base = ["-m", "30", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3"] + extra
+    r = _run_native(binary, base + ["-o", str(tmp_path / "dev.h5"), *case.files])
+    assert r.returncode == 0, r.stderr
+    saved = os.environ.get("SART_WARM_ON_DEVICE")
+    os.environ["SART_WARM_ON_DEVICE"] = "0"
+    try:
+        r = _run_native(binary, base + ["-o", str(tmp_path / "host.h5"), *case.files])
+    finally:
+        if saved is None:
+            os.environ.pop("SART_WARM_ON_DEVICE", None)
+        else:
+            os.environ["SART_WARM_ON_DEVICE"] = saved
+    assert r.returncode == 0, r.stderr
+    n = native()
+    X1 = n.read_dataset_f64(str(tmp_path / "dev.h5"), "solution/value")
+    X2 = n.read_dataset_f64(str(tmp_path / "host.h5"), "solution/value")
+    assert X1.shape[0] == 4
+    np.testing.assert_array_equal(X1, X2)
