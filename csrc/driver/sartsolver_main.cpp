@@ -388,7 +388,7 @@ int main(int argc, char** argv) {
         // --rtm_format: the single-frame GPU solver on pixel-row shards of fp32 values can keep a sparse RTM sparse
         // (decided from the files' metadata: the same on every rank)
         bool sparse = false;
-        if (gpu && !cols && cfg.batch_frames == 1 && !cfg.rtm_bf16 && cfg.rtm_format != "dense") {
+        if (!cols && (!gpu || cfg.batch_frames == 1) && !cfg.rtm_bf16 && cfg.rtm_format != "dense") {
             const double dens = rtm_sparse_density(in.rtm_files, in.rtm_name, in.npixel, in.nvoxel);
             // auto: the sparse kernels read 16 bytes per non-zero and sweep (CSR + CSC, index + value) against 4 bytes
             // per element for the dense fused sweep; measured at 32768 x 32768 (uniform random positions): sparse /
@@ -400,8 +400,11 @@ int main(int argc, char** argv) {
         size_t block_bytes = (size_t)256 << 20;  // per staging buffer (two of them)
         if (const char* e = std::getenv("SART_RTM_BLOCK_MB"); e && *e)
             block_bytes = (size_t)std::max(1.0, std::atof(e) * 1048576.0);
+        HostCsr hcsr;  // --use_cpu with a sparse shard
         auto load = [&]() {
-            if (sparse)
+            if (sparse && !gpu)
+                hcsr = RtmReader(in.rtm_files, in.rtm_name, in.nvoxel).read_csr(blk.offset, blk.offset + blk.size);
+            else if (sparse)
                 sshard = load_sparse_shard(in, blk.offset, blk.size, &lstats);
             else if (gpu)
                 dshard = load_device_shard(in, blk.offset, blk.size, block_bytes, vblk.offset, vblk.size,
@@ -462,8 +465,11 @@ int main(int argc, char** argv) {
             }
             if (lap.nnz()) engine->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
         } else {
-            cpu = std::make_unique<CpuSolver>(hshard.data(), (int64_t)blk.size, (int64_t)in.nvoxel,
-                                              (int64_t)in.nvoxel, host, params, false);
+            if (sparse)
+                cpu = std::make_unique<CpuSolver>(std::move(hcsr), host, params, false);
+            else
+                cpu = std::make_unique<CpuSolver>(hshard.data(), (int64_t)blk.size, (int64_t)in.nvoxel,
+                                                  (int64_t)in.nvoxel, host, params, false);
             if (lap.nnz()) cpu->set_laplacian(lap);
         }
 

@@ -363,14 +363,31 @@ double Engine::setup_frame(const double* g, const double* x0, bool x0_on_device)
     // normalisation by the global maximum and sum_{g > 0} g^2 (reference sartsolver_cuda.cpp:146-157);
     // the reference divides by zero when every pixel is <= 0, we keep norm = 1 then.
     // the previous frame's copies out of the pinned buffers have completed (solve() synchronises the stream)
-    double mx = -std::numeric_limits<double>::infinity(), gs = 0.0;
-    for (int64_t i = 0; i < P_; ++i) {
-        const double v = g[i];
-        hg_[i] = v;  // into pinned memory in the same pass
-        if (!std::isfinite(v)) continue;  // masked like a saturated pixel (k_prep_rows)
-        mx = std::max(mx, v);
-        if (v > 0) gs += v * v;
+    // eight interleaved max / sum chains combined pairwise (fixed order): one serial chain is bound by the
+    // add latency (65536 pixels: 67 us; eight: 23 us with the copy into pinned memory in the same pass)
+    double mx8[8], gs8[8];
+    for (int k = 0; k < 8; ++k) mx8[k] = -std::numeric_limits<double>::infinity(), gs8[k] = 0.0;
+    // a non-finite pixel is masked like a saturated one (k_prep_rows)
+    auto acc = [](double v, double& m, double& q) {
+        const bool ok = std::isfinite(v);
+        m = ok && v > m ? v : m;
+        q += (ok && v > 0) ? v * v : 0.0;
+    };
+    int64_t i0 = 0;
+    for (; i0 + 8 <= P_; i0 += 8)
+#pragma GCC unroll 8
+        for (int k = 0; k < 8; ++k) {
+            const double v = g[i0 + k];
+            hg_[i0 + k] = v;  // into pinned memory in the same pass
+            acc(v, mx8[k], gs8[k]);
+        }
+    for (; i0 < P_; ++i0) {
+        hg_[i0] = g[i0];
+        acc(g[i0], mx8[i0 & 7], gs8[i0 & 7]);
     }
+    const double mx = std::max(std::max(std::max(mx8[0], mx8[1]), std::max(mx8[2], mx8[3])),
+                               std::max(std::max(mx8[4], mx8[5]), std::max(mx8[6], mx8[7])));
+    const double gs = ((gs8[0] + gs8[1]) + (gs8[2] + gs8[3])) + ((gs8[4] + gs8[5]) + (gs8[6] + gs8[7]));
     const bool cols = cfg_.column_shard;  // every rank holds every pixel: the sums are already global
     double norm = cols ? mx : comm_->host().all_reduce_scalar(mx, ReduceOp::kMax);
     if (!(norm > 0)) norm = 1.0;

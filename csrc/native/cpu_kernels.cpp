@@ -1,5 +1,7 @@
 #include "cpu_kernels.hpp"
 
+#include "sparse_csr.hpp"
+
 #include <omp.h>
 
 #include <algorithm>
@@ -205,6 +207,42 @@ void cpu_backproject(const float* A, int64_t P, int64_t V, int64_t ld, const dou
         }
     }
     reduce_threads(acc, nt, V, out);
+}
+
+namespace {
+inline double sparse_row_dot(const HostCsr& a, int64_t r, const double* x) {
+    double s = 0.0;
+    for (int64_t k = a.ptr[r]; k < a.ptr[r + 1]; ++k) s += (double)a.val[k] * x[a.idx[k]];
+    return s;
+}
+}  // namespace
+
+void cpu_sparse_raysums(const HostCsr& rows, const HostCsr& cols, double* rho, double* ell) {
+#pragma omp parallel for schedule(static)
+    for (int64_t r = 0; r < rows.nrows; ++r) {
+        double s = 0.0;
+        for (int64_t k = rows.ptr[r]; k < rows.ptr[r + 1]; ++k) s += rows.val[k];
+        ell[r] = s;
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t c = 0; c < cols.nrows; ++c) {
+        double s = 0.0;
+        for (int64_t k = cols.ptr[c]; k < cols.ptr[c + 1]; ++k) s += cols.val[k];
+        rho[c] = s;
+    }
+}
+
+double cpu_csr_forward(const HostCsr& rows, const double* x, double* f) {
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t r = 0; r < rows.nrows; ++r) f[r] = sparse_row_dot(rows, r, x);
+    double f2 = 0.0;
+    for (int64_t r = 0; r < rows.nrows; ++r) f2 += f[r] * f[r];  // row order
+    return f2;
+}
+
+void cpu_csc_backproject(const HostCsr& cols, const double* w, double* out) {
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t c = 0; c < cols.nrows; ++c) out[c] = sparse_row_dot(cols, c, w);
 }
 
 }  // namespace sart

@@ -27,4 +27,12 @@ void cpu_backproject(const float* A, int64_t P, int64_t V, int64_t ld, const dou
 double cpu_sweep(const float* A, int64_t P, int64_t V, int64_t ld, const double* x, const double* g, const double* a,
                  bool logmode, double* f, double* out);
 
+// Sparse shard (the --rtm_format sparse CPU path): CSR rows and CSC columns of the same matrix (sparse_csr.hpp).
+// Every row / column sum runs in its entries' order, one output per loop iteration: the results do not depend on
+// the thread count.
+struct HostCsr;
+void cpu_sparse_raysums(const HostCsr& rows, const HostCsr& cols, double* rho, double* ell);
+double cpu_csr_forward(const HostCsr& rows, const double* x, double* f);  // returns sum_p f[p]^2
+void cpu_csc_backproject(const HostCsr& cols, const double* w, double* out);
+
 }  // namespace sart

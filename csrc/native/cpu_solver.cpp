@@ -21,6 +21,29 @@ CpuSolver::CpuSolver(const float* A, int64_t P, int64_t V, int64_t ld, HostComm*
     rho_.assign(V_, 0.0);
     ell_.assign(P_, 0.0);
     cpu_raysums(A_, P_, V_, ld_, rho_.data(), ell_.data());  // (reference sartsolver.cpp:38-56)
+    init_scales();
+}
+
+CpuSolver::CpuSolver(HostCsr rows, HostComm* comm, const SolverParams& params, bool gpu_semantics)
+    : A_(nullptr), sparse_(true), rows_(std::move(rows)), P_(rows_.nrows), V_(rows_.ncols), ld_(rows_.ncols),
+      comm_(comm), p_(params), gpu_(gpu_semantics) {
+    validate_params(p_);
+    if (!comm_) throw std::invalid_argument("CpuSolver: communicator required");
+    cols_ = csr_transpose(rows_);
+    rho_.assign(V_, 0.0);
+    ell_.assign(P_, 0.0);
+    cpu_sparse_raysums(rows_, cols_, rho_.data(), ell_.data());
+    init_scales();
+}
+
+void CpuSolver::backproject(const double* w, double* out) const {
+    if (sparse_)
+        cpu_csc_backproject(cols_, w, out);
+    else
+        cpu_backproject(A_, P_, V_, ld_, w, out);
+}
+
+void CpuSolver::init_scales() {
     comm_->all_reduce_host(rho_.data(), (size_t)V_, ReduceOp::kSum);
     dvalid_.assign(V_, 0);
     rho_s_.assign(V_, 1.0);
@@ -89,7 +112,7 @@ SolveInfo CpuSolver::solve(const double* g, const double* x0, double* x_out) {
     for (int64_t q = 0; q < P_; ++q) a[q] = gw[q] >= 0 ? inv_len_[q] : 0.0;
     if (!x0) {  // cold start (reference sartsolver.cpp:150-160)
         for (int64_t q = 0; q < P_; ++q) w[q] = gpu_ ? std::max(gw[q], 0.0) : gw[q];
-        cpu_backproject(A_, P_, V_, ld_, w.data(), red.data());
+        backproject(w.data(), red.data());
         comm_->all_reduce_host(red.data(), (size_t)V_, ReduceOp::kSum);
         for (int64_t v = 0; v < V_; ++v) x[v] = dvalid_[v] ? red[v] / rho_s_[v] : 0.0;
     } else {
@@ -100,7 +123,7 @@ SolveInfo CpuSolver::solve(const double* g, const double* x0, double* x_out) {
     if (lg) {
         O.assign(V_, 0.0);
         for (int64_t q = 0; q < P_; ++q) w[q] = a[q] * gw[q];
-        cpu_backproject(A_, P_, V_, ld_, w.data(), O.data());
+        backproject(w.data(), O.data());
         comm_->all_reduce_host(O.data(), (size_t)V_, ReduceOp::kSum);
         for (int64_t v = 0; v < V_; ++v)
             if (!dvalid_[v]) O[v] = 0.0;
@@ -114,7 +137,11 @@ SolveInfo CpuSolver::solve(const double* g, const double* x0, double* x_out) {
     const char* tp = std::getenv("SART_CPU_TWO_PASS");
     const bool two_pass = tp && *tp && std::atoi(tp) != 0;
     auto sweep = [&]() {
-        if (two_pass) {
+        if (sparse_) {  // two passes over the non-zeros (rows, then columns)
+            redF[V_] = cpu_csr_forward(rows_, x.data(), f.data());
+            for (int64_t q = 0; q < P_; ++q) w[q] = lg ? a[q] * f[q] : a[q] * (gw[q] - f[q]);
+            cpu_csc_backproject(cols_, w.data(), redF.data());
+        } else if (two_pass) {
             redF[V_] = cpu_forward(A_, P_, V_, ld_, x.data(), f.data());
             for (int64_t q = 0; q < P_; ++q) w[q] = lg ? a[q] * f[q] : a[q] * (gw[q] - f[q]);
             cpu_backproject(A_, P_, V_, ld_, w.data(), redF.data());

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "host_comm.hpp"
+#include "sparse_csr.hpp"
 #include "solver_params.hpp"
 
 namespace sart {
@@ -20,6 +21,10 @@ class CpuSolver {
     // A: row-major fp32 [P x ld] (not owned), comm: host collectives (not owned).
     CpuSolver(const float* A, int64_t P, int64_t V, int64_t ld, HostComm* comm, const SolverParams& params,
               bool gpu_semantics = false);
+    // sparse shard: the CSR rows (P x V) and their transpose (owned copies); forward and back-projection as two
+    // passes over the non-zeros
+    CpuSolver(HostCsr rows, HostComm* comm, const SolverParams& params, bool gpu_semantics = false);
+    bool sparse() const { return sparse_; }
     void set_laplacian(const Csr& L);
     SolveInfo solve(const double* g, const double* x0, double* x_out);
     const std::vector<double>& ray_density() const { return rho_; }
@@ -27,7 +32,11 @@ class CpuSolver {
 
    private:
     void penalty(const std::vector<double>& x, std::vector<double>& pen) const;
+    void init_scales();
+    void backproject(const double* w, double* out) const;
     const float* A_;
+    bool sparse_ = false;
+    HostCsr rows_, cols_;
     int64_t P_, V_, ld_;
     HostComm* comm_;
     SolverParams p_;

@@ -69,3 +69,31 @@ def test_read_rtm_csr_raytraced(tmp_path):
     rp, ci, vv, _ = native().read_rtm_csr(case.files, row_begin=0, row_end=P)
     assert vv.size == np.count_nonzero(case.A)
     np.testing.assert_array_equal(_dense(P, V, rp, ci, vv), case.A.astype(np.float32))
+
+
+@pytest.mark.parametrize("fmt", ["auto", "sparse"])
+def test_cli_cpu_sparse_matches_dense(tmp_path, capfd, fmt):
+    """--use_cpu on sparse COO files of the no-reflection ray-traced model: the CPU solver on the CSR / CSC shard
+    (auto picks it at ~1 % non-zeros) gives the dense CPU solver's solutions to fp64 rounding, and the reference CPU
+    semantics' oracle chain."""
+    from mpi_cuda_sartsolver_amd import cli
+    from mpi_cuda_sartsolver_amd.io.fixtures import make_case
+    from mpi_cuda_sartsolver_amd.models.reference import sart_cpu_semantics
+
+    case = make_case(str(tmp_path / "c"), shapes=((16, 16), (16, 16)), grid=(8, 8, 8), raytraced=True,
+                     direct_only=True, sparse_cameras=("cam_a", "cam_b"), nframes=3, saturate=0.02)
+    assert np.count_nonzero(case.A) / case.A.size < 0.1
+    outs = {}
+    for name, extra in (("sparse", ["--rtm_format", fmt]), ("dense", ["--rtm_format", "dense"])):
+        out = str(tmp_path / f"{name}.h5")
+        assert cli.main(["--use_cpu", "-m", "30", "-c", "1e-9", "-o", out] + extra + case.files) == 0
+        outs[name] = native().read_dataset_f64(out, "solution/value")
+    assert capfd.readouterr().out.count("Processed in:") == 6
+    np.testing.assert_allclose(outs["sparse"], outs["dense"], rtol=1e-11, atol=1e-14 * np.abs(outs["dense"]).max())
+    frames = [np.concatenate([case.frames[c][k].ravel()[case.masks[c].ravel() > 0] for c in sorted(case.masks)])
+              for k in range(3)]
+    prev = None
+    for k, g in enumerate(frames):
+        x, _, _ = sart_cpu_semantics(case.A, g, None, max_iterations=30, conv_tolerance=1e-9, x_prev=prev)
+        np.testing.assert_allclose(outs["sparse"][k], x, rtol=1e-9, atol=1e-15 * np.abs(x).max())
+        prev = x
