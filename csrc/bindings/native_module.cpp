@@ -129,6 +129,20 @@ PYBIND11_MODULE(_sart_native, m) {
         .def(py::init<SortedRtmFiles, std::string, uint64_t, uint64_t, uint64_t>(), py::arg("sorted_files"),
              py::arg("rtm_name"), py::arg("nvoxel"), py::arg("col_begin") = 0, py::arg("col_end") = 0)
         .def_property_readonly("ncols", &RtmReader::ncols)
+        .def(
+            "read_csr",
+            [](RtmReader& r, uint64_t r0, uint64_t r1) {
+                HostCsr a;
+                {
+                    py::gil_scoped_release nogil;
+                    a = r.read_csr(r0, r1);
+                }
+                return py::make_tuple(py::array_t<int64_t>(a.ptr.size(), a.ptr.data()),
+                                      py::array_t<int32_t>(a.idx.size(), a.idx.data()),
+                                      py::array_t<float>(a.val.size(), a.val.data()));
+            },
+            "Rows [r0, r1) x the column window as CSR (row_ptr, col, value) of the non-zeros", py::arg("row_begin"),
+            py::arg("row_end"))
         .def("set_rows_per_read", &RtmReader::set_rows_per_read, py::arg("rows"))
         .def(
             "read_ptr",
@@ -331,6 +345,8 @@ PYBIND11_MODULE(_sart_native, m) {
                               py::array_t<int32_t>(t.idx.size(), t.idx.data()),
                               py::array_t<float>(t.val.size(), t.val.data()));
     });
+    m.def("rtm_sparse_density", &rtm_sparse_density, py::arg("sorted_files"), py::arg("rtm_name"), py::arg("npixel"),
+          py::arg("nvoxel"));
     // the RTM rows [r0, r1) of validated inputs as CSR (RtmReader::read_csr)
     m.def("read_rtm_csr", [](const std::vector<std::string>& files, const std::string& rtm_name, uint64_t r0, uint64_t r1) {
         const sart::InputSet in = sart::validate_inputs(files, rtm_name, 50.0);

@@ -67,6 +67,22 @@ def read_rtm_rows(inputs: InputSet, row_begin: int, row_end: int, ld: Optional[i
     return out
 
 
+def rtm_sparse_density(inputs: InputSet) -> float:
+    """Stored entries / (npixel x nvoxel) when every RTM dataset is sparse COO, else -1 (the driver's
+    ``--rtm_format auto`` test)."""
+    return float(native().rtm_sparse_density(inputs.rtm_files, inputs.rtm_name, inputs.npixel, inputs.nvoxel))
+
+
+def load_rtm_shard_sparse(inputs: InputSet, row_offset: int, npixel_local: int, device):
+    """This rank's RTM rows as a device-resident ``SparseRTM`` (CSR + CSC of the non-zeros; COO datasets are read
+    directly, dense ones through row blocks): the ``--rtm_format sparse`` shard of the native driver."""
+    from ..models.rtm import SparseRTM
+
+    reader = native().RtmReader(inputs.rtm_files, inputs.rtm_name, inputs.nvoxel)
+    rp, col, val = reader.read_csr(row_offset, row_offset + npixel_local)
+    return SparseRTM(npixel_local, inputs.nvoxel, rp, col, val, row_offset=row_offset, device=device)
+
+
 def load_rtm_shard(inputs: InputSet, row_offset: int, npixel_local: int, device, ld: Optional[int] = None,
                    block_bytes: int = 256 << 20, col_offset: int = 0, ncols: Optional[int] = None,
                    storage: str = "fp32"):

@@ -173,3 +173,27 @@ def test_cli_dense_format_on_sparse_files(tmp_path, capfd):
     assert "sparse: " not in text and text.count("Processed in:") == 3
     e, e32 = chain_errors(case, out, warm=True, orders=("blas", "reference"))
     assert np.all(e <= e32 + 2e-8), (e, e32)
+
+
+def test_python_hdf5_sparse_loader(tmp_path, dev):
+    """io.hdf5.load_rtm_shard_sparse (two row shards of sparse COO files) against the dense loader: the same
+    forward projections to fp32 rounding and the same solve to the fp32 emulation's error."""
+    from mpi_cuda_sartsolver_amd.io.fixtures import make_case
+    from mpi_cuda_sartsolver_amd.io.hdf5 import load_rtm_shard, load_rtm_shard_sparse, validate_inputs
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+
+    case = make_case(str(tmp_path / "c"), shapes=((16, 16), (16, 16)), grid=(10, 10, 10), raytraced=True,
+                     direct_only=True, sparse_cameras=("cam_a", "cam_b"), nframes=1)
+    inp = validate_inputs(case.files)
+    P = inp.npixel
+    x = np.random.default_rng(0).random(inp.nvoxel)
+    for r0, r1 in ((0, P // 2), (P // 2, P)):
+        sp = load_rtm_shard_sparse(inp, r0, r1 - r0, dev)
+        dn = load_rtm_shard(inp, r0, r1 - r0, dev)
+        fs, fd = SARTSolver(sp).forward_project(x), SARTSolver(dn).forward_project(x)
+        np.testing.assert_allclose(fs, fd, rtol=2e-6, atol=1e-30)
+        assert sp.nnz == np.count_nonzero(case.A[r0:r1])
+    g = case.A.astype(np.float64) @ x
+    p = SolverParams(max_iterations=30, conv_tolerance=0.0)
+    r = SARTSolver(load_rtm_shard_sparse(inp, 0, P, dev), None, None, p, allow_zero_tolerance=True).solve(g)
+    check_fp32_bound(r.solution, case.A, g, None, iterations=30, slack=2e-8)

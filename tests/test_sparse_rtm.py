@@ -97,3 +97,20 @@ def test_cli_cpu_sparse_matches_dense(tmp_path, capfd, fmt):
         x, _, _ = sart_cpu_semantics(case.A, g, None, max_iterations=30, conv_tolerance=1e-9, x_prev=prev)
         np.testing.assert_allclose(outs["sparse"][k], x, rtol=1e-9, atol=1e-15 * np.abs(x).max())
         prev = x
+
+
+def test_python_sparse_loader_host_side(tmp_path):
+    """io.hdf5: the stored-entry density (the driver's --rtm_format auto test: -1 when a dataset is dense) and the
+    reader's CSR of a row window."""
+    from mpi_cuda_sartsolver_amd.io.fixtures import make_case
+    from mpi_cuda_sartsolver_amd.io.hdf5 import rtm_sparse_density, validate_inputs
+
+    case = make_case(str(tmp_path / "c"), shapes=((8, 8), (8, 8)), grid=(6, 6, 6), raytraced=True, direct_only=True,
+                     sparse_cameras=("cam_a", "cam_b"), nframes=1)
+    inp = validate_inputs(case.files)
+    d = rtm_sparse_density(inp)
+    assert d == pytest.approx(np.count_nonzero(case.A) / case.A.size)
+    mixed = make_case(str(tmp_path / "m"), sparse_cameras=("cam_b",), nframes=1)
+    assert rtm_sparse_density(validate_inputs(mixed.files)) == -1.0
+    rp, ci, vv = native().RtmReader(inp.rtm_files, inp.rtm_name, inp.nvoxel).read_csr(5, 70)
+    np.testing.assert_array_equal(_dense(65, inp.nvoxel, rp, ci, vv), case.A[5:70].astype(np.float32))
