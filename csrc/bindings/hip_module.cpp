@@ -278,6 +278,28 @@ static void bind_engine(py::module_& m) {
                  }
              }),
              py::keep_alive<1, 8>())
+        .def_static("from_sparse",
+                    [](int device, uintptr_t row_ptr, uintptr_t col, uintptr_t val, uintptr_t col_ptr, uintptr_t row,
+                       uintptr_t cval, int64_t nnz, int64_t nrows, int64_t nvoxel,
+                       std::shared_ptr<sart::Communicator> comm, const sart::EngineConfig& cfg) {
+                        sart::SparseRtm s;
+                        s.row_ptr = P<const int64_t>(row_ptr);
+                        s.col = P<const int32_t>(col);
+                        s.val = P<const float>(val);
+                        s.col_ptr = P<const int64_t>(col_ptr);
+                        s.row = P<const int32_t>(row);
+                        s.cval = P<const float>(cval);
+                        s.nnz = nnz;
+                        const int64_t pp = (nrows + 63) / 64 * 64, ld = (nvoxel + 63) / 64 * 64;
+                        try {
+                            return new sart::MultiFrameEngine(device, nullptr, nrows, pp, nvoxel, ld, comm.get(), cfg,
+                                                              &s);
+                        } catch (const std::invalid_argument& e) {
+                            throw py::value_error(e.what());
+                        }
+                    },
+                    py::keep_alive<0, 11>())
+        .def_property_readonly("sparse", &sart::MultiFrameEngine::sparse)
         .def_property_readonly("batch_frames", &sart::MultiFrameEngine::batch_frames)
         .def_property_readonly("split_a", &sart::MultiFrameEngine::split_a)
         .def_property_readonly("forward_split", &sart::MultiFrameEngine::forward_split)

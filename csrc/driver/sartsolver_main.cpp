@@ -388,7 +388,7 @@ int main(int argc, char** argv) {
         // --rtm_format: the single-frame GPU solver on pixel-row shards of fp32 values can keep a sparse RTM sparse
         // (decided from the files' metadata: the same on every rank)
         bool sparse = false;
-        if (!cols && (!gpu || cfg.batch_frames == 1) && !cfg.rtm_bf16 && cfg.rtm_format != "dense") {
+        if (!cols && !cfg.rtm_bf16 && cfg.rtm_format != "dense") {
             const double dens = rtm_sparse_density(in.rtm_files, in.rtm_name, in.npixel, in.nvoxel);
             // auto: the sparse kernels read 16 bytes per non-zero and sweep (CSR + CSC, index + value) against 4 bytes
             // per element for the dense fused sweep; measured at 32768 x 32768 (uniform random positions): sparse /
@@ -437,9 +437,16 @@ int main(int argc, char** argv) {
             EngineConfig ec;
             static_cast<SolverParams&>(ec) = params;
             ec.mf_frames = cfg.batch_frames;  // batch width 16, 32, 64 or 128 (rounded up; 128: bf16 storage and f16-pair split-A)
-            ec.rtm_bf16 = dshard->bf16;       // bf16 MFMA projections
-            mf = std::make_unique<MultiFrameEngine>(device, dshard->A, dshard->nrows,
-                                                    dshard->nrows_pad, dshard->nvoxel, dshard->ld, dcomm.get(), ec);
+            if (sparse) {  // fp32 SpMM projections of the CSR / CSC shard
+                const SparseRtm view = sshard->view();
+                mf = std::make_unique<MultiFrameEngine>(device, nullptr, sshard->nrows, (sshard->nrows + 63) / 64 * 64,
+                                                        sshard->nvoxel, (sshard->nvoxel + 63) / 64 * 64, dcomm.get(),
+                                                        ec, &view);
+            } else {
+                ec.rtm_bf16 = dshard->bf16;  // bf16 MFMA projections
+                mf = std::make_unique<MultiFrameEngine>(device, dshard->A, dshard->nrows, dshard->nrows_pad,
+                                                        dshard->nvoxel, dshard->ld, dcomm.get(), ec);
+            }
             if (lap.nnz()) mf->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
         } else if (gpu) {
             EngineConfig ec;

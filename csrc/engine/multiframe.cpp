@@ -25,10 +25,20 @@ int MultiFrameEngine::batch_width(int frames) {
 }
 
 MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel,
-                                   int64_t ld, Communicator* comm, const EngineConfig& cfg)
+                                   int64_t ld, Communicator* comm, const EngineConfig& cfg, const SparseRtm* sparse)
     : device_(device), A_(A), bf16_(cfg.rtm_bf16), P_(nrows), Pp_(nrows_pad), V_(nvoxel), ld_(ld), comm_(comm),
       cfg_(cfg) {
     validate_params(cfg_);
+    if (sparse) {
+        if (bf16_) throw std::invalid_argument("MultiFrameEngine: a sparse shard holds fp32 values");
+        if (!sparse->row_ptr || !sparse->col_ptr)
+            throw std::invalid_argument("MultiFrameEngine: sparse shard needs its CSR and CSC arrays");
+        sparse_ = true;
+        sp_ = *sparse;
+        cfg_.mf_split_a = 0;  // fp32 SpMM: no operand splits
+    } else if (!A_) {
+        throw std::invalid_argument("MultiFrameEngine: dense shard pointer required");
+    }
     if (const char* fn = std::getenv("SART_FAULT_NAN"); fn && *fn && cfg_.fault_nan_sweep < 0)
         cfg_.fault_nan_sweep = std::atoi(fn);
     if (!comm_) throw std::invalid_argument("MultiFrameEngine: communicator required");
@@ -47,11 +57,12 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     // split-A back-projection: f16 pairs (three products) unless SART_MF_BWD16=0 (bf16 hi + mid + lo, six); split-A
     // forward: f16 pairs unless SART_MF_FWD16=0 (bf16 hi + lo, whose 2^-17 per product is not fp32-grade on rows
     // dominated by a few entries: tests/test_gpu_realistic.py)
+    if (sparse_) x3_ = false;
     if (const char* e = std::getenv("SART_MF_BWD16"); x3_) h16_ = !(e && *e && std::atoi(e) == 0);
     if (const char* e = std::getenv("SART_MF_FWD16"); x3_) fwd16_ = !(e && *e && std::atoi(e) == 0);
     // 128 columns (8 MFMA column groups) exist for bf16 storage and for split-A with the f16-pair back-projection;
     // the fp32 MFMA and three-piece bf16 back-projection paths take 64-frame batches
-    if (nf_ == 128 && !(bf16_ || (x3_ && h16_))) nf_ = 64;
+    if (nf_ == 128 && !(sparse_ || bf16_ || (x3_ && h16_))) nf_ = 64;
     const int NF = nf_;
     split_ = bf16_ || x3_;
     if (split_) {  // X planes blocked [ld / 32][nf][32] for the forward (SART_MF_XBLK=0: frame-major, A/B runs)
@@ -70,6 +81,10 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     hip_ok(hipEventCreateWithFlags(&ev_copy_, hipEventDisableTiming), "hipEventCreate");
     nsf_ = mf_forward_num_splits(ld_, Pp_, bf16_ ? 512 : 0);  // bf16 storage: ~512 workgroups (see the back-projection)
     nsb_ = split_ ? mf_backproject_b16_num_splits(ld_, P_, x3_) : mf_backproject_num_splits(ld_, P_);
+    if (sparse_) {  // the SpMM kernels write complete sums
+        nsf_ = nsb_ = 1;
+        Xt_.resize((size_t)ld_ * NF);
+    }
     nwb_ = mf_weights_num_blocks(Pp_);
     X_.resize((size_t)NF * ld_);
     Xprev_.resize((size_t)NF * ld_);
@@ -107,7 +122,10 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
             Wl_.resize((size_t)NF * Pp_);
         }
     }
-    rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_, false, bf16_);
+    if (sparse_)
+        rs_.compute_sparse(sp_, P_, Pp_, V_, ld_, comm_, cfg_, stream_);
+    else
+        rs_.compute(A_, P_, Pp_, V_, ld_, comm_, cfg_, stream_, false, bf16_);
     // chunks of the overlapped back-projection / all-reduce pipeline (several ranks only): SART_MF_CHUNKS
     // (default 4) voxel ranges aligned to the back-projection's voxel tile, each >= 1 MiB of corrections
     int nchunks = 1;
@@ -172,14 +190,20 @@ void MultiFrameEngine::set_laplacian(const int64_t* row_ptr, const int32_t* col,
 }
 
 std::string MultiFrameEngine::forward_split() const {
+    if (sparse_) return "sparse-fp32";
     return bf16_ ? "bf16-storage" : (!x3_ ? "fp32" : (fwd16_ ? "f16x2" : "bf16x2"));
 }
 
 std::string MultiFrameEngine::backproject_split() const {
+    if (sparse_) return "sparse-fp32";
     return bf16_ ? "bf16-storage" : (!x3_ ? "fp32" : (h16_ ? "f16x2" : "bf16x3"));
 }
 
 void MultiFrameEngine::forward() {
+    if (sparse_) {
+        launch_mf_sparse_forward(sp_, P_, Pp_, X_.get(), ld_, Xt_.get(), Fs_.get(), nf_, stream_, g_mf_skip);
+        return;
+    }
     if (fwd16_) {
         uint16_t* x1 = reinterpret_cast<uint16_t*>(Xh_.get());
         uint16_t* x2 = reinterpret_cast<uint16_t*>(Xl_.get());
@@ -202,6 +226,10 @@ void MultiFrameEngine::forward() {
 }
 
 void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int64_t v1, bool have_max) {
+    if (sparse_) {
+        launch_mf_sparse_backproject(sp_, V_, W, part_.get(), nf_, v0, v1, stream_, g_mf_skip);
+        return;
+    }
     if (h16_) {
         uint16_t* w1 = W16_.get();
         uint16_t* w2 = W16_.get() + (size_t)nf_ * Pp_;

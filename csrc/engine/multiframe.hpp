@@ -25,8 +25,10 @@ class MultiFrameEngine {
    public:
     // A: fp32 [nrows_pad][ld], or bf16 when cfg.rtm_bf16 (bf16 MFMA projections, multiframe_bf16.hip); fp32
     // shards run on fp32 MFMA (multiframe.hip) or split into bf16 on the bf16 matrix cores (cfg.mf_split_a)
+    // sparse: the shard as device CSR + CSC arrays instead (A null; not owned): fp32 SpMM projections on the
+    // frames' fp32 state (csrc/kernels/sparse.hip), no operand splits
     MultiFrameEngine(int device, const void* A, int64_t nrows, int64_t nrows_pad, int64_t nvoxel, int64_t ld,
-                     Communicator* comm, const EngineConfig& cfg);
+                     Communicator* comm, const EngineConfig& cfg, const SparseRtm* sparse = nullptr);
     ~MultiFrameEngine();
     MultiFrameEngine(const MultiFrameEngine&) = delete;
     MultiFrameEngine& operator=(const MultiFrameEngine&) = delete;
@@ -43,6 +45,7 @@ class MultiFrameEngine {
     int64_t nvoxel() const { return V_; }
     int batch_frames() const { return nf_; }
     bool split_a() const { return x3_; }  // fp32 shard on the bf16 matrix cores
+    bool sparse() const { return sparse_; }
     // the operand pieces of the split-A projections ("f16x2" range-safe f16 pairs, "bf16x2" / "bf16x3" bf16 pieces),
     // "fp32" (fp32 MFMA) or "bf16-storage"
     std::string forward_split() const;
@@ -72,6 +75,9 @@ class MultiFrameEngine {
 
     int device_;
     const void* A_;
+    bool sparse_ = false;
+    SparseRtm sp_{};
+    DeviceArray<float> Xt_;  // sparse: X voxel-major [ld][nf] for the row gathers
     bool bf16_ = false;
     bool x3_ = false;     // fp32 shard on the bf16 matrix cores (EngineConfig::mf_split_a)
     bool split_ = false;  // X / W enter as hi + lo bf16 planes (bf16_ || x3_)

@@ -113,6 +113,143 @@ __global__ __launch_bounds__(256) void k_sparse_sum_f64(const int64_t* __restric
     if (sub == 0 && i < n) out[i] = acc;
 }
 
+static void check_sparse(const SparseRtm& s, const char* what) {
+    if (!s.row_ptr || !s.col_ptr || (s.nnz > 0 && (!s.col || !s.val || !s.row || !s.cval)))
+        throw std::runtime_error(std::string(what) + ": incomplete sparse RTM (CSR and CSC arrays required)");
+}
+
+// ------------------------------------------------------------------------------------------- multi-frame (SpMM)
+// The multi-frame engine's projections of a sparse shard (MultiFrameEngine sparse mode): one wave per row
+// (column), the batch's frames across the lanes (NF >= 64: NF / 64 frames per lane; NF < 64: 64 / NF entries of the
+// row in flight per wave, combined by a fixed xor tree), so each entry's operand row (NF consecutive fp32 of the
+// frame-contiguous copy of X, or of W) is one coalesced load. fp32 fma chains in entry order per lane.
+
+// W's back-projection layout [rows][16][nf / 16] (multiframe_glue.hip::mf_bp_slot)
+__device__ __forceinline__ int mf_bp_slot_s(int f, int nf) { return (f & 15) * (nf >> 4) + (f >> 4); }
+
+// X [nf][ld] (frame-major) -> Xt [ld][nf] (voxel-major), 64 x 64 tiles through LDS
+__global__ __launch_bounds__(256) void k_mf_transpose_x(const float* __restrict__ X, int64_t ld, int nf,
+                                                        float* __restrict__ Xt, const int* __restrict__ skip) {
+    if (skip && *skip) return;
+    __shared__ float t[64][65];
+    const int64_t v0 = (int64_t)blockIdx.x * 64;
+    const int f0 = blockIdx.y * 64;
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int ff = i >> 6, vv = i & 63;
+        if (f0 + ff < nf) t[ff][vv] = X[(int64_t)(f0 + ff) * ld + v0 + vv];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int vv = i >> 6, ff = i & 63;
+        if (f0 + ff < nf) Xt[(v0 + vv) * nf + f0 + ff] = t[ff][vv];
+    }
+}
+
+template <int NF, bool BWD>
+__global__ __launch_bounds__(256) void k_mf_sparse_spmm(const int64_t* __restrict__ ptr, const int32_t* __restrict__ idx,
+                                                        const float* __restrict__ val, int64_t n_valid, int64_t i0,
+                                                        int64_t i1, const float* __restrict__ Y,
+                                                        float* __restrict__ out, const int* __restrict__ skip) {
+    if (skip && *skip) return;
+    constexpr int LG = NF >= 64 ? 64 : NF;  // lanes per entry
+    constexpr int FL = NF / LG;             // frames per lane
+    constexpr int G = 64 / LG;              // entries in flight per wave
+    // eight fp32 chains per row and frame (G groups x CH chains per lane, entries dealt round robin): one chain over
+    // a dense row of thousands of entries would exceed an fp32 evaluation's error (tests/test_gpu_sparse.py)
+    constexpr int CH = G >= 8 ? 1 : 8 / G;
+    const int lane = threadIdx.x & 63, grp = lane / LG, fl = lane % LG;
+    const int64_t i = i0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // row (forward) / column (back-projection)
+    if (i >= i1) return;
+    float acc[CH][FL];
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+        for (int j = 0; j < FL; ++j) acc[c][j] = 0.f;
+    if (i < n_valid) {
+        const int64_t k1 = ptr[i + 1];
+        int64_t k = ptr[i] + grp;
+        for (; k + (CH - 1) * G < k1; k += CH * G)
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                const float a = val[k + c * G];
+                const float* y = Y + (int64_t)idx[k + c * G] * NF;
+#pragma unroll
+                for (int j = 0; j < FL; ++j) {
+                    const int f = fl + j * LG;
+                    acc[c][j] = __builtin_fmaf(a, y[BWD ? mf_bp_slot_s(f, NF) : f], acc[c][j]);
+                }
+            }
+        for (int c = 0; k < k1; k += G, ++c) {  // tail: chains 0, 1, ... in turn
+            const float a = val[k];
+            const float* y = Y + (int64_t)idx[k] * NF;
+#pragma unroll
+            for (int j = 0; j < FL; ++j) {
+                const int f = fl + j * LG;
+#pragma unroll
+                for (int cc = 0; cc < CH; ++cc)
+                    if (cc == c) acc[cc][j] = __builtin_fmaf(a, y[BWD ? mf_bp_slot_s(f, NF) : f], acc[cc][j]);
+            }
+        }
+    }
+    // chains pairwise, then the groups by a fixed xor tree
+#pragma unroll
+    for (int w = 1; w < CH; w <<= 1)
+#pragma unroll
+        for (int c = 0; c + w < CH; c += 2 * w)
+#pragma unroll
+            for (int j = 0; j < FL; ++j) acc[c][j] += acc[c + w][j];
+    float tot[FL];
+#pragma unroll
+    for (int j = 0; j < FL; ++j) tot[j] = acc[0][j];
+#pragma unroll
+    for (int o = LG; o < 64; o <<= 1)
+#pragma unroll
+        for (int j = 0; j < FL; ++j) tot[j] += __shfl_xor(tot[j], o);
+    if (grp == 0)
+#pragma unroll
+        for (int j = 0; j < FL; ++j) out[i * NF + fl + j * LG] = tot[j];  // zero for padded rows / columns
+}
+
+void launch_mf_sparse_forward(const SparseRtm& s, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ld,
+                              float* Xt, float* Fout, int nf, hipStream_t stream, const int* skip) {
+    check_sparse(s, "mf_sparse_forward");
+    if (ld % 64 != 0) throw std::runtime_error("mf_sparse_forward: ld must be a multiple of 64");
+    hipLaunchKernelGGL(k_mf_transpose_x, dim3((unsigned)(ld / 64), (unsigned)((nf + 63) / 64)), dim3(256), 0, stream,
+                       X, ld, nf, Xt, skip);
+    check_launch("k_mf_transpose_x");
+    const dim3 grid((unsigned)((nrows_pad + 3) / 4));
+    auto go = [&](auto k) {
+        hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, s.row_ptr, s.col, s.val, nrows, (int64_t)0, nrows_pad, Xt,
+                           Fout, skip);
+    };
+    switch (nf) {
+        case 16: go(k_mf_sparse_spmm<16, false>); break;
+        case 32: go(k_mf_sparse_spmm<32, false>); break;
+        case 64: go(k_mf_sparse_spmm<64, false>); break;
+        case 128: go(k_mf_sparse_spmm<128, false>); break;
+        default: throw std::runtime_error("mf_sparse_forward: nf must be 16, 32, 64 or 128");
+    }
+    check_launch("k_mf_sparse_spmm (forward)");
+}
+
+void launch_mf_sparse_backproject(const SparseRtm& s, int64_t nvoxel, const float* W, float* part, int nf,
+                                  int64_t v0, int64_t v1, hipStream_t stream, const int* skip) {
+    check_sparse(s, "mf_sparse_backproject");
+    if (v1 <= v0) return;
+    const dim3 grid((unsigned)((v1 - v0 + 3) / 4));
+    auto go = [&](auto k) {
+        hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, s.col_ptr, s.row, s.cval, nvoxel, v0, v1, W, part, skip);
+    };
+    switch (nf) {
+        case 16: go(k_mf_sparse_spmm<16, true>); break;
+        case 32: go(k_mf_sparse_spmm<32, true>); break;
+        case 64: go(k_mf_sparse_spmm<64, true>); break;
+        case 128: go(k_mf_sparse_spmm<128, true>); break;
+        default: throw std::runtime_error("mf_sparse_backproject: nf must be 16, 32, 64 or 128");
+    }
+    check_launch("k_mf_sparse_spmm (back-projection)");
+}
+
 int sparse_lanes(double avg) {
     if (const char* e = std::getenv("SART_SPARSE_LANES"); e && *e) {
         const int l = std::atoi(e);
@@ -134,10 +271,6 @@ int64_t csr_forward_num_blocks(const SparseRtm& s, int64_t nrows_pad) {
     return (nrows_pad + rpb - 1) / rpb;
 }
 
-static void check_sparse(const SparseRtm& s, const char* what) {
-    if (!s.row_ptr || !s.col_ptr || (s.nnz > 0 && (!s.col || !s.val || !s.row || !s.cval)))
-        throw std::runtime_error(std::string(what) + ": incomplete sparse RTM (CSR and CSC arrays required)");
-}
 
 template <int L>
 static void csr_forward_l(int epi, const SparseRtm& s, int64_t nrows, int64_t nrows_pad, const float* x,

@@ -87,8 +87,8 @@ std::string usage() {
            "                              block; all-reduce of A x per iteration) instead of by pixel rows.\n"
            "  --rtm_bf16                  Store the RTM in bf16 on the GPU (half the memory and bytes per sweep;\n"
            "                              products and sums stay fp32).\n"
-           "  --rtm_format F              auto | dense | sparse: keep a sparse RTM sparse (CSR + CSC; single-frame\n"
-           "                              GPU and CPU solvers, pixel-row shards). auto: when every RTM dataset is\n"
+           "  --rtm_format F              auto | dense | sparse: keep a sparse RTM sparse (CSR + CSC; the GPU\n"
+           "                              solvers and the CPU solver, pixel-row shards). auto: when every RTM dataset is\n"
            "                              sparse COO with at most 10 % non-zeros. [default: auto]\n"
            "  --profile FILE              Write per-frame timing/iteration telemetry as JSON lines.\n";
 }
@@ -180,8 +180,8 @@ Config parse_arguments(const std::vector<std::string>& argv) {
         throw Error("Argument rtm_bf16 applies to the GPU solvers with pixel-row shards only.");
     if (c.rtm_format != "auto" && c.rtm_format != "dense" && c.rtm_format != "sparse")
         throw Error("Argument rtm_format must be auto, dense or sparse, " + c.rtm_format + " given.");
-    if (c.rtm_format == "sparse" && (c.partition_voxels || c.batch_frames > 1 || c.rtm_bf16))
-        throw Error("Argument rtm_format sparse applies to the single-frame solvers with fp32 pixel-row shards only.");
+    if (c.rtm_format == "sparse" && (c.partition_voxels || c.rtm_bf16 || (c.use_cpu && c.batch_frames > 1)))
+        throw Error("Argument rtm_format sparse applies to fp32 pixel-row shards (and not to CPU batches).");
     if (c.input_files.size() < 2)
         throw Error("At least two input file, one with RTM and one with image, are required, " +
                     std::to_string(c.input_files.size()) + " given.");

@@ -37,7 +37,7 @@ MAX_BATCH = 128  # widest batch: 8 column groups (bf16 storage and split-A with 
 
 
 class MultiFrameSARTSolver:
-    def __init__(self, rtm: DenseRTM, laplacian: Optional[LaplacianCSR] = None, comm: Optional[Communicator] = None,
+    def __init__(self, rtm, laplacian: Optional[LaplacianCSR] = None, comm: Optional[Communicator] = None,
                  params: Optional[SolverParams] = None, logarithmic: bool = False, batch: int = NF,
                  check_interval: int = 16, allow_zero_tolerance: bool = False, split_a: Optional[bool] = None):
         if getattr(rtm, "is_column_shard", False):
@@ -71,8 +71,12 @@ class MultiFrameSARTSolver:
         cfg.mf_split_a = -1 if split_a is None else int(bool(split_a))
         device = self.dev.index if self.dev.index is not None else 0
         self.native_comm = native_communicator(self.comm, device)
-        self.engine = self.k.MultiFrameEngine(device, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld,
-                                              self.native_comm, cfg)
+        if getattr(rtm, "nnz", None) is not None:  # SparseRTM: fp32 SpMM projections (csrc/kernels/sparse.hip)
+            self.engine = self.k.MultiFrameEngine.from_sparse(device, *rtm.pointers(), rtm.nnz, rtm.npixel,
+                                                              rtm.nvoxel, self.native_comm, cfg)
+        else:
+            self.engine = self.k.MultiFrameEngine(device, rtm.A.data_ptr(), rtm.npixel, rtm.nrows_pad, rtm.nvoxel,
+                                                  rtm.ld, self.native_comm, cfg)
         if self.L is not None:
             self.engine.set_laplacian(self.L.row_ptr_host, self.L.col_host, self.L.val_host)
         self.P, self.Pp, self.V, self.ld = rtm.npixel, rtm.nrows_pad, rtm.nvoxel, rtm.ld

@@ -56,8 +56,8 @@ def test_short_and_long_aliases(n):
     (["--rtm_bf16", "--use_cpu", "a", "b"], "rtm_bf16 applies to the GPU solvers with pixel-row shards"),
     (["--rtm_bf16", "--partition_voxels", "a", "b"], "rtm_bf16 applies to the GPU solvers with pixel-row shards"),
     (["--rtm_format", "csr", "a", "b"], "rtm_format must be auto, dense or sparse"),
-    (["--rtm_format", "sparse", "--batch_frames", "16", "a", "b"], "rtm_format sparse applies to the single-frame"),
-    (["--rtm_format", "sparse", "--partition_voxels", "a", "b"], "rtm_format sparse applies to the single-frame"),
+    (["--rtm_format", "sparse", "--batch_frames", "16", "--use_cpu", "a", "b"], "rtm_format sparse applies to fp32"),
+    (["--rtm_format", "sparse", "--partition_voxels", "a", "b"], "rtm_format sparse applies to fp32"),
 ])
 def test_validation_errors(n, argv, msg):
     with pytest.raises(RuntimeError, match=msg.replace("(", r"\(").replace(")", r"\)").replace("]", r"\]")):

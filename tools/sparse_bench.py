@@ -31,6 +31,7 @@ def main():
                     help="instead of the ray-traced matrix: uniform random positions at this density, --shape rows x "
                          "--grid voxels (the break-even density of the sparse path against the dense fused sweep)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--frames", default="", help="comma list of multi-frame batch widths to time as well (SpMM)")
     a = ap.parse_args()
     import torch
 
@@ -80,6 +81,26 @@ def main():
     g = s_sp.forward_project(x_true)  # f = A x_true on the GPU (the sparse forward)
     x_sp = run("sparse (CSR + CSC)", s_sp, g)
     lines[-1].update(bytes_per_iter=2 * sp.nnz * 8, build_s=round(build_s, 2))
+    for nf in [int(t) for t in a.frames.split(",") if t]:
+        from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+
+        Xs = np.stack([phantom(grid, t=0.1 * k) for k in range(nf)]) if a.random_density <= 0 else \
+            np.random.default_rng(2).random((nf, V)) + 0.1
+        Gs = np.stack([s_sp.forward_project(Xs[k]) for k in range(nf)])
+        mf = MultiFrameSARTSolver(sp, None, None, p, batch=nf, allow_zero_tolerance=True)
+        mf.solve_batch(Gs)  # warm-up
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(a.steps):
+            mf.solve_batch(Gs)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t) / a.steps
+        rec = dict(path=f"sparse multi-frame x{nf} (SpMM)", P=P, V=V, nnz=sp.nnz, density=round(sp.density, 6),
+                   iters=a.iters, frames=nf, ms_per_solve=round(1e3 * dt, 3),
+                   frame_iters_per_s=round(nf * a.iters / dt, 1), grid=list(grid))
+        lines.append(rec)
+        print(json.dumps(rec), flush=True)
+        del mf
     if not a.no_dense:
         rt = DenseRTM(P, V, device=dev)
         rt.A.zero_()
