@@ -680,6 +680,23 @@ for step in "$@"; do
     r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r4bench) run bench_r4 300 python bench.py --steps 20 --warmup 5 ;;
     r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    pmcfinal)  # HBM bytes (FETCH_SIZE) and occupancy counters of the headline fused sweep, the sparse kernels and the
+               # 64-frame split-A kernels, each pass its own run with the kernel trace (durations) beside the counters
+      PMC_OCC="SQ_WAVES SQ_LEVEL_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_MFMA GRBM_GUI_ACTIVE"
+      for spec in "head|bench.py --steps 1 --warmup 0 --no-selfcheck" \
+                  "sparse|tools/sparse_bench.py --no-dense --steps 1 --iters 20 --frames 64" \
+                  "mf64|bench.py --steps 1 --warmup 0 --frames 64 --iters 5 --no-selfcheck"; do
+        tag=${spec%%|*}; cmd=${spec#*|}
+        for pass in fetch occ; do
+          if [ $pass = fetch ]; then ctr="FETCH_SIZE GRBM_GUI_ACTIVE"; else ctr=$PMC_OCC; fi
+          echo "=== pmc_${tag}_$pass ($(date +%T))" | tee -a "$OUT/session.log"
+          timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $ctr -d "$OUT/pmc_${tag}_$pass" -o run --output-format csv \
+            -- python3 $cmd > "$OUT/pmc_${tag}_$pass.log" 2>&1
+          rc=$?; echo "=== pmc_${tag}_$pass rc=$rc" | tee -a "$OUT/session.log"; tail -n 3 "$OUT/pmc_${tag}_$pass.log"
+          case $rc in 0|1) ;; *) echo "FATAL pmc rc=$rc" | tee -a "$OUT/session.log"; exit $rc ;; esac
+        done
+      done
+      python3 tools/pmc_summary.py "$OUT"/pmc_head_* "$OUT"/pmc_sparse_* "$OUT"/pmc_mf64_* > "$OUT/pmc_summary.txt" 2>&1 || true ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
