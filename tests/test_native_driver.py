@@ -350,12 +350,14 @@ def test_module_entry_point_does_not_orphan_the_driver(tmp_path, binary, sig):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("p2p", ["0", "1"])
-def test_native_sparse_two_ranks_one_device(tmp_path, binary, p2p):
+@pytest.mark.parametrize("batch", [[], ["--batch_frames", "16"]], ids=["frame", "batch16"])
+def test_native_sparse_two_ranks_one_device(tmp_path, binary, p2p, batch):
     """The sparse RTM path (--rtm_format sparse) on two ranks of the box's single GPU (row shards of the CSR, the
-    per-iteration all-reduce staged or P2P) against the one-rank sparse run and the dense run of the same files."""
+    per-iteration all-reduce staged or P2P) against the one-rank sparse run and the dense run of the same files;
+    frame by frame and as a batch (the multi-frame engine's SpMM, its chunked all-reduce of the back-projection)."""
     case = make_case(str(tmp_path / "c"), sparse_cameras=("cam_a", "cam_b"), laplacian=True, nframes=2,
                      grid=(12, 12, 12), shapes=((24, 32), (20, 30)), raytraced=True)
-    base = ["-m", "40", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3"]
+    base = ["-m", "40", "-c", "1e-6", "-l", case.laplacian_file, "-b", "1e-3"] + batch
     r = _run_native(binary, base + ["--rtm_format", "sparse", "-o", str(tmp_path / "one.h5"), *case.files])
     assert r.returncode == 0, r.stderr
     assert "sparse: " in r.stdout

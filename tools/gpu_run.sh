@@ -26,7 +26,7 @@ for step in "$@"; do
   case $step in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
-    testsall) run pytest_gpu_all 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    testsall) run pytest_gpu_all 1140 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     bench) run bench 600 python bench.py --steps 5 --warmup 1 ;;
     bench2) run bench_twopass 600 python bench.py --steps 5 --warmup 1 --no-fused ;;
     benchlog) run bench_log 600 python bench.py --steps 5 --warmup 1 --variant log ;;
