@@ -84,6 +84,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     if (sparse_) {  // the SpMM kernels write complete sums
         nsf_ = nsb_ = 1;
         Xt_.resize((size_t)ld_ * NF);
+        Wt_.resize((size_t)Pp_ * NF);  // W as frame-order planes (batches wider than mf_sparse_plane_width)
     }
     nwb_ = mf_weights_num_blocks(Pp_);
     X_.resize((size_t)NF * ld_);
@@ -227,7 +228,11 @@ void MultiFrameEngine::forward() {
 
 void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int64_t v1, bool have_max) {
     if (sparse_) {
-        launch_mf_sparse_backproject(sp_, V_, W, part_.get(), nf_, v0, v1, stream_, g_mf_skip);
+        if (mf_sparse_needs_w_planes(nf_)) {
+            if (split_w) launch_mf_w_planes(W, Pp_, nf_, Wt_.get(), stream_, g_mf_skip);
+            W = Wt_.get();
+        }
+        launch_mf_sparse_backproject(sp_, V_, W, Pp_, part_.get(), nf_, v0, v1, stream_, g_mf_skip);
         return;
     }
     if (h16_) {

@@ -77,7 +77,8 @@ class MultiFrameEngine {
     const void* A_;
     bool sparse_ = false;
     SparseRtm sp_{};
-    DeviceArray<float> Xt_;  // sparse: X voxel-major [ld][nf] for the row gathers
+    DeviceArray<float> Xt_;  // sparse: X voxel-major planes [nf / PW][ld][PW] for the row gathers
+    DeviceArray<float> Wt_;  // sparse: W as frame-order planes [nf / PW][rows][PW] (launch_mf_w_planes)
     bool bf16_ = false;
     bool x3_ = false;     // fp32 shard on the bf16 matrix cores (EngineConfig::mf_split_a)
     bool split_ = false;  // X / W enter as hi + lo bf16 planes (bf16_ || x3_)

@@ -120,15 +120,33 @@ static void check_sparse(const SparseRtm& s, const char* what) {
 
 // ------------------------------------------------------------------------------------------- multi-frame (SpMM)
 // The multi-frame engine's projections of a sparse shard (MultiFrameEngine sparse mode): one wave per row
-// (column), the batch's frames across the lanes (NF >= 64: NF / 64 frames per lane; NF < 64: 64 / NF entries of the
-// row in flight per wave, combined by a fixed xor tree), so each entry's operand row (NF consecutive fp32 of the
-// frame-contiguous copy of X, or of W) is one coalesced load. fp32 fma chains in entry order per lane.
+// (column), the frames of one plane across the lanes (PW < 64: 64 / PW entries of the row in flight per wave, combined
+// by a fixed xor tree), so each entry's operand row (PW consecutive fp32 of the voxel-major copy of X, or of W) is one
+// coalesced load. fp32 fma chains in entry order per lane. A batch of nf > PW frames runs as nf / PW planes of PW
+// frames (grid.y): a launch then gathers from the working set of one plane (the interleaved [n][128] rows of a
+// 128-frame batch ran at 83.1k frame-it/s, two 64-frame planes at 183k; mf_sparse_plane_width).
+
+int mf_sparse_plane_width(int nf) {
+    int pw = 64;
+    if (const char* e = std::getenv("SART_MF_SPARSE_PW"); e && *e) pw = std::atoi(e);
+    if (pw != 16 && pw != 32 && pw != 64) throw std::runtime_error("SART_MF_SPARSE_PW must be 16, 32 or 64");
+    return nf < pw ? nf : pw;
+}
+
+// The back-projection reads W in its slot layout only for one plane of <= 32 frames: there the 16 lanes of each quarter
+// wave (one pass of the address path) still touch a single 128-B line. At 64 frames the slot order spreads them over
+// the whole 256-B row, twice the lines per gather (113.5k against 183.5k frame-it/s per 64-frame plane,
+// profiles/sparse_r5_plane_width.txt), so W is re-laid in frame order first (launch_mf_w_planes).
+bool mf_sparse_needs_w_planes(int nf) {
+    const int pw = mf_sparse_plane_width(nf);
+    return pw < nf || pw > 32;
+}
 
 // W's back-projection layout [rows][16][nf / 16] (multiframe_glue.hip::mf_bp_slot)
 __device__ __forceinline__ int mf_bp_slot_s(int f, int nf) { return (f & 15) * (nf >> 4) + (f >> 4); }
 
-// X [nf][ld] (frame-major) -> Xt [ld][nf] (voxel-major), 64 x 64 tiles through LDS
-__global__ __launch_bounds__(256) void k_mf_transpose_x(const float* __restrict__ X, int64_t ld, int nf,
+// X [nf][ld] (frame-major) -> Xt [nf / pw][ld][pw] (voxel-major planes of pw frames), 64 x 64 tiles through LDS
+__global__ __launch_bounds__(256) void k_mf_transpose_x(const float* __restrict__ X, int64_t ld, int nf, int pw,
                                                         float* __restrict__ Xt, const int* __restrict__ skip) {
     if (skip && *skip) return;
     __shared__ float t[64][65];
@@ -140,114 +158,116 @@ __global__ __launch_bounds__(256) void k_mf_transpose_x(const float* __restrict_
     }
     __syncthreads();
     for (int i = threadIdx.x; i < 64 * 64; i += 256) {
-        const int vv = i >> 6, ff = i & 63;
-        if (f0 + ff < nf) Xt[(v0 + vv) * nf + f0 + ff] = t[ff][vv];
+        const int vv = i >> 6, ff = i & 63, f = f0 + ff;
+        if (f < nf) Xt[((int64_t)(f / pw) * ld + v0 + vv) * pw + f % pw] = t[ff][vv];
     }
 }
 
-template <int NF, bool BWD>
+// W [rows][nf] in the back-projection slot layout -> Wt [nf / pw][rows][pw] in frame order
+__global__ __launch_bounds__(256) void k_mf_w_planes(const float* __restrict__ W, int64_t rows, int nf, int pw,
+                                                     float* __restrict__ Wt, const int* __restrict__ skip) {
+    if (skip && *skip) return;
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (plane, row, frame) in Wt order
+    if (e >= rows * nf) return;
+    const int64_t p = (e / pw) % rows;
+    const int f = (int)(e % pw) + pw * (int)(e / (rows * pw));
+    Wt[e] = W[p * nf + mf_bp_slot_s(f, nf)];
+}
+
+// PW frames per plane (16, 32, 64); SLOT: W in the slot layout of a PW-frame batch (a one-plane back-projection);
+// plane blockIdx.y: Y + blockIdx.y * yplane, outputs at frame offset PW blockIdx.y of rows of nfs frames
+template <int PW, bool SLOT>
 __global__ __launch_bounds__(256) void k_mf_sparse_spmm(const int64_t* __restrict__ ptr, const int32_t* __restrict__ idx,
                                                         const float* __restrict__ val, int64_t n_valid, int64_t i0,
-                                                        int64_t i1, const float* __restrict__ Y,
-                                                        float* __restrict__ out, const int* __restrict__ skip) {
+                                                        int64_t i1, const float* __restrict__ Y, int64_t yplane,
+                                                        float* __restrict__ out, int nfs, const int* __restrict__ skip) {
     if (skip && *skip) return;
-    constexpr int LG = NF >= 64 ? 64 : NF;  // lanes per entry
-    constexpr int FL = NF / LG;             // frames per lane
-    constexpr int G = 64 / LG;              // entries in flight per wave
+    constexpr int G = 64 / PW;  // entries in flight per wave
     // eight fp32 chains per row and frame (G groups x CH chains per lane, entries dealt round robin): one chain over
     // a dense row of thousands of entries would exceed an fp32 evaluation's error (tests/test_gpu_sparse.py)
     constexpr int CH = G >= 8 ? 1 : 8 / G;
-    const int lane = threadIdx.x & 63, grp = lane / LG, fl = lane % LG;
+    const int lane = threadIdx.x & 63, grp = lane / PW, fl = lane % PW;
     const int64_t i = i0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // row (forward) / column (back-projection)
     if (i >= i1) return;
-    float acc[CH][FL];
+    Y += (int64_t)blockIdx.y * yplane + (SLOT ? mf_bp_slot_s(fl, PW) : fl);
+    float acc[CH];
 #pragma unroll
-    for (int c = 0; c < CH; ++c)
-#pragma unroll
-        for (int j = 0; j < FL; ++j) acc[c][j] = 0.f;
+    for (int c = 0; c < CH; ++c) acc[c] = 0.f;
     if (i < n_valid) {
         const int64_t k1 = ptr[i + 1];
         int64_t k = ptr[i] + grp;
         for (; k + (CH - 1) * G < k1; k += CH * G)
 #pragma unroll
-            for (int c = 0; c < CH; ++c) {
-                const float a = val[k + c * G];
-                const float* y = Y + (int64_t)idx[k + c * G] * NF;
-#pragma unroll
-                for (int j = 0; j < FL; ++j) {
-                    const int f = fl + j * LG;
-                    acc[c][j] = __builtin_fmaf(a, y[BWD ? mf_bp_slot_s(f, NF) : f], acc[c][j]);
-                }
-            }
+            for (int c = 0; c < CH; ++c) acc[c] = __builtin_fmaf(val[k + c * G], Y[(int64_t)idx[k + c * G] * PW], acc[c]);
         for (int c = 0; k < k1; k += G, ++c) {  // tail: chains 0, 1, ... in turn
-            const float a = val[k];
-            const float* y = Y + (int64_t)idx[k] * NF;
+            const float y = Y[(int64_t)idx[k] * PW], a = val[k];
 #pragma unroll
-            for (int j = 0; j < FL; ++j) {
-                const int f = fl + j * LG;
-#pragma unroll
-                for (int cc = 0; cc < CH; ++cc)
-                    if (cc == c) acc[cc][j] = __builtin_fmaf(a, y[BWD ? mf_bp_slot_s(f, NF) : f], acc[cc][j]);
-            }
+            for (int cc = 0; cc < CH; ++cc)
+                if (cc == c) acc[cc] = __builtin_fmaf(a, y, acc[cc]);
         }
     }
     // chains pairwise, then the groups by a fixed xor tree
 #pragma unroll
     for (int w = 1; w < CH; w <<= 1)
 #pragma unroll
-        for (int c = 0; c + w < CH; c += 2 * w)
+        for (int c = 0; c + w < CH; c += 2 * w) acc[c] += acc[c + w];
+    float tot = acc[0];
 #pragma unroll
-            for (int j = 0; j < FL; ++j) acc[c][j] += acc[c + w][j];
-    float tot[FL];
-#pragma unroll
-    for (int j = 0; j < FL; ++j) tot[j] = acc[0][j];
-#pragma unroll
-    for (int o = LG; o < 64; o <<= 1)
-#pragma unroll
-        for (int j = 0; j < FL; ++j) tot[j] += __shfl_xor(tot[j], o);
-    if (grp == 0)
-#pragma unroll
-        for (int j = 0; j < FL; ++j) out[i * NF + fl + j * LG] = tot[j];  // zero for padded rows / columns
+    for (int o = PW; o < 64; o <<= 1) tot += __shfl_xor(tot, o);
+    if (grp == 0) out[i * nfs + PW * blockIdx.y + fl] = tot;  // zero for padded rows / columns
+}
+
+template <bool SLOT>
+static void spmm(int pw, int nf, dim3 grid, hipStream_t stream, const int64_t* ptr, const int32_t* idx,
+                 const float* val, int64_t n_valid, int64_t i0, int64_t i1, const float* Y, int64_t yplane, float* out,
+                 const int* skip, const char* what) {
+    if ((nf != 16 && nf != 32 && nf != 64 && nf != 128) || nf % pw != 0)
+        throw std::runtime_error(std::string(what) + ": nf must be 16, 32, 64 or 128");
+    auto go = [&](auto k) {
+        hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, ptr, idx, val, n_valid, i0, i1, Y, yplane, out, nf, skip);
+    };
+    switch (pw) {
+        case 16: go(k_mf_sparse_spmm<16, SLOT>); break;
+        case 32: go(k_mf_sparse_spmm<32, SLOT>); break;
+        case 64: go(k_mf_sparse_spmm<64, SLOT>); break;
+        default: throw std::runtime_error(std::string(what) + ": plane width must be 16, 32 or 64");
+    }
+    check_launch(what);
 }
 
 void launch_mf_sparse_forward(const SparseRtm& s, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ld,
                               float* Xt, float* Fout, int nf, hipStream_t stream, const int* skip) {
     check_sparse(s, "mf_sparse_forward");
     if (ld % 64 != 0) throw std::runtime_error("mf_sparse_forward: ld must be a multiple of 64");
+    const int pw = mf_sparse_plane_width(nf);
     hipLaunchKernelGGL(k_mf_transpose_x, dim3((unsigned)(ld / 64), (unsigned)((nf + 63) / 64)), dim3(256), 0, stream,
-                       X, ld, nf, Xt, skip);
+                       X, ld, nf, pw, Xt, skip);
     check_launch("k_mf_transpose_x");
-    const dim3 grid((unsigned)((nrows_pad + 3) / 4));
-    auto go = [&](auto k) {
-        hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, s.row_ptr, s.col, s.val, nrows, (int64_t)0, nrows_pad, Xt,
-                           Fout, skip);
-    };
-    switch (nf) {
-        case 16: go(k_mf_sparse_spmm<16, false>); break;
-        case 32: go(k_mf_sparse_spmm<32, false>); break;
-        case 64: go(k_mf_sparse_spmm<64, false>); break;
-        case 128: go(k_mf_sparse_spmm<128, false>); break;
-        default: throw std::runtime_error("mf_sparse_forward: nf must be 16, 32, 64 or 128");
-    }
-    check_launch("k_mf_sparse_spmm (forward)");
+    const dim3 grid((unsigned)((nrows_pad + 3) / 4), (unsigned)(nf / pw));
+    spmm<false>(pw, nf, grid, stream, s.row_ptr, s.col, s.val, nrows, 0, nrows_pad, Xt, ld * pw, Fout, skip,
+                "k_mf_sparse_spmm (forward)");
 }
 
-void launch_mf_sparse_backproject(const SparseRtm& s, int64_t nvoxel, const float* W, float* part, int nf,
-                                  int64_t v0, int64_t v1, hipStream_t stream, const int* skip) {
+void launch_mf_w_planes(const float* W, int64_t rows, int nf, float* Wt, hipStream_t stream, const int* skip) {
+    const int pw = mf_sparse_plane_width(nf);
+    hipLaunchKernelGGL(k_mf_w_planes, dim3((unsigned)((rows * nf + 255) / 256)), dim3(256), 0, stream, W, rows, nf,
+                       pw, Wt, skip);
+    check_launch("k_mf_w_planes");
+}
+
+void launch_mf_sparse_backproject(const SparseRtm& s, int64_t nvoxel, const float* W, int64_t wrows, float* part,
+                                  int nf, int64_t v0, int64_t v1, hipStream_t stream, const int* skip) {
     check_sparse(s, "mf_sparse_backproject");
     if (v1 <= v0) return;
-    const dim3 grid((unsigned)((v1 - v0 + 3) / 4));
-    auto go = [&](auto k) {
-        hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, s.col_ptr, s.row, s.cval, nvoxel, v0, v1, W, part, skip);
-    };
-    switch (nf) {
-        case 16: go(k_mf_sparse_spmm<16, true>); break;
-        case 32: go(k_mf_sparse_spmm<32, true>); break;
-        case 64: go(k_mf_sparse_spmm<64, true>); break;
-        case 128: go(k_mf_sparse_spmm<128, true>); break;
-        default: throw std::runtime_error("mf_sparse_backproject: nf must be 16, 32, 64 or 128");
-    }
-    check_launch("k_mf_sparse_spmm (back-projection)");
+    const int pw = mf_sparse_plane_width(nf);
+    const dim3 grid((unsigned)((v1 - v0 + 3) / 4), (unsigned)(nf / pw));
+    // W in its slot layout or the frame-order planes of launch_mf_w_planes (mf_sparse_needs_w_planes)
+    if (!mf_sparse_needs_w_planes(nf))
+        spmm<true>(pw, nf, grid, stream, s.col_ptr, s.row, s.cval, nvoxel, v0, v1, W, 0, part, skip,
+                   "k_mf_sparse_spmm (back-projection)");
+    else
+        spmm<false>(pw, nf, grid, stream, s.col_ptr, s.row, s.cval, nvoxel, v0, v1, W, wrows * pw, part, skip,
+                    "k_mf_sparse_spmm (back-projection)");
 }
 
 int sparse_lanes(double avg) {

@@ -234,6 +234,28 @@ def test_multiframe_sparse_vs_oracle(dev, rtms, lap, frames128, which, batch, lo
                          slack=2e-8)
 
 
+@pytest.mark.parametrize("pw", ["16", "32"])
+@pytest.mark.parametrize("batch", [64, 128])
+def test_multiframe_sparse_plane_widths(dev, rtms, lap, frames128, monkeypatch, pw, batch):
+    """Batches as planes of fewer frames (SART_MF_SPARSE_PW: the transposed X and W planes, grid.y; the
+    back-projection's W re-laid from the slot layout in frame order) at the same bound as the default planes of 64."""
+    from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+    from mpi_cuda_sartsolver_amd.models.rtm import SparseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SolverParams
+
+    A, _ = rtms["reflections"]
+    G = frames128[:batch] @ A.T.astype(np.float64)
+    iters, beta = 20, 1e-3
+    monkeypatch.setenv("SART_MF_SPARSE_PW", pw)
+    s = MultiFrameSARTSolver(SparseRTM.from_dense(A, device=dev), lap, None,
+                             SolverParams(max_iterations=iters, conv_tolerance=0.0, beta_laplace=beta),
+                             batch=batch, allow_zero_tolerance=True)
+    res = s.solve_batch(G)
+    for f in sorted({0, 17, batch // 2 + 5, batch - 1}):
+        assert res[f].iterations == iters
+        check_fp32_bound(res[f].solution, A, G[f], lap, iterations=iters, beta_laplace=beta, factor=1.1, slack=2e-8)
+
+
 def test_cli_batched_sparse(tmp_path, capfd):
     """--batch_frames on sparse COO files (auto keeps the no-reflection matrix sparse): every frame of the output at
     the fp32 emulation's error of the oracle (cold starts, --no_guess)."""

@@ -110,6 +110,11 @@ for step in "$@"; do
     sparse) run pytest_sparse 900 python -u -m pytest tests/test_gpu_sparse.py tests/test_cli_e2e.py tests/test_native_driver.py \
               -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     sparsebench) run sparse_bench 600 python tools/sparse_bench.py --frames 16,64,128 --out "$OUT/sparse_bench.jsonl" ;;
+    sparsepw)  # SpMM plane width (SART_MF_SPARSE_PW) by batch width, two rounds
+      for i in 1 2; do for pw in 64 32 16; do
+        SART_MF_SPARSE_PW=$pw run sparse_pw_${pw}_$i 300 python tools/sparse_bench.py --no-dense --frames 32,64,128 \
+          --out "$OUT/sparse_pw_${pw}_$i.jsonl"
+      done; done ;;
     sparselanes) for l in 4 8 16 32; do
                    SART_SPARSE_LANES=$l run sparse_lanes_$l 300 python tools/sparse_bench.py --no-dense --out "$OUT/sparse_lanes_$l.jsonl" || exit 1
                  done
