@@ -228,7 +228,9 @@ void MultiFrameEngine::forward() {
 
 void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int64_t v1, bool have_max) {
     if (sparse_) {
-        if (mf_sparse_needs_w_planes(nf_)) {
+        // W_ comes from the weights kernel already in frame-order planes (sweep); the cold-start operands (gpos_,
+        // wo_) are re-laid here
+        if (mf_sparse_needs_w_planes(nf_) && W != W_.get()) {
             if (split_w) launch_mf_w_planes(W, Pp_, nf_, Wt_.get(), stream_, g_mf_skip);
             W = Wt_.get();
         }
@@ -265,7 +267,8 @@ void MultiFrameEngine::sweep(bool last) {
     forward();
     // f16-pair back-projection: the weights kernel also leaves each frame's max |w| (its f16 scale) in wmax_
     launch_mf_weights(Fs_.get(), nsf_, Pp_, ghat_.get(), arow_.get(), cfg_.logarithmic, W_.get(), F2part_.get(),
-                      NF, stream_, h16_ ? wmax_.get() : nullptr);
+                      NF, stream_, h16_ ? wmax_.get() : nullptr,
+                      sparse_ && mf_sparse_needs_w_planes(NF) ? mf_sparse_plane_width(NF) : 0);
     if (last && skip_last_bwd_) {
         // every running frame is decided at max_iter here (its update is skipped on all_done): ||A x||^2 only
         launch_mf_collect(part_.get(), nsb_, ld_, 0, 0, scale, D, F2part_.get(), nwb_, F2, NF, stream_);

@@ -285,7 +285,8 @@ void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, b
 int mf_weights_num_blocks(int64_t nrows_pad);
 // wmax (optional, nf words): also the per-frame max |w| over finite weights (zeroed here first; as k_mf_wmax)
 void launch_mf_weights(const float* Fs, int nsplit, int64_t nrows_pad, const float* ghat, const float* arow,
-                       bool logmode, float* W, double* F2part, int nf, hipStream_t stream, unsigned* wmax = nullptr);
+                       bool logmode, float* W, double* F2part, int nf, hipStream_t stream, unsigned* wmax = nullptr,
+                       int wplane = 0);
 // D[v][f] (voxel-major) for v in [v0, v1); F2out (optional) = per-frame sums of F2part
 void launch_mf_collect(const float* part, int nsplit, int64_t ld, int64_t v0, int64_t v1, const float* scale, float* D,
                        const double* F2part, int nF2, float* F2out, int nf, hipStream_t stream);

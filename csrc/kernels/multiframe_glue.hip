@@ -28,14 +28,15 @@ thread_local const int* g_mf_skip = nullptr;
 __device__ __forceinline__ int mf_bp_slot(int f, int nf) { return (f & 15) * (nf >> 4) + (f >> 4); }
 
 // F = sum_s Fsplit[s] (fixed order); W = a F (log) or a (ghat - F) (linear), written in the
-// back-projection layout (mf_bp_slot); per-block, per-frame partial sums of F^2 in fp64 (deterministic:
-// fixed thread-to-row assignment, fixed tree).
+// back-projection layout (mf_bp_slot), or with wplane > 0 in frame order as planes [nf / wplane][rows][wplane] (the
+// sparse SpMM back-projection, sparse.hip: one 16-byte store per thread); per-block, per-frame partial sums of F^2 in
+// fp64 (deterministic: fixed thread-to-row assignment, fixed tree).
 constexpr int kWRows = 64;  // rows per block (>= 1024 blocks at 64k rows: the kernel is latency-bound)
 __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs, int nsplit, int64_t nrows_pad,
                                                     const float* __restrict__ ghat, const float* __restrict__ arow,
                                                     int logmode, float* __restrict__ W, double* __restrict__ F2part,
                                                     int nf, const int* __restrict__ skip,
-                                                    unsigned* __restrict__ wmax) {
+                                                    unsigned* __restrict__ wmax, int wplane) {
     if (skip && *skip) return;
     __shared__ double red[1024];
     // four consecutive frames of one row per thread (16-byte loads of every split, in split order); q threads per
@@ -61,13 +62,18 @@ __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs
             const float4 g = *reinterpret_cast<const float4*>(ghat + i);
             gv[0] = g.x, gv[1] = g.y, gv[2] = g.z, gv[3] = g.w;
         }
+        float wv[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const float w = logmode ? av[k] * Fv[k] : av[k] * (gv[k] - Fv[k]);
-            W[row * nf + mf_bp_slot(f0 + k, nf)] = w;
+            wv[k] = w;
+            if (wplane == 0) W[row * nf + mf_bp_slot(f0 + k, nf)] = w;
             if (fabsf(w) <= 3.0e38f) wm[k] = max(wm[k], __float_as_uint(fabsf(w)));
             acc[k] += (double)Fv[k] * (double)Fv[k];
         }
+        if (wplane > 0)  // f0 .. f0 + 3 lie in one plane (wplane is a multiple of 4)
+            *reinterpret_cast<float4*>(W + ((int64_t)(f0 / wplane) * nrows_pad + row) * wplane + f0 % wplane) =
+                make_float4(wv[0], wv[1], wv[2], wv[3]);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) red[threadIdx.x * 4 + k] = acc[k];
@@ -481,11 +487,14 @@ static void check_nf(int nf, const char* what) {
 int mf_weights_num_blocks(int64_t nrows_pad) { return (int)((nrows_pad + kWRows - 1) / kWRows); }
 
 void launch_mf_weights(const float* Fs, int nsplit, int64_t nrows_pad, const float* ghat, const float* arow,
-                       bool logmode, float* W, double* F2part, int nf, hipStream_t stream, unsigned* wmax) {
+                       bool logmode, float* W, double* F2part, int nf, hipStream_t stream, unsigned* wmax,
+                       int wplane) {
     check_nf(nf, "mf_weights");
+    if (wplane < 0 || (wplane > 0 && (wplane % 16 != 0 || nf % wplane != 0)))
+        throw std::runtime_error("mf_weights: plane width must divide nf and be a multiple of 16");
     if (wmax) hip_call(hipMemsetAsync(wmax, 0, nf * sizeof(unsigned), stream), "hipMemsetAsync");
     hipLaunchKernelGGL(k_mf_weights, dim3((unsigned)mf_weights_num_blocks(nrows_pad)), dim3(256), 0, stream, Fs,
-                       nsplit, nrows_pad, ghat, arow, logmode ? 1 : 0, W, F2part, nf, g_mf_skip, wmax);
+                       nsplit, nrows_pad, ghat, arow, logmode ? 1 : 0, W, F2part, nf, g_mf_skip, wmax, wplane);
     check_launch("k_mf_weights");
 }
 

@@ -115,6 +115,10 @@ for step in "$@"; do
         SART_MF_SPARSE_PW=$pw run sparse_pw_${pw}_$i 300 python tools/sparse_bench.py --no-dense --frames 32,64,128 \
           --out "$OUT/sparse_pw_${pw}_$i.jsonl"
       done; done ;;
+    profsparsemf) for nf in 16 64; do
+        run rocprof_sparse_mf$nf 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_sparse_mf$nf" -o run --output-format csv \
+          -- python3 tools/sparse_bench.py --no-dense --steps 2 --frames $nf || exit 1
+      done ;;
     sparselanes) for l in 4 8 16 32; do
                    SART_SPARSE_LANES=$l run sparse_lanes_$l 300 python tools/sparse_bench.py --no-dense --out "$OUT/sparse_lanes_$l.jsonl" || exit 1
                  done
