@@ -226,7 +226,8 @@ void MultiFrameEngine::forward() {
     }
 }
 
-void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int64_t v1, bool have_max) {
+void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int64_t v1, bool have_max, float* out,
+                                   const float* oscale) {
     if (sparse_) {
         // W_ comes from the weights kernel already in frame-order planes (sweep); the cold-start operands (gpos_,
         // wo_) are re-laid here
@@ -234,7 +235,8 @@ void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int
             if (split_w) launch_mf_w_planes(W, Pp_, nf_, Wt_.get(), stream_, g_mf_skip);
             W = Wt_.get();
         }
-        launch_mf_sparse_backproject(sp_, V_, W, Pp_, part_.get(), nf_, v0, v1, stream_, g_mf_skip);
+        launch_mf_sparse_backproject(sp_, V_, W, Pp_, out ? out : part_.get(), out ? oscale : nullptr, nf_, v0, v1,
+                                     stream_, g_mf_skip);
         return;
     }
     if (h16_) {
@@ -277,6 +279,18 @@ void MultiFrameEngine::sweep(bool last) {
         ++host_sweep_;
         return;
     }
+    // D[v0, v1) = scale * A^T W and, with the last chunk, the per-frame ||A x||^2: a sparse shard's SpMM writes the
+    // scaled sums itself (the collect then only sums F2part)
+    auto bwd_collect = [&](int64_t v0, int64_t v1, bool first, bool lastc) {
+        if (sparse_) {
+            backproject(W_.get(), first, v0, v1, true, D, scale);
+            if (lastc) launch_mf_collect(part_.get(), nsb_, ld_, 0, 0, scale, D, F2part_.get(), nwb_, F2, NF, stream_);
+            return;
+        }
+        backproject(W_.get(), first, v0, v1, true);
+        launch_mf_collect(part_.get(), nsb_, ld_, v0, v1, scale, D, lastc ? F2part_.get() : nullptr, nwb_,
+                          lastc ? F2 : nullptr, NF, stream_);
+    };
     const int nc = (int)chunks_.size() - 1;
     if (comm_->size() > 1 && nc > 1) {
         // Overlap: the back-projection runs chunk by chunk over the voxel axis on the compute
@@ -286,10 +300,8 @@ void MultiFrameEngine::sweep(bool last) {
         // still overlaps with them.
         for (int c = 0; c < nc; ++c) {
             const int64_t v0 = chunks_[c], v1 = chunks_[c + 1];
-            backproject(W_.get(), c == 0, v0, v1, true);
             const bool last = c == nc - 1;
-            launch_mf_collect(part_.get(), nsb_, ld_, v0, v1, scale, D, last ? F2part_.get() : nullptr, nwb_,
-                              last ? F2 : nullptr, NF, stream_);
+            bwd_collect(v0, v1, c == 0, last);
             hip_ok(hipEventRecord(cev_[c], stream_), "event");
         }
         for (int c = 0; c < nc; ++c) {
@@ -300,8 +312,7 @@ void MultiFrameEngine::sweep(bool last) {
         }
         hip_ok(hipEventRecord(comm_done_, comm_stream_), "event");
     } else {
-        backproject(W_.get(), true, 0, ld_, true);
-        launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, scale, D, F2part_.get(), nwb_, F2, NF, stream_);
+        bwd_collect(0, ld_, true, true);
         if (comm_->size() > 1) comm_->all_reduce(buf_.get(), (size_t)NF * ld_ + NF, ReduceOp::kSum, stream_);
     }
     const float* pen = nullptr;

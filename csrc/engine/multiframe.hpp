@@ -71,7 +71,10 @@ class MultiFrameEngine {
     // part_ = A^T W for voxels [v0, v1) (W in the back-projection layout); the bf16 engine reads the W planes,
     // written from W when split_w
     // have_max: wmax_ already holds the max |w| per frame (the weights kernel of this sweep)
-    void backproject(const float* W, bool split_w, int64_t v0, int64_t v1, bool have_max = false);
+    // sparse shards with `out`: the scaled sums straight into out (oscale[v] * sum, voxel-major [ld][nf]: the
+    // collect's D, so the sweep's collect only sums ||A x||^2)
+    void backproject(const float* W, bool split_w, int64_t v0, int64_t v1, bool have_max = false,
+                     float* out = nullptr, const float* oscale = nullptr);
 
     int device_;
     const void* A_;

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_mf_weights(const float* __restrict__ Fs
 }
 
 // D[v][f] = scale[v] * sum_s part[s][v][f] for v in [v0, v1) (voxel-major, contiguous; fixed summation
-// order); block 0 also writes F2out[f] = (float) sum_b F2part[b][f] when F2part is given.
+// order); block f < nf also writes F2out[f] = (float) sum_b F2part[b][f] when F2part is given.
 __global__ __launch_bounds__(256) void k_mf_collect(const float* __restrict__ part, int nsplit, int64_t ld, int64_t v0,
                                                     int64_t v1, const float* __restrict__ scale, float* __restrict__ D,
                                                     const double* __restrict__ F2part, int nF2, float* __restrict__ F2out,
@@ -122,25 +122,24 @@ __global__ __launch_bounds__(256) void k_mf_collect(const float* __restrict__ pa
         }
         *reinterpret_cast<float4*>(D + i) = acc;
     }
-    if (F2part && blockIdx.x == 0) {  // block-uniform branch: all 256 threads, 256 / nf per frame
+    if (F2part && blockIdx.x < nf) {  // block-uniform branch: block f sums frame f's nF2 partials
+        // (fixed assignment and tree: deterministic). Block 0 for every frame made this kernel 15 us per 64-frame
+        // sweep (32 dependent loads per thread), which a sparse shard's sweep of ~330 us felt.
         __shared__ double f2[256];
-        const int f = threadIdx.x % nf, q = threadIdx.x / nf, nq = 256 / nf;
-        // eight independent partial sums per thread (fixed assignment and combination order: deterministic): one
-        // dependent chain of nF2 / nq loads made this block the kernel's tail (78 us per 64-frame sweep at 64k rows,
-        // profiles/rocprof_r4_mfx64_kernel_stats.csv)
-        double sp[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        int b = q;
-        for (; b + 7 * nq < nF2; b += 8 * nq)
+        const int f = blockIdx.x;
+        double sp[4] = {0.0, 0.0, 0.0, 0.0};
+        int b = threadIdx.x;
+        for (; b + 3 * 256 < nF2; b += 4 * 256)
 #pragma unroll
-            for (int k = 0; k < 8; ++k) sp[k] += F2part[(int64_t)(b + k * nq) * nf + f];
-        for (; b < nF2; b += nq) sp[0] += F2part[(int64_t)b * nf + f];
-        f2[threadIdx.x] = ((sp[0] + sp[1]) + (sp[2] + sp[3])) + ((sp[4] + sp[5]) + (sp[6] + sp[7]));
+            for (int k = 0; k < 4; ++k) sp[k] += F2part[(int64_t)(b + k * 256) * nf + f];
+        for (; b < nF2; b += 256) sp[0] += F2part[(int64_t)b * nf + f];
+        f2[threadIdx.x] = (sp[0] + sp[1]) + (sp[2] + sp[3]);
         __syncthreads();
-        if (threadIdx.x < nf) {  // fixed order over the 256 / nf partial sums: deterministic
-            double t = 0.0;
-            for (int k = 0; k < nq; ++k) t += f2[k * nf + threadIdx.x];
-            F2out[threadIdx.x] = (float)t;
+        for (int w = 128; w > 0; w >>= 1) {
+            if (threadIdx.x < w) f2[threadIdx.x] += f2[threadIdx.x + w];
+            __syncthreads();
         }
+        if (threadIdx.x == 0) F2out[f] = (float)f2[0];
     }
 }
 
@@ -503,7 +502,8 @@ void launch_mf_collect(const float* part, int nsplit, int64_t ld, int64_t v0, in
     check_nf(nf, "mf_collect");
     if (v0 < 0 || v1 > ld || v1 < v0) throw std::runtime_error("mf_collect: voxel range outside [0, ld)");
     const int64_t n = (v1 - v0) * nf;  // a multiple of 4 (nf is 16 .. 128): 4 elements per thread
-    hipLaunchKernelGGL(k_mf_collect, dim3(std::max<unsigned>(1, nb(n / 4))), dim3(256), 0, stream, part, nsplit, ld, v0, v1,
+    const unsigned blocks = std::max<unsigned>(F2part ? (unsigned)nf : 1u, nb(n / 4));  // F2: one block per frame
+    hipLaunchKernelGGL(k_mf_collect, dim3(blocks), dim3(256), 0, stream, part, nsplit, ld, v0, v1,
                        scale, D, F2part, nF2, F2out, nf, g_mf_skip);
     check_launch("k_mf_collect");
 }

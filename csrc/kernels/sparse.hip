@@ -175,12 +175,14 @@ __global__ __launch_bounds__(256) void k_mf_w_planes(const float* __restrict__ W
 }
 
 // PW frames per plane (16, 32, 64); SLOT: W in the slot layout of a PW-frame batch (a one-plane back-projection);
-// plane blockIdx.y: Y + blockIdx.y * yplane, outputs at frame offset PW blockIdx.y of rows of nfs frames
+// plane blockIdx.y: Y + blockIdx.y * yplane, outputs at frame offset PW blockIdx.y of rows of nfs frames, times
+// oscale[i] when given (the back-projection's voxel scales: the sums go straight into the engine's corrections)
 template <int PW, bool SLOT>
 __global__ __launch_bounds__(256) void k_mf_sparse_spmm(const int64_t* __restrict__ ptr, const int32_t* __restrict__ idx,
                                                         const float* __restrict__ val, int64_t n_valid, int64_t i0,
                                                         int64_t i1, const float* __restrict__ Y, int64_t yplane,
-                                                        float* __restrict__ out, int nfs, const int* __restrict__ skip) {
+                                                        float* __restrict__ out, const float* __restrict__ oscale,
+                                                        int nfs, const int* __restrict__ skip) {
     if (skip && *skip) return;
     constexpr int G = 64 / PW;  // entries in flight per wave
     // eight fp32 chains per row and frame (G groups x CH chains per lane, entries dealt round robin): one chain over
@@ -214,17 +216,19 @@ __global__ __launch_bounds__(256) void k_mf_sparse_spmm(const int64_t* __restric
     float tot = acc[0];
 #pragma unroll
     for (int o = PW; o < 64; o <<= 1) tot += __shfl_xor(tot, o);
+    if (oscale) tot *= oscale[i];
     if (grp == 0) out[i * nfs + PW * blockIdx.y + fl] = tot;  // zero for padded rows / columns
 }
 
 template <bool SLOT>
 static void spmm(int pw, int nf, dim3 grid, hipStream_t stream, const int64_t* ptr, const int32_t* idx,
                  const float* val, int64_t n_valid, int64_t i0, int64_t i1, const float* Y, int64_t yplane, float* out,
-                 const int* skip, const char* what) {
+                 const float* oscale, const int* skip, const char* what) {
     if ((nf != 16 && nf != 32 && nf != 64 && nf != 128) || nf % pw != 0)
         throw std::runtime_error(std::string(what) + ": nf must be 16, 32, 64 or 128");
     auto go = [&](auto k) {
-        hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, ptr, idx, val, n_valid, i0, i1, Y, yplane, out, nf, skip);
+        hipLaunchKernelGGL(k, grid, dim3(256), 0, stream, ptr, idx, val, n_valid, i0, i1, Y, yplane, out, oscale, nf,
+                           skip);
     };
     switch (pw) {
         case 16: go(k_mf_sparse_spmm<16, SLOT>); break;
@@ -244,7 +248,7 @@ void launch_mf_sparse_forward(const SparseRtm& s, int64_t nrows, int64_t nrows_p
                        X, ld, nf, pw, Xt, skip);
     check_launch("k_mf_transpose_x");
     const dim3 grid((unsigned)((nrows_pad + 3) / 4), (unsigned)(nf / pw));
-    spmm<false>(pw, nf, grid, stream, s.row_ptr, s.col, s.val, nrows, 0, nrows_pad, Xt, ld * pw, Fout, skip,
+    spmm<false>(pw, nf, grid, stream, s.row_ptr, s.col, s.val, nrows, 0, nrows_pad, Xt, ld * pw, Fout, nullptr, skip,
                 "k_mf_sparse_spmm (forward)");
 }
 
@@ -256,17 +260,18 @@ void launch_mf_w_planes(const float* W, int64_t rows, int nf, float* Wt, hipStre
 }
 
 void launch_mf_sparse_backproject(const SparseRtm& s, int64_t nvoxel, const float* W, int64_t wrows, float* part,
-                                  int nf, int64_t v0, int64_t v1, hipStream_t stream, const int* skip) {
+                                  const float* scale, int nf, int64_t v0, int64_t v1, hipStream_t stream,
+                                  const int* skip) {
     check_sparse(s, "mf_sparse_backproject");
     if (v1 <= v0) return;
     const int pw = mf_sparse_plane_width(nf);
     const dim3 grid((unsigned)((v1 - v0 + 3) / 4), (unsigned)(nf / pw));
     // W in its slot layout or the frame-order planes of launch_mf_w_planes (mf_sparse_needs_w_planes)
     if (!mf_sparse_needs_w_planes(nf))
-        spmm<true>(pw, nf, grid, stream, s.col_ptr, s.row, s.cval, nvoxel, v0, v1, W, 0, part, skip,
+        spmm<true>(pw, nf, grid, stream, s.col_ptr, s.row, s.cval, nvoxel, v0, v1, W, 0, part, scale, skip,
                    "k_mf_sparse_spmm (back-projection)");
     else
-        spmm<false>(pw, nf, grid, stream, s.col_ptr, s.row, s.cval, nvoxel, v0, v1, W, wrows * pw, part, skip,
+        spmm<false>(pw, nf, grid, stream, s.col_ptr, s.row, s.cval, nvoxel, v0, v1, W, wrows * pw, part, scale, skip,
                     "k_mf_sparse_spmm (back-projection)");
 }
 
