@@ -109,7 +109,7 @@ for step in "$@"; do
             run rocprof_2tb64 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_2tb64" -o run --output-format csv -- python3 bench.py --config 2tb --steps 1 --warmup 0 --frames 64 --no-selfcheck ;;
     sparse) run pytest_sparse 900 python -u -m pytest tests/test_gpu_sparse.py tests/test_cli_e2e.py tests/test_native_driver.py \
               -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    sparsebench) run sparse_bench 600 python tools/sparse_bench.py --frames 16,64,128 --out "$OUT/sparse_bench.jsonl" ;;
+    sparsebench) run sparse_bench 600 python tools/sparse_bench.py --frames 16,32,64,128 --out "$OUT/sparse_bench.jsonl" ;;
     sparsepw)  # SpMM plane width (SART_MF_SPARSE_PW) by batch width, two rounds
       for i in 1 2; do for pw in 64 32 16; do
         SART_MF_SPARSE_PW=$pw run sparse_pw_${pw}_$i 300 python tools/sparse_bench.py --no-dense --frames 32,64,128 \
