@@ -125,7 +125,7 @@ for step in "$@"; do
                  run sparse_lanes_auto 300 python tools/sparse_bench.py --no-dense --out "$OUT/sparse_lanes_auto.jsonl" &&
                  run rocprof_sparse 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_sparse" -o run --output-format csv -- python3 tools/sparse_bench.py --no-dense --steps 2 ;;
     seriessparse) run series_sparse 900 python tools/series_native.py --sparse-direct --runs ${SERIES_RUNS:-seq} --out "$OUT/series_sparse.jsonl" ;;
-    seriesdense) run series_dense 900 python tools/series_native.py --runs seq --out "$OUT/series_dense.jsonl" ;;
+    seriesdense) run series_dense 900 python tools/series_native.py --runs ${SERIES_RUNS:-seq} --out "$OUT/series_dense.jsonl" ;;
     sparsedens) for d in 0.01 0.03 0.05 0.1 0.2; do
                   run sparse_dens_$d 600 python tools/sparse_bench.py --random-density $d --shape 128,128 --grid 32,32,32 \
                     --out "$OUT/sparse_density.jsonl" || exit 1
