@@ -84,7 +84,8 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     if (sparse_) {  // the SpMM kernels write complete sums
         nsf_ = nsb_ = 1;
         Xt_.resize((size_t)ld_ * NF);
-        Wt_.resize((size_t)Pp_ * NF);  // W as frame-order planes (batches wider than mf_sparse_plane_width)
+        pw_ = mf_sparse_plane_width(NF);
+        if (mf_sparse_needs_w_planes(NF, pw_)) Wt_.resize((size_t)Pp_ * NF);  // cold-start / log operands re-laid
     }
     nwb_ = mf_weights_num_blocks(Pp_);
     X_.resize((size_t)NF * ld_);
@@ -202,7 +203,7 @@ std::string MultiFrameEngine::backproject_split() const {
 
 void MultiFrameEngine::forward() {
     if (sparse_) {
-        launch_mf_sparse_forward(sp_, P_, Pp_, X_.get(), ld_, Xt_.get(), Fs_.get(), nf_, stream_, g_mf_skip);
+        launch_mf_sparse_forward(sp_, P_, Pp_, X_.get(), ld_, Xt_.get(), Fs_.get(), nf_, pw_, stream_, g_mf_skip);
         return;
     }
     if (fwd16_) {
@@ -231,12 +232,12 @@ void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int
     if (sparse_) {
         // W_ comes from the weights kernel already in frame-order planes (sweep); the cold-start operands (gpos_,
         // wo_) are re-laid here
-        if (mf_sparse_needs_w_planes(nf_) && W != W_.get()) {
-            if (split_w) launch_mf_w_planes(W, Pp_, nf_, Wt_.get(), stream_, g_mf_skip);
+        if (mf_sparse_needs_w_planes(nf_, pw_) && W != W_.get()) {
+            if (split_w) launch_mf_w_planes(W, Pp_, nf_, pw_, Wt_.get(), stream_, g_mf_skip);
             W = Wt_.get();
         }
-        launch_mf_sparse_backproject(sp_, V_, W, Pp_, out ? out : part_.get(), out ? oscale : nullptr, nf_, v0, v1,
-                                     stream_, g_mf_skip);
+        launch_mf_sparse_backproject(sp_, V_, W, Pp_, out ? out : part_.get(), out ? oscale : nullptr, nf_, pw_, v0,
+                                     v1, stream_, g_mf_skip);
         return;
     }
     if (h16_) {
@@ -270,7 +271,7 @@ void MultiFrameEngine::sweep(bool last) {
     // f16-pair back-projection: the weights kernel also leaves each frame's max |w| (its f16 scale) in wmax_
     launch_mf_weights(Fs_.get(), nsf_, Pp_, ghat_.get(), arow_.get(), cfg_.logarithmic, W_.get(), F2part_.get(),
                       NF, stream_, h16_ ? wmax_.get() : nullptr,
-                      sparse_ && mf_sparse_needs_w_planes(NF) ? mf_sparse_plane_width(NF) : 0);
+                      sparse_ && mf_sparse_needs_w_planes(NF, pw_) ? pw_ : 0);
     if (last && skip_last_bwd_) {
         // every running frame is decided at max_iter here (its update is skipped on all_done): ||A x||^2 only
         launch_mf_collect(part_.get(), nsb_, ld_, 0, 0, scale, D, F2part_.get(), nwb_, F2, NF, stream_);

@@ -82,6 +82,7 @@ class MultiFrameEngine {
     SparseRtm sp_{};
     DeviceArray<float> Xt_;  // sparse: X voxel-major planes [nf / PW][ld][PW] for the row gathers
     DeviceArray<float> Wt_;  // sparse: W as frame-order planes [nf / PW][rows][PW] (launch_mf_w_planes)
+    int pw_ = 64;            // sparse: frames per SpMM plane (mf_sparse_plane_width, fixed at construction)
     bool bf16_ = false;
     bool x3_ = false;     // fp32 shard on the bf16 matrix cores (EngineConfig::mf_split_a)
     bool split_ = false;  // X / W enter as hi + lo bf16 planes (bf16_ || x3_)

@@ -55,18 +55,21 @@ void launch_csr_forward(int epi, const SparseRtm& s, int64_t nrows, int64_t nrow
 void launch_csc_backproject(const SparseRtm& s, int64_t nvoxel, const float* w, float* out, const SartState* st,
                             hipStream_t stream);
 // multi-frame engine, sparse shard: F [nrows_pad][nf] = A X^T (X frame-major [nf][ld], copied voxel-major into Xt
-// [nf / PW][ld][PW] first, PW = mf_sparse_plane_width(nf); padded rows written 0) and part [v][nf] = sum_p A[p][v]
+// [nf / PW][ld][PW] first, PW = pw (mf_sparse_plane_width); padded rows written 0) and part [v][nf] = sum_p A[p][v]
 // W[p][f] for v in [v0, v1) (columns >= nvoxel written 0; times scale[v] when given). W: the back-projection
-// layout of launch_mf_weights ([wrows][nf], mf_bp_slot), or with mf_sparse_needs_w_planes(nf) the frame-order
+// layout of launch_mf_weights ([wrows][nf], mf_bp_slot), or with mf_sparse_needs_w_planes(nf, pw) the frame-order
 // planes [nf / PW][wrows][PW] (launch_mf_w_planes, or launch_mf_weights with wplane = PW).
+// frames per SpMM plane for an nf-frame batch (64, or nf below; SART_MF_SPARSE_PW = 16 / 32 / 64 overrides): read
+// once by the engine, which lays X and W out for it
 int mf_sparse_plane_width(int nf);
-bool mf_sparse_needs_w_planes(int nf);
+bool mf_sparse_needs_w_planes(int nf, int pw);
 void launch_mf_sparse_forward(const SparseRtm& s, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ld,
-                              float* Xt, float* Fout, int nf, hipStream_t stream, const int* skip);
+                              float* Xt, float* Fout, int nf, int pw, hipStream_t stream, const int* skip);
 void launch_mf_sparse_backproject(const SparseRtm& s, int64_t nvoxel, const float* W, int64_t wrows, float* part,
-                                  const float* scale, int nf, int64_t v0, int64_t v1, hipStream_t stream,
+                                  const float* scale, int nf, int pw, int64_t v0, int64_t v1, hipStream_t stream,
                                   const int* skip);
-void launch_mf_w_planes(const float* W, int64_t rows, int nf, float* Wt, hipStream_t stream, const int* skip);
+void launch_mf_w_planes(const float* W, int64_t rows, int nf, int pw, float* Wt, hipStream_t stream,
+                        const int* skip);
 void launch_csr_rowsum_f64(const SparseRtm& s, int64_t nrows, double* out, hipStream_t stream);
 void launch_csc_colsum_f64(const SparseRtm& s, int64_t nvoxel, double* out, hipStream_t stream);
 // fp32 -> bf16, round to nearest even (n a multiple of 4)

@@ -137,9 +137,11 @@ int mf_sparse_plane_width(int nf) {
 // wave (one pass of the address path) still touch a single 128-B line. At 64 frames the slot order spreads them over
 // the whole 256-B row, twice the lines per gather (113.5k against 183.5k frame-it/s per 64-frame plane,
 // profiles/sparse_r5_plane_width.txt), so W is re-laid in frame order first (launch_mf_w_planes).
-bool mf_sparse_needs_w_planes(int nf) {
-    const int pw = mf_sparse_plane_width(nf);
-    return pw < nf || pw > 32;
+bool mf_sparse_needs_w_planes(int nf, int pw) { return pw < nf || pw > 32; }
+
+static void check_pw(int nf, int pw, const char* what) {
+    if ((pw != 16 && pw != 32 && pw != 64) || pw > nf || nf % pw != 0)
+        throw std::runtime_error(std::string(what) + ": plane width must be 16, 32 or 64 and divide nf");
 }
 
 // W's back-projection layout [rows][16][nf / 16] (multiframe_glue.hip::mf_bp_slot)
@@ -240,10 +242,10 @@ static void spmm(int pw, int nf, dim3 grid, hipStream_t stream, const int64_t* p
 }
 
 void launch_mf_sparse_forward(const SparseRtm& s, int64_t nrows, int64_t nrows_pad, const float* X, int64_t ld,
-                              float* Xt, float* Fout, int nf, hipStream_t stream, const int* skip) {
+                              float* Xt, float* Fout, int nf, int pw, hipStream_t stream, const int* skip) {
     check_sparse(s, "mf_sparse_forward");
+    check_pw(nf, pw, "mf_sparse_forward");
     if (ld % 64 != 0) throw std::runtime_error("mf_sparse_forward: ld must be a multiple of 64");
-    const int pw = mf_sparse_plane_width(nf);
     hipLaunchKernelGGL(k_mf_transpose_x, dim3((unsigned)(ld / 64), (unsigned)((nf + 63) / 64)), dim3(256), 0, stream,
                        X, ld, nf, pw, Xt, skip);
     check_launch("k_mf_transpose_x");
@@ -252,22 +254,23 @@ void launch_mf_sparse_forward(const SparseRtm& s, int64_t nrows, int64_t nrows_p
                 "k_mf_sparse_spmm (forward)");
 }
 
-void launch_mf_w_planes(const float* W, int64_t rows, int nf, float* Wt, hipStream_t stream, const int* skip) {
-    const int pw = mf_sparse_plane_width(nf);
+void launch_mf_w_planes(const float* W, int64_t rows, int nf, int pw, float* Wt, hipStream_t stream,
+                        const int* skip) {
+    check_pw(nf, pw, "mf_w_planes");
     hipLaunchKernelGGL(k_mf_w_planes, dim3((unsigned)((rows * nf + 255) / 256)), dim3(256), 0, stream, W, rows, nf,
                        pw, Wt, skip);
     check_launch("k_mf_w_planes");
 }
 
 void launch_mf_sparse_backproject(const SparseRtm& s, int64_t nvoxel, const float* W, int64_t wrows, float* part,
-                                  const float* scale, int nf, int64_t v0, int64_t v1, hipStream_t stream,
+                                  const float* scale, int nf, int pw, int64_t v0, int64_t v1, hipStream_t stream,
                                   const int* skip) {
     check_sparse(s, "mf_sparse_backproject");
+    check_pw(nf, pw, "mf_sparse_backproject");
     if (v1 <= v0) return;
-    const int pw = mf_sparse_plane_width(nf);
     const dim3 grid((unsigned)((v1 - v0 + 3) / 4), (unsigned)(nf / pw));
     // W in its slot layout or the frame-order planes of launch_mf_w_planes (mf_sparse_needs_w_planes)
-    if (!mf_sparse_needs_w_planes(nf))
+    if (!mf_sparse_needs_w_planes(nf, pw))
         spmm<true>(pw, nf, grid, stream, s.col_ptr, s.row, s.cval, nvoxel, v0, v1, W, 0, part, scale, skip,
                    "k_mf_sparse_spmm (back-projection)");
     else
