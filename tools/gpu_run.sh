@@ -689,6 +689,13 @@ for step in "$@"; do
     r4cli) run pytest_cli 900 python -u -m pytest tests/test_native_driver.py tests/test_cli_e2e.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     r4bench) run bench_r4 300 python bench.py --steps 20 --warmup 5 ;;
     r4dist) run pytest_dist 1100 python -u -m pytest tests/test_gpu_distributed.py -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    r5share)  # the round driver's launch (torchrun, one process per rank) rehearsed on ONE GPU: 2 and 8 ranks share it
+      for n in 2 8; do
+        run bench_share${n}_torchrun_r5 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
+          --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n --share-gpus --steps 3 --warmup 1 \
+          --watchdog 300 || exit 1
+        grep -h '^{' "$OUT/bench_share${n}_torchrun_r5.log" > "$OUT/bench_share${n}_torchrun_r5.json" || true
+      done ;;
     pmcfinal)  # HBM bytes (FETCH_SIZE) and occupancy counters of the headline fused sweep, the sparse kernels and the
                # 64-frame split-A kernels, each pass its own run with the kernel trace (durations) beside the counters
       PMC_OCC="SQ_WAVES SQ_LEVEL_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_MFMA GRBM_GUI_ACTIVE"
