@@ -44,9 +44,10 @@ def summarize(d):
             for row in csv.DictReader(fh):
                 k = short(row.get("Kernel_Name", "?"))
                 try:
-                    ctr[k][row["Counter_Name"]] += float(row["Counter_Value"])
-                except (KeyError, ValueError):
+                    v = float(row["Counter_Value"])
+                except (KeyError, TypeError, ValueError):  # a counter the pass could not read
                     continue
+                ctr[k][row["Counter_Name"]] += v
     out = []
     for k in sorted(set(durs) | set(ctr), key=lambda k: -durs.get(k, 0.0)):
         c = ctr.get(k, {})
