@@ -46,6 +46,7 @@ static py::dict solve_info(const sart::SolveInfo& i) {
     d["sweeps"] = i.sweeps;
     d["comm_ms"] = i.comm_ms;
     d["warm_from"] = i.warm_from;
+    d["warm_iter"] = i.warm_iter;
     return d;
 }
 
@@ -310,7 +311,7 @@ static void bind_engine(py::module_& m) {
                 py::array_t<float, py::array::c_style | py::array::forcecast> val) {
                  e.set_laplacian(rp.data(), col.data(), val.data(), (int64_t)val.size());
              })
-        .def("solve_batch", [](sart::MultiFrameEngine& e, f64arr g, py::object x0, bool chain) {
+        .def("solve_batch", [](sart::MultiFrameEngine& e, f64arr g, py::object x0, bool chain, bool record_starts) -> py::tuple {
             if (g.ndim() != 2 || g.shape(1) != e.nrows())
                 throw py::value_error("measurements must be [nframes, nrows of the local shard]");
             const int nf = (int)g.shape(0);
@@ -322,17 +323,41 @@ static void bind_engine(py::module_& m) {
                 x0p = x0a.data();
             }
             py::array_t<double> x({(py::ssize_t)nf, (py::ssize_t)e.nvoxel()});
+            py::array_t<double> st({(py::ssize_t)(record_starts ? nf : 0), (py::ssize_t)e.nvoxel()});
             double* xp = x.mutable_data();
+            double* sp = record_starts ? st.mutable_data() : nullptr;
             const double* gp = g.data();
             std::vector<sart::SolveInfo> infos;
             {
                 py::gil_scoped_release rel;
-                infos = e.solve_batch(gp, nf, xp, x0p, chain);
+                infos = e.solve_batch(gp, nf, xp, x0p, chain, sp);
             }
             py::list li;
             for (const auto& i : infos) li.append(solve_info(i));
+            if (record_starts) return py::make_tuple(x, li, st);
             return py::make_tuple(x, li);
-        }, py::arg("g"), py::arg("x0") = py::none(), py::arg("chain") = false);
+        }, py::arg("g"), py::arg("x0") = py::none(), py::arg("chain") = false, py::arg("record_starts") = false)
+        .def_property_readonly("series_stats", [](sart::MultiFrameEngine& e) {
+            const auto& s = e.series_stats();
+            py::dict d;
+            d["frames"] = s.frames;
+            d["sweeps"] = s.sweeps;
+            d["queued_sweeps"] = s.queued_sweeps;
+            d["busy_slot_sweeps"] = s.busy_slot_sweeps;
+            d["chained"] = s.chained;
+            d["slot_util"] = s.slot_util;
+            d["mean_iterations"] = s.mean_iterations;
+            d["mean_warm_age"] = s.mean_warm_age;
+            d["ms"] = s.ms;
+            d["chunk"] = s.chunk;
+            d["admit_cap"] = s.admit_cap;
+            d["src_age"] = s.src_age;
+            d["restarts"] = s.restarts;
+            d["src_finished"] = s.src_finished;
+            d["lead"] = s.lead;
+            d["src_extrap"] = s.src_extrap;
+            return d;
+        });
 }
 
 PYBIND11_MODULE(_sart_hip, m) {

@@ -28,7 +28,10 @@
 #include <future>
 #include <iostream>
 #include <limits>
+#include <map>
 #include <memory>
+#include <mutex>
+#include <condition_variable>
 #include <stdexcept>
 #include <string>
 #include <sys/prctl.h>
@@ -429,6 +432,32 @@ int main(int argc, char** argv) {
                       << (sparse ? ", sparse: " + std::to_string(sshard->nnz) + " non-zeros" : std::string()) << ")"
                       << std::endl;
 
+        // the single-frame engine (frame by frame; with --batch_frames it solves a cold time series' first frame)
+        auto make_engine = [&]() {
+            std::unique_ptr<Engine> e;
+            EngineConfig ec;
+            static_cast<SolverParams&>(ec) = params;
+            ec.use_fused = !cfg.two_pass;
+            ec.fused_min_bytes = fused_min_bytes_from_env();
+            if (const char* v = std::getenv("SART_FUSED_VARIANT"); v && *v) ec.fused_variant = std::atoi(v);
+            ec.time_collectives = !cfg.profile_file.empty();  // --profile: GPU time in the all-reduces per frame
+            if (cols) {
+                ec.column_shard = true;
+                ec.col_offset = (int64_t)vblk.offset;
+                ec.nvoxel_total = (int64_t)in.nvoxel;
+            }
+            if (sparse) {
+                const SparseRtm view = sshard->view();
+                e = std::make_unique<Engine>(device, nullptr, sshard->nrows, (sshard->nrows + 63) / 64 * 64,
+                                             sshard->nvoxel, (sshard->nvoxel + 63) / 64 * 64, dcomm.get(), ec, &view);
+            } else {
+                ec.rtm_bf16 = dshard->bf16;
+                e = std::make_unique<Engine>(device, dshard->A, dshard->nrows, dshard->nrows_pad, dshard->nvoxel,
+                                             dshard->ld, dcomm.get(), ec);
+            }
+            if (lap.nnz()) e->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
+            return e;
+        };
         std::unique_ptr<Engine> engine;
         std::unique_ptr<MultiFrameEngine> mf;
         std::unique_ptr<CpuSolver> cpu;
@@ -449,28 +478,7 @@ int main(int argc, char** argv) {
             }
             if (lap.nnz()) mf->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
         } else if (gpu) {
-            EngineConfig ec;
-            static_cast<SolverParams&>(ec) = params;
-            ec.use_fused = !cfg.two_pass;
-            ec.fused_min_bytes = fused_min_bytes_from_env();
-            if (const char* v = std::getenv("SART_FUSED_VARIANT"); v && *v) ec.fused_variant = std::atoi(v);
-            ec.time_collectives = !cfg.profile_file.empty();  // --profile: GPU time in the all-reduces per frame
-            if (cols) {
-                ec.column_shard = true;
-                ec.col_offset = (int64_t)vblk.offset;
-                ec.nvoxel_total = (int64_t)in.nvoxel;
-            }
-            if (sparse) {
-                const SparseRtm view = sshard->view();
-                engine = std::make_unique<Engine>(device, nullptr, sshard->nrows, (sshard->nrows + 63) / 64 * 64,
-                                                  sshard->nvoxel, (sshard->nvoxel + 63) / 64 * 64, dcomm.get(), ec,
-                                                  &view);
-            } else {
-                ec.rtm_bf16 = dshard->bf16;
-                engine = std::make_unique<Engine>(device, dshard->A, dshard->nrows, dshard->nrows_pad,
-                                                  dshard->nvoxel, dshard->ld, dcomm.get(), ec);
-            }
-            if (lap.nnz()) engine->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
+            engine = make_engine();
         } else {
             if (sparse)
                 cpu = std::make_unique<CpuSolver>(std::move(hcsr), host, params, false);
@@ -549,57 +557,164 @@ int main(int argc, char** argv) {
         const size_t nframes_total = frames.size();
         const auto t_loop = std::chrono::steady_clock::now();
         if (batched) {
-            // --batch_frames N: N slots on the matrix cores with continuous batching (a finished frame's slot takes
-            // the next frame between two sweeps). Frames are read in windows (N, then 4 N: only the first window's
-            // read is not hidden behind a solve; a first window of 4 N kept 240 frames of reads, ~0.5 ms each, ahead
-            // of the first sweep); without --no_guess they form a warm-started time series (the window's first N
-            // frames start from the previous window's last solution or the resumed one, later frames from the
-            // latest finished frame); with --no_guess every frame cold-starts.
-            const size_t nb = (size_t)cfg.batch_frames * 4;
-            auto window = [&](size_t c0) { return std::min(frames.size() - c0, c0 == 0 ? (size_t)cfg.batch_frames : nb); };
+            // --batch_frames N: N slots on the matrix cores, refilled on the device (MultiFrameEngine::solve_series):
+            // the sweep in which a frame finishes admits the next staged frame into its slot. The whole series is one
+            // stream: a reader thread keeps up to 4 N frames read ahead, the engine stages them into its device queue
+            // while earlier frames sweep, and finished frames (out of order) are written in time order. Without
+            // --no_guess the frames form a warm-started time series -- each starts from the current iterate of the
+            // newest frame in flight, rescaled (the resumed solution starts the first ones); with --no_guess every
+            // frame cold-starts.
+            const int64_t nfr = (int64_t)frames.size();
+            const int64_t ahead = 4 * (int64_t)cfg.batch_frames;
             std::vector<double> bwarm = cfg.no_guess ? std::vector<double>() : warm;
-            auto read_chunk = [&image, &frames](size_t c0, size_t n) {
-                std::vector<double> g;
-                for (size_t k = c0; k < c0 + n; ++k) {
-                    const std::vector<double> f = image.frame(frames[k]);
-                    g.insert(g.end(), f.begin(), f.end());
-                }
-                return g;
-            };
-            std::future<std::vector<double>> next;
-            if (!frames.empty()) next = std::async(std::launch::async, read_chunk, (size_t)0, window(0));
-            for (size_t c0 = 0; c0 < frames.size();) {
-                std::vector<double> g = next.get();
-                const int B = (int)window(c0);
-                if (c0 + B < frames.size())
-                    next = std::async(std::launch::async, read_chunk, c0 + B, window(c0 + B));
-                std::vector<double> xb((size_t)B * in.nvoxel);
+            // A cold time series: its first frame is solved alone by the single-frame engine (the fused sweep, half
+            // the time of a batched sweep) and starts the chain as a converged source -- frames chained from a cold
+            // start's young iterates would carry its error for ~100 frames (profiles/series_r6_*). SART_MF_LEAD_ENGINE=0:
+            // the multi-frame engine's own lead frame instead (MfQueue::lead).
+            int64_t off = 0;
+            int lead_iters = -1;
+            const char* le = std::getenv("SART_MF_LEAD_ENGINE");
+            if (!cfg.no_guess && bwarm.empty() && nfr > 0 && !(le && *le && std::atoi(le) == 0)) {
                 const auto t0 = std::chrono::steady_clock::now();
-                const int64_t first_warm = (c0 > 0 && !bwarm.empty()) ? (int64_t)frames[c0 - 1] : -1;
-                const std::vector<SolveInfo> infos =
-                    mf->solve_batch(g.data(), B, xb.data(), bwarm.empty() ? nullptr : bwarm.data(), !cfg.no_guess);
-                if (!cfg.no_guess) {
-                    bwarm.assign(xb.end() - (std::ptrdiff_t)in.nvoxel, xb.end());
-                    if (!std::all_of(bwarm.begin(), bwarm.end(), [](double v) { return std::isfinite(v); }))
-                        bwarm.clear();
+                std::vector<double> g0 = image.frame(frames[0]), x0s(in.nvoxel);
+                SolveInfo info;
+                {
+                    std::unique_ptr<Engine> lead = make_engine();
+                    info = lead->solve(g0.data(), nullptr, x0s.data());
                 }
                 const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 if (rank == 0) {
-                    for (int f = 0; f < B; ++f) {
-                        const uint64_t cur = frames[c0 + f];
-                        std::vector<double> xf(xb.begin() + (size_t)f * in.nvoxel, xb.begin() + (size_t)(f + 1) * in.nvoxel);
-                        writer->add(xf, infos[f].status, image.frame_time(cur), image.camera_frame_time(cur),
-                                    infos[f].iterations);
-                        std::cout << "Processed in: " << ms / B << " ms" << std::endl;
-                        if (profile.is_open())
-                            profile << "{\"frame\": " << cur << ", \"time\": " << image.frame_time(cur)
-                                    << ", \"status\": " << infos[f].status << ", \"iterations\": " << infos[f].iterations
-                                    << ", \"ms\": " << ms / B << ", \"batch\": " << cfg.batch_frames << ", \"warm_from\": "
-                                    << (infos[f].warm_from >= 0 ? (int64_t)frames[c0 + infos[f].warm_from] : first_warm)
-                                    << ", \"driver\": \"native\"}\n";
-                    }
+                    writer->add(x0s, info.status, image.frame_time(frames[0]), image.camera_frame_time(frames[0]),
+                                info.iterations);
+                    std::cout << "Processed in: " << ms << " ms" << std::endl;
+                    if (profile.is_open())
+                        profile << "{\"frame\": " << frames[0] << ", \"time\": " << image.frame_time(frames[0])
+                                << ", \"status\": " << info.status << ", \"iterations\": " << info.iterations
+                                << ", \"convergence\": " << info.convergence << ", \"ms\": " << ms
+                                << ", \"batch\": " << cfg.batch_frames << ", \"warm_from\": -1, \"warm_iter\": -1"
+                                << ", \"lead\": true, \"fused\": " << (info.used_fused ? "true" : "false")
+                                << ", \"driver\": \"native\"}\n";
                 }
-                c0 += B;
+                if (std::all_of(x0s.begin(), x0s.end(), [](double v) { return std::isfinite(v); })) bwarm = x0s;
+                off = 1;
+                lead_iters = info.iterations;
+            }
+            std::mutex mu, io_mu;
+            std::condition_variable cv;
+            std::map<int64_t, std::vector<double>> ready;  // frames read ahead, by series index
+            int64_t consumed = off, reader_next = off;
+            bool stop = false;
+            std::exception_ptr read_err;
+            std::thread reader([&] {
+                try {
+                    for (int64_t k = off; k < nfr; ++k) {
+                        {
+                            std::unique_lock<std::mutex> lk(mu);
+                            cv.wait(lk, [&] { return stop || k < consumed + ahead; });
+                            if (stop) return;
+                        }
+                        std::vector<double> f;
+                        {
+                            std::lock_guard<std::mutex> io(io_mu);
+                            f = image.frame(frames[k]);
+                        }
+                        std::lock_guard<std::mutex> lk(mu);
+                        ready.emplace(k, std::move(f));
+                        reader_next = k + 1;
+                        cv.notify_all();
+                    }
+                } catch (...) {
+                    std::lock_guard<std::mutex> lk(mu);
+                    read_err = std::current_exception();
+                    stop = true;
+                    cv.notify_all();
+                }
+            });
+            struct ReaderJoin {
+                std::thread& t;
+                std::mutex& m;
+                std::condition_variable& c;
+                bool& stop;
+                ~ReaderJoin() {
+                    {
+                        std::lock_guard<std::mutex> lk(m);
+                        stop = true;
+                    }
+                    c.notify_all();
+                    if (t.joinable()) t.join();
+                }
+            } join_reader{reader, mu, cv, stop};
+            const size_t npix = (size_t)mf->nrows();
+            auto src = [&](int64_t j, double* dst) {  // series index j = frame off + j
+                const int64_t k = j + off;
+                std::vector<double> f;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return read_err || ready.count(k) || k < reader_next; });
+                    if (read_err) std::rethrow_exception(read_err);
+                    auto it = ready.find(k);
+                    if (it != ready.end()) {
+                        f = std::move(it->second);
+                        ready.erase(it);
+                    }
+                    consumed = std::max(consumed, k + 1);
+                    cv.notify_all();
+                }
+                if (f.empty()) {  // asked again (a re-solve after a device all-reduce failure): read it here
+                    std::lock_guard<std::mutex> io(io_mu);
+                    f = image.frame(frames[k]);
+                }
+                if (f.size() != npix) throw std::runtime_error("frame size does not match the shard's pixels");
+                std::copy(f.begin(), f.end(), dst);
+            };
+            // rank 0: finished frames written in time order
+            std::map<int64_t, std::pair<std::vector<double>, SolveInfo>> done;
+            int64_t written = off;
+            auto t_prev = std::chrono::steady_clock::now();
+            auto sink = [&](int64_t j, const double* xs, const SolveInfo& info) {
+                if (rank != 0) return;
+                SolveInfo fi = info;
+                if (fi.warm_from >= 0) {
+                    fi.warm_from += (int)off;
+                } else if (off && !cfg.no_guess) {  // started from the lead frame's solution (the series' x0)
+                    fi.warm_from = 0;
+                    fi.warm_iter = lead_iters;
+                }
+                done.emplace(j + off, std::make_pair(std::vector<double>(xs, xs + in.nvoxel), fi));
+                for (auto it = done.find(written); it != done.end(); it = done.find(written)) {
+                    const uint64_t cur = frames[written];
+                    const SolveInfo& fi = it->second.second;
+                    writer->add(it->second.first, fi.status, image.frame_time(cur), image.camera_frame_time(cur),
+                                fi.iterations);
+                    const auto now = std::chrono::steady_clock::now();
+                    const double ms = std::chrono::duration<double, std::milli>(now - t_prev).count();
+                    t_prev = now;
+                    std::cout << "Processed in: " << ms << " ms" << std::endl;
+                    if (fi.nonfinite) std::cerr << "warning: frame " << cur << ": non-finite iterate, stopped" << std::endl;
+                    if (profile.is_open())
+                        profile << "{\"frame\": " << cur << ", \"time\": " << image.frame_time(cur)
+                                << ", \"status\": " << fi.status << ", \"iterations\": " << fi.iterations
+                                << ", \"convergence\": " << fi.convergence << ", \"ms\": " << ms
+                                << ", \"batch\": " << cfg.batch_frames << ", \"warm_from\": "
+                                << (fi.warm_from >= 0 ? (int64_t)frames[fi.warm_from] : -1)
+                                << ", \"warm_iter\": " << fi.warm_iter << ", \"comm_fallbacks\": " << fi.comm_fallbacks
+                                << ", \"driver\": \"native\"}\n";
+                    done.erase(it);
+                    ++written;
+                }
+            };
+            mf->solve_series(nfr - off, src, sink, bwarm.empty() ? nullptr : bwarm.data(), !cfg.no_guess);
+            if (rank == 0 && profile.is_open()) {
+                const auto& ss = mf->series_stats();
+                profile << "{\"series\": true, \"frames\": " << ss.frames << ", \"sweeps\": " << ss.sweeps
+                        << ", \"queued_sweeps\": " << ss.queued_sweeps << ", \"slot_util\": " << ss.slot_util
+                        << ", \"mean_iterations\": " << ss.mean_iterations << ", \"chained\": " << ss.chained
+                        << ", \"mean_warm_age\": " << ss.mean_warm_age << ", \"series_ms\": " << ss.ms
+                        << ", \"chunk\": " << ss.chunk << ", \"admit_cap\": " << ss.admit_cap
+                        << ", \"src_age\": " << ss.src_age << ", \"src_finished\": " << (ss.src_finished ? 1 : 0)
+                        << ", \"lead\": " << (ss.lead ? 1 : 0) << ", \"src_extrap\": " << ss.src_extrap
+                        << ", \"restarts\": " << ss.restarts
+                        << ", \"batch\": " << mf->batch_frames() << ", \"driver\": \"native\"}\n";
             }
             frames.clear();
         }

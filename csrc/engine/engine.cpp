@@ -69,6 +69,7 @@ template class DeviceArray<float>;
 template class DeviceArray<double>;
 template class DeviceArray<SartState>;
 template class DeviceArray<MfState>;
+template class DeviceArray<MfQueue>;
 template class DeviceArray<uint64_t>;
 template class DeviceArray<unsigned>;
 template class DeviceArray<int64_t>;

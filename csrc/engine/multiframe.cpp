@@ -73,12 +73,35 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     set_device();
     hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
     hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
-    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hstate_), 2 * sizeof(MfState)), "hipHostMalloc");
+    hip_ok(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking), "hipStreamCreate");
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hsnap_), 2 * sizeof(Snap)), "hipHostMalloc");
     for (auto& e : ev_) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hg_), std::max<int64_t>(P_, 1) * NF * sizeof(double)),
-           "hipHostMalloc");
-    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hx_), (size_t)NF * ld_ * sizeof(float)), "hipHostMalloc");
     hip_ok(hipEventCreateWithFlags(&ev_copy_, hipEventDisableTiming), "hipEventCreate");
+    hip_ok(hipEventCreateWithFlags(&ev_stage_, hipEventDisableTiming), "hipEventCreate");
+    // device refill: a queue and an output ring of 2 nf entries each (staging and draining run a chunk behind the
+    // sweeps, ~nf frames finish per chunk at ~8 sweeps per frame); sweeps per host check (SART_MF_CHUNK, default
+    // min(check_interval, 4): the host check no longer gates a refill, only the staging and the drain)
+    qcap_ = rcap_ = 2 * NF;
+    chunk_ = std::min(cfg_.check_interval, 4);
+    if (const char* e = std::getenv("SART_MF_CHUNK"); e && *e) chunk_ = std::max(1, std::atoi(e));
+    // admissions per sweep of a time series (SART_MF_ADMIT_CAP; 0: any): a frame admitted together with others
+    // starts from the same source iterate, so a burst of admissions starts frames far from their predecessors
+    admit_cap_ = std::max(1, NF / 4);
+    if (const char* e = std::getenv("SART_MF_ADMIT_CAP"); e && *e) admit_cap_ = std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("SART_MF_SRC_AGE"); e && *e) src_age_ = std::max(0, std::atoi(e));
+    // A/B knobs of the chain: SART_MF_SRC_FINISHED=1 (sources: finished frames only), SART_MF_LEAD=0 (no lead frame)
+    if (const char* e = std::getenv("SART_MF_SRC_FINISHED"); e && *e) src_finished_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SART_MF_LEAD"); e && *e) lead_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SART_MF_SRC_EXTRAP"); e && *e) src_extrap_ = std::atof(e);
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hq_), (size_t)qcap_ * Pp_ * sizeof(float)), "hipHostMalloc");
+    std::memset(hq_, 0, (size_t)qcap_ * Pp_ * sizeof(float));  // padding rows stay zero
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hx_), (size_t)rcap_ * ld_ * sizeof(float)), "hipHostMalloc");
+    hg_.resize((size_t)NF * std::max<int64_t>(P_, 1));
+    q_.resize(1);
+    ghq_.resize((size_t)qcap_ * Pp_);
+    ring_.resize((size_t)rcap_ * ld_);
+    xlast_.resize(ld_);
+    if (cfg_.logarithmic) oq_.resize((size_t)qcap_ * ld_);
     nsf_ = mf_forward_num_splits(ld_, Pp_, bf16_ ? 512 : 0);  // bf16 storage: ~512 workgroups (see the back-projection)
     nsb_ = split_ ? mf_backproject_b16_num_splits(ld_, P_, x3_) : mf_backproject_num_splits(ld_, P_);
     if (sparse_) {  // the SpMM kernels write complete sums
@@ -97,7 +120,6 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     pen_.resize((size_t)NF * ld_);
     if (cfg_.logarithmic) O_.resize((size_t)NF * ld_);
     for (auto* b : {&ghat_, &arow_, &gpos_, &wo_}) b->resize((size_t)Pp_ * NF);
-    g64_.resize((size_t)Pp_ * NF);
     G64_.resize(NF);
     F2part_.resize((size_t)nwb_ * NF);
     st_.resize(1);
@@ -166,12 +188,15 @@ MultiFrameEngine::~MultiFrameEngine() {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : cev_)
         if (e) (void)hipEventDestroy(e);
+    if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
     if (comm_done_) (void)hipEventDestroy(comm_done_);
     if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
-    if (hstate_) (void)hipHostFree(hstate_);
-    if (hg_) (void)hipHostFree(hg_);
+    if (hsnap_) (void)hipHostFree(hsnap_);
+    if (hq_) (void)hipHostFree(hq_);
     if (hx_) (void)hipHostFree(hx_);
     if (ev_copy_) (void)hipEventDestroy(ev_copy_);
+    if (ev_stage_) (void)hipEventDestroy(ev_stage_);
+    if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -260,10 +285,14 @@ void MultiFrameEngine::backproject(const float* W, bool split_w, int64_t v0, int
     }
 }
 
-void MultiFrameEngine::sweep(bool last) {
+void MultiFrameEngine::sweep() {
     const int NF = nf_;
     MfState* st = st_.get();
+    MfQueue* q = q_.get();
     const MfSkipScope skip(&st->all_done);  // every slot done: the sweep's heavy kernels return at once
+    // the back-projection (and its operand split) also returns when every running frame is decided at max_iter in
+    // this sweep (mf_plan's skip_bwd): its corrections would be discarded; the collect still sums ||A x||^2
+    const int* bskip = skip_last_bwd_ ? &q->skip_bwd : &st->all_done;
     float* D = buf_.get();                     // [ld][nf] voxel-major corrections
     float* F2 = buf_.get() + (int64_t)NF * ld_;  // [nf] ||A x||^2, all-reduced with the last chunk
     const float* scale = cfg_.logarithmic ? rs_.dmask.get() : rs_.dscale.get();
@@ -272,23 +301,21 @@ void MultiFrameEngine::sweep(bool last) {
     launch_mf_weights(Fs_.get(), nsf_, Pp_, ghat_.get(), arow_.get(), cfg_.logarithmic, W_.get(), F2part_.get(),
                       NF, stream_, h16_ ? wmax_.get() : nullptr,
                       sparse_ && mf_sparse_needs_w_planes(NF, pw_) ? pw_ : 0);
-    if (last && skip_last_bwd_) {
-        // every running frame is decided at max_iter here (its update is skipped on all_done): ||A x||^2 only
-        launch_mf_collect(part_.get(), nsb_, ld_, 0, 0, scale, D, F2part_.get(), nwb_, F2, NF, stream_);
-        if (comm_->size() > 1) comm_->all_reduce(F2, (size_t)NF, ReduceOp::kSum, stream_);
-        launch_mf_decide(st, F2, stream_);
-        ++host_sweep_;
-        return;
-    }
     // D[v0, v1) = scale * A^T W and, with the last chunk, the per-frame ||A x||^2: a sparse shard's SpMM writes the
     // scaled sums itself (the collect then only sums F2part)
     auto bwd_collect = [&](int64_t v0, int64_t v1, bool first, bool lastc) {
         if (sparse_) {
-            backproject(W_.get(), first, v0, v1, true, D, scale);
+            {
+                const MfSkipScope sb(bskip);
+                backproject(W_.get(), first, v0, v1, true, D, scale);
+            }
             if (lastc) launch_mf_collect(part_.get(), nsb_, ld_, 0, 0, scale, D, F2part_.get(), nwb_, F2, NF, stream_);
             return;
         }
-        backproject(W_.get(), first, v0, v1, true);
+        {
+            const MfSkipScope sb(bskip);
+            backproject(W_.get(), first, v0, v1, true);
+        }
         launch_mf_collect(part_.get(), nsb_, ld_, v0, v1, scale, D, lastc ? F2part_.get() : nullptr, nwb_,
                           lastc ? F2 : nullptr, NF, stream_);
     };
@@ -323,267 +350,333 @@ void MultiFrameEngine::sweep(bool last) {
         pen = pen_.get();
     }
     if (comm_->size() > 1 && nc > 1) hip_ok(hipStreamWaitEvent(stream_, comm_done_, 0), "wait all-reduce");
-    launch_mf_decide(st, F2, stream_);
+    launch_mf_decide(st, F2, stream_, q);
     launch_mf_update(X_.get(), D, O_.get(), pen, (float)cfg_.relaxation, cfg_.logarithmic, V_, ld_, st, NF, stream_,
-                     Xprev_.get());
+                     Xprev_.get(), q, &rf_);
+    launch_mf_admit_rows(q, ghq_.get(), P_, Pp_, rs_.ray_len.get(), (float)cfg_.ray_length_threshold, ghat_.get(),
+                         arow_.get(), NF, stream_);
     if (cfg_.fault_nan_sweep >= 0 && host_sweep_ == cfg_.fault_nan_sweep)  // fault injection (tests): slot 0
         hip_ok(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(X_.get()), 0x7fc00000, 1, stream_), "inject NaN");
     ++host_sweep_;
 }
 
-// Continuous batching. The batch's nf columns are slots: every slot holds one frame, and a slot whose frame has
-// finished (converged, non-finite, or max_iter) is refilled with the next frame between two sweeps, so no
-// sweep works on finished frames while frames are waiting (the former group-by-group solve ran every group
-// as long as its slowest frame). All ranks see the same device state (it follows all-reduced sums), so they
-// admit the same frames at the same chunk.
-// Start values: the first frames start from x0 (or cold); later frames of a time series (chain) from the
-// solution of the latest frame finished before them (SolveInfo::warm_from), otherwise cold (--no_guess).
-// The chunks of check_interval sweeps stay pipelined: chunk c + 1 is queued before the state after chunk c
-// is read, so a refill decided on chunk c's state is queued after chunk c + 1 and the slot's new frame is
-// visible in the states from chunk c + 2 on.
-void MultiFrameEngine::admit(const double* g, const std::vector<int>& slots, const std::vector<int>& frames,
-                             const double* warm, const float* dev_src, double src_norm,
-                             std::vector<double>& slot_norm) {
+void MultiFrameEngine::refill() {
     const int NF = nf_;
-    const int k = (int)slots.size();
-    if (k == 0) return;
+    float* D = buf_.get();
+    launch_mf_decide(st_.get(), D + (int64_t)NF * ld_, stream_, q_.get());  // every slot done: the plan only
+    launch_mf_update(X_.get(), D, O_.get(), nullptr, (float)cfg_.relaxation, cfg_.logarithmic, V_, ld_, st_.get(), NF,
+                     stream_, Xprev_.get(), q_.get(), &rf_);
+    launch_mf_admit_rows(q_.get(), ghq_.get(), P_, Pp_, rs_.ray_len.get(), (float)cfg_.ray_length_threshold,
+                         ghat_.get(), arow_.get(), NF, stream_);
+}
+
+void MultiFrameEngine::stage(int64_t first, int64_t e0, int k, const FrameSource& src, bool cold) {
+    const int NF = nf_;
+    if (k <= 0) return;
+    if (k > NF) throw std::logic_error("MultiFrameEngine::stage: at most nf frames per call");
+    RoctxRange r("sart::mf_stage");
+    for (int j = 0; j < k; ++j) src(first + e0 + j, hg_.data() + (size_t)j * P_);
     // per-frame maxima and positive sums of squares over all ranks' pixels (reference sartsolver_cuda.cpp:146-157)
     double mx[kMfMaxFrames], gs[kMfMaxFrames];
-    auto scan = [&](int q) {  // one frame, pixels in order (the sum is deterministic whatever thread runs it)
+    auto scan = [&](int j) {  // one frame, pixels in order (the sum is deterministic whatever thread runs it)
         double m = -std::numeric_limits<double>::infinity(), s = 0.0;
-        const double* gq = g + (int64_t)frames[q] * P_;
-        double* hq = hg_ + (int64_t)q * P_;
+        double* g = hg_.data() + (size_t)j * P_;
         for (int64_t p = 0; p < P_; ++p) {
-            double v = gq[p];
+            double v = g[p];
             if (!std::isfinite(v)) v = -1.0;  // non-finite pixel: masked like a saturated one
-            hq[p] = v;
+            g[p] = v;
             m = std::max(m, v);
             if (v > 0) s += v * v;
         }
-        mx[q] = m, gs[q] = s;
+        mx[j] = m, gs[j] = s;
     };
-    // frames on host threads when the batch is large (64 frames x 245760 pixels: 12 ms on one thread per solve)
+    MfPublish pub{};
+    pub.n = k;
+    pub.e0 = e0;
+    auto normalise = [&](int j) {  // ghat = (float)(g / s) (k_mf_prep_slots' arithmetic, on the host)
+        const double s = pub.norm[j];
+        const double* g = hg_.data() + (size_t)j * P_;
+        float* out = hq_ + (size_t)((e0 + j) % qcap_) * Pp_;
+        for (int64_t p = 0; p < P_; ++p) out[p] = (float)(g[p] / s);
+    };
+    // frames on host threads when the batch is large (64 frames x 245760 pixels: 12 ms on one thread)
     const int nth = (int)std::min<int64_t>({k, 8, std::max<int64_t>(1, (int64_t)k * P_ / (1 << 20))});
-    if (nth > 1) {
-        std::vector<std::thread> pool;
-        for (int t = 0; t < nth; ++t)
-            pool.emplace_back([&, t] {
-                for (int q = t; q < k; q += nth) scan(q);
-            });
-        for (auto& th : pool) th.join();
-    } else {
-        for (int q = 0; q < k; ++q) scan(q);
-    }
+    auto par = [&](const std::function<void(int)>& fn) {
+        if (nth > 1) {
+            std::vector<std::thread> pool;
+            for (int t = 0; t < nth; ++t)
+                pool.emplace_back([&, t] {
+                    for (int j = t; j < k; j += nth) fn(j);
+                });
+            for (auto& th : pool) th.join();
+        } else {
+            for (int j = 0; j < k; ++j) fn(j);
+        }
+    };
+    par(scan);
     comm_->host().all_reduce_host(mx, k, ReduceOp::kMax);
     comm_->host().all_reduce_host(gs, k, ReduceOp::kSum);
-    MfSlots sl{};
-    sl.n = k;
-    for (int q = 0; q < k; ++q) {
-        sl.slot[q] = slots[q];
-        sl.norm[q] = mx[q] > 0 ? mx[q] : 1.0;
-        sl.G[q] = gs[q] / (sl.norm[q] * sl.norm[q]);
-        if (!(sl.G[q] > 0)) sl.G[q] = 1.0;
-        slot_norm[slots[q]] = sl.norm[q];
+    for (int j = 0; j < k; ++j) {
+        pub.frame[j] = (int32_t)(first + e0 + j);
+        pub.cold[j] = cold ? 1 : 0;
+        pub.norm[j] = mx[j] > 0 ? mx[j] : 1.0;
+        pub.G[j] = gs[j] / (pub.norm[j] * pub.norm[j]);
+        if (!(pub.G[j] > 0)) pub.G[j] = 1.0;
     }
-    if (P_) hip_ok(hipMemcpyAsync(g64_.get(), hg_, (size_t)k * P_ * sizeof(double), hipMemcpyHostToDevice, stream_),
-                   "H2D g");
-    launch_mf_prep_slots(g64_.get(), P_, Pp_, sl, rs_.ray_len.get(), (float)cfg_.ray_length_threshold, ghat_.get(),
-                         arow_.get(), gpos_.get(), wo_.get(), NF, stream_);
-    if (warm) {  // x = x_prev / s, clamped (reference sartsolver_cuda.cpp:176-180)
-        if (V_) hip_ok(hipMemcpyAsync(x064_.get(), warm, V_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D x0");
-        launch_mf_init_slots_warm(X_.get(), x064_.get(), sl, V_, ld_, stream_);
-    } else if (dev_src) {  // copied first: a new frame may enter the source's own slot
-        if (V_) hip_ok(hipMemcpyAsync(xsrc_.get(), dev_src, V_ * sizeof(float), hipMemcpyDeviceToDevice, stream_), "D2D");
-        launch_mf_init_slots_scaled(X_.get(), xsrc_.get(), src_norm, sl, V_, ld_, stream_);
-    } else {  // x0 = max([rho > tau] A^T max(ghat, 0) / rho, 1e-7) (reference sart_kernels.cu:22-60)
-        backproject(gpos_.get(), true, 0, ld_);
-        launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, nullptr, buf_.get(), nullptr, 0, nullptr, NF, stream_);
-        comm_->all_reduce(buf_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
-        launch_mf_init_slots_cold(X_.get(), buf_.get(), rs_.dinv.get(), sl, V_, ld_, NF, stream_);
+    par(normalise);
+    // normalised pixels into the queue on the copy stream (one or two runs of ring positions), next to the sweeps
+    for (int j = 0; j < k;) {
+        const int pos = (int)((e0 + j) % qcap_);
+        const int run = std::min(k - j, qcap_ - pos);
+        if (P_)
+            hip_ok(hipMemcpyAsync(ghq_.get() + (size_t)pos * Pp_, hq_ + (size_t)pos * Pp_, (size_t)run * Pp_ * sizeof(float),
+                                  hipMemcpyHostToDevice, copy_stream_),
+                   "H2D queue");
+        j += run;
     }
-    if (cfg_.logarithmic) {  // frame-constant observed back-projection of the new frames
-        backproject(wo_.get(), true, 0, ld_);
-        launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, rs_.dmask.get(), Otmp_.get(), nullptr, 0, nullptr, NF,
-                          stream_);
-        comm_->all_reduce(Otmp_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
-        launch_mf_copy_slots(O_.get(), Otmp_.get(), sl, ld_, NF, stream_);
+    hip_ok(hipEventRecord(ev_stage_, copy_stream_), "event");
+    hip_ok(hipStreamWaitEvent(stream_, ev_stage_, 0), "wait staging");
+    if (cold || cfg_.logarithmic) {
+        // one batched back-projection of the k staged frames (columns 0 .. k - 1): cold starts
+        // x0 = max([rho > tau] A^T max(ghat, 0) / rho, 1e-7) (reference sart_kernels.cu:22-60) and / or the
+        // frame-constant observed back-projection O = mask A^T (a ghat) of log mode
+        const float thr = (float)cfg_.ray_length_threshold;
+        launch_mf_stage_ops(ghq_.get(), e0, qcap_, k, P_, Pp_, rs_.ray_len.get(), thr, gpos_.get(),
+                            cfg_.logarithmic ? wo_.get() : nullptr, NF, stream_);
+        if (cold) {
+            backproject(gpos_.get(), true, 0, ld_);
+            launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, nullptr, buf_.get(), nullptr, 0, nullptr, NF, stream_);
+            if (comm_->size() > 1) comm_->all_reduce(buf_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
+            launch_mf_stage_cols(buf_.get(), rs_.dinv.get(), e0, qcap_, k, V_, ld_, NF, x0q_.get(), stream_);
+        }
+        if (cfg_.logarithmic) {
+            backproject(wo_.get(), true, 0, ld_);
+            launch_mf_collect(part_.get(), nsb_, ld_, 0, ld_, rs_.dmask.get(), buf_.get(), nullptr, 0, nullptr, NF,
+                              stream_);
+            if (comm_->size() > 1) comm_->all_reduce(buf_.get(), (size_t)NF * ld_, ReduceOp::kSum, stream_);
+            launch_mf_stage_cols(buf_.get(), nullptr, e0, qcap_, k, V_, ld_, NF, oq_.get(), stream_);
+        }
     }
-    launch_mf_slot_reset(st_.get(), sl, stream_);
+    launch_mf_publish(q_.get(), pub, stream_);
 }
 
 std::vector<SolveInfo> MultiFrameEngine::solve_batch(const double* g, int nframes, double* x_out, const double* x0,
-                                                     bool chain) {
-    // a device all-reduce that timed out on some rank (P2P: a peer never arrived) is agreed over the host
-    // communicator; every rank then switches to the base communicator and re-solves the batch once
-    for (int attempt = 0;; ++attempt) {
-        std::vector<SolveInfo> out = solve_batch_once(g, nframes, x_out, x0, chain);
-        if (!device_comm_failed_anywhere(comm_)) {
-            comm_->check();
-            for (auto& info : out) {
-                info.comm_fallbacks = attempt;
-                info.comm = comm_->backend();
-            }
-            return out;
-        }
-        const bool had = comm_->degrade();
-        if (comm_->rank() == 0)
-            std::fprintf(stderr, "sart: device all-reduce timed out; re-solving the batch on %s\n", comm_->backend());
-        if (!had || attempt >= 1) throw std::runtime_error("MultiFrameEngine: device all-reduce failed");
-    }
-}
-
-std::vector<SolveInfo> MultiFrameEngine::solve_batch_once(const double* g, int nframes, double* x_out,
-                                                          const double* x0, bool chain) {
-    set_device();
-    RoctxRange range("sart::mf_solve");
-    const int NF = nf_;
+                                                     bool chain, double* starts) {
     std::vector<SolveInfo> out(std::max(nframes, 0));
     if (nframes <= 0) return out;
     const auto t0 = std::chrono::steady_clock::now();
+    if (starts) {  // the start value of every frame (normalised on the device; de-normalised below)
+        set_device();
+        starts_.resize((size_t)nframes * ld_);
+        rf_.starts = starts_.get();
+    }
+    try {
+        solve_series(
+            nframes, [&](int64_t k, double* dst) { std::memcpy(dst, g + k * P_, (size_t)P_ * sizeof(double)); },
+            [&](int64_t k, const double* x, const SolveInfo& info) {
+                std::memcpy(x_out + k * V_, x, (size_t)V_ * sizeof(double));
+                out[k] = info;
+            },
+            x0, chain);
+    } catch (...) {
+        rf_.starts = nullptr;
+        throw;
+    }
+    if (starts) {
+        rf_.starts = nullptr;
+        std::vector<float> h((size_t)nframes * ld_);
+        hip_ok(hipMemcpy(h.data(), starts_.get(), h.size() * sizeof(float), hipMemcpyDeviceToHost), "D2H starts");
+        for (int k = 0; k < nframes; ++k)
+            for (int64_t v = 0; v < V_; ++v)
+                starts[(size_t)k * V_ + v] = (double)h[(size_t)k * ld_ + v] * frame_norm_[k];
+    }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (auto& info : out) info.ms = ms / nframes;
+    return out;
+}
+
+void MultiFrameEngine::solve_series(int64_t nframes, const FrameSource& src, const FrameSink& sink, const double* x0,
+                                    bool chain) {
+    set_device();
+    RoctxRange range("sart::mf_series");
+    stats_ = SeriesStats{};
+    if (nframes <= 0) return;
+    if (nframes > std::numeric_limits<int32_t>::max()) throw std::invalid_argument("solve_series: too many frames");
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<char> delivered((size_t)nframes, 0);
+    frame_norm_.assign((size_t)nframes, 1.0);
+    std::vector<double> newest;  // the newest delivered finite solution (a re-solve's chain start)
+    int64_t newest_frame = -1;
+    int64_t first = 0;
+    for (int attempt = 0;; ++attempt) {
+        const bool failed = series_once(first, nframes, src, sink, attempt == 0 ? x0 : (newest_frame >= 0 && chain ? newest.data() : x0),
+                                        chain, delivered, attempt, newest, newest_frame);
+        if (!failed) break;
+        const bool had = comm_->degrade();
+        if (comm_->rank() == 0)
+            std::fprintf(stderr, "sart: device all-reduce timed out; re-solving the undelivered frames on %s\n",
+                         comm_->backend());
+        if (!had || attempt >= 1) throw std::runtime_error("MultiFrameEngine: device all-reduce failed");
+        ++stats_.restarts;
+        while (first < nframes && delivered[first]) ++first;
+    }
+    comm_->check();
+    stats_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+bool MultiFrameEngine::series_once(int64_t first, int64_t nframes, const FrameSource& src, const FrameSink& sink,
+                                   const double* x0, bool chain, std::vector<char>& delivered, int attempt,
+                                   std::vector<double>& newest, int64_t& newest_frame) {
+    const int NF = nf_;
+    const int64_t n = nframes - first;  // frames of this pass: queue entry e = frame first + e
     host_sweep_ = 0;
+    // cold starts are staged for every frame without --chain, and for the first nf frames of a chain without x0
+    // (later ones start from a frame in flight)
+    const bool any_cold = !(chain && x0);
+    if (any_cold && x0q_.size() == 0) x0q_.resize((size_t)qcap_ * ld_);
     if ((int64_t)x064_.size() < V_) x064_.resize(std::max<int64_t>(V_, 1));
-    if (cfg_.logarithmic && (int64_t)Otmp_.size() < (int64_t)NF * ld_) Otmp_.resize((size_t)NF * ld_);
-    if ((int64_t)xsrc_.size() < ld_) xsrc_.resize(ld_);
+    rf_.ring = ring_.get();
+    rf_.xlast = xlast_.get();
+    rf_.x0 = x064_.get();
+    rf_.x0q = x0q_.size() ? x0q_.get() : nullptr;
+    rf_.oq = oq_.size() ? oq_.get() : nullptr;
     // every slot starts empty (done) with finite zero columns
-    for (auto* b : {&X_, &Xprev_, &ghat_, &arow_, &gpos_, &wo_})
+    for (auto* b : {&X_, &Xprev_, &ghat_, &arow_})
         hip_ok(hipMemsetAsync(b->get(), 0, b->size() * sizeof(float), stream_), "memset");
     if (cfg_.logarithmic) hip_ok(hipMemsetAsync(O_.get(), 0, O_.size() * sizeof(float), stream_), "memset");
     hip_ok(hipMemsetAsync(G64_.get(), 0, G64_.size() * sizeof(double), stream_), "memset");
     launch_mf_state_begin(st_.get(), G64_.get(), 0, cfg_.conv_tolerance, cfg_.max_iterations, NF, stream_);
+    const int64_t x0_below = x0 ? (chain ? std::numeric_limits<int64_t>::max() : first + NF) : 0;
+    launch_mf_queue_begin(q_.get(), qcap_, rcap_, chain, chain ? admit_cap_ : 0, src_age_, x0_below, src_finished_,
+                          chain && !x0 && lead_, (float)src_extrap_, stream_);
+    if (x0 && V_) hip_ok(hipMemcpyAsync(x064_.get(), x0, V_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D x0");
+    stats_.chunk = chunk_;
+    stats_.admit_cap = chain ? admit_cap_ : 0;
+    stats_.src_age = src_age_;
+    stats_.src_finished = src_finished_;
+    stats_.src_extrap = src_extrap_;
+    stats_.lead = chain && !x0 && lead_;
 
-    std::vector<int> slot_frame(NF, -1), slot_valid(NF, 0), frame_warm(nframes, -1);
-    std::vector<double> slot_norm(NF, 1.0), frame_norm(nframes, 1.0);
-    int next = 0, finished = 0, latest = -1;  // latest: highest-index frame finished with a finite solution
+    int64_t staged = 0;
+    auto stage_upto = [&](int64_t head) {  // stage while the queue has room for a unit (nf with a back-projection)
+        while (staged < n) {
+            // the first nf frames start from x0 (or cold without it); later ones cold (!chain) or chained
+            const bool cold = chain ? (!x0 && staged < NF) : (!x0 || staged >= NF);
+            const int64_t lim = staged < NF ? NF - staged : NF;  // no unit straddles frame nf
+            const int64_t room = qcap_ - (staged - head);
+            const int64_t unit = (cold || cfg_.logarithmic) ? std::min<int64_t>(lim, n - staged)
+                                                            : std::max<int64_t>(1, std::min<int64_t>(NF / 4, n - staged));
+            if (room < unit) return;
+            const int k = (int)std::min<int64_t>({room, lim, n - staged});
+            stage(first, staged, k, src, cold);
+            staged += k;
+        }
+    };
+    stage_upto(0);
+    refill();
+
     int issued = 0, checked = 0;
-    // frames whose solution is being copied back (finalised at the next state check, after the copy)
+    auto issue = [&]() {
+        {
+            RoctxRange r("sart::mf_chunk");
+            for (int i = 0; i < chunk_; ++i) sweep();
+        }
+        const int slot = issued & 1;
+        hip_ok(hipMemcpyAsync(&hsnap_[slot].st, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
+        hip_ok(hipMemcpyAsync(&hsnap_[slot].q, q_.get(), sizeof(MfQueue), hipMemcpyDeviceToHost, stream_), "D2H queue");
+        hip_ok(hipEventRecord(ev_[slot], stream_), "event");
+        ++issued;
+    };
     struct Pending {
-        int frame, slot;
-        bool rollback;
+        MfFinish log;
+        int pos;
     };
     std::vector<Pending> pend;
+    std::vector<double> x(std::max<int64_t>(V_, 1));
+    int64_t seen_fin = 0, finished = 0, warm_age = 0;
     auto finalize = [&]() {
         for (const Pending& pd : pend) {
-            const float* src = hx_ + (size_t)pd.slot * ld_;
-            double* dst = x_out + (int64_t)pd.frame * V_;
-            for (int64_t v = 0; v < V_; ++v) dst[v] = (double)src[v] * frame_norm[pd.frame];
-            bool finite = true;
-            for (int64_t v = 0; v < V_ && finite; ++v) finite = std::isfinite(dst[v]);
-            if (finite && pd.frame > latest) latest = pd.frame;
+            const MfFinish& L = pd.log;
+            const float* hs = hx_ + (size_t)pd.pos * ld_;
+            for (int64_t v = 0; v < V_; ++v) x[v] = (double)hs[v] * L.norm;
             ++finished;
+            stats_.busy_slot_sweeps += L.iters + 1;
+            stats_.mean_iterations += L.iters;
+            if (L.warm_from >= 0) ++stats_.chained, warm_age += (L.frame - L.warm_from);
+            if (L.frame < 0 || L.frame >= nframes || delivered[L.frame]) continue;
+            SolveInfo info;
+            info.status = L.status;
+            info.iterations = L.iters;
+            info.convergence = L.conv;
+            info.nonfinite = (L.flags & 1) != 0;
+            info.used_fused = false;
+            info.warm_from = L.warm_from;
+            info.warm_iter = L.warm_iter;
+            info.comm_fallbacks = attempt;
+            info.comm = comm_->backend();
+            info.sweeps = L.iters + 1;
+            frame_norm_[L.frame] = L.norm;
+            delivered[L.frame] = 1;
+            sink(L.frame, x.data(), info);
+            if (L.frame > newest_frame && !info.nonfinite) {
+                newest.assign(x.begin(), x.begin() + V_);
+                newest_frame = L.frame;
+            }
         }
         pend.clear();
     };
-    // dev: the best finished frame whose solution is still only on the device (collected at this check)
-    struct DevSrc {
-        int frame = -1, slot = -1;
-        bool prev = false;
-    };
-    auto fill = [&](const std::vector<int>& free_slots, const DevSrc& dev) {
-        std::vector<int> slots, frames;
-        for (int f : free_slots) {
-            if (next >= nframes) break;
-            slots.push_back(f);
-            frames.push_back(next++);
-        }
-        if (slots.empty()) return;
-        const double* warm = nullptr;
-        const float* dsrc = nullptr;
-        double dnorm = 1.0;
-        int wsrc = -1;
-        if (issued == 0) {
-            warm = x0;  // the first frames: the caller's start value (or cold)
-        } else if (chain && dev.frame > latest) {
-            dsrc = (dev.prev ? Xprev_.get() : X_.get()) + (size_t)dev.slot * ld_;
-            dnorm = frame_norm[dev.frame];
-            wsrc = dev.frame;
-        } else if (chain && latest >= 0) {
-            warm = x_out + (int64_t)latest * V_;
-            wsrc = latest;
-        }
-        admit(g, slots, frames, warm, dsrc, dnorm, slot_norm);
-        for (size_t q = 0; q < slots.size(); ++q) {
-            slot_frame[slots[q]] = frames[q];
-            slot_valid[slots[q]] = issued;  // states from the next chunk on describe this frame
-            frame_warm[frames[q]] = wsrc;
-        }
-    };
-    // Sweeps are queued in chunks of at most check_interval, and never past the last sweep a running frame can
-    // need: a frame admitted after `enq` queued sweeps has made its final decision by sweep enq + max_iter + 1
-    // (its slot keeps the device sweep counter running), so a fixed-iteration batch queues exactly the sweeps
-    // it uses.
-    int64_t enq = 0;
-    std::vector<int64_t> slot_end(NF, 0);
-    auto issue = [&]() {
-        int64_t bound = 0;
-        for (int f = 0; f < NF; ++f)
-            if (slot_frame[f] >= 0) bound = std::max(bound, slot_end[f] - enq);
-        const int n = (int)std::min<int64_t>(cfg_.check_interval, bound);
-        if (n <= 0) return false;
-        {
-            RoctxRange r("sart::mf_chunk");
-            // the chunk that reaches the bound ends with the batch's final sweep (its frames are all decided there)
-            for (int i = 0; i < n; ++i) sweep(i == bound - 1);
-        }
-        enq += n;
-        const int slot = issued & 1;
-        hip_ok(hipMemcpyAsync(hstate_ + slot, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
-        hip_ok(hipEventRecord(ev_[slot], stream_), "event");
-        ++issued;
-        return true;
-    };
-    auto admitted = [&]() {  // after fill(): the end bound of the slots that just took frames
-        for (int f = 0; f < NF; ++f)
-            if (slot_frame[f] >= 0 && slot_valid[f] == issued) slot_end[f] = enq + cfg_.max_iterations + 1;
-    };
-    std::vector<int> all(NF);
-    for (int f = 0; f < NF; ++f) all[f] = f;
-    fill(all, DevSrc{});
-    admitted();
     issue();
-    while (finished < nframes) {
-        issue();  // keep the next chunk in flight while frames run
+    issue();
+    bool failed = false;
+    while (finished < n) {
         if (!pend.empty()) {  // the solutions copied at the previous check
             hip_ok(hipEventSynchronize(ev_copy_), "mf copy");
             finalize();
-            if (finished >= nframes) break;
+            if (finished >= n) break;
         }
         if (checked >= issued) throw std::runtime_error("MultiFrameEngine: no chunk in flight and frames unfinished");
         const int c = checked++;
         hip_ok(hipEventSynchronize(ev_[c & 1]), "mf chunk");
-        const MfState S = hstate_[c & 1];
-        std::vector<int> freed;
-        DevSrc best;
-        for (int f = 0; f < NF; ++f) {
-            const int fr = slot_frame[f];
-            if (fr < 0 || c < slot_valid[f] || !S.done[f]) continue;
-            const bool rollback = (S.rollback[f >> 6] >> (f & 63)) & 1;
-            SolveInfo& info = out[fr];
-            info.status = S.status[f] == kSuccess ? kSuccess : kMaxIterationsExceeded;
-            info.iterations = S.iters[f];
-            info.convergence = S.conv[f];
-            info.nonfinite = (S.flags[f >> 6] >> (f & 63)) & 1;
-            info.used_fused = false;
-            info.warm_from = frame_warm[fr];
-            frame_norm[fr] = slot_norm[f];
-            const float* src = (rollback ? Xprev_.get() : X_.get()) + (size_t)f * ld_;
-            hip_ok(hipMemcpyAsync(hx_ + (size_t)f * ld_, src, V_ * sizeof(float), hipMemcpyDeviceToHost, stream_),
+        const MfQueue& Q = hsnap_[c & 1].q;
+        const int64_t fin = Q.fin, head = Q.q_head;
+        const int sweeps = hsnap_[c & 1].st.sweep;
+        std::vector<Pending> fresh;
+        for (int64_t e = seen_fin; e < fin; ++e) {
+            const int pos = (int)(e % rcap_);
+            fresh.push_back({Q.log[pos], pos});
+        }
+        if (device_comm_failed_anywhere(comm_)) {  // collective: every rank sees the same device state
+            failed = true;
+            break;
+        }
+        for (const Pending& pd : fresh) {  // solutions from the output ring, behind the chunk that wrote them
+            hip_ok(hipMemcpyAsync(hx_ + (size_t)pd.pos * ld_, ring_.get() + (size_t)pd.pos * ld_, V_ * sizeof(float),
+                                  hipMemcpyDeviceToHost, stream_),
                    "D2H x");
-            pend.push_back({fr, f, rollback});
-            if (!(info.nonfinite && !rollback) && fr > best.frame) best = DevSrc{fr, f, rollback};
-            slot_frame[f] = -1;
-            freed.push_back(f);
+            pend.push_back(pd);
         }
-        if (!freed.empty()) {
-            hip_ok(hipEventRecord(ev_copy_, stream_), "event");  // the copies, before the refills' work
-            fill(freed, best);
-            admitted();
+        if (!fresh.empty()) {
+            seen_fin = fin;
+            launch_mf_drained(q_.get(), seen_fin, stream_);  // the ring positions are free again after the copies
+            hip_ok(hipEventRecord(ev_copy_, stream_), "event");
         }
+        stage_upto(head);
+        stats_.sweeps = sweeps;
+        if (fin < n) issue();  // frames left to finish on the device (a chunk still in flight may finish them)
     }
-    hip_ok(hipStreamSynchronize(stream_), "mf solve");
+    hip_ok(hipStreamSynchronize(stream_), "mf series");
     if (comm_stream_) hip_ok(hipStreamSynchronize(comm_stream_), "mf comm");
-    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    for (auto& info : out) info.ms = ms / nframes;
-    return out;
+    hip_ok(hipStreamSynchronize(copy_stream_), "mf copy stream");
+    if (!failed) {
+        const MfState& S = hsnap_[(issued - 1) & 1].st;
+        stats_.sweeps = S.sweep;
+        stats_.queued_sweeps = (int64_t)issued * chunk_;
+        stats_.frames = finished;
+        if (finished) stats_.mean_iterations /= finished;
+        if (stats_.chained) stats_.mean_warm_age = (double)warm_age / stats_.chained;
+        if (stats_.sweeps > 0) stats_.slot_util = (double)stats_.busy_slot_sweeps / ((double)stats_.sweeps * NF);
+    }
+    return failed;
 }
 
 }  // namespace sart

@@ -3,14 +3,16 @@
 // frame by frame (reference main.cpp:131-140), streaming the RTM twice per iteration per frame; batching
 // turns A.x and A^T.w into skinny GEMMs (nf right-hand sides) that reuse every byte of A nf times. Every frame
 // keeps its own normalisation, saturation mask, convergence history, status and iteration count; frames
-// that finish are frozen while the others continue. Groups are cold-started (like --no_guess), or warm-
-// started as a time series: group k + 1 starts from the solution of group k's last frame (the reference's
-// frame-to-frame warm start, main.cpp:127-139, applied per group of batch_frames() frames).
+// that finish are retired and their slots refilled on the device in the same sweep (solve_series). Frames are
+// cold-started (like --no_guess), or warm-started as a time series: each frame starts from the current iterate of
+// the newest frame in flight (the reference's frame k-1 -> k warm start, main.cpp:127-139, pipelined: the
+// predecessor need not have converged yet).
 #pragma once
 
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -34,13 +36,33 @@ class MultiFrameEngine {
     MultiFrameEngine& operator=(const MultiFrameEngine&) = delete;
 
     void set_laplacian(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t nnz);
-    // g: nframes x nrows (host fp64, frame-major); x_out: nframes x nvoxel. batch_frames() slots, refilled with
-    // the next frame as soon as a slot's frame finishes (continuous batching). x0 (optional, nvoxel,
-    // de-normalised like a solution): start value of the first batch_frames() frames (null: cold). chain: every
-    // later frame starts from the solution of the latest frame finished before it (time series; the index is
-    // SolveInfo::warm_from); otherwise later frames cold-start.
+    // A series of nframes frames through batch_frames() slots with device-side refill: the sweep in which a frame
+    // finishes retires it and admits the next staged frame into its slot (MfQueue, mf_plan in multiframe_glue.hip).
+    // src(k, dst): frame k's pixels of this rank (host fp64, nrows) -- asked once per frame in increasing order
+    // (again for the frames not delivered yet when a device all-reduce failure makes every rank re-solve them).
+    // sink(k, x, info): frame k finished (x: nvoxel, de-normalised); frames finish out of order, each is delivered
+    // once. x0 (optional, nvoxel, de-normalised): start value when no chain source exists (chain), or of the first
+    // batch_frames() frames (!chain); null: cold. chain (time series): every frame starts from the current iterate
+    // of the newest frame in flight or finished (SolveInfo::warm_from / warm_iter), rescaled to its own
+    // normalisation; otherwise frames cold-start. Collective over the communicator.
+    using FrameSource = std::function<void(int64_t k, double* dst)>;
+    using FrameSink = std::function<void(int64_t k, const double* x, const SolveInfo& info)>;
+    void solve_series(int64_t nframes, const FrameSource& src, const FrameSink& sink, const double* x0 = nullptr,
+                      bool chain = false);
+    // g: nframes x nrows (host fp64, frame-major); x_out: nframes x nvoxel: solve_series over an array.
+    // starts (optional, nframes x nvoxel): each frame's start value, de-normalised (tests of the chain semantics)
     std::vector<SolveInfo> solve_batch(const double* g, int nframes, double* x_out, const double* x0 = nullptr,
-                                       bool chain = false);
+                                       bool chain = false, double* starts = nullptr);
+    // counters of the last solve_series (--profile): sweeps the device ran with a frame in some slot, sweeps queued,
+    // slot-sweeps spent on frames (sum of sweeps per frame) over nf x sweeps, staged frames, restarts
+    struct SeriesStats {
+        int64_t frames = 0, sweeps = 0, queued_sweeps = 0, busy_slot_sweeps = 0, chained = 0;
+        double slot_util = 0.0, mean_iterations = 0.0, mean_warm_age = 0.0, ms = 0.0;
+        int chunk = 0, admit_cap = 0, src_age = 0, restarts = 0;
+        bool src_finished = false, lead = false;
+        double src_extrap = 0.0;
+    };
+    const SeriesStats& series_stats() const { return stats_; }
     int64_t nrows() const { return P_; }
     int64_t nvoxel() const { return V_; }
     int batch_frames() const { return nf_; }
@@ -55,16 +77,20 @@ class MultiFrameEngine {
     static int batch_width(int frames);
 
    private:
-    std::vector<SolveInfo> solve_batch_once(const double* g, int nframes, double* x_out, const double* x0, bool chain);
-    // frames[q] of g into slots[q] (normalisation, prep, start value, log observed back-projection, state)
-    // Start value: warm (host, de-normalised), else dev_src (a finished frame's normalised solution still on
-    // the device, normalisation src_norm), else cold.
-    void admit(const double* g, const std::vector<int>& slots, const std::vector<int>& frames, const double* warm,
-               const float* dev_src, double src_norm, std::vector<double>& slot_norm);
-    // last: the batch's final sweep (every running frame reaches max_iter at its decision): forward, ||A x||^2 and
-    // the decision only; its back-projection and update would be discarded (reference sartsolver_cuda.cpp:231-262
-    // runs max_iter back-projections after the initial guess)
-    void sweep(bool last = false);
+    // one pass over frames [first, nframes) (frames already delivered are solved again but not re-delivered);
+    // true when a device all-reduce failed on some rank (agreed over the host communicator)
+    bool series_once(int64_t first, int64_t nframes, const FrameSource& src, const FrameSink& sink, const double* x0,
+                     bool chain, std::vector<char>& delivered, int attempt, std::vector<double>& newest,
+                     int64_t& newest_frame);
+    // queue entries [e0, e0 + k) = frames first + e0 .. (k <= nf): normalisation over all ranks, normalised pixels
+    // into the queue (copy stream), cold starts (cold) and the observed back-projection (log) by one batched
+    // back-projection, then published to the plan
+    void stage(int64_t first, int64_t e0, int k, const FrameSource& src, bool cold);
+    // every sweep ends with the decision + refill plan, the update (with retire / start values) and the admitted
+    // frames' pixel columns. The final sweep of a frame decided at max_iter skips its back-projection (q->skip_bwd:
+    // reference sartsolver_cuda.cpp:231-262 runs max_iter back-projections after the initial guess)
+    void sweep();
+    void refill();  // the plan, start values and pixel columns without a sweep (the first admissions)
     void set_device() const;
     // F = A X (Fs_ split-K partials); the bf16 engine first writes the X planes
     void forward();
@@ -95,7 +121,7 @@ class MultiFrameEngine {
     int nsf_ = 1, nsb_ = 1, nwb_ = 1;
     DeviceRaySums rs_;
     DeviceArray<float> X_, Xprev_, Fs_, W_, part_, buf_, pen_, O_, ghat_, arow_, gpos_, wo_;
-    DeviceArray<double> g64_, G64_, F2part_, x064_;
+    DeviceArray<double> G64_, F2part_, x064_;
     DeviceArray<bf16_t> Xh_, Xl_, Wh_, Wl_;  // bf16 / split-A engine: hi / lo operand planes
     // split-A back-projection on f16 pairs (launch_mf_backproject_h16): planes w1 | w2 ([2][nf][Pp] f16 bits),
     // per-frame max scratch and 1 / s_f, and the per-column power-of-two scales of the shard (csc_: [2][ld])
@@ -118,15 +144,29 @@ class MultiFrameEngine {
     hipStream_t comm_stream_ = nullptr;
     std::vector<hipEvent_t> cev_;
     hipEvent_t comm_done_ = nullptr;
-    MfState* hstate_ = nullptr;  // pinned [2]: state after each of the two chunks in flight
+    // device refill: queue (normalised pixels ghq_ [qcap][Pp], cold starts x0q_ / observed back-projections oq_
+    // [qcap][ld] when staged), output ring ring_ [rcap][ld], xlast_ [ld], and the plan state q_
+    int qcap_ = 32, rcap_ = 32, chunk_ = 4, admit_cap_ = 0, src_age_ = 0;
+    bool src_finished_ = false, lead_ = true;
+    double src_extrap_ = 0.0;
+    DeviceArray<MfQueue> q_;
+    DeviceArray<float> ghq_, x0q_, oq_, ring_, xlast_, starts_;
+    MfRefill rf_{};
+    std::vector<double> frame_norm_;  // the last series' normalisation per frame (solve_batch's starts)
+    struct Snap {
+        MfState st;
+        MfQueue q;
+    };
+    Snap* hsnap_ = nullptr;      // pinned [2]: state after each of the two chunks in flight
     hipEvent_t ev_[2] = {nullptr, nullptr};
-    double* hg_ = nullptr;       // pinned [k][rows] staging of the frames entering slots
-    float* hx_ = nullptr;        // pinned [nf][ld]: solutions of finished frames, per slot
-    hipEvent_t ev_copy_ = nullptr;
+    std::vector<double> hg_;     // [nf][rows] frames being staged (fp64, as read)
+    float* hq_ = nullptr;        // pinned [qcap][Pp]: normalised pixels of the queue (H2D source)
+    float* hx_ = nullptr;        // pinned [rcap][ld]: solutions of finished frames (D2H target)
+    hipStream_t copy_stream_ = nullptr;
+    hipEvent_t ev_copy_ = nullptr, ev_stage_ = nullptr;
     bool skip_last_bwd_ = true;  // SART_MF_LAST_BWD=1: run the final sweep's back-projection anyway (A/B)
-    int host_sweep_ = 0;         // sweeps queued in the current solve_batch (EngineConfig::fault_nan_sweep)
-    DeviceArray<float> Otmp_;    // log mode: observed back-projection of the frames entering slots
-    DeviceArray<float> xsrc_;    // [ld] copy of the finished frame that warm-starts a refill
+    int host_sweep_ = 0;         // sweeps queued in the current series (EngineConfig::fault_nan_sweep)
+    SeriesStats stats_;
 };
 
 }  // namespace sart

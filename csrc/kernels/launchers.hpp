@@ -296,21 +296,27 @@ void launch_mf_collect(const float* part, int nsplit, int64_t ld, int64_t v0, in
                        const double* F2part, int nF2, float* F2out, int nf, hipStream_t stream);
 void launch_mf_penalty(const int64_t* row_ptr, const int32_t* col, const float* val, int64_t n, float beta, bool logx,
                        const float* X, int64_t ld, float* pen, const MfState* st, int nf, hipStream_t stream);
-void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream);
-// Xprev (optional): receives X before the update (NaN/Inf guard rollback)
-void launch_mf_update(float* X, const float* D, const float* O, const float* pen, float alpha, bool logmode,
-                      int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream, float* Xprev = nullptr);
-// continuous batching (multiframe_glue.hip): new frames enter the slots listed in MfSlots between sweeps
-void launch_mf_prep_slots(const double* gk, int64_t nrows, int64_t nrows_pad, const MfSlots& sl, const float* ray_length,
-                          float len_thres, float* ghat, float* arow, float* gpos, float* wo, int nf, hipStream_t stream);
-void launch_mf_init_slots_warm(float* X, const double* x0, const MfSlots& sl, int64_t nvox, int64_t ld,
-                               hipStream_t stream);
-void launch_mf_init_slots_scaled(float* X, const float* xs, double s_src, const MfSlots& sl, int64_t nvox, int64_t ld,
-                                 hipStream_t stream);
-void launch_mf_init_slots_cold(float* X, const float* D0, const float* dinv, const MfSlots& sl, int64_t nvox,
-                               int64_t ld, int nf, hipStream_t stream);
-void launch_mf_copy_slots(float* O, const float* src, const MfSlots& sl, int64_t ld, int nf, hipStream_t stream);
-void launch_mf_slot_reset(MfState* st, const MfSlots& sl, hipStream_t stream);
+// q (optional): the device refill plan follows the decisions (mf_plan, MultiFrameEngine::solve_series)
+void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream, MfQueue* q = nullptr);
+// Xprev (optional): receives X before the update (NaN/Inf guard rollback). q / rf: the refill of this sweep's plan
+// (retired iterates into the ring, start values and log O of the admitted frames)
+void launch_mf_update(float* X, const float* D, float* O, const float* pen, float alpha, bool logmode,
+                      int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream, float* Xprev = nullptr,
+                      const MfQueue* q = nullptr, const MfRefill* rf = nullptr);
+// device refill: ghat / arow columns of the admitted frames from the staged pixels ghq [qcap][nrows_pad]
+void launch_mf_admit_rows(const MfQueue* q, const float* ghq, int64_t nrows, int64_t nrows_pad, const float* ray_length,
+                          float len_thres, float* ghat, float* arow, int nf, hipStream_t stream);
+// back-projection operands (gpos, and wo unless null) of k staged entries, columns j < k (layout of k_mf_prep_slots)
+void launch_mf_stage_ops(const float* ghq, int64_t e0, int qcap, int k, int64_t nrows, int64_t nrows_pad,
+                         const float* ray_length, float len_thres, float* gpos, float* wo, int nf, hipStream_t stream);
+// columns j < k of a reduced voxel-major D [ld][nf] into rows (e0 + j) % qcap of out [qcap][ld]: cold starts
+// max(D dinv, 1e-7) with dinv, else copies
+void launch_mf_stage_cols(const float* D, const float* dinv, int64_t e0, int qcap, int k, int64_t nvox, int64_t ld,
+                          int nf, float* out, hipStream_t stream);
+void launch_mf_publish(MfQueue* q, const MfPublish& p, hipStream_t stream);
+void launch_mf_drained(MfQueue* q, int64_t drained, hipStream_t stream);
+void launch_mf_queue_begin(MfQueue* q, int qcap, int rcap, bool chain, int admit_cap, int src_age, int64_t x0_below,
+                           bool src_finished, bool lead, float src_extrap, hipStream_t stream);
 void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, int max_iter, int nf,
                            hipStream_t stream);
 }  // namespace sart

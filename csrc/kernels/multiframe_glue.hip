@@ -164,16 +164,164 @@ __global__ __launch_bounds__(256) void k_mf_penalty(const int64_t* __restrict__ 
     pen[(int64_t)f * ld + r] = beta * s;
 }
 
+__device__ __forceinline__ unsigned long long mf_below(int lane) { return (1ull << lane) - 1ull; }
+
+// Device-side refill plan (k_mf_decide with a queue; one block of kMaxNF threads, thread f = slot f), after the
+// decisions of this sweep: sweep_new is the sweep counter after it, ran: some slot runs this sweep's update.
+// 1. Retire: every occupied slot whose frame is done gets the next output ring position while the ring has room
+//    (slot order), its MfFinish entry, and is emptied; the update kernel copies its iterate (X, or Xprev after a
+//    rollback) into the ring. The newest retired finite frame also replaces xlast (the device copy of the newest
+//    finished solution) when it is newer.
+// 2. Source (time series): the newest frame among the occupied finite slots (their iterate after this sweep's
+//    update; in flight with >= src_age updates, or finished) and xlast.
+// 3. Admit: empty slots (slot order) take queue entries [q_head, ...) up to the entries staged and admit_cap; each
+//    starts from the source rescaled to its own normalisation (else the host x0, its staged cold start, or 1e-7) with
+//    a fresh convergence history and sweep0 = sweep_new. The update kernel writes the start values (after reading
+//    every source), k_mf_admit_rows the pixel columns.
+// Everything depends on device state only (identical on every rank: it follows all-reduced sums), so all ranks
+// retire and admit the same frames at the same sweep.
+__device__ void mf_plan(MfState* __restrict__ st, MfQueue* __restrict__ q, int sweep_new, bool ran) {
+    __shared__ unsigned long long m_fin[kMaxNF / 64], m_free[kMaxNF / 64], m_run[kMaxNF / 64], m_max[kMaxNF / 64];
+    __shared__ int best, best_ret;
+    __shared__ int s_kind, s_slot, s_iter, s_live;
+    __shared__ double s_norm;
+    const int f = threadIdx.x, w = f >> 6, lane = f & 63;
+    const int nf = st->nf;
+    const bool in = f < nf;
+    const int fr = in ? q->slot_frame[f] : -1;
+    const bool occ = fr >= 0;
+    const bool dn = in ? st->done[f] != 0 : true;
+    const bool nonfin = in && ((st->flags[f >> 6] >> (f & 63)) & 1ull);
+    const bool rb = in && ((st->rollback[f >> 6] >> (f & 63)) & 1ull);
+    const int sw0 = in ? st->sweep0[f] : 0;
+    const int upd = sweep_new - sw0;  // updates applied to a running slot's iterate after this sweep
+    const bool finished = occ && dn;
+    if (f == 0) best = best_ret = -1, s_kind = kSrcNone, s_slot = -1, s_iter = -1, s_norm = 1.0, s_live = 0;
+    const unsigned long long bf = __ballot(finished);
+    if (lane == 0) m_fin[w] = bf;
+    __syncthreads();
+    const int64_t fin = q->fin;
+    const int room = q->rcap - (int)(fin - q->drained);
+    const int nfin = __popcll(m_fin[0]) + __popcll(m_fin[1]);
+    const int rank_fin = (w ? __popcll(m_fin[0]) : 0) + __popcll(m_fin[w] & mf_below(lane));
+    const bool retire = finished && rank_fin < room;
+    const int nret = nfin < room ? nfin : (room > 0 ? room : 0);
+    // source candidates: occupied finite slots (in flight: at least src_age updates) and xlast
+    if (q->chain && occ && !nonfin && (dn || (!q->src_finished && upd >= q->src_age))) atomicMax(&best, fr);
+    if (retire && !nonfin && fr > q->xlast_frame) atomicMax(&best_ret, fr);
+    const bool fre = in && (!occ || retire);
+    const unsigned long long bfree = __ballot(fre);
+    if (lane == 0) m_free[w] = bfree;
+    __syncthreads();
+    if (f == 0 && q->chain && q->xlast_frame > best && q->xlast_frame >= 0) {
+        best = q->xlast_frame;  // (xlast is older than every retiring finite frame it would be replaced by)
+        s_kind = kSrcLast, s_iter = q->xlast_iter, s_norm = q->xlast_norm;
+    }
+    __syncthreads();
+    if (occ && fr == best)
+        s_kind = kSrcSlot, s_slot = f, s_iter = dn ? st->iters[f] : upd, s_norm = q->slot_norm[f], s_live = dn ? 0 : 1;
+    const bool xl = retire && fr == best_ret;
+    const int xlast_iter = xl ? st->iters[f] : 0;
+    const double xlast_norm = xl ? q->slot_norm[f] : 0.0;
+    __syncthreads();  // every read of this slot's old state and of the source is done
+    if (retire) {
+        const int pos = (int)((fin + rank_fin) % q->rcap);
+        MfFinish& L = q->log[pos];
+        L.frame = fr;
+        L.status = st->status[f] == kSuccess ? kSuccess : kMaxIterationsExceeded;
+        L.iters = st->iters[f];
+        L.flags = (nonfin ? 1 : 0) | (rb ? 2 : 0);
+        L.warm_from = q->slot_warm_from[f];
+        L.warm_iter = q->slot_warm_iter[f];
+        L.conv = st->conv[f];
+        L.norm = q->slot_norm[f];
+        q->ret_pos[f] = pos;
+        q->ret_prev[f] = rb ? 1 : 0;
+        q->slot_frame[f] = -1;
+    } else if (in) {
+        q->ret_pos[f] = -1;
+    }
+    if (xl) {
+        q->xlast_slot = f;
+        q->xlast_frame = fr;
+        q->xlast_iter = xlast_iter;
+        q->xlast_norm = xlast_norm;
+    }
+    const int64_t avail = q->q_tail - q->q_head;
+    const int nfree = __popcll(m_free[0]) + __popcll(m_free[1]);
+    int nadm = nfree;
+    if (q->admit_cap > 0 && nadm > q->admit_cap) nadm = q->admit_cap;
+    // lead: before any frame has finished finite, one frame runs alone (its cold start converges first; frames
+    // chained from its young iterates would all inherit the cold start's error: a transient of ~100 frames)
+    if (q->lead && best_ret < 0 && q->xlast_frame < 0) nadm = (nfree == nf && nadm > 0) ? 1 : 0;
+    if ((int64_t)nadm > avail) nadm = (int)avail;
+    const int rank_free = (w ? __popcll(m_free[0]) : 0) + __popcll(m_free[w] & mf_below(lane));
+    const bool adm = fre && rank_free < nadm;
+    if (adm) {
+        const int pos = (int)((q->q_head + rank_free) % q->qcap);
+        const int frame = q->q_frame[pos];
+        int kind = kSrcNone;
+        if (q->chain && s_kind != kSrcNone) kind = s_kind;
+        else if ((int64_t)frame < q->x0_below) kind = kSrcHostX0;
+        else if (q->q_cold[pos]) kind = kSrcCold;
+        q->adm_pos[f] = pos;
+        q->adm_kind[f] = kind;
+        q->slot_frame[f] = frame;
+        q->slot_norm[f] = q->q_norm[pos];
+        const bool chained = kind == kSrcSlot || kind == kSrcLast;
+        q->slot_warm_from[f] = chained ? best : -1;
+        q->slot_warm_iter[f] = chained ? s_iter : -1;
+        st->G[f] = q->q_G[pos];
+        st->conv_prev[f] = 0.0;
+        st->conv[f] = 0.0;
+        st->done[f] = 0;
+        st->status[f] = kMaxIterationsExceeded;
+        st->iters[f] = st->max_iter;
+        st->sweep0[f] = sweep_new;
+        atomicAnd(&st->flags[f >> 6], ~(1ull << (f & 63)));
+        atomicAnd(&st->rollback[f >> 6], ~(1ull << (f & 63)));
+    } else if (in) {
+        q->adm_pos[f] = -1;
+    }
+    // the next sweep: slots that run it, and whether every one of them is decided at max_iter there (then that
+    // sweep's back-projection and update would be discarded: only its forward and ||A x||^2 are used)
+    const bool run_next = adm || (occ && !dn);
+    const bool at_max = run_next && !adm && sweep_new - sw0 >= st->max_iter;
+    const unsigned long long br = __ballot(run_next), bm = __ballot(at_max);
+    if (lane == 0) m_run[w] = br, m_max[w] = bm;
+    __syncthreads();
+    if (f == 0) {
+        const int nrun = __popcll(m_run[0]) + __popcll(m_run[1]);
+        const int nmax = __popcll(m_max[0]) + __popcll(m_max[1]);
+        q->fin = fin + nret;
+        q->q_head += nadm;
+        q->n_ret = nret;
+        q->n_adm = nadm;
+        q->upd_any = ran ? 1 : 0;
+        q->src_kind = s_kind;
+        q->src_slot = s_slot;
+        q->src_frame = best;
+        q->src_iter = s_iter;
+        q->src_norm = s_norm;
+        q->src_live = s_live;
+        if (best_ret < 0) q->xlast_slot = -1;
+        st->all_done = nrun == 0 ? 1 : 0;
+        q->skip_bwd = (nrun == 0 || nmax == nrun) ? 1 : 0;
+    }
+}
+
 // Per-frame decision of sweep s (same rule as k_decide): conv_f = (G_f - F2_f) / G_f; a frame converges
-// when s >= 2 and |conv_f - conv_prev_f| < tol; frames done earlier keep their conv_prev.
-__global__ void k_mf_decide(MfState* __restrict__ st, const float* __restrict__ F2) {
+// when s >= 2 and |conv_f - conv_prev_f| < tol; frames done earlier keep their conv_prev. With a queue (device
+// refill) the refill plan follows (mf_plan); it also runs when every slot is done (no decision, no sweep counted).
+__global__ void k_mf_decide(MfState* __restrict__ st, const float* __restrict__ F2, MfQueue* __restrict__ q) {
     __shared__ int alld;
     const int f = threadIdx.x;
-    if (st->all_done) return;
+    const bool active = !st->all_done;
+    if (!active && !q) return;
     const int s = st->sweep;
     if (f == 0) alld = 1;
     __syncthreads();
-    if (f < st->nf) {
+    if (active && f < st->nf) {
         const double F = (double)F2[f];
         const int sf = s - st->sweep0[f];  // this frame's own sweep (continuous batching refills slots)
         int done = st->done[f];
@@ -200,10 +348,15 @@ __global__ void k_mf_decide(MfState* __restrict__ st, const float* __restrict__ 
         if (!done) atomicAnd(&alld, 0);
     }
     __syncthreads();
-    if (f == 0) {
-        st->all_done = alld ? 1 : 0;
-        st->sweep = s + 1;
+    if (!q) {
+        if (f == 0) {
+            st->all_done = alld ? 1 : 0;
+            st->sweep = s + 1;
+        }
+        return;
     }
+    if (active && f == 0) st->sweep = s + 1;
+    mf_plan(st, q, active ? s + 1 : s, active && !alld);
 }
 
 // Update of the frames that are still running (after the decision of this sweep). D and O are voxel-major
@@ -211,20 +364,27 @@ __global__ void k_mf_decide(MfState* __restrict__ st, const float* __restrict__ 
 // 64-voxel tile of D (and O) through LDS so both sides stay coalesced. Xprev (optional) receives the
 // iterate before the update: the rollback point of the NaN/Inf guard.
 // TN: LDS tile columns (64, or 128 for 128-frame batches; the narrower tile keeps 4 blocks per CU at <= 64 frames)
+// With a queue (device refill, mf_plan) the same block then, for its 64 voxels: copies the iterates of the frames
+// retired at this sweep into the output ring (and xlast), computes the start values of the admitted frames from
+// their sources (after the update: a source is the iterate after this sweep), and writes them after a barrier,
+// since a retiring slot may be both a source and re-admitted. Log mode: the admitted frames' staged O columns.
 template <int TN>
 __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const float* __restrict__ D,
-                                                   const float* __restrict__ O, const float* __restrict__ pen,
+                                                   float* __restrict__ O, const float* __restrict__ pen,
                                                    float alpha, int logmode, int64_t nvox, int64_t ld,
-                                                   const MfState* __restrict__ st, float* __restrict__ Xprev) {
+                                                   const MfState* __restrict__ st, float* __restrict__ Xprev,
+                                                   const MfQueue* __restrict__ q, MfRefill rf) {
     __shared__ float dt[64][TN + 1];
     __shared__ float ot[64][TN + 1];
-    if (st->all_done) return;
+    const bool refill = q && (q->n_ret || q->n_adm || q->xlast_slot >= 0);
+    if (q ? (!q->upd_any && !refill) : st->all_done) return;
     const int nf = st->nf;  // 16 .. 128 (<= TN): four consecutive e of a voxel-major row share one voxel
     const int64_t v0 = (int64_t)blockIdx.x * 64;  // v0 + 63 < ld (ld % 64 == 0, grid ld / 64)
     // float4 accesses throughout (D, O: the block's 64 nf contiguous floats; X, Xprev, pen: 4 voxels of one frame)
     const float4* D4 = reinterpret_cast<const float4*>(D + v0 * nf);
     const float4* O4 = logmode ? reinterpret_cast<const float4*>(O + v0 * nf) : nullptr;
-    for (int e4 = threadIdx.x; e4 < 16 * nf; e4 += 256) {
+    const bool upd = !q || q->upd_any;
+    for (int e4 = threadIdx.x; upd && e4 < 16 * nf; e4 += 256) {
         const int r = (4 * e4) / nf, c = (4 * e4) % nf;
         const float4 d = D4[e4];
         dt[r][c] = d.x, dt[r][c + 1] = d.y, dt[r][c + 2] = d.z, dt[r][c + 3] = d.w;
@@ -234,10 +394,10 @@ __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const 
         }
     }
     __syncthreads();
-    for (int e4 = threadIdx.x; e4 < 16 * nf; e4 += 256) {
+    for (int e4 = threadIdx.x; upd && e4 < 16 * nf; e4 += 256) {
         const int f = e4 / 16, vq = 4 * (e4 % 16);
         const int64_t v = v0 + vq;
-        if (v >= nvox || st->done[f]) continue;
+        if (v >= nvox || st->done[f] || (q && q->adm_pos[f] >= 0)) continue;  // (a slot admitted now: its new frame)
         const int64_t i = (int64_t)f * ld + v;
         const int m = nvox - v < 4 ? (int)(nvox - v) : 4;  // voxels of this quad inside the shard
         const float4 x4 = *reinterpret_cast<const float4*>(X + i);
@@ -266,6 +426,66 @@ __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const 
                 X[i + k] = out[k];
             }
         }
+    }
+    if (!refill) return;
+    __syncthreads();  // this block's updated iterates are visible to the whole block
+    // retired frames into the output ring (and the newest finite one into xlast); start values of the admissions
+    constexpr int kMaxQ = 16 * TN / 256;
+    float4 nv[kMaxQ];
+    const int src_kind = q->src_kind, src_slot = q->src_slot;
+    const double src_norm = q->src_norm;
+    // an in-flight source extrapolated along its last update (linear mode): x + c (x - x_prev)
+    const float cx = (q->src_live && !logmode) ? q->src_extrap : 0.f;
+#pragma unroll
+    for (int k = 0; k < kMaxQ; ++k) {
+        const int e4 = threadIdx.x + 256 * k;
+        if (e4 >= 16 * nf) break;
+        const int f = e4 / 16;
+        const int64_t v = v0 + 4 * (e4 % 16);
+        const int rp = q->ret_pos[f];
+        if (rp >= 0 || f == q->xlast_slot) {
+            const float4 val = *reinterpret_cast<const float4*>((rp >= 0 && q->ret_prev[f] ? Xprev : X) + f * ld + v);
+            if (rp >= 0) *reinterpret_cast<float4*>(rf.ring + rp * ld + v) = val;
+            if (f == q->xlast_slot) *reinterpret_cast<float4*>(rf.xlast + v) = val;
+        }
+        const int ap = q->adm_pos[f];
+        if (ap < 0) continue;
+        const int kind = q->adm_kind[f];
+        const double s_new = q->slot_norm[f];
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t vv = v + j;
+            float x = 0.f;
+            if (vv < nvox) {
+                if (kind == kSrcSlot) {
+                    float xs = X[src_slot * ld + vv];
+                    if (cx != 0.f) xs = fmaf(cx, xs - Xprev[src_slot * ld + vv], xs);
+                    x = (float)((double)xs * src_norm / s_new);
+                }
+                else if (kind == kSrcLast)
+                    x = (float)((double)rf.xlast[vv] * src_norm / s_new);
+                else if (kind == kSrcHostX0)
+                    x = (float)(rf.x0[vv] / s_new);
+                else if (kind == kSrcCold)
+                    x = rf.x0q[ap * ld + vv];
+                x = x > 1e-7f ? x : 1e-7f;  // (reference sartsolver_cuda.cpp:176-180)
+            }
+            o[j] = x;
+            if (logmode) O[vv * nf + f] = rf.oq[ap * ld + vv];  // the frame's observed back-projection (staged)
+        }
+        nv[k] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+    __syncthreads();  // every source read: the admitted slots may be overwritten (a retiring slot can be both)
+#pragma unroll
+    for (int k = 0; k < kMaxQ; ++k) {
+        const int e4 = threadIdx.x + 256 * k;
+        if (e4 >= 16 * nf) break;
+        const int f = e4 / 16;
+        const int64_t v = v0 + 4 * (e4 % 16);
+        if (q->adm_pos[f] < 0) continue;
+        *reinterpret_cast<float4*>(X + f * ld + v) = nv[k];
+        if (rf.starts) *reinterpret_cast<float4*>(rf.starts + (int64_t)q->slot_frame[f] * ld + v) = nv[k];
     }
 }
 
@@ -370,110 +590,120 @@ __global__ __launch_bounds__(256) void k_mf_split_w(const float* __restrict__ W,
     }
 }
 
-// ---- continuous batching: frames enter freed slots between sweeps (MultiFrameEngine::solve_batch)
+// ---- device-side refill (MultiFrameEngine::solve_series; plan in mf_plan)
 
-// Per-slot prep of k new frames from a compact frame-major staging gk [k][rows] (non-finite pixels already
-// -1): the columns `slot` of ghat / arow ([rows][nf]) and of gpos / wo (back-projection layout).
-__global__ __launch_bounds__(256) void k_mf_prep_slots(const double* __restrict__ gk, int64_t nrows, int64_t nrows_pad,
-                                                       MfSlots sl, const float* __restrict__ ray_length,
-                                                       float len_thres, float* __restrict__ ghat,
-                                                       float* __restrict__ arow, float* __restrict__ gpos,
-                                                       float* __restrict__ wo, int nf) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // element of [k][rows_pad]
-    if (i >= (int64_t)sl.n * nrows_pad) return;
-    const int q = (int)(i / nrows_pad);
-    const int64_t row = i % nrows_pad;
-    const int f = sl.slot[q];
-    float gh = 0.f, a = 0.f;
-    if (row < nrows) {
-        gh = (float)(gk[(int64_t)q * nrows + row] / sl.norm[q]);
-        const float len = ray_length[row];
-        const float inv_len = (len > len_thres) ? 1.f / len : 0.f;
-        a = (gh >= 0.f) ? inv_len : 0.f;
-    }
-    ghat[row * nf + f] = gh;
-    arow[row * nf + f] = a;
-    const int64_t ib = row * nf + mf_bp_slot(f, nf);
-    gpos[ib] = gh > 0.f ? gh : 0.f;
-    wo[ib] = a * gh;
-}
-
-// Warm start of the new frames from one (de-normalised, fp64) solution x0: X[slot][v] = max(x0[v] / s, 1e-7).
-__global__ __launch_bounds__(256) void k_mf_init_slots_warm(float* __restrict__ X, const double* __restrict__ x0,
-                                                            MfSlots sl, int64_t nvox, int64_t ld) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)sl.n * ld) return;
-    const int q = (int)(i / ld);
-    const int64_t v = i % ld;
-    float x = 0.f;
-    if (v < nvox) {
-        x = (float)(x0[v] / sl.norm[q]);
-        x = x > 1e-7f ? x : 1e-7f;
-    }
-    X[(int64_t)sl.slot[q] * ld + v] = x;
-}
-
-// Warm start of the new frames from the normalised solution xs of a frame that just finished in another slot
-// (still on the device): x_prev = xs * s_src, then X[slot][v] = max(x_prev / s, 1e-7) -- the same fp64
-// arithmetic as the host path (solution = X * s, then x0 / s).
-__global__ __launch_bounds__(256) void k_mf_init_slots_scaled(float* __restrict__ X, const float* __restrict__ xs,
-                                                              double s_src, MfSlots sl, int64_t nvox, int64_t ld) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)sl.n * ld) return;
-    const int q = (int)(i / ld);
-    const int64_t v = i % ld;
-    float x = 0.f;
-    if (v < nvox) {
-        x = (float)((double)xs[v] * s_src / sl.norm[q]);
-        x = x > 1e-7f ? x : 1e-7f;
-    }
-    X[(int64_t)sl.slot[q] * ld + v] = x;
-}
-
-// Cold start of the new frames: X[slot][v] = max(D0[v][slot] * dinv[v], 1e-7) (D0 voxel-major, reduced).
-__global__ __launch_bounds__(256) void k_mf_init_slots_cold(float* __restrict__ X, const float* __restrict__ D0,
-                                                            const float* __restrict__ dinv, MfSlots sl, int64_t nvox,
-                                                            int64_t ld, int nf) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)sl.n * ld) return;
-    const int q = (int)(i / ld);
-    const int64_t v = i % ld;
-    const int f = sl.slot[q];
-    float x = 0.f;
-    if (v < nvox) {
-        x = D0[v * nf + f] * dinv[v];
-        x = x > 1e-7f ? x : 1e-7f;
-    }
-    X[(int64_t)f * ld + v] = x;
-}
-
-// O[v][slot] = src[v][slot] for the new frames' columns (the frame-constant observed back-projection, log mode).
-__global__ __launch_bounds__(256) void k_mf_copy_slots(float* __restrict__ O, const float* __restrict__ src, MfSlots sl,
-                                                       int64_t ld, int nf) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)sl.n * ld) return;
-    const int f = sl.slot[(int)(i / ld)];
-    const int64_t v = i % ld;
-    O[v * nf + f] = src[v * nf + f];
-}
-
-// The new frames' state: fresh convergence history, sweep count from the current sweep.
-__global__ void k_mf_slot_reset(MfState* __restrict__ st, MfSlots sl) {
-    const int q = threadIdx.x;
-    if (q < sl.n) {
-        const int f = sl.slot[q];
-        st->G[f] = sl.G[q];
-        st->conv_prev[f] = 0.0;
-        st->conv[f] = 0.0;
-        st->done[f] = 0;
-        st->status[f] = kMaxIterationsExceeded;
-        st->iters[f] = st->max_iter;
-        st->sweep0[f] = st->sweep;
-        atomicAnd(&st->flags[f >> 6], ~(1ull << (f & 63)));
-        atomicAnd(&st->rollback[f >> 6], ~(1ull << (f & 63)));
+// The pixel columns of the frames admitted at this sweep: ghat / arow [rows][nf] from the staged normalised pixels
+// ghq [qcap][rows_pad] (same arithmetic as k_mf_prep_slots: a = 1 / ray length above the threshold where ghat >= 0).
+__global__ __launch_bounds__(256) void k_mf_admit_rows(const MfQueue* __restrict__ q, const float* __restrict__ ghq,
+                                                       int64_t nrows, int64_t nrows_pad,
+                                                       const float* __restrict__ ray_length, float len_thres,
+                                                       float* __restrict__ ghat, float* __restrict__ arow, int nf) {
+    if (q->n_adm == 0) return;
+    __shared__ int lf[kMaxNF], lp[kMaxNF];
+    __shared__ int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    if (threadIdx.x < nf) {
+        const int p = q->adm_pos[threadIdx.x];
+        if (p >= 0) {
+            const int j = atomicAdd(&cnt, 1);
+            lf[j] = threadIdx.x, lp[j] = p;
+        }
     }
     __syncthreads();
-    if (q == 0 && sl.n > 0) st->all_done = 0;
+    const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (row >= nrows_pad) return;
+    float inv_len = 0.f;
+    if (row < nrows) {
+        const float len = ray_length[row];
+        inv_len = (len > len_thres) ? 1.f / len : 0.f;
+    }
+    for (int j = 0; j < cnt; ++j) {
+        const float gh = row < nrows ? ghq[(int64_t)lp[j] * nrows_pad + row] : 0.f;
+        ghat[row * nf + lf[j]] = gh;
+        arow[row * nf + lf[j]] = (row < nrows && gh >= 0.f) ? inv_len : 0.f;
+    }
+}
+
+// Back-projection operands of k staged entries (positions (e0 + j) % qcap, j < k) in the back-projection layout of
+// columns j: gpos = max(ghat, 0) (the cold start), wo = a ghat (the observed back-projection, log mode); columns
+// j >= k zero.
+__global__ __launch_bounds__(256) void k_mf_stage_ops(const float* __restrict__ ghq, int64_t e0, int qcap, int k,
+                                                      int64_t nrows, int64_t nrows_pad,
+                                                      const float* __restrict__ ray_length, float len_thres,
+                                                      float* __restrict__ gpos, float* __restrict__ wo, int nf) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // element of [rows_pad][nf]
+    if (i >= nrows_pad * nf) return;
+    const int64_t row = i / nf;
+    const int j = (int)(i % nf);
+    float gh = 0.f, a = 0.f;
+    if (j < k && row < nrows) {
+        gh = ghq[((e0 + j) % qcap) * nrows_pad + row];
+        const float len = ray_length[row];
+        a = (gh >= 0.f && len > len_thres) ? 1.f / len : 0.f;
+    }
+    const int64_t ib = row * nf + mf_bp_slot(j, nf);
+    gpos[ib] = gh > 0.f ? gh : 0.f;
+    if (wo) wo[ib] = a * gh;
+}
+
+// Staged columns j < k of a reduced voxel-major D [ld][nf] into queue rows (e0 + j) % qcap of out [qcap][ld]:
+// cold: max(D * dinv, 1e-7) (k_mf_init_slots_cold's arithmetic; 0 past nvox), else a copy (log O).
+__global__ __launch_bounds__(256) void k_mf_stage_cols(const float* __restrict__ D, const float* __restrict__ dinv,
+                                                       int64_t e0, int qcap, int k, int64_t nvox, int64_t ld, int nf,
+                                                       float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // element of [k][ld]
+    if (i >= (int64_t)k * ld) return;
+    const int j = (int)(i / ld);
+    const int64_t v = i % ld;
+    float x = D[v * nf + j];
+    if (dinv) {
+        x = v < nvox ? x * dinv[v] : 0.f;
+        if (v < nvox) x = x > 1e-7f ? x : 1e-7f;
+    }
+    out[((e0 + j) % qcap) * ld + v] = x;
+}
+
+// Entries [e0, e0 + n) become visible to the plan: their metadata, then q_tail.
+__global__ void k_mf_publish(MfQueue* __restrict__ q, MfPublish p) {
+    const int j = threadIdx.x;
+    if (j < p.n) {
+        const int pos = (int)((p.e0 + j) % q->qcap);
+        q->q_frame[pos] = p.frame[j];
+        q->q_cold[pos] = p.cold[j];
+        q->q_norm[pos] = p.norm[j];
+        q->q_G[pos] = p.G[j];
+    }
+    __syncthreads();
+    if (j == 0) q->q_tail = p.e0 + p.n;
+}
+
+__global__ void k_mf_drained(MfQueue* __restrict__ q, int64_t drained) {
+    if (threadIdx.x == 0 && drained > q->drained) q->drained = drained;
+}
+
+__global__ void k_mf_queue_begin(MfQueue* __restrict__ q, int qcap, int rcap, int chain, int admit_cap, int src_age,
+                                 int64_t x0_below, int src_finished, int lead, float src_extrap) {
+    const int f = threadIdx.x;
+    if (f < kMaxNF) {
+        q->slot_frame[f] = -1;
+        q->slot_warm_from[f] = q->slot_warm_iter[f] = -1;
+        q->slot_norm[f] = 1.0;
+        q->ret_pos[f] = q->adm_pos[f] = -1;
+        q->ret_prev[f] = 0;
+        q->adm_kind[f] = kSrcNone;
+    }
+    if (f == 0) {
+        q->q_head = q->q_tail = q->fin = q->drained = 0;
+        q->qcap = qcap, q->rcap = rcap;
+        q->chain = chain, q->admit_cap = admit_cap, q->src_age = src_age, q->x0_below = x0_below;
+        q->src_finished = src_finished, q->lead = lead, q->src_extrap = src_extrap, q->src_live = 0;
+        q->n_ret = q->n_adm = q->upd_any = q->skip_bwd = 0;
+        q->xlast_frame = q->xlast_iter = q->xlast_slot = -1;
+        q->xlast_norm = 1.0;
+        q->src_kind = kSrcNone, q->src_slot = q->src_frame = q->src_iter = -1;
+        q->src_norm = 1.0;
+    }
 }
 
 static inline unsigned nb(int64_t n) { return (unsigned)((n + 255) / 256); }
@@ -517,18 +747,71 @@ void launch_mf_penalty(const int64_t* row_ptr, const int32_t* col, const float* 
     check_launch("k_mf_penalty");
 }
 
-void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream) {
-    hipLaunchKernelGGL(k_mf_decide, dim3(1), dim3(kMaxNF), 0, stream, st, F2);
+void launch_mf_decide(MfState* st, const float* F2, hipStream_t stream, MfQueue* q) {
+    hipLaunchKernelGGL(k_mf_decide, dim3(1), dim3(kMaxNF), 0, stream, st, F2, q);
     check_launch("k_mf_decide");
 }
 
-void launch_mf_update(float* X, const float* D, const float* O, const float* pen, float alpha, bool logmode,
-                      int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream, float* Xprev) {
+void launch_mf_update(float* X, const float* D, float* O, const float* pen, float alpha, bool logmode,
+                      int64_t nvox, int64_t ld, const MfState* st, int nf, hipStream_t stream, float* Xprev,
+                      const MfQueue* q, const MfRefill* rf) {
     check_nf(nf, "mf_update");
+    if (q && (!rf || !rf->ring || !rf->xlast || (logmode && !rf->oq)))
+        throw std::runtime_error("mf_update: a refill needs the output ring, xlast and (log) the staged O");
+    const MfRefill r = rf ? *rf : MfRefill{};
     hipLaunchKernelGGL((nf > 64 ? k_mf_update<128> : k_mf_update<64>), dim3((unsigned)((ld + 63) / 64)), dim3(256), 0,
                        stream, X, D, O, pen, alpha,
-                       logmode ? 1 : 0, nvox, ld, st, Xprev);
+                       logmode ? 1 : 0, nvox, ld, st, Xprev, q, r);
     check_launch("k_mf_update");
+}
+
+void launch_mf_admit_rows(const MfQueue* q, const float* ghq, int64_t nrows, int64_t nrows_pad, const float* ray_length,
+                          float len_thres, float* ghat, float* arow, int nf, hipStream_t stream) {
+    check_nf(nf, "mf_admit_rows");
+    if (nrows_pad <= 0) return;
+    hipLaunchKernelGGL(k_mf_admit_rows, dim3(nb(nrows_pad)), dim3(256), 0, stream, q, ghq, nrows, nrows_pad, ray_length,
+                       len_thres, ghat, arow, nf);
+    check_launch("k_mf_admit_rows");
+}
+
+void launch_mf_stage_ops(const float* ghq, int64_t e0, int qcap, int k, int64_t nrows, int64_t nrows_pad,
+                         const float* ray_length, float len_thres, float* gpos, float* wo, int nf, hipStream_t stream) {
+    check_nf(nf, "mf_stage_ops");
+    if (k < 0 || k > nf || qcap < k) throw std::runtime_error("mf_stage_ops: 0 <= k <= nf, k <= qcap");
+    if (nrows_pad <= 0) return;
+    hipLaunchKernelGGL(k_mf_stage_ops, dim3(nb(nrows_pad * nf)), dim3(256), 0, stream, ghq, e0, qcap, k, nrows,
+                       nrows_pad, ray_length, len_thres, gpos, wo, nf);
+    check_launch("k_mf_stage_ops");
+}
+
+void launch_mf_stage_cols(const float* D, const float* dinv, int64_t e0, int qcap, int k, int64_t nvox, int64_t ld,
+                          int nf, float* out, hipStream_t stream) {
+    check_nf(nf, "mf_stage_cols");
+    if (k < 0 || k > nf || qcap < k) throw std::runtime_error("mf_stage_cols: 0 <= k <= nf, k <= qcap");
+    if (k == 0) return;
+    hipLaunchKernelGGL(k_mf_stage_cols, dim3(nb((int64_t)k * ld)), dim3(256), 0, stream, D, dinv, e0, qcap, k, nvox, ld,
+                       nf, out);
+    check_launch("k_mf_stage_cols");
+}
+
+void launch_mf_publish(MfQueue* q, const MfPublish& p, hipStream_t stream) {
+    if (p.n < 0 || p.n > kMaxNF) throw std::runtime_error("mf_publish: at most 128 entries per call");
+    hipLaunchKernelGGL(k_mf_publish, dim3(1), dim3(kMaxNF), 0, stream, q, p);
+    check_launch("k_mf_publish");
+}
+
+void launch_mf_drained(MfQueue* q, int64_t drained, hipStream_t stream) {
+    hipLaunchKernelGGL(k_mf_drained, dim3(1), dim3(64), 0, stream, q, drained);
+    check_launch("k_mf_drained");
+}
+
+void launch_mf_queue_begin(MfQueue* q, int qcap, int rcap, bool chain, int admit_cap, int src_age, int64_t x0_below,
+                           bool src_finished, bool lead, float src_extrap, hipStream_t stream) {
+    if (qcap < 1 || qcap > kMfQueueMax || rcap < 1 || rcap > kMfQueueMax)
+        throw std::runtime_error("mf_queue_begin: queue and ring capacities in [1, 256]");
+    hipLaunchKernelGGL(k_mf_queue_begin, dim3(1), dim3(kMaxNF), 0, stream, q, qcap, rcap, chain ? 1 : 0, admit_cap,
+                       src_age, x0_below, src_finished ? 1 : 0, lead ? 1 : 0, src_extrap);
+    check_launch("k_mf_queue_begin");
 }
 
 void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, int max_iter, int nf,
@@ -842,48 +1125,5 @@ void launch_mf_split_w(const float* W, int64_t nrows_pad, int nf, int64_t ldw, b
     check_launch("k_mf_split_w");
 }
 
-void launch_mf_prep_slots(const double* gk, int64_t nrows, int64_t nrows_pad, const MfSlots& sl, const float* ray_length,
-                          float len_thres, float* ghat, float* arow, float* gpos, float* wo, int nf, hipStream_t stream) {
-    check_nf(nf, "mf_prep_slots");
-    if (sl.n <= 0) return;
-    hipLaunchKernelGGL(k_mf_prep_slots, dim3(nb((int64_t)sl.n * nrows_pad)), dim3(256), 0, stream, gk, nrows, nrows_pad,
-                       sl, ray_length, len_thres, ghat, arow, gpos, wo, nf);
-    check_launch("k_mf_prep_slots");
-}
-
-void launch_mf_init_slots_warm(float* X, const double* x0, const MfSlots& sl, int64_t nvox, int64_t ld,
-                               hipStream_t stream) {
-    if (sl.n <= 0) return;
-    hipLaunchKernelGGL(k_mf_init_slots_warm, dim3(nb((int64_t)sl.n * ld)), dim3(256), 0, stream, X, x0, sl, nvox, ld);
-    check_launch("k_mf_init_slots_warm");
-}
-
-void launch_mf_init_slots_scaled(float* X, const float* xs, double s_src, const MfSlots& sl, int64_t nvox, int64_t ld,
-                                 hipStream_t stream) {
-    if (sl.n <= 0) return;
-    hipLaunchKernelGGL(k_mf_init_slots_scaled, dim3(nb((int64_t)sl.n * ld)), dim3(256), 0, stream, X, xs, s_src, sl,
-                       nvox, ld);
-    check_launch("k_mf_init_slots_scaled");
-}
-
-void launch_mf_init_slots_cold(float* X, const float* D0, const float* dinv, const MfSlots& sl, int64_t nvox,
-                               int64_t ld, int nf, hipStream_t stream) {
-    if (sl.n <= 0) return;
-    hipLaunchKernelGGL(k_mf_init_slots_cold, dim3(nb((int64_t)sl.n * ld)), dim3(256), 0, stream, X, D0, dinv, sl, nvox,
-                       ld, nf);
-    check_launch("k_mf_init_slots_cold");
-}
-
-void launch_mf_copy_slots(float* O, const float* src, const MfSlots& sl, int64_t ld, int nf, hipStream_t stream) {
-    if (sl.n <= 0) return;
-    hipLaunchKernelGGL(k_mf_copy_slots, dim3(nb((int64_t)sl.n * ld)), dim3(256), 0, stream, O, src, sl, ld, nf);
-    check_launch("k_mf_copy_slots");
-}
-
-void launch_mf_slot_reset(MfState* st, const MfSlots& sl, hipStream_t stream) {
-    if (sl.n <= 0) return;
-    hipLaunchKernelGGL(k_mf_slot_reset, dim3(1), dim3(kMaxNF), 0, stream, st, sl);
-    check_launch("k_mf_slot_reset");
-}
 
 }  // namespace sart

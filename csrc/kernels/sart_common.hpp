@@ -62,12 +62,71 @@ struct alignas(16) MfState {
     int32_t sweep0[kMfMaxFrames];    // sweep at which the slot's current frame started (continuous batching)
 };
 
-// Slots (re)filled with new frames between two sweeps of the multi-frame engine: passed by value.
-struct MfSlots {
+// ---- device-side slot refill (MultiFrameEngine::solve_series) ----
+// The host stages frames into a device queue (normalised pixels, scalars; cold starts / observed back-projections
+// where needed) ahead of the sweeps; the decision kernel of every sweep retires the frames that finished (their
+// solutions into an output ring the host drains) and admits queued frames into the freed slots in the SAME sweep,
+// each starting from the current iterate of the newest frame in flight (a time series) -- no host round trip
+// between a frame finishing and its slot working on the next one.
+constexpr int kMfQueueMax = 2 * kMfMaxFrames;  // queue entries / output ring entries (2 nf)
+enum MfSrc : int32_t {
+    kSrcNone = 0,     // no start value known: x = 1e-7 (only when every earlier frame went non-finite)
+    kSrcSlot = 1,     // the iterate of a slot after this sweep's update (in flight, or finished at this sweep)
+    kSrcLast = 2,     // the newest finished frame's solution kept on the device (MfQueue::xlast_*)
+    kSrcHostX0 = 3,   // the caller's start value (fp64, de-normalised)
+    kSrcCold = 4,     // the entry's staged cold start max(A^T max(ghat, 0) / rho, 1e-7)
+};
+struct MfFinish {      // one finished frame in the output ring (read by the host from the state snapshot)
+    int32_t frame, status, iters, flags;  // flags: bit 0 non-finite, bit 1 rolled back to the last finite iterate
+    int32_t warm_from, warm_iter;         // the start value's frame and its update count (-1: x0 / cold)
+    double conv, norm;
+};
+struct alignas(16) MfQueue {
+    int64_t q_head, q_tail;  // staged entries [q_head, q_tail) (entry e at ring position e % qcap)
+    int64_t fin, drained;    // frames written to the output ring / copied out by the host (position fin % rcap)
+    int32_t qcap, rcap;
+    int32_t chain;        // admitted frames start from the newest frame in flight (time series)
+    int32_t admit_cap;    // admissions per sweep (0: any number)
+    int32_t src_age;      // an in-flight source needs at least this many updates
+    int32_t src_finished; // sources: finished frames only (xlast and the frames retiring now), not frames in flight
+    int32_t lead;         // chain without x0: the first frame runs alone until it has finished (a converged source)
+    float src_extrap;     // linear mode: an in-flight source's iterate is extrapolated, x + c (x - x_prev)
+    int32_t src_live;     // this sweep's source is in flight (its Xprev is the iterate before this sweep's update)
+    int64_t x0_below;     // frames below this index start from the host x0 when no chain source exists (!chain: always)
+    int32_t n_ret, n_adm, upd_any, skip_bwd;  // this sweep's plan; skip_bwd: the next sweep's back-projection is unused
+    int32_t xlast_frame, xlast_iter, xlast_slot, pad0;  // xlast_slot: the slot copied into xlast at this sweep (-1)
+    double xlast_norm;
+    int32_t src_kind, src_slot, src_frame, src_iter;  // the chain source of this sweep's admissions
+    double src_norm;
+    int32_t slot_frame[kMfMaxFrames];  // frame in each slot (-1: empty)
+    int32_t slot_warm_from[kMfMaxFrames], slot_warm_iter[kMfMaxFrames];
+    double slot_norm[kMfMaxFrames];
+    int32_t ret_pos[kMfMaxFrames];    // output ring position written at this sweep (-1), from X or Xprev (ret_prev)
+    int32_t ret_prev[kMfMaxFrames];
+    int32_t adm_pos[kMfMaxFrames];    // queue ring position admitted at this sweep (-1)
+    int32_t adm_kind[kMfMaxFrames];   // MfSrc of that admission
+    int32_t q_frame[kMfQueueMax];     // per queue ring position: frame index, cold start staged, norm, G
+    int32_t q_cold[kMfQueueMax];
+    double q_norm[kMfQueueMax], q_G[kMfQueueMax];
+    MfFinish log[kMfQueueMax];        // per output ring position
+};
+// Entries [e0, e0 + n) of the queue become visible to the plan (the publish kernel's argument, by value)
+struct MfPublish {
     int n;
-    int slot[kMfMaxFrames];
-    double norm[kMfMaxFrames];  // the frame's normalisation s = max(g) (1 if not positive)
-    double G[kMfMaxFrames];     // sum_{g>0} g^2 / s^2
+    int64_t e0;
+    int32_t frame[kMfMaxFrames], cold[kMfMaxFrames];
+    double norm[kMfMaxFrames], G[kMfMaxFrames];
+};
+// Device buffers of the refill (k_mf_update with a queue): output ring [rcap][ld], xlast [ld], host x0 (fp64 [nvox]),
+// staged cold starts and observed back-projections [qcap][ld] (null when not staged), optional start-value record
+// [frames][ld] (tests)
+struct MfRefill {
+    float* ring;
+    float* xlast;
+    const double* x0;
+    const float* x0q;
+    const float* oq;
+    float* starts;
 };
 
 __device__ __forceinline__ float wave_sum(float v) {

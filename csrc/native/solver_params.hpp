@@ -34,8 +34,9 @@ struct SolveInfo {
     double ms = 0.0;
     int sweeps = 0;           // sweeps executed on the device (iterations + the final decision sweep)
     double comm_ms = -1.0;    // GPU time inside the per-sweep all-reduces (EngineConfig::time_collectives; else -1)
-    int warm_from = -1;       // multi-frame time series: index of the frame whose solution started this one
+    int warm_from = -1;       // multi-frame time series: index of the frame whose iterate started this one
                               // (-1: the caller's x0, or cold)
+    int warm_iter = -1;       // the update count of that iterate (its final count when it had finished)
     // per-frame breakdown of ms (single-frame engine): host + device setup of the frame (normalisation, H2D of g
     // and x0, cold-start back-projection) up to the first queued sweep, the sweep loop up to the final state
     // check, the read-back of x (D2H and de-normalisation); sweeps queued in total (the chunks past the

@@ -7,12 +7,15 @@ frames can be batched: the forward and back projections become skinny GEMMs ``A.
 column groups; from 32 frames on A is split in registers into two f16 pieces of A scaled per row (forward) / per
 column (back-projection) for the 16-bit matrix cores, csrc/kernels/multiframe_bf16.hip, which also take 128 frames
 on 8 column groups), reading A twice per iteration for the whole batch. Every frame keeps its own normalisation,
-saturation mask, convergence history, iteration count and status. The batch's columns are slots with
-continuous batching: as soon as a frame finishes, its slot takes the next frame between two sweeps, so no
-sweep is spent on finished frames while frames wait. Frames are cold-started (``--no_guess``), or started as a
-time series: the first batch from ``x0``, every later frame from the solution of the latest frame finished
-before it (``SolveResult.warm_from``; the reference warm-starts frame by frame, main.cpp:127-139). A frame whose
-iterate turns non-finite returns its last finite iterate.
+saturation mask, convergence history, iteration count and status. The batch's columns are slots refilled on the
+device: frames are staged into a device queue ahead of the sweeps, and the sweep in which a frame finishes retires
+it (into an output ring the host drains) and admits the next queued frame into its slot, so no sweep is spent on
+finished frames while frames wait and the host never sits between a slot and its next frame. Frames are
+cold-started (``--no_guess``), or started as a time series: each frame from the current iterate of the newest
+frame in flight (or finished), rescaled to its own normalisation (``SolveResult.warm_from`` / ``warm_iter``; the
+reference warm-starts frame k from frame k-1's converged solution, main.cpp:127-139 -- here the chain is
+pipelined), the first ones from ``x0`` (or cold). A frame whose iterate turns non-finite returns its last finite
+iterate.
 
 The solver runs in the native engine (csrc/engine/multiframe.cpp, ``sart::MultiFrameEngine``; glue
 kernels in csrc/kernels/multiframe_glue.hip); this class is its Python face.
@@ -88,17 +91,21 @@ class MultiFrameSARTSolver:
         self.forward_split = str(self.engine.forward_split)
         self.backproject_split = str(self.engine.backproject_split)
 
-    def solve_batch(self, measurements, x0=None, chain: bool = False) -> List[SolveResult]:
-        """Frames [nframes, local pixels] through ``batch_width`` slots with continuous batching: a slot whose
-        frame finished takes the next frame between two sweeps. ``x0`` (nvoxel, optional): start value of the
-        first ``batch_width`` frames (None: cold). ``chain``: every later frame starts from the solution of the
-        latest frame finished before it (time series; ``SolveResult.warm_from``); otherwise later frames
-        cold-start."""
+    def solve_batch(self, measurements, x0=None, chain: bool = False, record_starts: bool = False) -> List[SolveResult]:
+        """Frames [nframes, local pixels] through ``batch_width`` slots refilled on the device. ``x0`` (nvoxel,
+        optional): with ``chain`` the start value while no frame is in flight yet, else of the first
+        ``batch_width`` frames (None: cold). ``chain``: a time series -- every frame starts from the current
+        iterate of the newest frame in flight or finished (``SolveResult.warm_from`` / ``warm_iter``); otherwise
+        frames cold-start. ``record_starts``: keep every frame's start value (de-normalised) in ``self.starts``
+        (tests of the chain). ``self.series_stats``: sweeps, slot utilisation, mean iterations of the run."""
         g_all = np.ascontiguousarray(np.asarray(measurements, dtype=np.float64))
         if g_all.ndim == 1:
             g_all = g_all[None]
         warm = None if x0 is None else _host_f64(x0)
-        x, infos = self.engine.solve_batch(g_all, warm, bool(chain))
+        ret = self.engine.solve_batch(g_all, warm, bool(chain), bool(record_starts))
+        x, infos = ret[0], ret[1]
+        self.starts = ret[2] if record_starts else None
+        self.series_stats = dict(self.engine.series_stats)
         out: List[SolveResult] = []
         for f, info in enumerate(infos):
             status = SUCCESS if info["status"] == SUCCESS else MAX_ITERATIONS_EXCEEDED
@@ -107,6 +114,7 @@ class MultiFrameSARTSolver:
                             elapsed_ms=float(info["ms"]), nonfinite=bool(info["nonfinite"]),
                             comm_fallbacks=int(info["comm_fallbacks"]), comm=str(info["comm"]))
             r.warm_from = int(info["warm_from"])
+            r.warm_iter = int(info["warm_iter"])
             out.append(r)
         return out
 

@@ -87,7 +87,8 @@ class SolveResult:
     comm: str = ""           # device communicator that produced the result (p2p / rccl / staged / local)
     fused_variant: int = -1  # fused sweep variant that produced the result (-1: two-pass kernels)
     nonfinite: bool = False  # stopped by the NaN/Inf guard: ``solution`` is the last finite iterate
-    warm_from: int = -1      # multi-frame time series: frame whose solution started this one (-1: x0 / cold)
+    warm_from: int = -1      # multi-frame time series: frame whose iterate started this one (-1: x0 / cold)
+    warm_iter: int = -1      # ... and that iterate's update count (its final count when it had finished)
 
 
 def _host_f64(v) -> np.ndarray:

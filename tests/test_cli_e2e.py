@@ -37,12 +37,14 @@ def _expected(case, oracle, warm=True, **kw):
     return np.array(xs), np.array(sts), its
 
 
-def chain_errors(case, out, *, log=False, warm=True, warm_from=None, beta_laplace=1e-3, A=None, orders=("blas",)):
+def chain_errors(case, out, *, log=False, warm=True, warm_from=None, warm_iter=None, beta_laplace=1e-3, A=None,
+                 orders=("blas",)):
     """Every frame of a CLI output file against the fp64 oracle of the reference GPU semantics, run for the frame's
     own recorded number of SART updates (solution/iterations) and warm-started like the run (warm: from frame k - 1;
-    warm_from: from the listed frame, -1 cold) from the oracle's own solutions; next to it the fp32 emulation of the
-    same chain (its inherent fp32 error; the largest over the summation ``orders``, see sart_fp32_emulation).
-    Returns (ours, fp32) relative errors per frame."""
+    warm_from: from the listed frame, -1 cold) from the oracle's own solutions -- or, with warm_iter (the pipelined
+    chain of --batch_frames), from the listed frame's oracle iterate after that many updates; next to it the fp32
+    emulation of the same chain (its inherent fp32 error; the largest over the summation ``orders``, see
+    sart_fp32_emulation). Returns (ours, fp32) relative errors per frame."""
     from mpi_cuda_sartsolver_amd.models.reference import sart_fp32_emulation
 
     n = native()
@@ -52,16 +54,31 @@ def chain_errors(case, out, *, log=False, warm=True, warm_from=None, beta_laplac
     L = _laplacian(case)
     kw = dict(logarithmic=log, beta_laplace=beta_laplace)
     e_ours, e_32 = [], []
+    frames = _frames(case)
     s64, s32 = {}, {o: {} for o in orders}
-    for k, g in enumerate(_frames(case)):
+    p64, p32 = {}, {o: {} for o in orders}  # each frame's start value (x_prev), for the iterates of in-flight sources
+
+    def start(k, src):
+        if src < 0:
+            return None, {o: None for o in orders}
+        n_it = None if warm_iter is None else int(warm_iter[k])
+        if n_it is None or n_it < 0 or n_it >= int(its[src]):
+            return s64[src], {o: s32[o][src] for o in orders}
+        x, _, _ = sart_gpu_semantics(A, frames[src], L, conv_tolerance=0.0, max_iterations=n_it, x_prev=p64[src], **kw)
+        return x, {o: sart_fp32_emulation(A, frames[src], L, max_iterations=n_it, x_prev=p32[o][src], order=o,
+                                          **kw)[0] for o in orders}
+
+    for k, g in enumerate(frames):
         src = (warm_from[k] if warm_from is not None else (k - 1 if warm else -1))
-        x64, _, _ = sart_gpu_semantics(A, g, L, conv_tolerance=0.0, max_iterations=int(its[k]),
-                                       x_prev=s64.get(src), **kw)
+        st64, st32 = start(k, src)
+        p64[k] = st64
+        x64, _, _ = sart_gpu_semantics(A, g, L, conv_tolerance=0.0, max_iterations=int(its[k]), x_prev=st64, **kw)
         nrm = np.linalg.norm(x64)
         e_ours.append(np.linalg.norm(X[k] - x64) / nrm)
         e = 0.0
         for o in orders:
-            x32, _, _ = sart_fp32_emulation(A, g, L, max_iterations=int(its[k]), x_prev=s32[o].get(src), order=o, **kw)
+            p32[o][k] = st32[o]
+            x32, _, _ = sart_fp32_emulation(A, g, L, max_iterations=int(its[k]), x_prev=st32[o], order=o, **kw)
             e = max(e, np.linalg.norm(x32 - x64) / nrm)
             s32[o][k] = x32
         e_32.append(e)
@@ -153,10 +170,11 @@ def test_cli_gpu_matches_gpu_semantics(tmp_path, capfd, log, extra):
 @pytest.mark.parametrize("log", [False, True])
 def test_cli_batched_time_series_warm_start(tmp_path, capfd, log):
     """--batch_frames keeps a warm-started time series (reference main.cpp:127-139) at MFMA throughput with
-    continuous batching: 16 slots, a finished frame's slot takes the next frame, every frame after the first
-    16 starts from the latest finished frame (reported as warm_from in --profile). 3 cameras, 64 frames: the
-    same status for every frame as the sequential warm-start series, every frame equal to the oracle started
-    from its reported warm_from, and the batched run solves the series faster than the frame-by-frame engine."""
+    device-side refill: 16 slots, the sweep in which a frame finishes admits the next one, which starts from the
+    current iterate of the newest frame in flight (reported as warm_from / warm_iter in --profile; the first frame
+    is solved alone, cold, by the single-frame engine). 3 cameras, 64 frames: the same status for every frame as the sequential
+    warm-start series, every frame equal to the oracle of its own pipelined chain, no more than twice the
+    sequential chain's mean iterations per frame, and a faster series than the frame-by-frame engine."""
     import json
     import time
 
@@ -176,16 +194,26 @@ def test_cli_batched_time_series_warm_start(tmp_path, capfd, log):
         t, last, st = native().read_solution_file(out)
         assert len(t) == 64
         np.testing.assert_array_equal(st, sts)  # same status per frame as the sequential warm-start series
-        recs = [r for r in (json.loads(ln) for ln in open(prof)) if "load" not in r]  # (first line: the RTM load)
+        lines = [json.loads(ln) for ln in open(prof)]
+        recs = [r for r in lines if "frame" in r]  # (first line: the RTM load; batched: a series summary last)
+        walls[mode + "_iters"] = float(np.mean([r["iterations"] for r in recs]))
         if mode == "batched":
-            # the batched chain's own oracle: each frame starts from its reported warm_from (the underdetermined
-            # problem's tolerance-stopped answer depends on the initial guess)
+            # the batched chain's own oracle: each frame starts from its reported source iterate (the
+            # underdetermined problem's tolerance-stopped answer depends on the initial guess)
+            series = [r for r in lines if r.get("series")][0]
+            cap = series["admit_cap"]
+            assert series["frames"] == 64 and 0 < series["slot_util"] <= 1.0
             wf = {r["frame"]: r["warm_from"] for r in recs}
-            assert all(wf[i] == -1 for i in range(16)) and all(0 <= wf[i] < i for i in range(16, 64))
-            e, e32 = chain_errors(case, out, log=log, warm_from=[wf[i] for i in range(64)])
+            wi = {r["frame"]: r["warm_iter"] for r in recs}
+            # frame 0: the lead frame (single-frame engine, cold); every later frame chained to an earlier one
+            assert wf[0] == -1 and all(0 <= wf[i] < i for i in range(1, 64)) and cap >= 1
+            e, e32 = chain_errors(case, out, log=log, warm_from=[wf[i] for i in range(64)],
+                                  warm_iter=[wi[i] for i in range(64)])
         else:  # the sequential chain
             e, e32 = chain_errors(case, out, log=log, warm=True)
         # every frame within the fp32 emulation's error of the same chain (update counts as recorded)
         assert np.all(e <= CLI_FP32_FACTOR * e32 + 1e-6), (mode, e, e32)
         walls[mode + "_solve_ms"] = sum(r["ms"] for r in recs)
     assert walls["batched_solve_ms"] < walls["sequential_solve_ms"], walls
+    # the pipelined chain keeps the warm start's iteration savings (round 5: the stale window start tripled them)
+    assert walls["batched_iters"] <= 2.0 * walls["sequential_iters"] + 1.0, walls

@@ -42,9 +42,11 @@ def test_multiframe_vs_oracle(log, nframes, batch):
 
 @pytest.mark.parametrize("log", [False, True])
 def test_multiframe_warm_chain(log):
-    """Time series with continuous batching: the first batch starts from x0, every later frame from the latest
-    frame finished before it (warm_from); each frame matches the oracle started from the same vector. Frames
-    converge after different iteration counts, so slots are refilled at different sweeps."""
+    """Time series with device-side refill: the first admit_cap frames start from x0, every later frame from the
+    current iterate of the newest frame in flight or finished (warm_from, with warm_iter updates), rescaled to its own
+    normalisation. Each frame matches the oracle started from its recorded start value; each start value is the
+    source's iterate (bitwise when the source had finished, at the oracle's fp32 drift when it was in flight).
+    Frames converge after different iteration counts, so slots are refilled at different sweeps."""
     from mpi_cuda_sartsolver_amd.models.laplacian import LaplacianCSR
     from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
     from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
@@ -64,24 +66,75 @@ def test_multiframe_warm_chain(log):
     s = MultiFrameSARTSolver(DenseRTM.from_dense(A, device=dev), L, None, SolverParams(**kw), logarithmic=log,
                              batch=batch)
     x0 = base * 1.5
-    res = s.solve_batch(G, x0=x0, chain=True)
-    assert all(res[f].warm_from == -1 for f in range(batch))
-    assert all(0 <= res[f].warm_from < f for f in range(batch, nframes))
+    res = s.solve_batch(G, x0=x0, chain=True, record_starts=True)
+    starts, stats = s.starts, s.series_stats
+    cap = stats["admit_cap"]
+    assert 1 <= cap < batch and stats["frames"] == nframes and 0 < stats["slot_util"] <= 1.0
+    assert all(res[f].warm_from == -1 for f in range(cap))
+    assert all(0 <= res[f].warm_from < f for f in range(cap, nframes))
     assert len({res[f].iterations for f in range(nframes)}) > 1  # slots really refill at different sweeps
+    assert any(res[f].warm_iter < res[res[f].warm_from].iterations for f in range(cap, nframes))  # in flight
+    norm = G.max(axis=1)
     for f in range(nframes):
-        wf = res[f].warm_from
-        prev = x0 if wf < 0 else res[wf].solution
-        x, st, it = sart_gpu_semantics(A, G[f], L, logarithmic=log, x_prev=prev, **kw)
+        wf, wi = res[f].warm_from, res[f].warm_iter
+        if wf < 0:
+            src = x0
+        elif wi == res[wf].iterations:  # the source had finished: its solution, rescaled (bitwise)
+            src = res[wf].solution
+        else:  # in flight: the oracle's iterate of the source after wi updates from its own recorded start
+            src, _, _ = sart_gpu_semantics(A, G[wf], L, logarithmic=log, x_prev=starts[wf],
+                                           **dict(kw, max_iterations=wi, conv_tolerance=0.0))
+        want = np.maximum((src / norm[f]).astype(np.float32), np.float32(1e-7))
+        got = (starts[f] / norm[f]).astype(np.float32)
+        if wf < 0 or wi == res[wf].iterations:
+            np.testing.assert_array_equal(got, want)
+        else:
+            assert np.linalg.norm(got - want) <= 1e-4 * np.linalg.norm(want), f
+        x, st, it = sart_gpu_semantics(A, G[f], L, logarithmic=log, x_prev=starts[f], **kw)
         assert res[f].status == st and abs(res[f].iterations - it) <= 2, (f, res[f].iterations, it)
         if f % 7 == 0 or f == nframes - 1:
             check_fp32_bound(res[f].solution, A, G[f], L, log=log, iterations=res[f].iterations, beta_laplace=1e-3,
-                             x_prev=prev)
+                             x_prev=starts[f])
     # without chain, every frame after the first batch cold-starts even when x0 is given
-    cold = s.solve_batch(G[:20], x0=None)
+    cold = s.solve_batch(G[:20], x0=x0)
     assert all(r.warm_from == -1 for r in cold)
     x, st, it = sart_gpu_semantics(A, G[17], L, logarithmic=log, **kw)
     assert cold[17].status == st
     check_fp32_bound(cold[17].solution, A, G[17], L, log=log, iterations=cold[17].iterations, beta_laplace=1e-3)
+    x, st, it = sart_gpu_semantics(A, G[3], L, logarithmic=log, x_prev=x0, **kw)  # the first batch: from x0
+    assert cold[3].status == st and abs(cold[3].iterations - it) <= 2
+
+
+def test_multiframe_series_iterations_near_sequential():
+    """A slowly drifting series (the ray-traced phantom's regime): the pipelined chain keeps the warm start's
+    iteration savings -- mean iterations per frame within 2x of the frame-by-frame chain's -- and the slots stay
+    busy (the plan admits in the sweep a frame finishes)."""
+    from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SARTSolver, SolverParams
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(3)
+    P, V, nframes = 1500, 1200, 96
+    A = rng.random((P, V), dtype=np.float32)
+    b = rng.random(V) + 0.5
+    ph = 2 * np.pi * rng.random(V)
+    X = np.stack([b * (1 + 0.05 * np.sin(2 * np.pi * t / 200.0 + ph)) for t in range(nframes)])
+    G = X @ A.T.astype(np.float64)
+    kw = dict(max_iterations=400, conv_tolerance=1e-7)
+    rtm = DenseRTM.from_dense(A, device=dev)
+    seq = SARTSolver(rtm, None, None, SolverParams(**kw))
+    its, prev = [], None
+    for f in range(nframes):
+        r = seq.solve(G[f], prev)
+        its.append(r.iterations)
+        prev = r.solution
+    mf = MultiFrameSARTSolver(rtm, None, None, SolverParams(**kw), batch=32)
+    res = mf.solve_batch(G, chain=True)
+    mean_b, mean_s = np.mean([r.iterations for r in res]), np.mean(its[1:])
+    assert all(r.status == 0 for r in res)
+    assert mean_b <= 2.0 * mean_s + 1.0, (mean_b, mean_s, mf.series_stats)
+    assert mf.series_stats["slot_util"] > 0.5, mf.series_stats
 
 
 @pytest.mark.parametrize("log", [False, True])

@@ -31,6 +31,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def _all_recs(d, tag):
+    p = os.path.join(d, f"prof_{tag}.jsonl")
+    return [json.loads(x) for x in open(p)] if os.path.exists(p) else []
+
+
 def pct(a, q):
     return float(np.percentile(np.asarray(a, dtype=float), q)) if len(a) else None
 
@@ -52,6 +57,8 @@ def main():
     ap.add_argument("--runs", default="seq", help="comma list: seq (frame by frame), batch<N> (--batch_frames N)")
     ap.add_argument("--extra", default="", help="extra driver arguments for every run")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "series_native.jsonl"))
+    ap.add_argument("--batch-sweep-ms", type=float, default=0.0,
+                    help="time of one batched sweep (tools/probe_mf.py) for the sweeps x t_sweep / loop figure")
     ap.add_argument("--keep", action="store_true")
     a = ap.parse_args()
     import torch
@@ -169,16 +176,17 @@ def main():
             "rtm_write_s": round(t_rtm, 1), "reads": "page cache (files written by this process)"}
     extra = a.extra.split() if a.extra else []
 
-    def drive(tag, argv):
+    def drive(tag, argv, env_over=None):
         prof = os.path.join(a.dir, f"prof_{tag}.jsonl")
         out = os.path.join(a.dir, f"sol_{tag}.h5")
         t = time.perf_counter()
-        r = subprocess.run([binary, *argv, *extra, "--profile", prof, "-o", out, *files], env=env,
+        r = subprocess.run([binary, *argv, *extra, "--profile", prof, "-o", out, *files], env=dict(env, **(env_over or {})),
                            capture_output=True, text=True, timeout=1500)
         wall = time.perf_counter() - t
         if r.returncode != 0:
             raise RuntimeError(f"{tag}: rc {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}")
         recs = [json.loads(x) for x in open(prof)]
+        recs = [x for x in recs if not x.get("series")] + [x for x in recs if x.get("series")]
         m = re.search(r"Frames processed: (\d+) in ([0-9.eE+-]+) s", r.stdout)
         return recs[0], [x for x in recs[1:] if "frame" in x], wall, (float(m.group(2)) if m else None), r.stdout
 
@@ -187,14 +195,22 @@ def main():
     # counted at zero, which errs towards a larger per-sweep time, i.e. a smaller overhead, by < 1 %)
     _, cal, _, _, _ = drive("cal", ["-m", "200", "-c", "1e-30", "-t", "0:0.005"])
     t_sweep = cal[0]["iterate_ms"] / cal[0]["sweeps"]
+    sols = {}
+    t_sweep_of = []
+    if a.batch_sweep_ms:  # the batched sweep time (per batch width) for the loop-share figure
+        t_sweep_of.append(a.batch_sweep_ms)
     emit(dict(base, run="calibration", sweeps=cal[0]["sweeps"], queued=cal[0]["queued_sweeps"],
               iterate_ms=cal[0]["iterate_ms"], t_sweep_ms=round(t_sweep, 4),
               valid=cal[0]["sweeps"] >= 100))
     for run in a.runs.split(","):
+        # a run: seq | batch<N>, optionally @VAR=value+VAR=value (environment of that run: A/B knobs)
+        spec, _, envs = run.partition("@")
+        env_over = dict(kv.split("=", 1) for kv in envs.split("+")) if envs else {}
         argv = ["-m", "2000", "-c", "1e-5"]
-        if run.startswith("batch"):
-            argv += ["--batch_frames", run[5:]]
-        load, fr, wall, loop_s, _ = drive(run, argv)
+        if spec.startswith("batch"):
+            argv += ["--batch_frames", spec[5:]]
+        run = run.replace("@", "_").replace("+", "_").replace("=", "")
+        load, fr, wall, loop_s, _ = drive(run, argv, env_over)
         ms = [x["ms"] for x in fr]
         rec = dict(base, run=run, process_wall_s=round(wall, 2), load_s=round(load.get("load_s", 0), 2),
                    load_GBps=round(load.get("load_GBps", 0), 2), load_rss_growth_MB=load.get("rss_growth_MB_max"),
@@ -208,6 +224,21 @@ def main():
                                "max": max(x["iterations"] for x in fr),
                                "first": fr[0]["iterations"]},
                    converged=sum(x["status"] == 0 for x in fr))
+        series = [x for x in [load, *fr] if x.get("series")] + [x for x in _all_recs(a.dir, run) if x.get("series")]
+        if series:  # batched: the device-refill counters (sweeps, slot utilisation, chain sources)
+            rec["series"] = series[-1]
+            rec["sweeps_x_t_sweep_over_loop"] = round(series[-1]["sweeps"] * t_sweep_of[0] / 1e3 / loop_s, 3) \
+                if t_sweep_of and loop_s else None
+        sols[run] = n.read_dataset_f64(os.path.join(a.dir, f"sol_{run}.h5"), "solution/value")
+        rec["env"] = env_over
+        if X is not None and sols[run].shape == X.shape:  # every frame against the phantom it was computed from
+            d = np.linalg.norm(sols[run] - X, axis=1) / np.linalg.norm(X, axis=1)
+            rec["rel_err_vs_truth"] = {"p50": pct(d, 50), "p90": pct(d, 90), "max": float(d.max()),
+                                       "mean": float(d.mean())}
+        if run != "seq" and "seq" in sols:  # every frame against the sequential chain's solution
+            ref = sols["seq"]
+            d = np.linalg.norm(sols[run] - ref, axis=1) / np.maximum(np.linalg.norm(ref, axis=1), 1e-300)
+            rec["rel_diff_vs_seq"] = {"p50": pct(d, 50), "p90": pct(d, 90), "p99": pct(d, 99), "max": float(d.max())}
         if "sweeps" in fr[0]:  # frame by frame: overhead beyond the sweeps actually needed
             over = [x["ms"] - x["sweeps"] * t_sweep for x in fr[1:]]  # warm-started frames
             keys = ("setup_ms", "iterate_ms", "finish_ms", "writer_ms", "wait_frame_ms")
