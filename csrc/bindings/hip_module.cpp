@@ -47,6 +47,7 @@ static py::dict solve_info(const sart::SolveInfo& i) {
     d["comm_ms"] = i.comm_ms;
     d["warm_from"] = i.warm_from;
     d["warm_iter"] = i.warm_iter;
+    d["warm_live"] = i.warm_live;
     return d;
 }
 
@@ -356,6 +357,10 @@ static void bind_engine(py::module_& m) {
             d["src_finished"] = s.src_finished;
             d["lead"] = s.lead;
             d["src_extrap"] = s.src_extrap;
+            d["host_wait_ms"] = s.host_wait_ms;
+            d["host_stage_ms"] = s.host_stage_ms;
+            d["host_src_ms"] = s.host_src_ms;
+            d["host_deliver_ms"] = s.host_deliver_ms;
             return d;
         });
 }

@@ -458,7 +458,7 @@ int main(int argc, char** argv) {
             if (lap.nnz()) e->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
             return e;
         };
-        std::unique_ptr<Engine> engine;
+        std::unique_ptr<Engine> engine, lead_engine;
         std::unique_ptr<MultiFrameEngine> mf;
         std::unique_ptr<CpuSolver> cpu;
         const bool batched = gpu && cfg.batch_frames > 1;
@@ -477,6 +477,10 @@ int main(int argc, char** argv) {
                                                         dshard->nvoxel, dshard->ld, dcomm.get(), ec);
             }
             if (lap.nnz()) mf->set_laplacian(lap.row_ptr.data(), lap.col.data(), lap.val.data(), lap.nnz());
+            // a cold time series' first frame: the single-frame engine, built with the set-up (before the frame loop's
+            // clock, like the frame-by-frame engine); dropped after that frame (SART_MF_LEAD_ENGINE=0: none)
+            const char* le = std::getenv("SART_MF_LEAD_ENGINE");
+            if (!cfg.no_guess && !(le && *le && std::atoi(le) == 0)) lead_engine = make_engine();
         } else if (gpu) {
             engine = make_engine();
         } else {
@@ -567,58 +571,31 @@ int main(int argc, char** argv) {
             const int64_t nfr = (int64_t)frames.size();
             const int64_t ahead = 4 * (int64_t)cfg.batch_frames;
             std::vector<double> bwarm = cfg.no_guess ? std::vector<double>() : warm;
-            // A cold time series: its first frame is solved alone by the single-frame engine (the fused sweep, half
-            // the time of a batched sweep) and starts the chain as a converged source -- frames chained from a cold
-            // start's young iterates would carry its error for ~100 frames (profiles/series_r6_*). SART_MF_LEAD_ENGINE=0:
-            // the multi-frame engine's own lead frame instead (MfQueue::lead).
-            int64_t off = 0;
-            int lead_iters = -1;
-            const char* le = std::getenv("SART_MF_LEAD_ENGINE");
-            if (!cfg.no_guess && bwarm.empty() && nfr > 0 && !(le && *le && std::atoi(le) == 0)) {
-                const auto t0 = std::chrono::steady_clock::now();
-                std::vector<double> g0 = image.frame(frames[0]), x0s(in.nvoxel);
-                SolveInfo info;
-                {
-                    std::unique_ptr<Engine> lead = make_engine();
-                    info = lead->solve(g0.data(), nullptr, x0s.data());
-                }
-                const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-                if (rank == 0) {
-                    writer->add(x0s, info.status, image.frame_time(frames[0]), image.camera_frame_time(frames[0]),
-                                info.iterations);
-                    std::cout << "Processed in: " << ms << " ms" << std::endl;
-                    if (profile.is_open())
-                        profile << "{\"frame\": " << frames[0] << ", \"time\": " << image.frame_time(frames[0])
-                                << ", \"status\": " << info.status << ", \"iterations\": " << info.iterations
-                                << ", \"convergence\": " << info.convergence << ", \"ms\": " << ms
-                                << ", \"batch\": " << cfg.batch_frames << ", \"warm_from\": -1, \"warm_iter\": -1"
-                                << ", \"lead\": true, \"fused\": " << (info.used_fused ? "true" : "false")
-                                << ", \"driver\": \"native\"}\n";
-                }
-                if (std::all_of(x0s.begin(), x0s.end(), [](double v) { return std::isfinite(v); })) bwarm = x0s;
-                off = 1;
-                lead_iters = info.iterations;
-            }
             std::mutex mu, io_mu;
             std::condition_variable cv;
             std::map<int64_t, std::vector<double>> ready;  // frames read ahead, by series index
-            int64_t consumed = off, reader_next = off;
+            int64_t consumed = 0, reader_next = 0;
+            double reader_ms = 0.0, sink_ms = 0.0;  // (--profile: the reader thread's frame reads, rank 0's writes)
             bool stop = false;
             std::exception_ptr read_err;
             std::thread reader([&] {
                 try {
-                    for (int64_t k = off; k < nfr; ++k) {
+                    for (int64_t k = 0; k < nfr; ++k) {
                         {
                             std::unique_lock<std::mutex> lk(mu);
                             cv.wait(lk, [&] { return stop || k < consumed + ahead; });
                             if (stop) return;
                         }
                         std::vector<double> f;
+                        const auto tr = std::chrono::steady_clock::now();
                         {
                             std::lock_guard<std::mutex> io(io_mu);
                             f = image.frame(frames[k]);
                         }
+                        const double rms =
+                            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr).count();
                         std::lock_guard<std::mutex> lk(mu);
+                        reader_ms += rms;
                         ready.emplace(k, std::move(f));
                         reader_next = k + 1;
                         cv.notify_all();
@@ -644,6 +621,44 @@ int main(int argc, char** argv) {
                     if (t.joinable()) t.join();
                 }
             } join_reader{reader, mu, cv, stop};
+            // A cold time series: its first frame is solved alone by the single-frame engine (the fused sweep, half
+            // the time of a batched sweep) and starts the chain as a converged source -- frames chained from a cold
+            // start's young iterates would carry its error for ~100 frames (profiles/series_r6_*). SART_MF_LEAD_ENGINE=0:
+            // the multi-frame engine's own lead frame instead (MfQueue::lead).
+            int64_t off = 0;
+            int lead_iters = -1;
+            if (lead_engine && bwarm.empty() && nfr > 0) {
+                const auto t0 = std::chrono::steady_clock::now();
+                std::vector<double> g0, x0s(in.nvoxel);
+                {  // frame 0 from the reader thread (which goes on reading the next frames meanwhile)
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return read_err || ready.count(0); });
+                    if (read_err) std::rethrow_exception(read_err);
+                    g0 = std::move(ready[0]);
+                    ready.erase(0);
+                    consumed = 1;
+                    cv.notify_all();
+                }
+                SolveInfo info = lead_engine->solve(g0.data(), nullptr, x0s.data());
+                lead_engine.reset();
+                const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                if (rank == 0) {
+                    writer->add(x0s, info.status, image.frame_time(frames[0]), image.camera_frame_time(frames[0]),
+                                info.iterations);
+                    std::cout << "Processed in: " << ms << " ms" << std::endl;
+                    if (profile.is_open())
+                        profile << "{\"frame\": " << frames[0] << ", \"time\": " << image.frame_time(frames[0])
+                                << ", \"status\": " << info.status << ", \"iterations\": " << info.iterations
+                                << ", \"convergence\": " << info.convergence << ", \"ms\": " << ms
+                                << ", \"batch\": " << cfg.batch_frames << ", \"warm_from\": -1, \"warm_iter\": -1"
+                                << ", \"lead\": true, \"fused\": " << (info.used_fused ? "true" : "false")
+                                << ", \"driver\": \"native\"}\n";
+                }
+                if (std::all_of(x0s.begin(), x0s.end(), [](double v) { return std::isfinite(v); })) bwarm = x0s;
+                off = 1;
+                lead_iters = info.iterations;
+            }
+            lead_engine.reset();  // (a resumed series starts from the stored solution instead)
             const size_t npix = (size_t)mf->nrows();
             auto src = [&](int64_t j, double* dst) {  // series index j = frame off + j
                 const int64_t k = j + off;
@@ -673,6 +688,12 @@ int main(int argc, char** argv) {
             auto t_prev = std::chrono::steady_clock::now();
             auto sink = [&](int64_t j, const double* xs, const SolveInfo& info) {
                 if (rank != 0) return;
+                const auto tsk = std::chrono::steady_clock::now();
+                struct Acc {
+                    double& ms;
+                    std::chrono::steady_clock::time_point t;
+                    ~Acc() { ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count(); }
+                } acc{sink_ms, tsk};
                 SolveInfo fi = info;
                 if (fi.warm_from >= 0) {
                     fi.warm_from += (int)off;
@@ -697,7 +718,8 @@ int main(int argc, char** argv) {
                                 << ", \"convergence\": " << fi.convergence << ", \"ms\": " << ms
                                 << ", \"batch\": " << cfg.batch_frames << ", \"warm_from\": "
                                 << (fi.warm_from >= 0 ? (int64_t)frames[fi.warm_from] : -1)
-                                << ", \"warm_iter\": " << fi.warm_iter << ", \"comm_fallbacks\": " << fi.comm_fallbacks
+                                << ", \"warm_iter\": " << fi.warm_iter << ", \"warm_live\": " << (fi.warm_live ? 1 : 0)
+                                << ", \"comm_fallbacks\": " << fi.comm_fallbacks
                                 << ", \"driver\": \"native\"}\n";
                     done.erase(it);
                     ++written;
@@ -713,7 +735,10 @@ int main(int argc, char** argv) {
                         << ", \"chunk\": " << ss.chunk << ", \"admit_cap\": " << ss.admit_cap
                         << ", \"src_age\": " << ss.src_age << ", \"src_finished\": " << (ss.src_finished ? 1 : 0)
                         << ", \"lead\": " << (ss.lead ? 1 : 0) << ", \"src_extrap\": " << ss.src_extrap
-                        << ", \"restarts\": " << ss.restarts
+                        << ", \"restarts\": " << ss.restarts << ", \"host_wait_ms\": " << ss.host_wait_ms
+                        << ", \"host_stage_ms\": " << ss.host_stage_ms << ", \"host_src_ms\": " << ss.host_src_ms
+                        << ", \"host_deliver_ms\": " << ss.host_deliver_ms << ", \"reader_ms\": " << reader_ms
+                        << ", \"sink_ms\": " << sink_ms
                         << ", \"batch\": " << mf->batch_frames() << ", \"driver\": \"native\"}\n";
             }
             frames.clear();

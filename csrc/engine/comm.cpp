@@ -14,6 +14,7 @@
 #include <stdexcept>
 #include <string>
 #include <utility>
+#include <thread>
 #include <vector>
 
 #include "../kernels/launchers.hpp"
@@ -70,19 +71,42 @@ class StagedComm final : public Communicator {
 class RcclComm final : public Communicator {
    public:
     explicit RcclComm(std::unique_ptr<HostComm> boot) : host_(std::move(boot)) {}
-    // ncclCommInitRank on this rank: "" on success, else the error (the communicator stays unusable)
-    std::string init(int device, const std::string& uid) {
+    // The communicator of this rank, brought up NON-blocking (ncclConfig_t::blocking = 0) and polled against a
+    // deadline (SART_RCCL_INIT_TIMEOUT_S, default 120 s): a peer that never enters the init (crashed, hung, or the
+    // SART_FAULT_RCCL_INIT_SKIP fault) makes this rank abort its half-built communicator and report failure instead
+    // of blocking forever in ncclCommInitRank. "" on success, else the error (the communicator stays unusable).
+    std::string init(int device, const std::string& uid, double timeout_s) {
         try {
             if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("RcclComm: bad unique id");
             ncclUniqueId id;
             std::memcpy(&id, uid.data(), sizeof(id));
             hip_ok(hipSetDevice(device), "hipSetDevice");
-            nccl_ok(ncclCommInitRank(&comm_, host_->size(), id, host_->rank()), "ncclCommInitRank");
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 0;
+            const ncclResult_t r = ncclCommInitRankConfig(&comm_, host_->size(), id, host_->rank(), &cfg);
+            if (r != ncclSuccess && r != ncclInProgress) nccl_ok(r, "ncclCommInitRankConfig");
+            if (!comm_) throw std::runtime_error("ncclCommInitRankConfig: no communicator");
+            wait_ready(timeout_s, "ncclCommInitRankConfig");
         } catch (const std::exception& e) {
+            if (comm_) (void)ncclCommAbort(comm_);  // (abort: a destroy would wait for the peers)
             comm_ = nullptr;
             return e.what();
         }
         return "";
+    }
+    // a non-blocking communicator's call may return before its work is enqueued (ncclInProgress): poll to a deadline
+    void wait_ready(double timeout_s, const char* what) {
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+        for (;;) {
+            ncclResult_t st = ncclInProgress;
+            nccl_ok(ncclCommGetAsyncError(comm_, &st), "ncclCommGetAsyncError");
+            if (st == ncclSuccess) return;
+            if (st != ncclInProgress) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(st));
+            if (std::chrono::steady_clock::now() > deadline)
+                throw std::runtime_error(std::string(what) + ": not complete after " + std::to_string((int)timeout_s) +
+                                         " s (a peer never joined?)");
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
     }
     void destroy() {
         if (comm_) (void)ncclCommDestroy(comm_);
@@ -93,10 +117,10 @@ class RcclComm final : public Communicator {
     HostComm& host() override { return *host_; }
     const char* backend() const override { return "rccl"; }
     void all_reduce(float* dev, size_t n, ReduceOp op, hipStream_t stream) override {
-        if (n) nccl_ok(ncclAllReduce(dev, dev, n, ncclFloat32, nop(op), comm_, stream), "ncclAllReduce");
+        if (n) enqueued(ncclAllReduce(dev, dev, n, ncclFloat32, nop(op), comm_, stream));
     }
     void all_reduce(double* dev, size_t n, ReduceOp op, hipStream_t stream) override {
-        if (n) nccl_ok(ncclAllReduce(dev, dev, n, ncclFloat64, nop(op), comm_, stream), "ncclAllReduce");
+        if (n) enqueued(ncclAllReduce(dev, dev, n, ncclFloat64, nop(op), comm_, stream));
     }
     bool graph_capturable() const override { return true; }
     void abort() override {
@@ -109,6 +133,16 @@ class RcclComm final : public Communicator {
 
    private:
     static ncclRedOp_t nop(ReduceOp op) { return op == ReduceOp::kSum ? ncclSum : ncclMax; }
+    void enqueued(ncclResult_t r) {  // (the first collective connects the peers: bounded like the init)
+        if (r == ncclInProgress)
+            wait_ready(env_seconds("SART_RCCL_INIT_TIMEOUT_S", 120.0), "ncclAllReduce");
+        else
+            nccl_ok(r, "ncclAllReduce");
+    }
+    static double env_seconds(const char* name, double dflt) {
+        const char* e = std::getenv(name);
+        return (e && *e) ? std::atof(e) : dflt;
+    }
     std::unique_ptr<HostComm> host_;
     ncclComm_t comm_ = nullptr;
 };
@@ -573,13 +607,19 @@ std::string rccl_unique_id() {
 std::unique_ptr<Communicator> make_rccl_comm(int device, const std::string& uid, std::unique_ptr<HostComm> bootstrap) {
     auto rc = std::make_unique<RcclComm>(std::move(bootstrap));
     // SART_FAULT_RCCL_INIT=1 (tests): the RCCL bring-up fails on every rank (no rank calls ncclCommInitRank), or,
-    // with SART_FAULT_RANK, on that rank only (it still takes part in the collective init, so its peers are not
-    // left waiting in it, and reports failure afterwards)
+    // with SART_FAULT_RANK, on that rank only (it still takes part in the collective init and reports failure
+    // afterwards). SART_FAULT_RCCL_INIT_SKIP=<rank>: that rank never enters the init, so its peers wait in theirs
+    // until the deadline (SART_RCCL_INIT_TIMEOUT_S) -- an uncooperative failure
     const char* f = std::getenv("SART_FAULT_RCCL_INIT");
     const char* fr = std::getenv("SART_FAULT_RANK");
+    const char* fs = std::getenv("SART_FAULT_RCCL_INIT_SKIP");
     const bool inject = f && *f && std::atoi(f) != 0;
     const bool inject_all = inject && !(fr && *fr);
-    std::string err = inject_all ? std::string("injected (SART_FAULT_RCCL_INIT)") : rc->init(device, uid);
+    const bool skip = fs && *fs && std::atoi(fs) == rc->host().rank();
+    const double timeout_s = env_double("SART_RCCL_INIT_TIMEOUT_S", 120.0);
+    std::string err = inject_all ? std::string("injected (SART_FAULT_RCCL_INIT)")
+                      : skip     ? std::string("injected: never entered the init (SART_FAULT_RCCL_INIT_SKIP)")
+                                 : rc->init(device, uid, timeout_s);
     if (inject && !inject_all && std::atoi(fr) == rc->host().rank()) {
         rc->destroy();
         err = "injected (SART_FAULT_RCCL_INIT)";

@@ -1,6 +1,10 @@
 #include "multiframe.hpp"
 
 #include <algorithm>
+#include <exception>
+#include <mutex>
+#include <deque>
+#include <condition_variable>
 #include <chrono>
 #include <cstdio>
 #include <cmath>
@@ -17,6 +21,9 @@ namespace sart {
 namespace {
 void hip_ok(hipError_t e, const char* what) {
     if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+double ms_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
 }  // namespace
 
@@ -81,22 +88,41 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     // device refill: a queue and an output ring of 2 nf entries each (staging and draining run a chunk behind the
     // sweeps, ~nf frames finish per chunk at ~8 sweeps per frame); sweeps per host check (SART_MF_CHUNK, default
     // min(check_interval, 4): the host check no longer gates a refill, only the staging and the drain)
-    qcap_ = rcap_ = 2 * NF;
-    chunk_ = std::min(cfg_.check_interval, 4);
+    // queue and output ring: 4 nf entries (at most 256), down to 2 nf where their pinned host rows (fp64 pixels /
+    // fp32 voxels) would pass 1 GiB
+    qcap_ = rcap_ = std::min(kMfQueueMax, 4 * NF);
+    while (qcap_ > 2 * NF && (double)qcap_ * Pp_ * 8 > 1073741824.0) qcap_ /= 2;
+    while (rcap_ > 2 * NF && (double)rcap_ * ld_ * 4 > 1073741824.0) rcap_ /= 2;
+    {  // sweeps per chunk: ~1.5 ms of estimated sweep time (dense: two reads of A at ~5 TB/s; sparse: two gathers over
+       // the entries; plus ~13 launches), at least min(check_interval, 4): the host's per-chunk work (snapshot,
+       // drain, staging) must hide behind the chunk in flight when sweeps are short (sparse shards)
+        const double bytes = sparse ? 2.0 * (double)sparse->nnz * 8.0 : 2.0 * (double)Pp_ * ld_ * (bf16_ ? 2 : 4);
+        const double t_sweep = bytes / 5e12 + 13 * 4e-6;
+        chunk_ = (int)std::min<double>(32, std::max<double>(std::min(cfg_.check_interval, 4), std::ceil(1.5e-3 / t_sweep)));
+    }
     if (const char* e = std::getenv("SART_MF_CHUNK"); e && *e) chunk_ = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("SART_MF_GRAPH"); e && *e) use_graph_ = std::atoi(e) != 0;
     // admissions per sweep of a time series (SART_MF_ADMIT_CAP; 0: any): a frame admitted together with others
     // starts from the same source iterate, so a burst of admissions starts frames far from their predecessors
     admit_cap_ = std::max(1, NF / 4);
     if (const char* e = std::getenv("SART_MF_ADMIT_CAP"); e && *e) admit_cap_ = std::max(0, std::atoi(e));
+    // chain sources: the newest frame with at least 3 updates, extrapolated along its last update by 4 x (linear mode):
+    // a young iterate's slowest modes decay by ~rho = 0.86 per sweep on the 64k ray-traced series, so x + c (x - x_prev)
+    // with c ~ rho / (1 - rho) removes most of the error it would pass on, once its fast modes are gone (>= 3 updates).
+    // Measured there at 64 frames: 27.8 -> 22.9 iterations per frame, 253 -> 290 frames/s
+    // (profiles/series_r6_raytraced_64k_refill_policies*.jsonl; SART_MF_SRC_AGE / SART_MF_SRC_EXTRAP override)
+    src_age_ = 3;
+    src_extrap_ = 4.0;
     if (const char* e = std::getenv("SART_MF_SRC_AGE"); e && *e) src_age_ = std::max(0, std::atoi(e));
     // A/B knobs of the chain: SART_MF_SRC_FINISHED=1 (sources: finished frames only), SART_MF_LEAD=0 (no lead frame)
     if (const char* e = std::getenv("SART_MF_SRC_FINISHED"); e && *e) src_finished_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SART_MF_LEAD"); e && *e) lead_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SART_MF_SRC_EXTRAP"); e && *e) src_extrap_ = std::atof(e);
-    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hq_), (size_t)qcap_ * Pp_ * sizeof(float)), "hipHostMalloc");
-    std::memset(hq_, 0, (size_t)qcap_ * Pp_ * sizeof(float));  // padding rows stay zero
+    hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hg64_), (size_t)qcap_ * Pp_ * sizeof(double)), "hipHostMalloc");
+    std::memset(hg64_, 0, (size_t)qcap_ * Pp_ * sizeof(double));  // padding rows stay zero
+    g64q_.resize((size_t)qcap_ * Pp_);
+    sstats_.resize((size_t)2 * NF);
     hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hx_), (size_t)rcap_ * ld_ * sizeof(float)), "hipHostMalloc");
-    hg_.resize((size_t)NF * std::max<int64_t>(P_, 1));
     q_.resize(1);
     ghq_.resize((size_t)qcap_ * Pp_);
     ring_.resize((size_t)rcap_ * ld_);
@@ -182,6 +208,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
 
 MultiFrameEngine::~MultiFrameEngine() {
     set_device();
+    drop_graph();
     if (stream_) (void)hipStreamSynchronize(stream_);
     if (comm_stream_) (void)hipStreamSynchronize(comm_stream_);
     for (auto& e : ev_)
@@ -192,7 +219,7 @@ MultiFrameEngine::~MultiFrameEngine() {
     if (comm_done_) (void)hipEventDestroy(comm_done_);
     if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
     if (hsnap_) (void)hipHostFree(hsnap_);
-    if (hq_) (void)hipHostFree(hq_);
+    if (hg64_) (void)hipHostFree(hg64_);
     if (hx_) (void)hipHostFree(hx_);
     if (ev_copy_) (void)hipEventDestroy(ev_copy_);
     if (ev_stage_) (void)hipEventDestroy(ev_stage_);
@@ -360,6 +387,50 @@ void MultiFrameEngine::sweep() {
     ++host_sweep_;
 }
 
+void MultiFrameEngine::drop_graph() {
+    if (graph_) (void)hipGraphExecDestroy(graph_);
+    graph_ = nullptr;
+}
+
+void MultiFrameEngine::run_chunk() {
+    RoctxRange r("sart::mf_chunk");
+    // capture only after an eager chunk with the current kernels (launchers may set function attributes on first
+    // use, which must not happen inside a capture); the captured update kernel holds rf_ by value
+    const bool graphable = use_graph_ && !graph_failed_ && warm_chunk_ && comm_->size() == 1 &&
+                           comm_->graph_capturable() && cfg_.fault_nan_sweep < 0;
+    if (graph_ && (!graphable || graph_chunk_ != chunk_ || std::memcmp(&graph_rf_, &rf_, sizeof(rf_)) != 0))
+        drop_graph();
+    if (graphable && !graph_) {
+        hipGraph_t g = nullptr;
+        bool ok = hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal) == hipSuccess;
+        if (ok) {
+            try {
+                for (int i = 0; i < chunk_; ++i) sweep();
+            } catch (...) {
+                ok = false;
+            }
+            ok = (hipStreamEndCapture(stream_, &g) == hipSuccess) && ok && g;
+        }
+        if (ok) ok = hipGraphInstantiate(&graph_, g, nullptr, nullptr, 0) == hipSuccess;
+        if (g) (void)hipGraphDestroy(g);
+        if (!ok) {  // eager launches from now on (the capture queued nothing)
+            (void)hipGetLastError();
+            graph_ = nullptr;
+            graph_failed_ = true;
+        } else {
+            graph_rf_ = rf_;
+            graph_chunk_ = chunk_;
+        }
+    }
+    if (graphable && graph_) {
+        hip_ok(hipGraphLaunch(graph_, stream_), "hipGraphLaunch");
+        host_sweep_ += chunk_;
+    } else {
+        for (int i = 0; i < chunk_; ++i) sweep();
+        warm_chunk_ = true;
+    }
+}
+
 void MultiFrameEngine::refill() {
     const int NF = nf_;
     float* D = buf_.get();
@@ -375,67 +446,29 @@ void MultiFrameEngine::stage(int64_t first, int64_t e0, int k, const FrameSource
     if (k <= 0) return;
     if (k > NF) throw std::logic_error("MultiFrameEngine::stage: at most nf frames per call");
     RoctxRange r("sart::mf_stage");
-    for (int j = 0; j < k; ++j) src(first + e0 + j, hg_.data() + (size_t)j * P_);
-    // per-frame maxima and positive sums of squares over all ranks' pixels (reference sartsolver_cuda.cpp:146-157)
-    double mx[kMfMaxFrames], gs[kMfMaxFrames];
-    auto scan = [&](int j) {  // one frame, pixels in order (the sum is deterministic whatever thread runs it)
-        double m = -std::numeric_limits<double>::infinity(), s = 0.0;
-        double* g = hg_.data() + (size_t)j * P_;
-        for (int64_t p = 0; p < P_; ++p) {
-            double v = g[p];
-            if (!std::isfinite(v)) v = -1.0;  // non-finite pixel: masked like a saturated one
-            g[p] = v;
-            m = std::max(m, v);
-            if (v > 0) s += v * v;
-        }
-        mx[j] = m, gs[j] = s;
-    };
-    MfPublish pub{};
-    pub.n = k;
-    pub.e0 = e0;
-    auto normalise = [&](int j) {  // ghat = (float)(g / s) (k_mf_prep_slots' arithmetic, on the host)
-        const double s = pub.norm[j];
-        const double* g = hg_.data() + (size_t)j * P_;
-        float* out = hq_ + (size_t)((e0 + j) % qcap_) * Pp_;
-        for (int64_t p = 0; p < P_; ++p) out[p] = (float)(g[p] / s);
-    };
-    // frames on host threads when the batch is large (64 frames x 245760 pixels: 12 ms on one thread)
-    const int nth = (int)std::min<int64_t>({k, 8, std::max<int64_t>(1, (int64_t)k * P_ / (1 << 20))});
-    auto par = [&](const std::function<void(int)>& fn) {
-        if (nth > 1) {
-            std::vector<std::thread> pool;
-            for (int t = 0; t < nth; ++t)
-                pool.emplace_back([&, t] {
-                    for (int j = t; j < k; j += nth) fn(j);
-                });
-            for (auto& th : pool) th.join();
-        } else {
-            for (int j = 0; j < k; ++j) fn(j);
-        }
-    };
-    par(scan);
-    comm_->host().all_reduce_host(mx, k, ReduceOp::kMax);
-    comm_->host().all_reduce_host(gs, k, ReduceOp::kSum);
-    for (int j = 0; j < k; ++j) {
-        pub.frame[j] = (int32_t)(first + e0 + j);
-        pub.cold[j] = cold ? 1 : 0;
-        pub.norm[j] = mx[j] > 0 ? mx[j] : 1.0;
-        pub.G[j] = gs[j] / (pub.norm[j] * pub.norm[j]);
-        if (!(pub.G[j] > 0)) pub.G[j] = 1.0;
-    }
-    par(normalise);
-    // normalised pixels into the queue on the copy stream (one or two runs of ring positions), next to the sweeps
+    // the frames' raw pixels straight into the pinned queue rows, then to the device on the copy stream (one or two
+    // runs of ring positions), next to the sweeps; normalisation and scalars on the device (k_mf_stage_*)
+    const auto ts = std::chrono::steady_clock::now();
+    for (int j = 0; j < k; ++j) src(first + e0 + j, hg64_ + (size_t)((e0 + j) % qcap_) * Pp_);
+    stats_.host_src_ms += ms_since(ts);
     for (int j = 0; j < k;) {
         const int pos = (int)((e0 + j) % qcap_);
         const int run = std::min(k - j, qcap_ - pos);
         if (P_)
-            hip_ok(hipMemcpyAsync(ghq_.get() + (size_t)pos * Pp_, hq_ + (size_t)pos * Pp_, (size_t)run * Pp_ * sizeof(float),
-                                  hipMemcpyHostToDevice, copy_stream_),
+            hip_ok(hipMemcpyAsync(g64q_.get() + (size_t)pos * Pp_, hg64_ + (size_t)pos * Pp_,
+                                  (size_t)run * Pp_ * sizeof(double), hipMemcpyHostToDevice, copy_stream_),
                    "H2D queue");
         j += run;
     }
     hip_ok(hipEventRecord(ev_stage_, copy_stream_), "event");
     hip_ok(hipStreamWaitEvent(stream_, ev_stage_, 0), "wait staging");
+    // per-frame maxima and positive sums of squares over all ranks' pixels (reference sartsolver_cuda.cpp:146-157)
+    launch_mf_stage_stats(g64q_.get(), e0, qcap_, k, P_, Pp_, sstats_.get(), NF, stream_);
+    if (comm_->size() > 1) {
+        comm_->all_reduce(sstats_.get(), (size_t)k, ReduceOp::kMax, stream_);
+        comm_->all_reduce(sstats_.get() + NF, (size_t)k, ReduceOp::kSum, stream_);
+    }
+    launch_mf_stage_norm(q_.get(), g64q_.get(), ghq_.get(), sstats_.get(), e0, first + e0, cold, k, P_, Pp_, NF, stream_);
     if (cold || cfg_.logarithmic) {
         // one batched back-projection of the k staged frames (columns 0 .. k - 1): cold starts
         // x0 = max([rho > tau] A^T max(ghat, 0) / rho, 1e-7) (reference sart_kernels.cu:22-60) and / or the
@@ -457,7 +490,7 @@ void MultiFrameEngine::stage(int64_t first, int64_t e0, int k, const FrameSource
             launch_mf_stage_cols(buf_.get(), nullptr, e0, qcap_, k, V_, ld_, NF, oq_.get(), stream_);
         }
     }
-    launch_mf_publish(q_.get(), pub, stream_);
+    launch_mf_publish(q_.get(), e0 + k, stream_);
 }
 
 std::vector<SolveInfo> MultiFrameEngine::solve_batch(const double* g, int nframes, double* x_out, const double* x0,
@@ -558,8 +591,9 @@ bool MultiFrameEngine::series_once(int64_t first, int64_t nframes, const FrameSo
     stats_.lead = chain && !x0 && lead_;
 
     int64_t staged = 0;
-    auto stage_upto = [&](int64_t head) {  // stage while the queue has room for a unit (nf with a back-projection)
-        while (staged < n) {
+    // stage while the queue has room for a unit (nf with a back-projection), up to `limit` frames
+    auto stage_upto = [&](int64_t head, int64_t limit) {
+        while (staged < std::min(n, limit)) {
             // the first nf frames start from x0 (or cold without it); later ones cold (!chain) or chained
             const bool cold = chain ? (!x0 && staged < NF) : (!x0 || staged >= NF);
             const int64_t lim = staged < NF ? NF - staged : NF;  // no unit straddles frame nf
@@ -568,19 +602,18 @@ bool MultiFrameEngine::series_once(int64_t first, int64_t nframes, const FrameSo
                                                             : std::max<int64_t>(1, std::min<int64_t>(NF / 4, n - staged));
             if (room < unit) return;
             const int k = (int)std::min<int64_t>({room, lim, n - staged});
+            const auto ts = std::chrono::steady_clock::now();
             stage(first, staged, k, src, cold);
+            stats_.host_stage_ms += ms_since(ts);
             staged += k;
         }
     };
-    stage_upto(0);
+    stage_upto(0, NF);  // the first nf frames: the first chunk starts as soon as they are read; the rest next to it
     refill();
 
     int issued = 0, checked = 0;
     auto issue = [&]() {
-        {
-            RoctxRange r("sart::mf_chunk");
-            for (int i = 0; i < chunk_; ++i) sweep();
-        }
+        run_chunk();
         const int slot = issued & 1;
         hip_ok(hipMemcpyAsync(&hsnap_[slot].st, st_.get(), sizeof(MfState), hipMemcpyDeviceToHost, stream_), "D2H state");
         hip_ok(hipMemcpyAsync(&hsnap_[slot].q, q_.get(), sizeof(MfQueue), hipMemcpyDeviceToHost, stream_), "D2H queue");
@@ -591,55 +624,109 @@ bool MultiFrameEngine::series_once(int64_t first, int64_t nframes, const FrameSo
         MfFinish log;
         int pos;
     };
-    std::vector<Pending> pend;
-    std::vector<double> x(std::max<int64_t>(V_, 1));
-    int64_t seen_fin = 0, finished = 0, warm_age = 0;
-    auto finalize = [&]() {
-        for (const Pending& pd : pend) {
-            const MfFinish& L = pd.log;
-            const float* hs = hx_ + (size_t)pd.pos * ld_;
-            for (int64_t v = 0; v < V_; ++v) x[v] = (double)hs[v] * L.norm;
-            ++finished;
-            stats_.busy_slot_sweeps += L.iters + 1;
-            stats_.mean_iterations += L.iters;
-            if (L.warm_from >= 0) ++stats_.chained, warm_age += (L.frame - L.warm_from);
-            if (L.frame < 0 || L.frame >= nframes || delivered[L.frame]) continue;
-            SolveInfo info;
-            info.status = L.status;
-            info.iterations = L.iters;
-            info.convergence = L.conv;
-            info.nonfinite = (L.flags & 1) != 0;
-            info.used_fused = false;
-            info.warm_from = L.warm_from;
-            info.warm_iter = L.warm_iter;
-            info.comm_fallbacks = attempt;
-            info.comm = comm_->backend();
-            info.sweeps = L.iters + 1;
-            frame_norm_[L.frame] = L.norm;
-            delivered[L.frame] = 1;
-            sink(L.frame, x.data(), info);
-            if (L.frame > newest_frame && !info.nonfinite) {
-                newest.assign(x.begin(), x.begin() + V_);
-                newest_frame = L.frame;
+    // Delivery thread: finished frames are de-normalised and handed to the sink (the driver's writer) next to the
+    // series thread, which only issues chunks, stages frames and queues the output-ring copies (at ~2000 sparse
+    // frames/s the sink alone took a third of the series thread's time, profiles/series_r6_sparse*).
+    struct Batch {
+        hipEvent_t ev;  // the batch's copies into hx_
+        std::vector<Pending> items;
+    };
+    std::mutex dm;
+    std::condition_variable dcv;
+    std::deque<Batch> dq;
+    bool dstop = false;
+    std::exception_ptr derr;
+    int64_t dcount = 0, warm_age = 0;  // entries delivered (FIFO: entries [0, dcount) are done with hx_)
+    std::thread deliver([&] {
+        try {
+            hip_ok(hipSetDevice(device_), "hipSetDevice");
+            std::vector<double> x(std::max<int64_t>(V_, 1));
+            for (;;) {
+                Batch b;
+                {
+                    std::unique_lock<std::mutex> lk(dm);
+                    dcv.wait(lk, [&] { return dstop || !dq.empty(); });
+                    if (dq.empty()) return;
+                    b = std::move(dq.front());
+                    dq.pop_front();
+                }
+                const auto tw = std::chrono::steady_clock::now();
+                const hipError_t se = hipEventSynchronize(b.ev);
+                (void)hipEventDestroy(b.ev);
+                hip_ok(se, "mf copy");
+                for (const Pending& pd : b.items) {
+                    const MfFinish& L = pd.log;
+                    const float* hs = hx_ + (size_t)pd.pos * ld_;
+                    for (int64_t v = 0; v < V_; ++v) x[v] = (double)hs[v] * L.norm;
+                    stats_.busy_slot_sweeps += L.iters + 1;
+                    stats_.mean_iterations += L.iters;
+                    if (L.warm_from >= 0) ++stats_.chained, warm_age += (L.frame - L.warm_from);
+                    if (L.frame < 0 || L.frame >= nframes || delivered[L.frame]) continue;
+                    SolveInfo info;
+                    info.status = L.status;
+                    info.iterations = L.iters;
+                    info.convergence = L.conv;
+                    info.nonfinite = (L.flags & 1) != 0;
+                    info.used_fused = false;
+                    info.warm_from = L.warm_from;
+                    info.warm_iter = L.warm_iter;
+                    info.warm_live = L.warm_live != 0;
+                    info.comm_fallbacks = attempt;
+                    info.comm = comm_->backend();
+                    info.sweeps = L.iters + 1;
+                    frame_norm_[L.frame] = L.norm;
+                    delivered[L.frame] = 1;
+                    sink(L.frame, x.data(), info);
+                    if (L.frame > newest_frame && !info.nonfinite) {
+                        newest.assign(x.begin(), x.begin() + V_);
+                        newest_frame = L.frame;
+                    }
+                }
+                stats_.host_deliver_ms += ms_since(tw);
+                std::lock_guard<std::mutex> lk(dm);
+                dcount += (int64_t)b.items.size();
+                dcv.notify_all();
             }
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(dm);
+            derr = std::current_exception();
+            dcv.notify_all();
         }
-        pend.clear();
+    });
+    struct JoinDelivery {  // also on an exception of the series thread (a source that throws, a HIP error)
+        std::thread& t;
+        std::mutex& m;
+        std::condition_variable& cv;
+        bool& stop;
+        std::deque<Batch>& q;
+        ~JoinDelivery() {
+            {
+                std::lock_guard<std::mutex> lk(m);
+                stop = true;
+            }
+            cv.notify_all();
+            if (t.joinable()) t.join();
+            for (Batch& b : q) (void)hipEventDestroy(b.ev);
+        }
+    } join_delivery{deliver, dm, dcv, dstop, dq};
+    auto check_delivery = [&]() {
+        std::lock_guard<std::mutex> lk(dm);
+        if (derr) std::rethrow_exception(derr);
     };
     issue();
+    stage_upto(0, n);
     issue();
     bool failed = false;
-    while (finished < n) {
-        if (!pend.empty()) {  // the solutions copied at the previous check
-            hip_ok(hipEventSynchronize(ev_copy_), "mf copy");
-            finalize();
-            if (finished >= n) break;
-        }
+    int64_t seen_fin = 0;
+    while (seen_fin < n) {
+        check_delivery();
         if (checked >= issued) throw std::runtime_error("MultiFrameEngine: no chunk in flight and frames unfinished");
         const int c = checked++;
+        const auto tw = std::chrono::steady_clock::now();
         hip_ok(hipEventSynchronize(ev_[c & 1]), "mf chunk");
+        stats_.host_wait_ms += ms_since(tw);
         const MfQueue& Q = hsnap_[c & 1].q;
         const int64_t fin = Q.fin, head = Q.q_head;
-        const int sweeps = hsnap_[c & 1].st.sweep;
         std::vector<Pending> fresh;
         for (int64_t e = seen_fin; e < fin; ++e) {
             const int pos = (int)(e % rcap_);
@@ -649,26 +736,45 @@ bool MultiFrameEngine::series_once(int64_t first, int64_t nframes, const FrameSo
             failed = true;
             break;
         }
-        for (const Pending& pd : fresh) {  // solutions from the output ring, behind the chunk that wrote them
-            hip_ok(hipMemcpyAsync(hx_ + (size_t)pd.pos * ld_, ring_.get() + (size_t)pd.pos * ld_, V_ * sizeof(float),
-                                  hipMemcpyDeviceToHost, stream_),
-                   "D2H x");
-            pend.push_back(pd);
-        }
         if (!fresh.empty()) {
+            {  // hx_ position of entry e is free once entry e - rcap has been delivered
+                const auto tw2 = std::chrono::steady_clock::now();
+                std::unique_lock<std::mutex> lk(dm);
+                dcv.wait(lk, [&] { return derr || fin - 1 - rcap_ < dcount; });
+                if (derr) std::rethrow_exception(derr);
+                stats_.host_wait_ms += ms_since(tw2);
+            }
+            // solutions from the output ring on the copy stream (the chunk that wrote them has completed: its
+            // snapshot was read), next to the sweeps; the ring positions are free again once the copies are done
+            for (const Pending& pd : fresh)
+                hip_ok(hipMemcpyAsync(hx_ + (size_t)pd.pos * ld_, ring_.get() + (size_t)pd.pos * ld_,
+                                      V_ * sizeof(float), hipMemcpyDeviceToHost, copy_stream_),
+                       "D2H x");
             seen_fin = fin;
-            launch_mf_drained(q_.get(), seen_fin, stream_);  // the ring positions are free again after the copies
-            hip_ok(hipEventRecord(ev_copy_, stream_), "event");
+            Batch b;
+            hip_ok(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming), "hipEventCreate");
+            hip_ok(hipEventRecord(b.ev, copy_stream_), "event");
+            hip_ok(hipStreamWaitEvent(stream_, b.ev, 0), "wait ring copies");
+            launch_mf_drained(q_.get(), seen_fin, stream_);
+            b.items = std::move(fresh);
+            std::lock_guard<std::mutex> lk(dm);
+            dq.push_back(std::move(b));
+            dcv.notify_all();
         }
-        stage_upto(head);
-        stats_.sweeps = sweeps;
+        stage_upto(head, n);
         if (fin < n) issue();  // frames left to finish on the device (a chunk still in flight may finish them)
     }
+    {  // every handed-over frame delivered (or the delivery failed)
+        std::unique_lock<std::mutex> lk(dm);
+        dcv.wait(lk, [&] { return derr || dcount >= seen_fin; });
+    }
+    check_delivery();
     hip_ok(hipStreamSynchronize(stream_), "mf series");
     if (comm_stream_) hip_ok(hipStreamSynchronize(comm_stream_), "mf comm");
     hip_ok(hipStreamSynchronize(copy_stream_), "mf copy stream");
     if (!failed) {
         const MfState& S = hsnap_[(issued - 1) & 1].st;
+        const int64_t finished = dcount;
         stats_.sweeps = S.sweep;
         stats_.queued_sweeps = (int64_t)issued * chunk_;
         stats_.frames = finished;

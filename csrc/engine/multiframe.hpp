@@ -58,6 +58,9 @@ class MultiFrameEngine {
     struct SeriesStats {
         int64_t frames = 0, sweeps = 0, queued_sweeps = 0, busy_slot_sweeps = 0, chained = 0;
         double slot_util = 0.0, mean_iterations = 0.0, mean_warm_age = 0.0, ms = 0.0;
+        // host time of the series thread: waiting for the GPU (chunk / copy events), staging frames (of which in
+        // the source callback: reading), delivering finished frames (de-normalisation and the sink)
+        double host_wait_ms = 0.0, host_stage_ms = 0.0, host_src_ms = 0.0, host_deliver_ms = 0.0;
         int chunk = 0, admit_cap = 0, src_age = 0, restarts = 0;
         bool src_finished = false, lead = false;
         double src_extrap = 0.0;
@@ -91,6 +94,10 @@ class MultiFrameEngine {
     // reference sartsolver_cuda.cpp:231-262 runs max_iter back-projections after the initial guess)
     void sweep();
     void refill();  // the plan, start values and pixel columns without a sweep (the first admissions)
+    // chunk_ sweeps: replayed from a HIP graph captured after one eager chunk (one rank, no fault injection;
+    // re-captured when the refill buffers change; SART_MF_GRAPH=0: eager launches)
+    void run_chunk();
+    void drop_graph();
     void set_device() const;
     // F = A X (Fs_ split-K partials); the bf16 engine first writes the X planes
     void forward();
@@ -148,6 +155,10 @@ class MultiFrameEngine {
     // [qcap][ld] when staged), output ring ring_ [rcap][ld], xlast_ [ld], and the plan state q_
     int qcap_ = 32, rcap_ = 32, chunk_ = 4, admit_cap_ = 0, src_age_ = 0;
     bool src_finished_ = false, lead_ = true;
+    hipGraphExec_t graph_ = nullptr;
+    MfRefill graph_rf_{};
+    int graph_chunk_ = 0;
+    bool use_graph_ = true, graph_failed_ = false, warm_chunk_ = false;
     double src_extrap_ = 0.0;
     DeviceArray<MfQueue> q_;
     DeviceArray<float> ghq_, x0q_, oq_, ring_, xlast_, starts_;
@@ -159,8 +170,8 @@ class MultiFrameEngine {
     };
     Snap* hsnap_ = nullptr;      // pinned [2]: state after each of the two chunks in flight
     hipEvent_t ev_[2] = {nullptr, nullptr};
-    std::vector<double> hg_;     // [nf][rows] frames being staged (fp64, as read)
-    float* hq_ = nullptr;        // pinned [qcap][Pp]: normalised pixels of the queue (H2D source)
+    double* hg64_ = nullptr;     // pinned [qcap][Pp]: the queue's raw pixels (the source writes them here; H2D source)
+    DeviceArray<double> g64q_, sstats_;  // device copy [qcap][Pp]; per-frame max / sum of squares [2][nf]
     float* hx_ = nullptr;        // pinned [rcap][ld]: solutions of finished frames (D2H target)
     hipStream_t copy_stream_ = nullptr;
     hipEvent_t ev_copy_ = nullptr, ev_stage_ = nullptr;

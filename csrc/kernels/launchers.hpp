@@ -313,7 +313,13 @@ void launch_mf_stage_ops(const float* ghq, int64_t e0, int qcap, int k, int64_t 
 // max(D dinv, 1e-7) with dinv, else copies
 void launch_mf_stage_cols(const float* D, const float* dinv, int64_t e0, int qcap, int k, int64_t nvox, int64_t ld,
                           int nf, float* out, hipStream_t stream);
-void launch_mf_publish(MfQueue* q, const MfPublish& p, hipStream_t stream);
+// staging on the device: raw fp64 pixels g64q [qcap][nrows_pad] of k entries -> per-frame max / positive sum of squares
+// (stats [2][nf], all-reduced by the caller) -> the queue metadata and the normalised pixels ghq [qcap][nrows_pad]
+void launch_mf_stage_stats(const double* g64q, int64_t e0, int qcap, int k, int64_t nrows, int64_t nrows_pad,
+                           double* stats, int nf, hipStream_t stream);
+void launch_mf_stage_norm(MfQueue* q, const double* g64q, float* ghq, const double* stats, int64_t e0, int64_t frame0,
+                          bool cold, int k, int64_t nrows, int64_t nrows_pad, int nf, hipStream_t stream);
+void launch_mf_publish(MfQueue* q, int64_t q_tail, hipStream_t stream);
 void launch_mf_drained(MfQueue* q, int64_t drained, hipStream_t stream);
 void launch_mf_queue_begin(MfQueue* q, int qcap, int rcap, bool chain, int admit_cap, int src_age, int64_t x0_below,
                            bool src_finished, bool lead, float src_extrap, hipStream_t stream);

@@ -233,6 +233,7 @@ __device__ void mf_plan(MfState* __restrict__ st, MfQueue* __restrict__ q, int s
         L.flags = (nonfin ? 1 : 0) | (rb ? 2 : 0);
         L.warm_from = q->slot_warm_from[f];
         L.warm_iter = q->slot_warm_iter[f];
+        L.warm_live = q->slot_warm_live[f];
         L.conv = st->conv[f];
         L.norm = q->slot_norm[f];
         q->ret_pos[f] = pos;
@@ -271,6 +272,7 @@ __device__ void mf_plan(MfState* __restrict__ st, MfQueue* __restrict__ q, int s
         const bool chained = kind == kSrcSlot || kind == kSrcLast;
         q->slot_warm_from[f] = chained ? best : -1;
         q->slot_warm_iter[f] = chained ? s_iter : -1;
+        q->slot_warm_live[f] = chained && s_kind == kSrcSlot ? s_live : 0;
         st->G[f] = q->q_G[pos];
         st->conv_prev[f] = 0.0;
         st->conv[f] = 0.0;
@@ -664,18 +666,68 @@ __global__ __launch_bounds__(256) void k_mf_stage_cols(const float* __restrict__
     out[((e0 + j) % qcap) * ld + v] = x;
 }
 
-// Entries [e0, e0 + n) become visible to the plan: their metadata, then q_tail.
-__global__ void k_mf_publish(MfQueue* __restrict__ q, MfPublish p) {
-    const int j = threadIdx.x;
-    if (j < p.n) {
-        const int pos = (int)((p.e0 + j) % q->qcap);
-        q->q_frame[pos] = p.frame[j];
-        q->q_cold[pos] = p.cold[j];
-        q->q_norm[pos] = p.norm[j];
-        q->q_G[pos] = p.G[j];
+// Staging on the device (the host only copies the frames' raw pixels in): per staged frame j (one block each) the
+// maximum and the sum of squares of the positive pixels over this rank's rows (non-finite pixels count as -1, masked
+// like saturated ones; reference sartsolver_cuda.cpp:146-157), in a fixed order (deterministic): stats[j] (max) and
+// stats[nf + j] (sum), all-reduced over the ranks by the caller.
+__global__ __launch_bounds__(1024) void k_mf_stage_stats(const double* __restrict__ g64q, int64_t e0, int qcap,
+                                                         int64_t nrows, int64_t nrows_pad, double* __restrict__ stats,
+                                                         int nf) {
+    __shared__ double rm[1024], rs[1024];
+    const int j = blockIdx.x;
+    const double* g = g64q + ((e0 + j) % qcap) * nrows_pad;
+    double m = -INFINITY, s = 0.0;
+    for (int64_t r = threadIdx.x; r < nrows; r += 1024) {
+        double v = g[r];
+        if (!isfinite(v)) v = -1.0;
+        m = fmax(m, v);
+        if (v > 0) s += v * v;
     }
+    rm[threadIdx.x] = m, rs[threadIdx.x] = s;
     __syncthreads();
-    if (j == 0) q->q_tail = p.e0 + p.n;
+    for (int w = 512; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            rm[threadIdx.x] = fmax(rm[threadIdx.x], rm[threadIdx.x + w]);
+            rs[threadIdx.x] += rs[threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) stats[j] = rm[0], stats[nf + j] = rs[0];
+}
+
+// The staged frames' normalisation s = max(g) (1 if not positive) and G = sum_{g>0} g^2 / s^2 (1 if not positive)
+// into the queue's metadata, with the frame index frame0 + j and the cold-start flag; ghq = (float)(g / s) (the
+// arithmetic of the oracle and of the single-frame engine's prep). Grid (row blocks, k).
+__global__ __launch_bounds__(256) void k_mf_stage_norm(MfQueue* __restrict__ q, const double* __restrict__ g64q,
+                                                       float* __restrict__ ghq, const double* __restrict__ stats,
+                                                       int64_t e0, int64_t frame0, int cold, int64_t nrows,
+                                                       int64_t nrows_pad, int nf) {
+    const int j = blockIdx.y;
+    const int pos = (int)((e0 + j) % q->qcap);
+    const double mx = stats[j];
+    const double norm = mx > 0 ? mx : 1.0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        double G = stats[nf + j] / (norm * norm);
+        if (!(G > 0)) G = 1.0;
+        q->q_norm[pos] = norm;
+        q->q_G[pos] = G;
+        q->q_frame[pos] = (int32_t)(frame0 + j);
+        q->q_cold[pos] = cold;
+    }
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= nrows_pad) return;
+    float gh = 0.f;
+    if (r < nrows) {
+        double v = g64q[(int64_t)pos * nrows_pad + r];
+        if (!isfinite(v)) v = -1.0;
+        gh = (float)(v / norm);
+    }
+    ghq[(int64_t)pos * nrows_pad + r] = gh;
+}
+
+// Entries below q_tail become visible to the plan (their metadata was written by k_mf_stage_norm before).
+__global__ void k_mf_publish(MfQueue* __restrict__ q, int64_t q_tail) {
+    if (threadIdx.x == 0) q->q_tail = q_tail;
 }
 
 __global__ void k_mf_drained(MfQueue* __restrict__ q, int64_t drained) {
@@ -688,6 +740,7 @@ __global__ void k_mf_queue_begin(MfQueue* __restrict__ q, int qcap, int rcap, in
     if (f < kMaxNF) {
         q->slot_frame[f] = -1;
         q->slot_warm_from[f] = q->slot_warm_iter[f] = -1;
+        q->slot_warm_live[f] = 0;
         q->slot_norm[f] = 1.0;
         q->ret_pos[f] = q->adm_pos[f] = -1;
         q->ret_prev[f] = 0;
@@ -794,9 +847,29 @@ void launch_mf_stage_cols(const float* D, const float* dinv, int64_t e0, int qca
     check_launch("k_mf_stage_cols");
 }
 
-void launch_mf_publish(MfQueue* q, const MfPublish& p, hipStream_t stream) {
-    if (p.n < 0 || p.n > kMaxNF) throw std::runtime_error("mf_publish: at most 128 entries per call");
-    hipLaunchKernelGGL(k_mf_publish, dim3(1), dim3(kMaxNF), 0, stream, q, p);
+void launch_mf_stage_stats(const double* g64q, int64_t e0, int qcap, int k, int64_t nrows, int64_t nrows_pad,
+                           double* stats, int nf, hipStream_t stream) {
+    check_nf(nf, "mf_stage_stats");
+    if (k < 0 || k > nf || qcap < k) throw std::runtime_error("mf_stage_stats: 0 <= k <= nf, k <= qcap");
+    if (k == 0) return;
+    hipLaunchKernelGGL(k_mf_stage_stats, dim3((unsigned)k), dim3(1024), 0, stream, g64q, e0, qcap, nrows, nrows_pad,
+                       stats, nf);
+    check_launch("k_mf_stage_stats");
+}
+
+void launch_mf_stage_norm(MfQueue* q, const double* g64q, float* ghq, const double* stats, int64_t e0, int64_t frame0,
+                          bool cold, int k, int64_t nrows, int64_t nrows_pad, int nf, hipStream_t stream) {
+    check_nf(nf, "mf_stage_norm");
+    if (k < 0 || k > nf) throw std::runtime_error("mf_stage_norm: 0 <= k <= nf");
+    if (k == 0) return;
+    const dim3 grid((unsigned)std::max<int64_t>(1, (nrows_pad + 255) / 256), (unsigned)k);
+    hipLaunchKernelGGL(k_mf_stage_norm, grid, dim3(256), 0, stream, q, g64q, ghq, stats, e0, frame0, cold ? 1 : 0,
+                       nrows, nrows_pad, nf);
+    check_launch("k_mf_stage_norm");
+}
+
+void launch_mf_publish(MfQueue* q, int64_t q_tail, hipStream_t stream) {
+    hipLaunchKernelGGL(k_mf_publish, dim3(1), dim3(64), 0, stream, q, q_tail);
     check_launch("k_mf_publish");
 }
 

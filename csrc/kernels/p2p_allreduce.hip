@@ -87,7 +87,11 @@ __global__ __launch_bounds__(256) void k_p2p_allreduce(const float* in, float* o
     }
     const int64_t mine = (int64_t)(parity * kP2pMaxRanks + rank) * cap;  // my slot in every receive buffer
 
-    // RED: the chunk holding [ld] and [ld + 1] (never split: chunks are multiples of 1024, ld of 64) sums Fpart first
+    // RED: the chunk holding [ld] and [ld + 1] (never split: chunks are multiples of 1024, ld of 64) sums Fpart first.
+    // With the fused update (UPD != 0) EVERY workgroup sums the nF partials to get this rank's tail values for its
+    // decision: blocks x nF fp64 loads, all L2 hits after the first workgroup (dense fused grid: nF <= 512; a sparse
+    // 64k-row shard: ~2k, i.e. ~16 KiB per workgroup, a few microseconds per sweep over the whole grid). Reading the
+    // own tail from the receive slot instead would make every workgroup wait for the tail chunk's flag first.
     __shared__ float tailv[2];
     if constexpr (RED) {
         if (UPD != 0 || (c0 <= src.ld && src.ld < c1)) {  // uniform over the workgroup

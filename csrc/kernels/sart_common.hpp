@@ -79,6 +79,7 @@ enum MfSrc : int32_t {
 struct MfFinish {      // one finished frame in the output ring (read by the host from the state snapshot)
     int32_t frame, status, iters, flags;  // flags: bit 0 non-finite, bit 1 rolled back to the last finite iterate
     int32_t warm_from, warm_iter;         // the start value's frame and its update count (-1: x0 / cold)
+    int32_t warm_live, pad;               // that frame was still in flight (its iterate extrapolated, src_extrap)
     double conv, norm;
 };
 struct alignas(16) MfQueue {
@@ -99,7 +100,7 @@ struct alignas(16) MfQueue {
     int32_t src_kind, src_slot, src_frame, src_iter;  // the chain source of this sweep's admissions
     double src_norm;
     int32_t slot_frame[kMfMaxFrames];  // frame in each slot (-1: empty)
-    int32_t slot_warm_from[kMfMaxFrames], slot_warm_iter[kMfMaxFrames];
+    int32_t slot_warm_from[kMfMaxFrames], slot_warm_iter[kMfMaxFrames], slot_warm_live[kMfMaxFrames];
     double slot_norm[kMfMaxFrames];
     int32_t ret_pos[kMfMaxFrames];    // output ring position written at this sweep (-1), from X or Xprev (ret_prev)
     int32_t ret_prev[kMfMaxFrames];
@@ -109,13 +110,6 @@ struct alignas(16) MfQueue {
     int32_t q_cold[kMfQueueMax];
     double q_norm[kMfQueueMax], q_G[kMfQueueMax];
     MfFinish log[kMfQueueMax];        // per output ring position
-};
-// Entries [e0, e0 + n) of the queue become visible to the plan (the publish kernel's argument, by value)
-struct MfPublish {
-    int n;
-    int64_t e0;
-    int32_t frame[kMfMaxFrames], cold[kMfMaxFrames];
-    double norm[kMfMaxFrames], G[kMfMaxFrames];
 };
 // Device buffers of the refill (k_mf_update with a queue): output ring [rcap][ld], xlast [ld], host x0 (fp64 [nvox]),
 // staged cold starts and observed back-projections [qcap][ld] (null when not staged), optional start-value record

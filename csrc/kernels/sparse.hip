@@ -279,9 +279,10 @@ void launch_mf_sparse_backproject(const SparseRtm& s, int64_t nvoxel, const floa
 }
 
 int sparse_lanes(double avg) {
-    if (const char* e = std::getenv("SART_SPARSE_LANES"); e && *e) {
+    if (const char* e = std::getenv("SART_SPARSE_LANES"); e && *e) {  // (an A/B knob: a typo must not run the default)
         const int l = std::atoi(e);
         if (l == 4 || l == 8 || l == 16 || l == 32) return l;
+        throw std::runtime_error(std::string("SART_SPARSE_LANES must be 4, 8, 16 or 32, not '") + e + "'");
     }
     // the largest group with >= 4 entries per lane (one unrolled step of gather_dot), 4 .. 32 lanes: rows of ~48
     // entries run best on 8 lanes (27.3k it/s at 64k x 64k; 4 / 16 / 32 lanes: 24.1k / 25.8k / 21.1k;

@@ -203,6 +203,23 @@ void h5_read_frame_f64(hid_t dset, uint64_t index, double* out, uint64_t frame_s
     check(H5Dread(dset, H5T_NATIVE_DOUBLE, msp, fsp, H5P_DEFAULT, out), "reading image frame");
 }
 
+static void read_range(hid_t dset, uint64_t off, uint64_t n, hid_t memtype, void* out) {
+    if (n == 0) return;
+    H5Id fsp(H5Dget_space(dset), H5Id::kSpace);
+    hsize_t o = off, c = n;
+    check(H5Sselect_hyperslab(fsp, H5S_SELECT_SET, &o, nullptr, &c, nullptr), "selecting a range");
+    H5Id msp(H5Screate_simple(1, &c, nullptr), H5Id::kSpace);
+    check(H5Dread(dset, memtype, msp, fsp, H5P_DEFAULT, out), "reading a range");
+}
+
+void h5_read_range_u64(hid_t dset, uint64_t off, uint64_t n, uint64_t* out) {
+    read_range(dset, off, n, H5T_NATIVE_UINT64, out);
+}
+
+void h5_read_range_f32(hid_t dset, uint64_t off, uint64_t n, float* out) {
+    read_range(dset, off, n, H5T_NATIVE_FLOAT, out);
+}
+
 H5Id h5_create_group(hid_t loc, const std::string& path) {
     hid_t g = H5Gcreate2(loc, path.c_str(), H5P_DEFAULT, H5P_DEFAULT, H5P_DEFAULT);
     if (g < 0) throw Error("Unable to create HDF5 group " + path + ".");

@@ -89,6 +89,9 @@ void h5_read_block_f32(hid_t dset, uint64_t row0, uint64_t nrows, uint64_t fcol0
                        uint64_t ld, uint64_t col0);
 // One [1, H, W] slab of a 3-D dataset as doubles.
 void h5_read_frame_f64(hid_t dset, uint64_t index, double* out, uint64_t frame_size);
+// elements [off, off + n) of a 1-D dataset (hyperslab reads of the sparse RTM's COO arrays in bounded chunks)
+void h5_read_range_u64(hid_t dset, uint64_t off, uint64_t n, uint64_t* out);
+void h5_read_range_f32(hid_t dset, uint64_t off, uint64_t n, float* out);
 
 // Writers (used by the solution writer, the voxel-map copy and the test-fixture writers).
 H5Id h5_create_group(hid_t loc, const std::string& path);

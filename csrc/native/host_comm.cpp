@@ -199,6 +199,10 @@ std::unique_ptr<HostComm> make_tcp_host_comm(int rank, int size, const std::stri
 }
 
 std::unique_ptr<HostComm> host_comm_from_env(double timeout_s) {
+    if (timeout_s < 0) {
+        const char* e = std::getenv("SART_HOST_TIMEOUT_S");
+        timeout_s = (e && *e && std::atof(e) > 0) ? std::atof(e) : 1800.0;
+    }
     if (mpi_launch_detected()) return make_mpi_host_comm();
     const EnvWorld w = env_world();
     if (w.size <= 1) return make_local_host_comm();

@@ -55,7 +55,10 @@ std::string mpi_library_version();
 // SART_HOST_COMM=mpi, or an MPI launcher (PMI_SIZE or OMPI_COMM_WORLD_SIZE > 1 without torchrun's RANK).
 bool mpi_launch_detected();
 // MPI when mpi_launch_detected(); else local for one rank, TCP otherwise (SART_HOST_COMM=tcp forces TCP).
-std::unique_ptr<HostComm> host_comm_from_env(double timeout_s = 3600.0);
+// timeout_s < 0: SART_HOST_TIMEOUT_S, default 1800 s -- every TCP send / receive / accept of the host collectives is
+// bounded by it (a peer that died or never came is an error on every rank, not a hang; rank 0 writing output between
+// frames is far below it)
+std::unique_ptr<HostComm> host_comm_from_env(double timeout_s = -1.0);
 
 // Balanced 1-D block partition (reference main.cpp:67-68): the first n % parts parts get one more.
 struct Block {

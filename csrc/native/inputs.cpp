@@ -1,6 +1,7 @@
 #include "inputs.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <limits>
 #include <numeric>
@@ -384,12 +385,24 @@ void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, ui
     RtmReader(sorted, rtm_name, nvoxel).read(row_begin, row_end, out, ld);
 }
 
+// Bounded-memory CSR reader. Camera by camera (cameras own disjoint row ranges), every voxel segment becomes a CSR
+// over the camera's rows of the shard: sparse (COO) datasets by a count pass and a fill pass over hyperslab chunks
+// of the three arrays (SART_COO_CHUNK entries, default 4M: ~80 MB of buffers) keeping only this shard's rows and
+// window columns -- no whole-array read, no global sort, no cache (the reference reads every array whole per rank,
+// raytransfer.cpp:67-91) -- and dense datasets from the non-zeros of row blocks. A row's entries are then ordered by
+// column (stable: the file order of an entry repeated at the same (row, col) is kept and the LAST one wins, exact
+// zeros dropped: csr_from_entries' semantics) and the camera's segments are concatenated row by row (their columns are
+// disjoint and ascending). Peak host memory: the CSR built so far plus the current camera's segments (<= 2x the CSR).
 HostCsr RtmReader::read_csr(uint64_t row_begin, uint64_t row_end) {
     SART_H5_LOCK;
-    std::vector<int64_t> rows;
-    std::vector<int32_t> cols;
-    std::vector<float> vals;
     const uint64_t nrows = row_end > row_begin ? row_end - row_begin : 0, ncols = c1_ - c0_;
+    if (ncols > (uint64_t)INT32_MAX) throw Error("read_csr: more than 2^31 - 1 columns");
+    HostCsr out;
+    out.nrows = (int64_t)nrows;
+    out.ncols = (int64_t)ncols;
+    out.ptr.assign(nrows + 1, 0);
+    uint64_t chunk = 4ull << 20;
+    if (const char* e = std::getenv("SART_COO_CHUNK"); e && *e && std::atoll(e) > 0) chunk = (uint64_t)std::atoll(e);
     const std::string grp = "rtm/" + name_;
     uint64_t start_pixel = 0;
     for (const auto& [cam, files] : sorted_) {
@@ -403,6 +416,8 @@ HostCsr RtmReader::read_csr(uint64_t row_begin, uint64_t row_end) {
         if (cam_end > row_begin && start_pixel < row_end) {
             const uint64_t lr0 = std::max(row_begin, start_pixel) - start_pixel;
             const uint64_t lr1 = std::min(row_end, cam_end) - start_pixel;
+            const uint64_t nr = lr1 - lr0, orow = start_pixel + lr0 - row_begin;  // camera rows, first output row
+            std::vector<HostCsr> segs;
             uint64_t start_voxel = 0;
             for (const auto& path : files) {
                 H5Id f = h5_open_file(path);
@@ -414,17 +429,70 @@ HostCsr RtmReader::read_csr(uint64_t row_begin, uint64_t row_end) {
                                         : 0;
                 if (s1 > s0) {
                     const uint64_t ocol = start_voxel + s0 - c0_;
+                    HostCsr seg;
+                    seg.nrows = (int64_t)nr;
+                    seg.ncols = (int64_t)ncols;
+                    seg.ptr.assign(nr + 1, 0);
                     if (h5_attr_i64(f, grp, "is_sparse")) {
-                        const SparseSegment& seg = sparse_segment(f, path, nvox_seg);
-                        auto lo = std::lower_bound(seg.pix.begin(), seg.pix.end(), lr0);
-                        auto hi = std::lower_bound(lo, seg.pix.end(), lr1);
-                        for (size_t n = (size_t)(lo - seg.pix.begin()); n < (size_t)(hi - seg.pix.begin()); ++n) {
-                            const uint64_t v = seg.vox[n];
-                            if (v < s0 || v >= s1) continue;
-                            rows.push_back((int64_t)(start_pixel + seg.pix[n] - row_begin));
-                            cols.push_back((int32_t)(ocol + (v - s0)));
-                            vals.push_back(seg.val[n]);
+                        H5Id dp = h5_open_dataset(f, grp + "/pixel_index");
+                        H5Id dv = h5_open_dataset(f, grp + "/voxel_index");
+                        H5Id dx = h5_open_dataset(f, grp + "/value");
+                        const auto np = h5_dims(dp), nv = h5_dims(dv), nx = h5_dims(dx);
+                        if (np.size() != 1 || nv.size() != 1 || nx.size() != 1 || np[0] != nx[0] || nv[0] != nx[0])
+                            throw Error("Inconsistent sparse RTM arrays in " + path + ".");
+                        const uint64_t n = nx[0];
+                        std::vector<uint64_t> pb(std::min(chunk, n)), vb(std::min(chunk, n));
+                        std::vector<float> xb;
+                        // pass 1: entries per row of the shard (and the checks of every entry)
+                        for (uint64_t o = 0; o < n; o += chunk) {
+                            const uint64_t m = std::min(chunk, n - o);
+                            h5_read_range_u64(dp, o, m, pb.data());
+                            h5_read_range_u64(dv, o, m, vb.data());
+                            for (uint64_t t = 0; t < m; ++t) {
+                                if (vb[t] >= nvox_seg) throw Error("Sparse RTM voxel index out of range in " + path + ".");
+                                if (pb[t] >= lr0 && pb[t] < lr1 && vb[t] >= s0 && vb[t] < s1) ++seg.ptr[pb[t] - lr0 + 1];
+                            }
                         }
+                        for (uint64_t r = 0; r < nr; ++r) seg.ptr[r + 1] += seg.ptr[r];
+                        seg.idx.resize((size_t)seg.ptr[nr]);
+                        seg.val.resize((size_t)seg.ptr[nr]);
+                        // pass 2: the entries into their rows, in file order
+                        std::vector<int64_t> next(seg.ptr.begin(), seg.ptr.end() - 1);
+                        xb.resize(std::min(chunk, n));
+                        for (uint64_t o = 0; o < n && seg.ptr[nr] > 0; o += chunk) {
+                            const uint64_t m = std::min(chunk, n - o);
+                            h5_read_range_u64(dp, o, m, pb.data());
+                            h5_read_range_u64(dv, o, m, vb.data());
+                            h5_read_range_f32(dx, o, m, xb.data());
+                            for (uint64_t t = 0; t < m; ++t)
+                                if (pb[t] >= lr0 && pb[t] < lr1 && vb[t] >= s0 && vb[t] < s1) {
+                                    const int64_t d = next[pb[t] - lr0]++;
+                                    seg.idx[(size_t)d] = (int32_t)(ocol + (vb[t] - s0));
+                                    seg.val[(size_t)d] = xb[t];
+                                }
+                        }
+                        // per row: ascending columns (stable), the last of repeated (row, col) entries, no zeros
+                        int64_t w = 0;
+                        std::vector<std::pair<int32_t, float>> row;
+                        for (uint64_t r = 0; r < nr; ++r) {
+                            row.clear();
+                            for (int64_t k = seg.ptr[r]; k < seg.ptr[r + 1]; ++k) row.push_back({seg.idx[k], seg.val[k]});
+                            std::stable_sort(row.begin(), row.end(),
+                                             [](const auto& p, const auto& q) { return p.first < q.first; });
+                            seg.ptr[r] = w;
+                            for (size_t k = 0; k < row.size(); ++k) {
+                                if (k + 1 < row.size() && row[k + 1].first == row[k].first) continue;
+                                if (row[k].second == 0.0f) continue;
+                                seg.idx[(size_t)w] = row[k].first;
+                                seg.val[(size_t)w] = row[k].second;
+                                ++w;
+                            }
+                        }
+                        seg.ptr[nr] = w;
+                        seg.idx.resize((size_t)w);
+                        seg.val.resize((size_t)w);
+                        seg.idx.shrink_to_fit();
+                        seg.val.shrink_to_fit();
                     } else {
                         H5Id d = h5_open_dataset(f, grp + "/value");
                         const auto dims = h5_dims(d);
@@ -434,26 +502,42 @@ HostCsr RtmReader::read_csr(uint64_t row_begin, uint64_t row_end) {
                         const uint64_t rpr = std::max<uint64_t>(1, (64ull << 20) / (4 * nc));
                         std::vector<float> blk;
                         for (uint64_t r = lr0; r < lr1; r += rpr) {
-                            const uint64_t n = std::min(rpr, lr1 - r);
-                            blk.assign(n * nc, 0.0f);
-                            h5_read_block_f32(d, r, n, s0, nc, blk.data(), nc, 0);
-                            for (uint64_t i = 0; i < n; ++i)
+                            const uint64_t m = std::min(rpr, lr1 - r);
+                            blk.assign(m * nc, 0.0f);
+                            h5_read_block_f32(d, r, m, s0, nc, blk.data(), nc, 0);
+                            for (uint64_t i = 0; i < m; ++i) {
                                 for (uint64_t c = 0; c < nc; ++c)
                                     if (blk[i * nc + c] != 0.0f) {
-                                        rows.push_back((int64_t)(start_pixel + r + i - row_begin));
-                                        cols.push_back((int32_t)(ocol + c));
-                                        vals.push_back(blk[i * nc + c]);
+                                        seg.idx.push_back((int32_t)(ocol + c));
+                                        seg.val.push_back(blk[i * nc + c]);
                                     }
+                                seg.ptr[r - lr0 + i + 1] = (int64_t)seg.val.size();
+                            }
                         }
                     }
+                    segs.push_back(std::move(seg));
                 }
                 start_voxel += nvox_seg;
+            }
+            // the camera's rows: its segments concatenated row by row
+            size_t total = out.idx.size();
+            for (const auto& sg : segs) total += sg.idx.size();
+            out.idx.reserve(total);
+            out.val.reserve(total);
+            for (uint64_t r = 0; r < nr; ++r) {
+                for (const auto& sg : segs) {
+                    out.idx.insert(out.idx.end(), sg.idx.begin() + sg.ptr[r], sg.idx.begin() + sg.ptr[r + 1]);
+                    out.val.insert(out.val.end(), sg.val.begin() + sg.ptr[r], sg.val.begin() + sg.ptr[r + 1]);
+                }
+                out.ptr[orow + r + 1] = (int64_t)out.idx.size();
             }
         }
         start_pixel = cam_end;
         if (start_pixel >= row_end) break;
     }
-    return csr_from_entries((int64_t)nrows, (int64_t)ncols, rows, cols, vals);
+    // rows of cameras past the files (none for validated inputs) keep the last offset
+    for (uint64_t r = 0; r < nrows; ++r) out.ptr[r + 1] = std::max(out.ptr[r + 1], out.ptr[r]);
+    return out;
 }
 
 LaplacianCOO read_laplacian(const std::string& path, uint64_t expected_nvoxel) {

@@ -37,6 +37,7 @@ struct SolveInfo {
     int warm_from = -1;       // multi-frame time series: index of the frame whose iterate started this one
                               // (-1: the caller's x0, or cold)
     int warm_iter = -1;       // the update count of that iterate (its final count when it had finished)
+    bool warm_live = false;   // that frame was still in flight (its iterate extrapolated along its last update)
     // per-frame breakdown of ms (single-frame engine): host + device setup of the frame (normalisation, H2D of g
     // and x0, cold-start back-projection) up to the first queued sweep, the sweep loop up to the final state
     // check, the read-back of x (D2H and de-normalisation); sweeps queued in total (the chunks past the

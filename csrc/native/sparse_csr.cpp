@@ -49,8 +49,28 @@ HostCsr csr_from_entries(int64_t nrows, int64_t ncols, const std::vector<int64_t
     return a;
 }
 
+void csr_validate(const HostCsr& a, const char* who) {
+    const std::string w(who);
+    if (a.nrows < 0 || a.ncols < 0) throw std::invalid_argument(w + ": negative shape");
+    if (a.ncols > INT32_MAX) throw std::invalid_argument(w + ": more than 2^31 - 1 columns");
+    if ((int64_t)a.ptr.size() != a.nrows + 1) throw std::invalid_argument(w + ": row pointer needs nrows + 1 entries");
+    if (a.idx.size() != a.val.size()) throw std::invalid_argument(w + ": column indices and values differ in length");
+    if (a.ptr[0] != 0 || a.ptr[a.nrows] != (int64_t)a.idx.size())
+        throw std::invalid_argument(w + ": row pointer must start at 0 and end at the number of entries");
+    for (int64_t r = 0; r < a.nrows; ++r)
+        if (a.ptr[r + 1] < a.ptr[r])
+            throw std::invalid_argument(w + ": row pointer decreases at row " + std::to_string(r));
+    for (size_t k = 0; k < a.idx.size(); ++k)
+        if (a.idx[k] < 0 || (int64_t)a.idx[k] >= a.ncols)
+            throw std::invalid_argument(w + ": column index " + std::to_string(a.idx[k]) + " outside [0, " +
+                                        std::to_string(a.ncols) + ")");
+}
+
 HostCsr csr_transpose(const HostCsr& a) {
     if (a.nrows > INT32_MAX) throw std::invalid_argument("csr_transpose: more than 2^31 - 1 rows");
+    // a malformed CSR (user arrays through SparseRTM) would index outside the buffers below, and its device copy
+    // would make the gather kernels read outside x / Xt
+    csr_validate(a, "csr_transpose");
     HostCsr t;
     t.nrows = a.ncols;
     t.ncols = a.nrows;

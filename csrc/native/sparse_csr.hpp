@@ -21,7 +21,10 @@ struct HostCsr {
 // dense shard in that order leaves); exact zeros are dropped. Throws std::invalid_argument on an index out of range.
 HostCsr csr_from_entries(int64_t nrows, int64_t ncols, const std::vector<int64_t>& rows,
                          const std::vector<int32_t>& cols, const std::vector<float>& vals);
-// A^T in CSR form (= A in CSC form): entries of each column in ascending row order.
+// Throws std::invalid_argument unless ptr has nrows + 1 non-decreasing entries from 0 to nnz and every column index
+// lies in [0, ncols) (who: the caller's name in the message).
+void csr_validate(const HostCsr& a, const char* who);
+// A^T in CSR form (= A in CSC form): entries of each column in ascending row order. Validates a first (csr_validate).
 HostCsr csr_transpose(const HostCsr& a);
 
 }  // namespace sart

@@ -115,6 +115,7 @@ class MultiFrameSARTSolver:
                             comm_fallbacks=int(info["comm_fallbacks"]), comm=str(info["comm"]))
             r.warm_from = int(info["warm_from"])
             r.warm_iter = int(info["warm_iter"])
+            r.warm_live = bool(info["warm_live"])
             out.append(r)
         return out
 

@@ -89,6 +89,7 @@ class SolveResult:
     nonfinite: bool = False  # stopped by the NaN/Inf guard: ``solution`` is the last finite iterate
     warm_from: int = -1      # multi-frame time series: frame whose iterate started this one (-1: x0 / cold)
     warm_iter: int = -1      # ... and that iterate's update count (its final count when it had finished)
+    warm_live: bool = False  # ... which was still in flight (extrapolated along its last update)
 
 
 def _host_f64(v) -> np.ndarray:

@@ -177,18 +177,28 @@ def test_p2p_production_launch_shape(tmp_path, extra):
     assert max(errs) <= RANK_FACTOR * e32 + 1e-7, (errs, e32)
 
 
-@pytest.mark.parametrize("fault_rank", ["", "1"])
+@pytest.mark.parametrize("fault_rank", ["", "1", "skip"])
 def test_rccl_init_failure_degrades_to_staged(tmp_path, fault_rank):
     """A failed RCCL bring-up (SART_FAULT_RCCL_INIT: on every rank, or reported by rank 1 only after the collective
-    init) is agreed on over the host communicator: every rank continues on staged collectives wrapped by the P2P
-    all-reduce instead of failing the run, ``describe`` names the failure, and a 2-rank solve matches the 1-rank one
-    at the fp32-emulation bound. (Without SART_DIST_BACKEND the ranks ask for RCCL, as on the node.)"""
+    init; "skip": rank 1 never enters the init, SART_FAULT_RCCL_INIT_SKIP, so rank 0 waits in its non-blocking init
+    until SART_RCCL_INIT_TIMEOUT_S and aborts it) is agreed on over the host communicator: every rank continues on
+    staged collectives wrapped by the P2P all-reduce instead of failing (or hanging) the run, ``describe`` names the
+    failure, and a 2-rank solve matches the 1-rank one at the fp32-emulation bound within the deadline + 30 s.
+    (Without SART_DIST_BACKEND the ranks ask for RCCL, as on the node.)"""
+    import time
+
     fixed = ["--tol", "0", "--iters", "12"]
     x1, m1 = _run(1, str(tmp_path / "r1"), fixed + ["--save-problem"])
     env = dict(SART_DIST_BACKEND="", SART_FAULT_RCCL_INIT="1", SART_P2P="1", SART_P2P_TIMEOUT_S="30")
-    if fault_rank:
+    if fault_rank == "skip":
+        env = dict(SART_DIST_BACKEND="", SART_FAULT_RCCL_INIT_SKIP="1", SART_RCCL_INIT_TIMEOUT_S="10", SART_P2P="1",
+                   SART_P2P_TIMEOUT_S="30")
+    elif fault_rank:
         env["SART_FAULT_RANK"] = fault_rank
+    t0 = time.perf_counter()
     x, m = _run(2, str(tmp_path / "f2"), fixed, timeout=240, **env)
+    if fault_rank == "skip":
+        assert time.perf_counter() - t0 < 10 + 30 + 60, "the init deadline did not bound the bring-up"
     d = m[0]["describe"]
     assert m[0]["comm"] == "p2p" and "RCCL init failed" in d and "staged" in d, d
     assert m[0]["x_bitwise_equal"]

@@ -114,3 +114,60 @@ def test_python_sparse_loader_host_side(tmp_path):
     assert rtm_sparse_density(validate_inputs(mixed.files)) == -1.0
     rp, ci, vv = native().RtmReader(inp.rtm_files, inp.rtm_name, inp.nvoxel).read_csr(5, 70)
     np.testing.assert_array_equal(_dense(65, inp.nvoxel, rp, ci, vv), case.A[5:70].astype(np.float32))
+
+
+@pytest.mark.parametrize("ptr,col,msg", [
+    ([0, 1, 2, 2], [0, 7], "outside"),          # column index past ncols
+    ([0, 1, 2, 2], [0, -1], "outside"),         # negative column index
+    ([0, 2, 1, 2], [0, 1], "decreases"),        # row pointer not monotone
+])
+def test_sparse_rtm_rejects_malformed_csr(ptr, col, msg):
+    """A malformed user CSR is rejected before anything indexes with it (csr_transpose validates): a bad
+    column index would write outside the host transpose and make the device gathers read outside x."""
+    import torch
+
+    from mpi_cuda_sartsolver_amd.models.rtm import SparseRTM
+
+    with pytest.raises(ValueError, match=msg):
+        SparseRTM(3, 4, np.array(ptr), np.array(col), np.ones(len(col), np.float32), device=torch.device("cpu"))
+    with pytest.raises(ValueError, match=msg):
+        native().csr_transpose(3, 4, np.array(ptr, np.int64), np.array(col, np.int32), np.ones(len(col), np.float32))
+
+
+@pytest.mark.parametrize("chunk", ["", "3"])
+def test_read_rtm_csr_streams_coo_with_duplicates(tmp_path, monkeypatch, chunk):
+    """RtmReader::read_csr streams the COO arrays in hyperslab chunks (SART_COO_CHUNK; 3 entries here: every row's
+    entries split across chunks) with a count and a fill pass: unsorted pixel order, an entry repeated at the same
+    (row, col) (the LAST one wins, as the dense scatter leaves it), exact zeros dropped, row windows -- equal to the
+    dense reader's matrix of the same file."""
+    if chunk:
+        monkeypatch.setenv("SART_COO_CHUNK", chunk)
+    n = native()
+    rng = np.random.default_rng(5)
+    h, w, V = 4, 4, 10
+    P = h * w
+    m = 60
+    pix = rng.integers(0, P, m).astype(np.uint64)
+    vox = rng.integers(0, V, m).astype(np.uint64)
+    val = (rng.random(m) + 0.5).astype(np.float32)
+    val[::7] = 0.0  # exact zeros (some of them the last of a repeated entry)
+    pix[5], vox[5], pix[40], vox[40] = 3, 2, 3, 2  # a repeated (row, col): the later value must win
+    val[5], val[40] = 9.0, 4.0
+    expected = np.zeros((P, V), np.float32)
+    for p, v, x in zip(pix, vox, val):
+        expected[p, v] = x
+    rtm, img = str(tmp_path / "rtm.h5"), str(tmp_path / "img.h5")
+    flat = np.arange(V)
+    n.write_rtm_file(path=rtm, camera_name="cam", wavelength=656.3, npixel=P, nvoxel=V,
+                     frame_mask=np.ones((h, w), np.uint8), vi=flat.astype(np.uint64), vj=np.zeros(V, np.uint64),
+                     vk=np.zeros(V, np.uint64), vvalue=np.arange(V, dtype=np.int32), nx=V, ny=1, nz=1,
+                     rtm_name="with_reflections", coordinate_system="", bounds=[], pixel_index=pix, voxel_index=vox,
+                     value=val)
+    n.write_image_file(img, "cam", 657.3, np.array([0.0]), np.ones((1, h, w)))
+    for r0, r1 in [(0, P), (3, 11), (7, 8)]:
+        rp, ci, vv, ncols = n.read_rtm_csr([rtm, img], row_begin=r0, row_end=r1)
+        assert ncols == V and np.all(vv != 0)
+        for r in range(r1 - r0):
+            assert np.all(np.diff(ci[rp[r]:rp[r + 1]]) > 0)  # ascending, unique columns per row
+        np.testing.assert_array_equal(_dense(r1 - r0, V, rp, ci, vv), expected[r0:r1])
+    assert expected[3, 2] == 4.0
