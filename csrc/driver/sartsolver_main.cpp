@@ -267,7 +267,9 @@ std::unique_ptr<DeviceSparseShard> load_sparse_shard(const InputSet& in, uint64_
     const auto t0 = std::chrono::steady_clock::now();
     RtmReader reader(in.rtm_files, in.rtm_name, in.nvoxel);
     const HostCsr a = reader.read_csr(row0, row0 + nrows);
+    ls.rss_after_first_read_mb = rss_hwm_mb();  // (streamed COO chunks: the CSR, at most twice while built)
     const HostCsr t = csr_transpose(a);
+    ls.rss_after_setup_mb = rss_hwm_mb();  // CSR + CSC
     ls.read_s = seconds_since(t0);
     auto sh = std::make_unique<DeviceSparseShard>();
     sh->nrows = (int64_t)nrows;
@@ -433,10 +435,11 @@ int main(int argc, char** argv) {
                       << std::endl;
 
         // the single-frame engine (frame by frame; with --batch_frames it solves a cold time series' first frame)
-        auto make_engine = [&]() {
+        auto make_engine = [&](double tol_factor) {
             std::unique_ptr<Engine> e;
             EngineConfig ec;
             static_cast<SolverParams&>(ec) = params;
+            ec.conv_tolerance *= tol_factor;
             ec.use_fused = !cfg.two_pass;
             ec.fused_min_bytes = fused_min_bytes_from_env();
             if (const char* v = std::getenv("SART_FUSED_VARIANT"); v && *v) ec.fused_variant = std::atoi(v);
@@ -459,6 +462,9 @@ int main(int argc, char** argv) {
             return e;
         };
         std::unique_ptr<Engine> engine, lead_engine;
+        // the lead frame stops at lead_tol x the tolerance and hands its iterate to the batch, where it finishes next
+        // to the frames chained from it (1: it finishes on the single-frame engine; SART_MF_LEAD_TOL)
+        double lead_tol = 1.0;
         std::unique_ptr<MultiFrameEngine> mf;
         std::unique_ptr<CpuSolver> cpu;
         const bool batched = gpu && cfg.batch_frames > 1;
@@ -480,9 +486,10 @@ int main(int argc, char** argv) {
             // a cold time series' first frame: the single-frame engine, built with the set-up (before the frame loop's
             // clock, like the frame-by-frame engine); dropped after that frame (SART_MF_LEAD_ENGINE=0: none)
             const char* le = std::getenv("SART_MF_LEAD_ENGINE");
-            if (!cfg.no_guess && !(le && *le && std::atoi(le) == 0)) lead_engine = make_engine();
+            if (const char* lt = std::getenv("SART_MF_LEAD_TOL"); lt && *lt) lead_tol = std::max(1.0, std::atof(lt));
+            if (!cfg.no_guess && !(le && *le && std::atoi(le) == 0)) lead_engine = make_engine(lead_tol);
         } else if (gpu) {
-            engine = make_engine();
+            engine = make_engine(1.0);
         } else {
             if (sparse)
                 cpu = std::make_unique<CpuSolver>(std::move(hcsr), host, params, false);
@@ -525,9 +532,10 @@ int main(int argc, char** argv) {
         if (rank == 0 && !cfg.profile_file.empty()) profile.open(cfg.profile_file);
         if (gpu && !cfg.profile_file.empty()) {
             // first profile line: the HDF5 -> HBM load (slowest rank's wall time; totals over ranks)
-            double mx[3] = {lstats.wall_s, lstats.rss_hwm_after_mb - lstats.rss_hwm_before_mb, lstats.setup_s};
+            double mx[4] = {lstats.wall_s, lstats.rss_hwm_after_mb - lstats.rss_hwm_before_mb, lstats.setup_s,
+                            (double)lstats.bytes};
             double sm[5] = {(double)lstats.bytes, lstats.read_s, lstats.h2d_s, lstats.wait_read_s, lstats.wait_copy_s};
-            host->all_reduce_host(mx, 3, ReduceOp::kMax);
+            host->all_reduce_host(mx, 4, ReduceOp::kMax);
             host->all_reduce_host(sm, 5, ReduceOp::kSum);
             if (profile.is_open())
                 profile << "{\"load\": true, \"load_s\": " << mx[0] << ", \"rtm_GB\": " << sm[0] / 1e9
@@ -549,7 +557,7 @@ int main(int argc, char** argv) {
                         << ", \"rss_hwm_after_setup_MB\": " << lstats.rss_after_setup_mb
                         << ", \"rss_hwm_after_first_read_MB\": " << lstats.rss_after_first_read_mb
                         << ", \"rss_hwm_after_MB\": " << lstats.rss_hwm_after_mb << "}"
-                        << ", \"rss_growth_MB_max\": " << mx[1]
+                        << ", \"rss_growth_MB_max\": " << mx[1] << ", \"shard_MB_max\": " << mx[3] / 1048576.0
                         << ", \"sparse\": " << (in.has_sparse ? "true" : "false")
                         << ", \"rtm_format\": \"" << (sparse ? "sparse" : "dense") << "\""
                         << ", \"nnz\": " << (sparse ? sshard->nnz : 0) << ", \"driver\": \"native\"}\n";
@@ -642,7 +650,7 @@ int main(int argc, char** argv) {
                 SolveInfo info = lead_engine->solve(g0.data(), nullptr, x0s.data());
                 lead_engine.reset();
                 const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-                if (rank == 0) {
+                if (rank == 0 && !(lead_tol > 1.0)) {
                     writer->add(x0s, info.status, image.frame_time(frames[0]), image.camera_frame_time(frames[0]),
                                 info.iterations);
                     std::cout << "Processed in: " << ms << " ms" << std::endl;
@@ -655,8 +663,10 @@ int main(int argc, char** argv) {
                                 << ", \"driver\": \"native\"}\n";
                 }
                 if (std::all_of(x0s.begin(), x0s.end(), [](double v) { return std::isfinite(v); })) bwarm = x0s;
-                off = 1;
                 lead_iters = info.iterations;
+                // handover (lead_tol > 1): frame 0 is solved on in the batch from this iterate (its reported update
+                // count includes the lead's), as are the first frames chained from it; else the lead is frame 0
+                off = (lead_tol > 1.0 && !bwarm.empty()) ? 0 : 1;
             }
             lead_engine.reset();  // (a resumed series starts from the stored solution instead)
             const size_t npix = (size_t)mf->nrows();
@@ -697,9 +707,12 @@ int main(int argc, char** argv) {
                 SolveInfo fi = info;
                 if (fi.warm_from >= 0) {
                     fi.warm_from += (int)off;
-                } else if (off && !cfg.no_guess) {  // started from the lead frame's solution (the series' x0)
+                } else if (lead_iters >= 0 && j + off == 0) {  // the lead frame, finished in the batch (handover)
+                    fi.iterations += lead_iters;
+                } else if (lead_iters >= 0) {  // started from the lead frame's solution / handed-over iterate
                     fi.warm_from = 0;
                     fi.warm_iter = lead_iters;
+                    fi.warm_live = false;
                 }
                 done.emplace(j + off, std::make_pair(std::vector<double>(xs, xs + in.nvoxel), fi));
                 for (auto it = done.find(written); it != done.end(); it = done.find(written)) {

@@ -57,6 +57,9 @@ __device__ __forceinline__ void load_groups(float (&dst)[NG], const float* __res
     }
 }
 
+#ifndef SART_MF_FLUSH
+#define SART_MF_FLUSH 2  // (see multiframe_bf16.hip)
+#endif
 // F[row][f] = sum_v A[row][v] X[f][v]. X is frame-major [nf][ldx] (ldx == ld), F is [rows][nf].
 // One wave: 16 * RT rows (RT 16-row tiles sharing each X fragment) x nf frames, K = the columns of its
 // split; every float4 of A feeds 4 * NG MFMAs (one per k-component and column group) and every X
@@ -90,6 +93,28 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
         for (int h = 0; h < 2; ++h)
 #pragma unroll
             for (int j = 0; j < NG; ++j) acc[t][h][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // two-level accumulation (as k_mf_forward_b16_lds, SART_MF_FLUSH): K = 4 per MFMA makes the chains of a
+    // 16k-voxel split 4096 fp32 additions long (9.8x the fp32 two-pass kernels' error at 64k x 64k after 20 SART
+    // updates). Where the second set fits the register budget (RT NG <= 8: the 16-frame default)
+    constexpr bool FL = SART_MF_FLUSH > 0 && RT * NG <= 8;
+    floatx4 sum[FL ? RT : 1][FL ? NG : 1];
+    if constexpr (FL) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+            for (int j = 0; j < NG; ++j) sum[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto flush = [&] {
+        if constexpr (FL) {
+#pragma unroll
+            for (int t = 0; t < RT; ++t)
+#pragma unroll
+                for (int j = 0; j < NG; ++j) {
+                    sum[t][j] += acc[t][0][j] + acc[t][1][j];
+                    acc[t][0][j] = acc[t][1][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+                }
+        }
+    };
 
     const int64_t nq = c1 > c0 ? (c1 - c0) / 4 : 0;  // float4 columns; 4 lane-groups x float4 = 16 voxels
     const int64_t nst = nq / 8;                        // 8-float4 steps
@@ -128,10 +153,12 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
                                                                                 comp(x[sl][h][j], c), acc[rt][h][j],
                                                                                 0, 0, 0);
         };
-        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+        for (int64_t t0 = 0, it = 0; t0 < nst; t0 += RS, ++it) {
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
                 (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
             }(std::make_integer_sequence<int, RS>{});
+            if constexpr (FL)
+                if (it % SART_MF_FLUSH == SART_MF_FLUSH - 1) flush();
         }
     }
     for (int64_t q = nst * 8; q < nq; q += 4) {  // 4-float4 tail of a ragged split
@@ -157,7 +184,11 @@ __global__ __launch_bounds__(256) void k_mf_forward(const float* __restrict__ A,
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int64_t ra = row0 + rt * 16 + g * 4 + i;
-                if (ra < nrows) Fout[ra * NF + 16 * j + r] = acc[rt][0][j][i] + acc[rt][1][j][i];
+                if constexpr (FL) {
+                    if (ra < nrows) Fout[ra * NF + 16 * j + r] = sum[rt][j][i] + (acc[rt][0][j][i] + acc[rt][1][j][i]);
+                } else {
+                    if (ra < nrows) Fout[ra * NF + 16 * j + r] = acc[rt][0][j][i] + acc[rt][1][j][i];
+                }
             }
 }
 
@@ -194,6 +225,27 @@ __global__ __launch_bounds__(256) void k_mf_backproject(const float* __restrict_
         for (int c = 0; c < 4; ++c)
 #pragma unroll
             for (int j = 0; j < NG; ++j) acc[vt][c][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // two-level accumulation (SART_MF_FLUSH, as k_mf_forward) where the second set fits (VT NG <= 2: 16 frames)
+    constexpr bool FL = SART_MF_FLUSH > 0 && VT * NG <= 2;
+    floatx4 sum[FL ? VT : 1][4][FL ? NG : 1];
+    if constexpr (FL) {
+#pragma unroll
+        for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int j = 0; j < NG; ++j) sum[vt][c][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto flush = [&] {
+        if constexpr (FL) {
+#pragma unroll
+            for (int vt = 0; vt < VT; ++vt)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int j = 0; j < NG; ++j) sum[vt][c][j] += acc[vt][c][j], acc[vt][c][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
 
     const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 16 : 0;  // 16-row steps
     if (nst > 0) {
@@ -227,10 +279,12 @@ __global__ __launch_bounds__(256) void k_mf_backproject(const float* __restrict_
                             acc[vt][c][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(av[sl][u][vt], c), wv[sl][u][j],
                                                                                 acc[vt][c][j], 0, 0, 0);
         };
-        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+        for (int64_t t0 = 0, it = 0; t0 < nst; t0 += RS, ++it) {
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
                 (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
             }(std::make_integer_sequence<int, RS>{});
+            if constexpr (FL)
+                if (it % SART_MF_FLUSH == SART_MF_FLUSH - 1) flush();
         }
     }
     for (int64_t r0 = r_begin + nst * 16; r0 < r_end; r0 += 4) {  // ragged tail, 4 rows per MFMA
@@ -263,7 +317,10 @@ __global__ __launch_bounds__(256) void k_mf_backproject(const float* __restrict_
             for (int q = 0; q < 4; ++q) {
                 const int64_t v = (vb * VT + vt) * 64 + 4 * (g * 4 + q) + c;
 #pragma unroll
-                for (int j = 0; j < NG; ++j) out[v * NF + 16 * j + i16] = acc[vt][c][j][q];
+                for (int j = 0; j < NG; ++j) {
+                    if constexpr (FL) out[v * NF + 16 * j + i16] = sum[vt][c][j][q] + acc[vt][c][j][q];
+                    else out[v * NF + 16 * j + i16] = acc[vt][c][j][q];
+                }
             }
 }
 
@@ -288,7 +345,10 @@ static int mf_vox(int64_t ld, int nf);
 int mf_backproject_num_splits(int64_t ld, int64_t nrows) {
     const int64_t nblk = (ld / (64 * mf_vox(ld, 64)) + 3) / 4;  // the fp32 kernels' widest batch
     const char* e = std::getenv("SART_MF_BP_BLOCKS");  // target workgroups (tuning knob)
-    const int64_t target = (e && *e) ? std::atoll(e) : 512;
+    // 2048 (4 x the 512 of round 1): a split's rows are one fp32 MFMA accumulation chain; 16k-row splits at 64k x 64k
+    // were the larger share of the multi-frame engine's error against the fp32 two-pass kernels
+    // (profiles/parity_r6_64k_mf_chains.jsonl); the extra partial slices cost k_mf_collect ~1.5 % of a sweep
+    const int64_t target = (e && *e) ? std::atoll(e) : 2048;
     int64_t s = (target + nblk - 1) / nblk;
     const int64_t smax = (nrows + 63) / 64;
     if (s > smax) s = smax;

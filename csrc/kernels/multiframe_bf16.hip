@@ -300,6 +300,13 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
 #ifndef SART_MF_STAGE_LATE
 #define SART_MF_STAGE_LATE 1
 #endif
+// Two-level accumulation of the split-K sums: every SART_MF_FLUSH outer iterations (of DEPTH + 1 steps) the MFMA
+// accumulators are added into a second fp32 sum and restarted, so no fp32 chain runs over a whole split. One chain
+// per split (16384 terms at 64k x 64k) measured 3.5x the fp32 two-pass kernels' error at 64 frames after 20 SART
+// updates on the ray-traced RTM (profiles/parity_r6_64k_raytraced.jsonl); 0 disables (A/B).
+#ifndef SART_MF_FLUSH
+#define SART_MF_FLUSH 2
+#endif
 // bf16 X / W fragments read from LDS all at once at the top of a step (A/B builds: -DSART_MF_XF_EARLY=0)
 #ifndef SART_MF_XF_EARLY
 #define SART_MF_XF_EARLY 1
@@ -360,11 +367,17 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) rs[rt] = H16 ? fc.rsc[row0 + rt * 16 + r] : 1.f;
 
-    floatx4 acc[RT][NG];
+    floatx4 acc[RT][NG], sum[RT][NG];
 #pragma unroll
     for (int t = 0; t < RT; ++t)
 #pragma unroll
-        for (int j = 0; j < NG; ++j) acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NG; ++j) acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f}, sum[t][j] = acc[t][j];
+    auto flush = [&] {  // the chain so far into the second-level sum (see SART_MF_FLUSH)
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+            for (int j = 0; j < NG; ++j) sum[t][j] += acc[t][j], acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    };
 
     const int64_t nst = c1 > c0 ? (c1 - c0) / (32 * KB) : 0;  // uniform for the workgroup
     if (nst > 0) {
@@ -562,12 +575,19 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
             if constexpr (LATE) stage_next();
             __syncthreads();
         };
-        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+        for (int64_t t0 = 0, it = 0; t0 < nst; t0 += RS, ++it) {
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
                 (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
             }(std::make_integer_sequence<int, RS>{});
+            if constexpr (SART_MF_FLUSH > 0)
+                if (it % SART_MF_FLUSH == SART_MF_FLUSH - 1) flush();
         }
     }
+    flush();
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int j = 0; j < NG; ++j) acc[t][j] = sum[t][j];
     if (!live) return;
     if constexpr (H16) {  // 1 / (s_p s_f), exact (powers of two)
 #pragma unroll
@@ -1326,7 +1346,10 @@ int mf_backproject_b16_num_splits(int64_t ld, int64_t nrows, bool a32) {
     const int64_t nblk = (ld / (64 * (a32 ? mf_x3_vt(ld) : mf_b16_vt(ld, 0))) + 3) / 4;
     // bf16 storage: ~512 (fewer partial slices for k_mf_collect: +1.3 % with 512-block forwards at 64 frames,
     // profiles/ab_r4_mf_split_blocks_low.jsonl); split-A ~1024 (256: -5 %)
-    const int64_t target = env_int("SART_MF_BP_BLOCKS", a32 ? 1024 : 512);
+    // x 4 in round 6 (split-A 4096, bf16 storage 2048): each split's rows are one fp32 MFMA accumulation chain, the
+    // larger share of the engine's error against the fp32 two-pass kernels at 64k x 64k (16k-row chains;
+    // profiles/parity_r6_64k_mf_chains.jsonl)
+    const int64_t target = env_int("SART_MF_BP_BLOCKS", a32 ? 4096 : 2048);
     int64_t s = (target + nblk - 1) / nblk;
     const int64_t smax = (nrows + 63) / 64;
     if (s > smax) s = smax;

@@ -387,7 +387,7 @@ void read_rtm_rows(const SortedRtmFiles& sorted, const std::string& rtm_name, ui
 
 // Bounded-memory CSR reader. Camera by camera (cameras own disjoint row ranges), every voxel segment becomes a CSR
 // over the camera's rows of the shard: sparse (COO) datasets by a count pass and a fill pass over hyperslab chunks
-// of the three arrays (SART_COO_CHUNK entries, default 4M: ~80 MB of buffers) keeping only this shard's rows and
+// of the three arrays (SART_COO_CHUNK entries, default 1M: 20 MB of buffers) keeping only this shard's rows and
 // window columns -- no whole-array read, no global sort, no cache (the reference reads every array whole per rank,
 // raytransfer.cpp:67-91) -- and dense datasets from the non-zeros of row blocks. A row's entries are then ordered by
 // column (stable: the file order of an entry repeated at the same (row, col) is kept and the LAST one wins, exact
@@ -401,7 +401,7 @@ HostCsr RtmReader::read_csr(uint64_t row_begin, uint64_t row_end) {
     out.nrows = (int64_t)nrows;
     out.ncols = (int64_t)ncols;
     out.ptr.assign(nrows + 1, 0);
-    uint64_t chunk = 4ull << 20;
+    uint64_t chunk = 1ull << 20;
     if (const char* e = std::getenv("SART_COO_CHUNK"); e && *e && std::atoll(e) > 0) chunk = (uint64_t)std::atoll(e);
     const std::string grp = "rtm/" + name_;
     uint64_t start_pixel = 0;
@@ -519,7 +519,16 @@ HostCsr RtmReader::read_csr(uint64_t row_begin, uint64_t row_end) {
                 }
                 start_voxel += nvox_seg;
             }
-            // the camera's rows: its segments concatenated row by row
+            // the camera's rows: its segments concatenated row by row (one segment into an empty CSR: moved)
+            if (segs.size() == 1 && out.idx.empty()) {
+                HostCsr& sg = segs.front();
+                for (uint64_t r = 0; r < nr; ++r) out.ptr[orow + r + 1] = sg.ptr[r + 1];
+                out.idx = std::move(sg.idx);
+                out.val = std::move(sg.val);
+                start_pixel = cam_end;
+                if (start_pixel >= row_end) break;
+                continue;
+            }
             size_t total = out.idx.size();
             for (const auto& sg : segs) total += sg.idx.size();
             out.idx.reserve(total);

@@ -32,9 +32,11 @@ def _all_reduce(t: torch.Tensor, comm, op: str = "sum") -> torch.Tensor:
 def sart_oracle_f64(rtm: DenseRTM, g, iterations: int, *, logarithmic: bool = False, comm=None,
                     ray_density_threshold: float = 1e-6, ray_length_threshold: float = 1e-6,
                     relaxation: float = 1.0, x_prev: Optional[np.ndarray] = None,
-                    block_bytes: int = 1 << 30) -> np.ndarray:
+                    block_bytes: int = 1 << 30, laplacian=None, beta_laplace: float = 0.0) -> np.ndarray:
     """``iterations`` SART updates in fp64 on ``rtm`` (this rank's rows; ``g`` this rank's pixels).
-    Returns the de-normalised solution (fp64, host), like ``SARTSolver.solve``."""
+    ``laplacian`` (LaplacianCSR, with ``beta_laplace``): the smoothing penalty beta L x (log mode: beta L log x,
+    applied as exp(-pen)), as reference.sart_gpu_semantics. Returns the de-normalised solution (fp64, host), like
+    ``SARTSolver.solve``."""
     dev = rtm.device
     P, V = rtm.npixel, rtm.nvoxel
     A = rtm.A
@@ -84,6 +86,18 @@ def sart_oracle_f64(rtm: DenseRTM, g, iterations: int, *, logarithmic: bool = Fa
             acc += a.T @ w
         return _all_reduce(acc, comm)
 
+    Lm = None
+    if laplacian is not None and beta_laplace > 0 and laplacian.nnz > 0:
+        Lm = torch.sparse_csr_tensor(torch.as_tensor(laplacian.row_ptr_host, dtype=torch.int64),
+                                     torch.as_tensor(laplacian.col_host, dtype=torch.int64),
+                                     torch.as_tensor(np.asarray(laplacian.val_host, dtype=np.float32), dtype=f64),
+                                     size=(V, V)).to(dev)
+
+    def penalty(x):
+        if Lm is None:
+            return None
+        return beta_laplace * (Lm @ (torch.log(x) if logarithmic else x).unsqueeze(1)).squeeze(1)
+
     zero = torch.zeros(V, dtype=f64, device=dev)
     if x_prev is None:
         x = torch.where(dvalid, bwd(torch.clamp(ghat, min=0.0)) / rho64, zero)
@@ -93,9 +107,13 @@ def sart_oracle_f64(rtm: DenseRTM, g, iterations: int, *, logarithmic: bool = Fa
     O = torch.where(dvalid, bwd(arow * ghat), zero) if logarithmic else None
     eps = 1e-7
     for _ in range(iterations):
+        pen = penalty(x)  # (from the iterate before the update, as the kernels)
         if logarithmic:
             Fv = torch.where(dvalid, sweep(x), zero)
             x = x * ((O + eps) / (Fv + eps)) ** relaxation
+            if pen is not None:
+                x = x * torch.exp(-pen)
         else:
-            x = torch.clamp(x + torch.where(dvalid, relaxation / rho64 * sweep(x), zero), min=0.0)
+            d = torch.where(dvalid, relaxation / rho64 * sweep(x), zero)
+            x = torch.clamp(x + d - (pen if pen is not None else 0.0), min=0.0)
     return (x * norm).cpu().numpy()
