@@ -262,12 +262,34 @@ struct DeviceSparseShard {
 std::unique_ptr<DeviceSparseShard> load_sparse_shard(const InputSet& in, uint64_t row0, uint64_t nrows,
                                                      LoadStats* stats) {
     LoadStats ls;
+    // The HIP runtime's one-time host footprint first, as in load_device_shard: each device queue comes up with its
+    // first command, ~0.19 GB resident apiece on the MI355X box whatever the shard size -- the null stream's (the
+    // fills of DeviceArray::resize, which the engine runs anyway), the copy stream's and the copy engine's, which a
+    // small copy does not use (profiles/sparse_load_rss_r6.jsonl: +0.19 / +0.41 GB after the CSR + CSC without
+    // these). The baseline is taken after them.
     hip_ok(hipFree(nullptr), "hipFree");
+    hipStream_t s;
+    hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    constexpr size_t kStage = (size_t)16 << 20;  // two pinned 16-MiB staging buffers (the upload's only host memory)
+    char* stg[2] = {nullptr, nullptr};
+    hipEvent_t ev[2];
+    {
+        DeviceArray<float> d;
+        d.resize(kStage / sizeof(float));  // (null-stream fill)
+        void* h = nullptr;
+        hip_ok(hipHostMalloc(&h, kStage), "hipHostMalloc(warm-up)");
+        for (auto& e : ev) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        hip_ok(hipMemsetAsync(d.get(), 0, kStage, s), "hipMemset(warm-up)");
+        hip_ok(hipMemcpyAsync(d.get(), h, kStage, hipMemcpyHostToDevice, s), "hipMemcpy(warm-up)");
+        for (auto& e : ev) hip_ok(hipEventRecord(e, s), "hipEventRecord");
+        hip_ok(hipStreamSynchronize(s), "warm-up sync");
+        (void)hipHostFree(h);
+    }
     ls.rss_hwm_before_mb = rss_hwm_mb();
     const auto t0 = std::chrono::steady_clock::now();
     RtmReader reader(in.rtm_files, in.rtm_name, in.nvoxel);
     const HostCsr a = reader.read_csr(row0, row0 + nrows);
-    ls.rss_after_first_read_mb = rss_hwm_mb();  // (streamed COO chunks: the CSR, at most twice while built)
+    ls.rss_after_first_read_mb = rss_hwm_mb();  // (streamed COO chunks: the CSR and the reader's 20 MB of chunks)
     const HostCsr t = csr_transpose(a);
     ls.rss_after_setup_mb = rss_hwm_mb();  // CSR + CSC
     ls.read_s = seconds_since(t0);
@@ -283,8 +305,18 @@ std::unique_ptr<DeviceSparseShard> load_sparse_shard(const InputSet& in, uint64_
     sh->val.resize(n);
     sh->cval.resize(n);
     const auto t1 = std::chrono::steady_clock::now();
-    auto up = [](void* d, const void* h, size_t bytes) {
-        if (bytes) hip_ok(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice), "H2D sparse RTM");
+    for (auto& b : stg) hip_ok(hipHostMalloc(reinterpret_cast<void**>(&b), kStage), "hipHostMalloc");
+    // through the pinned buffers, double-buffered: a pageable hipMemcpy of a large array stages through the
+    // runtime's own pinned memory, which stays resident after the load
+    int k = 0;
+    auto up = [&](void* d, const void* h, size_t bytes) {
+        for (size_t o = 0; o < bytes; o += kStage, k ^= 1) {
+            const size_t m = std::min(kStage, bytes - o);
+            hip_ok(hipEventSynchronize(ev[k]), "hipEventSynchronize");  // the copy that last used this buffer
+            std::memcpy(stg[k], static_cast<const char*>(h) + o, m);
+            hip_ok(hipMemcpyAsync(static_cast<char*>(d) + o, stg[k], m, hipMemcpyHostToDevice, s), "H2D sparse RTM");
+            hip_ok(hipEventRecord(ev[k], s), "hipEventRecord");
+        }
     };
     up(sh->rp.get(), a.ptr.data(), a.ptr.size() * sizeof(int64_t));
     up(sh->cp.get(), t.ptr.data(), t.ptr.size() * sizeof(int64_t));
@@ -292,6 +324,11 @@ std::unique_ptr<DeviceSparseShard> load_sparse_shard(const InputSet& in, uint64_
     up(sh->val.get(), a.val.data(), a.val.size() * sizeof(float));
     up(sh->row.get(), t.idx.data(), t.idx.size() * sizeof(int32_t));
     up(sh->cval.get(), t.val.data(), t.val.size() * sizeof(float));
+    hip_ok(hipStreamSynchronize(s), "H2D sparse RTM sync");
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    for (auto& b : stg) (void)hipHostFree(b);
+    (void)hipStreamDestroy(s);
+    ls.staging_bytes = 2 * kStage;
     ls.h2d_s = seconds_since(t1);
     ls.blocks = 1;
     ls.rows_per_block = nrows;
@@ -406,9 +443,17 @@ int main(int argc, char** argv) {
         if (const char* e = std::getenv("SART_RTM_BLOCK_MB"); e && *e)
             block_bytes = (size_t)std::max(1.0, std::atof(e) * 1048576.0);
         HostCsr hcsr;  // --use_cpu with a sparse shard
+        int64_t cpu_nnz = 0;
         auto load = [&]() {
-            if (sparse && !gpu)
+            if (sparse && !gpu) {  // (the CPU solver's CSR alone; the load line as on the GPU path)
+                lstats.rss_hwm_before_mb = rss_hwm_mb();
+                const auto t0 = std::chrono::steady_clock::now();
                 hcsr = RtmReader(in.rtm_files, in.rtm_name, in.nvoxel).read_csr(blk.offset, blk.offset + blk.size);
+                lstats.wall_s = lstats.read_s = seconds_since(t0);
+                cpu_nnz = hcsr.nnz();
+                lstats.bytes = (uint64_t)cpu_nnz * 8 + hcsr.ptr.size() * sizeof(int64_t);
+                lstats.rss_hwm_after_mb = rss_hwm_mb();
+            }
             else if (sparse)
                 sshard = load_sparse_shard(in, blk.offset, blk.size, &lstats);
             else if (gpu)
@@ -530,7 +575,7 @@ int main(int argc, char** argv) {
         }
         std::ofstream profile;
         if (rank == 0 && !cfg.profile_file.empty()) profile.open(cfg.profile_file);
-        if (gpu && !cfg.profile_file.empty()) {
+        if ((gpu || sparse) && !cfg.profile_file.empty()) {
             // first profile line: the HDF5 -> HBM load (slowest rank's wall time; totals over ranks)
             double mx[4] = {lstats.wall_s, lstats.rss_hwm_after_mb - lstats.rss_hwm_before_mb, lstats.setup_s,
                             (double)lstats.bytes};
@@ -560,7 +605,7 @@ int main(int argc, char** argv) {
                         << ", \"rss_growth_MB_max\": " << mx[1] << ", \"shard_MB_max\": " << mx[3] / 1048576.0
                         << ", \"sparse\": " << (in.has_sparse ? "true" : "false")
                         << ", \"rtm_format\": \"" << (sparse ? "sparse" : "dense") << "\""
-                        << ", \"nnz\": " << (sparse ? sshard->nnz : 0) << ", \"driver\": \"native\"}\n";
+                        << ", \"nnz\": " << (sparse ? (gpu ? sshard->nnz : cpu_nnz) : 0) << ", \"driver\": \"native\"}\n";
         }
 
         std::vector<uint64_t> frames;

@@ -941,6 +941,16 @@ __device__ __forceinline__ void split_phase_h(const u32x4 (&v)[8], float s, u32x
     h2 = u32x4{b[0], b[1], b[2], b[3]};
 }
 
+// Two-level accumulation of the back-projection's split-K sums through LDS: every SART_MF_BWD_FLUSH outer iterations
+// (of DEPTH + 1 steps of 32 rows) a lane adds its accumulators into its own LDS slots and restarts them, so no fp32
+// MFMA chain runs over a whole split (a second register set spilled: 64 / 128 more VGPRs). Slots are lane-private
+// (no barrier, no atomics): 16 NG KiB per wave, 64 / 128 KiB per workgroup at 64 / 128 frames beside the 16 / 32 KiB
+// W stage (two workgroups per CU at 64 frames, one at 128: the occupancy the registers allow anyway). 0 disables
+// (A/B builds); the split count then has to shorten the chains instead (SART_MF_BP_BLOCKS).
+#ifndef SART_MF_BWD_FLUSH
+#define SART_MF_BWD_FLUSH 4
+#endif
+
 // EW: W loaded a step ahead of A's batch (see k_mf_backproject_b16_lds); MW: waves per SIMD of the register budget
 template <int NG, int DEPTH, bool EW = false, int MW = 2>
 __global__ __launch_bounds__(256, MW) void k_mf_backproject_h16(const float* __restrict__ A, int64_t ld, int64_t nrows32,
@@ -973,6 +983,22 @@ __global__ __launch_bounds__(256, MW) void k_mf_backproject_h16(const float* __r
     for (int p = 0; p < 4; ++p)
 #pragma unroll
         for (int j = 0; j < NG; ++j) acc[p][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    constexpr int FLB = SART_MF_BWD_FLUSH;
+    __shared__ __attribute__((aligned(16))) floatx4 s_acc[FLB > 0 ? 4 : 1][FLB > 0 ? 4 * NG : 1][64];
+    floatx4* sacc = s_acc[FLB > 0 ? wave : 0][0] + lane;  // slot k of this lane: sacc[k * 64]
+    if constexpr (FLB > 0) {
+#pragma unroll
+        for (int k = 0; k < 4 * NG; ++k) sacc[k * 64] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto flush = [&] {
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int j = 0; j < NG; ++j) {
+                sacc[(p * NG + j) * 64] += acc[p][j];
+                acc[p][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
+    };
     const int64_t nst = r_end > r_begin ? (r_end - r_begin) / 32 : 0;  // uniform for the workgroup
     if (nst > 0) {
         u32x4 av[RS][8];
@@ -1036,11 +1062,19 @@ __global__ __launch_bounds__(256, MW) void k_mf_backproject_h16(const float* __r
             stage(std::integral_constant<int, (sl + 1) % RS>{}, t + 1);
             __syncthreads();
         };
-        for (int64_t t0 = 0; t0 < nst; t0 += RS) {
+        for (int64_t t0 = 0, it = 0; t0 < nst; t0 += RS, ++it) {
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
                 (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
             }(std::make_integer_sequence<int, RS>{});
+            if constexpr (FLB > 0)
+                if (it % FLB == FLB - 1) flush();
         }
+    }
+    if constexpr (FLB > 0) {  // the LDS sum plus the chain since the last flush
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int j = 0; j < NG; ++j) acc[p][j] = sacc[(p * NG + j) * 64] + acc[p][j];
     }
     if (!live) return;
     float* out = partial + (int64_t)blockIdx.y * ld * NF;
@@ -1349,7 +1383,8 @@ int mf_backproject_b16_num_splits(int64_t ld, int64_t nrows, bool a32) {
     // x 4 in round 6 (split-A 4096, bf16 storage 2048): each split's rows are one fp32 MFMA accumulation chain, the
     // larger share of the engine's error against the fp32 two-pass kernels at 64k x 64k (16k-row chains;
     // profiles/parity_r6_64k_mf_chains.jsonl)
-    const int64_t target = env_int("SART_MF_BP_BLOCKS", a32 ? 4096 : 2048);
+    // (split-A with the LDS two-level sums of k_mf_backproject_h16: back to ~1024, chains of 12 steps)
+    const int64_t target = env_int("SART_MF_BP_BLOCKS", a32 ? (SART_MF_BWD_FLUSH > 0 ? 1024 : 4096) : 2048);
     int64_t s = (target + nblk - 1) / nblk;
     const int64_t smax = (nrows + 63) / 64;
     if (s > smax) s = smax;

@@ -8,7 +8,9 @@ fixed number of SART updates against the fp64 oracle of the reference GPU semant
 of an fp32 evaluation of the same algorithm (``sart_fp32_emulation``: fp32 vectors and fp32 products, the larger
 error of BLAS sums and of the reference kernels' serial 256-term tiles) -- the bound of the single-frame solver tests
 (tests/test_gpu_solver.py) -- with FACTOR = 1.0 and an absolute slack of 2e-8 (the emulation's own error here is
-~2e-7: the matrix is well conditioned; summation order alone moves it by ~10 %).
+~2e-7: the matrix is well conditioned; summation order alone moves it by ~10 %). The split-A multi-frame paths get
+MF_FACTOR = 1.03: since round 6 their split-K partial sums are summed in two levels (fp32-grade at 64k-term sums,
+profiles/parity_r6_64k_raytraced.jsonl), a third order at this size, measured up to 1.017x (log, 64 frames).
 
 Paths: the fused sweep and the two-pass kernels (linear / log, with and without the Laplacian), the column
 shard, the multi-frame engine at 16 (fp32 MFMA), 32, 64 and 128 frames (split-A on f16 pairs with per-row /
@@ -21,6 +23,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 FACTOR = 1.0
+MF_FACTOR = 1.03
 SLACK = 2e-8
 
 
@@ -113,7 +116,8 @@ def test_column_shard(dev, realistic, lap, log):
 @pytest.mark.parametrize("batch", [16, 32, 64, 128])
 def test_multiframe_paths(dev, realistic, lap, batch, log):
     """The multi-frame engine's default path per batch width (16: fp32 MFMA; 32 / 64 / 128: split-A with f16-pair
-    forward and back-projection), fixed iterations, every checked frame at the fp32 emulation bound."""
+    forward and back-projection), fixed iterations, every checked frame at the fp32 emulation bound (split-A:
+    MF_FACTOR)."""
     from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
     from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
     from mpi_cuda_sartsolver_amd.models.sart import SolverParams
@@ -131,7 +135,7 @@ def test_multiframe_paths(dev, realistic, lap, batch, log):
         assert res[f].iterations == iters
         e, e32 = _errors(res[f].solution, A, G[f], lap, log=log, iters=iters, beta=beta)
         print(f"batch={batch} log={log} frame {f}: {e:.3e} (fp32 emulation {e32:.3e})")
-        assert e <= FACTOR * e32 + SLACK, (f, e, e32)
+        assert e <= (MF_FACTOR if batch >= 32 else FACTOR) * e32 + SLACK, (f, e, e32)
 
 
 def test_bf16_pair_forward_is_not_fp32_grade(dev, realistic):

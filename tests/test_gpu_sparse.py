@@ -206,15 +206,20 @@ def frames128():
     return np.stack([phantom((16, 16, 16), t=0.3 * t) for t in range(128)])
 
 
+# The SpMM's eight interleaved fp32 chains per row: measured <= 1.035x the emulation (see below).
+SPMM_FACTOR = 1.05
+
+
 @pytest.mark.parametrize("which", ["reflections", "direct"])
 @pytest.mark.parametrize("batch", [16, 64, 128])
 @pytest.mark.parametrize("log", [False, True])
 def test_multiframe_sparse_vs_oracle(dev, rtms, lap, frames128, which, batch, log):
     """The multi-frame engine on a sparse shard (fp32 SpMM, csrc/kernels/sparse.hip) at 16 / 64 / 128 frames:
-    every checked frame within 1.1x the fp32 emulation's error of the fp64 oracle (fixed iterations, Laplacian).
+    every checked frame within 1.05x the fp32 emulation's error of the fp64 oracle (fixed iterations, Laplacian).
     The SpMM kernels sum each row in eight interleaved fp32 chains, a third summation order beside the emulation's
     two (BLAS, the reference kernels' serial tiles), and the error of an fp32 evaluation moves by ~10 % with the
-    order (tests/test_gpu_realistic.py); measured up to 1.02x (log, 64 frames, the no-reflection matrix)."""
+    order (tests/test_gpu_realistic.py); measured up to 1.035x (round 6: log, 128 frames, the no-reflection matrix;
+    most frames 0.75 - 1.0x), so the bound is 1.05x (round 5: 1.1x)."""
     from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
     from mpi_cuda_sartsolver_amd.models.rtm import SparseRTM
     from mpi_cuda_sartsolver_amd.models.sart import SolverParams
@@ -230,8 +235,9 @@ def test_multiframe_sparse_vs_oracle(dev, rtms, lap, frames128, which, batch, lo
     res = s.solve_batch(G)
     for f in sorted({0, 1, batch // 2, batch - 1}):
         assert res[f].iterations == iters
-        check_fp32_bound(res[f].solution, A, G[f], lap, log=log, iterations=iters, beta_laplace=beta, factor=1.1,
-                         slack=2e-8)
+        e, e32 = check_fp32_bound(res[f].solution, A, G[f], lap, log=log, iterations=iters, beta_laplace=beta,
+                                  factor=SPMM_FACTOR, slack=2e-8)
+        print(f"sparse mf ratio which={which} batch={batch} log={log} frame={f}: {e / e32:.4f}")
 
 
 @pytest.mark.parametrize("pw", ["16", "32"])
@@ -253,7 +259,9 @@ def test_multiframe_sparse_plane_widths(dev, rtms, lap, frames128, monkeypatch, 
     res = s.solve_batch(G)
     for f in sorted({0, 17, batch // 2 + 5, batch - 1}):
         assert res[f].iterations == iters
-        check_fp32_bound(res[f].solution, A, G[f], lap, iterations=iters, beta_laplace=beta, factor=1.1, slack=2e-8)
+        e, e32 = check_fp32_bound(res[f].solution, A, G[f], lap, iterations=iters, beta_laplace=beta,
+                                  factor=SPMM_FACTOR, slack=2e-8)
+        print(f"sparse mf ratio pw={pw} batch={batch} frame={f}: {e / e32:.4f}")
 
 
 def test_cli_batched_sparse(tmp_path, capfd):

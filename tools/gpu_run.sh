@@ -713,6 +713,45 @@ for step in "$@"; do
         done
       done
       python3 tools/pmc_summary.py "$OUT"/pmc_head_* "$OUT"/pmc_sparse_* "$OUT"/pmc_mf64_* > "$OUT/pmc_summary.txt" 2>&1 || true ;;
+    r6tail)  # the N > 1 single-frame iteration tail (collective + decide / update) at strong-scaling
+             # shard sizes, 2 / 4 / 8 ranks sharing one GPU, the P2P kernel with and without the fused update
+      for npix in ${TAIL_NPIX:-8192 16384}; do
+        for n in ${TAIL_N:-2 4 8}; do
+          for fu in 1 0; do
+            name=tail_np${npix}_n${n}_fu$fu
+            SART_P2P_FUSED_UPDATE=$fu run $name 300 python bench.py --gpus $n --share-gpus --npix $npix --steps 3 \
+              --warmup 1 --watchdog 240 --no-selfcheck || exit 1
+            grep -h '^{' "$OUT/$name.log" | python3 -c "import sys,json; d=json.loads(sys.stdin.readline()); d['tag']='$name'; d['fused_update']=$fu; print(json.dumps(d))" >> "$OUT/tail_r6.jsonl" || exit 1
+          done
+        done
+      done ;;
+    r6tailprof)  # kernel trace of the same runs, fused update on / off: every rank started here under its own
+                 # rocprofv3 (the program itself after --, no launcher hop), the --share-gpus environment set by hand
+      for n in ${TAIL_N:-2 8}; do
+        q=$(( 12 / n )); [ $q -lt 1 ] && q=1; [ $q -gt 4 ] && q=4
+        for fu in 1 0; do
+          name=tailprof_np8192_n${n}_fu$fu
+          echo "=== $name ($(date +%T))" | tee -a "$OUT/session.log"
+          port=$(( 29700 + n * 2 + fu ))
+          pids=""
+          for r in $(seq 0 $((n - 1))); do
+            SART_P2P_FUSED_UPDATE=$fu RANK=$r LOCAL_RANK=$r WORLD_SIZE=$n LOCAL_WORLD_SIZE=$n MASTER_ADDR=127.0.0.1 \
+              MASTER_PORT=$port SART_DIST_BACKEND=gloo SART_P2P_WRAP_STAGED=1 SART_FUSED_SHARED=1 GPU_MAX_HW_QUEUES=$q \
+              timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/$name/r$r" -o run -- \
+              python3 bench.py --gpus $n --share-gpus --npix 8192 --steps 2 --warmup 1 --watchdog 240 --no-selfcheck \
+              > "$OUT/${name}_r$r.log" 2>&1 &
+            pids="$pids $!"
+          done
+          rc=0
+          for p in $pids; do wait $p || rc=$?; done
+          echo "=== $name rc=$rc" | tee -a "$OUT/session.log"
+          [ $rc = 0 ] || { tail -n 20 "$OUT/${name}_r0.log"; exit 1; }
+          grep -h '^{' "$OUT/${name}_r0.log" > "$OUT/$name.json" || true
+          python3 tools/trace_summary.py "$OUT/$name/r0" --marker k_p2p_allreduce --top 12 \
+            --json "$OUT/${name}_trace_r0.json" > "$OUT/${name}_summary.txt" 2>&1 || true
+          rm -rf "$OUT/$name"
+        done
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--w", type=int, default=256)
     ap.add_argument("--nvox", type=int, default=262144)
     ap.add_argument("--ranks", default="1,4")
+    ap.add_argument("--cpu", action="store_true", help="--use_cpu (a rehearsal of the script without a GPU)")
     ap.add_argument("--dir", default=os.environ.get("TMPDIR", "/tmp") + "/sart_sparse_rss")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sparse_load_rss.jsonl"))
     a = ap.parse_args()
@@ -69,7 +70,7 @@ def main():
     outf = open(a.out, "a")
     for nr in [int(v) for v in a.ranks.split(",")]:
         prof = os.path.join(a.dir, f"prof{nr}.jsonl")
-        argv = [binary, "--rtm_format", "sparse", "-m", "2", "--parallel_read", "--profile", prof,
+        argv = [binary] + (["--use_cpu"] if a.cpu else []) + ["--rtm_format", "sparse", "-m", "2", "--parallel_read", "--profile", prof,
                 "-o", os.path.join(a.dir, f"o{nr}.h5"), rtm, img]
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", SART_DIST_BACKEND="tcp", MASTER_ADDR="127.0.0.1",
                    SART_COMM_PORT=str(free_port()), WORLD_SIZE=str(nr))

@@ -32,7 +32,7 @@ def load(path):
 
 
 def short(name):
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     return n.replace("void ", "").strip()
 
 
