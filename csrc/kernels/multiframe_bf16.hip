@@ -307,6 +307,11 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
 #ifndef SART_MF_FLUSH
 #define SART_MF_FLUSH 2
 #endif
+// the forward's second-level sum in LDS (1) or registers (0, default: 13930 against 13300 frame-it/s at 128 frames,
+// equal at 64; profiles/ab_r6_mf_flush.txt)
+#ifndef SART_MF_FLUSH_LDS
+#define SART_MF_FLUSH_LDS 0
+#endif
 // bf16 X / W fragments read from LDS all at once at the top of a step (A/B builds: -DSART_MF_XF_EARLY=0)
 #ifndef SART_MF_XF_EARLY
 #define SART_MF_XF_EARLY 1
@@ -367,16 +372,32 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) rs[rt] = H16 ? fc.rsc[row0 + rt * 16 + r] : 1.f;
 
-    floatx4 acc[RT][NG], sum[RT][NG];
+    // The second-level sum: registers, or (SART_MF_FLUSH_LDS) lane-private LDS slots as in k_mf_backproject_h16 where
+    // the workgroup's LDS still fits. Either costs 8-12 % at 128 frames against no flush (SART_MF_FLUSH=0: 15.1k
+    // frame-it/s), less than the 4x split-K that gives the same error (profiles/ab_r6_mf_flush.txt)
+    constexpr size_t kLdsX = sizeof(u32x4) * 2 * C * 64, kLdsA = AS ? sizeof(u32x4) * 4 * 16 * RT * R16 : 16;
+    constexpr bool FL_LDS = SART_MF_FLUSH_LDS && SART_MF_FLUSH > 0 &&
+                            kLdsX + kLdsA + sizeof(floatx4) * 4 * RT * NG * 64 <= 163840;
+    floatx4 acc[RT][NG], sum[FL_LDS ? 1 : RT][FL_LDS ? 1 : NG];
+    __shared__ __attribute__((aligned(16))) floatx4 s_acc[FL_LDS ? 4 : 1][FL_LDS ? RT * NG : 1][64];
+    floatx4* sacc = s_acc[FL_LDS ? wave : 0][0] + lane;  // slot (t, j) of this lane: sacc[(t * NG + j) * 64]
 #pragma unroll
     for (int t = 0; t < RT; ++t)
 #pragma unroll
-        for (int j = 0; j < NG; ++j) acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f}, sum[t][j] = acc[t][j];
+        for (int j = 0; j < NG; ++j) {
+            acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (FL_LDS) sacc[(t * NG + j) * 64] = acc[t][j];
+            else sum[t][j] = acc[t][j];
+        }
     auto flush = [&] {  // the chain so far into the second-level sum (see SART_MF_FLUSH)
 #pragma unroll
         for (int t = 0; t < RT; ++t)
 #pragma unroll
-            for (int j = 0; j < NG; ++j) sum[t][j] += acc[t][j], acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < NG; ++j) {
+                if constexpr (FL_LDS) sacc[(t * NG + j) * 64] += acc[t][j];
+                else sum[t][j] += acc[t][j];
+                acc[t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+            }
     };
 
     const int64_t nst = c1 > c0 ? (c1 - c0) / (32 * KB) : 0;  // uniform for the workgroup
@@ -575,19 +596,28 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
             if constexpr (LATE) stage_next();
             __syncthreads();
         };
-        for (int64_t t0 = 0, it = 0; t0 < nst; t0 += RS, ++it) {
+        // SART_MF_FLUSH groups of RS steps per trip, then the flush: no branch inside the trip (steps past nst only
+        // re-issue the last step's loads, from cache)
+        constexpr int FLF = SART_MF_FLUSH > 0 ? SART_MF_FLUSH : 1;
+        auto group = [&](int64_t tb) __attribute__((always_inline)) {  // (not inlined: the ring went to scratch)
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
-                (step(std::integral_constant<int, Q>{}, t0 + Q), ...);
+                (step(std::integral_constant<int, Q>{}, tb + Q), ...);
             }(std::make_integer_sequence<int, RS>{});
-            if constexpr (SART_MF_FLUSH > 0)
-                if (it % SART_MF_FLUSH == SART_MF_FLUSH - 1) flush();
+        };
+        for (int64_t t0 = 0; t0 < nst; t0 += RS * FLF) {
+            [&]<int... F>(std::integer_sequence<int, F...>) {
+                (group(t0 + F * RS), ...);
+            }(std::make_integer_sequence<int, FLF>{});
+            if constexpr (SART_MF_FLUSH > 0) flush();
         }
     }
-    flush();
 #pragma unroll
     for (int t = 0; t < RT; ++t)
 #pragma unroll
-        for (int j = 0; j < NG; ++j) acc[t][j] = sum[t][j];
+        for (int j = 0; j < NG; ++j) {
+            if constexpr (FL_LDS) acc[t][j] = sacc[(t * NG + j) * 64] + acc[t][j];
+            else acc[t][j] = sum[t][j] + acc[t][j];
+        }
     if (!live) return;
     if constexpr (H16) {  // 1 / (s_p s_f), exact (powers of two)
 #pragma unroll

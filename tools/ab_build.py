@@ -31,6 +31,7 @@ def main():
     shutil.copytree(ROOT / "mpi_cuda_sartsolver_amd", pkg,
                     ignore=shutil.ignore_patterns("*.so", "*.objs", "__pycache__", "sartsolver", "hdf5"))
     shutil.copy2(ROOT / "bench.py", dst / "bench.py")
+    shutil.copytree(ROOT / "tools", dst / "tools", ignore=shutil.ignore_patterns("__pycache__"))
     src = b.CSRC / "kernels" / a.src
     obj = dst / (src.stem + ".o")
     flags = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={b.ARCH}", "-Wall", "-Wno-unused-function", "-x", "hip",
