@@ -1,6 +1,9 @@
 #include "inputs.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <omp.h>
 #include <cstdlib>
 #include <cmath>
 #include <limits>
@@ -441,29 +444,43 @@ HostCsr RtmReader::read_csr(uint64_t row_begin, uint64_t row_end) {
                         if (np.size() != 1 || nv.size() != 1 || nx.size() != 1 || np[0] != nx[0] || nv[0] != nx[0])
                             throw Error("Inconsistent sparse RTM arrays in " + path + ".");
                         const uint64_t n = nx[0];
+                        // SART_LOAD_TRACE=1: the passes' wall times on stderr
+                        const bool trace = std::getenv("SART_LOAD_TRACE") != nullptr;
+                        double t_read = 0, t_count = 0, t_fill = 0;
+                        auto now = [] { return std::chrono::steady_clock::now(); };
+                        auto since = [](auto t) { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count(); };
+                        const auto t_pass1 = now();
                         std::vector<uint64_t> pb(std::min(chunk, n)), vb(std::min(chunk, n));
                         std::vector<float> xb;
                         // pass 1: entries per row of the shard (and the checks of every entry)
                         for (uint64_t o = 0; o < n; o += chunk) {
                             const uint64_t m = std::min(chunk, n - o);
+                            auto tr = now();
                             h5_read_range_u64(dp, o, m, pb.data());
                             h5_read_range_u64(dv, o, m, vb.data());
+                            t_read += since(tr);
                             for (uint64_t t = 0; t < m; ++t) {
                                 if (vb[t] >= nvox_seg) throw Error("Sparse RTM voxel index out of range in " + path + ".");
                                 if (pb[t] >= lr0 && pb[t] < lr1 && vb[t] >= s0 && vb[t] < s1) ++seg.ptr[pb[t] - lr0 + 1];
                             }
                         }
+                        t_count = since(t_pass1);
+                        const auto t_pass2 = now();
                         for (uint64_t r = 0; r < nr; ++r) seg.ptr[r + 1] += seg.ptr[r];
                         seg.idx.resize((size_t)seg.ptr[nr]);
                         seg.val.resize((size_t)seg.ptr[nr]);
-                        // pass 2: the entries into their rows, in file order
+                        // pass 2: the entries into their rows, in file order (one thread: a parallel scatter over
+                        // row ranges measured no faster, every thread scanning every chunk)
                         std::vector<int64_t> next(seg.ptr.begin(), seg.ptr.end() - 1);
                         xb.resize(std::min(chunk, n));
+                        const int nth = std::max(1, std::min(omp_get_max_threads(), 16));
                         for (uint64_t o = 0; o < n && seg.ptr[nr] > 0; o += chunk) {
                             const uint64_t m = std::min(chunk, n - o);
+                            auto tr = now();
                             h5_read_range_u64(dp, o, m, pb.data());
                             h5_read_range_u64(dv, o, m, vb.data());
                             h5_read_range_f32(dx, o, m, xb.data());
+                            t_read += since(tr);
                             for (uint64_t t = 0; t < m; ++t)
                                 if (pb[t] >= lr0 && pb[t] < lr1 && vb[t] >= s0 && vb[t] < s1) {
                                     const int64_t d = next[pb[t] - lr0]++;
@@ -471,24 +488,48 @@ HostCsr RtmReader::read_csr(uint64_t row_begin, uint64_t row_end) {
                                     seg.val[(size_t)d] = xb[t];
                                 }
                         }
-                        // per row: ascending columns (stable), the last of repeated (row, col) entries, no zeros
-                        int64_t w = 0;
-                        std::vector<std::pair<int32_t, float>> row;
-                        for (uint64_t r = 0; r < nr; ++r) {
-                            row.clear();
-                            for (int64_t k = seg.ptr[r]; k < seg.ptr[r + 1]; ++k) row.push_back({seg.idx[k], seg.val[k]});
-                            std::stable_sort(row.begin(), row.end(),
-                                             [](const auto& p, const auto& q) { return p.first < q.first; });
-                            seg.ptr[r] = w;
-                            for (size_t k = 0; k < row.size(); ++k) {
-                                if (k + 1 < row.size() && row[k + 1].first == row[k].first) continue;
-                                if (row[k].second == 0.0f) continue;
-                                seg.idx[(size_t)w] = row[k].first;
-                                seg.val[(size_t)w] = row[k].second;
-                                ++w;
+                        // per row: ascending columns (stable), the last of repeated (row, col) entries, no zeros --
+                        // rows sorted in parallel (1.45 -> 0.25 s for 20M entries on 8 threads), their kept entries
+                        // at the start of their own range (kept[r]), then moved down in row order
+                        t_fill = since(t_pass2);
+                        const auto t_sort = now();
+                        std::vector<int64_t> kept(nr, 0);
+#pragma omp parallel num_threads(nth)
+                        {
+                            std::vector<std::pair<int32_t, float>> row;
+#pragma omp for schedule(dynamic, 256)
+                            for (int64_t r = 0; r < (int64_t)nr; ++r) {
+                                row.clear();
+                                for (int64_t k = seg.ptr[r]; k < seg.ptr[r + 1]; ++k) row.push_back({seg.idx[k], seg.val[k]});
+                                std::stable_sort(row.begin(), row.end(),
+                                                 [](const auto& p, const auto& q) { return p.first < q.first; });
+                                int64_t w = seg.ptr[r];
+                                for (size_t k = 0; k < row.size(); ++k) {
+                                    if (k + 1 < row.size() && row[k + 1].first == row[k].first) continue;
+                                    if (row[k].second == 0.0f) continue;
+                                    seg.idx[(size_t)w] = row[k].first;
+                                    seg.val[(size_t)w] = row[k].second;
+                                    ++w;
+                                }
+                                kept[r] = w - seg.ptr[r];
                             }
                         }
+                        int64_t w = 0;
+                        for (uint64_t r = 0; r < nr; ++r) {
+                            const int64_t b = seg.ptr[r];
+                            seg.ptr[r] = w;
+                            if (b != w)
+                                for (int64_t k = 0; k < kept[r]; ++k) {
+                                    seg.idx[(size_t)(w + k)] = seg.idx[(size_t)(b + k)];
+                                    seg.val[(size_t)(w + k)] = seg.val[(size_t)(b + k)];
+                                }
+                            w += kept[r];
+                        }
                         seg.ptr[nr] = w;
+                        if (trace)
+                            std::fprintf(stderr, "read_csr %s: %llu entries, pass 1 %.3f s, pass 2 %.3f s (HDF5 reads %.3f s "
+                                         "of both), sort + compact %.3f s, %d threads\n", path.c_str(),
+                                         (unsigned long long)n, t_count, t_fill, t_read, since(t_sort), nth);
                         seg.idx.resize((size_t)w);
                         seg.val.resize((size_t)w);
                         seg.idx.shrink_to_fit();

@@ -6,3 +6,4 @@ for nf in 64 128; do
 done
 timeout -k 10 240 python -u bench.py --steps 2 --warmup 1 --iters 100 --no-selfcheck --frames 64 --rtm-dtype bf16 > gpurun_out/mf_final_64b.json 2> gpurun_out/mf_final_64b.err || exit 1
 timeout -k 10 400 python -u tools/parity_at_scale.py --no-bf16 --no-sparse --no-single --batches 64,128 --tag " r6 final2" --out gpurun_out/parity_r6_mf_final2.jsonl > gpurun_out/pmf2.log 2>&1
+SART_LOAD_TRACE=1 timeout -k 10 300 python -u tools/sparse_load_rss.py --out gpurun_out/sparse_load_rss_r6e.jsonl > gpurun_out/srss5.log 2>&1

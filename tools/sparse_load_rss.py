@@ -79,6 +79,9 @@ def main():
                                   stderr=subprocess.PIPE, text=True) for r in range(nr)]
         outs = [p.communicate(timeout=900) for p in procs]
         wall = time.perf_counter() - t
+        for line in outs[0][1].splitlines():  # SART_LOAD_TRACE=1: the reader's pass times (rank 0)
+            if line.startswith("read_csr"):
+                print(line, flush=True)
         rc = [p.returncode for p in procs]
         if any(rc):
             raise SystemExit(f"ranks={nr}: rc {rc}\n{outs[0][1][-3000:]}")
