@@ -303,9 +303,10 @@ __global__ __launch_bounds__(256) void k_mf_forward_b16(const bf16_t* __restrict
 // Two-level accumulation of the split-K sums: every SART_MF_FLUSH outer iterations (of DEPTH + 1 steps) the MFMA
 // accumulators are added into a second fp32 sum and restarted, so no fp32 chain runs over a whole split. One chain
 // per split (16384 terms at 64k x 64k) measured 3.5x the fp32 two-pass kernels' error at 64 frames after 20 SART
-// updates on the ray-traced RTM (profiles/parity_r6_64k_raytraced.jsonl); 0 disables (A/B).
+// updates on the ray-traced RTM (profiles/parity_r6_64k_raytraced.jsonl); every 4 trips: 0.76-1.01x, every 2:
+// 0.75-1.07x, 4 is +0.3 / +0.7 % faster at 64 / 128 frames (profiles/ab_r6_mf_flush.txt); 0 disables (A/B).
 #ifndef SART_MF_FLUSH
-#define SART_MF_FLUSH 2
+#define SART_MF_FLUSH 4
 #endif
 // the forward's second-level sum in LDS (1) or registers (0, default: 13930 against 13300 frame-it/s at 128 frames,
 // equal at 64; profiles/ab_r6_mf_flush.txt)
@@ -376,7 +377,10 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
     // the workgroup's LDS still fits. Either costs 8-12 % at 128 frames against no flush (SART_MF_FLUSH=0: 15.1k
     // frame-it/s), less than the 4x split-K that gives the same error (profiles/ab_r6_mf_flush.txt)
     constexpr size_t kLdsX = sizeof(u32x4) * 2 * C * 64, kLdsA = AS ? sizeof(u32x4) * 4 * 16 * RT * R16 : 16;
-    constexpr bool FL_LDS = SART_MF_FLUSH_LDS && SART_MF_FLUSH > 0 &&
+    // (split-A only: with bf16 storage the X pieces' 2^-17 sets the error and the chains do not matter; the flush cost
+    // 3-5 % there, profiles/ab_r6_mf_flush.txt)
+    constexpr int FLUSH = A32 ? SART_MF_FLUSH : 0;
+    constexpr bool FL_LDS = SART_MF_FLUSH_LDS && FLUSH > 0 &&
                             kLdsX + kLdsA + sizeof(floatx4) * 4 * RT * NG * 64 <= 163840;
     floatx4 acc[RT][NG], sum[FL_LDS ? 1 : RT][FL_LDS ? 1 : NG];
     __shared__ __attribute__((aligned(16))) floatx4 s_acc[FL_LDS ? 4 : 1][FL_LDS ? RT * NG : 1][64];
@@ -598,7 +602,7 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
         };
         // SART_MF_FLUSH groups of RS steps per trip, then the flush: no branch inside the trip (steps past nst only
         // re-issue the last step's loads, from cache)
-        constexpr int FLF = SART_MF_FLUSH > 0 ? SART_MF_FLUSH : 1;
+        constexpr int FLF = FLUSH > 0 ? FLUSH : 1;
         auto group = [&](int64_t tb) __attribute__((always_inline)) {  // (not inlined: the ring went to scratch)
             [&]<int... Q>(std::integer_sequence<int, Q...>) {
                 (step(std::integral_constant<int, Q>{}, tb + Q), ...);
@@ -608,7 +612,7 @@ __global__ __launch_bounds__(256, (mf_fwd_min_waves<AT, NG>())) void k_mf_forwar
             [&]<int... F>(std::integer_sequence<int, F...>) {
                 (group(t0 + F * RS), ...);
             }(std::make_integer_sequence<int, FLF>{});
-            if constexpr (SART_MF_FLUSH > 0) flush();
+            if constexpr (FLUSH > 0) flush();
         }
     }
 #pragma unroll
