@@ -357,6 +357,7 @@ static void bind_engine(py::module_& m) {
             d["src_finished"] = s.src_finished;
             d["lead"] = s.lead;
             d["src_extrap"] = s.src_extrap;
+            d["drift"] = s.drift;
             d["host_wait_ms"] = s.host_wait_ms;
             d["host_stage_ms"] = s.host_stage_ms;
             d["host_src_ms"] = s.host_src_ms;

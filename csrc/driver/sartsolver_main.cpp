@@ -792,7 +792,7 @@ int main(int argc, char** argv) {
                         << ", \"mean_warm_age\": " << ss.mean_warm_age << ", \"series_ms\": " << ss.ms
                         << ", \"chunk\": " << ss.chunk << ", \"admit_cap\": " << ss.admit_cap
                         << ", \"src_age\": " << ss.src_age << ", \"src_finished\": " << (ss.src_finished ? 1 : 0)
-                        << ", \"lead\": " << (ss.lead ? 1 : 0) << ", \"src_extrap\": " << ss.src_extrap
+                        << ", \"lead\": " << (ss.lead ? 1 : 0) << ", \"src_extrap\": " << ss.src_extrap << ", \"drift\": " << ss.drift
                         << ", \"restarts\": " << ss.restarts << ", \"host_wait_ms\": " << ss.host_wait_ms
                         << ", \"host_stage_ms\": " << ss.host_stage_ms << ", \"host_src_ms\": " << ss.host_src_ms
                         << ", \"host_deliver_ms\": " << ss.host_deliver_ms << ", \"reader_ms\": " << reader_ms

@@ -118,6 +118,10 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     if (const char* e = std::getenv("SART_MF_SRC_FINISHED"); e && *e) src_finished_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SART_MF_LEAD"); e && *e) lead_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SART_MF_SRC_EXTRAP"); e && *e) src_extrap_ = std::atof(e);
+    // drift across the frame gap (linear mode): a source is >= src_age sweeps old, so frames newer than it are already
+    // in flight and an admitted frame sits several frames of drift away from its source; the start adds that many
+    // times the per-frame change between the two newest finished solutions (MfQueue::drift; SART_MF_DRIFT)
+    if (const char* e = std::getenv("SART_MF_DRIFT"); e && *e) drift_ = std::atof(e);
     hip_ok(hipHostMalloc(reinterpret_cast<void**>(&hg64_), (size_t)qcap_ * Pp_ * sizeof(double)), "hipHostMalloc");
     std::memset(hg64_, 0, (size_t)qcap_ * Pp_ * sizeof(double));  // padding rows stay zero
     g64q_.resize((size_t)qcap_ * Pp_);
@@ -127,6 +131,7 @@ MultiFrameEngine::MultiFrameEngine(int device, const void* A, int64_t nrows, int
     ghq_.resize((size_t)qcap_ * Pp_);
     ring_.resize((size_t)rcap_ * ld_);
     xlast_.resize(ld_);
+    xlast2_.resize(ld_);
     if (cfg_.logarithmic) oq_.resize((size_t)qcap_ * ld_);
     nsf_ = mf_forward_num_splits(ld_, Pp_, bf16_ ? 512 : 0);  // bf16 storage: ~512 workgroups (see the back-projection)
     nsb_ = split_ ? mf_backproject_b16_num_splits(ld_, P_, x3_) : mf_backproject_num_splits(ld_, P_);
@@ -570,6 +575,7 @@ bool MultiFrameEngine::series_once(int64_t first, int64_t nframes, const FrameSo
     if ((int64_t)x064_.size() < V_) x064_.resize(std::max<int64_t>(V_, 1));
     rf_.ring = ring_.get();
     rf_.xlast = xlast_.get();
+    rf_.xlast2 = xlast2_.get();
     rf_.x0 = x064_.get();
     rf_.x0q = x0q_.size() ? x0q_.get() : nullptr;
     rf_.oq = oq_.size() ? oq_.get() : nullptr;
@@ -581,13 +587,14 @@ bool MultiFrameEngine::series_once(int64_t first, int64_t nframes, const FrameSo
     launch_mf_state_begin(st_.get(), G64_.get(), 0, cfg_.conv_tolerance, cfg_.max_iterations, NF, stream_);
     const int64_t x0_below = x0 ? (chain ? std::numeric_limits<int64_t>::max() : first + NF) : 0;
     launch_mf_queue_begin(q_.get(), qcap_, rcap_, chain, chain ? admit_cap_ : 0, src_age_, x0_below, src_finished_,
-                          chain && !x0 && lead_, (float)src_extrap_, stream_);
+                          chain && !x0 && lead_, (float)src_extrap_, stream_, chain ? (float)drift_ : 0.f);
     if (x0 && V_) hip_ok(hipMemcpyAsync(x064_.get(), x0, V_ * sizeof(double), hipMemcpyHostToDevice, stream_), "H2D x0");
     stats_.chunk = chunk_;
     stats_.admit_cap = chain ? admit_cap_ : 0;
     stats_.src_age = src_age_;
     stats_.src_finished = src_finished_;
     stats_.src_extrap = src_extrap_;
+    stats_.drift = chain ? drift_ : 0.0;
     stats_.lead = chain && !x0 && lead_;
 
     int64_t staged = 0;

@@ -64,6 +64,7 @@ class MultiFrameEngine {
         int chunk = 0, admit_cap = 0, src_age = 0, restarts = 0;
         bool src_finished = false, lead = false;
         double src_extrap = 0.0;
+        double drift = 0.0;
     };
     const SeriesStats& series_stats() const { return stats_; }
     int64_t nrows() const { return P_; }
@@ -160,8 +161,9 @@ class MultiFrameEngine {
     int graph_chunk_ = 0;
     bool use_graph_ = true, graph_failed_ = false, warm_chunk_ = false;
     double src_extrap_ = 0.0;
+    double drift_ = 0.0;  // drift-extrapolated chain starts (MfQueue::drift; SART_MF_DRIFT)
     DeviceArray<MfQueue> q_;
-    DeviceArray<float> ghq_, x0q_, oq_, ring_, xlast_, starts_;
+    DeviceArray<float> ghq_, x0q_, oq_, ring_, xlast_, xlast2_, starts_;
     MfRefill rf_{};
     std::vector<double> frame_norm_;  // the last series' normalisation per frame (solve_batch's starts)
     struct Snap {

@@ -322,7 +322,7 @@ void launch_mf_stage_norm(MfQueue* q, const double* g64q, float* ghq, const doub
 void launch_mf_publish(MfQueue* q, int64_t q_tail, hipStream_t stream);
 void launch_mf_drained(MfQueue* q, int64_t drained, hipStream_t stream);
 void launch_mf_queue_begin(MfQueue* q, int qcap, int rcap, bool chain, int admit_cap, int src_age, int64_t x0_below,
-                           bool src_finished, bool lead, float src_extrap, hipStream_t stream);
+                           bool src_finished, bool lead, float src_extrap, hipStream_t stream, float drift = 0.f);
 void launch_mf_state_begin(MfState* st, const double* G, int nused, double tol, int max_iter, int nf,
                            hipStream_t stream);
 }  // namespace sart

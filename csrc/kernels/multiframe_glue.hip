@@ -196,7 +196,12 @@ __device__ void mf_plan(MfState* __restrict__ st, MfQueue* __restrict__ q, int s
     const int sw0 = in ? st->sweep0[f] : 0;
     const int upd = sweep_new - sw0;  // updates applied to a running slot's iterate after this sweep
     const bool finished = occ && dn;
-    if (f == 0) best = best_ret = -1, s_kind = kSrcNone, s_slot = -1, s_iter = -1, s_norm = 1.0, s_live = 0;
+    if (f == 0) {
+        best = best_ret = -1, s_kind = kSrcNone, s_slot = -1, s_iter = -1, s_norm = 1.0, s_live = 0;
+        // the drift pair as the update kernel finds it in xlast / xlast2 (before this sweep's retirement moves them)
+        q->drift_frame1 = q->xlast_frame, q->drift_norm1 = q->xlast_norm;
+        q->drift_frame2 = q->xlast2_frame, q->drift_norm2 = q->xlast2_norm;
+    }
     const unsigned long long bf = __ballot(finished);
     if (lane == 0) m_fin[w] = bf;
     __syncthreads();
@@ -243,6 +248,8 @@ __device__ void mf_plan(MfState* __restrict__ st, MfQueue* __restrict__ q, int s
         q->ret_pos[f] = -1;
     }
     if (xl) {
+        q->xlast2_frame = q->xlast_frame;  // (k_mf_update copies xlast into xlast2 before overwriting it)
+        q->xlast2_norm = q->xlast_norm;
         q->xlast_slot = f;
         q->xlast_frame = fr;
         q->xlast_iter = xlast_iter;
@@ -430,6 +437,17 @@ __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const 
         }
     }
     if (!refill) return;
+    // drift per voxel of this block (physical units per frame) from xlast / xlast2 before they move on (below)
+    __shared__ float drift_s[64];
+    const bool use_drift = q->n_adm > 0 && q->drift != 0.f && !logmode && rf.xlast2 && q->drift_frame2 >= 0 &&
+                           q->drift_frame1 > q->drift_frame2;
+    if (use_drift && threadIdx.x < 64) {
+        const int64_t v = v0 + threadIdx.x;
+        drift_s[threadIdx.x] =
+            v < nvox ? (float)(((double)rf.xlast[v] * q->drift_norm1 - (double)rf.xlast2[v] * q->drift_norm2) /
+                               (double)(q->drift_frame1 - q->drift_frame2))
+                     : 0.f;
+    }
     __syncthreads();  // this block's updated iterates are visible to the whole block
     // retired frames into the output ring (and the newest finite one into xlast); start values of the admissions
     constexpr int kMaxQ = 16 * TN / 256;
@@ -448,12 +466,17 @@ __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const 
         if (rp >= 0 || f == q->xlast_slot) {
             const float4 val = *reinterpret_cast<const float4*>((rp >= 0 && q->ret_prev[f] ? Xprev : X) + f * ld + v);
             if (rp >= 0) *reinterpret_cast<float4*>(rf.ring + rp * ld + v) = val;
-            if (f == q->xlast_slot) *reinterpret_cast<float4*>(rf.xlast + v) = val;
+            if (f == q->xlast_slot) {
+                if (rf.xlast2) *reinterpret_cast<float4*>(rf.xlast2 + v) = *reinterpret_cast<const float4*>(rf.xlast + v);
+                *reinterpret_cast<float4*>(rf.xlast + v) = val;
+            }
         }
         const int ap = q->adm_pos[f];
         if (ap < 0) continue;
         const int kind = q->adm_kind[f];
         const double s_new = q->slot_norm[f];
+        const bool chained = kind == kSrcSlot || kind == kSrcLast;
+        const float dgap = (use_drift && chained) ? q->drift * (float)(q->slot_frame[f] - q->src_frame) : 0.f;
         float o[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -463,10 +486,10 @@ __global__ __launch_bounds__(256) void k_mf_update(float* __restrict__ X, const 
                 if (kind == kSrcSlot) {
                     float xs = X[src_slot * ld + vv];
                     if (cx != 0.f) xs = fmaf(cx, xs - Xprev[src_slot * ld + vv], xs);
-                    x = (float)((double)xs * src_norm / s_new);
+                    x = (float)(((double)xs * src_norm + (double)(dgap * drift_s[vv - v0])) / s_new);
                 }
                 else if (kind == kSrcLast)
-                    x = (float)((double)rf.xlast[vv] * src_norm / s_new);
+                    x = (float)(((double)rf.xlast[vv] * src_norm + (double)(dgap * drift_s[vv - v0])) / s_new);
                 else if (kind == kSrcHostX0)
                     x = (float)(rf.x0[vv] / s_new);
                 else if (kind == kSrcCold)
@@ -735,7 +758,7 @@ __global__ void k_mf_drained(MfQueue* __restrict__ q, int64_t drained) {
 }
 
 __global__ void k_mf_queue_begin(MfQueue* __restrict__ q, int qcap, int rcap, int chain, int admit_cap, int src_age,
-                                 int64_t x0_below, int src_finished, int lead, float src_extrap) {
+                                 int64_t x0_below, int src_finished, int lead, float src_extrap, float drift) {
     const int f = threadIdx.x;
     if (f < kMaxNF) {
         q->slot_frame[f] = -1;
@@ -754,6 +777,9 @@ __global__ void k_mf_queue_begin(MfQueue* __restrict__ q, int qcap, int rcap, in
         q->n_ret = q->n_adm = q->upd_any = q->skip_bwd = 0;
         q->xlast_frame = q->xlast_iter = q->xlast_slot = -1;
         q->xlast_norm = 1.0;
+        q->xlast2_frame = q->drift_frame1 = q->drift_frame2 = -1;
+        q->xlast2_norm = q->drift_norm1 = q->drift_norm2 = 1.0;
+        q->drift = drift;
         q->src_kind = kSrcNone, q->src_slot = q->src_frame = q->src_iter = -1;
         q->src_norm = 1.0;
     }
@@ -879,11 +905,11 @@ void launch_mf_drained(MfQueue* q, int64_t drained, hipStream_t stream) {
 }
 
 void launch_mf_queue_begin(MfQueue* q, int qcap, int rcap, bool chain, int admit_cap, int src_age, int64_t x0_below,
-                           bool src_finished, bool lead, float src_extrap, hipStream_t stream) {
+                           bool src_finished, bool lead, float src_extrap, hipStream_t stream, float drift) {
     if (qcap < 1 || qcap > kMfQueueMax || rcap < 1 || rcap > kMfQueueMax)
         throw std::runtime_error("mf_queue_begin: queue and ring capacities in [1, 256]");
     hipLaunchKernelGGL(k_mf_queue_begin, dim3(1), dim3(kMaxNF), 0, stream, q, qcap, rcap, chain ? 1 : 0, admit_cap,
-                       src_age, x0_below, src_finished ? 1 : 0, lead ? 1 : 0, src_extrap);
+                       src_age, x0_below, src_finished ? 1 : 0, lead ? 1 : 0, src_extrap, drift);
     check_launch("k_mf_queue_begin");
 }
 

@@ -97,6 +97,15 @@ struct alignas(16) MfQueue {
     int32_t n_ret, n_adm, upd_any, skip_bwd;  // this sweep's plan; skip_bwd: the next sweep's back-projection is unused
     int32_t xlast_frame, xlast_iter, xlast_slot, pad0;  // xlast_slot: the slot copied into xlast at this sweep (-1)
     double xlast_norm;
+    // Drift (linear mode): the previous xlast is kept (xlast2), and an admitted frame q chained from source frame p
+    // starts at X_p + drift (q - p) (X_xlast - X_xlast2) / (xlast_frame - xlast2_frame) in de-normalised units -- the
+    // per-frame change between the two newest finished solutions, carried over the frame gap a pipelined chain
+    // leaves (a source is >= src_age sweeps old, so several newer frames are already in flight). drift_*: this
+    // sweep's snapshot of the pair, taken before xlast / xlast2 move on.
+    int32_t xlast2_frame, drift_frame1, drift_frame2, pad1;
+    double xlast2_norm, drift_norm1, drift_norm2;
+    float drift;
+    int32_t pad2;
     int32_t src_kind, src_slot, src_frame, src_iter;  // the chain source of this sweep's admissions
     double src_norm;
     int32_t slot_frame[kMfMaxFrames];  // frame in each slot (-1: empty)
@@ -117,6 +126,7 @@ struct alignas(16) MfQueue {
 struct MfRefill {
     float* ring;
     float* xlast;
+    float* xlast2;  // the previous xlast (drift; may be null: no drift)
     const double* x0;
     const float* x0q;
     const float* oq;
