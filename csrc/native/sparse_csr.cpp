@@ -1,5 +1,7 @@
 #include "sparse_csr.hpp"
 
+#include <omp.h>
+
 #include <algorithm>
 #include <numeric>
 #include <stdexcept>
@@ -75,17 +77,48 @@ HostCsr csr_transpose(const HostCsr& a) {
     t.nrows = a.ncols;
     t.ncols = a.nrows;
     t.ptr.assign(a.ncols + 1, 0);
-    for (int32_t c : a.idx) ++t.ptr[(int64_t)c + 1];
-    std::partial_sum(t.ptr.begin(), t.ptr.end(), t.ptr.begin());
     t.idx.resize(a.idx.size());
     t.val.resize(a.val.size());
-    std::vector<int64_t> next(t.ptr.begin(), t.ptr.end() - 1);
-    for (int64_t r = 0; r < a.nrows; ++r)  // rows ascending: each column's entries come out in row order
-        for (int64_t k = a.ptr[r]; k < a.ptr[r + 1]; ++k) {
-            const int64_t d = next[a.idx[k]]++;
-            t.idx[d] = (int32_t)r;
-            t.val[d] = a.val[k];
+    // Threads take contiguous row blocks of about equal entry counts: per-thread column counts, turned in place into
+    // each thread's cursors (a column's start plus the earlier blocks' entries), so every column's entries still come
+    // out in row order (the sequential transpose's result, bitwise). At most 4 threads: the cursors are 8 bytes per
+    // column and thread, host memory on top of the CSR + CSC. A small matrix runs on one thread.
+    const int64_t nnz = a.nnz();
+    const int nth = nnz < (1 << 20) ? 1 : std::max(1, std::min(omp_get_max_threads(), 4));
+    std::vector<int64_t> rcut(nth + 1, a.nrows);
+    rcut[0] = 0;
+    for (int q = 1, r = 0; q < nth; ++q) {
+        const int64_t goal = nnz * q / nth;
+        while (r < a.nrows && a.ptr[r] < goal) ++r;
+        rcut[q] = r;
+    }
+    std::vector<int64_t> cur((size_t)nth * a.ncols, 0);
+#pragma omp parallel num_threads(nth)
+    {
+        const int q = omp_get_thread_num();
+        int64_t* cq = cur.data() + (size_t)q * a.ncols;
+        for (int64_t k = a.ptr[rcut[q]]; k < a.ptr[rcut[q + 1]]; ++k) ++cq[a.idx[k]];
+    }
+    for (int64_t c = 0, base = 0; c < a.ncols; ++c) {
+        t.ptr[c] = base;
+        for (int q = 0; q < nth; ++q) {
+            const int64_t n = cur[(size_t)q * a.ncols + c];
+            cur[(size_t)q * a.ncols + c] = base;
+            base += n;
         }
+        t.ptr[c + 1] = base;
+    }
+#pragma omp parallel num_threads(nth)
+    {
+        const int q = omp_get_thread_num();
+        int64_t* next = cur.data() + (size_t)q * a.ncols;
+        for (int64_t r = rcut[q]; r < rcut[q + 1]; ++r)
+            for (int64_t k = a.ptr[r]; k < a.ptr[r + 1]; ++k) {
+                const int64_t d = next[a.idx[k]]++;
+                t.idx[d] = (int32_t)r;
+                t.val[d] = a.val[k];
+            }
+    }
     return t;
 }
 

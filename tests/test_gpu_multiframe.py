@@ -149,6 +149,43 @@ def test_multiframe_series_iterations_near_sequential():
     assert mf.series_stats["slot_util"] > 0.3, mf.series_stats
 
 
+def test_multiframe_drift_starts(monkeypatch):
+    """SART_MF_DRIFT=1 (MfQueue::drift): on a linearly drifting series a chained frame's start adds the frame gap to
+    its source times the per-frame change between the two newest finished solutions. Every frame still solves to
+    the oracle from its recorded start, and the starts land nearer the frames' own solutions than without the drift."""
+    from mpi_cuda_sartsolver_amd.models.multiframe import MultiFrameSARTSolver
+    from mpi_cuda_sartsolver_amd.models.reference import sart_gpu_semantics
+    from mpi_cuda_sartsolver_amd.models.rtm import DenseRTM
+    from mpi_cuda_sartsolver_amd.models.sart import SolverParams
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(11)
+    P, V, nframes = 800, 1000, 64
+    A = rng.random((P, V), dtype=np.float32)
+    b, d = rng.random(V) + 0.5, 0.01 * (rng.random(V) - 0.5)
+    X = np.stack([b + t * d for t in range(nframes)])
+    G = X @ A.T.astype(np.float64)
+    kw = dict(max_iterations=300, conv_tolerance=1e-7)
+    rtm = DenseRTM.from_dense(A, device=dev)
+    out = {}
+    for drift in ("0", "1"):
+        monkeypatch.setenv("SART_MF_DRIFT", drift)
+        s = MultiFrameSARTSolver(rtm, None, None, SolverParams(**kw), batch=16)
+        res = s.solve_batch(G, chain=True, record_starts=True)
+        assert s.series_stats["drift"] == float(drift)
+        assert all(r.status == 0 for r in res)
+        out[drift] = (res, s.starts.copy())
+    res, starts = out["1"]
+    for f in range(0, nframes, 9):
+        x, st, it = sart_gpu_semantics(A, G[f], None, x_prev=starts[f], **kw)
+        assert res[f].status == st and abs(res[f].iterations - it) <= 2, (f, res[f].iterations, it)
+    late = range(nframes // 2, nframes)  # (xlast and xlast2 both exist by then)
+    dist = {k: np.mean([np.linalg.norm(v[1][f] - v[0][f].solution) / np.linalg.norm(v[0][f].solution) for f in late])
+            for k, v in out.items()}
+    assert any(not np.array_equal(out["0"][1][f], starts[f]) for f in late)
+    assert dist["1"] < dist["0"], dist
+
+
 @pytest.mark.parametrize("log", [False, True])
 def test_multiframe_nonfinite_slot_is_rolled_back_and_refilled(monkeypatch, log):
     """A NaN injected into slot 0's iterate after sweep 5 (SART_FAULT_NAN) stops that frame at the next sweep:

@@ -30,7 +30,8 @@ def test_csr_from_entries_semantics():
         n.csr_from_entries(3, 4, np.array([3], np.int64), np.array([0], np.int32), np.array([1.0], np.float32))
 
 
-@pytest.mark.parametrize("shape,density", [((1, 1), 1.0), ((37, 129), 0.05), ((200, 300), 0.3), ((64, 64), 0.0)])
+@pytest.mark.parametrize("shape,density", [((1, 1), 1.0), ((37, 129), 0.05), ((200, 300), 0.3), ((64, 64), 0.0),
+                                           ((1500, 2000), 0.4)])  # (1.2M non-zeros: the multi-threaded transpose)
 def test_csr_transpose(shape, density):
     n = native()
     rng = np.random.default_rng(shape[0])
