@@ -165,7 +165,7 @@ def test_multiframe_drift_starts(monkeypatch):
     b, d = rng.random(V) + 0.5, 0.01 * (rng.random(V) - 0.5)
     X = np.stack([b + t * d for t in range(nframes)])
     G = X @ A.T.astype(np.float64)
-    kw = dict(max_iterations=300, conv_tolerance=1e-7)
+    kw = dict(max_iterations=300, conv_tolerance=1e-5)  # (the reference default; fp32 sums stall near 1e-7)
     rtm = DenseRTM.from_dense(A, device=dev)
     out = {}
     for drift in ("0", "1"):
@@ -176,7 +176,9 @@ def test_multiframe_drift_starts(monkeypatch):
         assert all(r.status == 0 for r in res)
         out[drift] = (res, s.starts.copy())
     res, starts = out["1"]
-    for f in range(0, nframes, 9):
+    chained = [f for f in range(nframes) if res[f].warm_from >= 0]
+    assert len(chained) > nframes // 2
+    for f in chained[::7]:
         x, st, it = sart_gpu_semantics(A, G[f], None, x_prev=starts[f], **kw)
         assert res[f].status == st and abs(res[f].iterations - it) <= 2, (f, res[f].iterations, it)
     late = range(nframes // 2, nframes)  # (xlast and xlast2 both exist by then)
